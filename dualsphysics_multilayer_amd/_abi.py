@@ -1,0 +1,200 @@
+"""ctypes mirror of the POD structs in include/sphcore.h (ABI version 1)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+SPH_ABI_VERSION = 1
+
+SPH_STATUS = {
+    0: "SPH_OK",
+    1: "SPH_ERR_ARG",
+    2: "SPH_ERR_HIP",
+    3: "SPH_ERR_STATE",
+    4: "SPH_ERR_DT",
+    5: "SPH_ERR_BOUNDOUT",
+    6: "SPH_ERR_NOMEM",
+    7: "SPH_ERR_UNSUPPORTED",
+}
+
+
+class SphCaseDef(C.Structure):
+    _fields_ = [
+        ("dp", C.c_double),
+        ("h", C.c_double),
+        ("cteb", C.c_double),
+        ("rhop0", C.c_double),
+        ("gamma", C.c_double),
+        ("massbound", C.c_double),
+        ("massfluid", C.c_double),
+        ("gravity", C.c_double * 3),
+        ("cflnumber", C.c_double),
+        ("step_algorithm", C.c_int),
+        ("verlet_steps", C.c_int),
+        ("kernel", C.c_int),
+        ("tdensity", C.c_int),
+        ("visco", C.c_double),
+        ("viscoboundfactor", C.c_double),
+        ("ddtvalue", C.c_double),
+        ("coefdtmin", C.c_double),
+        ("dtini", C.c_double),
+        ("dtmin", C.c_double),
+        ("rhopoutmin", C.c_double),
+        ("rhopoutmax", C.c_double),
+        ("map_realposmin", C.c_double * 3),
+        ("map_realposmax", C.c_double * 3),
+        ("cellmode", C.c_int),
+        ("celldomfixed", C.c_int),
+        ("npb", C.c_uint32),
+        ("np", C.c_uint32),
+    ]
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "SphCaseDef":
+        s = cls()
+        for name, ctype in cls._fields_:
+            v = d[name]
+            if isinstance(v, (tuple, list)):
+                arr = getattr(s, name)
+                for i, x in enumerate(v):
+                    arr[i] = x
+            else:
+                setattr(s, name, v)
+        return s
+
+
+class SphConstants(C.Structure):
+    _fields_ = [
+        ("kernelh", C.c_float),
+        ("kernelsize", C.c_float),
+        ("kernelsize2", C.c_float),
+        ("awen", C.c_float),
+        ("bwen", C.c_float),
+        ("cteb", C.c_float),
+        ("gamma", C.c_float),
+        ("rhopzero", C.c_float),
+        ("ovrhopzero", C.c_float),
+        ("massfluid", C.c_float),
+        ("massbound", C.c_float),
+        ("gravity", C.c_float * 3),
+        ("eta2", C.c_float),
+        ("ddtkh", C.c_float),
+        ("ddtgz", C.c_float),
+        ("visco", C.c_float),
+        ("viscoboundfactor", C.c_float),
+        ("rhopoutmin", C.c_float),
+        ("rhopoutmax", C.c_float),
+        ("scell", C.c_float),
+        ("movlimit", C.c_float),
+        ("pad0", C.c_float),
+        ("cs0", C.c_double),
+        ("cflnumber", C.c_double),
+        ("dtini", C.c_double),
+        ("dtmin", C.c_double),
+        ("dp", C.c_double),
+        ("tdensity", C.c_int),
+        ("step_algorithm", C.c_int),
+        ("verlet_steps", C.c_int),
+        ("scelldiv", C.c_int),
+        ("map_realposmin", C.c_double * 3),
+        ("map_realsize", C.c_double * 3),
+        ("dom_posmin", C.c_double * 3),
+        ("dom_cells", C.c_uint32 * 3),
+        ("dom_cellcode", C.c_uint32),
+    ]
+
+    def as_dict(self) -> dict:
+        out = {}
+        for name, _ in self._fields_:
+            v = getattr(self, name)
+            out[name] = list(v) if hasattr(v, "__len__") else v
+        return out
+
+
+class SphRunStats(C.Structure):
+    _fields_ = [
+        ("time", C.c_double),
+        ("last_dt", C.c_double),
+        ("sym_dtpre", C.c_double),
+        ("nstep", C.c_uint64),
+        ("np", C.c_uint32),
+        ("npb", C.c_uint32),
+        ("npbok", C.c_uint32),
+        ("nout", C.c_uint32),
+        ("dtmodif", C.c_uint32),
+        ("error_flags", C.c_uint32),
+        ("velmax", C.c_float),
+        ("acemax", C.c_float),
+        ("viscdtmax", C.c_float),
+        ("pad", C.c_float),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_ if name != "pad"}
+
+
+class SphParticlesHost(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint32),
+        ("idp", C.POINTER(C.c_uint32)),
+        ("pos", C.POINTER(C.c_double)),
+        ("vel", C.POINTER(C.c_float)),
+        ("rhop", C.POINTER(C.c_float)),
+        ("code", C.POINTER(C.c_uint16)),
+    ]
+
+
+class SphInterOut(C.Structure):
+    _fields_ = [
+        ("ar", C.POINTER(C.c_float)),
+        ("ace", C.POINTER(C.c_float)),
+        ("viscdtmax", C.c_float),
+        ("velmax", C.c_float),
+        ("acemax", C.c_float),
+    ]
+
+
+def _ptr(arr: np.ndarray | None, ctype):
+    if arr is None:
+        return C.POINTER(ctype)()
+    assert arr.flags["C_CONTIGUOUS"]
+    return arr.ctypes.data_as(C.POINTER(ctype))
+
+
+class HostParticles:
+    """Owns numpy arrays and exposes them as an SphParticlesHost view."""
+
+    def __init__(self, n: int, idp=None, pos=None, vel=None, rhop=None, code=None):
+        self.idp = np.ascontiguousarray(idp if idp is not None else np.zeros(n, np.uint32), dtype=np.uint32)
+        self.pos = np.ascontiguousarray(pos if pos is not None else np.zeros((n, 3)), dtype=np.float64)
+        self.vel = np.ascontiguousarray(vel if vel is not None else np.zeros((n, 3), np.float32), dtype=np.float32)
+        self.rhop = np.ascontiguousarray(rhop if rhop is not None else np.zeros(n, np.float32), dtype=np.float32)
+        self.code = np.ascontiguousarray(code if code is not None else np.zeros(n, np.uint16), dtype=np.uint16)
+        self.view = SphParticlesHost(
+            n,
+            _ptr(self.idp, C.c_uint32),
+            _ptr(self.pos, C.c_double),
+            _ptr(self.vel, C.c_float),
+            _ptr(self.rhop, C.c_float),
+            _ptr(self.code, C.c_uint16),
+        )
+
+    def trimmed(self, n: int) -> dict:
+        return dict(
+            idp=self.idp[:n].copy(),
+            pos=self.pos[:n].copy(),
+            vel=self.vel[:n].copy(),
+            rhop=self.rhop[:n].copy(),
+            code=self.code[:n].copy(),
+        )
+
+
+def check_struct_sizes() -> dict:
+    return {
+        "SphCaseDef": C.sizeof(SphCaseDef),
+        "SphConstants": C.sizeof(SphConstants),
+        "SphRunStats": C.sizeof(SphRunStats),
+        "SphParticlesHost": C.sizeof(SphParticlesHost),
+        "SphInterOut": C.sizeof(SphInterOut),
+    }

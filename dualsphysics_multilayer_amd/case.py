@@ -1,0 +1,188 @@
+"""Dam-break case definition: lattice, constants and map limits.
+
+GenCase is a missing blob in the reference, so cases are
+generated here.  The lattice/constant recipe is the SURVEY §8(c) one; the
+oracle-side writer ``oracle/tools/gencase_ref.cpp`` produces the same particles
+through the reference's own .bi4 code, and ``tests/test_case.py`` checks the two
+agree bit for bit.
+
+What the reference derives while loading a case is mirrored here so that
+``SphCaseDef`` carries exactly what ``JSph`` would hold:
+
+* constants are the XML text values (``%.10E`` for h, b and masses, as the case
+  XML stores them) parsed back to double — ``JSph::LoadConfigCtes``
+  (JSph.cpp:567-583) then narrows them to float inside the core;
+* map limits follow ``JSph::LoadCaseParticles`` (JSph.cpp:2051-2062):
+  ``JPartsLoad4::CalculeLimits`` (JPartsLoad4.cpp:339-347) with border
+  ``double(float(h))*BORDER_MAP`` (DualSphDef.h:130), then
+  ``JSph::ResizeMapLimits`` (JSph.cpp:1354-1387) with the case's
+  ``<simulationdomain>`` ``posmax z="default + 50%"``.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+BORDER_MAP = 0.05  # DualSphDef.h:130
+
+STEP_VERLET, STEP_SYMPLECTIC = 1, 2
+DDT_NONE, DDT_DDT, DDT_DDT2, DDT_DDT2FULL = 0, 1, 2, 3
+CELLMODE_FULL, CELLMODE_HALF = 1, 2
+CODE_TYPE_FIXED, CODE_TYPE_FLUID = 0x0, 0x1800
+
+
+def _cround(v: float) -> int:
+    """std::round (half away from zero) for v >= 0, exact in double."""
+    r = math.floor(v)
+    return int(r + 1 if v - r >= 0.5 else r)
+
+
+def _xml_e10(v: float) -> float:
+    """Value as written by ``%.10E`` in the case XML and parsed back."""
+    return float("%.10E" % v)
+
+
+@dataclass
+class DamBreakCase:
+    """3D dam break: tank 1.6 x 0.67 x 0.4 m, water column 0.4 x 0.67 x 0.3 m.
+
+    Walls: bottom, x=0, x=1.6, y=0, y=0.67.
+    """
+
+    dp: float
+    step_algorithm: int = STEP_VERLET
+    tdensity: int = DDT_DDT2
+    ddtvalue: float = 0.1
+    visco: float = 0.1
+    viscoboundfactor: float = 1.0
+    cflnumber: float = 0.2
+    verlet_steps: int = 40
+    coefdtmin: float = 0.05
+    rhopoutmin: float = 700.0
+    rhopoutmax: float = 1300.0
+    cellmode: int = CELLMODE_FULL
+    celldomfixed: bool = False
+    gravity: tuple = (0.0, 0.0, -9.81)
+    rhop0: float = 1000.0
+    gamma: float = 7.0
+    coefsound: float = 20.0
+    coefh: float = 1.0
+    # generated
+    pos: np.ndarray = field(init=False, repr=False)
+    vel: np.ndarray = field(init=False, repr=False)
+    rhop: np.ndarray = field(init=False, repr=False)
+    idp: np.ndarray = field(init=False, repr=False)
+    npb: int = field(init=False)
+    np: int = field(init=False)
+
+    def __post_init__(self) -> None:
+        dp = self.dp
+        nx, ny, nz = _cround(1.6 / dp), _cround(0.67 / dp), _cround(0.4 / dp)
+        mx, my, mz = _cround(0.4 / dp), _cround(0.67 / dp), _cround(0.3 / dp)
+        # Boundary: loop order k, j, i over the full tank lattice, walls only.
+        k, j, i = np.meshgrid(np.arange(nz + 1), np.arange(ny + 1), np.arange(nx + 1), indexing="ij")
+        wall = (k == 0) | (i == 0) | (i == nx) | (j == 0) | (j == ny)
+        bi, bj, bk = i[wall], j[wall], k[wall]
+        # Fluid: i in [1,mx], j in [1,my-1], k in [1,mz], loop order k, j, i.
+        fk, fj, fi = np.meshgrid(np.arange(1, mz + 1), np.arange(1, my), np.arange(1, mx + 1), indexing="ij")
+        ii = np.concatenate([bi, fi.ravel()]).astype(np.float64)
+        jj = np.concatenate([bj, fj.ravel()]).astype(np.float64)
+        kk = np.concatenate([bk, fk.ravel()]).astype(np.float64)
+        self.pos = np.stack([ii * dp, jj * dp, kk * dp], axis=1)
+        self.npb = int(bi.size)
+        self.np = int(self.pos.shape[0])
+        self.idp = np.arange(self.np, dtype=np.uint32)
+        self.vel = np.zeros((self.np, 3), dtype=np.float32)
+        g, rho0, gamma = -self.gravity[2], self.rhop0, self.gamma
+        hswl = mz * dp
+        cs0 = self.coefsound * math.sqrt(g * hswl)
+        b = cs0 * cs0 * rho0 / gamma
+        h = self.coefh * math.sqrt(3.0 * dp * dp)
+        mass = rho0 * dp * dp * dp
+        self._h, self._b, self._mass = h, b, mass
+        rhop = np.empty(self.np, dtype=np.float32)
+        rhop[: self.npb] = np.float32(rho0)
+        z = self.pos[self.npb :, 2]
+        rhop[self.npb :] = (rho0 * np.power(1.0 + rho0 * g * (hswl - z) / b, 1.0 / gamma)).astype(np.float32)
+        self.rhop = rhop
+
+    @property
+    def nf(self) -> int:
+        return self.np - self.npb
+
+    @property
+    def code(self) -> np.ndarray:
+        c = np.full(self.np, CODE_TYPE_FLUID, dtype=np.uint16)
+        c[: self.npb] = CODE_TYPE_FIXED
+        return c
+
+    # -- constants as the case XML stores them ------------------------------
+    @property
+    def h(self) -> float:
+        return _xml_e10(self._h)
+
+    @property
+    def cteb(self) -> float:
+        return _xml_e10(self._b)
+
+    @property
+    def mass(self) -> float:
+        return _xml_e10(self._mass)
+
+    def map_limits(self) -> tuple[np.ndarray, np.ndarray]:
+        """MapRealPosMin/Max as JSph::LoadCaseParticles computes them."""
+        kernelh = float(np.float32(self.h))
+        border = kernelh * BORDER_MAP
+        pmin = self.pos.min(axis=0)
+        pmax = self.pos.max(axis=0)
+        dmin = pmin - border
+        dmax = pmax + border
+        dif = dmax - dmin
+        prcmax = np.array([0.0, 0.0, 0.5])  # posmax z="default + 50%"
+        dmax = dmax + dif * prcmax
+        return dmin, dmax
+
+    def case_def(self) -> dict:
+        """Fields of the C ``SphCaseDef`` (include/sphcore.h)."""
+        pmin, pmax = self.map_limits()
+        dpx = float("%.10g" % self.dp)
+        return dict(
+            dp=dpx,
+            h=self.h,
+            cteb=self.cteb,
+            rhop0=self.rhop0,
+            gamma=self.gamma,
+            massbound=self.mass,
+            massfluid=self.mass,
+            gravity=tuple(self.gravity),
+            cflnumber=self.cflnumber,
+            step_algorithm=self.step_algorithm,
+            verlet_steps=self.verlet_steps,
+            kernel=2,
+            tdensity=self.tdensity,
+            visco=self.visco,
+            viscoboundfactor=self.viscoboundfactor,
+            ddtvalue=self.ddtvalue,
+            coefdtmin=self.coefdtmin,
+            dtini=0.0,
+            dtmin=0.0,
+            rhopoutmin=self.rhopoutmin,
+            rhopoutmax=self.rhopoutmax,
+            map_realposmin=tuple(pmin.tolist()),
+            map_realposmax=tuple(pmax.tolist()),
+            cellmode=self.cellmode,
+            celldomfixed=int(self.celldomfixed),
+            npb=self.npb,
+            np=self.np,
+        )
+
+
+def dambreak_np(dp: float) -> int:
+    """Particle count of the dam-break lattice without building it."""
+    nx, ny, nz = _cround(1.6 / dp), _cround(0.67 / dp), _cround(0.4 / dp)
+    mx, my, mz = _cround(0.4 / dp), _cround(0.67 / dp), _cround(0.3 / dp)
+    total = (nx + 1) * (ny + 1) * (nz + 1)
+    inner = (nx - 1) * (ny - 1) * nz  # k>=1, i in [1,nx-1], j in [1,ny-1]
+    return (total - inner) + mx * (my - 1) * mz

@@ -1,0 +1,216 @@
+/*
+ * sphcore.h — C-ABI of the MI355X-native SPH particle-interaction core.
+ *
+ * This is the drop-in boundary for the DualSPHysics v5.2 hot path
+ * (SURVEY.md §8(b)): cell-linked-list divide → Interaction_Forces →
+ * dt → Verlet/Symplectic update, as driven by JSphGpuSingle/JSphCpuSingle.
+ * Plain C types, device pointers as void*, sizes as unsigned; no torch, no
+ * C++ in the signatures.  Every function returns SphStatus (0 = ok); the text
+ * of the last error of the calling thread is in sph_last_error().  The C++
+ * host wrapper (csrc/sph_solver.hpp) turns a non-zero status back into an
+ * exception, preserving the reference's fail-fast behaviour
+ * (RunExceptionGpuDef.h:27, JSphGpu.cpp:118-125).
+ *
+ * Entry points and the reference interfaces they replace:
+ *   sph_case_derive ............ JSph::ConfigConstants1/2 (JSph.cpp:1392-1457),
+ *                                JSph::ConfigCellDivision (JSph.cpp:1772-1788),
+ *                                JSph::SelecDomain (JSph.cpp:1794-1829)
+ *   sph_solver_create .......... JSphGpuSingle::ConfigDomain + InitRunGpu
+ *                                (JSphGpuSingle.cpp; CPU twin JSphCpuSingle.cpp:107-167)
+ *   sph_divide ................. JSphGpuSingle::RunCellDivide (JSphGpuSingle.cpp:331-430):
+ *                                cudiv::LimitsCell/PreSortFull/Sort/CalcBeginEndCell/
+ *                                SortDataParticles (JCellDivGpu_ker.h:36-59,
+ *                                JCellDivGpuSingle_ker.h:26-29), cusphs::UpdatePosCell
+ *   sph_interaction_forces ..... JSphGpuSingle::Interaction_Forces (JSphGpuSingle.cpp:435-486):
+ *                                cusph::Interaction_Forces(StInterParmsg) (JSphGpu_ker.h:200)
+ *                                + ComputeVelMod/ReduMaxFloat/ComputeAceMod/AddDelta,
+ *                                CPU twin JSphCpu::Interaction_Forces_ct (JSphCpu.cpp:1012)
+ *   sph_compute_dt ............. JSph*::DtVariable (JSphGpu.cpp:984, JSphCpu.cpp:1614)
+ *   sph_step_verlet ............ JSphGpu::ComputeVerlet (JSphGpu.cpp:874) =
+ *                                cusphs::ComputeStepVerlet + cusph::ComputeStepPos
+ *   sph_step_symplectic_pre/cor  JSphGpu::ComputeSymplecticPre/Corr (JSphGpu.cpp:900-983)
+ *   sph_solver_run ............. JSphGpuSingle::Run main loop (JSphGpuSingle.cpp:853-880):
+ *                                ComputeStep_Ver/_Sym + RunCellDivide, device-resident dt
+ *   sph_download_particles ..... JSphGpuSingle::ParticlesDataDown (feeds SaveData)
+ *   sph_count_pairs ............ JDsPips::ComputeGpu (JDsPips.cpp:187-262) — work counter
+ *   sph_slab_* ................. new: slab decomposition across GPUs
+ */
+#ifndef SPHCORE_H
+#define SPHCORE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPH_ABI_VERSION 1
+
+typedef enum {
+  SPH_OK = 0,
+  SPH_ERR_ARG = 1,        /* invalid argument / configuration            */
+  SPH_ERR_HIP = 2,        /* HIP runtime error                           */
+  SPH_ERR_STATE = 3,      /* call out of order / object in a bad state   */
+  SPH_ERR_DT = 4,         /* dt NaN or infinite (JSphCpu.cpp:1622)       */
+  SPH_ERR_BOUNDOUT = 5,   /* boundary particle excluded (JSphCpuSingle.cpp:507-518) */
+  SPH_ERR_NOMEM = 6,      /* allocation failed                           */
+  SPH_ERR_UNSUPPORTED = 7 /* feature outside the implemented scope       */
+} SphStatus;
+
+/* TpStep (DualSphDef.h:316-319). */
+enum { SPH_STEP_VERLET = 1, SPH_STEP_SYMPLECTIC = 2 };
+/* TpDensity (DualSphDef.h:358-364). */
+enum { SPH_DDT_NONE = 0, SPH_DDT_DDT = 1, SPH_DDT_DDT2 = 2, SPH_DDT_DDT2FULL = 3 };
+/* TpCellMode (DualSphDef.h:477-481). */
+enum { SPH_CELLMODE_FULL = 1, SPH_CELLMODE_HALF = 2 };
+/* TpKernel (DualSphDef.h): only Wendland is on the hot path. */
+enum { SPH_KERNEL_WENDLAND = 2 };
+
+/* Particle code bits, identical to the 16-bit `typecode` of DualSphDef.h:161-221. */
+#define SPH_CODE_MASKSPECIAL 0xe000u
+#define SPH_CODE_NORMAL 0x0u
+#define SPH_CODE_PERIODIC 0x2000u
+#define SPH_CODE_OUTIGNORE 0x4000u
+#define SPH_CODE_OUTMOVE 0x6000u
+#define SPH_CODE_OUTPOS 0x8000u
+#define SPH_CODE_OUTRHOP 0xA000u
+#define SPH_CODE_MASKTYPE 0x1800u
+#define SPH_CODE_TYPE_FIXED 0x0u
+#define SPH_CODE_TYPE_MOVING 0x800u
+#define SPH_CODE_TYPE_FLOATING 0x1000u
+#define SPH_CODE_TYPE_FLUID 0x1800u
+
+/*
+ * Case definition: what JSph::LoadCaseConfig and JSph::LoadCaseParticles read
+ * from <case>.xml/<case>.bi4 (JSph.cpp:567-583 constants, :588-760 parameters,
+ * :2051-2076 map limits).  Floating-point members are given as the XML text
+ * parses them (double); sph_case_derive narrows them exactly as JSph does.
+ */
+typedef struct SphCaseDef {
+  double dp;                /* <dp>                                        */
+  double h;                 /* <h>   -> KernelH (float)                    */
+  double cteb;              /* <b>   -> CteB (float)                       */
+  double rhop0;             /* <rhop0>                                     */
+  double gamma;             /* <gamma>                                     */
+  double massbound, massfluid;
+  double gravity[3];
+  double cflnumber;
+  int step_algorithm;       /* SPH_STEP_*                                  */
+  int verlet_steps;         /* VerletSteps (40)                            */
+  int kernel;               /* SPH_KERNEL_WENDLAND                         */
+  int tdensity;             /* SPH_DDT_*                                   */
+  double visco;             /* artificial viscosity alpha                  */
+  double viscoboundfactor;
+  double ddtvalue;
+  double coefdtmin;         /* CoefDtMin (0.05)                            */
+  double dtini, dtmin;      /* 0 => derived (JSph.cpp:1448-1449)           */
+  double rhopoutmin, rhopoutmax;
+  double map_realposmin[3]; /* MapRealPosMin (after border + domain config)*/
+  double map_realposmax[3]; /* MapRealPosMax                               */
+  int cellmode;             /* SPH_CELLMODE_FULL / _HALF                   */
+  int celldomfixed;         /* 1: cell domain = whole map (-cellfixed:1)   */
+  uint32_t npb;             /* boundary particles are the first npb        */
+  uint32_t np;              /* total particles                             */
+} SphCaseDef;
+
+/*
+ * Derived constants (StCteSph, DualSphDef.h:374-402, plus the interaction and
+ * divide constants of JSph/JSphCpu), in the precision the reference holds them.
+ */
+typedef struct SphConstants {
+  float kernelh, kernelsize, kernelsize2;
+  float awen, bwen;                 /* Wendland (FunSphKernel.h:191-202) */
+  float cteb, gamma, rhopzero, ovrhopzero;
+  float massfluid, massbound;
+  float gravity[3];
+  float eta2, ddtkh, ddtgz;
+  float visco, viscoboundfactor;
+  float rhopoutmin, rhopoutmax;
+  float scell, movlimit;
+  float pad0;
+  double cs0, cflnumber, dtini, dtmin, dp;
+  int tdensity, step_algorithm, verlet_steps, scelldiv;
+  double map_realposmin[3], map_realsize[3];
+  double dom_posmin[3];             /* DomPosMin = Map_PosMin (single domain) */
+  uint32_t dom_cells[3];            /* Map_Cells = DomCells                   */
+  uint32_t dom_cellcode;            /* DomCellCode (JDsDcell.cpp:64-69)       */
+} SphConstants;
+
+/* Step statistics kept on the device and read back on demand. */
+typedef struct SphRunStats {
+  double time;            /* simulated time TimeStep                        */
+  double last_dt;         /* last dt                                        */
+  double sym_dtpre;       /* SymplecticDtPre                                */
+  uint64_t nstep;         /* steps done                                     */
+  uint32_t np, npb, npbok;/* current counts after the last divide           */
+  uint32_t nout;          /* fluid particles excluded so far                */
+  uint32_t dtmodif;       /* dt clamped to DtMin (JSphCpu.cpp:1623-1629)    */
+  uint32_t error_flags;   /* bit0: NaN/inf dt, bit1: boundary out           */
+  float velmax, acemax, viscdtmax; /* of the last interaction              */
+  float pad;
+} SphRunStats;
+
+/* Host particle view (SaveData layout: JSph::SaveData, JSph.cpp:2717). */
+typedef struct SphParticlesHost {
+  uint32_t n;
+  uint32_t* idp;        /* [n]    */
+  double* pos;          /* [n][3] */
+  float* vel;           /* [n][3] */
+  float* rhop;          /* [n]    */
+  uint16_t* code;       /* [n] (may be NULL on download) */
+} SphParticlesHost;
+
+/* Interaction outputs for kernel-level parity checks (StInterResultc + arrays). */
+typedef struct SphInterOut {
+  float* ar;      /* host [np]    density derivative (incl. DDT)            */
+  float* ace;     /* host [np][3] acceleration (without gravity)            */
+  float viscdtmax, velmax, acemax;
+} SphInterOut;
+
+typedef struct SphSolver SphSolver;
+
+/* ---- library ----------------------------------------------------------- */
+int sph_abi_version(void);
+const char* sph_last_error(void);
+
+/* ---- configuration ----------------------------------------------------- */
+int sph_case_derive(const SphCaseDef* cdef, SphConstants* out);
+
+/* ---- solver lifetime (device id = HIP device ordinal) ------------------- */
+int sph_solver_create(const SphCaseDef* cdef, const SphParticlesHost* init, int device, SphSolver** out);
+int sph_solver_destroy(SphSolver* s);
+
+/* ---- hot path: individual phases (all async on the solver stream) -------- */
+int sph_divide(SphSolver* s);                       /* RunCellDivide(true)        */
+int sph_interaction_forces(SphSolver* s, int interstep); /* 1 Verlet, 2 SymPre, 3 SymCor */
+int sph_compute_dt(SphSolver* s, int final_);       /* DtVariable(final)          */
+int sph_step_verlet(SphSolver* s);                  /* ComputeVerlet(dt)          */
+int sph_step_symplectic_pre(SphSolver* s);          /* ComputeSymplecticPre(dt)   */
+int sph_step_symplectic_cor(SphSolver* s);          /* ComputeSymplecticCorr(dt)  */
+
+/* ---- hot path: whole steps (ComputeStep + RunCellDivide), device-resident -- */
+int sph_solver_run(SphSolver* s, uint32_t nsteps);
+int sph_solver_sync(SphSolver* s);
+int sph_solver_stats(SphSolver* s, SphRunStats* out);
+/* Per-step dt trace (host array of length >= nsteps done); returns count.   */
+int sph_solver_dt_trace(SphSolver* s, double* out, uint32_t cap, uint32_t* count);
+
+/* ---- data out ------------------------------------------------------------ */
+int sph_download_particles(SphSolver* s, SphParticlesHost* out);
+int sph_download_interaction(SphSolver* s, SphInterOut* out);
+
+/* ---- measurement ----------------------------------------------------------- */
+/* Pair counts of one interaction pass (JDsPips): checked & real pairs for
+ * fluid-fluid, fluid-bound and bound-fluid.  out[6] = {ff_chk, ff_real,
+ * fb_chk, fb_real, bf_chk, bf_real}. */
+int sph_count_pairs(SphSolver* s, uint64_t out[6]);
+/* Average device time (ms) of the last timed region's kernels, by phase:
+ * out[0]=interaction, [1]=update, [2]=divide, [3]=dt/reductions. */
+int sph_solver_set_timing(SphSolver* s, int enabled);
+int sph_solver_timing(SphSolver* s, double out_ms[4], uint64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPHCORE_H */

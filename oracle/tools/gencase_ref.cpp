@@ -1,0 +1,107 @@
+// gencase_ref — dam-break case writer for the REFERENCE solver (test infrastructure).
+//
+// GenCase is a missing blob in the reference, so this tool writes
+// the <case>.xml + <case>.bi4 pair that JSphCpuSingle loads (JSph::LoadCaseConfig,
+// JSph.cpp:923; JPartsLoad4::LoadParticles, JPartsLoad4.cpp:151-252).  The .bi4 is
+// written through the reference's own JPartDataBi4 (JPartDataBi4.cpp:183-237,305-378,429).
+//
+// The lattice/constants are the SURVEY §8(c) recipe, restated independently in
+// dualsphysics_multilayer_amd/case_dambreak.py (the product-side generator); a CPU
+// test checks that both produce the same particles bit for bit.
+//
+// usage: gencase_ref <dp> <outdir> <step:1=Verlet|2=Symplectic> <ddt:0..3> [timemax] [casename]
+#include "JPartDataBi4.h"
+#include "Functions.h"
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+int main(int argc, char** argv) {
+  if (argc < 5) {
+    fprintf(stderr, "usage: %s dp outdir step ddt [timemax] [casename]\n", argv[0]);
+    return 1;
+  }
+  const double dp = atof(argv[1]);
+  const std::string dir = argv[2];
+  const int step = atoi(argv[3]);
+  const int ddt = atoi(argv[4]);
+  const double tmax = (argc > 5 ? atof(argv[5]) : 1.5);
+  const std::string name = (argc > 6 ? argv[6] : "CaseDambreak");
+
+  // Tank 1.6 x 0.67 x 0.4 (walls: bottom, x=0, x=L, y=0, y=W); water 0.4 x 0.67 x 0.3.
+  const int nx = int(std::round(1.6 / dp)), ny = int(std::round(0.67 / dp)), nz = int(std::round(0.4 / dp));
+  const int mx = int(std::round(0.4 / dp)), my = int(std::round(0.67 / dp)), mz = int(std::round(0.3 / dp));
+  std::vector<tdouble3> pos;
+  for (int k = 0; k <= nz; k++)
+    for (int j = 0; j <= ny; j++)
+      for (int i = 0; i <= nx; i++)
+        if (k == 0 || i == 0 || i == nx || j == 0 || j == ny) pos.push_back(TDouble3(i * dp, j * dp, k * dp));
+  const unsigned nb = unsigned(pos.size());
+  for (int k = 1; k <= mz; k++)
+    for (int j = 1; j < my; j++)
+      for (int i = 1; i <= mx; i++) pos.push_back(TDouble3(i * dp, j * dp, k * dp));
+  const unsigned np = unsigned(pos.size()), nf = np - nb;
+
+  const double g = 9.81, rho0 = 1000., gamma = 7., coefsound = 20., coefh = 1.0;
+  const double hswl = mz * dp;
+  const double cs0 = coefsound * std::sqrt(g * hswl);
+  const double b = cs0 * cs0 * rho0 / gamma;
+  const double h = coefh * std::sqrt(3. * dp * dp);
+  const double mass = rho0 * dp * dp * dp;
+
+  std::vector<unsigned> idp(np);
+  std::vector<tfloat3> vel(np, TFloat3(0));
+  std::vector<float> rhop(np);
+  tdouble3 pmin = TDouble3(DBL_MAX), pmax = TDouble3(-DBL_MAX);
+  for (unsigned p = 0; p < np; p++) {
+    idp[p] = p;
+    rhop[p] = (p < nb ? float(rho0) : float(rho0 * std::pow(1. + rho0 * g * (hswl - pos[p].z) / b, 1. / gamma)));
+    pmin = MinValues(pmin, pos[p]);
+    pmax = MaxValues(pmax, pos[p]);
+  }
+
+  JPartDataBi4 pd;
+  pd.ConfigBasic(0, 1, "gencase_ref", "gencase_ref", name, false, 0, dir);
+  pd.ConfigParticles(np, nb, 0, 0, nf, pmin, pmax, false, false);
+  pd.ConfigCtes(dp, h, b, rho0, gamma, mass, mass);
+  pd.AddPartInfo(0, 0, np, 0, 0, 0, pmin, pmax, 0, 0);
+  pd.AddPartData(np, idp.data(), pos.data(), vel.data(), rhop.data());
+  pd.SaveFileCase(name);
+
+  FILE* f = fopen((dir + "/" + name + ".xml").c_str(), "w");
+  if (!f) { perror("xml"); return 2; }
+  fprintf(f, "<?xml version=\"1.0\" encoding=\"UTF-8\" ?>\n<case app=\"gencase_ref\">\n<execution>\n<constants>\n");
+  fprintf(f, "<data2d value=\"false\"/>\n<gravity x=\"0\" y=\"0\" z=\"%g\"/>\n<cflnumber value=\"0.2\"/>\n", -g);
+  fprintf(f, "<gamma value=\"%g\"/>\n<rhop0 value=\"%g\"/>\n<dp value=\"%.10g\"/>\n", gamma, rho0, dp);
+  fprintf(f, "<h value=\"%.10E\"/>\n<b value=\"%.10E\"/>\n<massbound value=\"%.10E\"/>\n<massfluid value=\"%.10E\"/>\n", h, b, mass, mass);
+  fprintf(f, "</constants>\n<particles np=\"%u\" nb=\"%u\" nbf=\"%u\" mkboundfirst=\"10\" mkfluidfirst=\"0\">\n", np, nb, nb);
+  fprintf(f, "<fixed mkbound=\"0\" mk=\"10\" begin=\"0\" count=\"%u\"/>\n<fluid mkfluid=\"0\" mk=\"0\" begin=\"%u\" count=\"%u\"/>\n</particles>\n", nb, nb, nf);
+  fprintf(f, "<parameters>\n");
+  auto par = [&](const char* k, const std::string& v) { fprintf(f, "<parameter key=\"%s\" value=\"%s\"/>\n", k, v.c_str()); };
+  par("StepAlgorithm", std::to_string(step));
+  par("VerletSteps", "40");
+  par("Kernel", "2");
+  par("ViscoTreatment", "1");
+  par("Visco", "0.1");
+  par("ViscoBoundFactor", "1");
+  par("DensityDT", std::to_string(ddt));
+  par("DensityDTvalue", "0.1");
+  par("Shifting", "0");
+  par("RigidAlgorithm", "1");
+  par("CoefDtMin", "0.05");
+  par("DtIni", "0");
+  par("DtMin", "0");
+  par("TimeMax", fun::DoubleStr(tmax));
+  par("TimeOut", "0.01");
+  par("PartsOutMax", "1");
+  par("RhopOutMin", "700");
+  par("RhopOutMax", "1300");
+  fprintf(f, "<simulationdomain><posmin x=\"default\" y=\"default\" z=\"default\"/>"
+             "<posmax x=\"default\" y=\"default\" z=\"default + 50%%\"/></simulationdomain>\n");
+  fprintf(f, "</parameters>\n</execution>\n</case>\n");
+  fclose(f);
+  printf("np=%u nb=%u nf=%u h=%.10g b=%.10g cs0=%.10g mass=%.10g\n", np, nb, nf, h, b, cs0, mass);
+  return 0;
+}

@@ -1,0 +1,32 @@
+"""Loader for the golden fixtures written by tests/golden/make_golden.py."""
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"))
+
+
+def steps(g):
+    return sorted(int(k[1:].split("_")[0]) for k in g.files if k.endswith("_idp"))
+
+
+def snapshot(g, step):
+    return {k: g["s%d_%s" % (step, k)] for k in ("idp", "pos", "vel", "rhop", "time")}
+
+
+def meta(g):
+    dp, step, ddt, nsteps = g["meta"]
+    return float(dp), int(step), int(ddt), int(nsteps)
+
+
+def by_idp(p):
+    o = np.argsort(p["idp"], kind="stable")
+    return {k: (v[o] if isinstance(v, np.ndarray) and v.ndim >= 1 and len(v) == len(o) else v) for k, v in p.items()}
+
+
+def maxdiff(a, b, key):
+    return float(np.abs(a[key].astype(np.float64) - b[key].astype(np.float64)).max())

@@ -1,0 +1,69 @@
+"""Pins the CPU oracle (oracle/sph_oracle.cpp) to the REFERENCE solver's own output.
+
+Fixtures: PART files written by DualSPHysics v5.2 CPU built from the reference
+sources (oracle/Makefile), converted by tests/golden/make_golden.py.
+
+Tolerances: SURVEY.md §4 measured the reference's own rounding-noise floor
+(-ffast-math vs strict IEEE build of the same code, 17,295 particles): step 1
+|dv| 2.2e-6; step 100 |dx| 1.9e-7 m, |dv| 1.8e-5 m/s, |drho| 1.5e-3 kg/m3.
+The oracle must stay inside 2x that floor (it is built with the same flags).
+"""
+import numpy as np
+import pytest
+
+from golden_io import by_idp, load, maxdiff, meta, snapshot, steps
+
+from dualsphysics_multilayer_amd.case import DamBreakCase
+
+oracle = pytest.importorskip("oracle.pyoracle")
+
+CASES = ["verlet_ddt2_dp0.02", "symplectic_ddt1_dp0.025", "verlet_ddtnone_dp0.025", "symplectic_ddt3_dp0.03"]
+
+
+def tol(step):
+    # (pos m, vel m/s, rhop kg/m3): 2x the measured noise floor, interpolated in step count.
+    if step <= 1:
+        return 1e-8, 6e-6, 2e-3
+    if step <= 20:
+        return 2e-8, 1e-5, 4e-3
+    return 4e-7, 4e-5, 4e-3
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_matches_reference_parts(name):
+    g = load(name)
+    dp, step_alg, ddt, _ = meta(g)
+    case = DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt)
+    s = oracle.OracleSolver(case, nthreads=4)
+    done = 0
+    for k in steps(g):
+        s.run(k - done)
+        done = k
+        ref = snapshot(g, k)
+        got = by_idp(s.particles())
+        assert np.array_equal(got["idp"], ref["idp"]), "excluded-particle set differs"
+        tp, tv, tr = tol(k)
+        assert maxdiff(got, ref, "pos") <= tp, (k, maxdiff(got, ref, "pos"))
+        assert maxdiff(got, ref, "vel") <= tv, (k, maxdiff(got, ref, "vel"))
+        assert maxdiff(got, ref, "rhop") <= tr, (k, maxdiff(got, ref, "rhop"))
+        assert abs(s.stats()["time"] - float(ref["time"])) <= 1e-9
+
+
+def test_oracle_dt_trace_57k():
+    g = load("verlet_ddt2_dp0.0127_dt")
+    dp, step_alg, ddt, nsteps = meta(g)
+    case = DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt)
+    s = oracle.OracleSolver(case, nthreads=8)
+    s.run(nsteps)
+    dt = s.dt_trace()
+    assert len(dt) == nsteps
+    assert np.abs(dt / g["dt"] - 1).max() < 2e-6
+
+
+def test_generator_matches_reference_initial_state():
+    import hashlib
+
+    g = load("verlet_ddt2_dp0.02")
+    case = DamBreakCase(0.02)
+    assert case.np == 17295 and case.npb == 7395
+    assert hashlib.sha256(case.pos.tobytes()).digest() == bytes(g["s0_sha_pos"])
