@@ -1,0 +1,216 @@
+"""Benchmark: particle-steps/s of the SPH hot path on the 1M-particle dam break.
+
+A "step" is one JSphGpuSingle::ComputeStep_Ver + RunCellDivide over the whole
+particle set (interaction, dt, Verlet update, cell sort) — BASELINE.json cfg2
+(3D dam break, 1,025,964 particles, WCSPH + artificial viscosity + DDT2, 1 GPU).
+Inputs are resident in HBM when the timed region starts.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--dp DP] [--no-cpu-baseline]
+
+For N>1 (torchrun, one process per GPU) every rank runs its own dam break of the
+same size (weak scaling, "replicas"); value = sum over ranks / max time.
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "particle-steps/sec (whole node) + achieved HBM GB/s, dam-break 1M/10M"
+PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 vector (= FP32 MFMA) peak, MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+# Algorithmic work model: FP32 ops per fluid pair.
+FLOP_REAL_FLUID_PAIR = 135
+FLOP_REJECTED_CANDIDATE = 22
+FLOP_REAL_BOUND_PAIR = 45  # bound p1: kernel fac + continuity + visc-dt only
+BYTES_PER_PARTICLE_STEP = {1: 356, 2: 712}  # Verlet / Symplectic, SURVEY.md §8(d)
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def reference_cpu_baseline(dp: float, nsteps: int, threads: int) -> dict | None:
+    """Times the REFERENCE CPU solver (oracle/_ref, built from the reference sources)
+    on the same dam break; Steps/s is the solver's own 'Steps per second' (step loop only)."""
+    ref = os.path.join(ROOT, "oracle", "_ref")
+    exe, gen = os.path.join(ref, "DualSPHysics5.2CPU_ref"), os.path.join(ref, "gencase_ref")
+    if not (os.path.exists(exe) and os.path.exists(gen)):
+        return None
+    tmp = tempfile.mkdtemp(prefix="sphref_")
+    try:
+        out = subprocess.run([gen, repr(dp), tmp, "1", "2"], capture_output=True, text=True, check=True).stdout
+        np_ = int(re.search(r"np=(\d+)", out).group(1))
+        subprocess.run([exe, os.path.join(tmp, "CaseDambreak"), os.path.join(tmp, "out"), "-nsteps:%d" % nsteps,
+                        "-sv:none", "-svres:0", "-ompthreads:%d" % threads], capture_output=True, text=True,
+                       check=True, timeout=600)
+        log = open(os.path.join(tmp, "out", "Run.out")).read()
+        sps = float(re.search(r"Steps per second\.*:\s*([0-9.eE+-]+)", log).group(1))
+        return {"value": sps * np_, "unit": "particle-steps/s", "cores": threads, "kind": "reference",
+                "sample": "reference DualSPHysics5.2 CPU (built from /root/reference sources, -O3 -fopenmp "
+                          "-ffast-math), %d-particle dam break, %d Verlet steps, -ompthreads:%d, "
+                          "'Steps per second' of Run.out" % (np_, nsteps, threads)}
+    except Exception as e:  # noqa: BLE001
+        sys.stderr.write("reference CPU baseline failed: %r\n" % (e,))
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def port_cpu_baseline(case, nsteps: int, threads: int) -> dict:
+    from oracle.pyoracle import OracleSolver
+
+    o = OracleSolver(case, nthreads=threads)
+    o.run(nsteps)
+    sec = o.run_seconds()
+    return {"value": case.np * nsteps / sec, "unit": "particle-steps/s", "cores": o.threads(), "kind": "port",
+            "sample": "oracle restatement of JSphCpu (C++/OpenMP, -O3 -ffast-math), %d particles, %d Verlet steps"
+                      % (case.np, nsteps)}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--dp", type=float, default=0.0045)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=8)
+    args = ap.parse_args()
+
+    rank, world, local = dist_env()
+    if args.gpus != world and world > 1:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    from dualsphysics_multilayer_amd.case import DamBreakCase
+    from dualsphysics_multilayer_amd.core import SphGpuSingle
+
+    case = DamBreakCase(args.dp)
+    s = SphGpuSingle(case, device=local)
+    s.run(args.warmup)
+    s.sync()
+    pairs0 = s.count_pairs()
+
+    def barrier():
+        if dist is not None:
+            import torch
+
+            t = torch.zeros(1, device="cuda:%d" % local)
+            dist.all_reduce(t)
+            torch.cuda.synchronize(local)
+
+    s.set_timing(True)
+    barrier()
+    s.sync()
+    t0 = time.perf_counter()
+    s.run(args.steps)
+    s.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    phase_ms, nlaunch = s.timing()
+    pairs1 = s.count_pairs()
+    st = s.stats()
+
+    units = float(st["np"]) * args.steps
+    if dist is not None:
+        import torch
+
+        v = torch.tensor([elapsed, units], dtype=torch.float64, device="cuda:%d" % local)
+        tmax = v[:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tot = v[1:].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        elapsed, units = float(tmax.item()), float(tot.item())
+
+    if rank == 0:
+        pairs = (pairs0.astype("float64") + pairs1.astype("float64")) / 2.0
+        ff_chk, ff_real, fb_chk, fb_real, bf_chk, bf_real = pairs
+        flops = (FLOP_REAL_FLUID_PAIR * (ff_real + fb_real) + FLOP_REJECTED_CANDIDATE * (ff_chk - ff_real + fb_chk - fb_real)
+                 + FLOP_REAL_BOUND_PAIR * bf_real + FLOP_REJECTED_CANDIDATE * (bf_chk - bf_real))
+        inter_ms = float(phase_ms[0])
+        achieved = flops / (inter_ms * 1e-3) / 1e12 if inter_ms > 0 else None
+        value = units / elapsed
+        hbm_achieved = value * BYTES_PER_PARTICLE_STEP[case.step_algorithm] / 1e9
+        res = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "particle-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 (f64 positions/time integration)",
+            "data": "synthetic: generated 3D dam-break lattice (SURVEY.md §8(c) recipe)",
+            "config": {
+                "workload": "BASELINE cfg2: 3D dam break, %d particles (dp=%g), Verlet, Wendland, artificial "
+                            "viscosity 0.1, DDT2 0.1, DBC, CFL 0.2, CellMode full" % (case.np, args.dp),
+                "np": case.np,
+                "npb": case.npb,
+                "parallelism": "replicas" if world > 1 else "single",
+            },
+            "roofline": {
+                "kernel": "k_interaction<DDT2> (Interaction_Forces)",
+                "bound": "mfma",
+                "bound_note": "FP32-VALU-bound pairwise kernel (no MFMA: irregular pairs); gfx950's FP32 vector "
+                              "peak equals its FP32 MFMA peak, 157.3 TFLOP/s",
+                "achieved": achieved,
+                "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": (achieved / PEAK_FP32_TFLOPS) if achieved else None,
+                "traffic": None,
+                "avg_launch_ms": inter_ms,
+                "launches": int(nlaunch),
+                "algorithmic_flop_per_launch": flops,
+                "pairs_per_launch": {"ff_checked": ff_chk, "ff_real": ff_real, "fb_checked": fb_chk,
+                                     "fb_real": fb_real, "bf_checked": bf_chk, "bf_real": bf_real},
+            },
+            "roofline_hbm_step": {
+                "bound": "hbm",
+                "achieved": hbm_achieved,
+                "peak": PEAK_HBM_GBS,
+                "unit": "GB/s",
+                "frac": hbm_achieved / PEAK_HBM_GBS,
+                "bytes_per_particle_step": BYTES_PER_PARTICLE_STEP[case.step_algorithm],
+            },
+            "phase_ms_per_call": {"interaction": float(phase_ms[0]), "update": float(phase_ms[1]),
+                                  "divide": float(phase_ms[2])},
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), 64)
+            cb = reference_cpu_baseline(args.dp, args.cpu_steps, threads)
+            if cb is None:
+                cb = port_cpu_baseline(case, args.cpu_steps, threads)
+            cb["gpu_over_cpu"] = value / cb["value"]
+            res["cpu_baseline"] = cb
+        print(json.dumps(res))
+    s.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

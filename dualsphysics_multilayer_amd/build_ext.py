@@ -1,0 +1,82 @@
+"""Builds the HIP core libsphcore.so for gfx950, in-tree (no JIT cache).
+
+Each translation unit is compiled separately (parallel) and linked with hipcc.
+The product library never links the oracle.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUTDIR = os.path.join(HERE, "lib")
+LIBNAME = "libsphcore.so"
+SOURCES = ["sph_divide.hip", "sph_interaction.hip", "sph_step.hip", "sph_solver.cpp", "sph_capi.cpp"]
+ARCH = os.environ.get("SPH_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found: the HIP core cannot be built")
+
+
+CXXFLAGS = [
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "--offload-arch=" + ARCH,
+    "-ffp-contract=fast",
+    "-munsafe-fp-atomics",
+    "-Wall",
+    "-Wno-unused-function",
+]
+
+
+def lib_path() -> str:
+    return os.path.join(OUTDIR, LIBNAME)
+
+
+def _stale(obj: str, src: str) -> bool:
+    if not os.path.exists(obj):
+        return True
+    deps = [src] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith((".hpp", ".h"))]
+    deps.append(os.path.join(os.path.dirname(HERE), "include", "sphcore.h"))
+    return os.path.getmtime(obj) < max(os.path.getmtime(d) for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(os.path.join(OUTDIR, "obj"), exist_ok=True)
+    cc = hipcc()
+    objs = []
+    jobs = []
+    for s in SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(OUTDIR, "obj", s + ".o")
+        objs.append(obj)
+        if force or _stale(obj, src):
+            lang = ["-x", "hip"] if s.endswith(".hip") else []
+            jobs.append([cc] + CXXFLAGS + lang + ["-c", src, "-o", obj])
+    if jobs:
+        with cf.ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
+            for cmd, r in zip(jobs, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs)):
+                if verbose or r.returncode:
+                    sys.stderr.write(" ".join(cmd) + "\n" + r.stdout + r.stderr)
+                if r.returncode:
+                    raise RuntimeError("HIP compile failed: %s" % cmd[-3])
+    out = lib_path()
+    if jobs or not os.path.exists(out):
+        cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode:
+            raise RuntimeError("link failed:\n" + r.stdout + r.stderr)
+    return out
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv))

@@ -1,0 +1,198 @@
+"""Host-side mirror of the reference solver interface over the HIP core (C-ABI).
+
+``SphGpuSingle`` follows ``JSphGpuSingle`` (JSphGpuSingle.h:35): the same phase
+names (``RunCellDivide``, ``Interaction_Forces``, ``DtVariable``,
+``ComputeVerlet``, ``ComputeSymplecticPre/Corr``, ``ComputeStep``, ``Run``),
+the same fail-fast behaviour (a non-zero status raises ``SphError`` carrying the
+core's message, as ``Check_CudaErroor`` raises ``JException``,
+RunExceptionGpuDef.h:27) and the same data out (``ParticlesDataDown`` feeding
+SaveData).  Everything executes in ``libsphcore.so``; there is no CPU fallback:
+if the library or a HIP device is missing, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from ._abi import (
+    SPH_ABI_VERSION,
+    SPH_STATUS,
+    HostParticles,
+    SphCaseDef,
+    SphConstants,
+    SphInterOut,
+    SphRunStats,
+)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libsphcore.so")
+
+INTERSTEP_VERLET, INTERSTEP_SYMPREDICTOR, INTERSTEP_SYMCORRECTOR = 1, 2, 3
+
+EXPORTED_SYMBOLS = (
+    "sph_abi_version",
+    "sph_last_error",
+    "sph_case_derive",
+    "sph_solver_create",
+    "sph_solver_destroy",
+    "sph_divide",
+    "sph_interaction_forces",
+    "sph_compute_dt",
+    "sph_step_verlet",
+    "sph_step_symplectic_pre",
+    "sph_step_symplectic_cor",
+    "sph_solver_run",
+    "sph_solver_sync",
+    "sph_solver_stats",
+    "sph_solver_dt_trace",
+    "sph_download_particles",
+    "sph_download_interaction",
+    "sph_count_pairs",
+    "sph_solver_set_timing",
+    "sph_solver_timing",
+)
+
+
+class SphError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__("%s: %s" % (SPH_STATUS.get(status, status), msg))
+        self.status = status
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Loads libsphcore.so (no compute happens here; works without a GPU)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SphError(3, "HIP core %s is not built (run __graft_entry__.build())" % path)
+    L = C.CDLL(path)
+    vp = C.c_void_p
+    L.sph_abi_version.restype = C.c_int
+    L.sph_last_error.restype = C.c_char_p
+    L.sph_case_derive.argtypes = [C.POINTER(SphCaseDef), C.POINTER(SphConstants)]
+    L.sph_solver_create.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.POINTER(vp)]
+    for name in ("sph_solver_destroy", "sph_divide", "sph_step_verlet", "sph_step_symplectic_pre",
+                 "sph_step_symplectic_cor", "sph_solver_sync"):
+        getattr(L, name).argtypes = [vp]
+    L.sph_interaction_forces.argtypes = [vp, C.c_int]
+    L.sph_compute_dt.argtypes = [vp, C.c_int]
+    L.sph_solver_run.argtypes = [vp, C.c_uint32]
+    L.sph_solver_stats.argtypes = [vp, C.POINTER(SphRunStats)]
+    L.sph_solver_dt_trace.argtypes = [vp, C.POINTER(C.c_double), C.c_uint32, C.POINTER(C.c_uint32)]
+    L.sph_download_particles.argtypes = [vp, vp]
+    L.sph_download_interaction.argtypes = [vp, C.POINTER(SphInterOut)]
+    L.sph_count_pairs.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.sph_solver_set_timing.argtypes = [vp, C.c_int]
+    L.sph_solver_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
+    if L.sph_abi_version() != SPH_ABI_VERSION:
+        raise SphError(3, "ABI version mismatch")
+    _lib = L
+    return L
+
+
+def _check(r: int) -> None:
+    if r != 0:
+        raise SphError(r, load_library().sph_last_error().decode())
+
+
+def case_derive(case_def: dict) -> dict:
+    """JSph::ConfigConstants1/2 + cell division through the core (no GPU needed)."""
+    k = SphConstants()
+    _check(load_library().sph_case_derive(C.byref(SphCaseDef.from_dict(case_def)), C.byref(k)))
+    return k.as_dict()
+
+
+class SphGpuSingle:
+    """One MI355X running one domain: the JSphGpuSingle of this core."""
+
+    def __init__(self, case, device: int = 0):
+        L = load_library()
+        self.case = case
+        self._cdef = SphCaseDef.from_dict(case.case_def())
+        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop)
+        h = C.c_void_p()
+        _check(L.sph_solver_create(C.byref(self._cdef), C.byref(init.view), device, C.byref(h)))
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            load_library().sph_solver_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- phases (JSphGpuSingle names) --------------------------------------
+    def RunCellDivide(self) -> None:
+        _check(load_library().sph_divide(self._h))
+
+    def Interaction_Forces(self, interstep: int = INTERSTEP_VERLET) -> None:
+        _check(load_library().sph_interaction_forces(self._h, interstep))
+
+    def ComputeVerlet(self) -> None:
+        _check(load_library().sph_step_verlet(self._h))
+
+    def ComputeSymplecticPre(self) -> None:
+        _check(load_library().sph_step_symplectic_pre(self._h))
+
+    def ComputeSymplecticCorr(self) -> None:
+        _check(load_library().sph_step_symplectic_cor(self._h))
+
+    def Run(self, nsteps: int) -> None:
+        """nsteps x (ComputeStep + RunCellDivide); asynchronous until sync()."""
+        _check(load_library().sph_solver_run(self._h, nsteps))
+
+    run = Run
+
+    def sync(self) -> None:
+        _check(load_library().sph_solver_sync(self._h))
+
+    # -- data out ---------------------------------------------------------
+    def stats(self) -> dict:
+        s = SphRunStats()
+        _check(load_library().sph_solver_stats(self._h, C.byref(s)))
+        return s.as_dict()
+
+    def dt_trace(self) -> np.ndarray:
+        cnt = C.c_uint32()
+        _check(load_library().sph_solver_dt_trace(self._h, None, 0, C.byref(cnt)))
+        out = np.zeros(cnt.value, np.float64)
+        _check(load_library().sph_solver_dt_trace(self._h, out.ctypes.data_as(C.POINTER(C.c_double)), cnt.value,
+                                                  C.byref(cnt)))
+        return out
+
+    def particles(self) -> dict:
+        hp = HostParticles(self.case.np)
+        _check(load_library().sph_download_particles(self._h, C.byref(hp.view)))
+        return hp.trimmed(hp.view.n)
+
+    def interaction(self) -> dict:
+        n = self.stats()["np"]
+        ar = np.zeros(n, np.float32)
+        ace = np.zeros((n, 3), np.float32)
+        out = SphInterOut(ar.ctypes.data_as(C.POINTER(C.c_float)), ace.ctypes.data_as(C.POINTER(C.c_float)), 0, 0, 0)
+        _check(load_library().sph_download_interaction(self._h, C.byref(out)))
+        return dict(ar=ar, ace=ace, viscdtmax=out.viscdtmax, velmax=out.velmax, acemax=out.acemax)
+
+    def count_pairs(self) -> np.ndarray:
+        out = np.zeros(6, np.uint64)
+        _check(load_library().sph_count_pairs(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64))))
+        return out
+
+    def set_timing(self, on: bool) -> None:
+        _check(load_library().sph_solver_set_timing(self._h, int(on)))
+
+    def timing(self) -> tuple[np.ndarray, int]:
+        ms = np.zeros(4, np.float64)
+        n = C.c_uint64()
+        _check(load_library().sph_solver_timing(self._h, ms.ctypes.data_as(C.POINTER(C.c_double)), C.byref(n)))
+        return ms, n.value

@@ -1,0 +1,93 @@
+// sph_device.hpp — device-side data layout and helpers of the MI355X SPH core.
+//
+// Layout in HBM (all arrays in cell-sorted order, SoA, 16-B aligned):
+//   idp      u32     particle id                     (Idpg)
+//   code     u16     type/special bits (DualSphDef.h:161-221)
+//   dcell    u32     DCEL cell code (JDsDcellDef.h:24-43)
+//   posxy    double2 x,y   } positions in double (JSphGpu posxy/posz)
+//   posz     double  z     }
+//   velrhop  float4  vx,vy,vz,rho
+//   poscell  float4  position relative to the origin of its cell (float), w = dcell bits
+//   press    float   EOS pressure (FunSphEos.h:37-47), computed once per divide
+//   arace    float4  ace.x, ace.y, ace.z, ar  — interaction output (fused ar+ace)
+// Time-integration extras: velrhopm1 (Verlet), posxypre/poszpre/velrhoppre (Symplectic).
+// Device scalars (counts, maxima, dt, time) live in DevScalars so a whole step runs
+// without a host round trip (the reference does >=6 blocking DtoH copies per step,
+// SURVEY.md §3.2).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sphx {
+
+typedef uint16_t typecode;
+
+constexpr typecode CODE_MASKSPECIAL = 0xe000, CODE_OUTIGNORE = 0x4000, CODE_OUTMOVE = 0x6000,
+                   CODE_OUTPOS = 0x8000, CODE_OUTRHOP = 0xA000, CODE_MASKTYPE = 0x1800,
+                   CODE_TYPE_FLOATING = 0x1000, CODE_TYPE_FLUID = 0x1800;
+constexpr float ALMOSTZERO = 1e-18f;  // DualSphDef.h:132
+
+__host__ __device__ inline typecode CodeSpecial(typecode c) { return c & CODE_MASKSPECIAL; }
+__host__ __device__ inline typecode CodeType(typecode c) { return c & CODE_MASKTYPE; }
+__host__ __device__ inline typecode CodeSetNormal(typecode c) { return c & typecode(~CODE_MASKSPECIAL); }
+__host__ __device__ inline bool CodeIsNormal(typecode c) { return CodeSpecial(c) == 0; }
+__host__ __device__ inline bool CodeIsFluid(typecode c) { return CodeType(c) == CODE_TYPE_FLUID; }
+__host__ __device__ inline bool CodeIsOutRhop(typecode c) { return CodeSpecial(c) == CODE_OUTRHOP; }
+
+// DCEL decoding (JDsDcellDef.h:36-39).
+__host__ __device__ inline unsigned DcelCellx(unsigned dcc, unsigned cel) { return cel >> ((dcc >> 10) & 31); }
+__host__ __device__ inline unsigned DcelCelly(unsigned dcc, unsigned cel) { return (cel << (dcc >> 25)) >> ((dcc >> 5) & 31); }
+__host__ __device__ inline unsigned DcelCellz(unsigned dcc, unsigned cel) { return (cel << (dcc & 31)) >> (dcc & 31); }
+__host__ __device__ inline unsigned DcelCell(unsigned dcc, unsigned cx, unsigned cy, unsigned cz) {
+  return (cx << ((dcc >> 10) & 31)) | (cy << ((dcc >> 15) & 31)) | cz;
+}
+
+// Constants passed by value to every kernel (the reference's __constant__ CTE,
+// JSphGpu_ker.cu:180-182, uploaded by cudaMemcpyToSymbol; here kernarg-resident).
+struct KConst {
+  float kernelh, kernelsize2, bwen, ovkernelh;
+  float cteb, gamma, rhopzero, ovrhopzero;
+  float massfluid, massbound, eta2, ddtkh;
+  float ddtgz, cs0f, visco, viscobound;
+  float scell, movlimit, rhopoutmin, rhopoutmax;
+  float gravx, gravy, gravz, ovgamma;
+  double gravxd, gravyd, gravzd;
+  double map_realposmin_x, map_realposmin_y, map_realposmin_z;
+  double map_realsize_x, map_realsize_y, map_realsize_z;
+  double scelld;
+  unsigned domcellcode;
+  int tdensity;
+};
+
+// Cell grid of the (fixed) divide domain — StDivDataGpu (JCellDivDataGpu.h:26-79).
+struct DivGrid {
+  int ncx, ncy, ncz;
+  unsigned nsheet, nct;
+  unsigned boxboundignore, boxfluid, boxboundout, boxfluidout, boxboundoutignore, boxfluidoutignore;
+  unsigned nctt;  // size of begincell = 2*nct + 6
+};
+
+// Device-resident step scalars.
+struct DevScalars {
+  unsigned np, npb, npbok, nout;          // counts after the last divide
+  unsigned velmax2, acemax2, viscdt, pad; // float bits, max-reduced by atomicMax (values >= 0)
+  unsigned dtmodif, error_flags, npbout, ndiv;  // ndiv: particle count entering the divide
+  unsigned long long nstep;
+  double dt;        // dt of the step in flight
+  double time;      // simulated time TimeStep
+  double symdtpre;  // SymplecticDtPre
+  double ddt_p;     // predictor dt (Symplectic)
+  double last_dt;
+  float last_velmax, last_acemax, last_viscdt, pad3;
+};
+
+constexpr unsigned ERR_DT_NAN = 1u, ERR_BOUNDOUT = 2u;
+
+// Wave-level max of a non-negative float, then one atomicMax per wave.
+__device__ inline void wave_max_atomic(unsigned* dst, float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  if ((threadIdx.x & 63) == 0 && v > 0.f) atomicMax(dst, __float_as_uint(v));
+}
+
+}  // namespace sphx

@@ -1,0 +1,326 @@
+// sph_divide.hip — DivideGpu on CDNA4: cell keys, stable LSD radix sort, begincell,
+// fused gather + poscell + EOS pressure + VelMax.
+//
+// Reference behaviour (JCellDivGpuSingle::Divide, JCellDivGpuSingle.cpp:152-235;
+// CPU parity source JCellDivCpuSingle.cpp:134-344):
+//   * box key: bound cells [0,nct), BoundIgnore nct, fluid cells [nct+1, 2nct+1),
+//     then BoundOut, FluidOut, BoundOutIgnore, FluidOutIgnore (KerPreSortFull,
+//     JCellDivGpuSingle_ker.cu:41-102), cell index cx + cy*ncx + cz*nsheet (x fastest);
+//   * the order inside a box is the previous order (the CPU counting sort is stable,
+//     JCellDivCpuSingle.cpp:203-234), which fixes the neighbour summation order —
+//     so the sort here is a STABLE radix sort (the reference GPU leaves stability to
+//     thrust; -stable selects stable_sort_by_key, JCellDivGpu_ker.cu:116-124);
+//   * the cell domain is the whole map (CellDomFixed, -cellfixed:1): the box order is
+//     lexicographic in (z,y,x) either way, and bound particles outside a dynamic
+//     domain are never neighbours of fluid, so the interaction order is unchanged
+//     (checked on the oracle: tests/test_oracle_celldomfixed.py).  This removes the
+//     per-step DtoH read of the cell limits (cudiv::LimitsCell, 2 syncs per divide).
+#include "sph_kernels.hpp"
+
+namespace sphx {
+
+// ---------------------------------------------------------------------------------
+// PreSort (KerPreSortFull) — one thread per particle, bounded by the live count.
+__global__ __launch_bounds__(256) void k_presort(const DevScalars* __restrict__ sc, const unsigned* __restrict__ dcell,
+                                                 const typecode* __restrict__ code, DivGrid g, unsigned dcc,
+                                                 unsigned* __restrict__ keys, unsigned* __restrict__ vals) {
+  const unsigned n = sc->np;
+  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p == 0) const_cast<DevScalars*>(sc)->ndiv = n;
+  if (p >= n) return;
+  const unsigned rcell = dcell[p];
+  const unsigned cx = DcelCellx(dcc, rcell), cy = DcelCelly(dcc, rcell), cz = DcelCellz(dcc, rcell);
+  const unsigned cellsort = cx + cy * unsigned(g.ncx) + cz * g.nsheet;
+  const typecode rcode = code[p];
+  const typecode codetype = CodeType(rcode), codeout = CodeSpecial(rcode);
+  unsigned box;
+  if (codetype < CODE_TYPE_FLOATING) {
+    box = (codeout < CODE_OUTIGNORE
+               ? ((cx < unsigned(g.ncx) && cy < unsigned(g.ncy) && cz < unsigned(g.ncz)) ? cellsort : g.boxboundignore)
+               : (codeout == CODE_OUTIGNORE ? g.boxboundoutignore : g.boxboundout));
+  } else {
+    box = (codeout <= CODE_OUTIGNORE ? (codeout < CODE_OUTIGNORE ? g.boxfluid + cellsort : g.boxfluidoutignore)
+                                     : (codetype == CODE_TYPE_FLOATING ? g.boxboundout : g.boxfluidout));
+  }
+  keys[p] = box;
+  vals[p] = p;
+}
+
+void launch_presort(hipStream_t stm, unsigned cap, const DevScalars* sc, const unsigned* dcell, const typecode* code,
+                    DivGrid g, unsigned domcellcode, unsigned* keys, unsigned* vals) {
+  const unsigned nb = (cap + 255) / 256;
+  hipLaunchKernelGGL(k_presort, dim3(nb), dim3(256), 0, stm, sc, dcell, code, g, domcellcode, keys, vals);
+}
+
+// ---------------------------------------------------------------------------------
+// Stable LSD radix sort.  Per pass: tile histograms -> per-digit row scans ->
+// digit-total scan -> stable scatter (wave match via ballots + tagged LDS wave counts).
+__global__ __launch_bounds__(RS_BS) void k_rs_hist(const DevScalars* __restrict__ sc, const unsigned* __restrict__ keys,
+                                                   unsigned shift, unsigned rbits, unsigned ntiles,
+                                                   unsigned* __restrict__ hist) {
+  __shared__ unsigned cnt[1 << RS_MAXBITS];
+  const unsigned radix = 1u << rbits, mask = radix - 1;
+  for (unsigned d = threadIdx.x; d < radix; d += RS_BS) cnt[d] = 0;
+  __syncthreads();
+  const unsigned n = sc->ndiv;
+  const unsigned base = blockIdx.x * RS_TILE;
+#pragma unroll 4
+  for (int it = 0; it < RS_ITEMS; it++) {
+    const unsigned idx = base + it * RS_BS + threadIdx.x;
+    if (idx < n) atomicAdd(&cnt[(keys[idx] >> shift) & mask], 1u);
+  }
+  __syncthreads();
+  for (unsigned d = threadIdx.x; d < radix; d += RS_BS) hist[d * ntiles + blockIdx.x] = cnt[d];
+}
+
+// Exclusive scan of one digit row hist[d*ntiles .. +ntiles); row total to digtot[d].
+__global__ __launch_bounds__(256) void k_rs_scan_rows(unsigned* __restrict__ hist, unsigned ntiles,
+                                                      unsigned* __restrict__ digtot) {
+  __shared__ unsigned part[256];
+  unsigned* row = hist + size_t(blockIdx.x) * ntiles;
+  const unsigned per = (ntiles + 255) / 256;
+  const unsigned b0 = threadIdx.x * per, b1 = min(b0 + per, ntiles);
+  unsigned s = 0;
+  for (unsigned i = b0; i < b1; i++) s += row[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over 256 partials.
+  for (int off = 1; off < 256; off <<= 1) {
+    const unsigned v = (threadIdx.x >= unsigned(off) ? part[threadIdx.x - off] : 0u);
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  unsigned run = (threadIdx.x ? part[threadIdx.x - 1] : 0u);
+  for (unsigned i = b0; i < b1; i++) {
+    const unsigned v = row[i];
+    row[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == 255) digtot[blockIdx.x] = part[255];
+}
+
+// Exclusive scan of the digit totals (<= 2048 entries) in place.
+__global__ __launch_bounds__(256) void k_rs_scan_digits(unsigned* __restrict__ digtot, unsigned radix) {
+  __shared__ unsigned part[256];
+  const unsigned per = (radix + 255) / 256;
+  const unsigned b0 = threadIdx.x * per, b1 = min(b0 + per, radix);
+  unsigned s = 0;
+  for (unsigned i = b0; i < b1; i++) s += digtot[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const unsigned v = (threadIdx.x >= unsigned(off) ? part[threadIdx.x - off] : 0u);
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  unsigned run = (threadIdx.x ? part[threadIdx.x - 1] : 0u);
+  for (unsigned i = b0; i < b1; i++) {
+    const unsigned v = digtot[i];
+    digtot[i] = run;
+    run += v;
+  }
+}
+
+__global__ __launch_bounds__(RS_BS) void k_rs_scatter(const DevScalars* __restrict__ sc,
+                                                      const unsigned* __restrict__ kin, const unsigned* __restrict__ vin,
+                                                      unsigned* __restrict__ kout, unsigned* __restrict__ vout,
+                                                      unsigned shift, unsigned rbits, unsigned ntiles,
+                                                      const unsigned* __restrict__ hist,
+                                                      const unsigned* __restrict__ digtot) {
+  constexpr int NW = RS_BS / 64;
+  __shared__ unsigned s_off[1 << RS_MAXBITS];
+  __shared__ unsigned s_wc[NW][1 << RS_MAXBITS];
+  const unsigned radix = 1u << rbits, mask = radix - 1;
+  const unsigned n = sc->ndiv;
+  const unsigned base = blockIdx.x * RS_TILE;
+  if (base >= n) return;  // whole block uniform
+  for (unsigned d = threadIdx.x; d < radix; d += RS_BS) {
+    s_off[d] = digtot[d] + hist[d * ntiles + blockIdx.x];
+#pragma unroll
+    for (int w = 0; w < NW; w++) s_wc[w][d] = 0;
+  }
+  __syncthreads();
+  const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long lanemask_lt = (1ull << lane) - 1ull;
+  for (int it = 0; it < RS_ITEMS; it++) {
+    const unsigned idx = base + it * RS_BS + threadIdx.x;
+    const bool valid = idx < n;
+    const unsigned key = valid ? kin[idx] : 0u;
+    const unsigned val = valid ? vin[idx] : 0u;
+    const unsigned d = (key >> shift) & mask;
+    unsigned long long peers = __ballot(valid);
+    for (unsigned b = 0; b < rbits; b++) {
+      const bool bit = (d >> b) & 1u;
+      const unsigned long long bb = __ballot(bit);
+      peers &= (bit ? bb : ~bb);
+    }
+    const unsigned rank = __popcll(peers & lanemask_lt);
+    const unsigned cnt = __popcll(peers);
+    const bool leader = valid && (peers & lanemask_lt) == 0ull;
+    const unsigned tag = unsigned(it + 1) << 16;
+    if (leader) s_wc[w][d] = tag | cnt;
+    __syncthreads();
+    if (valid) {
+      unsigned pre = 0;
+      for (unsigned ww = 0; ww < w; ww++) {
+        const unsigned v = s_wc[ww][d];
+        if ((v & 0xffff0000u) == tag) pre += v & 0xffffu;
+      }
+      const unsigned pos = s_off[d] + pre + rank;
+      kout[pos] = key;
+      vout[pos] = val;
+    }
+    __syncthreads();
+    if (leader) {
+      bool last = true;
+      unsigned total = 0;
+      for (unsigned ww = 0; ww < NW; ww++) {
+        const unsigned v = s_wc[ww][d];
+        if ((v & 0xffff0000u) == tag) {
+          total += v & 0xffffu;
+          if (ww > w) last = false;
+        }
+      }
+      if (last) s_off[d] += total;
+    }
+    __syncthreads();
+  }
+}
+
+int launch_radix_sort(hipStream_t stm, unsigned cap, const DevScalars* sc, SortScratch& s, unsigned keybits) {
+  const unsigned passes = (keybits + RS_MAXBITS - 1) / RS_MAXBITS;
+  const unsigned rbits = (keybits + passes - 1) / passes;
+  const unsigned ntiles = (cap + RS_TILE - 1) / RS_TILE;
+  int cur = 0;
+  for (unsigned p = 0; p < passes; p++) {
+    const unsigned shift = p * rbits;
+    const unsigned radix = 1u << rbits;
+    hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(RS_BS), 0, stm, sc, s.keys[cur], shift, rbits, ntiles, s.hist);
+    hipLaunchKernelGGL(k_rs_scan_rows, dim3(radix), dim3(256), 0, stm, s.hist, ntiles, s.digtot);
+    hipLaunchKernelGGL(k_rs_scan_digits, dim3(1), dim3(256), 0, stm, s.digtot, radix);
+    hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(RS_BS), 0, stm, sc, s.keys[cur], s.vals[cur],
+                       s.keys[cur ^ 1], s.vals[cur ^ 1], shift, rbits, ntiles, s.hist, s.digtot);
+    cur ^= 1;
+  }
+  return cur;
+}
+
+// ---------------------------------------------------------------------------------
+// begincell[c] = first sorted index with key >= c (lower bound) for every box c.
+__device__ inline unsigned lower_bound_u32(const unsigned* __restrict__ a, unsigned n, unsigned v) {
+  unsigned lo = 0, hi = n;
+  while (lo < hi) {
+    const unsigned mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_begincell(DevScalars* __restrict__ sc, const unsigned* __restrict__ skeys,
+                                                   DivGrid g, unsigned* __restrict__ begincell) {
+  const unsigned n = sc->ndiv;
+  const unsigned c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < g.nctt) begincell[c] = lower_bound_u32(skeys, n, c);
+  if (c == 0) {
+    // JCellDivCpuSingle::Divide counts (JCellDivCpuSingle.cpp:330-339) + RunCellDivide (JSphCpuSingle.cpp:470-472).
+    const unsigned b_ignore = lower_bound_u32(skeys, n, g.boxboundignore);
+    const unsigned b_fluid = lower_bound_u32(skeys, n, g.boxfluid);
+    const unsigned b_bout = lower_bound_u32(skeys, n, g.boxboundout);
+    const unsigned b_fout = lower_bound_u32(skeys, n, g.boxfluidout);
+    const unsigned b_fout1 = lower_bound_u32(skeys, n, g.boxfluidout + 1);
+    sc->npbok = b_ignore;
+    sc->npb = b_fluid;
+    sc->np = b_bout;
+    sc->nout += b_fout1 - b_fout;
+    const unsigned npbout = b_fout - b_bout;
+    if (npbout) {
+      sc->npbout = npbout;
+      sc->error_flags |= ERR_BOUNDOUT;
+    }
+  }
+}
+
+void launch_begincell(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned* skeys, DivGrid g,
+                      unsigned* begincell) {
+  (void)cap;
+  const unsigned nb = (g.nctt + 255) / 256;
+  hipLaunchKernelGGL(k_begincell, dim3(nb), dim3(256), 0, stm, sc, skeys, g, begincell);
+}
+
+// ---------------------------------------------------------------------------------
+// Gather of every particle array + poscell + press + VelMax (fluid only).
+struct GatherArgs {
+  PartArrays src, dst;
+  const unsigned* sortpart;
+  float4* poscell;
+  float* press;
+  double posminx, posminy, posminz, scelld;
+  float cteb, ovrhopzero, gamma;
+  unsigned dcc;
+  int withm1, withpre;
+};
+
+__global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, GatherArgs a) {
+  const unsigned n = sc->np, npb = sc->npb;
+  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+  float v2 = 0.f;
+  if (i < n) {
+    const unsigned s = a.sortpart[i];
+    const unsigned dc = a.src.dcell[s];
+    const double2 pxy = a.src.posxy[s];
+    const double pz = a.src.posz[s];
+    const float4 vr = a.src.velrhop[s];
+    a.dst.idp[i] = a.src.idp[s];
+    a.dst.code[i] = a.src.code[s];
+    a.dst.dcell[i] = dc;
+    a.dst.posxy[i] = pxy;
+    a.dst.posz[i] = pz;
+    a.dst.velrhop[i] = vr;
+    if (a.withm1) a.dst.velrhopm1[i] = a.src.velrhopm1[s];
+    if (a.withpre) {
+      a.dst.posxypre[i] = a.src.posxypre[s];
+      a.dst.poszpre[i] = a.src.poszpre[s];
+      a.dst.velrhoppre[i] = a.src.velrhoppre[s];
+    }
+    // PosCell (KerUpdatePosCell): position relative to the origin of its divide cell.
+    const unsigned cx = DcelCellx(a.dcc, dc), cy = DcelCelly(a.dcc, dc), cz = DcelCellz(a.dcc, dc);
+    const double ox = a.posminx + double(cx) * a.scelld;
+    const double oy = a.posminy + double(cy) * a.scelld;
+    const double oz = a.posminz + double(cz) * a.scelld;
+    a.poscell[i] = make_float4(float(pxy.x - ox), float(pxy.y - oy), float(pz - oz), __uint_as_float(dc));
+    // Press (PreInteractionVars_Forces, JSphCpu.cpp:451-453; FunSphEos.h:37-47) as the
+    // reference binary evaluates it: the unqualified pow in namespace fsph is the C
+    // double pow, and -ffast-math makes rhop/rhop0 a product with 1/rhop0.
+    a.press[i] = float(double(a.cteb) * (pow(double(vr.w * a.ovrhopzero), double(a.gamma)) - 1.0));
+    if (i >= npb) v2 = vr.x * vr.x + vr.y * vr.y + vr.z * vr.z;  // CalcVelMaxOmp over fluid
+  }
+  wave_max_atomic(&sc->velmax2, v2);
+}
+
+void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned* sortpart, const PartArrays& src,
+                   const PartArrays& dst, bool withm1, bool withpre, const KConst& K, const double dom_posmin[3],
+                   float4* poscell, float* press) {
+  GatherArgs a;
+  a.src = src;
+  a.dst = dst;
+  a.sortpart = sortpart;
+  a.poscell = poscell;
+  a.press = press;
+  a.posminx = dom_posmin[0];
+  a.posminy = dom_posmin[1];
+  a.posminz = dom_posmin[2];
+  a.scelld = K.scelld;
+  a.cteb = K.cteb;
+  a.ovrhopzero = K.ovrhopzero;
+  a.gamma = K.gamma;
+  a.dcc = K.domcellcode;
+  a.withm1 = withm1;
+  a.withpre = withpre;
+  const unsigned nb = (cap + 255) / 256;
+  hipLaunchKernelGGL(k_gather, dim3(nb), dim3(256), 0, stm, sc, a);
+}
+
+}  // namespace sphx

@@ -1,0 +1,211 @@
+// sph_step.hip — dt control and time integration (Verlet, Symplectic) on CDNA4.
+//
+// dt (JSphCpu::DtVariable, JSphCpu.cpp:1614-1639; GPU JSphGpu.cpp:984-1013) is
+// computed ON THE DEVICE by one wave from the max-reduced VelMax, AceMax and
+// ViscDtMax, so the step needs none of the reference's blocking DtoH copies.
+// Update kernels follow JSphCpu.cpp:1240-1606 (double intermediates, float storage,
+// UpdatePos out-of-map / MovLimit / RhopOut exclusion) — GPU twins
+// KerComputeStepVerlet / KerComputeStepSymplecticPre/Cor / KerComputeStepPos
+// (JSphGpuSimple_ker.cu:129-450, JSphGpu_ker.cu:320-378,1598-1690).
+#include <cfloat>
+
+#include "sph_kernels.hpp"
+
+namespace sphx {
+
+__global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double dtmin, double cs0, int mode,
+                     double* __restrict__ dttrace, unsigned tracecap) {
+  if (threadIdx.x != 0) return;
+  const float velmaxf = sqrtf(__uint_as_float(sc->velmax2));  // CalcVelMaxOmp returns float sqrt
+  const double velmax = double(velmaxf);
+  const double acemax = sqrt(double(__uint_as_float(sc->acemax2)));
+  const float viscdt = __uint_as_float(sc->viscdt);
+  sc->last_velmax = velmaxf;
+  sc->last_acemax = float(acemax);
+  sc->last_viscdt = viscdt;
+  if (mode == DT_PEEK) return;
+  sc->velmax2 = 0u;
+  sc->acemax2 = 0u;
+  sc->viscdt = 0u;
+  const double kh = double(K.kernelh);
+  const double dt1 = (acemax ? sqrt(kh / acemax) : DBL_MAX);
+  const double dt2 = kh / (fmax(cs0, velmax * 10.) + kh * double(viscdt));
+  double dt = cfl * fmin(dt1, dt2);
+  if (isnan(dt) || isinf(dt)) {
+    sc->error_flags |= ERR_DT_NAN;
+    dt = dtmin;
+  }
+  if (dt < dtmin) {
+    dt = dtmin;
+    sc->dtmodif++;
+  }
+  if (mode == DT_VERLET) {
+    sc->dt = dt;
+  } else if (mode == DT_SYM_PRE) {
+    sc->ddt_p = dt;
+    sc->dt = sc->symdtpre;  // the step runs with SymplecticDtPre (JSphCpuSingle.cpp:696)
+  } else {                  // DT_SYM_COR
+    sc->symdtpre = fmin(sc->ddt_p, dt);  // JSphCpuSingle.cpp:719
+  }
+  if (mode != DT_SYM_COR) {
+    // Step bookkeeping: TimeStep+=stepdt (JSphCpuSingle.cpp:1099).
+    const double stepdt = sc->dt;
+    if (dttrace && tracecap) dttrace[sc->nstep % tracecap] = stepdt;
+    sc->time += stepdt;
+    sc->last_dt = stepdt;
+    sc->nstep++;
+  }
+}
+
+void launch_dt(hipStream_t stm, DevScalars* sc, const KConst& K, double cfl, double dtmin, double cs0, int mode,
+               double* dttrace, unsigned tracecap) {
+  hipLaunchKernelGGL(k_dt, dim3(1), dim3(64), 0, stm, sc, K, cfl, dtmin, cs0, mode, dttrace, tracecap);
+}
+
+// JSphCpu::UpdatePos (JSphCpu.cpp:1240-1293), single domain, no periodic/symmetry.
+__device__ __forceinline__ void update_pos(const KConst& K, double rx, double ry, double rz, double movx, double movy,
+                                           double movz, bool outrhop, unsigned p, const PartArrays& a) {
+  const bool outmove = (fabsf(float(movx)) > K.movlimit || fabsf(float(movy)) > K.movlimit ||
+                        fabsf(float(movz)) > K.movlimit);
+  rx += movx;
+  ry += movy;
+  rz += movz;
+  const double dx = rx - K.map_realposmin_x, dy = ry - K.map_realposmin_y, dz = rz - K.map_realposmin_z;
+  const bool out = (dx != dx || dy != dy || dz != dz || dx < 0 || dy < 0 || dz < 0 || dx >= K.map_realsize_x ||
+                    dy >= K.map_realsize_y || dz >= K.map_realsize_z);
+  a.posxy[p] = make_double2(rx, ry);
+  a.posz[p] = rz;
+  if (outrhop || outmove || out) {
+    typecode rcode = a.code[p];
+    if (out) rcode = CodeSetNormal(rcode) | CODE_OUTPOS;
+    else if (outrhop) rcode = CodeSetNormal(rcode) | CODE_OUTRHOP;
+    else rcode = CodeSetNormal(rcode) | CODE_OUTMOVE;
+    a.code[p] = rcode;
+    a.dcell[p] = 0xFFFFFFFFu;
+  } else {
+    const unsigned cx = unsigned(dx / K.scelld), cy = unsigned(dy / K.scelld), cz = unsigned(dz / K.scelld);
+    a.dcell[p] = DcelCell(K.domcellcode, cx, cy, cz);
+  }
+}
+
+// ComputeVerlet (JSphCpu.cpp:1381-1399): bound -> ComputeVelrhopBound, fluid -> ComputeVerletVarsFluid.
+// New values are written in velrhopm1 (the caller swaps velrhop/velrhopm1 afterwards).
+__global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ sc, KConst K, int euler,
+                                                const float4* __restrict__ arace, PartArrays a) {
+  const unsigned np = sc->np, npb = sc->npb;
+  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= np) return;
+  const double dt = sc->dt;
+  const double dt2 = (euler ? dt : dt + dt);
+  const float4 ra = arace[p];
+  const float4 vr2 = (euler ? a.velrhop[p] : a.velrhopm1[p]);
+  const float rhopnew = float(double(vr2.w) + dt2 * double(ra.w));
+  if (p < npb) {
+    a.velrhopm1[p] = make_float4(0.f, 0.f, 0.f, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
+    return;
+  }
+  const float4 vr1 = a.velrhop[p];
+  const double dt205 = 0.5 * dt * dt;
+  const double agx = double(ra.x) + K.gravxd, agy = double(ra.y) + K.gravyd, agz = double(ra.z) + K.gravzd;
+  const double dx = double(vr1.x) * dt + agx * dt205;
+  const double dy = double(vr1.y) * dt + agy * dt205;
+  const double dz = double(vr1.z) * dt + agz * dt205;
+  const bool outrhop = (rhopnew < K.rhopoutmin || rhopnew > K.rhopoutmax);
+  const float4 nv = make_float4(float(double(vr2.x) + agx * dt2), float(double(vr2.y) + agy * dt2),
+                                float(double(vr2.z) + agz * dt2), rhopnew);
+  const double2 pxy = a.posxy[p];
+  update_pos(K, pxy.x, pxy.y, a.posz[p], dx, dy, dz, outrhop, p, a);
+  a.velrhopm1[p] = nv;
+}
+
+void launch_verlet(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, bool euler, const float4* arace,
+                   PartArrays a) {
+  const unsigned nb = (cap + 255) / 256;
+  hipLaunchKernelGGL(k_verlet, dim3(nb), dim3(256), 0, stm, sc, K, int(euler), arace, a);
+}
+
+// ComputeSymplecticPre (JSphCpu.cpp:1406-1504).  The caller has already moved the
+// current pos/velrhop into the *pre arrays (pointer swap); new values go to pos/velrhop.
+__global__ __launch_bounds__(256) void k_sym_pre(const DevScalars* __restrict__ sc, KConst K,
+                                                 const float4* __restrict__ arace, PartArrays a) {
+  const unsigned np = sc->np, npb = sc->npb;
+  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= np) return;
+  const double dt = sc->dt, dt05 = dt * .5;
+  const float4 ra = arace[p];
+  const float4 vp = a.velrhoppre[p];
+  const float rhopnew = float(double(vp.w) + dt05 * double(ra.w));
+  const double2 pxy = a.posxypre[p];
+  const double pz = a.poszpre[p];
+  if (p < npb) {
+    a.velrhop[p] = make_float4(vp.x, vp.y, vp.z, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
+    a.posxy[p] = pxy;
+    a.posz[p] = pz;
+    return;
+  }
+  typecode rcode = a.code[p];
+  const double dx = double(vp.x) * dt05, dy = double(vp.y) * dt05, dz = double(vp.z) * dt05;
+  const bool outrhop = (rhopnew < K.rhopoutmin || rhopnew > K.rhopoutmax);
+  a.velrhop[p] = make_float4(float(double(vp.x) + (double(ra.x) + K.gravxd) * dt05),
+                             float(double(vp.y) + (double(ra.y) + K.gravyd) * dt05),
+                             float(double(vp.z) + (double(ra.z) + K.gravzd) * dt05), rhopnew);
+  if (outrhop && CodeIsNormal(rcode)) {
+    rcode = CodeSetNormal(rcode) | CODE_OUTRHOP;
+    a.code[p] = rcode;
+  }
+  if (CodeIsFluid(rcode)) update_pos(K, pxy.x, pxy.y, pz, dx, dy, dz, CodeIsOutRhop(rcode), p, a);
+  else {
+    a.posxy[p] = pxy;
+    a.posz[p] = pz;
+  }
+}
+
+void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a) {
+  const unsigned nb = (cap + 255) / 256;
+  hipLaunchKernelGGL(k_sym_pre, dim3(nb), dim3(256), 0, stm, sc, K, arace, a);
+}
+
+// ComputeSymplecticCorr (JSphCpu.cpp:1510-1606).
+__global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ sc, KConst K,
+                                                 const float4* __restrict__ arace, PartArrays a) {
+  const unsigned np = sc->np, npb = sc->npb;
+  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= np) return;
+  const double dt = sc->dt, dt05 = dt * .5;
+  const float4 ra = arace[p];
+  const float4 vr = a.velrhop[p];
+  const float4 vp = a.velrhoppre[p];
+  const double epsilon_rdot = (-double(ra.w) / double(vr.w)) * dt;
+  const float rhopnew = float(double(vp.w) * (2. - epsilon_rdot) / (2. + epsilon_rdot));
+  if (p < npb) {
+    a.velrhop[p] = make_float4(0.f, 0.f, 0.f, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
+    return;  // boundary keeps its position (already restored by the predictor)
+  }
+  typecode rcode = a.code[p];
+  const float4 nv = make_float4(float(double(vp.x) + (double(ra.x) + K.gravxd) * dt),
+                                float(double(vp.y) + (double(ra.y) + K.gravyd) * dt),
+                                float(double(vp.z) + (double(ra.z) + K.gravzd) * dt), rhopnew);
+  const double dx = (double(vp.x) + double(nv.x)) * dt05;
+  const double dy = (double(vp.y) + double(nv.y)) * dt05;
+  const double dz = (double(vp.z) + double(nv.z)) * dt05;
+  const bool outrhop = (rhopnew < K.rhopoutmin || rhopnew > K.rhopoutmax);
+  if (outrhop && CodeIsNormal(rcode)) {
+    rcode = CodeSetNormal(rcode) | CODE_OUTRHOP;
+    a.code[p] = rcode;
+  }
+  a.velrhop[p] = nv;
+  const double2 pxy = a.posxypre[p];
+  const double pz = a.poszpre[p];
+  if (CodeIsFluid(rcode)) update_pos(K, pxy.x, pxy.y, pz, dx, dy, dz, CodeIsOutRhop(rcode), p, a);
+  else {
+    a.posxy[p] = pxy;
+    a.posz[p] = pz;
+  }
+}
+
+void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a) {
+  const unsigned nb = (cap + 255) / 256;
+  hipLaunchKernelGGL(k_sym_cor, dim3(nb), dim3(256), 0, stm, sc, K, arace, a);
+}
+
+}  // namespace sphx

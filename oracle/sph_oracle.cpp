@@ -140,6 +140,15 @@ void Derive(const SphCaseDef& c, SphConstants& k) {
   if (!k.dom_cellcode) throw std::runtime_error("failed to select a valid CellCode");
 }
 
+// EOS as the reference binary evaluates it: FunSphEos.h:37-39 calls the unqualified
+// `pow` inside namespace fsph, which resolves to the C ::pow(double,double), and
+// -ffast-math turns rhop/rhop0 into rhop*(1/rhop0); so Press =
+// float(double(b)*(pow(double(rhop*(1/rhop0)),gamma)-1)).  With this the oracle is
+// BIT-IDENTICAL to the reference after the first step of the DDT-free case.  The pow
+// is kept out of line: if GCC vectorised the loop with libmvec, results would depend
+// on the OpenMP chunking (i.e. on the thread count).
+__attribute__((noinline)) double scalar_pow(double x, double y) { return std::pow(x, y); }
+
 // ---- Wendland kernel (FunSphKernel.h:217-224) and EOS (FunSphEos.h:37-47) -----------
 inline float WendlandFac(const SphConstants& k, float rr2) {
   const float rad = std::sqrt(rr2);
@@ -148,7 +157,7 @@ inline float WendlandFac(const SphConstants& k, float rr2) {
   return k.bwen * qq * wqq1 * wqq1 * wqq1 / rad;
 }
 inline float ComputePress(float rhop, const SphConstants& k) {
-  return k.cteb * (std::pow(rhop / k.rhopzero, k.gamma) - 1.0f);
+  return float(double(k.cteb) * (scalar_pow(double(rhop * k.ovrhopzero), double(k.gamma)) - 1.0f));
 }
 
 constexpr float ALMOSTZERO = 1e-18f;  // DualSphDef.h:132

@@ -1,0 +1,183 @@
+"""GPU parity: the HIP core (through the C-ABI) against the CPU oracle and the
+reference's own PART fixtures.
+
+Tolerances: the reference's rounding-noise floor is
+|dv| 2.2e-6 m/s after 1 step and |dx| 1.9e-7 m, |dv| 1.8e-5 m/s, |drho| 1.5e-3 kg/m3
+after 100 steps (-ffast-math vs strict build of the same code).  The GPU path
+(different libm, FMA contraction, float cell-relative positions) is held to 10x
+that floor; integer/ordering results (cell sort, pair counts, excluded set) are
+bit-exact.
+"""
+import numpy as np
+import pytest
+
+from golden_io import by_idp, load, maxdiff, meta, snapshot, steps
+
+from dualsphysics_multilayer_amd.case import DamBreakCase
+
+pytestmark = pytest.mark.gpu
+
+oracle = pytest.importorskip("oracle.pyoracle")
+
+
+def gpu(case):
+    from dualsphysics_multilayer_amd.core import SphGpuSingle
+
+    return SphGpuSingle(case, device=0)
+
+
+def tol(step):  # (pos, vel, rho), 10x the measured noise floor
+    if step <= 1:
+        return 1e-8, 2.2e-5, 1e-2
+    if step <= 20:
+        return 1e-7, 5e-5, 1e-2
+    return 2e-6, 2e-4, 2e-2
+
+
+def test_initial_divide_order_is_the_oracles():
+    """Stable cell sort: same particle order as the CPU counting sort (bit-exact)."""
+    case = DamBreakCase(0.03, celldomfixed=True)
+    g, o = gpu(case), oracle.OracleSolver(case, nthreads=4)
+    pg, po = g.particles(), o.particles()
+    assert np.array_equal(pg["idp"], po["idp"])
+    assert np.array_equal(pg["pos"], po["pos"])
+    sg, so = g.stats(), o.stats()
+    assert (sg["np"], sg["npb"], sg["npbok"]) == (so["np"], so["npb"], so["npbok"])
+
+
+def test_pair_counts_match_oracle():
+    """Checked candidates (the cell search itself) are bit-exact.  Real pairs may differ
+    by float rounding of |r|^2 at the support radius: on the initial lattice
+    2h = 2*sqrt(3)*dp, so every (2,2,2)*dp neighbour sits exactly at r = 2h and its
+    inclusion is decided by the last bit of rr2 (fac = 0 there, so such a pair adds
+    nothing to ace/ar)."""
+    case = DamBreakCase(0.025, celldomfixed=True)
+    g, o = gpu(case), oracle.OracleSolver(case, nthreads=4)
+    cg, co = g.count_pairs().astype(np.int64), o.count_pairs().astype(np.int64)
+    assert np.array_equal(cg[[0, 2, 4]], co[[0, 2, 4]])
+    assert np.all(np.abs(cg[[1, 3, 5]] - co[[1, 3, 5]]) <= 0.02 * co[[1, 3, 5]])
+    g.run(15)
+    o.run(15)
+    cg, co = g.count_pairs().astype(np.int64), o.count_pairs().astype(np.int64)
+    assert np.all(np.abs(cg - co) <= 0.001 * co + 8), (cg, co)
+
+
+@pytest.mark.parametrize("ddt", [0, 1, 2, 3])
+def test_interaction_matches_oracle(ddt):
+    """One Interaction_Forces on the same sorted input: ar, ace, maxima."""
+    case = DamBreakCase(0.025, tdensity=ddt, celldomfixed=True)
+    g, o = gpu(case), oracle.OracleSolver(case, nthreads=4)
+    g.run(3)
+    o.run(3)
+    # states after 3 steps differ by rounding; compare the interaction on the GPU's state
+    ig = g.interaction()
+    io = o.interaction()
+    # same particle order
+    assert np.array_equal(g.particles()["idp"], o.particles()["idp"])
+    ace_scale = np.abs(io["ace"]).max()
+    ar_scale = np.abs(io["ar"]).max()
+    assert np.abs(ig["ace"] - io["ace"]).max() <= 2e-4 * ace_scale
+    assert np.abs(ig["ar"] - io["ar"]).max() <= 2e-4 * ar_scale
+    assert ig["velmax"] == pytest.approx(io["velmax"], rel=1e-4)
+    assert ig["acemax"] == pytest.approx(io["acemax"], rel=1e-4)
+    assert ig["viscdtmax"] == pytest.approx(io["viscdtmax"], rel=1e-3)
+
+
+def test_interaction_first_step_tight():
+    """At t=0 (v=0) the interaction inputs are identical: ar/ace agree to float rounding."""
+    case = DamBreakCase(0.02, tdensity=0, celldomfixed=True)
+    ig = gpu(case).interaction()
+    io = oracle.OracleSolver(case, nthreads=4).interaction()
+    scale = np.abs(io["ace"]).max()
+    assert np.abs(ig["ace"] - io["ace"]).max() <= 1e-5 * scale
+    assert np.abs(ig["ar"] - io["ar"]).max() <= 1e-5 * max(np.abs(io["ar"]).max(), 1e-3)
+
+
+@pytest.mark.parametrize("name", ["verlet_ddt2_dp0.02", "symplectic_ddt1_dp0.025", "verlet_ddtnone_dp0.025",
+                                  "symplectic_ddt3_dp0.03"])
+def test_steps_match_reference_parts(name):
+    g_ = load(name)
+    dp, step_alg, ddt, _ = meta(g_)
+    s = gpu(DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt))
+    done = 0
+    for k in steps(g_):
+        s.run(k - done)
+        done = k
+        s.sync()
+        ref = snapshot(g_, k)
+        got = by_idp(s.particles())
+        assert np.array_equal(got["idp"], ref["idp"]), "excluded-particle set differs"
+        tp, tv, tr = tol(k)
+        assert maxdiff(got, ref, "pos") <= tp, (k, maxdiff(got, ref, "pos"))
+        assert maxdiff(got, ref, "vel") <= tv, (k, maxdiff(got, ref, "vel"))
+        assert maxdiff(got, ref, "rhop") <= tr, (k, maxdiff(got, ref, "rhop"))
+        assert abs(s.stats()["time"] - float(ref["time"])) <= 1e-8 * max(1.0, k)
+
+
+def test_dt_trace_matches_reference_57k():
+    g_ = load("verlet_ddt2_dp0.0127_dt")
+    dp, step_alg, ddt, nsteps = meta(g_)
+    s = gpu(DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt))
+    s.run(nsteps)
+    dt = s.dt_trace()
+    assert len(dt) == nsteps
+    assert np.abs(dt / g_["dt"] - 1).max() < 1e-5
+
+
+def test_deterministic_bitwise():
+    case = DamBreakCase(0.025)
+    a, b = gpu(case), gpu(case)
+    a.run(25)
+    b.run(25)
+    pa, pb = a.particles(), b.particles()
+    for k in ("idp", "pos", "vel", "rhop"):
+        assert np.array_equal(pa[k], pb[k]), k
+    assert np.array_equal(a.dt_trace(), b.dt_trace())
+
+
+def test_exclusion_matches_oracle():
+    """OUTRHOP / OUTPOS exclusion (JSphCpu.cpp:1240-1293, 1324) removes the same particles,
+    at the same step, as the oracle; excluded particles leave np and count in nout."""
+    case = DamBreakCase(0.03, celldomfixed=True, rhopoutmax=1010.0)
+    nb = case.npb
+    rng = np.random.default_rng(7)
+    pick = rng.choice(np.arange(nb, case.np), 12, replace=False)
+    case.vel[pick[:4]] = [0, 0, 400.0]
+    case.vel[pick[4:8]] = [0, 0, -30.0]  # compresses its neighbours -> rho > RhopOutMax
+    case.vel[pick[8:]] = [-120.0, 0, 0]  # leaves the map through x < MapRealPosMin
+    g, o = gpu(case), oracle.OracleSolver(case, nthreads=4)
+    for _ in range(6):
+        g.run(1)
+        o.run(1)
+        sg, so = g.stats(), o.stats()
+        assert (sg["np"], sg["nout"]) == (so["np"], so["nout"])
+        assert np.array_equal(np.sort(g.particles()["idp"]), np.sort(o.particles()["idp"]))
+    assert g.stats()["nout"] >= 3
+
+
+def test_large_case_properties():
+    """At 1M particles (BASELINE cfg2 size) the oracle is too slow for many steps:
+    check size-independent properties instead — particle count conserved, cell order
+    of the downloaded state sorted, finite and bounded fields, bitwise determinism."""
+    case = DamBreakCase(0.0045)
+    assert case.np == 1025964
+    a = gpu(case)
+    a.run(10)
+    sa = a.stats()
+    assert sa["np"] == case.np and sa["nout"] == 0 and sa["error_flags"] == 0
+    p = a.particles()
+    assert np.isfinite(p["pos"]).all() and np.isfinite(p["vel"]).all()
+    assert (p["rhop"] > 900).all() and (p["rhop"] < 1100).all()
+    # cell-sorted: (type, cz, cy, cx) nondecreasing
+    from dualsphysics_multilayer_amd.core import case_derive
+
+    k = case_derive(case.case_def())
+    c = np.floor((p["pos"] - np.array(k["map_realposmin"])) / np.float64(np.float32(k["scell"]))).astype(np.int64)
+    fluid = np.arange(len(c)) >= sa["npb"]
+    nc = np.array(k["dom_cells"], np.int64)
+    key = fluid * (nc.prod() + 1) + c[:, 0] + c[:, 1] * nc[0] + c[:, 2] * nc[0] * nc[1]
+    assert (np.diff(key) >= 0).all()
+    b = gpu(case)
+    b.run(10)
+    pb = b.particles()
+    assert np.array_equal(p["pos"], pb["pos"]) and np.array_equal(p["vel"], pb["vel"])

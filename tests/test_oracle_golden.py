@@ -67,3 +67,28 @@ def test_generator_matches_reference_initial_state():
     case = DamBreakCase(0.02)
     assert case.np == 17295 and case.npb == 7395
     assert hashlib.sha256(case.pos.tobytes()).digest() == bytes(g["s0_sha_pos"])
+
+
+def test_oracle_bit_exact_first_step_ddt_none():
+    """Step 1 of the DDT-free case: the oracle reproduces the reference's state bit for bit
+    (at step 1 all velocities are zero, so the viscosity branch, whose -ffast-math
+    rewriting is compiler-specific, does not contribute)."""
+    g = load("verlet_ddtnone_dp0.025")
+    case = DamBreakCase(0.025, step_algorithm=1, tdensity=0)
+    s = oracle.OracleSolver(case, nthreads=3)
+    s.run(1)
+    ref = snapshot(g, 1)
+    got = by_idp(s.particles())
+    for k in ("idp", "pos", "vel", "rhop"):
+        assert np.array_equal(got[k], ref[k]), k
+
+
+def test_oracle_thread_count_independent():
+    case = DamBreakCase(0.03)
+    runs = []
+    for nth in (1, 5):
+        s = oracle.OracleSolver(case, nthreads=nth)
+        s.run(12)
+        runs.append(by_idp(s.particles()))
+    for k in ("pos", "vel", "rhop"):
+        assert np.array_equal(runs[0][k], runs[1][k]), k
