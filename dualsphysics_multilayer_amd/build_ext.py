@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUTDIR = os.path.join(HERE, "lib")
 LIBNAME = "libsphcore.so"
-SOURCES = ["sph_divide.hip", "sph_interaction.hip", "sph_step.hip", "sph_solver.cpp", "sph_capi.cpp"]
+SOURCES = ["sph_divide.hip", "sph_interaction.hip", "sph_interaction_tiled.hip", "sph_step.hip", "sph_solver.cpp", "sph_capi.cpp"]
 ARCH = os.environ.get("SPH_OFFLOAD_ARCH", "gfx950")
 
 

@@ -70,7 +70,7 @@ struct DivGrid {
 // Device-resident step scalars.
 struct DevScalars {
   unsigned np, npb, npbok, nout;          // counts after the last divide
-  unsigned velmax2, acemax2, viscdt, pad; // float bits, max-reduced by atomicMax (values >= 0)
+  unsigned velmax2, acemax2, viscdt, nitems; // float bits, max-reduced by atomicMax (values >= 0)
   unsigned dtmodif, error_flags, npbout, ndiv;  // ndiv: particle count entering the divide
   unsigned long long nstep;
   double dt;        // dt of the step in flight

@@ -139,7 +139,7 @@ __device__ __forceinline__ void fluid_pass(const KConst& K, const DivGrid& g, co
   }
 }
 
-template <int TDENSITY>
+template <int TDENSITY, bool ONLYBOUND = false>
 __global__ __launch_bounds__(256) void k_interaction(DevScalars* __restrict__ sc, const float4* __restrict__ poscell,
                                                      const float4* __restrict__ velrhop,
                                                      const float* __restrict__ press,
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void k_interaction(DevScalars* __restrict__ sc
     const int cx = int(DcelCellx(K.domcellcode, dc)), cy = int(DcelCelly(K.domcellcode, dc)),
               cz = int(DcelCellz(K.domcellcode, dc));
     const Range3 rg = ngs_range(cx, cy, cz, g);
-    if (p1 >= npb) {
+    if (!ONLYBOUND && p1 >= npb) {
       // ---- fluid p1 ----
       const float pr1 = press[p1];
       Acc f = {0, 0, 0, 0, 0, 0};
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void k_interaction(DevScalars* __restrict__ sc
       arace[p1] = make_float4(ax, ay, az, ar);
       viscmax = fmaxf(f.visc, b.visc);
       ace2 = ax * ax + ay * ay + az * az;  // ComputeAceMaxOmp (JSphCpuSingle.cpp:612-644)
-    } else {
+    } else if (p1 < npb) {
       // ---- bound p1 (DBC) ----
       float arp1 = 0.f, visc = 0.f;
       if (p1 < npbok) {
@@ -232,6 +232,14 @@ void launch_interaction(hipStream_t stm, unsigned cap, DevScalars* sc, const flo
     case 2: hipLaunchKernelGGL(k_interaction<2>, dim3(nb), dim3(256), 0, stm, sc, poscell, velrhop, press, begincell, g, K, arace); break;
     default: hipLaunchKernelGGL(k_interaction<3>, dim3(nb), dim3(256), 0, stm, sc, poscell, velrhop, press, begincell, g, K, arace); break;
   }
+}
+
+void launch_interaction_bound(hipStream_t stm, unsigned npbcap, DevScalars* sc, const float4* poscell,
+                              const float4* velrhop, const unsigned* begincell, DivGrid g, const KConst& K,
+                              float4* arace) {
+  const unsigned nb = (npbcap + 255) / 256;
+  if (nb) hipLaunchKernelGGL((k_interaction<0, true>), dim3(nb), dim3(256), 0, stm, sc, poscell, velrhop, nullptr,
+                             begincell, g, K, arace);
 }
 
 // ---------------------------------------------------------------------------------

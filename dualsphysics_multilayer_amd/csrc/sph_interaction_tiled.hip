@@ -1,0 +1,349 @@
+// sph_interaction_tiled.hip — LDS-tiled fluid Interaction_Forces for CDNA4.
+//
+// Same semantics as k_interaction (sph_interaction.hip; reference JSphCpu.cpp:631-822 /
+// JSphGpu_ker.cu:512-745) for fluid p1, restructured for the MI355X:
+//
+//  * Work items: runs of <= TB consecutive fluid particles inside ONE (y,z) row of
+//    cells, spanning <= TMAXCELLS x-cells [a,b] (built per divide by k_items_*).  All
+//    p1 of an item share their 3x3 neighbour rows, and each neighbour row is ONE
+//    contiguous particle range (cells are x-fastest), so a block stages each of the
+//    9 fluid + 9 bound row ranges once into LDS (coalesced 16-B loads) and every lane
+//    reads its candidates from LDS.
+//  * Candidate test and pair body are split: a lane first tests 128 candidates and
+//    records the accepted ones as bits (two 64-bit masks, no LDS traffic), then walks
+//    the set bits.  The heavy body then runs only for real pairs (~16% of candidates)
+//    instead of for every candidate any lane of the wave accepted.
+//  * Persistent blocks with one atomic work counter per XCD group (blockIdx % 8),
+//    items of an XCD group are spatially contiguous -> neighbour rows stay in that
+//    XCD's L2.
+//  * Fast f32 transcendentals: v_rcp/v_sqrt/v_exp/v_log (<= 1 ulp) instead of the
+//    IEEE division/sqrt/pow expansions; Wendland fac rewritten without the 1/rad
+//    (fac = bwen*q*(1-q/2)^3/rad = (bwen/h)*(1-q/2)^3).  Rounding-level differences
+//    only; parity tests hold it to the reference's noise floor.
+#include <cfloat>
+
+#include "sph_kernels.hpp"
+
+namespace sphx {
+
+constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
+constexpr int TCAP = 512;      // staged neighbour records per segment (2 x 8 KB LDS)
+constexpr int TMAXCELLS = 4;   // max x-cells per item
+
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fsqrt_(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
+
+// ------------------------------------------------------------------------------------
+// Item list (per divide).  Greedy split of a fluid row into items; identical in the
+// count and write passes so the list is deterministic and spatially ordered.
+template <class F>
+__device__ __forceinline__ unsigned row_items(const unsigned* __restrict__ bc, unsigned rowbase, int ncx, F emit) {
+  unsigned nitems = 0;
+  int x = 0;
+  while (x < ncx) {
+    while (x < ncx && bc[rowbase + x + 1] == bc[rowbase + x]) x++;
+    if (x >= ncx) break;
+    const int a = x;
+    unsigned n = bc[rowbase + x + 1] - bc[rowbase + x];
+    x++;
+    while (x < ncx && x - a < TMAXCELLS) {
+      const unsigned c = bc[rowbase + x + 1] - bc[rowbase + x];
+      if (n + c > unsigned(TB)) break;
+      n += c;
+      x++;
+    }
+    emit(nitems, a, x - 1);
+    nitems++;
+  }
+  return nitems;
+}
+
+__global__ __launch_bounds__(256) void k_items_count(const unsigned* __restrict__ bc, DivGrid g,
+                                                     unsigned* __restrict__ counts) {
+  const unsigned r = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
+  if (r >= nrows) return;
+  const unsigned y = r % unsigned(g.ncy), z = r / unsigned(g.ncy);
+  const unsigned rowbase = g.boxfluid + z * g.nsheet + y * unsigned(g.ncx);
+  counts[r] = row_items(bc, rowbase, g.ncx, [](unsigned, int, int) {});
+}
+
+// Exclusive scan of the per-row item counts (one block) + reset of the work counters.
+__global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ counts, unsigned nrows,
+                                                     DevScalars* __restrict__ sc, unsigned* __restrict__ qctr) {
+  __shared__ unsigned part[1024];
+  const unsigned per = (nrows + 1023) / 1024;
+  const unsigned b0 = threadIdx.x * per, b1 = min(b0 + per, nrows);
+  unsigned s = 0;
+  for (unsigned i = b0; i < b1; i++) s += counts[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const unsigned v = (threadIdx.x >= unsigned(off) ? part[threadIdx.x - off] : 0u);
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  unsigned run = (threadIdx.x ? part[threadIdx.x - 1] : 0u);
+  for (unsigned i = b0; i < b1; i++) {
+    const unsigned v = counts[i];
+    counts[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == 1023) sc->nitems = part[1023];
+  if (threadIdx.x < 8) qctr[threadIdx.x] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_items_write(const unsigned* __restrict__ bc, DivGrid g,
+                                                     const unsigned* __restrict__ offsets, uint4* __restrict__ items) {
+  const unsigned r = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
+  if (r >= nrows) return;
+  const unsigned y = r % unsigned(g.ncy), z = r / unsigned(g.ncy);
+  const unsigned rowbase = g.boxfluid + z * g.nsheet + y * unsigned(g.ncx);
+  uint4* out = items + offsets[r];
+  row_items(bc, rowbase, g.ncx, [&](unsigned k, int a, int b) {
+    out[k] = make_uint4(y | (z << 16), unsigned(a) | (unsigned(b) << 16), bc[rowbase + a], bc[rowbase + b + 1]);
+  });
+}
+
+void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
+                  uint4* items, unsigned* qctr) {
+  const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
+  const unsigned nb = (nrows + 255) / 256;
+  hipLaunchKernelGGL(k_items_count, dim3(nb), dim3(256), 0, stm, begincell, g, rowtmp);
+  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, rowtmp, nrows, sc, qctr);
+  hipLaunchKernelGGL(k_items_write, dim3(nb), dim3(256), 0, stm, begincell, g, rowtmp, items);
+}
+
+// ------------------------------------------------------------------------------------
+struct TAcc {
+  float ax, ay, az, ar, delta, visc;
+};
+
+struct P1 {
+  float x, y, z;        // x relative to the item's x origin, y/z cell-relative
+  float4 vr;            // velocity, rho
+  float pr, inv_rho;
+};
+
+// One pair body (JSphCpu.cpp:682-797 semantics, fast f32 intrinsics).
+template <int TDENSITY, bool BOUNDP2>
+__device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float drx, float dry, float drz, float rr2,
+                                          float4 A, float4 B, float massp2, float cvisc, TAcc& a) {
+  const float rad = fsqrt_(rr2);
+  const float wqq1 = 1.f - 0.5f * (rad * K.ovkernelh);
+  const float fac = K.bwen * K.ovkernelh * (wqq1 * wqq1 * wqq1);
+  const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
+  const float inv2 = frcp(B.w);
+  {  // momentum
+    const float prs = (p.pr + A.w) * (p.inv_rho * inv2);
+    const float p_vpm = -prs * massp2;
+    a.ax += p_vpm * frx;
+    a.ay += p_vpm * fry;
+    a.az += p_vpm * frz;
+  }
+  const float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
+  a.ar += massp2 * (dvx * frx + dvy * fry + dvz * frz) * (p.vr.w * inv2);
+  const float inv_re = frcp(rr2 + K.eta2);
+  if (TDENSITY == 1 && a.delta != FLT_MAX) {
+    if (BOUNDP2) a.delta = FLT_MAX;
+    else {
+      const float visc_densi = K.ddtkh * K.cs0f * (p.vr.w * inv2 - 1.f) * inv_re;
+      const float dot3 = drx * frx + dry * fry + drz * frz;
+      a.delta += visc_densi * dot3 * massp2;
+    }
+  }
+  if ((TDENSITY == 2 || (TDENSITY == 3 && !BOUNDP2)) && a.delta != FLT_MAX) {
+    if (BOUNDP2) a.delta = FLT_MAX;
+    else {
+      const float rh = 1.f + K.ddtgz * drz;
+      const float drhop = K.rhopzero * fexp2(K.ovgamma * flog2(rh)) - K.rhopzero;
+      const float visc_densi = K.ddtkh * K.cs0f * ((B.w - p.vr.w) - drhop) * inv_re;
+      const float dot3 = drx * frx + dry * fry + drz * frz;
+      a.delta -= visc_densi * dot3 * massp2 * inv2;
+    }
+  }
+  const float dot = drx * dvx + dry * dvy + drz * dvz;
+  const float dot_rr2 = dot * inv_re;
+  a.visc = fmaxf(dot_rr2, a.visc);
+  if (dot < 0.f) {
+    // pi_visc = (-visco*cbar*h*dot_rr2/robar)*massp2, cvisc = -visco*cbar*h*massp2
+    const float pi_visc = cvisc * dot_rr2 * frcp((p.vr.w + B.w) * 0.5f);
+    a.ax -= pi_visc * frx;
+    a.ay -= pi_visc * fry;
+    a.az -= pi_visc * frz;
+  }
+}
+
+// Candidates [s0,s1) of the staged segment: test 128 at a time into bit masks, then
+// run the pair body over the set bits.
+template <int TDENSITY, bool BOUNDP2>
+__device__ __forceinline__ void tile_range(const KConst& K, const P1& p, float ry, float rz, int s0, int s1,
+                                           const float4* __restrict__ sA, const float4* __restrict__ sB,
+                                           float massp2, float cvisc, TAcc& a) {
+  for (int base = s0; base < s1; base += 128) {
+    unsigned long long m0 = 0, m1 = 0;
+#pragma unroll 8
+    for (int j = 0; j < 64; j++) {
+      const int c = min(base + j, TCAP - 1);
+      const float4 A = sA[c];
+      const float drx = p.x - A.x, dry = ry - A.y, drz = rz - A.z;
+      const float rr2 = drx * drx + dry * dry + drz * drz;
+      const bool ok = (base + j < s1) && rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO;
+      m0 |= (unsigned long long)ok << j;
+    }
+    if (base + 64 < s1) {
+#pragma unroll 8
+      for (int j = 0; j < 64; j++) {
+        const int c = min(base + 64 + j, TCAP - 1);
+        const float4 A = sA[c];
+        const float drx = p.x - A.x, dry = ry - A.y, drz = rz - A.z;
+        const float rr2 = drx * drx + dry * dry + drz * drz;
+        const bool ok = (base + 64 + j < s1) && rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO;
+        m1 |= (unsigned long long)ok << j;
+      }
+    }
+    while (m0 | m1) {
+      int j;
+      if (m0) {
+        j = __ffsll((long long)m0) - 1;
+        m0 &= m0 - 1;
+      } else {
+        j = 64 + __ffsll((long long)m1) - 1;
+        m1 &= m1 - 1;
+      }
+      const float4 A = sA[base + j];
+      const float4 B = sB[base + j];
+      const float drx = p.x - A.x, dry = ry - A.y, drz = rz - A.z;
+      const float rr2 = drx * drx + dry * dry + drz * drz;
+      pair_body<TDENSITY, BOUNDP2>(K, p, drx, dry, drz, rr2, A, B, massp2, cvisc, a);
+    }
+  }
+}
+
+template <int TDENSITY>
+__global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
+                                                    unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
+                                                    const float4* __restrict__ velrhop,
+                                                    const float* __restrict__ press,
+                                                    const unsigned* __restrict__ bc, DivGrid g, KConst K,
+                                                    float4* __restrict__ arace) {
+  __shared__ float4 sA[TCAP];
+  __shared__ float4 sB[TCAP];
+  __shared__ unsigned s_item;
+  const unsigned nitems = sc->nitems;
+  const unsigned per = (nitems + 7) / 8;
+  const unsigned grp = blockIdx.x & 7;
+  float viscmax = 0.f, ace2max = 0.f;
+  const float cvisc_f = -K.visco * K.cs0f * K.kernelh * K.massfluid;
+  const float cvisc_b = -K.viscobound * K.cs0f * K.kernelh * K.massbound;
+
+  for (unsigned q = 0; q < 8; q++) {
+    const unsigned xg = (grp + q) & 7;
+    const unsigned lo = xg * per, hi = min(nitems, lo + per);
+    for (;;) {
+      if (threadIdx.x == 0) s_item = lo + atomicAdd(&qctr[xg], 1u);
+      __syncthreads();
+      const unsigned it = s_item;
+      __syncthreads();
+      if (it >= hi) break;
+      const uint4 item = items[it];
+      const int cy = int(item.x & 0xffffu), cz = int(item.x >> 16);
+      const int a = int(item.y & 0xffffu), b = int(item.y >> 16);
+      const int xo = (a + b + 1) >> 1;
+      const int xa = max(a - 1, 0), xb = min(b + 1, g.ncx - 1);
+      for (unsigned p1base = item.z; p1base < item.w; p1base += TB) {
+        const unsigned p1 = p1base + threadIdx.x;
+        const bool act = p1 < item.w;
+        P1 p;
+        int cx1 = a;
+        if (act) {
+          const float4 pc1 = poscell[p1];
+          cx1 = int(DcelCellx(K.domcellcode, __float_as_uint(pc1.w)));
+          p.x = pc1.x + float(cx1 - xo) * K.scell;
+          p.y = pc1.y;
+          p.z = pc1.z;
+          p.vr = velrhop[p1];
+          p.pr = press[p1];
+        } else {
+          p.x = p.y = p.z = 1e30f;  // never within the support radius
+          p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
+          p.pr = 0.f;
+        }
+        p.inv_rho = frcp(p.vr.w);
+        const int lxa = max(cx1 - 1, 0), lxb = min(cx1 + 1, g.ncx - 1);
+        TAcc f = {0, 0, 0, 0, 0, 0}, bnd = {0, 0, 0, 0, 0, 0};
+        for (int pass = 0; pass < 2; pass++) {
+          const unsigned cellinit = (pass == 0 ? g.boxfluid : 0u);
+          for (int z = max(cz - 1, 0); z <= min(cz + 1, g.ncz - 1); z++) {
+            const float rz = p.z + float(cz - z) * K.scell;
+            for (int y = max(cy - 1, 0); y <= min(cy + 1, g.ncy - 1); y++) {
+              const unsigned rowbase = cellinit + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+              const unsigned rs = bc[rowbase + xa], re = bc[rowbase + xb + 1];
+              if (rs == re) continue;
+              const float ry = p.y + float(cy - y) * K.scell;
+              const unsigned ls = bc[rowbase + lxa], le = bc[rowbase + lxb + 1];
+              for (unsigned seg = rs; seg < re; seg += TCAP) {
+                const unsigned segn = min(unsigned(TCAP), re - seg);
+                __syncthreads();
+                for (unsigned i = threadIdx.x; i < segn; i += TB) {
+                  const float4 pc = poscell[seg + i];
+                  const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
+                  sA[i] = make_float4(pc.x + float(cx2 - xo) * K.scell, pc.y, pc.z, press[seg + i]);
+                  sB[i] = velrhop[seg + i];
+                }
+                __syncthreads();
+                const int s0 = int(max(ls, seg) - seg);
+                const int s1 = act ? int(min(le, seg + segn)) - int(seg) : 0;
+                if (pass == 0)
+                  tile_range<TDENSITY, false>(K, p, ry, rz, s0, s1, sA, sB, K.massfluid, cvisc_f, f);
+                else
+                  tile_range<TDENSITY, true>(K, p, ry, rz, s0, s1, sA, sB, K.massbound, cvisc_b, bnd);
+              }
+            }
+          }
+        }
+        if (act) {
+          // Combine exactly as the two CPU passes store (JSphCpu.cpp:800-818).
+          float ar = 0.f, ax = 0.f, ay = 0.f, az = 0.f, delta = 0.f;
+          if (f.ar != 0.f || f.ax != 0.f || f.ay != 0.f || f.az != 0.f || f.visc != 0.f) {
+            if (TDENSITY) delta = (f.delta == FLT_MAX ? FLT_MAX : 0.f + f.delta);
+            ar = f.ar;
+            ax = f.ax;
+            ay = f.ay;
+            az = f.az;
+          }
+          if (bnd.ar != 0.f || bnd.ax != 0.f || bnd.ay != 0.f || bnd.az != 0.f || bnd.visc != 0.f) {
+            if (TDENSITY) delta = (delta == FLT_MAX || bnd.delta == FLT_MAX ? FLT_MAX : delta + bnd.delta);
+            ar += bnd.ar;
+            ax += bnd.ax;
+            ay += bnd.ay;
+            az += bnd.az;
+          }
+          if (TDENSITY && delta != FLT_MAX) ar += delta;
+          arace[p1] = make_float4(ax, ay, az, ar);
+          viscmax = fmaxf(viscmax, fmaxf(f.visc, bnd.visc));
+          ace2max = fmaxf(ace2max, ax * ax + ay * ay + az * az);
+        }
+      }
+    }
+  }
+  wave_max_atomic(&sc->viscdt, viscmax);
+  wave_max_atomic(&sc->acemax2, ace2max);
+}
+
+void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
+                        const float4* poscell, const float4* velrhop, const float* press, const unsigned* begincell,
+                        DivGrid g, const KConst& K, float4* arace) {
+  switch (K.tdensity) {
+    case 0: hipLaunchKernelGGL(k_fluid_tiled<0>, dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace); break;
+    case 1: hipLaunchKernelGGL(k_fluid_tiled<1>, dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace); break;
+    case 2: hipLaunchKernelGGL(k_fluid_tiled<2>, dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace); break;
+    default: hipLaunchKernelGGL(k_fluid_tiled<3>, dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace); break;
+  }
+}
+
+}  // namespace sphx

@@ -54,6 +54,16 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
 // ---- interaction (cusph::Interaction_Forces, JSphGpu_ker.cu:788-885) ----
 void launch_interaction(hipStream_t stm, unsigned cap, DevScalars* sc, const float4* poscell, const float4* velrhop,
                         const float* press, const unsigned* begincell, DivGrid g, const KConst& K, float4* arace);
+// Bound p1 only (grid over the bound capacity) — used beside the tiled fluid kernel.
+void launch_interaction_bound(hipStream_t stm, unsigned npbcap, DevScalars* sc, const float4* poscell,
+                              const float4* velrhop, const unsigned* begincell, DivGrid g, const KConst& K,
+                              float4* arace);
+// Tiled fluid interaction (sph_interaction_tiled.hip) and its per-divide item list.
+void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
+                  uint4* items, unsigned* qctr);
+void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
+                        const float4* poscell, const float4* velrhop, const float* press, const unsigned* begincell,
+                        DivGrid g, const KConst& K, float4* arace);
 // Pair counters (JDsPips).
 void launch_count_pairs(hipStream_t stm, unsigned cap, const DevScalars* sc, const float4* poscell,
                         const unsigned* begincell, DivGrid g, const KConst& K, unsigned long long* out6);

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace sphx {
@@ -154,6 +155,7 @@ SphGpuSingle::SphGpuSingle(const SphCaseDef& cdef, const SphParticlesHost& init,
   cap_ = init.n;
   npb0_ = cdef.npb;
   keybits_ = bits_for(G.boxfluidoutignore, 1);
+  if (const char* e = std::getenv("SPH_INTERACTION")) tiled_ = std::string(e) != "simple";
   check_hip(hipSetDevice(device), "hipSetDevice");
   check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
   try {
@@ -208,6 +210,9 @@ void SphGpuSingle::Alloc() {
   press_ = (float*)dmalloc(4 * n);
   arace_ = (float4*)dmalloc(16 * n);
   begincell_ = (unsigned*)dmalloc(4 * size_t(G.nctt));
+  items_ = (uint4*)dmalloc(16 * size_t(G.nct + 1));
+  rowtmp_ = (unsigned*)dmalloc(4 * size_t(G.ncy) * size_t(G.ncz));
+  qctr_ = (unsigned*)dmalloc(4 * 8);
   for (int i = 0; i < 2; i++) {
     sort_.keys[i] = (unsigned*)dmalloc(4 * n);
     sort_.vals[i] = (unsigned*)dmalloc(4 * n);
@@ -315,13 +320,21 @@ void SphGpuSingle::RunCellDivide() {
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET);
   launch_gather(stream, cap_, sc_, sort_.vals[res], cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_);
   std::swap(cur_, alt_);
+  if (tiled_) launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_);
   TimedEnd(2);
 }
 
 void SphGpuSingle::Interaction_Forces(int interstep) {
   (void)interstep;  // mDBC / shifting are not on this path
   TimedBegin(0);
-  launch_interaction(stream, cap_, sc_, poscell_, cur_.velrhop, press_, begincell_, G, K, arace_);
+  if (tiled_) {
+    check_hip(hipMemsetAsync(qctr_, 0, 4 * 8, stream), "reset work counters");
+    launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, begincell_, G, K,
+                       arace_);
+    launch_interaction_bound(stream, npb0_, sc_, poscell_, cur_.velrhop, begincell_, G, K, arace_);
+  } else {
+    launch_interaction(stream, cap_, sc_, poscell_, cur_.velrhop, press_, begincell_, G, K, arace_);
+  }
   TimedEnd(0);
 }
 

@@ -75,6 +75,11 @@ class SphGpuSingle {
   float* press_ = nullptr;
   float4* arace_ = nullptr;
   unsigned* begincell_ = nullptr;
+  uint4* items_ = nullptr;        // tiled-interaction work items (per divide)
+  unsigned* rowtmp_ = nullptr;    // per-row item counts/offsets
+  unsigned* qctr_ = nullptr;      // per-XCD-group work counters
+  unsigned nblocks_tiled_ = 2048;
+  bool tiled_ = true;             // SPH_INTERACTION=simple selects the one-lane-per-particle kernel
   SortScratch sort_;
   DevScalars* sc_ = nullptr;
   DevScalars* sc_host_ = nullptr;  // pinned mirror for readback
