@@ -33,6 +33,7 @@ CXXFLAGS = [
     "--offload-arch=" + ARCH,
     "-ffp-contract=fast",
     "-munsafe-fp-atomics",
+    "-fno-slp-vectorize",  # packed-f32 SLP adds v_mov shuffles in the pair loops (guide §B)
     "-Wall",
     "-Wno-unused-function",
 ]

@@ -27,7 +27,7 @@
 namespace sphx {
 
 constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
-constexpr int TCAP = 512;      // staged neighbour records per segment (2 x 8 KB LDS)
+constexpr int TCAP = 512;      // staged neighbour records per segment (8+8+2 KB LDS)
 constexpr int TMAXCELLS = 4;   // max x-cells per item
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
@@ -179,32 +179,36 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
 }
 
 // Candidates [s0,s1) of the staged segment: test 128 at a time into bit masks, then
-// run the pair body over the set bits.
+// run the pair body over the set bits.  The test uses the staged |A|^2 (sA.w):
+// |p-A|^2 = |p|^2 + |A|^2 - 2 p.A  -> 3 FMAs + 1 compare per candidate on one
+// ds_read_b128, against a threshold inflated by 1e-4 (the rounding of the expanded
+// form is ~1e-6 relative); the body recomputes |p-A|^2 exactly and applies the
+// reference's test (rr2 <= KernelSize2 && rr2 >= ALMOSTZERO), so no pair is lost or added.
 template <int TDENSITY, bool BOUNDP2>
 __device__ __forceinline__ void tile_range(const KConst& K, const P1& p, float ry, float rz, int s0, int s1,
                                            const float4* __restrict__ sA, const float4* __restrict__ sB,
-                                           float massp2, float cvisc, TAcc& a) {
+                                           const float* __restrict__ sP, float massp2, float cvisc, TAcc& a) {
+  const float px2 = -2.f * p.x, py2 = -2.f * ry, pz2 = -2.f * rz;
+  const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + ry * ry + rz * rz);
   for (int base = s0; base < s1; base += 128) {
     unsigned long long m0 = 0, m1 = 0;
-#pragma unroll 8
-    for (int j = 0; j < 64; j++) {
-      const int c = min(base + j, TCAP - 1);
-      const float4 A = sA[c];
-      const float drx = p.x - A.x, dry = ry - A.y, drz = rz - A.z;
-      const float rr2 = drx * drx + dry * dry + drz * drz;
-      const bool ok = (base + j < s1) && rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO;
-      m0 |= (unsigned long long)ok << j;
-    }
-    if (base + 64 < s1) {
-#pragma unroll 8
-      for (int j = 0; j < 64; j++) {
-        const int c = min(base + 64 + j, TCAP - 1);
-        const float4 A = sA[c];
-        const float drx = p.x - A.x, dry = ry - A.y, drz = rz - A.z;
-        const float rr2 = drx * drx + dry * dry + drz * drz;
-        const bool ok = (base + 64 + j < s1) && rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO;
-        m1 |= (unsigned long long)ok << j;
+    const int n0 = s1 - base;  // candidates left for this lane (> 0)
+    // sA is padded by 128 records, so base+127 stays inside the array; bits past the
+    // lane's range are masked off per 8-candidate group.
+    const float4* __restrict__ sAb = sA + base;
+    for (int jo = 0; jo < 16; jo++) {
+      const int left = n0 - jo * 8;
+      if (left <= 0) break;
+      unsigned bits = 0;
+#pragma unroll
+      for (int ji = 0; ji < 8; ji++) {
+        const float4 A = sAb[jo * 8 + ji];
+        const float q = fmaf(px2, A.x, fmaf(py2, A.y, fmaf(pz2, A.z, A.w)));
+        bits |= (q <= thr) ? (1u << ji) : 0u;
       }
+      bits &= (left >= 8 ? 0xffu : ((1u << left) - 1u));
+      if (jo < 8) m0 |= (unsigned long long)bits << (jo * 8);
+      else m1 |= (unsigned long long)bits << ((jo - 8) * 8);
     }
     while (m0 | m1) {
       int j;
@@ -216,10 +220,13 @@ __device__ __forceinline__ void tile_range(const KConst& K, const P1& p, float r
         m1 &= m1 - 1;
       }
       const float4 A = sA[base + j];
-      const float4 B = sB[base + j];
       const float drx = p.x - A.x, dry = ry - A.y, drz = rz - A.z;
       const float rr2 = drx * drx + dry * dry + drz * drz;
-      pair_body<TDENSITY, BOUNDP2>(K, p, drx, dry, drz, rr2, A, B, massp2, cvisc, a);
+      if (rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO) {
+        const float4 B = sB[base + j];
+        pair_body<TDENSITY, BOUNDP2>(K, p, drx, dry, drz, rr2, make_float4(A.x, A.y, A.z, sP[base + j]), B, massp2,
+                                     cvisc, a);
+      }
     }
   }
 }
@@ -231,8 +238,9 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
                                                     const float* __restrict__ press,
                                                     const unsigned* __restrict__ bc, DivGrid g, KConst K,
                                                     float4* __restrict__ arace) {
-  __shared__ float4 sA[TCAP];
+  __shared__ float4 sA[TCAP + 128];  // +128: over-read pad of the 8-wide candidate test
   __shared__ float4 sB[TCAP];
+  __shared__ float sP[TCAP];
   __shared__ unsigned s_item;
   const unsigned nitems = sc->nitems;
   const unsigned per = (nitems + 7) / 8;
@@ -292,16 +300,18 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
                 for (unsigned i = threadIdx.x; i < segn; i += TB) {
                   const float4 pc = poscell[seg + i];
                   const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
-                  sA[i] = make_float4(pc.x + float(cx2 - xo) * K.scell, pc.y, pc.z, press[seg + i]);
+                  const float x2 = pc.x + float(cx2 - xo) * K.scell;
+                  sA[i] = make_float4(x2, pc.y, pc.z, x2 * x2 + pc.y * pc.y + pc.z * pc.z);
                   sB[i] = velrhop[seg + i];
+                  sP[i] = press[seg + i];
                 }
                 __syncthreads();
                 const int s0 = int(max(ls, seg) - seg);
                 const int s1 = act ? int(min(le, seg + segn)) - int(seg) : 0;
                 if (pass == 0)
-                  tile_range<TDENSITY, false>(K, p, ry, rz, s0, s1, sA, sB, K.massfluid, cvisc_f, f);
+                  tile_range<TDENSITY, false>(K, p, ry, rz, s0, s1, sA, sB, sP, K.massfluid, cvisc_f, f);
                 else
-                  tile_range<TDENSITY, true>(K, p, ry, rz, s0, s1, sA, sB, K.massbound, cvisc_b, bnd);
+                  tile_range<TDENSITY, true>(K, p, ry, rz, s0, s1, sA, sB, sP, K.massbound, cvisc_b, bnd);
               }
             }
           }
