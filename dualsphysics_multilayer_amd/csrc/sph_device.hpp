@@ -70,7 +70,7 @@ struct DivGrid {
 // Device-resident step scalars.
 struct DevScalars {
   unsigned np, npb, npbok, nout;          // counts after the last divide
-  unsigned velmax2, acemax2, viscdt, nitems; // float bits, max-reduced by atomicMax (values >= 0)
+  unsigned nitems, nitems_bound, pad0, pad1; // tiled-interaction work items (fluid, bound)
   unsigned dtmodif, error_flags, npbout, ndiv;  // ndiv: particle count entering the divide
   unsigned long long nstep;
   double dt;        // dt of the step in flight
@@ -79,15 +79,21 @@ struct DevScalars {
   double ddt_p;     // predictor dt (Symplectic)
   double last_dt;
   float last_velmax, last_acemax, last_viscdt, pad3;
+  // Max-reductions (float bits of values >= 0) spread over RED_SLOTS slots so that
+  // thousands of waves do not serialise on one address; k_dt folds and clears them.
+  unsigned red[3][64];
 };
+constexpr int RED_VELMAX2 = 0, RED_ACEMAX2 = 1, RED_VISCDT = 2, RED_SLOTS = 64;
 
 constexpr unsigned ERR_DT_NAN = 1u, ERR_BOUNDOUT = 2u;
 
-// Wave-level max of a non-negative float, then one atomicMax per wave.
-__device__ inline void wave_max_atomic(unsigned* dst, float v) {
+// Wave-level max of a non-negative float, then one atomicMax per wave into a slot
+// chosen by the wave's global index (64 slots).
+__device__ inline void wave_max_atomic(DevScalars* sc, int which, float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-  if ((threadIdx.x & 63) == 0 && v > 0.f) atomicMax(dst, __float_as_uint(v));
+  const unsigned wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && v > 0.f) atomicMax(&sc->red[which][wave & (RED_SLOTS - 1)], __float_as_uint(v));
 }
 
 }  // namespace sphx

@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, Gat
     a.press[i] = float(double(a.cteb) * (pow(double(vr.w * a.ovrhopzero), double(a.gamma)) - 1.0));
     if (i >= npb) v2 = vr.x * vr.x + vr.y * vr.y + vr.z * vr.z;  // CalcVelMaxOmp over fluid
   }
-  wave_max_atomic(&sc->velmax2, v2);
+  wave_max_atomic(sc, RED_VELMAX2, v2);
 }
 
 void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned* sortpart, const PartArrays& src,

@@ -219,8 +219,8 @@ __global__ __launch_bounds__(256) void k_interaction(DevScalars* __restrict__ sc
       viscmax = visc;
     }
   }
-  wave_max_atomic(&sc->viscdt, viscmax);
-  wave_max_atomic(&sc->acemax2, ace2);
+  wave_max_atomic(sc, RED_VISCDT, viscmax);
+  wave_max_atomic(sc, RED_ACEMAX2, ace2);
 }
 
 void launch_interaction(hipStream_t stm, unsigned cap, DevScalars* sc, const float4* poscell, const float4* velrhop,

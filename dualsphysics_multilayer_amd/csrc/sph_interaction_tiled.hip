@@ -36,46 +36,61 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 __device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
 
 // ------------------------------------------------------------------------------------
-// Item list (per divide).  Greedy split of a fluid row into items; identical in the
-// count and write passes so the list is deterministic and spatially ordered.
-template <class F>
-__device__ __forceinline__ unsigned row_items(const unsigned* __restrict__ bc, unsigned rowbase, int ncx, F emit) {
+// Item list (per divide).  Rows [0,nrows) are fluid rows (fluid p1), rows
+// [nrows,2*nrows) bound rows (bound p1, DBC).  One wave per row loads the row's cell
+// counts into LDS (coalesced), then lane 0 splits the row greedily into items; the
+// count and write passes run the same greedy, so the list is deterministic and in
+// spatial (z, y, x) order, fluid items first.
+constexpr int ROWCELLS_LDS = 1024;
+constexpr unsigned ITEM_BOUND = 0x80000000u;  // flag in item.x: p1 are boundary particles
+
+template <bool WRITE>
+__global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ bc, DivGrid g,
+                                                   unsigned* __restrict__ counts, uint4* __restrict__ items) {
+  __shared__ unsigned cnt[ROWCELLS_LDS];
+  const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
+  const unsigned r = blockIdx.x;
+  const bool bound = r >= nrows;
+  const unsigned rr = bound ? r - nrows : r;
+  const unsigned y = rr % unsigned(g.ncy), z = rr / unsigned(g.ncy);
+  const unsigned rowbase = (bound ? 0u : g.boxfluid) + z * g.nsheet + y * unsigned(g.ncx);
+  const int ncx = g.ncx;
+  const bool inlds = ncx <= ROWCELLS_LDS;
+  if (inlds)
+    for (int x = threadIdx.x; x < ncx; x += 64) cnt[x] = bc[rowbase + x + 1] - bc[rowbase + x];
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  auto count = [&](int x) { return inlds ? cnt[x] : bc[rowbase + x + 1] - bc[rowbase + x]; };
   unsigned nitems = 0;
+  uint4* out = WRITE ? items + counts[r] : nullptr;
   int x = 0;
   while (x < ncx) {
-    while (x < ncx && bc[rowbase + x + 1] == bc[rowbase + x]) x++;
+    while (x < ncx && count(x) == 0) x++;
     if (x >= ncx) break;
     const int a = x;
-    unsigned n = bc[rowbase + x + 1] - bc[rowbase + x];
+    unsigned n = count(x);
     x++;
     while (x < ncx && x - a < TMAXCELLS) {
-      const unsigned c = bc[rowbase + x + 1] - bc[rowbase + x];
+      const unsigned c = count(x);
       if (n + c > unsigned(TB)) break;
       n += c;
       x++;
     }
-    emit(nitems, a, x - 1);
+    if (WRITE)
+      out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(x - 1) << 16),
+                               bc[rowbase + a], bc[rowbase + x]);
     nitems++;
   }
-  return nitems;
+  if (!WRITE) counts[r] = nitems;
 }
 
-__global__ __launch_bounds__(256) void k_items_count(const unsigned* __restrict__ bc, DivGrid g,
-                                                     unsigned* __restrict__ counts) {
-  const unsigned r = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
-  if (r >= nrows) return;
-  const unsigned y = r % unsigned(g.ncy), z = r / unsigned(g.ncy);
-  const unsigned rowbase = g.boxfluid + z * g.nsheet + y * unsigned(g.ncx);
-  counts[r] = row_items(bc, rowbase, g.ncx, [](unsigned, int, int) {});
-}
-
-// Exclusive scan of the per-row item counts (one block) + reset of the work counters.
-__global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ counts, unsigned nrows,
-                                                     DevScalars* __restrict__ sc, unsigned* __restrict__ qctr) {
+// Exclusive scan of the per-row item counts (one block) -> item offsets, total.
+// (the per-XCD work counters are reset by a memset right before each launch)
+__global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ counts, unsigned nrows2,
+                                                     DevScalars* __restrict__ sc) {
   __shared__ unsigned part[1024];
-  const unsigned per = (nrows + 1023) / 1024;
-  const unsigned b0 = threadIdx.x * per, b1 = min(b0 + per, nrows);
+  const unsigned per = (nrows2 + 1023) / 1024;
+  const unsigned b0 = threadIdx.x * per, b1 = min(b0 + per, nrows2);
   unsigned s = 0;
   for (unsigned i = b0; i < b1; i++) s += counts[i];
   part[threadIdx.x] = s;
@@ -93,29 +108,15 @@ __global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ coun
     run += v;
   }
   if (threadIdx.x == 1023) sc->nitems = part[1023];
-  if (threadIdx.x < 8) qctr[threadIdx.x] = 0;
-}
-
-__global__ __launch_bounds__(256) void k_items_write(const unsigned* __restrict__ bc, DivGrid g,
-                                                     const unsigned* __restrict__ offsets, uint4* __restrict__ items) {
-  const unsigned r = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
-  if (r >= nrows) return;
-  const unsigned y = r % unsigned(g.ncy), z = r / unsigned(g.ncy);
-  const unsigned rowbase = g.boxfluid + z * g.nsheet + y * unsigned(g.ncx);
-  uint4* out = items + offsets[r];
-  row_items(bc, rowbase, g.ncx, [&](unsigned k, int a, int b) {
-    out[k] = make_uint4(y | (z << 16), unsigned(a) | (unsigned(b) << 16), bc[rowbase + a], bc[rowbase + b + 1]);
-  });
 }
 
 void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
                   uint4* items, unsigned* qctr) {
-  const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
-  const unsigned nb = (nrows + 255) / 256;
-  hipLaunchKernelGGL(k_items_count, dim3(nb), dim3(256), 0, stm, begincell, g, rowtmp);
-  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, rowtmp, nrows, sc, qctr);
-  hipLaunchKernelGGL(k_items_write, dim3(nb), dim3(256), 0, stm, begincell, g, rowtmp, items);
+  (void)qctr;
+  const unsigned nrows2 = 2u * unsigned(g.ncy) * unsigned(g.ncz);
+  hipLaunchKernelGGL(k_items_rows<false>, dim3(nrows2), dim3(64), 0, stm, begincell, g, rowtmp, nullptr);
+  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, rowtmp, nrows2, sc);
+  hipLaunchKernelGGL(k_items_rows<true>, dim3(nrows2), dim3(64), 0, stm, begincell, g, rowtmp, items);
 }
 
 // ------------------------------------------------------------------------------------
@@ -130,14 +131,24 @@ struct P1 {
 };
 
 // One pair body (JSphCpu.cpp:682-797 semantics, fast f32 intrinsics).
-template <int TDENSITY, bool BOUNDP2>
+// MODE 0: fluid p1 / fluid p2, 1: fluid p1 / bound p2, 2: bound p1 / fluid p2
+// (InteractionForcesBound, JSphCpu.cpp:577-612: continuity + visc-dt only).
+template <int TDENSITY, int MODE>
 __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float drx, float dry, float drz, float rr2,
                                           float4 A, float4 B, float massp2, float cvisc, TAcc& a) {
+  constexpr bool BOUNDP2 = (MODE == 1);
   const float rad = fsqrt_(rr2);
   const float wqq1 = 1.f - 0.5f * (rad * K.ovkernelh);
   const float fac = K.bwen * K.ovkernelh * (wqq1 * wqq1 * wqq1);
   const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
   const float inv2 = frcp(B.w);
+  if (MODE == 2) {
+    const float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
+    a.ar += massp2 * (dvx * frx + dvy * fry + dvz * frz) * (p.vr.w * inv2);
+    const float dot = drx * dvx + dry * dvy + drz * dvz;
+    a.visc = fmaxf(dot * frcp(rr2 + K.eta2), a.visc);
+    return;
+  }
   {  // momentum
     const float prs = (p.pr + A.w) * (p.inv_rho * inv2);
     const float p_vpm = -prs * massp2;
@@ -184,7 +195,7 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
 // ds_read_b128, against a threshold inflated by 1e-4 (the rounding of the expanded
 // form is ~1e-6 relative); the body recomputes |p-A|^2 exactly and applies the
 // reference's test (rr2 <= KernelSize2 && rr2 >= ALMOSTZERO), so no pair is lost or added.
-template <int TDENSITY, bool BOUNDP2>
+template <int TDENSITY, int MODE>
 __device__ __forceinline__ void tile_range(const KConst& K, const P1& p, float ry, float rz, int s0, int s1,
                                            const float4* __restrict__ sA, const float4* __restrict__ sB,
                                            const float* __restrict__ sP, float massp2, float cvisc, TAcc& a) {
@@ -224,7 +235,7 @@ __device__ __forceinline__ void tile_range(const KConst& K, const P1& p, float r
       const float rr2 = drx * drx + dry * dry + drz * drz;
       if (rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO) {
         const float4 B = sB[base + j];
-        pair_body<TDENSITY, BOUNDP2>(K, p, drx, dry, drz, rr2, make_float4(A.x, A.y, A.z, sP[base + j]), B, massp2,
+        pair_body<TDENSITY, MODE>(K, p, drx, dry, drz, rr2, make_float4(A.x, A.y, A.z, sP[base + j]), B, massp2,
                                      cvisc, a);
       }
     }
@@ -259,10 +270,22 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
       __syncthreads();
       if (it >= hi) break;
       const uint4 item = items[it];
-      const int cy = int(item.x & 0xffffu), cz = int(item.x >> 16);
+      const bool bitem = (item.x & ITEM_BOUND) != 0u;
+      const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
       const int a = int(item.y & 0xffffu), b = int(item.y >> 16);
       const int xo = (a + b + 1) >> 1;
       const int xa = max(a - 1, 0), xb = min(b + 1, g.ncx - 1);
+      if (bitem) {
+        // Bound item: nothing to do unless a fluid cell is in its 3x3x3 neighbourhood
+        // (arace of the boundary was zeroed before the launch).
+        bool any = false;
+        for (int z = max(cz - 1, 0); z <= min(cz + 1, g.ncz - 1); z++)
+          for (int y = max(cy - 1, 0); y <= min(cy + 1, g.ncy - 1); y++) {
+            const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+            any |= bc[rowbase + xa] != bc[rowbase + xb + 1];
+          }
+        if (!any) continue;
+      }
       for (unsigned p1base = item.z; p1base < item.w; p1base += TB) {
         const unsigned p1 = p1base + threadIdx.x;
         const bool act = p1 < item.w;
@@ -275,7 +298,7 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
           p.y = pc1.y;
           p.z = pc1.z;
           p.vr = velrhop[p1];
-          p.pr = press[p1];
+          p.pr = bitem ? 0.f : press[p1];
         } else {
           p.x = p.y = p.z = 1e30f;  // never within the support radius
           p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
@@ -284,7 +307,8 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
         p.inv_rho = frcp(p.vr.w);
         const int lxa = max(cx1 - 1, 0), lxb = min(cx1 + 1, g.ncx - 1);
         TAcc f = {0, 0, 0, 0, 0, 0}, bnd = {0, 0, 0, 0, 0, 0};
-        for (int pass = 0; pass < 2; pass++) {
+        const int npass = bitem ? 1 : 2;
+        for (int pass = 0; pass < npass; pass++) {
           const unsigned cellinit = (pass == 0 ? g.boxfluid : 0u);
           for (int z = max(cz - 1, 0); z <= min(cz + 1, g.ncz - 1); z++) {
             const float rz = p.z + float(cz - z) * K.scell;
@@ -308,15 +332,21 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
                 __syncthreads();
                 const int s0 = int(max(ls, seg) - seg);
                 const int s1 = act ? int(min(le, seg + segn)) - int(seg) : 0;
-                if (pass == 0)
-                  tile_range<TDENSITY, false>(K, p, ry, rz, s0, s1, sA, sB, sP, K.massfluid, cvisc_f, f);
+                if (bitem)
+                  tile_range<TDENSITY, 2>(K, p, ry, rz, s0, s1, sA, sB, sP, K.massfluid, 0.f, f);
+                else if (pass == 0)
+                  tile_range<TDENSITY, 0>(K, p, ry, rz, s0, s1, sA, sB, sP, K.massfluid, cvisc_f, f);
                 else
-                  tile_range<TDENSITY, true>(K, p, ry, rz, s0, s1, sA, sB, sP, K.massbound, cvisc_b, bnd);
+                  tile_range<TDENSITY, 1>(K, p, ry, rz, s0, s1, sA, sB, sP, K.massbound, cvisc_b, bnd);
               }
             }
           }
         }
-        if (act) {
+        if (act && bitem) {
+          // InteractionForcesBound store (JSphCpu.cpp:617-621).
+          if (f.ar != 0.f || f.visc != 0.f) arace[p1] = make_float4(0.f, 0.f, 0.f, 0.f + f.ar);
+          viscmax = fmaxf(viscmax, f.visc);
+        } else if (act) {
           // Combine exactly as the two CPU passes store (JSphCpu.cpp:800-818).
           float ar = 0.f, ax = 0.f, ay = 0.f, az = 0.f, delta = 0.f;
           if (f.ar != 0.f || f.ax != 0.f || f.ay != 0.f || f.az != 0.f || f.visc != 0.f) {
@@ -341,8 +371,8 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
       }
     }
   }
-  wave_max_atomic(&sc->viscdt, viscmax);
-  wave_max_atomic(&sc->acemax2, ace2max);
+  wave_max_atomic(sc, RED_VISCDT, viscmax);
+  wave_max_atomic(sc, RED_ACEMAX2, ace2max);
 }
 
 void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,

@@ -210,8 +210,8 @@ void SphGpuSingle::Alloc() {
   press_ = (float*)dmalloc(4 * n);
   arace_ = (float4*)dmalloc(16 * n);
   begincell_ = (unsigned*)dmalloc(4 * size_t(G.nctt));
-  items_ = (uint4*)dmalloc(16 * size_t(G.nct + 1));
-  rowtmp_ = (unsigned*)dmalloc(4 * size_t(G.ncy) * size_t(G.ncz));
+  items_ = (uint4*)dmalloc(16 * (2 * size_t(G.nct) + 1));
+  rowtmp_ = (unsigned*)dmalloc(4 * 2 * size_t(G.ncy) * size_t(G.ncz));
   qctr_ = (unsigned*)dmalloc(4 * 8);
   for (int i = 0; i < 2; i++) {
     sort_.keys[i] = (unsigned*)dmalloc(4 * n);
@@ -329,9 +329,10 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
   TimedBegin(0);
   if (tiled_) {
     check_hip(hipMemsetAsync(qctr_, 0, 4 * 8, stream), "reset work counters");
+    // Boundary rows without fluid neighbours are skipped by the tiled kernel: their ar=0.
+    check_hip(hipMemsetAsync(arace_, 0, sizeof(float4) * npb0_, stream), "zero boundary arace");
     launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, begincell_, G, K,
                        arace_);
-    launch_interaction_bound(stream, npb0_, sc_, poscell_, cur_.velrhop, begincell_, G, K, arace_);
   } else {
     launch_interaction(stream, cap_, sc_, poscell_, cur_.velrhop, press_, begincell_, G, K, arace_);
   }
@@ -468,10 +469,10 @@ void SphGpuSingle::DownloadInteraction(SphInterOut& out) {
   out.velmax = s.velmax;
   out.acemax = s.acemax;
   out.viscdtmax = s.viscdtmax;
-  // Leave the device maxima as a fresh interaction would find them.
-  const unsigned zero3[3] = {0, 0, 0};
-  check_hip(hipMemcpyAsync(&sc_->acemax2, zero3, 4, hipMemcpyHostToDevice, stream), "reset acemax");
-  check_hip(hipMemcpyAsync(&sc_->viscdt, zero3 + 1, 4, hipMemcpyHostToDevice, stream), "reset viscdt");
+  // Leave the device maxima as a fresh interaction would find them (VelMax stays:
+  // it belongs to the last divide).
+  check_hip(hipMemsetAsync(&sc_->red[RED_ACEMAX2][0], 0, 4 * RED_SLOTS, stream), "reset acemax");
+  check_hip(hipMemsetAsync(&sc_->red[RED_VISCDT][0], 0, 4 * RED_SLOTS, stream), "reset viscdt");
   Sync();
 }
 

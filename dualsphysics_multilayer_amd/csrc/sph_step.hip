@@ -15,18 +15,29 @@ namespace sphx {
 
 __global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double dtmin, double cs0, int mode,
                      double* __restrict__ dttrace, unsigned tracecap) {
-  if (threadIdx.x != 0) return;
-  const float velmaxf = sqrtf(__uint_as_float(sc->velmax2));  // CalcVelMaxOmp returns float sqrt
+  // One wave folds the reduction slots (max of non-negative floats as uint bits).
+  const unsigned l = threadIdx.x;
+  unsigned mv = sc->red[RED_VELMAX2][l], ma = sc->red[RED_ACEMAX2][l], mvd = sc->red[RED_VISCDT][l];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    mv = max(mv, (unsigned)__shfl_xor((int)mv, off, 64));
+    ma = max(ma, (unsigned)__shfl_xor((int)ma, off, 64));
+    mvd = max(mvd, (unsigned)__shfl_xor((int)mvd, off, 64));
+  }
+  if (mode != DT_PEEK) {
+    sc->red[RED_VELMAX2][l] = 0u;
+    sc->red[RED_ACEMAX2][l] = 0u;
+    sc->red[RED_VISCDT][l] = 0u;
+  }
+  if (l != 0) return;
+  const float velmaxf = sqrtf(__uint_as_float(mv));  // CalcVelMaxOmp returns float sqrt
   const double velmax = double(velmaxf);
-  const double acemax = sqrt(double(__uint_as_float(sc->acemax2)));
-  const float viscdt = __uint_as_float(sc->viscdt);
+  const double acemax = sqrt(double(__uint_as_float(ma)));
+  const float viscdt = __uint_as_float(mvd);
   sc->last_velmax = velmaxf;
   sc->last_acemax = float(acemax);
   sc->last_viscdt = viscdt;
   if (mode == DT_PEEK) return;
-  sc->velmax2 = 0u;
-  sc->acemax2 = 0u;
-  sc->viscdt = 0u;
   const double kh = double(K.kernelh);
   const double dt1 = (acemax ? sqrt(kh / acemax) : DBL_MAX);
   const double dt2 = kh / (fmax(cs0, velmax * 10.) + kh * double(viscdt));

@@ -48,14 +48,15 @@ def test_initial_divide_order_is_the_oracles():
 def test_pair_counts_match_oracle():
     """Checked candidates (the cell search itself) are bit-exact.  Real pairs may differ
     by float rounding of |r|^2 at the support radius: on the initial lattice
-    2h = 2*sqrt(3)*dp, so every (2,2,2)*dp neighbour sits exactly at r = 2h and its
-    inclusion is decided by the last bit of rr2 (fac = 0 there, so such a pair adds
-    nothing to ace/ar)."""
+    2h = 2*sqrt(3)*dp, so the 8 (+-2,+-2,+-2)*dp neighbours of every particle (~5% of its
+    ~167 real pairs) sit exactly at r = 2h and their inclusion is decided by the last bit
+    of rr2 (fac = 0 there, so such a pair adds nothing to ace/ar).  Once particles have
+    moved, the ties are gone and the counts agree to a few pairs."""
     case = DamBreakCase(0.025, celldomfixed=True)
     g, o = gpu(case), oracle.OracleSolver(case, nthreads=4)
     cg, co = g.count_pairs().astype(np.int64), o.count_pairs().astype(np.int64)
     assert np.array_equal(cg[[0, 2, 4]], co[[0, 2, 4]])
-    assert np.all(np.abs(cg[[1, 3, 5]] - co[[1, 3, 5]]) <= 0.02 * co[[1, 3, 5]])
+    assert np.all(np.abs(cg[[1, 3, 5]] - co[[1, 3, 5]]) <= 0.06 * co[[1, 3, 5]])
     g.run(15)
     o.run(15)
     cg, co = g.count_pairs().astype(np.int64), o.count_pairs().astype(np.int64)
