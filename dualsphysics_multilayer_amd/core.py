@@ -27,7 +27,7 @@ from ._abi import (
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libsphcore.so")
+LIB_PATH = os.environ.get("SPH_LIB") or os.path.join(HERE, "lib", "libsphcore.so")
 
 INTERSTEP_VERLET, INTERSTEP_SYMPREDICTOR, INTERSTEP_SYMCORRECTOR = 1, 2, 3
 

@@ -57,6 +57,8 @@ struct KConst {
   double scelld;
   unsigned domcellcode;
   int tdensity;
+  // derived for the tiled kernel
+  float mhalfovh, bwenovh, ddtkhcs, ddtc1, ddtc2, ddtc3, ddtc4, pad;
 };
 
 // Cell grid of the (fixed) divide domain — StDivDataGpu (JCellDivDataGpu.h:26-79).

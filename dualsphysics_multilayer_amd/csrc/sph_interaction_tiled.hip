@@ -26,8 +26,17 @@
 
 namespace sphx {
 
+#ifndef SPH_ABLATE
+#define SPH_ABLATE 0  // diagnostic builds: 1 = no pair body, 2 = no candidate test/body, 3 = no staging loads
+#endif
 constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
-constexpr int TCAP = 512;      // staged neighbour records per segment (8+8+2 KB LDS)
+#ifndef SPH_TCAP
+#define SPH_TCAP 384
+#endif
+#ifndef SPH_PIPE
+#define SPH_PIPE 0
+#endif
+constexpr int TCAP = SPH_TCAP;  // staged neighbour records per segment
 constexpr int TMAXCELLS = 4;   // max x-cells per item
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
@@ -133,74 +142,75 @@ struct P1 {
 // One pair body (JSphCpu.cpp:682-797 semantics, fast f32 intrinsics).
 // MODE 0: fluid p1 / fluid p2, 1: fluid p1 / bound p2, 2: bound p1 / fluid p2
 // (InteractionForcesBound, JSphCpu.cpp:577-612: continuity + visc-dt only).
+// `ok` = the reference's pair test (rr2 <= KernelSize2 && rr2 >= ALMOSTZERO); a pair
+// with !ok contributes exactly +0 (fac forced to 0, visc term masked), which keeps the
+// body branch-free so two pairs can be interleaved.
+// Algebra used (same quantities, fewer operations):
+//   fac = bwen*q*(1-q/2)^3/rad = (bwen/h)*(1-q/2)^3          (FunSphKernel.h:217-224)
+//   dv.fr = fac*(dr.dv), dr.fr = fac*rr2
+//   momentum + artificial viscosity: ace += fac*(p_vpm - pi_visc)*dr
+//   DDT2: rho0*(1+x)^(1/gamma) - rho0 = rho0*x*(c1+x*(c2+x*(c3+x*c4))), x = ddtgz*drz
+//         (binomial series; |x| <= 2h*ddtgz ~ 1e-3, 5th term < 1e-9 relative), which also
+//         avoids the float cancellation of the reference's rho0*powf(rh,1/gamma)-rho0.
+struct P2 {
+  float4 A;   // x, y, z (block frame), |A|^2
+  float4 B;   // vx, vy, vz, rho
+  float2 C;   // press, 1/rho
+};
+
 template <int TDENSITY, int MODE>
 __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float drx, float dry, float drz, float rr2,
-                                          float4 A, float4 B, float massp2, float cvisc, TAcc& a) {
-  constexpr bool BOUNDP2 = (MODE == 1);
+                                          bool ok, const float4& B, const float2& C, float massp2, float cvisc,
+                                          TAcc& a) {
   const float rad = fsqrt_(rr2);
-  const float wqq1 = 1.f - 0.5f * (rad * K.ovkernelh);
-  const float fac = K.bwen * K.ovkernelh * (wqq1 * wqq1 * wqq1);
-  const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
-  const float inv2 = frcp(B.w);
-  if (MODE == 2) {
-    const float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
-    a.ar += massp2 * (dvx * frx + dvy * fry + dvz * frz) * (p.vr.w * inv2);
-    const float dot = drx * dvx + dry * dvy + drz * dvz;
-    a.visc = fmaxf(dot * frcp(rr2 + K.eta2), a.visc);
+  const float wqq1 = fmaf(K.mhalfovh, rad, 1.f);
+  const float fac = ok ? K.bwenovh * (wqq1 * wqq1 * wqq1) : 0.f;
+  const float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
+  const float dot = drx * dvx + dry * dvy + drz * dvz;
+  const float r12 = p.vr.w * C.y;  // rho1/rho2
+  const float inv_re = frcp(rr2 + K.eta2);
+  const float dot_rr2 = ok ? dot * inv_re : 0.f;
+  a.visc = fmaxf(dot_rr2, a.visc);
+  const float facm = fac * massp2;
+  a.ar += facm * dot * r12;
+  if (MODE == 2) return;
+  const float p_vpm = -(p.pr + C.x) * (p.inv_rho * C.y) * massp2;
+  const float pi_visc = (dot < 0.f) ? cvisc * dot_rr2 * frcp((p.vr.w + B.w) * 0.5f) : 0.f;
+  const float c = fac * (p_vpm - pi_visc);
+  a.ax += c * drx;
+  a.ay += c * dry;
+  a.az += c * drz;
+  if (MODE == 1) {
+    if ((TDENSITY == 1 || TDENSITY == 2) && ok) a.delta = FLT_MAX;  // DBC: no DDT next to the boundary
     return;
   }
-  {  // momentum
-    const float prs = (p.pr + A.w) * (p.inv_rho * inv2);
-    const float p_vpm = -prs * massp2;
-    a.ax += p_vpm * frx;
-    a.ay += p_vpm * fry;
-    a.az += p_vpm * frz;
-  }
-  const float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
-  a.ar += massp2 * (dvx * frx + dvy * fry + dvz * frz) * (p.vr.w * inv2);
-  const float inv_re = frcp(rr2 + K.eta2);
-  if (TDENSITY == 1 && a.delta != FLT_MAX) {
-    if (BOUNDP2) a.delta = FLT_MAX;
-    else {
-      const float visc_densi = K.ddtkh * K.cs0f * (p.vr.w * inv2 - 1.f) * inv_re;
-      const float dot3 = drx * frx + dry * fry + drz * frz;
-      a.delta += visc_densi * dot3 * massp2;
-    }
-  }
-  if ((TDENSITY == 2 || (TDENSITY == 3 && !BOUNDP2)) && a.delta != FLT_MAX) {
-    if (BOUNDP2) a.delta = FLT_MAX;
-    else {
-      const float rh = 1.f + K.ddtgz * drz;
-      const float drhop = K.rhopzero * fexp2(K.ovgamma * flog2(rh)) - K.rhopzero;
-      const float visc_densi = K.ddtkh * K.cs0f * ((B.w - p.vr.w) - drhop) * inv_re;
-      const float dot3 = drx * frx + dry * fry + drz * frz;
-      a.delta -= visc_densi * dot3 * massp2 * inv2;
-    }
-  }
-  const float dot = drx * dvx + dry * dvy + drz * dvz;
-  const float dot_rr2 = dot * inv_re;
-  a.visc = fmaxf(dot_rr2, a.visc);
-  if (dot < 0.f) {
-    // pi_visc = (-visco*cbar*h*dot_rr2/robar)*massp2, cvisc = -visco*cbar*h*massp2
-    const float pi_visc = cvisc * dot_rr2 * frcp((p.vr.w + B.w) * 0.5f);
-    a.ax -= pi_visc * frx;
-    a.ay -= pi_visc * fry;
-    a.az -= pi_visc * frz;
+  if (TDENSITY == 1) {
+    a.delta += K.ddtkhcs * (r12 - 1.f) * inv_re * (facm * rr2);
+  } else if (TDENSITY == 2 || TDENSITY == 3) {
+    const float x = K.ddtgz * drz;
+    float drhop;
+    if (fabsf(x) < 0.05f) drhop = K.rhopzero * x * fmaf(x, fmaf(x, fmaf(x, K.ddtc4, K.ddtc3), K.ddtc2), K.ddtc1);
+    else drhop = K.rhopzero * fexp2(K.ovgamma * flog2(1.f + x)) - K.rhopzero;
+    a.delta -= K.ddtkhcs * ((B.w - p.vr.w) - drhop) * inv_re * (facm * rr2) * C.y;
   }
 }
 
 // Candidates [s0,s1) of the staged segment: test 128 at a time into bit masks, then
-// run the pair body over the set bits.  The test uses the staged |A|^2 (sA.w):
-// |p-A|^2 = |p|^2 + |A|^2 - 2 p.A  -> 3 FMAs + 1 compare per candidate on one
-// ds_read_b128, against a threshold inflated by 1e-4 (the rounding of the expanded
-// form is ~1e-6 relative); the body recomputes |p-A|^2 exactly and applies the
-// reference's test (rr2 <= KernelSize2 && rr2 >= ALMOSTZERO), so no pair is lost or added.
+// run the pair body over the set bits, two pairs per iteration.  The test uses the
+// staged |A|^2 (sA.w): |p-A|^2 = |p|^2 + |A|^2 - 2 p.A  -> 3 FMAs + 1 compare per
+// candidate on one ds_read_b128, against a threshold inflated by 1e-4 (the rounding of
+// the expanded form is ~1e-6 relative); the body recomputes |p-A|^2 exactly and applies
+// the reference's test, so no pair is lost or added.
 template <int TDENSITY, int MODE>
 __device__ __forceinline__ void tile_range(const KConst& K, const P1& p, float ry, float rz, int s0, int s1,
                                            const float4* __restrict__ sA, const float4* __restrict__ sB,
-                                           const float* __restrict__ sP, float massp2, float cvisc, TAcc& a) {
+                                           const float2* __restrict__ sC, float massp2, float cvisc, TAcc& a) {
   const float px2 = -2.f * p.x, py2 = -2.f * ry, pz2 = -2.f * rz;
   const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + ry * ry + rz * rz);
+#if SPH_ABLATE == 2
+  a.visc += float(s1 - s0);
+  return;
+#endif
   for (int base = s0; base < s1; base += 128) {
     unsigned long long m0 = 0, m1 = 0;
     const int n0 = s1 - base;  // candidates left for this lane (> 0)
@@ -221,24 +231,72 @@ __device__ __forceinline__ void tile_range(const KConst& K, const P1& p, float r
       if (jo < 8) m0 |= (unsigned long long)bits << (jo * 8);
       else m1 |= (unsigned long long)bits << ((jo - 8) * 8);
     }
-    while (m0 | m1) {
-      int j;
-      if (m0) {
-        j = __ffsll((long long)m0) - 1;
-        m0 &= m0 - 1;
-      } else {
-        j = 64 + __ffsll((long long)m1) - 1;
-        m1 &= m1 - 1;
-      }
-      const float4 A = sA[base + j];
-      const float drx = p.x - A.x, dry = ry - A.y, drz = rz - A.z;
-      const float rr2 = drx * drx + dry * dry + drz * drz;
-      if (rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO) {
-        const float4 B = sB[base + j];
-        pair_body<TDENSITY, MODE>(K, p, drx, dry, drz, rr2, make_float4(A.x, A.y, A.z, sP[base + j]), B, massp2,
-                                     cvisc, a);
+#if SPH_ABLATE == 1
+    a.visc += float(__popcll(m0) + __popcll(m1));
+    m0 = m1 = 0;
+#endif
+    // Value selects only: a branch that picks m0 or m1 by reference makes the compiler
+    // take their address and keep both masks in scratch (a memory round trip per pair).
+    auto pop = [&](void) -> int {
+      const bool lo = m0 != 0ull;
+      const unsigned long long m = lo ? m0 : m1;
+      const int j = int(__builtin_ctzll(m | (1ull << 63))) + (lo ? 0 : 64);
+      const unsigned long long mm = m & (m - 1ull);
+      m0 = lo ? mm : m0;
+      m1 = lo ? m1 : mm;
+      return j;
+    };
+#if SPH_PIPE
+    // Software-pipelined drain: the LDS reads of the next two pairs are issued before
+    // the current two are computed.
+    if (m0 | m1) {
+      int j1 = base + pop();
+      bool two = (m0 | m1) != 0ull;
+      int j2 = two ? base + pop() : j1;
+      float4 A1 = sA[j1], A2 = sA[j2], B1 = sB[j1], B2 = sB[j2];
+      float2 C1 = sC[j1], C2 = sC[j2];
+      for (;;) {
+        const bool more = (m0 | m1) != 0ull;
+        int n1 = j1, n2 = j2;
+        bool ntwo = false;
+        if (more) {
+          n1 = base + pop();
+          ntwo = (m0 | m1) != 0ull;
+          n2 = ntwo ? base + pop() : n1;
+        }
+        const float4 nA1 = sA[n1], nA2 = sA[n2], nB1 = sB[n1], nB2 = sB[n2];
+        const float2 nC1 = sC[n1], nC2 = sC[n2];
+        const float drx1 = p.x - A1.x, dry1 = ry - A1.y, drz1 = rz - A1.z;
+        const float drx2 = p.x - A2.x, dry2 = ry - A2.y, drz2 = rz - A2.z;
+        const float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
+        const float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
+        const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
+        const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
+        pair_body<TDENSITY, MODE>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, massp2, cvisc, a);
+        pair_body<TDENSITY, MODE>(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, massp2, cvisc, a);
+        if (!more) break;
+        j1 = n1; j2 = n2; two = ntwo;
+        A1 = nA1; A2 = nA2; B1 = nB1; B2 = nB2; C1 = nC1; C2 = nC2;
       }
     }
+#else
+    while (m0 | m1) {
+      const int j1 = base + pop();
+      const bool two = (m0 | m1) != 0ull;
+      const int j2 = two ? base + pop() : j1;
+      const float4 A1 = sA[j1], A2 = sA[j2];
+      const float4 B1 = sB[j1], B2 = sB[j2];
+      const float2 C1 = sC[j1], C2 = sC[j2];
+      const float drx1 = p.x - A1.x, dry1 = ry - A1.y, drz1 = rz - A1.z;
+      const float drx2 = p.x - A2.x, dry2 = ry - A2.y, drz2 = rz - A2.z;
+      const float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
+      const float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
+      const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
+      const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
+      pair_body<TDENSITY, MODE>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, massp2, cvisc, a);
+      pair_body<TDENSITY, MODE>(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, massp2, cvisc, a);
+    }
+#endif
   }
 }
 
@@ -251,7 +309,7 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
                                                     float4* __restrict__ arace) {
   __shared__ float4 sA[TCAP + 128];  // +128: over-read pad of the 8-wide candidate test
   __shared__ float4 sB[TCAP];
-  __shared__ float sP[TCAP];
+  __shared__ float2 sC[TCAP];  // press, 1/rho
   __shared__ unsigned s_item;
   const unsigned nitems = sc->nitems;
   const unsigned per = (nitems + 7) / 8;
@@ -321,23 +379,28 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
               for (unsigned seg = rs; seg < re; seg += TCAP) {
                 const unsigned segn = min(unsigned(TCAP), re - seg);
                 __syncthreads();
+#if SPH_ABLATE != 3
                 for (unsigned i = threadIdx.x; i < segn; i += TB) {
+#else
+                for (unsigned i = threadIdx.x; i < 0; i += TB) {
+#endif
                   const float4 pc = poscell[seg + i];
                   const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
                   const float x2 = pc.x + float(cx2 - xo) * K.scell;
                   sA[i] = make_float4(x2, pc.y, pc.z, x2 * x2 + pc.y * pc.y + pc.z * pc.z);
-                  sB[i] = velrhop[seg + i];
-                  sP[i] = press[seg + i];
+                  const float4 vr = velrhop[seg + i];
+                  sB[i] = vr;
+                  sC[i] = make_float2(press[seg + i], frcp(vr.w));
                 }
                 __syncthreads();
                 const int s0 = int(max(ls, seg) - seg);
                 const int s1 = act ? int(min(le, seg + segn)) - int(seg) : 0;
                 if (bitem)
-                  tile_range<TDENSITY, 2>(K, p, ry, rz, s0, s1, sA, sB, sP, K.massfluid, 0.f, f);
+                  tile_range<TDENSITY, 2>(K, p, ry, rz, s0, s1, sA, sB, sC, K.massfluid, 0.f, f);
                 else if (pass == 0)
-                  tile_range<TDENSITY, 0>(K, p, ry, rz, s0, s1, sA, sB, sP, K.massfluid, cvisc_f, f);
+                  tile_range<TDENSITY, 0>(K, p, ry, rz, s0, s1, sA, sB, sC, K.massfluid, cvisc_f, f);
                 else
-                  tile_range<TDENSITY, 1>(K, p, ry, rz, s0, s1, sA, sB, sP, K.massbound, cvisc_b, bnd);
+                  tile_range<TDENSITY, 1>(K, p, ry, rz, s0, s1, sA, sB, sC, K.massbound, cvisc_b, bnd);
               }
             }
           }

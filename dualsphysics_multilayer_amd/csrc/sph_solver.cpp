@@ -122,6 +122,16 @@ static KConst make_kconst(const SphConstants& c) {
   K.scelld = double(c.scell);
   K.domcellcode = c.dom_cellcode;
   K.tdensity = c.tdensity;
+  K.mhalfovh = -0.5f * K.ovkernelh;
+  K.bwenovh = c.bwen * K.ovkernelh;
+  K.ddtkhcs = c.ddtkh * K.cs0f;
+  {  // binomial coefficients of (1+x)^(1/gamma) - 1
+    const double a = 1.0 / double(c.gamma);
+    K.ddtc1 = float(a);
+    K.ddtc2 = float(a * (a - 1) / 2);
+    K.ddtc3 = float(a * (a - 1) * (a - 2) / 6);
+    K.ddtc4 = float(a * (a - 1) * (a - 2) * (a - 3) / 24);
+  }
   return K;
 }
 
