@@ -1,11 +1,11 @@
-"""ctypes mirror of the POD structs in include/sphcore.h (ABI version 1)."""
+"""ctypes mirror of the POD structs in include/sphcore.h (ABI version 2)."""
 from __future__ import annotations
 
 import ctypes as C
 
 import numpy as np
 
-SPH_ABI_VERSION = 1
+SPH_ABI_VERSION = 2
 
 SPH_STATUS = {
     0: "SPH_OK",
@@ -16,6 +16,7 @@ SPH_STATUS = {
     5: "SPH_ERR_BOUNDOUT",
     6: "SPH_ERR_NOMEM",
     7: "SPH_ERR_UNSUPPORTED",
+    8: "SPH_ERR_COMM",
 }
 
 
@@ -155,6 +156,16 @@ class SphInterOut(C.Structure):
     ]
 
 
+class SphSlabDef(C.Structure):
+    _fields_ = [
+        ("rank", C.c_int32),
+        ("nranks", C.c_int32),
+        ("cx_begin", C.c_int32),
+        ("cx_end", C.c_int32),
+        ("comm_id", C.c_ubyte * 128),
+    ]
+
+
 def _ptr(arr: np.ndarray | None, ctype):
     if arr is None:
         return C.POINTER(ctype)()
@@ -197,4 +208,5 @@ def check_struct_sizes() -> dict:
         "SphRunStats": C.sizeof(SphRunStats),
         "SphParticlesHost": C.sizeof(SphParticlesHost),
         "SphInterOut": C.sizeof(SphInterOut),
+        "SphSlabDef": C.sizeof(SphSlabDef),
     }

@@ -15,7 +15,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUTDIR = os.path.join(HERE, "lib")
 LIBNAME = "libsphcore.so"
-SOURCES = ["sph_divide.hip", "sph_interaction.hip", "sph_interaction_tiled.hip", "sph_step.hip", "sph_solver.cpp", "sph_capi.cpp"]
+SOURCES = ["sph_divide.hip", "sph_interaction.hip", "sph_interaction_tiled.hip", "sph_step.hip", "sph_slab.hip",
+           "sph_solver.cpp", "sph_comm.cpp", "sph_capi.cpp"]
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+LDFLAGS = ["-L" + os.path.join(ROCM, "lib"), "-lrccl", "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-pthread"]
 ARCH = os.environ.get("SPH_OFFLOAD_ARCH", "gfx950")
 
 
@@ -84,7 +87,7 @@ def _build(force: bool, verbose: bool, defines: list) -> str:
                     raise RuntimeError("HIP compile failed: %s" % cmd[-3])
     out = lib_path()
     if jobs or not os.path.exists(out):
-        cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out] + objs
+        cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out] + objs + LDFLAGS
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode:
             raise RuntimeError("link failed:\n" + r.stdout + r.stderr)

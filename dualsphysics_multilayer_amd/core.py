@@ -24,6 +24,7 @@ from ._abi import (
     SphConstants,
     SphInterOut,
     SphRunStats,
+    SphSlabDef,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -52,6 +53,13 @@ EXPORTED_SYMBOLS = (
     "sph_count_pairs",
     "sph_solver_set_timing",
     "sph_solver_timing",
+    "sph_slab_partition",
+    "sph_comm_unique_id",
+    "sph_slab_create",
+    "sph_slab_group_create",
+    "sph_slab_group_destroy",
+    "sph_slab_group_run",
+    "sph_slab_group_member",
 )
 
 
@@ -90,6 +98,14 @@ def load_library(path: str = LIB_PATH):
     L.sph_count_pairs.argtypes = [vp, C.POINTER(C.c_uint64)]
     L.sph_solver_set_timing.argtypes = [vp, C.c_int]
     L.sph_solver_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
+    L.sph_slab_partition.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.c_double, C.POINTER(C.c_int32)]
+    L.sph_comm_unique_id.argtypes = [C.POINTER(C.c_ubyte)]
+    L.sph_slab_create.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.POINTER(SphSlabDef), C.POINTER(vp)]
+    L.sph_slab_group_create.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.POINTER(C.c_int32),
+                                        C.POINTER(C.c_int32), C.POINTER(vp)]
+    L.sph_slab_group_destroy.argtypes = [vp]
+    L.sph_slab_group_run.argtypes = [vp, C.c_uint32]
+    L.sph_slab_group_member.argtypes = [vp, C.c_int, C.POINTER(vp)]
     if L.sph_abi_version() != SPH_ABI_VERSION:
         raise SphError(3, "ABI version mismatch")
     _lib = L
@@ -196,3 +212,110 @@ class SphGpuSingle:
         n = C.c_uint64()
         _check(load_library().sph_solver_timing(self._h, ms.ctypes.data_as(C.POINTER(C.c_double)), C.byref(n)))
         return ms, n.value
+
+
+# ---- slab decomposition over x -------------------------------------
+def slab_partition(case, nranks: int, bound_weight: float = 0.3) -> np.ndarray:
+    """x-cell column bounds [nranks+1] balancing fluid + bound_weight*bound particles."""
+    cdef = SphCaseDef.from_dict(case.case_def())
+    init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop)
+    out = np.zeros(nranks + 1, np.int32)
+    _check(load_library().sph_slab_partition(C.byref(cdef), C.byref(init.view), nranks, bound_weight,
+                                             out.ctypes.data_as(C.POINTER(C.c_int32))))
+    return out
+
+
+def comm_unique_id() -> bytes:
+    """RCCL bootstrap id (rank 0 creates it, the host broadcasts it to every rank)."""
+    buf = (C.c_ubyte * 128)()
+    _check(load_library().sph_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class SphGpuSlab(SphGpuSingle):
+    """One slab of a domain decomposed over x, one process per GPU over RCCL.
+
+    Every rank passes the full case; `bounds` are the column bounds of all ranks
+    (slab_partition) and `comm_id` the id rank 0 created.  Run/phase calls are
+    collective.  stats()["np"] and particles() cover the owned particles only."""
+
+    def __init__(self, case, rank: int, nranks: int, bounds, comm_id: bytes, device: int = 0):
+        L = load_library()
+        self.case = case
+        self._cdef = SphCaseDef.from_dict(case.case_def())
+        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop)
+        sd = SphSlabDef(rank, nranks, int(bounds[rank]), int(bounds[rank + 1]))
+        C.memmove(sd.comm_id, comm_id, 128)
+        h = C.c_void_p()
+        _check(L.sph_slab_create(C.byref(self._cdef), C.byref(init.view), device, C.byref(sd), C.byref(h)))
+        self._h = h
+        self.bounds = np.asarray(bounds)
+        self.rank = rank
+
+
+class _SlabMember(SphGpuSingle):
+    """Borrowed member handle of a SphSlabGroup (data-out calls only)."""
+
+    def __init__(self, group, h, case):
+        self.case = case
+        self._group = group
+        self._h = h
+
+    def close(self) -> None:
+        self._h = None
+
+
+class SphSlabGroup:
+    """Several slabs of one domain in ONE process (host threads; devices may repeat).
+
+    Runs the same pack / exchange / reduce code as SphGpuSlab over device-to-device
+    copies instead of RCCL — how the decomposition is tested on a one-GPU machine."""
+
+    def __init__(self, case, bounds, devices=None):
+        L = load_library()
+        bounds = np.ascontiguousarray(bounds, np.int32)
+        n = len(bounds) - 1
+        devices = np.ascontiguousarray(devices if devices is not None else np.zeros(n), np.int32)
+        self.case = case
+        self._cdef = SphCaseDef.from_dict(case.case_def())
+        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop)
+        h = C.c_void_p()
+        _check(L.sph_slab_group_create(C.byref(self._cdef), C.byref(init.view), n,
+                                       devices.ctypes.data_as(C.POINTER(C.c_int32)),
+                                       bounds.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(h)))
+        self._h = h
+        self.bounds = bounds
+        self.members = []
+        for i in range(n):
+            m = C.c_void_p()
+            _check(L.sph_slab_group_member(h, i, C.byref(m)))
+            self.members.append(_SlabMember(self, m, case))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            for m in self.members:
+                m.close()
+            load_library().sph_slab_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def Run(self, nsteps: int) -> None:
+        """nsteps whole steps on every slab (blocks until all slabs are done)."""
+        _check(load_library().sph_slab_group_run(self._h, nsteps))
+
+    run = Run
+
+    def stats(self) -> list:
+        return [m.stats() for m in self.members]
+
+    def particles(self) -> dict:
+        """Owned particles of all slabs, merged and sorted by idp."""
+        parts = [m.particles() for m in self.members]
+        cat = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+        o = np.argsort(cat["idp"], kind="stable")
+        return {k: v[o] for k, v in cat.items()}

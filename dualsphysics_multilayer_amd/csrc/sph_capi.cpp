@@ -1,11 +1,18 @@
 // sph_capi.cpp — extern "C" boundary (include/sphcore.h) over sphx::SphGpuSingle.
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "sph_solver.hpp"
 
 struct SphSolver {
   sphx::SphGpuSingle* impl;
+  bool member;  // borrowed from a SphSlabGroup: data-out calls only
+};
+
+struct SphSlabGroup {
+  sphx::SphSlabGroup* impl;
+  std::vector<SphSolver> members;
 };
 
 namespace {
@@ -27,6 +34,13 @@ int guard(F&& f) {
     return SPH_ERR_STATE;
   }
 }
+#define NOT_MEMBER(s)                                                               \
+  do {                                                                              \
+    if ((s)->member) {                                                              \
+      g_last_error = "slab group member: step the group (sph_slab_group_run)";     \
+      return SPH_ERR_STATE;                                                         \
+    }                                                                               \
+  } while (0)
 #define NEED(x)                                   \
   do {                                            \
     if (!(x)) {                                   \
@@ -51,12 +65,13 @@ int sph_solver_create(const SphCaseDef* cdef, const SphParticlesHost* init, int 
   NEED(init->idp && init->pos && init->vel && init->rhop);
   return guard([&] {
     auto* impl = new sphx::SphGpuSingle(*cdef, *init, device);
-    *out = new SphSolver{impl};
+    *out = new SphSolver{impl, false};
   });
 }
 
 int sph_solver_destroy(SphSolver* s) {
   if (!s) return SPH_OK;
+  NOT_MEMBER(s);
   const int r = guard([&] { delete s->impl; });
   delete s;
   return r;
@@ -64,30 +79,37 @@ int sph_solver_destroy(SphSolver* s) {
 
 int sph_divide(SphSolver* s) {
   NEED(s);
+  NOT_MEMBER(s);
   return guard([&] { s->impl->RunCellDivide(); });
 }
 int sph_interaction_forces(SphSolver* s, int interstep) {
   NEED(s && interstep >= 1 && interstep <= 3);
+  NOT_MEMBER(s);
   return guard([&] { s->impl->Interaction_Forces(interstep); });
 }
 int sph_compute_dt(SphSolver* s, int final_) {
   NEED(s);
+  NOT_MEMBER(s);
   return guard([&] { s->impl->DtVariable(final_ ? sphx::DT_VERLET : sphx::DT_PEEK); });
 }
 int sph_step_verlet(SphSolver* s) {
   NEED(s);
+  NOT_MEMBER(s);
   return guard([&] { s->impl->ComputeVerlet(); });
 }
 int sph_step_symplectic_pre(SphSolver* s) {
   NEED(s);
+  NOT_MEMBER(s);
   return guard([&] { s->impl->ComputeSymplecticPre(); });
 }
 int sph_step_symplectic_cor(SphSolver* s) {
   NEED(s);
+  NOT_MEMBER(s);
   return guard([&] { s->impl->ComputeSymplecticCorr(); });
 }
 int sph_solver_run(SphSolver* s, uint32_t nsteps) {
   NEED(s);
+  NOT_MEMBER(s);
   return guard([&] { s->impl->Run(nsteps); });
 }
 int sph_solver_sync(SphSolver* s) {
@@ -111,6 +133,7 @@ int sph_download_particles(SphSolver* s, SphParticlesHost* out) {
 }
 int sph_download_interaction(SphSolver* s, SphInterOut* out) {
   NEED(s && out);
+  NOT_MEMBER(s);
   return guard([&] { s->impl->DownloadInteraction(*out); });
 }
 int sph_count_pairs(SphSolver* s, uint64_t out[6]) {
@@ -124,6 +147,65 @@ int sph_solver_set_timing(SphSolver* s, int enabled) {
 int sph_solver_timing(SphSolver* s, double out_ms[4], uint64_t* launches) {
   NEED(s && out_ms);
   return guard([&] { s->impl->Timing(out_ms, launches); });
+}
+
+int sph_slab_partition(const SphCaseDef* cdef, const SphParticlesHost* all, int nranks, double bound_weight,
+                       int32_t* cx_bounds) {
+  NEED(cdef && all && all->pos && cx_bounds && nranks >= 1);
+  return guard([&] { sphx::slab_partition(*cdef, *all, nranks, bound_weight, cx_bounds); });
+}
+
+int sph_comm_unique_id(unsigned char id[128]) {
+  NEED(id);
+  return guard([&] { sphx::rccl_unique_id(id); });
+}
+
+int sph_slab_create(const SphCaseDef* cdef, const SphParticlesHost* all, int device, const SphSlabDef* slab,
+                    SphSolver** out) {
+  NEED(cdef && all && slab && out);
+  NEED(all->idp && all->pos && all->vel && all->rhop);
+  return guard([&] {
+    sphx::check_hip(hipSetDevice(device), "hipSetDevice");
+    sphx::SlabConfig sc;
+    sc.rank = slab->rank;
+    sc.nranks = slab->nranks;
+    sc.c0 = slab->cx_begin;
+    sc.c1 = slab->cx_end;
+    auto tr = sphx::make_rccl_transport(slab->comm_id, slab->rank, slab->nranks);
+    auto* impl = new sphx::SphGpuSingle(*cdef, *all, device, sc, std::move(tr));
+    *out = new SphSolver{impl, false};
+  });
+}
+
+int sph_slab_group_create(const SphCaseDef* cdef, const SphParticlesHost* all, int nslabs, const int32_t* devices,
+                          const int32_t* cx_bounds, SphSlabGroup** out) {
+  NEED(cdef && all && devices && cx_bounds && out && nslabs >= 1);
+  NEED(all->idp && all->pos && all->vel && all->rhop);
+  return guard([&] {
+    std::vector<int> dev(devices, devices + nslabs), b(cx_bounds, cx_bounds + nslabs + 1);
+    auto* impl = new sphx::SphSlabGroup(*cdef, *all, nslabs, dev.data(), b.data());
+    auto* g = new SphSlabGroup{impl, {}};
+    for (auto& sl : impl->slabs) g->members.push_back(SphSolver{sl.get(), true});
+    *out = g;
+  });
+}
+
+int sph_slab_group_destroy(SphSlabGroup* g) {
+  if (!g) return SPH_OK;
+  const int r = guard([&] { delete g->impl; });
+  delete g;
+  return r;
+}
+
+int sph_slab_group_run(SphSlabGroup* g, uint32_t nsteps) {
+  NEED(g);
+  return guard([&] { g->impl->Run(nsteps); });
+}
+
+int sph_slab_group_member(SphSlabGroup* g, int i, SphSolver** out) {
+  NEED(g && out && i >= 0 && size_t(i) < g->members.size());
+  *out = &g->members[size_t(i)];
+  return SPH_OK;
 }
 
 }  // extern "C"

@@ -62,17 +62,28 @@ struct KConst {
 };
 
 // Cell grid of the (fixed) divide domain — StDivDataGpu (JCellDivDataGpu.h:26-79).
+// Slab decomposition (sph_slab.hip): a rank's grid covers the global x-columns
+// [xoff, xoff+ncx); the columns it owns are the local [xown0, xown1) and the
+// columns either side of them hold read-only ghost copies of the neighbours'
+// particles.  dcell stays GLOBAL (same cell code as a single domain); poscell.w
+// carries the LOCAL cell (global cx - xoff).  Single domain: xoff 0, own [0, ncx).
 struct DivGrid {
   int ncx, ncy, ncz;
   unsigned nsheet, nct;
   unsigned boxboundignore, boxfluid, boxboundout, boxfluidout, boxboundoutignore, boxfluidoutignore;
-  unsigned nctt;  // size of begincell = 2*nct + 6
+  unsigned nctt;        // size of begincell = 2*nct + 6
+  unsigned boxdiscard;  // ghosts of the previous divide and particles handed to a neighbour
+  int xoff, xown0, xown1;
 };
+
+// dcell markers: excluded particle (JSphCpu::UpdatePos, JSphCpu.cpp:1262) and a
+// particle this rank drops at the next divide (slab ghosts).
+constexpr unsigned DCELL_OUT = 0xFFFFFFFFu, DCELL_DISCARD = 0xFFFFFFFEu;
 
 // Device-resident step scalars.
 struct DevScalars {
   unsigned np, npb, npbok, nout;          // counts after the last divide
-  unsigned nitems, nitems_bound, pad0, pad1; // tiled-interaction work items (fluid, bound)
+  unsigned nitems, nitems_bound, nown, pad1; // tiled-interaction work items; owned particles (slab)
   unsigned dtmodif, error_flags, npbout, ndiv;  // ndiv: particle count entering the divide
   unsigned long long nstep;
   double dt;        // dt of the step in flight

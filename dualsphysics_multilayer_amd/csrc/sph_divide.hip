@@ -29,7 +29,12 @@ __global__ __launch_bounds__(256) void k_presort(const DevScalars* __restrict__ 
   if (p == 0) const_cast<DevScalars*>(sc)->ndiv = n;
   if (p >= n) return;
   const unsigned rcell = dcell[p];
-  const unsigned cx = DcelCellx(dcc, rcell), cy = DcelCelly(dcc, rcell), cz = DcelCellz(dcc, rcell);
+  vals[p] = p;
+  if (rcell == DCELL_DISCARD) {  // slab: stale ghost / particle handed to a neighbour
+    keys[p] = g.boxdiscard;
+    return;
+  }
+  const unsigned cx = DcelCellx(dcc, rcell) - unsigned(g.xoff), cy = DcelCelly(dcc, rcell), cz = DcelCellz(dcc, rcell);
   const unsigned cellsort = cx + cy * unsigned(g.ncx) + cz * g.nsheet;
   const typecode rcode = code[p];
   const typecode codetype = CodeType(rcode), codeout = CodeSpecial(rcode);
@@ -43,7 +48,6 @@ __global__ __launch_bounds__(256) void k_presort(const DevScalars* __restrict__ 
                                      : (codetype == CODE_TYPE_FLOATING ? g.boxboundout : g.boxfluidout));
   }
   keys[p] = box;
-  vals[p] = p;
 }
 
 void launch_presort(hipStream_t stm, unsigned cap, const DevScalars* sc, const unsigned* dcell, const typecode* code,
@@ -261,6 +265,7 @@ struct GatherArgs {
   float cteb, ovrhopzero, gamma;
   unsigned dcc;
   int withm1, withpre;
+  int xoff;
 };
 
 __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, GatherArgs a) {
@@ -285,12 +290,14 @@ __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, Gat
       a.dst.poszpre[i] = a.src.poszpre[s];
       a.dst.velrhoppre[i] = a.src.velrhoppre[s];
     }
-    // PosCell (KerUpdatePosCell): position relative to the origin of its divide cell.
+    // PosCell (KerUpdatePosCell): position relative to the origin of its divide cell
+    // (global cell -> the same floats on every slab); w = the local cell.
     const unsigned cx = DcelCellx(a.dcc, dc), cy = DcelCelly(a.dcc, dc), cz = DcelCellz(a.dcc, dc);
     const double ox = a.posminx + double(cx) * a.scelld;
     const double oy = a.posminy + double(cy) * a.scelld;
     const double oz = a.posminz + double(cz) * a.scelld;
-    a.poscell[i] = make_float4(float(pxy.x - ox), float(pxy.y - oy), float(pz - oz), __uint_as_float(dc));
+    const unsigned ldc = a.xoff ? DcelCell(a.dcc, cx - unsigned(a.xoff), cy, cz) : dc;
+    a.poscell[i] = make_float4(float(pxy.x - ox), float(pxy.y - oy), float(pz - oz), __uint_as_float(ldc));
     // Press (PreInteractionVars_Forces, JSphCpu.cpp:451-453; FunSphEos.h:37-47) as the
     // reference binary evaluates it: the unqualified pow in namespace fsph is the C
     // double pow, and -ffast-math makes rhop/rhop0 a product with 1/rhop0.
@@ -302,8 +309,9 @@ __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, Gat
 
 void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned* sortpart, const PartArrays& src,
                    const PartArrays& dst, bool withm1, bool withpre, const KConst& K, const double dom_posmin[3],
-                   float4* poscell, float* press) {
+                   float4* poscell, float* press, int xoff) {
   GatherArgs a;
+  a.xoff = xoff;
   a.src = src;
   a.dst = dst;
   a.sortpart = sortpart;

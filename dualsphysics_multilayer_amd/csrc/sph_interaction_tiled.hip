@@ -72,14 +72,16 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
   auto count = [&](int x) { return inlds ? cnt[x] : bc[rowbase + x + 1] - bc[rowbase + x]; };
   unsigned nitems = 0;
   uint4* out = WRITE ? items + counts[r] : nullptr;
-  int x = 0;
-  while (x < ncx) {
-    while (x < ncx && count(x) == 0) x++;
-    if (x >= ncx) break;
+  // p1 only in the owned columns (slab ghosts are neighbours, never p1).
+  const int xend = g.xown1;
+  int x = g.xown0;
+  while (x < xend) {
+    while (x < xend && count(x) == 0) x++;
+    if (x >= xend) break;
     const int a = x;
     unsigned n = count(x);
     x++;
-    while (x < ncx && x - a < TMAXCELLS) {
+    while (x < xend && x - a < TMAXCELLS) {
       const unsigned c = count(x);
       if (n + c > unsigned(TB)) break;
       n += c;

@@ -49,7 +49,7 @@ void launch_begincell(hipStream_t stm, unsigned cap, DevScalars* sc, const unsig
 // JSphGpuSimple_ker.cu:41-69; PreInteraction press/VelMax, JSphGpu.cpp:831-870).
 void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned* sortpart, const PartArrays& src,
                    const PartArrays& dst, bool withm1, bool withpre, const KConst& K, const double dom_posmin[3],
-                   float4* poscell, float* press);
+                   float4* poscell, float* press, int xoff);
 
 // ---- interaction (cusph::Interaction_Forces, JSphGpu_ker.cu:788-885) ----
 void launch_interaction(hipStream_t stm, unsigned cap, DevScalars* sc, const float4* poscell, const float4* velrhop,
@@ -70,11 +70,52 @@ void launch_count_pairs(hipStream_t stm, unsigned cap, const DevScalars* sc, con
 
 // ---- dt and time integration ----
 enum DtMode { DT_VERLET = 0, DT_SYM_PRE = 1, DT_SYM_COR = 2, DT_PEEK = 3 };
+// `folded` (slab mode): the three maxima already folded and max-reduced over ranks
+// (launch_fold_maxima + SlabTransport::allreduce_max_u32); nullptr = fold the slots here.
 void launch_dt(hipStream_t stm, DevScalars* sc, const KConst& K, double cfl, double dtmin, double cs0, int mode,
-               double* dttrace, unsigned tracecap);
+               double* dttrace, unsigned tracecap, const unsigned* folded = nullptr);
+void launch_fold_maxima(hipStream_t stm, DevScalars* sc, unsigned* folded3, bool clear);
+// Update kernels skip slab ghosts (local column outside [g.xown0, g.xown1)) and mark
+// them DCELL_DISCARD for the next divide.
 void launch_verlet(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, bool euler, const float4* arace,
-                   PartArrays a);
-void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a);
-void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a);
+                   PartArrays a, DivGrid g);
+void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
+                    DivGrid g);
+void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
+                    DivGrid g);
+
+// ---- slab decomposition (sph_slab.hip) ----
+// One particle crossing a slab face: full state, 96 B.  Ghost copies use the same
+// record (the *pre / m1 fields are not read for ghosts).
+struct SlabRec {
+  double2 posxy;
+  double posz;
+  unsigned idp, dcell;
+  float4 velrhop;
+  float4 vr2;  // velrhopm1 (Verlet) or velrhoppre (Symplectic, inside a step)
+  double2 posxypre;
+  double poszpre;
+  unsigned short code, flags;
+  unsigned pad;
+};
+constexpr unsigned short SLABREC_MIGRANT = 1;
+constexpr int PK_BS = 256, PK_ITEMS = 16, PK_TILE = PK_BS * PK_ITEMS;
+// Device counters of one exchange.
+struct SlabCounts {
+  unsigned long long send[2];  // records for the left / right neighbour
+  unsigned long long recv[2];
+  unsigned np;                 // particles before the exchange (sc->np)
+  unsigned nkeep;              // particles staying owned (not migrating, not dropped)
+  unsigned pad[2];
+};
+// Classify every particle after an update (stable order) and write the records for
+// the two neighbours: tile counts -> scan -> scatter.  has_left/has_right: the
+// neighbour exists.  Records beyond `sendcap` are counted but not written.
+void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, DivGrid g, const KConst& K,
+                      bool has_left, bool has_right, bool withm1, bool withpre, unsigned* tilecnt, SlabCounts* cnt,
+                      SlabRec* sendl, SlabRec* sendr, unsigned long long sendcap);
+// Append nrecv received records at [np, np+nrecv) and set sc->np, sc->nown.
+void launch_slab_unpack(hipStream_t stm, DevScalars* sc, const SlabRec* recv, unsigned np, unsigned nrecv,
+                        const PartArrays& a, bool withm1, bool withpre, SlabCounts* cnt);
 
 }  // namespace sphx

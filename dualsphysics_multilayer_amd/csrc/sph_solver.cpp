@@ -6,6 +6,8 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <thread>
 
 namespace sphx {
 
@@ -136,14 +138,28 @@ static KConst make_kconst(const SphConstants& c) {
 }
 
 // Full-map cell grid (JCellDivCpuSingle::PrepareNct, JCellDivCpuSingle.cpp:105-121, with CellDomFixed).
-static DivGrid make_grid(const SphConstants& c) {
+// A slab keeps the global y/z extent and the x-columns [c0-1, c1] (owned + one ghost
+// column per face).
+static DivGrid make_grid(const SphConstants& c, const SlabConfig* slab) {
   DivGrid g;
   g.ncx = int(c.dom_cells[0]);
   g.ncy = int(c.dom_cells[1]);
   g.ncz = int(c.dom_cells[2]);
+  g.xoff = 0;
+  g.xown0 = 0;
+  g.xown1 = g.ncx;
+  if (slab) {
+    if (slab->nranks < 1 || slab->rank < 0 || slab->rank >= slab->nranks || slab->c0 < 0 || slab->c1 <= slab->c0 ||
+        slab->c1 > g.ncx)
+      throw SphError(SPH_ERR_ARG, "invalid slab columns");
+    g.xoff = slab->c0 - 1;
+    g.ncx = slab->c1 - slab->c0 + 2;
+    g.xown0 = 1;
+    g.xown1 = 1 + slab->c1 - slab->c0;
+  }
   g.nsheet = unsigned(g.ncx) * unsigned(g.ncy);
   const unsigned long long nct = (unsigned long long)g.nsheet * unsigned(g.ncz);
-  if (nct * 2 + 6 >= (1ull << 31)) throw SphError(SPH_ERR_ARG, "the number of cells is too big");
+  if (nct * 2 + 7 >= (1ull << 31)) throw SphError(SPH_ERR_ARG, "the number of cells is too big");
   g.nct = unsigned(nct);
   g.boxboundignore = g.nct;
   g.boxfluid = g.boxboundignore + 1;
@@ -151,28 +167,100 @@ static DivGrid make_grid(const SphConstants& c) {
   g.boxfluidout = g.boxboundout + 1;
   g.boxboundoutignore = g.boxfluidout + 1;
   g.boxfluidoutignore = g.boxboundoutignore + 1;
+  g.boxdiscard = g.boxfluidoutignore + 1;
   g.nctt = g.nct * 2 + 6;
   return g;
 }
 
+// Global x-cell column of every initial particle (JSph::LoadDcellParticles, JSph.cpp:1690-1711).
+static std::vector<unsigned> initial_columns(const SphConstants& C, const SphParticlesHost& h) {
+  std::vector<unsigned> cx(h.n);
+  for (unsigned p = 0; p < h.n; p++) {
+    const double dx = h.pos[3 * p] - C.dom_posmin[0];
+    cx[p] = dx >= 0 ? unsigned(dx / double(C.scell)) : 0u;
+  }
+  return cx;
+}
+
+void slab_partition(const SphCaseDef& cdef, const SphParticlesHost& all, int nranks, double bound_weight, int* b) {
+  SphConstants C;
+  derive_constants(cdef, C);
+  const int ncx = int(C.dom_cells[0]);
+  if (nranks < 1 || nranks > ncx) throw SphError(SPH_ERR_ARG, "nranks must be in [1, x-cells]");
+  if (all.n != cdef.np) throw SphError(SPH_ERR_ARG, "particle count does not match the case");
+  std::vector<double> w(size_t(ncx), 0.0);
+  const std::vector<unsigned> cx = initial_columns(C, all);
+  for (unsigned p = 0; p < all.n; p++) w[std::min<unsigned>(cx[p], unsigned(ncx - 1))] += (p < cdef.npb ? bound_weight : 1.0);
+  std::vector<double> pre(size_t(ncx) + 1, 0.0);
+  for (int c = 0; c < ncx; c++) pre[size_t(c) + 1] = pre[size_t(c)] + w[size_t(c)];
+  b[0] = 0;
+  b[nranks] = ncx;
+  int c = 0;
+  for (int r = 1; r < nranks; r++) {
+    const double target = pre[size_t(ncx)] * double(r) / double(nranks);
+    while (c < ncx && pre[size_t(c)] < target) c++;
+    // the boundary column goes to the side that leaves the split closer to the target
+    int cut = c;
+    if (cut > 0 && target - pre[size_t(cut) - 1] < pre[size_t(cut)] - target) cut--;
+    cut = std::max(cut, b[r - 1] + 1);
+    cut = std::min(cut, ncx - (nranks - r));
+    b[r] = cut;
+  }
+}
+
 SphGpuSingle::SphGpuSingle(const SphCaseDef& cdef, const SphParticlesHost& init, int dev) : device(dev) {
+  Init(cdef, init);
+}
+
+SphGpuSingle::SphGpuSingle(const SphCaseDef& cdef, const SphParticlesHost& all, int dev, const SlabConfig& slab,
+                           std::unique_ptr<SlabTransport> transport)
+    : device(dev), transport_(std::move(transport)), slabcfg_(slab) {
+  if (!transport_) throw SphError(SPH_ERR_ARG, "slab without a transport");
+  if (transport_->rank != slab.rank || transport_->nranks != slab.nranks)
+    throw SphError(SPH_ERR_ARG, "slab rank does not match the transport");
+  Init(cdef, all);
+}
+
+void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   derive_constants(cdef, C);
   K = make_kconst(C);
-  G = make_grid(C);
+  G = make_grid(C, slab() ? &slabcfg_ : nullptr);
   step_algorithm_ = cdef.step_algorithm;
   if (init.n != cdef.np) throw SphError(SPH_ERR_ARG, "particle count does not match the case");
   if (!init.n) throw SphError(SPH_ERR_ARG, "no particles");
-  cap_ = init.n;
-  npb0_ = cdef.npb;
-  keybits_ = bits_for(G.boxfluidoutignore, 1);
+  // Particles this solver holds: all (single domain) or owned + ghost columns (slab).
+  std::vector<unsigned> sel;
+  unsigned nown = init.n;
+  if (slab()) {
+    const std::vector<unsigned> cx = initial_columns(C, init);
+    const int lo = slabcfg_.c0 - (slabcfg_.rank > 0 ? 1 : 0);
+    const int hi = slabcfg_.c1 + (slabcfg_.rank + 1 < slabcfg_.nranks ? 1 : 0);
+    nown = 0;
+    for (unsigned p = 0; p < init.n; p++) {
+      const int c = int(cx[p]);
+      if (c >= lo && c < hi) sel.push_back(p);
+      if (c >= slabcfg_.c0 && c < slabcfg_.c1) nown++;
+    }
+    if (sel.empty()) throw SphError(SPH_ERR_ARG, "slab without particles");
+  } else {
+    sel.resize(init.n);
+    for (unsigned p = 0; p < init.n; p++) sel[p] = p;
+  }
+  npb0_ = 0;
+  for (unsigned p : sel) npb0_ += (p < cdef.npb ? 1u : 0u);
+  const unsigned n = unsigned(sel.size());
+  cap_ = slab() ? n + std::max(n / 2, 65536u) : n;
+  keybits_ = bits_for(G.boxdiscard, 1);
   if (const char* e = std::getenv("SPH_INTERACTION")) tiled_ = std::string(e) != "simple";
   check_hip(hipSetDevice(device), "hipSetDevice");
   check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
   try {
-    Alloc();
-    Upload(init);
+    AllocFixed();
+    AllocParticles(cap_);
+    Upload(init, sel, nown);
     // ConfigDomain: RunCellDivide(true) (JSphCpuSingle.cpp:165-166), then InitRunGpu.
     RunCellDivide();
+    exchange_armed_ = true;
     if (step_algorithm_ == SPH_STEP_VERLET)
       check_hip(hipMemcpyAsync(cur_.velrhopm1, cur_.velrhop, sizeof(float4) * cap_, hipMemcpyDeviceToDevice, stream),
                 "init VelrhopM1");
@@ -180,28 +268,52 @@ SphGpuSingle::SphGpuSingle(const SphCaseDef& cdef, const SphParticlesHost& init,
     CheckErrors();
   } catch (...) {
     Free();
-    hipStreamDestroy(stream);
+    (void)hipStreamDestroy(stream);
+    stream = nullptr;
     throw;
   }
 }
 
 SphGpuSingle::~SphGpuSingle() {
-  if (stream) hipStreamSynchronize(stream);
+  if (stream) (void)hipStreamSynchronize(stream);
   Free();
-  for (auto& e : pending_) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
-  for (auto e : evpool_) hipEventDestroy(e);
-  if (stream) hipStreamDestroy(stream);
+  for (auto& e : pending_) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+  for (auto e : evpool_) (void)hipEventDestroy(e);
+  if (stream) (void)hipStreamDestroy(stream);
 }
 
-void SphGpuSingle::Alloc() {
+void SphGpuSingle::AllocFixed() {
   auto dmalloc = [&](size_t bytes) -> void* {
     void* p = nullptr;
     check_hip(hipMalloc(&p, std::max<size_t>(bytes, 256)), "hipMalloc");
     allocs_.push_back(p);
     return p;
   };
-  const size_t n = cap_;
+  begincell_ = (unsigned*)dmalloc(4 * size_t(G.nctt));
+  items_ = (uint4*)dmalloc(16 * (2 * size_t(G.nct) + 1));
+  rowtmp_ = (unsigned*)dmalloc(4 * 2 * size_t(G.ncy) * size_t(G.ncz));
+  qctr_ = (unsigned*)dmalloc(4 * 8);
+  sort_.digtot = (unsigned*)dmalloc(4 * (1u << RS_MAXBITS));
+  sc_ = (DevScalars*)dmalloc(sizeof(DevScalars));
+  dttrace_ = (double*)dmalloc(8 * size_t(tracecap_));
+  pairs_ = (unsigned long long*)dmalloc(8 * 6);
+  folded_ = (unsigned*)dmalloc(4 * 4);
+  slabcnt_ = (SlabCounts*)dmalloc(sizeof(SlabCounts));
+  check_hip(hipHostMalloc((void**)&sc_host_, sizeof(DevScalars), hipHostMallocDefault), "hipHostMalloc");
+  check_hip(hipHostMalloc((void**)&slabcnt_host_, sizeof(SlabCounts), hipHostMallocDefault), "hipHostMalloc");
+}
+
+// Everything sized by the particle capacity (both gather sets, sort scratch, slab tiles).
+void SphGpuSingle::AllocParticles(unsigned cap) {
+  auto dmalloc = [&](size_t bytes) -> void* {
+    void* p = nullptr;
+    check_hip(hipMalloc(&p, std::max<size_t>(bytes, 256)), "hipMalloc");
+    pallocs_.push_back(p);
+    return p;
+  };
+  const size_t n = cap;
   for (PartArrays* a : {&cur_, &alt_}) {
+    *a = PartArrays();
     a->idp = (unsigned*)dmalloc(4 * n);
     a->code = (typecode*)dmalloc(2 * n);
     a->dcell = (unsigned*)dmalloc(4 * n);
@@ -219,55 +331,87 @@ void SphGpuSingle::Alloc() {
   poscell_ = (float4*)dmalloc(16 * n);
   press_ = (float*)dmalloc(4 * n);
   arace_ = (float4*)dmalloc(16 * n);
-  begincell_ = (unsigned*)dmalloc(4 * size_t(G.nctt));
-  items_ = (uint4*)dmalloc(16 * (2 * size_t(G.nct) + 1));
-  rowtmp_ = (unsigned*)dmalloc(4 * 2 * size_t(G.ncy) * size_t(G.ncz));
-  qctr_ = (unsigned*)dmalloc(4 * 8);
   for (int i = 0; i < 2; i++) {
     sort_.keys[i] = (unsigned*)dmalloc(4 * n);
     sort_.vals[i] = (unsigned*)dmalloc(4 * n);
   }
   sort_.ntiles = unsigned((n + RS_TILE - 1) / RS_TILE);
   sort_.hist = (unsigned*)dmalloc(4 * size_t(sort_.ntiles) * (1u << RS_MAXBITS));
-  sort_.digtot = (unsigned*)dmalloc(4 * (1u << RS_MAXBITS));
-  sc_ = (DevScalars*)dmalloc(sizeof(DevScalars));
-  dttrace_ = (double*)dmalloc(8 * size_t(tracecap_));
-  pairs_ = (unsigned long long*)dmalloc(8 * 6);
-  check_hip(hipHostMalloc((void**)&sc_host_, sizeof(DevScalars), hipHostMallocDefault), "hipHostMalloc");
+  packtiles_ = (unsigned*)dmalloc(4 * 2 * ((n + PK_TILE - 1) / PK_TILE));
+  cap_ = cap;
+}
+
+void SphGpuSingle::FreeParticles() {
+  for (void* p : pallocs_) (void)hipFree(p);
+  pallocs_.clear();
 }
 
 void SphGpuSingle::Free() {
-  for (void* p : allocs_) hipFree(p);
+  FreeParticles();
+  for (void* p : allocs_) (void)hipFree(p);
   allocs_.clear();
-  if (sc_host_) hipHostFree(sc_host_);
+  for (void* p : {slabbuf_, recvbuf_})
+    if (p) (void)hipFree(p);
+  slabbuf_ = recvbuf_ = nullptr;
+  if (sc_host_) (void)hipHostFree(sc_host_);
+  if (slabcnt_host_) (void)hipHostFree(slabcnt_host_);
   sc_host_ = nullptr;
+  slabcnt_host_ = nullptr;
 }
 
-void SphGpuSingle::Upload(const SphParticlesHost& h) {
-  const unsigned n = h.n;
-  std::vector<unsigned> dcell(n);
+// Slab capacity growth (a slab gains particles as the fluid moves across it): new
+// arrays, the live [0, np_live) of the current set copied over, the old set freed.
+void SphGpuSingle::Grow(unsigned np_live, unsigned newcap) {
+  check_hip(hipStreamSynchronize(stream), "grow: sync");
+  const PartArrays old = cur_;
+  std::vector<void*> oldallocs;
+  oldallocs.swap(pallocs_);
+  AllocParticles(newcap);
+  auto cp = [&](void* dst, const void* src, size_t bytes) {
+    if (src && dst && bytes) check_hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream), "grow: copy");
+  };
+  const size_t n = np_live;
+  cp(cur_.idp, old.idp, 4 * n);
+  cp(cur_.code, old.code, 2 * n);
+  cp(cur_.dcell, old.dcell, 4 * n);
+  cp(cur_.posxy, old.posxy, 16 * n);
+  cp(cur_.posz, old.posz, 8 * n);
+  cp(cur_.velrhop, old.velrhop, 16 * n);
+  cp(cur_.velrhopm1, old.velrhopm1, 16 * n);
+  cp(cur_.posxypre, old.posxypre, 16 * n);
+  cp(cur_.poszpre, old.poszpre, 8 * n);
+  cp(cur_.velrhoppre, old.velrhoppre, 16 * n);
+  check_hip(hipStreamSynchronize(stream), "grow: copy");
+  for (void* p : oldallocs) (void)hipFree(p);
+}
+
+void SphGpuSingle::Upload(const SphParticlesHost& h, const std::vector<unsigned>& sel, unsigned nown) {
+  const unsigned n = unsigned(sel.size());
+  std::vector<unsigned> dcell(n), idp(n);
   std::vector<typecode> code(n);
   std::vector<double2> pxy(n);
   std::vector<double> pz(n);
   std::vector<float4> vr(n);
-  for (unsigned p = 0; p < n; p++) {
+  for (unsigned i = 0; i < n; i++) {
+    const unsigned p = sel[i];
+    idp[i] = h.idp[p];
     const double x = h.pos[3 * p], y = h.pos[3 * p + 1], z = h.pos[3 * p + 2];
-    pxy[p] = make_double2(x, y);
-    pz[p] = z;
-    vr[p] = make_float4(h.vel[3 * p], h.vel[3 * p + 1], h.vel[3 * p + 2], h.rhop[p]);
+    pxy[i] = make_double2(x, y);
+    pz[i] = z;
+    vr[i] = make_float4(h.vel[3 * p], h.vel[3 * p + 1], h.vel[3 * p + 2], h.rhop[p]);
     // LoadCodeParticles (JSph.cpp:1257): the case has one fixed and one fluid MK block.
-    code[p] = (p < npb0_ ? typecode(0) : CODE_TYPE_FLUID);
+    code[i] = (i < npb0_ ? typecode(0) : CODE_TYPE_FLUID);
     // JSph::CheckRhopLimits (JSph.cpp:2021-2030).
-    if (p >= npb0_ && (vr[p].w < C.rhopoutmin || C.rhopoutmax < vr[p].w))
+    if (i >= npb0_ && (vr[i].w < C.rhopoutmin || C.rhopoutmax < vr[i].w))
       throw SphError(SPH_ERR_ARG, "Initial fluid density is out of limits.");
     // JSph::LoadDcellParticles (JSph.cpp:1690-1711).
     const double dx = x - C.dom_posmin[0], dy = y - C.dom_posmin[1], dz = z - C.dom_posmin[2];
     if (!(dx >= 0 && dy >= 0 && dz >= 0 && dx < C.map_realsize[0] && dy < C.map_realsize[1] && dz < C.map_realsize[2]))
       throw SphError(SPH_ERR_ARG, "Found new particles out.");
-    dcell[p] = DcelCell(C.dom_cellcode, unsigned(dx / double(C.scell)), unsigned(dy / double(C.scell)),
+    dcell[i] = DcelCell(C.dom_cellcode, unsigned(dx / double(C.scell)), unsigned(dy / double(C.scell)),
                         unsigned(dz / double(C.scell)));
   }
-  check_hip(hipMemcpy(cur_.idp, h.idp, 4 * size_t(n), hipMemcpyHostToDevice), "upload idp");
+  check_hip(hipMemcpy(cur_.idp, idp.data(), 4 * size_t(n), hipMemcpyHostToDevice), "upload idp");
   check_hip(hipMemcpy(cur_.code, code.data(), 2 * size_t(n), hipMemcpyHostToDevice), "upload code");
   check_hip(hipMemcpy(cur_.dcell, dcell.data(), 4 * size_t(n), hipMemcpyHostToDevice), "upload dcell");
   check_hip(hipMemcpy(cur_.posxy, pxy.data(), 16 * size_t(n), hipMemcpyHostToDevice), "upload posxy");
@@ -278,6 +422,7 @@ void SphGpuSingle::Upload(const SphParticlesHost& h) {
   s.np = n;
   s.npb = npb0_;
   s.npbok = npb0_;
+  s.nown = nown;
   s.symdtpre = C.dtini;  // InitRun (JSph.cpp:2090)
   check_hip(hipMemcpy(sc_, &s, sizeof(s), hipMemcpyHostToDevice), "upload scalars");
   verletstep_ = 0;
@@ -322,13 +467,59 @@ void SphGpuSingle::Timing(double out_ms[4], uint64_t* launches) {
 }
 
 // ---- phases ------------------------------------------------------------------------
+// Slab exchange before the divide's sort: pack migrants/ghosts (device), agree on the
+// record counts with both neighbours, move the records, append what arrived.  Two
+// host waits per exchange: the send counts (to size the sends) and the receive counts.
+void SphGpuSingle::Exchange() {
+  const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET), withpre = havepre_;
+  const bool hl = transport_->has_left(), hr = transport_->has_right();
+  for (;;) {
+    check_hip(hipMemsetAsync(slabcnt_, 0, sizeof(SlabCounts), stream), "exchange: reset counts");
+    launch_slab_pack(stream, cap_, sc_, cur_, G, K, hl, hr, withm1, withpre, packtiles_, slabcnt_, sendl_, sendr_,
+                     sendcap_);
+    check_hip(hipMemcpyAsync(slabcnt_host_, slabcnt_, sizeof(SlabCounts), hipMemcpyDeviceToHost, stream),
+              "exchange: read counts");
+    Sync();
+    const unsigned long long need = std::max(slabcnt_host_->send[0], slabcnt_host_->send[1]);
+    if (need <= sendcap_) break;
+    if (slabbuf_) check_hip(hipFree(slabbuf_), "hipFree");
+    sendcap_ = need + need / 2 + 4096;
+    check_hip(hipMalloc(&slabbuf_, 2 * sizeof(SlabRec) * sendcap_), "hipMalloc send buffers");
+    sendl_ = (SlabRec*)slabbuf_;
+    sendr_ = sendl_ + sendcap_;
+  }
+  const SlabCounts c = *slabcnt_host_;
+  transport_->exchange(&slabcnt_->send[0], 8, &slabcnt_->send[1], 8, &slabcnt_->recv[0], hl ? 8 : 0,
+                       &slabcnt_->recv[1], hr ? 8 : 0, stream);
+  check_hip(hipMemcpyAsync(slabcnt_host_, slabcnt_, sizeof(SlabCounts), hipMemcpyDeviceToHost, stream),
+            "exchange: read receive counts");
+  Sync();
+  const unsigned long long rl = hl ? slabcnt_host_->recv[0] : 0, rr = hr ? slabcnt_host_->recv[1] : 0;
+  if (rl + rr > recvcap_) {
+    if (recvbuf_) check_hip(hipFree(recvbuf_), "hipFree");
+    recvcap_ = rl + rr + (rl + rr) / 2 + 4096;
+    check_hip(hipMalloc(&recvbuf_, sizeof(SlabRec) * recvcap_), "hipMalloc receive buffer");
+    recv_ = (SlabRec*)recvbuf_;
+  }
+  if (c.np + rl + rr > cap_) {
+    const unsigned long long want = (c.np + rl + rr) + (c.np + rl + rr) / 2;
+    if (want >= (1ull << 31)) throw SphError(SPH_ERR_NOMEM, "slab particle capacity overflow");
+    Grow(c.np, unsigned(want));
+  }
+  transport_->exchange(sendl_, sizeof(SlabRec) * c.send[0], sendr_, sizeof(SlabRec) * c.send[1], recv_,
+                       sizeof(SlabRec) * rl, recv_ + rl, sizeof(SlabRec) * rr, stream);
+  launch_slab_unpack(stream, sc_, recv_, c.np, unsigned(rl + rr), cur_, withm1, withpre, slabcnt_);
+}
+
 void SphGpuSingle::RunCellDivide() {
   TimedBegin(2);
+  if (slab() && exchange_armed_) Exchange();
   launch_presort(stream, cap_, sc_, cur_.dcell, cur_.code, G, C.dom_cellcode, sort_.keys[0], sort_.vals[0]);
   const int res = launch_radix_sort(stream, cap_, sc_, sort_, keybits_);
   launch_begincell(stream, cap_, sc_, sort_.keys[res], G, begincell_);
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET);
-  launch_gather(stream, cap_, sc_, sort_.vals[res], cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_);
+  launch_gather(stream, cap_, sc_, sort_.vals[res], cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_,
+                G.xoff);
   std::swap(cur_, alt_);
   if (tiled_) launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_);
   TimedEnd(2);
@@ -350,14 +541,21 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
 }
 
 void SphGpuSingle::DtVariable(int mode) {
-  launch_dt(stream, sc_, K, C.cflnumber, C.dtmin, C.cs0, mode, dttrace_, tracecap_);
+  if (slab()) {
+    // The three maxima span the whole domain: fold locally, max over all slabs.
+    launch_fold_maxima(stream, sc_, folded_, mode != DT_PEEK);
+    transport_->allreduce_max_u32(folded_, 3, stream);
+    launch_dt(stream, sc_, K, C.cflnumber, C.dtmin, C.cs0, mode, dttrace_, tracecap_, folded_);
+  } else {
+    launch_dt(stream, sc_, K, C.cflnumber, C.dtmin, C.cs0, mode, dttrace_, tracecap_);
+  }
 }
 
 void SphGpuSingle::ComputeVerlet() {
   TimedBegin(1);
   verletstep_++;
   const bool euler = !(verletstep_ < C.verlet_steps);
-  launch_verlet(stream, cap_, sc_, K, euler, arace_, cur_);
+  launch_verlet(stream, cap_, sc_, K, euler, arace_, cur_, G);
   if (euler) verletstep_ = 0;
   std::swap(cur_.velrhop, cur_.velrhopm1);
   TimedEnd(1);
@@ -369,13 +567,13 @@ void SphGpuSingle::ComputeSymplecticPre() {
   std::swap(cur_.posz, cur_.poszpre);
   std::swap(cur_.velrhop, cur_.velrhoppre);
   havepre_ = true;
-  launch_sym_pre(stream, cap_, sc_, K, arace_, cur_);
+  launch_sym_pre(stream, cap_, sc_, K, arace_, cur_, G);
   TimedEnd(1);
 }
 
 void SphGpuSingle::ComputeSymplecticCorr() {
   TimedBegin(1);
-  launch_sym_cor(stream, cap_, sc_, K, arace_, cur_);
+  launch_sym_cor(stream, cap_, sc_, K, arace_, cur_, G);
   havepre_ = false;
   TimedEnd(1);
 }
@@ -398,6 +596,7 @@ void SphGpuSingle::ComputeStep() {
 }
 
 void SphGpuSingle::Run(unsigned nsteps) {
+  check_hip(hipSetDevice(device), "hipSetDevice");
   for (unsigned s = 0; s < nsteps; s++) ComputeStep();
   check_hip(hipGetLastError(), "kernel launch");
 }
@@ -414,7 +613,7 @@ SphRunStats SphGpuSingle::Stats() {
   r.last_dt = s.last_dt;
   r.sym_dtpre = s.symdtpre;
   r.nstep = s.nstep;
-  r.np = s.np;
+  r.np = slab() ? s.nown : s.np;  // a slab reports the particles it owns (no ghosts)
   r.npb = s.npb;
   r.npbok = s.npbok;
   r.nout = s.nout;
@@ -446,25 +645,38 @@ unsigned SphGpuSingle::DtTrace(double* out, unsigned cap) {
 
 void SphGpuSingle::Download(SphParticlesHost& out) {
   const SphRunStats s = Stats();
-  const unsigned n = s.np;
-  if (out.n < n) throw SphError(SPH_ERR_ARG, "output buffer too small");
+  const unsigned n = sc_host_->np;  // held particles (a slab also holds ghosts)
+  if (out.n < s.np) throw SphError(SPH_ERR_ARG, "output buffer too small");
   std::vector<double2> pxy(n);
   std::vector<double> pz(n);
   std::vector<float4> vr(n);
+  std::vector<unsigned> idp(n), dcell(n);
+  std::vector<typecode> code(n);
   check_hip(hipMemcpy(pxy.data(), cur_.posxy, 16 * size_t(n), hipMemcpyDeviceToHost), "download posxy");
   check_hip(hipMemcpy(pz.data(), cur_.posz, 8 * size_t(n), hipMemcpyDeviceToHost), "download posz");
   check_hip(hipMemcpy(vr.data(), cur_.velrhop, 16 * size_t(n), hipMemcpyDeviceToHost), "download velrhop");
-  if (out.idp) check_hip(hipMemcpy(out.idp, cur_.idp, 4 * size_t(n), hipMemcpyDeviceToHost), "download idp");
-  if (out.code) check_hip(hipMemcpy(out.code, cur_.code, 2 * size_t(n), hipMemcpyDeviceToHost), "download code");
+  check_hip(hipMemcpy(idp.data(), cur_.idp, 4 * size_t(n), hipMemcpyDeviceToHost), "download idp");
+  check_hip(hipMemcpy(code.data(), cur_.code, 2 * size_t(n), hipMemcpyDeviceToHost), "download code");
+  if (slab()) check_hip(hipMemcpy(dcell.data(), cur_.dcell, 4 * size_t(n), hipMemcpyDeviceToHost), "download dcell");
+  unsigned k = 0;
   for (unsigned p = 0; p < n; p++) {
-    if (out.pos) { out.pos[3 * p] = pxy[p].x; out.pos[3 * p + 1] = pxy[p].y; out.pos[3 * p + 2] = pz[p]; }
-    if (out.vel) { out.vel[3 * p] = vr[p].x; out.vel[3 * p + 1] = vr[p].y; out.vel[3 * p + 2] = vr[p].z; }
-    if (out.rhop) out.rhop[p] = vr[p].w;
+    if (slab()) {  // owned particles only
+      const int lcx = int(DcelCellx(C.dom_cellcode, dcell[p])) - G.xoff;
+      if (lcx < G.xown0 || lcx >= G.xown1) continue;
+    }
+    if (out.idp) out.idp[k] = idp[p];
+    if (out.code) out.code[k] = code[p];
+    if (out.pos) { out.pos[3 * k] = pxy[p].x; out.pos[3 * k + 1] = pxy[p].y; out.pos[3 * k + 2] = pz[p]; }
+    if (out.vel) { out.vel[3 * k] = vr[p].x; out.vel[3 * k + 1] = vr[p].y; out.vel[3 * k + 2] = vr[p].z; }
+    if (out.rhop) out.rhop[k] = vr[p].w;
+    k++;
   }
-  out.n = n;
+  if (k != s.np) throw SphError(SPH_ERR_STATE, "owned particle count mismatch");
+  out.n = k;
 }
 
 void SphGpuSingle::DownloadInteraction(SphInterOut& out) {
+  if (slab()) throw SphError(SPH_ERR_UNSUPPORTED, "interaction download is single-domain only");
   // Runs one interaction on the current state (like or_interaction) and reads ar/ace back.
   // Maxima accumulated so far (VelMax from the last divide) are kept for this call.
   Interaction_Forces(1);
@@ -493,6 +705,48 @@ void SphGpuSingle::CountPairs(uint64_t out[6]) {
   check_hip(hipMemcpyAsync(h, pairs_, 8 * 6, hipMemcpyDeviceToHost, stream), "read pairs");
   Sync();
   for (int i = 0; i < 6; i++) out[i] = h[i];
+}
+
+// ---- in-process slab group -----------------------------------------------------------
+SphSlabGroup::SphSlabGroup(const SphCaseDef& cdef, const SphParticlesHost& all, int nslabs, const int* devices,
+                           const int* bounds)
+    : hub_(std::make_shared<LocalHub>(nslabs)) {
+  if (nslabs < 1) throw SphError(SPH_ERR_ARG, "nslabs < 1");
+  for (int i = 0; i < nslabs; i++) {
+    SlabConfig sc;
+    sc.rank = i;
+    sc.nranks = nslabs;
+    sc.c0 = bounds[i];
+    sc.c1 = bounds[i + 1];
+    slabs.emplace_back(new SphGpuSingle(cdef, all, devices[i], sc, make_local_transport(hub_, i)));
+  }
+}
+
+void SphSlabGroup::Run(unsigned nsteps) {
+  const size_t n = slabs.size();
+  std::vector<std::thread> th;
+  std::vector<std::exception_ptr> err(n);
+  std::vector<int> primary(n, 0);
+  for (size_t i = 0; i < n; i++)
+    th.emplace_back([&, i] {
+      try {
+        slabs[i]->Run(nsteps);
+        slabs[i]->Sync();
+      } catch (const SphError& e) {
+        err[i] = std::current_exception();
+        primary[i] = std::string(e.what()).find("aborted by another slab") == std::string::npos;
+        hub_->abort();
+      } catch (...) {
+        err[i] = std::current_exception();
+        primary[i] = 1;
+        hub_->abort();
+      }
+    });
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < n; i++)
+    if (err[i] && primary[i]) std::rethrow_exception(err[i]);
+  for (size_t i = 0; i < n; i++)
+    if (err[i]) std::rethrow_exception(err[i]);
 }
 
 }  // namespace sphx

@@ -10,11 +10,13 @@
 //     gather), the role of JArraysGpu's pools (JArraysGpu.h:134-145).
 // Errors throw SphError; the C-ABI (sph_capi.cpp) turns them into SphStatus.
 #pragma once
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "../../include/sphcore.h"
+#include "sph_comm.hpp"
 #include "sph_kernels.hpp"
 
 namespace sphx {
@@ -26,11 +28,23 @@ struct SphError : std::runtime_error {
 
 void check_hip(hipError_t e, const char* what);
 void derive_constants(const SphCaseDef& c, SphConstants& k);
+// Column bounds of a particle-count-balanced x-slab split (sph_slab_partition).
+void slab_partition(const SphCaseDef& c, const SphParticlesHost& all, int nranks, double bound_weight, int* bounds);
+
+// This rank's slab: owned global x-cell columns [c0, c1) of nranks.
+struct SlabConfig {
+  int rank = 0, nranks = 1, c0 = 0, c1 = 0;
+};
 
 class SphGpuSingle {
  public:
   SphGpuSingle(const SphCaseDef& cdef, const SphParticlesHost& init, int device);
+  // Slab of a decomposed domain: `all` is the full initial particle set; this rank
+  // keeps its owned + ghost columns and talks to its neighbours through `transport`.
+  SphGpuSingle(const SphCaseDef& cdef, const SphParticlesHost& all, int device, const SlabConfig& slab,
+               std::unique_ptr<SlabTransport> transport);
   ~SphGpuSingle();
+  bool slab() const { return transport_ != nullptr; }
 
   // Phases (JSphGpuSingle::RunCellDivide / Interaction_Forces / DtVariable / ComputeVerlet ...).
   void RunCellDivide();
@@ -60,9 +74,14 @@ class SphGpuSingle {
   hipStream_t stream = nullptr;
 
  private:
-  void Alloc();
+  void Init(const SphCaseDef& cdef, const SphParticlesHost& init);
+  void AllocFixed();
+  void AllocParticles(unsigned cap);
+  void FreeParticles();
   void Free();
-  void Upload(const SphParticlesHost& init);
+  void Grow(unsigned np_live, unsigned newcap);
+  void Upload(const SphParticlesHost& init, const std::vector<unsigned>& sel, unsigned nown);
+  void Exchange();
   void TimedBegin(int phase);
   void TimedEnd(int phase);
 
@@ -86,7 +105,22 @@ class SphGpuSingle {
   double* dttrace_ = nullptr;
   unsigned tracecap_ = 1u << 16;
   unsigned long long* pairs_ = nullptr;
-  std::vector<void*> allocs_;
+  std::vector<void*> allocs_;   // fixed-size allocations
+  std::vector<void*> pallocs_;  // capacity-sized (per-particle) allocations
+  // slab decomposition
+  std::unique_ptr<SlabTransport> transport_;
+  SlabConfig slabcfg_;
+  bool exchange_armed_ = false;  // the initial divide has no exchange (ghosts come with the case)
+  unsigned* folded_ = nullptr;   // 3 maxima for the allreduce
+  SlabCounts* slabcnt_ = nullptr;
+  SlabCounts* slabcnt_host_ = nullptr;
+  unsigned* packtiles_ = nullptr;
+  SlabRec* sendl_ = nullptr;
+  SlabRec* sendr_ = nullptr;
+  SlabRec* recv_ = nullptr;
+  unsigned long long sendcap_ = 0, recvcap_ = 0;
+  void* slabbuf_ = nullptr;
+  void* recvbuf_ = nullptr;
   // timing (hipEvents on the solver stream)
   bool timing_ = false;
   struct Ev { hipEvent_t a, b; int phase; };
@@ -95,6 +129,18 @@ class SphGpuSingle {
   double phase_ms_[4] = {0, 0, 0, 0};
   uint64_t phase_n_[4] = {0, 0, 0, 0};
   hipEvent_t cur_a_ = nullptr;
+};
+
+// Several slabs of one domain driven by host threads of one process (LocalTransport).
+class SphSlabGroup {
+ public:
+  SphSlabGroup(const SphCaseDef& cdef, const SphParticlesHost& all, int nslabs, const int* devices,
+               const int* bounds);
+  void Run(unsigned nsteps);
+  std::vector<std::unique_ptr<SphGpuSingle>> slabs;
+
+ private:
+  std::shared_ptr<LocalHub> hub_;
 };
 
 }  // namespace sphx

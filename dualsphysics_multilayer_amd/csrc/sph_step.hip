@@ -13,21 +13,53 @@
 
 namespace sphx {
 
-__global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double dtmin, double cs0, int mode,
-                     double* __restrict__ dttrace, unsigned tracecap) {
-  // One wave folds the reduction slots (max of non-negative floats as uint bits).
+// One wave folds the reduction slots (max of non-negative floats as uint bits).
+__device__ __forceinline__ void fold_slots(DevScalars* __restrict__ sc, bool clear, unsigned& mv, unsigned& ma,
+                                           unsigned& mvd) {
   const unsigned l = threadIdx.x;
-  unsigned mv = sc->red[RED_VELMAX2][l], ma = sc->red[RED_ACEMAX2][l], mvd = sc->red[RED_VISCDT][l];
+  mv = sc->red[RED_VELMAX2][l];
+  ma = sc->red[RED_ACEMAX2][l];
+  mvd = sc->red[RED_VISCDT][l];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     mv = max(mv, (unsigned)__shfl_xor((int)mv, off, 64));
     ma = max(ma, (unsigned)__shfl_xor((int)ma, off, 64));
     mvd = max(mvd, (unsigned)__shfl_xor((int)mvd, off, 64));
   }
-  if (mode != DT_PEEK) {
+  if (clear) {
     sc->red[RED_VELMAX2][l] = 0u;
     sc->red[RED_ACEMAX2][l] = 0u;
     sc->red[RED_VISCDT][l] = 0u;
+  }
+}
+
+// Slab mode: fold the local slots into folded3[0..2] for the max-allreduce over ranks
+// (the reference's single-domain CalcVelMaxOmp/ComputeAceMaxOmp/ViscDtMax reductions
+// span the whole domain, so the slabs must agree on the same three maxima).
+__global__ void k_fold(DevScalars* __restrict__ sc, unsigned* __restrict__ folded3, int clear) {
+  unsigned mv, ma, mvd;
+  fold_slots(sc, clear != 0, mv, ma, mvd);
+  if (threadIdx.x == 0) {
+    folded3[0] = mv;
+    folded3[1] = ma;
+    folded3[2] = mvd;
+  }
+}
+
+void launch_fold_maxima(hipStream_t stm, DevScalars* sc, unsigned* folded3, bool clear) {
+  hipLaunchKernelGGL(k_fold, dim3(1), dim3(64), 0, stm, sc, folded3, int(clear));
+}
+
+__global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double dtmin, double cs0, int mode,
+                     double* __restrict__ dttrace, unsigned tracecap, const unsigned* __restrict__ folded) {
+  const unsigned l = threadIdx.x;
+  unsigned mv, ma, mvd;
+  if (folded) {
+    mv = folded[0];
+    ma = folded[1];
+    mvd = folded[2];
+  } else {
+    fold_slots(sc, mode != DT_PEEK, mv, ma, mvd);
   }
   if (l != 0) return;
   const float velmaxf = sqrtf(__uint_as_float(mv));  // CalcVelMaxOmp returns float sqrt
@@ -69,8 +101,18 @@ __global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double d
 }
 
 void launch_dt(hipStream_t stm, DevScalars* sc, const KConst& K, double cfl, double dtmin, double cs0, int mode,
-               double* dttrace, unsigned tracecap) {
-  hipLaunchKernelGGL(k_dt, dim3(1), dim3(64), 0, stm, sc, K, cfl, dtmin, cs0, mode, dttrace, tracecap);
+               double* dttrace, unsigned tracecap, const unsigned* folded) {
+  hipLaunchKernelGGL(k_dt, dim3(1), dim3(64), 0, stm, sc, K, cfl, dtmin, cs0, mode, dttrace, tracecap, folded);
+}
+
+// Slab ghost: its local column is outside the owned range.  The owner updates it; here
+// it is only dropped at the next divide (fresh copies arrive with the exchange).
+__device__ __forceinline__ bool slab_ghost(const KConst& K, const DivGrid& g, unsigned* dcell, unsigned p) {
+  if (g.xown0 == 0 && g.xown1 == g.ncx) return false;  // single domain
+  const int lcx = int(DcelCellx(K.domcellcode, dcell[p])) - g.xoff;
+  if (lcx >= g.xown0 && lcx < g.xown1) return false;
+  dcell[p] = DCELL_DISCARD;
+  return true;
 }
 
 // JSphCpu::UpdatePos (JSphCpu.cpp:1240-1293), single domain, no periodic/symmetry.
@@ -92,7 +134,7 @@ __device__ __forceinline__ void update_pos(const KConst& K, double rx, double ry
     else if (outrhop) rcode = CodeSetNormal(rcode) | CODE_OUTRHOP;
     else rcode = CodeSetNormal(rcode) | CODE_OUTMOVE;
     a.code[p] = rcode;
-    a.dcell[p] = 0xFFFFFFFFu;
+    a.dcell[p] = DCELL_OUT;
   } else {
     const unsigned cx = unsigned(dx / K.scelld), cy = unsigned(dy / K.scelld), cz = unsigned(dz / K.scelld);
     a.dcell[p] = DcelCell(K.domcellcode, cx, cy, cz);
@@ -102,10 +144,10 @@ __device__ __forceinline__ void update_pos(const KConst& K, double rx, double ry
 // ComputeVerlet (JSphCpu.cpp:1381-1399): bound -> ComputeVelrhopBound, fluid -> ComputeVerletVarsFluid.
 // New values are written in velrhopm1 (the caller swaps velrhop/velrhopm1 afterwards).
 __global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ sc, KConst K, int euler,
-                                                const float4* __restrict__ arace, PartArrays a) {
+                                                const float4* __restrict__ arace, PartArrays a, DivGrid g) {
   const unsigned np = sc->np, npb = sc->npb;
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= np) return;
+  if (p >= np || slab_ghost(K, g, a.dcell, p)) return;
   const double dt = sc->dt;
   const double dt2 = (euler ? dt : dt + dt);
   const float4 ra = arace[p];
@@ -130,18 +172,18 @@ __global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ s
 }
 
 void launch_verlet(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, bool euler, const float4* arace,
-                   PartArrays a) {
+                   PartArrays a, DivGrid g) {
   const unsigned nb = (cap + 255) / 256;
-  hipLaunchKernelGGL(k_verlet, dim3(nb), dim3(256), 0, stm, sc, K, int(euler), arace, a);
+  hipLaunchKernelGGL(k_verlet, dim3(nb), dim3(256), 0, stm, sc, K, int(euler), arace, a, g);
 }
 
 // ComputeSymplecticPre (JSphCpu.cpp:1406-1504).  The caller has already moved the
 // current pos/velrhop into the *pre arrays (pointer swap); new values go to pos/velrhop.
 __global__ __launch_bounds__(256) void k_sym_pre(const DevScalars* __restrict__ sc, KConst K,
-                                                 const float4* __restrict__ arace, PartArrays a) {
+                                                 const float4* __restrict__ arace, PartArrays a, DivGrid g) {
   const unsigned np = sc->np, npb = sc->npb;
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= np) return;
+  if (p >= np || slab_ghost(K, g, a.dcell, p)) return;
   const double dt = sc->dt, dt05 = dt * .5;
   const float4 ra = arace[p];
   const float4 vp = a.velrhoppre[p];
@@ -171,17 +213,18 @@ __global__ __launch_bounds__(256) void k_sym_pre(const DevScalars* __restrict__ 
   }
 }
 
-void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a) {
+void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
+                    DivGrid g) {
   const unsigned nb = (cap + 255) / 256;
-  hipLaunchKernelGGL(k_sym_pre, dim3(nb), dim3(256), 0, stm, sc, K, arace, a);
+  hipLaunchKernelGGL(k_sym_pre, dim3(nb), dim3(256), 0, stm, sc, K, arace, a, g);
 }
 
 // ComputeSymplecticCorr (JSphCpu.cpp:1510-1606).
 __global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ sc, KConst K,
-                                                 const float4* __restrict__ arace, PartArrays a) {
+                                                 const float4* __restrict__ arace, PartArrays a, DivGrid g) {
   const unsigned np = sc->np, npb = sc->npb;
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= np) return;
+  if (p >= np || slab_ghost(K, g, a.dcell, p)) return;
   const double dt = sc->dt, dt05 = dt * .5;
   const float4 ra = arace[p];
   const float4 vr = a.velrhop[p];
@@ -214,9 +257,10 @@ __global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ 
   }
 }
 
-void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a) {
+void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
+                    DivGrid g) {
   const unsigned nb = (cap + 255) / 256;
-  hipLaunchKernelGGL(k_sym_cor, dim3(nb), dim3(256), 0, stm, sc, K, arace, a);
+  hipLaunchKernelGGL(k_sym_cor, dim3(nb), dim3(256), 0, stm, sc, K, arace, a, g);
 }
 
 }  // namespace sphx

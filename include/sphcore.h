@@ -33,7 +33,9 @@
  *                                ComputeStep_Ver/_Sym + RunCellDivide, device-resident dt
  *   sph_download_particles ..... JSphGpuSingle::ParticlesDataDown (feeds SaveData)
  *   sph_count_pairs ............ JDsPips::ComputeGpu (JDsPips.cpp:187-262) — work counter
- *   sph_slab_* ................. new: slab decomposition across GPUs
+ *   sph_slab_* ................. new: slab decomposition across GPUs; the
+ *                                reference fork runs one domain per process (JSphGpuSingle)
+ *   sph_comm_unique_id ......... RCCL bootstrap id (ncclGetUniqueId) for sph_slab_create
  */
 #ifndef SPHCORE_H
 #define SPHCORE_H
@@ -45,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SPH_ABI_VERSION 1
+#define SPH_ABI_VERSION 2
 
 typedef enum {
   SPH_OK = 0,
@@ -55,7 +57,8 @@ typedef enum {
   SPH_ERR_DT = 4,         /* dt NaN or infinite (JSphCpu.cpp:1622)       */
   SPH_ERR_BOUNDOUT = 5,   /* boundary particle excluded (JSphCpuSingle.cpp:507-518) */
   SPH_ERR_NOMEM = 6,      /* allocation failed                           */
-  SPH_ERR_UNSUPPORTED = 7 /* feature outside the implemented scope       */
+  SPH_ERR_UNSUPPORTED = 7,/* feature outside the implemented scope       */
+  SPH_ERR_COMM = 8        /* RCCL / slab exchange failure                */
 } SphStatus;
 
 /* TpStep (DualSphDef.h:316-319). */
@@ -209,6 +212,41 @@ int sph_count_pairs(SphSolver* s, uint64_t out[6]);
  * out[0]=interaction, [1]=update, [2]=divide, [3]=dt/reductions. */
 int sph_solver_set_timing(SphSolver* s, int enabled);
 int sph_solver_timing(SphSolver* s, double out_ms[4], uint64_t* launches);
+
+/* ---- slab decomposition over x -------------------------------
+ * Rank r owns the global x-cell columns [cx_begin, cx_end) and holds ghost copies of
+ * the neighbours' particles in the column either side (one column = 2h, the support
+ * radius).  Every divide exchanges migrants and ghosts with rank-1 / rank+1, every
+ * dt max-reduces VelMax/AceMax/ViscDtMax over all ranks, so every rank steps with the
+ * single-domain dt and each particle sees its single-domain neighbour set.
+ * On a slab solver: sph_solver_run and the phase calls are COLLECTIVE (all ranks
+ * call them in the same order); stats.np is the number of OWNED particles;
+ * sph_download_particles returns the owned particles only. */
+typedef struct SphSlabDef {
+  int32_t rank, nranks;
+  int32_t cx_begin, cx_end;       /* owned global x-cell columns [begin, end)        */
+  unsigned char comm_id[128];     /* sph_comm_unique_id() of rank 0, same on all ranks */
+} SphSlabDef;
+
+/* Column bounds balancing sum(fluid) + bound_weight*sum(bound) particles per rank,
+ * from the full initial particle set; cx_bounds[nranks+1] (first 0, last = cells). */
+int sph_slab_partition(const SphCaseDef* cdef, const SphParticlesHost* all, int nranks, double bound_weight,
+                       int32_t* cx_bounds);
+int sph_comm_unique_id(unsigned char id[128]);
+/* One process per GPU over RCCL: every rank passes the FULL initial particle set
+ * and keeps its owned + ghost columns. */
+int sph_slab_create(const SphCaseDef* cdef, const SphParticlesHost* all, int device, const SphSlabDef* slab,
+                    SphSolver** out);
+
+/* Several slabs in ONE process (host threads, device-to-device copies; devices may
+ * repeat).  The member handles are borrowed (no destroy); members accept the data-out
+ * calls (stats, download, dt trace, timing) but not run/phase calls — run the group. */
+typedef struct SphSlabGroup SphSlabGroup;
+int sph_slab_group_create(const SphCaseDef* cdef, const SphParticlesHost* all, int nslabs, const int32_t* devices,
+                          const int32_t* cx_bounds, SphSlabGroup** out);
+int sph_slab_group_destroy(SphSlabGroup* g);
+int sph_slab_group_run(SphSlabGroup* g, uint32_t nsteps);
+int sph_slab_group_member(SphSlabGroup* g, int i, SphSolver** out);
 
 #ifdef __cplusplus
 }
