@@ -1,15 +1,22 @@
-"""Benchmark: particle-steps/s of the SPH hot path on the 1M-particle dam break.
+"""Benchmark: particle-steps/s of the SPH hot path on the dam break (BASELINE.json).
 
-A "step" is one JSphGpuSingle::ComputeStep_Ver + RunCellDivide over the whole
-particle set (interaction, dt, Verlet update, cell sort) — BASELINE.json cfg2
-(3D dam break, 1,025,964 particles, WCSPH + artificial viscosity + DDT2, 1 GPU).
-Inputs are resident in HBM when the timed region starts.
+A "step" is one JSphGpuSingle::ComputeStep + RunCellDivide over the whole particle
+set (interaction, dt, update, cell sort).  Inputs are resident in HBM when the
+timed region starts.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--dp DP] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg2|cfg3]
+                    [--dp DP] [--no-cpu-baseline]
 
-For N>1 (torchrun, one process per GPU) every rank runs its own dam break of the
-same size (weak scaling, "replicas"); value = sum over ranks / max time.
-Prints ONE JSON line on rank 0.
+Workloads:
+  cfg2 (default): 3D dam break, WCSPH + artificial viscosity + DDT2, Verlet.  N=1: the
+        BASELINE cfg2 case (1,025,964 particles).  N>1 (torchrun, one process per GPU):
+        weak scaling — a dam break of ~N x 1,025,964 particles slab-decomposed over x
+        across the N ranks (RCCL halo/migration exchange + max-allreduce of the dt
+        maxima inside libsphcore); value = all particles x steps / max rank time.
+  cfg3: BASELINE cfg3, 3D dam break of ~10M particles (dp 0.00205), Symplectic + DDT
+        (Molteni, delta-SPH) 0.1, slab-split over N ranks (strong scaling).
+torch.distributed (gloo, host only) bootstraps the RCCL id, barriers and reduces the
+timings; the data path never goes through torch.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -43,7 +50,7 @@ def dist_env():
     return rank, world, local
 
 
-def reference_cpu_baseline(dp: float, nsteps: int, threads: int) -> dict | None:
+def reference_cpu_baseline(dp: float, nsteps: int, threads: int, step: int = 1, ddt: int = 2) -> dict | None:
     """Times the REFERENCE CPU solver (oracle/_ref, built from the reference sources)
     on the same dam break; Steps/s is the solver's own 'Steps per second' (step loop only)."""
     ref = os.path.join(ROOT, "oracle", "_ref")
@@ -52,7 +59,8 @@ def reference_cpu_baseline(dp: float, nsteps: int, threads: int) -> dict | None:
         return None
     tmp = tempfile.mkdtemp(prefix="sphref_")
     try:
-        out = subprocess.run([gen, repr(dp), tmp, "1", "2"], capture_output=True, text=True, check=True).stdout
+        out = subprocess.run([gen, repr(dp), tmp, str(step), str(ddt)], capture_output=True, text=True,
+                             check=True).stdout
         np_ = int(re.search(r"np=(\d+)", out).group(1))
         subprocess.run([exe, os.path.join(tmp, "CaseDambreak"), os.path.join(tmp, "out"), "-nsteps:%d" % nsteps,
                         "-sv:none", "-svres:0", "-ompthreads:%d" % threads], capture_output=True, text=True,
@@ -61,8 +69,9 @@ def reference_cpu_baseline(dp: float, nsteps: int, threads: int) -> dict | None:
         sps = float(re.search(r"Steps per second\.*:\s*([0-9.eE+-]+)", log).group(1))
         return {"value": sps * np_, "unit": "particle-steps/s", "cores": threads, "kind": "reference",
                 "sample": "reference DualSPHysics5.2 CPU (built from /root/reference sources, -O3 -fopenmp "
-                          "-ffast-math), %d-particle dam break, %d Verlet steps, -ompthreads:%d, "
-                          "'Steps per second' of Run.out" % (np_, nsteps, threads)}
+                          "-ffast-math), %d-particle dam break, %d %s steps, -ompthreads:%d, "
+                          "'Steps per second' of Run.out" % (np_, nsteps, "Verlet" if step == 1 else "Symplectic",
+                                                             threads)}
     except Exception as e:  # noqa: BLE001
         sys.stderr.write("reference CPU baseline failed: %r\n" % (e,))
         return None
@@ -77,8 +86,26 @@ def port_cpu_baseline(case, nsteps: int, threads: int) -> dict:
     o.run(nsteps)
     sec = o.run_seconds()
     return {"value": case.np * nsteps / sec, "unit": "particle-steps/s", "cores": o.threads(), "kind": "port",
-            "sample": "oracle restatement of JSphCpu (C++/OpenMP, -O3 -ffast-math), %d particles, %d Verlet steps"
+            "sample": "oracle restatement of JSphCpu (C++/OpenMP, -O3 -ffast-math), %d particles, %d steps"
                       % (case.np, nsteps)}
+
+
+CFG2_DP, CFG2_NP = 0.0045, 1025964
+CFG3_DP = 0.00205  # 9,969,118 particles (BASELINE cfg3: ~10M)
+
+
+def weak_dp(target_np: int) -> float:
+    """Largest dp whose dam break has >= target_np particles (np falls as dp grows)."""
+    from dualsphysics_multilayer_amd.case import dambreak_np
+
+    lo, hi = 1e-4, CFG2_DP  # np(lo) >= target >= ... ; bisect on the step function
+    for _ in range(60):
+        mid = 0.5 * (lo + hi)
+        if dambreak_np(mid) >= target_np:
+            lo = mid
+        else:
+            hi = mid
+    return float("%.6g" % lo)
 
 
 def main() -> None:
@@ -86,7 +113,9 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--dp", type=float, default=0.0045)
+    ap.add_argument("--workload", choices=("cfg2", "cfg3"), default="cfg2")
+    ap.add_argument("--dp", type=float, default=None, help="override the particle spacing")
+    ap.add_argument("--bound-weight", type=float, default=0.3, help="slab balance weight of a bound particle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=8)
     args = ap.parse_args()
@@ -99,14 +128,26 @@ def main() -> None:
         import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # host-side bootstrap only (RCCL id broadcast, barriers, timing reduction)
+        dist.init_process_group("gloo")
 
     from dualsphysics_multilayer_amd.case import DamBreakCase
-    from dualsphysics_multilayer_amd.core import SphGpuSingle
+    from dualsphysics_multilayer_amd.core import SphGpuSingle, SphGpuSlab, comm_unique_id, slab_partition
 
-    case = DamBreakCase(args.dp)
-    s = SphGpuSingle(case, device=local)
+    if args.workload == "cfg2":
+        dp = args.dp or (CFG2_DP if world == 1 else weak_dp(world * CFG2_NP))
+        case = DamBreakCase(dp)
+    else:
+        dp = args.dp or CFG3_DP
+        case = DamBreakCase(dp, step_algorithm=2, tdensity=1)
+    bounds = None
+    if world > 1:
+        bounds = slab_partition(case, world, args.bound_weight)
+        ids = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=0)
+        s = SphGpuSlab(case, rank, world, bounds, ids[0], device=local)
+    else:
+        s = SphGpuSingle(case, device=local)
     s.run(args.warmup)
     s.sync()
     pairs0 = s.count_pairs()
@@ -115,13 +156,12 @@ def main() -> None:
         if dist is not None:
             import torch
 
-            t = torch.zeros(1, device="cuda:%d" % local)
-            dist.all_reduce(t)
+            dist.barrier()
             torch.cuda.synchronize(local)
 
     s.set_timing(True)
-    barrier()
     s.sync()
+    barrier()
     t0 = time.perf_counter()
     s.run(args.steps)
     s.sync()
@@ -132,15 +172,17 @@ def main() -> None:
     st = s.stats()
 
     units = float(st["np"]) * args.steps
+    per_rank_np = [int(st["np"])]
     if dist is not None:
         import torch
 
-        v = torch.tensor([elapsed, units], dtype=torch.float64, device="cuda:%d" % local)
-        tmax = v[:1].clone()
+        tmax = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tot = v[1:].clone()
+        tot = torch.tensor([units], dtype=torch.float64)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        elapsed, units = float(tmax.item()), float(tot.item())
+        nps = [None] * world
+        dist.all_gather_object(nps, int(st["np"]))
+        elapsed, units, per_rank_np = float(tmax.item()), float(tot.item()), nps
 
     if rank == 0:
         pairs = (pairs0.astype("float64") + pairs1.astype("float64")) / 2.0
@@ -160,19 +202,25 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.workload == "cfg2" else "strong",
             "vs_baseline": None,
             "dtype": "f32 (f64 positions/time integration)",
             "data": "synthetic: generated 3D dam-break lattice (SURVEY.md §8(c) recipe)",
             "config": {
-                "workload": "BASELINE cfg2: 3D dam break, %d particles (dp=%g), Verlet, Wendland, artificial "
-                            "viscosity 0.1, DDT2 0.1, DBC, CFL 0.2, CellMode full" % (case.np, args.dp),
+                "workload": (("BASELINE cfg2: 3D dam break, %d particles (dp=%g), Verlet, Wendland, artificial "
+                              "viscosity 0.1, DDT2 0.1, DBC, CFL 0.2, CellMode full" % (case.np, dp))
+                             if args.workload == "cfg2" else
+                             ("BASELINE cfg3: 3D dam break, %d particles (dp=%g), Symplectic, Wendland, artificial "
+                              "viscosity 0.1, DDT (Molteni delta-SPH) 0.1, DBC, CFL 0.2, CellMode full"
+                              % (case.np, dp))),
                 "np": case.np,
                 "npb": case.npb,
-                "parallelism": "replicas" if world > 1 else "single",
+                "parallelism": ("slab-x%d (RCCL halo + migration, max-allreduce dt)" % world) if world > 1 else "single",
+                "slab_bounds_cells": None if bounds is None else [int(b) for b in bounds],
+                "owned_np_per_rank": per_rank_np,
             },
             "roofline": {
-                "kernel": "k_interaction<DDT2> (Interaction_Forces)",
+                "kernel": "k_fluid_tiled<tdensity=%d> (Interaction_Forces)" % case.tdensity,
                 "bound": "mfma",
                 "bound_note": "FP32-VALU-bound pairwise kernel (no MFMA: irregular pairs); gfx950's FP32 vector "
                               "peak equals its FP32 MFMA peak, 157.3 TFLOP/s",
@@ -201,7 +249,7 @@ def main() -> None:
         }
         if not args.no_cpu_baseline and world == 1:
             threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), 64)
-            cb = reference_cpu_baseline(args.dp, args.cpu_steps, threads)
+            cb = reference_cpu_baseline(dp, args.cpu_steps, threads, case.step_algorithm, case.tdensity)
             if cb is None:
                 cb = port_cpu_baseline(case, args.cpu_steps, threads)
             cb["gpu_over_cpu"] = value / cb["value"]

@@ -146,3 +146,21 @@ def test_large_case_slabs_properties():
     pg, p1 = grp.particles(), by_idp(one.particles())
     assert np.array_equal(pg["idp"], p1["idp"])
     assert maxdiff(pg, p1, "pos") <= 1e-7 and maxdiff(pg, p1, "vel") <= 5e-5
+
+
+def test_rccl_transport_single_rank():
+    """The RCCL transport end to end on one GPU: a 1-rank slab (ncclCommInitRank,
+    grouped send/recv with no neighbours, ncclAllReduce of the dt maxima) must step
+    like the single-domain solver."""
+    from dualsphysics_multilayer_amd.core import SphGpuSlab, case_derive, comm_unique_id
+
+    case = DamBreakCase(0.025)
+    ncx = case_derive(case.case_def())["dom_cells"][0]
+    s = SphGpuSlab(case, 0, 1, [0, ncx], comm_unique_id(), device=0)
+    one = single(case)
+    s.run(20)
+    one.run(20)
+    assert s.stats()["np"] == one.stats()["np"]
+    assert s.stats()["time"] == pytest.approx(one.stats()["time"], rel=1e-9)
+    check_close(by_idp(s.particles()), by_idp(one.particles()), 20)
+    s.close()
