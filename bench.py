@@ -118,18 +118,23 @@ def main() -> None:
     ap.add_argument("--bound-weight", type=float, default=0.3, help="slab balance weight of a bound particle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=8)
+    ap.add_argument("--force-slab", action="store_true",
+                    help="run the N>1 code path (gloo bootstrap + RCCL slab) even with one rank")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
     if args.gpus != world and world > 1:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    use_slab = world > 1 or args.force_slab
     dist = None
-    if world > 1:
+    if use_slab:
         import torch
         import torch.distributed as dist
 
         # host-side bootstrap only (RCCL id broadcast, barriers, timing reduction)
-        dist.init_process_group("gloo")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from dualsphysics_multilayer_amd.case import DamBreakCase
     from dualsphysics_multilayer_amd.core import SphGpuSingle, SphGpuSlab, comm_unique_id, slab_partition
@@ -141,7 +146,7 @@ def main() -> None:
         dp = args.dp or CFG3_DP
         case = DamBreakCase(dp, step_algorithm=2, tdensity=1)
     bounds = None
-    if world > 1:
+    if use_slab:
         bounds = slab_partition(case, world, args.bound_weight)
         ids = [comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(ids, src=0)
@@ -215,7 +220,7 @@ def main() -> None:
                               % (case.np, dp))),
                 "np": case.np,
                 "npb": case.npb,
-                "parallelism": ("slab-x%d (RCCL halo + migration, max-allreduce dt)" % world) if world > 1 else "single",
+                "parallelism": ("slab-x%d (RCCL halo + migration, max-allreduce dt)" % world) if use_slab else "single",
                 "slab_bounds_cells": None if bounds is None else [int(b) for b in bounds],
                 "owned_np_per_rank": per_rank_np,
             },

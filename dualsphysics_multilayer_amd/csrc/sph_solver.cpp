@@ -467,35 +467,35 @@ void SphGpuSingle::Timing(double out_ms[4], uint64_t* launches) {
 }
 
 // ---- phases ------------------------------------------------------------------------
-// Slab exchange before the divide's sort: pack migrants/ghosts (device), agree on the
-// record counts with both neighbours, move the records, append what arrived.  Two
-// host waits per exchange: the send counts (to size the sends) and the receive counts.
+// Slab exchange before the divide's sort: pack migrants/ghosts (device), swap the
+// record counts with both neighbours device to device, then ONE host wait to size
+// the receives, move the records, append what arrived.
 void SphGpuSingle::Exchange() {
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET), withpre = havepre_;
   const bool hl = transport_->has_left(), hr = transport_->has_right();
-  for (;;) {
-    check_hip(hipMemsetAsync(slabcnt_, 0, sizeof(SlabCounts), stream), "exchange: reset counts");
-    launch_slab_pack(stream, cap_, sc_, cur_, G, K, hl, hr, withm1, withpre, packtiles_, slabcnt_, sendl_, sendr_,
-                     sendcap_);
-    check_hip(hipMemcpyAsync(slabcnt_host_, slabcnt_, sizeof(SlabCounts), hipMemcpyDeviceToHost, stream),
-              "exchange: read counts");
-    Sync();
-    const unsigned long long need = std::max(slabcnt_host_->send[0], slabcnt_host_->send[1]);
-    if (need <= sendcap_) break;
+  check_hip(hipMemsetAsync(slabcnt_, 0, sizeof(SlabCounts), stream), "exchange: reset counts");
+  launch_slab_pack(stream, cap_, sc_, cur_, G, K, hl, hr, withm1, withpre, packtiles_, slabcnt_, sendl_, sendr_,
+                   sendcap_);
+  transport_->exchange(&slabcnt_->send[0], 8, &slabcnt_->send[1], 8, &slabcnt_->recv[0], hl ? 8 : 0,
+                       &slabcnt_->recv[1], hr ? 8 : 0, stream);
+  check_hip(hipMemcpyAsync(slabcnt_host_, slabcnt_, sizeof(SlabCounts), hipMemcpyDeviceToHost, stream),
+            "exchange: read counts");
+  Sync();
+  const SlabCounts c = *slabcnt_host_;
+  const unsigned long long need = std::max(c.send[0], c.send[1]);
+  if (need > sendcap_) {  // records past the capacity were not written: grow and pack again
     if (slabbuf_) check_hip(hipFree(slabbuf_), "hipFree");
     sendcap_ = need + need / 2 + 4096;
     check_hip(hipMalloc(&slabbuf_, 2 * sizeof(SlabRec) * sendcap_), "hipMalloc send buffers");
     sendl_ = (SlabRec*)slabbuf_;
     sendr_ = sendl_ + sendcap_;
+    check_hip(hipMemsetAsync(&slabcnt_->nkeep, 0, sizeof(unsigned), stream), "exchange: reset nkeep");
+    launch_slab_pack(stream, cap_, sc_, cur_, G, K, hl, hr, withm1, withpre, packtiles_, slabcnt_, sendl_, sendr_,
+                     sendcap_);
   }
-  const SlabCounts c = *slabcnt_host_;
-  transport_->exchange(&slabcnt_->send[0], 8, &slabcnt_->send[1], 8, &slabcnt_->recv[0], hl ? 8 : 0,
-                       &slabcnt_->recv[1], hr ? 8 : 0, stream);
-  check_hip(hipMemcpyAsync(slabcnt_host_, slabcnt_, sizeof(SlabCounts), hipMemcpyDeviceToHost, stream),
-            "exchange: read receive counts");
-  Sync();
-  const unsigned long long rl = hl ? slabcnt_host_->recv[0] : 0, rr = hr ? slabcnt_host_->recv[1] : 0;
+  const unsigned long long rl = hl ? c.recv[0] : 0, rr = hr ? c.recv[1] : 0;
   if (rl + rr > recvcap_) {
+    check_hip(hipStreamSynchronize(stream), "exchange: sync");
     if (recvbuf_) check_hip(hipFree(recvbuf_), "hipFree");
     recvcap_ = rl + rr + (rl + rr) / 2 + 4096;
     check_hip(hipMalloc(&recvbuf_, sizeof(SlabRec) * recvcap_), "hipMalloc receive buffer");
