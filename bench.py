@@ -90,6 +90,30 @@ def port_cpu_baseline(case, nsteps: int, threads: int) -> dict:
                       % (case.np, nsteps)}
 
 
+def profiled_traffic(kernel_prefix: str, np_: int, workload: str):
+    """HBM bytes per launch of the dominant kernel from the latest committed PMC passes
+    (profiles/<round>/pmc_traffic.json: 2*FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md
+    §HBM) of the same workload on one GPU; None if there is none."""
+    import glob
+
+    found = None
+    for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*"))):
+        tj, bj = os.path.join(d, "pmc_traffic.json"), os.path.join(d, "bench.json")
+        if not (os.path.exists(tj) and os.path.exists(bj)):
+            continue
+        try:
+            b = json.load(open(bj))
+            if b["config"]["np"] != np_ or b["n_gpus"] != 1 or not b["config"]["workload"].startswith(workload):
+                continue
+            for k, v in json.load(open(tj)).items():
+                if k.startswith(kernel_prefix):
+                    found = {"bytes": v["traffic_bytes_per_launch"], "avg_ns": v.get("avg_ns"),
+                             "source": os.path.relpath(tj, ROOT) + " (2*FETCH_SIZE + WRITE_SIZE, %s)" % k}
+        except (KeyError, ValueError):
+            continue
+    return found
+
+
 CFG2_DP, CFG2_NP = 0.0045, 1025964
 CFG3_DP = 0.00205  # 9,969,118 particles (BASELINE cfg3: ~10M)
 
@@ -198,6 +222,8 @@ def main() -> None:
         achieved = flops / (inter_ms * 1e-3) / 1e12 if inter_ms > 0 else None
         value = units / elapsed
         hbm_achieved = value * BYTES_PER_PARTICLE_STEP[case.step_algorithm] / 1e9
+        traffic = profiled_traffic("sphx::k_fluid_tiled<%d>" % case.tdensity, case.np,
+                                   "BASELINE " + args.workload) if world == 1 else None
         res = {
             "metric": METRIC,
             "value": value,
@@ -233,7 +259,10 @@ def main() -> None:
                 "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": (achieved / PEAK_FP32_TFLOPS) if achieved else None,
-                "traffic": None,
+                "traffic": traffic["bytes"] if traffic else None,
+                "traffic_unit": "bytes per launch (HBM, PMC)",
+                "traffic_source": traffic["source"] if traffic else None,
+                "traffic_profiled_avg_ms": (traffic["avg_ns"] / 1e6) if traffic and traffic["avg_ns"] else None,
                 "avg_launch_ms": inter_ms,
                 "launches": int(nlaunch),
                 "algorithmic_flop_per_launch": flops,

