@@ -31,12 +31,15 @@ namespace sphx {
 #endif
 constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
 #ifndef SPH_TCAP
-#define SPH_TCAP 384
+#define SPH_TCAP 416
 #endif
 #ifndef SPH_PIPE
 #define SPH_PIPE 0
 #endif
-constexpr int TCAP = SPH_TCAP;  // staged neighbour records per segment
+// staged neighbour records per segment.  416 puts the block at 18.7 KB of LDS -> 8
+// blocks = 4 waves per SIMD, measured best (1.022 ms at 1M vs 1.056 at 5 waves/SIMD
+// and 1.27 at 2.5 waves/SIMD).
+constexpr int TCAP = SPH_TCAP;
 constexpr int TMAXCELLS = 4;   // max x-cells per item
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
