@@ -33,9 +33,6 @@ constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
 #ifndef SPH_TCAP
 #define SPH_TCAP 416
 #endif
-#ifndef SPH_PIPE
-#define SPH_PIPE 0
-#endif
 // staged neighbour records per segment.  416 puts the block at 18.7 KB of LDS -> 8
 // blocks = 4 waves per SIMD, measured best (1.022 ms at 1M vs 1.056 at 5 waves/SIMD
 // and 1.27 at 2.5 waves/SIMD).
@@ -141,62 +138,78 @@ struct TAcc {
 struct P1 {
   float x, y, z;        // x relative to the item's x origin, y/z cell-relative
   float4 vr;            // velocity, rho
-  float pr, inv_rho;
+  float prr, inv_rho;   // press/rho, 1/rho
+};
+
+// Per-pass constants of the pair body (the mass of p2 and the Wendland bwen/h folded in).
+struct PassK {
+  float ar1;  // bwen/h * m2 * rho1   (continuity)
+  float bm;   // bwen/h * m2          (momentum)
+  float cv;   // 2 * bwen/h * cvisc   (artificial viscosity; cvisc = -alpha*cs0*h*m2)
+  float kd;   // ddtkh*cs0 * bwen/h * m2 (density diffusion)
 };
 
 // One pair body (JSphCpu.cpp:682-797 semantics, fast f32 intrinsics).
 // MODE 0: fluid p1 / fluid p2, 1: fluid p1 / bound p2, 2: bound p1 / fluid p2
 // (InteractionForcesBound, JSphCpu.cpp:577-612: continuity + visc-dt only).
 // `ok` = the reference's pair test (rr2 <= KernelSize2 && rr2 >= ALMOSTZERO); a pair
-// with !ok contributes exactly +0 (fac forced to 0, visc term masked), which keeps the
-// body branch-free so two pairs can be interleaved.
-// Algebra used (same quantities, fewer operations):
-//   fac = bwen*q*(1-q/2)^3/rad = (bwen/h)*(1-q/2)^3          (FunSphKernel.h:217-224)
+// with !ok contributes exactly +0 (kernel factor forced to 0, visc term masked), which
+// keeps the body branch-free so two pairs can be interleaved.
+// Algebra used (same quantities, fewer operations; constants folded into PassK):
+//   fac = bwen*q*(1-q/2)^3/rad = (bwen/h)*w3,  w3 = (1-rad/(2h))^3   (FunSphKernel.h:217-224)
 //   dv.fr = fac*(dr.dv), dr.fr = fac*rr2
-//   momentum + artificial viscosity: ace += fac*(p_vpm - pi_visc)*dr
-//   DDT2: rho0*(1+x)^(1/gamma) - rho0 = rho0*x*(c1+x*(c2+x*(c3+x*c4))), x = ddtgz*drz
-//         (binomial series; |x| <= 2h*ddtgz ~ 1e-3, 5th term < 1e-9 relative), which also
-//         avoids the float cancellation of the reference's rho0*powf(rh,1/gamma)-rho0.
-struct P2 {
-  float4 A;   // x, y, z (block frame), |A|^2
-  float4 B;   // vx, vy, vz, rho
-  float2 C;   // press, 1/rho
-};
-
+//   continuity: ar += fac*m2*(dr.dv)*rho1/rho2
+//   momentum + artificial viscosity: ace += fac*(-m2*(p1+p2)/(rho1*rho2) - pi_visc)*dr with
+//     (p1+p2)/(rho1*rho2) = (p1/rho1)/rho2 + (p2/rho2)/rho1 and
+//     pi_visc = cvisc*(dr.dv)/(r^2+eta^2)/robar; one reciprocal 1/((r^2+eta^2)*(rho1+rho2))
+//     gives both 1/(r^2+eta^2) and 1/(rho1+rho2)
+//   DDT2: rho0*(1+x)^(1/gamma) - rho0, x = ddtgz*drz, as the binomial series in drz
+//         (|x| <= 2h*ddtgz ~ 1e-3, 5th term < 1e-9 relative; decided per case on the host),
+//         which also avoids the float cancellation of the reference's rho0*powf(rh,1/gamma)-rho0.
 template <int TDENSITY, int MODE>
 __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float drx, float dry, float drz, float rr2,
-                                          bool ok, const float4& B, const float2& C, float massp2, float cvisc,
-                                          TAcc& a) {
+                                          bool ok, const float4& B, const float2& C, const PassK& Q, TAcc& a) {
   const float rad = fsqrt_(rr2);
-  const float wqq1 = fmaf(K.mhalfovh, rad, 1.f);
-  const float fac = ok ? K.bwenovh * (wqq1 * wqq1 * wqq1) : 0.f;
+  const float wq = fmaf(K.mhalfovh, rad, 1.f);
+  const float w3 = ok ? wq * wq * wq : 0.f;
   const float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
   const float dot = drx * dvx + dry * dvy + drz * dvz;
-  const float r12 = p.vr.w * C.y;  // rho1/rho2
-  const float inv_re = frcp(rr2 + K.eta2);
+  const float re = rr2 + K.eta2;
+  float inv_re, inv_rs = 0.f;
+  if (MODE == 2) {
+    inv_re = frcp(re);
+  } else {
+    const float rs = p.vr.w + B.w;  // 2*robar
+    const float rr = frcp(re * rs);
+    inv_re = rr * rs;
+    inv_rs = rr * re;
+  }
   const float dot_rr2 = ok ? dot * inv_re : 0.f;
   a.visc = fmaxf(dot_rr2, a.visc);
-  const float facm = fac * massp2;
-  a.ar += facm * dot * r12;
+  const float wdr = w3 * dot * C.y;  // w3*(dr.dv)/rho2
+  a.ar = fmaf(wdr, Q.ar1, a.ar);
   if (MODE == 2) return;
-  const float p_vpm = -(p.pr + C.x) * (p.inv_rho * C.y) * massp2;
-  const float pi_visc = (dot < 0.f) ? cvisc * dot_rr2 * frcp((p.vr.w + B.w) * 0.5f) : 0.f;
-  const float c = fac * (p_vpm - pi_visc);
-  a.ax += c * drx;
-  a.ay += c * dry;
-  a.az += c * drz;
+  const float S = fmaf(C.y, p.prr, p.inv_rho * C.x);  // (p1+p2)/(rho1*rho2)
+  const float pv = (dot < 0.f) ? Q.cv * dot_rr2 * inv_rs : 0.f;
+  const float c = -w3 * fmaf(Q.bm, S, pv);
+  a.ax = fmaf(c, drx, a.ax);
+  a.ay = fmaf(c, dry, a.ay);
+  a.az = fmaf(c, drz, a.az);
   if (MODE == 1) {
     if ((TDENSITY == 1 || TDENSITY == 2) && ok) a.delta = FLT_MAX;  // DBC: no DDT next to the boundary
     return;
   }
   if (TDENSITY == 1) {
-    a.delta += K.ddtkhcs * (r12 - 1.f) * inv_re * (facm * rr2);
+    const float t = w3 * rr2 * inv_re;
+    a.delta = fmaf(Q.kd * t, fmaf(p.vr.w, C.y, -1.f), a.delta);
   } else if (TDENSITY == 2 || TDENSITY == 3) {
-    const float x = K.ddtgz * drz;
     float drhop;
-    if (fabsf(x) < 0.05f) drhop = K.rhopzero * x * fmaf(x, fmaf(x, fmaf(x, K.ddtc4, K.ddtc3), K.ddtc2), K.ddtc1);
-    else drhop = K.rhopzero * fexp2(K.ovgamma * flog2(1.f + x)) - K.rhopzero;
-    a.delta -= K.ddtkhcs * ((B.w - p.vr.w) - drhop) * inv_re * (facm * rr2) * C.y;
+    if (K.ddtseries)  // kernel-uniform (scalar) branch
+      drhop = drz * fmaf(drz, fmaf(drz, fmaf(drz, K.ddte4, K.ddte3), K.ddte2), K.ddte1);
+    else
+      drhop = K.rhopzero * fexp2(K.ovgamma * flog2(1.f + K.ddtgz * drz)) - K.rhopzero;
+    const float t = w3 * rr2 * inv_re * C.y;
+    a.delta = fmaf(-Q.kd * t, B.w - (p.vr.w + drhop), a.delta);
   }
 }
 
@@ -209,7 +222,7 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
 template <int TDENSITY, int MODE>
 __device__ __forceinline__ void tile_range(const KConst& K, const P1& p, float ry, float rz, int s0, int s1,
                                            const float4* __restrict__ sA, const float4* __restrict__ sB,
-                                           const float2* __restrict__ sC, float massp2, float cvisc, TAcc& a) {
+                                           const float2* __restrict__ sC, const PassK& Q, TAcc& a) {
   const float px2 = -2.f * p.x, py2 = -2.f * ry, pz2 = -2.f * rz;
   const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + ry * ry + rz * rz);
 #if SPH_ABLATE == 2
@@ -240,55 +253,27 @@ __device__ __forceinline__ void tile_range(const KConst& K, const P1& p, float r
     a.visc += float(__popcll(m0) + __popcll(m1));
     m0 = m1 = 0;
 #endif
-    // Value selects only: a branch that picks m0 or m1 by reference makes the compiler
-    // take their address and keep both masks in scratch (a memory round trip per pair).
+    // Drain: `cur` is the 64-bit word being popped (refilled from `nxt` when it runs
+    // dry), so a pop is ctz + clear-lowest + one refill select.  Value selects only: a
+    // branch that picks a mask word by reference makes the compiler keep the masks in
+    // scratch.  The second pop of an iteration is unconditional (an empty pop returns
+    // an index whose pair is masked off), so the loop body has no divergent branch.
+    unsigned long long cur = m0 ? m0 : m1, nxt = m0 ? m1 : 0ull;
+    int cbase = base + (m0 ? 0 : 64);
     auto pop = [&](void) -> int {
-      const bool lo = m0 != 0ull;
-      const unsigned long long m = lo ? m0 : m1;
-      const int j = int(__builtin_ctzll(m | (1ull << 63))) + (lo ? 0 : 64);
-      const unsigned long long mm = m & (m - 1ull);
-      m0 = lo ? mm : m0;
-      m1 = lo ? m1 : mm;
+      const int j = cbase + int(__builtin_ctzll(cur | (1ull << 63)));
+      cur &= cur - 1ull;
+      const bool e = cur == 0ull;
+      cur = e ? nxt : cur;
+      nxt = e ? 0ull : nxt;
+      cbase += e ? 64 : 0;
       return j;
     };
-#if SPH_PIPE
-    // Software-pipelined drain: the LDS reads of the next two pairs are issued before
-    // the current two are computed.
-    if (m0 | m1) {
-      int j1 = base + pop();
-      bool two = (m0 | m1) != 0ull;
-      int j2 = two ? base + pop() : j1;
-      float4 A1 = sA[j1], A2 = sA[j2], B1 = sB[j1], B2 = sB[j2];
-      float2 C1 = sC[j1], C2 = sC[j2];
-      for (;;) {
-        const bool more = (m0 | m1) != 0ull;
-        int n1 = j1, n2 = j2;
-        bool ntwo = false;
-        if (more) {
-          n1 = base + pop();
-          ntwo = (m0 | m1) != 0ull;
-          n2 = ntwo ? base + pop() : n1;
-        }
-        const float4 nA1 = sA[n1], nA2 = sA[n2], nB1 = sB[n1], nB2 = sB[n2];
-        const float2 nC1 = sC[n1], nC2 = sC[n2];
-        const float drx1 = p.x - A1.x, dry1 = ry - A1.y, drz1 = rz - A1.z;
-        const float drx2 = p.x - A2.x, dry2 = ry - A2.y, drz2 = rz - A2.z;
-        const float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
-        const float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
-        const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
-        const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
-        pair_body<TDENSITY, MODE>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, massp2, cvisc, a);
-        pair_body<TDENSITY, MODE>(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, massp2, cvisc, a);
-        if (!more) break;
-        j1 = n1; j2 = n2; two = ntwo;
-        A1 = nA1; A2 = nA2; B1 = nB1; B2 = nB2; C1 = nC1; C2 = nC2;
-      }
-    }
-#else
-    while (m0 | m1) {
-      const int j1 = base + pop();
-      const bool two = (m0 | m1) != 0ull;
-      const int j2 = two ? base + pop() : j1;
+    while (cur) {
+      const int j1 = pop();
+      const bool two = cur != 0ull;
+      const int j2p = pop();
+      const int j2 = two ? j2p : j1;
       const float4 A1 = sA[j1], A2 = sA[j2];
       const float4 B1 = sB[j1], B2 = sB[j2];
       const float2 C1 = sC[j1], C2 = sC[j2];
@@ -298,10 +283,9 @@ __device__ __forceinline__ void tile_range(const KConst& K, const P1& p, float r
       const float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
       const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
       const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
-      pair_body<TDENSITY, MODE>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, massp2, cvisc, a);
-      pair_body<TDENSITY, MODE>(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, massp2, cvisc, a);
+      pair_body<TDENSITY, MODE>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, Q, a);
+      pair_body<TDENSITY, MODE>(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, Q, a);
     }
-#endif
   }
 }
 
@@ -314,7 +298,7 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
                                                     float4* __restrict__ arace) {
   __shared__ float4 sA[TCAP + 128];  // +128: over-read pad of the 8-wide candidate test
   __shared__ float4 sB[TCAP];
-  __shared__ float2 sC[TCAP];  // press, 1/rho
+  __shared__ float2 sC[TCAP];  // press/rho, 1/rho
   __shared__ unsigned s_item;
   const unsigned nitems = sc->nitems;
   const unsigned per = (nitems + 7) / 8;
@@ -361,13 +345,24 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
           p.y = pc1.y;
           p.z = pc1.z;
           p.vr = velrhop[p1];
-          p.pr = bitem ? 0.f : press[p1];
+          p.prr = bitem ? 0.f : press[p1];
         } else {
           p.x = p.y = p.z = 1e30f;  // never within the support radius
           p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
-          p.pr = 0.f;
+          p.prr = 0.f;
         }
         p.inv_rho = frcp(p.vr.w);
+        p.prr *= p.inv_rho;
+        // pass constants: fluid p2 (pass 0 / bound p1) and bound p2 (pass 1)
+        PassK qf, qb;
+        qf.bm = K.bwenovh * K.massfluid;
+        qf.ar1 = qf.bm * p.vr.w;
+        qf.cv = 2.f * K.bwenovh * cvisc_f;
+        qf.kd = K.ddtkhcs * qf.bm;
+        qb.bm = K.bwenovh * K.massbound;
+        qb.ar1 = qb.bm * p.vr.w;
+        qb.cv = 2.f * K.bwenovh * cvisc_b;
+        qb.kd = K.ddtkhcs * qb.bm;
         const int lxa = max(cx1 - 1, 0), lxb = min(cx1 + 1, g.ncx - 1);
         TAcc f = {0, 0, 0, 0, 0, 0}, bnd = {0, 0, 0, 0, 0, 0};
         const int npass = bitem ? 1 : 2;
@@ -395,17 +390,18 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
                   sA[i] = make_float4(x2, pc.y, pc.z, x2 * x2 + pc.y * pc.y + pc.z * pc.z);
                   const float4 vr = velrhop[seg + i];
                   sB[i] = vr;
-                  sC[i] = make_float2(press[seg + i], frcp(vr.w));
+                  const float ir = frcp(vr.w);
+                  sC[i] = make_float2(press[seg + i] * ir, ir);
                 }
                 __syncthreads();
                 const int s0 = int(max(ls, seg) - seg);
                 const int s1 = act ? int(min(le, seg + segn)) - int(seg) : 0;
                 if (bitem)
-                  tile_range<TDENSITY, 2>(K, p, ry, rz, s0, s1, sA, sB, sC, K.massfluid, 0.f, f);
+                  tile_range<TDENSITY, 2>(K, p, ry, rz, s0, s1, sA, sB, sC, qf, f);
                 else if (pass == 0)
-                  tile_range<TDENSITY, 0>(K, p, ry, rz, s0, s1, sA, sB, sC, K.massfluid, cvisc_f, f);
+                  tile_range<TDENSITY, 0>(K, p, ry, rz, s0, s1, sA, sB, sC, qf, f);
                 else
-                  tile_range<TDENSITY, 1>(K, p, ry, rz, s0, s1, sA, sB, sC, K.massbound, cvisc_b, bnd);
+                  tile_range<TDENSITY, 1>(K, p, ry, rz, s0, s1, sA, sB, sC, qb, bnd);
               }
             }
           }

@@ -133,6 +133,14 @@ static KConst make_kconst(const SphConstants& c) {
     K.ddtc2 = float(a * (a - 1) / 2);
     K.ddtc3 = float(a * (a - 1) * (a - 2) / 6);
     K.ddtc4 = float(a * (a - 1) * (a - 2) * (a - 3) / 24);
+    // |drz| <= 2h for every pair, so the series applies to all pairs of the case when
+    // 2h*ddtgz is small (dam break: ~1e-3); decided once here, uniform in the kernel.
+    K.ddtseries = (double(c.kernelsize) * double(c.ddtgz) < 0.05) ? 1 : 0;
+    const double gz = double(c.ddtgz), r0 = double(c.rhopzero);
+    K.ddte1 = float(r0 * a * gz);
+    K.ddte2 = float(r0 * a * (a - 1) / 2 * gz * gz);
+    K.ddte3 = float(r0 * a * (a - 1) * (a - 2) / 6 * gz * gz * gz);
+    K.ddte4 = float(r0 * a * (a - 1) * (a - 2) * (a - 3) / 24 * gz * gz * gz * gz);
   }
   return K;
 }
