@@ -213,72 +213,109 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
   }
 }
 
-// Candidates [s0,s1) of the staged segment: test 128 at a time into bit masks, then
-// run the pair body over the set bits, two pairs per iteration.  The test uses the
-// staged |A|^2 (sA.w): |p-A|^2 = |p|^2 + |A|^2 - 2 p.A  -> 3 FMAs + 1 compare per
-// candidate on one ds_read_b128, against a threshold inflated by 1e-4 (the rounding of
-// the expanded form is ~1e-6 relative); the body recomputes |p-A|^2 exactly and applies
-// the reference's test, so no pair is lost or added.
+// Candidate test of one window: n (<= 128) staged records from sA+s0 with the expanded
+// form |p-A|^2 = |p|^2 + |A|^2 - 2 p.A (3 FMAs + 1 compare per candidate on one
+// ds_read_b128) against a threshold inflated by 1e-4 (the expanded form rounds to ~1e-6
+// relative); the body recomputes |p-A|^2 exactly and applies the reference's test, so no
+// pair is lost or added.  sA is padded past TCAP, so the 8-wide groups may over-read;
+// those bits are masked off.  n <= 0 gives empty masks.
+__device__ __forceinline__ void test128(const float4* __restrict__ sA, int s0, int n, float px2, float py2,
+                                        float pz2, float thr, unsigned long long& m0, unsigned long long& m1) {
+  m0 = 0ull;
+  m1 = 0ull;
+  const float4* __restrict__ b = sA + s0;
+  for (int jo = 0; jo < 16; jo++) {
+    const int left = n - jo * 8;
+    if (left <= 0) break;
+    unsigned bits = 0;
+#pragma unroll
+    for (int ji = 0; ji < 8; ji++) {
+      const float4 A = b[jo * 8 + ji];
+      const float q = fmaf(px2, A.x, fmaf(py2, A.y, fmaf(pz2, A.z, A.w)));
+      bits |= (q <= thr) ? (1u << ji) : 0u;
+    }
+    bits &= (left >= 8 ? 0xffu : ((1u << left) - 1u));
+    if (jo < 8) m0 |= (unsigned long long)bits << (jo * 8);
+    else m1 |= (unsigned long long)bits << ((jo - 8) * 8);
+  }
+}
+
+// One drain unit: the lane's candidates in up to two staged windows [wa0,wa1) and
+// [wb0,wb1) (two point-mirrored neighbour rows, or one row), all positions relative to
+// the item, drained as ONE set.  How many real neighbours a particle has in one row
+// depends on where it sits inside its cell; in a mirrored pair of rows the two counts
+// complement each other, so the loop length (the busiest lane's count / 2) is far closer
+// to the average lane's than with one row at a time.
+// The accepted candidates of a round (<= 128 per window) are four 64-bit words,
+// compacted once into a chain (empty words dropped): `cur` is popped, and when it runs
+// dry the next word shifts in.  Value selects only (a word picked by reference puts the
+// masks in scratch), no divergent branch in the loop (the second pop of an iteration is
+// unconditional; an empty pop's pair is masked off).
 template <int TDENSITY, int MODE>
-__device__ __forceinline__ void tile_range(const KConst& K, const P1& p, float ry, float rz, int s0, int s1,
-                                           const float4* __restrict__ sA, const float4* __restrict__ sB,
-                                           const float2* __restrict__ sC, const PassK& Q, TAcc& a) {
-  const float px2 = -2.f * p.x, py2 = -2.f * ry, pz2 = -2.f * rz;
-  const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + ry * ry + rz * rz);
+__device__ __forceinline__ void tile_unit(const KConst& K, const P1& p, float thr, int wa0, int wa1, int wb0, int wb1,
+                                          const float4* __restrict__ sA, const float4* __restrict__ sB,
+                                          const float2* __restrict__ sC, const PassK& Q, TAcc& a) {
+  const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
 #if SPH_ABLATE == 2
-  a.visc += float(s1 - s0);
+  a.visc += float(wa1 - wa0 + wb1 - wb0);
   return;
 #endif
-  for (int base = s0; base < s1; base += 128) {
-    unsigned long long m0 = 0, m1 = 0;
-    const int n0 = s1 - base;  // candidates left for this lane (> 0)
-    // sA is padded by 128 records, so base+127 stays inside the array; bits past the
-    // lane's range are masked off per 8-candidate group.
-    const float4* __restrict__ sAb = sA + base;
-    for (int jo = 0; jo < 16; jo++) {
-      const int left = n0 - jo * 8;
-      if (left <= 0) break;
-      unsigned bits = 0;
-#pragma unroll
-      for (int ji = 0; ji < 8; ji++) {
-        const float4 A = sAb[jo * 8 + ji];
-        const float q = fmaf(px2, A.x, fmaf(py2, A.y, fmaf(pz2, A.z, A.w)));
-        bits |= (q <= thr) ? (1u << ji) : 0u;
-      }
-      bits &= (left >= 8 ? 0xffu : ((1u << left) - 1u));
-      if (jo < 8) m0 |= (unsigned long long)bits << (jo * 8);
-      else m1 |= (unsigned long long)bits << ((jo - 8) * 8);
-    }
+  for (int off = 0;; off += 128) {  // a second round only for windows of > 128 candidates
+    const int na = wa1 - wa0 - off, nb = wb1 - wb0 - off;
+    if (na <= 0 && nb <= 0) break;
+    unsigned long long c0, c1, c2, c3;
+    test128(sA, wa0 + off, min(na, 128), px2, py2, pz2, thr, c0, c1);
+    test128(sA, wb0 + off, min(nb, 128), px2, py2, pz2, thr, c2, c3);
 #if SPH_ABLATE == 1
-    a.visc += float(__popcll(m0) + __popcll(m1));
-    m0 = m1 = 0;
+    a.visc += float(__popcll(c0) + __popcll(c1) + __popcll(c2) + __popcll(c3));
+    continue;
 #endif
-    // Drain: `cur` is the 64-bit word being popped (refilled from `nxt` when it runs
-    // dry), so a pop is ctz + clear-lowest + one refill select.  Value selects only: a
-    // branch that picks a mask word by reference makes the compiler keep the masks in
-    // scratch.  The second pop of an iteration is unconditional (an empty pop returns
-    // an index whose pair is masked off), so the loop body has no divergent branch.
-    unsigned long long cur = m0 ? m0 : m1, nxt = m0 ? m1 : 0ull;
-    int cbase = base + (m0 ? 0 : 64);
+    int b0 = wa0 + off, b1 = b0 + 64, b2 = wb0 + off, b3 = b2 + 64;
+    // compact: drop empty words, keep the order (three bubble passes)
+#pragma unroll
+    for (int pass = 0; pass < 3; pass++) {
+      const bool e2 = c2 == 0ull;
+      c2 = e2 ? c3 : c2;
+      b2 = e2 ? b3 : b2;
+      c3 = e2 ? 0ull : c3;
+      const bool e1 = c1 == 0ull;
+      c1 = e1 ? c2 : c1;
+      b1 = e1 ? b2 : b1;
+      c2 = e1 ? c3 : c2;
+      b2 = e1 ? b3 : b2;
+      c3 = e1 ? 0ull : c3;
+      const bool e0 = c0 == 0ull;
+      c0 = e0 ? c1 : c0;
+      b0 = e0 ? b1 : b0;
+      c1 = e0 ? c2 : c1;
+      b1 = e0 ? b2 : b1;
+      c2 = e0 ? c3 : c2;
+      b2 = e0 ? b3 : b2;
+      c3 = e0 ? 0ull : c3;
+    }
     auto pop = [&](void) -> int {
-      const int j = cbase + int(__builtin_ctzll(cur | (1ull << 63)));
-      cur &= cur - 1ull;
-      const bool e = cur == 0ull;
-      cur = e ? nxt : cur;
-      nxt = e ? 0ull : nxt;
-      cbase += e ? 64 : 0;
+      const int j = b0 + int(__builtin_ctzll(c0 | (1ull << 63)));
+      c0 &= c0 - 1ull;
+      const bool e = c0 == 0ull;
+      c0 = e ? c1 : c0;
+      b0 = e ? b1 : b0;
+      c1 = e ? c2 : c1;
+      b1 = e ? b2 : b1;
+      c2 = e ? c3 : c2;
+      b2 = e ? b3 : b2;
+      c3 = e ? 0ull : c3;
       return j;
     };
-    while (cur) {
+    while (c0) {
       const int j1 = pop();
-      const bool two = cur != 0ull;
+      const bool two = c0 != 0ull;
       const int j2p = pop();
       const int j2 = two ? j2p : j1;
       const float4 A1 = sA[j1], A2 = sA[j2];
       const float4 B1 = sB[j1], B2 = sB[j2];
       const float2 C1 = sC[j1], C2 = sC[j2];
-      const float drx1 = p.x - A1.x, dry1 = ry - A1.y, drz1 = rz - A1.z;
-      const float drx2 = p.x - A2.x, dry2 = ry - A2.y, drz2 = rz - A2.z;
+      const float drx1 = p.x - A1.x, dry1 = p.y - A1.y, drz1 = p.z - A1.z;
+      const float drx2 = p.x - A2.x, dry2 = p.y - A2.y, drz2 = p.z - A2.z;
       const float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
       const float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
       const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
@@ -286,6 +323,27 @@ __device__ __forceinline__ void tile_range(const KConst& K, const P1& p, float r
       pair_body<TDENSITY, MODE>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, Q, a);
       pair_body<TDENSITY, MODE>(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, Q, a);
     }
+  }
+}
+
+// Stage the records [rs, re) of the row at (dy, dz) from the item's row into sA/sB/sC at
+// dst: positions relative to the item (x to its x origin xo, y/z to its cell row), |A|^2,
+// velrhop, press/rho, 1/rho.
+__device__ __forceinline__ void stage_row(const KConst& K, unsigned rs, unsigned re, unsigned dst, int xo, int dy,
+                                          int dz, const float4* __restrict__ poscell,
+                                          const float4* __restrict__ velrhop, const float* __restrict__ press,
+                                          float4* __restrict__ sA, float4* __restrict__ sB, float2* __restrict__ sC) {
+  const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
+  for (unsigned i = threadIdx.x; i < re - rs; i += TB) {
+    const float4 pc = poscell[rs + i];
+    const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
+    const float x2 = pc.x + float(cx2 - xo) * K.scell;
+    const float y2 = pc.y + oy, z2 = pc.z + oz;
+    sA[dst + i] = make_float4(x2, y2, z2, x2 * x2 + y2 * y2 + z2 * z2);
+    const float4 vr = velrhop[rs + i];
+    sB[dst + i] = vr;
+    const float ir = frcp(vr.w);
+    sC[dst + i] = make_float2(press[rs + i] * ir, ir);
   }
 }
 
@@ -364,44 +422,64 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
         qb.cv = 2.f * K.bwenovh * cvisc_b;
         qb.kd = K.ddtkhcs * qb.bm;
         const int lxa = max(cx1 - 1, 0), lxb = min(cx1 + 1, g.ncx - 1);
+        const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
         TAcc f = {0, 0, 0, 0, 0, 0}, bnd = {0, 0, 0, 0, 0, 0};
         const int npass = bitem ? 1 : 2;
         for (int pass = 0; pass < npass; pass++) {
           const unsigned cellinit = (pass == 0 ? g.boxfluid : 0u);
-          for (int z = max(cz - 1, 0); z <= min(cz + 1, g.ncz - 1); z++) {
-            const float rz = p.z + float(cz - z) * K.scell;
-            for (int y = max(cy - 1, 0); y <= min(cy + 1, g.ncy - 1); y++) {
+          // drain units: point-mirrored row pairs, then the item's own row
+          for (int u = 0; u < 5; u++) {
+            const int dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
+            const int dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
+            const bool paired = u < 4;
+            // rows (dya, dza) and (-dya, -dza); an out-of-grid row is empty
+            unsigned rs[2] = {0, 0}, re[2] = {0, 0}, ls[2] = {0, 0}, le[2] = {0, 0};
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+              if (k == 1 && !paired) break;
+              const int dz = k ? -dza : dza, dy = k ? -dya : dya;
+              const int z = cz + dz, y = cy + dy;
+              if (z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;
               const unsigned rowbase = cellinit + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
-              const unsigned rs = bc[rowbase + xa], re = bc[rowbase + xb + 1];
-              if (rs == re) continue;
-              const float ry = p.y + float(cy - y) * K.scell;
-              const unsigned ls = bc[rowbase + lxa], le = bc[rowbase + lxb + 1];
-              for (unsigned seg = rs; seg < re; seg += TCAP) {
-                const unsigned segn = min(unsigned(TCAP), re - seg);
-                __syncthreads();
-#if SPH_ABLATE != 3
-                for (unsigned i = threadIdx.x; i < segn; i += TB) {
-#else
-                for (unsigned i = threadIdx.x; i < 0; i += TB) {
-#endif
-                  const float4 pc = poscell[seg + i];
-                  const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
-                  const float x2 = pc.x + float(cx2 - xo) * K.scell;
-                  sA[i] = make_float4(x2, pc.y, pc.z, x2 * x2 + pc.y * pc.y + pc.z * pc.z);
-                  const float4 vr = velrhop[seg + i];
-                  sB[i] = vr;
-                  const float ir = frcp(vr.w);
-                  sC[i] = make_float2(press[seg + i] * ir, ir);
+              rs[k] = bc[rowbase + xa];
+              re[k] = bc[rowbase + xb + 1];
+              ls[k] = bc[rowbase + lxa];
+              le[k] = bc[rowbase + lxb + 1];
+            }
+            const unsigned n0 = re[0] - rs[0], n1 = re[1] - rs[1];
+            if (n0 + n1 == 0u) continue;
+            if (n0 + n1 <= unsigned(TCAP)) {
+              // both rows in one segment: [row a][row b]
+              __syncthreads();
+              if (n0) stage_row(K, rs[0], re[0], 0u, xo, dya, dza, poscell, velrhop, press, sA, sB, sC);
+              if (n1) stage_row(K, rs[1], re[1], n0, xo, -dya, -dza, poscell, velrhop, press, sA, sB, sC);
+              __syncthreads();
+              const int wa0 = int(ls[0] - rs[0]), wa1 = act && n0 ? int(le[0] - rs[0]) : wa0;
+              const int wb0 = int(n0 + ls[1] - rs[1]), wb1 = act && n1 ? int(n0 + le[1] - rs[1]) : wb0;
+              if (bitem)
+                tile_unit<TDENSITY, 2>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, qf, f);
+              else if (pass == 0)
+                tile_unit<TDENSITY, 0>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, qf, f);
+              else
+                tile_unit<TDENSITY, 1>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, qb, bnd);
+            } else {
+              // too long for one segment: each row on its own, in TCAP segments
+              for (int k = 0; k < 2; k++) {
+                const int dz = k ? -dza : dza, dy = k ? -dya : dya;
+                for (unsigned seg = rs[k]; seg < re[k]; seg += TCAP) {
+                  const unsigned segn = min(unsigned(TCAP), re[k] - seg);
+                  __syncthreads();
+                  stage_row(K, seg, seg + segn, 0u, xo, dy, dz, poscell, velrhop, press, sA, sB, sC);
+                  __syncthreads();
+                  const int w0 = int(max(ls[k], seg) - seg);
+                  const int w1 = act ? max(w0, int(min(le[k], seg + segn)) - int(seg)) : w0;
+                  if (bitem)
+                    tile_unit<TDENSITY, 2>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, qf, f);
+                  else if (pass == 0)
+                    tile_unit<TDENSITY, 0>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, qf, f);
+                  else
+                    tile_unit<TDENSITY, 1>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, qb, bnd);
                 }
-                __syncthreads();
-                const int s0 = int(max(ls, seg) - seg);
-                const int s1 = act ? int(min(le, seg + segn)) - int(seg) : 0;
-                if (bitem)
-                  tile_range<TDENSITY, 2>(K, p, ry, rz, s0, s1, sA, sB, sC, qf, f);
-                else if (pass == 0)
-                  tile_range<TDENSITY, 0>(K, p, ry, rz, s0, s1, sA, sB, sC, qf, f);
-                else
-                  tile_range<TDENSITY, 1>(K, p, ry, rz, s0, s1, sA, sB, sC, qb, bnd);
               }
             }
           }
