@@ -47,9 +47,9 @@ __device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x
 // ------------------------------------------------------------------------------------
 // Item list (per divide).  Rows [0,nrows) are fluid rows (fluid p1), rows
 // [nrows,2*nrows) bound rows (bound p1, DBC).  One wave per row loads the row's cell
-// counts into LDS (coalesced), then lane 0 splits the row greedily into items; the
-// count and write passes run the same greedy, so the list is deterministic and in
-// spatial (z, y, x) order, fluid items first.
+// counts into LDS (coalesced) with their prefix sums, then lane 0 splits the row
+// greedily into items reading LDS only; the count and write passes run the same
+// greedy, so the list is deterministic and in spatial (z, y, x) order, fluid items first.
 constexpr int ROWCELLS_LDS = 1024;
 constexpr unsigned ITEM_BOUND = 0x80000000u;  // flag in item.x: p1 are boundary particles
 
@@ -57,6 +57,9 @@ template <bool WRITE>
 __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ bc, DivGrid g,
                                                    unsigned* __restrict__ counts, uint4* __restrict__ items) {
   __shared__ unsigned cnt[ROWCELLS_LDS];
+  __shared__ unsigned pre[ROWCELLS_LDS + 1];
+  __shared__ unsigned short iend[ROWCELLS_LDS];     // end (exclusive) of a greedy item starting at x
+  __shared__ unsigned short nzfrom[ROWCELLS_LDS + 1];  // first non-empty owned cell >= x (xend if none)
   const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
   const unsigned r = blockIdx.x;
   const bool bound = r >= nrows;
@@ -64,33 +67,89 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
   const unsigned y = rr % unsigned(g.ncy), z = rr / unsigned(g.ncy);
   const unsigned rowbase = (bound ? 0u : g.boxfluid) + z * g.nsheet + y * unsigned(g.ncx);
   const int ncx = g.ncx;
-  const bool inlds = ncx <= ROWCELLS_LDS;
-  if (inlds)
-    for (int x = threadIdx.x; x < ncx; x += 64) cnt[x] = bc[rowbase + x + 1] - bc[rowbase + x];
+  // p1 only in the owned columns (slab ghosts are neighbours, never p1).
+  const int xbeg = g.xown0, xend = g.xown1;
+  uint4* out = WRITE ? items + counts[r] : nullptr;
+  unsigned nitems = 0;
+  if (ncx > ROWCELLS_LDS) {  // very long rows: the plain serial greedy on global memory
+    if (threadIdx.x != 0) return;
+    auto count = [&](int x) { return bc[rowbase + x + 1] - bc[rowbase + x]; };
+    int x = xbeg;
+    while (x < xend) {
+      while (x < xend && count(x) == 0) x++;
+      if (x >= xend) break;
+      const int a = x;
+      unsigned n = count(x);
+      x++;
+      while (x < xend && x - a < TMAXCELLS) {
+        const unsigned c = count(x);
+        if (n + c > unsigned(TB)) break;
+        n += c;
+        x++;
+      }
+      if (WRITE)
+        out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(x - 1) << 16),
+                                 bc[rowbase + a], bc[rowbase + x]);
+      nitems++;
+    }
+    if (!WRITE) counts[r] = nitems;
+    return;
+  }
+  // Counts and their prefix sums (begin offsets): each lane a contiguous block of cells,
+  // lane totals scanned across the wave.
+  const int per = (ncx + 63) / 64, x0 = int(threadIdx.x) * per, x1 = min(x0 + per, ncx);
+  const unsigned rowstart = bc[rowbase];
+  unsigned run = 0;
+  for (int x = x0; x < x1; x++) {
+    const unsigned c = bc[rowbase + x + 1] - bc[rowbase + x];
+    cnt[x] = c;
+    pre[x] = run;
+    run += c;
+  }
+  unsigned incl = run;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned v = __shfl_up(incl, off, 64);
+    if (int(threadIdx.x) >= off) incl += v;
+  }
+  const unsigned excl = incl - run + rowstart;
+  for (int x = x0; x < x1; x++) pre[x] += excl;
+  if (threadIdx.x == 63) pre[ncx] = incl + rowstart;
+  __syncthreads();
+  // Per cell: where the greedy item starting there ends (<= TMAXCELLS cells, <= TB p1),
+  // and the first non-empty owned cell at or after it (block-local, then a wave
+  // suffix-min).
+  int nz = xend;
+  for (int x = x1 - 1; x >= x0; x--) {
+    unsigned n = cnt[x];
+    int e = x + 1;
+    while (e < xend && e - x < TMAXCELLS && n + cnt[e] <= unsigned(TB)) n += cnt[e++];
+    iend[x] = (unsigned short)e;
+    if (x >= xbeg && x < xend && cnt[x] != 0u) nz = x;
+    nzfrom[x] = (unsigned short)nz;
+  }
+  int suf = nz;  // min over this and later lanes' blocks
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int v = __shfl_down(suf, off, 64);
+    if (int(threadIdx.x) + off < 64) suf = min(suf, v);
+  }
+  const int later = __shfl_down(suf, 1, 64);
+  const int carry = int(threadIdx.x) < 63 ? later : xend;
+  for (int x = x0; x < x1; x++)
+    if (int(nzfrom[x]) == xend) nzfrom[x] = (unsigned short)carry;
+  if (threadIdx.x == 63) nzfrom[ncx] = (unsigned short)xend;
   __syncthreads();
   if (threadIdx.x != 0) return;
-  auto count = [&](int x) { return inlds ? cnt[x] : bc[rowbase + x + 1] - bc[rowbase + x]; };
-  unsigned nitems = 0;
-  uint4* out = WRITE ? items + counts[r] : nullptr;
-  // p1 only in the owned columns (slab ghosts are neighbours, never p1).
-  const int xend = g.xown1;
-  int x = g.xown0;
+  // Walk the items: one LDS hop per item.
+  int x = nzfrom[xbeg];
   while (x < xend) {
-    while (x < xend && count(x) == 0) x++;
-    if (x >= xend) break;
-    const int a = x;
-    unsigned n = count(x);
-    x++;
-    while (x < xend && x - a < TMAXCELLS) {
-      const unsigned c = count(x);
-      if (n + c > unsigned(TB)) break;
-      n += c;
-      x++;
-    }
+    const int e = iend[x];
     if (WRITE)
-      out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(x - 1) << 16),
-                               bc[rowbase + a], bc[rowbase + x]);
+      out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(x) | (unsigned(e - 1) << 16),
+                               pre[x], pre[e]);
     nitems++;
+    x = nzfrom[e];
   }
   if (!WRITE) counts[r] = nitems;
 }

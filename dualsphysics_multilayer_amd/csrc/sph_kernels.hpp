@@ -33,7 +33,10 @@ struct SortScratch {
 };
 
 constexpr int RS_BS = 256;        // threads per radix block
-constexpr int RS_ITEMS = 16;      // keys per thread per tile
+#ifndef SPH_RS_ITEMS
+#define SPH_RS_ITEMS 8
+#endif
+constexpr int RS_ITEMS = SPH_RS_ITEMS;  // keys per thread per tile
 constexpr int RS_TILE = RS_BS * RS_ITEMS;
 constexpr int RS_MAXBITS = 11;    // widest digit (2048 buckets)
 
