@@ -263,6 +263,7 @@ struct GatherArgs {
   float* press;
   double posminx, posminy, posminz, scelld;
   float cteb, ovrhopzero, gamma;
+  int igamma;  // gamma as a small positive integer, else 0
   unsigned dcc;
   int withm1, withpre;
   int xoff;
@@ -300,8 +301,22 @@ __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, Gat
     a.poscell[i] = make_float4(float(pxy.x - ox), float(pxy.y - oy), float(pz - oz), __uint_as_float(ldc));
     // Press (PreInteractionVars_Forces, JSphCpu.cpp:451-453; FunSphEos.h:37-47) as the
     // reference binary evaluates it: the unqualified pow in namespace fsph is the C
-    // double pow, and -ffast-math makes rhop/rhop0 a product with 1/rhop0.
-    a.press[i] = float(double(a.cteb) * (pow(double(vr.w * a.ovrhopzero), double(a.gamma)) - 1.0));
+    // double pow, and -ffast-math makes rhop/rhop0 a product with 1/rhop0.  For an
+    // integer gamma the double power is formed by squaring (<= 4 roundings at 1e-16,
+    // far below the float rounding of the result).
+    const double xr = double(vr.w * a.ovrhopzero);
+    double xg;
+    if (a.igamma > 0) {  // integer gamma (7 in every case here): exact squaring in double
+      double r = 1.0, b = xr;
+      for (int e = a.igamma; e; e >>= 1) {
+        if (e & 1) r *= b;
+        b *= b;
+      }
+      xg = r;
+    } else {
+      xg = pow(xr, double(a.gamma));
+    }
+    a.press[i] = float(double(a.cteb) * (xg - 1.0));
     if (i >= npb) v2 = vr.x * vr.x + vr.y * vr.y + vr.z * vr.z;  // CalcVelMaxOmp over fluid
   }
   wave_max_atomic(sc, RED_VELMAX2, v2);
@@ -324,6 +339,7 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
   a.cteb = K.cteb;
   a.ovrhopzero = K.ovrhopzero;
   a.gamma = K.gamma;
+  a.igamma = (K.gamma == float(int(K.gamma)) && K.gamma >= 1.f && K.gamma <= 16.f) ? int(K.gamma) : 0;
   a.dcc = K.domcellcode;
   a.withm1 = withm1;
   a.withpre = withpre;

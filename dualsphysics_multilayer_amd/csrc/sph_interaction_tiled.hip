@@ -440,15 +440,18 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
       const int xo = (a + b + 1) >> 1;
       const int xa = max(a - 1, 0), xb = min(b + 1, g.ncx - 1);
       if (bitem) {
-        // Bound item: nothing to do unless a fluid cell is in its 3x3x3 neighbourhood
-        // (arace of the boundary was zeroed before the launch).
+        // Bound item: nothing to compute unless a fluid cell is in its 3x3x3
+        // neighbourhood; then its particles get ar = 0 (PreInteraction's reset).
         bool any = false;
         for (int z = max(cz - 1, 0); z <= min(cz + 1, g.ncz - 1); z++)
           for (int y = max(cy - 1, 0); y <= min(cy + 1, g.ncy - 1); y++) {
             const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
             any |= bc[rowbase + xa] != bc[rowbase + xb + 1];
           }
-        if (!any) continue;
+        if (!any) {
+          for (unsigned p1 = item.z + threadIdx.x; p1 < item.w; p1 += TB) arace[p1] = make_float4(0.f, 0.f, 0.f, 0.f);
+          continue;
+        }
       }
       for (unsigned p1base = item.z; p1base < item.w; p1base += TB) {
         const unsigned p1 = p1base + threadIdx.x;
@@ -544,8 +547,8 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
           }
         }
         if (act && bitem) {
-          // InteractionForcesBound store (JSphCpu.cpp:617-621).
-          if (f.ar != 0.f || f.visc != 0.f) arace[p1] = make_float4(0.f, 0.f, 0.f, 0.f + f.ar);
+          // InteractionForcesBound store (JSphCpu.cpp:617-621) onto the reset ar = 0.
+          arace[p1] = make_float4(0.f, 0.f, 0.f, (f.ar != 0.f || f.visc != 0.f) ? 0.f + f.ar : 0.f);
           viscmax = fmaxf(viscmax, f.visc);
         } else if (act) {
           // Combine exactly as the two CPU passes store (JSphCpu.cpp:800-818).
@@ -574,6 +577,15 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
   }
   wave_max_atomic(sc, RED_VISCDT, viscmax);
   wave_max_atomic(sc, RED_ACEMAX2, ace2max);
+  // The last block out resets the work counters for the next launch (qctr[8] counts
+  // finished blocks), so no memset launch is needed before each interaction.
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(&qctr[8], 1u) == gridDim.x - 1) {
+      for (int i = 0; i < 9; i++) atomicExch(&qctr[i], 0u);
+    }
+  }
 }
 
 void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,

@@ -300,7 +300,8 @@ void SphGpuSingle::AllocFixed() {
   begincell_ = (unsigned*)dmalloc(4 * size_t(G.nctt));
   items_ = (uint4*)dmalloc(16 * (2 * size_t(G.nct) + 1));
   rowtmp_ = (unsigned*)dmalloc(4 * 2 * size_t(G.ncy) * size_t(G.ncz));
-  qctr_ = (unsigned*)dmalloc(4 * 8);
+  qctr_ = (unsigned*)dmalloc(4 * 16);
+  check_hip(hipMemset(qctr_, 0, 4 * 16), "zero work counters");
   sort_.digtot = (unsigned*)dmalloc(4 * (1u << RS_MAXBITS));
   sc_ = (DevScalars*)dmalloc(sizeof(DevScalars));
   dttrace_ = (double*)dmalloc(8 * size_t(tracecap_));
@@ -536,9 +537,8 @@ void SphGpuSingle::RunCellDivide() {
 void SphGpuSingle::Interaction_Forces(int interstep) {
   (void)interstep;  // mDBC / shifting are not on this path
   if (tiled_) {
-    check_hip(hipMemsetAsync(qctr_, 0, 4 * 8, stream), "reset work counters");
-    // Boundary rows without fluid neighbours are skipped by the tiled kernel: their ar=0.
-    check_hip(hipMemsetAsync(arace_, 0, sizeof(float4) * npb0_, stream), "zero boundary arace");
+    // The tiled kernel writes the arace of every owned particle (skipped boundary items
+    // get ar = 0) and resets its own work counters at exit (zeroed once at allocation).
     TimedBegin(0);  // the timed interval is the interaction kernel alone (rocprof's per-kernel average)
     launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, begincell_, G, K,
                        arace_);
