@@ -1,24 +1,28 @@
 #!/bin/bash
 # Round profile collection (run on the MI355X box from the repo root):
 #   profiles/collect.sh <tag> [bench args]
-#   1. bench.py (default flags, incl. the CPU baseline)        -> <tag>/bench.json
-#   2. rocprofv3 --kernel-trace --stats of the bench            -> <tag>/kernel_stats.csv
-#   3. rocprofv3 --pmc FETCH_SIZE, 4. --pmc WRITE_SIZE passes    -> <tag>/pmc_traffic.json
+#   1. rocprofv3 --kernel-trace --stats of the bench            -> <tag>/kernel_stats.csv
+#   2. rocprofv3 --pmc FETCH_SIZE, 3. --pmc WRITE_SIZE passes    -> <tag>/pmc_traffic.json
 #      (separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass,
 #       MI355X_MICROARCH.md §rocprofv3; never combined with sys/runtime traces)
+#   4. bench.py (default flags, incl. the CPU baseline)        -> <tag>/bench.json
+#      (reads the traffic of step 2-3 from profiles/<tag>/)
+# Results go to profiles/<tag>/ of the box copy and to gpurun_out/profiles/<tag>/.
 set -e
 TAG=${1:?tag}
 shift || true
 ARGS=${*:-"--steps 20 --warmup 3"}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
-DST=$R/gpurun_out/profiles/$TAG
+DST=$R/profiles/$TAG
 export TMPDIR=/tmp
 mkdir -p "$OUT" "$DST"
-timeout -k 10 400 python3 "$R/bench.py" $ARGS > "$OUT/bench.log" 2>&1
-grep '^{' "$OUT/bench.log" | tail -1 > "$DST/bench.json"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 "$R/bench.py" $ARGS --no-cpu-baseline > "$OUT/kt.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run -- python3 "$R/bench.py" $ARGS --no-cpu-baseline > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run -- python3 "$R/bench.py" $ARGS --no-cpu-baseline > "$OUT/write.log" 2>&1
 python3 "$R/profiles/summarize.py" "$OUT" "$DST"
+timeout -k 10 400 python3 "$R/bench.py" $ARGS > "$OUT/bench.log" 2>&1
+grep '^{' "$OUT/bench.log" | tail -1 > "$DST/bench.json"
+mkdir -p "$R/gpurun_out/profiles/$TAG"
+cp "$DST"/* "$R/gpurun_out/profiles/$TAG/"
 echo collect-done
