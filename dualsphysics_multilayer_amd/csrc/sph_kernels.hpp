@@ -88,8 +88,7 @@ void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst&
                     DivGrid g);
 
 // ---- slab decomposition (sph_slab.hip) ----
-// One particle crossing a slab face: full state, 96 B.  Ghost copies use the same
-// record (the *pre / m1 fields are not read for ghosts).
+// A particle MIGRATING to a neighbour: its full state, 96 B.
 struct SlabRec {
   double2 posxy;
   double posz;
@@ -101,24 +100,42 @@ struct SlabRec {
   unsigned short code, flags;
   unsigned pad;
 };
-constexpr unsigned short SLABREC_MIGRANT = 1;
+// A GHOST copy for a neighbour: what a neighbour of the interaction needs, 40 B.  The
+// position travels as the float offset from its (global) cell origin, i.e. exactly the
+// poscell the owner computes; the receiver rebuilds the double position as origin +
+// offset (exact: < 31 significant bits), so its poscell is bit-identical.
+struct SlabGhost {
+  float rx, ry, rz;
+  unsigned dcell;
+  float4 velrhop;
+  unsigned idp;
+  unsigned short code, pad;
+};
 constexpr int PK_BS = 256, PK_ITEMS = 16, PK_TILE = PK_BS * PK_ITEMS;
-// Device counters of one exchange.
+// Device counters of one exchange: [0] ghosts, [1] migrants, per neighbour.
 struct SlabCounts {
-  unsigned long long send[2];  // records for the left / right neighbour
-  unsigned long long recv[2];
-  unsigned np;                 // particles before the exchange (sc->np)
-  unsigned nkeep;              // particles staying owned (not migrating, not dropped)
+  unsigned long long sendl[2], sendr[2];  // records for the left / right neighbour
+  unsigned long long recvl[2], recvr[2];  // records from the left / right neighbour
+  unsigned np;                            // particles before the exchange (sc->np)
+  unsigned nkeep;                         // particles staying owned (not migrating, not dropped)
   unsigned pad[2];
 };
+struct SlabSendBufs {
+  SlabGhost* gl;
+  SlabGhost* gr;
+  SlabRec* ml;
+  SlabRec* mr;
+  unsigned long long gcap, mcap;  // records beyond the capacity are counted, not written
+};
 // Classify every particle after an update (stable order) and write the records for
-// the two neighbours: tile counts -> scan -> scatter.  has_left/has_right: the
-// neighbour exists.  Records beyond `sendcap` are counted but not written.
+// the two neighbours: tile counts -> scan -> scatter, four streams (ghost/migrant x
+// left/right).  has_left/has_right: the neighbour exists.
 void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, DivGrid g, const KConst& K,
-                      bool has_left, bool has_right, bool withm1, bool withpre, unsigned* tilecnt, SlabCounts* cnt,
-                      SlabRec* sendl, SlabRec* sendr, unsigned long long sendcap);
-// Append nrecv received records at [np, np+nrecv) and set sc->np, sc->nown.
-void launch_slab_unpack(hipStream_t stm, DevScalars* sc, const SlabRec* recv, unsigned np, unsigned nrecv,
-                        const PartArrays& a, bool withm1, bool withpre, SlabCounts* cnt);
+                      const double dom_posmin[3], bool has_left, bool has_right, bool withm1, bool withpre,
+                      unsigned* tilecnt, SlabCounts* cnt, SlabSendBufs bufs);
+// Append nm received migrants at [np, np+nm) and ng ghosts after them; set sc->np, sc->nown.
+void launch_slab_unpack(hipStream_t stm, DevScalars* sc, const SlabRec* mig, unsigned nm, const SlabGhost* gh,
+                        unsigned ng, unsigned np, const PartArrays& a, const KConst& K, const double dom_posmin[3],
+                        bool withm1, bool withpre, SlabCounts* cnt);
 
 }  // namespace sphx

@@ -10,12 +10,13 @@
 //     by MovLimit = 0.9*Scell < one column, so it lands exactly in the ghost column);
 //   * an owned particle in column c0 (c1-1) is copied to the left (right) neighbour
 //     as a ghost.
-// Records are written in particle order (tile counts -> scan -> ballot-ranked
-// scatter), so the receive order and hence the in-cell summation order of the next
-// interaction are deterministic.  The reference has no multi-GPU path in this fork
-// (JSphGpuSingle only); this follows the single-domain semantics exactly: the
-// owner of a particle computes it with the same neighbour set it would have in one
-// domain.
+// Migrants travel as full 96-B records, ghosts as 40-B records (cell-relative float
+// position, dcell, velrhop, idp, code).  Records are written in particle order (tile
+// counts -> scan -> ballot-ranked scatter), so the receive order and hence the in-cell
+// summation order of the next interaction are deterministic.  The reference has no
+// multi-GPU path in this fork (JSphGpuSingle only); this follows the single-domain
+// semantics exactly: the owner of a particle computes it with the same neighbour set
+// it would have in one domain.
 #include "sph_kernels.hpp"
 
 namespace sphx {
@@ -24,16 +25,16 @@ struct PackArgs {
   PartArrays a;
   DivGrid g;
   unsigned dcc;
+  double posminx, posminy, posminz, scelld;
   int has_left, has_right, withm1, withpre;
-  unsigned* tilecnt;  // [2][ntiles]
+  unsigned* tilecnt;  // [4][ntiles]: ghost L, ghost R, migrant L, migrant R
   unsigned ntiles;
   SlabCounts* cnt;
-  SlabRec* sendl;
-  SlabRec* sendr;
-  unsigned long long sendcap;
+  SlabSendBufs b;
 };
 
-// bit 0: record for the left neighbour, bit 1: record for the right, bit 2: stays owned.
+// bit 0: record for the left neighbour, bit 1: record for the right, bit 2: stays owned
+// (so a record with bit 2 is a ghost copy, without it a migrant).
 __device__ __forceinline__ unsigned pack_class(const PackArgs& q, unsigned p) {
   const unsigned dc = q.a.dcell[p];
   if (dc == DCELL_DISCARD || dc == DCELL_OUT) return 0u;
@@ -46,67 +47,68 @@ __device__ __forceinline__ unsigned pack_class(const PackArgs& q, unsigned p) {
   return c;
 }
 
+// the four stream flags of a class
+__device__ __forceinline__ void streams(unsigned c, bool f[4]) {
+  const bool stay = (c & 4u) != 0u;
+  f[0] = (c & 1u) && stay;   // ghost -> left
+  f[1] = (c & 2u) && stay;   // ghost -> right
+  f[2] = (c & 1u) && !stay;  // migrant -> left
+  f[3] = (c & 2u) && !stay;  // migrant -> right
+}
+
 __global__ __launch_bounds__(PK_BS) void k_pack_count(const DevScalars* __restrict__ sc, PackArgs q) {
-  __shared__ unsigned s[3][PK_BS / 64];
+  __shared__ unsigned s[5][PK_BS / 64];
   const unsigned n = sc->np;
   const unsigned base = blockIdx.x * PK_TILE;
-  unsigned cl = 0, cr = 0, ck = 0;
+  unsigned c4[5] = {0, 0, 0, 0, 0};
   for (int it = 0; it < PK_ITEMS; it++) {
     const unsigned p = base + it * PK_BS + threadIdx.x;
     if (p < n) {
       const unsigned c = pack_class(q, p);
-      cl += c & 1u;
-      cr += (c >> 1) & 1u;
-      ck += (c >> 2) & 1u;
+      bool f[4];
+      streams(c, f);
+#pragma unroll
+      for (int k = 0; k < 4; k++) c4[k] += f[k] ? 1u : 0u;
+      c4[4] += (c >> 2) & 1u;
     }
   }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    cl += __shfl_xor(cl, off, 64);
-    cr += __shfl_xor(cr, off, 64);
-    ck += __shfl_xor(ck, off, 64);
-  }
+  for (int k = 0; k < 5; k++)
+    for (int off = 32; off > 0; off >>= 1) c4[k] += __shfl_xor(c4[k], off, 64);
   const unsigned w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    s[0][w] = cl;
-    s[1][w] = cr;
-    s[2][w] = ck;
-  }
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < 5; k++) s[k][w] = c4[k];
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned tl = 0, tr = 0, tk = 0;
-    for (int i = 0; i < PK_BS / 64; i++) {
-      tl += s[0][i];
-      tr += s[1][i];
-      tk += s[2][i];
+    for (int k = 0; k < 5; k++) {
+      unsigned t = 0;
+      for (int i = 0; i < PK_BS / 64; i++) t += s[k][i];
+      if (k < 4) q.tilecnt[k * q.ntiles + blockIdx.x] = t;
+      else if (t) atomicAdd(&q.cnt->nkeep, t);
     }
-    q.tilecnt[blockIdx.x] = tl;
-    q.tilecnt[q.ntiles + blockIdx.x] = tr;
-    if (tk) atomicAdd(&q.cnt->nkeep, tk);
   }
 }
 
-// Exclusive scan of the tile counts (both directions), totals -> cnt->send.
+// Exclusive scan of the tile counts (four streams), totals -> cnt.
 __global__ __launch_bounds__(1024) void k_pack_scan(const DevScalars* __restrict__ sc, PackArgs q) {
-  __shared__ unsigned part[2][1024];
+  __shared__ unsigned part[4][1024];
   const unsigned nt = q.ntiles;
   const unsigned per = (nt + 1023) / 1024;
   const unsigned b0 = threadIdx.x * per, b1 = min(b0 + per, nt);
-  for (int d = 0; d < 2; d++) {
+  for (int d = 0; d < 4; d++) {
     unsigned s = 0;
     for (unsigned i = b0; i < b1; i++) s += q.tilecnt[d * nt + i];
     part[d][threadIdx.x] = s;
   }
   __syncthreads();
   for (int off = 1; off < 1024; off <<= 1) {
-    const unsigned v0 = threadIdx.x >= unsigned(off) ? part[0][threadIdx.x - off] : 0u;
-    const unsigned v1 = threadIdx.x >= unsigned(off) ? part[1][threadIdx.x - off] : 0u;
+    unsigned v[4];
+    for (int d = 0; d < 4; d++) v[d] = threadIdx.x >= unsigned(off) ? part[d][threadIdx.x - off] : 0u;
     __syncthreads();
-    part[0][threadIdx.x] += v0;
-    part[1][threadIdx.x] += v1;
+    for (int d = 0; d < 4; d++) part[d][threadIdx.x] += v[d];
     __syncthreads();
   }
-  for (int d = 0; d < 2; d++) {
+  for (int d = 0; d < 4; d++) {
     unsigned run = threadIdx.x ? part[d][threadIdx.x - 1] : 0u;
     for (unsigned i = b0; i < b1; i++) {
       const unsigned v = q.tilecnt[d * nt + i];
@@ -115,13 +117,35 @@ __global__ __launch_bounds__(1024) void k_pack_scan(const DevScalars* __restrict
     }
   }
   if (threadIdx.x == 1023) {
-    q.cnt->send[0] = part[0][1023];
-    q.cnt->send[1] = part[1][1023];
+    q.cnt->sendl[0] = part[0][1023];
+    q.cnt->sendr[0] = part[1][1023];
+    q.cnt->sendl[1] = part[2][1023];
+    q.cnt->sendr[1] = part[3][1023];
     q.cnt->np = sc->np;
   }
 }
 
-__device__ __forceinline__ void write_rec(const PackArgs& q, unsigned p, SlabRec* dst, bool migrant) {
+__device__ __forceinline__ void write_ghost(const PackArgs& q, unsigned p, SlabGhost* dst) {
+  const unsigned dc = q.a.dcell[p];
+  const double2 pxy = q.a.posxy[p];
+  const double pz = q.a.posz[p];
+  // the owner's poscell of this particle (KerUpdatePosCell, global cell origin)
+  const double ox = q.posminx + double(DcelCellx(q.dcc, dc)) * q.scelld;
+  const double oy = q.posminy + double(DcelCelly(q.dcc, dc)) * q.scelld;
+  const double oz = q.posminz + double(DcelCellz(q.dcc, dc)) * q.scelld;
+  SlabGhost r;
+  r.rx = float(pxy.x - ox);
+  r.ry = float(pxy.y - oy);
+  r.rz = float(pz - oz);
+  r.dcell = dc;
+  r.velrhop = q.a.velrhop[p];
+  r.idp = q.a.idp[p];
+  r.code = q.a.code[p];
+  r.pad = 0;
+  *dst = r;
+}
+
+__device__ __forceinline__ void write_migrant(const PackArgs& q, unsigned p, SlabRec* dst) {
   SlabRec r;
   r.posxy = q.a.posxy[p];
   r.posz = q.a.posz[p];
@@ -131,69 +155,71 @@ __device__ __forceinline__ void write_rec(const PackArgs& q, unsigned p, SlabRec
   r.vr2 = make_float4(0.f, 0.f, 0.f, 0.f);
   r.posxypre = make_double2(0., 0.);
   r.poszpre = 0.;
-  if (migrant) {
-    if (q.withm1) r.vr2 = q.a.velrhopm1[p];
-    if (q.withpre) {
-      r.vr2 = q.a.velrhoppre[p];
-      r.posxypre = q.a.posxypre[p];
-      r.poszpre = q.a.poszpre[p];
-    }
+  if (q.withm1) r.vr2 = q.a.velrhopm1[p];
+  if (q.withpre) {
+    r.vr2 = q.a.velrhoppre[p];
+    r.posxypre = q.a.posxypre[p];
+    r.poszpre = q.a.poszpre[p];
   }
   r.code = q.a.code[p];
-  r.flags = migrant ? SLABREC_MIGRANT : 0;
+  r.flags = 0;
   r.pad = 0;
   *dst = r;
 }
 
 __global__ __launch_bounds__(PK_BS) void k_pack_write(const DevScalars* __restrict__ sc, PackArgs q) {
   constexpr int NW = PK_BS / 64;
-  __shared__ unsigned s_w[2][NW];
+  __shared__ unsigned s_w[4][NW];
   const unsigned n = sc->np;
   const unsigned base = blockIdx.x * PK_TILE;
-  unsigned offl = q.tilecnt[blockIdx.x], offr = q.tilecnt[q.ntiles + blockIdx.x];
+  unsigned off[4];
+  for (int k = 0; k < 4; k++) off[k] = q.tilecnt[k * q.ntiles + blockIdx.x];
   const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const unsigned long long lt = (1ull << lane) - 1ull;
   for (int it = 0; it < PK_ITEMS; it++) {
     if (base + it * PK_BS >= n) break;  // uniform over the block
     const unsigned p = base + it * PK_BS + threadIdx.x;
     const unsigned c = p < n ? pack_class(q, p) : 0u;
-    const unsigned long long bl = __ballot(c & 1u), br = __ballot((c >> 1) & 1u);
-    if (lane == 0) {
-      s_w[0][w] = __popcll(bl);
-      s_w[1][w] = __popcll(br);
-    }
+    bool f[4];
+    streams(c, f);
+    unsigned long long bal[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) bal[k] = __ballot(f[k]);
+    if (lane == 0)
+      for (int k = 0; k < 4; k++) s_w[k][w] = __popcll(bal[k]);
     __syncthreads();
-    unsigned prel = 0, prer = 0, totl = 0, totr = 0;
-    for (int i = 0; i < NW; i++) {
-      if (i < int(w)) {
-        prel += s_w[0][i];
-        prer += s_w[1][i];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      unsigned pre = 0, tot = 0;
+      for (int i = 0; i < NW; i++) {
+        if (i < int(w)) pre += s_w[k][i];
+        tot += s_w[k][i];
       }
-      totl += s_w[0][i];
-      totr += s_w[1][i];
+      if (f[k]) {
+        const unsigned long long slot = off[k] + pre + __popcll(bal[k] & lt);
+        if (k < 2) {
+          if (slot < q.b.gcap) write_ghost(q, p, (k == 0 ? q.b.gl : q.b.gr) + slot);
+        } else {
+          if (slot < q.b.mcap) write_migrant(q, p, (k == 2 ? q.b.ml : q.b.mr) + slot);
+        }
+      }
+      off[k] += tot;
     }
-    const bool migrant = (c & 4u) == 0u;
-    if (c & 1u) {
-      const unsigned long long k = offl + prel + __popcll(bl & lt);
-      if (k < q.sendcap) write_rec(q, p, q.sendl + k, migrant);
-    }
-    if (c & 2u) {
-      const unsigned long long k = offr + prer + __popcll(br & lt);
-      if (k < q.sendcap) write_rec(q, p, q.sendr + k, migrant);
-    }
-    offl += totl;
-    offr += totr;
     __syncthreads();
   }
 }
 
 void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, DivGrid g, const KConst& K,
-                      bool has_left, bool has_right, bool withm1, bool withpre, unsigned* tilecnt, SlabCounts* cnt,
-                      SlabRec* sendl, SlabRec* sendr, unsigned long long sendcap) {
+                      const double dom_posmin[3], bool has_left, bool has_right, bool withm1, bool withpre,
+                      unsigned* tilecnt, SlabCounts* cnt, SlabSendBufs bufs) {
   PackArgs q;
   q.a = a;
   q.g = g;
   q.dcc = K.domcellcode;
+  q.posminx = dom_posmin[0];
+  q.posminy = dom_posmin[1];
+  q.posminz = dom_posmin[2];
+  q.scelld = K.scelld;
   q.has_left = has_left;
   q.has_right = has_right;
   q.withm1 = withm1;
@@ -201,53 +227,83 @@ void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartA
   q.tilecnt = tilecnt;
   q.ntiles = (cap + PK_TILE - 1) / PK_TILE;
   q.cnt = cnt;
-  q.sendl = sendl;
-  q.sendr = sendr;
-  q.sendcap = sendcap;
+  q.b = bufs;
   hipLaunchKernelGGL(k_pack_count, dim3(q.ntiles), dim3(PK_BS), 0, stm, sc, q);
   hipLaunchKernelGGL(k_pack_scan, dim3(1), dim3(1024), 0, stm, sc, q);
   hipLaunchKernelGGL(k_pack_write, dim3(q.ntiles), dim3(PK_BS), 0, stm, sc, q);
 }
 
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_unpack(const SlabRec* __restrict__ recv, unsigned np, unsigned nrecv,
-                                                PartArrays a, int withm1, int withpre, SlabCounts* __restrict__ cnt) {
+struct UnpackArgs {
+  PartArrays a;
+  const SlabRec* mig;
+  const SlabGhost* gh;
+  unsigned nm, ng, np;
+  unsigned dcc;
+  double posminx, posminy, posminz, scelld;
+  int withm1, withpre;
+  SlabCounts* cnt;
+};
+
+__global__ __launch_bounds__(256) void k_unpack(UnpackArgs u) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned mig = 0;
-  if (i < nrecv) {
-    const SlabRec r = recv[i];
-    const unsigned p = np + i;
+  if (i >= u.nm + u.ng) return;
+  const unsigned p = u.np + i;
+  PartArrays& a = u.a;
+  if (i < u.nm) {
+    const SlabRec r = u.mig[i];
     a.posxy[p] = r.posxy;
     a.posz[p] = r.posz;
     a.idp[p] = r.idp;
     a.dcell[p] = r.dcell;
     a.velrhop[p] = r.velrhop;
     a.code[p] = r.code;
-    if (withm1) a.velrhopm1[p] = r.vr2;
-    if (withpre) {
+    if (u.withm1) a.velrhopm1[p] = r.vr2;
+    if (u.withpre) {
       a.velrhoppre[p] = r.vr2;
       a.posxypre[p] = r.posxypre;
       a.poszpre[p] = r.poszpre;
     }
-    mig = (r.flags & SLABREC_MIGRANT) ? 1u : 0u;
+  } else {
+    const SlabGhost r = u.gh[i - u.nm];
+    const double ox = u.posminx + double(DcelCellx(u.dcc, r.dcell)) * u.scelld;
+    const double oy = u.posminy + double(DcelCelly(u.dcc, r.dcell)) * u.scelld;
+    const double oz = u.posminz + double(DcelCellz(u.dcc, r.dcell)) * u.scelld;
+    a.posxy[p] = make_double2(ox + double(r.rx), oy + double(r.ry));
+    a.posz[p] = oz + double(r.rz);
+    a.idp[p] = r.idp;
+    a.dcell[p] = r.dcell;
+    a.velrhop[p] = r.velrhop;
+    a.code[p] = r.code;
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) mig += __shfl_xor(mig, off, 64);
-  if ((threadIdx.x & 63) == 0 && mig) atomicAdd(&cnt->nkeep, mig);
 }
 
 __global__ void k_unpack_finish(DevScalars* __restrict__ sc, const SlabCounts* __restrict__ cnt, unsigned np,
-                                unsigned nrecv) {
-  sc->np = np + nrecv;
-  sc->nown = cnt->nkeep;
+                                unsigned nm, unsigned ng) {
+  sc->np = np + nm + ng;
+  sc->nown = cnt->nkeep + nm;
 }
 
-void launch_slab_unpack(hipStream_t stm, DevScalars* sc, const SlabRec* recv, unsigned np, unsigned nrecv,
-                        const PartArrays& a, bool withm1, bool withpre, SlabCounts* cnt) {
-  if (nrecv)
-    hipLaunchKernelGGL(k_unpack, dim3((nrecv + 255) / 256), dim3(256), 0, stm, recv, np, nrecv, a, int(withm1),
-                       int(withpre), cnt);
-  hipLaunchKernelGGL(k_unpack_finish, dim3(1), dim3(1), 0, stm, sc, cnt, np, nrecv);
+void launch_slab_unpack(hipStream_t stm, DevScalars* sc, const SlabRec* mig, unsigned nm, const SlabGhost* gh,
+                        unsigned ng, unsigned np, const PartArrays& a, const KConst& K, const double dom_posmin[3],
+                        bool withm1, bool withpre, SlabCounts* cnt) {
+  UnpackArgs u;
+  u.a = a;
+  u.mig = mig;
+  u.gh = gh;
+  u.nm = nm;
+  u.ng = ng;
+  u.np = np;
+  u.dcc = K.domcellcode;
+  u.posminx = dom_posmin[0];
+  u.posminy = dom_posmin[1];
+  u.posminz = dom_posmin[2];
+  u.scelld = K.scelld;
+  u.withm1 = withm1;
+  u.withpre = withpre;
+  u.cnt = cnt;
+  if (nm + ng) hipLaunchKernelGGL(k_unpack, dim3((nm + ng + 255) / 256), dim3(256), 0, stm, u);
+  hipLaunchKernelGGL(k_unpack_finish, dim3(1), dim3(1), 0, stm, sc, cnt, np, nm, ng);
 }
 
 }  // namespace sphx

@@ -359,9 +359,11 @@ void SphGpuSingle::Free() {
   FreeParticles();
   for (void* p : allocs_) (void)hipFree(p);
   allocs_.clear();
-  for (void* p : {slabbuf_, recvbuf_})
+  for (void* p : {sendgbuf_, sendmbuf_, (void*)recvg_, (void*)recvm_})
     if (p) (void)hipFree(p);
-  slabbuf_ = recvbuf_ = nullptr;
+  sendgbuf_ = sendmbuf_ = nullptr;
+  recvg_ = nullptr;
+  recvm_ = nullptr;
   if (sc_host_) (void)hipHostFree(sc_host_);
   if (slabcnt_host_) (void)hipHostFree(slabcnt_host_);
   sc_host_ = nullptr;
@@ -476,48 +478,69 @@ void SphGpuSingle::Timing(double out_ms[4], uint64_t* launches) {
 }
 
 // ---- phases ------------------------------------------------------------------------
-// Slab exchange before the divide's sort: pack migrants/ghosts (device), swap the
+// Slab exchange before the divide's sort: pack ghosts and migrants (device), swap the
 // record counts with both neighbours device to device, then ONE host wait to size
-// the receives, move the records, append what arrived.
+// the receives, move the records (ghosts 40 B, migrants 96 B), append what arrived.
 void SphGpuSingle::Exchange() {
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET), withpre = havepre_;
   const bool hl = transport_->has_left(), hr = transport_->has_right();
+  auto pack = [&] {
+    launch_slab_pack(stream, cap_, sc_, cur_, G, K, C.dom_posmin, hl, hr, withm1, withpre, packtiles_, slabcnt_,
+                     send_);
+  };
   check_hip(hipMemsetAsync(slabcnt_, 0, sizeof(SlabCounts), stream), "exchange: reset counts");
-  launch_slab_pack(stream, cap_, sc_, cur_, G, K, hl, hr, withm1, withpre, packtiles_, slabcnt_, sendl_, sendr_,
-                   sendcap_);
-  transport_->exchange(&slabcnt_->send[0], 8, &slabcnt_->send[1], 8, &slabcnt_->recv[0], hl ? 8 : 0,
-                       &slabcnt_->recv[1], hr ? 8 : 0, stream);
+  pack();
+  transport_->exchange(slabcnt_->sendl, 16, slabcnt_->sendr, 16, slabcnt_->recvl, hl ? 16 : 0, slabcnt_->recvr,
+                       hr ? 16 : 0, stream);
   check_hip(hipMemcpyAsync(slabcnt_host_, slabcnt_, sizeof(SlabCounts), hipMemcpyDeviceToHost, stream),
             "exchange: read counts");
   Sync();
   const SlabCounts c = *slabcnt_host_;
-  const unsigned long long need = std::max(c.send[0], c.send[1]);
-  if (need > sendcap_) {  // records past the capacity were not written: grow and pack again
-    if (slabbuf_) check_hip(hipFree(slabbuf_), "hipFree");
-    sendcap_ = need + need / 2 + 4096;
-    check_hip(hipMalloc(&slabbuf_, 2 * sizeof(SlabRec) * sendcap_), "hipMalloc send buffers");
-    sendl_ = (SlabRec*)slabbuf_;
-    sendr_ = sendl_ + sendcap_;
+  const unsigned long long gneed = std::max(c.sendl[0], c.sendr[0]), mneed = std::max(c.sendl[1], c.sendr[1]);
+  if (gneed > send_.gcap || mneed > send_.mcap) {  // records past a capacity were not written: grow, pack again
+    if (gneed > send_.gcap) {
+      if (sendgbuf_) check_hip(hipFree(sendgbuf_), "hipFree");
+      send_.gcap = gneed + gneed / 2 + 4096;
+      check_hip(hipMalloc(&sendgbuf_, 2 * sizeof(SlabGhost) * send_.gcap), "hipMalloc ghost send buffers");
+      send_.gl = (SlabGhost*)sendgbuf_;
+      send_.gr = send_.gl + send_.gcap;
+    }
+    if (mneed > send_.mcap) {
+      if (sendmbuf_) check_hip(hipFree(sendmbuf_), "hipFree");
+      send_.mcap = mneed + mneed / 2 + 1024;
+      check_hip(hipMalloc(&sendmbuf_, 2 * sizeof(SlabRec) * send_.mcap), "hipMalloc migrant send buffers");
+      send_.ml = (SlabRec*)sendmbuf_;
+      send_.mr = send_.ml + send_.mcap;
+    }
     check_hip(hipMemsetAsync(&slabcnt_->nkeep, 0, sizeof(unsigned), stream), "exchange: reset nkeep");
-    launch_slab_pack(stream, cap_, sc_, cur_, G, K, hl, hr, withm1, withpre, packtiles_, slabcnt_, sendl_, sendr_,
-                     sendcap_);
+    pack();
   }
-  const unsigned long long rl = hl ? c.recv[0] : 0, rr = hr ? c.recv[1] : 0;
-  if (rl + rr > recvcap_) {
+  const unsigned long long rgl = hl ? c.recvl[0] : 0, rgr = hr ? c.recvr[0] : 0;
+  const unsigned long long rml = hl ? c.recvl[1] : 0, rmr = hr ? c.recvr[1] : 0;
+  if (rgl + rgr > recvgcap_) {
     check_hip(hipStreamSynchronize(stream), "exchange: sync");
-    if (recvbuf_) check_hip(hipFree(recvbuf_), "hipFree");
-    recvcap_ = rl + rr + (rl + rr) / 2 + 4096;
-    check_hip(hipMalloc(&recvbuf_, sizeof(SlabRec) * recvcap_), "hipMalloc receive buffer");
-    recv_ = (SlabRec*)recvbuf_;
+    if (recvg_) check_hip(hipFree(recvg_), "hipFree");
+    recvgcap_ = rgl + rgr + (rgl + rgr) / 2 + 4096;
+    check_hip(hipMalloc((void**)&recvg_, sizeof(SlabGhost) * recvgcap_), "hipMalloc ghost receive buffer");
   }
-  if (c.np + rl + rr > cap_) {
-    const unsigned long long want = (c.np + rl + rr) + (c.np + rl + rr) / 2;
+  if (rml + rmr > recvmcap_) {
+    check_hip(hipStreamSynchronize(stream), "exchange: sync");
+    if (recvm_) check_hip(hipFree(recvm_), "hipFree");
+    recvmcap_ = rml + rmr + (rml + rmr) / 2 + 1024;
+    check_hip(hipMalloc((void**)&recvm_, sizeof(SlabRec) * recvmcap_), "hipMalloc migrant receive buffer");
+  }
+  const unsigned long long nin = rgl + rgr + rml + rmr;
+  if (c.np + nin > cap_) {
+    const unsigned long long want = (c.np + nin) + (c.np + nin) / 2;
     if (want >= (1ull << 31)) throw SphError(SPH_ERR_NOMEM, "slab particle capacity overflow");
     Grow(c.np, unsigned(want));
   }
-  transport_->exchange(sendl_, sizeof(SlabRec) * c.send[0], sendr_, sizeof(SlabRec) * c.send[1], recv_,
-                       sizeof(SlabRec) * rl, recv_ + rl, sizeof(SlabRec) * rr, stream);
-  launch_slab_unpack(stream, sc_, recv_, c.np, unsigned(rl + rr), cur_, withm1, withpre, slabcnt_);
+  transport_->exchange(send_.gl, sizeof(SlabGhost) * c.sendl[0], send_.gr, sizeof(SlabGhost) * c.sendr[0], recvg_,
+                       sizeof(SlabGhost) * rgl, recvg_ + rgl, sizeof(SlabGhost) * rgr, stream);
+  transport_->exchange(send_.ml, sizeof(SlabRec) * c.sendl[1], send_.mr, sizeof(SlabRec) * c.sendr[1], recvm_,
+                       sizeof(SlabRec) * rml, recvm_ + rml, sizeof(SlabRec) * rmr, stream);
+  launch_slab_unpack(stream, sc_, recvm_, unsigned(rml + rmr), recvg_, unsigned(rgl + rgr), c.np, cur_, K,
+                     C.dom_posmin, withm1, withpre, slabcnt_);
 }
 
 void SphGpuSingle::RunCellDivide() {

@@ -115,12 +115,12 @@ class SphGpuSingle {
   SlabCounts* slabcnt_ = nullptr;
   SlabCounts* slabcnt_host_ = nullptr;
   unsigned* packtiles_ = nullptr;
-  SlabRec* sendl_ = nullptr;
-  SlabRec* sendr_ = nullptr;
-  SlabRec* recv_ = nullptr;
-  unsigned long long sendcap_ = 0, recvcap_ = 0;
-  void* slabbuf_ = nullptr;
-  void* recvbuf_ = nullptr;
+  SlabSendBufs send_{nullptr, nullptr, nullptr, nullptr, 0, 0};
+  SlabGhost* recvg_ = nullptr;
+  SlabRec* recvm_ = nullptr;
+  unsigned long long recvgcap_ = 0, recvmcap_ = 0;
+  void* sendgbuf_ = nullptr;
+  void* sendmbuf_ = nullptr;
   // timing (hipEvents on the solver stream)
   bool timing_ = false;
   struct Ev { hipEvent_t a, b; int phase; };
