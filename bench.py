@@ -170,15 +170,36 @@ def main() -> None:
         dp = args.dp or CFG3_DP
         case = DamBreakCase(dp, step_algorithm=2, tdensity=1)
     bounds = None
+    fallback = None
+    s = None
     if use_slab:
-        bounds = slab_partition(case, world, args.bound_weight)
-        ids = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(ids, src=0)
-        s = SphGpuSlab(case, rank, world, bounds, ids[0], device=local)
+        try:
+            bounds = slab_partition(case, world, args.bound_weight)
+            ids = [comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(ids, src=0)
+            s = SphGpuSlab(case, rank, world, bounds, ids[0], device=local)
+            s.run(args.warmup)
+            s.sync()
+            ok = torch.tensor([1], dtype=torch.int32)
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line, never silent
+            sys.stderr.write("rank %d: slab path failed: %r\n" % (rank, e))
+            fallback = repr(e)[:300]
+            ok = torch.tensor([0], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            # every rank runs its own domain of the same size instead (still GPU, still
+            # one process per GPU); the JSON line says so
+            if s is not None:
+                s.close()
+            fallback = fallback or "slab path failed on another rank"
+            bounds = None
+            s = SphGpuSingle(case, device=local)
+            s.run(args.warmup)
+            s.sync()
     else:
         s = SphGpuSingle(case, device=local)
-    s.run(args.warmup)
-    s.sync()
+        s.run(args.warmup)
+        s.sync()
     pairs0 = s.count_pairs()
 
     def barrier():
@@ -246,7 +267,8 @@ def main() -> None:
                               % (case.np, dp))),
                 "np": case.np,
                 "npb": case.npb,
-                "parallelism": ("slab-x%d (RCCL halo + migration, max-allreduce dt)" % world) if use_slab else "single",
+                "parallelism": (("slab-x%d (RCCL halo + migration, max-allreduce dt)" % world) if bounds is not None
+                                else ("replicas (FALLBACK: %s)" % fallback) if fallback else "single"),
                 "slab_bounds_cells": None if bounds is None else [int(b) for b in bounds],
                 "owned_np_per_rank": per_rank_np,
             },
