@@ -166,6 +166,85 @@ class SphSlabDef(C.Structure):
     ]
 
 
+class SphPartHeader(C.Structure):
+    _fields_ = [
+        ("app_name", C.c_char * 64),
+        ("case_name", C.c_char * 64),
+        ("cpart", C.c_uint32),
+        ("npok", C.c_uint32),
+        ("nout", C.c_uint32),
+        ("step", C.c_uint32),
+        ("timestep", C.c_double),
+        ("runtime", C.c_double),
+        ("domain_min", C.c_double * 3),
+        ("domain_max", C.c_double * 3),
+        ("symplectic_dtpre", C.c_double),
+        ("np_total", C.c_uint64),
+        ("case_np", C.c_uint64),
+        ("case_nfixed", C.c_uint64),
+        ("case_nmoving", C.c_uint64),
+        ("case_nfloat", C.c_uint64),
+        ("case_nfluid", C.c_uint64),
+        ("dp", C.c_double),
+        ("h", C.c_double),
+        ("b", C.c_double),
+        ("rhop0", C.c_double),
+        ("gamma", C.c_double),
+        ("massbound", C.c_double),
+        ("massfluid", C.c_double),
+        ("map_posmin", C.c_double * 3),
+        ("map_posmax", C.c_double * 3),
+        ("case_posmin", C.c_double * 3),
+        ("case_posmax", C.c_double * 3),
+        ("peri_xinc", C.c_double * 3),
+        ("peri_yinc", C.c_double * 3),
+        ("peri_zinc", C.c_double * 3),
+        ("data2d_posy", C.c_double),
+        ("data2d", C.c_int32),
+        ("peri_mode", C.c_int32),
+        ("axis_div", C.c_int32),
+        ("np_dynamic", C.c_int32),
+        ("reuse_ids", C.c_int32),
+        ("symmetry", C.c_int32),
+        ("splitting", C.c_int32),
+        ("pos_double", C.c_int32),
+        ("visco_type", C.c_int32),
+        ("visco", C.c_float),
+        ("viscoboundfactor", C.c_float),
+        ("gravity", C.c_float * 3),
+        ("mkbound", C.c_uint32),
+        ("mkfluid", C.c_uint32),
+    ]
+
+    def as_dict(self) -> dict:
+        d = {}
+        for name, t in self._fields_:
+            v = getattr(self, name)
+            if isinstance(v, bytes):
+                v = v.decode()
+            elif hasattr(v, "__len__"):
+                v = list(v)
+            d[name] = v
+        return d
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "SphPartHeader":
+        h = cls()
+        for name, t in cls._fields_:
+            if name not in d:
+                continue
+            v = d[name]
+            if isinstance(v, str):
+                v = v.encode()
+            if hasattr(getattr(h, name), "__len__") and not isinstance(v, bytes):
+                arr = getattr(h, name)
+                for i, x in enumerate(v):
+                    arr[i] = x
+            else:
+                setattr(h, name, v)
+        return h
+
+
 def _ptr(arr: np.ndarray | None, ctype):
     if arr is None:
         return C.POINTER(ctype)()
@@ -209,4 +288,5 @@ def check_struct_sizes() -> dict:
         "SphParticlesHost": C.sizeof(SphParticlesHost),
         "SphInterOut": C.sizeof(SphInterOut),
         "SphSlabDef": C.sizeof(SphSlabDef),
+        "SphPartHeader": C.sizeof(SphPartHeader),
     }

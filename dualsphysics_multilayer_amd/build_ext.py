@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUTDIR = os.path.join(HERE, "lib")
 LIBNAME = "libsphcore.so"
 SOURCES = ["sph_divide.hip", "sph_interaction.hip", "sph_interaction_tiled.hip", "sph_step.hip", "sph_slab.hip",
-           "sph_solver.cpp", "sph_comm.cpp", "sph_capi.cpp"]
+           "sph_solver.cpp", "sph_comm.cpp", "sph_bi4.cpp", "sph_capi.cpp"]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 LDFLAGS = ["-L" + os.path.join(ROCM, "lib"), "-lrccl", "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-pthread"]
 ARCH = os.environ.get("SPH_OFFLOAD_ARCH", "gfx950")

@@ -131,8 +131,28 @@ class DamBreakCase:
     def mass(self) -> float:
         return _xml_e10(self._mass)
 
+    def restart_from(self, header: dict, particles: dict) -> "DamBreakCase":
+        """This case continued from a loaded PART (JPartsLoad4 + JSph::InitRun with
+        PartBegin): particles in file order, the map limits of the PART file
+        (MapPosMin/Max), simulated time TimeStep (apply with solver.set_time)."""
+        import copy
+
+        c = copy.copy(self)
+        c.idp = np.ascontiguousarray(particles["idp"], np.uint32)
+        c.pos = np.ascontiguousarray(particles["pos"], np.float64)
+        c.vel = np.ascontiguousarray(particles["vel"], np.float32)
+        c.rhop = np.ascontiguousarray(particles["rhop"], np.float32)
+        c.np = len(c.idp)
+        c.npb = int(header["case_nfixed"])
+        c._map = (np.array(header["map_posmin"]), np.array(header["map_posmax"]))
+        c.time0 = float(header["timestep"])
+        c.symdtpre0 = float(header.get("symplectic_dtpre", 0.0))
+        return c
+
     def map_limits(self) -> tuple[np.ndarray, np.ndarray]:
         """MapRealPosMin/Max as JSph::LoadCaseParticles computes them."""
+        if getattr(self, "_map", None) is not None:
+            return self._map
         kernelh = float(np.float32(self.h))
         border = kernelh * BORDER_MAP
         pmin = self.pos.min(axis=0)

@@ -24,6 +24,7 @@ from ._abi import (
     SphConstants,
     SphInterOut,
     SphRunStats,
+    SphPartHeader,
     SphSlabDef,
 )
 
@@ -51,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "sph_download_particles",
     "sph_download_interaction",
     "sph_count_pairs",
+    "sph_solver_set_time",
     "sph_solver_set_timing",
     "sph_solver_timing",
     "sph_slab_partition",
@@ -60,6 +62,10 @@ EXPORTED_SYMBOLS = (
     "sph_slab_group_destroy",
     "sph_slab_group_run",
     "sph_slab_group_member",
+    "sph_part_read",
+    "sph_part_write",
+    "sph_part_head_write",
+    "sph_bi4_rewrite",
 )
 
 
@@ -97,6 +103,7 @@ def load_library(path: str = LIB_PATH):
     L.sph_download_interaction.argtypes = [vp, C.POINTER(SphInterOut)]
     L.sph_count_pairs.argtypes = [vp, C.POINTER(C.c_uint64)]
     L.sph_solver_set_timing.argtypes = [vp, C.c_int]
+    L.sph_solver_set_time.argtypes = [vp, C.c_double, C.c_double]
     L.sph_solver_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
     L.sph_slab_partition.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.c_double, C.POINTER(C.c_int32)]
     L.sph_comm_unique_id.argtypes = [C.POINTER(C.c_ubyte)]
@@ -106,6 +113,10 @@ def load_library(path: str = LIB_PATH):
     L.sph_slab_group_destroy.argtypes = [vp]
     L.sph_slab_group_run.argtypes = [vp, C.c_uint32]
     L.sph_slab_group_member.argtypes = [vp, C.c_int, C.POINTER(vp)]
+    L.sph_part_read.argtypes = [C.c_char_p, C.POINTER(SphPartHeader), vp]
+    L.sph_part_write.argtypes = [C.c_char_p, C.POINTER(SphPartHeader), vp]
+    L.sph_bi4_rewrite.argtypes = [C.c_char_p, C.c_char_p]
+    L.sph_part_head_write.argtypes = [C.c_char_p, C.POINTER(SphPartHeader)]
     if L.sph_abi_version() != SPH_ABI_VERSION:
         raise SphError(3, "ABI version mismatch")
     _lib = L
@@ -203,6 +214,18 @@ class SphGpuSingle:
         out = np.zeros(6, np.uint64)
         _check(load_library().sph_count_pairs(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64))))
         return out
+
+    def set_time(self, time: float, symplectic_dtpre: float = 0.0) -> None:
+        """Restart from a PART: its TimeStep (and SymplecticDtPre)."""
+        _check(load_library().sph_solver_set_time(self._h, time, symplectic_dtpre))
+
+    def save_part(self, path: str, cpart: int, head_path: str | None = None) -> None:
+        """SaveData: this solver's state as a reference PART file (+ Part_Head.ibi4)."""
+        p = self.particles()  # solver (cell-sorted) order, as the reference saves
+        hdr = part_header(self.case, self.stats(), cpart)
+        write_part(path, hdr, {k: p[k] for k in ("idp", "pos", "vel", "rhop")})
+        if head_path:
+            write_part_head(head_path, hdr)
 
     def set_timing(self, on: bool) -> None:
         _check(load_library().sph_solver_set_timing(self._h, int(on)))
@@ -319,3 +342,57 @@ class SphSlabGroup:
         cat = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
         o = np.argsort(cat["idp"], kind="stable")
         return {k: v[o] for k, v in cat.items()}
+
+
+# ---- PART / case files (.bi4), SURVEY.md §8(f) row 2 ---------------------------------
+def read_part(path: str) -> tuple[dict, dict]:
+    """JPartDataBi4::LoadFilePart / LoadFileCase: (header values, particles by file order)."""
+    L = load_library()
+    h = SphPartHeader()
+    _check(L.sph_part_read(os.fsencode(path), C.byref(h), None))
+    hp = HostParticles(h.npok)
+    hp.view.code = C.POINTER(C.c_uint16)()
+    _check(L.sph_part_read(os.fsencode(path), C.byref(h), C.byref(hp.view)))
+    p = hp.trimmed(h.npok)
+    del p["code"]
+    return h.as_dict(), p
+
+
+def write_part(path: str, header: dict, particles: dict) -> None:
+    """JPartDataBi4::AddPartInfo + AddPartData + SaveFilePart for host particle arrays."""
+    h = SphPartHeader.from_dict(header)
+    n = len(particles["idp"])
+    h.npok = n
+    hp = HostParticles(n, particles["idp"], particles["pos"], particles["vel"], particles["rhop"])
+    _check(load_library().sph_part_write(os.fsencode(path), C.byref(h), C.byref(hp.view)))
+
+
+def write_part_head(path: str, header: dict) -> None:
+    """Part_Head.ibi4 (JPartDataHead) for a restart directory."""
+    h = SphPartHeader.from_dict(header)
+    _check(load_library().sph_part_head_write(os.fsencode(path), C.byref(h)))
+
+
+def bi4_rewrite(src: str, dst: str) -> None:
+    _check(load_library().sph_bi4_rewrite(os.fsencode(src), os.fsencode(dst)))
+
+
+def part_header(case, stats: dict | None = None, cpart: int = 0, app_name: str = "dualsphysics_multilayer_amd",
+                case_name: str = "CaseDambreak") -> dict:
+    """PART header of a DamBreakCase (+ solver stats for time, counts, SymplecticDtPre)."""
+    cd = case.case_def()
+    k = case_derive(cd)
+    pmin, pmax = case.pos.min(axis=0), case.pos.max(axis=0)
+    st = stats or {}
+    return dict(app_name=app_name, case_name=case_name, cpart=cpart, nout=int(st.get("nout", 0)),
+                step=int(st.get("nstep", 0)), timestep=float(st.get("time", 0.0)),
+                symplectic_dtpre=float(st.get("sym_dtpre", 0.0)) if case.step_algorithm == 2 else 0.0,
+                domain_min=list(k["map_realposmin"]),
+                domain_max=[k["map_realposmin"][i] + k["map_realsize"][i] for i in range(3)],
+                case_np=case.np, case_nfixed=case.npb, case_nfluid=case.np - case.npb,
+                dp=cd["dp"], h=cd["h"], b=cd["cteb"], rhop0=cd["rhop0"], gamma=cd["gamma"],
+                massbound=cd["massbound"], massfluid=cd["massfluid"],
+                map_posmin=list(cd["map_realposmin"]), map_posmax=list(cd["map_realposmax"]),
+                case_posmin=pmin.tolist(), case_posmax=pmax.tolist(), pos_double=1,
+                visco_type=1, visco=case.visco, viscoboundfactor=case.viscoboundfactor,
+                gravity=list(case.gravity), mkbound=10, mkfluid=0)

@@ -1,0 +1,508 @@
+// sph_bi4.cpp — .bi4 container reader/writer (layout documented in sph_bi4.hpp).
+#include "sph_bi4.hpp"
+
+#include <cstring>
+#include <fstream>
+
+#include "sph_solver.hpp"
+
+namespace sphx {
+namespace bi4 {
+
+static const char* kItem = "\nITEM\n";
+static const char* kValues = "\nVALUES";
+static const char* kArray = "\nARRAY";
+
+size_t type_size(int32_t t) {
+  switch (t) {
+    case Bool: return 4;
+    case Char: case Uchar: return 1;
+    case Short: case Ushort: return 2;
+    case Int: case Uint: case Float: return 4;
+    case Llong: case Ullong: case Double: return 8;
+    case Int3: case Uint3: case Float3: return 12;
+    case Double3: return 24;
+    default: return 0;
+  }
+}
+
+// ---- cursor over a byte buffer ---------------------------------------------------
+namespace {
+struct Reader {
+  const uint8_t* p;
+  size_t n, i = 0;
+  Reader(const uint8_t* d, size_t sz) : p(d), n(sz) {}
+  void need(size_t k) const {
+    if (i + k > n) throw SphError(SPH_ERR_ARG, "bi4: truncated data");
+  }
+  void raw(void* dst, size_t k) {
+    need(k);
+    std::memcpy(dst, p + i, k);
+    i += k;
+  }
+  uint32_t u32() {
+    uint32_t v;
+    raw(&v, 4);
+    return v;
+  }
+  int32_t i32() {
+    int32_t v;
+    raw(&v, 4);
+    return v;
+  }
+  std::string str() {
+    const uint32_t len = u32();
+    need(len);
+    std::string s(reinterpret_cast<const char*>(p + i), len);
+    i += len;
+    return s;
+  }
+  void expect(const char* code) {
+    if (str() != code) throw SphError(SPH_ERR_ARG, "bi4: invalid validation code");
+  }
+};
+
+struct Writer {
+  std::vector<uint8_t> b;
+  void raw(const void* d, size_t k) {
+    const uint8_t* s = static_cast<const uint8_t*>(d);
+    b.insert(b.end(), s, s + k);
+  }
+  void u32(uint32_t v) { raw(&v, 4); }
+  void i32(int32_t v) { raw(&v, 4); }
+  void str(const std::string& s) {
+    u32(uint32_t(s.size()));
+    raw(s.data(), s.size());
+  }
+};
+
+void parse_item(Reader& r, Item& it) {
+  const uint32_t defsize = r.u32();
+  const size_t def0 = r.i;
+  r.expect(kItem);
+  it.name = r.str();
+  it.hide = r.i32() != 0;
+  it.hide_values = r.i32() != 0;
+  it.fmt_float = r.str();
+  it.fmt_double = r.str();
+  const uint32_t narrays = r.u32(), nitems = r.u32(), vsize = r.u32();
+  if (r.i - def0 != defsize) throw SphError(SPH_ERR_ARG, "bi4: item definition size mismatch");
+  if (vsize) {
+    const size_t v0 = r.i;
+    r.expect(kValues);
+    const uint32_t nv = r.u32();
+    for (uint32_t k = 0; k < nv; k++) {
+      Value v;
+      v.name = r.str();
+      v.type = r.i32();
+      size_t sz;
+      if (v.type == Text) sz = r.u32();
+      else if (!(sz = type_size(v.type))) throw SphError(SPH_ERR_ARG, "bi4: invalid value type");
+      v.bytes.resize(sz);
+      r.raw(v.bytes.data(), sz);
+      it.values.push_back(std::move(v));
+    }
+    if (r.i - v0 != vsize) throw SphError(SPH_ERR_ARG, "bi4: values size mismatch");
+  }
+  for (uint32_t k = 0; k < narrays; k++) {
+    const uint32_t adef = r.u32();
+    const size_t a0 = r.i;
+    Array a;
+    r.expect(kArray);
+    a.name = r.str();
+    a.hide = r.i32() != 0;
+    a.type = r.i32();
+    a.count = r.u32();
+    const uint32_t dsize = r.u32();
+    if (r.i - a0 != adef) throw SphError(SPH_ERR_ARG, "bi4: array definition size mismatch");
+    if (a.type != Text && size_t(dsize) != type_size(a.type) * a.count)
+      throw SphError(SPH_ERR_ARG, "bi4: array data size is invalid");
+    a.bytes.resize(dsize);
+    r.raw(a.bytes.data(), dsize);
+    it.arrays.push_back(std::move(a));
+  }
+  for (uint32_t k = 0; k < nitems; k++) {
+    Item c;
+    parse_item(r, c);
+    it.items.push_back(std::move(c));
+  }
+}
+
+void emit_item(Writer& w, const Item& it) {
+  Writer vals;
+  if (!it.values.empty()) {
+    vals.str(kValues);
+    vals.u32(uint32_t(it.values.size()));
+    for (const Value& v : it.values) {
+      vals.str(v.name);
+      vals.i32(v.type);
+      if (v.type == Text) vals.u32(uint32_t(v.bytes.size()));
+      vals.raw(v.bytes.data(), v.bytes.size());
+    }
+  }
+  Writer def;
+  def.str(kItem);
+  def.str(it.name);
+  def.i32(it.hide ? 1 : 0);
+  def.i32(it.hide_values ? 1 : 0);
+  def.str(it.fmt_float);
+  def.str(it.fmt_double);
+  def.u32(uint32_t(it.arrays.size()));
+  def.u32(uint32_t(it.items.size()));
+  def.u32(uint32_t(vals.b.size()));
+  w.u32(uint32_t(def.b.size()));
+  w.raw(def.b.data(), def.b.size());
+  w.raw(vals.b.data(), vals.b.size());
+  for (const Array& a : it.arrays) {
+    Writer ad;
+    ad.str(kArray);
+    ad.str(a.name);
+    ad.i32(a.hide ? 1 : 0);
+    ad.i32(a.type);
+    ad.u32(a.count);
+    ad.u32(uint32_t(a.bytes.size()));
+    w.u32(uint32_t(ad.b.size()));
+    w.raw(ad.b.data(), ad.b.size());
+    w.raw(a.bytes.data(), a.bytes.size());
+  }
+  for (const Item& c : it.items) emit_item(w, c);
+}
+
+std::vector<uint8_t> head(const std::string& filecode) {
+  std::vector<uint8_t> h(64, 0);
+  const std::string t = "#FileJBD " + filecode;
+  const size_t n = std::min<size_t>(58, t.size());
+  for (size_t c = 0; c < 58; c++) h[c] = uint8_t(c < n ? t[c] : ' ');
+  h[58] = '\n';
+  h[60] = 0;  // little endian
+  return h;
+}
+}  // namespace
+
+// ---- Item helpers --------------------------------------------------------------------
+const Value* Item::value(const std::string& n) const {
+  for (const Value& v : values)
+    if (v.name == n) return &v;
+  return nullptr;
+}
+const Array* Item::array(const std::string& n) const {
+  for (const Array& a : arrays)
+    if (a.name == n) return &a;
+  return nullptr;
+}
+const Item* Item::item_prefix(const std::string& prefix) const {
+  for (const Item& c : items)
+    if (c.name.compare(0, prefix.size(), prefix) == 0) return &c;
+  return nullptr;
+}
+void Item::set(const std::string& n, int32_t type, const void* data, size_t bytes) {
+  for (Value& v : values)
+    if (v.name == n) {
+      v.type = type;
+      v.bytes.assign((const uint8_t*)data, (const uint8_t*)data + bytes);
+      return;
+    }
+  Value v;
+  v.name = n;
+  v.type = type;
+  v.bytes.assign((const uint8_t*)data, (const uint8_t*)data + bytes);
+  values.push_back(std::move(v));
+}
+void Item::add_array(const std::string& n, int32_t type, uint32_t count, const void* data) {
+  Array a;
+  a.name = n;
+  a.type = type;
+  a.count = count;
+  a.bytes.assign((const uint8_t*)data, (const uint8_t*)data + type_size(type) * count);
+  arrays.push_back(std::move(a));
+}
+double Item::get_double(const std::string& n, double def) const {
+  const Value* v = value(n);
+  if (!v) return def;
+  switch (v->type) {
+    case Double: { double d; std::memcpy(&d, v->bytes.data(), 8); return d; }
+    case Float: { float f; std::memcpy(&f, v->bytes.data(), 4); return f; }
+    default: return double(get_uint(n, 0));
+  }
+}
+uint64_t Item::get_uint(const std::string& n, uint64_t def) const {
+  const Value* v = value(n);
+  if (!v) return def;
+  switch (v->type) {
+    case Uint: case Int: case Bool: { uint32_t u; std::memcpy(&u, v->bytes.data(), 4); return u; }
+    case Ullong: case Llong: { uint64_t u; std::memcpy(&u, v->bytes.data(), 8); return u; }
+    case Uchar: case Char: return v->bytes[0];
+    case Ushort: case Short: { uint16_t u; std::memcpy(&u, v->bytes.data(), 2); return u; }
+    default: throw SphError(SPH_ERR_ARG, "bi4: value " + n + " is not an integer");
+  }
+}
+bool Item::get_bool(const std::string& n, bool def) const { return value(n) ? get_uint(n, 0) != 0 : def; }
+std::string Item::get_text(const std::string& n, const std::string& def) const {
+  const Value* v = value(n);
+  return (v && v->type == Text) ? std::string(v->bytes.begin(), v->bytes.end()) : def;
+}
+bool Item::get_double3(const std::string& n, double out[3]) const {
+  const Value* v = value(n);
+  if (!v) return false;
+  if (v->type == Double3) std::memcpy(out, v->bytes.data(), 24);
+  else if (v->type == Float3) {
+    float f[3];
+    std::memcpy(f, v->bytes.data(), 12);
+    for (int k = 0; k < 3; k++) out[k] = f[k];
+  } else throw SphError(SPH_ERR_ARG, "bi4: value " + n + " is not a triple");
+  return true;
+}
+
+// ---- files -------------------------------------------------------------------------
+Item read_file(const std::string& path, const std::string& filecode) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw SphError(SPH_ERR_ARG, "bi4: cannot open " + path);
+  std::vector<uint8_t> d((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  if (d.size() < 64) throw SphError(SPH_ERR_ARG, "bi4: no header in " + path);
+  const std::vector<uint8_t> h = head(filecode);
+  if (std::memcmp(d.data(), h.data(), 59) != 0) throw SphError(SPH_ERR_ARG, "bi4: file code is not " + filecode);
+  if (d[60] != 0) throw SphError(SPH_ERR_UNSUPPORTED, "bi4: big-endian files are not supported");
+  Reader r(d.data() + 64, d.size() - 64);
+  Item root;
+  parse_item(r, root);
+  return root;
+}
+
+void write_file(const std::string& path, const std::string& filecode, const Item& root) {
+  Writer w;
+  const std::vector<uint8_t> h = head(filecode);
+  w.raw(h.data(), h.size());
+  emit_item(w, root);
+  std::ofstream f(path, std::ios::binary);
+  if (!f) throw SphError(SPH_ERR_ARG, "bi4: cannot create " + path);
+  f.write(reinterpret_cast<const char*>(w.b.data()), std::streamsize(w.b.size()));
+  if (!f) throw SphError(SPH_ERR_ARG, "bi4: write failed for " + path);
+}
+
+}  // namespace bi4
+}  // namespace sphx
+
+// ---- PART / case files (JPartDataBi4) --------------------------------------------------
+namespace sphx {
+
+static const char* kPartCode = "JPartDataBi4";
+
+void part_read(const std::string& path, SphPartHeader& h, SphParticlesHost* out) {
+  const bi4::Item root = bi4::read_file(path, kPartCode);
+  const bi4::Item* part = root.item_prefix("PART_");
+  if (!part) throw SphError(SPH_ERR_ARG, "bi4: no PART item in " + path);
+  SphPartHeader z;
+  std::memset(&z, 0, sizeof(z));
+  h = z;
+  std::strncpy(h.app_name, root.get_text("AppName", "").c_str(), sizeof(h.app_name) - 1);
+  std::strncpy(h.case_name, root.get_text("CaseName", "").c_str(), sizeof(h.case_name) - 1);
+  h.cpart = uint32_t(part->get_uint("Cpart", 0));
+  h.npok = uint32_t(part->get_uint("Npok", 0));
+  h.nout = uint32_t(part->get_uint("Nout", 0));
+  h.step = uint32_t(part->get_uint("Step", 0));
+  h.timestep = part->get_double("TimeStep", 0);
+  h.runtime = part->get_double("RunTime", 0);
+  part->get_double3("DomainMin", h.domain_min);
+  part->get_double3("DomainMax", h.domain_max);
+  h.symplectic_dtpre = part->get_double("SymplecticDtPre", 0);
+  h.np_total = part->get_uint("NpTotal", 0);
+  h.case_np = root.get_uint("CaseNp", 0);
+  h.case_nfixed = root.get_uint("CaseNfixed", 0);
+  h.case_nmoving = root.get_uint("CaseNmoving", 0);
+  h.case_nfloat = root.get_uint("CaseNfloat", 0);
+  h.case_nfluid = root.get_uint("CaseNfluid", 0);
+  h.dp = root.get_double("Dp", 0);
+  h.h = root.get_double("H", 0);
+  h.b = root.get_double("B", 0);
+  h.rhop0 = root.get_double("Rhop0", 0);
+  h.gamma = root.get_double("Gamma", 0);
+  h.massbound = root.get_double("MassBound", 0);
+  h.massfluid = root.get_double("MassFluid", 0);
+  root.get_double3("MapPosMin", h.map_posmin);
+  root.get_double3("MapPosMax", h.map_posmax);
+  root.get_double3("CasePosMin", h.case_posmin);
+  root.get_double3("CasePosMax", h.case_posmax);
+  root.get_double3("PeriXinc", h.peri_xinc);
+  root.get_double3("PeriYinc", h.peri_yinc);
+  root.get_double3("PeriZinc", h.peri_zinc);
+  h.data2d_posy = root.get_double("Data2dPosY", 0);
+  h.data2d = root.get_bool("Data2d", false);
+  h.peri_mode = int32_t(root.get_uint("PeriMode", 0));
+  h.axis_div = int32_t(root.get_uint("AxisDiv", 0));
+  h.np_dynamic = root.get_bool("NpDynamic", false);
+  h.reuse_ids = root.get_bool("ReuseIds", false);
+  h.symmetry = root.get_bool("Symmetry", false);
+  h.splitting = root.get_bool("Splitting", false);
+  const bi4::Array* posd = part->array("Posd");
+  const bi4::Array* posf = part->array("Pos");
+  h.pos_double = posd ? 1 : 0;
+  if (!out || out->n < h.npok) return;
+  const bi4::Array* idp = part->array("Idp");
+  const bi4::Array* vel = part->array("Vel");
+  const bi4::Array* rhop = part->array("Rhop");
+  if (!idp || !vel || !rhop || !(posd || posf)) throw SphError(SPH_ERR_ARG, "bi4: PART arrays missing");
+  if (idp->type != bi4::Uint) throw SphError(SPH_ERR_UNSUPPORTED, "bi4: only 32-bit Idp is supported");
+  const uint32_t n = h.npok;
+  if (idp->count != n || vel->count != n || rhop->count != n || (posd ? posd->count : posf->count) != n)
+    throw SphError(SPH_ERR_ARG, "bi4: array sizes do not match Npok");
+  if (out->idp) std::memcpy(out->idp, idp->bytes.data(), 4 * size_t(n));
+  if (out->vel) std::memcpy(out->vel, vel->bytes.data(), 12 * size_t(n));
+  if (out->rhop) std::memcpy(out->rhop, rhop->bytes.data(), 4 * size_t(n));
+  if (out->pos) {
+    if (posd) std::memcpy(out->pos, posd->bytes.data(), 24 * size_t(n));
+    else {
+      const float* f = reinterpret_cast<const float*>(posf->bytes.data());
+      for (size_t k = 0; k < 3 * size_t(n); k++) out->pos[k] = f[k];
+    }
+  }
+  out->n = n;
+}
+
+void part_write(const std::string& path, const SphPartHeader& h, const SphParticlesHost& p) {
+  if (p.n != h.npok) throw SphError(SPH_ERR_ARG, "particle count does not match Npok");
+  if (!p.idp || !p.pos || !p.vel || !p.rhop) throw SphError(SPH_ERR_ARG, "particle arrays missing");
+  auto name = [](const char* s, size_t cap) { return std::string(s, strnlen(s, cap)); };
+  // root values in the order JPartDataBi4::Config* writes them (ConfigBasic, ConfigSimMap,
+  // ConfigSimPeri, ConfigSimDiv, ConfigParticles, ConfigCtes, ConfigSymmetry,
+  // ConfigSplitting); execution-dependent values as with -nortimes
+  bi4::Item root;
+  root.name = kPartCode;
+  root.set_pod("Piece", bi4::Uint, uint32_t(0));
+  root.set_pod("Npiece", bi4::Uint, uint32_t(1));
+  root.set_text("RunCode", "00000000");
+  root.set_text("Date", "???");
+  root.set_text("AppName", name(h.app_name, sizeof(h.app_name)));
+  root.set_text("CaseName", name(h.case_name, sizeof(h.case_name)));
+  root.set_pod("Data2d", bi4::Bool, int32_t(h.data2d ? 1 : 0));
+  root.set_pod("Data2dPosY", bi4::Double, h.data2d_posy);
+  root.set("MapPosMin", bi4::Double3, h.map_posmin, 24);
+  root.set("MapPosMax", bi4::Double3, h.map_posmax, 24);
+  root.set_pod("PeriMode", bi4::Int, int32_t(h.peri_mode));
+  root.set("PeriXinc", bi4::Double3, h.peri_xinc, 24);
+  root.set("PeriYinc", bi4::Double3, h.peri_yinc, 24);
+  root.set("PeriZinc", bi4::Double3, h.peri_zinc, 24);
+  root.set_pod("AxisDiv", bi4::Int, int32_t(h.axis_div));
+  root.set_pod("CaseNp", bi4::Ullong, uint64_t(h.case_np));
+  root.set_pod("CaseNfixed", bi4::Ullong, uint64_t(h.case_nfixed));
+  root.set_pod("CaseNmoving", bi4::Ullong, uint64_t(h.case_nmoving));
+  root.set_pod("CaseNfloat", bi4::Ullong, uint64_t(h.case_nfloat));
+  root.set_pod("CaseNfluid", bi4::Ullong, uint64_t(h.case_nfluid));
+  root.set("CasePosMin", bi4::Double3, h.case_posmin, 24);
+  root.set("CasePosMax", bi4::Double3, h.case_posmax, 24);
+  root.set_pod("NpDynamic", bi4::Bool, int32_t(h.np_dynamic ? 1 : 0));
+  root.set_pod("ReuseIds", bi4::Bool, int32_t(h.reuse_ids ? 1 : 0));
+  root.set_pod("Dp", bi4::Double, h.dp);
+  root.set_pod("H", bi4::Double, h.h);
+  root.set_pod("B", bi4::Double, h.b);
+  root.set_pod("Rhop0", bi4::Double, h.rhop0);
+  root.set_pod("Gamma", bi4::Double, h.gamma);
+  root.set_pod("MassBound", bi4::Double, h.massbound);
+  root.set_pod("MassFluid", bi4::Double, h.massfluid);
+  root.set_pod("Symmetry", bi4::Bool, int32_t(h.symmetry ? 1 : 0));
+  root.set_pod("Splitting", bi4::Bool, int32_t(h.splitting ? 1 : 0));
+  // PART item (JPartDataBi4::AddPartInfo + AddPartData)
+  bi4::Item part;
+  char pname[32];
+  std::snprintf(pname, sizeof(pname), "PART_%04u", h.cpart);
+  part.name = pname;
+  part.set_pod("Cpart", bi4::Uint, uint32_t(h.cpart));
+  part.set_pod("TimeStep", bi4::Double, h.timestep);
+  part.set_pod("Npok", bi4::Uint, uint32_t(h.npok));
+  part.set_pod("Nout", bi4::Uint, uint32_t(h.nout));
+  part.set_pod("Step", bi4::Uint, uint32_t(h.step));
+  part.set_pod("RunTime", bi4::Double, h.runtime);
+  part.set("DomainMin", bi4::Double3, h.domain_min, 24);
+  part.set("DomainMax", bi4::Double3, h.domain_max, 24);
+  if (h.np_total) part.set_pod("NpTotal", bi4::Ullong, uint64_t(h.np_total));
+  if (h.symplectic_dtpre > 0) part.set_pod("SymplecticDtPre", bi4::Double, h.symplectic_dtpre);
+  const uint32_t n = h.npok;
+  part.add_array("Idp", bi4::Uint, n, p.idp);
+  if (h.pos_double) {
+    part.add_array("Posd", bi4::Double3, n, p.pos);
+  } else {
+    std::vector<float> f(3 * size_t(n));
+    for (size_t k = 0; k < f.size(); k++) f[k] = float(p.pos[k]);
+    part.add_array("Pos", bi4::Float3, n, f.data());
+  }
+  part.add_array("Vel", bi4::Float3, n, p.vel);
+  part.add_array("Rhop", bi4::Float, n, p.rhop);
+  root.items.push_back(std::move(part));
+  bi4::write_file(path, kPartCode, root);
+}
+
+// Run header (JPartDataHead, Part_Head.ibi4): the case values the restart needs, in the
+// reference's names and order, plus the MK blocks of a fixed-boundary + fluid case.
+void part_head_write(const std::string& path, const SphPartHeader& h) {
+  auto name = [](const char* s, size_t cap) { return std::string(s, strnlen(s, cap)); };
+  bi4::Item root;
+  root.name = "JPartDataHead";
+  root.set_pod("FmtVersion", bi4::Uint, uint32_t(180324));
+  root.set_text("AppName", name(h.app_name, sizeof(h.app_name)));
+  root.set_text("Date", "???");
+  root.set_text("RunCode", "00000000");
+  root.set_text("CaseName", name(h.case_name, sizeof(h.case_name)));
+  root.set_pod("Data2d", bi4::Bool, int32_t(h.data2d ? 1 : 0));
+  root.set_pod("Data2dPosY", bi4::Double, h.data2d_posy);
+  root.set_pod("Npiece", bi4::Uint, uint32_t(1));
+  root.set_pod("FirstPart", bi4::Uint, uint32_t(0));
+  root.set("CasePosMin", bi4::Double3, h.case_posmin, 24);
+  root.set("CasePosMax", bi4::Double3, h.case_posmax, 24);
+  root.set_pod("NpDynamic", bi4::Bool, int32_t(h.np_dynamic ? 1 : 0));
+  root.set_pod("ReuseIds", bi4::Bool, int32_t(h.reuse_ids ? 1 : 0));
+  root.set("MapPosMin", bi4::Double3, h.map_posmin, 24);
+  root.set("MapPosMax", bi4::Double3, h.map_posmax, 24);
+  root.set_pod("PeriMode", bi4::Int, int32_t(h.peri_mode));
+  root.set("PeriXinc", bi4::Double3, h.peri_xinc, 24);
+  root.set("PeriYinc", bi4::Double3, h.peri_yinc, 24);
+  root.set("PeriZinc", bi4::Double3, h.peri_zinc, 24);
+  root.set_pod("ViscoType", bi4::Uint, uint32_t(h.visco_type));
+  root.set_pod("ViscoValue", bi4::Float, h.visco);
+  root.set_pod("ViscoBoundFactor", bi4::Float, h.viscoboundfactor);
+  root.set_pod("Symmetry", bi4::Bool, int32_t(h.symmetry ? 1 : 0));
+  root.set_pod("Splitting", bi4::Bool, int32_t(h.splitting ? 1 : 0));
+  root.set_pod("Dp", bi4::Double, h.dp);
+  root.set_pod("H", bi4::Double, h.h);
+  root.set_pod("B", bi4::Double, h.b);
+  root.set_pod("Gamma", bi4::Double, h.gamma);
+  root.set_pod("RhopZero", bi4::Double, h.rhop0);
+  root.set_pod("MassBound", bi4::Double, h.massbound);
+  root.set_pod("MassFluid", bi4::Double, h.massfluid);
+  root.set("Gravity", bi4::Float3, h.gravity, 12);
+  root.set_pod("CaseNp", bi4::Ullong, uint64_t(h.case_np));
+  root.set_pod("CaseNfixed", bi4::Ullong, uint64_t(h.case_nfixed));
+  root.set_pod("CaseNmoving", bi4::Ullong, uint64_t(h.case_nmoving));
+  root.set_pod("CaseNfloat", bi4::Ullong, uint64_t(h.case_nfloat));
+  root.set_pod("CaseNfluid", bi4::Ullong, uint64_t(h.case_nfluid));
+  bi4::Item mk;
+  mk.name = "MkBlocks";
+  mk.set_pod("Count", bi4::Uint, uint32_t(2));
+  const struct { const char* type; uint32_t mk; uint64_t count; } blocks[2] = {
+      {"Fixed", h.mkbound, h.case_nfixed}, {"Fluid", h.mkfluid, h.case_nfluid}};
+  for (int b = 0; b < 2; b++) {
+    bi4::Item blk;
+    char bn[32];
+    std::snprintf(bn, sizeof(bn), "MkBlock_%03d", b);
+    blk.name = bn;
+    blk.set_text("Type", blocks[b].type);
+    blk.set_pod("Mk", bi4::Uint, blocks[b].mk);
+    blk.set_pod("MkType", bi4::Uint, uint32_t(0));
+    blk.set_pod("Count", bi4::Uint, uint32_t(blocks[b].count));
+    mk.items.push_back(std::move(blk));
+  }
+  root.items.push_back(std::move(mk));
+  bi4::write_file(path, "JPartDataHead", root);
+}
+
+void bi4_rewrite(const std::string& src, const std::string& dst) {
+  // the file code is the header title after "#FileJBD " (up to the padding)
+  std::ifstream f(src, std::ios::binary);
+  char t[64] = {0};
+  if (!f.read(t, 64)) throw SphError(SPH_ERR_ARG, "bi4: no header in " + src);
+  std::string title(t, 58);
+  if (title.compare(0, 9, "#FileJBD ") != 0) throw SphError(SPH_ERR_ARG, "bi4: not a container file");
+  std::string code = title.substr(9);
+  code.erase(code.find_last_not_of(' ') + 1);
+  bi4::write_file(dst, code, bi4::read_file(src, code));
+}
+
+}  // namespace sphx

@@ -140,6 +140,10 @@ int sph_count_pairs(SphSolver* s, uint64_t out[6]) {
   NEED(s && out);
   return guard([&] { s->impl->CountPairs(out); });
 }
+int sph_solver_set_time(SphSolver* s, double time, double symplectic_dtpre) {
+  NEED(s);
+  return guard([&] { s->impl->SetTime(time, symplectic_dtpre); });
+}
 int sph_solver_set_timing(SphSolver* s, int enabled) {
   NEED(s);
   return guard([&] { s->impl->SetTiming(enabled != 0); });
@@ -206,6 +210,26 @@ int sph_slab_group_member(SphSlabGroup* g, int i, SphSolver** out) {
   NEED(g && out && i >= 0 && size_t(i) < g->members.size());
   *out = &g->members[size_t(i)];
   return SPH_OK;
+}
+
+int sph_part_read(const char* path, SphPartHeader* hdr, SphParticlesHost* out) {
+  NEED(path && hdr);
+  return guard([&] { sphx::part_read(path, *hdr, out); });
+}
+
+int sph_part_write(const char* path, const SphPartHeader* hdr, const SphParticlesHost* parts) {
+  NEED(path && hdr && parts);
+  return guard([&] { sphx::part_write(path, *hdr, *parts); });
+}
+
+int sph_part_head_write(const char* path, const SphPartHeader* hdr) {
+  NEED(path && hdr);
+  return guard([&] { sphx::part_head_write(path, *hdr); });
+}
+
+int sph_bi4_rewrite(const char* src, const char* dst) {
+  NEED(src && dst);
+  return guard([&] { sphx::bi4_rewrite(src, dst); });
 }
 
 }  // extern "C"

@@ -439,6 +439,14 @@ void SphGpuSingle::Upload(const SphParticlesHost& h, const std::vector<unsigned>
   verletstep_ = 0;
 }
 
+// Restart: TimeStep and SymplecticDtPre of the loaded PART (JSph::InitRun, JSph.cpp:2094-2106).
+void SphGpuSingle::SetTime(double time, double symdtpre) {
+  Sync();
+  check_hip(hipMemcpy(&sc_->time, &time, sizeof(double), hipMemcpyHostToDevice), "set time");
+  if (symdtpre > 0)
+    check_hip(hipMemcpy(&sc_->symdtpre, &symdtpre, sizeof(double), hipMemcpyHostToDevice), "set SymplecticDtPre");
+}
+
 // ---- timing -----------------------------------------------------------------------
 void SphGpuSingle::SetTiming(bool on) {
   Sync();

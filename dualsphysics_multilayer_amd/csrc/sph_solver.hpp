@@ -30,6 +30,11 @@ void check_hip(hipError_t e, const char* what);
 void derive_constants(const SphCaseDef& c, SphConstants& k);
 // Column bounds of a particle-count-balanced x-slab split (sph_slab_partition).
 void slab_partition(const SphCaseDef& c, const SphParticlesHost& all, int nranks, double bound_weight, int* bounds);
+// PART / case files (sph_bi4.cpp)
+void part_read(const std::string& path, SphPartHeader& h, SphParticlesHost* out);
+void part_write(const std::string& path, const SphPartHeader& h, const SphParticlesHost& p);
+void part_head_write(const std::string& path, const SphPartHeader& h);
+void bi4_rewrite(const std::string& src, const std::string& dst);
 
 // This rank's slab: owned global x-cell columns [c0, c1) of nranks.
 struct SlabConfig {
@@ -64,6 +69,7 @@ class SphGpuSingle {
   void DownloadInteraction(SphInterOut& out);
   void CountPairs(uint64_t out[6]);
   void SetTiming(bool on);
+  void SetTime(double time, double symdtpre);
   void Timing(double out_ms[4], uint64_t* launches);
   void CheckErrors();
 

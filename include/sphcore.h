@@ -36,6 +36,10 @@
  *   sph_slab_* ................. new: slab decomposition across GPUs; the
  *                                reference fork runs one domain per process (JSphGpuSingle)
  *   sph_comm_unique_id ......... RCCL bootstrap id (ncclGetUniqueId) for sph_slab_create
+ *   sph_part_read/write ........ JPartDataBi4::LoadFilePart/LoadFileCase and AddPartInfo +
+ *                                AddPartData + SaveFilePart (JPartDataBi4.cpp:304-440,
+ *                                492-516) over the .bi4 container of JBinaryData
+ *                                (JBinaryData.cpp:700-1160,1467-1545): PART and case files
  */
 #ifndef SPHCORE_H
 #define SPHCORE_H
@@ -210,6 +214,10 @@ int sph_download_interaction(SphSolver* s, SphInterOut* out);
 int sph_count_pairs(SphSolver* s, uint64_t out[6]);
 /* Average device time (ms) of the last timed region's kernels, by phase:
  * out[0]=interaction, [1]=update, [2]=divide, [3]=dt/reductions. */
+/* Restart from a PART (JSph::InitRun with PartBegin, JSph.cpp:2087-2106): simulated
+ * time TimeStep of the loaded PART, and SymplecticDtPre if > 0 (else DtIni stays).
+ * VelrhopM1 = Velrhop and VerletStep = 0 hold from creation, as in the reference. */
+int sph_solver_set_time(SphSolver* s, double time, double symplectic_dtpre);
 int sph_solver_set_timing(SphSolver* s, int enabled);
 int sph_solver_timing(SphSolver* s, double out_ms[4], uint64_t* launches);
 
@@ -247,6 +255,42 @@ int sph_slab_group_create(const SphCaseDef* cdef, const SphParticlesHost* all, i
 int sph_slab_group_destroy(SphSlabGroup* g);
 int sph_slab_group_run(SphSlabGroup* g, uint32_t nsteps);
 int sph_slab_group_member(SphSlabGroup* g, int i, SphSolver** out);
+
+/* ---- PART / case files (.bi4), SURVEY.md §8(f) row 2 ------------------------------
+ * Root values of JPartDataBi4 (case) + the values of its PART_%04u item, in the
+ * reference's own names and types.  Positions are double on this interface; files
+ * store them as Posd (double3, pos_double=1) or Pos (float3). */
+typedef struct SphPartHeader {
+  char app_name[64], case_name[64];
+  uint32_t cpart, npok, nout, step;   /* Cpart, Npok, Nout, Step                          */
+  double timestep, runtime;           /* TimeStep, RunTime                                */
+  double domain_min[3], domain_max[3];/* DomainMin, DomainMax                             */
+  double symplectic_dtpre;            /* SymplecticDtPre (written if > 0; read on restart) */
+  uint64_t np_total;                  /* NpTotal (written if > 0)                         */
+  uint64_t case_np, case_nfixed, case_nmoving, case_nfloat, case_nfluid;
+  double dp, h, b, rhop0, gamma, massbound, massfluid;
+  double map_posmin[3], map_posmax[3], case_posmin[3], case_posmax[3];
+  double peri_xinc[3], peri_yinc[3], peri_zinc[3];
+  double data2d_posy;
+  int32_t data2d, peri_mode, axis_div, np_dynamic, reuse_ids, symmetry, splitting, pos_double;
+  /* run header (Part_Head.ibi4, JPartDataHead) */
+  int32_t visco_type;                 /* ViscoType (1 artificial)                         */
+  float visco, viscoboundfactor;      /* ViscoValue, ViscoBoundFactor                     */
+  float gravity[3];                   /* Gravity                                          */
+  uint32_t mkbound, mkfluid;          /* Mk of the fixed and the fluid block              */
+} SphPartHeader;
+
+/* Read a PART or case file.  With out == NULL (or out->n < Npok) only *hdr is filled;
+ * call again with arrays of hdr->npok entries (code may be NULL). */
+int sph_part_read(const char* path, SphPartHeader* hdr, SphParticlesHost* out);
+/* Write a PART file as the reference's SaveFilePart does (no solver statistics values). */
+int sph_part_write(const char* path, const SphPartHeader* hdr, const SphParticlesHost* parts);
+/* Write the run header Part_Head.ibi4 (JPartDataHead) that the reference's restart
+ * (-partbegin) reads beside the PART files: case values + one Fixed and one Fluid MK block. */
+int sph_part_head_write(const char* path, const SphPartHeader* hdr);
+/* Parse any .bi4 container and write it back (format round trip; byte-identical for
+ * files written by the reference). */
+int sph_bi4_rewrite(const char* src, const char* dst);
 
 #ifdef __cplusplus
 }

@@ -46,9 +46,9 @@ def test_struct_layouts_match_c(tmp_path):
     prog = tmp_path / "sizes.c"
     prog.write_text(
         '#include <stdio.h>\n#include <stddef.h>\n#include "%s"\n'
-        "int main(){printf(\"%%zu %%zu %%zu %%zu %%zu %%zu %%zu %%zu %%zu\\n\",sizeof(SphCaseDef),sizeof(SphConstants),"
+        "int main(){printf(\"%%zu %%zu %%zu %%zu %%zu %%zu %%zu %%zu %%zu %%zu %%zu\\n\",sizeof(SphCaseDef),sizeof(SphConstants),"
         "sizeof(SphRunStats),sizeof(SphParticlesHost),sizeof(SphInterOut),offsetof(SphCaseDef,npb),"
-        "offsetof(SphConstants,dom_cellcode),sizeof(SphSlabDef),offsetof(SphSlabDef,comm_id));return 0;}\n" % HEADER
+        "offsetof(SphConstants,dom_cellcode),sizeof(SphSlabDef),offsetof(SphSlabDef,comm_id),sizeof(SphPartHeader),offsetof(SphPartHeader,pos_double));return 0;}\n" % HEADER
     )
     exe = tmp_path / "sizes"
     subprocess.check_call(["gcc", str(prog), "-o", str(exe)])
@@ -63,6 +63,8 @@ def test_struct_layouts_match_c(tmp_path):
         _abi.SphConstants.dom_cellcode.offset,
         C.sizeof(_abi.SphSlabDef),
         _abi.SphSlabDef.comm_id.offset,
+        C.sizeof(_abi.SphPartHeader),
+        _abi.SphPartHeader.pos_double.offset,
     ]
     assert got == py
 
