@@ -1,0 +1,519 @@
+"""A DualSPHysics case as the reference solver loads it: ``<case>.xml`` + ``<case>.bi4``
+(SURVEY.md §8(f) row 2).
+
+Mirrors what ``JSph`` reads before the first step, restricted to what the hot path of
+this core runs (fixed DBC boundaries + fluid, Wendland, artificial viscosity, DDT 0-3,
+Verlet / Symplectic, no periodicity); anything else raises ``CaseError`` the way the
+reference refuses an invalid configuration, never silently ignored:
+
+* constants  — ``JCaseCtes::ReadXmlRun`` (JCaseCtes.cpp:201-215) via
+  ``JSph::LoadConfigCtes`` (JSph.cpp:567-583);
+* parameters — ``JCaseEParms::ReadXml`` (JCaseEParms.cpp:351-375) and the keys and
+  defaults of ``JSph::LoadConfigParameters`` (JSph.cpp:588-757), including the
+  ``<simulationdomain>`` grammar of ``JCaseEParms::CheckPosValue``
+  (JCaseEParms.cpp:283-320) and the legacy IncZ / DomainFixed* keys;
+* command-line overrides — the subset of ``JSph::LoadConfigCommands``
+  (JSph.cpp:762-870) this core supports (``overrides`` below);
+* particle blocks — ``JCaseParts`` (``<particles>``) and the block codes of
+  ``JSphMk::Config`` (JSphMk.cpp:86-123);
+* particles and map limits — ``JSph::LoadCaseParticles`` (JSph.cpp:2036-2062):
+  ``JPartsLoad4::LoadParticles`` (JPartsLoad4.cpp:151-252) from the case file or, for a
+  restart (``partbegin``), from ``Part_%04u.bi4``; the map is the file's MapPosMin/Max
+  when stored, else ``CalculeLimits`` (JPartsLoad4.cpp:339-347) + ``ResizeMapLimits``
+  (JSph.cpp:1354-1387).
+
+The solver holds boundary particles before fluid ones (``SphCaseDef.npb`` leading
+entries).  Particles are therefore stably partitioned bound-first; the divide's cell
+sort is stable and bound/fluid never share a box, so the sorted order the reference
+builds from the file order is unchanged.
+"""
+from __future__ import annotations
+
+import os
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+from .case import BORDER_MAP, CELLMODE_FULL, CODE_TYPE_FIXED, CODE_TYPE_FLUID
+
+DBL_MAX = float(np.finfo(np.float64).max)
+CODE_TYPE_MOVING, CODE_TYPE_FLOATING = 0x800, 0x1000  # 16-bit typecode, DualSphDef.h:200-205
+
+
+class CaseError(ValueError):
+    """An invalid or unsupported case configuration (the reference's JException)."""
+
+
+# ---- XML helpers (JXml semantics) --------------------------------------------------------
+def _node(root, path: str, optional: bool = False):
+    n = root
+    for part in path.split("."):
+        n = n.find(part) if n is not None else None
+    if n is None and not optional:
+        raise CaseError(f"The item is not found '{path}'.")
+    return n
+
+
+def _attr_double(ele, name: str, what: str) -> float:
+    v = ele.get(name)
+    if v is None:
+        raise CaseError(f"The attribute '{name}' of '{what}' is missing.")
+    try:
+        return float(v)
+    except ValueError:
+        raise CaseError(f"The attribute '{name}' of '{what}' is not a number: {v!r}") from None
+
+
+def _elem_double(node, name: str, optional: bool = False, default: float = 0.0) -> float:
+    e = node.find(name)
+    if e is None:
+        if optional:
+            return default
+        raise CaseError(f"The item is not found '{name}'.")
+    return _attr_double(e, "value", name)
+
+
+def _elem_bool(node, name: str) -> bool:
+    e = node.find(name)
+    if e is None:
+        raise CaseError(f"The item is not found '{name}'.")
+    v = (e.get("value") or "").strip().lower()
+    if v in ("true", "1"):
+        return True
+    if v in ("false", "0"):
+        return False
+    raise CaseError(f"The value of '{name}' is not a valid boolean: {v!r}")
+
+
+# ---- <simulationdomain> (JCaseEParms::CheckPosValue, JCaseEParms.cpp:283-320) ------------
+DC_DEFAULT, DC_FIXED, DC_DEFVALUE, DC_DEFPRC = 0, 1, 2, 3
+
+
+def parse_pos_value(value: str, isposmin: bool) -> tuple[int, float]:
+    """(mode, value) of one posmin/posmax attribute: "default", "default +/- v",
+    "default +/- v%" or a fixed coordinate.  The sign must enlarge the domain."""
+    v = value.replace(" ", "").replace("\t", "").lower()
+    if v == "default":
+        return DC_DEFAULT, 0.0
+    posdef = max(v.find("default+"), v.find("default-"))
+    posprc = v.find("%")
+    err = None
+    if posdef < 0 and posprc >= 0:
+        err = "The use of %"
+    if err is None and posdef > 0:
+        err = "The use of default"
+    if err is None and posprc >= 0 and posprc != len(v) - 1:
+        err = "The use of %"
+    if err is None and posdef == 0 and len(v) <= len("default+"):
+        err = "The use of default"
+    if err is None:
+        if posdef == 0:
+            sign = v[7]
+            prc = posprc >= 0
+            if (isposmin and sign == "+") or (not isposmin and sign == "-"):
+                err = "The sign + " if isposmin else "The sign - "
+                raise CaseError(f"{err}is invalid in {'posmin' if isposmin else 'posmax'}=\"{value}\" "
+                                "to increase the domain.")
+            mode = DC_DEFPRC if prc else DC_DEFVALUE
+            num = v[8:len(v) - (1 if prc else 0)]
+        else:
+            mode, num = DC_FIXED, v
+        try:
+            return mode, float(num)
+        except ValueError:
+            err = "Number"
+    raise CaseError(f"{err} is invalid in {'posmin' if isposmin else 'posmax'}=\"{value}\"")
+
+
+class _Params:
+    """<parameters> as a key -> string map (JCaseEParms)."""
+
+    def __init__(self, node):
+        self.values: dict[str, str] = {}
+        self.posmin = ["default"] * 3
+        self.posmax = ["default"] * 3
+        if node is None:
+            return
+        for e in node.findall("parameter"):
+            key, val = e.get("key"), e.get("value")
+            if key is None or val is None:
+                raise CaseError("A <parameter> needs key and value attributes.")
+            if val.startswith("#") and ":" not in val:
+                raise CaseError(f"Parameter {key}: user expressions ('#...') are not supported.")
+            self.values[key] = val
+        dom = node.find("simulationdomain")
+        if dom is not None:
+            for tag, lst, ismin in (("posmin", self.posmin, True), ("posmax", self.posmax, False)):
+                e = dom.find(tag)
+                for i, ax in enumerate("xyz"):
+                    lst[i] = (e.get(ax) if e is not None else None) or "default"
+                    parse_pos_value(lst[i], ismin)  # validates
+
+    def exists(self, key: str) -> bool:
+        return key in self.values
+
+    def num(self, key: str, optional: bool = False, default: float = 0.0) -> float:
+        if key not in self.values:
+            if optional:
+                return default
+            raise CaseError(f"The parameter '{key}' is missing.")
+        s = self.values[key]
+        try:
+            return float(s)
+        except ValueError:
+            raise CaseError(f"The parameter '{key}' is not a number: {s!r}") from None
+
+    def int(self, key: str, optional: bool = False, default: int = 0) -> int:
+        return int(self.num(key, optional, default))
+
+    def is_pos_default(self) -> bool:
+        return all(parse_pos_value(v, True)[0] == DC_DEFAULT for v in self.posmin) and all(
+            parse_pos_value(v, False)[0] == DC_DEFAULT for v in self.posmax)
+
+
+# ---- domain configuration (JSph.cpp:334-427, 1354-1387) ----------------------------------
+class _DomainCfg:
+    def __init__(self):
+        self.clear()
+
+    def clear(self):
+        self.pmin = [DBL_MAX] * 3   # CfgDomainParticlesMin
+        self.pmax = [DBL_MAX] * 3
+        self.prcmin = [DBL_MAX] * 3  # CfgDomainParticlesPrcMin
+        self.prcmax = [DBL_MAX] * 3
+        self.fmin = [DBL_MAX] * 3   # CfgDomainFixedMin
+        self.fmax = [DBL_MAX] * 3
+
+    def resize(self, rmin, rmax, simulate2d: bool) -> tuple[list, list]:
+        """JSph::ResizeMapLimits without periodicity and symmetry."""
+        if simulate2d:
+            for lst in (self.pmin, self.pmax, self.prcmin, self.prcmax, self.fmin, self.fmax):
+                lst[1] = DBL_MAX
+        dflt = lambda lst, d: [d[i] if lst[i] == DBL_MAX else lst[i] for i in range(3)]  # noqa: E731
+        pmin, pmax = dflt(self.pmin, [0.0] * 3), dflt(self.pmax, [0.0] * 3)
+        prcmin, prcmax = dflt(self.prcmin, [0.0] * 3), dflt(self.prcmax, [0.0] * 3)
+        dif = [rmax[i] - rmin[i] for i in range(3)]
+        dmin = [rmin[i] - dif[i] * prcmin[i] for i in range(3)]
+        dmax = [rmax[i] + dif[i] * prcmax[i] for i in range(3)]
+        dmin = [dmin[i] - pmin[i] for i in range(3)]
+        dmax = [dmax[i] + pmax[i] for i in range(3)]
+        dmin, dmax = dflt(self.fmin, dmin), dflt(self.fmax, dmax)
+        if any(dmin[i] > rmin[i] or dmax[i] < rmax[i] for i in range(3)):
+            raise CaseError(f"Domain limits {dmin}-{dmax} are not valid.")
+        return dmin, dmax
+
+
+def _config_domain(p: _Params) -> _DomainCfg:
+    """Domain part of JSph::LoadConfigParameters (JSph.cpp:732-756)."""
+    d = _DomainCfg()
+    resizeold = False
+    incz = float(np.float32(p.num("IncZ", True, 0.0)))
+    if incz:
+        d.clear()
+        d.prcmax[2] = incz
+        resizeold = True
+    if p.exists("DomainFixed"):
+        vals = [float(x) for x in p.values["DomainFixed"].split(":")]
+        if len(vals) != 6:
+            raise CaseError("DomainFixed needs six values xmin:ymin:zmin:xmax:ymax:zmax.")
+        d.clear()
+        d.fmin, d.fmax = vals[:3], vals[3:]
+        resizeold = True
+    for key in ("DomainFixedXmin", "DomainFixedYmin", "DomainFixedZmin", "DomainFixedXmax",
+                "DomainFixedYmax", "DomainFixedZmax"):
+        if p.exists(key):
+            ax = "xyz".index(key[-4].lower())
+            (d.fmin if key.endswith("min") else d.fmax)[ax] = p.num(key)
+            resizeold = True
+    if not p.is_pos_default() and resizeold:
+        raise CaseError("Combination of <simulationdomain> with IncZ or DomainFixedXXX in <parameters> "
+                        "section of XML is not allowed.")
+    for i in range(3):
+        for ismin, text in ((True, p.posmin[i]), (False, p.posmax[i])):
+            mode, v = parse_pos_value(text, ismin)
+            if mode == DC_FIXED:
+                (d.fmin if ismin else d.fmax)[i] = v
+            elif mode == DC_DEFVALUE:
+                (d.pmin if ismin else d.pmax)[i] = v
+            elif mode == DC_DEFPRC:
+                (d.prcmin if ismin else d.prcmax)[i] = v / 100
+    return d
+
+
+# ---- the case -----------------------------------------------------------------------------
+# command-line overrides (JSphCfgRun -> JSph::LoadConfigCommands) this core takes
+OVERRIDES = ("step_algorithm", "verlet_steps", "tdensity", "ddtvalue", "visco", "viscoboundfactor", "cellmode",
+             "celldomfixed", "cflnumber", "rhopoutmin", "rhopoutmax", "timemax", "timeout", "dtini", "dtmin",
+             "coefdtmin", "domain_fixed")
+
+
+class XmlCase:
+    """``<dir>/<name>.xml`` + ``<dir>/<name>.bi4`` (or, with ``partbegin``, the PART
+    ``<partbegin_dir>/Part_%04u.bi4``).  Exposes what ``SphGpuSingle`` / ``SphGpuSlab``
+    and the PART writer read from a case: ``np, npb, idp, pos, vel, rhop, case_def()``,
+    plus the run parameters (``timemax``, ``timeout``, ``time0``, ``symdtpre0``)."""
+
+    def __init__(self, casepath: str, partbegin: int = 0, partbegin_dir: str | None = None, **overrides):
+        from .core import read_part  # the .bi4 reader of the core library
+
+        bad = set(overrides) - set(OVERRIDES)
+        if bad:
+            raise CaseError(f"unknown overrides {sorted(bad)}")
+        if casepath.endswith(".xml"):
+            casepath = casepath[:-4]
+        self.casepath = casepath
+        self.case_name = os.path.basename(casepath)
+        xmlfile = casepath + ".xml"
+        if not os.path.exists(xmlfile):
+            raise CaseError(f"Case configuration was not found: {xmlfile}")
+        root = ET.parse(xmlfile).getroot()
+        if root.tag != "case":
+            raise CaseError(f"{xmlfile}: the root element is not <case>.")
+        self.app = root.get("app", "unknown")
+        ex = _node(root, "execution")
+        self._load_constants(_node(ex, "constants"))
+        p = _Params(ex.find("parameters"))
+        self._load_parameters(p)
+        self._domain = _config_domain(p)
+        sp = ex.find("special")
+        if sp is not None:
+            for ch in sp:  # accinputs, chrono, wavepaddles, mlayerpistons, inout, gauges, ...
+                raise CaseError(f"<special><{ch.tag}> is not supported by this core.")
+        if ex.find("motion") is not None and len(list(ex.find("motion"))):
+            raise CaseError("<motion> (moving boundaries) is not supported by this core.")
+        self._load_blocks(_node(ex, "particles"))
+        dfix = overrides.pop("domain_fixed", None)
+        if dfix is not None:  # -domain_fixed: JSph::ConfigDomainFixed (JSph.cpp:343-346, 856)
+            self._domain.clear()
+            self._domain.fmin, self._domain.fmax = list(dfix[:3]), list(dfix[3:])
+        for k, v in overrides.items():
+            if k in ("timemax", "timeout") and v < 0 or k == "timemax" and v == 0:
+                continue  # JSph::LoadConfigCommands applies TimeMax>0, TimePart>=0 only
+            setattr(self, k, v)
+        if self.tdensity == 0:
+            self.ddtvalue = 0.0
+        if not self.rhopoutmin < self.rhopoutmax:  # RhopOut disabled (JSph.cpp:862-863)
+            self.rhopoutmin, self.rhopoutmax = -float(np.finfo(np.float32).max), float(np.finfo(np.float32).max)
+        if not self.rhopoutmin <= self.rhop0 <= self.rhopoutmax:
+            raise CaseError(f"The reference density value {self.rhop0} is outside the defined limits "
+                            f"[{self.rhopoutmin},{self.rhopoutmax}].")
+        if self.cellmode != CELLMODE_FULL:
+            raise CaseError("Only CellMode=full runs on the GPU path.")
+        # -- particles (JPartsLoad4::LoadParticles) ------------------------------------
+        self.partbegin = int(partbegin)
+        if self.partbegin:
+            d = partbegin_dir if partbegin_dir is not None else os.path.dirname(casepath)
+            fn = os.path.join(d, "Part_%04u.bi4" % self.partbegin)
+        else:
+            fn = casepath + ".bi4"
+        if not os.path.exists(fn):
+            raise CaseError(f"File of the particles was not found: {fn}")
+        h, prt = read_part(fn)
+        self.file_header = h
+        self._check_loaded(h, prt)
+        self.time0 = float(h["timestep"]) if self.partbegin else 0.0
+        self.symdtpre0 = float(h.get("symplectic_dtpre", 0.0)) if self.partbegin else 0.0
+        # bound (fixed) blocks first, stable: the solver's npb leading entries
+        isb = prt["idp"] < np.uint32(self.case_nbound)
+        order = np.concatenate([np.flatnonzero(isb), np.flatnonzero(~isb)])
+        self.idp = np.ascontiguousarray(prt["idp"][order], np.uint32)
+        self.pos = np.ascontiguousarray(prt["pos"][order], np.float64)
+        self.vel = np.ascontiguousarray(prt["vel"][order], np.float32)
+        self.rhop = np.ascontiguousarray(prt["rhop"][order], np.float32)
+        self.np = int(self.idp.size)
+        self.npb = int(isb.sum())
+        if self.npb != self.case_nfixed:
+            raise CaseError(f"{fn}: {self.npb} boundary particles loaded, the case has {self.case_nfixed}.")
+        # case limits (JPartsLoad4 CasePosMin/Max; computed when the file has none)
+        cmin, cmax = list(h["case_posmin"]), list(h["case_posmax"])
+        if cmin == cmax:
+            cmin, cmax = self.pos.min(axis=0).tolist(), self.pos.max(axis=0).tolist()
+        self.case_posmin, self.case_posmax = cmin, cmax
+        if list(h["map_posmin"]) != list(h["map_posmax"]):
+            self._map = (np.array(h["map_posmin"]), np.array(h["map_posmax"]))
+        else:
+            border = float(np.float32(self.h)) * BORDER_MAP
+            rmin = [c - border for c in cmin]
+            rmax = [c + border for c in cmax]
+            dmin, dmax = self._domain.resize(rmin, rmax, self.data2d)
+            self._map = (np.array(dmin), np.array(dmax))
+        # JSph::CheckRhopLimits (JSph.cpp:2021-2030) is done by the core at creation.
+
+    # -- JSph::LoadConfigCtes ---------------------------------------------------------------
+    def _load_constants(self, c):
+        self.data2d = _elem_bool(c, "data2d")
+        if self.data2d:
+            raise CaseError("2-D simulations (data2d) are not supported by this core.")
+        g = c.find("gravity")
+        if g is None:
+            raise CaseError("The item is not found 'gravity'.")
+        self.gravity = tuple(_attr_double(g, a, "gravity") for a in "xyz")
+        self.cflnumber = _elem_double(c, "cflnumber")
+        self.gamma = _elem_double(c, "gamma")
+        self.rhop0 = _elem_double(c, "rhop0")
+        self.dp = _elem_double(c, "dp")
+        self.h = _elem_double(c, "h")
+        self.cteb = _elem_double(c, "b")
+        self.massbound = _elem_double(c, "massbound")
+        self.massfluid = _elem_double(c, "massfluid")
+
+    # -- JSph::LoadConfigParameters (the keys this core acts on; others refused) -----------
+    def _load_parameters(self, p: _Params):
+        kern = p.int("Kernel", True, 2)
+        if kern not in (1, 2):
+            raise CaseError("Kernel choice is not valid.")
+        if kern != 2:
+            raise CaseError("Only the Wendland kernel (Kernel=2) runs on the GPU path.")
+        rig = p.int("RigidAlgorithm", True, 1)
+        if rig not in (0, 1, 2, 3):
+            raise CaseError("Rigid algorithm is not valid.")
+        self.step_algorithm = p.int("StepAlgorithm", True, 1)
+        if self.step_algorithm not in (1, 2):
+            raise CaseError("Step algorithm is not valid.")
+        self.verlet_steps = p.int("VerletSteps", True, 40)
+        tv = p.int("ViscoTreatment", True, 1)
+        if tv not in (1, 2):
+            raise CaseError("Viscosity treatment is not valid.")
+        if tv != 1:
+            raise CaseError("Only artificial viscosity (ViscoTreatment=1) is supported by this core.")
+        self.visco = p.num("Visco")
+        self.viscoboundfactor = p.num("ViscoBoundFactor", True, 1.0)
+        if p.values.get("ViscoTime"):
+            raise CaseError("ViscoTime is not supported by this core.")
+        bc = p.int("Boundary", True, 1)
+        if bc not in (1, 2):
+            raise CaseError("Boundary Condition method is not valid.")
+        if bc != 1:
+            raise CaseError("Only DBC boundaries (Boundary=1) are supported by this core.")
+        if p.exists("DeltaSPH"):
+            if p.exists("DensityDT"):
+                raise CaseError("The parameters 'DeltaSPH' and 'DensityDT' cannot be combined.")
+            v = p.num("DeltaSPH")
+            self.tdensity, self.ddtvalue = (1, v) if v > 0 else (0, 0.1)
+        else:
+            self.tdensity = p.int("DensityDT", True, 0)
+            if self.tdensity not in (0, 1, 2, 3):
+                raise CaseError("Density Diffusion Term mode is not valid.")
+            self.ddtvalue = p.num("DensityDTvalue", True, 0.1)
+        if p.exists("Shifting"):
+            sm = p.int("Shifting", True, 0)
+            if sm not in (0, 1, 2, 3):
+                raise CaseError("Shifting mode in <execution><parameters> is not valid.")
+            if sm != 0 and p.num("ShiftCoef", True, -2) != 0:
+                raise CaseError("Shifting is not supported by this core.")
+        self.timemax = p.num("TimeMax")
+        self.timeout = p.num("TimeOut")
+        self.dtini = max(0.0, p.num("DtIni", True, 0.0))
+        self.dtmin = max(0.0, p.num("DtMin", True, 0.0))
+        self.coefdtmin = p.num("CoefDtMin", True, 0.05)
+        if p.int("DtAllParticles", True, 0) == 1:
+            raise CaseError("DtAllParticles is not supported by this core.")
+        if p.num("DtFixed", True, 0.0) > 0 or p.values.get("DtFixedFile", "none").lower() not in ("", "none"):
+            raise CaseError("DtFixed / DtFixedFile are not supported by this core.")
+        self.rhopoutmin = p.num("RhopOutMin") if p.exists("RhopOutMin") else 700.0
+        self.rhopoutmax = p.num("RhopOutMax") if p.exists("RhopOutMax") else 1300.0
+        self.partsoutmax = p.num("PartsOutMax", True, 1.0)
+        if p.int("Symmetry", True, 0):
+            raise CaseError("Symmetry is not supported by this core.")
+        for k in ("XPeriodicIncY", "XPeriodicIncZ", "YPeriodicIncX", "YPeriodicIncZ", "ZPeriodicIncX",
+                  "ZPeriodicIncY", "XYPeriodic", "XZPeriodic", "YZPeriodic"):
+            if p.exists(k):
+                raise CaseError("Periodic boundaries are not supported by this core.")
+        self.cellmode = CELLMODE_FULL   # JSphCfgRun default for the GPU (-cellmode:full)
+        self.celldomfixed = False
+
+    # -- JCaseParts + JSphMk::Config ---------------------------------------------------------
+    def _load_blocks(self, node):
+        self.mkboundfirst = int(node.get("mkboundfirst", 11))
+        self.mkfluidfirst = int(node.get("mkfluidfirst", 1))
+        blocks = []
+        for e in node:
+            if e.tag not in ("fixed", "moving", "floating", "fluid"):
+                raise CaseError(f"<particles>: unknown block <{e.tag}>.")
+            blocks.append(dict(type=e.tag, mk=int(e.get("mk")), begin=int(e.get("begin")),
+                               count=int(e.get("count")),
+                               mktype=int(e.get("mkfluid") if e.tag == "fluid" else e.get("mkbound"))))
+        if any(b["type"] in ("moving", "floating") for b in blocks):
+            raise CaseError("Moving / floating particle blocks are not supported by this core.")
+        nfix = [b for b in blocks if b["type"] == "fixed"]
+        nfl = [b for b in blocks if b["type"] == "fluid"]
+        if [b["type"] for b in blocks] != ["fixed"] * len(nfix) + ["fluid"] * len(nfl):
+            raise CaseError("<particles>: fixed blocks must precede fluid blocks.")
+        begin = 0
+        for b in blocks:
+            if b["begin"] != begin:
+                raise CaseError("<particles>: blocks must be contiguous in idp.")
+            begin += b["count"]
+        # JSphMk::Config codes: the block index within its type
+        for i, b in enumerate(nfix):
+            b["code"] = CODE_TYPE_FIXED | i
+        for i, b in enumerate(nfl):
+            b["code"] = CODE_TYPE_FLUID | i
+        self.blocks = blocks
+        self.case_np = begin
+        self.case_nfixed = sum(b["count"] for b in nfix)
+        self.case_nbound = self.case_nfixed
+        self.case_nfluid = sum(b["count"] for b in nfl)
+
+    def _check_loaded(self, h, prt):
+        """JPartsLoad4::CheckConfig (JPartsLoad4.cpp:264-300)."""
+        if (h["case_np"], h["case_nfixed"], h["case_nmoving"], h["case_nfloat"], h["case_nfluid"]) != (
+                self.case_np, self.case_nfixed, 0, 0, self.case_nfluid):
+            raise CaseError("Data file does not match the configuration of the case.")
+        if bool(h["data2d"]) != self.data2d:
+            raise CaseError("Data file does not match the dimension of the case.")
+        if h["peri_mode"] not in (0, 96):  # PERI_None, PERI_Unknown (case files)
+            raise CaseError("Data file uses periodic boundaries.")
+
+    # -- what the core and the PART writer read -----------------------------------------
+    @property
+    def nf(self) -> int:
+        return self.np - self.npb
+
+    @property
+    def code(self) -> np.ndarray:
+        c = np.empty(self.np, np.uint16)
+        for b in self.blocks:
+            sel = (self.idp >= b["begin"]) & (self.idp < b["begin"] + b["count"])
+            c[sel] = b["code"]
+        return c
+
+    @property
+    def mass(self) -> float:
+        return self.massfluid
+
+    def map_limits(self) -> tuple[np.ndarray, np.ndarray]:
+        return self._map
+
+    def dt_cap(self) -> float:
+        """Upper bound of every dt the core can compute (JSphGpu::DtVariable:
+        dt = CFL*min(sqrt(h/AceMax), h/(max(Cs0,10*VelMax) + h*ViscDtMax)) <= CFL*h/Cs0,
+        floored at DtMin), used by the run driver to batch steps between outputs."""
+        k = self._derived()
+        return max(k["cflnumber"] * k["kernelh"] / k["cs0"], k["dtmin"]) * (1 + 1e-9)
+
+    def _derived(self) -> dict:
+        from .core import case_derive
+
+        if getattr(self, "_k", None) is None:
+            self._k = case_derive(self.case_def())
+        return self._k
+
+    def case_def(self) -> dict:
+        """Fields of the C ``SphCaseDef`` (include/sphcore.h)."""
+        pmin, pmax = self.map_limits()
+        return dict(
+            dp=self.dp, h=self.h, cteb=self.cteb, rhop0=self.rhop0, gamma=self.gamma,
+            massbound=self.massbound, massfluid=self.massfluid, gravity=tuple(self.gravity),
+            cflnumber=self.cflnumber, step_algorithm=self.step_algorithm, verlet_steps=self.verlet_steps,
+            kernel=2, tdensity=self.tdensity, visco=self.visco, viscoboundfactor=self.viscoboundfactor,
+            ddtvalue=self.ddtvalue, coefdtmin=self.coefdtmin, dtini=self.dtini, dtmin=self.dtmin,
+            rhopoutmin=self.rhopoutmin, rhopoutmax=self.rhopoutmax,
+            map_realposmin=tuple(float(v) for v in pmin), map_realposmax=tuple(float(v) for v in pmax),
+            cellmode=self.cellmode, celldomfixed=int(self.celldomfixed), npb=self.npb, np=self.np,
+        )
+
+
+def load_case(casepath: str, partbegin: int = 0, partbegin_dir: str | None = None, **overrides) -> XmlCase:
+    return XmlCase(casepath, partbegin, partbegin_dir, **overrides)
+
