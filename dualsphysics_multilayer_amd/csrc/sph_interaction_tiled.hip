@@ -31,11 +31,30 @@ namespace sphx {
 #endif
 constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
 #ifndef SPH_TCAP
-#define SPH_TCAP 416
+#define SPH_TCAP 504
 #endif
-// staged neighbour records per segment.  416 puts the block at 18.7 KB of LDS -> 8
-// blocks = 4 waves per SIMD, measured best (1.022 ms at 1M vs 1.056 at 5 waves/SIMD
-// and 1.27 at 2.5 waves/SIMD).
+#ifndef SPH_PAD
+#define SPH_PAD 8
+#endif
+#ifndef SPH_WAVES
+#define SPH_WAVES 0  // >0: register budget of the fluid kernel for that many waves per SIMD (512/n VGPRs)
+#endif
+#if SPH_WAVES
+#define SPH_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SPH_WAVES, SPH_WAVES)))
+#else
+#define SPH_WAVES_ATTR
+#endif
+#ifndef SPH_PACKED
+// 1: the two pairs of a drain iteration as one packed-f32 body (v_pk_fma/mul/add_f32).
+// Measured slower (1M: 0.935 ms at 128 VGPRs / 4 waves vs 0.842 ms scalar; 0.99 ms at
+// 135 VGPRs): one packed stream halves the independent instructions that hide the
+// dependent-issue latency of the body.  Kept as a build option for the record.
+#define SPH_PACKED 0
+#endif
+// staged neighbour records per segment.  504 (+8 over-read pad) puts the block at
+// 20.3 KB of LDS, the most that keeps 8 blocks = 4 waves per SIMD.  Measured at 1M:
+// 0.806 ms vs 0.838 at 416 (a mirrored row pair fits one segment for 94% of the units
+// instead of 81%); 0.936 at 580 (7 blocks/CU), 1.02 at 672 (6 blocks/CU).
 constexpr int TCAP = SPH_TCAP;
 constexpr int TMAXCELLS = 4;   // max x-cells per item
 
@@ -272,6 +291,97 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
   }
 }
 
+// Two pairs per lane as the low/high halves of packed f32 values: gfx950 issues
+// v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 (two f32 operations) at the cost of one
+// scalar VALU op, so the arithmetic of the pair body runs at half the issue count; only
+// the transcendentals (sqrt, rcp), the compares and the selects stay per pair.  The
+// accumulators are packed too (pairs 1, 3, 5, ... in .x, 2, 4, 6, ... in .y) and added
+// once per particle — a fixed summation order, so runs stay bitwise reproducible.
+typedef float f2 __attribute__((ext_vector_type(2)));
+struct TAcc2 {
+  f2 ax, ay, az, ar, delta;
+  float visc;
+};
+__device__ __forceinline__ f2 pk(float a, float b) { return f2{a, b}; }
+
+template <int TDENSITY, int MODE>
+__device__ __forceinline__ void pair_body2(const KConst& K, const P1& p, const float4& A1, const float4& A2,
+                                           const float4& B1, const float4& B2, const float2& C1, const float2& C2,
+                                           bool two, const PassK& Q, TAcc2& a) {
+  const f2 drx = p.x - pk(A1.x, A2.x), dry = p.y - pk(A1.y, A2.y), drz = p.z - pk(A1.z, A2.z);
+  const f2 rr2 = drx * drx + dry * dry + drz * drz;
+  const bool ok1 = rr2.x <= K.kernelsize2 && rr2.x >= ALMOSTZERO;
+  const bool ok2 = two && rr2.y <= K.kernelsize2 && rr2.y >= ALMOSTZERO;
+  const f2 wq = K.mhalfovh * pk(fsqrt_(rr2.x), fsqrt_(rr2.y)) + 1.f;
+  f2 w3 = wq * wq * wq;
+  w3 = pk(ok1 ? w3.x : 0.f, ok2 ? w3.y : 0.f);
+  const f2 dvx = p.vr.x - pk(B1.x, B2.x), dvy = p.vr.y - pk(B1.y, B2.y), dvz = p.vr.z - pk(B1.z, B2.z);
+  const f2 dot = drx * dvx + dry * dvy + drz * dvz;
+  const f2 re = rr2 + K.eta2;
+  f2 inv_re, inv_rs;
+  if (MODE == 2) {
+    inv_re = pk(frcp(re.x), frcp(re.y));
+  } else {
+    const f2 rs = p.vr.w + pk(B1.w, B2.w);  // 2*robar
+    const f2 t = re * rs;
+    const f2 rr = pk(frcp(t.x), frcp(t.y));
+    inv_re = rr * rs;
+    inv_rs = rr * re;
+  }
+  f2 dot_rr2 = dot * inv_re;
+  dot_rr2 = pk(ok1 ? dot_rr2.x : 0.f, ok2 ? dot_rr2.y : 0.f);
+  a.visc = fmaxf(fmaxf(dot_rr2.x, dot_rr2.y), a.visc);
+  const f2 cy = pk(C1.y, C2.y);
+  const f2 wdr = w3 * dot * cy;  // w3*(dr.dv)/rho2
+  a.ar = wdr * Q.ar1 + a.ar;
+  if (MODE == 2) return;
+  const f2 S = cy * p.prr + p.inv_rho * pk(C1.x, C2.x);  // (p1+p2)/(rho1*rho2)
+  f2 pv = Q.cv * dot_rr2 * inv_rs;
+  pv = pk(dot.x < 0.f ? pv.x : 0.f, dot.y < 0.f ? pv.y : 0.f);
+  const f2 c = -w3 * (Q.bm * S + pv);
+  a.ax = c * drx + a.ax;
+  a.ay = c * dry + a.ay;
+  a.az = c * drz + a.az;
+  if (MODE == 1) {
+    if (TDENSITY == 1 || TDENSITY == 2) {  // DBC: no DDT next to the boundary
+      if (ok1) a.delta.x = FLT_MAX;
+      if (ok2) a.delta.y = FLT_MAX;
+    }
+    return;
+  }
+  if (TDENSITY == 1) {
+    const f2 t = w3 * rr2 * inv_re;
+    a.delta = (Q.kd * t) * (p.vr.w * cy - 1.f) + a.delta;
+  } else if (TDENSITY == 2 || TDENSITY == 3) {
+    f2 drhop;
+    if (K.ddtseries) {  // kernel-uniform (scalar) branch
+      drhop = drz * (drz * (drz * (drz * K.ddte4 + K.ddte3) + K.ddte2) + K.ddte1);
+    } else {
+      const f2 l = 1.f + K.ddtgz * drz;
+      drhop = pk(fexp2(K.ovgamma * flog2(l.x)), fexp2(K.ovgamma * flog2(l.y))) * K.rhopzero - K.rhopzero;
+    }
+    const f2 t = w3 * rr2 * inv_re * cy;
+    a.delta = (-Q.kd * t) * (pk(B1.w, B2.w) - (p.vr.w + drhop)) + a.delta;
+  }
+}
+
+__device__ __forceinline__ TAcc unpack(const TAcc2& a) {
+  TAcc r;
+  r.ax = a.ax.x + a.ax.y;
+  r.ay = a.ay.x + a.ay.y;
+  r.az = a.az.x + a.az.y;
+  r.ar = a.ar.x + a.ar.y;
+  r.delta = (a.delta.x == FLT_MAX || a.delta.y == FLT_MAX) ? FLT_MAX : a.delta.x + a.delta.y;
+  r.visc = a.visc;
+  return r;
+}
+
+#if SPH_PACKED
+typedef TAcc2 UAcc;
+#else
+typedef TAcc UAcc;
+#endif
+
 // Candidate test of one window: n (<= 128) staged records from sA+s0 with the expanded
 // form |p-A|^2 = |p|^2 + |A|^2 - 2 p.A (3 FMAs + 1 compare per candidate on one
 // ds_read_b128) against a threshold inflated by 1e-4 (the expanded form rounds to ~1e-6
@@ -313,7 +423,7 @@ __device__ __forceinline__ void test128(const float4* __restrict__ sA, int s0, i
 template <int TDENSITY, int MODE>
 __device__ __forceinline__ void tile_unit(const KConst& K, const P1& p, float thr, int wa0, int wa1, int wb0, int wb1,
                                           const float4* __restrict__ sA, const float4* __restrict__ sB,
-                                          const float2* __restrict__ sC, const PassK& Q, TAcc& a) {
+                                          const float2* __restrict__ sC, const PassK& Q, UAcc& a) {
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
 #if SPH_ABLATE == 2
   a.visc += float(wa1 - wa0 + wb1 - wb0);
@@ -373,14 +483,20 @@ __device__ __forceinline__ void tile_unit(const KConst& K, const P1& p, float th
       const float4 A1 = sA[j1], A2 = sA[j2];
       const float4 B1 = sB[j1], B2 = sB[j2];
       const float2 C1 = sC[j1], C2 = sC[j2];
+#if SPH_PACKED
+      pair_body2<TDENSITY, MODE>(K, p, A1, A2, B1, B2, C1, C2, two, Q, a);
+      continue;
+#endif
       const float drx1 = p.x - A1.x, dry1 = p.y - A1.y, drz1 = p.z - A1.z;
       const float drx2 = p.x - A2.x, dry2 = p.y - A2.y, drz2 = p.z - A2.z;
       const float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
       const float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
       const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
       const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
+#if !SPH_PACKED
       pair_body<TDENSITY, MODE>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, Q, a);
       pair_body<TDENSITY, MODE>(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, Q, a);
+#endif
     }
   }
 }
@@ -406,14 +522,97 @@ __device__ __forceinline__ void stage_row(const KConst& K, unsigned rs, unsigned
   }
 }
 
+// Item geometry shared by the passes of one p1.
+struct RowCtx {
+  int cy, cz;     // the item's cell row
+  int xa, xb;     // x-cell range staged for the item
+  int lxa, lxb;   // this lane's own 3-cell x range
+  int xo;         // x origin of item-relative positions
+  bool act;       // lane holds a p1
+};
+
+// Per-pass constants of the pair body for p2 of mass m2 (the Wendland bwen/h folded in).
+__device__ __forceinline__ PassK pass_k(const KConst& K, float cvisc, float m2, float rho1) {
+  PassK q;
+  q.bm = K.bwenovh * m2;
+  q.ar1 = q.bm * rho1;
+  q.cv = 2.f * K.bwenovh * cvisc;
+  q.kd = K.ddtkhcs * q.bm;
+  return q;
+}
+
+// One interaction pass of the item's p1 over the 3x3 neighbour rows of one particle
+// kind: MODE 0/2 the fluid rows (fluid / bound p1), MODE 1 the bound rows (fluid p1).
+// Drain units: point-mirrored row pairs, then the item's own row; a pair of rows is
+// staged as one segment [row a][row b] when it fits TCAP, else row by row in segments.
+template <int TDENSITY, int MODE>
+__device__ __forceinline__ TAcc run_pass(const KConst& K, const DivGrid& g, const RowCtx& rc, const P1& p, float thr,
+                                         const PassK Q, const unsigned* __restrict__ bc,
+                                         const float4* __restrict__ poscell, const float4* __restrict__ velrhop,
+                                         const float* __restrict__ press, float4* __restrict__ sA,
+                                         float4* __restrict__ sB, float2* __restrict__ sC) {
+  UAcc acc = {};
+  const unsigned cellinit = (MODE == 1 ? 0u : g.boxfluid);
+  for (int u = 0; u < 5; u++) {
+    const int dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
+    const int dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
+    const bool paired = u < 4;
+    // rows (dya, dza) and (-dya, -dza); an out-of-grid row is empty
+    unsigned rs[2] = {0, 0}, re[2] = {0, 0}, ls[2] = {0, 0}, le[2] = {0, 0};
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      if (k == 1 && !paired) break;
+      const int dz = k ? -dza : dza, dy = k ? -dya : dya;
+      const int z = rc.cz + dz, y = rc.cy + dy;
+      if (z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;
+      const unsigned rowbase = cellinit + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+      rs[k] = bc[rowbase + rc.xa];
+      re[k] = bc[rowbase + rc.xb + 1];
+      ls[k] = bc[rowbase + rc.lxa];
+      le[k] = bc[rowbase + rc.lxb + 1];
+    }
+    const unsigned n0 = re[0] - rs[0], n1 = re[1] - rs[1];
+    if (n0 + n1 == 0u) continue;
+    if (n0 + n1 <= unsigned(TCAP)) {
+      // both rows in one segment: [row a][row b]
+      __syncthreads();
+      if (n0) stage_row(K, rs[0], re[0], 0u, rc.xo, dya, dza, poscell, velrhop, press, sA, sB, sC);
+      if (n1) stage_row(K, rs[1], re[1], n0, rc.xo, -dya, -dza, poscell, velrhop, press, sA, sB, sC);
+      __syncthreads();
+      const int wa0 = int(ls[0] - rs[0]), wa1 = rc.act && n0 ? int(le[0] - rs[0]) : wa0;
+      const int wb0 = int(n0 + ls[1] - rs[1]), wb1 = rc.act && n1 ? int(n0 + le[1] - rs[1]) : wb0;
+      tile_unit<TDENSITY, MODE>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, Q, acc);
+    } else {
+      // too long for one segment: each row on its own, in TCAP segments
+      for (int k = 0; k < 2; k++) {
+        const int dz = k ? -dza : dza, dy = k ? -dya : dya;
+        for (unsigned seg = rs[k]; seg < re[k]; seg += TCAP) {
+          const unsigned segn = min(unsigned(TCAP), re[k] - seg);
+          __syncthreads();
+          stage_row(K, seg, seg + segn, 0u, rc.xo, dy, dz, poscell, velrhop, press, sA, sB, sC);
+          __syncthreads();
+          const int w0 = int(max(ls[k], seg) - seg);
+          const int w1 = rc.act ? max(w0, int(min(le[k], seg + segn)) - int(seg)) : w0;
+          tile_unit<TDENSITY, MODE>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, Q, acc);
+        }
+      }
+    }
+  }
+#if SPH_PACKED
+  return unpack(acc);
+#else
+  return acc;
+#endif
+}
+
 template <int TDENSITY>
-__global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
+__global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
                                                     unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
                                                     const float4* __restrict__ velrhop,
                                                     const float* __restrict__ press,
                                                     const unsigned* __restrict__ bc, DivGrid g, KConst K,
                                                     float4* __restrict__ arace) {
-  __shared__ float4 sA[TCAP + 128];  // +128: over-read pad of the 8-wide candidate test
+  __shared__ float4 sA[TCAP + SPH_PAD];  // over-read pad of the 8-wide candidate test (<= 7 records)
   __shared__ float4 sB[TCAP];
   __shared__ float2 sC[TCAP];  // press/rho, 1/rho
   __shared__ unsigned s_item;
@@ -473,78 +672,20 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
         }
         p.inv_rho = frcp(p.vr.w);
         p.prr *= p.inv_rho;
-        // pass constants: fluid p2 (pass 0 / bound p1) and bound p2 (pass 1)
-        PassK qf, qb;
-        qf.bm = K.bwenovh * K.massfluid;
-        qf.ar1 = qf.bm * p.vr.w;
-        qf.cv = 2.f * K.bwenovh * cvisc_f;
-        qf.kd = K.ddtkhcs * qf.bm;
-        qb.bm = K.bwenovh * K.massbound;
-        qb.ar1 = qb.bm * p.vr.w;
-        qb.cv = 2.f * K.bwenovh * cvisc_b;
-        qb.kd = K.ddtkhcs * qb.bm;
         const int lxa = max(cx1 - 1, 0), lxb = min(cx1 + 1, g.ncx - 1);
         const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
-        TAcc f = {0, 0, 0, 0, 0, 0}, bnd = {0, 0, 0, 0, 0, 0};
-        const int npass = bitem ? 1 : 2;
-        for (int pass = 0; pass < npass; pass++) {
-          const unsigned cellinit = (pass == 0 ? g.boxfluid : 0u);
-          // drain units: point-mirrored row pairs, then the item's own row
-          for (int u = 0; u < 5; u++) {
-            const int dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
-            const int dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
-            const bool paired = u < 4;
-            // rows (dya, dza) and (-dya, -dza); an out-of-grid row is empty
-            unsigned rs[2] = {0, 0}, re[2] = {0, 0}, ls[2] = {0, 0}, le[2] = {0, 0};
-#pragma unroll
-            for (int k = 0; k < 2; k++) {
-              if (k == 1 && !paired) break;
-              const int dz = k ? -dza : dza, dy = k ? -dya : dya;
-              const int z = cz + dz, y = cy + dy;
-              if (z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;
-              const unsigned rowbase = cellinit + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
-              rs[k] = bc[rowbase + xa];
-              re[k] = bc[rowbase + xb + 1];
-              ls[k] = bc[rowbase + lxa];
-              le[k] = bc[rowbase + lxb + 1];
-            }
-            const unsigned n0 = re[0] - rs[0], n1 = re[1] - rs[1];
-            if (n0 + n1 == 0u) continue;
-            if (n0 + n1 <= unsigned(TCAP)) {
-              // both rows in one segment: [row a][row b]
-              __syncthreads();
-              if (n0) stage_row(K, rs[0], re[0], 0u, xo, dya, dza, poscell, velrhop, press, sA, sB, sC);
-              if (n1) stage_row(K, rs[1], re[1], n0, xo, -dya, -dza, poscell, velrhop, press, sA, sB, sC);
-              __syncthreads();
-              const int wa0 = int(ls[0] - rs[0]), wa1 = act && n0 ? int(le[0] - rs[0]) : wa0;
-              const int wb0 = int(n0 + ls[1] - rs[1]), wb1 = act && n1 ? int(n0 + le[1] - rs[1]) : wb0;
-              if (bitem)
-                tile_unit<TDENSITY, 2>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, qf, f);
-              else if (pass == 0)
-                tile_unit<TDENSITY, 0>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, qf, f);
-              else
-                tile_unit<TDENSITY, 1>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, qb, bnd);
-            } else {
-              // too long for one segment: each row on its own, in TCAP segments
-              for (int k = 0; k < 2; k++) {
-                const int dz = k ? -dza : dza, dy = k ? -dya : dya;
-                for (unsigned seg = rs[k]; seg < re[k]; seg += TCAP) {
-                  const unsigned segn = min(unsigned(TCAP), re[k] - seg);
-                  __syncthreads();
-                  stage_row(K, seg, seg + segn, 0u, xo, dy, dz, poscell, velrhop, press, sA, sB, sC);
-                  __syncthreads();
-                  const int w0 = int(max(ls[k], seg) - seg);
-                  const int w1 = act ? max(w0, int(min(le[k], seg + segn)) - int(seg)) : w0;
-                  if (bitem)
-                    tile_unit<TDENSITY, 2>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, qf, f);
-                  else if (pass == 0)
-                    tile_unit<TDENSITY, 0>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, qf, f);
-                  else
-                    tile_unit<TDENSITY, 1>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, qb, bnd);
-                }
-              }
-            }
-          }
+        const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act};
+        // pass 0: fluid p2 (fluid p1: momentum/continuity/DDT; bound p1: continuity),
+        // pass 1: bound p2 of fluid p1.  Each pass holds only its own accumulator.
+        TAcc f, bnd = {0, 0, 0, 0, 0, 0};
+        if (bitem) {
+          f = run_pass<TDENSITY, 2>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell, velrhop,
+                                    press, sA, sB, sC);
+        } else {
+          f = run_pass<TDENSITY, 0>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell, velrhop,
+                                    press, sA, sB, sC);
+          bnd = run_pass<TDENSITY, 1>(K, g, rc, p, thr, pass_k(K, cvisc_b, K.massbound, p.vr.w), bc, poscell,
+                                      velrhop, press, sA, sB, sC);
         }
         if (act && bitem) {
           // InteractionForcesBound store (JSphCpu.cpp:617-621) onto the reset ar = 0.
