@@ -3,8 +3,9 @@
 // Same semantics as k_interaction (sph_interaction.hip; reference JSphCpu.cpp:631-822 /
 // JSphGpu_ker.cu:512-745) for fluid p1, restructured for the MI355X:
 //
-//  * Work items: runs of <= TB consecutive fluid particles inside ONE (y,z) row of
-//    cells, spanning <= TMAXCELLS x-cells [a,b] (built per divide by k_items_*).  All
+//  * Work items: runs of TB consecutive fluid particles inside ONE (y,z) row of cells
+//    (fewer at a row end), spanning <= TMAXCELLS x-cells [a,b], free to start and end
+//    inside a cell (built per divide by k_items_*).  All
 //    p1 of an item share their 3x3 neighbour rows, and each neighbour row is ONE
 //    contiguous particle range (cells are x-fastest), so a block stages each of the
 //    9 fluid + 9 bound row ranges once into LDS (coalesced 16-B loads) and every lane
@@ -65,19 +66,21 @@ __device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x
 
 // ------------------------------------------------------------------------------------
 // Item list (per divide).  Rows [0,nrows) are fluid rows (fluid p1), rows
-// [nrows,2*nrows) bound rows (bound p1, DBC).  One wave per row loads the row's cell
-// counts into LDS (coalesced) with their prefix sums, then lane 0 splits the row
-// greedily into items reading LDS only; the count and write passes run the same
-// greedy, so the list is deterministic and in spatial (z, y, x) order, fluid items first.
+// [nrows,2*nrows) bound rows (bound p1, DBC).  An item is a run of TB consecutive
+// particles of one row (the row's last item shorter), cut earlier only where it would
+// span more than TMAXCELLS x-cells; items may start and end inside a cell.  Full items
+// keep both waves of a block busy (cell-aligned items averaged 103 of 128 lanes at 1M)
+// and make the lanes' candidate counts more alike.  One wave per row copies the row's
+// cell begin offsets to LDS, then lane 0 walks the items; the count and write passes
+// run the same walk, so the list is deterministic and in spatial (z, y, x) order, fluid
+// items first.
 constexpr int ROWCELLS_LDS = 1024;
 constexpr unsigned ITEM_BOUND = 0x80000000u;  // flag in item.x: p1 are boundary particles
 
 template <bool WRITE>
 __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ bc, DivGrid g,
                                                    unsigned* __restrict__ counts, uint4* __restrict__ items) {
-  __shared__ unsigned cnt[ROWCELLS_LDS];
-  __shared__ unsigned pre[ROWCELLS_LDS + 1];
-  __shared__ unsigned short iend[ROWCELLS_LDS];     // end (exclusive) of a greedy item starting at x
+  __shared__ unsigned pre[ROWCELLS_LDS + 1];            // begin offset of every cell of the row, + row end
   __shared__ unsigned short nzfrom[ROWCELLS_LDS + 1];  // first non-empty owned cell >= x (xend if none)
   const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
   const unsigned r = blockIdx.x;
@@ -90,64 +93,39 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
   const int xbeg = g.xown0, xend = g.xown1;
   uint4* out = WRITE ? items + counts[r] : nullptr;
   unsigned nitems = 0;
-  if (ncx > ROWCELLS_LDS) {  // very long rows: the plain serial greedy on global memory
+  auto emit = [&](int a, int e, unsigned p, unsigned q) {
+    if (WRITE)
+      out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(e) << 16), p, q);
+    nitems++;
+  };
+  if (ncx > ROWCELLS_LDS) {  // very long rows: the same walk on global memory, cell by cell
     if (threadIdx.x != 0) return;
-    auto count = [&](int x) { return bc[rowbase + x + 1] - bc[rowbase + x]; };
-    int x = xbeg;
-    while (x < xend) {
-      while (x < xend && count(x) == 0) x++;
-      if (x >= xend) break;
-      const int a = x;
-      unsigned n = count(x);
-      x++;
-      while (x < xend && x - a < TMAXCELLS) {
-        const unsigned c = count(x);
-        if (n + c > unsigned(TB)) break;
-        n += c;
-        x++;
-      }
-      if (WRITE)
-        out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(x - 1) << 16),
-                                 bc[rowbase + a], bc[rowbase + x]);
-      nitems++;
+    auto PRE = [&](int x) -> unsigned { return bc[rowbase + x]; };
+    unsigned p = PRE(xbeg);
+    const unsigned pend = PRE(xend);
+    int c = xbeg;
+    while (p < pend) {
+      while (PRE(c + 1) <= p) c++;
+      const unsigned q = min(min(p + unsigned(TB), pend), PRE(min(c + TMAXCELLS, xend)));
+      int e = c;
+      while (PRE(e + 1) < q) e++;
+      emit(c, e, p, q);
+      p = q;
+      c = e;
     }
     if (!WRITE) counts[r] = nitems;
     return;
   }
-  // Counts and their prefix sums (begin offsets): each lane a contiguous block of cells,
-  // lane totals scanned across the wave.
-  const int per = (ncx + 63) / 64, x0 = int(threadIdx.x) * per, x1 = min(x0 + per, ncx);
-  const unsigned rowstart = bc[rowbase];
-  unsigned run = 0;
-  for (int x = x0; x < x1; x++) {
-    const unsigned c = bc[rowbase + x + 1] - bc[rowbase + x];
-    cnt[x] = c;
-    pre[x] = run;
-    run += c;
-  }
-  unsigned incl = run;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const unsigned v = __shfl_up(incl, off, 64);
-    if (int(threadIdx.x) >= off) incl += v;
-  }
-  const unsigned excl = incl - run + rowstart;
-  for (int x = x0; x < x1; x++) pre[x] += excl;
-  if (threadIdx.x == 63) pre[ncx] = incl + rowstart;
+  for (int x = int(threadIdx.x); x <= ncx; x += 64) pre[x] = bc[rowbase + x];
   __syncthreads();
-  // Per cell: where the greedy item starting there ends (<= TMAXCELLS cells, <= TB p1),
-  // and the first non-empty owned cell at or after it (block-local, then a wave
-  // suffix-min).
+  // first non-empty owned cell at or after x: lane-local blocks, then a wave suffix-min
+  const int per = (ncx + 63) / 64, x0 = int(threadIdx.x) * per, x1 = min(x0 + per, ncx);
   int nz = xend;
   for (int x = x1 - 1; x >= x0; x--) {
-    unsigned n = cnt[x];
-    int e = x + 1;
-    while (e < xend && e - x < TMAXCELLS && n + cnt[e] <= unsigned(TB)) n += cnt[e++];
-    iend[x] = (unsigned short)e;
-    if (x >= xbeg && x < xend && cnt[x] != 0u) nz = x;
+    if (x >= xbeg && x < xend && pre[x + 1] > pre[x]) nz = x;
     nzfrom[x] = (unsigned short)nz;
   }
-  int suf = nz;  // min over this and later lanes' blocks
+  int suf = nz;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const int v = __shfl_down(suf, off, 64);
@@ -160,15 +138,18 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
   if (threadIdx.x == 63) nzfrom[ncx] = (unsigned short)xend;
   __syncthreads();
   if (threadIdx.x != 0) return;
-  // Walk the items: one LDS hop per item.
-  int x = nzfrom[xbeg];
-  while (x < xend) {
-    const int e = iend[x];
-    if (WRITE)
-      out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(x) | (unsigned(e - 1) << 16),
-                               pre[x], pre[e]);
-    nitems++;
-    x = nzfrom[e];
+  // Walk the items: the cell holding p is known (c), the cell holding q-1 is at most
+  // TMAXCELLS-1 cells further, an item ending at a cell end jumps to the next non-empty.
+  const unsigned pend = pre[xend];
+  int c = nzfrom[xbeg];
+  unsigned p = c < xend ? pre[c] : pend;
+  while (p < pend) {
+    const unsigned q = min(min(p + unsigned(TB), pend), pre[min(c + TMAXCELLS, xend)]);
+    int e = c;
+    while (pre[e + 1] < q) e++;
+    emit(c, e, p, q);
+    p = q;
+    c = pre[e + 1] == q ? int(nzfrom[e + 1]) : e;
   }
   if (!WRITE) counts[r] = nitems;
 }

@@ -298,7 +298,6 @@ void SphGpuSingle::AllocFixed() {
     return p;
   };
   begincell_ = (unsigned*)dmalloc(4 * size_t(G.nctt));
-  items_ = (uint4*)dmalloc(16 * (2 * size_t(G.nct) + 1));
   rowtmp_ = (unsigned*)dmalloc(4 * 2 * size_t(G.ncy) * size_t(G.ncz));
   qctr_ = (unsigned*)dmalloc(4 * 16);
   check_hip(hipMemset(qctr_, 0, 4 * 16), "zero work counters");
@@ -339,6 +338,9 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
   }
   poscell_ = (float4*)dmalloc(16 * n);
   press_ = (float*)dmalloc(4 * n);
+  // Interaction items (launch_items): an item holds TB particles unless it ends a row
+  // (<= 2 per row: fluid and bound) or reaches TMAXCELLS = 4 cells (<= 1 per 4 cells).
+  items_ = (uint4*)dmalloc(16 * (n / 128 + 2 * size_t(G.ncy) * size_t(G.ncz) + size_t(G.nct) / 2 + 2));
   arace_ = (float4*)dmalloc(16 * n);
   for (int i = 0; i < 2; i++) {
     sort_.keys[i] = (unsigned*)dmalloc(4 * n);
