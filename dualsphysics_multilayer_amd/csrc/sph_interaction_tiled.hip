@@ -45,13 +45,6 @@ constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
 #else
 #define SPH_WAVES_ATTR
 #endif
-#ifndef SPH_PACKED
-// 1: the two pairs of a drain iteration as one packed-f32 body (v_pk_fma/mul/add_f32).
-// Measured slower (1M: 0.935 ms at 128 VGPRs / 4 waves vs 0.842 ms scalar; 0.99 ms at
-// 135 VGPRs): one packed stream halves the independent instructions that hide the
-// dependent-issue latency of the body.  Kept as a build option for the record.
-#define SPH_PACKED 0
-#endif
 // staged neighbour records per segment.  504 (+8 over-read pad) puts the block at
 // 20.3 KB of LDS, the most that keeps 8 blocks = 4 waves per SIMD.  Measured at 1M:
 // 0.806 ms vs 0.838 at 416 (a mirrored row pair fits one segment for 94% of the units
@@ -197,14 +190,20 @@ struct TAcc {
 struct P1 {
   float x, y, z;        // x relative to the item's x origin, y/z cell-relative
   float4 vr;            // velocity, rho
-  float prr, inv_rho;   // press/rho, 1/rho
+  float press, inv_rho; // pressure (0 for a boundary p1), 1/rho
 };
 
-// Per-pass constants of the pair body (the mass of p2 and the Wendland bwen/h folded in).
+// Per-pass constants.  The pair body accumulates sums with the per-pass factors
+// taken out; finish() applies them once per particle:
+//   ar    = ar1 * sum w3 (dr.dv)/rho2
+//   ace   = -(bm/rho1) * sum w3 [(p1/rho2 + p2/rho2) + pv'] dr,  pv' = cvp (dr.dv) rr  (dr.dv < 0)
+//           with rr = 1/((r2+eta2)(rho1+rho2)): the reference's (p1+p2)/(rho1 rho2) and
+//           Pi = cvisc (dr.dv)/(r2+eta2) / robar with the masses and 1/rho1 folded out
+//   delta = kd * sum ...  (DDT: Molteni + , Fourtakas -)
 struct PassK {
   float ar1;  // bwen/h * m2 * rho1   (continuity)
   float bm;   // bwen/h * m2          (momentum)
-  float cv;   // 2 * bwen/h * cvisc   (artificial viscosity; cvisc = -alpha*cs0*h*m2)
+  float cvp;  // 2 * cvisc * rho1 / m2 (artificial viscosity; cvisc = -alpha*cs0*h*m2)
   float kd;   // ddtkh*cs0 * bwen/h * m2 (density diffusion)
 };
 
@@ -234,23 +233,22 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
   const float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
   const float dot = drx * dvx + dry * dvy + drz * dvz;
   const float re = rr2 + K.eta2;
-  float inv_re, inv_rs = 0.f;
+  float inv_re, rr = 0.f;
   if (MODE == 2) {
     inv_re = frcp(re);
   } else {
     const float rs = p.vr.w + B.w;  // 2*robar
-    const float rr = frcp(re * rs);
+    rr = frcp(re * rs);
     inv_re = rr * rs;
-    inv_rs = rr * re;
   }
   const float dot_rr2 = ok ? dot * inv_re : 0.f;
   a.visc = fmaxf(dot_rr2, a.visc);
-  const float wdr = w3 * dot * C.y;  // w3*(dr.dv)/rho2
-  a.ar = fmaf(wdr, Q.ar1, a.ar);
+  const float wc = w3 * C.y;  // w3/rho2
+  a.ar = fmaf(wc, dot, a.ar);
   if (MODE == 2) return;
-  const float S = fmaf(C.y, p.prr, p.inv_rho * C.x);  // (p1+p2)/(rho1*rho2)
-  const float pv = (dot < 0.f) ? Q.cv * dot_rr2 * inv_rs : 0.f;
-  const float c = -w3 * fmaf(Q.bm, S, pv);
+  const float S = fmaf(C.y, p.press, C.x);  // (p1+p2)/rho2
+  const float pv = (dot < 0.f) ? Q.cvp * dot * rr : 0.f;
+  const float c = w3 * (S + pv);
   a.ax = fmaf(c, drx, a.ax);
   a.ay = fmaf(c, dry, a.ay);
   a.az = fmaf(c, drz, a.az);
@@ -260,108 +258,34 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
   }
   if (TDENSITY == 1) {
     const float t = w3 * rr2 * inv_re;
-    a.delta = fmaf(Q.kd * t, fmaf(p.vr.w, C.y, -1.f), a.delta);
+    a.delta = fmaf(t, fmaf(p.vr.w, C.y, -1.f), a.delta);
   } else if (TDENSITY == 2 || TDENSITY == 3) {
     float drhop;
     if (K.ddtseries)  // kernel-uniform (scalar) branch
       drhop = drz * fmaf(drz, fmaf(drz, fmaf(drz, K.ddte4, K.ddte3), K.ddte2), K.ddte1);
     else
       drhop = K.rhopzero * fexp2(K.ovgamma * flog2(1.f + K.ddtgz * drz)) - K.rhopzero;
-    const float t = w3 * rr2 * inv_re * C.y;
-    a.delta = fmaf(-Q.kd * t, B.w - (p.vr.w + drhop), a.delta);
+    const float t = wc * rr2 * inv_re;
+    a.delta = fmaf(t, B.w - (p.vr.w + drhop), a.delta);
   }
 }
 
-// Two pairs per lane as the low/high halves of packed f32 values: gfx950 issues
-// v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 (two f32 operations) at the cost of one
-// scalar VALU op, so the arithmetic of the pair body runs at half the issue count; only
-// the transcendentals (sqrt, rcp), the compares and the selects stay per pair.  The
-// accumulators are packed too (pairs 1, 3, 5, ... in .x, 2, 4, 6, ... in .y) and added
-// once per particle — a fixed summation order, so runs stay bitwise reproducible.
-typedef float f2 __attribute__((ext_vector_type(2)));
-struct TAcc2 {
-  f2 ax, ay, az, ar, delta;
-  float visc;
-};
-__device__ __forceinline__ f2 pk(float a, float b) { return f2{a, b}; }
-
+// The per-pass factors of the sums (PassK) applied once per particle.
 template <int TDENSITY, int MODE>
-__device__ __forceinline__ void pair_body2(const KConst& K, const P1& p, const float4& A1, const float4& A2,
-                                           const float4& B1, const float4& B2, const float2& C1, const float2& C2,
-                                           bool two, const PassK& Q, TAcc2& a) {
-  const f2 drx = p.x - pk(A1.x, A2.x), dry = p.y - pk(A1.y, A2.y), drz = p.z - pk(A1.z, A2.z);
-  const f2 rr2 = drx * drx + dry * dry + drz * drz;
-  const bool ok1 = rr2.x <= K.kernelsize2 && rr2.x >= ALMOSTZERO;
-  const bool ok2 = two && rr2.y <= K.kernelsize2 && rr2.y >= ALMOSTZERO;
-  const f2 wq = K.mhalfovh * pk(fsqrt_(rr2.x), fsqrt_(rr2.y)) + 1.f;
-  f2 w3 = wq * wq * wq;
-  w3 = pk(ok1 ? w3.x : 0.f, ok2 ? w3.y : 0.f);
-  const f2 dvx = p.vr.x - pk(B1.x, B2.x), dvy = p.vr.y - pk(B1.y, B2.y), dvz = p.vr.z - pk(B1.z, B2.z);
-  const f2 dot = drx * dvx + dry * dvy + drz * dvz;
-  const f2 re = rr2 + K.eta2;
-  f2 inv_re, inv_rs;
-  if (MODE == 2) {
-    inv_re = pk(frcp(re.x), frcp(re.y));
-  } else {
-    const f2 rs = p.vr.w + pk(B1.w, B2.w);  // 2*robar
-    const f2 t = re * rs;
-    const f2 rr = pk(frcp(t.x), frcp(t.y));
-    inv_re = rr * rs;
-    inv_rs = rr * re;
+__device__ __forceinline__ TAcc finish(TAcc a, const P1& p, const PassK& Q) {
+  a.ar *= Q.ar1;
+  if (MODE != 2) {
+    const float s = -Q.bm * p.inv_rho;
+    a.ax *= s;
+    a.ay *= s;
+    a.az *= s;
   }
-  f2 dot_rr2 = dot * inv_re;
-  dot_rr2 = pk(ok1 ? dot_rr2.x : 0.f, ok2 ? dot_rr2.y : 0.f);
-  a.visc = fmaxf(fmaxf(dot_rr2.x, dot_rr2.y), a.visc);
-  const f2 cy = pk(C1.y, C2.y);
-  const f2 wdr = w3 * dot * cy;  // w3*(dr.dv)/rho2
-  a.ar = wdr * Q.ar1 + a.ar;
-  if (MODE == 2) return;
-  const f2 S = cy * p.prr + p.inv_rho * pk(C1.x, C2.x);  // (p1+p2)/(rho1*rho2)
-  f2 pv = Q.cv * dot_rr2 * inv_rs;
-  pv = pk(dot.x < 0.f ? pv.x : 0.f, dot.y < 0.f ? pv.y : 0.f);
-  const f2 c = -w3 * (Q.bm * S + pv);
-  a.ax = c * drx + a.ax;
-  a.ay = c * dry + a.ay;
-  a.az = c * drz + a.az;
-  if (MODE == 1) {
-    if (TDENSITY == 1 || TDENSITY == 2) {  // DBC: no DDT next to the boundary
-      if (ok1) a.delta.x = FLT_MAX;
-      if (ok2) a.delta.y = FLT_MAX;
-    }
-    return;
+  if (MODE == 0) {
+    if (TDENSITY == 1) a.delta *= Q.kd;
+    else if (TDENSITY == 2 || TDENSITY == 3) a.delta *= -Q.kd;
   }
-  if (TDENSITY == 1) {
-    const f2 t = w3 * rr2 * inv_re;
-    a.delta = (Q.kd * t) * (p.vr.w * cy - 1.f) + a.delta;
-  } else if (TDENSITY == 2 || TDENSITY == 3) {
-    f2 drhop;
-    if (K.ddtseries) {  // kernel-uniform (scalar) branch
-      drhop = drz * (drz * (drz * (drz * K.ddte4 + K.ddte3) + K.ddte2) + K.ddte1);
-    } else {
-      const f2 l = 1.f + K.ddtgz * drz;
-      drhop = pk(fexp2(K.ovgamma * flog2(l.x)), fexp2(K.ovgamma * flog2(l.y))) * K.rhopzero - K.rhopzero;
-    }
-    const f2 t = w3 * rr2 * inv_re * cy;
-    a.delta = (-Q.kd * t) * (pk(B1.w, B2.w) - (p.vr.w + drhop)) + a.delta;
-  }
+  return a;
 }
-
-__device__ __forceinline__ TAcc unpack(const TAcc2& a) {
-  TAcc r;
-  r.ax = a.ax.x + a.ax.y;
-  r.ay = a.ay.x + a.ay.y;
-  r.az = a.az.x + a.az.y;
-  r.ar = a.ar.x + a.ar.y;
-  r.delta = (a.delta.x == FLT_MAX || a.delta.y == FLT_MAX) ? FLT_MAX : a.delta.x + a.delta.y;
-  r.visc = a.visc;
-  return r;
-}
-
-#if SPH_PACKED
-typedef TAcc2 UAcc;
-#else
-typedef TAcc UAcc;
-#endif
 
 // Candidate test of one window: n (<= 128) staged records from sA+s0 with the expanded
 // form |p-A|^2 = |p|^2 + |A|^2 - 2 p.A (3 FMAs + 1 compare per candidate on one
@@ -404,7 +328,7 @@ __device__ __forceinline__ void test128(const float4* __restrict__ sA, int s0, i
 template <int TDENSITY, int MODE>
 __device__ __forceinline__ void tile_unit(const KConst& K, const P1& p, float thr, int wa0, int wa1, int wb0, int wb1,
                                           const float4* __restrict__ sA, const float4* __restrict__ sB,
-                                          const float2* __restrict__ sC, const PassK& Q, UAcc& a) {
+                                          const float2* __restrict__ sC, const PassK& Q, TAcc& a) {
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
 #if SPH_ABLATE == 2
   a.visc += float(wa1 - wa0 + wb1 - wb0);
@@ -464,20 +388,14 @@ __device__ __forceinline__ void tile_unit(const KConst& K, const P1& p, float th
       const float4 A1 = sA[j1], A2 = sA[j2];
       const float4 B1 = sB[j1], B2 = sB[j2];
       const float2 C1 = sC[j1], C2 = sC[j2];
-#if SPH_PACKED
-      pair_body2<TDENSITY, MODE>(K, p, A1, A2, B1, B2, C1, C2, two, Q, a);
-      continue;
-#endif
       const float drx1 = p.x - A1.x, dry1 = p.y - A1.y, drz1 = p.z - A1.z;
       const float drx2 = p.x - A2.x, dry2 = p.y - A2.y, drz2 = p.z - A2.z;
       const float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
       const float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
       const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
       const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
-#if !SPH_PACKED
       pair_body<TDENSITY, MODE>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, Q, a);
       pair_body<TDENSITY, MODE>(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, Q, a);
-#endif
     }
   }
 }
@@ -503,6 +421,39 @@ __device__ __forceinline__ void stage_row(const KConst& K, unsigned rs, unsigned
   }
 }
 
+// Which p1 of the item each lane computes.  A lane's drain loops run as long as the
+// busiest lane of its wave, and a particle's candidate counts per mirrored row pair
+// depend mostly on how far it sits from its cell's centre in y and z; so the n (<= TB)
+// particles are split between the two waves by that distance (|dy| + |dz| below or
+// above half a cell, stable ballot ranks): simulated on the 1M lattice, drain
+// utilisation 0.68 -> 0.74.  Results do not depend on the assignment: every p1 is
+// summed by one lane over the same candidates in the same order.
+__device__ __forceinline__ unsigned lane_order(const float4* __restrict__ poscell, unsigned first, unsigned n,
+                                               float hs, unsigned char* s_perm, unsigned* s_nwave) {
+  const unsigned me = threadIdx.x, wv = me >> 6, ln = me & 63u;
+  const bool valid = me < n;
+  bool low = false;
+  if (valid) {
+    const float4 pc = poscell[first + me];
+    low = fabsf(pc.y - hs) + fabsf(pc.z - hs) < hs;
+  }
+  const unsigned long long bl = __ballot(low), bh = __ballot(valid && !low);
+  const unsigned long long lt = (1ull << ln) - 1ull;
+  if (ln == 0) {
+    s_nwave[wv] = unsigned(__popcll(bl));
+    s_nwave[2 + wv] = unsigned(__popcll(bh));
+  }
+  __syncthreads();
+  const unsigned nl0 = s_nwave[0], nl = nl0 + s_nwave[1], nh0 = s_nwave[2];
+  if (valid) {
+    const unsigned pos = low ? (wv ? nl0 : 0u) + unsigned(__popcll(bl & lt))
+                             : nl + (wv ? nh0 : 0u) + unsigned(__popcll(bh & lt));
+    s_perm[pos] = (unsigned char)me;
+  }
+  __syncthreads();
+  return valid ? s_perm[me] : me;
+}
+
 // Item geometry shared by the passes of one p1.
 struct RowCtx {
   int cy, cz;     // the item's cell row
@@ -517,7 +468,7 @@ __device__ __forceinline__ PassK pass_k(const KConst& K, float cvisc, float m2, 
   PassK q;
   q.bm = K.bwenovh * m2;
   q.ar1 = q.bm * rho1;
-  q.cv = 2.f * K.bwenovh * cvisc;
+  q.cvp = 2.f * cvisc * rho1 / m2;
   q.kd = K.ddtkhcs * q.bm;
   return q;
 }
@@ -532,7 +483,7 @@ __device__ __forceinline__ TAcc run_pass(const KConst& K, const DivGrid& g, cons
                                          const float4* __restrict__ poscell, const float4* __restrict__ velrhop,
                                          const float* __restrict__ press, float4* __restrict__ sA,
                                          float4* __restrict__ sB, float2* __restrict__ sC) {
-  UAcc acc = {};
+  TAcc acc = {};
   const unsigned cellinit = (MODE == 1 ? 0u : g.boxfluid);
   for (int u = 0; u < 5; u++) {
     const int dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
@@ -579,11 +530,7 @@ __device__ __forceinline__ TAcc run_pass(const KConst& K, const DivGrid& g, cons
       }
     }
   }
-#if SPH_PACKED
-  return unpack(acc);
-#else
-  return acc;
-#endif
+  return finish<TDENSITY, MODE>(acc, p, Q);
 }
 
 template <int TDENSITY>
@@ -597,6 +544,8 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
   __shared__ float4 sB[TCAP];
   __shared__ float2 sC[TCAP];  // press/rho, 1/rho
   __shared__ unsigned s_item;
+  __shared__ unsigned char s_perm[TB];  // lane -> p1 of the item (see lane_order)
+  __shared__ unsigned s_nwave[4];
   const unsigned nitems = sc->nitems;
   const unsigned per = (nitems + 7) / 8;
   const unsigned grp = blockIdx.x & 7;
@@ -633,9 +582,9 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
           continue;
         }
       }
-      for (unsigned p1base = item.z; p1base < item.w; p1base += TB) {
-        const unsigned p1 = p1base + threadIdx.x;
-        const bool act = p1 < item.w;
+      {  // items hold <= TB particles: one p1 per lane
+        const unsigned p1 = item.z + lane_order(poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
+        const bool act = threadIdx.x < item.w - item.z;
         P1 p;
         int cx1 = a;
         if (act) {
@@ -645,14 +594,13 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
           p.y = pc1.y;
           p.z = pc1.z;
           p.vr = velrhop[p1];
-          p.prr = bitem ? 0.f : press[p1];
+          p.press = bitem ? 0.f : press[p1];
         } else {
           p.x = p.y = p.z = 1e30f;  // never within the support radius
           p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
-          p.prr = 0.f;
+          p.press = 0.f;
         }
         p.inv_rho = frcp(p.vr.w);
-        p.prr *= p.inv_rho;
         const int lxa = max(cx1 - 1, 0), lxb = min(cx1 + 1, g.ncx - 1);
         const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
         const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act};
