@@ -213,8 +213,10 @@ int launch_radix_sort(hipStream_t stm, unsigned cap, const DevScalars* sc, SortS
 
 // ---------------------------------------------------------------------------------
 // begincell[c] = first sorted index with key >= c (lower bound) for every box c.
-__device__ inline unsigned lower_bound_u32(const unsigned* __restrict__ a, unsigned n, unsigned v) {
-  unsigned lo = 0, hi = n;
+// Particles move less than a cell per step, so the previous divide's begincell[c] is
+// close to the new one: a galloping search from it (1-3 probes typically, any guess
+// is correct, just slower) instead of a 20-probe binary search.
+__device__ inline unsigned lower_bound_u32(const unsigned* __restrict__ a, unsigned lo, unsigned hi, unsigned v) {
   while (lo < hi) {
     const unsigned mid = (lo + hi) >> 1;
     if (a[mid] < v) lo = mid + 1;
@@ -223,23 +225,45 @@ __device__ inline unsigned lower_bound_u32(const unsigned* __restrict__ a, unsig
   return lo;
 }
 
+__device__ inline unsigned gallop_lb(const unsigned* __restrict__ a, unsigned n, unsigned v, unsigned g) {
+  g = min(g, n);
+  if (g > 0 && a[g - 1] >= v) {  // answer in [0, g-1]: step left
+    unsigned hi = g - 1, step = 1;
+    while (hi >= step && a[hi - step] >= v) {
+      hi -= step;
+      step <<= 1;
+    }
+    const unsigned lo = hi >= step ? hi - step + 1 : 0u;
+    return lower_bound_u32(a, lo, hi, v);
+  }
+  if (g < n && a[g] < v) {  // answer in [g+1, n]: step right
+    unsigned lo = g + 1, step = 1;
+    while (lo + step - 1 < n && a[lo + step - 1] < v) {
+      lo += step;
+      step <<= 1;
+    }
+    const unsigned hi = min(lo + step - 1, n);
+    return lower_bound_u32(a, lo, hi, v);
+  }
+  return g;
+}
+
 __global__ __launch_bounds__(256) void k_begincell(DevScalars* __restrict__ sc, const unsigned* __restrict__ skeys,
                                                    DivGrid g, unsigned* __restrict__ begincell) {
   const unsigned n = sc->ndiv;
   const unsigned c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < g.nctt) begincell[c] = lower_bound_u32(skeys, n, c);
-  if (c == 0) {
-    // JCellDivCpuSingle::Divide counts (JCellDivCpuSingle.cpp:330-339) + RunCellDivide (JSphCpuSingle.cpp:470-472).
-    const unsigned b_ignore = lower_bound_u32(skeys, n, g.boxboundignore);
-    const unsigned b_fluid = lower_bound_u32(skeys, n, g.boxfluid);
-    const unsigned b_bout = lower_bound_u32(skeys, n, g.boxboundout);
-    const unsigned b_fout = lower_bound_u32(skeys, n, g.boxfluidout);
-    const unsigned b_fout1 = lower_bound_u32(skeys, n, g.boxfluidout + 1);
-    sc->npbok = b_ignore;
-    sc->npb = b_fluid;
-    sc->np = b_bout;
-    sc->nout += b_fout1 - b_fout;
-    const unsigned npbout = b_fout - b_bout;
+  if (c >= g.nctt) return;
+  const unsigned b = gallop_lb(skeys, n, c, begincell[c]);
+  begincell[c] = b;
+  // JCellDivCpuSingle::Divide counts (JCellDivCpuSingle.cpp:330-339) + RunCellDivide
+  // (JSphCpuSingle.cpp:470-472), each from the thread of its box.
+  if (c == g.boxboundignore) sc->npbok = b;
+  if (c == g.boxfluid) sc->npb = b;
+  if (c == g.boxboundout) sc->np = b;
+  if (c == g.boxfluidout) {
+    const unsigned b1 = lower_bound_u32(skeys, b, n, c + 1);
+    sc->nout += b1 - b;
+    const unsigned npbout = b - lower_bound_u32(skeys, 0, b, g.boxboundout);
     if (npbout) {
       sc->npbout = npbout;
       sc->error_flags |= ERR_BOUNDOUT;
@@ -269,6 +293,10 @@ struct GatherArgs {
   int xoff;
 };
 
+// WITHM1 / WITHPRE are template parameters so every load of a particle is issued before
+// the first store (as runtime flags the compiler kept the optional arrays in separate
+// load -> wait -> store round trips).
+template <bool WITHM1, bool WITHPRE>
 __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, GatherArgs a) {
   const unsigned n = sc->np, npb = sc->npb;
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -279,17 +307,28 @@ __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, Gat
     const double2 pxy = a.src.posxy[s];
     const double pz = a.src.posz[s];
     const float4 vr = a.src.velrhop[s];
-    a.dst.idp[i] = a.src.idp[s];
-    a.dst.code[i] = a.src.code[s];
+    const unsigned idp = a.src.idp[s];
+    const typecode code = a.src.code[s];
+    float4 m1, vpre;
+    double2 pxypre;
+    double pzpre;
+    if (WITHM1) m1 = a.src.velrhopm1[s];
+    if (WITHPRE) {
+      pxypre = a.src.posxypre[s];
+      pzpre = a.src.poszpre[s];
+      vpre = a.src.velrhoppre[s];
+    }
+    a.dst.idp[i] = idp;
+    a.dst.code[i] = code;
     a.dst.dcell[i] = dc;
     a.dst.posxy[i] = pxy;
     a.dst.posz[i] = pz;
     a.dst.velrhop[i] = vr;
-    if (a.withm1) a.dst.velrhopm1[i] = a.src.velrhopm1[s];
-    if (a.withpre) {
-      a.dst.posxypre[i] = a.src.posxypre[s];
-      a.dst.poszpre[i] = a.src.poszpre[s];
-      a.dst.velrhoppre[i] = a.src.velrhoppre[s];
+    if (WITHM1) a.dst.velrhopm1[i] = m1;
+    if (WITHPRE) {
+      a.dst.posxypre[i] = pxypre;
+      a.dst.poszpre[i] = pzpre;
+      a.dst.velrhoppre[i] = vpre;
     }
     // PosCell (KerUpdatePosCell): position relative to the origin of its divide cell
     // (global cell -> the same floats on every slab); w = the local cell.
@@ -344,7 +383,10 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
   a.withm1 = withm1;
   a.withpre = withpre;
   const unsigned nb = (cap + 255) / 256;
-  hipLaunchKernelGGL(k_gather, dim3(nb), dim3(256), 0, stm, sc, a);
+  if (withm1 && withpre) hipLaunchKernelGGL((k_gather<true, true>), dim3(nb), dim3(256), 0, stm, sc, a);
+  else if (withm1) hipLaunchKernelGGL((k_gather<true, false>), dim3(nb), dim3(256), 0, stm, sc, a);
+  else if (withpre) hipLaunchKernelGGL((k_gather<false, true>), dim3(nb), dim3(256), 0, stm, sc, a);
+  else hipLaunchKernelGGL((k_gather<false, false>), dim3(nb), dim3(256), 0, stm, sc, a);
 }
 
 }  // namespace sphx
