@@ -295,68 +295,91 @@ struct GatherArgs {
 
 // WITHM1 / WITHPRE are template parameters so every load of a particle is issued before
 // the first store (as runtime flags the compiler kept the optional arrays in separate
-// load -> wait -> store round trips).
+// load -> wait -> store round trips).  GP particles per thread (i, i + 256, ...): the
+// kernel is bound by two dependent memory latencies (sortpart, then the particle), so
+// more bytes in flight per wave shorten it.
+#ifndef SPH_GP
+#define SPH_GP 4
+#endif
+constexpr int GP = SPH_GP;
+
+template <bool WITHM1, bool WITHPRE>
+__device__ __forceinline__ void gather_one(const GatherArgs& a, unsigned i, unsigned s, float4& vr_out, bool& fluid,
+                                           unsigned npb) {
+  const unsigned dc = a.src.dcell[s];
+  const double2 pxy = a.src.posxy[s];
+  const double pz = a.src.posz[s];
+  const float4 vr = a.src.velrhop[s];
+  const unsigned idp = a.src.idp[s];
+  const typecode code = a.src.code[s];
+  float4 m1, vpre;
+  double2 pxypre;
+  double pzpre;
+  if (WITHM1) m1 = a.src.velrhopm1[s];
+  if (WITHPRE) {
+    pxypre = a.src.posxypre[s];
+    pzpre = a.src.poszpre[s];
+    vpre = a.src.velrhoppre[s];
+  }
+  a.dst.idp[i] = idp;
+  a.dst.code[i] = code;
+  a.dst.dcell[i] = dc;
+  a.dst.posxy[i] = pxy;
+  a.dst.posz[i] = pz;
+  a.dst.velrhop[i] = vr;
+  if (WITHM1) a.dst.velrhopm1[i] = m1;
+  if (WITHPRE) {
+    a.dst.posxypre[i] = pxypre;
+    a.dst.poszpre[i] = pzpre;
+    a.dst.velrhoppre[i] = vpre;
+  }
+  // PosCell (KerUpdatePosCell): position relative to the origin of its divide cell
+  // (global cell -> the same floats on every slab); w = the local cell.
+  const unsigned cx = DcelCellx(a.dcc, dc), cy = DcelCelly(a.dcc, dc), cz = DcelCellz(a.dcc, dc);
+  const double ox = a.posminx + double(cx) * a.scelld;
+  const double oy = a.posminy + double(cy) * a.scelld;
+  const double oz = a.posminz + double(cz) * a.scelld;
+  const unsigned ldc = a.xoff ? DcelCell(a.dcc, cx - unsigned(a.xoff), cy, cz) : dc;
+  a.poscell[i] = make_float4(float(pxy.x - ox), float(pxy.y - oy), float(pz - oz), __uint_as_float(ldc));
+  // Press (PreInteractionVars_Forces, JSphCpu.cpp:451-453; FunSphEos.h:37-47) as the
+  // reference binary evaluates it: the unqualified pow in namespace fsph is the C
+  // double pow, and -ffast-math makes rhop/rhop0 a product with 1/rhop0.  For an
+  // integer gamma the double power is formed by squaring (<= 4 roundings at 1e-16,
+  // far below the float rounding of the result).
+  const double xr = double(vr.w * a.ovrhopzero);
+  double xg;
+  if (a.igamma > 0) {  // integer gamma (7 in every case here): exact squaring in double
+    double r = 1.0, b = xr;
+    for (int e = a.igamma; e; e >>= 1) {
+      if (e & 1) r *= b;
+      b *= b;
+    }
+    xg = r;
+  } else {
+    xg = pow(xr, double(a.gamma));
+  }
+  a.press[i] = float(double(a.cteb) * (xg - 1.0));
+  vr_out = vr;
+  fluid = i >= npb;
+}
+
 template <bool WITHM1, bool WITHPRE>
 __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, GatherArgs a) {
   const unsigned n = sc->np, npb = sc->npb;
-  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned i0 = blockIdx.x * (256 * GP) + threadIdx.x;
+  unsigned sp[GP];
+#pragma unroll
+  for (int k = 0; k < GP; k++) sp[k] = (i0 + 256 * k < n) ? a.sortpart[i0 + 256 * k] : 0u;
   float v2 = 0.f;
-  if (i < n) {
-    const unsigned s = a.sortpart[i];
-    const unsigned dc = a.src.dcell[s];
-    const double2 pxy = a.src.posxy[s];
-    const double pz = a.src.posz[s];
-    const float4 vr = a.src.velrhop[s];
-    const unsigned idp = a.src.idp[s];
-    const typecode code = a.src.code[s];
-    float4 m1, vpre;
-    double2 pxypre;
-    double pzpre;
-    if (WITHM1) m1 = a.src.velrhopm1[s];
-    if (WITHPRE) {
-      pxypre = a.src.posxypre[s];
-      pzpre = a.src.poszpre[s];
-      vpre = a.src.velrhoppre[s];
+#pragma unroll
+  for (int k = 0; k < GP; k++) {
+    const unsigned i = i0 + 256 * k;
+    if (i < n) {
+      float4 vr;
+      bool fluid;
+      gather_one<WITHM1, WITHPRE>(a, i, sp[k], vr, fluid, npb);
+      if (fluid) v2 = fmaxf(v2, vr.x * vr.x + vr.y * vr.y + vr.z * vr.z);  // CalcVelMaxOmp over fluid
     }
-    a.dst.idp[i] = idp;
-    a.dst.code[i] = code;
-    a.dst.dcell[i] = dc;
-    a.dst.posxy[i] = pxy;
-    a.dst.posz[i] = pz;
-    a.dst.velrhop[i] = vr;
-    if (WITHM1) a.dst.velrhopm1[i] = m1;
-    if (WITHPRE) {
-      a.dst.posxypre[i] = pxypre;
-      a.dst.poszpre[i] = pzpre;
-      a.dst.velrhoppre[i] = vpre;
-    }
-    // PosCell (KerUpdatePosCell): position relative to the origin of its divide cell
-    // (global cell -> the same floats on every slab); w = the local cell.
-    const unsigned cx = DcelCellx(a.dcc, dc), cy = DcelCelly(a.dcc, dc), cz = DcelCellz(a.dcc, dc);
-    const double ox = a.posminx + double(cx) * a.scelld;
-    const double oy = a.posminy + double(cy) * a.scelld;
-    const double oz = a.posminz + double(cz) * a.scelld;
-    const unsigned ldc = a.xoff ? DcelCell(a.dcc, cx - unsigned(a.xoff), cy, cz) : dc;
-    a.poscell[i] = make_float4(float(pxy.x - ox), float(pxy.y - oy), float(pz - oz), __uint_as_float(ldc));
-    // Press (PreInteractionVars_Forces, JSphCpu.cpp:451-453; FunSphEos.h:37-47) as the
-    // reference binary evaluates it: the unqualified pow in namespace fsph is the C
-    // double pow, and -ffast-math makes rhop/rhop0 a product with 1/rhop0.  For an
-    // integer gamma the double power is formed by squaring (<= 4 roundings at 1e-16,
-    // far below the float rounding of the result).
-    const double xr = double(vr.w * a.ovrhopzero);
-    double xg;
-    if (a.igamma > 0) {  // integer gamma (7 in every case here): exact squaring in double
-      double r = 1.0, b = xr;
-      for (int e = a.igamma; e; e >>= 1) {
-        if (e & 1) r *= b;
-        b *= b;
-      }
-      xg = r;
-    } else {
-      xg = pow(xr, double(a.gamma));
-    }
-    a.press[i] = float(double(a.cteb) * (xg - 1.0));
-    if (i >= npb) v2 = vr.x * vr.x + vr.y * vr.y + vr.z * vr.z;  // CalcVelMaxOmp over fluid
   }
   wave_max_atomic(sc, RED_VELMAX2, v2);
 }
@@ -382,7 +405,7 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
   a.dcc = K.domcellcode;
   a.withm1 = withm1;
   a.withpre = withpre;
-  const unsigned nb = (cap + 255) / 256;
+  const unsigned nb = (cap + 256 * GP - 1) / (256 * GP);
   if (withm1 && withpre) hipLaunchKernelGGL((k_gather<true, true>), dim3(nb), dim3(256), 0, stm, sc, a);
   else if (withm1) hipLaunchKernelGGL((k_gather<true, false>), dim3(nb), dim3(256), 0, stm, sc, a);
   else if (withpre) hipLaunchKernelGGL((k_gather<false, true>), dim3(nb), dim3(256), 0, stm, sc, a);

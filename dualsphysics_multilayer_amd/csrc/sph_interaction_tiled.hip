@@ -133,16 +133,21 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
   if (threadIdx.x != 0) return;
   // Walk the items: the cell holding p is known (c), the cell holding q-1 is at most
   // TMAXCELLS-1 cells further, an item ending at a cell end jumps to the next non-empty.
+  // The five offsets pre[c..c+4] of an item are independent LDS reads (one latency);
+  // the cell holding q-1 is c + #{k = 1..3 : pre[c+k] <= q-1}.
+  static_assert(TMAXCELLS == 4, "the walk reads pre[c..c+4]");
   const unsigned pend = pre[xend];
   int c = nzfrom[xbeg];
   unsigned p = c < xend ? pre[c] : pend;
   while (p < pend) {
-    const unsigned q = min(min(p + unsigned(TB), pend), pre[min(c + TMAXCELLS, xend)]);
-    int e = c;
-    while (pre[e + 1] < q) e++;
+    const unsigned p1 = pre[min(c + 1, xend)], p2 = pre[min(c + 2, xend)], p3 = pre[min(c + 3, xend)];
+    const unsigned p4 = pre[min(c + 4, xend)];
+    const unsigned q = min(min(p + unsigned(TB), pend), p4);
+    const int e = c + int(p1 <= q - 1) + int(p2 <= q - 1) + int(p3 <= q - 1);
     emit(c, e, p, q);
     p = q;
-    c = pre[e + 1] == q ? int(nzfrom[e + 1]) : e;
+    const unsigned pe1 = e + 1 - c == 1 ? p1 : e + 1 - c == 2 ? p2 : e + 1 - c == 3 ? p3 : p4;
+    c = pe1 == q ? int(nzfrom[e + 1]) : e;
   }
   if (!WRITE) counts[r] = nitems;
 }
