@@ -57,8 +57,9 @@ void launch_presort(hipStream_t stm, unsigned cap, const DevScalars* sc, const u
 }
 
 // ---------------------------------------------------------------------------------
-// Stable LSD radix sort.  Per pass: tile histograms -> per-digit row scans ->
-// digit-total scan -> stable scatter (wave match via ballots + tagged LDS wave counts).
+// Stable LSD radix sort.  Per pass: tile histograms (tile-major) -> per-digit scans over
+// the tiles (digit totals) -> stable scatter (digit totals scanned in each block's
+// prologue; wave match via ballots + tagged LDS wave counts).
 __global__ __launch_bounds__(RS_BS) void k_rs_hist(const DevScalars* __restrict__ sc, const unsigned* __restrict__ keys,
                                                    unsigned shift, unsigned rbits, unsigned ntiles,
                                                    unsigned* __restrict__ hist) {
@@ -74,57 +75,54 @@ __global__ __launch_bounds__(RS_BS) void k_rs_hist(const DevScalars* __restrict_
     if (idx < n) atomicAdd(&cnt[(keys[idx] >> shift) & mask], 1u);
   }
   __syncthreads();
-  for (unsigned d = threadIdx.x; d < radix; d += RS_BS) hist[d * ntiles + blockIdx.x] = cnt[d];
+  for (unsigned d = threadIdx.x; d < radix; d += RS_BS) hist[blockIdx.x * radix + d] = cnt[d];
 }
 
-// Exclusive scan of one digit row hist[d*ntiles .. +ntiles); row total to digtot[d].
-__global__ __launch_bounds__(256) void k_rs_scan_rows(unsigned* __restrict__ hist, unsigned ntiles,
-                                                      unsigned* __restrict__ digtot) {
-  __shared__ unsigned part[256];
-  unsigned* row = hist + size_t(blockIdx.x) * ntiles;
-  const unsigned per = (ntiles + 255) / 256;
-  const unsigned b0 = threadIdx.x * per, b1 = min(b0 + per, ntiles);
-  unsigned s = 0;
-  for (unsigned i = b0; i < b1; i++) s += row[i];
-  part[threadIdx.x] = s;
+// Per digit, the exclusive scan over the tiles of hist[tile*radix + d] (tile-major, so
+// the histogram and scatter kernels read and write whole rows); the digit total to
+// digtot[d].  A block takes SCAN_D consecutive digits x SCAN_C tile chunks: a lane
+// (digit j, chunk c) walks its chunk, the lanes of a digit group read consecutive words.
+constexpr int SCAN_D = 4, SCAN_C = 64;
+__global__ __launch_bounds__(256) void k_rs_scan_tiles(unsigned* __restrict__ hist, unsigned ntiles, unsigned radix,
+                                                       unsigned* __restrict__ digtot) {
+  __shared__ unsigned s_sum[SCAN_C][SCAN_D];
+  const unsigned j = threadIdx.x % SCAN_D, c = threadIdx.x / SCAN_D;
+  const unsigned d = blockIdx.x * SCAN_D + j;
+  const unsigned per = (ntiles + SCAN_C - 1) / SCAN_C, b0 = c * per;
+  const unsigned b1 = d < radix ? min(b0 + per, ntiles) : b0;  // radix < SCAN_D: idle lanes
+  // chunks of <= CH tiles stay in registers (one round of independent loads)
+  constexpr unsigned CH = 8;
+  const bool inreg = per <= CH;
+  unsigned v[CH];
+  unsigned sum = 0;
+  if (inreg) {
+#pragma unroll
+    for (unsigned k = 0; k < CH; k++) {
+      v[k] = (b0 + k < b1) ? hist[size_t(b0 + k) * radix + d] : 0u;
+      sum += v[k];
+    }
+  } else {
+    for (unsigned b = b0; b < b1; b++) sum += hist[size_t(b) * radix + d];
+  }
+  s_sum[c][j] = sum;
   __syncthreads();
-  // Hillis-Steele inclusive scan over 256 partials.
-  for (int off = 1; off < 256; off <<= 1) {
-    const unsigned v = (threadIdx.x >= unsigned(off) ? part[threadIdx.x - off] : 0u);
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
+  unsigned run = 0;
+  for (unsigned cc = 0; cc < c; cc++) run += s_sum[cc][j];
+  if (inreg) {
+#pragma unroll
+    for (unsigned k = 0; k < CH; k++) {
+      if (b0 + k < b1) hist[size_t(b0 + k) * radix + d] = run;
+      run += v[k];
+    }
+  } else {
+    for (unsigned b = b0; b < b1; b++) {
+      const size_t k = size_t(b) * radix + d;
+      const unsigned x = hist[k];
+      hist[k] = run;
+      run += x;
+    }
   }
-  unsigned run = (threadIdx.x ? part[threadIdx.x - 1] : 0u);
-  for (unsigned i = b0; i < b1; i++) {
-    const unsigned v = row[i];
-    row[i] = run;
-    run += v;
-  }
-  if (threadIdx.x == 255) digtot[blockIdx.x] = part[255];
-}
-
-// Exclusive scan of the digit totals (<= 2048 entries) in place.
-__global__ __launch_bounds__(256) void k_rs_scan_digits(unsigned* __restrict__ digtot, unsigned radix) {
-  __shared__ unsigned part[256];
-  const unsigned per = (radix + 255) / 256;
-  const unsigned b0 = threadIdx.x * per, b1 = min(b0 + per, radix);
-  unsigned s = 0;
-  for (unsigned i = b0; i < b1; i++) s += digtot[i];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    const unsigned v = (threadIdx.x >= unsigned(off) ? part[threadIdx.x - off] : 0u);
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  unsigned run = (threadIdx.x ? part[threadIdx.x - 1] : 0u);
-  for (unsigned i = b0; i < b1; i++) {
-    const unsigned v = digtot[i];
-    digtot[i] = run;
-    run += v;
-  }
+  if (c == SCAN_C - 1 && d < radix) digtot[d] = run;
 }
 
 __global__ __launch_bounds__(RS_BS) void k_rs_scatter(const DevScalars* __restrict__ sc,
@@ -136,12 +134,32 @@ __global__ __launch_bounds__(RS_BS) void k_rs_scatter(const DevScalars* __restri
   constexpr int NW = RS_BS / 64;
   __shared__ unsigned s_off[1 << RS_MAXBITS];
   __shared__ unsigned s_wc[NW][1 << RS_MAXBITS];
+  __shared__ unsigned s_part[RS_BS];
   const unsigned radix = 1u << rbits, mask = radix - 1;
   const unsigned n = sc->ndiv;
   const unsigned base = blockIdx.x * RS_TILE;
   if (base >= n) return;  // whole block uniform
+  // exclusive scan of the digit totals (<= 2048, contiguous per thread) in LDS
+  const unsigned per = (radix + RS_BS - 1) / RS_BS, d0 = threadIdx.x * per, d1 = min(d0 + per, radix);
+  unsigned run = 0;
+  for (unsigned d = d0; d < d1; d++) {
+    const unsigned v = digtot[d];
+    s_off[d] = run;
+    run += v;
+  }
+  s_part[threadIdx.x] = run;
+  __syncthreads();
+  for (int off = 1; off < RS_BS; off <<= 1) {
+    const unsigned v = threadIdx.x >= unsigned(off) ? s_part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    s_part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  const unsigned pre = threadIdx.x ? s_part[threadIdx.x - 1] : 0u;
+  for (unsigned d = d0; d < d1; d++) s_off[d] += pre;
+  __syncthreads();
   for (unsigned d = threadIdx.x; d < radix; d += RS_BS) {
-    s_off[d] = digtot[d] + hist[d * ntiles + blockIdx.x];
+    s_off[d] += hist[size_t(blockIdx.x) * radix + d];
 #pragma unroll
     for (int w = 0; w < NW; w++) s_wc[w][d] = 0;
   }
@@ -202,8 +220,7 @@ int launch_radix_sort(hipStream_t stm, unsigned cap, const DevScalars* sc, SortS
     const unsigned shift = p * rbits;
     const unsigned radix = 1u << rbits;
     hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(RS_BS), 0, stm, sc, s.keys[cur], shift, rbits, ntiles, s.hist);
-    hipLaunchKernelGGL(k_rs_scan_rows, dim3(radix), dim3(256), 0, stm, s.hist, ntiles, s.digtot);
-    hipLaunchKernelGGL(k_rs_scan_digits, dim3(1), dim3(256), 0, stm, s.digtot, radix);
+    hipLaunchKernelGGL(k_rs_scan_tiles, dim3((radix + SCAN_D - 1) / SCAN_D), dim3(256), 0, stm, s.hist, ntiles, radix, s.digtot);
     hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(RS_BS), 0, stm, sc, s.keys[cur], s.vals[cur],
                        s.keys[cur ^ 1], s.vals[cur ^ 1], shift, rbits, ntiles, s.hist, s.digtot);
     cur ^= 1;
