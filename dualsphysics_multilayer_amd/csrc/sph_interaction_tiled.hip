@@ -588,7 +588,14 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
         }
       }
       {  // items hold <= TB particles: one p1 per lane
+#ifndef SPH_LANEORDER
+#define SPH_LANEORDER 1
+#endif
+#if SPH_LANEORDER
         const unsigned p1 = item.z + lane_order(poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
+#else
+        const unsigned p1 = item.z + threadIdx.x;
+#endif
         const bool act = threadIdx.x < item.w - item.z;
         P1 p;
         int cx1 = a;

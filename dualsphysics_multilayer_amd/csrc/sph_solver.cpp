@@ -287,6 +287,7 @@ SphGpuSingle::~SphGpuSingle() {
   Free();
   for (auto& e : pending_) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto e : evpool_) (void)hipEventDestroy(e);
+  if (xev_) (void)hipEventDestroy(xev_);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -494,6 +495,7 @@ void SphGpuSingle::Timing(double out_ms[4], uint64_t* launches) {
 void SphGpuSingle::Exchange() {
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET), withpre = havepre_;
   const bool hl = transport_->has_left(), hr = transport_->has_right();
+  if (!hl && !hr) return;  // a slab alone holds the whole domain: no ghosts, no migrants
   auto pack = [&] {
     launch_slab_pack(stream, cap_, sc_, cur_, G, K, C.dom_posmin, hl, hr, withm1, withpre, packtiles_, slabcnt_,
                      send_);
@@ -504,7 +506,16 @@ void SphGpuSingle::Exchange() {
                        hr ? 16 : 0, stream);
   check_hip(hipMemcpyAsync(slabcnt_host_, slabcnt_, sizeof(SlabCounts), hipMemcpyDeviceToHost, stream),
             "exchange: read counts");
-  Sync();
+  // The receive sizes must be on the host before the data transfers are posted: the one
+  // host wait of a step.  Spin on an event (a blocking synchronise wakes up tens of us
+  // later); the GPU idles from the counts copy until the next launches arrive.
+  if (!xev_) check_hip(hipEventCreateWithFlags(&xev_, hipEventDisableTiming), "hipEventCreate");
+  check_hip(hipEventRecord(xev_, stream), "exchange: event");
+  for (;;) {
+    const hipError_t q = hipEventQuery(xev_);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) check_hip(q, "exchange: wait counts");
+  }
   const SlabCounts c = *slabcnt_host_;
   const unsigned long long gneed = std::max(c.sendl[0], c.sendr[0]), mneed = std::max(c.sendl[1], c.sendr[1]);
   if (gneed > send_.gcap || mneed > send_.mcap) {  // records past a capacity were not written: grow, pack again
@@ -655,7 +666,8 @@ SphRunStats SphGpuSingle::Stats() {
   r.last_dt = s.last_dt;
   r.sym_dtpre = s.symdtpre;
   r.nstep = s.nstep;
-  r.np = slab() ? s.nown : s.np;  // a slab reports the particles it owns (no ghosts)
+  // a slab reports the particles it owns (no ghosts); alone it holds exactly those
+  r.np = (slab() && (transport_->has_left() || transport_->has_right())) ? s.nown : s.np;
   r.npb = s.npb;
   r.npbok = s.npbok;
   r.nout = s.nout;

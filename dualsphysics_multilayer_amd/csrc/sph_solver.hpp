@@ -132,6 +132,7 @@ class SphGpuSingle {
   struct Ev { hipEvent_t a, b; int phase; };
   std::vector<Ev> pending_;
   std::vector<hipEvent_t> evpool_;
+  hipEvent_t xev_ = nullptr;  // exchange: counts arrived on the host (spin-waited)
   double phase_ms_[4] = {0, 0, 0, 0};
   uint64_t phase_n_[4] = {0, 0, 0, 0};
   hipEvent_t cur_a_ = nullptr;
