@@ -1,11 +1,11 @@
-"""ctypes mirror of the POD structs in include/sphcore.h (ABI version 2)."""
+"""ctypes mirror of the POD structs in include/sphcore.h (ABI version 3)."""
 from __future__ import annotations
 
 import ctypes as C
 
 import numpy as np
 
-SPH_ABI_VERSION = 2
+SPH_ABI_VERSION = 3
 
 SPH_STATUS = {
     0: "SPH_OK",
@@ -18,6 +18,11 @@ SPH_STATUS = {
     7: "SPH_ERR_UNSUPPORTED",
     8: "SPH_ERR_COMM",
 }
+
+
+SPH_BOUND_DBC, SPH_BOUND_MDBC = 1, 2
+SPH_SLIP_VEL0, SPH_SLIP_NOSLIP, SPH_SLIP_FREESLIP = 1, 2, 3
+_CASEDEF_DEFAULTS = {"tboundary": SPH_BOUND_DBC, "slipmode": SPH_SLIP_VEL0, "mdbc_threshold": 0.0}
 
 
 class SphCaseDef(C.Structure):
@@ -49,13 +54,19 @@ class SphCaseDef(C.Structure):
         ("celldomfixed", C.c_int),
         ("npb", C.c_uint32),
         ("np", C.c_uint32),
+        ("tboundary", C.c_int32),
+        ("slipmode", C.c_int32),
+        ("mdbc_threshold", C.c_double),
     ]
 
     @classmethod
     def from_dict(cls, d: dict) -> "SphCaseDef":
         s = cls()
         for name, ctype in cls._fields_:
-            v = d[name]
+            if name not in d and name in _CASEDEF_DEFAULTS:
+                v = _CASEDEF_DEFAULTS[name]
+            else:
+                v = d[name]
             if isinstance(v, (tuple, list)):
                 arr = getattr(s, name)
                 for i, x in enumerate(v):
@@ -103,6 +114,10 @@ class SphConstants(C.Structure):
         ("dom_posmin", C.c_double * 3),
         ("dom_cells", C.c_uint32 * 3),
         ("dom_cellcode", C.c_uint32),
+        ("tboundary", C.c_int32),
+        ("slipmode", C.c_int32),
+        ("mdbc_threshold", C.c_float),
+        ("pad1", C.c_uint32),
     ]
 
     def as_dict(self) -> dict:
@@ -143,6 +158,7 @@ class SphParticlesHost(C.Structure):
         ("vel", C.POINTER(C.c_float)),
         ("rhop", C.POINTER(C.c_float)),
         ("code", C.POINTER(C.c_uint16)),
+        ("boundnormal", C.POINTER(C.c_float)),
     ]
 
 
@@ -255,12 +271,14 @@ def _ptr(arr: np.ndarray | None, ctype):
 class HostParticles:
     """Owns numpy arrays and exposes them as an SphParticlesHost view."""
 
-    def __init__(self, n: int, idp=None, pos=None, vel=None, rhop=None, code=None):
+    def __init__(self, n: int, idp=None, pos=None, vel=None, rhop=None, code=None, boundnormal=None):
         self.idp = np.ascontiguousarray(idp if idp is not None else np.zeros(n, np.uint32), dtype=np.uint32)
         self.pos = np.ascontiguousarray(pos if pos is not None else np.zeros((n, 3)), dtype=np.float64)
         self.vel = np.ascontiguousarray(vel if vel is not None else np.zeros((n, 3), np.float32), dtype=np.float32)
         self.rhop = np.ascontiguousarray(rhop if rhop is not None else np.zeros(n, np.float32), dtype=np.float32)
         self.code = np.ascontiguousarray(code if code is not None else np.zeros(n, np.uint16), dtype=np.uint16)
+        self.boundnormal = (None if boundnormal is None
+                            else np.ascontiguousarray(boundnormal, dtype=np.float32).reshape(n, 3))
         self.view = SphParticlesHost(
             n,
             _ptr(self.idp, C.c_uint32),
@@ -268,6 +286,7 @@ class HostParticles:
             _ptr(self.vel, C.c_float),
             _ptr(self.rhop, C.c_float),
             _ptr(self.code, C.c_uint16),
+            _ptr(self.boundnormal, C.c_float),
         )
 
     def trimmed(self, n: int) -> dict:

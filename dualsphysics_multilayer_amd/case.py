@@ -69,6 +69,9 @@ class DamBreakCase:
     gamma: float = 7.0
     coefsound: float = 20.0
     coefh: float = 1.0
+    tboundary: int = 1  # 1 DBC, 2 mDBC (<parameter Boundary>, JSph.cpp:626-640)
+    slipmode: int = 1  # mDBC: only SLIP_Vel0 in this fork (JSph.cpp:788)
+    mdbc_threshold: float = 0.0  # -mdbc_threshold (JSphCfgRun.cpp:124)
     # generated
     pos: np.ndarray = field(init=False, repr=False)
     vel: np.ndarray = field(init=False, repr=False)
@@ -85,6 +88,7 @@ class DamBreakCase:
         k, j, i = np.meshgrid(np.arange(nz + 1), np.arange(ny + 1), np.arange(nx + 1), indexing="ij")
         wall = (k == 0) | (i == 0) | (i == nx) | (j == 0) | (j == ny)
         bi, bj, bk = i[wall], j[wall], k[wall]
+        self._wall_ijk = (bi, bj, bk, nx, ny)
         # Fluid: i in [1,mx], j in [1,my-1], k in [1,mz], loop order k, j, i.
         fk, fj, fi = np.meshgrid(np.arange(1, mz + 1), np.arange(1, my), np.arange(1, mx + 1), indexing="ij")
         ii = np.concatenate([bi, fi.ravel()]).astype(np.float64)
@@ -107,6 +111,31 @@ class DamBreakCase:
         z = self.pos[self.npb :, 2]
         rhop[self.npb :] = (rho0 * np.power(1.0 + rho0 * g * (hswl - z) / b, 1.0 / gamma)).astype(np.float32)
         self.rhop = rhop
+
+    def normals_double(self) -> np.ndarray:
+        """Final normals of the boundary particles (double3[npb]), what GenCase stores in
+        <case>_Normals.nbi4 (PartNormals, JPartNormalData.cpp:178-207) and what
+        oracle/tools/gencase_ref writes: from the particle to the boundary limit, dp/2
+        beyond the wall layer towards the fluid (summed over the walls of edges/corners)."""
+        bi, bj, bk, nx, ny = self._wall_ijk
+        hd = self.dp * 0.5
+        nor = np.zeros((bi.size, 3))
+        nor[:, 0] = np.where(bi == 0, hd, np.where(bi == nx, -hd, 0.0))
+        nor[:, 1] = np.where(bj == 0, hd, np.where(bj == ny, -hd, 0.0))
+        nor[:, 2] = np.where(bk == 0, hd, 0.0)
+        return nor
+
+    @property
+    def boundnormal(self) -> np.ndarray | None:
+        """Per-particle normals as JSph::LoadBoundNormals holds them (float3, zero for
+        fluid), or None without mDBC."""
+        if self.tboundary != 2:
+            return None
+        if getattr(self, "_boundnormal", None) is not None:
+            return self._boundnormal
+        out = np.zeros((self.np, 3), np.float32)
+        out[: self.npb] = self.normals_double().astype(np.float32)
+        return out
 
     @property
     def nf(self) -> int:
@@ -137,6 +166,10 @@ class DamBreakCase:
         (MapPosMin/Max), simulated time TimeStep (apply with solver.set_time)."""
         import copy
 
+        if self.tboundary == 2:
+            # JSph::ConfigBoundNormals needs the extra-data files of the run to restart
+            # with mDBC (JSph.cpp:1308-1315), which this core does not write.
+            raise NotImplementedError("restart with mDBC needs the reference's extra data files")
         c = copy.copy(self)
         c.idp = np.ascontiguousarray(particles["idp"], np.uint32)
         c.pos = np.ascontiguousarray(particles["pos"], np.float64)
@@ -196,6 +229,9 @@ class DamBreakCase:
             celldomfixed=int(self.celldomfixed),
             npb=self.npb,
             np=self.np,
+            tboundary=self.tboundary,
+            slipmode=self.slipmode,
+            mdbc_threshold=self.mdbc_threshold,
         )
 
 

@@ -65,6 +65,8 @@ EXPORTED_SYMBOLS = (
     "sph_part_read",
     "sph_part_write",
     "sph_part_head_write",
+    "sph_normals_read",
+    "sph_normals_write",
     "sph_bi4_rewrite",
 )
 
@@ -117,6 +119,9 @@ def load_library(path: str = LIB_PATH):
     L.sph_part_write.argtypes = [C.c_char_p, C.POINTER(SphPartHeader), vp]
     L.sph_bi4_rewrite.argtypes = [C.c_char_p, C.c_char_p]
     L.sph_part_head_write.argtypes = [C.c_char_p, C.POINTER(SphPartHeader)]
+    L.sph_normals_read.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
+    L.sph_normals_write.argtypes = [C.c_char_p, C.c_char_p, C.c_double, C.c_double, C.c_double, C.c_uint32,
+                                    C.POINTER(C.c_double)]
     if L.sph_abi_version() != SPH_ABI_VERSION:
         raise SphError(3, "ABI version mismatch")
     _lib = L
@@ -142,7 +147,7 @@ class SphGpuSingle:
         L = load_library()
         self.case = case
         self._cdef = SphCaseDef.from_dict(case.case_def())
-        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop)
+        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop, boundnormal=getattr(case, "boundnormal", None))
         h = C.c_void_p()
         _check(L.sph_solver_create(C.byref(self._cdef), C.byref(init.view), device, C.byref(h)))
         self._h = h
@@ -241,7 +246,7 @@ class SphGpuSingle:
 def slab_partition(case, nranks: int, bound_weight: float = 0.3) -> np.ndarray:
     """x-cell column bounds [nranks+1] balancing fluid + bound_weight*bound particles."""
     cdef = SphCaseDef.from_dict(case.case_def())
-    init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop)
+    init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop, boundnormal=getattr(case, "boundnormal", None))
     out = np.zeros(nranks + 1, np.int32)
     _check(load_library().sph_slab_partition(C.byref(cdef), C.byref(init.view), nranks, bound_weight,
                                              out.ctypes.data_as(C.POINTER(C.c_int32))))
@@ -266,7 +271,7 @@ class SphGpuSlab(SphGpuSingle):
         L = load_library()
         self.case = case
         self._cdef = SphCaseDef.from_dict(case.case_def())
-        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop)
+        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop, boundnormal=getattr(case, "boundnormal", None))
         sd = SphSlabDef(rank, nranks, int(bounds[rank]), int(bounds[rank + 1]))
         C.memmove(sd.comm_id, comm_id, 128)
         h = C.c_void_p()
@@ -301,7 +306,7 @@ class SphSlabGroup:
         devices = np.ascontiguousarray(devices if devices is not None else np.zeros(n), np.int32)
         self.case = case
         self._cdef = SphCaseDef.from_dict(case.case_def())
-        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop)
+        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop, boundnormal=getattr(case, "boundnormal", None))
         h = C.c_void_p()
         _check(L.sph_slab_group_create(C.byref(self._cdef), C.byref(init.view), n,
                                        devices.ctypes.data_as(C.POINTER(C.c_int32)),
@@ -371,6 +376,23 @@ def write_part_head(path: str, header: dict) -> None:
     """Part_Head.ibi4 (JPartDataHead) for a restart directory."""
     h = SphPartHeader.from_dict(header)
     _check(load_library().sph_part_head_write(os.fsencode(path), C.byref(h)))
+
+
+def read_normals(path: str) -> np.ndarray:
+    """<case>_Normals.nbi4 (JPartNormalData::LoadFile): PartNormals, double3[Nbound]."""
+    L = load_library()
+    n = C.c_uint32(0)
+    _check(L.sph_normals_read(os.fsencode(path), 0, None, C.byref(n)))
+    out = np.zeros((n.value, 3), np.float64)
+    _check(L.sph_normals_read(os.fsencode(path), n.value, out.ctypes.data_as(C.POINTER(C.c_double)), C.byref(n)))
+    return out
+
+
+def write_normals(path: str, normals: np.ndarray, dp: float, h: float, case_name: str = "") -> None:
+    """<case>_Normals.nbi4 with the final normals of the boundary particles (as GenCase writes it)."""
+    nor = np.ascontiguousarray(normals, np.float64).reshape(-1, 3)
+    _check(load_library().sph_normals_write(os.fsencode(path), case_name.encode(), dp, h, 2.0 * h, len(nor),
+                                            nor.ctypes.data_as(C.POINTER(C.c_double))))
 
 
 def bi4_rewrite(src: str, dst: str) -> None:

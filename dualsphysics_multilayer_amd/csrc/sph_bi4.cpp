@@ -493,6 +493,46 @@ void part_head_write(const std::string& path, const SphPartHeader& h) {
   bi4::write_file(path, "JPartDataHead", root);
 }
 
+// ---- boundary normals (<case>_Normals.nbi4, JPartNormalData.cpp:178-257) -----------------
+// Root values FmtVersion, AppName, Date, CaseName, Data2d, Data2dPosY, Dp, H, Dist,
+// PartNormalsName, Nbound, CountNormals, plus the array PartNormals (double3[Nbound]):
+// the final normal of each boundary particle, from the particle to the boundary limit.
+static const char* kNormalsCode = "JPartNormalData";
+
+uint32_t normals_read(const std::string& path, uint32_t cap, double* out) {
+  const bi4::Item root = bi4::read_file(path, kNormalsCode);
+  const uint32_t nbound = uint32_t(root.get_uint("Nbound", 0));
+  const bi4::Array* a = root.array("PartNormals");
+  if (!a) throw SphError(SPH_ERR_ARG, "bi4: no PartNormals array in " + path);
+  if (a->type != bi4::Double3 || a->count != nbound)
+    throw SphError(SPH_ERR_ARG, "bi4: PartNormals is not double3[Nbound] in " + path);
+  if (out) {
+    if (cap < nbound) throw SphError(SPH_ERR_ARG, "bi4: normals buffer too small");
+    std::memcpy(out, a->bytes.data(), size_t(nbound) * 24);
+  }
+  return nbound;
+}
+
+void normals_write(const std::string& path, const char* case_name, double dp, double h, double dist, uint32_t nbound,
+                   const double* nor) {
+  bi4::Item root;
+  root.name = kNormalsCode;
+  root.set_pod("FmtVersion", bi4::Uint, uint32_t(1));
+  root.set_text("AppName", "dualsphysics_multilayer_amd");
+  root.set_text("Date", "");
+  root.set_text("CaseName", case_name ? case_name : "");
+  root.set_pod("Data2d", bi4::Bool, int32_t(0));
+  root.set_pod("Data2dPosY", bi4::Double, 0.0);
+  root.set_pod("Dp", bi4::Double, dp);
+  root.set_pod("H", bi4::Double, h);
+  root.set_pod("Dist", bi4::Double, dist);
+  root.set_text("PartNormalsName", "Plane");
+  root.set_pod("Nbound", bi4::Uint, nbound);
+  root.set_pod("CountNormals", bi4::Uint, uint32_t(0));
+  root.add_array("PartNormals", bi4::Double3, nbound, nor);
+  bi4::write_file(path, kNormalsCode, root);
+}
+
 void bi4_rewrite(const std::string& src, const std::string& dst) {
   // the file code is the header title after "#FileJBD " (up to the padding)
   std::ifstream f(src, std::ios::binary);

@@ -227,6 +227,17 @@ int sph_part_head_write(const char* path, const SphPartHeader* hdr) {
   return guard([&] { sphx::part_head_write(path, *hdr); });
 }
 
+int sph_normals_read(const char* path, uint32_t cap, double* out, uint32_t* nbound) {
+  NEED(path && nbound);
+  return guard([&] { *nbound = sphx::normals_read(path, cap, out); });
+}
+
+int sph_normals_write(const char* path, const char* case_name, double dp, double h, double dist, uint32_t nbound,
+                      const double* normals) {
+  NEED(path && (normals || !nbound));
+  return guard([&] { sphx::normals_write(path, case_name, dp, h, dist, nbound, normals); });
+}
+
 int sph_bi4_rewrite(const char* src, const char* dst) {
   NEED(src && dst);
   return guard([&] { sphx::bi4_rewrite(src, dst); });

@@ -61,6 +61,8 @@ struct KConst {
   float mhalfovh, bwenovh, ddtkhcs, ddtc1, ddtc2, ddtc3, ddtc4;
   int ddtseries;  // 1: |ddtgz*drz| <= 2h*ddtgz < 0.05 for every pair -> DDT2 hydrostatic term by series
   float ddte1, ddte2, ddte3, ddte4;  // the series in drz: rho0*((1+ddtgz*drz)^(1/gamma)-1) = drz*(e1+drz*(e2+...))
+  float awen;  // Wendland W normalisation (mDBC)
+  int mdbc;    // TBoundary == BC_MDBC: DDT (Molteni) keeps bound neighbours (JSphCpu.cpp:730)
 };
 
 // Cell grid of the (fixed) divide domain — StDivDataGpu (JCellDivDataGpu.h:26-79).

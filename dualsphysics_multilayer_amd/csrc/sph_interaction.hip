@@ -65,7 +65,7 @@ __device__ __forceinline__ void fluid_cell(const KConst& K, float rx, float ry, 
       a.ar += massp2 * (dvx * frx + dvy * fry + dvz * frz) * (vr1.w / vr2.w);
       // Density diffusion (JSphCpu.cpp:724-740).
       if (TDENSITY == 1 && a.delta != FLT_MAX) {
-        if (BOUNDP2) a.delta = FLT_MAX;  // DBC: DDT off next to the boundary
+        if (BOUNDP2 && !K.mdbc) a.delta = FLT_MAX;  // DBC: DDT off next to the boundary
         else {
           const float rhop1over2 = vr1.w / vr2.w;
           const float visc_densi = K.ddtkh * K.cs0f * (rhop1over2 - 1.f) / (rr2 + K.eta2);

@@ -258,7 +258,12 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
   a.ay = fmaf(c, dry, a.ay);
   a.az = fmaf(c, drz, a.az);
   if (MODE == 1) {
-    if ((TDENSITY == 1 || TDENSITY == 2) && ok) a.delta = FLT_MAX;  // DBC: no DDT next to the boundary
+    if (TDENSITY == 1 && K.mdbc) {  // mDBC: Molteni DDT over bound neighbours too (JSphCpu.cpp:730)
+      const float t = w3 * rr2 * inv_re;
+      a.delta = fmaf(t, fmaf(p.vr.w, C.y, -1.f), a.delta);
+    } else if ((TDENSITY == 1 || TDENSITY == 2) && ok) {
+      a.delta = FLT_MAX;  // DBC: no DDT next to the boundary
+    }
     return;
   }
   if (TDENSITY == 1) {
@@ -277,7 +282,7 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
 
 // The per-pass factors of the sums (PassK) applied once per particle.
 template <int TDENSITY, int MODE>
-__device__ __forceinline__ TAcc finish(TAcc a, const P1& p, const PassK& Q) {
+__device__ __forceinline__ TAcc finish(const KConst& K, TAcc a, const P1& p, const PassK& Q) {
   a.ar *= Q.ar1;
   if (MODE != 2) {
     const float s = -Q.bm * p.inv_rho;
@@ -285,7 +290,7 @@ __device__ __forceinline__ TAcc finish(TAcc a, const P1& p, const PassK& Q) {
     a.ay *= s;
     a.az *= s;
   }
-  if (MODE == 0) {
+  if (MODE == 0 || (MODE == 1 && TDENSITY == 1 && K.mdbc)) {
     if (TDENSITY == 1) a.delta *= Q.kd;
     else if (TDENSITY == 2 || TDENSITY == 3) a.delta *= -Q.kd;
   }
@@ -535,7 +540,7 @@ __device__ __forceinline__ TAcc run_pass(const KConst& K, const DivGrid& g, cons
       }
     }
   }
-  return finish<TDENSITY, MODE>(acc, p, Q);
+  return finish<TDENSITY, MODE>(K, acc, p, Q);
 }
 
 template <int TDENSITY>

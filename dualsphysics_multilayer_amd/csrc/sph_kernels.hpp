@@ -67,6 +67,12 @@ void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, Di
 void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
                         const float4* poscell, const float4* velrhop, const float* press, const unsigned* begincell,
                         DivGrid g, const KConst& K, float4* arace);
+// mDBC boundary correction (sph_mdbc.hip; JSphCpu.cpp:1020-1187): density of every
+// boundary particle p1 < npbok with a normal extrapolated from its ghost node; press
+// refreshed.  `normal` is indexed by idp.
+void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& cur, float* press,
+                 const float4* normal, const unsigned* begincell, DivGrid g, const KConst& K,
+                 const double dom_posmin[3], float threshold);
 // Pair counters (JDsPips).
 void launch_count_pairs(hipStream_t stm, unsigned cap, const DevScalars* sc, const float4* poscell,
                         const unsigned* begincell, DivGrid g, const KConst& K, unsigned long long* out6);

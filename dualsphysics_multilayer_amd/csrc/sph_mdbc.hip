@@ -1,0 +1,204 @@
+// sph_mdbc.hip — modified Dynamic Boundary Conditions (mDBC) on gfx950, SURVEY.md §8(f) row 1.
+//
+// Reference: JSphCpu::InteractionMdbcCorrectionT2<tker,sim2d=false,SLIP_Vel0>
+// (JSphCpu.cpp:1020-1187), called once per interaction before PreInteraction_Forces
+// except in the Symplectic corrector (JSphCpuSingle.cpp:525, MDBCCorrector=0); the GPU
+// twin is KerInteractionMdbcCorrection_Dbl (JSphGpu_ker.cu:1088-1250, the MDBCFastSingle=0
+// path: the 4x4 correction matrix accumulated and inverted in double, as the CPU does).
+//
+// For every boundary particle p1 < NpbOk with a normal, the ghost node sits at
+// pos + normal (normals already doubled by ConfigBoundNormals: particle -> ghost node).
+// Over the fluid particles within the support of the ghost node:
+//   rho_g     = sum m W,   grad rho_g = sum m gradW
+//   A (4x4)   = sum V [W, dx W, dy W, dz W; gradW, dx gradW, ...]   (V = m / rho2)
+// If |det A| >= 1e-3: the first-order extrapolation (A^-1 [rho_g, grad rho_g]) mirrored
+// back to the particle; else if A11 > 0 the Shepard value rho_g / A11; with no fluid the
+// density is RhopZero.  Vel0 keeps the boundary velocity (zero for fixed walls).
+//
+// Layout/parallelism: one lane per boundary particle (the boundary particles of one
+// cell row are consecutive, so the lanes of a wave walk the same neighbour rows and
+// their candidate loads coalesce).  Positions are read in double (posxy/posz) so the
+// distances are the reference's float(gpos - pos2) bit for bit.  The normals are kept
+// in case (idp) order — boundary ids are < CaseNbound and fixed boundaries never move —
+// so the divide never has to reorder them.  The corrected density also refreshes the
+// boundary particle's EOS pressure (PreInteraction recomputes it on the CPU).
+#include <cfloat>
+
+#include "sph_kernels.hpp"
+
+namespace sphx {
+
+struct MdbcArgs {
+  const unsigned* idp;
+  const typecode* code;
+  const double2* posxy;
+  const double* posz;
+  float4* velrhop;
+  float* press;
+  const float4* normal;  // [CaseNbound], by idp
+  const unsigned* bc;
+  double posminx, posminy, posminz, scelld;
+  float kernelsize2, ovh, awen, bwenovh, massfluid, rhopzero, threshold, determlimit;
+  float cteb, ovrhopzero, gamma;
+  int igamma;
+};
+
+// fmath::Determinant4x4 (FunctionsMath.h:186-199), double.
+struct M4 { double a11, a12, a13, a14, a21, a22, a23, a24, a31, a32, a33, a34, a41, a42, a43, a44; };
+__device__ inline double det4(const M4& d) {
+  return (d.a14 * d.a23 * d.a32 * d.a41 - d.a13 * d.a24 * d.a32 * d.a41 -
+          d.a14 * d.a22 * d.a33 * d.a41 + d.a12 * d.a24 * d.a33 * d.a41 +
+          d.a13 * d.a22 * d.a34 * d.a41 - d.a12 * d.a23 * d.a34 * d.a41 -
+          d.a14 * d.a23 * d.a31 * d.a42 + d.a13 * d.a24 * d.a31 * d.a42 +
+          d.a14 * d.a21 * d.a33 * d.a42 - d.a11 * d.a24 * d.a33 * d.a42 -
+          d.a13 * d.a21 * d.a34 * d.a42 + d.a11 * d.a23 * d.a34 * d.a42 +
+          d.a14 * d.a22 * d.a31 * d.a43 - d.a12 * d.a24 * d.a31 * d.a43 -
+          d.a14 * d.a21 * d.a32 * d.a43 + d.a11 * d.a24 * d.a32 * d.a43 +
+          d.a12 * d.a21 * d.a34 * d.a43 - d.a11 * d.a22 * d.a34 * d.a43 -
+          d.a13 * d.a22 * d.a31 * d.a44 + d.a12 * d.a23 * d.a31 * d.a44 +
+          d.a13 * d.a21 * d.a32 * d.a44 - d.a11 * d.a23 * d.a32 * d.a44 -
+          d.a12 * d.a21 * d.a33 * d.a44 + d.a11 * d.a22 * d.a33 * d.a44);
+}
+
+// EOS of the corrected density, as the gather evaluates it (sph_divide.hip gather_one).
+__device__ inline float eos_press(const MdbcArgs& a, float rho) {
+  const double xr = double(rho * a.ovrhopzero);
+  double xg;
+  if (a.igamma > 0) {
+    double r = 1.0, b = xr;
+    for (int e = a.igamma; e; e >>= 1) {
+      if (e & 1) r *= b;
+      b *= b;
+    }
+    xg = r;
+  } else {
+    xg = pow(xr, double(a.gamma));
+  }
+  return float(double(a.cteb) * (xg - 1.0));
+}
+
+__global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc, MdbcArgs a, DivGrid g) {
+  const unsigned p1 = blockIdx.x * 256 + threadIdx.x;
+  if (p1 >= sc->npbok) return;
+  const float4 bn = a.normal[a.idp[p1]];
+  if (bn.x == 0.f && bn.y == 0.f && bn.z == 0.f) return;
+  const double2 pxy = a.posxy[p1];
+  const double gx = pxy.x + double(bn.x), gy = pxy.y + double(bn.y), gz = a.posz[p1] + double(bn.z);
+  // nsearch::Init by position (JCellSearch_inline.h:52-67) on the full-map grid, the
+  // ranges clamped to the grid (equal to the reference's for a ghost node inside it).
+  const int cx = int((gx - a.posminx) / a.scelld) - g.xoff;
+  const int cy = int((gy - a.posminy) / a.scelld);
+  const int cz = int((gz - a.posminz) / a.scelld);
+  const int xini = max(cx - 1, 0), xfin = min(cx + 2, g.ncx);
+  const int yini = max(cy - 1, 0), yfin = min(cy + 2, g.ncy);
+  const int zini = max(cz - 1, 0), zfin = min(cz + 2, g.ncz);
+  float rhopp1 = 0.f, gx_ = 0.f, gy_ = 0.f, gz_ = 0.f, sumwab = 0.f;
+  M4 m = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if (xini < xfin) {
+    for (int z = zini; z < zfin; z++)
+      for (int y = yini; y < yfin; y++) {
+        const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+        const unsigned pini = a.bc[rowbase + xini], pfin = a.bc[rowbase + xfin];
+        for (unsigned p2 = pini; p2 < pfin; p2++) {
+          const double2 q = a.posxy[p2];
+          const float drx = float(gx - q.x);
+          const float dry = float(gy - q.y);
+          const float drz = float(gz - a.posz[p2]);
+          const float rr2 = drx * drx + dry * dry + drz * drz;
+          if (rr2 <= a.kernelsize2 && CodeIsFluid(a.code[p2])) {
+            // GetKernelWendland_WabFac (FunSphKernel.h:226-234); fac in its r -> 0
+            // form (bwen/h)(1-q/2)^3, finite when a fluid particle sits on the ghost node.
+            const float rad = sqrtf(rr2);
+            const float qq = rad * a.ovh;
+            const float wqq1 = 1.f - 0.5f * qq;
+            const float wqq2 = wqq1 * wqq1;
+            const float fac = a.bwenovh * wqq2 * wqq1;
+            const float wqq = qq + qq + 1.f;
+            const float wab = a.awen * wqq * wqq2 * wqq2;
+            const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
+            const float volp2 = a.massfluid / a.velrhop[p2].w;
+            rhopp1 += a.massfluid * wab;
+            gx_ += a.massfluid * frx;
+            gy_ += a.massfluid * fry;
+            gz_ += a.massfluid * frz;
+            const float vwab = wab * volp2;
+            sumwab += vwab;
+            const float vfrx = frx * volp2, vfry = fry * volp2, vfrz = frz * volp2;
+            m.a11 += vwab;  m.a12 += drx * vwab;  m.a13 += dry * vwab;  m.a14 += drz * vwab;
+            m.a21 += vfrx;  m.a22 += drx * vfrx;  m.a23 += dry * vfrx;  m.a24 += drz * vfrx;
+            m.a31 += vfry;  m.a32 += drx * vfry;  m.a33 += dry * vfry;  m.a34 += drz * vfry;
+            m.a41 += vfrz;  m.a42 += drx * vfrz;  m.a43 += dry * vfrz;  m.a44 += drz * vfrz;
+          }
+        }
+      }
+  }
+  const float thr = a.threshold;
+  if (!(sumwab >= thr || (thr >= 2.f && sumwab + 2.f >= thr))) return;
+  float rhopfinal = FLT_MAX;
+  const double determ = det4(m);
+  if (fabs(determ) >= double(a.determlimit)) {
+    // Rows of fmath::InverseMatrix4x4 (FunctionsMath.h:260-282) that the extrapolation reads.
+    const M4& d = m;
+    const double i11 = (d.a22 * (d.a33 * d.a44 - d.a34 * d.a43) + d.a23 * (d.a34 * d.a42 - d.a32 * d.a44) + d.a24 * (d.a32 * d.a43 - d.a33 * d.a42)) / determ;
+    const double i21 = (d.a21 * (d.a34 * d.a43 - d.a33 * d.a44) + d.a23 * (d.a31 * d.a44 - d.a34 * d.a41) + d.a24 * (d.a33 * d.a41 - d.a31 * d.a43)) / determ;
+    const double i31 = (d.a21 * (d.a32 * d.a44 - d.a34 * d.a42) + d.a22 * (d.a34 * d.a41 - d.a31 * d.a44) + d.a24 * (d.a31 * d.a42 - d.a32 * d.a41)) / determ;
+    const double i41 = (d.a21 * (d.a33 * d.a42 - d.a32 * d.a43) + d.a22 * (d.a31 * d.a43 - d.a33 * d.a41) + d.a23 * (d.a32 * d.a41 - d.a31 * d.a42)) / determ;
+    const double i12 = (d.a12 * (d.a34 * d.a43 - d.a33 * d.a44) + d.a13 * (d.a32 * d.a44 - d.a34 * d.a42) + d.a14 * (d.a33 * d.a42 - d.a32 * d.a43)) / determ;
+    const double i22 = (d.a11 * (d.a33 * d.a44 - d.a34 * d.a43) + d.a13 * (d.a34 * d.a41 - d.a31 * d.a44) + d.a14 * (d.a31 * d.a43 - d.a33 * d.a41)) / determ;
+    const double i32 = (d.a11 * (d.a34 * d.a42 - d.a32 * d.a44) + d.a12 * (d.a31 * d.a44 - d.a34 * d.a41) + d.a14 * (d.a32 * d.a41 - d.a31 * d.a42)) / determ;
+    const double i42 = (d.a11 * (d.a32 * d.a43 - d.a33 * d.a42) + d.a12 * (d.a33 * d.a41 - d.a31 * d.a43) + d.a13 * (d.a31 * d.a42 - d.a32 * d.a41)) / determ;
+    const double i13 = (d.a12 * (d.a23 * d.a44 - d.a24 * d.a43) + d.a13 * (d.a24 * d.a42 - d.a22 * d.a44) + d.a14 * (d.a22 * d.a43 - d.a23 * d.a42)) / determ;
+    const double i23 = (d.a11 * (d.a24 * d.a43 - d.a23 * d.a44) + d.a13 * (d.a21 * d.a44 - d.a24 * d.a41) + d.a14 * (d.a23 * d.a41 - d.a21 * d.a43)) / determ;
+    const double i33 = (d.a11 * (d.a22 * d.a44 - d.a24 * d.a42) + d.a12 * (d.a24 * d.a41 - d.a21 * d.a44) + d.a14 * (d.a21 * d.a42 - d.a22 * d.a41)) / determ;
+    const double i43 = (d.a11 * (d.a23 * d.a42 - d.a22 * d.a43) + d.a12 * (d.a21 * d.a43 - d.a23 * d.a41) + d.a13 * (d.a22 * d.a41 - d.a21 * d.a42)) / determ;
+    const double i14 = (d.a12 * (d.a24 * d.a33 - d.a23 * d.a34) + d.a13 * (d.a22 * d.a34 - d.a24 * d.a32) + d.a14 * (d.a23 * d.a32 - d.a22 * d.a33)) / determ;
+    const double i24 = (d.a11 * (d.a23 * d.a34 - d.a24 * d.a33) + d.a13 * (d.a24 * d.a31 - d.a21 * d.a34) + d.a14 * (d.a21 * d.a33 - d.a23 * d.a31)) / determ;
+    const double i34 = (d.a11 * (d.a24 * d.a32 - d.a22 * d.a34) + d.a12 * (d.a21 * d.a34 - d.a24 * d.a31) + d.a14 * (d.a22 * d.a31 - d.a21 * d.a32)) / determ;
+    const double i44 = (d.a11 * (d.a22 * d.a33 - d.a23 * d.a32) + d.a12 * (d.a23 * d.a31 - d.a21 * d.a33) + d.a13 * (d.a21 * d.a32 - d.a22 * d.a31)) / determ;
+    const float rhoghost = float(i11 * rhopp1 + i12 * gx_ + i13 * gy_ + i14 * gz_);
+    const float grx = -float(i21 * rhopp1 + i22 * gx_ + i23 * gy_ + i24 * gz_);
+    const float gry = -float(i31 * rhopp1 + i32 * gx_ + i33 * gy_ + i34 * gz_);
+    const float grz = -float(i41 * rhopp1 + i42 * gx_ + i43 * gy_ + i44 * gz_);
+    // dpos = boundary particle - ghost node = -normal
+    rhopfinal = (rhoghost + grx * (-bn.x) + gry * (-bn.y) + grz * (-bn.z));
+  } else if (m.a11 > 0) {
+    rhopfinal = float(rhopp1 / m.a11);
+  }
+  rhopfinal = (rhopfinal != FLT_MAX ? rhopfinal : a.rhopzero);
+  a.velrhop[p1].w = rhopfinal;  // SLIP_Vel0: density only
+  a.press[p1] = eos_press(a, rhopfinal);
+}
+
+void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& cur, float* press,
+                 const float4* normal, const unsigned* begincell, DivGrid g, const KConst& K,
+                 const double dom_posmin[3], float threshold) {
+  if (!npbcap) return;
+  MdbcArgs a;
+  a.idp = cur.idp;
+  a.code = cur.code;
+  a.posxy = cur.posxy;
+  a.posz = cur.posz;
+  a.velrhop = cur.velrhop;
+  a.press = press;
+  a.normal = normal;
+  a.bc = begincell;
+  a.posminx = dom_posmin[0];
+  a.posminy = dom_posmin[1];
+  a.posminz = dom_posmin[2];
+  a.scelld = K.scelld;
+  a.kernelsize2 = K.kernelsize2;
+  a.ovh = K.ovkernelh;
+  a.awen = K.awen;
+  a.bwenovh = K.bwenovh;
+  a.massfluid = K.massfluid;
+  a.rhopzero = K.rhopzero;
+  a.threshold = threshold;
+  a.determlimit = 1e-3f;  // JSphCpu.cpp:1197
+  a.cteb = K.cteb;
+  a.ovrhopzero = K.ovrhopzero;
+  a.gamma = K.gamma;
+  a.igamma = (K.gamma == float(int(K.gamma)) && K.gamma >= 1.f && K.gamma <= 16.f) ? int(K.gamma) : 0;
+  hipLaunchKernelGGL(k_mdbc, dim3((npbcap + 255) / 256), dim3(256), 0, stm, sc, a, g);
+}
+
+}  // namespace sphx

@@ -83,6 +83,14 @@ void derive_constants(const SphCaseDef& c, SphConstants& k) {
   }
   k.dom_cellcode = cell_code(k.dom_cells[0] + 1, k.dom_cells[1] + 1, k.dom_cells[2] + 1);
   if (!k.dom_cellcode) throw SphError(SPH_ERR_ARG, "failed to select a valid CellCode");
+  // Boundary configuration (JSph.cpp:626-640, 785-790).
+  k.tboundary = (c.tboundary == 0 ? SPH_BOUND_DBC : c.tboundary);
+  if (k.tboundary != SPH_BOUND_DBC && k.tboundary != SPH_BOUND_MDBC)
+    throw SphError(SPH_ERR_ARG, "Boundary Condition method is not valid.");
+  k.slipmode = (k.tboundary == SPH_BOUND_MDBC ? (c.slipmode == 0 ? SPH_SLIP_VEL0 : c.slipmode) : SPH_SLIP_VEL0);
+  if (k.slipmode != SPH_SLIP_VEL0)
+    throw SphError(SPH_ERR_UNSUPPORTED, "Only the slip mode velocity=0 is allowed with mDBC conditions.");
+  k.mdbc_threshold = (k.tboundary == SPH_BOUND_MDBC ? float(c.mdbc_threshold) : 0.f);
 }
 
 static KConst make_kconst(const SphConstants& c) {
@@ -127,6 +135,8 @@ static KConst make_kconst(const SphConstants& c) {
   K.mhalfovh = -0.5f * K.ovkernelh;
   K.bwenovh = c.bwen * K.ovkernelh;
   K.ddtkhcs = c.ddtkh * K.cs0f;
+  K.awen = c.awen;
+  K.mdbc = (c.tboundary == SPH_BOUND_MDBC) ? 1 : 0;
   {  // binomial coefficients of (1+x)^(1/gamma) - 1
     const double a = 1.0 / double(c.gamma);
     K.ddtc1 = float(a);
@@ -226,6 +236,8 @@ SphGpuSingle::SphGpuSingle(const SphCaseDef& cdef, const SphParticlesHost& all, 
   if (!transport_) throw SphError(SPH_ERR_ARG, "slab without a transport");
   if (transport_->rank != slab.rank || transport_->nranks != slab.nranks)
     throw SphError(SPH_ERR_ARG, "slab rank does not match the transport");
+  if (cdef.tboundary == SPH_BOUND_MDBC)
+    throw SphError(SPH_ERR_UNSUPPORTED, "mDBC is not implemented on the slab decomposition");
   Init(cdef, all);
 }
 
@@ -266,6 +278,7 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
     AllocFixed();
     AllocParticles(cap_);
     Upload(init, sel, nown);
+    if (C.tboundary == SPH_BOUND_MDBC) UploadNormals(cdef, init);
     // ConfigDomain: RunCellDivide(true) (JSphCpuSingle.cpp:165-166), then InitRunGpu.
     RunCellDivide();
     exchange_armed_ = true;
@@ -442,6 +455,26 @@ void SphGpuSingle::Upload(const SphParticlesHost& h, const std::vector<unsigned>
   verletstep_ = 0;
 }
 
+// JSph::LoadBoundNormals + ConfigBoundNormals (JSph.cpp:1265-1340): the case's normals
+// (particle -> boundary limit) as float, doubled (particle -> ghost node), kept by idp.
+void SphGpuSingle::UploadNormals(const SphCaseDef& cdef, const SphParticlesHost& h) {
+  if (!h.boundnormal) throw SphError(SPH_ERR_ARG, "mDBC needs the boundary normals (<case>_Normals.nbi4)");
+  const unsigned nbound = cdef.npb;
+  std::vector<float4> nor(std::max(nbound, 1u), make_float4(0.f, 0.f, 0.f, 0.f));
+  unsigned nerr = 0;
+  for (unsigned p = 0; p < h.n; p++) {
+    const unsigned id = h.idp[p];
+    if (id >= nbound) continue;
+    const float x = h.boundnormal[3 * p], y = h.boundnormal[3 * p + 1], z = h.boundnormal[3 * p + 2];
+    if (x == 0.f && y == 0.f && z == 0.f) nerr++;
+    nor[id] = make_float4(x * 2.f, y * 2.f, z * 2.f, 0.f);
+  }
+  if (nerr == nbound) throw SphError(SPH_ERR_ARG, "No valid normal vectors for using mDBC.");
+  check_hip(hipMalloc((void**)&normal_, sizeof(float4) * nor.size()), "hipMalloc normals");
+  allocs_.push_back(normal_);
+  check_hip(hipMemcpy(normal_, nor.data(), sizeof(float4) * nor.size(), hipMemcpyHostToDevice), "upload normals");
+}
+
 // Restart: TimeStep and SymplecticDtPre of the loaded PART (JSph::InitRun, JSph.cpp:2094-2106).
 void SphGpuSingle::SetTime(double time, double symdtpre) {
   Sync();
@@ -579,7 +612,9 @@ void SphGpuSingle::RunCellDivide() {
 }
 
 void SphGpuSingle::Interaction_Forces(int interstep) {
-  (void)interstep;  // mDBC / shifting are not on this path
+  // mDBC boundary correction first, except in the Symplectic corrector (JSphCpuSingle.cpp:525).
+  if (normal_ && interstep != 3)
+    launch_mdbc(stream, npb0_, sc_, cur_, press_, normal_, begincell_, G, K, C.dom_posmin, C.mdbc_threshold);
   if (tiled_) {
     // The tiled kernel writes the arace of every owned particle (skipped boundary items
     // get ar = 0) and resets its own work counters at exit (zeroed once at allocation).

@@ -35,6 +35,9 @@ void part_read(const std::string& path, SphPartHeader& h, SphParticlesHost* out)
 void part_write(const std::string& path, const SphPartHeader& h, const SphParticlesHost& p);
 void part_head_write(const std::string& path, const SphPartHeader& h);
 void bi4_rewrite(const std::string& src, const std::string& dst);
+uint32_t normals_read(const std::string& path, uint32_t cap, double* out);
+void normals_write(const std::string& path, const char* case_name, double dp, double h, double dist, uint32_t nbound,
+                   const double* nor);
 
 // This rank's slab: owned global x-cell columns [c0, c1) of nranks.
 struct SlabConfig {
@@ -87,6 +90,7 @@ class SphGpuSingle {
   void Free();
   void Grow(unsigned np_live, unsigned newcap);
   void Upload(const SphParticlesHost& init, const std::vector<unsigned>& sel, unsigned nown);
+  void UploadNormals(const SphCaseDef& cdef, const SphParticlesHost& init);
   void Exchange();
   void TimedBegin(int phase);
   void TimedEnd(int phase);
@@ -98,6 +102,7 @@ class SphGpuSingle {
   PartArrays cur_, alt_;
   float4* poscell_ = nullptr;
   float* press_ = nullptr;
+  float4* normal_ = nullptr;      // mDBC: particle -> ghost node, by idp [CaseNbound]
   float4* arace_ = nullptr;
   unsigned* begincell_ = nullptr;
   uint4* items_ = nullptr;        // tiled-interaction work items (per divide)

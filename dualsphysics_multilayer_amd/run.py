@@ -212,7 +212,7 @@ class CaseRun:
 USAGE = """usage: python -m dualsphysics_multilayer_amd <case> [<dirout>] [options]
   <case>        case path without extension (<case>.xml + <case>.bi4)
   options (as DualSPHysics): -gpu[:id] -symplectic -verlet[:steps] -wendland -viscoart:v
-  -viscoboundfactor:v -ddt:0..3 -ddtvalue:v -dbc -cellmode:full -cellfixed[:0|1]
+  -viscoboundfactor:v -ddt:0..3 -ddtvalue:v -dbc -mdbc -mdbc_threshold:v -cellmode:full -cellfixed[:0|1]
   -saveposdouble[:0|1] -sv:binx|none -partbegin:n <dir> -rhopout:min:max -cfl:v -tmax:t
   -tout:t -domain_fixed:xmin:ymin:zmin:xmax:ymax:zmax -nsteps:n -svsteps[:0|1] -nortimes[:0|1]
   -dirout <dir> -name <case> -stable -svres -svtimers -ompthreads:n (accepted, no effect)"""
@@ -250,7 +250,9 @@ def parse_args(argv: list[str]) -> dict:
             o["device"] = int(full) if full else 0
         elif word == "CPU":
             raise CaseError("this core runs on the GPU (-cpu is the reference's CPU solver).")
-        elif word in ("STABLE", "SVRES", "SVTIMERS", "SVDOMAINVTK", "CREATEDIRS", "CSVSEP", "OMPTHREADS", "DBC",
+        elif word == "DBC":
+            ov["tboundary"], ov["slipmode"] = 1, 1
+        elif word in ("STABLE", "SVRES", "SVTIMERS", "SVDOMAINVTK", "CREATEDIRS", "CSVSEP", "OMPTHREADS",
                       "WENDLAND"):
             pass  # the sort is always stable; logs / threads / defaults have no effect here
         elif word == "SAVEPOSDOUBLE":
@@ -261,9 +263,19 @@ def parse_args(argv: list[str]) -> dict:
                 raise CaseError("Only -cellmode:full runs on the GPU path.")
         elif word == "CELLFIXED":
             ov["celldomfixed"] = (int(full) if full else 1) != 0
-        elif word in ("MDBC", "MDBC_NOSLIP", "MDBC_FREESLIP", "MDBC_FAST", "MDBC_THRESHOLD", "INITNORPLA",
-                      "INITNORPART", "SVNORMALS"):
-            raise CaseError("mDBC boundaries are not supported by this core.")
+        elif word == "MDBC":  # JSphCfgRun.cpp:306, JSph::LoadConfigCommands (JSph.cpp:766-790)
+            ov["tboundary"], ov["slipmode"] = 2, 1
+        elif word in ("MDBC_NOSLIP", "MDBC_FREESLIP"):
+            raise CaseError("Only the slip mode velocity=0 is allowed with mDBC conditions.")
+        elif word == "MDBC_THRESHOLD":
+            v = _f32(full)
+            if not 0 <= v:
+                raise CaseError(f"invalid option {a}")
+            ov["mdbc_threshold"] = v
+        elif word == "MDBC_FAST":
+            pass  # the correction is always accumulated and inverted in double (the CPU path)
+        elif word in ("INITNORPLA", "INITNORPART", "SVNORMALS"):
+            raise CaseError(f"-{w.lower()} is not supported by this core (normals come from <case>_Normals.nbi4).")
         elif word == "SYMPLECTIC":
             ov["step_algorithm"] = 2
         elif word == "VERLET":

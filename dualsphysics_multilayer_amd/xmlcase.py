@@ -244,7 +244,7 @@ def _config_domain(p: _Params) -> _DomainCfg:
 # command-line overrides (JSphCfgRun -> JSph::LoadConfigCommands) this core takes
 OVERRIDES = ("step_algorithm", "verlet_steps", "tdensity", "ddtvalue", "visco", "viscoboundfactor", "cellmode",
              "celldomfixed", "cflnumber", "rhopoutmin", "rhopoutmax", "timemax", "timeout", "dtini", "dtmin",
-             "coefdtmin", "domain_fixed")
+             "coefdtmin", "domain_fixed", "tboundary", "slipmode", "mdbc_threshold")
 
 
 class XmlCase:
@@ -299,6 +299,8 @@ class XmlCase:
                             f"[{self.rhopoutmin},{self.rhopoutmax}].")
         if self.cellmode != CELLMODE_FULL:
             raise CaseError("Only CellMode=full runs on the GPU path.")
+        if self.tboundary == 2 and self.slipmode != 1:  # JSph.cpp:788
+            raise CaseError("Only the slip mode velocity=0 is allowed with mDBC conditions.")
         # -- particles (JPartsLoad4::LoadParticles) ------------------------------------
         self.partbegin = int(partbegin)
         if self.partbegin:
@@ -338,6 +340,33 @@ class XmlCase:
             dmin, dmax = self._domain.resize(rmin, rmax, self.data2d)
             self._map = (np.array(dmin), np.array(dmax))
         # JSph::CheckRhopLimits (JSph.cpp:2021-2030) is done by the core at creation.
+        self._boundnormal = None
+        if self.tboundary == 2:
+            self._boundnormal = self._load_normals()
+
+    # -- JSph::LoadBoundNormals (JSph.cpp:1265-1295) ------------------------------------------
+    def _load_normals(self) -> np.ndarray:
+        from .core import read_normals
+
+        if self.partbegin:  # JSph::ConfigBoundNormals needs the run's extra data (JSph.cpp:1308-1315)
+            raise CaseError("No extra data available to restart at PART_%04d with mDBC." % self.partbegin)
+        out = np.zeros((self.np, 3), np.float32)
+        fn = self.casepath + "_Normals.nbi4"
+        if os.path.exists(fn):
+            nor = read_normals(fn)
+            if len(nor) != self.case_nbound:
+                raise CaseError(f"{fn}: The number of final normals does not match boundary particles.")
+            isb = self.idp < np.uint32(self.case_nbound)
+            out[isb] = nor[self.idp[isb]].astype(np.float32)
+        elif os.path.exists(self.casepath + "_NormalData.nbi4"):
+            raise CaseError("Old normal data file format (XXX_NormalData.nbi4) is invalid for current version.")
+        if not out[: self.npb].any():
+            raise CaseError("No valid normal vectors for using mDBC.")
+        return out
+
+    @property
+    def boundnormal(self) -> np.ndarray | None:
+        return self._boundnormal
 
     # -- JSph::LoadConfigCtes ---------------------------------------------------------------
     def _load_constants(self, c):
@@ -383,8 +412,15 @@ class XmlCase:
         bc = p.int("Boundary", True, 1)
         if bc not in (1, 2):
             raise CaseError("Boundary Condition method is not valid.")
-        if bc != 1:
-            raise CaseError("Only DBC boundaries (Boundary=1) are supported by this core.")
+        self.tboundary = bc
+        self.slipmode = 1
+        self.mdbc_threshold = 0.0
+        if bc == 2:  # JSph.cpp:631-641
+            self.slipmode = p.int("SlipMode", True, 1)
+            if self.slipmode not in (1, 2, 3):
+                raise CaseError("Slip mode is not valid.")
+            if p.int("MDBCCorrector", True, 0) != 0:
+                raise CaseError("MDBCCorrector=1 is not supported by this core.")
         if p.exists("DeltaSPH"):
             if p.exists("DensityDT"):
                 raise CaseError("The parameters 'DeltaSPH' and 'DensityDT' cannot be combined.")
@@ -511,6 +547,7 @@ class XmlCase:
             rhopoutmin=self.rhopoutmin, rhopoutmax=self.rhopoutmax,
             map_realposmin=tuple(float(v) for v in pmin), map_realposmax=tuple(float(v) for v in pmax),
             cellmode=self.cellmode, celldomfixed=int(self.celldomfixed), npb=self.npb, np=self.np,
+            tboundary=self.tboundary, slipmode=self.slipmode, mdbc_threshold=self.mdbc_threshold,
         )
 
 

@@ -32,6 +32,8 @@
  *   sph_solver_run ............. JSphGpuSingle::Run main loop (JSphGpuSingle.cpp:853-880):
  *                                ComputeStep_Ver/_Sym + RunCellDivide, device-resident dt
  *   sph_download_particles ..... JSphGpuSingle::ParticlesDataDown (feeds SaveData)
+ *   sph_normals_read/write ..... JSph::LoadBoundNormals (JSph.cpp:1265-1295) over
+ *                                JPartNormalData::LoadFile/SaveFile (JPartNormalData.cpp:178-257)
  *   sph_count_pairs ............ JDsPips::ComputeGpu (JDsPips.cpp:187-262) — work counter
  *   sph_slab_* ................. new: slab decomposition across GPUs; the
  *                                reference fork runs one domain per process (JSphGpuSingle)
@@ -51,7 +53,7 @@
 extern "C" {
 #endif
 
-#define SPH_ABI_VERSION 2
+#define SPH_ABI_VERSION 3
 
 typedef enum {
   SPH_OK = 0,
@@ -71,6 +73,10 @@ enum { SPH_STEP_VERLET = 1, SPH_STEP_SYMPLECTIC = 2 };
 enum { SPH_DDT_NONE = 0, SPH_DDT_DDT = 1, SPH_DDT_DDT2 = 2, SPH_DDT_DDT2FULL = 3 };
 /* TpCellMode (DualSphDef.h:477-481). */
 enum { SPH_CELLMODE_FULL = 1, SPH_CELLMODE_HALF = 2 };
+/* TpBoundary (DualSphDef.h:336-340) and TpSlipMode (DualSphDef.h:343-348); this fork
+ * allows only SLIP_Vel0 with mDBC (JSph.cpp:788). */
+enum { SPH_BOUND_DBC = 1, SPH_BOUND_MDBC = 2 };
+enum { SPH_SLIP_VEL0 = 1, SPH_SLIP_NOSLIP = 2, SPH_SLIP_FREESLIP = 3 };
 /* TpKernel (DualSphDef.h): only Wendland is on the hot path. */
 enum { SPH_KERNEL_WENDLAND = 2 };
 
@@ -119,6 +125,9 @@ typedef struct SphCaseDef {
   int celldomfixed;         /* 1: cell domain = whole map (-cellfixed:1)   */
   uint32_t npb;             /* boundary particles are the first npb        */
   uint32_t np;              /* total particles                             */
+  int32_t tboundary;        /* SPH_BOUND_* (<parameter Boundary>; 0 = DBC) */
+  int32_t slipmode;         /* SPH_SLIP_* (<parameter SlipMode>)           */
+  double mdbc_threshold;    /* MdbcThreshold (-mdbc_threshold, default 0)  */
 } SphCaseDef;
 
 /*
@@ -142,6 +151,9 @@ typedef struct SphConstants {
   double dom_posmin[3];             /* DomPosMin = Map_PosMin (single domain) */
   uint32_t dom_cells[3];            /* Map_Cells = DomCells                   */
   uint32_t dom_cellcode;            /* DomCellCode (JDsDcell.cpp:64-69)       */
+  int32_t tboundary, slipmode;      /* TBoundary, SlipMode (JSph.cpp:626-640) */
+  float mdbc_threshold;             /* MdbcThreshold                          */
+  uint32_t pad1;
 } SphConstants;
 
 /* Step statistics kept on the device and read back on demand. */
@@ -166,6 +178,9 @@ typedef struct SphParticlesHost {
   float* vel;           /* [n][3] */
   float* rhop;          /* [n]    */
   uint16_t* code;       /* [n] (may be NULL on download) */
+  float* boundnormal;   /* [n][3] mDBC only: normal from the particle to the boundary
+                           limit, as the case's _Normals.nbi4 holds it (JSph::
+                           LoadBoundNormals, JSph.cpp:1265); NULL otherwise and on download */
 } SphParticlesHost;
 
 /* Interaction outputs for kernel-level parity checks (StInterResultc + arrays). */
@@ -288,6 +303,11 @@ int sph_part_write(const char* path, const SphPartHeader* hdr, const SphParticle
 /* Write the run header Part_Head.ibi4 (JPartDataHead) that the reference's restart
  * (-partbegin) reads beside the PART files: case values + one Fixed and one Fluid MK block. */
 int sph_part_head_write(const char* path, const SphPartHeader* hdr);
+/* Boundary normals file <case>_Normals.nbi4 (PartNormals, double3[Nbound]): *nbound is
+ * set; the normals are copied when out != NULL and cap >= Nbound. */
+int sph_normals_read(const char* path, uint32_t cap, double* out, uint32_t* nbound);
+int sph_normals_write(const char* path, const char* case_name, double dp, double h, double dist, uint32_t nbound,
+                      const double* normals);
 /* Parse any .bi4 container and write it back (format round trip; byte-identical for
  * files written by the reference). */
 int sph_bi4_rewrite(const char* src, const char* dst);

@@ -78,7 +78,7 @@ class OracleSolver:
     def __init__(self, case, nthreads: int = 0):
         self.case = case
         self._cdef = SphCaseDef.from_dict(case.case_def())
-        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop)
+        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop, boundnormal=getattr(case, "boundnormal", None))
         h = C.c_void_p()
         _check(lib().or_create(C.byref(self._cdef), C.byref(init.view), nthreads, C.byref(h)))
         self._h = h

@@ -138,6 +138,13 @@ void Derive(const SphCaseDef& c, SphConstants& k) {
   // SelecDomain(TUint3(0),Map_Cells) (JSph.cpp:1794-1829).
   k.dom_cellcode = CalcCellCode(u3{k.dom_cells[0] + 1, k.dom_cells[1] + 1, k.dom_cells[2] + 1});
   if (!k.dom_cellcode) throw std::runtime_error("failed to select a valid CellCode");
+  // Boundary configuration (JSph.cpp:626-640, 785-790).
+  k.tboundary = (c.tboundary == 0 ? SPH_BOUND_DBC : c.tboundary);
+  if (k.tboundary != SPH_BOUND_DBC && k.tboundary != SPH_BOUND_MDBC)
+    throw std::runtime_error("Boundary Condition method is not valid.");
+  k.slipmode = (k.tboundary == SPH_BOUND_MDBC ? (c.slipmode == 0 ? SPH_SLIP_VEL0 : c.slipmode) : SPH_SLIP_VEL0);
+  if (k.slipmode != SPH_SLIP_VEL0) throw std::runtime_error("Only the slip mode velocity=0 is allowed with mDBC conditions.");
+  k.mdbc_threshold = (k.tboundary == SPH_BOUND_MDBC ? float(c.mdbc_threshold) : 0.f);
 }
 
 // EOS as the reference binary evaluates it: FunSphEos.h:37-39 calls the unqualified
@@ -156,6 +163,16 @@ inline float WendlandFac(const SphConstants& k, float rr2) {
   const float wqq1 = 1.f - 0.5f * qq;
   return k.bwen * qq * wqq1 * wqq1 * wqq1 / rad;
 }
+// GetKernelWendland_WabFac (FunSphKernel.h:226-234).
+inline float WendlandWabFac(const SphConstants& k, float rr2, float& fac) {
+  const float rad = std::sqrt(rr2);
+  const float qq = rad / k.kernelh;
+  const float wqq1 = 1.f - 0.5f * qq;
+  const float wqq2 = wqq1 * wqq1;
+  fac = k.bwen * qq * wqq2 * wqq1 / rad;
+  const float wqq = qq + qq + 1.f;
+  return k.awen * wqq * wqq2 * wqq2;
+}
 inline float ComputePress(float rhop, const SphConstants& k) {
   return float(double(k.cteb) * (scalar_pow(double(rhop * k.ovrhopzero), double(k.gamma)) - 1.0f));
 }
@@ -170,6 +187,8 @@ struct DivData {
   unsigned cellfluid;
   const unsigned* begincell;
   unsigned domcellcode;
+  float scell;
+  d3 domposmin;
 };
 // nsearch::Init / ParticleRange (JCellSearch_inline.h:33-82).
 struct NgSearch { int cellinit, cxini, cxfin, yini, yfin, zini, zfin; };
@@ -186,6 +205,62 @@ inline NgSearch NgInit(unsigned rcell, bool boundp2, const DivData& d) {
   r.zini = cz - (cz < d.scelldiv ? cz : d.scelldiv);
   r.zfin = cz + (d.ncz - cz - 1 < d.scelldiv ? d.ncz - cz - 1 : d.scelldiv) + 1;
   return r;
+}
+// nsearch::Init by position (JCellSearch_inline.h:52-67).
+inline NgSearch NgInitPos(const d3& ps, bool boundp2, const DivData& d) {
+  const int cx = int((ps.x - d.domposmin.x) / d.scell) - int(d.cellzero.x);
+  const int cy = int((ps.y - d.domposmin.y) / d.scell) - int(d.cellzero.y);
+  const int cz = int((ps.z - d.domposmin.z) / d.scell) - int(d.cellzero.z);
+  NgSearch r;
+  r.cellinit = (boundp2 ? 0 : int(d.cellfluid));
+  r.cxini = cx - (cx < d.scelldiv ? cx : d.scelldiv);
+  r.cxfin = cx + (d.ncx - cx - 1 < d.scelldiv ? d.ncx - cx - 1 : d.scelldiv) + 1;
+  r.yini = cy - (cy < d.scelldiv ? cy : d.scelldiv);
+  r.yfin = cy + (d.ncy - cy - 1 < d.scelldiv ? d.ncy - cy - 1 : d.scelldiv) + 1;
+  r.zini = cz - (cz < d.scelldiv ? cz : d.scelldiv);
+  r.zfin = cz + (d.ncz - cz - 1 < d.scelldiv ? d.ncz - cz - 1 : d.scelldiv) + 1;
+  return r;
+}
+// tmatrix4d (TypesDef.h) and fmath::Determinant4x4 / InverseMatrix4x4 for doubles
+// (FunctionsMath.h:186-199, 260-282).
+struct m4d { double a11, a12, a13, a14, a21, a22, a23, a24, a31, a32, a33, a34, a41, a42, a43, a44; };
+inline double Determinant4x4(const m4d& d) {
+  return (d.a14 * d.a23 * d.a32 * d.a41 - d.a13 * d.a24 * d.a32 * d.a41 -
+          d.a14 * d.a22 * d.a33 * d.a41 + d.a12 * d.a24 * d.a33 * d.a41 +
+          d.a13 * d.a22 * d.a34 * d.a41 - d.a12 * d.a23 * d.a34 * d.a41 -
+          d.a14 * d.a23 * d.a31 * d.a42 + d.a13 * d.a24 * d.a31 * d.a42 +
+          d.a14 * d.a21 * d.a33 * d.a42 - d.a11 * d.a24 * d.a33 * d.a42 -
+          d.a13 * d.a21 * d.a34 * d.a42 + d.a11 * d.a23 * d.a34 * d.a42 +
+          d.a14 * d.a22 * d.a31 * d.a43 - d.a12 * d.a24 * d.a31 * d.a43 -
+          d.a14 * d.a21 * d.a32 * d.a43 + d.a11 * d.a24 * d.a32 * d.a43 +
+          d.a12 * d.a21 * d.a34 * d.a43 - d.a11 * d.a22 * d.a34 * d.a43 -
+          d.a13 * d.a22 * d.a31 * d.a44 + d.a12 * d.a23 * d.a31 * d.a44 +
+          d.a13 * d.a21 * d.a32 * d.a44 - d.a11 * d.a23 * d.a32 * d.a44 -
+          d.a12 * d.a21 * d.a33 * d.a44 + d.a11 * d.a22 * d.a33 * d.a44);
+}
+// The rows of the inverse that the density extrapolation reads (a11..a14, a21..a24,
+// a31..a34, a41..a44), each the cofactor expression of FunctionsMath.h:263-278 / det.
+inline m4d InverseMatrix4x4(const m4d& d, double det) {
+  m4d inv{};
+  if (det) {
+    inv.a11 = (d.a22 * (d.a33 * d.a44 - d.a34 * d.a43) + d.a23 * (d.a34 * d.a42 - d.a32 * d.a44) + d.a24 * (d.a32 * d.a43 - d.a33 * d.a42)) / det;
+    inv.a21 = (d.a21 * (d.a34 * d.a43 - d.a33 * d.a44) + d.a23 * (d.a31 * d.a44 - d.a34 * d.a41) + d.a24 * (d.a33 * d.a41 - d.a31 * d.a43)) / det;
+    inv.a31 = (d.a21 * (d.a32 * d.a44 - d.a34 * d.a42) + d.a22 * (d.a34 * d.a41 - d.a31 * d.a44) + d.a24 * (d.a31 * d.a42 - d.a32 * d.a41)) / det;
+    inv.a41 = (d.a21 * (d.a33 * d.a42 - d.a32 * d.a43) + d.a22 * (d.a31 * d.a43 - d.a33 * d.a41) + d.a23 * (d.a32 * d.a41 - d.a31 * d.a42)) / det;
+    inv.a12 = (d.a12 * (d.a34 * d.a43 - d.a33 * d.a44) + d.a13 * (d.a32 * d.a44 - d.a34 * d.a42) + d.a14 * (d.a33 * d.a42 - d.a32 * d.a43)) / det;
+    inv.a22 = (d.a11 * (d.a33 * d.a44 - d.a34 * d.a43) + d.a13 * (d.a34 * d.a41 - d.a31 * d.a44) + d.a14 * (d.a31 * d.a43 - d.a33 * d.a41)) / det;
+    inv.a32 = (d.a11 * (d.a34 * d.a42 - d.a32 * d.a44) + d.a12 * (d.a31 * d.a44 - d.a34 * d.a41) + d.a14 * (d.a32 * d.a41 - d.a31 * d.a42)) / det;
+    inv.a42 = (d.a11 * (d.a32 * d.a43 - d.a33 * d.a42) + d.a12 * (d.a33 * d.a41 - d.a31 * d.a43) + d.a13 * (d.a31 * d.a42 - d.a32 * d.a41)) / det;
+    inv.a13 = (d.a12 * (d.a23 * d.a44 - d.a24 * d.a43) + d.a13 * (d.a24 * d.a42 - d.a22 * d.a44) + d.a14 * (d.a22 * d.a43 - d.a23 * d.a42)) / det;
+    inv.a23 = (d.a11 * (d.a24 * d.a43 - d.a23 * d.a44) + d.a13 * (d.a21 * d.a44 - d.a24 * d.a41) + d.a14 * (d.a23 * d.a41 - d.a21 * d.a43)) / det;
+    inv.a33 = (d.a11 * (d.a22 * d.a44 - d.a24 * d.a42) + d.a12 * (d.a24 * d.a41 - d.a21 * d.a44) + d.a14 * (d.a21 * d.a42 - d.a22 * d.a41)) / det;
+    inv.a43 = (d.a11 * (d.a23 * d.a42 - d.a22 * d.a43) + d.a12 * (d.a21 * d.a43 - d.a23 * d.a41) + d.a13 * (d.a22 * d.a41 - d.a21 * d.a42)) / det;
+    inv.a14 = (d.a12 * (d.a24 * d.a33 - d.a23 * d.a34) + d.a13 * (d.a22 * d.a34 - d.a24 * d.a32) + d.a14 * (d.a23 * d.a32 - d.a22 * d.a33)) / det;
+    inv.a24 = (d.a11 * (d.a23 * d.a34 - d.a24 * d.a33) + d.a13 * (d.a24 * d.a31 - d.a21 * d.a34) + d.a14 * (d.a21 * d.a33 - d.a23 * d.a31)) / det;
+    inv.a34 = (d.a11 * (d.a24 * d.a32 - d.a22 * d.a34) + d.a12 * (d.a21 * d.a34 - d.a24 * d.a31) + d.a14 * (d.a22 * d.a31 - d.a21 * d.a32)) / det;
+    inv.a44 = (d.a11 * (d.a22 * d.a33 - d.a23 * d.a32) + d.a12 * (d.a23 * d.a31 - d.a21 * d.a33) + d.a13 * (d.a21 * d.a32 - d.a22 * d.a31)) / det;
+  }
+  return inv;
 }
 inline void NgRange(int y, int z, const NgSearch& g, const DivData& d, unsigned& pini, unsigned& pfin) {
   const int v = d.nsheet * z + d.ncx * y + g.cellinit;
@@ -204,6 +279,8 @@ class Solver {
   std::vector<typecode> code;
   std::vector<d3> pos, pospre;
   std::vector<f4> velrhop, velrhopm1, velrhoppre;
+  std::vector<f3> boundnormal;  // BoundNormalc (mDBC): particle -> ghost node after ConfigBoundNormals
+  bool mdbc = false;
   bool havepre = false;
   // interaction scratch
   std::vector<float> ar, delta, press;
@@ -254,6 +331,21 @@ class Solver {
     for (unsigned p = npb; p < np; p++)
       if (velrhop[p].w < K.rhopoutmin || K.rhopoutmax < velrhop[p].w)
         throw std::runtime_error("Initial fluid density is out of limits.");
+    // JSph::LoadBoundNormals + ConfigBoundNormals (JSph.cpp:1265-1340): the file's
+    // normals (boundary -> boundary limit) as float, doubled (boundary -> ghost node).
+    mdbc = (K.tboundary == SPH_BOUND_MDBC);
+    if (mdbc) {
+      if (!h.boundnormal) throw std::runtime_error("mDBC needs the boundary normals (<case>_Normals.nbi4)");
+      boundnormal.assign(np, f3{0, 0, 0});
+      unsigned nerr = 0;
+      for (unsigned p = 0; p < np; p++)
+        if (idp[p] < c.npb) {
+          const f3 n{h.boundnormal[3 * p], h.boundnormal[3 * p + 1], h.boundnormal[3 * p + 2]};
+          if (n.x == 0 && n.y == 0 && n.z == 0) nerr++;
+          boundnormal[p] = f3{n.x * 2.f, n.y * 2.f, n.z * 2.f};
+        }
+      if (nerr == c.npb) throw std::runtime_error("No valid normal vectors for using mDBC.");
+    }
     // JSph::LoadDcellParticles (JSph.cpp:1690-1711), DomRealPos = MapRealPos (single domain).
     for (unsigned p = 0; p < np; p++) {
       const d3 ps = pos[p];
@@ -283,6 +375,8 @@ class Solver {
     d.cellfluid = boxfluid;
     d.begincell = begincell.data();
     d.domcellcode = K.dom_cellcode;
+    d.scell = K.scell;
+    d.domposmin = d3{K.dom_posmin[0], K.dom_posmin[1], K.dom_posmin[2]};
     return d;
   }
   // JCellDivCpu::LimitsCellBound/LimitsCellFluid (JCellDivCpu.cpp:246-352).
@@ -437,6 +531,7 @@ class Solver {
     SortArray(dcell);
     SortArray(pos);
     SortArray(velrhop);
+    if (mdbc) SortArray(boundnormal);  // JSphCpuSingle.cpp:464-467
     if (K.step_algorithm == SPH_STEP_VERLET && !velrhopm1.empty()) SortArray(velrhopm1);
     else if (K.step_algorithm == SPH_STEP_SYMPLECTIC && havepre) { SortArray(pospre); SortArray(velrhoppre); }
     np = npfinal;
@@ -509,7 +604,7 @@ class Solver {
                 const float visc_densi = K.ddtkh * cbar * (rhop1over2 - 1.f) / (rr2 + K.eta2);
                 const float dot3 = (drx * frx + dry * fry + drz * frz);
                 const float delta_ = visc_densi * dot3 * massp2;
-                deltap1 = (boundp2 ? FLT_MAX : deltap1 + delta_);  // TBoundary==BC_DBC
+                deltap1 = (boundp2 && !mdbc ? FLT_MAX : deltap1 + delta_);  // TBoundary==BC_DBC
               }
               // DDT Fourtakas (JSphCpu.cpp:733-740).
               if ((tdensity == SPH_DDT_DDT2 || (tdensity == SPH_DDT_DDT2FULL && !boundp2)) && deltap1 != FLT_MAX) {
@@ -599,7 +694,77 @@ class Solver {
     }
     if (npbok) InteractionForcesBound(dv, viscdt);
   }
-  void Interaction_Forces() {
+  // JSphCpu::InteractionMdbcCorrectionT2<Wendland,sim2d=false,SLIP_Vel0> (JSphCpu.cpp:1020-1187)
+  // over n = NpbOk boundary particles (UseNormalsFt=false; JSphCpu.cpp:1193-1210).
+  void MdbcCorrection() {
+    const DivData dv = GetDivData();
+    const float determlimit = 1e-3f;
+    const float mdbcthreshold = K.mdbc_threshold;
+    const int nn = int(npbok);
+#pragma omp parallel for schedule(guided)
+    for (int p1 = 0; p1 < nn; p1++) {
+      const f3 bn = boundnormal[p1];
+      if (bn.x == 0 && bn.y == 0 && bn.z == 0) continue;
+      float rhopfinal = FLT_MAX;
+      float sumwab = 0;
+      const d3 gposp1{pos[p1].x + double(bn.x), pos[p1].y + double(bn.y), pos[p1].z + double(bn.z)};
+      float rhopp1 = 0;
+      f3 gradrhopp1{0, 0, 0};
+      m4d a{};
+      const NgSearch g = NgInitPos(gposp1, false, dv);
+      for (int z = g.zini; z < g.zfin; z++)
+        for (int y = g.yini; y < g.yfin; y++) {
+          unsigned pif, pfi;
+          NgRange(y, z, g, dv, pif, pfi);
+          for (unsigned p2 = pif; p2 < pfi; p2++) {
+            const float drx = float(gposp1.x - pos[p2].x);
+            const float dry = float(gposp1.y - pos[p2].y);
+            const float drz = float(gposp1.z - pos[p2].z);
+            const float rr2 = (drx * drx + dry * dry + drz * drz);
+            if (rr2 <= K.kernelsize2 && CodeIsFluid(code[p2])) {
+              float fac;
+              const float wab = WendlandWabFac(K, rr2, fac);
+              const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
+              const f4 velrhopp2 = velrhop[p2];
+              const float massp2 = K.massfluid;
+              const float volp2 = massp2 / velrhopp2.w;
+              rhopp1 += massp2 * wab;
+              gradrhopp1.x += massp2 * frx;
+              gradrhopp1.y += massp2 * fry;
+              gradrhopp1.z += massp2 * frz;
+              const float vwab = wab * volp2;
+              sumwab += vwab;
+              const float vfrx = frx * volp2, vfry = fry * volp2, vfrz = frz * volp2;
+              a.a11 += vwab;  a.a12 += drx * vwab;  a.a13 += dry * vwab;  a.a14 += drz * vwab;
+              a.a21 += vfrx;  a.a22 += drx * vfrx;  a.a23 += dry * vfrx;  a.a24 += drz * vfrx;
+              a.a31 += vfry;  a.a32 += drx * vfry;  a.a33 += dry * vfry;  a.a34 += drz * vfry;
+              a.a41 += vfrz;  a.a42 += drx * vfrz;  a.a43 += dry * vfrz;  a.a44 += drz * vfrz;
+            }
+          }
+        }
+      if (sumwab >= mdbcthreshold || (mdbcthreshold >= 2 && sumwab + 2 >= mdbcthreshold)) {
+        const f3 dpos{bn.x * (-1.f), bn.y * (-1.f), bn.z * (-1.f)};
+        const double determ = Determinant4x4(a);
+        if (std::fabs(determ) >= determlimit) {
+          const m4d inv = InverseMatrix4x4(a, determ);
+          const float rhoghost = float(inv.a11 * rhopp1 + inv.a12 * gradrhopp1.x + inv.a13 * gradrhopp1.y + inv.a14 * gradrhopp1.z);
+          const float grx = -float(inv.a21 * rhopp1 + inv.a22 * gradrhopp1.x + inv.a23 * gradrhopp1.y + inv.a24 * gradrhopp1.z);
+          const float gry = -float(inv.a31 * rhopp1 + inv.a32 * gradrhopp1.x + inv.a33 * gradrhopp1.y + inv.a34 * gradrhopp1.z);
+          const float grz = -float(inv.a41 * rhopp1 + inv.a42 * gradrhopp1.x + inv.a43 * gradrhopp1.y + inv.a44 * gradrhopp1.z);
+          rhopfinal = (rhoghost + grx * dpos.x + gry * dpos.y + grz * dpos.z);
+        } else if (a.a11 > 0) {
+          rhopfinal = float(rhopp1 / a.a11);
+        }
+        rhopfinal = (rhopfinal != FLT_MAX ? rhopfinal : K.rhopzero);
+        velrhop[p1].w = rhopfinal;  // SLIP_Vel0
+      }
+    }
+  }
+
+  // JSphCpuSingle::Interaction_Forces (JSphCpuSingle.cpp:524-567): mDBC correction first,
+  // except in the Symplectic corrector (MDBCCorrector=0).
+  void Interaction_Forces(int interstep = 1) {
+    if (mdbc && interstep != 3) MdbcCorrection();
     PreInteraction();
     float viscdt = 0;
     switch (K.tdensity) {
@@ -777,11 +942,11 @@ class Solver {
   // JSphCpuSingle::ComputeStep_Sym (JSphCpuSingle.cpp:695-721).
   double ComputeStep_Sym() {
     const double dt = symdtpre;
-    Interaction_Forces();
+    Interaction_Forces(2);
     const double ddt_p = DtVariable(false);
     ComputeSymplecticPre(dt);
     RunCellDivide();
-    Interaction_Forces();
+    Interaction_Forces(3);
     const double ddt_c = DtVariable(true);
     ComputeSymplecticCorr(dt);
     symdtpre = std::min(ddt_p, ddt_c);
@@ -904,11 +1069,10 @@ int or_download(OrSolver* o, SphParticlesHost* out) {
 
 int or_interaction(OrSolver* o, int interstep, SphInterOut* out) {
   if (!o || !out) return SPH_ERR_ARG;
-  (void)interstep;
   return Guard([&] {
     Solver& s = o->s;
     omp_set_num_threads(s.nthreads);
-    s.Interaction_Forces();
+    s.Interaction_Forces(interstep);
     for (unsigned p = 0; p < s.np; p++) {
       if (out->ar) out->ar[p] = s.ar[p];
       if (out->ace) { out->ace[3 * p] = s.ace[p].x; out->ace[3 * p + 1] = s.ace[p].y; out->ace[3 * p + 2] = s.ace[p].z; }

@@ -10,7 +10,15 @@
 // test checks that both produce the same particles bit for bit.
 //
 // usage: gencase_ref <dp> <outdir> <step:1=Verlet|2=Symplectic> <ddt:0..3> [timemax] [casename]
+//                    [boundary:1=DBC|2=mDBC]
+//
+// With boundary=2 the case also gets <casename>_Normals.nbi4, written through the
+// reference's own JPartNormalData (JPartNormalData.cpp:178-207), as GenCase would: the
+// final normal of each boundary particle points from the particle to the boundary limit,
+// dp/2 beyond the wall layer towards the fluid (the sum of those vectors on edges and
+// corners).  JSph::LoadBoundNormals/ConfigBoundNormals (JSph.cpp:1265-1340) read it.
 #include "JPartDataBi4.h"
+#include "JPartNormalData.h"
 #include "Functions.h"
 #include <cmath>
 #include <cstdio>
@@ -29,15 +37,20 @@ int main(int argc, char** argv) {
   const int ddt = atoi(argv[4]);
   const double tmax = (argc > 5 ? atof(argv[5]) : 1.5);
   const std::string name = (argc > 6 ? argv[6] : "CaseDambreak");
+  const int boundary = (argc > 7 ? atoi(argv[7]) : 1);
 
   // Tank 1.6 x 0.67 x 0.4 (walls: bottom, x=0, x=L, y=0, y=W); water 0.4 x 0.67 x 0.3.
   const int nx = int(std::round(1.6 / dp)), ny = int(std::round(0.67 / dp)), nz = int(std::round(0.4 / dp));
   const int mx = int(std::round(0.4 / dp)), my = int(std::round(0.67 / dp)), mz = int(std::round(0.3 / dp));
-  std::vector<tdouble3> pos;
+  std::vector<tdouble3> pos, nor;
   for (int k = 0; k <= nz; k++)
     for (int j = 0; j <= ny; j++)
       for (int i = 0; i <= nx; i++)
-        if (k == 0 || i == 0 || i == nx || j == 0 || j == ny) pos.push_back(TDouble3(i * dp, j * dp, k * dp));
+        if (k == 0 || i == 0 || i == nx || j == 0 || j == ny) {
+          pos.push_back(TDouble3(i * dp, j * dp, k * dp));
+          const double hd = dp * 0.5;
+          nor.push_back(TDouble3(i == 0 ? hd : (i == nx ? -hd : 0.), j == 0 ? hd : (j == ny ? -hd : 0.), k == 0 ? hd : 0.));
+        }
   const unsigned nb = unsigned(pos.size());
   for (int k = 1; k <= mz; k++)
     for (int j = 1; j < my; j++)
@@ -69,6 +82,12 @@ int main(int argc, char** argv) {
   pd.AddPartInfo(0, 0, np, 0, 0, 0, pmin, pmax, 0, 0);
   pd.AddPartData(np, idp.data(), pos.data(), vel.data(), rhop.data());
   pd.SaveFileCase(name);
+  if (boundary == 2) {
+    JPartNormalData nd;
+    nd.ConfigBasic("gencase_ref", name, false, 0, dp, h, 2. * h);
+    nd.AddNormalData("Plane", nb, nor.data());
+    nd.SaveFile(dir);
+  }
 
   FILE* f = fopen((dir + "/" + name + ".xml").c_str(), "w");
   if (!f) { perror("xml"); return 2; }
@@ -89,6 +108,8 @@ int main(int argc, char** argv) {
   par("DensityDT", std::to_string(ddt));
   par("DensityDTvalue", "0.1");
   par("Shifting", "0");
+  par("Boundary", std::to_string(boundary));
+  if (boundary == 2) par("SlipMode", "1");
   par("RigidAlgorithm", "1");
   par("CoefDtMin", "0.05");
   par("DtIni", "0");

@@ -24,13 +24,16 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 REF = os.path.join(ROOT, "oracle", "_ref")
 
-# name: (dp, step(1 Verlet/2 Symplectic), ddt, nsteps, steps kept)
+# name: (dp, step(1 Verlet/2 Symplectic), ddt, nsteps, steps kept[, boundary 1 DBC/2 mDBC])
 CASES = {
     "verlet_ddt2_dp0.02": (0.02, 1, 2, 100, (1, 10, 100)),
     "symplectic_ddt1_dp0.025": (0.025, 2, 1, 100, (1, 10, 100)),
     "verlet_ddtnone_dp0.025": (0.025, 1, 0, 45, (1, 41, 45)),
     "symplectic_ddt3_dp0.03": (0.03, 2, 3, 20, (1, 20)),
     "verlet_ddt2_dp0.0127_dt": (0.0127, 1, 2, 100, ()),
+    # mDBC (Boundary=2, SlipMode=1): normals from gencase_ref's <case>_Normals.nbi4
+    "verlet_ddt2_mdbc_dp0.025": (0.025, 1, 2, 100, (1, 10, 100), 2),
+    "symplectic_ddt1_mdbc_dp0.03": (0.03, 2, 1, 60, (1, 20, 60), 2),
 }
 
 
@@ -46,10 +49,11 @@ def load_dump(fn):
     return t, idp.copy(), pos.copy(), vel.copy(), rho.copy()
 
 
-def make(name, dp, step, ddt, nsteps, keep):
+def make(name, dp, step, ddt, nsteps, keep, boundary=1):
     tmp = tempfile.mkdtemp(prefix="golden_")
     try:
-        subprocess.check_call([os.path.join(REF, "gencase_ref"), repr(dp), tmp, str(step), str(ddt)], stdout=subprocess.DEVNULL)
+        subprocess.check_call([os.path.join(REF, "gencase_ref"), repr(dp), tmp, str(step), str(ddt), "1.5",
+                               "CaseDambreak", str(boundary)], stdout=subprocess.DEVNULL)
         out = os.path.join(tmp, "out")
         subprocess.check_call(
             [os.path.join(REF, "DualSPHysics5.2CPU_ref"), os.path.join(tmp, "CaseDambreak"), out,
@@ -69,7 +73,7 @@ def make(name, dp, step, ddt, nsteps, keep):
                                "s%d_rhop" % part: rho, "s%d_time" % part: np.float64(t)})
         arrays["times"] = np.array(times)
         arrays["dt"] = np.diff(np.array(times))
-        arrays["meta"] = np.array([dp, step, ddt, nsteps], np.float64)
+        arrays["meta"] = np.array([dp, step, ddt, nsteps] + ([boundary] if boundary != 1 else []), np.float64)
         np.savez_compressed(os.path.join(ROOT, "tests", "golden", name + ".npz"), **arrays)
         print(name, "ok", os.path.getsize(os.path.join(ROOT, "tests", "golden", name + ".npz")))
     finally:

@@ -19,8 +19,13 @@ def snapshot(g, step):
 
 
 def meta(g):
-    dp, step, ddt, nsteps = g["meta"]
+    dp, step, ddt, nsteps = g["meta"][:4]
     return float(dp), int(step), int(ddt), int(nsteps)
+
+
+def boundary(g):
+    """1 DBC, 2 mDBC (fixtures written before mDBC carry 4 meta values)."""
+    return int(g["meta"][4]) if len(g["meta"]) > 4 else 1
 
 
 def by_idp(p):

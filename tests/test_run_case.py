@@ -99,7 +99,10 @@ def test_simulationdomain_with_legacy_keys_is_refused(tmp_path):
 @pytest.mark.parametrize("edit,match", [
     (lambda x: x.replace('key="Kernel" value="2"', 'key="Kernel" value="1"'), "Wendland"),
     (lambda x: x.replace('key="ViscoTreatment" value="1"', 'key="ViscoTreatment" value="2"'), "artificial"),
-    (lambda x: x.replace("<parameters>", '<parameters>\n<parameter key="Boundary" value="2"/>'), "DBC"),
+    # mDBC without a <case>_Normals.nbi4 beside the case (JSph.cpp:1337)
+    (lambda x: x.replace("<parameters>", '<parameters>\n<parameter key="Boundary" value="2"/>'), "normal vectors"),
+    (lambda x: x.replace("<parameters>", '<parameters>\n<parameter key="Boundary" value="2"/>'
+                         '<parameter key="SlipMode" value="2"/>'), "slip mode"),
     (lambda x: x.replace("<parameters>", '<parameters>\n<parameter key="XPeriodicIncY" value="0"/>'), "Periodic"),
     (lambda x: x.replace('key="Shifting" value="0"', 'key="Shifting" value="3"'), "Shifting"),
     (lambda x: x.replace('<data2d value="false"/>', '<data2d value="true"/>'), "2-D"),
@@ -122,7 +125,7 @@ def test_case_particle_count_must_match(tmp_path):
 
 
 @pytest.mark.parametrize("argv,match", [
-    (["-cpu"], "GPU"), (["-mdbc"], "mDBC"), (["-cubic"], "Wendland"), (["-viscolamsps:1e-6"], "Laminar"),
+    (["-cpu"], "GPU"), (["-mdbc_noslip"], "slip mode"), (["-initnorpla:mkbound=0"], "Normals"), (["-cubic"], "Wendland"), (["-viscolamsps:1e-6"], "Laminar"),
     (["-shifting:full"], "Shifting"), (["-sv:vtk"], "not supported"), (["-cellmode:half"], "full"),
     (["-ddt:4"], "invalid"), (["-bogus"], "not supported"),
 ])
