@@ -50,7 +50,8 @@ def dist_env():
     return rank, world, local
 
 
-def reference_cpu_baseline(dp: float, nsteps: int, threads: int, step: int = 1, ddt: int = 2) -> dict | None:
+def reference_cpu_baseline(dp: float, nsteps: int, threads: int, step: int = 1, ddt: int = 2,
+                           boundary: int = 1) -> dict | None:
     """Times the REFERENCE CPU solver (oracle/_ref, built from the reference sources)
     on the same dam break; Steps/s is the solver's own 'Steps per second' (step loop only)."""
     ref = os.path.join(ROOT, "oracle", "_ref")
@@ -59,8 +60,8 @@ def reference_cpu_baseline(dp: float, nsteps: int, threads: int, step: int = 1, 
         return None
     tmp = tempfile.mkdtemp(prefix="sphref_")
     try:
-        out = subprocess.run([gen, repr(dp), tmp, str(step), str(ddt)], capture_output=True, text=True,
-                             check=True).stdout
+        out = subprocess.run([gen, repr(dp), tmp, str(step), str(ddt), "1.5", "CaseDambreak", str(boundary)],
+                             capture_output=True, text=True, check=True).stdout
         np_ = int(re.search(r"np=(\d+)", out).group(1))
         subprocess.run([exe, os.path.join(tmp, "CaseDambreak"), os.path.join(tmp, "out"), "-nsteps:%d" % nsteps,
                         "-sv:none", "-svres:0", "-ompthreads:%d" % threads], capture_output=True, text=True,
@@ -69,9 +70,9 @@ def reference_cpu_baseline(dp: float, nsteps: int, threads: int, step: int = 1, 
         sps = float(re.search(r"Steps per second\.*:\s*([0-9.eE+-]+)", log).group(1))
         return {"value": sps * np_, "unit": "particle-steps/s", "cores": threads, "kind": "reference",
                 "sample": "reference DualSPHysics5.2 CPU (built from /root/reference sources, -O3 -fopenmp "
-                          "-ffast-math), %d-particle dam break, %d %s steps, -ompthreads:%d, "
-                          "'Steps per second' of Run.out" % (np_, nsteps, "Verlet" if step == 1 else "Symplectic",
-                                                             threads)}
+                          "-ffast-math), %d-particle dam break (%s), %d %s steps, -ompthreads:%d, "
+                          "'Steps per second' of Run.out" % (np_, "mDBC" if boundary == 2 else "DBC", nsteps,
+                                                             "Verlet" if step == 1 else "Symplectic", threads)}
     except Exception as e:  # noqa: BLE001
         sys.stderr.write("reference CPU baseline failed: %r\n" % (e,))
         return None
@@ -139,6 +140,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=("cfg2", "cfg3"), default="cfg2")
     ap.add_argument("--dp", type=float, default=None, help="override the particle spacing")
+    ap.add_argument("--boundary", choices=("dbc", "mdbc"), default="dbc",
+                    help="boundary conditions (mdbc: modified DBC, Vel0, normals to the wall limit)")
     ap.add_argument("--bound-weight", type=float, default=0.3, help="slab balance weight of a bound particle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=8)
@@ -165,10 +168,10 @@ def main() -> None:
 
     if args.workload == "cfg2":
         dp = args.dp or (CFG2_DP if world == 1 else weak_dp(world * CFG2_NP))
-        case = DamBreakCase(dp)
+        case = DamBreakCase(dp, tboundary=2 if args.boundary == "mdbc" else 1)
     else:
         dp = args.dp or CFG3_DP
-        case = DamBreakCase(dp, step_algorithm=2, tdensity=1)
+        case = DamBreakCase(dp, step_algorithm=2, tdensity=1, tboundary=2 if args.boundary == "mdbc" else 1)
     bounds = None
     fallback = None
     s = None
@@ -260,11 +263,11 @@ def main() -> None:
             "data": "synthetic: generated 3D dam-break lattice (SURVEY.md §8(c) recipe)",
             "config": {
                 "workload": (("BASELINE cfg2: 3D dam break, %d particles (dp=%g), Verlet, Wendland, artificial "
-                              "viscosity 0.1, DDT2 0.1, DBC, CFL 0.2, CellMode full" % (case.np, dp))
+                              "viscosity 0.1, DDT2 0.1, %s, CFL 0.2, CellMode full" % (case.np, dp, args.boundary.upper()))
                              if args.workload == "cfg2" else
                              ("BASELINE cfg3: 3D dam break, %d particles (dp=%g), Symplectic, Wendland, artificial "
-                              "viscosity 0.1, DDT (Molteni delta-SPH) 0.1, DBC, CFL 0.2, CellMode full"
-                              % (case.np, dp))),
+                              "viscosity 0.1, DDT (Molteni delta-SPH) 0.1, %s, CFL 0.2, CellMode full"
+                              % (case.np, dp, args.boundary.upper()))),
                 "np": case.np,
                 "npb": case.npb,
                 "parallelism": (("slab-x%d (RCCL halo + migration, max-allreduce dt)" % world) if bounds is not None
@@ -300,12 +303,13 @@ def main() -> None:
                 "bytes_per_particle_step": BYTES_PER_PARTICLE_STEP[case.step_algorithm],
             },
             "phase_ms_per_call": {"interaction": float(phase_ms[0]), "update": float(phase_ms[1]),
-                                  "divide": float(phase_ms[2])},
+                                  "divide": float(phase_ms[2]), "mdbc": float(phase_ms[3])},
             "cpu_baseline": None,
         }
         if not args.no_cpu_baseline and world == 1:
             threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), 64)
-            cb = reference_cpu_baseline(dp, args.cpu_steps, threads, case.step_algorithm, case.tdensity)
+            cb = reference_cpu_baseline(dp, args.cpu_steps, threads, case.step_algorithm, case.tdensity,
+                                        case.tboundary)
             if cb is None:
                 cb = port_cpu_baseline(case, args.cpu_steps, threads)
             cb["gpu_over_cpu"] = value / cb["value"]

