@@ -63,6 +63,7 @@ struct KConst {
   float ddte1, ddte2, ddte3, ddte4;  // the series in drz: rho0*((1+ddtgz*drz)^(1/gamma)-1) = drz*(e1+drz*(e2+...))
   float awen;  // Wendland W normalisation (mDBC)
   int mdbc;    // TBoundary == BC_MDBC: DDT (Molteni) keeps bound neighbours (JSphCpu.cpp:730)
+  int scelldiv;  // 1 CellMode=full (cells of 2h), 2 half (cells of h): neighbour rows +-scelldiv
 };
 
 // Cell grid of the (fixed) divide domain — StDivDataGpu (JCellDivDataGpu.h:26-79).

@@ -100,18 +100,19 @@ __device__ __forceinline__ void fluid_cell(const KConst& K, float rx, float ry, 
   }
 }
 
-// Neighbour-cell range of p1's cell, clamped to the grid (nsearch::Init, JCellSearch_inline.h:33-47).
+// Neighbour-cell range of p1's cell, clamped to the grid (nsearch::Init, JCellSearch_inline.h:33-47):
+// +-scelldiv cells (1 full, 2 half).
 struct Range3 {
   int xi, xf, yi, yf, zi, zf;
 };
-__device__ __forceinline__ Range3 ngs_range(int cx, int cy, int cz, const DivGrid& g) {
+__device__ __forceinline__ Range3 ngs_range(int cx, int cy, int cz, const DivGrid& g, int sd) {
   Range3 r;
-  r.xi = cx - (cx < 1 ? cx : 1);
-  r.xf = cx + (g.ncx - cx - 1 < 1 ? g.ncx - cx - 1 : 1) + 1;
-  r.yi = cy - (cy < 1 ? cy : 1);
-  r.yf = cy + (g.ncy - cy - 1 < 1 ? g.ncy - cy - 1 : 1) + 1;
-  r.zi = cz - (cz < 1 ? cz : 1);
-  r.zf = cz + (g.ncz - cz - 1 < 1 ? g.ncz - cz - 1 : 1) + 1;
+  r.xi = cx - (cx < sd ? cx : sd);
+  r.xf = cx + (g.ncx - cx - 1 < sd ? g.ncx - cx - 1 : sd) + 1;
+  r.yi = cy - (cy < sd ? cy : sd);
+  r.yf = cy + (g.ncy - cy - 1 < sd ? g.ncy - cy - 1 : sd) + 1;
+  r.zi = cz - (cz < sd ? cz : sd);
+  r.zf = cz + (g.ncz - cz - 1 < sd ? g.ncz - cz - 1 : sd) + 1;
   return r;
 }
 
@@ -154,7 +155,7 @@ __global__ __launch_bounds__(256) void k_interaction(DevScalars* __restrict__ sc
     const unsigned dc = __float_as_uint(pc1.w);
     const int cx = int(DcelCellx(K.domcellcode, dc)), cy = int(DcelCelly(K.domcellcode, dc)),
               cz = int(DcelCellz(K.domcellcode, dc));
-    const Range3 rg = ngs_range(cx, cy, cz, g);
+    const Range3 rg = ngs_range(cx, cy, cz, g, K.scelldiv);
     const bool own = cx >= g.xown0 && cx < g.xown1;  // slab ghosts are not p1
     if (!own) {
     } else if (!ONLYBOUND && p1 >= npb) {
@@ -259,7 +260,7 @@ __global__ __launch_bounds__(256) void k_count_pairs(const DevScalars* __restric
   if (p1 < np && (p1 >= npb || p1 < npbok) && cx >= g.xown0 && cx < g.xown1) {
     const unsigned dc = __float_as_uint(pc1.w);
     const int cy = int(DcelCelly(K.domcellcode, dc)), cz = int(DcelCellz(K.domcellcode, dc));
-    const Range3 rg = ngs_range(cx, cy, cz, g);
+    const Range3 rg = ngs_range(cx, cy, cz, g, K.scelldiv);
     const bool fluid = p1 >= npb;
     for (int pass = 0; pass < (fluid ? 2 : 1); pass++) {
       const unsigned cellinit = (fluid && pass == 1) ? 0u : g.boxfluid;

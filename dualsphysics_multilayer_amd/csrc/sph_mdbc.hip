@@ -41,6 +41,7 @@ struct MdbcArgs {
   float kernelsize2, ovh, awen, bwenovh, massfluid, rhopzero, threshold, determlimit;
   float cteb, ovrhopzero, gamma;
   int igamma;
+  int scelldiv;
 };
 
 // fmath::Determinant4x4 (FunctionsMath.h:186-199), double.
@@ -89,9 +90,10 @@ __global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc,
   const int cx = int((gx - a.posminx) / a.scelld) - g.xoff;
   const int cy = int((gy - a.posminy) / a.scelld);
   const int cz = int((gz - a.posminz) / a.scelld);
-  const int xini = max(cx - 1, 0), xfin = min(cx + 2, g.ncx);
-  const int yini = max(cy - 1, 0), yfin = min(cy + 2, g.ncy);
-  const int zini = max(cz - 1, 0), zfin = min(cz + 2, g.ncz);
+  const int sd = a.scelldiv;
+  const int xini = max(cx - sd, 0), xfin = min(cx + sd + 1, g.ncx);
+  const int yini = max(cy - sd, 0), yfin = min(cy + sd + 1, g.ncy);
+  const int zini = max(cz - sd, 0), zfin = min(cz + sd + 1, g.ncz);
   float rhopp1 = 0.f, gx_ = 0.f, gy_ = 0.f, gz_ = 0.f, sumwab = 0.f;
   M4 m = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   if (xini < xfin) {
@@ -198,6 +200,7 @@ void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const P
   a.ovrhopzero = K.ovrhopzero;
   a.gamma = K.gamma;
   a.igamma = (K.gamma == float(int(K.gamma)) && K.gamma >= 1.f && K.gamma <= 16.f) ? int(K.gamma) : 0;
+  a.scelldiv = K.scelldiv;
   hipLaunchKernelGGL(k_mdbc, dim3((npbcap + 255) / 256), dim3(256), 0, stm, sc, a, g);
 }
 

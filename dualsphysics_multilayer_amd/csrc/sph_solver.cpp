@@ -36,8 +36,7 @@ static unsigned cell_code(unsigned nx, unsigned ny, unsigned nz) {
 
 void derive_constants(const SphCaseDef& c, SphConstants& k) {
   if (c.kernel != SPH_KERNEL_WENDLAND) throw SphError(SPH_ERR_UNSUPPORTED, "only the Wendland kernel is implemented");
-  if (c.cellmode != SPH_CELLMODE_FULL)
-    throw SphError(SPH_ERR_UNSUPPORTED, "only CellMode=Full is implemented on the GPU path");
+  if (c.cellmode != SPH_CELLMODE_FULL && c.cellmode != SPH_CELLMODE_HALF) throw SphError(SPH_ERR_ARG, "invalid cellmode");
   if (c.step_algorithm != SPH_STEP_VERLET && c.step_algorithm != SPH_STEP_SYMPLECTIC)
     throw SphError(SPH_ERR_ARG, "invalid step algorithm");
   if (c.tdensity < 0 || c.tdensity > 3) throw SphError(SPH_ERR_ARG, "invalid DDT mode");
@@ -71,7 +70,7 @@ void derive_constants(const SphCaseDef& c, SphConstants& k) {
   k.ddtgz = float(double(k.rhopzero) * double(std::fabs(k.gravity[2])) / double(k.cteb));
   k.dtini = c.dtini ? c.dtini : k.kernelh / k.cs0;
   k.dtmin = c.dtmin ? c.dtmin : (k.kernelh / k.cs0) * float(c.coefdtmin);
-  k.scelldiv = 1;
+  k.scelldiv = (c.cellmode == SPH_CELLMODE_HALF ? 2 : 1);  // cells of 2h (full) or h (half)
   k.scell = k.kernelsize / k.scelldiv;
   k.movlimit = k.scell * 0.9f;
   for (int i = 0; i < 3; i++) {
@@ -137,6 +136,7 @@ static KConst make_kconst(const SphConstants& c) {
   K.ddtkhcs = c.ddtkh * K.cs0f;
   K.awen = c.awen;
   K.mdbc = (c.tboundary == SPH_BOUND_MDBC) ? 1 : 0;
+  K.scelldiv = c.scelldiv;
   {  // binomial coefficients of (1+x)^(1/gamma) - 1
     const double a = 1.0 / double(c.gamma);
     K.ddtc1 = float(a);
@@ -238,6 +238,8 @@ SphGpuSingle::SphGpuSingle(const SphCaseDef& cdef, const SphParticlesHost& all, 
     throw SphError(SPH_ERR_ARG, "slab rank does not match the transport");
   if (cdef.tboundary == SPH_BOUND_MDBC)
     throw SphError(SPH_ERR_UNSUPPORTED, "mDBC is not implemented on the slab decomposition");
+  if (cdef.cellmode == SPH_CELLMODE_HALF)
+    throw SphError(SPH_ERR_UNSUPPORTED, "CellMode=half is not implemented on the slab decomposition");
   Init(cdef, all);
 }
 
@@ -272,6 +274,9 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   cap_ = slab() ? n + std::max(n / 2, 65536u) : n;
   keybits_ = bits_for(G.boxdiscard, 1);
   if (const char* e = std::getenv("SPH_INTERACTION")) tiled_ = std::string(e) != "simple";
+  // The tiled kernel stages the 3x3 rows of 3 cells of CellMode=full; half runs the
+  // one-lane-per-particle kernel over its 5x5 rows of 5 cells.
+  if (C.scelldiv != 1) tiled_ = false;
   check_hip(hipSetDevice(device), "hipSetDevice");
   check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
   try {

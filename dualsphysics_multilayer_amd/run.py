@@ -212,7 +212,7 @@ class CaseRun:
 USAGE = """usage: python -m dualsphysics_multilayer_amd <case> [<dirout>] [options]
   <case>        case path without extension (<case>.xml + <case>.bi4)
   options (as DualSPHysics): -gpu[:id] -symplectic -verlet[:steps] -wendland -viscoart:v
-  -viscoboundfactor:v -ddt:0..3 -ddtvalue:v -dbc -mdbc -mdbc_threshold:v -cellmode:full -cellfixed[:0|1]
+  -viscoboundfactor:v -ddt:0..3 -ddtvalue:v -dbc -mdbc -mdbc_threshold:v -cellmode:full|half -cellfixed[:0|1]
   -saveposdouble[:0|1] -sv:binx|none -partbegin:n <dir> -rhopout:min:max -cfl:v -tmax:t
   -tout:t -domain_fixed:xmin:ymin:zmin:xmax:ymax:zmax -nsteps:n -svsteps[:0|1] -nortimes[:0|1]
   -dirout <dir> -name <case> -stable -svres -svtimers -ompthreads:n (accepted, no effect)"""
@@ -258,9 +258,13 @@ def parse_args(argv: list[str]) -> dict:
         elif word == "SAVEPOSDOUBLE":
             o["saveposdouble"] = (int(full) if full else 1) != 0
         elif word == "CELLMODE":
-            v = full.upper()
-            if v not in ("", "FULL", "2H"):
-                raise CaseError("Only -cellmode:full runs on the GPU path.")
+            v = full.upper()  # JSphCfgRun.cpp:295-299
+            if v in ("HALF", "H"):
+                ov["cellmode"] = 2
+            elif v in ("", "FULL", "2H"):
+                ov["cellmode"] = 1
+            else:
+                raise CaseError(f"invalid option {a}")
         elif word == "CELLFIXED":
             ov["celldomfixed"] = (int(full) if full else 1) != 0
         elif word == "MDBC":  # JSphCfgRun.cpp:306, JSph::LoadConfigCommands (JSph.cpp:766-790)

@@ -297,8 +297,8 @@ class XmlCase:
         if not self.rhopoutmin <= self.rhop0 <= self.rhopoutmax:
             raise CaseError(f"The reference density value {self.rhop0} is outside the defined limits "
                             f"[{self.rhopoutmin},{self.rhopoutmax}].")
-        if self.cellmode != CELLMODE_FULL:
-            raise CaseError("Only CellMode=full runs on the GPU path.")
+        if self.cellmode not in (CELLMODE_FULL, 2):
+            raise CaseError("Cell mode is not valid.")
         if self.tboundary == 2 and self.slipmode != 1:  # JSph.cpp:788
             raise CaseError("Only the slip mode velocity=0 is allowed with mDBC conditions.")
         # -- particles (JPartsLoad4::LoadParticles) ------------------------------------

@@ -24,7 +24,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 REF = os.path.join(ROOT, "oracle", "_ref")
 
-# name: (dp, step(1 Verlet/2 Symplectic), ddt, nsteps, steps kept[, boundary 1 DBC/2 mDBC])
+# name: (dp, step(1 Verlet/2 Symplectic), ddt, nsteps, steps kept[, boundary 1 DBC/2 mDBC[, extra options]])
 CASES = {
     "verlet_ddt2_dp0.02": (0.02, 1, 2, 100, (1, 10, 100)),
     "symplectic_ddt1_dp0.025": (0.025, 2, 1, 100, (1, 10, 100)),
@@ -34,6 +34,8 @@ CASES = {
     # mDBC (Boundary=2, SlipMode=1): normals from gencase_ref's <case>_Normals.nbi4
     "verlet_ddt2_mdbc_dp0.025": (0.025, 1, 2, 100, (1, 10, 100), 2),
     "symplectic_ddt1_mdbc_dp0.03": (0.03, 2, 1, 60, (1, 20, 60), 2),
+    # CellMode=half (cells of h, 5x5 rows of 5 cells; JSph.cpp:1772-1788): meta[5] = 2
+    "verlet_ddt2_half_dp0.025": (0.025, 1, 2, 60, (1, 20, 60), 1, ("-cellmode:half",)),
 }
 
 
@@ -49,7 +51,7 @@ def load_dump(fn):
     return t, idp.copy(), pos.copy(), vel.copy(), rho.copy()
 
 
-def make(name, dp, step, ddt, nsteps, keep, boundary=1):
+def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=()):
     tmp = tempfile.mkdtemp(prefix="golden_")
     try:
         subprocess.check_call([os.path.join(REF, "gencase_ref"), repr(dp), tmp, str(step), str(ddt), "1.5",
@@ -57,7 +59,7 @@ def make(name, dp, step, ddt, nsteps, keep, boundary=1):
         out = os.path.join(tmp, "out")
         subprocess.check_call(
             [os.path.join(REF, "DualSPHysics5.2CPU_ref"), os.path.join(tmp, "CaseDambreak"), out,
-             "-nsteps:%d" % nsteps, "-svsteps:1", "-saveposdouble:1", "-sv:binx", "-svres:0"],
+             "-nsteps:%d" % nsteps, "-svsteps:1", "-saveposdouble:1", "-sv:binx", "-svres:0"] + list(extra),
             stdout=subprocess.DEVNULL)
         arrays = {}
         times = []
@@ -73,7 +75,12 @@ def make(name, dp, step, ddt, nsteps, keep, boundary=1):
                                "s%d_rhop" % part: rho, "s%d_time" % part: np.float64(t)})
         arrays["times"] = np.array(times)
         arrays["dt"] = np.diff(np.array(times))
-        arrays["meta"] = np.array([dp, step, ddt, nsteps] + ([boundary] if boundary != 1 else []), np.float64)
+        m = [dp, step, ddt, nsteps]
+        if boundary != 1 or extra:
+            m.append(boundary)
+        if "-cellmode:half" in extra:
+            m.append(2)
+        arrays["meta"] = np.array(m, np.float64)
         np.savez_compressed(os.path.join(ROOT, "tests", "golden", name + ".npz"), **arrays)
         print(name, "ok", os.path.getsize(os.path.join(ROOT, "tests", "golden", name + ".npz")))
     finally:

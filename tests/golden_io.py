@@ -28,6 +28,11 @@ def boundary(g):
     return int(g["meta"][4]) if len(g["meta"]) > 4 else 1
 
 
+def cellmode(g):
+    """1 full, 2 half."""
+    return int(g["meta"][5]) if len(g["meta"]) > 5 else 1
+
+
 def by_idp(p):
     o = np.argsort(p["idp"], kind="stable")
     return {k: (v[o] if isinstance(v, np.ndarray) and v.ndim >= 1 and len(v) == len(o) else v) for k, v in p.items()}

@@ -11,7 +11,7 @@ bit-exact.
 import numpy as np
 import pytest
 
-from golden_io import by_idp, load, maxdiff, meta, snapshot, steps
+from golden_io import by_idp, cellmode, load, maxdiff, meta, snapshot, steps
 
 from dualsphysics_multilayer_amd.case import DamBreakCase
 
@@ -84,6 +84,23 @@ def test_interaction_matches_oracle(ddt):
     assert ig["viscdtmax"] == pytest.approx(io["viscdtmax"], rel=1e-3)
 
 
+def test_half_cells_match_oracle():
+    """CellMode=half (cells of h, +-2 cells: JCellSearch_inline.h:33-47 with scelldiv 2):
+    the same stable sort order and candidate counts as the oracle (bit-exact), the
+    interaction to float rounding."""
+    case = DamBreakCase(0.025, cellmode=2, celldomfixed=True)
+    g, o = gpu(case), oracle.OracleSolver(case, nthreads=4)
+    assert np.array_equal(g.particles()["idp"], o.particles()["idp"])
+    cg, co = g.count_pairs().astype(np.int64), o.count_pairs().astype(np.int64)
+    assert np.array_equal(cg[[0, 2, 4]], co[[0, 2, 4]])
+    g.run(4)
+    o.run(4)
+    assert np.array_equal(g.particles()["idp"], o.particles()["idp"])
+    ig, io = g.interaction(), o.interaction()
+    assert np.abs(ig["ace"] - io["ace"]).max() <= 2e-4 * np.abs(io["ace"]).max()
+    assert np.abs(ig["ar"] - io["ar"]).max() <= 2e-4 * np.abs(io["ar"]).max()
+
+
 def test_interaction_first_step_tight():
     """At t=0 (v=0) the interaction inputs are identical: ar/ace agree to float rounding."""
     case = DamBreakCase(0.02, tdensity=0, celldomfixed=True)
@@ -95,11 +112,11 @@ def test_interaction_first_step_tight():
 
 
 @pytest.mark.parametrize("name", ["verlet_ddt2_dp0.02", "symplectic_ddt1_dp0.025", "verlet_ddtnone_dp0.025",
-                                  "symplectic_ddt3_dp0.03"])
+                                  "symplectic_ddt3_dp0.03", "verlet_ddt2_half_dp0.025"])
 def test_steps_match_reference_parts(name):
     g_ = load(name)
     dp, step_alg, ddt, _ = meta(g_)
-    s = gpu(DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt))
+    s = gpu(DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt, cellmode=cellmode(g_)))
     done = 0
     for k in steps(g_):
         s.run(k - done)

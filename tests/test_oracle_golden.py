@@ -11,14 +11,14 @@ The oracle must stay inside 2x that floor (it is built with the same flags).
 import numpy as np
 import pytest
 
-from golden_io import boundary, by_idp, load, maxdiff, meta, snapshot, steps
+from golden_io import boundary, by_idp, cellmode, load, maxdiff, meta, snapshot, steps
 
 from dualsphysics_multilayer_amd.case import DamBreakCase
 
 oracle = pytest.importorskip("oracle.pyoracle")
 
 CASES = ["verlet_ddt2_dp0.02", "symplectic_ddt1_dp0.025", "verlet_ddtnone_dp0.025", "symplectic_ddt3_dp0.03",
-         "verlet_ddt2_mdbc_dp0.025", "symplectic_ddt1_mdbc_dp0.03"]
+         "verlet_ddt2_mdbc_dp0.025", "symplectic_ddt1_mdbc_dp0.03", "verlet_ddt2_half_dp0.025"]
 
 
 def tol(step):
@@ -34,7 +34,7 @@ def tol(step):
 def test_oracle_matches_reference_parts(name):
     g = load(name)
     dp, step_alg, ddt, _ = meta(g)
-    case = DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt, tboundary=boundary(g))
+    case = DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt, tboundary=boundary(g), cellmode=cellmode(g))
     s = oracle.OracleSolver(case, nthreads=4)
     done = 0
     for k in steps(g):

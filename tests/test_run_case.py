@@ -126,7 +126,7 @@ def test_case_particle_count_must_match(tmp_path):
 
 @pytest.mark.parametrize("argv,match", [
     (["-cpu"], "GPU"), (["-mdbc_noslip"], "slip mode"), (["-initnorpla:mkbound=0"], "Normals"), (["-cubic"], "Wendland"), (["-viscolamsps:1e-6"], "Laminar"),
-    (["-shifting:full"], "Shifting"), (["-sv:vtk"], "not supported"), (["-cellmode:half"], "full"),
+    (["-shifting:full"], "Shifting"), (["-sv:vtk"], "not supported"), (["-cellmode:quarter"], "invalid"),
     (["-ddt:4"], "invalid"), (["-bogus"], "not supported"),
 ])
 def test_unsupported_options_raise(argv, match):
