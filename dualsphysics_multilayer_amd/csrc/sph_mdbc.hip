@@ -15,13 +15,14 @@
 // back to the particle; else if A11 > 0 the Shepard value rho_g / A11; with no fluid the
 // density is RhopZero.  Vel0 keeps the boundary velocity (zero for fixed walls).
 //
-// Layout/parallelism: one lane per boundary particle (the boundary particles of one
-// cell row are consecutive, so the lanes of a wave walk the same neighbour rows and
-// their candidate loads coalesce).  Positions are read in double (posxy/posz) so the
+// Layout/parallelism: one wave per boundary particle, its lanes splitting the candidates
+// (see k_mdbc); the summation order therefore differs from the CPU's sequential sums by
+// rounding only.  Positions are read in double (posxy/posz) so the
 // distances are the reference's float(gpos - pos2) bit for bit.  The normals are kept
 // in case (idp) order — boundary ids are < CaseNbound and fixed boundaries never move —
 // so the divide never has to reorder them.  The corrected density also refreshes the
 // boundary particle's EOS pressure (PreInteraction recomputes it on the CPU).
+#include <algorithm>
 #include <cfloat>
 
 #include "sph_kernels.hpp"
@@ -78,97 +79,164 @@ __device__ inline float eos_press(const MdbcArgs& a, float rho) {
   return float(double(a.cteb) * (xg - 1.0));
 }
 
+// One WAVE per boundary particle (grid-stride over p1 < NpbOk): the lanes split the
+// candidates of each neighbour row (coalesced loads, 64 candidates in flight instead of
+// one dependent chain per lane), then the 5 float and 16 double partial sums are
+// reduced across the wave in a fixed butterfly order (deterministic) and lane 0 solves.
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int MAXR>
 __global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc, MdbcArgs a, DivGrid g) {
-  const unsigned p1 = blockIdx.x * 256 + threadIdx.x;
-  if (p1 >= sc->npbok) return;
-  const float4 bn = a.normal[a.idp[p1]];
-  if (bn.x == 0.f && bn.y == 0.f && bn.z == 0.f) return;
-  const double2 pxy = a.posxy[p1];
-  const double gx = pxy.x + double(bn.x), gy = pxy.y + double(bn.y), gz = a.posz[p1] + double(bn.z);
-  // nsearch::Init by position (JCellSearch_inline.h:52-67) on the full-map grid, the
-  // ranges clamped to the grid (equal to the reference's for a ghost node inside it).
-  const int cx = int((gx - a.posminx) / a.scelld) - g.xoff;
-  const int cy = int((gy - a.posminy) / a.scelld);
-  const int cz = int((gz - a.posminz) / a.scelld);
-  const int sd = a.scelldiv;
-  const int xini = max(cx - sd, 0), xfin = min(cx + sd + 1, g.ncx);
-  const int yini = max(cy - sd, 0), yfin = min(cy + sd + 1, g.ncy);
-  const int zini = max(cz - sd, 0), zfin = min(cz + sd + 1, g.ncz);
-  float rhopp1 = 0.f, gx_ = 0.f, gy_ = 0.f, gz_ = 0.f, sumwab = 0.f;
-  M4 m = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  if (xini < xfin) {
-    for (int z = zini; z < zfin; z++)
-      for (int y = yini; y < yfin; y++) {
-        const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
-        const unsigned pini = a.bc[rowbase + xini], pfin = a.bc[rowbase + xfin];
-        for (unsigned p2 = pini; p2 < pfin; p2++) {
-          const double2 q = a.posxy[p2];
-          const float drx = float(gx - q.x);
-          const float dry = float(gy - q.y);
-          const float drz = float(gz - a.posz[p2]);
-          const float rr2 = drx * drx + dry * dry + drz * drz;
-          if (rr2 <= a.kernelsize2 && CodeIsFluid(a.code[p2])) {
-            // GetKernelWendland_WabFac (FunSphKernel.h:226-234); fac in its r -> 0
-            // form (bwen/h)(1-q/2)^3, finite when a fluid particle sits on the ghost node.
-            const float rad = sqrtf(rr2);
-            const float qq = rad * a.ovh;
-            const float wqq1 = 1.f - 0.5f * qq;
-            const float wqq2 = wqq1 * wqq1;
-            const float fac = a.bwenovh * wqq2 * wqq1;
-            const float wqq = qq + qq + 1.f;
-            const float wab = a.awen * wqq * wqq2 * wqq2;
-            const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
-            const float volp2 = a.massfluid / a.velrhop[p2].w;
-            rhopp1 += a.massfluid * wab;
-            gx_ += a.massfluid * frx;
-            gy_ += a.massfluid * fry;
-            gz_ += a.massfluid * frz;
-            const float vwab = wab * volp2;
-            sumwab += vwab;
-            const float vfrx = frx * volp2, vfry = fry * volp2, vfrz = frz * volp2;
-            m.a11 += vwab;  m.a12 += drx * vwab;  m.a13 += dry * vwab;  m.a14 += drz * vwab;
-            m.a21 += vfrx;  m.a22 += drx * vfrx;  m.a23 += dry * vfrx;  m.a24 += drz * vfrx;
-            m.a31 += vfry;  m.a32 += drx * vfry;  m.a33 += dry * vfry;  m.a34 += drz * vfry;
-            m.a41 += vfrz;  m.a42 += drx * vfrz;  m.a43 += dry * vfrz;  m.a44 += drz * vfrz;
+  const unsigned lane = threadIdx.x & 63u;
+  const unsigned nwaves = gridDim.x * 4u;
+  const unsigned n = sc->npbok;
+  for (unsigned p1 = blockIdx.x * 4u + (threadIdx.x >> 6); p1 < n; p1 += nwaves) {
+    const float4 bn = a.normal[a.idp[p1]];
+    if (bn.x == 0.f && bn.y == 0.f && bn.z == 0.f) continue;
+    const double2 pxy = a.posxy[p1];
+    const double gx = pxy.x + double(bn.x), gy = pxy.y + double(bn.y), gz = a.posz[p1] + double(bn.z);
+    // nsearch::Init by position (JCellSearch_inline.h:52-67) on the full-map grid, the
+    // ranges clamped to the grid (equal to the reference's for a ghost node inside it).
+    const int cx = int((gx - a.posminx) / a.scelld) - g.xoff;
+    const int cy = int((gy - a.posminy) / a.scelld);
+    const int cz = int((gz - a.posminz) / a.scelld);
+    const int sd = (MAXR == 9 ? 1 : 2);
+    const int xini = max(cx - sd, 0), xfin = min(cx + sd + 1, g.ncx);
+    const int yini = max(cy - sd, 0), yfin = min(cy + sd + 1, g.ncy);
+    const int zini = max(cz - sd, 0), zfin = min(cz + sd + 1, g.ncz);
+    float rhopp1 = 0.f, gx_ = 0.f, gy_ = 0.f, gz_ = 0.f, sumwab = 0.f;
+    M4 m = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // The non-empty fluid ranges of the neighbour rows, flattened into one candidate
+    // index space k in [0, total): row r holds k in [o[r], o[r+1]), p2 = k + d[r].
+    // (wave-uniform values; MAXR = (2*scelldiv+1)^2 rows)
+    unsigned o[MAXR], d[MAXR];
+    int nr = 0;
+    unsigned total = 0;
+    if (xini < xfin) {
+      for (int z = zini; z < zfin; z++)
+        for (int y = yini; y < yfin; y++) {
+          const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+          const unsigned pini = a.bc[rowbase + xini], pfin = a.bc[rowbase + xfin];
+          if (pfin > pini) {
+            o[nr] = total;
+            d[nr] = pini - total;
+            total += pfin - pini;
+            nr++;
           }
         }
+    }
+    const bool any = total > 0u;
+    // Four candidates per lane per round, all loads issued before the arithmetic: the
+    // kernel is bound by the latency of these L2 reads, not by its FP work.
+    for (unsigned k0 = lane; k0 < total; k0 += 256u) {
+      unsigned p2[4];
+      bool v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const unsigned k = k0 + 64u * unsigned(u);
+        v[u] = k < total;
+        unsigned dd = d[0];
+#pragma unroll
+        for (int r = 1; r < MAXR; r++)
+          if (r < nr && k >= o[r]) dd = d[r];
+        p2[u] = v[u] ? k + dd : d[0];
       }
+      double2 q[4];
+      double qz[4];
+      typecode c2[4];
+      float rho2[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        q[u] = a.posxy[p2[u]];
+        qz[u] = a.posz[p2[u]];
+        c2[u] = a.code[p2[u]];
+        rho2[u] = a.velrhop[p2[u]].w;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const float drx = float(gx - q[u].x);
+        const float dry = float(gy - q[u].y);
+        const float drz = float(gz - qz[u]);
+        const float rr2 = drx * drx + dry * dry + drz * drz;
+        if (v[u] && rr2 <= a.kernelsize2 && CodeIsFluid(c2[u])) {
+          // GetKernelWendland_WabFac (FunSphKernel.h:226-234); fac in its r -> 0
+          // form (bwen/h)(1-q/2)^3, finite when a fluid particle sits on the ghost node.
+          const float rad = sqrtf(rr2);
+          const float qq = rad * a.ovh;
+          const float wqq1 = 1.f - 0.5f * qq;
+          const float wqq2 = wqq1 * wqq1;
+          const float fac = a.bwenovh * wqq2 * wqq1;
+          const float wqq = qq + qq + 1.f;
+          const float wab = a.awen * wqq * wqq2 * wqq2;
+          const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
+          const float volp2 = a.massfluid / rho2[u];
+          rhopp1 += a.massfluid * wab;
+          gx_ += a.massfluid * frx;
+          gy_ += a.massfluid * fry;
+          gz_ += a.massfluid * frz;
+          const float vwab = wab * volp2;
+          sumwab += vwab;
+          const float vfrx = frx * volp2, vfry = fry * volp2, vfrz = frz * volp2;
+          m.a11 += vwab;  m.a12 += drx * vwab;  m.a13 += dry * vwab;  m.a14 += drz * vwab;
+          m.a21 += vfrx;  m.a22 += drx * vfrx;  m.a23 += dry * vfrx;  m.a24 += drz * vfrx;
+          m.a31 += vfry;  m.a32 += drx * vfry;  m.a33 += dry * vfry;  m.a34 += drz * vfry;
+          m.a41 += vfrz;  m.a42 += drx * vfrz;  m.a43 += dry * vfrz;  m.a44 += drz * vfrz;
+        }
+      }
+    }
+    if (any) {  // wave-uniform
+      rhopp1 = wsum(rhopp1); gx_ = wsum(gx_); gy_ = wsum(gy_); gz_ = wsum(gz_); sumwab = wsum(sumwab);
+      m.a11 = wsum(m.a11); m.a12 = wsum(m.a12); m.a13 = wsum(m.a13); m.a14 = wsum(m.a14);
+      m.a21 = wsum(m.a21); m.a22 = wsum(m.a22); m.a23 = wsum(m.a23); m.a24 = wsum(m.a24);
+      m.a31 = wsum(m.a31); m.a32 = wsum(m.a32); m.a33 = wsum(m.a33); m.a34 = wsum(m.a34);
+      m.a41 = wsum(m.a41); m.a42 = wsum(m.a42); m.a43 = wsum(m.a43); m.a44 = wsum(m.a44);
+    }
+    if (lane != 0u) continue;
+    const float thr = a.threshold;
+    if (!(sumwab >= thr || (thr >= 2.f && sumwab + 2.f >= thr))) continue;
+    float rhopfinal = FLT_MAX;
+    const double determ = det4(m);
+    if (fabs(determ) >= double(a.determlimit)) {
+      // Rows of fmath::InverseMatrix4x4 (FunctionsMath.h:260-282) that the extrapolation reads.
+      const M4& d = m;
+      const double i11 = (d.a22 * (d.a33 * d.a44 - d.a34 * d.a43) + d.a23 * (d.a34 * d.a42 - d.a32 * d.a44) + d.a24 * (d.a32 * d.a43 - d.a33 * d.a42)) / determ;
+      const double i21 = (d.a21 * (d.a34 * d.a43 - d.a33 * d.a44) + d.a23 * (d.a31 * d.a44 - d.a34 * d.a41) + d.a24 * (d.a33 * d.a41 - d.a31 * d.a43)) / determ;
+      const double i31 = (d.a21 * (d.a32 * d.a44 - d.a34 * d.a42) + d.a22 * (d.a34 * d.a41 - d.a31 * d.a44) + d.a24 * (d.a31 * d.a42 - d.a32 * d.a41)) / determ;
+      const double i41 = (d.a21 * (d.a33 * d.a42 - d.a32 * d.a43) + d.a22 * (d.a31 * d.a43 - d.a33 * d.a41) + d.a23 * (d.a32 * d.a41 - d.a31 * d.a42)) / determ;
+      const double i12 = (d.a12 * (d.a34 * d.a43 - d.a33 * d.a44) + d.a13 * (d.a32 * d.a44 - d.a34 * d.a42) + d.a14 * (d.a33 * d.a42 - d.a32 * d.a43)) / determ;
+      const double i22 = (d.a11 * (d.a33 * d.a44 - d.a34 * d.a43) + d.a13 * (d.a34 * d.a41 - d.a31 * d.a44) + d.a14 * (d.a31 * d.a43 - d.a33 * d.a41)) / determ;
+      const double i32 = (d.a11 * (d.a34 * d.a42 - d.a32 * d.a44) + d.a12 * (d.a31 * d.a44 - d.a34 * d.a41) + d.a14 * (d.a32 * d.a41 - d.a31 * d.a42)) / determ;
+      const double i42 = (d.a11 * (d.a32 * d.a43 - d.a33 * d.a42) + d.a12 * (d.a33 * d.a41 - d.a31 * d.a43) + d.a13 * (d.a31 * d.a42 - d.a32 * d.a41)) / determ;
+      const double i13 = (d.a12 * (d.a23 * d.a44 - d.a24 * d.a43) + d.a13 * (d.a24 * d.a42 - d.a22 * d.a44) + d.a14 * (d.a22 * d.a43 - d.a23 * d.a42)) / determ;
+      const double i23 = (d.a11 * (d.a24 * d.a43 - d.a23 * d.a44) + d.a13 * (d.a21 * d.a44 - d.a24 * d.a41) + d.a14 * (d.a23 * d.a41 - d.a21 * d.a43)) / determ;
+      const double i33 = (d.a11 * (d.a22 * d.a44 - d.a24 * d.a42) + d.a12 * (d.a24 * d.a41 - d.a21 * d.a44) + d.a14 * (d.a21 * d.a42 - d.a22 * d.a41)) / determ;
+      const double i43 = (d.a11 * (d.a23 * d.a42 - d.a22 * d.a43) + d.a12 * (d.a21 * d.a43 - d.a23 * d.a41) + d.a13 * (d.a22 * d.a41 - d.a21 * d.a42)) / determ;
+      const double i14 = (d.a12 * (d.a24 * d.a33 - d.a23 * d.a34) + d.a13 * (d.a22 * d.a34 - d.a24 * d.a32) + d.a14 * (d.a23 * d.a32 - d.a22 * d.a33)) / determ;
+      const double i24 = (d.a11 * (d.a23 * d.a34 - d.a24 * d.a33) + d.a13 * (d.a24 * d.a31 - d.a21 * d.a34) + d.a14 * (d.a21 * d.a33 - d.a23 * d.a31)) / determ;
+      const double i34 = (d.a11 * (d.a24 * d.a32 - d.a22 * d.a34) + d.a12 * (d.a21 * d.a34 - d.a24 * d.a31) + d.a14 * (d.a22 * d.a31 - d.a21 * d.a32)) / determ;
+      const double i44 = (d.a11 * (d.a22 * d.a33 - d.a23 * d.a32) + d.a12 * (d.a23 * d.a31 - d.a21 * d.a33) + d.a13 * (d.a21 * d.a32 - d.a22 * d.a31)) / determ;
+      const float rhoghost = float(i11 * rhopp1 + i12 * gx_ + i13 * gy_ + i14 * gz_);
+      const float grx = -float(i21 * rhopp1 + i22 * gx_ + i23 * gy_ + i24 * gz_);
+      const float gry = -float(i31 * rhopp1 + i32 * gx_ + i33 * gy_ + i34 * gz_);
+      const float grz = -float(i41 * rhopp1 + i42 * gx_ + i43 * gy_ + i44 * gz_);
+      // dpos = boundary particle - ghost node = -normal
+      rhopfinal = (rhoghost + grx * (-bn.x) + gry * (-bn.y) + grz * (-bn.z));
+    } else if (m.a11 > 0) {
+      rhopfinal = float(rhopp1 / m.a11);
+    }
+    rhopfinal = (rhopfinal != FLT_MAX ? rhopfinal : a.rhopzero);
+    a.velrhop[p1].w = rhopfinal;  // SLIP_Vel0: density only
+    a.press[p1] = eos_press(a, rhopfinal);
   }
-  const float thr = a.threshold;
-  if (!(sumwab >= thr || (thr >= 2.f && sumwab + 2.f >= thr))) return;
-  float rhopfinal = FLT_MAX;
-  const double determ = det4(m);
-  if (fabs(determ) >= double(a.determlimit)) {
-    // Rows of fmath::InverseMatrix4x4 (FunctionsMath.h:260-282) that the extrapolation reads.
-    const M4& d = m;
-    const double i11 = (d.a22 * (d.a33 * d.a44 - d.a34 * d.a43) + d.a23 * (d.a34 * d.a42 - d.a32 * d.a44) + d.a24 * (d.a32 * d.a43 - d.a33 * d.a42)) / determ;
-    const double i21 = (d.a21 * (d.a34 * d.a43 - d.a33 * d.a44) + d.a23 * (d.a31 * d.a44 - d.a34 * d.a41) + d.a24 * (d.a33 * d.a41 - d.a31 * d.a43)) / determ;
-    const double i31 = (d.a21 * (d.a32 * d.a44 - d.a34 * d.a42) + d.a22 * (d.a34 * d.a41 - d.a31 * d.a44) + d.a24 * (d.a31 * d.a42 - d.a32 * d.a41)) / determ;
-    const double i41 = (d.a21 * (d.a33 * d.a42 - d.a32 * d.a43) + d.a22 * (d.a31 * d.a43 - d.a33 * d.a41) + d.a23 * (d.a32 * d.a41 - d.a31 * d.a42)) / determ;
-    const double i12 = (d.a12 * (d.a34 * d.a43 - d.a33 * d.a44) + d.a13 * (d.a32 * d.a44 - d.a34 * d.a42) + d.a14 * (d.a33 * d.a42 - d.a32 * d.a43)) / determ;
-    const double i22 = (d.a11 * (d.a33 * d.a44 - d.a34 * d.a43) + d.a13 * (d.a34 * d.a41 - d.a31 * d.a44) + d.a14 * (d.a31 * d.a43 - d.a33 * d.a41)) / determ;
-    const double i32 = (d.a11 * (d.a34 * d.a42 - d.a32 * d.a44) + d.a12 * (d.a31 * d.a44 - d.a34 * d.a41) + d.a14 * (d.a32 * d.a41 - d.a31 * d.a42)) / determ;
-    const double i42 = (d.a11 * (d.a32 * d.a43 - d.a33 * d.a42) + d.a12 * (d.a33 * d.a41 - d.a31 * d.a43) + d.a13 * (d.a31 * d.a42 - d.a32 * d.a41)) / determ;
-    const double i13 = (d.a12 * (d.a23 * d.a44 - d.a24 * d.a43) + d.a13 * (d.a24 * d.a42 - d.a22 * d.a44) + d.a14 * (d.a22 * d.a43 - d.a23 * d.a42)) / determ;
-    const double i23 = (d.a11 * (d.a24 * d.a43 - d.a23 * d.a44) + d.a13 * (d.a21 * d.a44 - d.a24 * d.a41) + d.a14 * (d.a23 * d.a41 - d.a21 * d.a43)) / determ;
-    const double i33 = (d.a11 * (d.a22 * d.a44 - d.a24 * d.a42) + d.a12 * (d.a24 * d.a41 - d.a21 * d.a44) + d.a14 * (d.a21 * d.a42 - d.a22 * d.a41)) / determ;
-    const double i43 = (d.a11 * (d.a23 * d.a42 - d.a22 * d.a43) + d.a12 * (d.a21 * d.a43 - d.a23 * d.a41) + d.a13 * (d.a22 * d.a41 - d.a21 * d.a42)) / determ;
-    const double i14 = (d.a12 * (d.a24 * d.a33 - d.a23 * d.a34) + d.a13 * (d.a22 * d.a34 - d.a24 * d.a32) + d.a14 * (d.a23 * d.a32 - d.a22 * d.a33)) / determ;
-    const double i24 = (d.a11 * (d.a23 * d.a34 - d.a24 * d.a33) + d.a13 * (d.a24 * d.a31 - d.a21 * d.a34) + d.a14 * (d.a21 * d.a33 - d.a23 * d.a31)) / determ;
-    const double i34 = (d.a11 * (d.a24 * d.a32 - d.a22 * d.a34) + d.a12 * (d.a21 * d.a34 - d.a24 * d.a31) + d.a14 * (d.a22 * d.a31 - d.a21 * d.a32)) / determ;
-    const double i44 = (d.a11 * (d.a22 * d.a33 - d.a23 * d.a32) + d.a12 * (d.a23 * d.a31 - d.a21 * d.a33) + d.a13 * (d.a21 * d.a32 - d.a22 * d.a31)) / determ;
-    const float rhoghost = float(i11 * rhopp1 + i12 * gx_ + i13 * gy_ + i14 * gz_);
-    const float grx = -float(i21 * rhopp1 + i22 * gx_ + i23 * gy_ + i24 * gz_);
-    const float gry = -float(i31 * rhopp1 + i32 * gx_ + i33 * gy_ + i34 * gz_);
-    const float grz = -float(i41 * rhopp1 + i42 * gx_ + i43 * gy_ + i44 * gz_);
-    // dpos = boundary particle - ghost node = -normal
-    rhopfinal = (rhoghost + grx * (-bn.x) + gry * (-bn.y) + grz * (-bn.z));
-  } else if (m.a11 > 0) {
-    rhopfinal = float(rhopp1 / m.a11);
-  }
-  rhopfinal = (rhopfinal != FLT_MAX ? rhopfinal : a.rhopzero);
-  a.velrhop[p1].w = rhopfinal;  // SLIP_Vel0: density only
-  a.press[p1] = eos_press(a, rhopfinal);
 }
 
 void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& cur, float* press,
@@ -201,7 +269,9 @@ void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const P
   a.gamma = K.gamma;
   a.igamma = (K.gamma == float(int(K.gamma)) && K.gamma >= 1.f && K.gamma <= 16.f) ? int(K.gamma) : 0;
   a.scelldiv = K.scelldiv;
-  hipLaunchKernelGGL(k_mdbc, dim3((npbcap + 255) / 256), dim3(256), 0, stm, sc, a, g);
+  const unsigned nb = std::min((npbcap + 3u) / 4u, 4096u);  // 4 waves per block, one boundary particle per wave
+  if (K.scelldiv == 1) hipLaunchKernelGGL(k_mdbc<9>, dim3(nb), dim3(256), 0, stm, sc, a, g);
+  else hipLaunchKernelGGL(k_mdbc<25>, dim3(nb), dim3(256), 0, stm, sc, a, g);
 }
 
 }  // namespace sphx

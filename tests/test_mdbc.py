@@ -119,12 +119,18 @@ def _gpu(case):
     return SphGpuSingle(case, device=0)
 
 
-def _tol(step):  # test_gpu_parity.tol: 10x the reference's noise floor
+def _tol(step):
+    """10x the reference's own noise floor WITH mDBC: the same solver built with and
+    without -ffast-math (the oracle, bit-exact to the reference at step 1) differs from
+    the reference by pos 1.4e-9 / vel 1.8e-6 / rho 3.7e-4 after step 1, 1.9e-8 / 6e-6 /
+    1.0e-3 after 10-20 steps and 1.8e-7 / 2.1e-5 / 1.8e-3 after 60-100 steps (Verlet DDT2
+    and Symplectic DDT1 mDBC goldens) — 2-4x the DBC floor of test_gpu_parity: the
+    first-order extrapolation of the boundary density amplifies rounding."""
     if step <= 1:
-        return 1e-8, 2.2e-5, 1e-2
+        return 1.4e-8, 2.2e-5, 1e-2
     if step <= 20:
-        return 1e-7, 5e-5, 1e-2
-    return 2e-6, 2e-4, 2e-2
+        return 2e-7, 6e-5, 1e-2
+    return 2e-6, 2.1e-4, 2e-2
 
 
 @pytest.mark.gpu
@@ -148,9 +154,12 @@ def test_gpu_mdbc_densities_match_oracle(nsteps):
     assert (ro != 1000.0).sum() > 50
     assert np.abs(rg - ro).max() <= (2e-3 if nsteps == 0 else 2e-2), np.abs(rg - ro).max()
     scale = np.abs(io["ace"]).max()
-    # the boundary pressures carry those densities (dP = cs0^2 drho ~ 1 Pa): 1e-4 of the scale
-    assert np.abs(ig["ace"] - io["ace"]).max() <= 2e-4 * scale
-    assert np.abs(ig["ar"] - io["ar"]).max() <= 2e-4 * np.abs(io["ar"]).max()
+    # the boundary pressures carry those densities (dP = cs0^2 drho ~ 1 Pa); after some
+    # steps the two states themselves differ by the mDBC noise floor (see _tol)
+    tol = 2e-4 if nsteps == 0 else 1e-3
+    assert np.abs(ig["ace"] - io["ace"]).max() <= tol * scale
+    # at t=0 ar is DDT round-off (|ar| ~ 0.02 kg/m3/s): an absolute floor of 0.01
+    assert np.abs(ig["ar"] - io["ar"]).max() <= tol * np.abs(io["ar"]).max() + 1e-2
 
 
 @pytest.mark.gpu
@@ -162,8 +171,9 @@ def test_gpu_mdbc_ddt1_interaction_matches_oracle():
     g.run(5)
     o.run(5)
     ig, io = g.interaction(), o.interaction()
-    assert np.abs(ig["ar"] - io["ar"]).max() <= 2e-4 * np.abs(io["ar"]).max()
-    assert np.abs(ig["ace"] - io["ace"]).max() <= 2e-4 * np.abs(io["ace"]).max()
+    # each state after 5 steps carries the mDBC noise floor (see _tol)
+    assert np.abs(ig["ar"] - io["ar"]).max() <= 1e-3 * np.abs(io["ar"]).max()
+    assert np.abs(ig["ace"] - io["ace"]).max() <= 1e-3 * np.abs(io["ace"]).max()
 
 
 @pytest.mark.gpu
