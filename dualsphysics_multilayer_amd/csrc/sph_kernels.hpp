@@ -69,10 +69,11 @@ void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const
                         DivGrid g, const KConst& K, float4* arace);
 // mDBC boundary correction (sph_mdbc.hip; JSphCpu.cpp:1020-1187): density of every
 // boundary particle p1 < npbok with a normal extrapolated from its ghost node; press
-// refreshed.  `normal` is indexed by idp.
+// refreshed.  `normal` is indexed by idp; list[npbcap] + nlist: scratch of the
+// wet-particle list.
 void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& cur, float* press,
                  const float4* normal, const unsigned* begincell, DivGrid g, const KConst& K,
-                 const double dom_posmin[3], float threshold);
+                 const double dom_posmin[3], float threshold, unsigned* list, unsigned* nlist);
 // Pair counters (JDsPips).
 void launch_count_pairs(hipStream_t stm, unsigned cap, const DevScalars* sc, const float4* poscell,
                         const unsigned* begincell, DivGrid g, const KConst& K, unsigned long long* out6);

@@ -79,10 +79,6 @@ __device__ inline float eos_press(const MdbcArgs& a, float rho) {
   return float(double(a.cteb) * (xg - 1.0));
 }
 
-// One WAVE per boundary particle (grid-stride over p1 < NpbOk): the lanes split the
-// candidates of each neighbour row (coalesced loads, 64 candidates in flight instead of
-// one dependent chain per lane), then the 5 float and 16 double partial sums are
-// reduced across the wave in a fixed butterfly order (deterministic) and lane 0 solves.
 __device__ __forceinline__ float wsum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -94,45 +90,113 @@ __device__ __forceinline__ double wsum(double v) {
   return v;
 }
 
-template <int MAXR>
-__global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc, MdbcArgs a, DivGrid g) {
+// Ghost node of p1 and its neighbour-cell box: nsearch::Init by position
+// (JCellSearch_inline.h:52-67) on the full-map grid, clamped to the grid (equal to the
+// reference's ranges for a ghost node inside it).
+struct GhostBox {
+  double gx, gy, gz;
+  int xini, xfin, yini, yfin, zini, zfin;
+};
+template <int SD>
+__device__ __forceinline__ GhostBox ghost_box(const MdbcArgs& a, const DivGrid& g, unsigned p1, float4 bn) {
+  GhostBox b;
+  const double2 pxy = a.posxy[p1];
+  b.gx = pxy.x + double(bn.x);
+  b.gy = pxy.y + double(bn.y);
+  b.gz = a.posz[p1] + double(bn.z);
+  const int cx = int((b.gx - a.posminx) / a.scelld) - g.xoff;
+  const int cy = int((b.gy - a.posminy) / a.scelld);
+  const int cz = int((b.gz - a.posminz) / a.scelld);
+  b.xini = max(cx - SD, 0);
+  b.xfin = min(cx + SD + 1, g.ncx);
+  b.yini = max(cy - SD, 0);
+  b.yfin = min(cy + SD + 1, g.ncy);
+  b.zini = max(cz - SD, 0);
+  b.zfin = min(cz + SD + 1, g.ncz);
+  return b;
+}
+
+// Pass 1, one lane per boundary particle p1 < NpbOk: list the particles that have a
+// normal and fluid in the cells around their ghost node; a dry one gets what the
+// reference's correction gives it with empty sums (RhopZero when 0 >= threshold, else
+// unchanged).  Most of the tank's walls are dry, so pass 2 runs over a short list.
+template <int SD>
+__global__ __launch_bounds__(256) void k_mdbc_list(const DevScalars* __restrict__ sc, MdbcArgs a, DivGrid g,
+                                                   unsigned* __restrict__ list, unsigned* __restrict__ nlist) {
+  const unsigned p1 = blockIdx.x * 256u + threadIdx.x;
+  bool keep = false;
+  if (p1 < sc->npbok) {
+    const float4 bn = a.normal[a.idp[p1]];
+    if (bn.x != 0.f || bn.y != 0.f || bn.z != 0.f) {
+      const GhostBox b = ghost_box<SD>(a, g, p1, bn);
+      unsigned tot = 0;
+      if (b.xini < b.xfin)
+        for (int z = b.zini; z < b.zfin; z++)
+          for (int y = b.yini; y < b.yfin; y++) {
+            const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+            tot += a.bc[rowbase + b.xfin] - a.bc[rowbase + b.xini];
+          }
+      keep = tot > 0u;
+      if (!keep && a.threshold <= 0.f) {
+        // no fluid around: all sums 0 >= threshold, det 0 and A11 0 -> rhopfinal = RhopZero
+        a.velrhop[p1].w = a.rhopzero;
+        a.press[p1] = eos_press(a, a.rhopzero);
+      }
+    }
+  }
+  const unsigned long long bal = __ballot(keep);
+  const unsigned lane = threadIdx.x & 63u;
+  unsigned base = 0;
+  if (lane == 0 && bal) base = atomicAdd(nlist, unsigned(__popcll(bal)));
+  base = __shfl(base, 0, 64);
+  if (keep) list[base + unsigned(__popcll(bal & ((1ull << lane) - 1ull)))] = p1;
+}
+
+// Pass 2, one WAVE per listed boundary particle: lanes 0..MAXR-1 read the fluid range of
+// one neighbour row each (all row lookups in flight at once), a wave scan flattens the
+// non-empty rows into one candidate index space k in [0, total) (row r holds
+// [o_r, o_r + n_r), p2 = k + d_r), and the lanes split the candidates, four per lane per
+// round with all loads issued before the arithmetic (the kernel is bound by the latency
+// of these L2 reads, not by its FP work).  The 5 float and 16 double partial sums are
+// reduced across the wave in a fixed butterfly order (deterministic) and lane 0 solves.
+template <int SD>
+__global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc, MdbcArgs a, DivGrid g,
+                                              const unsigned* __restrict__ list, const unsigned* __restrict__ nlist) {
+  constexpr int W = 2 * SD + 1, MAXR = W * W;
   const unsigned lane = threadIdx.x & 63u;
   const unsigned nwaves = gridDim.x * 4u;
-  const unsigned n = sc->npbok;
-  for (unsigned p1 = blockIdx.x * 4u + (threadIdx.x >> 6); p1 < n; p1 += nwaves) {
+  const unsigned n = *nlist;
+  for (unsigned it = blockIdx.x * 4u + (threadIdx.x >> 6); it < n; it += nwaves) {
+    const unsigned p1 = list[it];
     const float4 bn = a.normal[a.idp[p1]];
-    if (bn.x == 0.f && bn.y == 0.f && bn.z == 0.f) continue;
-    const double2 pxy = a.posxy[p1];
-    const double gx = pxy.x + double(bn.x), gy = pxy.y + double(bn.y), gz = a.posz[p1] + double(bn.z);
-    // nsearch::Init by position (JCellSearch_inline.h:52-67) on the full-map grid, the
-    // ranges clamped to the grid (equal to the reference's for a ghost node inside it).
-    const int cx = int((gx - a.posminx) / a.scelld) - g.xoff;
-    const int cy = int((gy - a.posminy) / a.scelld);
-    const int cz = int((gz - a.posminz) / a.scelld);
-    const int sd = (MAXR == 9 ? 1 : 2);
-    const int xini = max(cx - sd, 0), xfin = min(cx + sd + 1, g.ncx);
-    const int yini = max(cy - sd, 0), yfin = min(cy + sd + 1, g.ncy);
-    const int zini = max(cz - sd, 0), zfin = min(cz + sd + 1, g.ncz);
+    const GhostBox b = ghost_box<SD>(a, g, p1, bn);
+    const double gx = b.gx, gy = b.gy, gz = b.gz;
     float rhopp1 = 0.f, gx_ = 0.f, gy_ = 0.f, gz_ = 0.f, sumwab = 0.f;
     M4 m = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    // The non-empty fluid ranges of the neighbour rows, flattened into one candidate
-    // index space k in [0, total): row r holds k in [o[r], o[r+1]), p2 = k + d[r].
-    // (wave-uniform values; MAXR = (2*scelldiv+1)^2 rows)
+    unsigned rini = 0, rlen = 0;
+    if (int(lane) < MAXR && b.xini < b.xfin) {
+      const int z = b.zini + int(lane) / W, y = b.yini + int(lane) % W;
+      if (z < b.zfin && y < b.yfin) {
+        const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+        rini = a.bc[rowbase + b.xini];
+        rlen = a.bc[rowbase + b.xfin] - rini;
+      }
+    }
+    // exclusive scan of the row lengths over the first MAXR lanes (row order = the
+    // reference's z, y loop order)
+    unsigned incl = rlen;
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1) {
+      const unsigned t = __shfl_up(incl, off, 64);
+      if (int(lane) >= off) incl += t;
+    }
+    const unsigned total = __shfl(incl, MAXR - 1, 64);
+    const unsigned ofs = incl - rlen;
     unsigned o[MAXR], d[MAXR];
-    int nr = 0;
-    unsigned total = 0;
-    if (xini < xfin) {
-      for (int z = zini; z < zfin; z++)
-        for (int y = yini; y < yfin; y++) {
-          const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
-          const unsigned pini = a.bc[rowbase + xini], pfin = a.bc[rowbase + xfin];
-          if (pfin > pini) {
-            o[nr] = total;
-            d[nr] = pini - total;
-            total += pfin - pini;
-            nr++;
-          }
-        }
+#pragma unroll
+    for (int r = 0; r < MAXR; r++) {
+      o[r] = __shfl(ofs, r, 64);
+      d[r] = __shfl(rini, r, 64) - o[r];
     }
     const bool any = total > 0u;
     // Four candidates per lane per round, all loads issued before the arithmetic: the
@@ -144,11 +208,13 @@ __global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc,
       for (int u = 0; u < 4; u++) {
         const unsigned k = k0 + 64u * unsigned(u);
         v[u] = k < total;
+        // the row holding k: the last one starting at or before k (an empty row shares
+        // its offset with the next one, which then wins)
         unsigned dd = d[0];
 #pragma unroll
         for (int r = 1; r < MAXR; r++)
-          if (r < nr && k >= o[r]) dd = d[r];
-        p2[u] = v[u] ? k + dd : d[0];
+          if (k >= o[r]) dd = d[r];
+        p2[u] = v[u] ? k + dd : p1;
       }
       double2 q[4];
       double qz[4];
@@ -241,7 +307,7 @@ __global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc,
 
 void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& cur, float* press,
                  const float4* normal, const unsigned* begincell, DivGrid g, const KConst& K,
-                 const double dom_posmin[3], float threshold) {
+                 const double dom_posmin[3], float threshold, unsigned* list, unsigned* nlist) {
   if (!npbcap) return;
   MdbcArgs a;
   a.idp = cur.idp;
@@ -269,9 +335,16 @@ void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const P
   a.gamma = K.gamma;
   a.igamma = (K.gamma == float(int(K.gamma)) && K.gamma >= 1.f && K.gamma <= 16.f) ? int(K.gamma) : 0;
   a.scelldiv = K.scelldiv;
-  const unsigned nb = std::min((npbcap + 3u) / 4u, 4096u);  // 4 waves per block, one boundary particle per wave
-  if (K.scelldiv == 1) hipLaunchKernelGGL(k_mdbc<9>, dim3(nb), dim3(256), 0, stm, sc, a, g);
-  else hipLaunchKernelGGL(k_mdbc<25>, dim3(nb), dim3(256), 0, stm, sc, a, g);
+  (void)hipMemsetAsync(nlist, 0, sizeof(unsigned), stm);
+  const unsigned nb1 = (npbcap + 255u) / 256u;
+  const unsigned nb2 = std::min((npbcap + 3u) / 4u, 2048u);  // 4 waves per block, one listed particle per wave
+  if (K.scelldiv == 1) {
+    hipLaunchKernelGGL(k_mdbc_list<1>, dim3(nb1), dim3(256), 0, stm, sc, a, g, list, nlist);
+    hipLaunchKernelGGL(k_mdbc<1>, dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
+  } else {
+    hipLaunchKernelGGL(k_mdbc_list<2>, dim3(nb1), dim3(256), 0, stm, sc, a, g, list, nlist);
+    hipLaunchKernelGGL(k_mdbc<2>, dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
+  }
 }
 
 }  // namespace sphx

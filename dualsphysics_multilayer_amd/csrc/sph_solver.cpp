@@ -478,6 +478,8 @@ void SphGpuSingle::UploadNormals(const SphCaseDef& cdef, const SphParticlesHost&
   check_hip(hipMalloc((void**)&normal_, sizeof(float4) * nor.size()), "hipMalloc normals");
   allocs_.push_back(normal_);
   check_hip(hipMemcpy(normal_, nor.data(), sizeof(float4) * nor.size(), hipMemcpyHostToDevice), "upload normals");
+  check_hip(hipMalloc((void**)&mdbclist_, sizeof(unsigned) * (size_t(npb0_) + 1)), "hipMalloc mDBC list");
+  allocs_.push_back(mdbclist_);
 }
 
 // Restart: TimeStep and SymplecticDtPre of the loaded PART (JSph::InitRun, JSph.cpp:2094-2106).
@@ -620,7 +622,8 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
   // mDBC boundary correction first, except in the Symplectic corrector (JSphCpuSingle.cpp:525).
   if (normal_ && interstep != 3) {
     TimedBegin(3);
-    launch_mdbc(stream, npb0_, sc_, cur_, press_, normal_, begincell_, G, K, C.dom_posmin, C.mdbc_threshold);
+    launch_mdbc(stream, npb0_, sc_, cur_, press_, normal_, begincell_, G, K, C.dom_posmin, C.mdbc_threshold,
+                mdbclist_ + 1, mdbclist_);
     TimedEnd(3);
   }
   if (tiled_) {

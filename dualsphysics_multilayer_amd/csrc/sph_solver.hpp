@@ -103,6 +103,7 @@ class SphGpuSingle {
   float4* poscell_ = nullptr;
   float* press_ = nullptr;
   float4* normal_ = nullptr;      // mDBC: particle -> ghost node, by idp [CaseNbound]
+  unsigned* mdbclist_ = nullptr;  // mDBC: wet boundary particles of this interaction [npb] + count
   float4* arace_ = nullptr;
   unsigned* begincell_ = nullptr;
   uint4* items_ = nullptr;        // tiled-interaction work items (per divide)
