@@ -1,11 +1,11 @@
-"""ctypes mirror of the POD structs in include/sphcore.h (ABI version 3)."""
+"""ctypes mirror of the POD structs in include/sphcore.h (ABI version 4)."""
 from __future__ import annotations
 
 import ctypes as C
 
 import numpy as np
 
-SPH_ABI_VERSION = 3
+SPH_ABI_VERSION = 4
 
 SPH_STATUS = {
     0: "SPH_OK",
@@ -268,6 +268,68 @@ def _ptr(arr: np.ndarray | None, ctype):
     return arr.ctypes.data_as(C.POINTER(ctype))
 
 
+class SphMotionMov(C.Structure):
+    _fields_ = [
+        ("obj", C.c_int32), ("id", C.c_int32), ("next", C.c_int32), ("type", C.c_int32), ("prev", C.c_int32),
+        ("pad", C.c_int32), ("duration", C.c_double), ("vec", C.c_double * 3), ("vec2", C.c_double * 3),
+        ("phase", C.c_double * 3), ("axisp1", C.c_double * 3), ("axisp2", C.c_double * 3),
+        ("ang", C.c_double), ("ang2", C.c_double), ("ang3", C.c_double),
+    ]
+
+
+class SphMotionEvent(C.Structure):
+    _fields_ = [("obj", C.c_int32), ("mov", C.c_int32), ("start", C.c_double), ("finish", C.c_double)]
+
+
+class SphFloatingDef(C.Structure):
+    _fields_ = [
+        ("idbegin", C.c_uint32), ("count", C.c_uint32), ("massbody", C.c_double), ("masspart", C.c_double),
+        ("center", C.c_double * 3), ("inertia", C.c_double * 9), ("linvelini", C.c_double * 3),
+        ("angvelini", C.c_double * 3), ("translationfree", C.c_int32 * 3), ("rotationfree", C.c_int32 * 3),
+    ]
+
+
+class SphFloatingState(C.Structure):
+    _fields_ = [
+        ("center", C.c_double * 3), ("fvel", C.c_float * 3), ("fomega", C.c_float * 3), ("angles", C.c_float * 3),
+        ("facelin", C.c_float * 3), ("faceang", C.c_float * 3), ("pad", C.c_float),
+    ]
+
+    def as_dict(self) -> dict:
+        return {k: np.array(getattr(self, k)) for k in ("center", "fvel", "fomega", "angles", "facelin", "faceang")}
+
+
+def _fill(struct, d: dict):
+    for k, v in d.items():
+        if k not in dict(struct._fields_):
+            continue
+        f = getattr(struct, k)
+        if isinstance(f, C.Array):
+            for i, x in enumerate(v):
+                f[i] = x
+        else:
+            setattr(struct, k, v)
+    return struct
+
+
+def motion_arrays(motion: dict):
+    """SphMotionMov[] / SphMotionEvent[] of a case's motion program (XmlCase.motion)."""
+    movs = (SphMotionMov * max(1, len(motion["movs"])))()
+    for i, m in enumerate(motion["movs"]):
+        _fill(movs[i], m)
+    evts = (SphMotionEvent * max(1, len(motion["evts"])))()
+    for i, e in enumerate(motion["evts"]):
+        _fill(evts[i], e)
+    return movs, evts
+
+
+def floating_array(floatings: list):
+    arr = (SphFloatingDef * len(floatings))()
+    for i, f in enumerate(floatings):
+        _fill(arr[i], f)
+    return arr
+
+
 class HostParticles:
     """Owns numpy arrays and exposes them as an SphParticlesHost view."""
 
@@ -308,4 +370,8 @@ def check_struct_sizes() -> dict:
         "SphInterOut": C.sizeof(SphInterOut),
         "SphSlabDef": C.sizeof(SphSlabDef),
         "SphPartHeader": C.sizeof(SphPartHeader),
+        "SphMotionMov": C.sizeof(SphMotionMov),
+        "SphMotionEvent": C.sizeof(SphMotionEvent),
+        "SphFloatingDef": C.sizeof(SphFloatingDef),
+        "SphFloatingState": C.sizeof(SphFloatingState),
     }

@@ -26,6 +26,12 @@ from ._abi import (
     SphRunStats,
     SphPartHeader,
     SphSlabDef,
+    SphFloatingDef,
+    SphFloatingState,
+    SphMotionEvent,
+    SphMotionMov,
+    floating_array,
+    motion_arrays,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -68,6 +74,9 @@ EXPORTED_SYMBOLS = (
     "sph_normals_read",
     "sph_normals_write",
     "sph_bi4_rewrite",
+    "sph_solver_set_motion",
+    "sph_solver_set_floatings",
+    "sph_solver_floatings",
 )
 
 
@@ -122,6 +131,10 @@ def load_library(path: str = LIB_PATH):
     L.sph_normals_read.argtypes = [C.c_char_p, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
     L.sph_normals_write.argtypes = [C.c_char_p, C.c_char_p, C.c_double, C.c_double, C.c_double, C.c_uint32,
                                     C.POINTER(C.c_double)]
+    L.sph_solver_set_motion.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(SphMotionMov), C.c_uint32,
+                                        C.POINTER(SphMotionEvent)]
+    L.sph_solver_set_floatings.argtypes = [vp, C.c_uint32, C.POINTER(SphFloatingDef), C.c_double]
+    L.sph_solver_floatings.argtypes = [vp, C.c_uint32, C.POINTER(SphFloatingState), C.POINTER(C.c_uint32)]
     if L.sph_abi_version() != SPH_ABI_VERSION:
         raise SphError(3, "ABI version mismatch")
     _lib = L
@@ -140,6 +153,17 @@ def case_derive(case_def: dict) -> dict:
     return k.as_dict()
 
 
+def case_particles(case) -> HostParticles:
+    """Initial particles of a case; the particle codes travel only when the case has moving or
+    floating blocks (else the core assigns one fixed + one fluid block, JSph::LoadCodeParticles)."""
+    bodies = getattr(case, "has_bodies", False)
+    hp = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop, code=case.code if bodies else None,
+                       boundnormal=getattr(case, "boundnormal", None))
+    if not bodies:
+        hp.view.code = C.POINTER(C.c_uint16)()
+    return hp
+
+
 class SphGpuSingle:
     """One MI355X running one domain: the JSphGpuSingle of this core."""
 
@@ -147,10 +171,22 @@ class SphGpuSingle:
         L = load_library()
         self.case = case
         self._cdef = SphCaseDef.from_dict(case.case_def())
-        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop, boundnormal=getattr(case, "boundnormal", None))
+        init = case_particles(case)
         h = C.c_void_p()
         _check(L.sph_solver_create(C.byref(self._cdef), C.byref(init.view), device, C.byref(h)))
         self._h = h
+        self._time_set = None
+        if getattr(case, "has_bodies", False):
+            # a restart sets the PART time first: the motion program is advanced to it
+            if getattr(case, "time0", 0.0) or getattr(case, "symdtpre0", 0.0):
+                self.set_time(case.time0, case.symdtpre0)
+            if getattr(case, "motion", None):
+                movs, evts = motion_arrays(case.motion)
+                _check(L.sph_solver_set_motion(self._h, case.motion["nobj"], len(case.motion["movs"]), movs,
+                                               len(case.motion["evts"]), evts))
+            if getattr(case, "floatings", None):
+                fts = floating_array(case.floatings)
+                _check(L.sph_solver_set_floatings(self._h, len(case.floatings), fts, case.ftpause))
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -222,7 +258,18 @@ class SphGpuSingle:
 
     def set_time(self, time: float, symplectic_dtpre: float = 0.0) -> None:
         """Restart from a PART: its TimeStep (and SymplecticDtPre)."""
+        if getattr(self, "_time_set", None) == (time, symplectic_dtpre):
+            return  # already applied at creation (cases with moving/floating bodies)
         _check(load_library().sph_solver_set_time(self._h, time, symplectic_dtpre))
+        self._time_set = (time, symplectic_dtpre)
+
+    def floatings(self) -> list:
+        """State of the floating bodies (FtObjs: center, fvel, fomega, angles, facelin, faceang)."""
+        n = C.c_uint32()
+        _check(load_library().sph_solver_floatings(self._h, 0, None, C.byref(n)))
+        out = (SphFloatingState * max(1, n.value))()
+        _check(load_library().sph_solver_floatings(self._h, n.value, out, C.byref(n)))
+        return [out[i].as_dict() for i in range(n.value)]
 
     def save_part(self, path: str, cpart: int, head_path: str | None = None) -> None:
         """SaveData: this solver's state as a reference PART file (+ Part_Head.ibi4)."""
@@ -246,7 +293,7 @@ class SphGpuSingle:
 def slab_partition(case, nranks: int, bound_weight: float = 0.3) -> np.ndarray:
     """x-cell column bounds [nranks+1] balancing fluid + bound_weight*bound particles."""
     cdef = SphCaseDef.from_dict(case.case_def())
-    init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop, boundnormal=getattr(case, "boundnormal", None))
+    init = case_particles(case)
     out = np.zeros(nranks + 1, np.int32)
     _check(load_library().sph_slab_partition(C.byref(cdef), C.byref(init.view), nranks, bound_weight,
                                              out.ctypes.data_as(C.POINTER(C.c_int32))))
@@ -271,7 +318,7 @@ class SphGpuSlab(SphGpuSingle):
         L = load_library()
         self.case = case
         self._cdef = SphCaseDef.from_dict(case.case_def())
-        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop, boundnormal=getattr(case, "boundnormal", None))
+        init = case_particles(case)
         sd = SphSlabDef(rank, nranks, int(bounds[rank]), int(bounds[rank + 1]))
         C.memmove(sd.comm_id, comm_id, 128)
         h = C.c_void_p()
@@ -306,7 +353,7 @@ class SphSlabGroup:
         devices = np.ascontiguousarray(devices if devices is not None else np.zeros(n), np.int32)
         self.case = case
         self._cdef = SphCaseDef.from_dict(case.case_def())
-        init = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop, boundnormal=getattr(case, "boundnormal", None))
+        init = case_particles(case)
         h = C.c_void_p()
         _check(L.sph_slab_group_create(C.byref(self._cdef), C.byref(init.view), n,
                                        devices.ctypes.data_as(C.POINTER(C.c_int32)),

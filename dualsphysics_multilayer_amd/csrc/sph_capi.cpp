@@ -144,6 +144,22 @@ int sph_solver_set_time(SphSolver* s, double time, double symplectic_dtpre) {
   NEED(s);
   return guard([&] { s->impl->SetTime(time, symplectic_dtpre); });
 }
+int sph_solver_set_motion(SphSolver* s, uint32_t nobj, uint32_t nmov, const SphMotionMov* movs, uint32_t nevt,
+                          const SphMotionEvent* evts) {
+  NEED(s);
+  return guard([&] { s->impl->SetMotion(nobj, nmov, movs, nevt, evts); });
+}
+int sph_solver_set_floatings(SphSolver* s, uint32_t nft, const SphFloatingDef* defs, double ftpause) {
+  NEED(s && defs);
+  return guard([&] { s->impl->SetFloatings(nft, defs, ftpause); });
+}
+int sph_solver_floatings(SphSolver* s, uint32_t cap, SphFloatingState* out, uint32_t* nft) {
+  NEED(s);
+  return guard([&] {
+    const unsigned n = s->impl->Floatings(out, cap);
+    if (nft) *nft = n;
+  });
+}
 int sph_solver_set_timing(SphSolver* s, int enabled) {
   NEED(s);
   return guard([&] { s->impl->SetTiming(enabled != 0); });

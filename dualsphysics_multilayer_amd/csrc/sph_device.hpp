@@ -24,7 +24,8 @@ typedef uint16_t typecode;
 
 constexpr typecode CODE_MASKSPECIAL = 0xe000, CODE_OUTIGNORE = 0x4000, CODE_OUTMOVE = 0x6000,
                    CODE_OUTPOS = 0x8000, CODE_OUTRHOP = 0xA000, CODE_MASKTYPE = 0x1800,
-                   CODE_TYPE_FLOATING = 0x1000, CODE_TYPE_FLUID = 0x1800;
+                   CODE_TYPE_MOVING = 0x800, CODE_TYPE_FLOATING = 0x1000, CODE_TYPE_FLUID = 0x1800,
+                   CODE_MASKVALUE = 0x7ff;
 constexpr float ALMOSTZERO = 1e-18f;  // DualSphDef.h:132
 
 __host__ __device__ inline typecode CodeSpecial(typecode c) { return c & CODE_MASKSPECIAL; }
@@ -96,6 +97,7 @@ struct DevScalars {
   double symdtpre;  // SymplecticDtPre
   double ddt_p;     // predictor dt (Symplectic)
   double last_dt;
+  double tstep0;    // TimeStep at the start of the step in flight (motion, FtPause)
   float last_velmax, last_acemax, last_viscdt, pad3;
   // Max-reductions (float bits of values >= 0) spread over RED_SLOTS slots so that
   // thousands of waves do not serialise on one address; k_dt folds and clears them.

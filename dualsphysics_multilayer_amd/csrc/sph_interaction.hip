@@ -39,16 +39,34 @@ __device__ __forceinline__ float wendland_fac(const KConst& K, float rr2) {
 }
 
 // One fluid p1 against the particles of one neighbour cell [pini,pfin).
-template <int TDENSITY, bool BOUNDP2>
+// Floating bodies present (FT): a floating p2 carries its body's particle mass, switches
+// DDT off for p1 (Molteni: unless the body is heavy, DELTA_HEAVYFLOATING; Fourtakas: the
+// term is skipped) (JSphCpu.cpp:692-703,743).
+struct FtView {
+  const typecode* code;
+  const float* massp;  // per floating body
+};
+
+template <int TDENSITY, bool BOUNDP2, bool FT = false>
 __device__ __forceinline__ void fluid_cell(const KConst& K, float rx, float ry, float rz, float4 vr1, float pr1,
                                            unsigned pini, unsigned pfin, const float4* __restrict__ poscell,
                                            const float4* __restrict__ velrhop, const float* __restrict__ press,
-                                           float massp2, float visco, Acc& a) {
+                                           float massp2c, float visco, Acc& a, FtView ft = {}) {
   for (unsigned p2 = pini; p2 < pfin; p2++) {
     const float4 pc2 = poscell[p2];
     const float drx = rx - pc2.x, dry = ry - pc2.y, drz = rz - pc2.z;
     const float rr2 = drx * drx + dry * dry + drz * drz;
     if (rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO) {
+      float massp2 = massp2c;
+      bool ftp2 = false;
+      if (FT && !BOUNDP2) {
+        const typecode c2 = ft.code[p2];
+        ftp2 = CodeType(c2) == CODE_TYPE_FLOATING;
+        if (ftp2) {
+          massp2 = ft.massp[c2 & CODE_MASKVALUE];
+          if (TDENSITY == 1 && massp2 <= K.massfluid * 1.2f) a.delta = FLT_MAX;
+        }
+      }
       const float fac = wendland_fac(K, rr2);
       const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
       const float4 vr2 = velrhop[p2];
@@ -73,7 +91,7 @@ __device__ __forceinline__ void fluid_cell(const KConst& K, float rx, float ry, 
           a.delta += visc_densi * dot3 * massp2;
         }
       }
-      if ((TDENSITY == 2 || (TDENSITY == 3 && !BOUNDP2)) && a.delta != FLT_MAX) {
+      if ((TDENSITY == 2 || (TDENSITY == 3 && !BOUNDP2)) && a.delta != FLT_MAX && !ftp2) {
         if (BOUNDP2) a.delta = FLT_MAX;
         else {
           const float rh = 1.f + K.ddtgz * drz;
@@ -116,11 +134,12 @@ __device__ __forceinline__ Range3 ngs_range(int cx, int cy, int cz, const DivGri
   return r;
 }
 
-template <int TDENSITY, bool BOUNDP2>
+template <int TDENSITY, bool BOUNDP2, bool FT = false>
 __device__ __forceinline__ void fluid_pass(const KConst& K, const DivGrid& g, const unsigned* __restrict__ begincell,
                                            const float4 pc1, int cx, int cy, int cz, const Range3& rg, float4 vr1,
                                            float pr1, const float4* __restrict__ poscell,
-                                           const float4* __restrict__ velrhop, const float* __restrict__ press, Acc& a) {
+                                           const float4* __restrict__ velrhop, const float* __restrict__ press, Acc& a,
+                                           FtView ft = {}) {
   const unsigned cellinit = (BOUNDP2 ? 0u : g.boxfluid);
   const float massp2 = (BOUNDP2 ? K.massbound : K.massfluid);
   const float visco = (BOUNDP2 ? K.viscobound : K.visco);
@@ -133,19 +152,20 @@ __device__ __forceinline__ void fluid_pass(const KConst& K, const DivGrid& g, co
       for (int x = rg.xi; x < rg.xf; x++) {
         const unsigned pfin = begincell[row + x + 1];
         const float rx = pc1.x + float(cx - x) * K.scell;
-        fluid_cell<TDENSITY, BOUNDP2>(K, rx, ry, rz, vr1, pr1, pini, pfin, poscell, velrhop, press, massp2, visco, a);
+        fluid_cell<TDENSITY, BOUNDP2, FT>(K, rx, ry, rz, vr1, pr1, pini, pfin, poscell, velrhop, press, massp2, visco, a,
+                                          ft);
         pini = pfin;
       }
     }
   }
 }
 
-template <int TDENSITY, bool ONLYBOUND = false>
+template <int TDENSITY, bool ONLYBOUND = false, bool FT = false>
 __global__ __launch_bounds__(256) void k_interaction(DevScalars* __restrict__ sc, const float4* __restrict__ poscell,
                                                      const float4* __restrict__ velrhop,
                                                      const float* __restrict__ press,
                                                      const unsigned* __restrict__ begincell, DivGrid g, KConst K,
-                                                     float4* __restrict__ arace) {
+                                                     float4* __restrict__ arace, FtView ft = {}) {
   const unsigned np = sc->np, npb = sc->npb, npbok = sc->npbok;
   const unsigned p1 = blockIdx.x * blockDim.x + threadIdx.x;
   float viscmax = 0.f, ace2 = 0.f;
@@ -163,8 +183,10 @@ __global__ __launch_bounds__(256) void k_interaction(DevScalars* __restrict__ sc
       const float pr1 = press[p1];
       Acc f = {0, 0, 0, 0, 0, 0};
       Acc b = {0, 0, 0, 0, 0, 0};
-      fluid_pass<TDENSITY, false>(K, g, begincell, pc1, cx, cy, cz, rg, vr1, pr1, poscell, velrhop, press, f);
-      fluid_pass<TDENSITY, true>(K, g, begincell, pc1, cx, cy, cz, rg, vr1, pr1, poscell, velrhop, press, b);
+      // a floating p1 gets no DDT (JSphCpu.cpp:659-662): both passes start sticky
+      if (FT && TDENSITY && CodeType(ft.code[p1]) == CODE_TYPE_FLOATING) f.delta = b.delta = FLT_MAX;
+      fluid_pass<TDENSITY, false, FT>(K, g, begincell, pc1, cx, cy, cz, rg, vr1, pr1, poscell, velrhop, press, f, ft);
+      fluid_pass<TDENSITY, true, FT>(K, g, begincell, pc1, cx, cy, cz, rg, vr1, pr1, poscell, velrhop, press, b, ft);
       // Store exactly as the two CPU passes do (JSphCpu.cpp:800-818).
       float ar = 0.f, ax = 0.f, ay = 0.f, az = 0.f, delta = 0.f;
       if (f.ar != 0.f || f.ax != 0.f || f.ay != 0.f || f.az != 0.f || f.visc != 0.f) {
@@ -207,7 +229,12 @@ __global__ __launch_bounds__(256) void k_interaction(DevScalars* __restrict__ sc
                   const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
                   const float4 vr2 = velrhop[p2];
                   const float dvx = vr1.x - vr2.x, dvy = vr1.y - vr2.y, dvz = vr1.z - vr2.z;
-                  arp1 += K.massfluid * (dvx * frx + dvy * fry + dvz * frz) * (vr1.w / vr2.w);
+                  float massp2 = K.massfluid;  // JSphCpu.cpp:589-594
+                  if (FT) {
+                    const typecode c2 = ft.code[p2];
+                    if (CodeType(c2) == CODE_TYPE_FLOATING) massp2 = ft.massp[c2 & CODE_MASKVALUE];
+                  }
+                  arp1 += massp2 * (dvx * frx + dvy * fry + dvz * frz) * (vr1.w / vr2.w);
                   const float dot = drx * dvx + dry * dvy + drz * dvz;
                   const float dot_rr2 = dot / (rr2 + K.eta2);
                   visc = fmaxf(dot_rr2, visc);
@@ -227,8 +254,19 @@ __global__ __launch_bounds__(256) void k_interaction(DevScalars* __restrict__ sc
 }
 
 void launch_interaction(hipStream_t stm, unsigned cap, DevScalars* sc, const float4* poscell, const float4* velrhop,
-                        const float* press, const unsigned* begincell, DivGrid g, const KConst& K, float4* arace) {
+                        const float* press, const unsigned* begincell, DivGrid g, const KConst& K, float4* arace,
+                        const typecode* code, const float* ftmassp) {
   const unsigned nb = (cap + 255) / 256;
+  if (ftmassp) {
+    const FtView ft = {code, ftmassp};
+    switch (K.tdensity) {
+      case 0: hipLaunchKernelGGL((k_interaction<0, false, true>), dim3(nb), dim3(256), 0, stm, sc, poscell, velrhop, press, begincell, g, K, arace, ft); break;
+      case 1: hipLaunchKernelGGL((k_interaction<1, false, true>), dim3(nb), dim3(256), 0, stm, sc, poscell, velrhop, press, begincell, g, K, arace, ft); break;
+      case 2: hipLaunchKernelGGL((k_interaction<2, false, true>), dim3(nb), dim3(256), 0, stm, sc, poscell, velrhop, press, begincell, g, K, arace, ft); break;
+      default: hipLaunchKernelGGL((k_interaction<3, false, true>), dim3(nb), dim3(256), 0, stm, sc, poscell, velrhop, press, begincell, g, K, arace, ft); break;
+    }
+    return;
+  }
   switch (K.tdensity) {
     case 0: hipLaunchKernelGGL(k_interaction<0>, dim3(nb), dim3(256), 0, stm, sc, poscell, velrhop, press, begincell, g, K, arace); break;
     case 1: hipLaunchKernelGGL(k_interaction<1>, dim3(nb), dim3(256), 0, stm, sc, poscell, velrhop, press, begincell, g, K, arace); break;

@@ -5,6 +5,7 @@
 // particle capacity; the live counts (np, npb, npbok) are read on the device from
 // DevScalars, so no host round trip is needed between phases.
 #pragma once
+#include "../../include/sphcore.h"
 #include "sph_device.hpp"
 
 namespace sphx {
@@ -22,6 +23,40 @@ struct PartArrays {
   double* poszpre = nullptr;
   float4* velrhoppre = nullptr;
 };
+
+// JSphCpu::UpdatePos (JSphCpu.cpp:1240-1293), single domain, no periodic/symmetry.
+__device__ __forceinline__ void update_pos(const KConst& K, double rx, double ry, double rz, double movx, double movy,
+                                           double movz, bool outrhop, unsigned p, const PartArrays& a) {
+  const bool outmove = (fabsf(float(movx)) > K.movlimit || fabsf(float(movy)) > K.movlimit ||
+                        fabsf(float(movz)) > K.movlimit);
+  rx += movx;
+  ry += movy;
+  rz += movz;
+  const double dx = rx - K.map_realposmin_x, dy = ry - K.map_realposmin_y, dz = rz - K.map_realposmin_z;
+  const bool out = (dx != dx || dy != dy || dz != dz || dx < 0 || dy < 0 || dz < 0 || dx >= K.map_realsize_x ||
+                    dy >= K.map_realsize_y || dz >= K.map_realsize_z);
+  a.posxy[p] = make_double2(rx, ry);
+  a.posz[p] = rz;
+  if (outrhop || outmove || out) {
+    typecode rcode = a.code[p];
+    if (out) rcode = CodeSetNormal(rcode) | CODE_OUTPOS;
+    else if (outrhop) rcode = CodeSetNormal(rcode) | CODE_OUTRHOP;
+    else rcode = CodeSetNormal(rcode) | CODE_OUTMOVE;
+    a.code[p] = rcode;
+    a.dcell[p] = DCELL_OUT;
+  } else {
+    const unsigned cx = unsigned(dx / K.scelld), cy = unsigned(dy / K.scelld), cz = unsigned(dz / K.scelld);
+    a.dcell[p] = DcelCell(K.domcellcode, cx, cy, cz);
+  }
+}
+// Boundary and floating particles: UpdatePos with outrhop=false (MoveLinBound/MoveMatBound,
+// JSphCpu.cpp:1699,1721; RunFloating, JSphCpuSingle.cpp:969).
+__device__ __forceinline__ void update_pos_bound(const KConst& K, double rx, double ry, double rz, double movx,
+                                                 double movy, double movz, unsigned p, const PartArrays& a,
+                                                 DevScalars* sc) {
+  (void)sc;
+  update_pos(K, rx, ry, rz, movx, movy, movz, false, p, a);
+}
 
 // Scratch of the cell sort (DivideGpu).
 struct SortScratch {
@@ -55,8 +90,11 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
                    float4* poscell, float* press, int xoff);
 
 // ---- interaction (cusph::Interaction_Forces, JSphGpu_ker.cu:788-885) ----
+// With floating bodies (ftmassp != nullptr: particle mass per body, `code` of the
+// sorted particles) the kernel reads the p2 codes (JSphCpu.cpp:692-703).
 void launch_interaction(hipStream_t stm, unsigned cap, DevScalars* sc, const float4* poscell, const float4* velrhop,
-                        const float* press, const unsigned* begincell, DivGrid g, const KConst& K, float4* arace);
+                        const float* press, const unsigned* begincell, DivGrid g, const KConst& K, float4* arace,
+                        const typecode* code = nullptr, const float* ftmassp = nullptr);
 // Bound p1 only (grid over the bound capacity) — used beside the tiled fluid kernel.
 void launch_interaction_bound(hipStream_t stm, unsigned npbcap, DevScalars* sc, const float4* poscell,
                               const float4* velrhop, const unsigned* begincell, DivGrid g, const KConst& K,
@@ -93,6 +131,61 @@ void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst&
                     DivGrid g);
 void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
                     DivGrid g);
+
+// ---- moving boundaries and floating bodies (sph_bodies.hip) ----
+constexpr int MOT_MAXOBJ = 32, MOT_MAXACT = 4;
+struct MotMov {     // one movement of the program (JMotionMov*), units as SphMotionMov
+  int type, nextidx, prev, pad;
+  double time;      // duration
+  double v[3], v2[3], phase[3], p1[3], p2[3];
+  double ang, ang2, ang3;
+};
+struct MotEvt {     // JMotionEvent
+  int obj, mov;
+  double start, finish;
+};
+struct MotAct {     // JMotionMovActive
+  int mov, del;
+  double start, finish, eventfinish;
+  double vel[3], velang, phase[3], phaseuni;
+};
+struct MotObj {     // JMotionObj run state
+  int active, moving, na, pad;
+  MotAct act[MOT_MAXACT];
+};
+struct MotOut {     // JMotionListData of one object for the step: 0 none, 1 linear, 2 matrix
+  int type, pad;
+  double mov[3], vel[3];
+  double m[12];
+};
+struct MotionDev {
+  int nobj, eventnext, objsactive, overflow;
+  MotObj obj[MOT_MAXOBJ];
+  MotOut out[MOT_MAXOBJ];
+};
+// Floating body (StFloatingData + StFtoForces/StFtoForcesRes), device resident.
+struct FtBody {
+  unsigned begin, count;   // floating-particle index range (idp - CaseNpb)
+  unsigned constraints;    // FTCON_* bits (DualSphDef.h:445-453)
+  int skip;                // TimeStep < FtPause in this call
+  float mass, massp, ftpause, pad;
+  float inertia[9];
+  double center[3];
+  float angles[3], fvel[3], fomega[3], facelin[3], faceang[3];
+  // per call
+  float face[3], fomegaace[3], fvelres[3], fomegares[3];
+  double fcenterres[3];
+};
+// k_motion over [sc->tstep0, +sc->last_dt) (or [t0, t0+dt) when t0 >= 0: restart
+// catch-up, no particle update), then the boundary particles.
+void launch_motion(hipStream_t stm, unsigned npbcap, DevScalars* sc, const KConst& K, MotionDev* md,
+                   const MotMov* movs, const MotEvt* evts, const PartArrays& a, float4* normal);
+void launch_motion_advance(hipStream_t stm, DevScalars* sc, MotionDev* md, const MotMov* movs, const MotEvt* evts,
+                           double t0, double dt);
+void launch_ft_ridp(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, unsigned casenpb,
+                    unsigned nftp, unsigned* ftridp);
+void launch_floating(hipStream_t stm, DevScalars* sc, const KConst& K, FtBody* bodies, int nbodies,
+                     const unsigned* ftridp, unsigned nftp, const float4* arace, const PartArrays& a, bool predictor);
 
 // ---- slab decomposition (sph_slab.hip) ----
 // A particle MIGRATING to a neighbour: its full state, 96 B.

@@ -270,6 +270,7 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   }
   npb0_ = 0;
   for (unsigned p : sel) npb0_ += (p < cdef.npb ? 1u : 0u);
+  casenpb_ = cdef.npb;
   const unsigned n = unsigned(sel.size());
   cap_ = slab() ? n + std::max(n / 2, 65536u) : n;
   keybits_ = bits_for(G.boxdiscard, 1);
@@ -431,8 +432,19 @@ void SphGpuSingle::Upload(const SphParticlesHost& h, const std::vector<unsigned>
     pxy[i] = make_double2(x, y);
     pz[i] = z;
     vr[i] = make_float4(h.vel[3 * p], h.vel[3 * p + 1], h.vel[3 * p + 2], h.rhop[p]);
-    // LoadCodeParticles (JSph.cpp:1257): the case has one fixed and one fluid MK block.
-    code[i] = (i < npb0_ ? typecode(0) : CODE_TYPE_FLUID);
+    // LoadCodeParticles (JSph.cpp:1257): the codes of the case's MK blocks when given,
+    // else one fixed and one fluid block.
+    if (h.code) {
+      code[i] = h.code[p];
+      const typecode t = CodeType(code[i]);
+      if (!CodeIsNormal(code[i]) || (i < npb0_) != (t < CODE_TYPE_FLOATING))
+        throw SphError(SPH_ERR_ARG, "particle codes: boundary (fixed/moving) particles must be the first npb");
+      if (slab() && (t == CODE_TYPE_MOVING || t == CODE_TYPE_FLOATING))
+        throw SphError(SPH_ERR_UNSUPPORTED,
+                       "moving/floating bodies are not implemented on the slab decomposition");
+    } else {
+      code[i] = (i < npb0_ ? typecode(0) : CODE_TYPE_FLUID);
+    }
     // JSph::CheckRhopLimits (JSph.cpp:2021-2030).
     if (i >= npb0_ && (vr[i].w < C.rhopoutmin || C.rhopoutmax < vr[i].w))
       throw SphError(SPH_ERR_ARG, "Initial fluid density is out of limits.");
@@ -484,6 +496,7 @@ void SphGpuSingle::UploadNormals(const SphCaseDef& cdef, const SphParticlesHost&
 
 // Restart: TimeStep and SymplecticDtPre of the loaded PART (JSph::InitRun, JSph.cpp:2094-2106).
 void SphGpuSingle::SetTime(double time, double symdtpre) {
+  if (motion_) throw SphError(SPH_ERR_STATE, "set the restart time before the motion (it is advanced to that time)");
   Sync();
   check_hip(hipMemcpy(&sc_->time, &time, sizeof(double), hipMemcpyHostToDevice), "set time");
   if (symdtpre > 0)
@@ -615,6 +628,7 @@ void SphGpuSingle::RunCellDivide() {
                 G.xoff);
   std::swap(cur_, alt_);
   if (tiled_) launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_);
+  if (nftp_) launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_);
   TimedEnd(2);
 }
 
@@ -634,7 +648,8 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
                        arace_);
   } else {
     TimedBegin(0);
-    launch_interaction(stream, cap_, sc_, poscell_, cur_.velrhop, press_, begincell_, G, K, arace_);
+    launch_interaction(stream, cap_, sc_, poscell_, cur_.velrhop, press_, begincell_, G, K, arace_, cur_.code,
+                       ftmassp_);
   }
   TimedEnd(0);
 }
@@ -678,20 +693,177 @@ void SphGpuSingle::ComputeSymplecticCorr() {
 }
 
 void SphGpuSingle::ComputeStep() {
+  stepped_ = true;
   if (step_algorithm_ == SPH_STEP_VERLET) {
     Interaction_Forces(1);
     DtVariable(DT_VERLET);
     ComputeVerlet();
+    if (nftbodies_) RunFloating(false);
   } else {
     Interaction_Forces(2);
     DtVariable(DT_SYM_PRE);
     ComputeSymplecticPre();
+    if (nftbodies_) RunFloating(true);
     RunCellDivide();
     Interaction_Forces(3);
     DtVariable(DT_SYM_COR);
     ComputeSymplecticCorr();
+    if (nftbodies_) RunFloating(false);
   }
+  if (nmotobj_) RunMotion();
   RunCellDivide();
+}
+
+// ---- moving boundaries and floating bodies ------------------------------------------------
+void SphGpuSingle::RunMotion() {
+  TimedBegin(1);
+  launch_motion(stream, npb0_, sc_, K, motion_, motmovs_, motevts_, cur_, normal_);
+  TimedEnd(1);
+}
+
+void SphGpuSingle::RunFloating(bool predictor) {
+  TimedBegin(1);
+  launch_floating(stream, sc_, K, ftbodies_, nftbodies_, ftridp_, nftp_, arace_, cur_, predictor);
+  TimedEnd(1);
+}
+
+// JDsMotion::Init (JDsMotion.cpp:94-106) + JMotion::Prepare (JMotion.cpp:303-317).
+void SphGpuSingle::SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* movs, unsigned nevt,
+                             const SphMotionEvent* evts) {
+  if (stepped_ || motion_) throw SphError(SPH_ERR_STATE, "the motion is configured once, before the first step");
+  if (slab()) throw SphError(SPH_ERR_UNSUPPORTED, "moving boundaries are not implemented on the slab decomposition");
+  if (!nobj || nobj > unsigned(MOT_MAXOBJ)) throw SphError(SPH_ERR_UNSUPPORTED, "number of moving objects out of range");
+  if ((nmov && !movs) || (nevt && !evts)) throw SphError(SPH_ERR_ARG, "motion arrays missing");
+  std::vector<MotMov> mv(std::max(nmov, 1u));
+  auto find = [&](int obj, int id) -> int {
+    for (unsigned k = 0; k < nmov; k++)
+      if (movs[k].obj == obj && movs[k].id == id) return int(k);
+    return -1;
+  };
+  for (unsigned k = 0; k < nmov; k++) {
+    const SphMotionMov& m = movs[k];
+    if (m.obj < 0 || unsigned(m.obj) >= nobj) throw SphError(SPH_ERR_ARG, "movement of an unknown object");
+    if (m.type < SPH_MOV_WAIT || m.type > SPH_MOV_ROTSINU) throw SphError(SPH_ERR_UNSUPPORTED, "movement type");
+    if (!(m.duration >= 0)) throw SphError(SPH_ERR_UNSUPPORTED, "movements with a negative duration (flash)");
+    MotMov& d = mv[k];
+    std::memset(&d, 0, sizeof(d));
+    d.type = m.type;
+    d.prev = m.prev;
+    d.time = m.duration;
+    d.nextidx = -1;
+    if (m.next) {
+      d.nextidx = find(m.obj, m.next);
+      if (d.nextidx < 0) throw SphError(SPH_ERR_ARG, "movement `next` is not defined in its object");
+    }
+    for (int c = 0; c < 3; c++) {
+      d.v[c] = m.vec[c];
+      d.v2[c] = m.vec2[c];
+      d.phase[c] = m.phase[c];
+      d.p1[c] = m.axisp1[c];
+      d.p2[c] = m.axisp2[c];
+    }
+    d.ang = m.ang;
+    d.ang2 = m.ang2;
+    d.ang3 = m.ang3;
+  }
+  // events ordered from last to first start, with the reference's exchange sort
+  std::vector<MotEvt> ev(nevt);
+  for (unsigned k = 0; k < nevt; k++) {
+    ev[k].obj = evts[k].obj;
+    ev[k].mov = find(evts[k].obj, evts[k].mov);
+    if (ev[k].mov < 0) throw SphError(SPH_ERR_ARG, "event of an undefined movement");
+    ev[k].start = evts[k].start;
+    ev[k].finish = evts[k].finish;
+  }
+  for (unsigned c = 0; c + 1 < nevt; c++)
+    for (unsigned c2 = c + 1; c2 < nevt; c2++)
+      if (ev[c].start < ev[c2].start) std::swap(ev[c], ev[c2]);
+  MotionDev md;
+  std::memset(&md, 0, sizeof(md));
+  md.nobj = int(nobj);
+  md.eventnext = int(nevt) - 1;
+  check_hip(hipMalloc((void**)&motion_, sizeof(MotionDev)), "hipMalloc motion");
+  allocs_.push_back(motion_);
+  check_hip(hipMalloc((void**)&motmovs_, sizeof(MotMov) * mv.size()), "hipMalloc motion");
+  allocs_.push_back(motmovs_);
+  check_hip(hipMalloc((void**)&motevts_, sizeof(MotEvt) * std::max(nevt, 1u)), "hipMalloc motion");
+  allocs_.push_back(motevts_);
+  check_hip(hipMemcpy(motion_, &md, sizeof(md), hipMemcpyHostToDevice), "upload motion");
+  check_hip(hipMemcpy(motmovs_, mv.data(), sizeof(MotMov) * mv.size(), hipMemcpyHostToDevice), "upload motion");
+  if (nevt) check_hip(hipMemcpy(motevts_, ev.data(), sizeof(MotEvt) * nevt, hipMemcpyHostToDevice), "upload motion");
+  nmotobj_ = nobj;
+  // restart: JDsMotion::SetTimeMod/ResetTime run the program from 0 to the PART time
+  double t0 = 0;
+  check_hip(hipMemcpy(&t0, &sc_->time, sizeof(double), hipMemcpyDeviceToHost), "read time");
+  if (t0 > 0) launch_motion_advance(stream, sc_, motion_, motmovs_, motevts_, 0.0, t0);
+  Sync();
+}
+
+// JSph::LoadCaseConfig floating objects (JSph.cpp:1046-1100).
+void SphGpuSingle::SetFloatings(unsigned nft, const SphFloatingDef* defs, double ftpause) {
+  if (stepped_ || ftbodies_) throw SphError(SPH_ERR_STATE, "the floating bodies are configured once, before the first step");
+  if (slab()) throw SphError(SPH_ERR_UNSUPPORTED, "floating bodies are not implemented on the slab decomposition");
+  if (!nft || !defs) throw SphError(SPH_ERR_ARG, "no floating bodies");
+  std::vector<FtBody> b(nft);
+  std::vector<float> massp(nft);
+  unsigned begin = casenpb_;
+  for (unsigned c = 0; c < nft; c++) {
+    const SphFloatingDef& d = defs[c];
+    if (d.idbegin != begin || !d.count) throw SphError(SPH_ERR_ARG, "floating blocks must follow the boundary in idp");
+    FtBody& f = b[c];
+    std::memset(&f, 0, sizeof(f));
+    f.begin = d.idbegin - casenpb_;
+    f.count = d.count;
+    f.mass = float(d.massbody);
+    f.massp = float(d.masspart);
+    f.ftpause = float(ftpause);  // GetValueFloat (JSph.cpp:688)
+    for (int k = 0; k < 9; k++) f.inertia[k] = float(d.inertia[k]);
+    for (int k = 0; k < 3; k++) {
+      f.center[k] = d.center[k];
+      f.fvel[k] = float(d.linvelini[k]);
+      f.fomega[k] = float(d.angvelini[k]);
+    }
+    // ComputeConstraintsValue (DualSphDef.h:456-464)
+    f.constraints = (d.translationfree[0] ? 0u : 1u) | (d.translationfree[1] ? 0u : 2u) |
+                    (d.translationfree[2] ? 0u : 4u) | (d.rotationfree[0] ? 0u : 8u) |
+                    (d.rotationfree[1] ? 0u : 16u) | (d.rotationfree[2] ? 0u : 32u);
+    massp[c] = f.massp;
+    begin += d.count;
+  }
+  const unsigned nftp = begin - casenpb_;
+  check_hip(hipMalloc((void**)&ftbodies_, sizeof(FtBody) * nft), "hipMalloc floatings");
+  allocs_.push_back(ftbodies_);
+  check_hip(hipMalloc((void**)&ftmassp_, sizeof(float) * nft), "hipMalloc floatings");
+  allocs_.push_back(ftmassp_);
+  check_hip(hipMalloc((void**)&ftridp_, sizeof(unsigned) * nftp), "hipMalloc floatings");
+  allocs_.push_back(ftridp_);
+  check_hip(hipMemcpy(ftbodies_, b.data(), sizeof(FtBody) * nft, hipMemcpyHostToDevice), "upload floatings");
+  check_hip(hipMemcpy(ftmassp_, massp.data(), sizeof(float) * nft, hipMemcpyHostToDevice), "upload floatings");
+  nftbodies_ = int(nft);
+  nftp_ = nftp;
+  tiled_ = false;  // floating p2 carry their own mass: the per-particle kernel (csrc/sph_interaction.hip)
+  launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_);
+  Sync();
+}
+
+unsigned SphGpuSingle::Floatings(SphFloatingState* out, unsigned cap) {
+  if (!nftbodies_) return 0;
+  std::vector<FtBody> b(nftbodies_);
+  Sync();
+  check_hip(hipMemcpy(b.data(), ftbodies_, sizeof(FtBody) * b.size(), hipMemcpyDeviceToHost), "read floatings");
+  for (unsigned c = 0; c < unsigned(nftbodies_) && c < cap && out; c++) {
+    SphFloatingState& o = out[c];
+    std::memset(&o, 0, sizeof(o));
+    for (int k = 0; k < 3; k++) {
+      o.center[k] = b[c].center[k];
+      o.fvel[k] = b[c].fvel[k];
+      o.fomega[k] = b[c].fomega[k];
+      o.angles[k] = b[c].angles[k];
+      o.facelin[k] = b[c].facelin[k];
+      o.faceang[k] = b[c].faceang[k];
+    }
+  }
+  return unsigned(nftbodies_);
 }
 
 void SphGpuSingle::Run(unsigned nsteps) {

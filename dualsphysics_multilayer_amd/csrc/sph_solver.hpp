@@ -75,6 +75,10 @@ class SphGpuSingle {
   void SetTime(double time, double symdtpre);
   void Timing(double out_ms[4], uint64_t* launches);
   void CheckErrors();
+  // Moving boundaries / floating bodies (sph_bodies.hip), configured before the first step.
+  void SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* movs, unsigned nevt, const SphMotionEvent* evts);
+  void SetFloatings(unsigned nft, const SphFloatingDef* defs, double ftpause);
+  unsigned Floatings(SphFloatingState* out, unsigned cap);
 
   SphConstants C{};
   KConst K{};
@@ -92,6 +96,8 @@ class SphGpuSingle {
   void Upload(const SphParticlesHost& init, const std::vector<unsigned>& sel, unsigned nown);
   void UploadNormals(const SphCaseDef& cdef, const SphParticlesHost& init);
   void Exchange();
+  void RunMotion();                 // JSphCpu::RunMotion after ComputeStep (JSphCpuSingle.cpp:1096)
+  void RunFloating(bool predictor); // JSphCpuSingle::RunFloating
   void TimedBegin(int phase);
   void TimedEnd(int phase);
 
@@ -117,6 +123,18 @@ class SphGpuSingle {
   double* dttrace_ = nullptr;
   unsigned tracecap_ = 1u << 16;
   unsigned long long* pairs_ = nullptr;
+  // moving boundaries (device motion program) and floating bodies
+  MotionDev* motion_ = nullptr;
+  MotMov* motmovs_ = nullptr;
+  MotEvt* motevts_ = nullptr;
+  unsigned nmotobj_ = 0;
+  FtBody* ftbodies_ = nullptr;
+  unsigned* ftridp_ = nullptr;   // floating particle (idp - CaseNpb) -> position, per divide
+  float* ftmassp_ = nullptr;     // particle mass per body (interaction)
+  int nftbodies_ = 0;
+  unsigned nftp_ = 0;            // floating particles of the case (CaseNfloat)
+  unsigned casenpb_ = 0;         // CaseNpb: first floating idp
+  bool stepped_ = false;         // a step was issued (bodies are configured before it)
   std::vector<void*> allocs_;   // fixed-size allocations
   std::vector<void*> pallocs_;  // capacity-sized (per-particle) allocations
   // slab decomposition

@@ -93,6 +93,7 @@ __global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double d
   if (mode != DT_SYM_COR) {
     // Step bookkeeping: TimeStep+=stepdt (JSphCpuSingle.cpp:1099).
     const double stepdt = sc->dt;
+    sc->tstep0 = sc->time;
     if (dttrace && tracecap) dttrace[sc->nstep % tracecap] = stepdt;
     sc->time += stepdt;
     sc->last_dt = stepdt;
@@ -115,32 +116,6 @@ __device__ __forceinline__ bool slab_ghost(const KConst& K, const DivGrid& g, un
   return true;
 }
 
-// JSphCpu::UpdatePos (JSphCpu.cpp:1240-1293), single domain, no periodic/symmetry.
-__device__ __forceinline__ void update_pos(const KConst& K, double rx, double ry, double rz, double movx, double movy,
-                                           double movz, bool outrhop, unsigned p, const PartArrays& a) {
-  const bool outmove = (fabsf(float(movx)) > K.movlimit || fabsf(float(movy)) > K.movlimit ||
-                        fabsf(float(movz)) > K.movlimit);
-  rx += movx;
-  ry += movy;
-  rz += movz;
-  const double dx = rx - K.map_realposmin_x, dy = ry - K.map_realposmin_y, dz = rz - K.map_realposmin_z;
-  const bool out = (dx != dx || dy != dy || dz != dz || dx < 0 || dy < 0 || dz < 0 || dx >= K.map_realsize_x ||
-                    dy >= K.map_realsize_y || dz >= K.map_realsize_z);
-  a.posxy[p] = make_double2(rx, ry);
-  a.posz[p] = rz;
-  if (outrhop || outmove || out) {
-    typecode rcode = a.code[p];
-    if (out) rcode = CodeSetNormal(rcode) | CODE_OUTPOS;
-    else if (outrhop) rcode = CodeSetNormal(rcode) | CODE_OUTRHOP;
-    else rcode = CodeSetNormal(rcode) | CODE_OUTMOVE;
-    a.code[p] = rcode;
-    a.dcell[p] = DCELL_OUT;
-  } else {
-    const unsigned cx = unsigned(dx / K.scelld), cy = unsigned(dy / K.scelld), cz = unsigned(dz / K.scelld);
-    a.dcell[p] = DcelCell(K.domcellcode, cx, cy, cz);
-  }
-}
-
 // ComputeVerlet (JSphCpu.cpp:1381-1399): bound -> ComputeVelrhopBound, fluid -> ComputeVerletVarsFluid.
 // New values are written in velrhopm1 (the caller swaps velrhop/velrhopm1 afterwards).
 __global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ sc, KConst K, int euler,
@@ -158,6 +133,10 @@ __global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ s
     return;
   }
   const float4 vr1 = a.velrhop[p];
+  if (CodeType(a.code[p]) == CODE_TYPE_FLOATING) {  // JSphCpu.cpp:1352-1355: RunFloating moves it
+    a.velrhopm1[p] = make_float4(vr1.x, vr1.y, vr1.z, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
+    return;
+  }
   const double dt205 = 0.5 * dt * dt;
   const double agx = double(ra.x) + K.gravxd, agy = double(ra.y) + K.gravyd, agz = double(ra.z) + K.gravzd;
   const double dx = double(vr1.x) * dt + agx * dt205;
@@ -197,6 +176,12 @@ __global__ __launch_bounds__(256) void k_sym_pre(const DevScalars* __restrict__ 
     return;
   }
   typecode rcode = a.code[p];
+  if (CodeType(rcode) == CODE_TYPE_FLOATING) {  // JSphCpu.cpp:1475-1478 (+ position copied, :1498)
+    a.velrhop[p] = make_float4(vp.x, vp.y, vp.z, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
+    a.posxy[p] = pxy;
+    a.posz[p] = pz;
+    return;
+  }
   const double dx = double(vp.x) * dt05, dy = double(vp.y) * dt05, dz = double(vp.z) * dt05;
   const bool outrhop = (rhopnew < K.rhopoutmin || rhopnew > K.rhopoutmax);
   a.velrhop[p] = make_float4(float(double(vp.x) + (double(ra.x) + K.gravxd) * dt05),
@@ -236,6 +221,12 @@ __global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ 
     return;  // boundary keeps its position (already restored by the predictor)
   }
   typecode rcode = a.code[p];
+  if (CodeType(rcode) == CODE_TYPE_FLOATING) {  // JSphCpu.cpp:1577-1580, 1595
+    a.velrhop[p] = make_float4(vp.x, vp.y, vp.z, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
+    a.posxy[p] = a.posxypre[p];
+    a.posz[p] = a.poszpre[p];
+    return;
+  }
   const float4 nv = make_float4(float(double(vp.x) + (double(ra.x) + K.gravxd) * dt),
                                 float(double(vp.y) + (double(ra.y) + K.gravyd) * dt),
                                 float(double(vp.z) + (double(ra.z) + K.gravzd) * dt), rhopnew);

@@ -2,7 +2,8 @@
 (SURVEY.md §8(f) row 2).
 
 Mirrors what ``JSph`` reads before the first step, restricted to what the hot path of
-this core runs (fixed DBC boundaries + fluid, Wendland, artificial viscosity, DDT 0-3,
+this core runs (fixed and moving DBC/mDBC boundaries, RigidAlgorithm=1 floating bodies, fluid,
+Wendland, artificial viscosity, DDT 0-3,
 Verlet / Symplectic, no periodicity); anything else raises ``CaseError`` the way the
 reference refuses an invalid configuration, never silently ignored:
 
@@ -279,9 +280,8 @@ class XmlCase:
         if sp is not None:
             for ch in sp:  # accinputs, chrono, wavepaddles, mlayerpistons, inout, gauges, ...
                 raise CaseError(f"<special><{ch.tag}> is not supported by this core.")
-        if ex.find("motion") is not None and len(list(ex.find("motion"))):
-            raise CaseError("<motion> (moving boundaries) is not supported by this core.")
         self._load_blocks(_node(ex, "particles"))
+        self._load_motion(ex.find("motion"))
         dfix = overrides.pop("domain_fixed", None)
         if dfix is not None:  # -domain_fixed: JSph::ConfigDomainFixed (JSph.cpp:343-346, 856)
             self._domain.clear()
@@ -315,8 +315,9 @@ class XmlCase:
         self._check_loaded(h, prt)
         self.time0 = float(h["timestep"]) if self.partbegin else 0.0
         self.symdtpre0 = float(h.get("symplectic_dtpre", 0.0)) if self.partbegin else 0.0
-        # bound (fixed) blocks first, stable: the solver's npb leading entries
-        isb = prt["idp"] < np.uint32(self.case_nbound)
+        # boundary (fixed + moving) blocks first, stable: the solver's npb leading entries;
+        # floating particles sit among the fluid ones (CaseNpb, JSph.cpp)
+        isb = prt["idp"] < np.uint32(self.case_npb)
         order = np.concatenate([np.flatnonzero(isb), np.flatnonzero(~isb)])
         self.idp = np.ascontiguousarray(prt["idp"][order], np.uint32)
         self.pos = np.ascontiguousarray(prt["pos"][order], np.float64)
@@ -324,8 +325,13 @@ class XmlCase:
         self.rhop = np.ascontiguousarray(prt["rhop"][order], np.float32)
         self.np = int(self.idp.size)
         self.npb = int(isb.sum())
-        if self.npb != self.case_nfixed:
-            raise CaseError(f"{fn}: {self.npb} boundary particles loaded, the case has {self.case_nfixed}.")
+        if self.npb != self.case_npb:
+            raise CaseError(f"{fn}: {self.npb} boundary particles loaded, the case has {self.case_npb}.")
+        if self.floatings and self.partbegin:
+            raise CaseError("Restart of a case with floating bodies (PartFloat.fbi4 state) is not supported by "
+                            "this core.")
+        if self.floatings and self.rigidalgorithm != 1:
+            raise CaseError("Only RigidAlgorithm=1 (SPH) floating bodies are supported by this core.")
         # case limits (JPartsLoad4 CasePosMin/Max; computed when the file has none)
         cmin, cmax = list(h["case_posmin"]), list(h["case_posmax"])
         if cmin == cmax:
@@ -362,6 +368,8 @@ class XmlCase:
             raise CaseError("Old normal data file format (XXX_NormalData.nbi4) is invalid for current version.")
         if not out[: self.npb].any():
             raise CaseError("No valid normal vectors for using mDBC.")
+        if out[self.npb:].any():  # UseNormalsFt (JSph.cpp:1305): mDBC on floating bodies
+            raise CaseError("mDBC on floating bodies (floating normals) is not supported by this core.")
         return out
 
     @property
@@ -396,6 +404,8 @@ class XmlCase:
         rig = p.int("RigidAlgorithm", True, 1)
         if rig not in (0, 1, 2, 3):
             raise CaseError("Rigid algorithm is not valid.")
+        self.rigidalgorithm = rig
+        self.ftpause = float(np.float32(p.num("FtPause", True, 0.0)))  # GetValueFloat (JSph.cpp:688)
         self.step_algorithm = p.int("StepAlgorithm", True, 1)
         if self.step_algorithm not in (1, 2):
             raise CaseError("Step algorithm is not valid.")
@@ -465,36 +475,167 @@ class XmlCase:
         blocks = []
         for e in node:
             if e.tag not in ("fixed", "moving", "floating", "fluid"):
+                if e.tag == "properties" or e.tag.startswith("_") or e.tag == "summary":
+                    continue
                 raise CaseError(f"<particles>: unknown block <{e.tag}>.")
-            blocks.append(dict(type=e.tag, mk=int(e.get("mk")), begin=int(e.get("begin")),
-                               count=int(e.get("count")),
-                               mktype=int(e.get("mkfluid") if e.tag == "fluid" else e.get("mkbound"))))
-        if any(b["type"] in ("moving", "floating") for b in blocks):
-            raise CaseError("Moving / floating particle blocks are not supported by this core.")
-        nfix = [b for b in blocks if b["type"] == "fixed"]
-        nfl = [b for b in blocks if b["type"] == "fluid"]
-        if [b["type"] for b in blocks] != ["fixed"] * len(nfix) + ["fluid"] * len(nfl):
-            raise CaseError("<particles>: fixed blocks must precede fluid blocks.")
+            b = dict(type=e.tag, mk=int(e.get("mk")), begin=int(e.get("begin")), count=int(e.get("count")),
+                     mktype=int(e.get("mkfluid") if e.tag == "fluid" else e.get("mkbound")))
+            if e.tag == "floating":
+                b["floating"] = self._load_floating(e)
+            blocks.append(b)
+        kinds = ("fixed", "moving", "floating", "fluid")
+        bytype = {k: [b for b in blocks if b["type"] == k] for k in kinds}
+        if [b["type"] for b in blocks] != [k for k in kinds for _ in bytype[k]]:
+            raise CaseError("<particles>: blocks must be ordered fixed, moving, floating, fluid.")
         begin = 0
         for b in blocks:
             if b["begin"] != begin:
                 raise CaseError("<particles>: blocks must be contiguous in idp.")
             begin += b["count"]
-        # JSphMk::Config codes: the block index within its type
-        for i, b in enumerate(nfix):
-            b["code"] = CODE_TYPE_FIXED | i
-        for i, b in enumerate(nfl):
-            b["code"] = CODE_TYPE_FLUID | i
+        # JSphMk::Config codes: the block index within its type (JSphMk.cpp:108-114)
+        base = {"fixed": CODE_TYPE_FIXED, "moving": CODE_TYPE_MOVING, "floating": CODE_TYPE_FLOATING,
+                "fluid": CODE_TYPE_FLUID}
+        for k in kinds:
+            for i, b in enumerate(bytype[k]):
+                b["code"] = base[k] | i
         self.blocks = blocks
         self.case_np = begin
-        self.case_nfixed = sum(b["count"] for b in nfix)
-        self.case_nbound = self.case_nfixed
-        self.case_nfluid = sum(b["count"] for b in nfl)
+        self.case_nfixed = sum(b["count"] for b in bytype["fixed"])
+        self.case_nmoving = sum(b["count"] for b in bytype["moving"])
+        self.case_nfloat = sum(b["count"] for b in bytype["floating"])
+        self.case_npb = self.case_nfixed + self.case_nmoving
+        self.case_nbound = self.case_npb + self.case_nfloat
+        self.case_nfluid = sum(b["count"] for b in bytype["fluid"])
+        self.moving_blocks = bytype["moving"]
+        self.floatings = [dict(b["floating"], idbegin=b["begin"], count=b["count"], mkbound=b["mktype"])
+                          for b in bytype["floating"]]
+
+    # -- JCasePartBlock_Floating::ReadXml (JCaseParts.cpp:248-290) ------------------------------
+    @staticmethod
+    def _load_floating(e) -> dict:
+        def d3(name, optional=False, default=(0.0, 0.0, 0.0)):
+            x = e.find(name)
+            if x is None:
+                if optional:
+                    return tuple(default)
+                raise CaseError(f"<floating>: the item is not found '{name}'.")
+            return tuple(_attr_double(x, a, name) for a in "xyz")
+
+        for unsup in ("linearvel", "angularvel", "linearforce", "angularforce"):
+            if e.find(unsup) is not None:
+                raise CaseError(f"<floating><{unsup}> (imposed velocity/force) is not supported by this core.")
+        f = dict(massbody=_elem_double(e, "massbody"), masspart=_elem_double(e, "masspart"), center=d3("center"))
+        ine = e.find("inertia")
+        if ine is None:
+            raise CaseError("<floating>: the item is not found 'inertia'.")
+        if all(ine.get(a) is not None for a in "xyz"):
+            v = d3("inertia")
+            f["inertia"] = (v[0], 0.0, 0.0, 0.0, v[1], 0.0, 0.0, 0.0, v[2])
+        else:  # JXml::ReadElementMatrix3d: <values v11=.. v12=.. ... v33=../>
+            vals = ine.find("values")
+            src = vals if vals is not None else ine
+            f["inertia"] = tuple(_attr_double(src, "v%d%d" % (r, c), "inertia") for r in (1, 2, 3) for c in (1, 2, 3))
+
+        def i3(a, b):
+            if e.find(a) is not None and e.find(b) is not None:
+                raise CaseError(f"Only '{a}' or '{b}' must be defined.")
+            x = e.find(a) if e.find(a) is not None else e.find(b)
+            if x is None:
+                return (1, 1, 1)
+            return tuple(0 if int(float(x.get(k, "1"))) == 0 else 1 for k in "xyz")
+
+        f["translationfree"] = i3("translation", "translationDOF")
+        f["rotationfree"] = i3("rotation", "rotationDOF")
+        f["linvelini"] = d3("linearvelini" if e.find("linearvelini") is not None else "velini", True)
+        f["angvelini"] = d3("angularvelini" if e.find("angularvelini") is not None else "omegaini", True)
+        return f
+
+    # -- JMotion::ReadXml (JMotion.cpp:556-700) + JDsMotion::ConfigObjects (JDsMotion.cpp:67-89) --
+    def _load_motion(self, node):
+        self.motion = None
+        nobj = len(self.moving_blocks)
+        if node is None or not len(list(node)):
+            if nobj:
+                raise CaseError("The number of mobile objects do not match the predefined motions in XML file.")
+            return
+        movs, evts, refs = [], [], []
+        deg2rad, rad2deg = 0.017453292519943295769, 57.29577951308232087684
+        f32 = lambda v: float(np.float32(v))  # JXml::GetAttributeFloat
+        for obj in node:
+            if obj.tag.startswith("_"):
+                continue
+            if obj.tag not in ("objreal", "obj"):
+                raise CaseError(f"<motion>: unknown element <{obj.tag}>.")
+            if obj.tag == "obj" or obj.find("objreal") is not None or obj.find("obj") is not None:
+                raise CaseError("<motion>: nested or virtual motion objects are not supported by this core.")
+            ref = int(obj.get("ref"))
+            refs.append(ref)
+            for m in obj:
+                t = m.tag
+                if t.startswith("_") or t == "begin":
+                    continue
+                types = {"wait": 1, "mvrect": 2, "mvrectace": 3, "mvrot": 4, "mvrotace": 5, "mvrectsinu": 6,
+                         "mvrotsinu": 7}
+                if t not in types:
+                    raise CaseError(f"<motion>: movement <{t}> is not supported by this core.")
+                units = m.get("anglesunits", "degrees")
+                if units not in ("degrees", "radians"):
+                    raise CaseError("<motion>: invalid anglesunits.")
+                deg = units == "degrees"
+                mv = dict(obj=ref, id=int(m.get("id")), next=int(m.get("next", 0)), type=types[t], prev=0,
+                          duration=f32(m.get("duration")), vec=(0.0,) * 3, vec2=(0.0,) * 3, phase=(0.0,) * 3,
+                          axisp1=(0.0,) * 3, axisp2=(0.0,) * 3, ang=0.0, ang2=0.0, ang3=0.0)
+                if mv["duration"] < 0:
+                    raise CaseError("<motion>: flash movements (negative duration) are not supported by this core.")
+
+                def v3(name):
+                    x = m.find(name)
+                    if x is None:
+                        raise CaseError(f"<motion><{t}>: the item is not found '{name}'.")
+                    return tuple(_attr_double(x, a, name) for a in "xyz")
+
+                def v1(name, attr):
+                    x = m.find(name)
+                    if x is None:
+                        raise CaseError(f"<motion><{t}>: the item is not found '{name}'.")
+                    return _attr_double(x, attr, name)
+
+                if t == "mvrect":
+                    mv["vec"] = v3("vel")
+                elif t == "mvrectace":
+                    mv["vec"] = v3("ace")
+                    mv["prev"] = int(m.find("velini") is None)
+                    mv["vec2"] = v3("velini") if not mv["prev"] else (0.0,) * 3
+                elif t in ("mvrot", "mvrotace", "mvrotsinu"):
+                    mv["axisp1"], mv["axisp2"] = v3("axisp1"), v3("axisp2")
+                    if t == "mvrot":  # MovAddRotation: kept in degrees
+                        mv["ang"] = v1("vel", "ang") * (1.0 if deg else rad2deg)
+                    elif t == "mvrotace":
+                        mv["ang"] = v1("ace", "ang") * (1.0 if deg else rad2deg)
+                        mv["prev"] = int(m.find("velini") is None)
+                        mv["ang2"] = (v1("velini", "ang") * (1.0 if deg else rad2deg)) if not mv["prev"] else 0.0
+                    else:  # MovAddRotSinu: ampl in degrees, phase in radians
+                        mv["ang"] = v1("freq", "v")
+                        mv["ang2"] = v1("ampl", "v") * (1.0 if deg else rad2deg)
+                        mv["prev"] = int(m.find("phase") is None)
+                        mv["ang3"] = (v1("phase", "v") * (deg2rad if deg else 1.0)) if not mv["prev"] else 0.0
+                elif t == "mvrectsinu":  # MovAddRecSinu: phase in radians
+                    mv["vec"], mv["vec2"] = v3("freq"), v3("ampl")
+                    mv["prev"] = int(m.find("phase") is None)
+                    mv["phase"] = (tuple(x * deg2rad for x in v3("phase")) if deg else v3("phase")) \
+                        if not mv["prev"] else (0.0,) * 3
+                movs.append(mv)
+            for b in obj.findall("begin"):
+                evts.append(dict(obj=ref, mov=int(b.get("mov")), start=f32(b.get("start")),
+                                 finish=f32(b.get("finish")) if b.get("finish") is not None else -1.0))
+        if nobj != max(refs, default=-1) + 1:
+            raise CaseError("The number of mobile objects do not match the predefined motions in XML file.")
+        self.motion = dict(nobj=nobj, movs=movs, evts=evts)
 
     def _check_loaded(self, h, prt):
         """JPartsLoad4::CheckConfig (JPartsLoad4.cpp:264-300)."""
         if (h["case_np"], h["case_nfixed"], h["case_nmoving"], h["case_nfloat"], h["case_nfluid"]) != (
-                self.case_np, self.case_nfixed, 0, 0, self.case_nfluid):
+                self.case_np, self.case_nfixed, self.case_nmoving, self.case_nfloat, self.case_nfluid):
             raise CaseError("Data file does not match the configuration of the case.")
         if bool(h["data2d"]) != self.data2d:
             raise CaseError("Data file does not match the dimension of the case.")
@@ -513,6 +654,11 @@ class XmlCase:
             sel = (self.idp >= b["begin"]) & (self.idp < b["begin"] + b["count"])
             c[sel] = b["code"]
         return c
+
+    @property
+    def has_bodies(self) -> bool:
+        """Moving or floating blocks: the core takes the block codes (JSphMk) of the case."""
+        return bool(self.case_nmoving or self.case_nfloat)
 
     @property
     def mass(self) -> float:

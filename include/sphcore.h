@@ -42,6 +42,11 @@
  *                                AddPartData + SaveFilePart (JPartDataBi4.cpp:304-440,
  *                                492-516) over the .bi4 container of JBinaryData
  *                                (JBinaryData.cpp:700-1160,1467-1545): PART and case files
+ *   sph_solver_set_motion ...... JDsMotion::Init + JSph::CalcMotion/JSphCpu::RunMotion
+ *                                (JDsMotion.cpp:94-137, JSph.cpp:2308, JSphCpu.cpp:1692-1789)
+ *   sph_solver_set_floatings ... JSph::LoadCaseConfig floating objects (JSph.cpp:1046-1100) +
+ *                                JSphCpuSingle::RunFloating (JSphCpuSingle.cpp:897-1010)
+ *   sph_solver_floatings ....... FtObjs[] (feeds PartFloat.fbi4, JPartFloatBi4)
  */
 #ifndef SPHCORE_H
 #define SPHCORE_H
@@ -53,7 +58,7 @@
 extern "C" {
 #endif
 
-#define SPH_ABI_VERSION 3
+#define SPH_ABI_VERSION 4
 
 typedef enum {
   SPH_OK = 0,
@@ -311,6 +316,69 @@ int sph_normals_write(const char* path, const char* case_name, double dp, double
 /* Parse any .bi4 container and write it back (format round trip; byte-identical for
  * files written by the reference). */
 int sph_bi4_rewrite(const char* src, const char* dst);
+
+/* ---- moving boundaries and floating bodies -------------------
+ * Particle codes: sph_solver_create takes SphParticlesHost.code when it is not NULL (the
+ * codes of JSphMk::Config, JSphMk.cpp:86-123: moving = SPH_CODE_TYPE_MOVING | moving-block
+ * index, floating = SPH_CODE_TYPE_FLOATING | floating-block index); boundary (fixed and
+ * moving) particles are the first npb, floating particles sit among the fluid ones. */
+
+/* Movements of the JMotion program (JMotion::ReadXml, JMotion.cpp:556-700), in the units
+ * JMotion holds them: lengths m, times s (durations/starts as JXml::GetAttributeFloat
+ * reads them, i.e. float values), rotation speeds/accelerations/amplitudes in degrees,
+ * phases in radians, frequencies in Hz. */
+enum {
+  SPH_MOV_WAIT = 1,      /* <wait>                                                   */
+  SPH_MOV_RECT = 2,      /* <mvrect>      vec = vel                                  */
+  SPH_MOV_RECTACE = 3,   /* <mvrectace>   vec = ace, vec2 = velini (prev: no velini) */
+  SPH_MOV_ROT = 4,       /* <mvrot>       ang = vel, axis                            */
+  SPH_MOV_ROTACE = 5,    /* <mvrotace>    ang = ace, ang2 = velini (prev)            */
+  SPH_MOV_RECTSINU = 6,  /* <mvrectsinu>  vec = freq, vec2 = ampl, phase (prev)      */
+  SPH_MOV_ROTSINU = 7    /* <mvrotsinu>   ang = freq, ang2 = ampl, ang3 = phase (prev), axis */
+};
+typedef struct SphMotionMov {
+  int32_t obj;       /* moving object = objreal ref = moving-block index             */
+  int32_t id;        /* movement id inside the object                               */
+  int32_t next;      /* id of the next movement of the object (0: none)             */
+  int32_t type;      /* SPH_MOV_*                                                   */
+  int32_t prev;      /* velprev / phaseprev: take the value of the previous movement */
+  int32_t pad;
+  double duration;   /* >= 0 (flash movements are not supported)                    */
+  double vec[3], vec2[3], phase[3];
+  double axisp1[3], axisp2[3];
+  double ang, ang2, ang3;
+} SphMotionMov;
+/* <begin mov start finish>: movement `mov` (id) of object `obj` starts at `start`
+ * (finish < 0: no forced finish). */
+typedef struct SphMotionEvent {
+  int32_t obj, mov;
+  double start, finish;
+} SphMotionEvent;
+/* Motion program of the case's moving objects (JDsMotion::Init, JDsMotion.cpp:94-106);
+ * call once after sph_solver_create and before the first step.  Evaluated on the device
+ * every step (no host round trip), applied as JSphCpu::RunMotion (JSphCpu.cpp:1758-1789). */
+int sph_solver_set_motion(SphSolver* s, uint32_t nobj, uint32_t nmov, const SphMotionMov* movs, uint32_t nevt,
+                          const SphMotionEvent* evts);
+
+/* Floating body (JCasePartBlock_Floating, JCaseParts.cpp:248-290 -> StFloatingData,
+ * JSph.cpp:1046-1100), RigidAlgorithm=1 (SPH forces). */
+typedef struct SphFloatingDef {
+  uint32_t idbegin, count;     /* idp range of its particles                        */
+  double massbody, masspart;   /* <massbody>, <masspart> (narrowed to float)        */
+  double center[3];            /* <center>                                          */
+  double inertia[9];           /* <inertia> row major (narrowed to float)           */
+  double linvelini[3], angvelini[3];
+  int32_t translationfree[3], rotationfree[3];
+} SphFloatingDef;
+/* Floating body state (StFloatingData members; PartFloat.fbi4 contents). */
+typedef struct SphFloatingState {
+  double center[3];
+  float fvel[3], fomega[3], angles[3], facelin[3], faceang[3];
+  float pad;
+} SphFloatingState;
+/* Configure the floating bodies (call once, before the first step); ftpause = FtPause. */
+int sph_solver_set_floatings(SphSolver* s, uint32_t nft, const SphFloatingDef* defs, double ftpause);
+int sph_solver_floatings(SphSolver* s, uint32_t cap, SphFloatingState* out, uint32_t* nft);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,87 @@
+"""Generate the wave-flume fixtures (moving boundaries + floating body) by running the
+REFERENCE solver (build container only: needs the binaries of ``make -C oracle``).
+
+tests/golden/bi4/flume_<variant>/
+  CaseFlume.xml / .bi4 [/ _Normals.nbi4]   case written by genflume_ref: fixed walls, a piston
+                                           (mvrectsinu), a flap (wait -> mvrotsinu), a floating
+                                           box (RigidAlgorithm=1) and still water
+  ref.npz                                  reference run -nsteps:N -svsteps:1 -saveposdouble:1:
+                                           PART snapshots (partdump_ref, sorted by idp) at the
+                                           kept steps, the PART times, and the floating-body
+                                           state of every PART (PartFloat.fbi4 via ftdump_ref:
+                                           center, fvel, fomega)
+Usage: python tests/golden/make_flume_case.py
+"""
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = os.path.join(ROOT, "oracle", "_ref")
+sys.path.insert(0, HERE)
+from make_golden import load_dump  # noqa: E402
+
+# variant: (dp, step 1 Verlet / 2 Symplectic, ddt, boundary 1 DBC / 2 mDBC, nsteps, kept steps)
+VARIANTS = {
+    "verlet_ddt2": (0.025, 1, 2, 1, 100, (1, 10, 50, 100)),
+    "symplectic_ddt1_mdbc": (0.025, 2, 1, 2, 60, (1, 10, 60)),
+}
+
+
+def load_ft(fn):
+    b = open(fn, "rb").read()
+    nft, nparts = (int(v) for v in np.frombuffer(b, np.uint32, 4)[1:3])
+    o = 16
+    t, c, v, w = [], [], [], []
+    for _ in range(nparts):
+        t.append(np.frombuffer(b, np.float64, 1, o)[0]); o += 8
+        for _ in range(nft):
+            c.append(np.frombuffer(b, np.float64, 3, o)); o += 24
+            v.append(np.frombuffer(b, np.float32, 3, o)); o += 12
+            w.append(np.frombuffer(b, np.float32, 3, o)); o += 12
+    sh = (nparts, nft, 3)
+    return np.array(t), np.array(c).reshape(sh), np.array(v).reshape(sh), np.array(w).reshape(sh)
+
+
+def make(name, dp, step, ddt, boundary, nsteps, keep):
+    out_dir = os.path.join(HERE, "bi4", "flume_" + name)
+    os.makedirs(out_dir, exist_ok=True)
+    tmp = tempfile.mkdtemp(prefix="flume_")
+    try:
+        subprocess.check_call([os.path.join(REF, "genflume_ref"), repr(dp), tmp, str(step), str(ddt), "1.0",
+                               "CaseFlume", str(boundary)], stdout=subprocess.DEVNULL)
+        files = ["CaseFlume.xml", "CaseFlume.bi4"] + (["CaseFlume_Normals.nbi4"] if boundary == 2 else [])
+        for f in files:
+            shutil.copy(os.path.join(tmp, f), os.path.join(out_dir, f))
+        out = os.path.join(tmp, "out")
+        subprocess.check_call([os.path.join(REF, "DualSPHysics5.2CPU_ref"), os.path.join(tmp, "CaseFlume"), out,
+                               "-nsteps:%d" % nsteps, "-svsteps:1", "-nortimes:1", "-saveposdouble:1", "-sv:binx",
+                               "-svres:0", "-ompthreads:4"], stdout=subprocess.DEVNULL)
+        arrays, times = {}, []
+        for part in range(nsteps + 1):
+            fn = os.path.join(tmp, "p.bin")
+            subprocess.check_call([os.path.join(REF, "partdump_ref"), out, str(part), fn], stdout=subprocess.DEVNULL)
+            t, idp, pos, vel, rho = load_dump(fn)
+            times.append(t)
+            if part in keep:
+                arrays.update({"s%d_idp" % part: idp, "s%d_pos" % part: pos, "s%d_vel" % part: vel,
+                               "s%d_rhop" % part: rho, "s%d_time" % part: np.float64(t)})
+        subprocess.check_call([os.path.join(REF, "ftdump_ref"), out, os.path.join(tmp, "ft.bin")],
+                              stdout=subprocess.DEVNULL)
+        ft, fc, fv, fw = load_ft(os.path.join(tmp, "ft.bin"))
+        arrays.update(times=np.array(times), ft_time=ft, ft_center=fc, ft_fvel=fv, ft_fomega=fw,
+                      meta=np.array([dp, step, ddt, nsteps, boundary], np.float64))
+        np.savez_compressed(os.path.join(out_dir, "ref.npz"), **arrays)
+        print(name, "ok", sorted(os.listdir(out_dir)))
+    finally:
+        shutil.rmtree(tmp)
+
+
+if __name__ == "__main__":
+    for k, v in VARIANTS.items():
+        make(k, *v)

@@ -1,0 +1,214 @@
+"""Moving boundaries and floating bodies.
+
+Reference: JSph::CalcMotion / JMotion::ProcesTimeSimple + JSphCpu::RunMotion (moving
+objects, JSph.cpp:2308, JMotion.cpp:347-366, JMotionObj.cpp:368-580, JSphCpu.cpp:1692-1789)
+and JSphCpuSingle::RunFloating (RigidAlgorithm=1, JSphCpuSingle.cpp:748-1010); floating
+particles in the interaction (JSphCpu.cpp:656-705) and in the updates (JSphCpu.cpp:1352,
+1475, 1577).
+
+Fixtures (written by the REFERENCE solver, tests/golden/make_flume_case.py): a wave flume
+with a piston (mvrectsinu), a flap (wait -> mvrotsinu about the hinge line), a floating
+box and still water; PART snapshots + the floating-body state of every PART
+(PartFloat.fbi4).  CPU tests pin the case loader and the motion semantics (units, the
+wait -> rotation chain) against the moving particles of the reference PARTs with a small
+restatement of the two movements; GPU tests run the HIP path through the C-ABI against
+the reference PARTs and body states.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from golden_io import by_idp, maxdiff
+
+from dualsphysics_multilayer_amd.xmlcase import CaseError, XmlCase
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FIX = os.path.join(HERE, "golden", "bi4")
+VARIANTS = ["verlet_ddt2", "symplectic_ddt1_mdbc"]
+
+
+def _case(variant):
+    return XmlCase(os.path.join(FIX, "flume_" + variant, "CaseFlume"))
+
+
+def _ref(variant):
+    return np.load(os.path.join(FIX, "flume_" + variant, "ref.npz"))
+
+
+def _snap(g, k):
+    return {q: g["s%d_%s" % (k, q)] for q in ("idp", "pos", "vel", "rhop")}
+
+
+def _kept(g):
+    return sorted(int(k[1:].split("_")[0]) for k in g.files if k.startswith("s") and k.endswith("_idp"))
+
+
+# ---- case loader (CPU) ---------------------------------------------------------------------
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_flume_case_blocks_and_codes(variant):
+    x = _case(variant)
+    assert x.has_bodies and x.case_nmoving == 2 * 16 * 11 and x.case_nfloat == 125
+    assert x.npb == x.case_nfixed + x.case_nmoving
+    code = x.code
+    # JSphMk::Config: moving blocks 0,1 and floating block 0 (JSphMk.cpp:108-114)
+    assert set(np.unique(code[: x.npb])) == {0x0, 0x800, 0x801}
+    assert set(np.unique(code[x.npb:])) == {0x1000, 0x1800}
+    assert (x.idp[: x.npb] < x.case_npb).all() and (x.idp[x.npb:] >= x.case_npb).all()
+    f = x.floatings[0]
+    assert f["idbegin"] == x.case_npb and f["count"] == 125
+    assert f["massbody"] == pytest.approx(500.0 * 125 * 0.025 ** 3)
+    m = x.motion
+    assert m["nobj"] == 2 and [v["type"] for v in m["movs"]] == [6, 1, 7]
+    assert m["movs"][1]["duration"] == float(np.float32(0.004))  # GetAttributeFloat
+
+
+def test_unsupported_body_features_refused(tmp_path):
+    src = os.path.join(FIX, "flume_verlet_ddt2")
+    xml = open(os.path.join(src, "CaseFlume.xml")).read()
+    import shutil
+
+    def variant(edit):
+        d = tmp_path / ("c%d" % len(list(tmp_path.iterdir())))
+        d.mkdir()
+        shutil.copy(os.path.join(src, "CaseFlume.bi4"), d / "CaseFlume.bi4")
+        (d / "CaseFlume.xml").write_text(edit(xml))
+        return str(d / "CaseFlume")
+
+    with pytest.raises(CaseError, match="RigidAlgorithm"):
+        XmlCase(variant(lambda s: s.replace('key="RigidAlgorithm" value="1"', 'key="RigidAlgorithm" value="2"')))
+    with pytest.raises(CaseError, match="imposed"):
+        XmlCase(variant(lambda s: s.replace("</floating>", '<linearvel><velvalues time="0" x="1" y="0" z="0"/>'
+                                                          "</linearvel></floating>")))
+    with pytest.raises(CaseError, match="mvcir"):
+        XmlCase(variant(lambda s: s.replace("<wait ", "<mvcir ")))
+    with pytest.raises(CaseError, match="mobile objects"):
+        XmlCase(variant(lambda s: s.replace('<objreal ref="1">', '<objreal ref="3">')))
+
+
+def _rot_y(p, hinge_x, ang_deg):
+    """Rotation about the line from (hinge_x, 0, 0) to (hinge_x, 1, 0) (JMatrix4::MatrixRot:
+    x' = c x - s z, z' = s x + c z)."""
+    a = math.radians(ang_deg)
+    c, s = math.cos(a), math.sin(a)
+    x, z = p[:, 0] - hinge_x, p[:, 2]
+    return np.stack([hinge_x + c * x - s * z, p[:, 1], s * x + c * z], axis=1)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_motion_semantics_match_reference_parts(variant):
+    """The parsed program, restated for the piston (x += A sin(phase) increments) and the
+    flap (rotation by A sin(2 pi f (t - 0.004)) degrees once the wait ends), reproduces the
+    moving particles of the reference PARTs from the reference's own times."""
+    x, g = _case(variant), _ref(variant)
+    times = g["times"]
+    pist = [b for b in x.moving_blocks][0]
+    flap = [b for b in x.moving_blocks][1]
+    mp, mf = x.motion["movs"][0], x.motion["movs"][2]
+    wait = x.motion["movs"][1]["duration"]
+    hinge = mf["axisp1"][0]
+    p0 = by_idp(dict(idp=x.idp, pos=x.pos))
+    for k in _kept(g):
+        ref = _snap(g, k)
+        t = times[k]
+        # piston: the phase accumulates per step; its sum telescopes to A sin(2 pi f t)
+        dx = mp["vec2"][0] * math.sin(mp["vec"][0] * 2 * math.pi * t)
+        sel = (ref["idp"] >= pist["begin"]) & (ref["idp"] < pist["begin"] + pist["count"])
+        exp = p0["pos"][ref["idp"][sel]].copy()
+        exp[:, 0] += dx
+        assert np.abs(ref["pos"][sel] - exp).max() < 1e-12
+        assert np.abs(ref["vel"][sel][:, 1:]).max() == 0
+        # flap
+        ang = mf["ang2"] * math.sin(mf["ang"] * 2 * math.pi * max(0.0, t - wait))
+        sel = (ref["idp"] >= flap["begin"]) & (ref["idp"] < flap["begin"] + flap["count"])
+        exp = _rot_y(p0["pos"][ref["idp"][sel]], hinge, ang)
+        assert np.abs(ref["pos"][sel] - exp).max() < 1e-11, (k, np.abs(ref["pos"][sel] - exp).max())
+
+
+# ---- HIP path (GPU) --------------------------------------------------------------------------
+def _gpu(case):
+    from dualsphysics_multilayer_amd.core import SphGpuSingle
+
+    return SphGpuSingle(case, device=0)
+
+
+def _tol(step):
+    """Per-particle tolerances vs the reference PARTs: 10x the reference's own noise floor
+    (the same solver with and without -ffast-math; the mDBC floor of test_mdbc, which the
+    floating body does not widen at these step counts)."""
+    if step <= 1:
+        return 1.4e-8, 2.2e-5, 1e-2
+    if step <= 20:
+        return 2e-7, 6e-5, 1e-2
+    return 2e-6, 2.1e-4, 2e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_gpu_flume_matches_reference_parts(variant):
+    x, g = _case(variant), _ref(variant)
+    s = _gpu(x)
+    done = 0
+    for k in _kept(g):
+        s.run(k - done)
+        done = k
+        ref = _snap(g, k)
+        got = by_idp(s.particles())
+        assert np.array_equal(got["idp"], ref["idp"]), "excluded-particle set differs"
+        tp, tv, tr = _tol(k)
+        # the dt sequence carries the float noise of the maxima (measured 2e-8 relative)
+        assert abs(s.stats()["time"] - g["times"][k]) <= 1e-6 * g["times"][k]
+        # moving particles: a pure function of the dt sequence (measured <= 2.4e-10 m)
+        mv = (ref["idp"] >= x.case_nfixed) & (ref["idp"] < x.case_npb)
+        assert np.abs(got["pos"][mv] - ref["pos"][mv]).max() <= 2e-9
+        assert np.abs(got["vel"][mv] - ref["vel"][mv]).max() <= 1e-5
+        for q, t in (("pos", tp), ("vel", tv), ("rhop", tr)):
+            assert maxdiff(got, ref, q) <= t, (k, q, maxdiff(got, ref, q))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_gpu_floating_body_matches_reference(variant):
+    """Body state after every step vs PartFloat.fbi4 (center, fvel, fomega).  Measured on
+    MI355X: center <= 2e-8 m, fvel <= 3.4e-6 m/s (|fvel| up to 0.12), fomega <= 3.9e-6
+    rad/s (|fomega| up to 5e-3) over 60-100 steps."""
+    x, g = _case(variant), _ref(variant)
+    s = _gpu(x)
+    n = int(g["meta"][3])
+    worst = np.zeros(3)
+    for k in range(1, n + 1):
+        s.run(1)
+        b = s.floatings()[0]
+        dc = np.abs(b["center"] - g["ft_center"][k, 0]).max()
+        dv = np.abs(b["fvel"] - g["ft_fvel"][k, 0]).max()
+        dw = np.abs(b["fomega"] - g["ft_fomega"][k, 0]).max()
+        worst = np.maximum(worst, [dc, dv, dw])
+    vscale = np.abs(g["ft_fvel"]).max()
+    wscale = np.abs(g["ft_fomega"]).max()
+    assert worst[0] <= 1e-7, worst
+    assert worst[1] <= 2e-3 * vscale + 1e-6, (worst, vscale)
+    assert worst[2] <= 2e-2 * wscale + 1e-4, (worst, wscale)
+
+
+@pytest.mark.gpu
+def test_gpu_bodies_deterministic():
+    x = _case("verlet_ddt2")
+    outs = []
+    for _ in range(2):
+        s = _gpu(x)
+        s.run(15)
+        outs.append((by_idp(s.particles()), s.floatings()[0]))
+    for q in ("pos", "vel", "rhop"):
+        assert np.array_equal(outs[0][0][q], outs[1][0][q])
+    assert np.array_equal(outs[0][1]["center"], outs[1][1]["center"])
+
+
+@pytest.mark.gpu
+def test_gpu_bodies_slab_refused():
+    from dualsphysics_multilayer_amd.core import SphError, SphSlabGroup, slab_partition
+
+    x = _case("verlet_ddt2")
+    with pytest.raises(SphError):
+        g = SphSlabGroup(x, slab_partition(x, 2))
+        g.Run(1)

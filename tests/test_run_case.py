@@ -108,7 +108,10 @@ def test_simulationdomain_with_legacy_keys_is_refused(tmp_path):
     (lambda x: x.replace('<data2d value="false"/>', '<data2d value="true"/>'), "2-D"),
     (lambda x: x.replace("</parameters>", "</parameters>\n<special><wavepaddles/></special>"), "special"),
     (lambda x: x.replace('<fixed mkbound="0" mk="10"', '<moving mkbound="0" mk="10"').replace(
-        'count="1182"/>\n<fluid', 'count="1182"/>\n<fluid'), "Moving|unknown"),
+        'count="1182"/>\n<fluid', 'count="1182"/>\n<fluid'), "mobile objects"),
+    (lambda x: x.replace('<fixed mkbound="0" mk="10"', '<moving mkbound="0" mk="10"').replace(
+        "</constants>", '</constants>\n<motion><objreal ref="0"><begin mov="1" start="0"/>'
+        '<mvfile id="1" duration="1"/></objreal></motion>'), "mvfile"),
     (lambda x: x.replace('key="DensityDT" value="2"', 'key="DensityDT" value="7"'), "not valid"),
     (lambda x: x.replace('<parameter key="TimeMax" value="1.5"/>', ''), "TimeMax"),
     (lambda x: x.replace('key="RhopOutMin" value="700"', 'key="RhopOutMin" value="1001"'), "outside"),
