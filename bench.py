@@ -4,7 +4,7 @@ A "step" is one JSphGpuSingle::ComputeStep + RunCellDivide over the whole partic
 set (interaction, dt, update, cell sort).  Inputs are resident in HBM when the
 timed region starts.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg2|cfg3]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg2|cfg3|cfg4]
                     [--dp DP] [--no-cpu-baseline]
 
 Workloads:
@@ -15,6 +15,9 @@ Workloads:
         maxima inside libsphcore); value = all particles x steps / max rank time.
   cfg3: BASELINE cfg3, 3D dam break of ~10M particles (dp 0.00205), Symplectic + DDT
         (Molteni, delta-SPH) 0.1, slab-split over N ranks (strong scaling).
+  cfg4: BASELINE cfg4, wave flume of ~4.0M particles (dp 0.00265): piston (mvrectsinu) +
+        flap (mvrotsinu) moving boundaries, a floating box (RigidAlgorithm=1), mDBC,
+        Verlet + DDT2; one GPU (moving/floating bodies do not run on the slabs yet).
 torch.distributed (gloo, host only) bootstraps the RCCL id, barriers and reduces the
 timings; the data path never goes through torch.  Prints ONE JSON line on rank 0.
 """
@@ -51,27 +54,31 @@ def dist_env():
 
 
 def reference_cpu_baseline(dp: float, nsteps: int, threads: int, step: int = 1, ddt: int = 2,
-                           boundary: int = 1) -> dict | None:
+                           boundary: int = 1, flume: bool = False) -> dict | None:
     """Times the REFERENCE CPU solver (oracle/_ref, built from the reference sources)
-    on the same dam break; Steps/s is the solver's own 'Steps per second' (step loop only)."""
+    on the same dam break (or wave flume); Steps/s is the solver's own 'Steps per second'
+    (step loop only)."""
     ref = os.path.join(ROOT, "oracle", "_ref")
-    exe, gen = os.path.join(ref, "DualSPHysics5.2CPU_ref"), os.path.join(ref, "gencase_ref")
+    exe = os.path.join(ref, "DualSPHysics5.2CPU_ref")
+    gen = os.path.join(ref, "genflume_ref" if flume else "gencase_ref")
+    name = "CaseFlume" if flume else "CaseDambreak"
     if not (os.path.exists(exe) and os.path.exists(gen)):
         return None
     tmp = tempfile.mkdtemp(prefix="sphref_")
     try:
-        out = subprocess.run([gen, repr(dp), tmp, str(step), str(ddt), "1.5", "CaseDambreak", str(boundary)],
+        out = subprocess.run([gen, repr(dp), tmp, str(step), str(ddt), "1.5", name, str(boundary)],
                              capture_output=True, text=True, check=True).stdout
         np_ = int(re.search(r"np=(\d+)", out).group(1))
-        subprocess.run([exe, os.path.join(tmp, "CaseDambreak"), os.path.join(tmp, "out"), "-nsteps:%d" % nsteps,
+        subprocess.run([exe, os.path.join(tmp, name), os.path.join(tmp, "out"), "-nsteps:%d" % nsteps,
                         "-sv:none", "-svres:0", "-ompthreads:%d" % threads], capture_output=True, text=True,
                        check=True, timeout=600)
         log = open(os.path.join(tmp, "out", "Run.out")).read()
         sps = float(re.search(r"Steps per second\.*:\s*([0-9.eE+-]+)", log).group(1))
         return {"value": sps * np_, "unit": "particle-steps/s", "cores": threads, "kind": "reference",
                 "sample": "reference DualSPHysics5.2 CPU (built from /root/reference sources, -O3 -fopenmp "
-                          "-ffast-math), %d-particle dam break (%s), %d %s steps, -ompthreads:%d, "
-                          "'Steps per second' of Run.out" % (np_, "mDBC" if boundary == 2 else "DBC", nsteps,
+                          "-ffast-math), %d-particle %s (%s), %d %s steps, -ompthreads:%d, "
+                          "'Steps per second' of Run.out" % (np_, "wave flume" if flume else "dam break",
+                                                             "mDBC" if boundary == 2 else "DBC", nsteps,
                                                              "Verlet" if step == 1 else "Symplectic", threads)}
     except Exception as e:  # noqa: BLE001
         sys.stderr.write("reference CPU baseline failed: %r\n" % (e,))
@@ -117,6 +124,7 @@ def profiled_traffic(kernel_prefix: str, np_: int, workload: str):
 
 CFG2_DP, CFG2_NP = 0.0045, 1025964
 CFG3_DP = 0.00205  # 9,969,118 particles (BASELINE cfg3: ~10M)
+CFG4_DP = 0.00265  # 4,007,978 particles (BASELINE cfg4: wave flume ~4M)
 
 
 def weak_dp(target_np: int) -> float:
@@ -138,9 +146,9 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=("cfg2", "cfg3"), default="cfg2")
+    ap.add_argument("--workload", choices=("cfg2", "cfg3", "cfg4"), default="cfg2")
     ap.add_argument("--dp", type=float, default=None, help="override the particle spacing")
-    ap.add_argument("--boundary", choices=("dbc", "mdbc"), default="dbc",
+    ap.add_argument("--boundary", choices=("dbc", "mdbc"), default=None,
                     help="boundary conditions (mdbc: modified DBC, Vel0, normals to the wall limit)")
     ap.add_argument("--bound-weight", type=float, default=0.3, help="slab balance weight of a bound particle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -148,6 +156,8 @@ def main() -> None:
     ap.add_argument("--force-slab", action="store_true",
                     help="run the N>1 code path (gloo bootstrap + RCCL slab) even with one rank")
     args = ap.parse_args()
+    if args.boundary is None:
+        args.boundary = "mdbc" if args.workload == "cfg4" else "dbc"
 
     rank, world, local = dist_env()
     if args.gpus != world and world > 1:
@@ -163,15 +173,20 @@ def main() -> None:
         os.environ.setdefault("MASTER_PORT", "29517")
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    from dualsphysics_multilayer_amd.case import DamBreakCase
+    from dualsphysics_multilayer_amd.case import DamBreakCase, WaveFlumeCase
     from dualsphysics_multilayer_amd.core import SphGpuSingle, SphGpuSlab, comm_unique_id, slab_partition
 
     if args.workload == "cfg2":
         dp = args.dp or (CFG2_DP if world == 1 else weak_dp(world * CFG2_NP))
         case = DamBreakCase(dp, tboundary=2 if args.boundary == "mdbc" else 1)
-    else:
+    elif args.workload == "cfg3":
         dp = args.dp or CFG3_DP
         case = DamBreakCase(dp, step_algorithm=2, tdensity=1, tboundary=2 if args.boundary == "mdbc" else 1)
+    else:
+        if world > 1:
+            raise SystemExit("cfg4 (moving/floating bodies) runs on one GPU")
+        dp = args.dp or CFG4_DP
+        case = WaveFlumeCase(dp, tboundary=2 if args.boundary == "mdbc" else 1)
     bounds = None
     fallback = None
     s = None
@@ -257,17 +272,23 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak" if args.workload == "cfg2" else "strong",
+            "scaling": "strong" if args.workload == "cfg3" else "weak",
             "vs_baseline": None,
             "dtype": "f32 (f64 positions/time integration)",
-            "data": "synthetic: generated 3D dam-break lattice (SURVEY.md §8(c) recipe)",
+            "data": ("synthetic: generated wave-flume lattice (case.py WaveFlumeCase = oracle/tools/genflume_ref)"
+                     if args.workload == "cfg4" else
+                     "synthetic: generated 3D dam-break lattice (SURVEY.md §8(c) recipe)"),
             "config": {
                 "workload": (("BASELINE cfg2: 3D dam break, %d particles (dp=%g), Verlet, Wendland, artificial "
                               "viscosity 0.1, DDT2 0.1, %s, CFL 0.2, CellMode full" % (case.np, dp, args.boundary.upper()))
                              if args.workload == "cfg2" else
                              ("BASELINE cfg3: 3D dam break, %d particles (dp=%g), Symplectic, Wendland, artificial "
                               "viscosity 0.1, DDT (Molteni delta-SPH) 0.1, %s, CFL 0.2, CellMode full"
-                              % (case.np, dp, args.boundary.upper()))),
+                              % (case.np, dp, args.boundary.upper())) if args.workload == "cfg3" else
+                             ("BASELINE cfg4: wave flume, %d particles (dp=%g): piston mvrectsinu + flap mvrotsinu "
+                              "moving boundaries, floating box (RigidAlgorithm=1, %d particles), %s, Verlet, "
+                              "Wendland, artificial viscosity 0.1, DDT2 0.1, CFL 0.2"
+                              % (case.np, dp, case.case_nfloat, args.boundary.upper()))),
                 "np": case.np,
                 "npb": case.npb,
                 "parallelism": (("slab-x%d (RCCL halo + migration, max-allreduce dt)" % world) if bounds is not None
@@ -276,7 +297,9 @@ def main() -> None:
                 "owned_np_per_rank": per_rank_np,
             },
             "roofline": {
-                "kernel": "k_fluid_tiled<tdensity=%d> (Interaction_Forces)" % case.tdensity,
+                "kernel": (("k_interaction<tdensity=%d, floating> (Interaction_Forces, one lane per particle)"
+                            if getattr(case, "floatings", None) else "k_fluid_tiled<tdensity=%d> (Interaction_Forces)")
+                           % case.tdensity),
                 "bound": "mfma",
                 "bound_note": "FP32-VALU-bound pairwise kernel (no MFMA: irregular pairs); gfx950's FP32 vector "
                               "peak equals its FP32 MFMA peak, 157.3 TFLOP/s",
@@ -309,7 +332,7 @@ def main() -> None:
         if not args.no_cpu_baseline and world == 1:
             threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), 64)
             cb = reference_cpu_baseline(dp, args.cpu_steps, threads, case.step_algorithm, case.tdensity,
-                                        case.tboundary)
+                                        case.tboundary, flume=args.workload == "cfg4")
             if cb is None:
                 cb = port_cpu_baseline(case, args.cpu_steps, threads)
             cb["gpu_over_cpu"] = value / cb["value"]

@@ -242,3 +242,177 @@ def dambreak_np(dp: float) -> int:
     total = (nx + 1) * (ny + 1) * (nz + 1)
     inner = (nx - 1) * (ny - 1) * nz  # k>=1, i in [1,nx-1], j in [1,ny-1]
     return (total - inner) + mx * (my - 1) * mz
+
+
+@dataclass
+class WaveFlumeCase:
+    """Wave flume with a piston, a flap and a floating box (BASELINE cfg4):
+    the lattice, blocks, motion program and floating body that oracle/tools/genflume_ref
+    writes for the reference (tests/test_bodies.py checks the two agree bit for bit).
+
+    Tank L x W x H (walls: bottom, y=0, y=W), still water of depth D from the piston
+    (x = 2dp, mvrectsinu along x) to the flap (x = L, a 0.004 s wait then mvrotsinu about
+    the hinge line (L, y, 0)); a box of rhopbody 500 floats at mid-length.  Block order and
+    codes as JSphMk::Config: fixed, moving (piston, flap), floating, fluid."""
+
+    dp: float
+    step_algorithm: int = STEP_VERLET
+    tdensity: int = DDT_DDT2
+    tboundary: int = 1
+    length: float = 1.2
+    width: float = 0.3
+    height: float = 0.4
+    depth: float = 0.2
+    ddtvalue: float = 0.1
+    visco: float = 0.1
+    viscoboundfactor: float = 1.0
+    cflnumber: float = 0.2
+    verlet_steps: int = 40
+    coefdtmin: float = 0.05
+    rhopoutmin: float = 700.0
+    rhopoutmax: float = 1300.0
+    cellmode: int = CELLMODE_FULL
+    celldomfixed: bool = False
+    gravity: tuple = (0.0, 0.0, -9.81)
+    rhop0: float = 1000.0
+    gamma: float = 7.0
+    coefsound: float = 20.0
+    coefh: float = 1.0
+    rhopbody: float = 500.0
+    slipmode: int = 1
+    mdbc_threshold: float = 0.0
+    ftpause: float = 0.0
+    time0: float = 0.0
+    symdtpre0: float = 0.0
+    has_bodies: bool = True
+
+    def __post_init__(self) -> None:
+        dp = self.dp
+        nx, ny, nz = _cround(self.length / dp), _cround(self.width / dp), _cround(self.height / dp)
+        kd, ip = _cround(self.depth / dp), 2
+        nbh = max(2, _cround(0.03 / dp))
+        bic, bjc, bkc = _cround(0.55 * self.length / dp), ny // 2, kd - 1
+        hd = dp * 0.5
+        blocks, nor = [], []
+        # fixed: bottom and side walls, loop order k, j, i
+        k, j, i = np.meshgrid(np.arange(nz + 1), np.arange(ny + 1), np.arange(nx + 1), indexing="ij")
+        wall = (k == 0) | (j == 0) | (j == ny)
+        fi, fj, fk = i[wall], j[wall], k[wall]
+        blocks.append((fi, fj, fk))
+        nor.append(np.stack([np.zeros(fi.size), np.where(fj == 0, hd, np.where(fj == ny, -hd, 0.0)),
+                             np.where(fk == 0, hd, 0.0)], axis=1))
+        # piston (x = ip dp) and flap (x = nx dp): k = 1..nz, j = 1..ny-1
+        pk, pj = np.meshgrid(np.arange(1, nz + 1), np.arange(1, ny), indexing="ij")
+        pk, pj = pk.ravel(), pj.ravel()
+        for xi, sgn in ((ip, 1.0), (nx, -1.0)):
+            blocks.append((np.full(pk.size, xi), pj, pk))
+            nor.append(np.stack([np.full(pk.size, sgn * hd), np.zeros(pk.size), np.zeros(pk.size)], axis=1))
+        # floating box
+        bk, bj, bi = np.meshgrid(np.arange(bkc - nbh, bkc + nbh + 1), np.arange(bjc - nbh, bjc + nbh + 1),
+                                 np.arange(bic - nbh, bic + nbh + 1), indexing="ij")
+        blocks.append((bi.ravel(), bj.ravel(), bk.ravel()))
+        nor.append(np.zeros((bi.size, 3)))
+        # fluid minus the box
+        wk, wj, wi = np.meshgrid(np.arange(1, kd + 1), np.arange(1, ny), np.arange(ip + 1, nx), indexing="ij")
+        inbox = (np.abs(wi - bic) <= nbh) & (np.abs(wj - bjc) <= nbh) & (np.abs(wk - bkc) <= nbh)
+        blocks.append((wi[~inbox], wj[~inbox], wk[~inbox]))
+        counts = [b[0].size for b in blocks]
+        ii = np.concatenate([b[0] for b in blocks]).astype(np.float64)
+        jj = np.concatenate([b[1] for b in blocks]).astype(np.float64)
+        kk = np.concatenate([b[2] for b in blocks]).astype(np.float64)
+        self.pos = np.stack([ii * dp, jj * dp, kk * dp], axis=1)
+        self.np = int(self.pos.shape[0])
+        self.case_nfixed, npist, nflap, self.case_nfloat = counts[0], counts[1], counts[2], counts[3]
+        self.case_nmoving = npist + nflap
+        self.npb = self.case_npb = self.case_nfixed + self.case_nmoving
+        self.case_nbound = self.case_npb + self.case_nfloat
+        self.idp = np.arange(self.np, dtype=np.uint32)
+        self.vel = np.zeros((self.np, 3), dtype=np.float32)
+        code = np.empty(self.np, np.uint16)
+        edges = np.cumsum([0] + counts)
+        for c, v in zip(range(5), (CODE_TYPE_FIXED, 0x800, 0x801, 0x1000, CODE_TYPE_FLUID)):
+            code[edges[c]:edges[c + 1]] = v
+        self._code = code
+        self._normals = np.concatenate(nor)
+        g, rho0, gamma = -self.gravity[2], self.rhop0, self.gamma
+        hswl = kd * dp
+        cs0 = self.coefsound * math.sqrt(g * hswl)
+        b = cs0 * cs0 * rho0 / gamma
+        self._h, self._b, self._mass = self.coefh * math.sqrt(3.0 * dp * dp), b, rho0 * dp * dp * dp
+        rhop = np.full(self.np, np.float32(rho0), dtype=np.float32)
+        z = self.pos[self.case_nbound:, 2]
+        rhop[self.case_nbound:] = (rho0 * np.power(1.0 + rho0 * g * (hswl - z) / b, 1.0 / gamma)).astype(np.float32)
+        self.rhop = rhop
+        # floating body: GenCase-style centre and diagonal inertia, summed in particle order
+        fp = self.pos[self.case_npb:self.case_nbound]
+        cen = [0.0, 0.0, 0.0]
+        for p in fp:
+            cen = [cen[0] + p[0], cen[1] + p[1], cen[2] + p[2]]
+        cen = [c / len(fp) for c in cen]
+        massp = self.rhopbody * dp * dp * dp
+        ixx = iyy = izz = 0.0
+        for p in fp:
+            rx, ry, rz = p[0] - cen[0], p[1] - cen[1], p[2] - cen[2]
+            ixx += massp * (ry * ry + rz * rz)
+            iyy += massp * (rx * rx + rz * rz)
+            izz += massp * (rx * rx + ry * ry)
+        self.floatings = [dict(idbegin=self.case_npb, count=self.case_nfloat, massbody=massp * len(fp),
+                               masspart=massp, center=tuple(cen), inertia=(ixx, 0.0, 0.0, 0.0, iyy, 0.0, 0.0, 0.0, izz),
+                               translationfree=(1, 1, 1), rotationfree=(1, 1, 1), linvelini=(0.0,) * 3,
+                               angvelini=(0.0,) * 3, mkbound=3)]
+        f32 = lambda v: float(np.float32(v))  # noqa: E731  (JXml::GetAttributeFloat)
+        hinge = float("%.10g" % (nx * dp))
+        zero3 = (0.0, 0.0, 0.0)
+        mov = lambda **kw: dict(dict(obj=0, id=1, next=0, type=1, prev=0, duration=f32(100), vec=zero3,  # noqa: E731
+                                     vec2=zero3, phase=zero3, axisp1=zero3, axisp2=zero3, ang=0.0, ang2=0.0,
+                                     ang3=0.0), **kw)
+        self.motion = dict(nobj=2, movs=[
+            mov(obj=0, type=6, vec=(1.5, 0.0, 0.0), vec2=(0.02, 0.0, 0.0)),
+            mov(obj=1, id=1, next=2, type=1, duration=f32(0.004)),
+            mov(obj=1, id=2, type=7, axisp1=(hinge, 0.0, 0.0), axisp2=(hinge, 1.0, 0.0), ang=2.0, ang2=3.0),
+        ], evts=[dict(obj=0, mov=1, start=0.0, finish=-1.0), dict(obj=1, mov=1, start=0.0, finish=-1.0)])
+
+    @property
+    def code(self) -> np.ndarray:
+        return self._code
+
+    @property
+    def nf(self) -> int:
+        return self.np - self.npb
+
+    @property
+    def h(self) -> float:
+        return _xml_e10(self._h)
+
+    @property
+    def cteb(self) -> float:
+        return _xml_e10(self._b)
+
+    @property
+    def mass(self) -> float:
+        return _xml_e10(self._mass)
+
+    def normals_double(self) -> np.ndarray:
+        """<case>_Normals.nbi4 contents (double3[CaseNbound]; zero for the floating box)."""
+        return self._normals[: self.case_nbound]
+
+    @property
+    def boundnormal(self) -> np.ndarray | None:
+        if self.tboundary != 2:
+            return None
+        out = np.zeros((self.np, 3), np.float32)
+        out[: self.case_nbound] = self._normals.astype(np.float32)
+        return out
+
+    def map_limits(self) -> tuple[np.ndarray, np.ndarray]:
+        """posmin x "default - 10%", posmax x "default + 10%", z "default + 50%"
+        (JSph::ResizeMapLimits)."""
+        border = float(np.float32(self.h)) * BORDER_MAP
+        rmin = self.pos.min(axis=0) - border
+        rmax = self.pos.max(axis=0) + border
+        dif = rmax - rmin
+        return rmin - dif * np.array([0.1, 0.0, 0.0]), rmax + dif * np.array([0.1, 0.0, 0.5])
+
+    def case_def(self) -> dict:
+        d = DamBreakCase.case_def(self)
+        return d

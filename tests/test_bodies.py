@@ -212,3 +212,21 @@ def test_gpu_bodies_slab_refused():
     with pytest.raises(SphError):
         g = SphSlabGroup(x, slab_partition(x, 2))
         g.Run(1)
+
+
+@pytest.mark.parametrize("variant,kw", [("verlet_ddt2", dict()),
+                                        ("symplectic_ddt1_mdbc", dict(step_algorithm=2, tdensity=1, tboundary=2))])
+def test_product_flume_generator_is_the_reference_case(variant, kw):
+    """case.py WaveFlumeCase (the bench's cfg4 generator) == the case genflume_ref wrote
+    for the reference, bit for bit: particles, codes, normals, constants, motion program
+    and floating body."""
+    from dualsphysics_multilayer_amd.case import WaveFlumeCase
+
+    w, x = WaveFlumeCase(0.025, **kw), _case(variant)
+    assert w.case_def() == x.case_def()
+    for q in ("idp", "pos", "vel", "rhop", "code"):
+        assert np.array_equal(getattr(w, q), getattr(x, q)), q
+    assert w.motion == x.motion
+    assert w.floatings == x.floatings
+    if kw.get("tboundary") == 2:
+        assert np.array_equal(w.boundnormal, x.boundnormal)
