@@ -50,6 +50,13 @@ constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
 // 0.806 ms vs 0.838 at 416 (a mirrored row pair fits one segment for 94% of the units
 // instead of 81%); 0.936 at 580 (7 blocks/CU), 1.02 at 672 (6 blocks/CU).
 constexpr int TCAP = SPH_TCAP;
+// With floating bodies a record is 48 B (the third part a float4): 416 records keep the
+// block at <= 20 KB of LDS, i.e. the same 8 blocks (4 waves/SIMD) per CU.
+#ifndef SPH_TCAP_FT
+#define SPH_TCAP_FT 416
+#endif
+template <bool FT> struct TcapT { static constexpr int v = TCAP; };
+template <> struct TcapT<true> { static constexpr int v = SPH_TCAP_FT; };
 constexpr int TMAXCELLS = 4;   // max x-cells per item
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
@@ -190,7 +197,19 @@ void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, Di
 // ------------------------------------------------------------------------------------
 struct TAcc {
   float ax, ay, az, ar, delta, visc;
+  bool dstop;  // FT: the DDT of p1 is off (floating p1, or a light floating p2 under DDT1)
 };
+
+// Third record of a staged p2: float2 {press/rho, 1/rho}, or with floating bodies (FT)
+// float4 {r press/rho, r/rho, r, kind} with r = m2/MassFluid and kind 0 fluid/bound,
+// 1 heavy floating, 2 light floating (massp <= 1.2 MassFluid, DELTA_HEAVYFLOATING,
+// JSphCpu.cpp:697-703).
+template <bool FT> struct CRecT { typedef float2 type; };
+template <> struct CRecT<true> { typedef float4 type; };
+__device__ __forceinline__ float crec_r(const float2&) { return 1.f; }
+__device__ __forceinline__ float crec_r(const float4& c) { return c.z; }
+__device__ __forceinline__ float crec_kind(const float2&) { return 0.f; }
+__device__ __forceinline__ float crec_kind(const float4& c) { return c.w; }
 
 struct P1 {
   float x, y, z;        // x relative to the item's x origin, y/z cell-relative
@@ -229,9 +248,9 @@ struct PassK {
 //   DDT2: rho0*(1+x)^(1/gamma) - rho0, x = ddtgz*drz, as the binomial series in drz
 //         (|x| <= 2h*ddtgz ~ 1e-3, 5th term < 1e-9 relative; decided per case on the host),
 //         which also avoids the float cancellation of the reference's rho0*powf(rh,1/gamma)-rho0.
-template <int TDENSITY, int MODE>
+template <int TDENSITY, int MODE, bool FT = false, typename CR = float2>
 __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float drx, float dry, float drz, float rr2,
-                                          bool ok, const float4& B, const float2& C, const PassK& Q, TAcc& a) {
+                                          bool ok, const float4& B, const CR& C, const PassK& Q, TAcc& a) {
   const float rad = fsqrt_(rr2);
   const float wq = fmaf(K.mhalfovh, rad, 1.f);
   const float w3 = ok ? wq * wq * wq : 0.f;
@@ -252,7 +271,8 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
   a.ar = fmaf(wc, dot, a.ar);
   if (MODE == 2) return;
   const float S = fmaf(C.y, p.press, C.x);  // (p1+p2)/rho2
-  const float pv = (dot < 0.f) ? Q.cvp * dot * rr : 0.f;
+  float pv = (dot < 0.f) ? Q.cvp * dot * rr : 0.f;
+  if (FT) pv *= crec_r(C);  // viscosity with the p2 mass
   const float c = w3 * (S + pv);
   a.ax = fmaf(c, drx, a.ax);
   a.ay = fmaf(c, dry, a.ay);
@@ -268,20 +288,22 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
   }
   if (TDENSITY == 1) {
     const float t = w3 * rr2 * inv_re;
-    a.delta = fmaf(t, fmaf(p.vr.w, C.y, -1.f), a.delta);
+    a.delta = fmaf(t, fmaf(p.vr.w, C.y, FT ? -crec_r(C) : -1.f), a.delta);
+    if (FT && ok && crec_kind(C) == 2.f) a.dstop = true;  // light floating p2
   } else if (TDENSITY == 2 || TDENSITY == 3) {
     float drhop;
     if (K.ddtseries)  // kernel-uniform (scalar) branch
       drhop = drz * fmaf(drz, fmaf(drz, fmaf(drz, K.ddte4, K.ddte3), K.ddte2), K.ddte1);
     else
       drhop = K.rhopzero * fexp2(K.ovgamma * flog2(1.f + K.ddtgz * drz)) - K.rhopzero;
-    const float t = wc * rr2 * inv_re;
+    float t = wc * rr2 * inv_re;
+    if (FT && crec_kind(C) != 0.f) t = 0.f;  // no Fourtakas term with a floating p2 (JSphCpu.cpp:743)
     a.delta = fmaf(t, B.w - (p.vr.w + drhop), a.delta);
   }
 }
 
 // The per-pass factors of the sums (PassK) applied once per particle.
-template <int TDENSITY, int MODE>
+template <int TDENSITY, int MODE, bool FT = false>
 __device__ __forceinline__ TAcc finish(const KConst& K, TAcc a, const P1& p, const PassK& Q) {
   a.ar *= Q.ar1;
   if (MODE != 2) {
@@ -294,6 +316,7 @@ __device__ __forceinline__ TAcc finish(const KConst& K, TAcc a, const P1& p, con
     if (TDENSITY == 1) a.delta *= Q.kd;
     else if (TDENSITY == 2 || TDENSITY == 3) a.delta *= -Q.kd;
   }
+  if (FT && TDENSITY && a.dstop) a.delta = FLT_MAX;
   return a;
 }
 
@@ -335,10 +358,10 @@ __device__ __forceinline__ void test128(const float4* __restrict__ sA, int s0, i
 // dry the next word shifts in.  Value selects only (a word picked by reference puts the
 // masks in scratch), no divergent branch in the loop (the second pop of an iteration is
 // unconditional; an empty pop's pair is masked off).
-template <int TDENSITY, int MODE>
+template <int TDENSITY, int MODE, bool FT = false>
 __device__ __forceinline__ void tile_unit(const KConst& K, const P1& p, float thr, int wa0, int wa1, int wb0, int wb1,
                                           const float4* __restrict__ sA, const float4* __restrict__ sB,
-                                          const float2* __restrict__ sC, const PassK& Q, TAcc& a) {
+                                          const typename CRecT<FT>::type* __restrict__ sC, const PassK& Q, TAcc& a) {
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
 #if SPH_ABLATE == 2
   a.visc += float(wa1 - wa0 + wb1 - wb0);
@@ -397,15 +420,15 @@ __device__ __forceinline__ void tile_unit(const KConst& K, const P1& p, float th
       const int j2 = two ? j2p : j1;
       const float4 A1 = sA[j1], A2 = sA[j2];
       const float4 B1 = sB[j1], B2 = sB[j2];
-      const float2 C1 = sC[j1], C2 = sC[j2];
+      const typename CRecT<FT>::type C1 = sC[j1], C2 = sC[j2];
       const float drx1 = p.x - A1.x, dry1 = p.y - A1.y, drz1 = p.z - A1.z;
       const float drx2 = p.x - A2.x, dry2 = p.y - A2.y, drz2 = p.z - A2.z;
       const float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
       const float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
       const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
       const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
-      pair_body<TDENSITY, MODE>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, Q, a);
-      pair_body<TDENSITY, MODE>(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, Q, a);
+      pair_body<TDENSITY, MODE, FT>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, Q, a);
+      pair_body<TDENSITY, MODE, FT>(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, Q, a);
     }
   }
 }
@@ -413,10 +436,32 @@ __device__ __forceinline__ void tile_unit(const KConst& K, const P1& p, float th
 // Stage the records [rs, re) of the row at (dy, dz) from the item's row into sA/sB/sC at
 // dst: positions relative to the item (x to its x origin xo, y/z to its cell row), |A|^2,
 // velrhop, press/rho, 1/rho.
+struct FtRec {
+  const typecode* code;
+  const float* massp;  // particle mass per floating body
+};
+__device__ __forceinline__ void put_c(float2* sC, unsigned i, float pr, float ir, const KConst&, const FtRec&,
+                                      unsigned) {
+  sC[i] = make_float2(pr * ir, ir);
+}
+__device__ __forceinline__ void put_c(float4* sC, unsigned i, float pr, float ir, const KConst& K, const FtRec& ft,
+                                      unsigned p2) {
+  const typecode c = ft.code[p2];
+  float r = 1.f, kind = 0.f;
+  if (CodeType(c) == CODE_TYPE_FLOATING) {
+    const float m = ft.massp[c & CODE_MASKVALUE];
+    r = m / K.massfluid;
+    kind = (m <= K.massfluid * 1.2f) ? 2.f : 1.f;
+  }
+  const float rir = r * ir;
+  sC[i] = make_float4(pr * rir, rir, r, kind);
+}
+template <typename CR>
 __device__ __forceinline__ void stage_row(const KConst& K, unsigned rs, unsigned re, unsigned dst, int xo, int dy,
                                           int dz, const float4* __restrict__ poscell,
                                           const float4* __restrict__ velrhop, const float* __restrict__ press,
-                                          float4* __restrict__ sA, float4* __restrict__ sB, float2* __restrict__ sC) {
+                                          float4* __restrict__ sA, float4* __restrict__ sB, CR* __restrict__ sC,
+                                          const FtRec& ft) {
   const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
   for (unsigned i = threadIdx.x; i < re - rs; i += TB) {
     const float4 pc = poscell[rs + i];
@@ -427,7 +472,7 @@ __device__ __forceinline__ void stage_row(const KConst& K, unsigned rs, unsigned
     const float4 vr = velrhop[rs + i];
     sB[dst + i] = vr;
     const float ir = frcp(vr.w);
-    sC[dst + i] = make_float2(press[rs + i] * ir, ir);
+    put_c(sC, dst + i, press[rs + i], ir, K, ft, rs + i);
   }
 }
 
@@ -487,13 +532,15 @@ __device__ __forceinline__ PassK pass_k(const KConst& K, float cvisc, float m2, 
 // kind: MODE 0/2 the fluid rows (fluid / bound p1), MODE 1 the bound rows (fluid p1).
 // Drain units: point-mirrored row pairs, then the item's own row; a pair of rows is
 // staged as one segment [row a][row b] when it fits TCAP, else row by row in segments.
-template <int TDENSITY, int MODE>
+template <int TDENSITY, int MODE, bool FT = false>
 __device__ __forceinline__ TAcc run_pass(const KConst& K, const DivGrid& g, const RowCtx& rc, const P1& p, float thr,
                                          const PassK Q, const unsigned* __restrict__ bc,
                                          const float4* __restrict__ poscell, const float4* __restrict__ velrhop,
                                          const float* __restrict__ press, float4* __restrict__ sA,
-                                         float4* __restrict__ sB, float2* __restrict__ sC) {
+                                         float4* __restrict__ sB, typename CRecT<FT>::type* __restrict__ sC,
+                                         const FtRec& ft, bool dstop0 = false) {
   TAcc acc = {};
+  acc.dstop = dstop0;
   const unsigned cellinit = (MODE == 1 ? 0u : g.boxfluid);
   for (int u = 0; u < 5; u++) {
     const int dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
@@ -515,44 +562,46 @@ __device__ __forceinline__ TAcc run_pass(const KConst& K, const DivGrid& g, cons
     }
     const unsigned n0 = re[0] - rs[0], n1 = re[1] - rs[1];
     if (n0 + n1 == 0u) continue;
-    if (n0 + n1 <= unsigned(TCAP)) {
+    constexpr int tcap = TcapT<FT>::v;
+    if (n0 + n1 <= unsigned(tcap)) {
       // both rows in one segment: [row a][row b]
       __syncthreads();
-      if (n0) stage_row(K, rs[0], re[0], 0u, rc.xo, dya, dza, poscell, velrhop, press, sA, sB, sC);
-      if (n1) stage_row(K, rs[1], re[1], n0, rc.xo, -dya, -dza, poscell, velrhop, press, sA, sB, sC);
+      if (n0) stage_row(K, rs[0], re[0], 0u, rc.xo, dya, dza, poscell, velrhop, press, sA, sB, sC, ft);
+      if (n1) stage_row(K, rs[1], re[1], n0, rc.xo, -dya, -dza, poscell, velrhop, press, sA, sB, sC, ft);
       __syncthreads();
       const int wa0 = int(ls[0] - rs[0]), wa1 = rc.act && n0 ? int(le[0] - rs[0]) : wa0;
       const int wb0 = int(n0 + ls[1] - rs[1]), wb1 = rc.act && n1 ? int(n0 + le[1] - rs[1]) : wb0;
-      tile_unit<TDENSITY, MODE>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, Q, acc);
+      tile_unit<TDENSITY, MODE, FT>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, Q, acc);
     } else {
       // too long for one segment: each row on its own, in TCAP segments
       for (int k = 0; k < 2; k++) {
         const int dz = k ? -dza : dza, dy = k ? -dya : dya;
-        for (unsigned seg = rs[k]; seg < re[k]; seg += TCAP) {
-          const unsigned segn = min(unsigned(TCAP), re[k] - seg);
+        for (unsigned seg = rs[k]; seg < re[k]; seg += tcap) {
+          const unsigned segn = min(unsigned(tcap), re[k] - seg);
           __syncthreads();
-          stage_row(K, seg, seg + segn, 0u, rc.xo, dy, dz, poscell, velrhop, press, sA, sB, sC);
+          stage_row(K, seg, seg + segn, 0u, rc.xo, dy, dz, poscell, velrhop, press, sA, sB, sC, ft);
           __syncthreads();
           const int w0 = int(max(ls[k], seg) - seg);
           const int w1 = rc.act ? max(w0, int(min(le[k], seg + segn)) - int(seg)) : w0;
-          tile_unit<TDENSITY, MODE>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, Q, acc);
+          tile_unit<TDENSITY, MODE, FT>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, Q, acc);
         }
       }
     }
   }
-  return finish<TDENSITY, MODE>(K, acc, p, Q);
+  return finish<TDENSITY, MODE, FT>(K, acc, p, Q);
 }
 
-template <int TDENSITY>
+template <int TDENSITY, bool FT = false>
 __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
                                                     unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
                                                     const float4* __restrict__ velrhop,
                                                     const float* __restrict__ press,
                                                     const unsigned* __restrict__ bc, DivGrid g, KConst K,
-                                                    float4* __restrict__ arace) {
-  __shared__ float4 sA[TCAP + SPH_PAD];  // over-read pad of the 8-wide candidate test (<= 7 records)
-  __shared__ float4 sB[TCAP];
-  __shared__ float2 sC[TCAP];  // press/rho, 1/rho
+                                                    float4* __restrict__ arace, FtRec ft) {
+  constexpr int tcap = TcapT<FT>::v;
+  __shared__ float4 sA[tcap + SPH_PAD];  // over-read pad of the 8-wide candidate test (<= 7 records)
+  __shared__ float4 sB[tcap];
+  __shared__ typename CRecT<FT>::type sC[tcap];  // press/rho, 1/rho (FT: mass-scaled + kind)
   __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];  // lane -> p1 of the item (see lane_order)
   __shared__ unsigned s_nwave[4];
@@ -623,15 +672,17 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
         const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act};
         // pass 0: fluid p2 (fluid p1: momentum/continuity/DDT; bound p1: continuity),
         // pass 1: bound p2 of fluid p1.  Each pass holds only its own accumulator.
-        TAcc f, bnd = {0, 0, 0, 0, 0, 0};
+        TAcc f, bnd = {0, 0, 0, 0, 0, 0, false};
         if (bitem) {
-          f = run_pass<TDENSITY, 2>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell, velrhop,
-                                    press, sA, sB, sC);
+          f = run_pass<TDENSITY, 2, FT>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell,
+                                        velrhop, press, sA, sB, sC, ft);
         } else {
-          f = run_pass<TDENSITY, 0>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell, velrhop,
-                                    press, sA, sB, sC);
-          bnd = run_pass<TDENSITY, 1>(K, g, rc, p, thr, pass_k(K, cvisc_b, K.massbound, p.vr.w), bc, poscell,
-                                      velrhop, press, sA, sB, sC);
+          // a floating p1 gets no DDT (JSphCpu.cpp:659-662)
+          const bool ftp1 = FT && act && CodeType(ft.code[p1]) == CODE_TYPE_FLOATING;
+          f = run_pass<TDENSITY, 0, FT>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell,
+                                        velrhop, press, sA, sB, sC, ft, ftp1);
+          bnd = run_pass<TDENSITY, 1, FT>(K, g, rc, p, thr, pass_k(K, cvisc_b, K.massbound, p.vr.w), bc, poscell,
+                                          velrhop, press, sA, sB, sC, ft, ftp1);
         }
         if (act && bitem) {
           // InteractionForcesBound store (JSphCpu.cpp:617-621) onto the reset ar = 0.
@@ -677,13 +728,27 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
 
 void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
                         const float4* poscell, const float4* velrhop, const float* press, const unsigned* begincell,
-                        DivGrid g, const KConst& K, float4* arace) {
-  switch (K.tdensity) {
-    case 0: hipLaunchKernelGGL(k_fluid_tiled<0>, dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace); break;
-    case 1: hipLaunchKernelGGL(k_fluid_tiled<1>, dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace); break;
-    case 2: hipLaunchKernelGGL(k_fluid_tiled<2>, dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace); break;
-    default: hipLaunchKernelGGL(k_fluid_tiled<3>, dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace); break;
+                        DivGrid g, const KConst& K, float4* arace, const typecode* code, const float* ftmassp) {
+  const FtRec ft = {code, ftmassp};
+#define SPH_TILED(TD, FTB)                                                                                    \
+  hipLaunchKernelGGL((k_fluid_tiled<TD, FTB>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, \
+                     press, begincell, g, K, arace, ft)
+  if (ftmassp) {
+    switch (K.tdensity) {
+      case 0: SPH_TILED(0, true); break;
+      case 1: SPH_TILED(1, true); break;
+      case 2: SPH_TILED(2, true); break;
+      default: SPH_TILED(3, true); break;
+    }
+  } else {
+    switch (K.tdensity) {
+      case 0: SPH_TILED(0, false); break;
+      case 1: SPH_TILED(1, false); break;
+      case 2: SPH_TILED(2, false); break;
+      default: SPH_TILED(3, false); break;
+    }
   }
+#undef SPH_TILED
 }
 
 }  // namespace sphx

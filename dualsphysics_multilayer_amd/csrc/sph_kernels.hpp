@@ -102,9 +102,12 @@ void launch_interaction_bound(hipStream_t stm, unsigned npbcap, DevScalars* sc, 
 // Tiled fluid interaction (sph_interaction_tiled.hip) and its per-divide item list.
 void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
                   uint4* items, unsigned* qctr);
+// With floating bodies (ftmassp != nullptr) the staged p2 records carry their mass ratio
+// and kind (the FT instantiation; one more float2 of LDS per record).
 void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
                         const float4* poscell, const float4* velrhop, const float* press, const unsigned* begincell,
-                        DivGrid g, const KConst& K, float4* arace);
+                        DivGrid g, const KConst& K, float4* arace, const typecode* code = nullptr,
+                        const float* ftmassp = nullptr);
 // mDBC boundary correction (sph_mdbc.hip; JSphCpu.cpp:1020-1187): density of every
 // boundary particle p1 < npbok with a normal extrapolated from its ghost node; press
 // refreshed.  `normal` is indexed by idp; list[npbcap] + nlist: scratch of the

@@ -645,7 +645,7 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
     // get ar = 0) and resets its own work counters at exit (zeroed once at allocation).
     TimedBegin(0);  // the timed interval is the interaction kernel alone (rocprof's per-kernel average)
     launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, begincell_, G, K,
-                       arace_);
+                       arace_, cur_.code, ftmassp_);
   } else {
     TimedBegin(0);
     launch_interaction(stream, cap_, sc_, poscell_, cur_.velrhop, press_, begincell_, G, K, arace_, cur_.code,
@@ -841,7 +841,8 @@ void SphGpuSingle::SetFloatings(unsigned nft, const SphFloatingDef* defs, double
   check_hip(hipMemcpy(ftmassp_, massp.data(), sizeof(float) * nft, hipMemcpyHostToDevice), "upload floatings");
   nftbodies_ = int(nft);
   nftp_ = nftp;
-  tiled_ = false;  // floating p2 carry their own mass: the per-particle kernel (csrc/sph_interaction.hip)
+  // floating p2 carry their own mass: the FT instantiation of the tiled kernel (or the
+  // per-particle kernel under SPH_INTERACTION=simple / CellMode=half)
   launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_);
   Sync();
 }
