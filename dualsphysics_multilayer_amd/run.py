@@ -128,12 +128,13 @@ class CaseRun:
         c, cd = self.case, self.case.case_def()
         fb = [b for b in c.blocks if b["type"] == "fixed"]
         fl = [b for b in c.blocks if b["type"] == "fluid"]
-        if len(fb) != 1 or len(fl) != 1:
-            raise CaseError("PART headers are written for cases with one fixed and one fluid block.")
+        if len(fl) != 1 or not fb:
+            raise CaseError("PART headers are written for cases with one fluid block.")
         return dict(app_name=self.app_name, case_name=c.case_name, cpart=cpart, nout=nout, step=step,
                     timestep=float(st["time"]),
                     symplectic_dtpre=float(st["sym_dtpre"]) if c.step_algorithm == 2 else 0.0,
                     np_total=c.case_np, case_np=c.case_np, case_nfixed=c.case_nfixed, case_nfluid=c.case_nfluid,
+                    case_nmoving=getattr(c, "case_nmoving", 0), case_nfloat=getattr(c, "case_nfloat", 0),
                     dp=c.dp, h=c.h, b=c.cteb, rhop0=c.rhop0, gamma=c.gamma, massbound=c.massbound,
                     massfluid=c.massfluid, map_posmin=list(cd["map_realposmin"]),
                     map_posmax=list(cd["map_realposmax"]), case_posmin=list(c.case_posmin),
@@ -153,7 +154,11 @@ class CaseRun:
             hdr["domain_min"], hdr["domain_max"] = cell_domain_limits(self.k, p["pos"], int(st["npb"]))
             write_part(os.path.join(self.dirout, "Part_%04u.bi4" % cpart), hdr,
                        {k: p[k] for k in ("idp", "pos", "vel", "rhop")})
-            write_part_head(os.path.join(self.dirout, "Part_Head.ibi4"), hdr)
+            # Part_Head.ibi4 (restart header) lists one fixed and one fluid MK block; cases with
+            # moving/floating blocks are not restartable by this core and get no Part_Head
+            if not getattr(self.case, "has_bodies", False) and len(
+                    [b for b in self.case.blocks if b["type"] == "fixed"]) == 1:
+                write_part_head(os.path.join(self.dirout, "Part_Head.ibi4"), hdr)
         self.parts.append(info)
         self.log("Part_%04u  %12.6f  %12d  np=%u  out=%u" % (cpart, info["time"], step, info["np"], nout))
         return info

@@ -255,3 +255,21 @@ def test_gpu_tiled_floating_interaction_matches_per_particle_kernel(variant, mon
         scale = np.abs(b[q]).max()
         assert np.abs(a[q] - b[q]).max() <= tol * scale, (q, np.abs(a[q] - b[q]).max(), scale)
         assert np.abs(a[q][flt] - b[q][flt]).max() <= tol * np.abs(b[q][flt]).max() + 1e-6, q
+
+
+@pytest.mark.gpu
+def test_gpu_run_driver_flume_matches_reference(tmp_path):
+    """The flume case through the reference's command line (run driver): PART 10 vs the
+    reference's PART 10 (moving/floating counts in the header)."""
+    from dualsphysics_multilayer_amd.core import read_part
+    from dualsphysics_multilayer_amd.run import main
+
+    case = os.path.join(FIX, "flume_verlet_ddt2", "CaseFlume")
+    out = str(tmp_path / "out")
+    assert main([case, out, "-nsteps:10", "-svsteps:1", "-saveposdouble:1", "-sv:binx"]) == 0
+    h, p = read_part(os.path.join(out, "Part_0010.bi4"))
+    assert (h["case_nmoving"], h["case_nfloat"]) == (352, 125)
+    got, ref = by_idp(p), _snap(_ref("verlet_ddt2"), 10)
+    assert np.array_equal(got["idp"], ref["idp"])
+    for q, t in zip(("pos", "vel", "rhop"), _tol(10)):
+        assert maxdiff(got, ref, q) <= t, (q, maxdiff(got, ref, q))
