@@ -176,17 +176,23 @@ class SphGpuSingle:
         _check(L.sph_solver_create(C.byref(self._cdef), C.byref(init.view), device, C.byref(h)))
         self._h = h
         self._time_set = None
-        if getattr(case, "has_bodies", False):
-            # a restart sets the PART time first: the motion program is advanced to it
-            if getattr(case, "time0", 0.0) or getattr(case, "symdtpre0", 0.0):
-                self.set_time(case.time0, case.symdtpre0)
-            if getattr(case, "motion", None):
-                movs, evts = motion_arrays(case.motion)
-                _check(L.sph_solver_set_motion(self._h, case.motion["nobj"], len(case.motion["movs"]), movs,
-                                               len(case.motion["evts"]), evts))
-            if getattr(case, "floatings", None):
-                fts = floating_array(case.floatings)
-                _check(L.sph_solver_set_floatings(self._h, len(case.floatings), fts, case.ftpause))
+        self._configure_bodies()
+
+    def _configure_bodies(self) -> None:
+        """Motion program and floating bodies of the case (JSph::LoadCaseConfig)."""
+        case, L = self.case, load_library()
+        if not getattr(case, "has_bodies", False):
+            return
+        # a restart sets the PART time first: the motion program is advanced to it
+        if getattr(case, "time0", 0.0) or getattr(case, "symdtpre0", 0.0):
+            self.set_time(case.time0, case.symdtpre0)
+        if getattr(case, "motion", None):
+            movs, evts = motion_arrays(case.motion)
+            _check(L.sph_solver_set_motion(self._h, case.motion["nobj"], len(case.motion["movs"]), movs,
+                                           len(case.motion["evts"]), evts))
+        if getattr(case, "floatings", None):
+            fts = floating_array(case.floatings)
+            _check(L.sph_solver_set_floatings(self._h, len(case.floatings), fts, case.ftpause))
 
     def close(self) -> None:
         if getattr(self, "_h", None):
@@ -324,8 +330,10 @@ class SphGpuSlab(SphGpuSingle):
         h = C.c_void_p()
         _check(L.sph_slab_create(C.byref(self._cdef), C.byref(init.view), device, C.byref(sd), C.byref(h)))
         self._h = h
+        self._time_set = None
         self.bounds = np.asarray(bounds)
         self.rank = rank
+        self._configure_bodies()
 
 
 class _SlabMember(SphGpuSingle):
@@ -335,6 +343,7 @@ class _SlabMember(SphGpuSingle):
         self.case = case
         self._group = group
         self._h = h
+        self._time_set = None
 
     def close(self) -> None:
         self._h = None
@@ -365,6 +374,11 @@ class SphSlabGroup:
             m = C.c_void_p()
             _check(L.sph_slab_group_member(h, i, C.byref(m)))
             self.members.append(_SlabMember(self, m, case))
+        for m in self.members:  # every slab runs the same motion program / body integration
+            m._configure_bodies()
+
+    def floatings(self) -> list:
+        return self.members[0].floatings()
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -18,8 +18,9 @@
 //   (JSphCpuSingle.cpp:897-1010): FtCalcForcesSum (:748-768), FtCalcForces (:775-815),
 //   FtCalcForcesRes (:822-858), constraints (:863-873), then the particle update and the
 //   body state.  GPU twins: cusph::FtCalcForcesSum/FtCalcForces/FtUpdate
-//   (JSphGpu_ker.cu:1749-2030).  k_ft_forces: one block per body sums the particle
-//   forces (fixed-order LDS tree: deterministic) and one lane integrates the body;
+//   (JSphGpu_ker.cu:1749-2030).  k_ft_partial: FT_NBLK blocks per body sum the particle
+//   forces (fixed-order LDS trees), k_ft_forces: one lane per body adds the partials in
+//   order (deterministic) and integrates the body;
 //   k_ft_update moves the particles and stores the body state.
 //
 // Matrix algebra follows JMatrix4 (JMatrix4.h:131-366) operation for operation and the
@@ -324,6 +325,7 @@ __global__ __launch_bounds__(256) void k_move_bound(const DevScalars* __restrict
                                                     float4* __restrict__ normal) {
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= sc->npb) return;
+  if (a.dcell[p] == DCELL_DISCARD) return;  // slab ghost (marked by the update): its owner moves it
   const typecode c = a.code[p];
   if (CodeType(c) != CODE_TYPE_MOVING || !CodeIsNormal(c)) return;
   const unsigned obj = c & CODE_MASKVALUE;
@@ -368,7 +370,7 @@ __global__ __launch_bounds__(256) void k_move_bound(const DevScalars* __restrict
 }
 
 void launch_motion(hipStream_t stm, unsigned npbcap, DevScalars* sc, const KConst& K, MotionDev* md,
-                   const MotMov* movs, const MotEvt* evts, const PartArrays& a, float4* normal) {
+                   const MotMov* movs, const MotEvt* evts, const PartArrays& a, float4* normal, const DivGrid&) {
   hipLaunchKernelGGL(k_motion, dim3(1), dim3(64), 0, stm, sc, md, movs, evts, -1.0, 0.0);
   const unsigned nb = (npbcap + 255) / 256;
   if (nb) hipLaunchKernelGGL(k_move_bound, dim3(nb), dim3(256), 0, stm, sc, K, md, a, normal);
@@ -383,19 +385,23 @@ void launch_motion_advance(hipStream_t stm, DevScalars* sc, MotionDev* md, const
 // CalcRidp (JSphCpu.cpp CalcRidp; JSphCpuSingle.cpp:478): position of each floating
 // particle after a divide, by idp - CaseNpb.
 __global__ __launch_bounds__(256) void k_ft_ridp(const DevScalars* __restrict__ sc, const typecode* __restrict__ code,
-                                                 const unsigned* __restrict__ idp, unsigned casenpb,
-                                                 unsigned nftp, unsigned* __restrict__ ftridp) {
+                                                 const unsigned* __restrict__ idp, const unsigned* __restrict__ dcell,
+                                                 unsigned casenpb, unsigned nftp, unsigned* __restrict__ ftridp,
+                                                 KConst K, DivGrid g) {
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p < sc->npb || p >= sc->np) return;
   if (CodeType(code[p]) != CODE_TYPE_FLOATING) return;
+  const int lcx = int(DcelCellx(K.domcellcode, dcell[p])) - g.xoff;
+  if (lcx < g.xown0 || lcx >= g.xown1) return;  // slab ghost
   const unsigned k = idp[p] - casenpb;
   if (k < nftp) ftridp[k] = p;
 }
 
 void launch_ft_ridp(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, unsigned casenpb,
-                    unsigned nftp, unsigned* ftridp) {
+                    unsigned nftp, unsigned* ftridp, const KConst& K, const DivGrid& g) {
   (void)hipMemsetAsync(ftridp, 0xff, sizeof(unsigned) * nftp, stm);
-  hipLaunchKernelGGL(k_ft_ridp, dim3((cap + 255) / 256), dim3(256), 0, stm, sc, a.code, a.idp, casenpb, nftp, ftridp);
+  hipLaunchKernelGGL(k_ft_ridp, dim3((cap + 255) / 256), dim3(256), 0, stm, sc, a.code, a.idp, a.dcell, casenpb, nftp,
+                     ftridp, K, g);
 }
 
 // float 3x3 helpers (FunctionsMath.h:91-329)
@@ -430,23 +436,22 @@ __device__ inline M3f m3_inv(const M3f& d) {
 
 constexpr int FT_BS = 256;
 
-// One block per body: FtCalcForcesSum + FtCalcForces + FtCalcForcesRes + constraints.
-__global__ __launch_bounds__(FT_BS) void k_ft_forces(const DevScalars* __restrict__ sc, KConst K,
-                                                     FtBody* __restrict__ bodies, const unsigned* __restrict__ ftridp,
-                                                     const float4* __restrict__ arace, const double2* __restrict__ posxy,
-                                                     const double* __restrict__ posz, int predictor) {
+// FtCalcForcesSum, stage 1: block (j, cf) sums force = ace*massp and torque = r x force
+// over the particles fp = j*FT_BS + t (+ FT_NBLK*FT_BS strides) of body cf with a
+// fixed-order LDS tree -> part[cf][j][6].
+__global__ __launch_bounds__(FT_BS) void k_ft_partial(const DevScalars* __restrict__ sc,
+                                                      const FtBody* __restrict__ bodies,
+                                                      const unsigned* __restrict__ ftridp,
+                                                      const float4* __restrict__ arace,
+                                                      const double2* __restrict__ posxy,
+                                                      const double* __restrict__ posz, float* __restrict__ part) {
   __shared__ float red[6][FT_BS];
-  const int cf = blockIdx.x;
-  FtBody& b = bodies[cf];
-  const double dt = (predictor ? sc->dt * .5 : sc->dt);
-  if (!(sc->tstep0 >= double(b.ftpause))) {
-    if (threadIdx.x == 0) b.skip = 1;
-    return;
-  }
+  const int cf = blockIdx.y, j = blockIdx.x;
+  const FtBody& b = bodies[cf];
   const double cx = b.center[0], cy = b.center[1], cz = b.center[2];
   const float massp = b.massp;
   float s[6] = {0, 0, 0, 0, 0, 0};
-  for (unsigned fp = threadIdx.x; fp < b.count; fp += FT_BS) {
+  for (unsigned fp = unsigned(j) * FT_BS + threadIdx.x; fp < b.count; fp += FT_NBLK * FT_BS) {
     const unsigned p = ftridp[b.begin + fp];
     if (p == 0xffffffffu) continue;
     const float4 ra = arace[p];
@@ -467,7 +472,24 @@ __global__ __launch_bounds__(FT_BS) void k_ft_forces(const DevScalars* __restric
       for (int k = 0; k < 6; k++) red[k][threadIdx.x] += red[k][threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x != 0) return;
+  if (threadIdx.x < 6) part[(size_t(cf) * FT_NBLK + j) * 6 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// Stage 2, one lane per body: the partial sums in order, then FtCalcForces +
+// FtCalcForcesRes + constraints.
+__global__ void k_ft_forces(const DevScalars* __restrict__ sc, KConst K, FtBody* __restrict__ bodies, int nbodies,
+                            const float* __restrict__ part, int predictor) {
+  const int cf = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cf >= nbodies) return;
+  FtBody& b = bodies[cf];
+  const double dt = (predictor ? sc->dt * .5 : sc->dt);
+  if (!(sc->tstep0 >= double(b.ftpause))) {
+    b.skip = 1;
+    return;
+  }
+  float red[6] = {0, 0, 0, 0, 0, 0};
+  for (int j = 0; j < FT_NBLK; j++)
+    for (int k = 0; k < 6; k++) red[k] += part[(size_t(cf) * FT_NBLK + j) * 6 + k];
   b.skip = 0;
   // FtCalcForces: inertia rotated to the current orientation, I^-1 * torque, + gravity.
   const M3f frot = m3_rot(b.angles[0], b.angles[1], b.angles[2]);
@@ -475,8 +497,8 @@ __global__ __launch_bounds__(FT_BS) void k_ft_forces(const DevScalars* __restric
                    b.inertia[5], b.inertia[6], b.inertia[7], b.inertia[8]};
   const M3f inert = m3_mul(m3_mul(frot, ini), m3_tras(frot));
   const M3f inv = m3_inv(inert);
-  float face[3] = {red[0][0], red[1][0], red[2][0]};
-  const float fo[3] = {red[3][0], red[4][0], red[5][0]};
+  float face[3] = {red[0], red[1], red[2]};
+  const float fo[3] = {red[3], red[4], red[5]};
   float omegaace[3] = {fo[0] * inv.a11 + fo[1] * inv.a12 + fo[2] * inv.a13,
                        fo[0] * inv.a21 + fo[1] * inv.a22 + fo[2] * inv.a23,
                        fo[0] * inv.a31 + fo[1] * inv.a32 + fo[2] * inv.a33};
@@ -550,9 +572,15 @@ __global__ __launch_bounds__(256) void k_ft_update(DevScalars* __restrict__ sc, 
   }
 }
 
-void launch_floating(hipStream_t stm, DevScalars* sc, const KConst& K, FtBody* bodies, int nbodies,
-                     const unsigned* ftridp, unsigned nftp, const float4* arace, const PartArrays& a, bool predictor) {
-  hipLaunchKernelGGL(k_ft_forces, dim3(nbodies), dim3(FT_BS), 0, stm, sc, K, bodies, ftridp, arace, a.posxy, a.posz,
+void launch_ft_partial(hipStream_t stm, DevScalars* sc, const FtBody* bodies, int nbodies, const unsigned* ftridp,
+                       const float4* arace, const PartArrays& a, float* part) {
+  hipLaunchKernelGGL(k_ft_partial, dim3(FT_NBLK, nbodies), dim3(FT_BS), 0, stm, sc, bodies, ftridp, arace, a.posxy,
+                     a.posz, part);
+}
+
+void launch_ft_body(hipStream_t stm, DevScalars* sc, const KConst& K, FtBody* bodies, int nbodies,
+                    const unsigned* ftridp, unsigned nftp, const PartArrays& a, bool predictor, const float* part) {
+  hipLaunchKernelGGL(k_ft_forces, dim3((nbodies + 63) / 64), dim3(64), 0, stm, sc, K, bodies, nbodies, part,
                      int(predictor));
   hipLaunchKernelGGL(k_ft_update, dim3((nftp + 255) / 256), dim3(256), 0, stm, sc, K, bodies, nbodies, ftridp, nftp,
                      a, int(predictor));

@@ -51,6 +51,9 @@ class RcclTransport final : public SlabTransport {
   void allreduce_max_u32(unsigned* d, int n, hipStream_t s) override {
     check_nccl(ncclAllReduce(d, d, size_t(n), ncclUint32, ncclMax, comm_, s), "ncclAllReduce");
   }
+  void allreduce_sum_f32(float* d, int n, hipStream_t s) override {
+    check_nccl(ncclAllReduce(d, d, size_t(n), ncclFloat, ncclSum, comm_, s), "ncclAllReduce sum");
+  }
 
  private:
   ncclComm_t comm_ = nullptr;
@@ -122,6 +125,20 @@ class LocalTransport final : public SlabTransport {
       for (int i = 0; i < n; i++) v[i] = std::max(v[i], hub_->slots[size_t(r)].vals[i]);
     hub_->barrier();
     check_hip(hipMemcpyAsync(d, v, 4 * size_t(n), hipMemcpyHostToDevice, s), "allreduce: write");
+    check_hip(hipStreamSynchronize(s), "allreduce: write");
+  }
+  // Summed in rank order (deterministic).
+  void allreduce_sum_f32(float* d, int n, hipStream_t s) override {
+    std::vector<float>& mine = hub_->slots[size_t(rank)].fvals;
+    mine.resize(size_t(n));
+    check_hip(hipMemcpyAsync(mine.data(), d, 4 * size_t(n), hipMemcpyDeviceToHost, s), "allreduce: read");
+    check_hip(hipStreamSynchronize(s), "allreduce: read");
+    hub_->barrier();
+    std::vector<float> v(size_t(n), 0.f);
+    for (int r = 0; r < nranks; r++)
+      for (int i = 0; i < n; i++) v[size_t(i)] += hub_->slots[size_t(r)].fvals[size_t(i)];
+    hub_->barrier();
+    check_hip(hipMemcpyAsync(d, v.data(), 4 * size_t(n), hipMemcpyHostToDevice, s), "allreduce: write");
     check_hip(hipStreamSynchronize(s), "allreduce: write");
   }
 

@@ -29,6 +29,8 @@ class SlabTransport {
                         size_t nrr, hipStream_t s) = 0;
   // In-place max over ranks of n uint32 values in device memory.
   virtual void allreduce_max_u32(unsigned* d, int n, hipStream_t s) = 0;
+  // In-place sum over ranks of n floats in device memory (floating-body force sums).
+  virtual void allreduce_sum_f32(float* d, int n, hipStream_t s) = 0;
   int rank = 0, nranks = 1;
   bool has_left() const { return rank > 0; }
   bool has_right() const { return rank + 1 < nranks; }
@@ -52,6 +54,7 @@ class LocalHub {
     const void* sr = nullptr;
     size_t nsr = 0;
     unsigned vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    std::vector<float> fvals;
   };
   std::vector<Slot> slots;
   int n;

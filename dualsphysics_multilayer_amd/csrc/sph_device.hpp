@@ -105,7 +105,7 @@ struct DevScalars {
 };
 constexpr int RED_VELMAX2 = 0, RED_ACEMAX2 = 1, RED_VISCDT = 2, RED_SLOTS = 64;
 
-constexpr unsigned ERR_DT_NAN = 1u, ERR_BOUNDOUT = 2u;
+constexpr unsigned ERR_DT_NAN = 1u, ERR_BOUNDOUT = 2u, ERR_HALO = 4u;
 
 // Wave-level max of a non-negative float, then one atomicMax per wave into a slot
 // chosen by the wave's global index (64 slots).

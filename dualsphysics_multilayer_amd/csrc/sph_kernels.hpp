@@ -115,6 +115,17 @@ void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const
 void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& cur, float* press,
                  const float4* normal, const unsigned* begincell, DivGrid g, const KConst& K,
                  const double dom_posmin[3], float threshold, unsigned* list, unsigned* nlist);
+// Slabs: (idp, rho, press) of the owned face-column boundary particles after mDBC, for
+// the neighbours' ghost copies (slot 0 holds the count; fixed capacity).
+struct MdbcFaceRec {
+  unsigned idp;
+  float rho, press;
+};
+void launch_mdbc_face_pack(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& a,
+                           const float* press, const KConst& K, const DivGrid& g, MdbcFaceRec* sl, MdbcFaceRec* sr,
+                           unsigned cap, unsigned* bidx, unsigned nbidx);
+void launch_mdbc_face_apply(hipStream_t stm, const MdbcFaceRec* rl, const MdbcFaceRec* rr, unsigned cap,
+                            const unsigned* bidx, unsigned nbidx, float4* velrhop, float* press);
 // Pair counters (JDsPips).
 void launch_count_pairs(hipStream_t stm, unsigned cap, const DevScalars* sc, const float4* poscell,
                         const unsigned* begincell, DivGrid g, const KConst& K, unsigned long long* out6);
@@ -182,13 +193,19 @@ struct FtBody {
 // k_motion over [sc->tstep0, +sc->last_dt) (or [t0, t0+dt) when t0 >= 0: restart
 // catch-up, no particle update), then the boundary particles.
 void launch_motion(hipStream_t stm, unsigned npbcap, DevScalars* sc, const KConst& K, MotionDev* md,
-                   const MotMov* movs, const MotEvt* evts, const PartArrays& a, float4* normal);
+                   const MotMov* movs, const MotEvt* evts, const PartArrays& a, float4* normal, const DivGrid& g);
 void launch_motion_advance(hipStream_t stm, DevScalars* sc, MotionDev* md, const MotMov* movs, const MotEvt* evts,
                            double t0, double dt);
+// Owned floating particles only (slab ghosts are summed by their owner).
 void launch_ft_ridp(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, unsigned casenpb,
-                    unsigned nftp, unsigned* ftridp);
-void launch_floating(hipStream_t stm, DevScalars* sc, const KConst& K, FtBody* bodies, int nbodies,
-                     const unsigned* ftridp, unsigned nftp, const float4* arace, const PartArrays& a, bool predictor);
+                    unsigned nftp, unsigned* ftridp, const KConst& K, const DivGrid& g);
+constexpr int FT_NBLK = 32;  // partial-sum blocks per body; part = float[nbodies][FT_NBLK][6]
+// RunFloating in two halves: partial force sums (a slab adds them over the slabs in
+// between), then body integration + particle update + body state.
+void launch_ft_partial(hipStream_t stm, DevScalars* sc, const FtBody* bodies, int nbodies, const unsigned* ftridp,
+                       const float4* arace, const PartArrays& a, float* part);
+void launch_ft_body(hipStream_t stm, DevScalars* sc, const KConst& K, FtBody* bodies, int nbodies,
+                    const unsigned* ftridp, unsigned nftp, const PartArrays& a, bool predictor, const float* part);
 
 // ---- slab decomposition (sph_slab.hip) ----
 // A particle MIGRATING to a neighbour: its full state, 96 B.

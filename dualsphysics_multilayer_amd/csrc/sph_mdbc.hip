@@ -37,6 +37,8 @@ struct MdbcArgs {
   float4* velrhop;
   float* press;
   const float4* normal;  // [CaseNbound], by idp
+  const unsigned* dcell;
+  unsigned domcellcode;
   const unsigned* bc;
   double posminx, posminy, posminz, scelld;
   float kernelsize2, ovh, awen, bwenovh, massfluid, rhopzero, threshold, determlimit;
@@ -96,6 +98,7 @@ __device__ __forceinline__ double wsum(double v) {
 struct GhostBox {
   double gx, gy, gz;
   int xini, xfin, yini, yfin, zini, zfin;
+  int cxu;  // unclamped local x cell of the ghost node
 };
 template <int SD>
 __device__ __forceinline__ GhostBox ghost_box(const MdbcArgs& a, const DivGrid& g, unsigned p1, float4 bn) {
@@ -105,6 +108,7 @@ __device__ __forceinline__ GhostBox ghost_box(const MdbcArgs& a, const DivGrid& 
   b.gy = pxy.y + double(bn.y);
   b.gz = a.posz[p1] + double(bn.z);
   const int cx = int((b.gx - a.posminx) / a.scelld) - g.xoff;
+  b.cxu = cx;
   const int cy = int((b.gy - a.posminy) / a.scelld);
   const int cz = int((b.gz - a.posminz) / a.scelld);
   b.xini = max(cx - SD, 0);
@@ -125,10 +129,20 @@ __global__ __launch_bounds__(256) void k_mdbc_list(const DevScalars* __restrict_
                                                    unsigned* __restrict__ list, unsigned* __restrict__ nlist) {
   const unsigned p1 = blockIdx.x * 256u + threadIdx.x;
   bool keep = false;
-  if (p1 < sc->npbok) {
+  bool own = true;
+  if (p1 < sc->npbok && (g.xown0 > 0 || g.xown1 < g.ncx)) {  // slab: owned p1 only
+    const int lcx = int(DcelCellx(a.domcellcode, a.dcell[p1])) - g.xoff;
+    own = lcx >= g.xown0 && lcx < g.xown1;
+  }
+  if (p1 < sc->npbok && own) {
     const float4 bn = a.normal[a.idp[p1]];
     if (bn.x != 0.f || bn.y != 0.f || bn.z != 0.f) {
       const GhostBox b = ghost_box<SD>(a, g, p1, bn);
+      // slab: the ghost node's cells must lie inside this slab's grid where a neighbour
+      // holds the rest of the domain (the grid edge of the whole map clamps, as the
+      // reference's search does)
+      if ((b.cxu - SD < 0 && g.xown0 > 0) || (b.cxu + SD >= g.ncx && g.xown1 < g.ncx))
+        atomicOr(&const_cast<DevScalars*>(sc)->error_flags, ERR_HALO);
       unsigned tot = 0;
       if (b.xini < b.xfin)
         for (int z = b.zini; z < b.zfin; z++)
@@ -312,6 +326,8 @@ void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const P
   MdbcArgs a;
   a.idp = cur.idp;
   a.code = cur.code;
+  a.dcell = cur.dcell;
+  a.domcellcode = K.domcellcode;
   a.posxy = cur.posxy;
   a.posz = cur.posz;
   a.velrhop = cur.velrhop;
@@ -345,6 +361,68 @@ void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const P
     hipLaunchKernelGGL(k_mdbc_list<2>, dim3(nb1), dim3(256), 0, stm, sc, a, g, list, nlist);
     hipLaunchKernelGGL(k_mdbc<2>, dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
   }
+}
+
+}  // namespace sphx
+
+// ---- slabs: corrected densities of the face-column boundary particles ------------------------
+// mDBC corrects the OWNED boundary particles at the start of an interaction, after the
+// divide's exchange sent their (uncorrected) copies to the neighbours as ghosts.  Each
+// slab therefore re-sends (idp, rho, press) of its owned boundary particles in its first /
+// last owned column (exactly the set the neighbour holds as ghosts, nothing moves in
+// between) in a fixed-size buffer (count in slot 0: no host round trip), and the receiver
+// writes them into its ghosts located by idp (bidx, rebuilt here).
+namespace sphx {
+
+__global__ __launch_bounds__(256) void k_mdbc_face_pack(const DevScalars* __restrict__ sc, PartArrays a,
+                                                        const float* __restrict__ press, KConst K, DivGrid g,
+                                                        MdbcFaceRec* __restrict__ sl, MdbcFaceRec* __restrict__ sr,
+                                                        unsigned cap, unsigned* __restrict__ bidx, unsigned nbidx) {
+  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= sc->npb) return;
+  const unsigned id = a.idp[p];
+  if (id < nbidx) bidx[id] = p;
+  const int lcx = int(DcelCellx(K.domcellcode, a.dcell[p])) - g.xoff;
+  // a slab of one owned column sends the same particle both ways
+  for (int side = 0; side < 2; side++) {
+    MdbcFaceRec* dst = nullptr;
+    if (side == 0 && lcx == g.xown0 && g.xown0 > 0) dst = sl;
+    if (side == 1 && lcx == g.xown1 - 1 && g.xown1 < g.ncx) dst = sr;
+    if (!dst) continue;
+    const unsigned k = atomicAdd(&dst[0].idp, 1u);
+    if (k + 1 < cap) dst[k + 1] = MdbcFaceRec{id, a.velrhop[p].w, press[p]};
+    else atomicOr(&const_cast<DevScalars*>(sc)->error_flags, ERR_HALO);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mdbc_face_apply(const MdbcFaceRec* __restrict__ rl,
+                                                         const MdbcFaceRec* __restrict__ rr, unsigned cap,
+                                                         const unsigned* __restrict__ bidx, unsigned nbidx,
+                                                         float4* __restrict__ velrhop, float* __restrict__ press) {
+  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+  const MdbcFaceRec* r = (blockIdx.y == 0 ? rl : rr);
+  if (!r || i + 1 >= cap || i >= r[0].idp) return;
+  const MdbcFaceRec q = r[i + 1];
+  if (q.idp >= nbidx) return;
+  const unsigned p = bidx[q.idp];
+  velrhop[p].w = q.rho;
+  press[p] = q.press;
+}
+
+void launch_mdbc_face_pack(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& a,
+                           const float* press, const KConst& K, const DivGrid& g, MdbcFaceRec* sl, MdbcFaceRec* sr,
+                           unsigned cap, unsigned* bidx, unsigned nbidx) {
+  (void)hipMemsetAsync(sl, 0, sizeof(MdbcFaceRec), stm);
+  (void)hipMemsetAsync(sr, 0, sizeof(MdbcFaceRec), stm);
+  if (npbcap)
+    hipLaunchKernelGGL(k_mdbc_face_pack, dim3((npbcap + 255) / 256), dim3(256), 0, stm, sc, a, press, K, g, sl, sr, cap,
+                       bidx, nbidx);
+}
+
+void launch_mdbc_face_apply(hipStream_t stm, const MdbcFaceRec* rl, const MdbcFaceRec* rr, unsigned cap,
+                            const unsigned* bidx, unsigned nbidx, float4* velrhop, float* press) {
+  hipLaunchKernelGGL(k_mdbc_face_apply, dim3((cap + 255) / 256, 2), dim3(256), 0, stm, rl, rr, cap, bidx, nbidx,
+                     velrhop, press);
 }
 
 }  // namespace sphx

@@ -236,8 +236,6 @@ SphGpuSingle::SphGpuSingle(const SphCaseDef& cdef, const SphParticlesHost& all, 
   if (!transport_) throw SphError(SPH_ERR_ARG, "slab without a transport");
   if (transport_->rank != slab.rank || transport_->nranks != slab.nranks)
     throw SphError(SPH_ERR_ARG, "slab rank does not match the transport");
-  if (cdef.tboundary == SPH_BOUND_MDBC)
-    throw SphError(SPH_ERR_UNSUPPORTED, "mDBC is not implemented on the slab decomposition");
   if (cdef.cellmode == SPH_CELLMODE_HALF)
     throw SphError(SPH_ERR_UNSUPPORTED, "CellMode=half is not implemented on the slab decomposition");
   Init(cdef, all);
@@ -439,9 +437,6 @@ void SphGpuSingle::Upload(const SphParticlesHost& h, const std::vector<unsigned>
       const typecode t = CodeType(code[i]);
       if (!CodeIsNormal(code[i]) || (i < npb0_) != (t < CODE_TYPE_FLOATING))
         throw SphError(SPH_ERR_ARG, "particle codes: boundary (fixed/moving) particles must be the first npb");
-      if (slab() && (t == CODE_TYPE_MOVING || t == CODE_TYPE_FLOATING))
-        throw SphError(SPH_ERR_UNSUPPORTED,
-                       "moving/floating bodies are not implemented on the slab decomposition");
     } else {
       code[i] = (i < npb0_ ? typecode(0) : CODE_TYPE_FLUID);
     }
@@ -490,7 +485,24 @@ void SphGpuSingle::UploadNormals(const SphCaseDef& cdef, const SphParticlesHost&
   check_hip(hipMalloc((void**)&normal_, sizeof(float4) * nor.size()), "hipMalloc normals");
   allocs_.push_back(normal_);
   check_hip(hipMemcpy(normal_, nor.data(), sizeof(float4) * nor.size(), hipMemcpyHostToDevice), "upload normals");
-  check_hip(hipMalloc((void**)&mdbclist_, sizeof(unsigned) * (size_t(npb0_) + 1)), "hipMalloc mDBC list");
+  if (slab()) {
+    // face-column boundary records: capacity from the densest x column of the case, x2
+    std::vector<unsigned> cnt(size_t(C.dom_cells[0]) + 1, 0u);
+    unsigned mx = 0;
+    for (unsigned p = 0; p < h.n; p++) {
+      if (h.idp[p] >= cdef.npb) continue;
+      const unsigned cx = unsigned((h.pos[3 * p] - C.dom_posmin[0]) / double(C.scell));
+      if (cx < cnt.size()) mx = std::max(mx, ++cnt[cx]);
+    }
+    mdbcfacecap_ = 2 * mx + 64;
+    check_hip(hipMalloc((void**)&mdbcface_, sizeof(MdbcFaceRec) * 4 * size_t(mdbcfacecap_)), "hipMalloc mDBC faces");
+    allocs_.push_back(mdbcface_);
+    check_hip(hipMalloc((void**)&bidx_, sizeof(unsigned) * std::max(cdef.npb, 1u)), "hipMalloc mDBC faces");
+    allocs_.push_back(bidx_);
+  }
+  // boundary particles migrate between slabs: the list is sized for the capacity
+  check_hip(hipMalloc((void**)&mdbclist_, sizeof(unsigned) * (size_t(slab() ? cap_ : npb0_) + 1)),
+            "hipMalloc mDBC list");
   allocs_.push_back(mdbclist_);
 }
 
@@ -628,7 +640,7 @@ void SphGpuSingle::RunCellDivide() {
                 G.xoff);
   std::swap(cur_, alt_);
   if (tiled_) launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_);
-  if (nftp_) launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_);
+  if (nftp_) launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_, K, G);
   TimedEnd(2);
 }
 
@@ -636,8 +648,17 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
   // mDBC boundary correction first, except in the Symplectic corrector (JSphCpuSingle.cpp:525).
   if (normal_ && interstep != 3) {
     TimedBegin(3);
-    launch_mdbc(stream, npb0_, sc_, cur_, press_, normal_, begincell_, G, K, C.dom_posmin, C.mdbc_threshold,
+    launch_mdbc(stream, slab() ? cap_ : npb0_, sc_, cur_, press_, normal_, begincell_, G, K, C.dom_posmin, C.mdbc_threshold,
                 mdbclist_ + 1, mdbclist_);
+    if (slab() && (transport_->has_left() || transport_->has_right())) {
+      const size_t fb = sizeof(MdbcFaceRec) * mdbcfacecap_;
+      MdbcFaceRec *sl = mdbcface_, *sr = mdbcface_ + mdbcfacecap_, *rl = sr + mdbcfacecap_, *rr = rl + mdbcfacecap_;
+      launch_mdbc_face_pack(stream, cap_, sc_, cur_, press_, K, G, sl, sr, mdbcfacecap_, bidx_, casenpb_);
+      transport_->exchange(sl, transport_->has_left() ? fb : 0, sr, transport_->has_right() ? fb : 0, rl,
+                           transport_->has_left() ? fb : 0, rr, transport_->has_right() ? fb : 0, stream);
+      launch_mdbc_face_apply(stream, transport_->has_left() ? rl : nullptr, transport_->has_right() ? rr : nullptr,
+                             mdbcfacecap_, bidx_, casenpb_, cur_.velrhop, press_);
+    }
     TimedEnd(3);
   }
   if (tiled_) {
@@ -717,13 +738,17 @@ void SphGpuSingle::ComputeStep() {
 // ---- moving boundaries and floating bodies ------------------------------------------------
 void SphGpuSingle::RunMotion() {
   TimedBegin(1);
-  launch_motion(stream, npb0_, sc_, K, motion_, motmovs_, motevts_, cur_, normal_);
+  launch_motion(stream, slab() ? cap_ : npb0_, sc_, K, motion_, motmovs_, motevts_, cur_, normal_, G);
   TimedEnd(1);
 }
 
 void SphGpuSingle::RunFloating(bool predictor) {
   TimedBegin(1);
-  launch_floating(stream, sc_, K, ftbodies_, nftbodies_, ftridp_, nftp_, arace_, cur_, predictor);
+  // the body sums span the whole domain: each slab sums its owned particles, the
+  // partial sums are added over the slabs, every slab integrates the same body
+  launch_ft_partial(stream, sc_, ftbodies_, nftbodies_, ftridp_, arace_, cur_, ftpart_);
+  if (slab()) transport_->allreduce_sum_f32(ftpart_, nftbodies_ * FT_NBLK * 6, stream);
+  launch_ft_body(stream, sc_, K, ftbodies_, nftbodies_, ftridp_, nftp_, cur_, predictor, ftpart_);
   TimedEnd(1);
 }
 
@@ -731,7 +756,6 @@ void SphGpuSingle::RunFloating(bool predictor) {
 void SphGpuSingle::SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* movs, unsigned nevt,
                              const SphMotionEvent* evts) {
   if (stepped_ || motion_) throw SphError(SPH_ERR_STATE, "the motion is configured once, before the first step");
-  if (slab()) throw SphError(SPH_ERR_UNSUPPORTED, "moving boundaries are not implemented on the slab decomposition");
   if (!nobj || nobj > unsigned(MOT_MAXOBJ)) throw SphError(SPH_ERR_UNSUPPORTED, "number of moving objects out of range");
   if ((nmov && !movs) || (nevt && !evts)) throw SphError(SPH_ERR_ARG, "motion arrays missing");
   std::vector<MotMov> mv(std::max(nmov, 1u));
@@ -802,7 +826,6 @@ void SphGpuSingle::SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* m
 // JSph::LoadCaseConfig floating objects (JSph.cpp:1046-1100).
 void SphGpuSingle::SetFloatings(unsigned nft, const SphFloatingDef* defs, double ftpause) {
   if (stepped_ || ftbodies_) throw SphError(SPH_ERR_STATE, "the floating bodies are configured once, before the first step");
-  if (slab()) throw SphError(SPH_ERR_UNSUPPORTED, "floating bodies are not implemented on the slab decomposition");
   if (!nft || !defs) throw SphError(SPH_ERR_ARG, "no floating bodies");
   std::vector<FtBody> b(nft);
   std::vector<float> massp(nft);
@@ -837,13 +860,15 @@ void SphGpuSingle::SetFloatings(unsigned nft, const SphFloatingDef* defs, double
   allocs_.push_back(ftmassp_);
   check_hip(hipMalloc((void**)&ftridp_, sizeof(unsigned) * nftp), "hipMalloc floatings");
   allocs_.push_back(ftridp_);
+  check_hip(hipMalloc((void**)&ftpart_, sizeof(float) * 6 * FT_NBLK * nft), "hipMalloc floatings");
+  allocs_.push_back(ftpart_);
   check_hip(hipMemcpy(ftbodies_, b.data(), sizeof(FtBody) * nft, hipMemcpyHostToDevice), "upload floatings");
   check_hip(hipMemcpy(ftmassp_, massp.data(), sizeof(float) * nft, hipMemcpyHostToDevice), "upload floatings");
   nftbodies_ = int(nft);
   nftp_ = nftp;
   // floating p2 carry their own mass: the FT instantiation of the tiled kernel (or the
   // per-particle kernel under SPH_INTERACTION=simple / CellMode=half)
-  launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_);
+  launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_, K, G);
   Sync();
 }
 
@@ -902,6 +927,8 @@ void SphGpuSingle::CheckErrors() {
   const SphRunStats s = Stats();
   if (s.error_flags & ERR_BOUNDOUT) throw SphError(SPH_ERR_BOUNDOUT, "boundary particles were excluded (AbortBoundOut)");
   if (s.error_flags & ERR_DT_NAN) throw SphError(SPH_ERR_DT, "The computed Dt is NaN or infinity");
+  if (s.error_flags & ERR_HALO)
+    throw SphError(SPH_ERR_UNSUPPORTED, "mDBC: a ghost node needs particles beyond the slab's ghost column");
 }
 
 unsigned SphGpuSingle::DtTrace(double* out, unsigned cap) {

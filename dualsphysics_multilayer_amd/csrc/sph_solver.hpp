@@ -110,6 +110,9 @@ class SphGpuSingle {
   float* press_ = nullptr;
   float4* normal_ = nullptr;      // mDBC: particle -> ghost node, by idp [CaseNbound]
   unsigned* mdbclist_ = nullptr;  // mDBC: wet boundary particles of this interaction [npb] + count
+  MdbcFaceRec* mdbcface_ = nullptr;  // slabs + mDBC: send left, send right, recv left, recv right [4][facecap]
+  unsigned mdbcfacecap_ = 0;
+  unsigned* bidx_ = nullptr;         // slabs + mDBC: boundary idp -> index [CaseNpb]
   float4* arace_ = nullptr;
   unsigned* begincell_ = nullptr;
   uint4* items_ = nullptr;        // tiled-interaction work items (per divide)
@@ -131,6 +134,7 @@ class SphGpuSingle {
   FtBody* ftbodies_ = nullptr;
   unsigned* ftridp_ = nullptr;   // floating particle (idp - CaseNpb) -> position, per divide
   float* ftmassp_ = nullptr;     // particle mass per body (interaction)
+  float* ftpart_ = nullptr;      // partial force sums [body][FT_NBLK][6]
   int nftbodies_ = 0;
   unsigned nftp_ = 0;            // floating particles of the case (CaseNfloat)
   unsigned casenpb_ = 0;         // CaseNpb: first floating idp

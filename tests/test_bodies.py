@@ -205,13 +205,26 @@ def test_gpu_bodies_deterministic():
 
 
 @pytest.mark.gpu
-def test_gpu_bodies_slab_refused():
-    from dualsphysics_multilayer_amd.core import SphError, SphSlabGroup, slab_partition
+@pytest.mark.parametrize("variant,nslabs", [("verlet_ddt2", 3), ("symplectic_ddt1_mdbc", 2)])
+def test_gpu_bodies_on_slabs_match_reference(variant, nslabs):
+    """Moving boundaries, the floating body (force sums added over the slabs) and mDBC on
+    the x-slab decomposition (in-process slabs on one GPU: the same pack / exchange /
+    reduce code as RCCL) vs the reference PARTs and body states."""
+    from dualsphysics_multilayer_amd.core import SphSlabGroup, slab_partition
 
-    x = _case("verlet_ddt2")
-    with pytest.raises(SphError):
-        g = SphSlabGroup(x, slab_partition(x, 2))
-        g.Run(1)
+    x, g = _case(variant), _ref(variant)
+    grp = SphSlabGroup(x, slab_partition(x, nslabs))
+    done = 0
+    for k in _kept(g):
+        grp.run(k - done)
+        done = k
+        got, ref = grp.particles(), _snap(g, k)
+        assert np.array_equal(got["idp"], ref["idp"]), "excluded/duplicated particles"
+        for q, t in zip(("pos", "vel", "rhop"), _tol(k)):
+            assert maxdiff(got, ref, q) <= t, (k, q, maxdiff(got, ref, q))
+        b = grp.floatings()[0]
+        assert np.abs(b["center"] - g["ft_center"][k, 0]).max() <= 1e-7
+        assert np.abs(b["fvel"] - g["ft_fvel"][k, 0]).max() <= 2e-3 * np.abs(g["ft_fvel"]).max() + 1e-6
 
 
 @pytest.mark.parametrize("variant,kw", [("verlet_ddt2", dict()),

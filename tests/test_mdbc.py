@@ -211,9 +211,21 @@ def test_gpu_xml_mdbc_case_matches_reference(tmp_path):
 
 
 @pytest.mark.gpu
-def test_gpu_mdbc_slab_refused():
-    from dualsphysics_multilayer_amd.core import SphError, SphSlabGroup, slab_partition
+@pytest.mark.parametrize("nslabs", [2, 4])
+def test_gpu_mdbc_on_slabs_matches_reference(nslabs):
+    """mDBC on the x-slab decomposition: owned boundary particles only, ghost nodes checked
+    to stay inside the slab's grid (their x-normal walls sit at the map ends)."""
+    from dualsphysics_multilayer_amd.core import SphSlabGroup, slab_partition
 
-    case = DamBreakCase(0.03, tboundary=2)
-    with pytest.raises(SphError, match="mDBC"):
-        SphSlabGroup(case, slab_partition(case, 2))
+    g_ = load("verlet_ddt2_mdbc_dp0.025")
+    dp, step_alg, ddt, _ = meta(g_)
+    case = DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt, tboundary=2)
+    grp = SphSlabGroup(case, slab_partition(case, nslabs))
+    done = 0
+    for k in steps(g_):
+        grp.run(k - done)
+        done = k
+        ref, got = snapshot(g_, k), grp.particles()
+        assert np.array_equal(got["idp"], ref["idp"])
+        for q, t in zip(("pos", "vel", "rhop"), _tol(k)):
+            assert maxdiff(got, ref, q) <= t, (k, q, maxdiff(got, ref, q))
