@@ -221,3 +221,63 @@ def test_halo_gives_single_domain_interaction():
 
 def test_exchange_protocol_invariants():
     _spawn(_protocol_worker)
+
+
+def _bodies_worker(rank, world, port):
+    """3. Floating bodies and mDBC on slabs (no GPU), on the wave flume (case.py
+    WaveFlumeCase, the bench's cfg4 generator): (a) the body force/torque sums of
+    k_ft_partial restated in numpy over each rank's OWNED floating particles, all-reduced
+    (SUM) over gloo, equal the single-domain sums to float rounding; (b) the post-mDBC
+    face records: the owned boundary particles a rank sends from its first/last owned
+    column are exactly the boundary ghosts its neighbour holds in its ghost column."""
+    _init(rank, world, port)
+    from dualsphysics_multilayer_amd.case import WaveFlumeCase
+    from dualsphysics_multilayer_amd.core import case_derive, slab_partition
+
+    case = WaveFlumeCase(0.025, tboundary=2)
+    k = case_derive(case.case_def())
+    bounds = slab_partition(case, world, 0.3)
+    col = _columns(case, k)
+    c0, c1 = int(bounds[rank]), int(bounds[rank + 1])
+    owned = (col >= c0) & (col < c1)
+    # (a) floating sums: ace from a seeded generator, identical on every rank
+    rng = np.random.default_rng(11)
+    ace = rng.normal(size=(case.np, 3)).astype(np.float32)
+    f = case.floatings[0]
+    sel = np.arange(f["idbegin"], f["idbegin"] + f["count"])
+    cen = np.array(f["center"])
+    massp = np.float32(f["masspart"])
+
+    def sums(idx):
+        force = ace[idx] * massp
+        d = (case.pos[idx] - cen).astype(np.float32)
+        tq = np.cross(d, force)
+        return np.concatenate([force.sum(axis=0, dtype=np.float64), tq.sum(axis=0, dtype=np.float64)])
+
+    mine = sel[owned[sel]]
+    t = torch.from_numpy(sums(mine).astype(np.float32))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    whole = sums(sel)
+    assert np.allclose(t.numpy(), whole, rtol=1e-5, atol=1e-6 * np.abs(whole).max()), (t.numpy(), whole)
+    cnt = torch.tensor([len(mine)], dtype=torch.int64)
+    dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+    assert int(cnt.item()) == f["count"], "floating particles not partitioned"
+    # (b) face records vs the neighbours' boundary ghosts
+    isb = np.arange(case.np) < case.npb
+    left = rank - 1 if rank > 0 else None
+    right = rank + 1 if rank + 1 < world else None
+    send_l = case.idp[isb & owned & (col == c0)] if left is not None else np.zeros(0, np.uint32)
+    send_r = case.idp[isb & owned & (col == c1 - 1)] if right is not None else np.zeros(0, np.uint32)
+    got_from_left = _sendrecv_arrays([send_r], right, left, [np.uint32])
+    got_from_right = _sendrecv_arrays([send_l], left, right, [np.uint32])
+    if left is not None:
+        ghosts = case.idp[isb & (col == c0 - 1)]
+        assert np.array_equal(np.sort(got_from_left[0]), np.sort(ghosts))
+    if right is not None:
+        ghosts = case.idp[isb & (col == c1)]
+        assert np.array_equal(np.sort(got_from_right[0]), np.sort(ghosts))
+    dist.destroy_process_group()
+
+
+def test_bodies_and_mdbc_faces_on_slabs():
+    _spawn(_bodies_worker)
