@@ -114,7 +114,8 @@ void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const
 // wet-particle list.
 void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& cur, float* press,
                  const float4* normal, const unsigned* begincell, DivGrid g, const KConst& K,
-                 const double dom_posmin[3], float threshold, unsigned* list, unsigned* nlist);
+                 const double dom_posmin[3], float threshold, unsigned* list, unsigned* nlist, void* sums);
+constexpr size_t MDBC_SUM_BYTES = 152;  // sizeof(MdbcSum): 16 doubles + 5 floats + index
 // Slabs: (idp, rho, press) of the owned face-column boundary particles after mDBC, for
 // the neighbours' ghost copies (slot 0 holds the count; fixed capacity).
 struct MdbcFaceRec {

@@ -29,7 +29,10 @@
 
 namespace sphx {
 
+struct MdbcSum;
+
 struct MdbcArgs {
+  MdbcSum* sums;  // per listed particle: the wave-reduced sums (pass 2 -> pass 3)
   const unsigned* idp;
   const typecode* code;
   const double2* posxy;
@@ -49,6 +52,12 @@ struct MdbcArgs {
 
 // fmath::Determinant4x4 (FunctionsMath.h:186-199), double.
 struct M4 { double a11, a12, a13, a14, a21, a22, a23, a24, a31, a32, a33, a34, a41, a42, a43, a44; };
+struct MdbcSum {
+  M4 m;
+  float r, gx, gy, gz, sumwab;
+  unsigned p1;
+};
+static_assert(sizeof(MdbcSum) == MDBC_SUM_BYTES, "MdbcSum layout");
 __device__ inline double det4(const M4& d) {
   return (d.a14 * d.a23 * d.a32 * d.a41 - d.a13 * d.a24 * d.a32 * d.a41 -
           d.a14 * d.a22 * d.a33 * d.a41 + d.a12 * d.a24 * d.a33 * d.a41 +
@@ -174,9 +183,11 @@ __global__ __launch_bounds__(256) void k_mdbc_list(const DevScalars* __restrict_
 // of these L2 reads, not by its FP work).  The 5 float and 16 double partial sums are
 // reduced across the wave in a fixed butterfly order (deterministic) and lane 0 solves.
 template <int SD>
-__global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc, MdbcArgs a, DivGrid g,
+__global__ __launch_bounds__(256) void k_mdbc(
+    const DevScalars* __restrict__ sc, MdbcArgs a, DivGrid g,
                                               const unsigned* __restrict__ list, const unsigned* __restrict__ nlist) {
   constexpr int W = 2 * SD + 1, MAXR = W * W;
+  __shared__ float4 s_acc[4][256];  // accepted pairs of a round, per wave
   const unsigned lane = threadIdx.x & 63u;
   const unsigned nwaves = gridDim.x * 4u;
   const unsigned n = *nlist;
@@ -204,17 +215,22 @@ __global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc,
       const unsigned t = __shfl_up(incl, off, 64);
       if (int(lane) >= off) incl += t;
     }
-    const unsigned total = __shfl(incl, MAXR - 1, 64);
+    const unsigned total = __builtin_amdgcn_readfirstlane(__shfl(incl, MAXR - 1, 64));
     const unsigned ofs = incl - rlen;
     unsigned o[MAXR], d[MAXR];
 #pragma unroll
-    for (int r = 0; r < MAXR; r++) {
-      o[r] = __shfl(ofs, r, 64);
-      d[r] = __shfl(rini, r, 64) - o[r];
+    for (int r = 0; r < MAXR; r++) {  // wave-uniform: scalar registers
+      o[r] = __builtin_amdgcn_readfirstlane(__shfl(ofs, r, 64));
+      d[r] = __builtin_amdgcn_readfirstlane(__shfl(rini, r, 64)) - o[r];
     }
     const bool any = total > 0u;
-    // Four candidates per lane per round, all loads issued before the arithmetic: the
-    // kernel is bound by the latency of these L2 reads, not by its FP work.
+    // Rounds of 256 candidates (four per lane, all loads issued before the arithmetic):
+    // each lane tests its four, the accepted pairs of the round are compacted into the
+    // wave's LDS slab (ballot ranks: the reference's candidate order is not needed, the
+    // sums are reduced in a fixed order below) and the pair body then runs once per 64
+    // ACCEPTED pairs instead of once per candidate slot (only ~1 in 6 candidates lies
+    // inside the support, and a divergent body costs the whole wave).
+    float4* acc = s_acc[threadIdx.x >> 6];
     for (unsigned k0 = lane; k0 < total; k0 += 256u) {
       unsigned p2[4];
       bool v[4];
@@ -241,13 +257,24 @@ __global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc,
         c2[u] = a.code[p2[u]];
         rho2[u] = a.velrhop[p2[u]].w;
       }
+      unsigned nacc = 0;
 #pragma unroll
       for (int u = 0; u < 4; u++) {
         const float drx = float(gx - q[u].x);
         const float dry = float(gy - q[u].y);
         const float drz = float(gz - qz[u]);
         const float rr2 = drx * drx + dry * dry + drz * drz;
-        if (v[u] && rr2 <= a.kernelsize2 && CodeIsFluid(c2[u])) {
+        const bool ok = v[u] && rr2 <= a.kernelsize2 && CodeIsFluid(c2[u]);
+        const unsigned long long bal = __ballot(ok);
+        if (ok) acc[nacc + unsigned(__popcll(bal & ((1ull << lane) - 1ull)))] = make_float4(drx, dry, drz, rho2[u]);
+        nacc += unsigned(__popcll(bal));
+      }
+      __builtin_amdgcn_wave_barrier();
+      for (unsigned j = lane; j < ((nacc + 63u) & ~63u); j += 64u) {
+        if (j < nacc) {
+          const float4 e = acc[j];
+          const float drx = e.x, dry = e.y, drz = e.z;
+          const float rr2 = drx * drx + dry * dry + drz * drz;
           // GetKernelWendland_WabFac (FunSphKernel.h:226-234); fac in its r -> 0
           // form (bwen/h)(1-q/2)^3, finite when a fluid particle sits on the ghost node.
           const float rad = sqrtf(rr2);
@@ -258,7 +285,7 @@ __global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc,
           const float wqq = qq + qq + 1.f;
           const float wab = a.awen * wqq * wqq2 * wqq2;
           const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
-          const float volp2 = a.massfluid / rho2[u];
+          const float volp2 = a.massfluid / e.w;
           rhopp1 += a.massfluid * wab;
           gx_ += a.massfluid * frx;
           gy_ += a.massfluid * fry;
@@ -272,6 +299,7 @@ __global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc,
           m.a41 += vfrz;  m.a42 += drx * vfrz;  m.a43 += dry * vfrz;  m.a44 += drz * vfrz;
         }
       }
+      __builtin_amdgcn_wave_barrier();
     }
     if (any) {  // wave-uniform
       rhopp1 = wsum(rhopp1); gx_ = wsum(gx_); gy_ = wsum(gy_); gz_ = wsum(gz_); sumwab = wsum(sumwab);
@@ -281,8 +309,30 @@ __global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc,
       m.a41 = wsum(m.a41); m.a42 = wsum(m.a42); m.a43 = wsum(m.a43); m.a44 = wsum(m.a44);
     }
     if (lane != 0u) continue;
+    MdbcSum& res = a.sums[it];
+    res.m = m;
+    res.r = rhopp1;
+    res.gx = gx_;
+    res.gy = gy_;
+    res.gz = gz_;
+    res.sumwab = sumwab;
+    res.p1 = p1;
+  }
+}
+
+// Pass 3, one lane per listed particle: the reference's solve of the summed system
+// (kept out of pass 2, whose registers then hold only the accumulation).
+__global__ __launch_bounds__(256) void k_mdbc_solve(MdbcArgs a, const unsigned* __restrict__ nlist) {
+  const unsigned it = blockIdx.x * blockDim.x + threadIdx.x;
+  if (it >= *nlist) return;
+  const MdbcSum& s = a.sums[it];
+  const M4 m = s.m;
+  const float rhopp1 = s.r, gx_ = s.gx, gy_ = s.gy, gz_ = s.gz, sumwab = s.sumwab;
+  const unsigned p1 = s.p1;
+  {
+    const float4 bn = a.normal[a.idp[p1]];
     const float thr = a.threshold;
-    if (!(sumwab >= thr || (thr >= 2.f && sumwab + 2.f >= thr))) continue;
+    if (!(sumwab >= thr || (thr >= 2.f && sumwab + 2.f >= thr))) return;
     float rhopfinal = FLT_MAX;
     const double determ = det4(m);
     if (fabs(determ) >= double(a.determlimit)) {
@@ -321,9 +371,10 @@ __global__ __launch_bounds__(256) void k_mdbc(const DevScalars* __restrict__ sc,
 
 void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& cur, float* press,
                  const float4* normal, const unsigned* begincell, DivGrid g, const KConst& K,
-                 const double dom_posmin[3], float threshold, unsigned* list, unsigned* nlist) {
+                 const double dom_posmin[3], float threshold, unsigned* list, unsigned* nlist, void* sums) {
   if (!npbcap) return;
   MdbcArgs a;
+  a.sums = static_cast<MdbcSum*>(sums);
   a.idp = cur.idp;
   a.code = cur.code;
   a.dcell = cur.dcell;
@@ -353,13 +404,17 @@ void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const P
   a.scelldiv = K.scelldiv;
   (void)hipMemsetAsync(nlist, 0, sizeof(unsigned), stm);
   const unsigned nb1 = (npbcap + 255u) / 256u;
-  const unsigned nb2 = std::min((npbcap + 3u) / 4u, 2048u);  // 4 waves per block, one listed particle per wave
+  // 4 waves per block, one listed particle per wave at a time: enough blocks that the
+  // latency-bound waves fill the CUs (2048 blocks left 2 waves per SIMD: 0.76 ms at 4M)
+  const unsigned nb2 = std::min((npbcap + 3u) / 4u, 32768u);
   if (K.scelldiv == 1) {
     hipLaunchKernelGGL(k_mdbc_list<1>, dim3(nb1), dim3(256), 0, stm, sc, a, g, list, nlist);
     hipLaunchKernelGGL(k_mdbc<1>, dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
+    hipLaunchKernelGGL(k_mdbc_solve, dim3((npbcap + 255u) / 256u), dim3(256), 0, stm, a, nlist);
   } else {
     hipLaunchKernelGGL(k_mdbc_list<2>, dim3(nb1), dim3(256), 0, stm, sc, a, g, list, nlist);
     hipLaunchKernelGGL(k_mdbc<2>, dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
+    hipLaunchKernelGGL(k_mdbc_solve, dim3((npbcap + 255u) / 256u), dim3(256), 0, stm, a, nlist);
   }
 }
 

@@ -504,6 +504,8 @@ void SphGpuSingle::UploadNormals(const SphCaseDef& cdef, const SphParticlesHost&
   check_hip(hipMalloc((void**)&mdbclist_, sizeof(unsigned) * (size_t(slab() ? cap_ : npb0_) + 1)),
             "hipMalloc mDBC list");
   allocs_.push_back(mdbclist_);
+  check_hip(hipMalloc(&mdbcsums_, MDBC_SUM_BYTES * (size_t(slab() ? cap_ : npb0_) + 1)), "hipMalloc mDBC sums");
+  allocs_.push_back(mdbcsums_);
 }
 
 // Restart: TimeStep and SymplecticDtPre of the loaded PART (JSph::InitRun, JSph.cpp:2094-2106).
@@ -649,7 +651,7 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
   if (normal_ && interstep != 3) {
     TimedBegin(3);
     launch_mdbc(stream, slab() ? cap_ : npb0_, sc_, cur_, press_, normal_, begincell_, G, K, C.dom_posmin, C.mdbc_threshold,
-                mdbclist_ + 1, mdbclist_);
+                mdbclist_ + 1, mdbclist_, mdbcsums_);
     if (slab() && (transport_->has_left() || transport_->has_right())) {
       const size_t fb = sizeof(MdbcFaceRec) * mdbcfacecap_;
       MdbcFaceRec *sl = mdbcface_, *sr = mdbcface_ + mdbcfacecap_, *rl = sr + mdbcfacecap_, *rr = rl + mdbcfacecap_;

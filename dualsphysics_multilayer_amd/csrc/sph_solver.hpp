@@ -110,6 +110,7 @@ class SphGpuSingle {
   float* press_ = nullptr;
   float4* normal_ = nullptr;      // mDBC: particle -> ghost node, by idp [CaseNbound]
   unsigned* mdbclist_ = nullptr;  // mDBC: wet boundary particles of this interaction [npb] + count
+  void* mdbcsums_ = nullptr;      // mDBC: reduced sums per listed particle (pass 2 -> solve)
   MdbcFaceRec* mdbcface_ = nullptr;  // slabs + mDBC: send left, send right, recv left, recv right [4][facecap]
   unsigned mdbcfacecap_ = 0;
   unsigned* bidx_ = nullptr;         // slabs + mDBC: boundary idp -> index [CaseNpb]
