@@ -260,7 +260,8 @@ def main() -> None:
         achieved = flops / (inter_ms * 1e-3) / 1e12 if inter_ms > 0 else None
         value = units / elapsed
         hbm_achieved = value * BYTES_PER_PARTICLE_STEP[case.step_algorithm] / 1e9
-        traffic = profiled_traffic("sphx::k_fluid_tiled<%d>" % case.tdensity, case.np,
+        traffic = profiled_traffic("sphx::k_fluid_tiled<%d, %s>" % (case.tdensity, "true" if getattr(
+            case, "floatings", None) else "false"), case.np,
                                    "BASELINE " + args.workload) if world == 1 else None
         res = {
             "metric": METRIC,
@@ -296,7 +297,7 @@ def main() -> None:
                 "owned_np_per_rank": per_rank_np,
             },
             "roofline": {
-                "kernel": (("k_interaction<tdensity=%d, floating> (Interaction_Forces, one lane per particle)"
+                "kernel": (("k_fluid_tiled<tdensity=%d, floating records> (Interaction_Forces)"
                             if getattr(case, "floatings", None) else "k_fluid_tiled<tdensity=%d> (Interaction_Forces)")
                            % case.tdensity),
                 "bound": "mfma",
