@@ -355,7 +355,8 @@ typedef struct SphMotionEvent {
   double start, finish;
 } SphMotionEvent;
 /* Motion program of the case's moving objects (JDsMotion::Init, JDsMotion.cpp:94-106);
- * call once after sph_solver_create and before the first step.  Evaluated on the device
+ * call once after sph_solver_create (or sph_slab_create, on every rank) and before the
+ * first step; a restart calls sph_solver_set_time first (the program is advanced to it).  Evaluated on the device
  * every step (no host round trip), applied as JSphCpu::RunMotion (JSphCpu.cpp:1758-1789). */
 int sph_solver_set_motion(SphSolver* s, uint32_t nobj, uint32_t nmov, const SphMotionMov* movs, uint32_t nevt,
                           const SphMotionEvent* evts);
@@ -376,7 +377,8 @@ typedef struct SphFloatingState {
   float fvel[3], fomega[3], angles[3], facelin[3], faceang[3];
   float pad;
 } SphFloatingState;
-/* Configure the floating bodies (call once, before the first step); ftpause = FtPause. */
+/* Configure the floating bodies (call once, before the first step); ftpause = FtPause.
+ * On slabs every rank passes all bodies; their force sums are added over the ranks. */
 int sph_solver_set_floatings(SphSolver* s, uint32_t nft, const SphFloatingDef* defs, double ftpause);
 int sph_solver_floatings(SphSolver* s, uint32_t cap, SphFloatingState* out, uint32_t* nft);
 
