@@ -77,6 +77,7 @@ EXPORTED_SYMBOLS = (
     "sph_solver_set_motion",
     "sph_solver_set_floatings",
     "sph_solver_floatings",
+    "sph_partfloat_write",
 )
 
 
@@ -135,6 +136,7 @@ def load_library(path: str = LIB_PATH):
                                         C.POINTER(SphMotionEvent)]
     L.sph_solver_set_floatings.argtypes = [vp, C.c_uint32, C.POINTER(SphFloatingDef), C.c_double]
     L.sph_solver_floatings.argtypes = [vp, C.c_uint32, C.POINTER(SphFloatingState), C.POINTER(C.c_uint32)]
+    L.sph_partfloat_write.argtypes = [C.c_char_p, C.c_char_p, C.c_uint32, C.c_uint32] + [vp] * 6 + [C.c_uint32] + [vp] * 8
     if L.sph_abi_version() != SPH_ABI_VERSION:
         raise SphError(3, "ABI version mismatch")
     _lib = L
@@ -479,3 +481,27 @@ def part_header(case, stats: dict | None = None, cpart: int = 0, app_name: str =
                 case_posmin=pmin.tolist(), case_posmax=pmax.tolist(), pos_double=1,
                 visco_type=1, visco=case.visco, viscoboundfactor=case.viscoboundfactor,
                 gravity=list(case.gravity), mkbound=10, mkfluid=0)
+
+
+def write_partfloat(path: str, floatings: list, parts: list, mkboundfirst: int = 10,
+                    app: str = "dualsphysics_multilayer_amd") -> None:
+    """PartFloat.fbi4 of a run: `floatings` = the case's bodies (XmlCase.floatings),
+    `parts` = [{cpart, step, time, bodies: [SphGpuSingle.floatings() dicts]}]."""
+    nft = len(floatings)
+    u16 = lambda a: np.ascontiguousarray(a, np.uint16)  # noqa: E731
+    u32 = lambda a: np.ascontiguousarray(a, np.uint32)  # noqa: E731
+    f32 = lambda a: np.ascontiguousarray(a, np.float32)  # noqa: E731
+    head = [u16([f["mkbound"] for f in floatings]), u32([f["idbegin"] for f in floatings]),
+            u32([f["count"] for f in floatings]), f32([f["massbody"] for f in floatings]),
+            f32([f["masspart"] for f in floatings]), f32([f.get("radius", 0.0) for f in floatings])]
+    cp = u32([p["cpart"] for p in parts])
+    st = u32([p["step"] for p in parts])
+    ts = np.ascontiguousarray([p["time"] for p in parts], np.float64)
+    cen = np.ascontiguousarray([[b["center"] for b in p["bodies"]] for p in parts], np.float64).reshape(-1)
+    arr = {k: f32([[b[k] for b in p["bodies"]] for p in parts]).reshape(-1)
+           for k in ("fvel", "fomega", "facelin", "faceang")}
+    ptr = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    _check(load_library().sph_partfloat_write(path.encode(), app.encode(), mkboundfirst, nft,
+                                              *[ptr(a) for a in head], len(parts), ptr(cp), ptr(st), ptr(ts),
+                                              ptr(cen), *[ptr(arr[k]) for k in ("fvel", "fomega", "facelin",
+                                                                                "faceang")]))

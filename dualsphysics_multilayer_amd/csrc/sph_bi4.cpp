@@ -268,6 +268,19 @@ Item read_file(const std::string& path, const std::string& filecode) {
   return root;
 }
 
+void write_list_file(const std::string& path, const std::string& filecode, const Item& head,
+                     const std::vector<Item>& items) {
+  Writer w;
+  const std::vector<uint8_t> h = bi4::head(filecode);
+  w.raw(h.data(), h.size());
+  emit_item(w, head);
+  for (const Item& it : items) emit_item(w, it);
+  std::ofstream f(path, std::ios::binary);
+  if (!f) throw SphError(SPH_ERR_ARG, "bi4: cannot create " + path);
+  f.write(reinterpret_cast<const char*>(w.b.data()), std::streamsize(w.b.size()));
+  if (!f) throw SphError(SPH_ERR_ARG, "bi4: write failed for " + path);
+}
+
 void write_file(const std::string& path, const std::string& filecode, const Item& root) {
   Writer w;
   const std::vector<uint8_t> h = head(filecode);
@@ -531,6 +544,47 @@ void normals_write(const std::string& path, const char* case_name, double dp, do
   root.set_pod("CountNormals", bi4::Uint, uint32_t(0));
   root.add_array("PartNormals", bi4::Double3, nbound, nor);
   bi4::write_file(path, kNormalsCode, root);
+}
+
+// Floating-body PART data PartFloat.fbi4 (JPartFloatBi4Save, JPartFloatBi4.cpp:243-346): a
+// list file — the head item (SaveInitial: AppName, FormatVer, MkBoundFirst, PosRefData,
+// FtCount + per-body arrays) followed by one appended PART_%04u item per saved PART
+// (SaveFileListApp), read back by JPartFloatBi4Load as items 1..n.
+void partfloat_write(const std::string& path, const char* app, uint32_t mkboundfirst, uint32_t nft,
+                     const uint16_t* mkbound, const uint32_t* begin, const uint32_t* count, const float* mass,
+                     const float* massp, const float* radius, uint32_t nparts, const uint32_t* cpart,
+                     const uint32_t* step, const double* timestep, const double* center, const float* fvel,
+                     const float* fomega, const float* facelin, const float* faceang) {
+  bi4::Item head;
+  head.name = "JPartFloatBi4";  // the loader finds it as LS0000_JPartFloatBi4 (JPartFloatBi4.cpp:531)
+  head.set_text("AppName", app ? app : "");
+  head.set_pod("FormatVer", bi4::Uint, uint32_t(180423));
+  head.set_pod("MkBoundFirst", bi4::Ushort, uint16_t(mkboundfirst));
+  head.set_pod("PosRefData", bi4::Bool, int32_t(0));
+  head.set_pod("FtCount", bi4::Uint, nft);
+  head.add_array("mkbound", bi4::Ushort, nft, mkbound);
+  head.add_array("begin", bi4::Uint, nft, begin);
+  head.add_array("count", bi4::Uint, nft, count);
+  head.add_array("mass", bi4::Float, nft, mass);
+  head.add_array("massp", bi4::Float, nft, massp);
+  head.add_array("radius", bi4::Float, nft, radius);
+  std::vector<bi4::Item> parts(nparts);
+  for (uint32_t k = 0; k < nparts; k++) {
+    bi4::Item& it = parts[k];
+    char nm[32];
+    std::snprintf(nm, sizeof(nm), "PART_%04u", cpart[k]);
+    it.name = nm;
+    it.set_pod("Cpart", bi4::Uint, cpart[k]);
+    it.set_pod("Step", bi4::Uint, step[k]);
+    it.set_pod("TimeStep", bi4::Double, timestep[k]);
+    it.set_pod("DemDtForce", bi4::Double, 0.0);
+    it.add_array("center", bi4::Double3, nft, center + size_t(3) * nft * k);
+    it.add_array("fvel", bi4::Float3, nft, fvel + size_t(3) * nft * k);
+    it.add_array("fomega", bi4::Float3, nft, fomega + size_t(3) * nft * k);
+    it.add_array("facelin", bi4::Float3, nft, facelin + size_t(3) * nft * k);
+    it.add_array("faceang", bi4::Float3, nft, faceang + size_t(3) * nft * k);
+  }
+  bi4::write_list_file(path, "JPartFloatBi4", head, parts);
 }
 
 void bi4_rewrite(const std::string& src, const std::string& dst) {

@@ -160,6 +160,18 @@ int sph_solver_floatings(SphSolver* s, uint32_t cap, SphFloatingState* out, uint
     if (nft) *nft = n;
   });
 }
+int sph_partfloat_write(const char* path, const char* app, uint32_t mkboundfirst, uint32_t nft,
+                        const uint16_t* mkbound, const uint32_t* begin, const uint32_t* count, const float* mass,
+                        const float* massp, const float* radius, uint32_t nparts, const uint32_t* cpart,
+                        const uint32_t* step, const double* timestep, const double* center, const float* fvel,
+                        const float* fomega, const float* facelin, const float* faceang) {
+  NEED(path && nft && mkbound && begin && count && mass && massp && radius && (!nparts || (cpart && step &&
+       timestep && center && fvel && fomega && facelin && faceang)));
+  return guard([&] {
+    sphx::partfloat_write(path, app, mkboundfirst, nft, mkbound, begin, count, mass, massp, radius, nparts, cpart,
+                          step, timestep, center, fvel, fomega, facelin, faceang);
+  });
+}
 int sph_solver_set_timing(SphSolver* s, int enabled) {
   NEED(s);
   return guard([&] { s->impl->SetTiming(enabled != 0); });

@@ -35,6 +35,11 @@ void part_read(const std::string& path, SphPartHeader& h, SphParticlesHost* out)
 void part_write(const std::string& path, const SphPartHeader& h, const SphParticlesHost& p);
 void part_head_write(const std::string& path, const SphPartHeader& h);
 void bi4_rewrite(const std::string& src, const std::string& dst);
+void partfloat_write(const std::string& path, const char* app, uint32_t mkboundfirst, uint32_t nft,
+                     const uint16_t* mkbound, const uint32_t* begin, const uint32_t* count, const float* mass,
+                     const float* massp, const float* radius, uint32_t nparts, const uint32_t* cpart,
+                     const uint32_t* step, const double* timestep, const double* center, const float* fvel,
+                     const float* fomega, const float* facelin, const float* faceang);
 uint32_t normals_read(const std::string& path, uint32_t cap, double* out);
 void normals_write(const std::string& path, const char* case_name, double dp, double h, double dist, uint32_t nbound,
                    const double* nor);

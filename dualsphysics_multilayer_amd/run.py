@@ -120,6 +120,7 @@ class CaseRun:
         self.output = OutputTime(case.timeout)
         self.parts: list[dict] = []
         self._nout_prev = 0
+        self._ftparts: list[dict] = []
         if save:
             os.makedirs(dirout, exist_ok=True)
 
@@ -159,6 +160,15 @@ class CaseRun:
             if not getattr(self.case, "has_bodies", False) and len(
                     [b for b in self.case.blocks if b["type"] == "fixed"]) == 1:
                 write_part_head(os.path.join(self.dirout, "Part_Head.ibi4"), hdr)
+            if getattr(self.case, "floatings", None):
+                # PartFloat.fbi4: the body states of every saved PART (JSphCpuSingle SaveData ->
+                # JPartFloatBi4Save::AddPartFloat/SavePartFloat)
+                from .core import write_partfloat
+
+                self._ftparts.append(dict(cpart=cpart, step=step, time=float(st["time"]),
+                                          bodies=self.solver.floatings()))
+                write_partfloat(os.path.join(self.dirout, "PartFloat.fbi4"), self.case.floatings, self._ftparts,
+                                mkboundfirst=self.case.mkboundfirst, app=self.app_name)
         self.parts.append(info)
         self.log("Part_%04u  %12.6f  %12d  np=%u  out=%u" % (cpart, info["time"], step, info["np"], nout))
         return info

@@ -381,6 +381,15 @@ typedef struct SphFloatingState {
  * On slabs every rank passes all bodies; their force sums are added over the ranks. */
 int sph_solver_set_floatings(SphSolver* s, uint32_t nft, const SphFloatingDef* defs, double ftpause);
 int sph_solver_floatings(SphSolver* s, uint32_t cap, SphFloatingState* out, uint32_t* nft);
+/* PartFloat.fbi4 (JPartFloatBi4Save::SaveInitial + AddPartFloat/SavePartFloat,
+ * JPartFloatBi4.cpp:243-346): per-body head arrays [nft] and, per saved PART k, its
+ * Cpart/Step/TimeStep and the body states center[k][nft][3], fvel, fomega, facelin,
+ * faceang [k][nft][3]; readable by the reference's JPartFloatBi4Load (FloatingInfo). */
+int sph_partfloat_write(const char* path, const char* app, uint32_t mkboundfirst, uint32_t nft,
+                        const uint16_t* mkbound, const uint32_t* begin, const uint32_t* count, const float* mass,
+                        const float* massp, const float* radius, uint32_t nparts, const uint32_t* cpart,
+                        const uint32_t* step, const double* timestep, const double* center, const float* fvel,
+                        const float* fomega, const float* facelin, const float* faceang);
 
 #ifdef __cplusplus
 }

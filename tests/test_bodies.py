@@ -284,5 +284,48 @@ def test_gpu_run_driver_flume_matches_reference(tmp_path):
     assert (h["case_nmoving"], h["case_nfloat"]) == (352, 125)
     got, ref = by_idp(p), _snap(_ref("verlet_ddt2"), 10)
     assert np.array_equal(got["idp"], ref["idp"])
+    # PartFloat.fbi4 through the reference's reader (oracle/_ref travels with the tree)
+    exe = os.path.join(os.path.dirname(HERE), "oracle", "_ref", "ftdump_ref")
+    if os.path.exists(exe):
+        import subprocess
+        import sys
+
+        sys.path.insert(0, os.path.join(HERE, "golden"))
+        from make_flume_case import load_ft
+
+        subprocess.check_call([exe, out, str(tmp_path / "ft.bin")], stdout=subprocess.DEVNULL)
+        t, c, v, w = load_ft(str(tmp_path / "ft.bin"))
+        g = _ref("verlet_ddt2")
+        assert len(t) == 11 and np.abs(c[10, 0] - g["ft_center"][10, 0]).max() <= 1e-7
     for q, t in zip(("pos", "vel", "rhop"), _tol(10)):
         assert maxdiff(got, ref, q) <= t, (q, maxdiff(got, ref, q))
+
+
+def test_partfloat_file_reads_with_the_reference_reader(tmp_path):
+    """PartFloat.fbi4 written by the core (sph_partfloat_write) is read by the reference's
+    own JPartFloatBi4Load (oracle/_ref/ftdump_ref): times, centres and velocities."""
+    import subprocess
+
+    from dualsphysics_multilayer_amd.core import write_partfloat
+
+    exe = os.path.join(os.path.dirname(HERE), "oracle", "_ref", "ftdump_ref")
+    if not os.path.exists(exe):
+        pytest.skip("reference tools (oracle/_ref) not built here")
+    sys_path = os.path.join(HERE, "golden")
+    import sys
+
+    sys.path.insert(0, sys_path)
+    from make_flume_case import load_ft
+
+    fl = _case("verlet_ddt2").floatings + [dict(mkbound=4, idbegin=9999, count=27, massbody=0.1, masspart=0.1 / 27)]
+    rng = np.random.default_rng(1)
+    parts = [dict(cpart=k, step=10 * k, time=0.001 * k,
+                  bodies=[dict(center=rng.normal(size=3), fvel=rng.normal(size=3), fomega=rng.normal(size=3),
+                               facelin=np.zeros(3), faceang=np.zeros(3)) for _ in fl]) for k in range(4)]
+    write_partfloat(str(tmp_path / "PartFloat.fbi4"), fl, parts)
+    subprocess.check_call([exe, str(tmp_path), str(tmp_path / "ft.bin")], stdout=subprocess.DEVNULL)
+    t, c, v, w = load_ft(str(tmp_path / "ft.bin"))
+    assert np.array_equal(t, [p["time"] for p in parts])
+    assert np.array_equal(c, np.array([[b["center"] for b in p["bodies"]] for p in parts]))
+    assert np.array_equal(v, np.array([[b["fvel"] for b in p["bodies"]] for p in parts], np.float32))
+    assert np.array_equal(w, np.array([[b["fomega"] for b in p["bodies"]] for p in parts], np.float32))
