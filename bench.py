@@ -34,6 +34,7 @@ import sys
 import tempfile
 import time
 
+T_START = time.perf_counter()
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -54,11 +55,42 @@ def dist_env():
     return rank, world, local
 
 
+def host_info(threads: int) -> dict:
+    """What the CPU baseline ran on: logical CPUs of the machine, CPUs this process may use,
+    the CPU model, and the thread rule (BASELINE.md asks for count and model)."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": model,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+            "thread_rule": "threads = min(OMP_NUM_THREADS (else nproc), 64): the reference caps OpenMP at "
+                           "OMP_MAXTHREADS=64 (OmpDefs.h:39); on the GPU box OMP_NUM_THREADS is the box's CPU "
+                           "share of one GPU (16)", "threads": threads}
+
+
+def _ref_run(exe: str, case: str, out: str, nsteps: int, threads: int) -> float:
+    """Simulation Runtime (step loop, s) of one reference run of `nsteps` steps."""
+    subprocess.run([exe, case, out, "-nsteps:%d" % nsteps, "-sv:none", "-svres:0", "-ompthreads:%d" % threads],
+                   capture_output=True, text=True, check=True, timeout=900)
+    log = open(os.path.join(out, "Run.out")).read()
+    return float(re.search(r"Simulation Runtime\.*:\s*([0-9.eE+-]+)", log).group(1))
+
+
 def reference_cpu_baseline(dp: float, nsteps: int, threads: int, step: int = 1, ddt: int = 2,
-                           boundary: int = 1, flume: bool = False) -> dict | None:
+                           boundary: int = 1, flume: bool = False, first: int = 10) -> dict | None:
     """Times the REFERENCE CPU solver (oracle/_ref, built from the reference sources)
-    on the same dam break (or wave flume); Steps/s is the solver's own 'Steps per second'
-    (step loop only)."""
+    on the same dam break (or wave flume) over the steady step window [first, first+nsteps)
+    (steps 10-110): two runs of `first` and `first+nsteps` steps, the
+    difference of their 'Simulation Runtime' (step loop only, no output) over nsteps."""
     ref = os.path.join(ROOT, "oracle", "_ref")
     exe = os.path.join(ref, "DualSPHysics5.2CPU_ref")
     gen = os.path.join(ref, "genflume_ref" if flume else "gencase_ref")
@@ -70,17 +102,18 @@ def reference_cpu_baseline(dp: float, nsteps: int, threads: int, step: int = 1, 
         out = subprocess.run([gen, repr(dp), tmp, str(step), str(ddt), "1.5", name, str(boundary)],
                              capture_output=True, text=True, check=True).stdout
         np_ = int(re.search(r"np=(\d+)", out).group(1))
-        subprocess.run([exe, os.path.join(tmp, name), os.path.join(tmp, "out"), "-nsteps:%d" % nsteps,
-                        "-sv:none", "-svres:0", "-ompthreads:%d" % threads], capture_output=True, text=True,
-                       check=True, timeout=600)
-        log = open(os.path.join(tmp, "out", "Run.out")).read()
-        sps = float(re.search(r"Steps per second\.*:\s*([0-9.eE+-]+)", log).group(1))
-        return {"value": sps * np_, "unit": "particle-steps/s", "cores": threads, "kind": "reference",
+        case = os.path.join(tmp, name)
+        t_a = _ref_run(exe, case, os.path.join(tmp, "a"), first, threads)
+        t_b = _ref_run(exe, case, os.path.join(tmp, "b"), first + nsteps, threads)
+        sec = t_b - t_a
+        return {"value": np_ * nsteps / sec, "unit": "particle-steps/s", "cores": threads, "kind": "reference",
+                "window_steps": [first, first + nsteps], "window_seconds": sec,
                 "sample": "reference DualSPHysics5.2 CPU (built from /root/reference sources, -O3 -fopenmp "
-                          "-ffast-math), %d-particle %s (%s), %d %s steps, -ompthreads:%d, "
-                          "'Steps per second' of Run.out" % (np_, "wave flume" if flume else "dam break",
-                                                             "mDBC" if boundary == 2 else "DBC", nsteps,
-                                                             "Verlet" if step == 1 else "Symplectic", threads)}
+                          "-ffast-math), %d-particle %s (%s), %s, steps %d-%d (Simulation Runtime of a %d-step "
+                          "run minus that of a %d-step run), -ompthreads:%d"
+                          % (np_, "wave flume" if flume else "dam break", "mDBC" if boundary == 2 else "DBC",
+                             "Verlet" if step == 1 else "Symplectic", first, first + nsteps, first + nsteps,
+                             first, threads)}
     except Exception as e:  # noqa: BLE001
         sys.stderr.write("reference CPU baseline failed: %r\n" % (e,))
         return None
@@ -153,7 +186,8 @@ def main() -> None:
                     help="boundary conditions (mdbc: modified DBC, Vel0, normals to the wall limit)")
     ap.add_argument("--bound-weight", type=float, default=0.3, help="slab balance weight of a bound particle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=8)
+    ap.add_argument("--cpu-steps", type=int, default=100,
+                    help="reference CPU steps timed (window 10 .. 10+K, BASELINE.md: 10-110)")
     ap.add_argument("--force-slab", action="store_true",
                     help="run the N>1 code path (gloo bootstrap + RCCL slab) even with one rank")
     args = ap.parse_args()
@@ -187,9 +221,13 @@ def main() -> None:
         dp = args.dp or CFG4_DP
         case = WaveFlumeCase(dp, tboundary=2 if args.boundary == "mdbc" else 1)
     bounds = None
-    fallback = None
     s = None
+    wall = {}
+    t_setup = time.perf_counter()
     if use_slab:
+        # A failed slab setup on any rank ends every rank with a non-zero status: the run
+        # never degrades into per-GPU replicas.
+        err = None
         try:
             bounds = slab_partition(case, world, args.bound_weight)
             ids = [comm_unique_id() if rank == 0 else None]
@@ -198,25 +236,18 @@ def main() -> None:
             s.run(args.warmup)
             s.sync()
             ok = torch.tensor([1], dtype=torch.int32)
-        except Exception as e:  # noqa: BLE001 -- reported in the JSON line, never silent
-            sys.stderr.write("rank %d: slab path failed: %r\n" % (rank, e))
-            fallback = repr(e)[:300]
+        except Exception as e:  # noqa: BLE001
+            err = e
             ok = torch.tensor([0], dtype=torch.int32)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         if int(ok.item()) == 0:
-            # every rank runs its own domain of the same size instead (still GPU, still
-            # one process per GPU); the JSON line says so
-            if s is not None:
-                s.close()
-            fallback = fallback or "slab path failed on another rank"
-            bounds = None
-            s = SphGpuSingle(case, device=local)
-            s.run(args.warmup)
-            s.sync()
+            sys.stderr.write("rank %d: slab run failed: %r\n" % (rank, err if err else "failed on another rank"))
+            raise SystemExit(3)
     else:
         s = SphGpuSingle(case, device=local)
         s.run(args.warmup)
         s.sync()
+    wall["setup_and_warmup_s"] = time.perf_counter() - t_setup
     pairs0 = s.count_pairs()
 
     def barrier():
@@ -292,7 +323,7 @@ def main() -> None:
                 "np": case.np,
                 "npb": case.npb,
                 "parallelism": (("slab-x%d (RCCL halo + migration, max-allreduce dt)" % world) if bounds is not None
-                                else ("replicas (FALLBACK: %s)" % fallback) if fallback else "single"),
+                                else "single"),
                 "slab_bounds_cells": None if bounds is None else [int(b) for b in bounds],
                 "owned_np_per_rank": per_rank_np,
             },
@@ -329,14 +360,20 @@ def main() -> None:
                                   "divide": float(phase_ms[2]), "mdbc": float(phase_ms[3])},
             "cpu_baseline": None,
         }
+        wall["timed_s"] = elapsed
         if not args.no_cpu_baseline and world == 1:
             threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), 64)
+            t_cpu = time.perf_counter()
             cb = reference_cpu_baseline(dp, args.cpu_steps, threads, case.step_algorithm, case.tdensity,
                                         case.tboundary, flume=args.workload == "cfg4")
             if cb is None:
-                cb = port_cpu_baseline(case, args.cpu_steps, threads)
+                cb = port_cpu_baseline(case, min(args.cpu_steps, 10), threads)
             cb["gpu_over_cpu"] = value / cb["value"]
+            cb["host"] = host_info(threads)
             res["cpu_baseline"] = cb
+            wall["cpu_baseline_s"] = time.perf_counter() - t_cpu
+        wall["process_s"] = time.perf_counter() - T_START
+        res["wall_breakdown"] = wall
         print(json.dumps(res))
     s.close()
     if dist is not None:

@@ -125,8 +125,11 @@ struct MdbcFaceRec {
 void launch_mdbc_face_pack(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& a,
                            const float* press, const KConst& K, const DivGrid& g, MdbcFaceRec* sl, MdbcFaceRec* sr,
                            unsigned cap, unsigned* bidx, unsigned nbidx);
-void launch_mdbc_face_apply(hipStream_t stm, const MdbcFaceRec* rl, const MdbcFaceRec* rr, unsigned cap,
-                            const unsigned* bidx, unsigned nbidx, float4* velrhop, float* press);
+// A record whose idp this slab does not hold as a boundary particle this step (bidx
+// stale or missing) raises ERR_HALO instead of writing.
+void launch_mdbc_face_apply(hipStream_t stm, DevScalars* sc, const MdbcFaceRec* rl, const MdbcFaceRec* rr,
+                            unsigned cap, const unsigned* bidx, unsigned nbidx, const unsigned* idp, float4* velrhop,
+                            float* press);
 // Pair counters (JDsPips).
 void launch_count_pairs(hipStream_t stm, unsigned cap, const DevScalars* sc, const float4* poscell,
                         const unsigned* begincell, DivGrid g, const KConst& K, unsigned long long* out6);
@@ -233,6 +236,8 @@ struct SlabGhost {
   unsigned short code, pad;
 };
 constexpr int PK_BS = 256, PK_ITEMS = 16, PK_TILE = PK_BS * PK_ITEMS;
+// Bytes of the pack kernels' tile counters for a capacity of n particles: [4][ntiles] u32.
+constexpr size_t PK_TILECNT_BYTES(size_t n) { return 4 * sizeof(unsigned) * ((n + PK_TILE - 1) / PK_TILE); }
 // Device counters of one exchange: [0] ghosts, [1] migrants, per neighbour.
 struct SlabCounts {
   unsigned long long sendl[2], sendr[2];  // records for the left / right neighbour

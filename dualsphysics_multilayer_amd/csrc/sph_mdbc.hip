@@ -450,16 +450,23 @@ __global__ __launch_bounds__(256) void k_mdbc_face_pack(const DevScalars* __rest
   }
 }
 
-__global__ __launch_bounds__(256) void k_mdbc_face_apply(const MdbcFaceRec* __restrict__ rl,
+__global__ __launch_bounds__(256) void k_mdbc_face_apply(DevScalars* __restrict__ sc,
+                                                         const MdbcFaceRec* __restrict__ rl,
                                                          const MdbcFaceRec* __restrict__ rr, unsigned cap,
                                                          const unsigned* __restrict__ bidx, unsigned nbidx,
+                                                         const unsigned* __restrict__ idp,
                                                          float4* __restrict__ velrhop, float* __restrict__ press) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
   const MdbcFaceRec* r = (blockIdx.y == 0 ? rl : rr);
   if (!r || i + 1 >= cap || i >= r[0].idp) return;
   const MdbcFaceRec q = r[i + 1];
-  if (q.idp >= nbidx) return;
-  const unsigned p = bidx[q.idp];
+  // bidx was rebuilt by this divide's face pack for the boundary particles held now; a
+  // stale entry (the particle left this slab) would point at another particle
+  const unsigned p = (q.idp < nbidx ? bidx[q.idp] : 0xffffffffu);
+  if (p >= sc->npb || idp[p] != q.idp) {
+    atomicOr(&sc->error_flags, ERR_HALO);
+    return;
+  }
   velrhop[p].w = q.rho;
   press[p] = q.press;
 }
@@ -474,10 +481,11 @@ void launch_mdbc_face_pack(hipStream_t stm, unsigned npbcap, const DevScalars* s
                        bidx, nbidx);
 }
 
-void launch_mdbc_face_apply(hipStream_t stm, const MdbcFaceRec* rl, const MdbcFaceRec* rr, unsigned cap,
-                            const unsigned* bidx, unsigned nbidx, float4* velrhop, float* press) {
-  hipLaunchKernelGGL(k_mdbc_face_apply, dim3((cap + 255) / 256, 2), dim3(256), 0, stm, rl, rr, cap, bidx, nbidx,
-                     velrhop, press);
+void launch_mdbc_face_apply(hipStream_t stm, DevScalars* sc, const MdbcFaceRec* rl, const MdbcFaceRec* rr,
+                            unsigned cap, const unsigned* bidx, unsigned nbidx, const unsigned* idp, float4* velrhop,
+                            float* press) {
+  hipLaunchKernelGGL(k_mdbc_face_apply, dim3((cap + 255) / 256, 2), dim3(256), 0, stm, sc, rl, rr, cap, bidx, nbidx,
+                     idp, velrhop, press);
 }
 
 }  // namespace sphx

@@ -366,7 +366,8 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
   }
   sort_.ntiles = unsigned((n + RS_TILE - 1) / RS_TILE);
   sort_.hist = (unsigned*)dmalloc(4 * size_t(sort_.ntiles) * (1u << RS_MAXBITS));
-  packtiles_ = (unsigned*)dmalloc(4 * 2 * ((n + PK_TILE - 1) / PK_TILE));
+  // slab pack tile counts: tilecnt[4][ntiles] (ghost L/R, migrant L/R; sph_slab.hip)
+  packtiles_ = (unsigned*)dmalloc(PK_TILECNT_BYTES(n));
   cap_ = cap;
 }
 
@@ -500,11 +501,13 @@ void SphGpuSingle::UploadNormals(const SphCaseDef& cdef, const SphParticlesHost&
     check_hip(hipMalloc((void**)&bidx_, sizeof(unsigned) * std::max(cdef.npb, 1u)), "hipMalloc mDBC faces");
     allocs_.push_back(bidx_);
   }
-  // boundary particles migrate between slabs: the list is sized for the capacity
-  check_hip(hipMalloc((void**)&mdbclist_, sizeof(unsigned) * (size_t(slab() ? cap_ : npb0_) + 1)),
-            "hipMalloc mDBC list");
+  // boundary particles migrate between slabs, but a slab never holds more boundary
+  // particles (owned + ghost) than the case has: CaseNpb bounds every slab's npbok, so
+  // the list and sums keep their size when Grow() raises the particle capacity
+  const size_t nlist = size_t(slab() ? cdef.npb : npb0_) + 1;
+  check_hip(hipMalloc((void**)&mdbclist_, sizeof(unsigned) * nlist), "hipMalloc mDBC list");
   allocs_.push_back(mdbclist_);
-  check_hip(hipMalloc(&mdbcsums_, MDBC_SUM_BYTES * (size_t(slab() ? cap_ : npb0_) + 1)), "hipMalloc mDBC sums");
+  check_hip(hipMalloc(&mdbcsums_, MDBC_SUM_BYTES * nlist), "hipMalloc mDBC sums");
   allocs_.push_back(mdbcsums_);
 }
 
@@ -658,8 +661,9 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
       launch_mdbc_face_pack(stream, cap_, sc_, cur_, press_, K, G, sl, sr, mdbcfacecap_, bidx_, casenpb_);
       transport_->exchange(sl, transport_->has_left() ? fb : 0, sr, transport_->has_right() ? fb : 0, rl,
                            transport_->has_left() ? fb : 0, rr, transport_->has_right() ? fb : 0, stream);
-      launch_mdbc_face_apply(stream, transport_->has_left() ? rl : nullptr, transport_->has_right() ? rr : nullptr,
-                             mdbcfacecap_, bidx_, casenpb_, cur_.velrhop, press_);
+      launch_mdbc_face_apply(stream, sc_, transport_->has_left() ? rl : nullptr,
+                             transport_->has_right() ? rr : nullptr, mdbcfacecap_, bidx_, casenpb_, cur_.idp,
+                             cur_.velrhop, press_);
     }
     TimedEnd(3);
   }

@@ -167,8 +167,12 @@ class CaseRun:
 
                 self._ftparts.append(dict(cpart=cpart, step=step, time=float(st["time"]),
                                           bodies=self.solver.floatings()))
-                write_partfloat(os.path.join(self.dirout, "PartFloat.fbi4"), self.case.floatings, self._ftparts,
+                # rewritten whole into a temporary file and renamed over the previous one, so a
+                # crash mid-write never truncates the records of earlier PARTs
+                path = os.path.join(self.dirout, "PartFloat.fbi4")
+                write_partfloat(path + ".tmp", self.case.floatings, self._ftparts,
                                 mkboundfirst=self.case.mkboundfirst, app=self.app_name)
+                os.replace(path + ".tmp", path)
         self.parts.append(info)
         self.log("Part_%04u  %12.6f  %12d  np=%u  out=%u" % (cpart, info["time"], step, info["np"], nout))
         return info

@@ -11,7 +11,7 @@ bit-exact.
 import numpy as np
 import pytest
 
-from golden_io import by_idp, cellmode, load, maxdiff, meta, snapshot, steps
+from golden_io import tol, by_idp, cellmode, load, maxdiff, meta, snapshot, steps
 
 from dualsphysics_multilayer_amd.case import DamBreakCase
 
@@ -19,20 +19,10 @@ pytestmark = pytest.mark.gpu
 
 oracle = pytest.importorskip("oracle.pyoracle")
 
-
 def gpu(case):
     from dualsphysics_multilayer_amd.core import SphGpuSingle
 
     return SphGpuSingle(case, device=0)
-
-
-def tol(step):  # (pos, vel, rho), 10x the measured noise floor
-    if step <= 1:
-        return 1e-8, 2.2e-5, 1e-2
-    if step <= 20:
-        return 1e-7, 5e-5, 1e-2
-    return 2e-6, 2e-4, 2e-2
-
 
 def test_initial_divide_order_is_the_oracles():
     """Stable cell sort: same particle order as the CPU counting sort (bit-exact)."""
@@ -43,7 +33,6 @@ def test_initial_divide_order_is_the_oracles():
     assert np.array_equal(pg["pos"], po["pos"])
     sg, so = g.stats(), o.stats()
     assert (sg["np"], sg["npb"], sg["npbok"]) == (so["np"], so["npb"], so["npbok"])
-
 
 def test_pair_counts_match_oracle():
     """Checked candidates (the cell search itself) are bit-exact.  Real pairs may differ
@@ -61,7 +50,6 @@ def test_pair_counts_match_oracle():
     o.run(15)
     cg, co = g.count_pairs().astype(np.int64), o.count_pairs().astype(np.int64)
     assert np.all(np.abs(cg - co) <= 0.001 * co + 8), (cg, co)
-
 
 @pytest.mark.parametrize("ddt", [0, 1, 2, 3])
 def test_interaction_matches_oracle(ddt):
@@ -83,7 +71,6 @@ def test_interaction_matches_oracle(ddt):
     assert ig["acemax"] == pytest.approx(io["acemax"], rel=1e-4)
     assert ig["viscdtmax"] == pytest.approx(io["viscdtmax"], rel=1e-3)
 
-
 def test_half_cells_match_oracle():
     """CellMode=half (cells of h, +-2 cells: JCellSearch_inline.h:33-47 with scelldiv 2):
     the same stable sort order and candidate counts as the oracle (bit-exact), the
@@ -100,7 +87,6 @@ def test_half_cells_match_oracle():
     assert np.abs(ig["ace"] - io["ace"]).max() <= 2e-4 * np.abs(io["ace"]).max()
     assert np.abs(ig["ar"] - io["ar"]).max() <= 2e-4 * np.abs(io["ar"]).max()
 
-
 def test_interaction_first_step_tight():
     """At t=0 (v=0) the interaction inputs are identical: ar/ace agree to float rounding."""
     case = DamBreakCase(0.02, tdensity=0, celldomfixed=True)
@@ -109,7 +95,6 @@ def test_interaction_first_step_tight():
     scale = np.abs(io["ace"]).max()
     assert np.abs(ig["ace"] - io["ace"]).max() <= 1e-5 * scale
     assert np.abs(ig["ar"] - io["ar"]).max() <= 1e-5 * max(np.abs(io["ar"]).max(), 1e-3)
-
 
 @pytest.mark.parametrize("name", ["verlet_ddt2_dp0.02", "symplectic_ddt1_dp0.025", "verlet_ddtnone_dp0.025",
                                   "symplectic_ddt3_dp0.03", "verlet_ddt2_half_dp0.025"])
@@ -131,7 +116,6 @@ def test_steps_match_reference_parts(name):
         assert maxdiff(got, ref, "rhop") <= tr, (k, maxdiff(got, ref, "rhop"))
         assert abs(s.stats()["time"] - float(ref["time"])) <= 1e-8 * max(1.0, k)
 
-
 def test_dt_trace_matches_reference_57k():
     g_ = load("verlet_ddt2_dp0.0127_dt")
     dp, step_alg, ddt, nsteps = meta(g_)
@@ -140,7 +124,6 @@ def test_dt_trace_matches_reference_57k():
     dt = s.dt_trace()
     assert len(dt) == nsteps
     assert np.abs(dt / g_["dt"] - 1).max() < 1e-5
-
 
 def test_deterministic_bitwise():
     case = DamBreakCase(0.025)
@@ -151,7 +134,6 @@ def test_deterministic_bitwise():
     for k in ("idp", "pos", "vel", "rhop"):
         assert np.array_equal(pa[k], pb[k]), k
     assert np.array_equal(a.dt_trace(), b.dt_trace())
-
 
 def test_exclusion_matches_oracle():
     """OUTRHOP / OUTPOS exclusion (JSphCpu.cpp:1240-1293, 1324) removes the same particles,
@@ -171,7 +153,6 @@ def test_exclusion_matches_oracle():
         assert (sg["np"], sg["nout"]) == (so["np"], so["nout"])
         assert np.array_equal(np.sort(g.particles()["idp"]), np.sort(o.particles()["idp"]))
     assert g.stats()["nout"] >= 3
-
 
 def test_large_case_properties():
     """At 1M particles (BASELINE cfg2 size) the oracle is too slow for many steps:
@@ -199,3 +180,23 @@ def test_large_case_properties():
     b.run(10)
     pb = b.particles()
     assert np.array_equal(p["pos"], pb["pos"]) and np.array_equal(p["vel"], pb["vel"])
+
+def test_cfg2_1m_matches_oracle():
+    """BASELINE cfg2 at its full size (1,025,964 particles): the GPU state after 1 and 3
+    Verlet steps against the oracle's (the C++ restatement pinned to the reference's PARTs,
+    test_oracle_golden.py) on the same case, at the step tolerances of the small cases."""
+    case = DamBreakCase(0.0045, celldomfixed=True)
+    assert case.np == 1025964
+    g, o = gpu(case), oracle.OracleSolver(case, nthreads=16)
+    done = 0
+    for k in (1, 3):
+        g.run(k - done)
+        o.run(k - done)
+        done = k
+        pg, po = by_idp(g.particles()), by_idp(o.particles())
+        assert np.array_equal(pg["idp"], po["idp"])
+        tp, tv, tr = tol(k)
+        assert maxdiff(pg, po, "pos") <= tp, (k, maxdiff(pg, po, "pos"))
+        assert maxdiff(pg, po, "vel") <= tv, (k, maxdiff(pg, po, "vel"))
+        assert maxdiff(pg, po, "rhop") <= tr, (k, maxdiff(pg, po, "rhop"))
+        assert g.stats()["time"] == pytest.approx(o.stats()["time"], rel=1e-7)

@@ -11,7 +11,7 @@ device-to-device copies as the transport — RCCL refuses two ranks on one devic
 import numpy as np
 import pytest
 
-from golden_io import by_idp, load, maxdiff, meta, snapshot, steps
+from golden_io import tol, by_idp, load, maxdiff, meta, snapshot, steps
 
 from dualsphysics_multilayer_amd.case import DamBreakCase
 
@@ -20,12 +20,6 @@ pytestmark = pytest.mark.gpu
 oracle = pytest.importorskip("oracle.pyoracle")
 
 
-def tol(step):  # same as test_gpu_parity.tol: 10x the reference's noise floor
-    if step <= 1:
-        return 1e-8, 2.2e-5, 1e-2
-    if step <= 20:
-        return 1e-7, 5e-5, 1e-2
-    return 2e-6, 2e-4, 2e-2
 
 
 def group(case, nslabs, bounds=None):
@@ -164,3 +158,26 @@ def test_rccl_transport_single_rank():
     assert s.stats()["time"] == pytest.approx(one.stats()["time"], rel=1e-9)
     check_close(by_idp(s.particles()), by_idp(one.particles()), 20)
     s.close()
+
+
+def test_cfg3_10m_slabs_match_single_domain():
+    """BASELINE cfg3 at its full size (9,969,118 particles, Symplectic + DDT Molteni): four
+    in-process slabs against one domain over 5 steps — particle count conserved, the same
+    excluded set and simulated time, fields within the 5-step noise tolerance."""
+    case = DamBreakCase(0.00205, step_algorithm=2, tdensity=1)
+    assert case.np == 9969118
+    one = single(case)
+    one.run(5)
+    s1 = one.stats()
+    p1 = by_idp(one.particles())
+    one.close()
+    del one
+    grp = group(case, 4)
+    grp.run(5)
+    st = grp.stats()
+    assert sum(s["np"] for s in st) == s1["np"] == case.np
+    assert sum(s["nout"] for s in st) == s1["nout"] == 0
+    assert abs(st[0]["time"] - s1["time"]) <= 1e-9
+    pg = grp.particles()
+    assert np.array_equal(pg["idp"], p1["idp"])
+    check_close(pg, p1, 5)
