@@ -1,11 +1,11 @@
-"""ctypes mirror of the POD structs in include/sphcore.h (ABI version 4)."""
+"""ctypes mirror of the POD structs in include/sphcore.h (ABI version 5)."""
 from __future__ import annotations
 
 import ctypes as C
 
 import numpy as np
 
-SPH_ABI_VERSION = 4
+SPH_ABI_VERSION = 5
 
 SPH_STATUS = {
     0: "SPH_OK",
@@ -22,7 +22,33 @@ SPH_STATUS = {
 
 SPH_BOUND_DBC, SPH_BOUND_MDBC = 1, 2
 SPH_SLIP_VEL0, SPH_SLIP_NOSLIP, SPH_SLIP_FREESLIP = 1, 2, 3
-_CASEDEF_DEFAULTS = {"tboundary": SPH_BOUND_DBC, "slipmode": SPH_SLIP_VEL0, "mdbc_threshold": 0.0}
+SPH_RHEOLOGY_SINGLE, SPH_RHEOLOGY_NN = 1, 2
+SPH_VELGRAD_FDA, SPH_VELGRAD_SPH = 1, 2
+SPH_VISCO_ARTIFICIAL, SPH_VISCO_LAMINARSPS, SPH_VISCO_CONSTEQ = 1, 2, 3
+SPH_SHIFT_NONE, SPH_SHIFT_NOBOUND, SPH_SHIFT_NOFIXED, SPH_SHIFT_FULL = 0, 1, 2, 3
+SPH_MAXPHASES = 8
+_CASEDEF_DEFAULTS = {"tboundary": SPH_BOUND_DBC, "slipmode": SPH_SLIP_VEL0, "mdbc_threshold": 0.0,
+                     "rheology": SPH_RHEOLOGY_SINGLE, "velgrad": SPH_VELGRAD_FDA, "tvisco": SPH_VISCO_ARTIFICIAL,
+                     "nphases": 0, "relaxation_dt": 0.2, "shift_mode": SPH_SHIFT_NONE, "pad_shift": 0,
+                     "shift_coef": -2.0, "shift_tfs": 0.0, "phases": (),
+                     "data2d": 0, "pad2d": 0, "data2d_posy": 0.0}
+
+
+class SphPhaseDef(C.Structure):
+    """One <nnphases><phase> (JSph::InitMultiPhase, JSph.cpp:3137-3215)."""
+    _fields_ = [
+        ("mkfluid", C.c_int32),
+        ("phasetype", C.c_int32),
+        ("rho", C.c_double),
+        ("cs0", C.c_double),
+        ("gamma", C.c_double),
+        ("visco", C.c_double),
+        ("tau_yield", C.c_double),
+        ("tau_max", C.c_double),
+        ("bi_multi", C.c_double),
+        ("hbp_m", C.c_double),
+        ("hbp_n", C.c_double),
+    ]
 
 
 class SphCaseDef(C.Structure):
@@ -57,6 +83,19 @@ class SphCaseDef(C.Structure):
         ("tboundary", C.c_int32),
         ("slipmode", C.c_int32),
         ("mdbc_threshold", C.c_double),
+        ("rheology", C.c_int32),
+        ("velgrad", C.c_int32),
+        ("tvisco", C.c_int32),
+        ("nphases", C.c_uint32),
+        ("relaxation_dt", C.c_double),
+        ("shift_mode", C.c_int32),
+        ("pad_shift", C.c_int32),
+        ("shift_coef", C.c_double),
+        ("shift_tfs", C.c_double),
+        ("phases", SphPhaseDef * SPH_MAXPHASES),
+        ("data2d", C.c_int32),
+        ("pad2d", C.c_int32),
+        ("data2d_posy", C.c_double),
     ]
 
     @classmethod
@@ -67,6 +106,13 @@ class SphCaseDef(C.Structure):
                 v = _CASEDEF_DEFAULTS[name]
             else:
                 v = d[name]
+            if name == "phases":
+                if len(v) > SPH_MAXPHASES:
+                    raise ValueError("at most %d phases" % SPH_MAXPHASES)
+                for i, ph in enumerate(v):
+                    for k, x in ph.items():
+                        setattr(s.phases[i], k, x)
+                continue
             if isinstance(v, (tuple, list)):
                 arr = getattr(s, name)
                 for i, x in enumerate(v):
@@ -118,6 +164,18 @@ class SphConstants(C.Structure):
         ("slipmode", C.c_int32),
         ("mdbc_threshold", C.c_float),
         ("pad1", C.c_uint32),
+        ("rheology", C.c_int32),
+        ("velgrad", C.c_int32),
+        ("tvisco", C.c_int32),
+        ("shift_mode", C.c_int32),
+        ("nphases", C.c_uint32),
+        ("relaxation_dt", C.c_float),
+        ("shift_coef", C.c_float),
+        ("shift_tfs", C.c_float),
+        ("phase_mass", C.c_float * SPH_MAXPHASES),
+        ("phase_cteb", C.c_float * SPH_MAXPHASES),
+        ("data2d", C.c_int32),
+        ("pad3", C.c_int32),
     ]
 
     def as_dict(self) -> dict:
@@ -143,11 +201,11 @@ class SphRunStats(C.Structure):
         ("velmax", C.c_float),
         ("acemax", C.c_float),
         ("viscdtmax", C.c_float),
-        ("pad", C.c_float),
+        ("viscetadtmax", C.c_float),
     ]
 
     def as_dict(self) -> dict:
-        return {name: getattr(self, name) for name, _ in self._fields_ if name != "pad"}
+        return {name: getattr(self, name) for name, _ in self._fields_}
 
 
 class SphParticlesHost(C.Structure):

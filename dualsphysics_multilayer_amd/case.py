@@ -416,3 +416,133 @@ class WaveFlumeCase:
     def case_def(self) -> dict:
         d = DamBreakCase.case_def(self)
         return d
+
+
+# Example phases of examples/mphase_nnewtonian/01_WetDambreak/CaseWetDambreak2DNN_Def.xml:72-99
+NN_EXAMPLE_PHASES = (
+    dict(mkfluid=0, phasetype=0, rho=2000.0, cs0=0.0, gamma=0.0, visco=0.2, tau_yield=0.0001, tau_max=0.0,
+         bi_multi=0.0, hbp_m=100.0, hbp_n=1.5),
+    dict(mkfluid=1, phasetype=0, rho=1500.0, cs0=0.0, gamma=0.0, visco=0.1, tau_yield=0.001, tau_max=0.0,
+         bi_multi=0.0, hbp_m=10.0, hbp_n=1.0),
+    dict(mkfluid=2, phasetype=0, rho=1000.0, cs0=0.0, gamma=0.0, visco=0.05, tau_yield=0.0005, tau_max=0.0,
+         bi_multi=0.0, hbp_m=0.0, hbp_n=1.0),
+)
+
+
+@dataclass
+class WetDambreakNNCase:
+    """Three-phase non-Newtonian wet dam break (BASELINE cfg5): the
+    2-D reference example CaseWetDambreak2DNN_Def.xml extruded along y, as
+    oracle/tools/gennn_ref writes it for the v5.0 NN solver (tests/test_nn.py checks the two
+    agree bit for bit).
+
+    Lattice (i, j, k)*dp; lengths scale with `scale` except the 0.04 m walls: tank x in
+    [0, 4s], z in [0, 1.25s], y in [0, width]; walls bottom, x = 0, x = 4s, y = 0, y = width;
+    phases drawn in the example's order (later replaces earlier, walls last): mkfluid 0
+    x <= 4s, z <= 0.5s; mkfluid 1 x <= 1s, 0.5s <= z <= 0.75s; mkfluid 2 x <= 0.5s,
+    0.75s <= z <= 1s.  Boundary first, then the phases, each in k, j, i order.  Constants:
+    cs0 = 20 (speedsystem 1 x coefsound 20), b = cs0^2 rho0/gamma, h = 0.91924 sqrt(3) dp,
+    Symplectic, Wendland, RheologyTreatment 2, FDA gradients, Laminar viscosity, DDT 3 (0.1),
+    shifting Full (coef -10, TFS 2.75), CFL 0.1, RelaxationDt 0.2, RhopOut [500, 3000]."""
+
+    dp: float
+    width: float = 0.64
+    scale: float = 1.0
+    shift_tfs: float = 2.75
+    tvisco: int = 2
+    tdensity: int = DDT_DDT2FULL
+    shift_mode: int = 3
+    step_algorithm: int = STEP_SYMPLECTIC
+    ddtvalue: float = 0.1
+    visco: float = 0.05
+    viscoboundfactor: float = 1.0
+    cflnumber: float = 0.1
+    verlet_steps: int = 40
+    coefdtmin: float = 0.05
+    rhopoutmin: float = 500.0
+    rhopoutmax: float = 3000.0
+    relaxation_dt: float = 0.2
+    shift_coef: float = -10.0
+    cellmode: int = CELLMODE_FULL
+    celldomfixed: bool = False
+    gravity: tuple = (0.0, 0.0, -9.81)
+    rhop0: float = 1000.0
+    gamma: float = 7.0
+    coefh: float = 0.91924
+    tboundary: int = 1
+    slipmode: int = 1
+    mdbc_threshold: float = 0.0
+    phases: tuple = NN_EXAMPLE_PHASES
+    csound: float = 0.0  # > 0: phase k gets <csound> csound*(1+0.1k) (gennn_ref's option)
+    explicit_codes: bool = True  # the fluid codes carry the phase (fluid block index)
+
+    def __post_init__(self) -> None:
+        if self.csound > 0:
+            self.phases = tuple(dict(ph, cs0=float("%.10g" % (self.csound * (1.0 + 0.1 * k))))
+                                for k, ph in enumerate(self.phases))
+        dp, s = self.dp, self.scale
+        nx, nz, ny = _cround(4.0 * s / dp), _cround(1.25 * s / dp), _cround(self.width / dp)
+        nw = _cround(0.04 / dp)
+        x0, z0 = _cround(4.0 * s / dp), _cround(0.5 * s / dp)
+        x1, z1b = _cround(1.0 * s / dp), _cround(0.75 * s / dp)
+        x2, z2b = _cround(0.5 * s / dp), _cround(1.0 * s / dp)
+        k, j, i = np.meshgrid(np.arange(nz + 1), np.arange(ny + 1), np.arange(nx + 1), indexing="ij")
+        k, j, i = k.ravel(), j.ravel(), i.ravel()
+        wall = (k <= nw) | (i <= nw) | (i >= nx - nw) | (j <= nw) | (j >= ny - nw)
+        ph = np.full(k.size, -1, np.int64)
+        ph[(i <= x0) & (k <= z0)] = 0
+        ph[(i <= x1) & (k >= z0) & (k <= z1b)] = 1
+        ph[(i <= x2) & (k >= z1b) & (k <= z2b)] = 2
+        ph[wall] = -1
+        sel = [wall] + [(~wall) & (ph == p) for p in range(3)]
+        self.nph = [int(m.sum()) for m in sel[1:]]
+        ii = np.concatenate([i[m] for m in sel]).astype(np.float64)
+        jj = np.concatenate([j[m] for m in sel]).astype(np.float64)
+        kk = np.concatenate([k[m] for m in sel]).astype(np.float64)
+        self.pos = np.stack([ii * dp, jj * dp, kk * dp], axis=1)
+        self.npb = int(wall.sum())
+        self.np = int(self.pos.shape[0])
+        self.idp = np.arange(self.np, dtype=np.uint32)
+        self.vel = np.zeros((self.np, 3), dtype=np.float32)
+        code = np.full(self.np, CODE_TYPE_FIXED, np.uint16)
+        rhop = np.full(self.np, np.float32(self.rhop0), np.float32)
+        o = self.npb
+        for p, n in enumerate(self.nph):
+            code[o:o + n] = CODE_TYPE_FLUID | p
+            rhop[o:o + n] = np.float32(self.phases[p]["rho"])
+            o += n
+        self._code = code
+        self.rhop = rhop
+        cs0 = 20.0 * 1.0
+        self._h = self.coefh * math.sqrt(3.0 * dp * dp)
+        self._b = cs0 * cs0 * self.rhop0 / self.gamma
+        self._mass = self.rhop0 * dp * dp * dp
+
+    @property
+    def code(self) -> np.ndarray:
+        return self._code
+
+    @property
+    def nf(self) -> int:
+        return self.np - self.npb
+
+    @property
+    def boundnormal(self):
+        return None
+
+    h = DamBreakCase.h
+    cteb = DamBreakCase.cteb
+    mass = DamBreakCase.mass
+    map_limits = DamBreakCase.map_limits
+
+    def case_def(self) -> dict:
+        d = DamBreakCase.case_def(self)
+        d.update(rheology=2, velgrad=1, tvisco=self.tvisco, nphases=len(self.phases), phases=self.phases,
+                 relaxation_dt=self.relaxation_dt, shift_mode=self.shift_mode, shift_coef=self.shift_coef,
+                 shift_tfs=self.shift_tfs)
+        return d
+
+
+def wetdambreak_nn_np(dp: float, width: float = 0.64, scale: float = 1.0) -> int:
+    """Particle count of the NN wet dam break (lattice sizes only)."""
+    return WetDambreakNNCase(dp, width=width, scale=scale).np

@@ -158,7 +158,7 @@ def case_derive(case_def: dict) -> dict:
 def case_particles(case) -> HostParticles:
     """Initial particles of a case; the particle codes travel only when the case has moving or
     floating blocks (else the core assigns one fixed + one fluid block, JSph::LoadCodeParticles)."""
-    bodies = getattr(case, "has_bodies", False)
+    bodies = getattr(case, "has_bodies", False) or getattr(case, "explicit_codes", False)
     hp = HostParticles(case.np, case.idp, case.pos, case.vel, case.rhop, code=case.code if bodies else None,
                        boundnormal=getattr(case, "boundnormal", None))
     if not bodies:

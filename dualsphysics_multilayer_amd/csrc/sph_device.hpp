@@ -65,7 +65,23 @@ struct KConst {
   float awen;  // Wendland W normalisation (mDBC)
   int mdbc;    // TBoundary == BC_MDBC: DDT (Molteni) keeps bound neighbours (JSphCpu.cpp:730)
   int scelldiv;  // 1 CellMode=full (cells of 2h), 2 half (cells of h): neighbour rows +-scelldiv
+  // v5.0 NN multiphase (sph_nn.hip) and shifting (JSphShifting::RunCpu, JSphShifting.cpp:388-418)
+  int nn;          // RheologyTreatment == 2
+  int nntvisco;    // TpVisco of the NN interaction: 1 artificial, 2 laminar, 3 constitutive eq.
+  int shiftmode;   // TpShifting: 0 none, 1 NoBound, 2 NoFixed, 3 Full
+  int sim2d;       // Simulate2D: ace.y = 0 after the interaction
+  float lamda;     // RelaxationDt of the viscous dt (JSphCpu.cpp:1687)
+  float shifttfs;  // ShiftTFS (0: no free-surface detection)
+  float shiftmaxdist;   // float(Dp*0.1)
+  float shiftcoef;      // ShiftCoef
+  double coeftfs;       // (Simulate2D ? 2 : 3) - ShiftTFS
 };
+
+// NN phase constants on the device, two float4 per phase (sph_nn.hip loads them to LDS):
+//   [2k]   = {mass, cs0, visco, tau_yield}
+//   [2k+1] = {HBP_m, HBP_n, tau_max, Bi_multi}
+// and the EOS of each phase for the divide's press: {rho0, 1/rho0, cteb, gamma}.
+constexpr int NN_MAXPH = 8;
 
 // Cell grid of the (fixed) divide domain — StDivDataGpu (JCellDivDataGpu.h:26-79).
 // Slab decomposition (sph_slab.hip): a rank's grid covers the global x-columns
@@ -98,12 +114,13 @@ struct DevScalars {
   double ddt_p;     // predictor dt (Symplectic)
   double last_dt;
   double tstep0;    // TimeStep at the start of the step in flight (motion, FtPause)
-  float last_velmax, last_acemax, last_viscdt, pad3;
+  float last_velmax, last_acemax, last_viscdt, last_visceta;
   // Max-reductions (float bits of values >= 0) spread over RED_SLOTS slots so that
   // thousands of waves do not serialise on one address; k_dt folds and clears them.
-  unsigned red[3][64];
+  unsigned red[4][64];
 };
-constexpr int RED_VELMAX2 = 0, RED_ACEMAX2 = 1, RED_VISCDT = 2, RED_SLOTS = 64;
+// RED_VISCETA: NN max effective viscosity (ViscEtaDtMax, JSphCpuSingle.cpp:633 in the v5.0 solver)
+constexpr int RED_VELMAX2 = 0, RED_ACEMAX2 = 1, RED_VISCDT = 2, RED_VISCETA = 3, RED_SLOTS = 64;
 
 constexpr unsigned ERR_DT_NAN = 1u, ERR_BOUNDOUT = 2u, ERR_HALO = 4u;
 

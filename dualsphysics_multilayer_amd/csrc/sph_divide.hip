@@ -308,6 +308,8 @@ struct GatherArgs {
   unsigned dcc;
   int withm1, withpre;
   int xoff;
+  // NN multiphase: per-phase EOS {rho0, cteb, gamma, integer gamma or 0} (nullptr: single phase)
+  const float4* phase_eos;
 };
 
 // WITHM1 / WITHPRE are template parameters so every load of a particle is issued before
@@ -363,19 +365,36 @@ __device__ __forceinline__ void gather_one(const GatherArgs& a, unsigned i, unsi
   // double pow, and -ffast-math makes rhop/rhop0 a product with 1/rhop0.  For an
   // integer gamma the double power is formed by squaring (<= 4 roundings at 1e-16,
   // far below the float rounding of the result).
-  const double xr = double(vr.w * a.ovrhopzero);
-  double xg;
-  if (a.igamma > 0) {  // integer gamma (7 in every case here): exact squaring in double
-    double r = 1.0, b = xr;
-    for (int e = a.igamma; e; e >>= 1) {
-      if (e & 1) r *= b;
-      b *= b;
+  auto powg = [](double x, int ig, double g) -> double {
+    if (ig > 0) {  // integer gamma (7 in every case here): exact squaring in double
+      double r = 1.0, b = x;
+      for (int e = ig; e; e >>= 1) {
+        if (e & 1) r *= b;
+        b *= b;
+      }
+      return r;
     }
-    xg = r;
+    return pow(x, g);
+  };
+  if (a.phase_eos) {
+    // ComputePress_NN (JSphCpu_Tensors.cpp:40-62 of the v5.0 solver): the phase's rho0, CteB
+    // and gamma for fluid particles, the case's for the boundary, in float arithmetic
+    // (cteb*(powf(rhop/rho0,gamma)-1)); the power is rounded once from double.
+    float rho0 = 1.f / a.ovrhopzero, cteb = a.cteb, gam = a.gamma;
+    int ig = a.igamma;
+    if (CodeIsFluid(code)) {
+      const float4 e = a.phase_eos[code & CODE_MASKVALUE];
+      rho0 = e.x;
+      cteb = e.y;
+      gam = e.z;
+      ig = int(e.w);
+    }
+    const float r = vr.w / rho0;
+    a.press[i] = cteb * (float(powg(double(r), ig, double(gam))) - 1.0f);
   } else {
-    xg = pow(xr, double(a.gamma));
+    const double xr = double(vr.w * a.ovrhopzero);
+    a.press[i] = float(double(a.cteb) * (powg(xr, a.igamma, double(a.gamma)) - 1.0));
   }
-  a.press[i] = float(double(a.cteb) * (xg - 1.0));
   vr_out = vr;
   fluid = i >= npb;
 }
@@ -403,8 +422,9 @@ __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, Gat
 
 void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned* sortpart, const PartArrays& src,
                    const PartArrays& dst, bool withm1, bool withpre, const KConst& K, const double dom_posmin[3],
-                   float4* poscell, float* press, int xoff) {
+                   float4* poscell, float* press, int xoff, const float4* phase_eos) {
   GatherArgs a;
+  a.phase_eos = phase_eos;
   a.xoff = xoff;
   a.src = src;
   a.dst = dst;

@@ -204,6 +204,7 @@ __global__ __launch_bounds__(256) void k_interaction(DevScalars* __restrict__ sc
         az += b.az;
       }
       if (TDENSITY && delta != FLT_MAX) ar += delta;  // JSphCpuSingle.cpp:553-559
+      if (K.sim2d) ay = 0.f;  // Simulate2D: Acec[].y = 0 (JSphCpuSingle.cpp:544-549)
       arace[p1] = make_float4(ax, ay, az, ar);
       viscmax = fmaxf(f.visc, b.visc);
       ace2 = ax * ax + ay * ay + az * az;  // ComputeAceMaxOmp (JSphCpuSingle.cpp:612-644)

@@ -58,6 +58,26 @@ __device__ __forceinline__ void update_pos_bound(const KConst& K, double rx, dou
   update_pos(K, rx, ry, rz, movx, movy, movz, false, p, a);
 }
 
+// JSphShifting::RunCpu (JSphShifting.cpp:388-418) for one fluid particle, added to its
+// displacement as ComputeSymplecticCorr / ComputeVerletVarsFluid do: rs = the interaction's
+// shifting sums (x = FLT_MAX: cancelled next to the boundary), v = the velocity RunShifting
+// reads, dt = the step's dt.
+__device__ __forceinline__ void shift_displacement(const KConst& K, float4 rs, float4 v, double dt, double& dx,
+                                                   double& dy, double& dz) {
+  if (rs.x == 3.402823466e+38f) return;
+  const double coefumagn = dt * double(K.shiftcoef) * double(K.kernelh);
+  const double vx = double(v.x), vy = double(v.y), vz = double(v.z);
+  double umagn = coefumagn * sqrt(vx * vx + vy * vy + vz * vz);
+  if (K.shifttfs != 0.f) {
+    if (rs.w < K.shifttfs) umagn = 0;
+    else umagn *= (double(rs.w) - double(K.shifttfs)) / K.coeftfs;
+  }
+  const float sx = float(double(rs.x) * umagn), sy = float(double(rs.y) * umagn), sz = float(double(rs.z) * umagn);
+  dx += double(sx < K.shiftmaxdist ? sx : K.shiftmaxdist);
+  dy += double(sy < K.shiftmaxdist ? sy : K.shiftmaxdist);
+  dz += double(sz < K.shiftmaxdist ? sz : K.shiftmaxdist);
+}
+
 // Scratch of the cell sort (DivideGpu).
 struct SortScratch {
   unsigned* keys[2] = {nullptr, nullptr};
@@ -87,7 +107,7 @@ void launch_begincell(hipStream_t stm, unsigned cap, DevScalars* sc, const unsig
 // JSphGpuSimple_ker.cu:41-69; PreInteraction press/VelMax, JSphGpu.cpp:831-870).
 void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned* sortpart, const PartArrays& src,
                    const PartArrays& dst, bool withm1, bool withpre, const KConst& K, const double dom_posmin[3],
-                   float4* poscell, float* press, int xoff);
+                   float4* poscell, float* press, int xoff, const float4* phase_eos = nullptr);
 
 // ---- interaction (cusph::Interaction_Forces, JSphGpu_ker.cu:788-885) ----
 // With floating bodies (ftmassp != nullptr: particle mass per body, `code` of the
@@ -130,6 +150,13 @@ void launch_mdbc_face_pack(hipStream_t stm, unsigned npbcap, const DevScalars* s
 void launch_mdbc_face_apply(hipStream_t stm, DevScalars* sc, const MdbcFaceRec* rl, const MdbcFaceRec* rr,
                             unsigned cap, const unsigned* bidx, unsigned nbidx, const unsigned* idp, float4* velrhop,
                             float* press);
+// NN multiphase interaction (sph_nn.hip; JSphCpu_NN_FDA.cpp of the v5.0 solver): all items
+// (fluid and bound p1) of the tiled item list; phases = the device phase table (2 float4
+// per phase, sph_device.hpp); shiftpos written when `shift` (the corrector's interaction).
+void launch_nn_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
+                     const float4* poscell, const float4* velrhop, const float* press, const typecode* code,
+                     const unsigned* begincell, DivGrid g, const KConst& K, const float4* phases, float4* arace,
+                     float4* shiftpos, bool shift);
 // Pair counters (JDsPips).
 void launch_count_pairs(hipStream_t stm, unsigned cap, const DevScalars* sc, const float4* poscell,
                         const unsigned* begincell, DivGrid g, const KConst& K, unsigned long long* out6);
@@ -140,15 +167,18 @@ enum DtMode { DT_VERLET = 0, DT_SYM_PRE = 1, DT_SYM_COR = 2, DT_PEEK = 3 };
 // (launch_fold_maxima + SlabTransport::allreduce_max_u32); nullptr = fold the slots here.
 void launch_dt(hipStream_t stm, DevScalars* sc, const KConst& K, double cfl, double dtmin, double cs0, int mode,
                double* dttrace, unsigned tracecap, const unsigned* folded = nullptr);
-void launch_fold_maxima(hipStream_t stm, DevScalars* sc, unsigned* folded3, bool clear);
+// folded[4]: VelMax^2, AceMax^2, ViscDtMax, ViscEtaDtMax
+void launch_fold_maxima(hipStream_t stm, DevScalars* sc, unsigned* folded, bool clear);
 // Update kernels skip slab ghosts (local column outside [g.xown0, g.xown1)) and mark
 // them DCELL_DISCARD for the next divide.
+// shiftpos (nullptr: no shifting): the interaction's shifting sums, turned into the
+// displacement of JSphShifting::RunCpu inside the update.
 void launch_verlet(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, bool euler, const float4* arace,
-                   PartArrays a, DivGrid g);
+                   PartArrays a, DivGrid g, const float4* shiftpos = nullptr);
 void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
                     DivGrid g);
 void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
-                    DivGrid g);
+                    DivGrid g, const float4* shiftpos = nullptr);
 
 // ---- moving boundaries and floating bodies (sph_bodies.hip) ----
 constexpr int MOT_MAXOBJ = 32, MOT_MAXACT = 4;

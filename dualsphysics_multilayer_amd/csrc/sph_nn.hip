@@ -1,0 +1,404 @@
+// sph_nn.hip — non-Newtonian multiphase Interaction_Forces (the v5.0 NNewtonian solver,
+// SURVEY.md §8(f) row 4) as an LDS-tiled CDNA4 kernel.
+//
+// Reference: JSphCpu::InteractionForcesFluid_NN_FDA_All / InteractionForcesBound_NN_FDA
+// (src_mphase/DSPH_v5.0_NNewtonian/source/JSphCpu_NN_FDA.cpp:45-332), the tensor helpers
+// GetVelocityGradients_FDA / GetStrainRateTensor / GetEta_Effective / GetStressTensor
+// (JSphCpu_Tensors.cpp:40-139), GPU twin KerInteractionForcesFluid_NN_FDA
+// (JSphGpu_NN_ker.cu:421-1555).  Per fluid p1 and pair: per-phase mass and sound speed of
+// p2, momentum, continuity, DDT (only between particles of the same phase), multiphase
+// shifting sums, and the viscous term with the effective viscosity of the Herschel-
+// Bulkley-Papanastasiou law evaluated from the pair's FDA velocity gradient
+// (Laminar: Morris operator; ConstEq: the stress tensor 2 eta D).
+//
+// Work decomposition: the items and LDS staging of sph_interaction_tiled.hip (sph_tiled.hpp),
+// with one difference that parity needs: the shifting x sum of the reference is RESET by
+// every pair with a heavier-phase neighbour (`heavyphase ? 0 : x + ...`,
+// JSphCpu_NN_FDA.cpp:206), so its value depends on the pair order.  The reference visits
+// the 3x3 rows z-major, y, then p2 ascending in the row — i.e. p2 in ascending cell-sorted
+// index.  Here every lane drains its candidates row by row in that same order (no mirrored
+// row pairs) and pops its candidate bits from low to high, one pair per iteration: every
+// p1 accumulates its pairs in exactly the reference's order.
+#include "sph_tiled.hpp"
+
+namespace sphx {
+
+// Phase table in LDS: two float4 per phase.
+//   a = {mass, cs0, visco, tau_yield}, b = {m (HBP_m), n (HBP_n), tau_max, bi_multi}
+struct NNAcc {
+  float ax, ay, az, ar, delta, visc, visceta;
+  float sx, sy, sz, sw;  // shifting sums (shiftposfsp1)
+};
+
+struct NNP1 {
+  float x, y, z;   // item-relative position
+  float4 vr;       // velocity, rho
+  float press;
+  int ph;          // phase of p1
+};
+
+// GetEta_Effective (JSphCpu_Tensors.cpp:84-108): Herschel-Bulkley-Papanastasiou effective
+// viscosity with the optional bi-viscosity region of p1's phase (tau_max, Bi_multi).
+__device__ __forceinline__ float nn_eta(float dmag, float tau_yield, float visco, float m, float n, float taumax1,
+                                        float bimulti1) {
+  if (dmag <= ALMOSTZERO) dmag = ALMOSTZERO;
+  float miou_yield = (taumax1 != 0.f ? taumax1 : tau_yield) * frcp(2.f * dmag);
+  const bool bi_region = taumax1 != 0.f && dmag <= taumax1 * frcp(2.f * bimulti1 * visco);
+  if (bi_region) miou_yield = bimulti1 * visco;
+  const float miou_pap = miou_yield * (1.f - fexp2(-m * dmag * 1.4426950408889634f));  // exp(-m D)
+  const bool cap = (miou_pap > m * tau_yield || dmag == ALMOSTZERO);
+  const float term1 = (taumax1 != 0.f ? miou_yield : (cap ? m * tau_yield : miou_pap));
+  const float miou_hb = visco * fexp2((n - 1.f) * flog2(dmag));  // visco * D^(n-1)
+  const float term2 = (bi_region ? visco : (cap ? visco : miou_hb));
+  return term1 + term2;
+}
+
+// One pair of the fluid p1 (InteractionForcesFluid_NN_FDA_All, JSphCpu_NN_FDA.cpp:141-275).
+// BOUNDP2: p2 is a boundary particle (mass MassBound, phase = p1's phase).
+template <int TVISCO, int TDENSITY, bool SHIFT, bool BOUNDP2>
+__device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restrict__ sph, const NNP1& p, float drx,
+                                        float dry, float drz, float rr2, const float4& B, const float2& C, NNAcc& a) {
+  // kernel (Wendland fac = bwen q (1-q/2)^3 / r = (bwen/h) (1-q/2)^3)
+  const float rad = fsqrt_(rr2);
+  const float wq = fmaf(K.mhalfovh, rad, 1.f);
+  const float fac = K.bwenovh * (wq * wq * wq);
+  const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
+  const int pp2 = BOUNDP2 ? p.ph : int(__float_as_uint(C.y));
+  const float4 ph2 = sph[2 * pp2];
+  const float massp2 = BOUNDP2 ? K.massbound : ph2.x;
+  const float rho1 = p.vr.w, rho2 = B.w;
+  const float inv_rho2 = frcp(rho2);
+  // momentum (pressure)
+  {
+    const float prs = (p.press + C.x) * frcp(rho1 * rho2);
+    const float p_vpm = -prs * massp2;
+    a.ax = fmaf(p_vpm, frx, a.ax);
+    a.ay = fmaf(p_vpm, fry, a.ay);
+    a.az = fmaf(p_vpm, frz, a.az);
+  }
+  // continuity
+  const float rhop1over2 = rho1 * inv_rho2;
+  float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
+  a.ar = fmaf(massp2 * (dvx * frx + dvy * fry + dvz * frz), rhop1over2, a.ar);
+  const float cbar = ph2.y;  // max(Cs0[pp2], Cs0[pp2])
+  const float dot3 = fac * rr2;  // drx*frx+dry*fry+drz*frz
+  const float inv_re = frcp(rr2 + K.eta2);
+  // density diffusion, only between particles of the same phase (JSphCpu_NN_FDA.cpp:181-199)
+  if (TDENSITY == 1 && a.delta != FLT_MAX) {
+    const float visc_densi = K.ddtkh * cbar * (rhop1over2 - 1.f) * inv_re;
+    const float delta = (p.ph == pp2 ? visc_densi * dot3 * massp2 : 0.f);
+    a.delta = (BOUNDP2 && !K.mdbc) ? FLT_MAX : a.delta + delta;
+  }
+  if ((TDENSITY == 2 || (TDENSITY == 3 && !BOUNDP2)) && a.delta != FLT_MAX) {
+    const float rh = 1.f + K.ddtgz * drz;
+    const float drhop = K.rhopzero * fexp2(K.ovgamma * flog2(rh)) - K.rhopzero;
+    const float visc_densi = K.ddtkh * cbar * ((rho2 - rho1) - drhop) * inv_re;
+    const float delta = (p.ph == pp2 ? visc_densi * dot3 * massp2 * inv_rho2 : 0.f);
+    a.delta = BOUNDP2 ? FLT_MAX : a.delta - delta;
+  }
+  // multiphase shifting (JSphCpu_NN_FDA.cpp:202-209): a heavier-phase neighbour resets x
+  if (SHIFT && a.sx != FLT_MAX) {
+    const bool heavy = !BOUNDP2 && (sph[2 * p.ph].x > ph2.x) && p.ph != pp2;
+    const float massrhop = massp2 * inv_rho2;
+    const bool noshift = BOUNDP2 && (K.shiftmode == 1 || (K.shiftmode == 2 && C.y != 0.f));
+    a.sx = noshift ? FLT_MAX : (heavy ? 0.f : a.sx + massrhop * frx);
+    a.sy += heavy ? 0.f : massrhop * fry;
+    a.sz += heavy ? 0.f : massrhop * frz;
+    a.sw -= heavy ? 0.f : massrhop * dot3;
+  }
+  // viscosity
+  const float dot = drx * dvx + dry * dvy + drz * dvz;
+  const float dot_rr2 = dot * inv_re;
+  a.visc = fmaxf(dot_rr2, a.visc);
+  const float visco_nn = ph2.z;
+  if (TVISCO == 1) {  // artificial
+    if (dot < 0.f) {
+      const float amubar = K.kernelh * dot_rr2;
+      const float robar = (rho1 + rho2) * 0.5f;
+      const float pi_visc = (-visco_nn * cbar * amubar * frcp(robar)) * massp2;
+      a.ax = fmaf(-pi_visc, frx, a.ax);
+      a.ay = fmaf(-pi_visc, fry, a.ay);
+      a.az = fmaf(-pi_visc, frz, a.az);
+    }
+  } else {  // Laminar (2) or constitutive equation (3) with the FDA velocity gradient
+    if (BOUNDP2) {  // no slip on the tensor: u_g = 2 u_b - u_f with u_b = 0
+      dvx = 2.f * p.vr.x;
+      dvy = 2.f * p.vr.y;
+      dvz = 2.f * p.vr.z;
+    }
+    // GetVelocityGradients_FDA + GetStrainRateTensor (JSphCpu_Tensors.cpp:40-82)
+    const float irr2 = frcp(rr2);
+    const float a11 = dvx * drx * irr2, a12 = dvx * dry * irr2, a13 = dvx * drz * irr2;
+    const float a21 = dvy * drx * irr2, a22 = dvy * dry * irr2, a23 = dvy * drz * irr2;
+    const float a31 = dvz * drx * irr2, a32 = dvz * dry * irr2, a33 = dvz * drz * irr2;
+    const float div_vel = (a11 + a22 + a33) * (1.f / 3.f);
+    const float d11 = a11 - div_vel, d22 = a22 - div_vel, d33 = a33 - div_vel;
+    const float d12 = 0.5f * (a12 + a21), d13 = 0.5f * (a13 + a31), d23 = 0.5f * (a23 + a32);
+    const float ii1 = d11 * d22 + d22 * d33 + d11 * d33;
+    const float ii2 = d12 * d12 + d23 * d23 + d13 * d13;
+    const float ii_d = ii1 - ii2;
+    const float dmag = fabsf(ii_d);  // sqrt(II_D * II_D)
+    const float4 ph2b = sph[2 * pp2 + 1];
+    const float4 ph1b = sph[2 * p.ph + 1];
+    const float eta = nn_eta(dmag, ph2.w, visco_nn, ph2b.x, ph2b.y, ph1b.z, ph1b.w);
+    a.visceta = fmaxf(eta, a.visceta);
+    if (TVISCO == 2) {  // Morris operator
+      const float temp = 2.f * eta * frcp((rr2 + K.eta2) * rho2);
+      const float vtemp = massp2 * temp * dot3;
+      a.ax = fmaf(vtemp, dvx, a.ax);
+      a.ay = fmaf(vtemp, dvy, a.ay);
+      a.az = fmaf(vtemp, dvz, a.az);
+    } else {  // GetStressTensor: tau = 2 eta D
+      const float e2 = 2.f * eta;
+      const float t11 = e2 * d11, t12 = e2 * d12, t13 = e2 * d13, t22 = e2 * d22, t23 = e2 * d23, t33 = e2 * d33;
+      a.ax = fmaf((t11 * frx + t12 * fry + t13 * frz) * inv_rho2, massp2, a.ax);
+      a.ay = fmaf((t12 * frx + t22 * fry + t23 * frz) * inv_rho2, massp2, a.ay);
+      a.az = fmaf((t13 * frx + t23 * fry + t33 * frz) * inv_rho2, massp2, a.az);
+    }
+  }
+}
+
+// Boundary p1 over fluid p2 (InteractionForcesBound_NN_FDA, JSphCpu_NN_FDA.cpp:48-113):
+// continuity with MassFluid and the visc-dt maximum.
+__device__ __forceinline__ void nn_bound_pair(const KConst& K, const NNP1& p, float drx, float dry, float drz,
+                                              float rr2, const float4& B, NNAcc& a) {
+  const float rad = fsqrt_(rr2);
+  const float wq = fmaf(K.mhalfovh, rad, 1.f);
+  const float fac = K.bwenovh * (wq * wq * wq);
+  const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
+  const float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
+  a.ar = fmaf(K.massfluid * (dvx * frx + dvy * fry + dvz * frz), p.vr.w * frcp(B.w), a.ar);
+  const float dot = drx * dvx + dry * dvy + drz * dvz;
+  a.visc = fmaxf(dot * frcp(rr2 + K.eta2), a.visc);
+}
+
+// Staging of one row segment: positions relative to the item (sA + |A|^2), velrhop (sB),
+// {press, tag} (sC): tag = phase index (fluid rows) or 1 for a fixed boundary particle.
+__device__ __forceinline__ void nn_stage(const KConst& K, unsigned rs, unsigned n, int xo, int dy, int dz,
+                                         bool boundrow, const float4* __restrict__ poscell,
+                                         const float4* __restrict__ velrhop, const float* __restrict__ press,
+                                         const typecode* __restrict__ code, float4* __restrict__ sA,
+                                         float4* __restrict__ sB, float2* __restrict__ sC) {
+  const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
+  for (unsigned i = threadIdx.x; i < n; i += TB) {
+    const float4 pc = poscell[rs + i];
+    const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
+    const float x2 = pc.x + float(cx2 - xo) * K.scell;
+    const float y2 = pc.y + oy, z2 = pc.z + oz;
+    sA[i] = make_float4(x2, y2, z2, x2 * x2 + y2 * y2 + z2 * z2);
+    sB[i] = velrhop[rs + i];
+    const typecode c = code[rs + i];
+    const unsigned tag = boundrow ? (CodeType(c) == 0 ? 1u : 0u) : unsigned(c & CODE_MASKVALUE);
+    sC[i] = make_float2(press[rs + i], boundrow ? float(tag) : __uint_as_float(tag));
+  }
+}
+
+// One pass of a p1 over its 9 rows of one kind, z-major then y, p2 ascending.
+// KIND 0: fluid p1 / fluid p2, 1: fluid p1 / bound p2, 2: bound p1 / fluid p2.
+template <int TVISCO, int TDENSITY, bool SHIFT, int KIND>
+__device__ __forceinline__ void nn_pass(const KConst& K, const DivGrid& g, const RowCtx& rc, const NNP1& p, float thr,
+                                        const unsigned* __restrict__ bc, const float4* __restrict__ poscell,
+                                        const float4* __restrict__ velrhop, const float* __restrict__ press,
+                                        const typecode* __restrict__ code, float4* __restrict__ sA,
+                                        float4* __restrict__ sB, float2* __restrict__ sC,
+                                        const float4* __restrict__ sph, NNAcc& a) {
+  const unsigned cellinit = (KIND == 1 ? 0u : g.boxfluid);
+  const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
+  for (int dz = -1; dz <= 1; dz++) {
+    for (int dy = -1; dy <= 1; dy++) {
+      const int z = rc.cz + dz, y = rc.cy + dy;
+      if (z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;  // block-uniform
+      const unsigned rowbase = cellinit + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+      const unsigned rs = bc[rowbase + rc.xa], re = bc[rowbase + rc.xb + 1];
+      const unsigned ls = bc[rowbase + rc.lxa], le = bc[rowbase + rc.lxb + 1];
+      for (unsigned seg = rs; seg < re; seg += TCAP) {
+        const unsigned segn = min(unsigned(TCAP), re - seg);
+        __syncthreads();
+        nn_stage(K, seg, segn, rc.xo, dy, dz, KIND == 1, poscell, velrhop, press, code, sA, sB, sC);
+        __syncthreads();
+        const int w0 = int(max(ls, seg) - seg);
+        const int w1 = rc.act ? max(w0, int(min(le, seg + segn)) - int(seg)) : w0;
+        for (int off = w0; off < w1; off += 128) {
+          unsigned long long c0, c1;
+          test128(sA, off, min(w1 - off, 128), px2, py2, pz2, thr, c0, c1);
+          int b0 = off;
+          if (!c0) {
+            c0 = c1;
+            c1 = 0ull;
+            b0 += 64;
+          }
+          while (c0) {  // ascending p2
+            const int j = b0 + int(__builtin_ctzll(c0));
+            c0 &= c0 - 1ull;
+            if (!c0 && c1) {
+              c0 = c1;
+              c1 = 0ull;
+              b0 += 64;
+            }
+            const float4 A = sA[j];
+            const float drx = p.x - A.x, dry = p.y - A.y, drz = p.z - A.z;
+            const float rr2 = drx * drx + dry * dry + drz * drz;
+            if (!(rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO)) continue;
+            const float4 B = sB[j];
+            if (KIND == 2) nn_bound_pair(K, p, drx, dry, drz, rr2, B, a);
+            else nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1>(K, sph, p, drx, dry, drz, rr2, B, sC[j], a);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int TVISCO, int TDENSITY, bool SHIFT>
+__global__ __launch_bounds__(TB) void k_nn_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
+                                                 unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
+                                                 const float4* __restrict__ velrhop, const float* __restrict__ press,
+                                                 const typecode* __restrict__ code, const unsigned* __restrict__ bc,
+                                                 DivGrid g, KConst K, const float4* __restrict__ phases,
+                                                 float4* __restrict__ arace, float4* __restrict__ shiftpos) {
+  __shared__ float4 sA[TCAP + SPH_PAD];
+  __shared__ float4 sB[TCAP];
+  __shared__ float2 sC[TCAP];
+  __shared__ float4 sph[2 * SPH_MAXPHASES];
+  __shared__ unsigned s_item;
+  __shared__ unsigned char s_perm[TB];
+  __shared__ unsigned s_nwave[4];
+  if (threadIdx.x < 2 * SPH_MAXPHASES) sph[threadIdx.x] = phases[threadIdx.x];
+  const unsigned nitems = sc->nitems;
+  const unsigned per = (nitems + 7) / 8;
+  const unsigned grp = blockIdx.x & 7;
+  float viscmax = 0.f, ace2max = 0.f, etamax = 0.f;
+  for (unsigned q = 0; q < 8; q++) {
+    const unsigned xg = (grp + q) & 7;
+    const unsigned lo = xg * per, hi = min(nitems, lo + per);
+    for (;;) {
+      if (threadIdx.x == 0) s_item = lo + atomicAdd(&qctr[xg], 1u);
+      __syncthreads();
+      const unsigned it = s_item;
+      __syncthreads();
+      if (it >= hi) break;
+      const uint4 item = items[it];
+      const bool bitem = (item.x & ITEM_BOUND) != 0u;
+      const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
+      const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);
+      const int xo = (ia + ib + 1) >> 1;
+      const int xa = max(ia - 1, 0), xb = min(ib + 1, g.ncx - 1);
+      if (bitem) {  // no fluid within reach: ar = 0 (PreInteraction reset), nothing else
+        bool any = false;
+        for (int z = max(cz - 1, 0); z <= min(cz + 1, g.ncz - 1); z++)
+          for (int y = max(cy - 1, 0); y <= min(cy + 1, g.ncy - 1); y++) {
+            const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+            any |= bc[rowbase + xa] != bc[rowbase + xb + 1];
+          }
+        if (!any) {
+          for (unsigned p1 = item.z + threadIdx.x; p1 < item.w; p1 += TB) arace[p1] = make_float4(0.f, 0.f, 0.f, 0.f);
+          continue;
+        }
+      }
+      const unsigned p1 = item.z + lane_order(poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
+      const bool act = threadIdx.x < item.w - item.z;
+      NNP1 p;
+      int cx1 = ia;
+      if (act) {
+        const float4 pc1 = poscell[p1];
+        cx1 = int(DcelCellx(K.domcellcode, __float_as_uint(pc1.w)));
+        p.x = pc1.x + float(cx1 - xo) * K.scell;
+        p.y = pc1.y;
+        p.z = pc1.z;
+        p.vr = velrhop[p1];
+        p.press = press[p1];
+        p.ph = bitem ? 0 : int(code[p1] & CODE_MASKVALUE);
+      } else {
+        p.x = p.y = p.z = 1e30f;
+        p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
+        p.press = 0.f;
+        p.ph = 0;
+      }
+      const int lxa = max(cx1 - 1, 0), lxb = min(cx1 + 1, g.ncx - 1);
+      const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
+      const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act};
+      if (bitem) {
+        NNAcc f = {};
+        nn_pass<TVISCO, TDENSITY, SHIFT, 2>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f);
+        if (act) {
+          arace[p1] = make_float4(0.f, 0.f, 0.f, (f.ar != 0.f || f.visc != 0.f) ? 0.f + f.ar : 0.f);
+          viscmax = fmaxf(viscmax, f.visc);
+        }
+        continue;
+      }
+      // fluid p1: the fluid pass, then the bound pass; the shifting sums carry over
+      // (shiftposfs[p1] is stored by the first pass and loaded by the second)
+      NNAcc f = {}, b = {};
+      nn_pass<TVISCO, TDENSITY, SHIFT, 0>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f);
+      b.sx = f.sx;
+      b.sy = f.sy;
+      b.sz = f.sz;
+      b.sw = f.sw;
+      nn_pass<TVISCO, TDENSITY, SHIFT, 1>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, b);
+      if (act) {
+        // the two CPU passes' stores (JSphCpu_NN_FDA.cpp:278-296); with shifting both store
+        float ar = 0.f, ax = 0.f, ay = 0.f, az = 0.f, delta = 0.f;
+        if (SHIFT || f.ar != 0.f || f.ax != 0.f || f.ay != 0.f || f.az != 0.f || f.visc != 0.f) {
+          if (TDENSITY) delta = (f.delta == FLT_MAX ? FLT_MAX : 0.f + f.delta);
+          ar = f.ar;
+          ax = f.ax;
+          ay = f.ay;
+          az = f.az;
+        }
+        if (SHIFT || b.ar != 0.f || b.ax != 0.f || b.ay != 0.f || b.az != 0.f || b.visc != 0.f) {
+          if (TDENSITY) delta = (delta == FLT_MAX || b.delta == FLT_MAX ? FLT_MAX : delta + b.delta);
+          ar += b.ar;
+          ax += b.ax;
+          ay += b.ay;
+          az += b.az;
+        }
+        if (TDENSITY && delta != FLT_MAX) ar += delta;
+        if (K.sim2d) ay = 0.f;  // Simulate2D: Acec[].y = 0 (JSphCpuSingle.cpp:614-620)
+        arace[p1] = make_float4(ax, ay, az, ar);
+        if (SHIFT) shiftpos[p1] = make_float4(b.sx, b.sy, b.sz, b.sw);
+        viscmax = fmaxf(viscmax, fmaxf(f.visc, b.visc));
+        etamax = fmaxf(etamax, fmaxf(f.visceta, b.visceta));
+        ace2max = fmaxf(ace2max, ax * ax + ay * ay + az * az);
+      }
+    }
+  }
+  wave_max_atomic(sc, RED_VISCDT, viscmax);
+  wave_max_atomic(sc, RED_ACEMAX2, ace2max);
+  wave_max_atomic(sc, RED_VISCETA, etamax);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(&qctr[8], 1u) == gridDim.x - 1) {
+      for (int i = 0; i < 9; i++) atomicExch(&qctr[i], 0u);
+    }
+  }
+}
+
+void launch_nn_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
+                     const float4* poscell, const float4* velrhop, const float* press, const typecode* code,
+                     const unsigned* begincell, DivGrid g, const KConst& K, const float4* phases, float4* arace,
+                     float4* shiftpos, bool shift) {
+#define SPH_NN(TV, TD, SH)                                                                                       \
+  hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, \
+                     press, code, begincell, g, K, phases, arace, shiftpos)
+#define SPH_NN_TD(TV, SH)          \
+  switch (K.tdensity) {            \
+    case 0: SPH_NN(TV, 0, SH); break; \
+    case 1: SPH_NN(TV, 1, SH); break; \
+    case 2: SPH_NN(TV, 2, SH); break; \
+    default: SPH_NN(TV, 3, SH); break; \
+  }
+  if (shift) {
+    if (K.nntvisco == 1) SPH_NN_TD(1, true)
+    else if (K.nntvisco == 2) SPH_NN_TD(2, true)
+    else SPH_NN_TD(3, true)
+  } else {
+    if (K.nntvisco == 1) SPH_NN_TD(1, false)
+    else if (K.nntvisco == 2) SPH_NN_TD(2, false)
+    else SPH_NN_TD(3, false)
+  }
+#undef SPH_NN_TD
+#undef SPH_NN
+}
+
+}  // namespace sphx

@@ -61,8 +61,14 @@ void derive_constants(const SphCaseDef& c, SphConstants& k) {
   const double h = k.kernelh;
   k.kernelsize = float(h * 2.0f);  // Wendland factor 2 (FunSphKernel.h:190)
   k.kernelsize2 = k.kernelsize * k.kernelsize;
-  k.awen = float(0.41778 / (h * h * h));
-  k.bwen = float(-2.08891 / (h * h * h * h));
+  k.data2d = c.data2d ? 1 : 0;
+  if (k.data2d) {  // GetKernelWendland_Ctes(sim2d) (FunSphKernel.h:193-196)
+    k.awen = float(0.557 / (h * h));
+    k.bwen = float(-2.7852 / (h * h * h));
+  } else {
+    k.awen = float(0.41778 / (h * h * h));
+    k.bwen = float(-2.08891 / (h * h * h * h));
+  }
   k.cs0 = std::sqrt(double(k.gamma) * double(k.cteb) / double(k.rhopzero));
   k.eta2 = float((h * 0.1) * (h * 0.1));
   k.ovrhopzero = 1.0f / k.rhopzero;
@@ -90,6 +96,60 @@ void derive_constants(const SphCaseDef& c, SphConstants& k) {
   if (k.slipmode != SPH_SLIP_VEL0)
     throw SphError(SPH_ERR_UNSUPPORTED, "Only the slip mode velocity=0 is allowed with mDBC conditions.");
   k.mdbc_threshold = (k.tboundary == SPH_BOUND_MDBC ? float(c.mdbc_threshold) : 0.f);
+  if (k.data2d && k.tboundary == SPH_BOUND_MDBC)
+    throw SphError(SPH_ERR_UNSUPPORTED, "mDBC in 2-D simulations is not implemented");
+  // Rheology, viscosity and shifting options (JSph::LoadConfigParameters, JSph.cpp:608-700 of
+  // the v5.0 solver; JSph.cpp:620-700 of v5.2).
+  k.rheology = (c.rheology == 0 ? SPH_RHEOLOGY_SINGLE : c.rheology);
+  k.velgrad = (c.velgrad == 0 ? SPH_VELGRAD_FDA : c.velgrad);
+  k.tvisco = (c.tvisco == 0 ? SPH_VISCO_ARTIFICIAL : c.tvisco);
+  k.shift_mode = c.shift_mode;
+  k.shift_coef = float(c.shift_coef);
+  k.shift_tfs = float(c.shift_tfs);
+  k.relaxation_dt = float(c.relaxation_dt);
+  if (k.rheology != SPH_RHEOLOGY_SINGLE && k.rheology != SPH_RHEOLOGY_NN)
+    throw SphError(SPH_ERR_ARG, "Rheology treatment is not valid.");
+  if (k.velgrad != SPH_VELGRAD_FDA && k.velgrad != SPH_VELGRAD_SPH)
+    throw SphError(SPH_ERR_ARG, "Velocity gradient treatment is not valid.");
+  if (k.tvisco < SPH_VISCO_ARTIFICIAL || k.tvisco > SPH_VISCO_CONSTEQ)
+    throw SphError(SPH_ERR_ARG, "Viscosity treatment is not valid.");
+  if (k.shift_mode < SPH_SHIFT_NONE || k.shift_mode > SPH_SHIFT_FULL)
+    throw SphError(SPH_ERR_ARG, "Shifting mode is not valid.");
+  if (k.rheology == SPH_RHEOLOGY_SINGLE) {
+    if (k.tvisco == SPH_VISCO_CONSTEQ)
+      throw SphError(SPH_ERR_ARG, "ViscoTreatment 'Constitutive  eq.' not valid for Single-phase classic formulation.");
+    if (k.tvisco != SPH_VISCO_ARTIFICIAL)
+      throw SphError(SPH_ERR_UNSUPPORTED, "single-phase Laminar+SPS viscosity is not implemented");
+    if (k.shift_mode != SPH_SHIFT_NONE)
+      throw SphError(SPH_ERR_UNSUPPORTED, "shifting is implemented for the NN multiphase formulation only");
+    return;
+  }
+  // NN multiphase: JSph::InitMultiPhase + ConfigConstantsMP (JSph.cpp:3137-3242, v5.0 solver)
+  if (k.tboundary == SPH_BOUND_MDBC)
+    throw SphError(SPH_ERR_ARG, "Multiphase formulations are not supported with BC_mDBC.");
+  if (k.velgrad != SPH_VELGRAD_FDA)
+    throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase: only the FDA velocity gradients are implemented");
+  if (c.nphases < 1 || c.nphases > SPH_MAXPHASES) throw SphError(SPH_ERR_ARG, "The number of phases is invalid.");
+  k.nphases = c.nphases;
+  bool cs0_present = true;
+  for (unsigned p = 0; p < c.nphases; p++) {
+    if (c.phases[p].phasetype != 0) throw SphError(SPH_ERR_UNSUPPORTED, "only phasetype 0 (non-Newtonian) exists in v5.0");
+    if (p && c.phases[p].mkfluid <= c.phases[p - 1].mkfluid)
+      throw SphError(SPH_ERR_ARG, "phases must be sorted by mkfluid");
+    if (!float(c.phases[p].cs0)) cs0_present = false;
+  }
+  for (unsigned p = 0; p < c.nphases; p++) {
+    const SphPhaseDef& ph = c.phases[p];
+    const float rho = float(ph.rho), gam = (float(ph.gamma) ? float(ph.gamma) : k.gamma), cs = float(ph.cs0);
+    k.phase_mass[p] = float(double(rho) * (k.data2d ? c.dp * c.dp : c.dp * c.dp * c.dp));
+    // with a <csound> for every phase: CteB of InitMultiPhase (float arithmetic), else from
+    // the case's Cs0 (ConfigConstantsMP, double arithmetic)
+    k.phase_cteb[p] = cs0_present ? cs * cs * rho / gam : float(k.cs0 * k.cs0 * double(rho) / double(gam));
+  }
+  // DtMin is set here whatever the XML gives (ConfigConstantsMP runs after the parameters
+  // are read, and ConfigConstants2 keeps a non-zero DtMin)
+  const float coefdtmin = float(c.coefdtmin) * 1.0e-5f;  // CoefDtMin*=1.0e-5f
+  k.dtmin = (double(k.kernelh) / k.cs0) * double(coefdtmin);
 }
 
 static KConst make_kconst(const SphConstants& c) {
@@ -137,6 +197,15 @@ static KConst make_kconst(const SphConstants& c) {
   K.awen = c.awen;
   K.mdbc = (c.tboundary == SPH_BOUND_MDBC) ? 1 : 0;
   K.scelldiv = c.scelldiv;
+  K.nn = (c.rheology == SPH_RHEOLOGY_NN) ? 1 : 0;
+  K.nntvisco = c.tvisco;
+  K.shiftmode = c.shift_mode;
+  K.sim2d = c.data2d;
+  K.lamda = c.relaxation_dt;
+  K.shifttfs = c.shift_tfs;
+  K.shiftcoef = c.shift_coef;
+  K.shiftmaxdist = float(c.dp * 0.1);
+  K.coeftfs = (c.data2d ? 2.0 : 3.0) - double(c.shift_tfs);
   {  // binomial coefficients of (1+x)^(1/gamma) - 1
     const double a = 1.0 / double(c.gamma);
     K.ddtc1 = float(a);
@@ -276,10 +345,18 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   // The tiled kernel stages the 3x3 rows of 3 cells of CellMode=full; half runs the
   // one-lane-per-particle kernel over its 5x5 rows of 5 cells.
   if (C.scelldiv != 1) tiled_ = false;
+  nn_ = (C.rheology == SPH_RHEOLOGY_NN);
+  shift_ = (C.shift_mode != SPH_SHIFT_NONE);
+  if (nn_) {
+    // the NN interaction is the tiled kernel of sph_nn.hip only
+    if (C.scelldiv != 1) throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase: CellMode=half is not implemented");
+    tiled_ = true;
+  }
   check_hip(hipSetDevice(device), "hipSetDevice");
   check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
   try {
     AllocFixed();
+    if (nn_) UploadPhases(cdef);
     AllocParticles(cap_);
     Upload(init, sel, nown);
     if (C.tboundary == SPH_BOUND_MDBC) UploadNormals(cdef, init);
@@ -329,6 +406,27 @@ void SphGpuSingle::AllocFixed() {
   check_hip(hipHostMalloc((void**)&slabcnt_host_, sizeof(SlabCounts), hipHostMallocDefault), "hipHostMalloc");
 }
 
+// NN phase tables (JSph::InitMultiPhase + ConfigConstantsMP): the interaction's constants
+// (sph_device.hpp layout) and the EOS of every phase for the divide's pressure.
+void SphGpuSingle::UploadPhases(const SphCaseDef& cdef) {
+  std::vector<float4> tab(2 * NN_MAXPH, make_float4(0.f, 0.f, 0.f, 0.f)), eos(NN_MAXPH, make_float4(1.f, 0.f, 1.f, 0.f));
+  for (unsigned p = 0; p < C.nphases; p++) {
+    const SphPhaseDef& ph = cdef.phases[p];
+    tab[2 * p] = make_float4(C.phase_mass[p], float(ph.cs0), float(ph.visco), float(ph.tau_yield));
+    tab[2 * p + 1] = make_float4(float(ph.hbp_m), float(ph.hbp_n), float(ph.tau_max), float(ph.bi_multi));
+    const float gam = float(ph.gamma) ? float(ph.gamma) : C.gamma;
+    const int ig = (gam == float(int(gam)) && gam >= 1.f && gam <= 16.f) ? int(gam) : 0;
+    eos[p] = make_float4(float(ph.rho), C.phase_cteb[p], gam, float(ig));
+    phase_rho_[p] = float(ph.rho);
+  }
+  for (float4** dst : {&phasek_, &phaseeos_}) {
+    check_hip(hipMalloc((void**)dst, sizeof(float4) * 2 * NN_MAXPH), "hipMalloc phases");
+    allocs_.push_back(*dst);
+  }
+  check_hip(hipMemcpy(phasek_, tab.data(), sizeof(float4) * tab.size(), hipMemcpyHostToDevice), "upload phases");
+  check_hip(hipMemcpy(phaseeos_, eos.data(), sizeof(float4) * eos.size(), hipMemcpyHostToDevice), "upload phases");
+}
+
 // Everything sized by the particle capacity (both gather sets, sort scratch, slab tiles).
 void SphGpuSingle::AllocParticles(unsigned cap) {
   auto dmalloc = [&](size_t bytes) -> void* {
@@ -360,6 +458,7 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
   // (<= 2 per row: fluid and bound) or reaches TMAXCELLS = 4 cells (<= 1 per 4 cells).
   items_ = (uint4*)dmalloc(16 * (n / 128 + 2 * size_t(G.ncy) * size_t(G.ncz) + size_t(G.nct) / 2 + 2));
   arace_ = (float4*)dmalloc(16 * n);
+  if (shift_) shiftpos_ = (float4*)dmalloc(16 * n);  // the interaction's shifting sums
   for (int i = 0; i < 2; i++) {
     sort_.keys[i] = (unsigned*)dmalloc(4 * n);
     sort_.vals[i] = (unsigned*)dmalloc(4 * n);
@@ -440,6 +539,13 @@ void SphGpuSingle::Upload(const SphParticlesHost& h, const std::vector<unsigned>
         throw SphError(SPH_ERR_ARG, "particle codes: boundary (fixed/moving) particles must be the first npb");
     } else {
       code[i] = (i < npb0_ ? typecode(0) : CODE_TYPE_FLUID);
+    }
+    // JSph::LoadMultiphaseData (JSph.cpp:3248-3263 of the v5.0 solver): a fluid particle's
+    // density starts at its phase's rho; its code value must name a phase.
+    if (nn_ && CodeIsFluid(code[i])) {
+      const unsigned ph = code[i] & CODE_MASKVALUE;
+      if (ph >= C.nphases) throw SphError(SPH_ERR_ARG, "Fluid particle without phase information...");
+      vr[i].w = phase_rho_[ph];
     }
     // JSph::CheckRhopLimits (JSph.cpp:2021-2030).
     if (i >= npb0_ && (vr[i].w < C.rhopoutmin || C.rhopoutmax < vr[i].w))
@@ -642,7 +748,7 @@ void SphGpuSingle::RunCellDivide() {
   launch_begincell(stream, cap_, sc_, sort_.keys[res], G, begincell_);
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET);
   launch_gather(stream, cap_, sc_, sort_.vals[res], cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_,
-                G.xoff);
+                G.xoff, nn_ ? phaseeos_ : nullptr);
   std::swap(cur_, alt_);
   if (tiled_) launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_);
   if (nftp_) launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_, K, G);
@@ -667,7 +773,14 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
     }
     TimedEnd(3);
   }
-  if (tiled_) {
+  if (nn_) {
+    // NN multiphase (sph_nn.hip); the shifting sums only where they are applied: the
+    // corrector (the predictor's RunShifting result is never used, shift=false in
+    // ComputeSymplecticPre) and Verlet
+    TimedBegin(0);
+    launch_nn_tiled(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, cur_.code, begincell_,
+                    G, K, phasek_, arace_, shiftpos_, shift_ && interstep != 2);
+  } else if (tiled_) {
     // The tiled kernel writes the arace of every owned particle (skipped boundary items
     // get ar = 0) and resets its own work counters at exit (zeroed once at allocation).
     TimedBegin(0);  // the timed interval is the interaction kernel alone (rocprof's per-kernel average)
@@ -685,7 +798,7 @@ void SphGpuSingle::DtVariable(int mode) {
   if (slab()) {
     // The three maxima span the whole domain: fold locally, max over all slabs.
     launch_fold_maxima(stream, sc_, folded_, mode != DT_PEEK);
-    transport_->allreduce_max_u32(folded_, 3, stream);
+    transport_->allreduce_max_u32(folded_, 4, stream);
     launch_dt(stream, sc_, K, C.cflnumber, C.dtmin, C.cs0, mode, dttrace_, tracecap_, folded_);
   } else {
     launch_dt(stream, sc_, K, C.cflnumber, C.dtmin, C.cs0, mode, dttrace_, tracecap_);
@@ -696,7 +809,7 @@ void SphGpuSingle::ComputeVerlet() {
   TimedBegin(1);
   verletstep_++;
   const bool euler = !(verletstep_ < C.verlet_steps);
-  launch_verlet(stream, cap_, sc_, K, euler, arace_, cur_, G);
+  launch_verlet(stream, cap_, sc_, K, euler, arace_, cur_, G, shift_ ? shiftpos_ : nullptr);
   if (euler) verletstep_ = 0;
   std::swap(cur_.velrhop, cur_.velrhopm1);
   TimedEnd(1);
@@ -714,7 +827,7 @@ void SphGpuSingle::ComputeSymplecticPre() {
 
 void SphGpuSingle::ComputeSymplecticCorr() {
   TimedBegin(1);
-  launch_sym_cor(stream, cap_, sc_, K, arace_, cur_, G);
+  launch_sym_cor(stream, cap_, sc_, K, arace_, cur_, G, shift_ ? shiftpos_ : nullptr);
   havepre_ = false;
   TimedEnd(1);
 }
@@ -833,6 +946,7 @@ void SphGpuSingle::SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* m
 void SphGpuSingle::SetFloatings(unsigned nft, const SphFloatingDef* defs, double ftpause) {
   if (stepped_ || ftbodies_) throw SphError(SPH_ERR_STATE, "the floating bodies are configured once, before the first step");
   if (!nft || !defs) throw SphError(SPH_ERR_ARG, "no floating bodies");
+  if (nn_) throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase with floating bodies is not implemented");
   std::vector<FtBody> b(nft);
   std::vector<float> massp(nft);
   unsigned begin = casenpb_;
@@ -926,6 +1040,7 @@ SphRunStats SphGpuSingle::Stats() {
   r.velmax = s.last_velmax;
   r.acemax = s.last_acemax;
   r.viscdtmax = s.last_viscdt;
+  r.viscetadtmax = s.last_visceta;
   return r;
 }
 

@@ -100,6 +100,7 @@ class SphGpuSingle {
   void Grow(unsigned np_live, unsigned newcap);
   void Upload(const SphParticlesHost& init, const std::vector<unsigned>& sel, unsigned nown);
   void UploadNormals(const SphCaseDef& cdef, const SphParticlesHost& init);
+  void UploadPhases(const SphCaseDef& cdef);
   void Exchange();
   void RunMotion();                 // JSphCpu::RunMotion after ComputeStep (JSphCpuSingle.cpp:1096)
   void RunFloating(bool predictor); // JSphCpuSingle::RunFloating
@@ -120,6 +121,12 @@ class SphGpuSingle {
   unsigned mdbcfacecap_ = 0;
   unsigned* bidx_ = nullptr;         // slabs + mDBC: boundary idp -> index [CaseNpb]
   float4* arace_ = nullptr;
+  // NN multiphase (v5.0 solver) and shifting
+  bool nn_ = false, shift_ = false;
+  float4* phasek_ = nullptr;    // interaction constants, 2 float4 per phase
+  float4* phaseeos_ = nullptr;  // {rho0, cteb, gamma, integer gamma} per phase
+  float phase_rho_[SPH_MAXPHASES] = {};
+  float4* shiftpos_ = nullptr;  // shifting sums of the last interaction [cap]
   unsigned* begincell_ = nullptr;
   uint4* items_ = nullptr;        // tiled-interaction work items (per divide)
   unsigned* rowtmp_ = nullptr;    // per-row item counts/offsets

@@ -13,67 +13,62 @@
 
 namespace sphx {
 
-// One wave folds the reduction slots (max of non-negative floats as uint bits).
-__device__ __forceinline__ void fold_slots(DevScalars* __restrict__ sc, bool clear, unsigned& mv, unsigned& ma,
-                                           unsigned& mvd) {
+// One wave folds the reduction slots (max of non-negative floats as uint bits):
+// m[0] VelMax^2, m[1] AceMax^2, m[2] ViscDtMax, m[3] ViscEtaDtMax (NN).
+__device__ __forceinline__ void fold_slots(DevScalars* __restrict__ sc, bool clear, unsigned m[4]) {
   const unsigned l = threadIdx.x;
-  mv = sc->red[RED_VELMAX2][l];
-  ma = sc->red[RED_ACEMAX2][l];
-  mvd = sc->red[RED_VISCDT][l];
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    mv = max(mv, (unsigned)__shfl_xor((int)mv, off, 64));
-    ma = max(ma, (unsigned)__shfl_xor((int)ma, off, 64));
-    mvd = max(mvd, (unsigned)__shfl_xor((int)mvd, off, 64));
-  }
-  if (clear) {
-    sc->red[RED_VELMAX2][l] = 0u;
-    sc->red[RED_ACEMAX2][l] = 0u;
-    sc->red[RED_VISCDT][l] = 0u;
-  }
+  for (int k = 0; k < 4; k++) m[k] = sc->red[k][l];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int k = 0; k < 4; k++) m[k] = max(m[k], (unsigned)__shfl_xor((int)m[k], off, 64));
+  if (clear)
+#pragma unroll
+    for (int k = 0; k < 4; k++) sc->red[k][l] = 0u;
 }
 
-// Slab mode: fold the local slots into folded3[0..2] for the max-allreduce over ranks
+// Slab mode: fold the local slots into folded[0..3] for the max-allreduce over ranks
 // (the reference's single-domain CalcVelMaxOmp/ComputeAceMaxOmp/ViscDtMax reductions
-// span the whole domain, so the slabs must agree on the same three maxima).
-__global__ void k_fold(DevScalars* __restrict__ sc, unsigned* __restrict__ folded3, int clear) {
-  unsigned mv, ma, mvd;
-  fold_slots(sc, clear != 0, mv, ma, mvd);
-  if (threadIdx.x == 0) {
-    folded3[0] = mv;
-    folded3[1] = ma;
-    folded3[2] = mvd;
-  }
+// span the whole domain, so the slabs must agree on the same maxima).
+__global__ void k_fold(DevScalars* __restrict__ sc, unsigned* __restrict__ folded, int clear) {
+  unsigned m[4];
+  fold_slots(sc, clear != 0, m);
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 4; k++) folded[k] = m[k];
 }
 
-void launch_fold_maxima(hipStream_t stm, DevScalars* sc, unsigned* folded3, bool clear) {
-  hipLaunchKernelGGL(k_fold, dim3(1), dim3(64), 0, stm, sc, folded3, int(clear));
+void launch_fold_maxima(hipStream_t stm, DevScalars* sc, unsigned* folded, bool clear) {
+  hipLaunchKernelGGL(k_fold, dim3(1), dim3(64), 0, stm, sc, folded, int(clear));
 }
 
 __global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double dtmin, double cs0, int mode,
                      double* __restrict__ dttrace, unsigned tracecap, const unsigned* __restrict__ folded) {
   const unsigned l = threadIdx.x;
-  unsigned mv, ma, mvd;
+  unsigned m[4];
   if (folded) {
-    mv = folded[0];
-    ma = folded[1];
-    mvd = folded[2];
+    for (int k = 0; k < 4; k++) m[k] = folded[k];
   } else {
-    fold_slots(sc, mode != DT_PEEK, mv, ma, mvd);
+    fold_slots(sc, mode != DT_PEEK, m);
   }
   if (l != 0) return;
-  const float velmaxf = sqrtf(__uint_as_float(mv));  // CalcVelMaxOmp returns float sqrt
+  const float velmaxf = sqrtf(__uint_as_float(m[0]));  // CalcVelMaxOmp returns float sqrt
   const double velmax = double(velmaxf);
-  const double acemax = sqrt(double(__uint_as_float(ma)));
-  const float viscdt = __uint_as_float(mvd);
+  const double acemax = sqrt(double(__uint_as_float(m[1])));
+  const float viscdt = __uint_as_float(m[2]);
+  const float visceta = __uint_as_float(m[3]);
   sc->last_velmax = velmaxf;
   sc->last_acemax = float(acemax);
   sc->last_viscdt = viscdt;
+  sc->last_visceta = visceta;
   if (mode == DT_PEEK) return;
   const double kh = double(K.kernelh);
   const double dt1 = (acemax ? sqrt(kh / acemax) : DBL_MAX);
   const double dt2 = kh / (fmax(cs0, velmax * 10.) + kh * double(viscdt));
-  double dt = cfl * fmin(dt1, dt2);
+  // NN: viscous time step h^2/(ViscEtaDtMax*RelaxationDt), float products as the v5.0
+  // solver forms them (JSphCpu.cpp:1687 of src_mphase/DSPH_v5.0_NNewtonian)
+  const double dt3 = (K.nn ? double(K.kernelh * K.kernelh) / double(visceta * K.lamda) : DBL_MAX);
+  double dt = cfl * fmin(dt3, fmin(dt1, dt2));
   if (isnan(dt) || isinf(dt)) {
     sc->error_flags |= ERR_DT_NAN;
     dt = dtmin;
@@ -119,7 +114,8 @@ __device__ __forceinline__ bool slab_ghost(const KConst& K, const DivGrid& g, un
 // ComputeVerlet (JSphCpu.cpp:1381-1399): bound -> ComputeVelrhopBound, fluid -> ComputeVerletVarsFluid.
 // New values are written in velrhopm1 (the caller swaps velrhop/velrhopm1 afterwards).
 __global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ sc, KConst K, int euler,
-                                                const float4* __restrict__ arace, PartArrays a, DivGrid g) {
+                                                const float4* __restrict__ arace, PartArrays a, DivGrid g,
+                                                const float4* __restrict__ shiftpos) {
   const unsigned np = sc->np, npb = sc->npb;
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= np || slab_ghost(K, g, a.dcell, p)) return;
@@ -139,9 +135,10 @@ __global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ s
   }
   const double dt205 = 0.5 * dt * dt;
   const double agx = double(ra.x) + K.gravxd, agy = double(ra.y) + K.gravyd, agz = double(ra.z) + K.gravzd;
-  const double dx = double(vr1.x) * dt + agx * dt205;
-  const double dy = double(vr1.y) * dt + agy * dt205;
-  const double dz = double(vr1.z) * dt + agz * dt205;
+  double dx = double(vr1.x) * dt + agx * dt205;
+  double dy = double(vr1.y) * dt + agy * dt205;
+  double dz = double(vr1.z) * dt + agz * dt205;
+  if (shiftpos) shift_displacement(K, shiftpos[p], vr1, dt, dx, dy, dz);  // RunShifting(dt) before ComputeVerlet
   const bool outrhop = (rhopnew < K.rhopoutmin || rhopnew > K.rhopoutmax);
   const float4 nv = make_float4(float(double(vr2.x) + agx * dt2), float(double(vr2.y) + agy * dt2),
                                 float(double(vr2.z) + agz * dt2), rhopnew);
@@ -151,9 +148,9 @@ __global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ s
 }
 
 void launch_verlet(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, bool euler, const float4* arace,
-                   PartArrays a, DivGrid g) {
+                   PartArrays a, DivGrid g, const float4* shiftpos) {
   const unsigned nb = (cap + 255) / 256;
-  hipLaunchKernelGGL(k_verlet, dim3(nb), dim3(256), 0, stm, sc, K, int(euler), arace, a, g);
+  hipLaunchKernelGGL(k_verlet, dim3(nb), dim3(256), 0, stm, sc, K, int(euler), arace, a, g, shiftpos);
 }
 
 // ComputeSymplecticPre (JSphCpu.cpp:1406-1504).  The caller has already moved the
@@ -206,7 +203,8 @@ void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst&
 
 // ComputeSymplecticCorr (JSphCpu.cpp:1510-1606).
 __global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ sc, KConst K,
-                                                 const float4* __restrict__ arace, PartArrays a, DivGrid g) {
+                                                 const float4* __restrict__ arace, PartArrays a, DivGrid g,
+                                                 const float4* __restrict__ shiftpos) {
   const unsigned np = sc->np, npb = sc->npb;
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= np || slab_ghost(K, g, a.dcell, p)) return;
@@ -230,9 +228,12 @@ __global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ 
   const float4 nv = make_float4(float(double(vp.x) + (double(ra.x) + K.gravxd) * dt),
                                 float(double(vp.y) + (double(ra.y) + K.gravyd) * dt),
                                 float(double(vp.z) + (double(ra.z) + K.gravzd) * dt), rhopnew);
-  const double dx = (double(vp.x) + double(nv.x)) * dt05;
-  const double dy = (double(vp.y) + double(nv.y)) * dt05;
-  const double dz = (double(vp.z) + double(nv.z)) * dt05;
+  double dx = (double(vp.x) + double(nv.x)) * dt05;
+  double dy = (double(vp.y) + double(nv.y)) * dt05;
+  double dz = (double(vp.z) + double(nv.z)) * dt05;
+  // RunShifting(dt) after the corrector's interaction, with the predicted velocity
+  // (JSphCpuSingle.cpp:764 of the v5.0 solver, JSphShifting.cpp:388-418)
+  if (shiftpos) shift_displacement(K, shiftpos[p], vr, dt, dx, dy, dz);
   const bool outrhop = (rhopnew < K.rhopoutmin || rhopnew > K.rhopoutmax);
   if (outrhop && CodeIsNormal(rcode)) {
     rcode = CodeSetNormal(rcode) | CODE_OUTRHOP;
@@ -249,9 +250,9 @@ __global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ 
 }
 
 void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
-                    DivGrid g) {
+                    DivGrid g, const float4* shiftpos) {
   const unsigned nb = (cap + 255) / 256;
-  hipLaunchKernelGGL(k_sym_cor, dim3(nb), dim3(256), 0, stm, sc, K, arace, a, g);
+  hipLaunchKernelGGL(k_sym_cor, dim3(nb), dim3(256), 0, stm, sc, K, arace, a, g, shiftpos);
 }
 
 }  // namespace sphx

@@ -1,0 +1,120 @@
+// sph_tiled.hpp — pieces shared by the LDS-tiled interaction kernels (the single-phase
+// k_fluid_tiled of sph_interaction_tiled.hip and the NN multiphase k_nn_tiled of
+// sph_nn.hip): block shape and LDS capacities, fast f32 intrinsics, the item flag, the
+// expanded-form candidate test and the lane order of an item's particles.
+#pragma once
+#include <cfloat>
+
+#include "sph_kernels.hpp"
+
+namespace sphx {
+
+#ifndef SPH_ABLATE
+#define SPH_ABLATE 0  // diagnostic builds: 1 = no pair body, 2 = no candidate test/body, 3 = no staging loads
+#endif
+constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
+#ifndef SPH_TCAP
+#define SPH_TCAP 504
+#endif
+#ifndef SPH_PAD
+#define SPH_PAD 8
+#endif
+#ifndef SPH_WAVES
+#define SPH_WAVES 0  // >0: register budget of the fluid kernel for that many waves per SIMD (512/n VGPRs)
+#endif
+#if SPH_WAVES
+#define SPH_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SPH_WAVES, SPH_WAVES)))
+#else
+#define SPH_WAVES_ATTR
+#endif
+// staged neighbour records per segment.  504 (+8 over-read pad) puts the block at
+// 20.3 KB of LDS, the most that keeps 8 blocks = 4 waves per SIMD.  Measured at 1M:
+// 0.806 ms vs 0.838 at 416 (a mirrored row pair fits one segment for 94% of the units
+// instead of 81%); 0.936 at 580 (7 blocks/CU), 1.02 at 672 (6 blocks/CU).
+constexpr int TCAP = SPH_TCAP;
+// With floating bodies a record is 48 B (the third part a float4): 416 records keep the
+// block at <= 20 KB of LDS, i.e. the same 8 blocks (4 waves/SIMD) per CU.
+#ifndef SPH_TCAP_FT
+#define SPH_TCAP_FT 416
+#endif
+template <bool FT> struct TcapT { static constexpr int v = TCAP; };
+template <> struct TcapT<true> { static constexpr int v = SPH_TCAP_FT; };
+constexpr int TMAXCELLS = 4;   // max x-cells per item
+
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fsqrt_(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
+
+constexpr unsigned ITEM_BOUND = 0x80000000u;  // flag in item.x: p1 are boundary particles
+
+// Candidate test of one window: n (<= 128) staged records from sA+s0 with the expanded
+// form |p-A|^2 = |p|^2 + |A|^2 - 2 p.A (3 FMAs + 1 compare per candidate on one
+// ds_read_b128) against a threshold inflated by 1e-4 (the expanded form rounds to ~1e-6
+// relative); the body recomputes |p-A|^2 exactly and applies the reference's test, so no
+// pair is lost or added.  sA is padded past TCAP, so the 8-wide groups may over-read;
+// those bits are masked off.  n <= 0 gives empty masks.
+__device__ __forceinline__ void test128(const float4* __restrict__ sA, int s0, int n, float px2, float py2,
+                                        float pz2, float thr, unsigned long long& m0, unsigned long long& m1) {
+  m0 = 0ull;
+  m1 = 0ull;
+  const float4* __restrict__ b = sA + s0;
+  for (int jo = 0; jo < 16; jo++) {
+    const int left = n - jo * 8;
+    if (left <= 0) break;
+    unsigned bits = 0;
+#pragma unroll
+    for (int ji = 0; ji < 8; ji++) {
+      const float4 A = b[jo * 8 + ji];
+      const float q = fmaf(px2, A.x, fmaf(py2, A.y, fmaf(pz2, A.z, A.w)));
+      bits |= (q <= thr) ? (1u << ji) : 0u;
+    }
+    bits &= (left >= 8 ? 0xffu : ((1u << left) - 1u));
+    if (jo < 8) m0 |= (unsigned long long)bits << (jo * 8);
+    else m1 |= (unsigned long long)bits << ((jo - 8) * 8);
+  }
+}
+
+// Which p1 of the item each lane computes.  A lane's drain loops run as long as the
+// busiest lane of its wave, and a particle's candidate counts per mirrored row pair
+// depend mostly on how far it sits from its cell's centre in y and z; so the n (<= TB)
+// particles are split between the two waves by that distance (|dy| + |dz| below or
+// above half a cell, stable ballot ranks): simulated on the 1M lattice, drain
+// utilisation 0.68 -> 0.74.  Results do not depend on the assignment: every p1 is
+// summed by one lane over the same candidates in the same order.
+__device__ __forceinline__ unsigned lane_order(const float4* __restrict__ poscell, unsigned first, unsigned n,
+                                               float hs, unsigned char* s_perm, unsigned* s_nwave) {
+  const unsigned me = threadIdx.x, wv = me >> 6, ln = me & 63u;
+  const bool valid = me < n;
+  bool low = false;
+  if (valid) {
+    const float4 pc = poscell[first + me];
+    low = fabsf(pc.y - hs) + fabsf(pc.z - hs) < hs;
+  }
+  const unsigned long long bl = __ballot(low), bh = __ballot(valid && !low);
+  const unsigned long long lt = (1ull << ln) - 1ull;
+  if (ln == 0) {
+    s_nwave[wv] = unsigned(__popcll(bl));
+    s_nwave[2 + wv] = unsigned(__popcll(bh));
+  }
+  __syncthreads();
+  const unsigned nl0 = s_nwave[0], nl = nl0 + s_nwave[1], nh0 = s_nwave[2];
+  if (valid) {
+    const unsigned pos = low ? (wv ? nl0 : 0u) + unsigned(__popcll(bl & lt))
+                             : nl + (wv ? nh0 : 0u) + unsigned(__popcll(bh & lt));
+    s_perm[pos] = (unsigned char)me;
+  }
+  __syncthreads();
+  return valid ? s_perm[me] : me;
+}
+
+// Item geometry shared by the passes of one p1.
+struct RowCtx {
+  int cy, cz;     // the item's cell row
+  int xa, xb;     // x-cell range staged for the item
+  int lxa, lxb;   // this lane's own 3-cell x range
+  int xo;         // x origin of item-relative positions
+  bool act;       // lane holds a p1
+};
+
+}  // namespace sphx

@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define SPH_ABI_VERSION 4
+#define SPH_ABI_VERSION 5
 
 typedef enum {
   SPH_OK = 0,
@@ -84,6 +84,29 @@ enum { SPH_BOUND_DBC = 1, SPH_BOUND_MDBC = 2 };
 enum { SPH_SLIP_VEL0 = 1, SPH_SLIP_NOSLIP = 2, SPH_SLIP_FREESLIP = 3 };
 /* TpKernel (DualSphDef.h): only Wendland is on the hot path. */
 enum { SPH_KERNEL_WENDLAND = 2 };
+/* v5.0 NN multiphase solver (src_mphase/DSPH_v5.0_NNewtonian):
+ * RheologyTreatment (JSph.cpp:608-614), VelocityGradientType (:616-621), TpVisco
+ * (DualSphDef.h:374-378) and TpShifting (JSphShifting.h). */
+enum { SPH_RHEOLOGY_SINGLE = 1, SPH_RHEOLOGY_NN = 2 };
+enum { SPH_VELGRAD_FDA = 1, SPH_VELGRAD_SPH = 2 };
+enum { SPH_VISCO_ARTIFICIAL = 1, SPH_VISCO_LAMINARSPS = 2, SPH_VISCO_CONSTEQ = 3 };
+enum { SPH_SHIFT_NONE = 0, SPH_SHIFT_NOBOUND = 1, SPH_SHIFT_NOFIXED = 2, SPH_SHIFT_FULL = 3 };
+#define SPH_MAXPHASES 8
+
+/* One <nnphases><phase> (JSph::InitMultiPhase, JSph.cpp:3137-3215 -> StPhaseArray +
+ * StPhaseCte, DualSphDef.h:304-331), values as the XML gives them. */
+typedef struct SphPhaseDef {
+  int32_t mkfluid;          /* phase of the fluid block with this mkfluid              */
+  int32_t phasetype;        /* <phasetype> (0 non-Newtonian: the only one in v5.0)      */
+  double rho;               /* <rhop>                                                  */
+  double cs0;               /* <csound> (0: not given -> CteB from the case's Cs0)     */
+  double gamma;             /* <gamma> (0: the case's gamma)                           */
+  double visco;             /* <visco> kinematic viscosity / consistency index         */
+  double tau_yield;         /* <tau_yield>                                             */
+  double tau_max;           /* <tau_max> (0: none)                                     */
+  double bi_multi;          /* <Bi_multi> (with tau_max)                               */
+  double hbp_m, hbp_n;      /* <HBP_m>, <HBP_n>                                        */
+} SphPhaseDef;
 
 /* Particle code bits, identical to the 16-bit `typecode` of DualSphDef.h:161-221. */
 #define SPH_CODE_MASKSPECIAL 0xe000u
@@ -133,6 +156,23 @@ typedef struct SphCaseDef {
   int32_t tboundary;        /* SPH_BOUND_* (<parameter Boundary>; 0 = DBC) */
   int32_t slipmode;         /* SPH_SLIP_* (<parameter SlipMode>)           */
   double mdbc_threshold;    /* MdbcThreshold (-mdbc_threshold, default 0)  */
+  /* v5.0 NN multiphase (RheologyTreatment=2).  Phases are sorted by mkfluid (JSph.cpp:
+   * 3187-3195); a fluid particle's phase is its code value (the fluid block index).  */
+  int32_t rheology;         /* SPH_RHEOLOGY_* (0 = single)                 */
+  int32_t velgrad;          /* SPH_VELGRAD_* (0 = FDA)                     */
+  int32_t tvisco;           /* SPH_VISCO_* (0 = artificial)                */
+  uint32_t nphases;
+  double relaxation_dt;     /* RelaxationDt, lamda of the viscous dt       */
+  /* shifting (JSphShifting::ConfigBasic; <parameter Shifting/ShiftCoef/ShiftTFS>) */
+  int32_t shift_mode;       /* SPH_SHIFT_*                                 */
+  int32_t pad_shift;
+  double shift_coef, shift_tfs;
+  SphPhaseDef phases[SPH_MAXPHASES];
+  /* 2-D simulation (<data2d>, JSph::LoadConfigCtes JSph.cpp:571-572): particles in the
+   * plane y = data2d_posy, 2-D Wendland constants (FunSphKernel.h:193-196), ace.y = 0 */
+  int32_t data2d;
+  int32_t pad2d;
+  double data2d_posy;
 } SphCaseDef;
 
 /*
@@ -159,6 +199,13 @@ typedef struct SphConstants {
   int32_t tboundary, slipmode;      /* TBoundary, SlipMode (JSph.cpp:626-640) */
   float mdbc_threshold;             /* MdbcThreshold                          */
   uint32_t pad1;
+  /* NN multiphase and shifting (JSph::ConfigConstantsMP, JSph.cpp:3220-3242) */
+  int32_t rheology, velgrad, tvisco, shift_mode;
+  uint32_t nphases;
+  float relaxation_dt, shift_coef, shift_tfs;
+  float phase_mass[SPH_MAXPHASES];  /* StPhaseArray.mass = rho dp^3               */
+  float phase_cteb[SPH_MAXPHASES];  /* StPhaseArray.CteB                          */
+  int32_t data2d, pad3;
 } SphConstants;
 
 /* Step statistics kept on the device and read back on demand. */
@@ -172,7 +219,7 @@ typedef struct SphRunStats {
   uint32_t dtmodif;       /* dt clamped to DtMin (JSphCpu.cpp:1623-1629)    */
   uint32_t error_flags;   /* bit0: NaN/inf dt, bit1: boundary out           */
   float velmax, acemax, viscdtmax; /* of the last interaction              */
-  float pad;
+  float viscetadtmax;     /* NN: max effective viscosity (ViscEtaDtMax)     */
 } SphRunStats;
 
 /* Host particle view (SaveData layout: JSph::SaveData, JSph.cpp:2717). */

@@ -27,7 +27,9 @@ def build_oracle(force: bool = False) -> str:
     """Compile the oracle restatement with the reference's flags (Makefile_cpu:19-28)."""
     src = os.path.join(HERE, "sph_oracle.cpp")
     hdr = os.path.join(HERE, "sph_oracle.h")
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(src), os.path.getmtime(hdr)):
+    abi = os.path.join(os.path.dirname(HERE), "include", "sphcore.h")  # the PODs it shares with the core
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(src), os.path.getmtime(hdr),
+                                                                         os.path.getmtime(abi)):
         return LIB
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     cmd = ["g++", "-O3", "-fopenmp", "-ffast-math", "-shared", "-fPIC", "-o", LIB, src]

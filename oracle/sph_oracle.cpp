@@ -108,8 +108,14 @@ void Derive(const SphCaseDef& c, SphConstants& k) {
   const double h = k.kernelh;
   k.kernelsize = float(h * kernelk);
   k.kernelsize2 = k.kernelsize * k.kernelsize;
-  k.awen = float(0.41778 / (h * h * h));  // FunSphKernel.h:191-202 (3D)
-  k.bwen = float(-2.08891 / (h * h * h * h));
+  k.data2d = c.data2d ? 1 : 0;
+  if (k.data2d) {  // FunSphKernel.h:193-196 (2D)
+    k.awen = float(0.557 / (h * h));
+    k.bwen = float(-2.7852 / (h * h * h));
+  } else {
+    k.awen = float(0.41778 / (h * h * h));  // FunSphKernel.h:198-199 (3D)
+    k.bwen = float(-2.08891 / (h * h * h * h));
+  }
   k.cs0 = std::sqrt(double(k.gamma) * double(k.cteb) / double(k.rhopzero));
   k.eta2 = float((h * 0.1) * (h * 0.1));
   k.ovrhopzero = 1.0f / k.rhopzero;
@@ -145,6 +151,17 @@ void Derive(const SphCaseDef& c, SphConstants& k) {
   k.slipmode = (k.tboundary == SPH_BOUND_MDBC ? (c.slipmode == 0 ? SPH_SLIP_VEL0 : c.slipmode) : SPH_SLIP_VEL0);
   if (k.slipmode != SPH_SLIP_VEL0) throw std::runtime_error("Only the slip mode velocity=0 is allowed with mDBC conditions.");
   k.mdbc_threshold = (k.tboundary == SPH_BOUND_MDBC ? float(c.mdbc_threshold) : 0.f);
+  // Single-phase classic formulation, artificial viscosity, no shifting: the only options
+  // this restatement covers (the v5.0 NN solver is pinned to its own binary's PARTs).
+  k.rheology = (c.rheology == 0 ? SPH_RHEOLOGY_SINGLE : c.rheology);
+  k.velgrad = (c.velgrad == 0 ? SPH_VELGRAD_FDA : c.velgrad);
+  k.tvisco = (c.tvisco == 0 ? SPH_VISCO_ARTIFICIAL : c.tvisco);
+  k.shift_mode = c.shift_mode;
+  k.shift_coef = float(c.shift_coef);
+  k.shift_tfs = float(c.shift_tfs);
+  k.relaxation_dt = float(c.relaxation_dt);
+  if (k.rheology != SPH_RHEOLOGY_SINGLE || k.tvisco != SPH_VISCO_ARTIFICIAL || k.shift_mode != SPH_SHIFT_NONE)
+    throw std::runtime_error("the oracle restates the single-phase artificial-viscosity path only");
 }
 
 // EOS as the reference binary evaluates it: FunSphEos.h:37-39 calls the unqualified
@@ -693,6 +710,9 @@ class Solver {
       InteractionForcesFluid<tdensity>(true, K.visco * K.viscoboundfactor, dv, viscdt);
     }
     if (npbok) InteractionForcesBound(dv, viscdt);
+    // For 2-D simulations zero the 2nd component (JSphCpuSingle.cpp:544-549).
+    if (K.data2d)
+      for (unsigned p = npb; p < np; p++) ace[p].y = 0;
   }
   // JSphCpu::InteractionMdbcCorrectionT2<Wendland,sim2d=false,SLIP_Vel0> (JSphCpu.cpp:1020-1187)
   // over n = NpbOk boundary particles (UseNormalsFt=false; JSphCpu.cpp:1193-1210).

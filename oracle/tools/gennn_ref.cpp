@@ -1,0 +1,181 @@
+// gennn_ref — non-Newtonian multiphase wet dam break for the REFERENCE v5.0 NN solver
+// (test infrastructure; SURVEY.md §8(f) row 4, BASELINE cfg5).
+//
+// The reference example examples/mphase_nnewtonian/01_WetDambreak/CaseWetDambreak2DNN_Def.xml
+// (lines 28-124) is a 2-D GenCase definition; GenCase is a missing blob,
+// so this tool writes the <case>.xml + <case>.bi4 pair for the v5.0 solver directly, with
+// the example's geometry EXTRUDED along y (BASELINE cfg5: "the 3-phase NN case extruded to
+// 3D"), through the reference's own JPartDataBi4.  The product-side generator
+// (dualsphysics_multilayer_amd/case.py WetDambreakNNCase) restates this recipe; a CPU test
+// checks both give the same particles bit for bit.
+//
+// Lattice (indices i, j, k; position (i,j,k)*dp), lengths scaled by `scale` (1 = the example):
+//   tank   x in [0, 4s], z in [0, 1.25s], y in [0, W]; walls 0.04 thick (the example's
+//          drawbox sizes; not scaled): bottom, left (x=0), right (x=4s), front (y=0) and back
+//          (y=W) — the y walls are the extrusion's, every other wall is the example's;
+//   phases drawn in the example's order, later boxes replacing earlier ones, walls last:
+//          mkfluid 0: x <= 4s, z <= 0.5s;  mkfluid 1: x <= 1s, 0.5s <= z <= 0.75s;
+//          mkfluid 2: x <= 0.5s, 0.75s <= z <= 1.0s.
+// Particles: boundary (one fixed block) then the three phases, each in k, j, i loop order.
+// Constants as GenCase derives them from the example: speedsystem 1 x coefsound 20 = cs0 20,
+// b = cs0^2 rho0/gamma, h = coefh sqrt(3 dp^2) with coefh 0.91924 (the 3-D formula), masses
+// rho0 dp^3; <nnphases> and <parameters> are the example's (lines 72-124), ShiftTFS the
+// example's 3-D recommendation 2.75 unless given.
+//
+// usage: gennn_ref <dp> <outdir> [width=0.64] [scale=1] [timemax=5] [casename] [shifttfs=2.75]
+//                  [velgrad=1] [viscotreatment=2] [ddt=3] [shifting=3] [csound=0] [step=2]
+// csound > 0 gives every phase <csound> (phase k: csound*(1 + 0.1 k)), the branch of
+// ConfigConstantsMP where each phase has its own sound speed and CteB (JSph.cpp:3222-3231).
+#include "JPartDataBi4.h"
+#include "Functions.h"
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+int main(int argc, char** argv) {
+  if (argc < 3) {
+    fprintf(stderr, "usage: %s dp outdir [width] [scale] [timemax] [casename] [shifttfs] [velgrad] [visco] [ddt] [shifting]\n",
+            argv[0]);
+    return 1;
+  }
+  const double dp = atof(argv[1]);
+  const std::string dir = argv[2];
+  const double width = (argc > 3 ? atof(argv[3]) : 0.64);
+  const double s = (argc > 4 ? atof(argv[4]) : 1.0);
+  const double tmax = (argc > 5 ? atof(argv[5]) : 5.0);
+  const std::string name = (argc > 6 ? argv[6] : "CaseWetDambreakNN");
+  const std::string shifttfs = (argc > 7 ? argv[7] : "2.75");
+  const int velgrad = (argc > 8 ? atoi(argv[8]) : 1);
+  const int tvisco = (argc > 9 ? atoi(argv[9]) : 2);
+  const int ddt = (argc > 10 ? atoi(argv[10]) : 3);
+  const int shifting = (argc > 11 ? atoi(argv[11]) : 3);
+  const double csound = (argc > 12 ? atof(argv[12]) : 0.0);
+  const int step = (argc > 13 ? atoi(argv[13]) : 2);
+
+  const int nx = int(std::round(4.0 * s / dp)), nz = int(std::round(1.25 * s / dp)), ny = int(std::round(width / dp));
+  const int nw = int(std::round(0.04 / dp));
+  const int x0 = int(std::round(4.0 * s / dp)), z0 = int(std::round(0.5 * s / dp));
+  const int x1 = int(std::round(1.0 * s / dp)), z1a = z0, z1b = int(std::round(0.75 * s / dp));
+  const int x2 = int(std::round(0.5 * s / dp)), z2a = z1b, z2b = int(std::round(1.0 * s / dp));
+  auto wall = [&](int i, int j, int k) { return k <= nw || i <= nw || i >= nx - nw || j <= nw || j >= ny - nw; };
+  auto phase = [&](int i, int k) -> int {
+    if (i <= x2 && k >= z2a && k <= z2b) return 2;
+    if (i <= x1 && k >= z1a && k <= z1b) return 1;
+    if (i <= x0 && k <= z0) return 0;
+    return -1;
+  };
+  std::vector<tdouble3> pos;
+  for (int k = 0; k <= nz; k++)
+    for (int j = 0; j <= ny; j++)
+      for (int i = 0; i <= nx; i++)
+        if (wall(i, j, k)) pos.push_back(TDouble3(i * dp, j * dp, k * dp));
+  const unsigned nb = unsigned(pos.size());
+  unsigned nph[3] = {0, 0, 0};
+  for (int ph = 0; ph < 3; ph++)
+    for (int k = 0; k <= nz; k++)
+      for (int j = 0; j <= ny; j++)
+        for (int i = 0; i <= nx; i++)
+          if (!wall(i, j, k) && phase(i, k) == ph) {
+            pos.push_back(TDouble3(i * dp, j * dp, k * dp));
+            nph[ph]++;
+          }
+  const unsigned np = unsigned(pos.size()), nf = np - nb;
+
+  const double g = 9.81, rho0 = 1000., gamma = 7., cs0 = 20. * 1.0, coefh = 0.91924;
+  const double b = cs0 * cs0 * rho0 / gamma;
+  const double h = coefh * std::sqrt(3. * dp * dp);
+  const double mass = rho0 * dp * dp * dp;
+  const double rhoph[3] = {2000., 1500., 1000.};
+
+  std::vector<unsigned> idp(np);
+  std::vector<tfloat3> vel(np, TFloat3(0));
+  std::vector<float> rhop(np);
+  tdouble3 pmin = TDouble3(DBL_MAX), pmax = TDouble3(-DBL_MAX);
+  unsigned p = 0;
+  for (; p < nb; p++) rhop[p] = float(rho0);
+  for (int ph = 0; ph < 3; ph++)
+    for (unsigned c = 0; c < nph[ph]; c++, p++) rhop[p] = float(rhoph[ph]);  // JSph::LoadMultiphaseData sets them too
+  for (p = 0; p < np; p++) {
+    idp[p] = p;
+    pmin = MinValues(pmin, pos[p]);
+    pmax = MaxValues(pmax, pos[p]);
+  }
+
+  JPartDataBi4 pd;
+  pd.ConfigBasic(0, 1, "gennn_ref", "gennn_ref", name, false, 0, dir);
+  pd.ConfigParticles(np, nb, 0, 0, nf, pmin, pmax, false, false);
+  pd.ConfigCtes(dp, h, b, rho0, gamma, mass, mass);
+  pd.AddPartInfo(0, 0, np, 0, 0, 0, pmin, pmax, 0, 0);
+  pd.AddPartData(np, idp.data(), pos.data(), vel.data(), rhop.data());
+  pd.SaveFileCase(name);
+
+  FILE* f = fopen((dir + "/" + name + ".xml").c_str(), "w");
+  if (!f) { perror("xml"); return 2; }
+  fprintf(f, "<?xml version=\"1.0\" encoding=\"UTF-8\" ?>\n<case app=\"gennn_ref\">\n<execution>\n<constants>\n");
+  fprintf(f, "<data2d value=\"false\"/>\n<gravity x=\"0\" y=\"0\" z=\"%g\"/>\n<cflnumber value=\"0.1\"/>\n", -g);
+  fprintf(f, "<gamma value=\"%g\"/>\n<rhop0 value=\"%g\"/>\n<dp value=\"%.10g\"/>\n", gamma, rho0, dp);
+  fprintf(f, "<h value=\"%.10E\"/>\n<b value=\"%.10E\"/>\n<massbound value=\"%.10E\"/>\n<massfluid value=\"%.10E\"/>\n", h, b, mass, mass);
+  fprintf(f, "</constants>\n");
+  fprintf(f, "<particles np=\"%u\" nb=\"%u\" nbf=\"%u\" mkboundfirst=\"11\" mkfluidfirst=\"1\">\n", np, nb, nb);
+  fprintf(f, "<fixed mkbound=\"0\" mk=\"11\" begin=\"0\" count=\"%u\"/>\n", nb);
+  unsigned begin = nb;
+  for (int ph = 0; ph < 3; ph++) {
+    fprintf(f, "<fluid mkfluid=\"%d\" mk=\"%d\" begin=\"%u\" count=\"%u\"/>\n", ph, ph + 1, begin, nph[ph]);
+    begin += nph[ph];
+  }
+  fprintf(f, "</particles>\n");
+  // <special><nnphases> of the example (CaseWetDambreak2DNN_Def.xml:72-99)
+  fprintf(f, "<special>\n<nnphases>\n");
+  auto cs = [&](int k) -> std::string {
+    if (csound <= 0) return "";
+    char b[96];
+    snprintf(b, sizeof(b), "<csound value=\"%.10g\"/>", csound * (1.0 + 0.1 * k));
+    return b;
+  };
+  fprintf(f, "<phase mkfluid=\"0\"><rhop value=\"2000\"/>%s<visco value=\"0.2\"/><tau_yield value=\"0.0001\"/>"
+             "<HBP_m value=\"100\"/><HBP_n value=\"1.5\"/><phasetype value=\"0\"/></phase>\n", cs(0).c_str());
+  fprintf(f, "<phase mkfluid=\"1\"><rhop value=\"1500\"/>%s<visco value=\"0.1\"/><tau_yield value=\"0.001\"/>"
+             "<HBP_m value=\"10\"/><HBP_n value=\"1\"/><phasetype value=\"0\"/></phase>\n", cs(1).c_str());
+  fprintf(f, "<phase mkfluid=\"2\"><rhop value=\"1000\"/>%s<visco value=\"0.05\"/><tau_yield value=\"0.0005\"/>"
+             "<HBP_m value=\"0\"/><HBP_n value=\"1\"/><phasetype value=\"0\"/></phase>\n", cs(2).c_str());
+  fprintf(f, "</nnphases>\n</special>\n");
+  fprintf(f, "<parameters>\n");
+  auto par = [&](const char* k, const std::string& v) { fprintf(f, "<parameter key=\"%s\" value=\"%s\"/>\n", k, v.c_str()); };
+  par("SavePosDouble", "0");
+  par("StepAlgorithm", std::to_string(step));
+  par("VerletSteps", "40");
+  par("Kernel", "2");
+  par("RheologyTreatment", "2");
+  par("VelocityGradientType", std::to_string(velgrad));
+  par("ViscoTreatment", std::to_string(tvisco));
+  par("Visco", "0.05");
+  par("ViscoBoundFactor", "1");
+  par("DensityDT", std::to_string(ddt));
+  par("DensityDTvalue", "0.1");
+  par("Shifting", std::to_string(shifting));
+  par("ShiftCoef", "-10");
+  par("ShiftTFS", shifttfs);
+  par("RigidAlgorithm", "1");
+  par("FtPause", "0.0");
+  par("CoefDtMin", "0.05");
+  par("RelaxationDt", "0.2");
+  par("DtIni", "0");
+  par("DtMin", "0");
+  par("DtFixed", "0");
+  par("DtAllParticles", "0");
+  par("TimeMax", fun::DoubleStr(tmax));
+  par("TimeOut", "0.05");
+  par("PartsOutMax", "1");
+  par("RhopOutMin", "500");
+  par("RhopOutMax", "3000");
+  fprintf(f, "<simulationdomain><posmin x=\"default\" y=\"default\" z=\"default\"/>"
+             "<posmax x=\"default\" y=\"default\" z=\"default + 50%%\"/></simulationdomain>\n");
+  fprintf(f, "</parameters>\n</execution>\n</case>\n");
+  fclose(f);
+  printf("np=%u nb=%u nf=%u nph0=%u nph1=%u nph2=%u h=%.10g b=%.10g cs0=%.10g mass=%.10g\n", np, nb, nf, nph[0], nph[1],
+         nph[2], h, b, cs0, mass);
+  return 0;
+}

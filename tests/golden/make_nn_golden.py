@@ -1,0 +1,101 @@
+"""Golden fixtures of the v5.0 NN multiphase solver (BASELINE cfg5).
+
+Run in the build container only: needs the REFERENCE NN solver built from
+src_mphase/DSPH_v5.0_NNewtonian/source by ``make -C oracle`` (oracle/_ref/
+DualSPHysics5.0NN_CPU_ref) plus oracle/_ref/{gennn_ref,partdump_ref}.  Each case is the
+3-D extruded wet dam break written by gennn_ref, run with ``-nsteps:N -svsteps:1
+-saveposdouble:1 -sv:binx``; the kept PARTs are stored sorted by idp as
+
+    tests/golden/nn_<name>.npz : s<step>_{idp,pos,vel,rhop,time}, times, dt, meta
+
+meta = [dp, width, scale, shifttfs, velgrad, tvisco, ddt, shifting, csound, step, nsteps].
+
+With ``--noise`` the same cases also run on the reference built WITHOUT -ffast-math
+(``make -C oracle nnstrict``); the largest fast-math-vs-strict differences per kept step
+are the reference's own rounding-noise floor (stored as noise_<step> = [dpos, dvel, drho]),
+and the GPU tests hold the core to 10x that floor.
+
+Usage: python tests/golden/make_nn_golden.py [--only NAME] [--noise]
+"""
+import argparse
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = os.path.join(ROOT, "oracle", "_ref")
+sys.path.insert(0, HERE)
+from make_golden import load_dump  # noqa: E402
+
+# name: (dp, width, scale, shifttfs, velgrad, tvisco, ddt, shifting, csound, step, nsteps, kept steps)
+CASES = {
+    # the example's configuration (FDA, Laminar, DDT Fourtakas full, shifting Full), Symplectic
+    "sym_lam_dp0.02": (0.02, 0.2, 0.5, 2.75, 1, 2, 3, 3, 0.0, 2, 60, (1, 10, 60)),
+    # every phase with its own <csound>: DDT and phase CteB active; constitutive equation
+    "sym_consteq_cs_dp0.025": (0.025, 0.2, 0.5, 2.75, 1, 3, 3, 3, 20.0, 2, 30, (1, 30)),
+    # artificial viscosity with phase sound speeds, Molteni DDT, shifting NoBound, Verlet
+    "ver_art_ddt1_cs_dp0.025": (0.025, 0.2, 0.5, 2.75, 1, 1, 1, 1, 20.0, 1, 45, (1, 41, 45)),
+}
+
+
+def run_case(exe, spec, tmp, nsteps):
+    dp, width, scale, tfs, vg, tv, ddt, sh, cs, step = spec[:10]
+    subprocess.check_call([os.path.join(REF, "gennn_ref"), repr(dp), tmp, repr(width), repr(scale), "5",
+                           "CaseNN", repr(tfs), str(vg), str(tv), str(ddt), str(sh), repr(cs), str(step)],
+                          stdout=subprocess.DEVNULL)
+    out = os.path.join(tmp, "out_" + os.path.basename(exe))
+    subprocess.check_call([exe, os.path.join(tmp, "CaseNN"), out, "-nsteps:%d" % nsteps, "-svsteps:1",
+                           "-saveposdouble:1", "-sv:binx", "-svres:0"], stdout=subprocess.DEVNULL)
+    return out
+
+
+def dump(out, part, tmp):
+    fn = os.path.join(tmp, "p.bin")
+    subprocess.check_call([os.path.join(REF, "partdump_ref"), out, str(part), fn], stdout=subprocess.DEVNULL)
+    t, idp, pos, vel, rho = load_dump(fn)
+    o = np.argsort(idp, kind="stable")
+    return t, idp[o], pos[o], vel[o], rho[o]
+
+
+def make(name, spec, noise):
+    nsteps, keep = spec[10], spec[11]
+    tmp = tempfile.mkdtemp(prefix="nngolden_")
+    try:
+        out = run_case(os.path.join(REF, "DualSPHysics5.0NN_CPU_ref"), spec, tmp, nsteps)
+        outs = run_case(os.path.join(REF, "DualSPHysics5.0NN_CPU_strict"), spec, tmp, nsteps) if noise else None
+        arrays, times = {}, []
+        for part in range(nsteps + 1):
+            t, idp, pos, vel, rho = dump(out, part, tmp)
+            times.append(t)
+            if part in keep:
+                arrays.update({"s%d_idp" % part: idp, "s%d_pos" % part: pos, "s%d_vel" % part: vel,
+                               "s%d_rhop" % part: rho, "s%d_time" % part: np.float64(t)})
+                if outs:
+                    ts, idps, poss, vels, rhos = dump(outs, part, tmp)
+                    assert np.array_equal(idp, idps), "strict build excluded other particles"
+                    arrays["noise_%d" % part] = np.array([np.abs(pos - poss).max(), np.abs(vel - vels).max(),
+                                                          np.abs(rho.astype(np.float64) - rhos).max()])
+        arrays["times"] = np.array(times)
+        arrays["dt"] = np.diff(np.array(times))
+        arrays["meta"] = np.array(list(spec[:11]), np.float64)
+        fn = os.path.join(HERE, "nn_%s.npz" % name)
+        np.savez_compressed(fn, **arrays)
+        print(name, "ok", os.path.getsize(fn), {k: arrays[k] for k in arrays if k.startswith("noise")})
+    finally:
+        shutil.rmtree(tmp)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only")
+    ap.add_argument("--noise", action="store_true")
+    a = ap.parse_args()
+    for name, spec in CASES.items():
+        if a.only and a.only != name:
+            continue
+        make(name, spec, a.noise)
