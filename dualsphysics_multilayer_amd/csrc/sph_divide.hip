@@ -303,7 +303,7 @@ struct GatherArgs {
   float4* poscell;
   float* press;
   double posminx, posminy, posminz, scelld;
-  float cteb, ovrhopzero, gamma;
+  float cteb, ovrhopzero, gamma, rhopzero;
   int igamma;  // gamma as a small positive integer, else 0
   unsigned dcc;
   int withm1, withpre;
@@ -380,7 +380,7 @@ __device__ __forceinline__ void gather_one(const GatherArgs& a, unsigned i, unsi
     // ComputePress_NN (JSphCpu_Tensors.cpp:40-62 of the v5.0 solver): the phase's rho0, CteB
     // and gamma for fluid particles, the case's for the boundary, in float arithmetic
     // (cteb*(powf(rhop/rho0,gamma)-1)); the power is rounded once from double.
-    float rho0 = 1.f / a.ovrhopzero, cteb = a.cteb, gam = a.gamma;
+    float rho0 = a.rhopzero, cteb = a.cteb, gam = a.gamma;
     int ig = a.igamma;
     if (CodeIsFluid(code)) {
       const float4 e = a.phase_eos[code & CODE_MASKVALUE];
@@ -437,6 +437,7 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
   a.scelld = K.scelld;
   a.cteb = K.cteb;
   a.ovrhopzero = K.ovrhopzero;
+  a.rhopzero = K.rhopzero;
   a.gamma = K.gamma;
   a.igamma = (K.gamma == float(int(K.gamma)) && K.gamma >= 1.f && K.gamma <= 16.f) ? int(K.gamma) : 0;
   a.dcc = K.domcellcode;

@@ -336,16 +336,19 @@ __global__ __launch_bounds__(TB) void k_nn_tiled(DevScalars* __restrict__ sc, co
       b.sw = f.sw;
       nn_pass<TVISCO, TDENSITY, SHIFT, 1>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, b);
       if (act) {
-        // the two CPU passes' stores (JSphCpu_NN_FDA.cpp:278-296); with shifting both store
+        // the two CPU passes' stores (JSphCpu_NN_FDA.cpp:278-296).  With shifting configured
+        // the reference instantiates every interaction with shift=true (the predictor's too,
+        // whose sums ComputeSymplecticPre then ignores), so both passes always store.
+        const bool store = SHIFT || K.shiftmode != 0;
         float ar = 0.f, ax = 0.f, ay = 0.f, az = 0.f, delta = 0.f;
-        if (SHIFT || f.ar != 0.f || f.ax != 0.f || f.ay != 0.f || f.az != 0.f || f.visc != 0.f) {
+        if (store || f.ar != 0.f || f.ax != 0.f || f.ay != 0.f || f.az != 0.f || f.visc != 0.f) {
           if (TDENSITY) delta = (f.delta == FLT_MAX ? FLT_MAX : 0.f + f.delta);
           ar = f.ar;
           ax = f.ax;
           ay = f.ay;
           az = f.az;
         }
-        if (SHIFT || b.ar != 0.f || b.ax != 0.f || b.ay != 0.f || b.az != 0.f || b.visc != 0.f) {
+        if (store || b.ar != 0.f || b.ax != 0.f || b.ay != 0.f || b.az != 0.f || b.visc != 0.f) {
           if (TDENSITY) delta = (delta == FLT_MAX || b.delta == FLT_MAX ? FLT_MAX : delta + b.delta);
           ar += b.ar;
           ax += b.ax;
