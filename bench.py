@@ -45,6 +45,12 @@ PEAK_HBM_GBS = 8000.0
 FLOP_REAL_FLUID_PAIR = 135
 FLOP_REJECTED_CANDIDATE = 22
 FLOP_REAL_BOUND_PAIR = 45  # bound p1: kernel fac + continuity + visc-dt only
+# NN multiphase pair (sph_nn.hip nn_pair, Laminar + FDA, DDT Fourtakas, shifting; counted in
+# DESIGN.md §4b): kernel 8, pressure 9, continuity 9, DDT 16, shifting 5, visc-dt 5, FDA
+# gradient + strain-rate invariant 43, effective viscosity 17, Morris term 10 -> 126; a
+# bound p1 pair (continuity + visc-dt) 25; rejected candidates as above.
+FLOP_NN_PAIR = 126
+FLOP_NN_BOUND_PAIR = 25
 BYTES_PER_PARTICLE_STEP = {1: 356, 2: 712}  # Verlet / Symplectic, SURVEY.md §8(d)
 
 
@@ -86,21 +92,26 @@ def _ref_run(exe: str, case: str, out: str, nsteps: int, threads: int) -> float:
 
 
 def reference_cpu_baseline(dp: float, nsteps: int, threads: int, step: int = 1, ddt: int = 2,
-                           boundary: int = 1, flume: bool = False, first: int = 10) -> dict | None:
+                           boundary: int = 1, flume: bool = False, first: int = 10, nn_width: float = 0.0
+                           ) -> dict | None:
     """Times the REFERENCE CPU solver (oracle/_ref, built from the reference sources)
-    on the same dam break (or wave flume) over the steady step window [first, first+nsteps)
-    (steps 10-110): two runs of `first` and `first+nsteps` steps, the
-    difference of their 'Simulation Runtime' (step loop only, no output) over nsteps."""
+    on the same dam break (or wave flume, or -- nn_width > 0 -- the v5.0 NN solver on the
+    NN wet dam break) over the step window [first, first+nsteps) (steps
+    10-110): two runs of `first` and `first+nsteps` steps, the difference of their
+    'Simulation Runtime' (step loop only, no output) over nsteps."""
     ref = os.path.join(ROOT, "oracle", "_ref")
-    exe = os.path.join(ref, "DualSPHysics5.2CPU_ref")
-    gen = os.path.join(ref, "genflume_ref" if flume else "gencase_ref")
-    name = "CaseFlume" if flume else "CaseDambreak"
+    exe = os.path.join(ref, "DualSPHysics5.0NN_CPU_ref" if nn_width else "DualSPHysics5.2CPU_ref")
+    gen = os.path.join(ref, "gennn_ref" if nn_width else "genflume_ref" if flume else "gencase_ref")
+    name = "CaseNN" if nn_width else "CaseFlume" if flume else "CaseDambreak"
     if not (os.path.exists(exe) and os.path.exists(gen)):
         return None
     tmp = tempfile.mkdtemp(prefix="sphref_")
     try:
-        out = subprocess.run([gen, repr(dp), tmp, str(step), str(ddt), "1.5", name, str(boundary)],
-                             capture_output=True, text=True, check=True).stdout
+        if nn_width:
+            args = [gen, repr(dp), tmp, repr(nn_width), "1", "5", name]
+        else:
+            args = [gen, repr(dp), tmp, str(step), str(ddt), "1.5", name, str(boundary)]
+        out = subprocess.run(args, capture_output=True, text=True, check=True).stdout
         np_ = int(re.search(r"np=(\d+)", out).group(1))
         case = os.path.join(tmp, name)
         t_a = _ref_run(exe, case, os.path.join(tmp, "a"), first, threads)
@@ -108,10 +119,12 @@ def reference_cpu_baseline(dp: float, nsteps: int, threads: int, step: int = 1, 
         sec = t_b - t_a
         return {"value": np_ * nsteps / sec, "unit": "particle-steps/s", "cores": threads, "kind": "reference",
                 "window_steps": [first, first + nsteps], "window_seconds": sec,
-                "sample": "reference DualSPHysics5.2 CPU (built from /root/reference sources, -O3 -fopenmp "
+                "sample": "reference %s CPU (built from /root/reference sources, -O3 -fopenmp "
                           "-ffast-math), %d-particle %s (%s), %s, steps %d-%d (Simulation Runtime of a %d-step "
                           "run minus that of a %d-step run), -ompthreads:%d"
-                          % (np_, "wave flume" if flume else "dam break", "mDBC" if boundary == 2 else "DBC",
+                          % ("DualSPHysics5.0 NNewtonian" if nn_width else "DualSPHysics5.2", np_,
+                             "NN 3-phase wet dam break" if nn_width else "wave flume" if flume else "dam break",
+                             "mDBC" if boundary == 2 else "DBC",
                              "Verlet" if step == 1 else "Symplectic", first, first + nsteps, first + nsteps,
                              first, threads)}
     except Exception as e:  # noqa: BLE001
@@ -159,6 +172,7 @@ def profiled_traffic(kernel_prefix: str, np_: int, workload: str):
 CFG2_DP, CFG2_NP = 0.0045, 1025964
 CFG3_DP = 0.00205  # 9,969,118 particles (BASELINE cfg3: ~10M)
 CFG4_DP = 0.00265  # 4,007,978 particles (BASELINE cfg4: wave flume ~4M)
+CFG5_DP, CFG5_WIDTH = 0.01, 0.70  # ~2.0M particles (BASELINE cfg5: NN multiphase 2M), the example's dp
 
 
 def weak_dp(target_np: int) -> float:
@@ -180,7 +194,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=("cfg2", "cfg3", "cfg4"), default="cfg2")
+    ap.add_argument("--workload", choices=("cfg2", "cfg3", "cfg4", "cfg5"), default="cfg2")
     ap.add_argument("--dp", type=float, default=None, help="override the particle spacing")
     ap.add_argument("--boundary", choices=("dbc", "mdbc"), default=None,
                     help="boundary conditions (mdbc: modified DBC, Vel0, normals to the wall limit)")
@@ -208,7 +222,7 @@ def main() -> None:
         os.environ.setdefault("MASTER_PORT", "29517")
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    from dualsphysics_multilayer_amd.case import DamBreakCase, WaveFlumeCase
+    from dualsphysics_multilayer_amd.case import DamBreakCase, WaveFlumeCase, WetDambreakNNCase
     from dualsphysics_multilayer_amd.core import SphGpuSingle, SphGpuSlab, comm_unique_id, slab_partition
 
     if args.workload == "cfg2":
@@ -217,9 +231,12 @@ def main() -> None:
     elif args.workload == "cfg3":
         dp = args.dp or CFG3_DP
         case = DamBreakCase(dp, step_algorithm=2, tdensity=1, tboundary=2 if args.boundary == "mdbc" else 1)
-    else:
+    elif args.workload == "cfg4":
         dp = args.dp or CFG4_DP
         case = WaveFlumeCase(dp, tboundary=2 if args.boundary == "mdbc" else 1)
+    else:
+        dp = args.dp or CFG5_DP
+        case = WetDambreakNNCase(dp, width=CFG5_WIDTH)
     bounds = None
     s = None
     wall = {}
@@ -285,15 +302,17 @@ def main() -> None:
     if rank == 0:
         pairs = (pairs0.astype("float64") + pairs1.astype("float64")) / 2.0
         ff_chk, ff_real, fb_chk, fb_real, bf_chk, bf_real = pairs
-        flops = (FLOP_REAL_FLUID_PAIR * (ff_real + fb_real) + FLOP_REJECTED_CANDIDATE * (ff_chk - ff_real + fb_chk - fb_real)
-                 + FLOP_REAL_BOUND_PAIR * bf_real + FLOP_REJECTED_CANDIDATE * (bf_chk - bf_real))
+        nn = args.workload == "cfg5"
+        fpair, fbound = (FLOP_NN_PAIR, FLOP_NN_BOUND_PAIR) if nn else (FLOP_REAL_FLUID_PAIR, FLOP_REAL_BOUND_PAIR)
+        flops = (fpair * (ff_real + fb_real) + FLOP_REJECTED_CANDIDATE * (ff_chk - ff_real + fb_chk - fb_real)
+                 + fbound * bf_real + FLOP_REJECTED_CANDIDATE * (bf_chk - bf_real))
         inter_ms = float(phase_ms[0])
         achieved = flops / (inter_ms * 1e-3) / 1e12 if inter_ms > 0 else None
         value = units / elapsed
         hbm_achieved = value * BYTES_PER_PARTICLE_STEP[case.step_algorithm] / 1e9
-        traffic = profiled_traffic("sphx::k_fluid_tiled<%d, %s>" % (case.tdensity, "true" if getattr(
-            case, "floatings", None) else "false"), case.np,
-                                   "BASELINE " + args.workload) if world == 1 else None
+        kname = ("sphx::k_nn_tiled<%d, %d, true>" % (case.tvisco, case.tdensity) if nn else
+                 "sphx::k_fluid_tiled<%d, %s>" % (case.tdensity, "true" if getattr(case, "floatings", None) else "false"))
+        traffic = profiled_traffic(kname, case.np, "BASELINE " + args.workload) if world == 1 else None
         res = {
             "metric": METRIC,
             "value": value,
@@ -308,6 +327,8 @@ def main() -> None:
             "dtype": "f32 (f64 positions/time integration)",
             "data": ("synthetic: generated wave-flume lattice (case.py WaveFlumeCase = oracle/tools/genflume_ref)"
                      if args.workload == "cfg4" else
+                     "synthetic: the NN wet dam break example extruded to 3D (case.py WetDambreakNNCase = "
+                     "oracle/tools/gennn_ref)" if nn else
                      "synthetic: generated 3D dam-break lattice (SURVEY.md §8(c) recipe)"),
             "config": {
                 "workload": (("BASELINE cfg2: 3D dam break, %d particles (dp=%g), Verlet, Wendland, artificial "
@@ -319,7 +340,11 @@ def main() -> None:
                              ("BASELINE cfg4: wave flume, %d particles (dp=%g): piston mvrectsinu + flap mvrotsinu "
                               "moving boundaries, floating box (RigidAlgorithm=1, %d particles), %s, Verlet, "
                               "Wendland, artificial viscosity 0.1, DDT2 0.1, CFL 0.2"
-                              % (case.np, dp, case.case_nfloat, args.boundary.upper()))),
+                              % (case.np, dp, case.case_nfloat, args.boundary.upper())) if args.workload == "cfg4" else
+                             ("BASELINE cfg5: NN multiphase (v5.0 NNewtonian solver), 3-phase wet dam break extruded to "
+                              "3D, %d particles (dp=%g, width %g m), Symplectic, Wendland, FDA velocity gradients, "
+                              "Laminar viscosity with the HBP effective viscosity, DDT Fourtakas full 0.1, shifting "
+                              "Full (-10, TFS 2.75), CFL 0.1, RelaxationDt 0.2" % (case.np, dp, CFG5_WIDTH))),
                 "np": case.np,
                 "npb": case.npb,
                 "parallelism": (("slab-x%d (RCCL halo + migration, max-allreduce dt)" % world) if bounds is not None
@@ -328,7 +353,9 @@ def main() -> None:
                 "owned_np_per_rank": per_rank_np,
             },
             "roofline": {
-                "kernel": (("k_fluid_tiled<tdensity=%d, floating records> (Interaction_Forces)"
+                "kernel": ("k_nn_tiled<tvisco=%d, tdensity=%d> (Interaction_Forces NN)" % (case.tvisco, case.tdensity)
+                           if nn else
+                           ("k_fluid_tiled<tdensity=%d, floating records> (Interaction_Forces)"
                             if getattr(case, "floatings", None) else "k_fluid_tiled<tdensity=%d> (Interaction_Forces)")
                            % case.tdensity),
                 "bound": "mfma",
@@ -364,12 +391,16 @@ def main() -> None:
         if not args.no_cpu_baseline and world == 1:
             threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), 64)
             t_cpu = time.perf_counter()
-            cb = reference_cpu_baseline(dp, args.cpu_steps, threads, case.step_algorithm, case.tdensity,
-                                        case.tboundary, flume=args.workload == "cfg4")
-            if cb is None:
+            if nn:  # the v5.0 NN CPU solver runs ~3 s per step at 2M particles: a bounded sample
+                cb = reference_cpu_baseline(dp, min(args.cpu_steps, 6), threads, nn_width=CFG5_WIDTH, first=1)
+            else:
+                cb = reference_cpu_baseline(dp, args.cpu_steps, threads, case.step_algorithm, case.tdensity,
+                                            case.tboundary, flume=args.workload == "cfg4")
+            if cb is None and not nn:  # the oracle restates the single-phase solver only
                 cb = port_cpu_baseline(case, min(args.cpu_steps, 10), threads)
-            cb["gpu_over_cpu"] = value / cb["value"]
-            cb["host"] = host_info(threads)
+            if cb is not None:
+                cb["gpu_over_cpu"] = value / cb["value"]
+                cb["host"] = host_info(threads)
             res["cpu_baseline"] = cb
             wall["cpu_baseline_s"] = time.perf_counter() - t_cpu
         wall["process_s"] = time.perf_counter() - T_START
