@@ -202,6 +202,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=100,
                     help="reference CPU steps timed (window 10 .. 10+K, BASELINE.md: 10-110)")
+    ap.add_argument("--repartition", type=int, default=20,
+                    help="N>1: re-balance the slab bounds every K steps when the load is >5%% off (0: never)")
     ap.add_argument("--force-slab", action="store_true",
                     help="run the N>1 code path (gloo bootstrap + RCCL slab) even with one rank")
     args = ap.parse_args()
@@ -250,6 +252,8 @@ def main() -> None:
             ids = [comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(ids, src=0)
             s = SphGpuSlab(case, rank, world, bounds, ids[0], device=local)
+            if args.repartition and world > 1:
+                s.set_repartition(args.repartition, args.bound_weight, 0.05)
             s.run(args.warmup)
             s.sync()
             ok = torch.tensor([1], dtype=torch.int32)
@@ -288,6 +292,7 @@ def main() -> None:
 
     units = float(st["np"]) * args.steps
     per_rank_np = [int(st["np"])]
+    slab_info = None
     if dist is not None:
         import torch
 
@@ -297,7 +302,9 @@ def main() -> None:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         nps = [None] * world
         dist.all_gather_object(nps, int(st["np"]))
-        elapsed, units, per_rank_np = float(tmax.item()), float(tot.item()), nps
+        infos = [None] * world
+        dist.all_gather_object(infos, s.slab_info() if bounds is not None else None)
+        elapsed, units, per_rank_np, slab_info = float(tmax.item()), float(tot.item()), nps, infos
 
     if rank == 0:
         pairs = (pairs0.astype("float64") + pairs1.astype("float64")) / 2.0
@@ -350,6 +357,8 @@ def main() -> None:
                 "parallelism": (("slab-x%d (RCCL halo + migration, max-allreduce dt)" % world) if bounds is not None
                                 else "single"),
                 "slab_bounds_cells": None if bounds is None else [int(b) for b in bounds],
+                "slab_repartition_every": args.repartition if bounds is not None and world > 1 else None,
+                "slab_final_info": slab_info,
                 "owned_np_per_rank": per_rank_np,
             },
             "roofline": {

@@ -240,6 +240,18 @@ class SphSlabDef(C.Structure):
     ]
 
 
+class SphSlabInfo(C.Structure):
+    _fields_ = [
+        ("rank", C.c_int32),
+        ("nranks", C.c_int32),
+        ("cx_begin", C.c_int32),
+        ("cx_end", C.c_int32),
+        ("repartitions", C.c_uint32),
+        ("pad", C.c_uint32),
+        ("last_imbalance", C.c_double),
+    ]
+
+
 class SphPartHeader(C.Structure):
     _fields_ = [
         ("app_name", C.c_char * 64),

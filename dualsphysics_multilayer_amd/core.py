@@ -26,6 +26,7 @@ from ._abi import (
     SphRunStats,
     SphPartHeader,
     SphSlabDef,
+    SphSlabInfo,
     SphFloatingDef,
     SphFloatingState,
     SphMotionEvent,
@@ -68,6 +69,9 @@ EXPORTED_SYMBOLS = (
     "sph_slab_group_destroy",
     "sph_slab_group_run",
     "sph_slab_group_member",
+    "sph_slab_set_repartition",
+    "sph_slab_group_set_repartition",
+    "sph_slab_info",
     "sph_part_read",
     "sph_part_write",
     "sph_part_head_write",
@@ -125,6 +129,9 @@ def load_library(path: str = LIB_PATH):
     L.sph_slab_group_destroy.argtypes = [vp]
     L.sph_slab_group_run.argtypes = [vp, C.c_uint32]
     L.sph_slab_group_member.argtypes = [vp, C.c_int, C.POINTER(vp)]
+    L.sph_slab_set_repartition.argtypes = [vp, C.c_uint32, C.c_double, C.c_double]
+    L.sph_slab_group_set_repartition.argtypes = [vp, C.c_uint32, C.c_double, C.c_double]
+    L.sph_slab_info.argtypes = [vp, C.POINTER(SphSlabInfo)]
     L.sph_part_read.argtypes = [C.c_char_p, C.POINTER(SphPartHeader), vp]
     L.sph_part_write.argtypes = [C.c_char_p, C.POINTER(SphPartHeader), vp]
     L.sph_bi4_rewrite.argtypes = [C.c_char_p, C.c_char_p]
@@ -290,6 +297,16 @@ class SphGpuSingle:
     def set_timing(self, on: bool) -> None:
         _check(load_library().sph_solver_set_timing(self._h, int(on)))
 
+    def slab_info(self) -> dict:
+        """Current owned columns of a slab, re-partitions so far, last measured imbalance."""
+        out = SphSlabInfo()
+        _check(load_library().sph_slab_info(self._h, C.byref(out)))
+        return {k: getattr(out, k) for k, _ in SphSlabInfo._fields_ if k != "pad"}
+
+    def set_repartition(self, every: int, bound_weight: float = 0.3, tolerance: float = 0.05) -> None:
+        """Slabs: re-balance the column bounds every `every` steps (collective)."""
+        _check(load_library().sph_slab_set_repartition(self._h, every, bound_weight, tolerance))
+
     def timing(self) -> tuple[np.ndarray, int]:
         ms = np.zeros(4, np.float64)
         n = C.c_uint64()
@@ -403,6 +420,13 @@ class SphSlabGroup:
 
     def stats(self) -> list:
         return [m.stats() for m in self.members]
+
+    def set_repartition(self, every: int, bound_weight: float = 0.3, tolerance: float = 0.05) -> None:
+        """Re-balance the slabs' column bounds every `every` steps."""
+        _check(load_library().sph_slab_group_set_repartition(self._h, every, bound_weight, tolerance))
+
+    def slab_info(self) -> list:
+        return [m.slab_info() for m in self.members]
 
     def particles(self) -> dict:
         """Owned particles of all slabs, merged and sorted by idp."""

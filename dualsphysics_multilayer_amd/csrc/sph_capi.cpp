@@ -234,6 +234,33 @@ int sph_slab_group_run(SphSlabGroup* g, uint32_t nsteps) {
   return guard([&] { g->impl->Run(nsteps); });
 }
 
+int sph_slab_set_repartition(SphSolver* s, uint32_t every, double bound_weight, double tolerance) {
+  NEED(s);
+  NOT_MEMBER(s);
+  return guard([&] { s->impl->SetRepartition(every, bound_weight, tolerance); });
+}
+
+int sph_slab_group_set_repartition(SphSlabGroup* g, uint32_t every, double bound_weight, double tolerance) {
+  NEED(g);
+  return guard([&] {
+    for (auto& m : g->impl->slabs) m->SetRepartition(every, bound_weight, tolerance);
+  });
+}
+
+int sph_slab_info(SphSolver* s, SphSlabInfo* out) {
+  NEED(s && out);
+  return guard([&] {
+    const sphx::SlabConfig c = s->impl->Slab();
+    std::memset(out, 0, sizeof(*out));
+    out->rank = c.rank;
+    out->nranks = c.nranks;
+    out->cx_begin = c.c0;
+    out->cx_end = c.c1;
+    out->repartitions = s->impl->RepartitionCount();
+    out->last_imbalance = s->impl->LastImbalance();
+  });
+}
+
 int sph_slab_group_member(SphSlabGroup* g, int i, SphSolver** out) {
   NEED(g && out && i >= 0 && size_t(i) < g->members.size());
   *out = &g->members[size_t(i)];

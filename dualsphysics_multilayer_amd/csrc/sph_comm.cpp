@@ -31,7 +31,24 @@ class RcclTransport final : public SlabTransport {
     check_nccl(ncclCommInitRank(&comm_, n, u, r), "ncclCommInitRank");
   }
   ~RcclTransport() override {
-    if (comm_) ncclCommDestroy(comm_);
+    if (comm_) (aborted_ ? ncclCommAbort(comm_) : ncclCommDestroy(comm_));
+    if (gather_) (void)hipFree(gather_);
+  }
+  void group_begin() override { check_nccl(ncclGroupStart(), "ncclGroupStart"); }
+  void group_end() override { check_nccl(ncclGroupEnd(), "ncclGroupEnd"); }
+  void check_async() override {
+    if (!comm_) throw SphError(SPH_ERR_COMM, "RCCL communicator aborted");
+    ncclResult_t st = ncclSuccess;
+    check_nccl(ncclCommGetAsyncError(comm_, &st), "ncclCommGetAsyncError");
+    if (st != ncclSuccess && st != ncclInProgress)
+      throw SphError(SPH_ERR_COMM, std::string("RCCL asynchronous error: ") + ncclGetErrorString(st));
+  }
+  void abort() override {
+    if (comm_ && !aborted_) {
+      aborted_ = true;
+      (void)ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
   }
   void exchange(const void* sl, size_t nsl, const void* sr, size_t nsr, void* rl, size_t nrl, void* rr, size_t nrr,
                 hipStream_t s) override {
@@ -51,12 +68,25 @@ class RcclTransport final : public SlabTransport {
   void allreduce_max_u32(unsigned* d, int n, hipStream_t s) override {
     check_nccl(ncclAllReduce(d, d, size_t(n), ncclUint32, ncclMax, comm_, s), "ncclAllReduce");
   }
+  // All-gather + a rank-ordered sum on the device: the same additions, in the same order,
+  // as LocalTransport's host sum (ncclAllReduce's reduction order is the library's).
   void allreduce_sum_f32(float* d, int n, hipStream_t s) override {
-    check_nccl(ncclAllReduce(d, d, size_t(n), ncclFloat, ncclSum, comm_, s), "ncclAllReduce sum");
+    const size_t need = size_t(n) * size_t(nranks);
+    if (need > gathercap_) {
+      check_hip(hipStreamSynchronize(s), "allreduce: sync");
+      if (gather_) check_hip(hipFree(gather_), "hipFree");
+      gathercap_ = need;
+      check_hip(hipMalloc((void**)&gather_, sizeof(float) * gathercap_), "hipMalloc allreduce scratch");
+    }
+    check_nccl(ncclAllGather(d, gather_, size_t(n), ncclFloat, comm_, s), "ncclAllGather");
+    launch_rank_ordered_sum(s, gather_, n, nranks, d);
   }
 
  private:
   ncclComm_t comm_ = nullptr;
+  bool aborted_ = false;
+  float* gather_ = nullptr;
+  size_t gathercap_ = 0;
 };
 
 std::unique_ptr<SlabTransport> make_rccl_transport(const unsigned char id[128], int rank, int nranks) {

@@ -1,6 +1,6 @@
 // sph_comm.hpp — transports of the slab decomposition.
 //
-// A slab talks only to its two x-neighbours (rank-1, rank+1) plus one 3-value
+// A slab talks only to its two x-neighbours (rank-1, rank+1) plus one 4-value
 // max-allreduce per dt.  Two implementations behind one interface:
 //   * RcclTransport: one process per GPU, RCCL (ncclSend/ncclRecv in a group, point to
 //     point over xGMI; ncclAllReduce max) on the solver's stream — the product path;
@@ -29,8 +29,17 @@ class SlabTransport {
                         size_t nrr, hipStream_t s) = 0;
   // In-place max over ranks of n uint32 values in device memory.
   virtual void allreduce_max_u32(unsigned* d, int n, hipStream_t s) = 0;
-  // In-place sum over ranks of n floats in device memory (floating-body force sums).
+  // In-place sum over ranks of n floats in device memory (floating-body force sums,
+  // column counts of the re-partition), added in rank order from 0.f so that both
+  // transports give the same bits.
   virtual void allreduce_sum_f32(float* d, int n, hipStream_t s) = 0;
+  // Several exchanges fused into one transfer group (RCCL: ncclGroupStart/End).
+  virtual void group_begin() {}
+  virtual void group_end() {}
+  // Raise SphError if the transport failed asynchronously (RCCL: ncclCommGetAsyncError).
+  virtual void check_async() {}
+  // Tear the transport down after an error (RCCL: ncclCommAbort); later calls fail.
+  virtual void abort() {}
   int rank = 0, nranks = 1;
   bool has_left() const { return rank > 0; }
   bool has_right() const { return rank + 1 < nranks; }

@@ -35,6 +35,10 @@ __global__ __launch_bounds__(256) void k_presort(const DevScalars* __restrict__ 
     return;
   }
   const unsigned cx = DcelCellx(dcc, rcell) - unsigned(g.xoff), cy = DcelCelly(dcc, rcell), cz = DcelCellz(dcc, rcell);
+  if (rcell != DCELL_OUT && (g.xown0 != 0 || g.xown1 != g.ncx) && cx >= unsigned(g.ncx)) {
+    keys[p] = g.boxdiscard;  // slab: a migrant handed over beyond this slab's ghost columns (re-partition)
+    return;
+  }
   const unsigned cellsort = cx + cy * unsigned(g.ncx) + cz * g.nsheet;
   const typecode rcode = code[p];
   const typecode codetype = CodeType(rcode), codeout = CodeSpecial(rcode);

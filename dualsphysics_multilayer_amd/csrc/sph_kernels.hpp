@@ -242,7 +242,9 @@ void launch_ft_body(hipStream_t stm, DevScalars* sc, const KConst& K, FtBody* bo
                     const unsigned* ftridp, unsigned nftp, const PartArrays& a, bool predictor, const float* part);
 
 // ---- slab decomposition (sph_slab.hip) ----
-// A particle MIGRATING to a neighbour: its full state, 96 B.
+// A particle MIGRATING to a neighbour: its full state, 112 B.  A boundary particle also
+// carries its mDBC normal (kept by idp, turned with moving objects by its owner), so the
+// new owner continues with the turned normal (JSphCpu.cpp:1724-1728).
 struct SlabRec {
   double2 posxy;
   double posz;
@@ -253,6 +255,7 @@ struct SlabRec {
   double poszpre;
   unsigned short code, flags;
   unsigned pad;
+  float4 normal;  // mDBC normal of a boundary particle (idp < nbound), else 0
 };
 // A GHOST copy for a neighbour: what a neighbour of the interaction needs, 40 B.  The
 // position travels as the float offset from its (global) cell origin, i.e. exactly the
@@ -288,10 +291,17 @@ struct SlabSendBufs {
 // left/right).  has_left/has_right: the neighbour exists.
 void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, DivGrid g, const KConst& K,
                       const double dom_posmin[3], bool has_left, bool has_right, bool withm1, bool withpre,
-                      unsigned* tilecnt, SlabCounts* cnt, SlabSendBufs bufs);
+                      unsigned* tilecnt, SlabCounts* cnt, SlabSendBufs bufs, const float4* normal = nullptr,
+                      unsigned nbound = 0);
+// out[i] = (((0 + g[0][i]) + g[1][i]) + ...) over nranks rows of n floats (rank order).
+void launch_rank_ordered_sum(hipStream_t stm, const float* gathered, int n, int nranks, float* out);
+// Owned particles per GLOBAL x-column: counts[c] fluid (incl. floating), counts[ncxg + c]
+// boundary (the re-partition's weights), as floats (exact integers).
+void launch_column_counts(hipStream_t stm, unsigned cap, const DevScalars* sc, const PartArrays& a, DivGrid g,
+                          const KConst& K, int ncxg, float* counts);
 // Append nm received migrants at [np, np+nm) and ng ghosts after them; set sc->np, sc->nown.
 void launch_slab_unpack(hipStream_t stm, DevScalars* sc, const SlabRec* mig, unsigned nm, const SlabGhost* gh,
                         unsigned ng, unsigned np, const PartArrays& a, const KConst& K, const double dom_posmin[3],
-                        bool withm1, bool withpre, SlabCounts* cnt);
+                        bool withm1, bool withpre, SlabCounts* cnt, float4* normal = nullptr, unsigned nbound = 0);
 
 }  // namespace sphx

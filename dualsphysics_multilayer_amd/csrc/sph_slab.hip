@@ -31,6 +31,8 @@ struct PackArgs {
   unsigned ntiles;
   SlabCounts* cnt;
   SlabSendBufs b;
+  const float4* normal;  // mDBC normals by idp (nullptr without mDBC)
+  unsigned nbound;
 };
 
 // bit 0: record for the left neighbour, bit 1: record for the right, bit 2: stays owned
@@ -164,6 +166,7 @@ __device__ __forceinline__ void write_migrant(const PackArgs& q, unsigned p, Sla
   r.code = q.a.code[p];
   r.flags = 0;
   r.pad = 0;
+  r.normal = (q.normal && r.idp < q.nbound) ? q.normal[r.idp] : make_float4(0.f, 0.f, 0.f, 0.f);
   *dst = r;
 }
 
@@ -211,7 +214,8 @@ __global__ __launch_bounds__(PK_BS) void k_pack_write(const DevScalars* __restri
 
 void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, DivGrid g, const KConst& K,
                       const double dom_posmin[3], bool has_left, bool has_right, bool withm1, bool withpre,
-                      unsigned* tilecnt, SlabCounts* cnt, SlabSendBufs bufs) {
+                      unsigned* tilecnt, SlabCounts* cnt, SlabSendBufs bufs, const float4* normal,
+                      unsigned nbound) {
   PackArgs q;
   q.a = a;
   q.g = g;
@@ -228,6 +232,8 @@ void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartA
   q.ntiles = (cap + PK_TILE - 1) / PK_TILE;
   q.cnt = cnt;
   q.b = bufs;
+  q.normal = normal;
+  q.nbound = nbound;
   hipLaunchKernelGGL(k_pack_count, dim3(q.ntiles), dim3(PK_BS), 0, stm, sc, q);
   hipLaunchKernelGGL(k_pack_scan, dim3(1), dim3(1024), 0, stm, sc, q);
   hipLaunchKernelGGL(k_pack_write, dim3(q.ntiles), dim3(PK_BS), 0, stm, sc, q);
@@ -243,6 +249,8 @@ struct UnpackArgs {
   double posminx, posminy, posminz, scelld;
   int withm1, withpre;
   SlabCounts* cnt;
+  float4* normal;
+  unsigned nbound;
 };
 
 __global__ __launch_bounds__(256) void k_unpack(UnpackArgs u) {
@@ -264,6 +272,7 @@ __global__ __launch_bounds__(256) void k_unpack(UnpackArgs u) {
       a.posxypre[p] = r.posxypre;
       a.poszpre[p] = r.poszpre;
     }
+    if (u.normal && r.idp < u.nbound) u.normal[r.idp] = r.normal;  // the owner's turned normal
   } else {
     const SlabGhost r = u.gh[i - u.nm];
     const double ox = u.posminx + double(DcelCellx(u.dcc, r.dcell)) * u.scelld;
@@ -286,8 +295,10 @@ __global__ void k_unpack_finish(DevScalars* __restrict__ sc, const SlabCounts* _
 
 void launch_slab_unpack(hipStream_t stm, DevScalars* sc, const SlabRec* mig, unsigned nm, const SlabGhost* gh,
                         unsigned ng, unsigned np, const PartArrays& a, const KConst& K, const double dom_posmin[3],
-                        bool withm1, bool withpre, SlabCounts* cnt) {
+                        bool withm1, bool withpre, SlabCounts* cnt, float4* normal, unsigned nbound) {
   UnpackArgs u;
+  u.normal = normal;
+  u.nbound = nbound;
   u.a = a;
   u.mig = mig;
   u.gh = gh;
@@ -304,6 +315,47 @@ void launch_slab_unpack(hipStream_t stm, DevScalars* sc, const SlabRec* mig, uns
   u.cnt = cnt;
   if (nm + ng) hipLaunchKernelGGL(k_unpack, dim3((nm + ng + 255) / 256), dim3(256), 0, stm, u);
   hipLaunchKernelGGL(k_unpack_finish, dim3(1), dim3(1), 0, stm, sc, cnt, np, nm, ng);
+}
+
+// ---------------------------------------------------------------------------------
+__global__ void k_rank_ordered_sum(const float* __restrict__ g, int n, int nranks, float* __restrict__ out) {
+  const int i = int(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= n) return;
+  float v = 0.f;
+  for (int r = 0; r < nranks; r++) v = __fadd_rn(v, g[size_t(r) * size_t(n) + size_t(i)]);
+  out[i] = v;
+}
+
+void launch_rank_ordered_sum(hipStream_t stm, const float* gathered, int n, int nranks, float* out) {
+  if (n > 0) hipLaunchKernelGGL(k_rank_ordered_sum, dim3((n + 255) / 256), dim3(256), 0, stm, gathered, n, nranks, out);
+}
+
+// Owned particles per global column (u32 atomics in LDS-free global memory: integer counts
+// are order independent, so every run and every rank sees the same numbers).
+__global__ __launch_bounds__(256) void k_column_counts(const DevScalars* __restrict__ sc, PartArrays a, DivGrid g,
+                                                       unsigned dcc, int ncxg, unsigned* __restrict__ cnt) {
+  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= sc->np) return;
+  const unsigned dc = a.dcell[p];
+  if (dc == DCELL_DISCARD || dc == DCELL_OUT) return;
+  const int gcx = int(DcelCellx(dcc, dc));
+  const int lcx = gcx - g.xoff;
+  if (lcx < g.xown0 || lcx >= g.xown1 || gcx >= ncxg) return;  // ghosts are counted by their owner
+  const bool fluid = CodeType(a.code[p]) >= CODE_TYPE_FLOATING;
+  atomicAdd(&cnt[(fluid ? 0 : ncxg) + gcx], 1u);
+}
+
+__global__ void k_counts_to_float(unsigned* __restrict__ c, int n) {
+  const int i = int(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i < n) reinterpret_cast<float*>(c)[i] = float(c[i]);
+}
+
+void launch_column_counts(hipStream_t stm, unsigned cap, const DevScalars* sc, const PartArrays& a, DivGrid g,
+                          const KConst& K, int ncxg, float* counts) {
+  unsigned* c = reinterpret_cast<unsigned*>(counts);
+  (void)hipMemsetAsync(c, 0, sizeof(unsigned) * 2 * size_t(ncxg), stm);
+  hipLaunchKernelGGL(k_column_counts, dim3((cap + 255) / 256), dim3(256), 0, stm, sc, a, g, K.domcellcode, ncxg, c);
+  hipLaunchKernelGGL(k_counts_to_float, dim3((2 * ncxg + 255) / 256), dim3(256), 0, stm, c, 2 * ncxg);
 }
 
 }  // namespace sphx

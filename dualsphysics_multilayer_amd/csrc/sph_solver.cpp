@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <exception>
 #include <thread>
 
@@ -269,6 +270,24 @@ static std::vector<unsigned> initial_columns(const SphConstants& C, const SphPar
   return cx;
 }
 
+// Column bounds b[0..nranks] at the quantiles of the weight prefix pre[0..ncx] (each slab
+// at least one column; a bound column goes to the side closer to its target).
+void partition_from_prefix(const std::vector<double>& pre, int nranks, int* b) {
+  const int ncx = int(pre.size()) - 1;
+  b[0] = 0;
+  b[nranks] = ncx;
+  int c = 0;
+  for (int r = 1; r < nranks; r++) {
+    const double target = pre[size_t(ncx)] * double(r) / double(nranks);
+    while (c < ncx && pre[size_t(c)] < target) c++;
+    int cut = c;
+    if (cut > 0 && target - pre[size_t(cut) - 1] < pre[size_t(cut)] - target) cut--;
+    cut = std::max(cut, b[r - 1] + 1);
+    cut = std::min(cut, ncx - (nranks - r));
+    b[r] = cut;
+  }
+}
+
 void slab_partition(const SphCaseDef& cdef, const SphParticlesHost& all, int nranks, double bound_weight, int* b) {
   SphConstants C;
   derive_constants(cdef, C);
@@ -280,19 +299,7 @@ void slab_partition(const SphCaseDef& cdef, const SphParticlesHost& all, int nra
   for (unsigned p = 0; p < all.n; p++) w[std::min<unsigned>(cx[p], unsigned(ncx - 1))] += (p < cdef.npb ? bound_weight : 1.0);
   std::vector<double> pre(size_t(ncx) + 1, 0.0);
   for (int c = 0; c < ncx; c++) pre[size_t(c) + 1] = pre[size_t(c)] + w[size_t(c)];
-  b[0] = 0;
-  b[nranks] = ncx;
-  int c = 0;
-  for (int r = 1; r < nranks; r++) {
-    const double target = pre[size_t(ncx)] * double(r) / double(nranks);
-    while (c < ncx && pre[size_t(c)] < target) c++;
-    // the boundary column goes to the side that leaves the split closer to the target
-    int cut = c;
-    if (cut > 0 && target - pre[size_t(cut) - 1] < pre[size_t(cut)] - target) cut--;
-    cut = std::max(cut, b[r - 1] + 1);
-    cut = std::min(cut, ncx - (nranks - r));
-    b[r] = cut;
-  }
+  partition_from_prefix(pre, nranks, b);
 }
 
 SphGpuSingle::SphGpuSingle(const SphCaseDef& cdef, const SphParticlesHost& init, int dev) : device(dev) {
@@ -341,7 +348,11 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   const unsigned n = unsigned(sel.size());
   cap_ = slab() ? n + std::max(n / 2, 65536u) : n;
   keybits_ = bits_for(G.boxdiscard, 1);
+  // grid-sized buffers hold the widest grid a slab can get from a re-partition (all
+  // columns + the two ghost columns), so they never move
+  nctmax_ = slab() ? unsigned(C.dom_cells[0] + 2) * unsigned(G.ncy) * unsigned(G.ncz) : G.nct;
   if (const char* e = std::getenv("SPH_INTERACTION")) tiled_ = std::string(e) != "simple";
+  if (const char* e = std::getenv("SPH_COMM_TIMEOUT_S")) comm_timeout_s_ = std::max(1.0, std::atof(e));
   // The tiled kernel stages the 3x3 rows of 3 cells of CellMode=full; half runs the
   // one-lane-per-particle kernel over its 5x5 rows of 5 cells.
   if (C.scelldiv != 1) tiled_ = false;
@@ -392,7 +403,10 @@ void SphGpuSingle::AllocFixed() {
     allocs_.push_back(p);
     return p;
   };
-  begincell_ = (unsigned*)dmalloc(4 * size_t(G.nctt));
+  begincell_ = (unsigned*)dmalloc(4 * (2 * size_t(nctmax_) + 6));
+  if (slab()) {  // re-partition: column counts [2 ncx] + the ranks' bounds [nranks + 1]
+    colcnt_ = (float*)dmalloc(4 * (2 * size_t(C.dom_cells[0]) + size_t(slabcfg_.nranks) + 1));
+  }
   rowtmp_ = (unsigned*)dmalloc(4 * 2 * size_t(G.ncy) * size_t(G.ncz));
   qctr_ = (unsigned*)dmalloc(4 * 16);
   check_hip(hipMemset(qctr_, 0, 4 * 16), "zero work counters");
@@ -456,7 +470,7 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
   press_ = (float*)dmalloc(4 * n);
   // Interaction items (launch_items): an item holds TB particles unless it ends a row
   // (<= 2 per row: fluid and bound) or reaches TMAXCELLS = 4 cells (<= 1 per 4 cells).
-  items_ = (uint4*)dmalloc(16 * (n / 128 + 2 * size_t(G.ncy) * size_t(G.ncz) + size_t(G.nct) / 2 + 2));
+  items_ = (uint4*)dmalloc(16 * (n / 128 + 2 * size_t(G.ncy) * size_t(G.ncz) + size_t(nctmax_) / 2 + 2));
   arace_ = (float4*)dmalloc(16 * n);
   if (shift_) shiftpos_ = (float4*)dmalloc(16 * n);  // the interaction's shifting sums
   for (int i = 0; i < 2; i++) {
@@ -674,7 +688,7 @@ void SphGpuSingle::Exchange() {
   if (!hl && !hr) return;  // a slab alone holds the whole domain: no ghosts, no migrants
   auto pack = [&] {
     launch_slab_pack(stream, cap_, sc_, cur_, G, K, C.dom_posmin, hl, hr, withm1, withpre, packtiles_, slabcnt_,
-                     send_);
+                     send_, normal_, casenpb_);
   };
   check_hip(hipMemsetAsync(slabcnt_, 0, sizeof(SlabCounts), stream), "exchange: reset counts");
   pack();
@@ -687,11 +701,7 @@ void SphGpuSingle::Exchange() {
   // later); the GPU idles from the counts copy until the next launches arrive.
   if (!xev_) check_hip(hipEventCreateWithFlags(&xev_, hipEventDisableTiming), "hipEventCreate");
   check_hip(hipEventRecord(xev_, stream), "exchange: event");
-  for (;;) {
-    const hipError_t q = hipEventQuery(xev_);
-    if (q == hipSuccess) break;
-    if (q != hipErrorNotReady) check_hip(q, "exchange: wait counts");
-  }
+  WaitEvent(xev_, "exchange: wait counts");
   const SlabCounts c = *slabcnt_host_;
   const unsigned long long gneed = std::max(c.sendl[0], c.sendr[0]), mneed = std::max(c.sendl[1], c.sendr[1]);
   if (gneed > send_.gcap || mneed > send_.mcap) {  // records past a capacity were not written: grow, pack again
@@ -732,16 +742,113 @@ void SphGpuSingle::Exchange() {
     if (want >= (1ull << 31)) throw SphError(SPH_ERR_NOMEM, "slab particle capacity overflow");
     Grow(c.np, unsigned(want));
   }
+  // ghosts and migrants of both faces in ONE transfer group (four concurrent streams over
+  // the two xGMI links)
+  transport_->group_begin();
   transport_->exchange(send_.gl, sizeof(SlabGhost) * c.sendl[0], send_.gr, sizeof(SlabGhost) * c.sendr[0], recvg_,
                        sizeof(SlabGhost) * rgl, recvg_ + rgl, sizeof(SlabGhost) * rgr, stream);
   transport_->exchange(send_.ml, sizeof(SlabRec) * c.sendl[1], send_.mr, sizeof(SlabRec) * c.sendr[1], recvm_,
                        sizeof(SlabRec) * rml, recvm_ + rml, sizeof(SlabRec) * rmr, stream);
+  transport_->group_end();
   launch_slab_unpack(stream, sc_, recvm_, unsigned(rml + rmr), recvg_, unsigned(rgl + rgr), c.np, cur_, K,
-                     C.dom_posmin, withm1, withpre, slabcnt_);
+                     C.dom_posmin, withm1, withpre, slabcnt_, normal_, casenpb_);
+}
+
+// The one host wait of a slab divide: spin on the event (a blocking synchronise wakes up
+// tens of us later) with a deadline, polling the transport's asynchronous error state.  A
+// dead or failed peer ends this rank with SPH_ERR_COMM instead of a hang (the transport is
+// aborted first, so the other ranks' pending transfers fail or time out too).
+void SphGpuSingle::WaitEvent(hipEvent_t ev, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 0;; spin++) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) check_hip(q, what);
+    if ((spin & 1023u) == 1023u) {
+      try {
+        transport_->check_async();
+      } catch (...) {
+        transport_->abort();
+        throw;
+      }
+      const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (sec > comm_timeout_s_) {
+        transport_->abort();
+        throw SphError(SPH_ERR_COMM, std::string(what) + ": no progress for " + std::to_string(int(sec)) +
+                                         " s (a neighbour slab is gone or stalled)");
+      }
+    }
+  }
+}
+
+// Periodic re-balancing of the x-slabs ("re-balanced every K steps"): the
+// owned particles per global column (fluid + bound_weight x bound, the weights of
+// sph_slab_partition) are summed over the ranks, every rank derives the same new column
+// bounds from them, and the next exchange hands over whole columns as migrants.  Each
+// bound stays strictly inside the two slabs it separates, so a particle moves at most
+// one rank, and the copies a rank keeps of its outgoing migrants in its new ghost column
+// (the usual pack rule) give the neighbours their ghost columns during the hand-over.
+// Called between an update and the divide (all ranks, same step).
+void SphGpuSingle::Repartition() {
+  const int ncxg = int(C.dom_cells[0]), nr = slabcfg_.nranks;
+  launch_column_counts(stream, cap_, sc_, cur_, G, K, ncxg, colcnt_);
+  std::vector<float> bnd(size_t(nr) + 1, 0.f);
+  bnd[size_t(slabcfg_.rank)] = float(slabcfg_.c0);  // each rank contributes its own bound
+  if (slabcfg_.rank == nr - 1) bnd[size_t(nr)] = float(slabcfg_.c1);
+  check_hip(hipMemcpyAsync(colcnt_ + 2 * ncxg, bnd.data(), 4 * bnd.size(), hipMemcpyHostToDevice, stream),
+            "repartition: bounds");
+  transport_->allreduce_sum_f32(colcnt_, 2 * ncxg + nr + 1, stream);
+  std::vector<float> h(2 * size_t(ncxg) + size_t(nr) + 1);
+  check_hip(hipMemcpyAsync(h.data(), colcnt_, 4 * h.size(), hipMemcpyDeviceToHost, stream), "repartition: read");
+  if (!xev_) check_hip(hipEventCreateWithFlags(&xev_, hipEventDisableTiming), "hipEventCreate");
+  check_hip(hipEventRecord(xev_, stream), "repartition: event");
+  WaitEvent(xev_, "repartition: column counts");
+  std::vector<int> old(size_t(nr) + 1);
+  for (int r = 0; r <= nr; r++) old[size_t(r)] = int(h[2 * size_t(ncxg) + size_t(r)]);
+  std::vector<double> w(static_cast<size_t>(ncxg));
+  double total = 0;
+  for (int c = 0; c < ncxg; c++) {
+    w[size_t(c)] = double(h[size_t(c)]) + repart_bw_ * double(h[size_t(ncxg + c)]);
+    total += w[size_t(c)];
+  }
+  std::vector<double> pre(size_t(ncxg) + 1, 0.0);
+  for (int c = 0; c < ncxg; c++) pre[size_t(c) + 1] = pre[size_t(c)] + w[size_t(c)];
+  double maxload = 0;
+  for (int r = 0; r < nr; r++) maxload = std::max(maxload, pre[size_t(old[size_t(r) + 1])] - pre[size_t(old[size_t(r)])]);
+  repart_last_imbalance_ = total > 0 ? maxload / (total / nr) : 1.0;
+  if (!(repart_last_imbalance_ > 1.0 + repart_tol_)) return;
+  std::vector<int> nb(old);
+  partition_from_prefix(pre, nr, nb.data());
+  for (int r = 1; r < nr; r++) {  // inside the two slabs it separates, and increasing
+    nb[size_t(r)] = std::min(std::max(nb[size_t(r)], old[size_t(r) - 1] + 1), old[size_t(r) + 1] - 1);
+    nb[size_t(r)] = std::max(nb[size_t(r)], nb[size_t(r) - 1] + 1);
+  }
+  bool changed = false;
+  for (int r = 1; r < nr; r++) {
+    if (nb[size_t(r)] >= nb[size_t(r) + 1]) return;  // the clamps left no valid split: keep the old one
+    changed |= nb[size_t(r)] != old[size_t(r)];
+  }
+  if (!changed) return;
+  slabcfg_.c0 = nb[size_t(slabcfg_.rank)];
+  slabcfg_.c1 = nb[size_t(slabcfg_.rank) + 1];
+  G = make_grid(C, &slabcfg_);
+  keybits_ = bits_for(G.boxdiscard, 1);
+  repart_count_++;
+}
+
+void SphGpuSingle::SetRepartition(unsigned every, double bound_weight, double tolerance) {
+  if (!slab()) throw SphError(SPH_ERR_STATE, "re-partitioning applies to slab solvers only");
+  if (!(bound_weight >= 0) || !(tolerance >= 0)) throw SphError(SPH_ERR_ARG, "invalid re-partition weights");
+  repart_every_ = every;
+  repart_bw_ = bound_weight;
+  repart_tol_ = tolerance;
 }
 
 void SphGpuSingle::RunCellDivide() {
   TimedBegin(2);
+  if (slab() && exchange_armed_ && repart_every_ && (stepsdone_ % repart_every_) == 0 && transport_->nranks > 1 &&
+      !havepre_)
+    Repartition();
   if (slab() && exchange_armed_) Exchange();
   launch_presort(stream, cap_, sc_, cur_.dcell, cur_.code, G, C.dom_cellcode, sort_.keys[0], sort_.vals[0]);
   const int res = launch_radix_sort(stream, cap_, sc_, sort_, keybits_);
@@ -834,6 +941,7 @@ void SphGpuSingle::ComputeSymplecticCorr() {
 
 void SphGpuSingle::ComputeStep() {
   stepped_ = true;
+  stepsdone_++;
   if (step_algorithm_ == SPH_STEP_VERLET) {
     Interaction_Forces(1);
     DtVariable(DT_VERLET);

@@ -30,6 +30,7 @@ void check_hip(hipError_t e, const char* what);
 void derive_constants(const SphCaseDef& c, SphConstants& k);
 // Column bounds of a particle-count-balanced x-slab split (sph_slab_partition).
 void slab_partition(const SphCaseDef& c, const SphParticlesHost& all, int nranks, double bound_weight, int* bounds);
+void partition_from_prefix(const std::vector<double>& prefix, int nranks, int* bounds);
 // PART / case files (sph_bi4.cpp)
 void part_read(const std::string& path, SphPartHeader& h, SphParticlesHost* out);
 void part_write(const std::string& path, const SphPartHeader& h, const SphParticlesHost& p);
@@ -83,6 +84,12 @@ class SphGpuSingle {
   // Moving boundaries / floating bodies (sph_bodies.hip), configured before the first step.
   void SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* movs, unsigned nevt, const SphMotionEvent* evts);
   void SetFloatings(unsigned nft, const SphFloatingDef* defs, double ftpause);
+  // Slabs: re-balance the column bounds every `every` steps (0: never) when the most loaded
+  // slab exceeds the mean by more than `tolerance`; collective (all ranks the same values).
+  void SetRepartition(unsigned every, double bound_weight, double tolerance);
+  SlabConfig Slab() const { return slabcfg_; }
+  unsigned RepartitionCount() const { return repart_count_; }
+  double LastImbalance() const { return repart_last_imbalance_; }
   unsigned Floatings(SphFloatingState* out, unsigned cap);
 
   SphConstants C{};
@@ -102,6 +109,8 @@ class SphGpuSingle {
   void UploadNormals(const SphCaseDef& cdef, const SphParticlesHost& init);
   void UploadPhases(const SphCaseDef& cdef);
   void Exchange();
+  void WaitEvent(hipEvent_t ev, const char* what);
+  void Repartition();
   void RunMotion();                 // JSphCpu::RunMotion after ComputeStep (JSphCpuSingle.cpp:1096)
   void RunFloating(bool predictor); // JSphCpuSingle::RunFloating
   void TimedBegin(int phase);
@@ -158,6 +167,12 @@ class SphGpuSingle {
   std::unique_ptr<SlabTransport> transport_;
   SlabConfig slabcfg_;
   bool exchange_armed_ = false;  // the initial divide has no exchange (ghosts come with the case)
+  double comm_timeout_s_ = 120.0;  // SPH_COMM_TIMEOUT_S: deadline of a slab host wait
+  unsigned nctmax_ = 0;            // cells of the widest grid (grid-sized buffers)
+  float* colcnt_ = nullptr;        // re-partition: column counts + bounds (device)
+  unsigned repart_every_ = 0, repart_count_ = 0;
+  double repart_bw_ = 0.3, repart_tol_ = 0.05, repart_last_imbalance_ = 1.0;
+  unsigned long long stepsdone_ = 0;
   unsigned* folded_ = nullptr;   // 3 maxima for the allreduce
   SlabCounts* slabcnt_ = nullptr;
   SlabCounts* slabcnt_host_ = nullptr;

@@ -322,6 +322,21 @@ int sph_slab_group_create(const SphCaseDef* cdef, const SphParticlesHost* all, i
 int sph_slab_group_destroy(SphSlabGroup* g);
 int sph_slab_group_run(SphSlabGroup* g, uint32_t nsteps);
 int sph_slab_group_member(SphSlabGroup* g, int i, SphSolver** out);
+/* Periodic re-balancing of the column bounds: every `every` steps (0:
+ * never) the owned particles per column (fluid + bound_weight x boundary) are summed over
+ * the ranks and, when the most loaded slab exceeds the mean by more than `tolerance`
+ * (relative), every rank moves to the same new bounds (each strictly inside the two slabs
+ * it separates); the next exchange hands the columns over.  Collective: every rank (or
+ * the group) with the same values, before or between runs. */
+int sph_slab_set_repartition(SphSolver* s, uint32_t every, double bound_weight, double tolerance);
+int sph_slab_group_set_repartition(SphSlabGroup* g, uint32_t every, double bound_weight, double tolerance);
+typedef struct SphSlabInfo {
+  int32_t rank, nranks, cx_begin, cx_end;  /* current owned columns [cx_begin, cx_end)        */
+  uint32_t repartitions;                   /* bounds changes so far                          */
+  uint32_t pad;
+  double last_imbalance;                   /* max slab load / mean at the last check (1 = even) */
+} SphSlabInfo;
+int sph_slab_info(SphSolver* s, SphSlabInfo* out);
 
 /* ---- PART / case files (.bi4), SURVEY.md §8(f) row 2 ------------------------------
  * Root values of JPartDataBi4 (case) + the values of its PART_%04u item, in the

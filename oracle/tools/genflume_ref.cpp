@@ -30,7 +30,8 @@
 
 int main(int argc, char** argv) {
   if (argc < 5) {
-    fprintf(stderr, "usage: %s dp outdir step ddt [timemax] [casename] [boundary] [L W H depth]\n", argv[0]);
+    fprintf(stderr, "usage: %s dp outdir step ddt [timemax] [casename] [boundary] [L W H depth] [flapwait flapfreq flapampl]\n",
+            argv[0]);
     return 1;
   }
   const double dp = atof(argv[1]);
@@ -42,6 +43,9 @@ int main(int argc, char** argv) {
   const int boundary = (argc > 7 ? atoi(argv[7]) : 1);
   const double L = (argc > 8 ? atof(argv[8]) : 1.2), W = (argc > 9 ? atof(argv[9]) : 0.3);
   const double H = (argc > 10 ? atof(argv[10]) : 0.4), D = (argc > 11 ? atof(argv[11]) : 0.2);
+  // flap motion: wait, then mvrotsinu of this frequency (Hz) and amplitude (degrees)
+  const std::string fwait = (argc > 12 ? argv[12] : "0.004"), ffreq = (argc > 13 ? argv[13] : "2"),
+                    fampl = (argc > 14 ? argv[14] : "3");
 
   const int nx = int(std::round(L / dp)), ny = int(std::round(W / dp)), nz = int(std::round(H / dp));
   const int kd = int(std::round(D / dp));
@@ -151,10 +155,10 @@ int main(int argc, char** argv) {
   fprintf(f, "<objreal ref=\"0\"><begin mov=\"1\" start=\"0\"/>\n"
              "<mvrectsinu id=\"1\" duration=\"100\" anglesunits=\"degrees\"><freq x=\"1.5\" y=\"0\" z=\"0\"/>"
              "<ampl x=\"0.02\" y=\"0\" z=\"0\"/><phase x=\"0\" y=\"0\" z=\"0\"/></mvrectsinu>\n</objreal>\n");
-  fprintf(f, "<objreal ref=\"1\"><begin mov=\"1\" start=\"0\"/>\n<wait id=\"1\" duration=\"0.004\" next=\"2\"/>\n"
+  fprintf(f, "<objreal ref=\"1\"><begin mov=\"1\" start=\"0\"/>\n<wait id=\"1\" duration=\"%s\" next=\"2\"/>\n"
              "<mvrotsinu id=\"2\" duration=\"100\" anglesunits=\"degrees\"><axisp1 x=\"%.10g\" y=\"0\" z=\"0\"/>"
-             "<axisp2 x=\"%.10g\" y=\"1\" z=\"0\"/><freq v=\"2\"/><ampl v=\"3\"/><phase v=\"0\"/></mvrotsinu>\n"
-             "</objreal>\n", nx * dp, nx * dp);
+             "<axisp2 x=\"%.10g\" y=\"1\" z=\"0\"/><freq v=\"%s\"/><ampl v=\"%s\"/><phase v=\"0\"/></mvrotsinu>\n"
+             "</objreal>\n", fwait.c_str(), nx * dp, nx * dp, ffreq.c_str(), fampl.c_str());
   fprintf(f, "</motion>\n");
   fprintf(f, "<particles np=\"%u\" nb=\"%u\" nbf=\"%u\" mkboundfirst=\"10\" mkfluidfirst=\"0\">\n", np, nbound, nfixed);
   fprintf(f, "<fixed mkbound=\"0\" mk=\"10\" begin=\"0\" count=\"%u\"/>\n", nfixed);

@@ -30,6 +30,9 @@ from make_golden import load_dump  # noqa: E402
 VARIANTS = {
     "verlet_ddt2": (0.025, 1, 2, 1, 100, (1, 10, 50, 100)),
     "symplectic_ddt1_mdbc": (0.025, 2, 1, 2, 60, (1, 10, 60)),
+    # a fast, wide flap (no wait, 8 Hz, 12 degrees): its mDBC particles cross cell columns
+    # within the run (the slab hand-over of turned normals, tests/test_bodies.py)
+    "symplectic_ddt1_mdbc_fastflap": (0.025, 2, 1, 2, 80, (1, 40, 80), ("1.2", "0.3", "0.4", "0.2", "0", "8", "12")),
 }
 
 
@@ -48,13 +51,13 @@ def load_ft(fn):
     return np.array(t), np.array(c).reshape(sh), np.array(v).reshape(sh), np.array(w).reshape(sh)
 
 
-def make(name, dp, step, ddt, boundary, nsteps, keep):
+def make(name, dp, step, ddt, boundary, nsteps, keep, extra=()):
     out_dir = os.path.join(HERE, "bi4", "flume_" + name)
     os.makedirs(out_dir, exist_ok=True)
     tmp = tempfile.mkdtemp(prefix="flume_")
     try:
         subprocess.check_call([os.path.join(REF, "genflume_ref"), repr(dp), tmp, str(step), str(ddt), "1.0",
-                               "CaseFlume", str(boundary)], stdout=subprocess.DEVNULL)
+                               "CaseFlume", str(boundary)] + list(extra), stdout=subprocess.DEVNULL)
         files = ["CaseFlume.xml", "CaseFlume.bi4"] + (["CaseFlume_Normals.nbi4"] if boundary == 2 else [])
         for f in files:
             shutil.copy(os.path.join(tmp, f), os.path.join(out_dir, f))
@@ -83,5 +86,7 @@ def make(name, dp, step, ddt, boundary, nsteps, keep):
 
 
 if __name__ == "__main__":
+    only = sys.argv[1] if len(sys.argv) > 1 else None
     for k, v in VARIANTS.items():
-        make(k, *v)
+        if only is None or k == only:
+            make(k, *v)

@@ -329,3 +329,60 @@ def test_partfloat_file_reads_with_the_reference_reader(tmp_path):
     assert np.array_equal(c, np.array([[b["center"] for b in p["bodies"]] for p in parts]))
     assert np.array_equal(v, np.array([[b["fvel"] for b in p["bodies"]] for p in parts], np.float32))
     assert np.array_equal(w, np.array([[b["fomega"] for b in p["bodies"]] for p in parts], np.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_gpu_bodies_on_slabs_with_repartition_match_reference(variant):
+    """Moving boundaries, the floating box (and mDBC) on 3 slabs re-partitioned every 4 steps
+    from an uneven start: the reference PARTs and body states still hold."""
+    from dualsphysics_multilayer_amd.core import SphSlabGroup, case_derive
+
+    x, g = _case(variant), _ref(variant)
+    ncx = case_derive(x.case_def())["dom_cells"][0]
+    grp = SphSlabGroup(x, np.array([0, ncx // 5, ncx // 3, ncx], np.int32))
+    grp.set_repartition(4, 0.3, 0.0)
+    done = 0
+    for k in _kept(g):
+        grp.run(k - done)
+        done = k
+        got, ref = grp.particles(), _snap(g, k)
+        assert np.array_equal(got["idp"], ref["idp"]), "excluded/duplicated particles"
+        for q, t in zip(("pos", "vel", "rhop"), _tol(k)):
+            assert maxdiff(got, ref, q) <= t, (k, q, maxdiff(got, ref, q))
+        b = grp.floatings()[0]
+        assert np.abs(b["center"] - g["ft_center"][k, 0]).max() <= 1e-7
+    assert max(i["repartitions"] for i in grp.slab_info()) >= 1
+
+
+@pytest.mark.gpu
+def test_gpu_mdbc_flap_normals_cross_slab_faces():
+    """A fast, wide flap (no wait, 8 Hz, 12 degrees; mDBC, Symplectic): its particles cross
+    cell columns within the run.  On 3 slabs whose middle one is the flap's initial column
+    alone, every crossing flap particle migrates with its turned mDBC normal; the merged
+    state holds the reference PARTs (single-domain tolerance) and the single-domain GPU run."""
+    from dualsphysics_multilayer_amd.core import SphSlabGroup, case_derive
+
+    x, g = _case("symplectic_ddt1_mdbc_fastflap"), _ref("symplectic_ddt1_mdbc_fastflap")
+    k = case_derive(x.case_def())
+    flap = np.where((x.code & 0x1800) == 0x800)[0]
+    flap = flap[x.pos[flap, 0] > x.pos[:, 0].mean()]  # the flap, not the piston
+    cflap = int((x.pos[flap[0], 0] - k["map_realposmin"][0]) // np.float32(k["scell"]))
+    grp = SphSlabGroup(x, np.array([0, cflap, cflap + 1, k["dom_cells"][0]], np.int32))
+    one = _gpu(x)
+    done = 0
+    for kk in _kept(g):
+        grp.run(kk - done)
+        one.run(kk - done)
+        done = kk
+        got, ref = grp.particles(), _snap(g, kk)
+        assert np.array_equal(got["idp"], ref["idp"]), "excluded/duplicated particles"
+        for q, t in zip(("pos", "vel", "rhop"), _tol(kk)):
+            assert maxdiff(got, ref, q) <= t, (kk, q, maxdiff(got, ref, q))
+        p1 = by_idp(one.particles())
+        for q, t in zip(("pos", "vel", "rhop"), _tol(kk)):
+            assert maxdiff(got, p1, q) <= t, (kk, q, maxdiff(got, p1, q))
+    # flap particles did leave their initial column (the hand-over happened)
+    fin = grp.particles()["pos"][flap]
+    cols = ((fin[:, 0] - k["map_realposmin"][0]) // np.float32(k["scell"])).astype(int)
+    assert (cols != cflap).any()
