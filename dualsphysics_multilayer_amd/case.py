@@ -232,7 +232,50 @@ class DamBreakCase:
             tboundary=self.tboundary,
             slipmode=self.slipmode,
             mdbc_threshold=self.mdbc_threshold,
+            rheology=1, velgrad=1, tvisco=1, nphases=0, phases=(), relaxation_dt=0.2,
+            shift_mode=0, shift_coef=-2.0, shift_tfs=0.0,
+            data2d=int(getattr(self, "data2d", False)),
+            data2d_posy=0.0,
         )
+
+
+@dataclass
+class DamBreak2DCase(DamBreakCase):
+    """2-D dam break (Simulate2D) in the geometry of examples/main/01_DamBreak/
+    CaseDambreakVal2D_Def.xml: tank 4 x 3 m (x, z) with bottom, left and right walls, water
+    column 1 x 2 m, all particles at y = 0; h = coefh sqrt(2 dp^2), mass rho0 dp^2, Visco
+    0.02 (the example's), Wendland, DDT2.  oracle/tools/gencase_ref (dim 2) writes the same
+    case for the reference (tests/test_2d.py checks the two agree bit for bit)."""
+
+    visco: float = 0.02
+    data2d: bool = True
+
+    def __post_init__(self) -> None:
+        dp = self.dp
+        nx, nz = _cround(4.0 / dp), _cround(3.0 / dp)
+        mx, mz = _cround(1.0 / dp), _cround(2.0 / dp)
+        k, i = np.meshgrid(np.arange(nz + 1), np.arange(nx + 1), indexing="ij")
+        wall = (k == 0) | (i == 0) | (i == nx)
+        bi, bk = i[wall], k[wall]
+        self._wall_ijk = (bi, np.zeros_like(bi), bk, nx, 0)
+        fk, fi = np.meshgrid(np.arange(1, mz + 1), np.arange(1, mx + 1), indexing="ij")
+        ii = np.concatenate([bi, fi.ravel()]).astype(np.float64)
+        kk = np.concatenate([bk, fk.ravel()]).astype(np.float64)
+        self.pos = np.stack([ii * dp, np.zeros_like(ii), kk * dp], axis=1)
+        self.npb = int(bi.size)
+        self.np = int(self.pos.shape[0])
+        self.idp = np.arange(self.np, dtype=np.uint32)
+        self.vel = np.zeros((self.np, 3), dtype=np.float32)
+        g, rho0, gamma = -self.gravity[2], self.rhop0, self.gamma
+        hswl = mz * dp
+        cs0 = self.coefsound * math.sqrt(g * hswl)
+        b = cs0 * cs0 * rho0 / gamma
+        self._h, self._b, self._mass = self.coefh * math.sqrt(2.0 * dp * dp), b, rho0 * dp * dp
+        rhop = np.empty(self.np, dtype=np.float32)
+        rhop[: self.npb] = np.float32(rho0)
+        z = self.pos[self.npb:, 2]
+        rhop[self.npb:] = (rho0 * np.power(1.0 + rho0 * g * (hswl - z) / b, 1.0 / gamma)).astype(np.float32)
+        self.rhop = rhop
 
 
 def dambreak_np(dp: float) -> int:
@@ -537,9 +580,11 @@ class WetDambreakNNCase:
 
     def case_def(self) -> dict:
         d = DamBreakCase.case_def(self)
-        d.update(rheology=2, velgrad=1, tvisco=self.tvisco, nphases=len(self.phases), phases=self.phases,
-                 relaxation_dt=self.relaxation_dt, shift_mode=self.shift_mode, shift_coef=self.shift_coef,
-                 shift_tfs=self.shift_tfs)
+        f32 = lambda v: float(np.float32(v))  # noqa: E731  (JXml ReadElementFloat / GetValueFloat)
+        phases = tuple({k: (f32(v) if isinstance(v, float) else v) for k, v in ph.items()} for ph in self.phases)
+        d.update(rheology=2, velgrad=1, tvisco=self.tvisco, nphases=len(self.phases), phases=phases,
+                 relaxation_dt=f32(self.relaxation_dt), shift_mode=self.shift_mode, shift_coef=f32(self.shift_coef),
+                 shift_tfs=f32(self.shift_tfs))
         return d
 
 

@@ -129,8 +129,8 @@ class CaseRun:
         c, cd = self.case, self.case.case_def()
         fb = [b for b in c.blocks if b["type"] == "fixed"]
         fl = [b for b in c.blocks if b["type"] == "fluid"]
-        if len(fl) != 1 or not fb:
-            raise CaseError("PART headers are written for cases with one fluid block.")
+        if not fl or not fb:
+            raise CaseError("PART headers are written for cases with a fixed and a fluid block.")
         return dict(app_name=self.app_name, case_name=c.case_name, cpart=cpart, nout=nout, step=step,
                     timestep=float(st["time"]),
                     symplectic_dtpre=float(st["sym_dtpre"]) if c.step_algorithm == 2 else 0.0,
@@ -158,7 +158,8 @@ class CaseRun:
             # Part_Head.ibi4 (restart header) lists one fixed and one fluid MK block; cases with
             # moving/floating blocks are not restartable by this core and get no Part_Head
             if not getattr(self.case, "has_bodies", False) and len(
-                    [b for b in self.case.blocks if b["type"] == "fixed"]) == 1:
+                    [b for b in self.case.blocks if b["type"] == "fixed"]) == 1 and len(
+                    [b for b in self.case.blocks if b["type"] == "fluid"]) == 1:
                 write_part_head(os.path.join(self.dirout, "Part_Head.ibi4"), hdr)
             if getattr(self.case, "floatings", None):
                 # PartFloat.fbi4: the body states of every saved PART (JSphCpuSingle SaveData ->

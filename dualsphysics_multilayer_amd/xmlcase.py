@@ -277,10 +277,19 @@ class XmlCase:
         self._load_parameters(p)
         self._domain = _config_domain(p)
         sp = ex.find("special")
+        self.phases = ()
         if sp is not None:
             for ch in sp:  # accinputs, chrono, wavepaddles, mlayerpistons, inout, gauges, ...
+                if ch.tag == "nnphases" and self.rheology == 2:
+                    continue
                 raise CaseError(f"<special><{ch.tag}> is not supported by this core.")
         self._load_blocks(_node(ex, "particles"))
+        if self.rheology == 2:  # JSph::InitMultiPhase (JSph.cpp:3137-3215 of the v5.0 solver)
+            node = sp.find("nnphases") if sp is not None else None
+            if node is not None:
+                self._load_phases(node)
+            else:  # the v5.0 solver would run multiphase without phase data
+                raise CaseError("RheologyTreatment=2 needs the phases in <special><nnphases>.")
         self._load_motion(ex.find("motion"))
         dfix = overrides.pop("domain_fixed", None)
         if dfix is not None:  # -domain_fixed: JSph::ConfigDomainFixed (JSph.cpp:343-346, 856)
@@ -378,9 +387,9 @@ class XmlCase:
 
     # -- JSph::LoadConfigCtes ---------------------------------------------------------------
     def _load_constants(self, c):
+        # JCaseCtes::ReadXmlRun (JCaseCtes.cpp:202-204): <data2d> and, when true, <data2dposy>
         self.data2d = _elem_bool(c, "data2d")
-        if self.data2d:
-            raise CaseError("2-D simulations (data2d) are not supported by this core.")
+        self.data2d_posy = _elem_double(c, "data2dposy") if self.data2d and c.find("data2dposy") is not None else 0.0
         g = c.find("gravity")
         if g is None:
             raise CaseError("The item is not found 'gravity'.")
@@ -410,11 +419,23 @@ class XmlCase:
         if self.step_algorithm not in (1, 2):
             raise CaseError("Step algorithm is not valid.")
         self.verlet_steps = p.int("VerletSteps", True, 40)
+        # RheologyTreatment / VelocityGradientType / RelaxationDt: the v5.0 NN solver's keys
+        # (JSph.cpp:608-623 of src_mphase/DSPH_v5.0_NNewtonian)
+        self.rheology = p.int("RheologyTreatment", True, 1)
+        if self.rheology not in (1, 2):
+            raise CaseError("Rheology treatment is not valid.")
+        self.relaxation_dt = float(np.float32(p.num("RelaxationDt", True, 0.2))) if self.rheology == 2 else 0.2
+        self.velgrad = p.int("VelocityGradientType", True, 1)
+        if self.velgrad not in (1, 2):
+            raise CaseError("Velocity gradient treatment is not valid.")
         tv = p.int("ViscoTreatment", True, 1)
-        if tv not in (1, 2):
+        if tv not in (1, 2, 3):
             raise CaseError("Viscosity treatment is not valid.")
-        if tv != 1:
-            raise CaseError("Only artificial viscosity (ViscoTreatment=1) is supported by this core.")
+        if tv == 3 and self.rheology != 2:
+            raise CaseError("ViscoTreatment 'Constitutive  eq.' not valid for Single-phase classic formulation.")
+        if tv != 1 and self.rheology != 2:
+            raise CaseError("Single-phase Laminar+SPS viscosity (ViscoTreatment=2) is not supported by this core.")
+        self.tvisco = tv
         self.visco = p.num("Visco")
         self.viscoboundfactor = p.num("ViscoBoundFactor", True, 1.0)
         if p.values.get("ViscoTime"):
@@ -441,12 +462,17 @@ class XmlCase:
             if self.tdensity not in (0, 1, 2, 3):
                 raise CaseError("Density Diffusion Term mode is not valid.")
             self.ddtvalue = p.num("DensityDTvalue", True, 0.1)
-        if p.exists("Shifting"):
+        self.shift_mode, self.shift_coef, self.shift_tfs = 0, -2.0, 0.0
+        if p.exists("Shifting"):  # JSph.cpp:684-700; JSphShifting::ConfigBasic
             sm = p.int("Shifting", True, 0)
             if sm not in (0, 1, 2, 3):
                 raise CaseError("Shifting mode in <execution><parameters> is not valid.")
-            if sm != 0 and p.num("ShiftCoef", True, -2) != 0:
-                raise CaseError("Shifting is not supported by this core.")
+            coef = float(np.float32(p.num("ShiftCoef", True, -2)))
+            if sm != 0 and coef != 0:
+                if self.rheology != 2:
+                    raise CaseError("Shifting is supported by this core in NN multiphase cases only.")
+                self.shift_mode, self.shift_coef = sm, coef
+                self.shift_tfs = float(np.float32(p.num("ShiftTFS", True, 0)))
         self.timemax = p.num("TimeMax")
         self.timeout = p.num("TimeOut")
         self.dtini = max(0.0, p.num("DtIni", True, 0.0))
@@ -509,6 +535,50 @@ class XmlCase:
         self.moving_blocks = bytype["moving"]
         self.floatings = [dict(b["floating"], idbegin=b["begin"], count=b["count"], mkbound=b["mktype"])
                           for b in bytype["floating"]]
+
+    # -- JSph::InitMultiPhase (JSph.cpp:3137-3215, v5.0 NN solver) -----------------------------
+    def _load_phases(self, node):
+        known = {"rhop", "csound", "gamma", "visco", "tau_yield", "tau_max", "Bi_multi", "HBP_n", "HBP_m",
+                 "cohesion", "phi", "phasetype"}
+        phases = []
+        for e in node:
+            if e.tag != "phase":
+                if e.tag.startswith("_"):
+                    continue
+                raise CaseError(f"<nnphases>: unknown element <{e.tag}>.")
+            for ch in e:
+                if ch.tag not in known and not ch.tag.startswith("_"):
+                    raise CaseError(f"<phase>: unknown element <{ch.tag}>.")
+
+            def val(name, optional=False):
+                x = e.find(name)
+                if x is None:
+                    if optional:
+                        return 0.0
+                    raise CaseError(f"<phase>: the item is not found '{name}'.")
+                return float(np.float32(float(x.get("value"))))  # ReadElementFloat
+
+            mkf = int(e.get("mkfluid"))
+            if not any(b["type"] == "fluid" and b["mktype"] == mkf for b in self.blocks):
+                raise CaseError("No particles with mkfluid=%d" % mkf)
+            taumax = val("tau_max", True)
+            phases.append(dict(mkfluid=mkf, phasetype=int(val("phasetype")), rho=val("rhop"), cs0=val("csound", True),
+                               gamma=val("gamma", True), visco=val("visco"), tau_yield=val("tau_yield"),
+                               tau_max=taumax, bi_multi=val("Bi_multi") if taumax else 0.0, hbp_m=val("HBP_m"),
+                               hbp_n=val("HBP_n")))
+        if not phases:
+            raise CaseError("The number of phases is invalid.")
+        phases.sort(key=lambda ph: ph["mkfluid"])  # sorted by mkfluid (JSph.cpp:3187-3195)
+        # a fluid particle's phase is its code value, the index of its fluid block
+        fl = [b for b in self.blocks if b["type"] == "fluid"]
+        if [b["mktype"] for b in fl] != [ph["mkfluid"] for ph in phases]:
+            raise CaseError("Every fluid block needs its <phase>, in mkfluid order.")
+        self.phases = tuple(phases)
+
+    @property
+    def explicit_codes(self) -> bool:
+        """NN multiphase: the core takes the fluid block codes (the phase of each particle)."""
+        return self.rheology == 2
 
     # -- JCasePartBlock_Floating::ReadXml (JCaseParts.cpp:248-290) ------------------------------
     @staticmethod
@@ -694,6 +764,10 @@ class XmlCase:
             map_realposmin=tuple(float(v) for v in pmin), map_realposmax=tuple(float(v) for v in pmax),
             cellmode=self.cellmode, celldomfixed=int(self.celldomfixed), npb=self.npb, np=self.np,
             tboundary=self.tboundary, slipmode=self.slipmode, mdbc_threshold=self.mdbc_threshold,
+            rheology=self.rheology, velgrad=self.velgrad, tvisco=self.tvisco, nphases=len(self.phases),
+            phases=self.phases, relaxation_dt=self.relaxation_dt, shift_mode=self.shift_mode,
+            shift_coef=self.shift_coef, shift_tfs=self.shift_tfs, data2d=int(self.data2d),
+            data2d_posy=self.data2d_posy,
         )
 
 

@@ -10,7 +10,7 @@
 // test checks that both produce the same particles bit for bit.
 //
 // usage: gencase_ref <dp> <outdir> <step:1=Verlet|2=Symplectic> <ddt:0..3> [timemax] [casename]
-//                    [boundary:1=DBC|2=mDBC]
+//                    [boundary:1=DBC|2=mDBC] [dim:3|2]
 //
 // With boundary=2 the case also gets <casename>_Normals.nbi4, written through the
 // reference's own JPartNormalData (JPartNormalData.cpp:178-207), as GenCase would: the
@@ -38,22 +38,28 @@ int main(int argc, char** argv) {
   const double tmax = (argc > 5 ? atof(argv[5]) : 1.5);
   const std::string name = (argc > 6 ? argv[6] : "CaseDambreak");
   const int boundary = (argc > 7 ? atoi(argv[7]) : 1);
+  // dim 2: the 2-D dam break of examples/main/01_DamBreak/CaseDambreakVal2D_Def.xml (tank
+  // 4 x 3 in x-z with bottom, left and right walls, water column 1 x 2, y = 0, Visco 0.02)
+  const int dim = (argc > 8 ? atoi(argv[8]) : 3);
+  const bool d2 = (dim == 2);
 
-  // Tank 1.6 x 0.67 x 0.4 (walls: bottom, x=0, x=L, y=0, y=W); water 0.4 x 0.67 x 0.3.
-  const int nx = int(std::round(1.6 / dp)), ny = int(std::round(0.67 / dp)), nz = int(std::round(0.4 / dp));
-  const int mx = int(std::round(0.4 / dp)), my = int(std::round(0.67 / dp)), mz = int(std::round(0.3 / dp));
+  // 3-D: tank 1.6 x 0.67 x 0.4 (walls: bottom, x=0, x=L, y=0, y=W); water 0.4 x 0.67 x 0.3.
+  const int nx = int(std::round((d2 ? 4.0 : 1.6) / dp)), ny = d2 ? 0 : int(std::round(0.67 / dp));
+  const int nz = int(std::round((d2 ? 3.0 : 0.4) / dp));
+  const int mx = int(std::round((d2 ? 1.0 : 0.4) / dp)), my = d2 ? 0 : int(std::round(0.67 / dp));
+  const int mz = int(std::round((d2 ? 2.0 : 0.3) / dp));
   std::vector<tdouble3> pos, nor;
   for (int k = 0; k <= nz; k++)
     for (int j = 0; j <= ny; j++)
       for (int i = 0; i <= nx; i++)
-        if (k == 0 || i == 0 || i == nx || j == 0 || j == ny) {
+        if (k == 0 || i == 0 || i == nx || (!d2 && (j == 0 || j == ny))) {
           pos.push_back(TDouble3(i * dp, j * dp, k * dp));
           const double hd = dp * 0.5;
           nor.push_back(TDouble3(i == 0 ? hd : (i == nx ? -hd : 0.), j == 0 ? hd : (j == ny ? -hd : 0.), k == 0 ? hd : 0.));
         }
   const unsigned nb = unsigned(pos.size());
   for (int k = 1; k <= mz; k++)
-    for (int j = 1; j < my; j++)
+    for (int j = (d2 ? 0 : 1); j < (d2 ? 1 : my); j++)
       for (int i = 1; i <= mx; i++) pos.push_back(TDouble3(i * dp, j * dp, k * dp));
   const unsigned np = unsigned(pos.size()), nf = np - nb;
 
@@ -61,8 +67,8 @@ int main(int argc, char** argv) {
   const double hswl = mz * dp;
   const double cs0 = coefsound * std::sqrt(g * hswl);
   const double b = cs0 * cs0 * rho0 / gamma;
-  const double h = coefh * std::sqrt(3. * dp * dp);
-  const double mass = rho0 * dp * dp * dp;
+  const double h = coefh * std::sqrt((d2 ? 2. : 3.) * dp * dp);  // JCaseCtes::ComputeFinalH
+  const double mass = rho0 * dp * dp * (d2 ? 1.0 : dp);
 
   std::vector<unsigned> idp(np);
   std::vector<tfloat3> vel(np, TFloat3(0));
@@ -76,7 +82,7 @@ int main(int argc, char** argv) {
   }
 
   JPartDataBi4 pd;
-  pd.ConfigBasic(0, 1, "gencase_ref", "gencase_ref", name, false, 0, dir);
+  pd.ConfigBasic(0, 1, "gencase_ref", "gencase_ref", name, d2, 0, dir);
   pd.ConfigParticles(np, nb, 0, 0, nf, pmin, pmax, false, false);
   pd.ConfigCtes(dp, h, b, rho0, gamma, mass, mass);
   pd.AddPartInfo(0, 0, np, 0, 0, 0, pmin, pmax, 0, 0);
@@ -92,7 +98,8 @@ int main(int argc, char** argv) {
   FILE* f = fopen((dir + "/" + name + ".xml").c_str(), "w");
   if (!f) { perror("xml"); return 2; }
   fprintf(f, "<?xml version=\"1.0\" encoding=\"UTF-8\" ?>\n<case app=\"gencase_ref\">\n<execution>\n<constants>\n");
-  fprintf(f, "<data2d value=\"false\"/>\n<gravity x=\"0\" y=\"0\" z=\"%g\"/>\n<cflnumber value=\"0.2\"/>\n", -g);
+  fprintf(f, "%s\n<gravity x=\"0\" y=\"0\" z=\"%g\"/>\n<cflnumber value=\"0.2\"/>\n",
+          d2 ? "<data2d value=\"true\"/>\n<data2dposy value=\"0\"/>" : "<data2d value=\"false\"/>", -g);
   fprintf(f, "<gamma value=\"%g\"/>\n<rhop0 value=\"%g\"/>\n<dp value=\"%.10g\"/>\n", gamma, rho0, dp);
   fprintf(f, "<h value=\"%.10E\"/>\n<b value=\"%.10E\"/>\n<massbound value=\"%.10E\"/>\n<massfluid value=\"%.10E\"/>\n", h, b, mass, mass);
   fprintf(f, "</constants>\n<particles np=\"%u\" nb=\"%u\" nbf=\"%u\" mkboundfirst=\"10\" mkfluidfirst=\"0\">\n", np, nb, nb);
@@ -103,7 +110,7 @@ int main(int argc, char** argv) {
   par("VerletSteps", "40");
   par("Kernel", "2");
   par("ViscoTreatment", "1");
-  par("Visco", "0.1");
+  par("Visco", d2 ? "0.02" : "0.1");
   par("ViscoBoundFactor", "1");
   par("DensityDT", std::to_string(ddt));
   par("DensityDTvalue", "0.1");

@@ -36,6 +36,9 @@ CASES = {
     "symplectic_ddt1_mdbc_dp0.03": (0.03, 2, 1, 60, (1, 20, 60), 2),
     # CellMode=half (cells of h, 5x5 rows of 5 cells; JSph.cpp:1772-1788): meta[5] = 2
     "verlet_ddt2_half_dp0.025": (0.025, 1, 2, 60, (1, 20, 60), 1, ("-cellmode:half",)),
+    # 2-D (Simulate2D): the CaseDambreakVal2D geometry (gencase_ref dim 2); meta[6] = 2
+    "verlet_ddt2_2d_dp0.02": (0.02, 1, 2, 100, (1, 10, 100), 1, (), 2),
+    "symplectic_ddt1_2d_dp0.02": (0.02, 2, 1, 60, (1, 20, 60), 1, (), 2),
 }
 
 
@@ -51,11 +54,11 @@ def load_dump(fn):
     return t, idp.copy(), pos.copy(), vel.copy(), rho.copy()
 
 
-def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=()):
+def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=(), dim=3):
     tmp = tempfile.mkdtemp(prefix="golden_")
     try:
         subprocess.check_call([os.path.join(REF, "gencase_ref"), repr(dp), tmp, str(step), str(ddt), "1.5",
-                               "CaseDambreak", str(boundary)], stdout=subprocess.DEVNULL)
+                               "CaseDambreak", str(boundary), str(dim)], stdout=subprocess.DEVNULL)
         out = os.path.join(tmp, "out")
         subprocess.check_call(
             [os.path.join(REF, "DualSPHysics5.2CPU_ref"), os.path.join(tmp, "CaseDambreak"), out,
@@ -76,10 +79,12 @@ def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=()):
         arrays["times"] = np.array(times)
         arrays["dt"] = np.diff(np.array(times))
         m = [dp, step, ddt, nsteps]
-        if boundary != 1 or extra:
+        if boundary != 1 or extra or dim != 3:
             m.append(boundary)
-        if "-cellmode:half" in extra:
-            m.append(2)
+        if "-cellmode:half" in extra or dim != 3:
+            m.append(2 if "-cellmode:half" in extra else 1)
+        if dim != 3:
+            m.append(dim)
         arrays["meta"] = np.array(m, np.float64)
         np.savez_compressed(os.path.join(ROOT, "tests", "golden", name + ".npz"), **arrays)
         print(name, "ok", os.path.getsize(os.path.join(ROOT, "tests", "golden", name + ".npz")))

@@ -33,6 +33,11 @@ def cellmode(g):
     return int(g["meta"][5]) if len(g["meta"]) > 5 else 1
 
 
+def dim(g):
+    """3 or 2 (2-D fixtures carry meta[6] = 2)."""
+    return int(g["meta"][6]) if len(g["meta"]) > 6 else 3
+
+
 def by_idp(p):
     o = np.argsort(p["idp"], kind="stable")
     return {k: (v[o] if isinstance(v, np.ndarray) and v.ndim >= 1 and len(v) == len(o) else v) for k, v in p.items()}

@@ -174,3 +174,21 @@ def test_gpu_nn_deterministic():
     pa, pb = a.particles(), b.particles()
     for q in ("idp", "pos", "vel", "rhop"):
         assert np.array_equal(pa[q], pb[q]), q
+
+
+def test_xml_loader_reads_the_nn_case(tmp_path):
+    """xmlcase (the run driver's JSph::LoadCaseConfig) reads gennn_ref's case for the v5.0
+    solver — RheologyTreatment, VelocityGradientType, ViscoTreatment, shifting, RelaxationDt
+    and <special><nnphases> — into the same SphCaseDef and particle codes as the generator."""
+    exe = os.path.join(REF, "gennn_ref")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref not built")
+    from dualsphysics_multilayer_amd.xmlcase import XmlCase
+
+    subprocess.check_call([exe, "0.025", str(tmp_path), "0.2", "0.5", "5", "CaseNN", "2.75", "1", "3", "1", "1", "20"],
+                          stdout=subprocess.DEVNULL)
+    x = XmlCase(str(tmp_path / "CaseNN"))
+    c = WetDambreakNNCase(0.025, width=0.2, scale=0.5, csound=20.0, tvisco=3, tdensity=1, shift_mode=1)
+    assert x.case_def() == c.case_def()
+    assert np.array_equal(x.code, c.code) and np.array_equal(x.idp, c.idp)
+    assert np.array_equal(x.pos, c.pos)

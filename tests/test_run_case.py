@@ -98,14 +98,14 @@ def test_simulationdomain_with_legacy_keys_is_refused(tmp_path):
 
 @pytest.mark.parametrize("edit,match", [
     (lambda x: x.replace('key="Kernel" value="2"', 'key="Kernel" value="1"'), "Wendland"),
-    (lambda x: x.replace('key="ViscoTreatment" value="1"', 'key="ViscoTreatment" value="2"'), "artificial"),
+    (lambda x: x.replace('key="ViscoTreatment" value="1"', 'key="ViscoTreatment" value="2"'), "Laminar\\+SPS"),
     # mDBC without a <case>_Normals.nbi4 beside the case (JSph.cpp:1337)
     (lambda x: x.replace("<parameters>", '<parameters>\n<parameter key="Boundary" value="2"/>'), "normal vectors"),
     (lambda x: x.replace("<parameters>", '<parameters>\n<parameter key="Boundary" value="2"/>'
                          '<parameter key="SlipMode" value="2"/>'), "slip mode"),
     (lambda x: x.replace("<parameters>", '<parameters>\n<parameter key="XPeriodicIncY" value="0"/>'), "Periodic"),
-    (lambda x: x.replace('key="Shifting" value="0"', 'key="Shifting" value="3"'), "Shifting"),
-    (lambda x: x.replace('<data2d value="false"/>', '<data2d value="true"/>'), "2-D"),
+    (lambda x: x.replace('key="Shifting" value="0"', 'key="Shifting" value="3"'), "NN multiphase cases only"),
+    (lambda x: x.replace('<data2d value="false"/>', '<data2d value="true"/>'), "dimension of the case"),
     (lambda x: x.replace("</parameters>", "</parameters>\n<special><wavepaddles/></special>"), "special"),
     (lambda x: x.replace('<fixed mkbound="0" mk="10"', '<moving mkbound="0" mk="10"').replace(
         'count="1182"/>\n<fluid', 'count="1182"/>\n<fluid'), "mobile objects"),
