@@ -199,6 +199,8 @@ def main() -> None:
     ap.add_argument("--boundary", choices=("dbc", "mdbc"), default=None,
                     help="boundary conditions (mdbc: modified DBC, Vel0, normals to the wall limit)")
     ap.add_argument("--bound-weight", type=float, default=0.3, help="slab balance weight of a bound particle")
+    ap.add_argument("--cellmode", choices=("full", "half"), default="full",
+                    help="cfg2/cfg3 cell size: full = 2h (the reference default), half = h (-cellmode:half)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=100,
                     help="reference CPU steps timed (window 10 .. 10+K, BASELINE.md: 10-110)")
@@ -227,12 +229,16 @@ def main() -> None:
     from dualsphysics_multilayer_amd.case import DamBreakCase, WaveFlumeCase, WetDambreakNNCase
     from dualsphysics_multilayer_amd.core import SphGpuSingle, SphGpuSlab, comm_unique_id, slab_partition
 
+    cmode = 2 if args.cellmode == "half" else 1
+    if cmode == 2 and args.workload not in ("cfg2", "cfg3"):
+        raise SystemExit("--cellmode half applies to the dam-break workloads (cfg2, cfg3)")
     if args.workload == "cfg2":
         dp = args.dp or (CFG2_DP if world == 1 else weak_dp(world * CFG2_NP))
-        case = DamBreakCase(dp, tboundary=2 if args.boundary == "mdbc" else 1)
+        case = DamBreakCase(dp, tboundary=2 if args.boundary == "mdbc" else 1, cellmode=cmode)
     elif args.workload == "cfg3":
         dp = args.dp or CFG3_DP
-        case = DamBreakCase(dp, step_algorithm=2, tdensity=1, tboundary=2 if args.boundary == "mdbc" else 1)
+        case = DamBreakCase(dp, step_algorithm=2, tdensity=1, tboundary=2 if args.boundary == "mdbc" else 1,
+                            cellmode=cmode)
     elif args.workload == "cfg4":
         dp = args.dp or CFG4_DP
         case = WaveFlumeCase(dp, tboundary=2 if args.boundary == "mdbc" else 1)
@@ -339,11 +345,12 @@ def main() -> None:
                      "synthetic: generated 3D dam-break lattice (SURVEY.md §8(c) recipe)"),
             "config": {
                 "workload": (("BASELINE cfg2: 3D dam break, %d particles (dp=%g), Verlet, Wendland, artificial "
-                              "viscosity 0.1, DDT2 0.1, %s, CFL 0.2, CellMode full" % (case.np, dp, args.boundary.upper()))
+                              "viscosity 0.1, DDT2 0.1, %s, CFL 0.2, CellMode %s"
+                              % (case.np, dp, args.boundary.upper(), args.cellmode))
                              if args.workload == "cfg2" else
                              ("BASELINE cfg3: 3D dam break, %d particles (dp=%g), Symplectic, Wendland, artificial "
-                              "viscosity 0.1, DDT (Molteni delta-SPH) 0.1, %s, CFL 0.2, CellMode full"
-                              % (case.np, dp, args.boundary.upper())) if args.workload == "cfg3" else
+                              "viscosity 0.1, DDT (Molteni delta-SPH) 0.1, %s, CFL 0.2, CellMode %s"
+                              % (case.np, dp, args.boundary.upper(), args.cellmode)) if args.workload == "cfg3" else
                              ("BASELINE cfg4: wave flume, %d particles (dp=%g): piston mvrectsinu + flap mvrotsinu "
                               "moving boundaries, floating box (RigidAlgorithm=1, %d particles), %s, Verlet, "
                               "Wendland, artificial viscosity 0.1, DDT2 0.1, CFL 0.2"

@@ -40,7 +40,7 @@ namespace sphx {
 constexpr int ROWCELLS_LDS = 1024;
 
 template <bool WRITE>
-__global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ bc, DivGrid g,
+__global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ bc, DivGrid g, int tmaxc,
                                                    unsigned* __restrict__ counts, uint4* __restrict__ items) {
   __shared__ unsigned pre[ROWCELLS_LDS + 1];            // begin offset of every cell of the row, + row end
   __shared__ unsigned short nzfrom[ROWCELLS_LDS + 1];  // first non-empty owned cell >= x (xend if none)
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
     int c = xbeg;
     while (p < pend) {
       while (PRE(c + 1) <= p) c++;
-      const unsigned q = min(min(p + unsigned(TB), pend), PRE(min(c + TMAXCELLS, xend)));
+      const unsigned q = min(min(p + unsigned(TB), pend), PRE(min(c + tmaxc, xend)));
       int e = c;
       while (PRE(e + 1) < q) e++;
       emit(c, e, p, q);
@@ -108,6 +108,18 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
   const unsigned pend = pre[xend];
   int c = nzfrom[xbeg];
   unsigned p = c < xend ? pre[c] : pend;
+  if (tmaxc != TMAXCELLS) {  // CellMode=half: longer items, the cell holding q-1 by a short scan
+    while (p < pend) {
+      const unsigned q = min(min(p + unsigned(TB), pend), pre[min(c + tmaxc, xend)]);
+      int e = c;
+      while (pre[e + 1] <= q - 1) e++;
+      emit(c, e, p, q);
+      p = q;
+      c = pre[e + 1] == q ? int(nzfrom[e + 1]) : e;
+    }
+    if (!WRITE) counts[r] = nitems;
+    return;
+  }
   while (p < pend) {
     const unsigned p1 = pre[min(c + 1, xend)], p2 = pre[min(c + 2, xend)], p3 = pre[min(c + 3, xend)];
     const unsigned p4 = pre[min(c + 4, xend)];
@@ -148,12 +160,13 @@ __global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ coun
 }
 
 void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
-                  uint4* items, unsigned* qctr) {
+                  uint4* items, unsigned* qctr, int scelldiv) {
   (void)qctr;
+  const int tmaxc = scelldiv == 1 ? TMAXCELLS : TMAXCELLS_HALF;
   const unsigned nrows2 = 2u * unsigned(g.ncy) * unsigned(g.ncz);
-  hipLaunchKernelGGL(k_items_rows<false>, dim3(nrows2), dim3(64), 0, stm, begincell, g, rowtmp, nullptr);
+  hipLaunchKernelGGL(k_items_rows<false>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, nullptr);
   hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, rowtmp, nrows2, sc);
-  hipLaunchKernelGGL(k_items_rows<true>, dim3(nrows2), dim3(64), 0, stm, begincell, g, rowtmp, items);
+  hipLaunchKernelGGL(k_items_rows<true>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, items);
 }
 
 // ------------------------------------------------------------------------------------
@@ -242,15 +255,18 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
   if (MODE == 1) {
     if (TDENSITY == 1 && K.mdbc) {  // mDBC: Molteni DDT over bound neighbours too (JSphCpu.cpp:730)
       const float t = w3 * rr2 * inv_re;
-      a.delta = fmaf(t, fmaf(p.vr.w, C.y, -1.f), a.delta);
+      a.delta = fmaf(t, (p.vr.w - B.w) * C.y, a.delta);
     } else if ((TDENSITY == 1 || TDENSITY == 2) && ok) {
       a.delta = FLT_MAX;  // DBC: no DDT next to the boundary
     }
     return;
   }
   if (TDENSITY == 1) {
+    // rho1/rho2 - 1 as (rho1 - rho2)*(1/rho2): exactly 0 for equal densities (rho1*rcp(rho2)
+    // - 1 with the approximate v_rcp leaves a +-1 ulp residue, which at t=0 is the whole
+    // Molteni sum); C.y = r/rho2 carries the p2 mass ratio r (1 without floating bodies)
     const float t = w3 * rr2 * inv_re;
-    a.delta = fmaf(t, fmaf(p.vr.w, C.y, FT ? -crec_r(C) : -1.f), a.delta);
+    a.delta = fmaf(t, (p.vr.w - B.w) * C.y, a.delta);
     if (FT && ok && crec_kind(C) == 2.f) a.dstop = true;  // light floating p2
   } else if (TDENSITY == 2 || TDENSITY == 3) {
     float drhop;
@@ -282,6 +298,14 @@ __device__ __forceinline__ TAcc finish(const KConst& K, TAcc a, const P1& p, con
   return a;
 }
 
+template <int TDENSITY, int MODE, bool FT>
+__device__ __forceinline__ void drain_words(const KConst& K, const P1& p, unsigned long long c0,
+                                            unsigned long long c1, unsigned long long c2, unsigned long long c3,
+                                            int b0, int b1, int b2, int b3, const float4* __restrict__ sA,
+                                            const float4* __restrict__ sB,
+                                            const typename CRecT<FT>::type* __restrict__ sC, const PassK& Q,
+                                            TAcc& a);
+
 // One drain unit: the lane's candidates in up to two staged windows [wa0,wa1) and
 // [wb0,wb1) (two point-mirrored neighbour rows, or one row), all positions relative to
 // the item, drained as ONE set.  How many real neighbours a particle has in one row
@@ -312,7 +336,41 @@ __device__ __forceinline__ void tile_unit(const KConst& K, const P1& p, float th
     a.visc += float(__popcll(c0) + __popcll(c1) + __popcll(c2) + __popcll(c3));
     continue;
 #endif
-    int b0 = wa0 + off, b1 = b0 + 64, b2 = wb0 + off, b3 = b2 + 64;
+    drain_words<TDENSITY, MODE, FT>(K, p, c0, c1, c2, c3, wa0 + off, wa0 + off + 64, wb0 + off, wb0 + off + 64, sA,
+                                    sB, sC, Q, a);
+  }
+}
+
+// CellMode=half drain unit: four windows (two mirrored row pairs) of 5 half-cells each,
+// <= 64 candidates per window and round (one word each), drained as ONE set.
+template <int TDENSITY, int MODE, bool FT = false>
+__device__ __forceinline__ void tile_unit4(const KConst& K, const P1& p, float thr, int4 w0, int4 w1,
+                                           const float4* __restrict__ sA, const float4* __restrict__ sB,
+                                           const typename CRecT<FT>::type* __restrict__ sC, const PassK& Q,
+                                           TAcc& a) {
+  const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
+  for (int off = 0;; off += 64) {  // a second round only for windows of > 64 candidates
+    const int n0 = w1.x - w0.x - off, n1 = w1.y - w0.y - off, n2 = w1.z - w0.z - off, n3 = w1.w - w0.w - off;
+    if (n0 <= 0 && n1 <= 0 && n2 <= 0 && n3 <= 0) break;
+    const unsigned long long c0 = test64(sA, w0.x + off, min(n0, 64), px2, py2, pz2, thr);
+    const unsigned long long c1 = test64(sA, w0.y + off, min(n1, 64), px2, py2, pz2, thr);
+    const unsigned long long c2 = test64(sA, w0.z + off, min(n2, 64), px2, py2, pz2, thr);
+    const unsigned long long c3 = test64(sA, w0.w + off, min(n3, 64), px2, py2, pz2, thr);
+    drain_words<TDENSITY, MODE, FT>(K, p, c0, c1, c2, c3, w0.x + off, w0.y + off, w0.z + off, w0.w + off, sA, sB,
+                                    sC, Q, a);
+  }
+}
+
+// Drain of one round of accepted candidates: four 64-bit words c0..c3 of staged records
+// from bases b0..b3 (see tile_unit).
+template <int TDENSITY, int MODE, bool FT>
+__device__ __forceinline__ void drain_words(const KConst& K, const P1& p, unsigned long long c0,
+                                            unsigned long long c1, unsigned long long c2, unsigned long long c3,
+                                            int b0, int b1, int b2, int b3, const float4* __restrict__ sA,
+                                            const float4* __restrict__ sB,
+                                            const typename CRecT<FT>::type* __restrict__ sC, const PassK& Q,
+                                            TAcc& a) {
+  {
     // compact: drop empty words, keep the order (three bubble passes)
 #pragma unroll
     for (int pass = 0; pass < 3; pass++) {
@@ -484,7 +542,115 @@ __device__ __forceinline__ TAcc run_pass(const KConst& K, const DivGrid& g, cons
   return finish<TDENSITY, MODE, FT>(K, acc, p, Q);
 }
 
-template <int TDENSITY, bool FT = false>
+// i-th of the 12 "lower" rows of the 5x5 CellMode=half stencil (dz < 0, or dz = 0 and
+// dy < 0); the other 12 are their point mirrors, the 25th the item's own row.
+__device__ __forceinline__ void half_row(int i, int& dy, int& dz) {
+  if (i < 10) {
+    dz = -2 + i / 5;
+    dy = -2 + i % 5;
+  } else {
+    dz = 0;
+    dy = i - 12;
+  }
+}
+
+// CellMode=half pass: 6 units of two lower rows + their mirrors (4 rows staged as one
+// segment when they fit TCAP, drained as one set by tile_unit4), then the own row; a
+// unit too long for one segment goes row by row in TCAP segments.
+template <int TDENSITY, int MODE, bool FT = false>
+__device__ __forceinline__ TAcc run_pass_half(const KConst& K, const DivGrid& g, const RowCtx& rc, const P1& p,
+                                              float thr, const PassK Q, const unsigned* __restrict__ bc,
+                                              const float4* __restrict__ poscell,
+                                              const float4* __restrict__ velrhop, const float* __restrict__ press,
+                                              float4* __restrict__ sA, float4* __restrict__ sB,
+                                              typename CRecT<FT>::type* __restrict__ sC, const FtRec& ft,
+                                              bool dstop0 = false) {
+  TAcc acc = {};
+  acc.dstop = dstop0;
+  const unsigned cellinit = (MODE == 1 ? 0u : g.boxfluid);
+  constexpr int tcap = TcapT<FT>::v;
+  for (int u = 0; u < 7; u++) {
+    int dyr[4], dzr[4];
+    unsigned rs[4], re[4], ls[4], le[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int dy = 0, dz = 0;
+      if (u < 6) half_row(2 * u + (k >> 1), dy, dz);
+      if (k & 1) {
+        dy = -dy;
+        dz = -dz;
+      }
+      dyr[k] = dy;
+      dzr[k] = dz;
+      rs[k] = re[k] = ls[k] = le[k] = 0u;
+      const int z = rc.cz + dz, y = rc.cy + dy;
+      if ((u == 6 && k) || z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;
+      const unsigned rowbase = cellinit + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+      rs[k] = bc[rowbase + rc.xa];
+      re[k] = bc[rowbase + rc.xb + 1];
+      ls[k] = bc[rowbase + rc.lxa];
+      le[k] = bc[rowbase + rc.lxb + 1];
+    }
+    const unsigned n0 = re[0] - rs[0], n1 = re[1] - rs[1], n2 = re[2] - rs[2], n3 = re[3] - rs[3];
+    const unsigned ntot = n0 + n1 + n2 + n3;
+    if (ntot == 0u) continue;
+    if (ntot <= unsigned(tcap)) {
+      const unsigned o1 = n0, o2 = o1 + n1, o3 = o2 + n2;
+      __syncthreads();
+      if (n0) stage_row(K, rs[0], re[0], 0u, rc.xo, dyr[0], dzr[0], poscell, velrhop, press, sA, sB, sC, ft);
+      if (n1) stage_row(K, rs[1], re[1], o1, rc.xo, dyr[1], dzr[1], poscell, velrhop, press, sA, sB, sC, ft);
+      if (n2) stage_row(K, rs[2], re[2], o2, rc.xo, dyr[2], dzr[2], poscell, velrhop, press, sA, sB, sC, ft);
+      if (n3) stage_row(K, rs[3], re[3], o3, rc.xo, dyr[3], dzr[3], poscell, velrhop, press, sA, sB, sC, ft);
+      __syncthreads();
+      int4 w0, w1;
+      w0.x = int(ls[0] - rs[0]);
+      w1.x = rc.act && n0 ? int(le[0] - rs[0]) : w0.x;
+      w0.y = int(o1 + ls[1] - rs[1]);
+      w1.y = rc.act && n1 ? int(o1 + le[1] - rs[1]) : w0.y;
+      w0.z = int(o2 + ls[2] - rs[2]);
+      w1.z = rc.act && n2 ? int(o2 + le[2] - rs[2]) : w0.z;
+      w0.w = int(o3 + ls[3] - rs[3]);
+      w1.w = rc.act && n3 ? int(o3 + le[3] - rs[3]) : w0.w;
+      tile_unit4<TDENSITY, MODE, FT>(K, p, thr, w0, w1, sA, sB, sC, Q, acc);
+    } else {
+      // too long for one segment: each row on its own, in TCAP segments (values picked
+      // by selects: a runtime index into the row arrays would put them in scratch)
+      for (int k = 0; k < 4; k++) {
+        auto pick = [&](const unsigned* v) { return k == 0 ? v[0] : k == 1 ? v[1] : k == 2 ? v[2] : v[3]; };
+        const unsigned rsk = pick(rs), rek = pick(re), lsk = pick(ls), lek = pick(le);
+        const int dy = k == 0 ? dyr[0] : k == 1 ? dyr[1] : k == 2 ? dyr[2] : dyr[3];
+        const int dz = k == 0 ? dzr[0] : k == 1 ? dzr[1] : k == 2 ? dzr[2] : dzr[3];
+        for (unsigned seg = rsk; seg < rek; seg += tcap) {
+          const unsigned segn = min(unsigned(tcap), rek - seg);
+          __syncthreads();
+          stage_row(K, seg, seg + segn, 0u, rc.xo, dy, dz, poscell, velrhop, press, sA, sB, sC, ft);
+          __syncthreads();
+          const int w0 = int(max(lsk, seg) - seg);
+          const int w1 = rc.act ? max(w0, int(min(lek, seg + segn)) - int(seg)) : w0;
+          tile_unit<TDENSITY, MODE, FT>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, Q, acc);
+        }
+      }
+    }
+  }
+  return finish<TDENSITY, MODE, FT>(K, acc, p, Q);
+}
+
+// The pass of the cell mode: S = scelldiv (1 full, 2 half).
+template <int TDENSITY, int MODE, bool FT, int S>
+__device__ __forceinline__ TAcc pass_s(const KConst& K, const DivGrid& g, const RowCtx& rc, const P1& p, float thr,
+                                       const PassK Q, const unsigned* __restrict__ bc,
+                                       const float4* __restrict__ poscell, const float4* __restrict__ velrhop,
+                                       const float* __restrict__ press, float4* __restrict__ sA,
+                                       float4* __restrict__ sB, typename CRecT<FT>::type* __restrict__ sC,
+                                       const FtRec& ft, bool dstop0 = false) {
+  if constexpr (S == 1)
+    return run_pass<TDENSITY, MODE, FT>(K, g, rc, p, thr, Q, bc, poscell, velrhop, press, sA, sB, sC, ft, dstop0);
+  else
+    return run_pass_half<TDENSITY, MODE, FT>(K, g, rc, p, thr, Q, bc, poscell, velrhop, press, sA, sB, sC, ft,
+                                             dstop0);
+}
+
+template <int TDENSITY, bool FT = false, int S = 1>
 __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
                                                     unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
                                                     const float4* __restrict__ velrhop,
@@ -519,13 +685,13 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
       const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
       const int a = int(item.y & 0xffffu), b = int(item.y >> 16);
       const int xo = (a + b + 1) >> 1;
-      const int xa = max(a - 1, 0), xb = min(b + 1, g.ncx - 1);
+      const int xa = max(a - S, 0), xb = min(b + S, g.ncx - 1);
       if (bitem) {
-        // Bound item: nothing to compute unless a fluid cell is in its 3x3x3
-        // neighbourhood; then its particles get ar = 0 (PreInteraction's reset).
+        // Bound item: nothing to compute unless a fluid cell is in its neighbourhood;
+        // then its particles get ar = 0 (PreInteraction's reset).
         bool any = false;
-        for (int z = max(cz - 1, 0); z <= min(cz + 1, g.ncz - 1); z++)
-          for (int y = max(cy - 1, 0); y <= min(cy + 1, g.ncy - 1); y++) {
+        for (int z = max(cz - S, 0); z <= min(cz + S, g.ncz - 1); z++)
+          for (int y = max(cy - S, 0); y <= min(cy + S, g.ncy - 1); y++) {
             const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
             any |= bc[rowbase + xa] != bc[rowbase + xb + 1];
           }
@@ -560,22 +726,22 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
           p.press = 0.f;
         }
         p.inv_rho = frcp(p.vr.w);
-        const int lxa = max(cx1 - 1, 0), lxb = min(cx1 + 1, g.ncx - 1);
+        const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
         const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
         const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act};
         // pass 0: fluid p2 (fluid p1: momentum/continuity/DDT; bound p1: continuity),
         // pass 1: bound p2 of fluid p1.  Each pass holds only its own accumulator.
         TAcc f, bnd = {0, 0, 0, 0, 0, 0, false};
         if (bitem) {
-          f = run_pass<TDENSITY, 2, FT>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell,
-                                        velrhop, press, sA, sB, sC, ft);
+          f = pass_s<TDENSITY, 2, FT, S>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell,
+                                         velrhop, press, sA, sB, sC, ft);
         } else {
           // a floating p1 gets no DDT (JSphCpu.cpp:659-662)
           const bool ftp1 = FT && act && CodeType(ft.code[p1]) == CODE_TYPE_FLOATING;
-          f = run_pass<TDENSITY, 0, FT>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell,
-                                        velrhop, press, sA, sB, sC, ft, ftp1);
-          bnd = run_pass<TDENSITY, 1, FT>(K, g, rc, p, thr, pass_k(K, cvisc_b, K.massbound, p.vr.w), bc, poscell,
-                                          velrhop, press, sA, sB, sC, ft, ftp1);
+          f = pass_s<TDENSITY, 0, FT, S>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell,
+                                         velrhop, press, sA, sB, sC, ft, ftp1);
+          bnd = pass_s<TDENSITY, 1, FT, S>(K, g, rc, p, thr, pass_k(K, cvisc_b, K.massbound, p.vr.w), bc, poscell,
+                                           velrhop, press, sA, sB, sC, ft, ftp1);
         }
         if (act && bitem) {
           // InteractionForcesBound store (JSphCpu.cpp:617-621) onto the reset ar = 0.
@@ -620,14 +786,15 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
   }
 }
 
-void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
-                        const float4* poscell, const float4* velrhop, const float* press, const unsigned* begincell,
-                        DivGrid g, const KConst& K, float4* arace, const typecode* code, const float* ftmassp) {
-  const FtRec ft = {code, ftmassp};
+template <int S>
+static void launch_fluid_tiled_s(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items,
+                                 unsigned* qctr, const float4* poscell, const float4* velrhop, const float* press,
+                                 const unsigned* begincell, DivGrid g, const KConst& K, float4* arace,
+                                 const FtRec& ft) {
 #define SPH_TILED(TD, FTB)                                                                                    \
-  hipLaunchKernelGGL((k_fluid_tiled<TD, FTB>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, \
-                     press, begincell, g, K, arace, ft)
-  if (ftmassp) {
+  hipLaunchKernelGGL((k_fluid_tiled<TD, FTB, S>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell,   \
+                     velrhop, press, begincell, g, K, arace, ft)
+  if (ft.massp) {
     switch (K.tdensity) {
       case 0: SPH_TILED(0, true); break;
       case 1: SPH_TILED(1, true); break;
@@ -643,6 +810,16 @@ void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const
     }
   }
 #undef SPH_TILED
+}
+
+void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
+                        const float4* poscell, const float4* velrhop, const float* press, const unsigned* begincell,
+                        DivGrid g, const KConst& K, float4* arace, const typecode* code, const float* ftmassp) {
+  const FtRec ft = {code, ftmassp};
+  if (K.scelldiv == 2)
+    launch_fluid_tiled_s<2>(stm, nblocks, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft);
+  else
+    launch_fluid_tiled_s<1>(stm, nblocks, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft);
 }
 
 }  // namespace sphx

@@ -120,8 +120,9 @@ void launch_interaction_bound(hipStream_t stm, unsigned npbcap, DevScalars* sc, 
                               const float4* velrhop, const unsigned* begincell, DivGrid g, const KConst& K,
                               float4* arace);
 // Tiled fluid interaction (sph_interaction_tiled.hip) and its per-divide item list.
+// scelldiv 1 (CellMode=full): items of <= 4 cells; 2 (half): <= TMAXCELLS_HALF half-cells.
 void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
-                  uint4* items, unsigned* qctr);
+                  uint4* items, unsigned* qctr, int scelldiv = 1);
 // With floating bodies (ftmassp != nullptr) the staged p2 records carry their mass ratio
 // and kind (the FT instantiation; one more float2 of LDS per record).
 void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,

@@ -353,9 +353,8 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   nctmax_ = slab() ? unsigned(C.dom_cells[0] + 2) * unsigned(G.ncy) * unsigned(G.ncz) : G.nct;
   if (const char* e = std::getenv("SPH_INTERACTION")) tiled_ = std::string(e) != "simple";
   if (const char* e = std::getenv("SPH_COMM_TIMEOUT_S")) comm_timeout_s_ = std::max(1.0, std::atof(e));
-  // The tiled kernel stages the 3x3 rows of 3 cells of CellMode=full; half runs the
-  // one-lane-per-particle kernel over its 5x5 rows of 5 cells.
-  if (C.scelldiv != 1) tiled_ = false;
+  // The tiled kernel stages the 3x3 rows of 3 cells of CellMode=full, or the 5x5 rows of
+  // 5 half-cells of CellMode=half (run_pass_half).
   nn_ = (C.rheology == SPH_RHEOLOGY_NN);
   shift_ = (C.shift_mode != SPH_SHIFT_NONE);
   if (nn_) {
@@ -857,7 +856,7 @@ void SphGpuSingle::RunCellDivide() {
   launch_gather(stream, cap_, sc_, sort_.vals[res], cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_,
                 G.xoff, nn_ ? phaseeos_ : nullptr);
   std::swap(cur_, alt_);
-  if (tiled_) launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_);
+  if (tiled_) launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv);
   if (nftp_) launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_, K, G);
   TimedEnd(2);
 }

@@ -39,7 +39,36 @@ constexpr int TCAP = SPH_TCAP;
 #endif
 template <bool FT> struct TcapT { static constexpr int v = TCAP; };
 template <> struct TcapT<true> { static constexpr int v = SPH_TCAP_FT; };
-constexpr int TMAXCELLS = 4;   // max x-cells per item
+constexpr int TMAXCELLS = 4;   // max x-cells per item (CellMode=full: cells of 2h)
+// CellMode=half (cells of h, +-2-cell stencil): an item spans <= 16 half-cells, so its
+// staged rows [a-2, b+2] are <= 20 half-cells = 10h long and two mirrored row pairs
+// (4 rows) fit one TCAP segment at the lattice density (~5.2 particles per half-cell).
+#ifndef SPH_TMAXCELLS_HALF
+#define SPH_TMAXCELLS_HALF 16
+#endif
+constexpr int TMAXCELLS_HALF = SPH_TMAXCELLS_HALF;
+
+// Candidate test of one window of n (<= 64) staged records -> one 64-bit mask (as
+// test128; used for the short 5-cell windows of CellMode=half).
+__device__ __forceinline__ unsigned long long test64(const float4* __restrict__ sA, int s0, int n, float px2,
+                                                     float py2, float pz2, float thr) {
+  unsigned long long m = 0ull;
+  const float4* __restrict__ b = sA + s0;
+  for (int jo = 0; jo < 8; jo++) {
+    const int left = n - jo * 8;
+    if (left <= 0) break;
+    unsigned bits = 0;
+#pragma unroll
+    for (int ji = 0; ji < 8; ji++) {
+      const float4 A = b[jo * 8 + ji];
+      const float q = fmaf(px2, A.x, fmaf(py2, A.y, fmaf(pz2, A.z, A.w)));
+      bits |= (q <= thr) ? (1u << ji) : 0u;
+    }
+    bits &= (left >= 8 ? 0xffu : ((1u << left) - 1u));
+    m |= (unsigned long long)bits << (jo * 8);
+  }
+  return m;
+}
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float fsqrt_(float x) { return __builtin_amdgcn_sqrtf(x); }

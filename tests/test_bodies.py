@@ -245,13 +245,33 @@ def test_product_flume_generator_is_the_reference_case(variant, kw):
         assert np.array_equal(w.boundnormal, x.boundnormal)
 
 
+def _moved_case(x, nsteps, cellmode):
+    """The case with the particle state of the tiled solver after nsteps (bodies in motion,
+    densities off the initial hydrostatic lattice), so an interaction has physical ar/ace
+    instead of the t=0 round-off of a balanced lattice."""
+    import copy
+
+    y = copy.copy(x)
+    y.cellmode = cellmode
+    s = _gpu(y)
+    s.run(nsteps)
+    p = by_idp(s.particles())
+    assert np.array_equal(p["idp"], np.sort(x.idp))
+    row = np.searchsorted(p["idp"], x.idp)
+    y.pos, y.vel, y.rhop = p["pos"][row].copy(), p["vel"][row].copy(), p["rhop"][row].copy()
+    return y
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant", VARIANTS)
-def test_gpu_tiled_floating_interaction_matches_per_particle_kernel(variant, monkeypatch):
+@pytest.mark.parametrize("cellmode", [1, 2])
+def test_gpu_tiled_floating_interaction_matches_per_particle_kernel(variant, cellmode, monkeypatch):
     """The floating (FT) instantiation of the LDS-tiled kernel (mass-scaled records, DDT
-    rules of floating p1/p2) vs the one-lane-per-particle kernel on the same initial state
-    (fluid around and below the box, the box's own particles as p1)."""
-    x = _case(variant)
+    rules of floating p1/p2; CellMode full and half) vs the one-lane-per-particle kernel on
+    the same state: the flume after 6 steps (fluid around and below the moving box, the
+    box's own particles as p1), both within 2e-4 of max|ar| / max|ace| (float rounding of
+    different summation orders and fast intrinsics)."""
+    x = _moved_case(_case(variant), 6, cellmode)
     monkeypatch.setenv("SPH_INTERACTION", "simple")
     ref = _gpu(x)
     monkeypatch.delenv("SPH_INTERACTION")
@@ -259,15 +279,13 @@ def test_gpu_tiled_floating_interaction_matches_per_particle_kernel(variant, mon
     for s in (ref, til):
         s.Interaction_Forces(1 if x.step_algorithm == 1 else 2)
     a, b = til.interaction(), ref.interaction()
+    assert np.array_equal(til.particles()["idp"], ref.particles()["idp"])
     flt = (til.particles()["code"] & 0x1800) == 0x1000
     assert flt.sum() == x.case_nfloat
-    # At t=0 ar is dominated by DDT round-off: the tiled kernel sums the Fourtakas
-    # hydrostatic term as a series and in a different order (measured 1.1e-3 of max|ar|
-    # with DDT2, 3.2e-3 with DDT1); a wrong floating mass would show as O(1) relative.
-    for q, tol in (("ar", 5e-3), ("ace", 2e-4)):
+    for q in ("ar", "ace"):
         scale = np.abs(b[q]).max()
-        assert np.abs(a[q] - b[q]).max() <= tol * scale, (q, np.abs(a[q] - b[q]).max(), scale)
-        assert np.abs(a[q][flt] - b[q][flt]).max() <= tol * np.abs(b[q][flt]).max() + 1e-6, q
+        assert np.abs(a[q] - b[q]).max() <= 2e-4 * scale, (q, np.abs(a[q] - b[q]).max(), scale)
+        assert np.abs(a[q][flt] - b[q][flt]).max() <= 2e-4 * np.abs(b[q][flt]).max() + 1e-6, q
 
 
 @pytest.mark.gpu

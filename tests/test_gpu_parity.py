@@ -71,11 +71,12 @@ def test_interaction_matches_oracle(ddt):
     assert ig["acemax"] == pytest.approx(io["acemax"], rel=1e-4)
     assert ig["viscdtmax"] == pytest.approx(io["viscdtmax"], rel=1e-3)
 
-def test_half_cells_match_oracle():
-    """CellMode=half (cells of h, +-2 cells: JCellSearch_inline.h:33-47 with scelldiv 2):
-    the same stable sort order and candidate counts as the oracle (bit-exact), the
-    interaction to float rounding."""
-    case = DamBreakCase(0.025, cellmode=2, celldomfixed=True)
+@pytest.mark.parametrize("ddt", [0, 1, 2, 3])
+def test_half_cells_match_oracle(ddt):
+    """CellMode=half (cells of h, +-2 cells: JCellSearch_inline.h:33-47 with scelldiv 2),
+    through the LDS-tiled kernel (run_pass_half): the same stable sort order and candidate
+    counts as the oracle (bit-exact), the interaction to float rounding."""
+    case = DamBreakCase(0.025, tdensity=ddt, cellmode=2, celldomfixed=True)
     g, o = gpu(case), oracle.OracleSolver(case, nthreads=4)
     assert np.array_equal(g.particles()["idp"], o.particles()["idp"])
     cg, co = g.count_pairs().astype(np.int64), o.count_pairs().astype(np.int64)
@@ -181,11 +182,13 @@ def test_large_case_properties():
     pb = b.particles()
     assert np.array_equal(p["pos"], pb["pos"]) and np.array_equal(p["vel"], pb["vel"])
 
-def test_cfg2_1m_matches_oracle():
-    """BASELINE cfg2 at its full size (1,025,964 particles): the GPU state after 1 and 3
-    Verlet steps against the oracle's (the C++ restatement pinned to the reference's PARTs,
-    test_oracle_golden.py) on the same case, at the step tolerances of the small cases."""
-    case = DamBreakCase(0.0045, celldomfixed=True)
+@pytest.mark.parametrize("cellmode", [1, 2])
+def test_cfg2_1m_matches_oracle(cellmode):
+    """BASELINE cfg2 at its full size (1,025,964 particles; CellMode full and half): the GPU
+    state after 1 and 3 Verlet steps against the oracle's (the C++ restatement pinned to the
+    reference's PARTs, test_oracle_golden.py) on the same case, at the step tolerances of
+    the small cases."""
+    case = DamBreakCase(0.0045, celldomfixed=True, cellmode=cellmode)
     assert case.np == 1025964
     g, o = gpu(case), oracle.OracleSolver(case, nthreads=16)
     done = 0
