@@ -80,9 +80,14 @@ EXPORTED_SYMBOLS = (
     "sph_bi4_rewrite",
     "sph_solver_set_motion",
     "sph_solver_set_floatings",
+    "sph_solver_set_floating_table",
     "sph_solver_floatings",
     "sph_partfloat_write",
 )
+
+
+# <floating> tables of a body, in SPH_FTTAB_* order (sphcore.h)
+FT_TABLES = ("linearvel", "angularvel", "linearforce", "angularforce")
 
 
 class SphError(RuntimeError):
@@ -142,6 +147,8 @@ def load_library(path: str = LIB_PATH):
     L.sph_solver_set_motion.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(SphMotionMov), C.c_uint32,
                                         C.POINTER(SphMotionEvent)]
     L.sph_solver_set_floatings.argtypes = [vp, C.c_uint32, C.POINTER(SphFloatingDef), C.c_double]
+    L.sph_solver_set_floating_table.argtypes = [vp, C.c_uint32, C.c_int32, C.c_uint32, C.POINTER(C.c_double),
+                                                C.POINTER(C.c_double)]
     L.sph_solver_floatings.argtypes = [vp, C.c_uint32, C.POINTER(SphFloatingState), C.POINTER(C.c_uint32)]
     L.sph_partfloat_write.argtypes = [C.c_char_p, C.c_char_p, C.c_uint32, C.c_uint32] + [vp] * 6 + [C.c_uint32] + [vp] * 8
     if L.sph_abi_version() != SPH_ABI_VERSION:
@@ -202,6 +209,17 @@ class SphGpuSingle:
         if getattr(case, "floatings", None):
             fts = floating_array(case.floatings)
             _check(L.sph_solver_set_floatings(self._h, len(case.floatings), fts, case.ftpause))
+            # imposed velocities / external forces (SPH_FTTAB_* order): rows (time, x, y, z)
+            for b, f in enumerate(case.floatings):
+                for kind, key in enumerate(FT_TABLES):
+                    rows = f.get(key)
+                    if rows is None or not len(rows):
+                        continue
+                    rows = np.ascontiguousarray(rows, np.float64)
+                    t, v = np.ascontiguousarray(rows[:, 0]), np.ascontiguousarray(rows[:, 1:4])
+                    dp = C.POINTER(C.c_double)
+                    _check(L.sph_solver_set_floating_table(self._h, b, kind, len(rows), t.ctypes.data_as(dp),
+                                                           v.ctypes.data_as(dp)))
 
     def close(self) -> None:
         if getattr(self, "_h", None):

@@ -475,10 +475,46 @@ __global__ __launch_bounds__(FT_BS) void k_ft_partial(const DevScalars* __restri
   if (threadIdx.x < 6) part[(size_t(cf) * FT_NBLK + j) * 6 + threadIdx.x] = red[threadIdx.x][0];
 }
 
+// JLinearValue::GetValue3f at time t (JLinearValue.cpp:209-247 FindTime, :301-329
+// GetValue3d, :387-390) of one table of n (time, x, y, z) rows with nondecreasing times:
+// the bracketing rows are the first row >= 1 whose time is >= t (else the last) and the
+// row before it (what FindTime's cached search settles on for sorted times), the factor
+// (t - tpre)/(tnext - tpre) clamped to [0,1] (0 for equal times), linear interpolation in
+// double without contraction; DBL_MAX ("none") propagates from the earlier row, an
+// interval ending in "none" keeps the earlier value; DBL_MAX -> FLT_MAX.
+__device__ void ft_table_eval(const double4* __restrict__ tab, int2 d, double t, float out[3]) {
+  const double4* T = tab + d.x;
+  const int n = d.y;
+  int pos = 0, posnext = 0;
+  if (n > 1) {
+    posnext = 1;
+    while (posnext + 1 < n && T[posnext].x < t) posnext++;
+    pos = posnext - 1;
+  }
+  const double tpre = T[pos].x, tnext = T[posnext].x, tdif = tnext - tpre;
+  double f = tdif != 0.0 ? (t - tpre) / tdif : 0.0;
+  if (f < 0.) f = 0.;
+  if (f > 1.) f = 1.;
+  const double vi[3] = {T[pos].y, T[pos].z, T[pos].w}, vn[3] = {T[posnext].y, T[posnext].z, T[posnext].w};
+  for (int k = 0; k < 3; k++) {
+    double v;
+    if (f == 0.) v = vi[k];
+    else if (f >= 1.) v = vn[k];
+    else {
+      v = __dadd_rn(__dmul_rn(__dsub_rn(vn[k], vi[k]), f), vi[k]);
+      if (vi[k] == DBL_MAX) v = DBL_MAX;
+      else if (vn[k] == DBL_MAX) v = vi[k];
+    }
+    out[k] = (v == DBL_MAX ? FLT_MAX : float(v));
+  }
+}
+
 // Stage 2, one lane per body: the partial sums in order, then FtCalcForces +
-// FtCalcForcesRes + constraints.
+// FtCalcForcesRes + imposed velocities + constraints.  tab/desc: the bodies' JLinearValue
+// tables (desc[body*4 + kind] = {first row, rows}, kinds SPH_FTTAB_*; nullptr: none).
 __global__ void k_ft_forces(const DevScalars* __restrict__ sc, KConst K, FtBody* __restrict__ bodies, int nbodies,
-                            const float* __restrict__ part, int predictor) {
+                            const float* __restrict__ part, int predictor, const double4* __restrict__ tab,
+                            const int2* __restrict__ desc) {
   const int cf = blockIdx.x * blockDim.x + threadIdx.x;
   if (cf >= nbodies) return;
   FtBody& b = bodies[cf];
@@ -498,7 +534,19 @@ __global__ void k_ft_forces(const DevScalars* __restrict__ sc, KConst K, FtBody*
   const M3f inert = m3_mul(m3_mul(frot, ini), m3_tras(frot));
   const M3f inv = m3_inv(inert);
   float face[3] = {red[0], red[1], red[2]};
-  const float fo[3] = {red[3], red[4], red[5]};
+  float fo[3] = {red[3], red[4], red[5]};
+  // external forces (RunFloating, JSphCpuSingle.cpp:904-914; added in FtCalcForces :797-798)
+  const double tstep = sc->tstep0;
+  if (desc && desc[cf * 4 + 2].y) {
+    float e[3];
+    ft_table_eval(tab, desc[cf * 4 + 2], tstep, e);
+    for (int k = 0; k < 3; k++) face[k] = face[k] + e[k];
+  }
+  if (desc && desc[cf * 4 + 3].y) {
+    float e[3];
+    ft_table_eval(tab, desc[cf * 4 + 3], tstep, e);
+    for (int k = 0; k < 3; k++) fo[k] = fo[k] + e[k];
+  }
   float omegaace[3] = {fo[0] * inv.a11 + fo[1] * inv.a12 + fo[2] * inv.a13,
                        fo[0] * inv.a21 + fo[1] * inv.a22 + fo[2] * inv.a23,
                        fo[0] * inv.a31 + fo[1] * inv.a32 + fo[2] * inv.a33};
@@ -507,11 +555,30 @@ __global__ void k_ft_forces(const DevScalars* __restrict__ sc, KConst K, FtBody*
   face[1] = (face[1] + fmass * K.gravy) / fmass;
   face[2] = (face[2] + fmass * K.gravz) / fmass;
   // FtCalcForcesRes
-  float fomega[3], fvel[3];
+  float fomega[3], fvel[3], fvel0[3] = {b.fvel[0], b.fvel[1], b.fvel[2]};
   for (int k = 0; k < 3; k++) fomega[k] = float(dt * omegaace[k] + b.fomega[k]);
+  if (K.sim2d) {  // Simulate2D (JSphCpuSingle.cpp:839)
+    face[1] = 0;
+    fomega[0] = 0;
+    fomega[2] = 0;
+    fvel0[1] = 0;
+  }
   double fcenter[3];
-  for (int k = 0; k < 3; k++) fcenter[k] = b.center[k] + dt * b.fvel[k];
-  for (int k = 0; k < 3; k++) fvel[k] = float(dt * face[k] + b.fvel[k]);
+  for (int k = 0; k < 3; k++) fcenter[k] = b.center[k] + dt * fvel0[k];
+  for (int k = 0; k < 3; k++) fvel[k] = float(dt * face[k] + fvel0[k]);
+  // FtApplyImposedVel (JSphCpuSingle.cpp:874-891): components given by the tables
+  if (desc && desc[cf * 4 + 0].y) {
+    float v[3];
+    ft_table_eval(tab, desc[cf * 4 + 0], tstep, v);
+    for (int k = 0; k < 3; k++)
+      if (v[k] != FLT_MAX) fvel[k] = v[k];
+  }
+  if (desc && desc[cf * 4 + 1].y) {
+    float v[3];
+    ft_table_eval(tab, desc[cf * 4 + 1], tstep, v);
+    for (int k = 0; k < 3; k++)
+      if (v[k] != FLT_MAX) fomega[k] = v[k];
+  }
   // FtApplyConstraints (DualSphDef.h:466-473)
   const unsigned con = b.constraints;
   if (con) {
@@ -579,9 +646,10 @@ void launch_ft_partial(hipStream_t stm, DevScalars* sc, const FtBody* bodies, in
 }
 
 void launch_ft_body(hipStream_t stm, DevScalars* sc, const KConst& K, FtBody* bodies, int nbodies,
-                    const unsigned* ftridp, unsigned nftp, const PartArrays& a, bool predictor, const float* part) {
+                    const unsigned* ftridp, unsigned nftp, const PartArrays& a, bool predictor, const float* part,
+                    const double4* fttab, const int2* ftdesc) {
   hipLaunchKernelGGL(k_ft_forces, dim3((nbodies + 63) / 64), dim3(64), 0, stm, sc, K, bodies, nbodies, part,
-                     int(predictor));
+                     int(predictor), fttab, ftdesc);
   hipLaunchKernelGGL(k_ft_update, dim3((nftp + 255) / 256), dim3(256), 0, stm, sc, K, bodies, nbodies, ftridp, nftp,
                      a, int(predictor));
 }

@@ -153,6 +153,11 @@ int sph_solver_set_floatings(SphSolver* s, uint32_t nft, const SphFloatingDef* d
   NEED(s && defs);
   return guard([&] { s->impl->SetFloatings(nft, defs, ftpause); });
 }
+int sph_solver_set_floating_table(SphSolver* s, uint32_t body, int32_t kind, uint32_t n, const double* times,
+                                  const double* values) {
+  NEED(s && times && values);
+  return guard([&] { s->impl->SetFloatingTable(body, kind, n, times, values); });
+}
 int sph_solver_floatings(SphSolver* s, uint32_t cap, SphFloatingState* out, uint32_t* nft) {
   NEED(s);
   return guard([&] {

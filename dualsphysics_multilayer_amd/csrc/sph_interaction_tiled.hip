@@ -554,9 +554,14 @@ __device__ __forceinline__ void half_row(int i, int& dy, int& dz) {
   }
 }
 
-// CellMode=half pass: 6 units of two lower rows + their mirrors (4 rows staged as one
-// segment when they fit TCAP, drained as one set by tile_unit4), then the own row; a
+// CellMode=half pass: units of HALF_LPU lower rows + their mirrors (2 or 4 rows staged as
+// one segment when they fit TCAP, drained as one set by tile_unit4), then the own row; a
 // unit too long for one segment goes row by row in TCAP segments.
+#ifndef SPH_HALF_LPU
+#define SPH_HALF_LPU 1
+#endif
+constexpr int HALF_LPU = SPH_HALF_LPU;
+static_assert(HALF_LPU == 1 || HALF_LPU == 2, "1 or 2 lower rows per unit");
 template <int TDENSITY, int MODE, bool FT = false>
 __device__ __forceinline__ TAcc run_pass_half(const KConst& K, const DivGrid& g, const RowCtx& rc, const P1& p,
                                               float thr, const PassK Q, const unsigned* __restrict__ bc,
@@ -569,13 +574,14 @@ __device__ __forceinline__ TAcc run_pass_half(const KConst& K, const DivGrid& g,
   acc.dstop = dstop0;
   const unsigned cellinit = (MODE == 1 ? 0u : g.boxfluid);
   constexpr int tcap = TcapT<FT>::v;
-  for (int u = 0; u < 7; u++) {
+  constexpr int NU = 12 / HALF_LPU;  // units of lower rows; unit NU is the own row
+  for (int u = 0; u <= NU; u++) {
     int dyr[4], dzr[4];
     unsigned rs[4], re[4], ls[4], le[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       int dy = 0, dz = 0;
-      if (u < 6) half_row(2 * u + (k >> 1), dy, dz);
+      if (u < NU) half_row(HALF_LPU * u + (k >> 1), dy, dz);
       if (k & 1) {
         dy = -dy;
         dz = -dz;
@@ -584,7 +590,7 @@ __device__ __forceinline__ TAcc run_pass_half(const KConst& K, const DivGrid& g,
       dzr[k] = dz;
       rs[k] = re[k] = ls[k] = le[k] = 0u;
       const int z = rc.cz + dz, y = rc.cy + dy;
-      if ((u == 6 && k) || z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;
+      if ((u == NU && k) || (k >> 1) >= HALF_LPU || z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;
       const unsigned rowbase = cellinit + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
       rs[k] = bc[rowbase + rc.xa];
       re[k] = bc[rowbase + rc.xb + 1];

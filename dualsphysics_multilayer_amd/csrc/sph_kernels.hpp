@@ -239,8 +239,10 @@ constexpr int FT_NBLK = 32;  // partial-sum blocks per body; part = float[nbodie
 // between), then body integration + particle update + body state.
 void launch_ft_partial(hipStream_t stm, DevScalars* sc, const FtBody* bodies, int nbodies, const unsigned* ftridp,
                        const float4* arace, const PartArrays& a, float* part);
+// fttab/ftdesc: the bodies' imposed-velocity / external-force tables (SPH_FTTAB_*), or nullptr.
 void launch_ft_body(hipStream_t stm, DevScalars* sc, const KConst& K, FtBody* bodies, int nbodies,
-                    const unsigned* ftridp, unsigned nftp, const PartArrays& a, bool predictor, const float* part);
+                    const unsigned* ftridp, unsigned nftp, const PartArrays& a, bool predictor, const float* part,
+                    const double4* fttab = nullptr, const int2* ftdesc = nullptr);
 
 // ---- slab decomposition (sph_slab.hip) ----
 // A particle MIGRATING to a neighbour: its full state, 112 B.  A boundary particle also

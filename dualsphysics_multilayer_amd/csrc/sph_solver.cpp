@@ -974,7 +974,8 @@ void SphGpuSingle::RunFloating(bool predictor) {
   // partial sums are added over the slabs, every slab integrates the same body
   launch_ft_partial(stream, sc_, ftbodies_, nftbodies_, ftridp_, arace_, cur_, ftpart_);
   if (slab()) transport_->allreduce_sum_f32(ftpart_, nftbodies_ * FT_NBLK * 6, stream);
-  launch_ft_body(stream, sc_, K, ftbodies_, nftbodies_, ftridp_, nftp_, cur_, predictor, ftpart_);
+  launch_ft_body(stream, sc_, K, ftbodies_, nftbodies_, ftridp_, nftp_, cur_, predictor, ftpart_, fttab_,
+                 fttabdesc_);
   TimedEnd(1);
 }
 
@@ -1097,6 +1098,43 @@ void SphGpuSingle::SetFloatings(unsigned nft, const SphFloatingDef* defs, double
   // per-particle kernel under SPH_INTERACTION=simple / CellMode=half)
   launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_, K, G);
   Sync();
+}
+
+// FtLinearVel / FtAngularVel / FtLinearForce / FtAngularForce of one body (JSph.cpp:1060-1082):
+// the rows are re-uploaded as one buffer with a {first row, rows} descriptor per table.
+void SphGpuSingle::SetFloatingTable(unsigned body, int kind, unsigned n, const double* times, const double* values) {
+  if (stepped_) throw SphError(SPH_ERR_STATE, "floating tables are configured before the first step");
+  if (!ftbodies_ || body >= unsigned(nftbodies_)) throw SphError(SPH_ERR_ARG, "floating table of an unknown body");
+  if (kind < SPH_FTTAB_LINVEL || kind > SPH_FTTAB_ANGFORCE) throw SphError(SPH_ERR_ARG, "invalid floating table kind");
+  if (!n || !times || !values) throw SphError(SPH_ERR_ARG, "There are not times.");
+  std::vector<double4> rows(n);
+  for (unsigned i = 0; i < n; i++) {
+    if (i && !(times[i] >= times[i - 1])) throw SphError(SPH_ERR_ARG, "floating table times must be nondecreasing");
+    const double* v = values + 3 * size_t(i);
+    if (kind >= SPH_FTTAB_LINFORCE && (v[0] == DBL_MAX || v[1] == DBL_MAX || v[2] == DBL_MAX))
+      throw SphError(SPH_ERR_ARG, "external forces have no 'none' components");
+    rows[i] = make_double4(times[i], v[0], v[1], v[2]);
+  }
+  fttabs_.resize(size_t(nftbodies_) * 4);
+  fttabs_[size_t(body) * 4 + size_t(kind)] = rows;
+  std::vector<double4> all;
+  std::vector<int2> desc(fttabs_.size(), make_int2(0, 0));
+  for (size_t t = 0; t < fttabs_.size(); t++) {
+    desc[t] = make_int2(int(all.size()), int(fttabs_[t].size()));
+    all.insert(all.end(), fttabs_[t].begin(), fttabs_[t].end());
+  }
+  Sync();
+  for (void* p : {(void*)fttab_, (void*)fttabdesc_}) {
+    if (!p) continue;
+    (void)hipFree(p);
+    allocs_.erase(std::remove(allocs_.begin(), allocs_.end(), p), allocs_.end());
+  }
+  check_hip(hipMalloc((void**)&fttab_, sizeof(double4) * all.size()), "hipMalloc floating tables");
+  allocs_.push_back(fttab_);
+  check_hip(hipMalloc((void**)&fttabdesc_, sizeof(int2) * desc.size()), "hipMalloc floating tables");
+  allocs_.push_back(fttabdesc_);
+  check_hip(hipMemcpy(fttab_, all.data(), sizeof(double4) * all.size(), hipMemcpyHostToDevice), "upload tables");
+  check_hip(hipMemcpy(fttabdesc_, desc.data(), sizeof(int2) * desc.size(), hipMemcpyHostToDevice), "upload tables");
 }
 
 unsigned SphGpuSingle::Floatings(SphFloatingState* out, unsigned cap) {

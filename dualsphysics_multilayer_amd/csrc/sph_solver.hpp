@@ -84,6 +84,8 @@ class SphGpuSingle {
   // Moving boundaries / floating bodies (sph_bodies.hip), configured before the first step.
   void SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* movs, unsigned nevt, const SphMotionEvent* evts);
   void SetFloatings(unsigned nft, const SphFloatingDef* defs, double ftpause);
+  // Imposed velocity / external force table of one body (SPH_FTTAB_*), before the first step.
+  void SetFloatingTable(unsigned body, int kind, unsigned n, const double* times, const double* values);
   // Slabs: re-balance the column bounds every `every` steps (0: never) when the most loaded
   // slab exceeds the mean by more than `tolerance`; collective (all ranks the same values).
   void SetRepartition(unsigned every, double bound_weight, double tolerance);
@@ -157,6 +159,9 @@ class SphGpuSingle {
   unsigned* ftridp_ = nullptr;   // floating particle (idp - CaseNpb) -> position, per divide
   float* ftmassp_ = nullptr;     // particle mass per body (interaction)
   float* ftpart_ = nullptr;      // partial force sums [body][FT_NBLK][6]
+  double4* fttab_ = nullptr;     // JLinearValue rows (time, x, y, z) of every body's tables
+  int2* fttabdesc_ = nullptr;    // [body][SPH_FTTAB_*] = {first row, rows}
+  std::vector<std::vector<double4>> fttabs_;  // host copy, [body * 4 + kind]
   int nftbodies_ = 0;
   unsigned nftp_ = 0;            // floating particles of the case (CaseNfloat)
   unsigned casenpb_ = 0;         // CaseNpb: first floating idp

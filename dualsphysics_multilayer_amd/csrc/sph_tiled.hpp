@@ -40,11 +40,13 @@ constexpr int TCAP = SPH_TCAP;
 template <bool FT> struct TcapT { static constexpr int v = TCAP; };
 template <> struct TcapT<true> { static constexpr int v = SPH_TCAP_FT; };
 constexpr int TMAXCELLS = 4;   // max x-cells per item (CellMode=full: cells of 2h)
-// CellMode=half (cells of h, +-2-cell stencil): an item spans <= 16 half-cells, so its
-// staged rows [a-2, b+2] are <= 20 half-cells = 10h long and two mirrored row pairs
-// (4 rows) fit one TCAP segment at the lattice density (~5.2 particles per half-cell).
+// CellMode=half (cells of h, +-2-cell stencil): an item spans <= 32 half-cells (at the
+// lattice density, ~5.2 particles per half-cell, TB particles take ~25), so its staged
+// rows [a-2, b+2] hold ~150 records and a mirrored row pair fits one TCAP segment.
+// Measured at 1M (interaction ms): 12 cells 1.13, 16: 0.95, 20: 0.87 with units of two
+// mirrored pairs; 24: 0.84, 32: 0.77 with units of one pair (SPH_HALF_LPU=1).
 #ifndef SPH_TMAXCELLS_HALF
-#define SPH_TMAXCELLS_HALF 16
+#define SPH_TMAXCELLS_HALF 32
 #endif
 constexpr int TMAXCELLS_HALF = SPH_TMAXCELLS_HALF;
 

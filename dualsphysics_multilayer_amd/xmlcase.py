@@ -591,9 +591,6 @@ class XmlCase:
                 raise CaseError(f"<floating>: the item is not found '{name}'.")
             return tuple(_attr_double(x, a, name) for a in "xyz")
 
-        for unsup in ("linearvel", "angularvel", "linearforce", "angularforce"):
-            if e.find(unsup) is not None:
-                raise CaseError(f"<floating><{unsup}> (imposed velocity/force) is not supported by this core.")
         f = dict(massbody=_elem_double(e, "massbody"), masspart=_elem_double(e, "masspart"), center=d3("center"))
         ine = e.find("inertia")
         if ine is None:
@@ -618,7 +615,41 @@ class XmlCase:
         f["rotationfree"] = i3("rotation", "rotationDOF")
         f["linvelini"] = d3("linearvelini" if e.find("linearvelini") is not None else "velini", True)
         f["angvelini"] = d3("angularvelini" if e.find("angularvelini") is not None else "omegaini", True)
+        # imposed velocities ("none" components free) and external forces (JCaseParts.cpp:272-285)
+        for name, sub, special in (("linearvel", "vel", True), ("angularvel", "vel", True),
+                                   ("linearforce", "force", False), ("angularforce", "force", False)):
+            tab = XmlCase._load_linear_values(e, name, sub, special)
+            if tab is not None:
+                f[name] = tab
         return f
+
+    # -- JLinearValue::ReadXmlValues (JLinearValue.cpp:493-527), attributes time:x:y:z ---------------
+    @staticmethod
+    def _load_linear_values(e, name, sub, special):
+        x = e.find(name)
+        if x is None:
+            return None
+        if x.get("file"):
+            raise CaseError(f"<{name} file=...>: tables from files are not supported by this core.")
+        rows = []
+        for r in x.findall(sub):
+            t = _attr_double(r, "time", sub)
+            vals = []
+            for a in "xyz":
+                txt = r.get(a)
+                if special:  # "none" or missing -> DBL_MAX (the component is not imposed)
+                    vals.append(np.finfo(np.float64).max if txt is None or txt.strip().lower() == "none"
+                                else _attr_double(r, a, sub))
+                else:
+                    if txt is None:
+                        raise CaseError(f"<{name}><{sub}>: the attribute '{a}' is not found.")
+                    vals.append(_attr_double(r, a, sub))
+            rows.append((t,) + tuple(vals))
+        if not rows:
+            raise CaseError("There are not times.")
+        if any(rows[i][0] < rows[i - 1][0] for i in range(1, len(rows))):
+            raise CaseError(f"<{name}>: times must be nondecreasing.")
+        return np.array(rows, np.float64)
 
     # -- JMotion::ReadXml (JMotion.cpp:556-700) + JDsMotion::ConfigObjects (JDsMotion.cpp:67-89) --
     def _load_motion(self, node):

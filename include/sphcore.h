@@ -46,6 +46,8 @@
  *                                (JDsMotion.cpp:94-137, JSph.cpp:2308, JSphCpu.cpp:1692-1789)
  *   sph_solver_set_floatings ... JSph::LoadCaseConfig floating objects (JSph.cpp:1046-1100) +
  *                                JSphCpuSingle::RunFloating (JSphCpuSingle.cpp:897-1010)
+ *   sph_solver_set_floating_table  FtLinearVel/FtAngularVel/FtLinearForce/FtAngularForce
+ *                                (JSph.cpp:1060-1082; JSphCpuSingle.cpp:874-914)
  *   sph_solver_floatings ....... FtObjs[] (feeds PartFloat.fbi4, JPartFloatBi4)
  */
 #ifndef SPHCORE_H
@@ -442,6 +444,18 @@ typedef struct SphFloatingState {
 /* Configure the floating bodies (call once, before the first step); ftpause = FtPause.
  * On slabs every rank passes all bodies; their force sums are added over the ranks. */
 int sph_solver_set_floatings(SphSolver* s, uint32_t nft, const SphFloatingDef* defs, double ftpause);
+/* Imposed velocities and external forces of floating body `body` (JCasePartBlock_Floating
+ * <linearvel> <angularvel> <linearforce> <angularforce>, JCaseParts.cpp:270-285 -> FtLinearVel,
+ * FtAngularVel, FtLinearForce, FtAngularForce, JSph.cpp:1060-1082): a JLinearValue table of n
+ * rows, times[n] nondecreasing and values[n][3], evaluated at the step's TimeStep by linear
+ * interpolation (JLinearValue::GetValue3f, JLinearValue.cpp:209-390) inside RunFloating
+ * (JSphCpuSingle.cpp:897-924): forces are added to the particle force sums before FtCalcForces;
+ * velocities replace the integrated fvel/fomega components that are not "none" (DBL_MAX,
+ * FtApplyImposedVel, :874-891), before the constraints.  Call after sph_solver_set_floatings,
+ * before the first step (again for another table); on slabs on every rank. */
+enum { SPH_FTTAB_LINVEL = 0, SPH_FTTAB_ANGVEL = 1, SPH_FTTAB_LINFORCE = 2, SPH_FTTAB_ANGFORCE = 3 };
+int sph_solver_set_floating_table(SphSolver* s, uint32_t body, int32_t kind, uint32_t n, const double* times,
+                                  const double* values);
 int sph_solver_floatings(SphSolver* s, uint32_t cap, SphFloatingState* out, uint32_t* nft);
 /* PartFloat.fbi4 (JPartFloatBi4Save::SaveInitial + AddPartFloat/SavePartFloat,
  * JPartFloatBi4.cpp:243-346): per-body head arrays [nft] and, per saved PART k, its

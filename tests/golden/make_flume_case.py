@@ -33,6 +33,21 @@ VARIANTS = {
     # a fast, wide flap (no wait, 8 Hz, 12 degrees): its mDBC particles cross cell columns
     # within the run (the slab hand-over of turned normals, tests/test_bodies.py)
     "symplectic_ddt1_mdbc_fastflap": (0.025, 2, 1, 2, 80, (1, 40, 80), ("1.2", "0.3", "0.4", "0.2", "0", "8", "12")),
+    # the floating box with imposed velocities ("none" components stay free) and external
+    # forces (JLinearValue tables of <floating>, FtApplyImposedVel / GetFtExternalForce*)
+    "verlet_ddt2_ftvel": (0.025, 1, 2, 1, 100, (1, 10, 50, 100), (), "ftvel"),
+}
+
+# <floating> additions of the XML edits (JCasePartBlock_Floating::ReadXml, JCaseParts.cpp:270-285)
+XML_EDITS = {
+    "ftvel": ('<linearvel><vel time="0" x="0.05" y="none" z="none"/><vel time="0.006" x="0.2"/>'
+              '<vel time="0.02" x="-0.1" z="0.05"/><vel time="0.025" x="0" z="none"/></linearvel>'
+              '<angularvel><vel time="0" x="none" y="0.4" z="none"/><vel time="0.012" x="none" y="-0.6" z="none"/>'
+              '</angularvel>'
+              '<linearforce><force time="0" x="0" y="0.2" z="3"/><force time="0.03" x="0.5" y="0.2" z="1"/>'
+              '</linearforce>'
+              '<angularforce><force time="0" x="0.002" y="0" z="-0.001"/><force time="0.015" x="0" y="0" z="0.003"/>'
+              '</angularforce>'),
 }
 
 
@@ -51,13 +66,18 @@ def load_ft(fn):
     return np.array(t), np.array(c).reshape(sh), np.array(v).reshape(sh), np.array(w).reshape(sh)
 
 
-def make(name, dp, step, ddt, boundary, nsteps, keep, extra=()):
+def make(name, dp, step, ddt, boundary, nsteps, keep, extra=(), xml_edit=None):
     out_dir = os.path.join(HERE, "bi4", "flume_" + name)
     os.makedirs(out_dir, exist_ok=True)
     tmp = tempfile.mkdtemp(prefix="flume_")
     try:
         subprocess.check_call([os.path.join(REF, "genflume_ref"), repr(dp), tmp, str(step), str(ddt), "1.0",
                                "CaseFlume", str(boundary)] + list(extra), stdout=subprocess.DEVNULL)
+        if xml_edit:
+            fx = os.path.join(tmp, "CaseFlume.xml")
+            txt = open(fx).read()
+            assert txt.count("</floating>") == 1
+            open(fx, "w").write(txt.replace("</floating>", XML_EDITS[xml_edit] + "</floating>"))
         files = ["CaseFlume.xml", "CaseFlume.bi4"] + (["CaseFlume_Normals.nbi4"] if boundary == 2 else [])
         for f in files:
             shutil.copy(os.path.join(tmp, f), os.path.join(out_dir, f))

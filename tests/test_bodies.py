@@ -78,9 +78,11 @@ def test_unsupported_body_features_refused(tmp_path):
 
     with pytest.raises(CaseError, match="RigidAlgorithm"):
         XmlCase(variant(lambda s: s.replace('key="RigidAlgorithm" value="1"', 'key="RigidAlgorithm" value="2"')))
-    with pytest.raises(CaseError, match="imposed"):
-        XmlCase(variant(lambda s: s.replace("</floating>", '<linearvel><velvalues time="0" x="1" y="0" z="0"/>'
-                                                          "</linearvel></floating>")))
+    with pytest.raises(CaseError, match="from files"):
+        XmlCase(variant(lambda s: s.replace("</floating>", '<linearvel file="vel.csv"/></floating>')))
+    with pytest.raises(CaseError, match="nondecreasing"):
+        XmlCase(variant(lambda s: s.replace("</floating>", '<linearforce><force time="1" x="0" y="0" z="0"/>'
+                                                          '<force time="0" x="0" y="0" z="0"/></linearforce></floating>')))
     with pytest.raises(CaseError, match="mvcir"):
         XmlCase(variant(lambda s: s.replace("<wait ", "<mvcir ")))
     with pytest.raises(CaseError, match="mobile objects"):
@@ -404,3 +406,72 @@ def test_gpu_mdbc_flap_normals_cross_slab_faces():
     fin = grp.particles()["pos"][flap]
     cols = ((fin[:, 0] - k["map_realposmin"][0]) // np.float32(k["scell"])).astype(int)
     assert (cols != cflap).any()
+
+
+# ---- imposed floating velocities and external forces -----------------------------------------
+FTVEL = "verlet_ddt2_ftvel"
+
+
+def test_floating_tables_loaded():
+    """<linearvel>/<angularvel> (JLinearValue with special values: "none" or a missing
+    component -> DBL_MAX, not imposed) and <linearforce>/<angularforce> rows (time, x, y, z)."""
+    f = _case(FTVEL).floatings[0]
+    big = np.finfo(np.float64).max
+    lv = f["linearvel"]
+    assert lv.shape == (4, 4) and list(lv[:, 0]) == [0.0, 0.006, 0.02, 0.025]
+    assert lv[0, 1] == 0.05 and lv[0, 2] == big and lv[1, 2] == big and lv[2, 3] == 0.05 and lv[3, 3] == big
+    assert f["angularvel"][1, 2] == -0.6 and f["angularvel"][1, 1] == big
+    assert f["linearforce"][1].tolist() == [0.03, 0.5, 0.2, 1.0]
+    assert f["angularforce"].shape == (2, 4)
+    assert "linearvel" not in _case("verlet_ddt2").floatings[0]
+
+
+@pytest.mark.gpu
+def test_gpu_floating_imposed_velocity_matches_reference():
+    """The floating box with imposed x/z velocities and y rotation rate over time (free
+    components integrated) and external forces/torques (JSphCpuSingle.cpp:874-924): body
+    state after every step vs the reference's PartFloat.fbi4 -- imposed components equal the
+    reference's to float rounding of the table time --, particles vs the reference PARTs."""
+    x, g = _case(FTVEL), _ref(FTVEL)
+    s = _gpu(x)
+    n = int(g["meta"][3])
+    kept = set(_kept(g))
+    worst = np.zeros(3)
+    for k in range(1, n + 1):
+        s.run(1)
+        b = s.floatings()[0]
+        worst = np.maximum(worst, [np.abs(b["center"] - g["ft_center"][k, 0]).max(),
+                                   np.abs(b["fvel"] - g["ft_fvel"][k, 0]).max(),
+                                   np.abs(b["fomega"] - g["ft_fomega"][k, 0]).max()])
+        if k in kept:
+            got, ref = by_idp(s.particles()), _snap(g, k)
+            assert np.array_equal(got["idp"], ref["idp"])
+            for q, t in zip(("pos", "vel", "rhop"), _tol(k)):
+                assert maxdiff(got, ref, q) <= t, (k, q, maxdiff(got, ref, q))
+    assert worst[0] <= 1e-7, worst
+    assert worst[1] <= 2e-3 * np.abs(g["ft_fvel"]).max() + 1e-6, worst
+    assert worst[2] <= 2e-3 * np.abs(g["ft_fomega"]).max() + 1e-5, worst
+    # the imposed components are the table's values (step 1: TimeStep 0)
+    b1 = g["ft_fvel"][1, 0]
+    assert b1[0] == np.float32(0.05) and g["ft_fomega"][1, 0][1] == np.float32(0.4)
+
+
+@pytest.mark.gpu
+def test_gpu_floating_imposed_velocity_on_slabs():
+    """The same case on 2 in-process slabs (every rank evaluates the tables; force sums added
+    over the slabs) vs the reference PARTs and body states."""
+    from dualsphysics_multilayer_amd.core import SphSlabGroup, slab_partition
+
+    x, g = _case(FTVEL), _ref(FTVEL)
+    grp = SphSlabGroup(x, slab_partition(x, 2))
+    done = 0
+    for k in _kept(g):
+        grp.run(k - done)
+        done = k
+        got, ref = grp.particles(), _snap(g, k)
+        assert np.array_equal(got["idp"], ref["idp"])
+        for q, t in zip(("pos", "vel", "rhop"), _tol(k)):
+            assert maxdiff(got, ref, q) <= t, (k, q, maxdiff(got, ref, q))
+        b = grp.floatings()[0]
+        assert np.abs(b["center"] - g["ft_center"][k, 0]).max() <= 1e-7
+        assert np.abs(b["fvel"] - g["ft_fvel"][k, 0]).max() <= 2e-3 * np.abs(g["ft_fvel"]).max() + 1e-6
