@@ -145,7 +145,7 @@ def port_cpu_baseline(case, nsteps: int, threads: int) -> dict:
                       % (case.np, nsteps)}
 
 
-def profiled_traffic(kernel_prefix: str, np_: int, workload: str):
+def profiled_traffic(kernel_prefix, np_: int, workload: str):
     """HBM bytes per launch of the dominant kernel from the latest committed PMC passes
     (profiles/<round>/pmc_traffic.json: 2*FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md
     §HBM) of the same workload on one GPU; None if there is none."""
@@ -160,8 +160,9 @@ def profiled_traffic(kernel_prefix: str, np_: int, workload: str):
             b = json.load(open(bj))
             if b["config"]["np"] != np_ or b["n_gpus"] != 1 or not b["config"]["workload"].startswith(workload):
                 continue
+            prefixes = (kernel_prefix,) if isinstance(kernel_prefix, str) else tuple(kernel_prefix)
             for k, v in json.load(open(tj)).items():
-                if k.startswith(kernel_prefix):
+                if k.startswith(prefixes):
                     found = {"bytes": v["traffic_bytes_per_launch"], "avg_ns": v.get("avg_ns"),
                              "source": os.path.relpath(tj, ROOT) + " (2*FETCH_SIZE + WRITE_SIZE, %s)" % k}
         except (KeyError, ValueError):
@@ -323,8 +324,12 @@ def main() -> None:
         achieved = flops / (inter_ms * 1e-3) / 1e12 if inter_ms > 0 else None
         value = units / elapsed
         hbm_achieved = value * BYTES_PER_PARTICLE_STEP[case.step_algorithm] / 1e9
-        kname = ("sphx::k_nn_tiled<%d, %d, true>" % (case.tvisco, case.tdensity) if nn else
-                 "sphx::k_fluid_tiled<%d, %s>" % (case.tdensity, "true" if getattr(case, "floatings", None) else "false"))
+        # the tiled kernel's instantiation: DDT mode (| 8: Fourtakas term as its series),
+        # floating records, cell mode (sph_interaction_tiled.hip launch_fluid_tiled_s)
+        ftb = "true" if getattr(case, "floatings", None) else "false"
+        kname = (["sphx::k_nn_tiled<%d, %d, true>" % (case.tvisco, case.tdensity)] if nn else
+                 ["sphx::k_fluid_tiled<%d, %s, %d>" % (td, ftb, case.cellmode)
+                  for td in ((case.tdensity | 8, case.tdensity) if case.tdensity >= 2 else (case.tdensity,))])
         traffic = profiled_traffic(kname, case.np, "BASELINE " + args.workload) if world == 1 else None
         res = {
             "metric": METRIC,

@@ -209,9 +209,11 @@ struct PassK {
 // One pair body (JSphCpu.cpp:682-797 semantics, fast f32 intrinsics).
 // MODE 0: fluid p1 / fluid p2, 1: fluid p1 / bound p2, 2: bound p1 / fluid p2
 // (InteractionForcesBound, JSphCpu.cpp:577-612: continuity + visc-dt only).
-// `ok` = the reference's pair test (rr2 <= KernelSize2 && rr2 >= ALMOSTZERO); a pair
-// with !ok contributes exactly +0 (kernel factor forced to 0, visc term masked), which
-// keeps the body branch-free so two pairs can be interleaved.
+// `ok` = rr2 <= KernelSize2, the reference's pair test (JSphCpu.cpp:679); a pair beyond it
+// contributes exactly +0 (kernel factor clamped to 0, visc term masked), which keeps the
+// body branch-free so two pairs can be interleaved.  The test's lower bound rr2 >=
+// ALMOSTZERO only removes p1 itself (and exactly coincident particles), whose terms all
+// carry a factor dr = 0 or dr.dv = 0 and add +0 here.
 // Algebra used (same quantities, fewer operations; constants folded into PassK):
 //   fac = bwen*q*(1-q/2)^3/rad = (bwen/h)*w3,  w3 = (1-rad/(2h))^3   (FunSphKernel.h:217-224)
 //   dv.fr = fac*(dr.dv), dr.fr = fac*rr2
@@ -226,9 +228,12 @@ struct PassK {
 template <int TDENSITY, int MODE, bool FT = false, typename CR = float2>
 __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float drx, float dry, float drz, float rr2,
                                           bool ok, const float4& B, const CR& C, const PassK& Q, TAcc& a) {
+  constexpr int TD = TDENSITY & 7;  // DDT mode; bit 3: the Fourtakas term as its series (K.ddtseries)
   const float rad = fsqrt_(rr2);
-  const float wq = fmaf(K.mhalfovh, rad, 1.f);
-  const float w3 = ok ? wq * wq * wq : 0.f;
+  // 1 - rad/2h clamped to [0, 1] (the fma's clamp modifier): 0 beyond the support radius,
+  // so the kernel factor needs no pair test
+  const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
+  const float w3 = wq * wq * wq;
   const float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
   const float dot = drx * dvx + dry * dvy + drz * dvz;
   const float re = rr2 + K.eta2;
@@ -246,31 +251,31 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
   a.ar = fmaf(wc, dot, a.ar);
   if (MODE == 2) return;
   const float S = fmaf(C.y, p.press, C.x);  // (p1+p2)/rho2
-  float pv = (dot < 0.f) ? Q.cvp * dot * rr : 0.f;
+  float pv = Q.cvp * fminf(dot, 0.f) * rr;  // artificial viscosity only for approaching pairs
   if (FT) pv *= crec_r(C);  // viscosity with the p2 mass
   const float c = w3 * (S + pv);
   a.ax = fmaf(c, drx, a.ax);
   a.ay = fmaf(c, dry, a.ay);
   a.az = fmaf(c, drz, a.az);
   if (MODE == 1) {
-    if (TDENSITY == 1 && K.mdbc) {  // mDBC: Molteni DDT over bound neighbours too (JSphCpu.cpp:730)
+    if (TD == 1 && K.mdbc) {  // mDBC: Molteni DDT over bound neighbours too (JSphCpu.cpp:730)
       const float t = w3 * rr2 * inv_re;
       a.delta = fmaf(t, (p.vr.w - B.w) * C.y, a.delta);
-    } else if ((TDENSITY == 1 || TDENSITY == 2) && ok) {
+    } else if ((TD == 1 || TD == 2) && ok) {
       a.delta = FLT_MAX;  // DBC: no DDT next to the boundary
     }
     return;
   }
-  if (TDENSITY == 1) {
+  if (TD == 1) {
     // rho1/rho2 - 1 as (rho1 - rho2)*(1/rho2): exactly 0 for equal densities (rho1*rcp(rho2)
     // - 1 with the approximate v_rcp leaves a +-1 ulp residue, which at t=0 is the whole
     // Molteni sum); C.y = r/rho2 carries the p2 mass ratio r (1 without floating bodies)
     const float t = w3 * rr2 * inv_re;
     a.delta = fmaf(t, (p.vr.w - B.w) * C.y, a.delta);
     if (FT && ok && crec_kind(C) == 2.f) a.dstop = true;  // light floating p2
-  } else if (TDENSITY == 2 || TDENSITY == 3) {
+  } else if (TD == 2 || TD == 3) {
     float drhop;
-    if (K.ddtseries)  // kernel-uniform (scalar) branch
+    if (TDENSITY & 8)  // K.ddtseries, a template flag (no per-pair branch)
       drhop = drz * fmaf(drz, fmaf(drz, fmaf(drz, K.ddte4, K.ddte3), K.ddte2), K.ddte1);
     else
       drhop = K.rhopzero * fexp2(K.ovgamma * flog2(1.f + K.ddtgz * drz)) - K.rhopzero;
@@ -283,6 +288,7 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
 // The per-pass factors of the sums (PassK) applied once per particle.
 template <int TDENSITY, int MODE, bool FT = false>
 __device__ __forceinline__ TAcc finish(const KConst& K, TAcc a, const P1& p, const PassK& Q) {
+  constexpr int TD = TDENSITY & 7;
   a.ar *= Q.ar1;
   if (MODE != 2) {
     const float s = -Q.bm * p.inv_rho;
@@ -290,11 +296,11 @@ __device__ __forceinline__ TAcc finish(const KConst& K, TAcc a, const P1& p, con
     a.ay *= s;
     a.az *= s;
   }
-  if (MODE == 0 || (MODE == 1 && TDENSITY == 1 && K.mdbc)) {
-    if (TDENSITY == 1) a.delta *= Q.kd;
-    else if (TDENSITY == 2 || TDENSITY == 3) a.delta *= -Q.kd;
+  if (MODE == 0 || (MODE == 1 && TD == 1 && K.mdbc)) {
+    if (TD == 1) a.delta *= Q.kd;
+    else if (TD == 2 || TD == 3) a.delta *= -Q.kd;
   }
-  if (FT && TDENSITY && a.dstop) a.delta = FLT_MAX;
+  if (FT && TD && a.dstop) a.delta = FLT_MAX;
   return a;
 }
 
@@ -418,10 +424,11 @@ __device__ __forceinline__ void drain_words(const KConst& K, const P1& p, unsign
       const float drx2 = p.x - A2.x, dry2 = p.y - A2.y, drz2 = p.z - A2.z;
       const float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
       const float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
-      const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
-      const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
+      // a missing second pair (j2 = j1) is moved beyond the support radius: factor 0
+      const float rr22m = two ? rr22 : 1e30f;
+      const bool ok1 = rr21 <= K.kernelsize2, ok2 = rr22m <= K.kernelsize2;
       pair_body<TDENSITY, MODE, FT>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, Q, a);
-      pair_body<TDENSITY, MODE, FT>(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, Q, a);
+      pair_body<TDENSITY, MODE, FT>(K, p, drx2, dry2, drz2, rr22m, ok2, B2, C2, Q, a);
     }
   }
 }
@@ -664,6 +671,7 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
                                                     const unsigned* __restrict__ bc, DivGrid g, KConst K,
                                                     float4* __restrict__ arace, FtRec ft) {
   constexpr int tcap = TcapT<FT>::v;
+  constexpr int TD = TDENSITY & 7;
   __shared__ float4 sA[tcap + SPH_PAD];  // over-read pad of the 8-wide candidate test (<= 7 records)
   __shared__ float4 sB[tcap];
   __shared__ typename CRecT<FT>::type sC[tcap];  // press/rho, 1/rho (FT: mass-scaled + kind)
@@ -757,20 +765,20 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
           // Combine exactly as the two CPU passes store (JSphCpu.cpp:800-818).
           float ar = 0.f, ax = 0.f, ay = 0.f, az = 0.f, delta = 0.f;
           if (f.ar != 0.f || f.ax != 0.f || f.ay != 0.f || f.az != 0.f || f.visc != 0.f) {
-            if (TDENSITY) delta = (f.delta == FLT_MAX ? FLT_MAX : 0.f + f.delta);
+            if (TD) delta = (f.delta == FLT_MAX ? FLT_MAX : 0.f + f.delta);
             ar = f.ar;
             ax = f.ax;
             ay = f.ay;
             az = f.az;
           }
           if (bnd.ar != 0.f || bnd.ax != 0.f || bnd.ay != 0.f || bnd.az != 0.f || bnd.visc != 0.f) {
-            if (TDENSITY) delta = (delta == FLT_MAX || bnd.delta == FLT_MAX ? FLT_MAX : delta + bnd.delta);
+            if (TD) delta = (delta == FLT_MAX || bnd.delta == FLT_MAX ? FLT_MAX : delta + bnd.delta);
             ar += bnd.ar;
             ax += bnd.ax;
             ay += bnd.ay;
             az += bnd.az;
           }
-          if (TDENSITY && delta != FLT_MAX) ar += delta;
+          if (TD && delta != FLT_MAX) ar += delta;
           if (K.sim2d) ay = 0.f;  // Simulate2D: Acec[].y = 0 (JSphCpuSingle.cpp:544-549)
           arace[p1] = make_float4(ax, ay, az, ar);
           viscmax = fmaxf(viscmax, fmaxf(f.visc, bnd.visc));
@@ -800,19 +808,25 @@ static void launch_fluid_tiled_s(hipStream_t stm, unsigned nblocks, DevScalars* 
 #define SPH_TILED(TD, FTB)                                                                                    \
   hipLaunchKernelGGL((k_fluid_tiled<TD, FTB, S>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell,   \
                      velrhop, press, begincell, g, K, arace, ft)
+  // DDT 2/3 with the binomial series of the hydrostatic term (K.ddtseries) as TDENSITY | 8
+  const int td = (K.tdensity >= 2 && K.ddtseries) ? K.tdensity | 8 : K.tdensity;
   if (ft.massp) {
-    switch (K.tdensity) {
+    switch (td) {
       case 0: SPH_TILED(0, true); break;
       case 1: SPH_TILED(1, true); break;
       case 2: SPH_TILED(2, true); break;
-      default: SPH_TILED(3, true); break;
+      case 3: SPH_TILED(3, true); break;
+      case 10: SPH_TILED(10, true); break;
+      default: SPH_TILED(11, true); break;
     }
   } else {
-    switch (K.tdensity) {
+    switch (td) {
       case 0: SPH_TILED(0, false); break;
       case 1: SPH_TILED(1, false); break;
       case 2: SPH_TILED(2, false); break;
-      default: SPH_TILED(3, false); break;
+      case 3: SPH_TILED(3, false); break;
+      case 10: SPH_TILED(10, false); break;
+      default: SPH_TILED(11, false); break;
     }
   }
 #undef SPH_TILED
