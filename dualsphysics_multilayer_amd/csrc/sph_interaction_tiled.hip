@@ -222,9 +222,11 @@ struct PassK {
 //     (p1+p2)/(rho1*rho2) = (p1/rho1)/rho2 + (p2/rho2)/rho1 and
 //     pi_visc = cvisc*(dr.dv)/(r^2+eta^2)/robar; one reciprocal 1/((r^2+eta^2)*(rho1+rho2))
 //     gives both 1/(r^2+eta^2) and 1/(rho1+rho2)
-//   DDT2: rho0*(1+x)^(1/gamma) - rho0, x = ddtgz*drz, as the binomial series in drz
-//         (|x| <= 2h*ddtgz ~ 1e-3, 5th term < 1e-9 relative; decided per case on the host),
-//         which also avoids the float cancellation of the reference's rho0*powf(rh,1/gamma)-rho0.
+//   DDT2: rho0*(1+x)^(1/gamma) - rho0, x = ddtgz*drz, as the binomial series in drz up to
+//         x^3 (|x| <= 2h*ddtgz < 0.02, decided per case on the host: the x^4 term is < 2e-6
+//         of the first, < 1e-8 at the dam break's 1e-3), evaluated by Horner with rho1 as the
+//         constant term; this also avoids the float cancellation of the reference's
+//         rho0*powf(rh,1/gamma)-rho0.
 template <int TDENSITY, int MODE, bool FT = false, typename CR = float2>
 __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float drx, float dry, float drz, float rr2,
                                           bool ok, const float4& B, const CR& C, const PassK& Q, TAcc& a) {
@@ -274,14 +276,14 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
     a.delta = fmaf(t, (p.vr.w - B.w) * C.y, a.delta);
     if (FT && ok && crec_kind(C) == 2.f) a.dstop = true;  // light floating p2
   } else if (TD == 2 || TD == 3) {
-    float drhop;
-    if (TDENSITY & 8)  // K.ddtseries, a template flag (no per-pair branch)
-      drhop = drz * fmaf(drz, fmaf(drz, fmaf(drz, K.ddte4, K.ddte3), K.ddte2), K.ddte1);
+    float rho1h;  // rho1 + drhop
+    if (TDENSITY & 8)  // K.ddtseries (a template flag: no per-pair branch), Horner with rho1
+      rho1h = fmaf(drz, fmaf(drz, fmaf(drz, K.ddte3, K.ddte2), K.ddte1), p.vr.w);
     else
-      drhop = K.rhopzero * fexp2(K.ovgamma * flog2(1.f + K.ddtgz * drz)) - K.rhopzero;
+      rho1h = p.vr.w + (K.rhopzero * fexp2(K.ovgamma * flog2(1.f + K.ddtgz * drz)) - K.rhopzero);
     float t = wc * rr2 * inv_re;
     if (FT && crec_kind(C) != 0.f) t = 0.f;  // no Fourtakas term with a floating p2 (JSphCpu.cpp:743)
-    a.delta = fmaf(t, B.w - (p.vr.w + drhop), a.delta);
+    a.delta = fmaf(t, B.w - rho1h, a.delta);
   }
 }
 
