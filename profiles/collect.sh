@@ -18,6 +18,8 @@ DST=$R/profiles/$TAG
 export TMPDIR=/tmp
 mkdir -p "$OUT" "$DST"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 "$R/bench.py" $ARGS --no-cpu-baseline > "$OUT/kt.log" 2>&1
+# provisional bench.json (workload, np) so step 4's bench finds this round's traffic
+grep '^{' "$OUT/kt.log" | tail -1 > "$DST/bench.json"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run -- python3 "$R/bench.py" $ARGS --no-cpu-baseline > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run -- python3 "$R/bench.py" $ARGS --no-cpu-baseline > "$OUT/write.log" 2>&1
 python3 "$R/profiles/summarize.py" "$OUT" "$DST"
