@@ -65,6 +65,7 @@ EXPORTED_SYMBOLS = (
     "sph_slab_partition",
     "sph_comm_unique_id",
     "sph_slab_create",
+    "sph_slab_create_shm",
     "sph_slab_group_create",
     "sph_slab_group_destroy",
     "sph_slab_group_run",
@@ -129,6 +130,8 @@ def load_library(path: str = LIB_PATH):
     L.sph_slab_partition.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.c_double, C.POINTER(C.c_int32)]
     L.sph_comm_unique_id.argtypes = [C.POINTER(C.c_ubyte)]
     L.sph_slab_create.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.POINTER(SphSlabDef), C.POINTER(vp)]
+    L.sph_slab_create_shm.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int,
+                                      C.POINTER(SphSlabDef), C.c_char_p, C.c_uint64, C.POINTER(vp)]
     L.sph_slab_group_create.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.POINTER(C.c_int32),
                                         C.POINTER(C.c_int32), C.POINTER(vp)]
     L.sph_slab_group_destroy.argtypes = [vp]
@@ -357,15 +360,26 @@ class SphGpuSlab(SphGpuSingle):
     (slab_partition) and `comm_id` the id rank 0 created.  Run/phase calls are
     collective.  stats()["np"] and particles() cover the owned particles only."""
 
-    def __init__(self, case, rank: int, nranks: int, bounds, comm_id: bytes, device: int = 0):
+    def __init__(self, case, rank: int, nranks: int, bounds, comm_id, device: int = 0, transport: str = "rccl",
+                 slot_bytes: int = 16 << 20):
+        """transport "rccl": comm_id = comm_unique_id() of rank 0 (one process per GPU);
+        "shm": comm_id = the shared-memory segment name ("/...", same on every rank; ranks of
+        one node without RCCL, e.g. several on one GPU), slot_bytes per mailbox."""
         L = load_library()
         self.case = case
         self._cdef = SphCaseDef.from_dict(case.case_def())
         init = case_particles(case)
         sd = SphSlabDef(rank, nranks, int(bounds[rank]), int(bounds[rank + 1]))
-        C.memmove(sd.comm_id, comm_id, 128)
         h = C.c_void_p()
-        _check(L.sph_slab_create(C.byref(self._cdef), C.byref(init.view), device, C.byref(sd), C.byref(h)))
+        if transport == "shm":
+            _check(L.sph_slab_create_shm(C.byref(self._cdef), C.byref(init.view), device, C.byref(sd),
+                                         comm_id.encode() if isinstance(comm_id, str) else comm_id, slot_bytes,
+                                         C.byref(h)))
+        elif transport == "rccl":
+            C.memmove(sd.comm_id, comm_id, 128)
+            _check(L.sph_slab_create(C.byref(self._cdef), C.byref(init.view), device, C.byref(sd), C.byref(h)))
+        else:
+            raise ValueError("transport must be 'rccl' or 'shm'")
         self._h = h
         self._time_set = None
         self.bounds = np.asarray(bounds)

@@ -214,6 +214,23 @@ int sph_slab_create(const SphCaseDef* cdef, const SphParticlesHost* all, int dev
   });
 }
 
+int sph_slab_create_shm(const SphCaseDef* cdef, const SphParticlesHost* all, int device, const SphSlabDef* slab,
+                        const char* shm_name, uint64_t slot_bytes, SphSolver** out) {
+  NEED(cdef && all && slab && out && shm_name && slot_bytes);
+  NEED(all->idp && all->pos && all->vel && all->rhop);
+  return guard([&] {
+    sphx::check_hip(hipSetDevice(device), "hipSetDevice");
+    sphx::SlabConfig sc;
+    sc.rank = slab->rank;
+    sc.nranks = slab->nranks;
+    sc.c0 = slab->cx_begin;
+    sc.c1 = slab->cx_end;
+    auto tr = sphx::make_shm_transport(shm_name, slab->rank, slab->nranks, slot_bytes);
+    auto* impl = new sphx::SphGpuSingle(*cdef, *all, device, sc, std::move(tr));
+    *out = new SphSolver{impl, false};
+  });
+}
+
 int sph_slab_group_create(const SphCaseDef* cdef, const SphParticlesHost* all, int nslabs, const int32_t* devices,
                           const int32_t* cx_bounds, SphSlabGroup** out) {
   NEED(cdef && all && devices && cx_bounds && out && nslabs >= 1);

@@ -1,10 +1,19 @@
 // sph_comm.cpp — RCCL and in-process transports of the slab decomposition.
 #include "sph_comm.hpp"
 
+#include <fcntl.h>
 #include <rccl/rccl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 
 #include "sph_solver.hpp"
 
@@ -178,6 +187,178 @@ class LocalTransport final : public SlabTransport {
 
 std::unique_ptr<SlabTransport> make_local_transport(std::shared_ptr<LocalHub> hub, int rank) {
   return std::unique_ptr<SlabTransport>(new LocalTransport(std::move(hub), rank));
+}
+
+// ---------------------------------------------------------------------------------
+// Host-staged transport over a POSIX shared-memory segment: ranks of one node (separate
+// processes, any devices, several ranks on one GPU included) without RCCL.  Layout: a
+// 4 KiB head (generation counters, message sizes, abort flag) and per rank two mailboxes
+// of `slot` bytes (data for the left / right neighbour; the left one also carries the
+// values of a reduction).  Every call is synchronous: device -> mailbox, barrier, the
+// neighbours' mailboxes -> device, barrier (nobody refills a mailbox before it was read).
+// A barrier that waits past the deadline or sees the abort flag raises SPH_ERR_COMM
+// after setting the flag, so every rank ends instead of hanging.
+namespace {
+constexpr int SHM_MAXRANKS = 64;
+constexpr uint64_t SHM_MAGIC = 0x53504853484d3031ull;  // "SPHSHM01"
+struct ShmHead {
+  std::atomic<uint64_t> magic;
+  int32_t nranks, pad;
+  uint64_t slot;
+  std::atomic<uint64_t> abort;
+  std::atomic<uint64_t> arrive[SHM_MAXRANKS];
+  uint64_t nsl[SHM_MAXRANKS], nsr[SHM_MAXRANKS];
+};
+static_assert(sizeof(ShmHead) <= 4096, "shm head");
+static_assert(std::atomic<uint64_t>::is_always_lock_free, "lock-free atomics in shared memory");
+}  // namespace
+
+class ShmTransport final : public SlabTransport {
+ public:
+  ShmTransport(const std::string& name, int r, int n, uint64_t slot) : name_(name) {
+    rank = r;
+    nranks = n;
+    if (n < 1 || n > SHM_MAXRANKS || r < 0 || r >= n) throw SphError(SPH_ERR_ARG, "shm transport: invalid rank");
+    if (name.empty() || name[0] != '/') throw SphError(SPH_ERR_ARG, "shm transport: the name must start with '/'");
+    if (const char* e = std::getenv("SPH_COMM_TIMEOUT_S")) timeout_s_ = std::max(1.0, std::atof(e));
+    bytes_ = 4096 + uint64_t(n) * 2 * slot;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (r == 0) {
+      (void)shm_unlink(name.c_str());
+      const int fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+      if (fd < 0) throw SphError(SPH_ERR_COMM, "shm_open(create) " + name);
+      if (ftruncate(fd, off_t(bytes_)) != 0) {
+        ::close(fd);
+        throw SphError(SPH_ERR_NOMEM, "shm transport: ftruncate");
+      }
+      map(fd);
+      head_->nranks = n;
+      head_->slot = slot;
+      head_->abort.store(0);
+      for (int k = 0; k < SHM_MAXRANKS; k++) head_->arrive[k].store(0);
+      head_->magic.store(SHM_MAGIC);
+    } else {
+      for (;;) {  // wait for rank 0's segment
+        const int fd = shm_open(name.c_str(), O_RDWR, 0600);
+        if (fd >= 0) {
+          struct stat st;
+          if (fstat(fd, &st) == 0 && uint64_t(st.st_size) == bytes_) {
+            map(fd);
+            if (head_->magic.load() == SHM_MAGIC) break;
+            unmap();
+          } else {
+            ::close(fd);
+          }
+        }
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s_)
+          throw SphError(SPH_ERR_COMM, "shm transport: rank 0's segment " + name + " did not appear");
+        std::this_thread::sleep_for(std::chrono::milliseconds(2));
+      }
+      if (head_->nranks != n || head_->slot != slot) throw SphError(SPH_ERR_ARG, "shm transport: layout mismatch");
+    }
+    slot_ = slot;
+  }
+  ~ShmTransport() override {
+    unmap();
+    if (rank == 0) (void)shm_unlink(name_.c_str());
+  }
+  void check_async() override {
+    if (head_->abort.load()) throw SphError(SPH_ERR_COMM, "shm transport aborted by another rank");
+  }
+  void abort() override { head_->abort.store(1); }
+  void exchange(const void* sl, size_t nsl, const void* sr, size_t nsr, void* rl, size_t nrl, void* rr, size_t nrr,
+                hipStream_t s) override {
+    if (nsl > slot_ || nsr > slot_ || nrl > slot_ || nrr > slot_)
+      throw SphError(SPH_ERR_NOMEM, "shm transport: message larger than the mailbox");
+    check_hip(hipStreamSynchronize(s), "exchange: send buffers");
+    if (has_left() && nsl) check_hip(hipMemcpy(box(rank, 0), sl, nsl, hipMemcpyDeviceToHost), "exchange: to mailbox");
+    if (has_right() && nsr) check_hip(hipMemcpy(box(rank, 1), sr, nsr, hipMemcpyDeviceToHost), "exchange: to mailbox");
+    head_->nsl[rank] = has_left() ? nsl : 0;
+    head_->nsr[rank] = has_right() ? nsr : 0;
+    barrier();
+    if (has_left() && nrl) {
+      if (head_->nsr[rank - 1] != nrl) throw SphError(SPH_ERR_COMM, "exchange: size mismatch with the left rank");
+      check_hip(hipMemcpy(rl, box(rank - 1, 1), nrl, hipMemcpyHostToDevice), "exchange: from left");
+    }
+    if (has_right() && nrr) {
+      if (head_->nsl[rank + 1] != nrr) throw SphError(SPH_ERR_COMM, "exchange: size mismatch with the right rank");
+      check_hip(hipMemcpy(rr, box(rank + 1, 0), nrr, hipMemcpyHostToDevice), "exchange: from right");
+    }
+    barrier();
+  }
+  void allreduce_max_u32(unsigned* d, int n, hipStream_t s) override {
+    std::vector<unsigned> v(size_t(n), 0u);
+    reduce_in(d, 4 * size_t(n), s);
+    for (int r = 0; r < nranks; r++) {
+      const unsigned* x = (const unsigned*)box(r, 0);
+      for (int i = 0; i < n; i++) v[size_t(i)] = std::max(v[size_t(i)], x[i]);
+    }
+    reduce_out(d, v.data(), 4 * size_t(n), s);
+  }
+  // Summed in rank order from 0.f, as LocalTransport and launch_rank_ordered_sum do.
+  void allreduce_sum_f32(float* d, int n, hipStream_t s) override {
+    std::vector<float> v(size_t(n), 0.f);
+    reduce_in(d, 4 * size_t(n), s);
+    for (int r = 0; r < nranks; r++) {
+      const float* x = (const float*)box(r, 0);
+      for (int i = 0; i < n; i++) v[size_t(i)] += x[i];
+    }
+    reduce_out(d, v.data(), 4 * size_t(n), s);
+  }
+
+ private:
+  void map(int fd) {
+    void* p = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    ::close(fd);
+    if (p == MAP_FAILED) throw SphError(SPH_ERR_COMM, "shm transport: mmap");
+    base_ = (char*)p;
+    head_ = (ShmHead*)p;
+  }
+  void unmap() {
+    if (base_) munmap(base_, bytes_);
+    base_ = nullptr;
+    head_ = nullptr;
+  }
+  char* box(int r, int side) { return base_ + 4096 + (uint64_t(r) * 2 + uint64_t(side)) * slot_; }
+  void barrier() {
+    const uint64_t g = ++gen_;
+    head_->arrive[rank].store(g);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 0;; spin++) {
+      bool all = true;
+      for (int r = 0; r < nranks && all; r++) all = head_->arrive[r].load() >= g;
+      if (all) return;
+      if (head_->abort.load()) throw SphError(SPH_ERR_COMM, "shm transport aborted by another rank");
+      if ((spin & 255u) == 255u) {
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s_) {
+          abort();
+          throw SphError(SPH_ERR_COMM, "shm transport: a rank is gone or stalled (no progress for " +
+                                           std::to_string(int(timeout_s_)) + " s)");
+        }
+        std::this_thread::yield();
+      }
+    }
+  }
+  void reduce_in(const void* d, size_t bytes, hipStream_t s) {
+    if (bytes > slot_) throw SphError(SPH_ERR_NOMEM, "shm transport: reduction larger than the mailbox");
+    check_hip(hipStreamSynchronize(s), "allreduce: values");
+    check_hip(hipMemcpy(box(rank, 0), d, bytes, hipMemcpyDeviceToHost), "allreduce: read");
+    barrier();
+  }
+  void reduce_out(void* d, const void* v, size_t bytes, hipStream_t s) {
+    barrier();  // every rank has read every mailbox
+    check_hip(hipMemcpyAsync(d, v, bytes, hipMemcpyHostToDevice, s), "allreduce: write");
+    check_hip(hipStreamSynchronize(s), "allreduce: write");
+  }
+  std::string name_;
+  char* base_ = nullptr;
+  ShmHead* head_ = nullptr;
+  uint64_t bytes_ = 0, slot_ = 0, gen_ = 0;
+  double timeout_s_ = 120.0;
+};
+
+std::unique_ptr<SlabTransport> make_shm_transport(const char* name, int rank, int nranks, uint64_t slot_bytes) {
+  return std::unique_ptr<SlabTransport>(new ShmTransport(name ? name : "", rank, nranks, slot_bytes));
 }
 
 }  // namespace sphx

@@ -1,9 +1,11 @@
 // sph_comm.hpp — transports of the slab decomposition.
 //
 // A slab talks only to its two x-neighbours (rank-1, rank+1) plus one 4-value
-// max-allreduce per dt.  Two implementations behind one interface:
+// max-allreduce per dt.  Three implementations behind one interface:
 //   * RcclTransport: one process per GPU, RCCL (ncclSend/ncclRecv in a group, point to
 //     point over xGMI; ncclAllReduce max) on the solver's stream — the product path;
+//   * ShmTransport: separate processes of one node through a shared-memory segment,
+//     host-staged (the multi-process path where RCCL cannot run, e.g. 2 ranks on 1 GPU);
 //   * LocalTransport: several slabs driven by host threads of ONE process (any
 //     devices, including several slabs on one GPU), device-to-device copies through
 //     a shared hub.  Used by SphSlabGroup: it runs the exact same pack / divide /
@@ -77,5 +79,10 @@ class LocalHub {
 };
 
 std::unique_ptr<SlabTransport> make_local_transport(std::shared_ptr<LocalHub> hub, int rank);
+
+// Host-staged ranks of one node over POSIX shared memory `name` (separate processes, e.g.
+// several ranks on one GPU, where RCCL refuses duplicate devices): two mailboxes of
+// slot_bytes per rank; rank 0 creates the segment, the others attach.
+std::unique_ptr<SlabTransport> make_shm_transport(const char* name, int rank, int nranks, uint64_t slot_bytes);
 
 }  // namespace sphx

@@ -314,6 +314,13 @@ int sph_comm_unique_id(unsigned char id[128]);
  * and keeps its owned + ghost columns. */
 int sph_slab_create(const SphCaseDef* cdef, const SphParticlesHost* all, int device, const SphSlabDef* slab,
                     SphSolver** out);
+/* The same slab with a host-staged transport over the POSIX shared-memory segment
+ * `shm_name` ("/..."; two mailboxes of slot_bytes per rank; comm_id unused): separate
+ * processes of ONE node without RCCL, e.g. several ranks on one GPU, where RCCL refuses
+ * duplicate devices.  Rank 0 creates the segment, the others attach.  Same collective
+ * calls and failure semantics (deadline SPH_COMM_TIMEOUT_S, abort flag -> SPH_ERR_COMM). */
+int sph_slab_create_shm(const SphCaseDef* cdef, const SphParticlesHost* all, int device, const SphSlabDef* slab,
+                        const char* shm_name, uint64_t slot_bytes, SphSolver** out);
 
 /* Several slabs in ONE process (host threads, device-to-device copies; devices may
  * repeat).  The member handles are borrowed (no destroy); members accept the data-out

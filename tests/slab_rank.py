@@ -1,0 +1,60 @@
+"""One rank of a multi-process slab run on the shared-memory transport (launched by
+tests/test_gpu_slab_mp.py; every rank a separate process, all on cuda:0).
+
+    python tests/slab_rank.py <rank> <nranks> <shm name> <golden> <out.npz> [skew|balanced]
+                              [repartition K] [die-after-create]
+
+Runs the golden's dam break to each of its kept steps (SphGpuSlab, collective calls in
+the same order on every rank) and saves this rank's OWNED particles at every kept step."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+
+import numpy as np  # noqa: E402
+
+from golden_io import load, meta, steps  # noqa: E402
+
+from dualsphysics_multilayer_amd.case import DamBreakCase  # noqa: E402
+from dualsphysics_multilayer_amd.core import SphError, SphGpuSlab, case_derive, slab_partition  # noqa: E402
+
+
+def main(argv):
+    rank, nranks, name, golden, out = int(argv[0]), int(argv[1]), argv[2], argv[3], argv[4]
+    layout = argv[5] if len(argv) > 5 else "balanced"
+    every = int(argv[6]) if len(argv) > 6 else 0
+    die = len(argv) > 7 and argv[7] == "die-after-create"
+    g = load(golden)
+    dp, step_alg, ddt, _ = meta(g)
+    case = DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt)
+    if layout == "skew":  # rank 0 holds all but the last 2 columns per other rank
+        ncx = case_derive(case.case_def())["dom_cells"][0]
+        bounds = [0] + [ncx - 2 * (nranks - r) for r in range(1, nranks)] + [ncx]
+    else:
+        bounds = list(slab_partition(case, nranks))
+    s = SphGpuSlab(case, rank, nranks, bounds, name, device=0, transport="shm", slot_bytes=8 << 20)
+    if every:
+        s.set_repartition(every, 0.3, 0.0)
+    if die:
+        os._exit(0)  # a rank that disappears: the others must end with SPH_ERR_COMM
+    res, done = {}, 0
+    try:
+        for k in steps(g):
+            s.run(k - done)
+            done = k
+            p = s.particles()
+            for q in ("idp", "pos", "vel", "rhop"):
+                res["s%d_%s" % (k, q)] = p[q]
+            res["s%d_time" % k] = np.float64(s.stats()["time"])
+        info = s.slab_info()
+        res["info"] = np.array([info["cx_begin"], info["cx_end"], info["repartitions"]], np.int64)
+    except SphError as e:
+        res["error"] = np.array(str(e))
+    np.savez(out, **res)
+    return 0 if "error" not in res else 3
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))
