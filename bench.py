@@ -207,6 +207,11 @@ def main() -> None:
                     help="reference CPU steps timed (window 10 .. 10+K, BASELINE.md: 10-110)")
     ap.add_argument("--repartition", type=int, default=20,
                     help="N>1: re-balance the slab bounds every K steps when the load is >5%% off (0: never)")
+    ap.add_argument("--transport", choices=("rccl", "shm"), default="rccl",
+                    help="N>1 slab transport: rccl (one process per GPU, the product path) or shm "
+                         "(host-staged shared memory: ranks of one node without RCCL)")
+    ap.add_argument("--ranks-per-gpu", type=int, default=1,
+                    help="ranks sharing one GPU (device = LOCAL_RANK // this; needs --transport shm)")
     ap.add_argument("--force-slab", action="store_true",
                     help="run the N>1 code path (gloo bootstrap + RCCL slab) even with one rank")
     args = ap.parse_args()
@@ -216,6 +221,9 @@ def main() -> None:
     rank, world, local = dist_env()
     if args.gpus != world and world > 1:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.ranks_per_gpu > 1 and args.transport == "rccl":
+        raise SystemExit("--ranks-per-gpu > 1 needs --transport shm (RCCL refuses two ranks on one device)")
+    device = local // max(1, args.ranks_per_gpu)
     use_slab = world > 1 or args.force_slab
     dist = None
     if use_slab:
@@ -256,9 +264,15 @@ def main() -> None:
         err = None
         try:
             bounds = slab_partition(case, world, args.bound_weight)
-            ids = [comm_unique_id() if rank == 0 else None]
+            if args.transport == "shm":
+                import uuid
+
+                ids = ["/sphbench_%s" % uuid.uuid4().hex[:12] if rank == 0 else None]
+            else:
+                ids = [comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(ids, src=0)
-            s = SphGpuSlab(case, rank, world, bounds, ids[0], device=local)
+            s = SphGpuSlab(case, rank, world, bounds, ids[0], device=device, transport=args.transport,
+                           slot_bytes=256 << 20)
             if args.repartition and world > 1:
                 s.set_repartition(args.repartition, args.bound_weight, 0.05)
             s.run(args.warmup)
@@ -272,7 +286,7 @@ def main() -> None:
             sys.stderr.write("rank %d: slab run failed: %r\n" % (rank, err if err else "failed on another rank"))
             raise SystemExit(3)
     else:
-        s = SphGpuSingle(case, device=local)
+        s = SphGpuSingle(case, device=device)
         s.run(args.warmup)
         s.sync()
     wall["setup_and_warmup_s"] = time.perf_counter() - t_setup
@@ -283,7 +297,7 @@ def main() -> None:
             import torch
 
             dist.barrier()
-            torch.cuda.synchronize(local)
+            torch.cuda.synchronize(device)
 
     s.set_timing(True)
     s.sync()
@@ -366,8 +380,10 @@ def main() -> None:
                               "Full (-10, TFS 2.75), CFL 0.1, RelaxationDt 0.2" % (case.np, dp, CFG5_WIDTH))),
                 "np": case.np,
                 "npb": case.npb,
-                "parallelism": (("slab-x%d (RCCL halo + migration, max-allreduce dt)" % world) if bounds is not None
-                                else "single"),
+                "parallelism": (("slab-x%d (%s halo + migration, max-allreduce dt%s)"
+                                 % (world, "RCCL" if args.transport == "rccl" else "shared-memory",
+                                    "" if args.ranks_per_gpu == 1 else ", %d ranks per GPU" % args.ranks_per_gpu))
+                                if bounds is not None else "single"),
                 "slab_bounds_cells": None if bounds is None else [int(b) for b in bounds],
                 "slab_repartition_every": args.repartition if bounds is not None and world > 1 else None,
                 "slab_final_info": slab_info,
