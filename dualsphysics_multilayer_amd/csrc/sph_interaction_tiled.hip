@@ -133,11 +133,12 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
   if (!WRITE) counts[r] = nitems;
 }
 
-// Exclusive scan of the per-row item counts (one block) -> item offsets, total.
-// (the per-XCD work counters are reset by a memset right before each launch)
+// Exclusive scan of the per-row item counts (one block) -> item offsets, total; zeroes
+// the per-XCD work queues of the next interaction.
 __global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ counts, unsigned nrows2,
-                                                     DevScalars* __restrict__ sc) {
+                                                     DevScalars* __restrict__ sc, unsigned* __restrict__ qctr) {
   __shared__ unsigned part[1024];
+  if (threadIdx.x < 8) qctr[threadIdx.x * QSTRIDE] = 0u;  // the interaction's item queues start over
   const unsigned per = (nrows2 + 1023) / 1024;
   const unsigned b0 = threadIdx.x * per, b1 = min(b0 + per, nrows2);
   unsigned s = 0;
@@ -161,11 +162,10 @@ __global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ coun
 
 void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
                   uint4* items, unsigned* qctr, int scelldiv) {
-  (void)qctr;
   const int tmaxc = scelldiv == 1 ? TMAXCELLS : TMAXCELLS_HALF;
   const unsigned nrows2 = 2u * unsigned(g.ncy) * unsigned(g.ncz);
   hipLaunchKernelGGL(k_items_rows<false>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, nullptr);
-  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, rowtmp, nrows2, sc);
+  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, rowtmp, nrows2, sc, qctr);
   hipLaunchKernelGGL(k_items_rows<true>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, items);
 }
 
@@ -330,7 +330,7 @@ __device__ __forceinline__ void tile_unit(const KConst& K, const P1& p, float th
                                           const float4* __restrict__ sA, const float4* __restrict__ sB,
                                           const typename CRecT<FT>::type* __restrict__ sC, const PassK& Q, TAcc& a) {
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
-#if SPH_ABLATE == 2
+#if SPH_ABLATE == 2 || SPH_ABLATE == 3
   a.visc += float(wa1 - wa0 + wb1 - wb0);
   return;
 #endif
@@ -464,6 +464,9 @@ __device__ __forceinline__ void stage_row(const KConst& K, unsigned rs, unsigned
                                           const float4* __restrict__ velrhop, const float* __restrict__ press,
                                           float4* __restrict__ sA, float4* __restrict__ sB, CR* __restrict__ sC,
                                           const FtRec& ft) {
+#if SPH_ABLATE == 3
+  return;  // diagnostic: no staging loads
+#endif
   const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
   for (unsigned i = threadIdx.x; i < re - rs; i += TB) {
     const float4 pc = poscell[rs + i];
@@ -502,6 +505,9 @@ __device__ __forceinline__ TAcc run_pass(const KConst& K, const DivGrid& g, cons
   TAcc acc = {};
   acc.dstop = dstop0;
   const unsigned cellinit = (MODE == 1 ? 0u : g.boxfluid);
+#if SPH_ABLATE == 4
+  return acc;  // diagnostic: items, lane order, p1 loads and stores only
+#endif
   for (int u = 0; u < 5; u++) {
     const int dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
     const int dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
@@ -691,7 +697,12 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
     const unsigned xg = (grp + q) & 7;
     const unsigned lo = xg * per, hi = min(nitems, lo + per);
     for (;;) {
-      if (threadIdx.x == 0) s_item = lo + atomicAdd(&qctr[xg], 1u);
+      // a group known to be exhausted (counters only grow; a stale read is smaller) costs
+      // no atomic: probing all 8 queues was ~16k same-line atomics per launch
+      if (threadIdx.x == 0)
+        s_item = (lo + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= hi)
+                     ? hi
+                     : lo + atomicAdd(&qctr[xg * QSTRIDE], 1u);
       __syncthreads();
       const unsigned it = s_item;
       __syncthreads();
@@ -791,15 +802,8 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
   }
   wave_max_atomic(sc, RED_VISCDT, viscmax);
   wave_max_atomic(sc, RED_ACEMAX2, ace2max);
-  // The last block out resets the work counters for the next launch (qctr[8] counts
-  // finished blocks), so no memset launch is needed before each interaction.
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(&qctr[8], 1u) == gridDim.x - 1) {
-      for (int i = 0; i < 9; i++) atomicExch(&qctr[i], 0u);
-    }
-  }
+  // (the queue counters are zeroed by k_items_scan, or by the solver before an interaction
+  // without a new item list)
 }
 
 template <int S>

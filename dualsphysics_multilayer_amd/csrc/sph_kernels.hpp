@@ -119,6 +119,10 @@ void launch_interaction(hipStream_t stm, unsigned cap, DevScalars* sc, const flo
 void launch_interaction_bound(hipStream_t stm, unsigned npbcap, DevScalars* sc, const float4* poscell,
                               const float4* velrhop, const unsigned* begincell, DivGrid g, const KConst& K,
                               float4* arace);
+// Work counters of the persistent tiled kernels (qctr): 8 per-XCD item queues + the
+// finished-block count, each on its own 128-B line (device-scope atomics serialize per line).
+constexpr int QSTRIDE = 32;
+constexpr size_t QCTR_BYTES = 9 * QSTRIDE * sizeof(unsigned);
 // Tiled fluid interaction (sph_interaction_tiled.hip) and its per-divide item list.
 // scelldiv 1 (CellMode=full): items of <= 4 cells; 2 (half): <= TMAXCELLS_HALF half-cells.
 void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,

@@ -408,8 +408,8 @@ void SphGpuSingle::AllocFixed() {
     colcnt_ = (float*)dmalloc(4 * (2 * size_t(C.dom_cells[0]) + size_t(slabcfg_.nranks) + 1));
   }
   rowtmp_ = (unsigned*)dmalloc(4 * 2 * size_t(G.ncy) * size_t(G.ncz));
-  qctr_ = (unsigned*)dmalloc(4 * 16);
-  check_hip(hipMemset(qctr_, 0, 4 * 16), "zero work counters");
+  qctr_ = (unsigned*)dmalloc(QCTR_BYTES);
+  check_hip(hipMemset(qctr_, 0, QCTR_BYTES), "zero work counters");
   sort_.digtot = (unsigned*)dmalloc(4 * (1u << RS_MAXBITS));
   sc_ = (DevScalars*)dmalloc(sizeof(DevScalars));
   dttrace_ = (double*)dmalloc(8 * size_t(tracecap_));
@@ -857,7 +857,10 @@ void SphGpuSingle::RunCellDivide() {
   launch_gather(stream, cap_, sc_, sort_.vals[res], cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_,
                 G.xoff, nn_ ? phaseeos_ : nullptr);
   std::swap(cur_, alt_);
-  if (tiled_) launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv);
+  if (tiled_) {
+    launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv);  // also zeroes the queues
+    qfresh_ = true;
+  }
   if (nftp_) launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_, K, G);
   TimedEnd(2);
 }
@@ -880,6 +883,9 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
     }
     TimedEnd(3);
   }
+  if (tiled_ && !qfresh_)  // a second interaction on the same item list: queues start over
+    check_hip(hipMemsetAsync(qctr_, 0, QCTR_BYTES, stream), "zero work counters");
+  qfresh_ = false;
   if (nn_) {
     // NN multiphase (sph_nn.hip); the shifting sums only where they are applied: the
     // corrector (the predictor's RunShifting result is never used, shift=false in

@@ -143,6 +143,7 @@ class SphGpuSingle {
   unsigned* rowtmp_ = nullptr;    // per-row item counts/offsets
   unsigned* qctr_ = nullptr;      // per-XCD-group work counters
   unsigned nblocks_tiled_ = 2048;
+  bool qfresh_ = false;  // the tiled kernels' work queues were zeroed by the last item build
   bool tiled_ = true;             // SPH_INTERACTION=simple selects the one-lane-per-particle kernel
   SortScratch sort_;
   DevScalars* sc_ = nullptr;

@@ -10,7 +10,8 @@
 namespace sphx {
 
 #ifndef SPH_ABLATE
-#define SPH_ABLATE 0  // diagnostic builds: 1 = no pair body, 2 = no candidate test/body, 3 = no staging loads
+#define SPH_ABLATE 0  // diagnostic builds: 1 = no pair body, 2 = no candidate test/body, 3 = 2 + no staging
+                     // loads, 4 = no neighbour rows at all (item overhead only)
 #endif
 constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
 #ifndef SPH_TCAP
