@@ -20,7 +20,23 @@
 namespace sphx {
 
 // ---------------------------------------------------------------------------------
-// PreSort (KerPreSortFull) — one thread per particle, bounded by the live count.
+// Box key of one particle (KerPreSortFull, JCellDivGpuSingle_ker.cu:41-102).
+__device__ __forceinline__ unsigned box_key(unsigned rcell, typecode rcode, const DivGrid& g, unsigned dcc) {
+  if (rcell == DCELL_DISCARD) return g.boxdiscard;  // slab: stale ghost / particle handed to a neighbour
+  const unsigned cx = DcelCellx(dcc, rcell) - unsigned(g.xoff), cy = DcelCelly(dcc, rcell), cz = DcelCellz(dcc, rcell);
+  if (rcell != DCELL_OUT && (g.xown0 != 0 || g.xown1 != g.ncx) && cx >= unsigned(g.ncx))
+    return g.boxdiscard;  // slab: a migrant handed over beyond this slab's ghost columns (re-partition)
+  const unsigned cellsort = cx + cy * unsigned(g.ncx) + cz * g.nsheet;
+  const typecode codetype = CodeType(rcode), codeout = CodeSpecial(rcode);
+  if (codetype < CODE_TYPE_FLOATING)
+    return codeout < CODE_OUTIGNORE
+               ? ((cx < unsigned(g.ncx) && cy < unsigned(g.ncy) && cz < unsigned(g.ncz)) ? cellsort : g.boxboundignore)
+               : (codeout == CODE_OUTIGNORE ? g.boxboundoutignore : g.boxboundout);
+  return codeout <= CODE_OUTIGNORE ? (codeout < CODE_OUTIGNORE ? g.boxfluid + cellsort : g.boxfluidoutignore)
+                                   : (codetype == CODE_TYPE_FLOATING ? g.boxboundout : g.boxfluidout);
+}
+
+// PreSort — one thread per particle, bounded by the live count.
 __global__ __launch_bounds__(256) void k_presort(const DevScalars* __restrict__ sc, const unsigned* __restrict__ dcell,
                                                  const typecode* __restrict__ code, DivGrid g, unsigned dcc,
                                                  unsigned* __restrict__ keys, unsigned* __restrict__ vals) {
@@ -28,30 +44,8 @@ __global__ __launch_bounds__(256) void k_presort(const DevScalars* __restrict__ 
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p == 0) const_cast<DevScalars*>(sc)->ndiv = n;
   if (p >= n) return;
-  const unsigned rcell = dcell[p];
   vals[p] = p;
-  if (rcell == DCELL_DISCARD) {  // slab: stale ghost / particle handed to a neighbour
-    keys[p] = g.boxdiscard;
-    return;
-  }
-  const unsigned cx = DcelCellx(dcc, rcell) - unsigned(g.xoff), cy = DcelCelly(dcc, rcell), cz = DcelCellz(dcc, rcell);
-  if (rcell != DCELL_OUT && (g.xown0 != 0 || g.xown1 != g.ncx) && cx >= unsigned(g.ncx)) {
-    keys[p] = g.boxdiscard;  // slab: a migrant handed over beyond this slab's ghost columns (re-partition)
-    return;
-  }
-  const unsigned cellsort = cx + cy * unsigned(g.ncx) + cz * g.nsheet;
-  const typecode rcode = code[p];
-  const typecode codetype = CodeType(rcode), codeout = CodeSpecial(rcode);
-  unsigned box;
-  if (codetype < CODE_TYPE_FLOATING) {
-    box = (codeout < CODE_OUTIGNORE
-               ? ((cx < unsigned(g.ncx) && cy < unsigned(g.ncy) && cz < unsigned(g.ncz)) ? cellsort : g.boxboundignore)
-               : (codeout == CODE_OUTIGNORE ? g.boxboundoutignore : g.boxboundout));
-  } else {
-    box = (codeout <= CODE_OUTIGNORE ? (codeout < CODE_OUTIGNORE ? g.boxfluid + cellsort : g.boxfluidoutignore)
-                                     : (codetype == CODE_TYPE_FLOATING ? g.boxboundout : g.boxfluidout));
-  }
-  keys[p] = box;
+  keys[p] = box_key(dcell[p], code[p], g, dcc);
 }
 
 void launch_presort(hipStream_t stm, unsigned cap, const DevScalars* sc, const unsigned* dcell, const typecode* code,
@@ -326,35 +320,48 @@ struct GatherArgs {
 #endif
 constexpr int GP = SPH_GP;
 
-template <bool WITHM1, bool WITHPRE>
-__device__ __forceinline__ void gather_one(const GatherArgs& a, unsigned i, unsigned s, float4& vr_out, bool& fluid,
-                                           unsigned npb) {
-  const unsigned dc = a.src.dcell[s];
-  const double2 pxy = a.src.posxy[s];
-  const double pz = a.src.posz[s];
-  const float4 vr = a.src.velrhop[s];
-  const unsigned idp = a.src.idp[s];
-  const typecode code = a.src.code[s];
-  float4 m1, vpre;
-  double2 pxypre;
-  double pzpre;
-  if (WITHM1) m1 = a.src.velrhopm1[s];
-  if (WITHPRE) {
-    pxypre = a.src.posxypre[s];
-    pzpre = a.src.poszpre[s];
-    vpre = a.src.velrhoppre[s];
+// One particle's state, loaded from its source index (all loads issued before any store).
+template <bool WITHM1, bool WITHPRE> struct GatherRec {
+  unsigned dc, idp;
+  double2 pxy, pxypre;
+  double pz, pzpre;
+  float4 vr, m1, vpre;
+  typecode code;
+  __device__ __forceinline__ void load(const PartArrays& src, unsigned s) {
+    dc = src.dcell[s];
+    pxy = src.posxy[s];
+    pz = src.posz[s];
+    vr = src.velrhop[s];
+    idp = src.idp[s];
+    code = src.code[s];
+    if (WITHM1) m1 = src.velrhopm1[s];
+    if (WITHPRE) {
+      pxypre = src.posxypre[s];
+      pzpre = src.poszpre[s];
+      vpre = src.velrhoppre[s];
+    }
   }
-  a.dst.idp[i] = idp;
+};
+
+// Stores a loaded particle at its sorted index i with its poscell and press.
+template <bool WITHM1, bool WITHPRE>
+__device__ __forceinline__ void gather_store(const GatherArgs& a, unsigned i, const GatherRec<WITHM1, WITHPRE>& q) {
+  const unsigned dc = q.dc;
+  const double2 pxy = q.pxy;
+  const double pz = q.pz;
+  const float4 vr = q.vr;
+  const typecode code = q.code;
+  a.dst.idp[i] = q.idp;
   a.dst.code[i] = code;
   a.dst.dcell[i] = dc;
   a.dst.posxy[i] = pxy;
   a.dst.posz[i] = pz;
   a.dst.velrhop[i] = vr;
-  if (WITHM1) a.dst.velrhopm1[i] = m1;
+  if (WITHM1) a.dst.velrhopm1[i] = q.m1;
   if (WITHPRE) {
-    a.dst.posxypre[i] = pxypre;
-    a.dst.poszpre[i] = pzpre;
-    a.dst.velrhoppre[i] = vpre;
+    a.dst.posxypre[i] = q.pxypre;
+    a.dst.poszpre[i] = q.pzpre;
+    a.dst.velrhoppre[i] = q.vpre;
   }
   // PosCell (KerUpdatePosCell): position relative to the origin of its divide cell
   // (global cell -> the same floats on every slab); w = the local cell.
@@ -399,7 +406,16 @@ __device__ __forceinline__ void gather_one(const GatherArgs& a, unsigned i, unsi
     const double xr = double(vr.w * a.ovrhopzero);
     a.press[i] = float(double(a.cteb) * (powg(xr, a.igamma, double(a.gamma)) - 1.0));
   }
-  vr_out = vr;
+}
+
+
+template <bool WITHM1, bool WITHPRE>
+__device__ __forceinline__ void gather_one(const GatherArgs& a, unsigned i, unsigned s, float4& vr_out, bool& fluid,
+                                           unsigned npb) {
+  GatherRec<WITHM1, WITHPRE> q;
+  q.load(a.src, s);
+  gather_store<WITHM1, WITHPRE>(a, i, q);
+  vr_out = q.vr;
   fluid = i >= npb;
 }
 
@@ -453,5 +469,547 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
   else if (withpre) hipLaunchKernelGGL((k_gather<false, true>), dim3(nb), dim3(256), 0, stm, sc, a);
   else hipLaunchKernelGGL((k_gather<false, false>), dim3(nb), dim3(256), 0, stm, sc, a);
 }
+
+// ---------------------------------------------------------------------------------
+// Incremental divide (single domain, every divide after the first).
+//
+// Particles move less than one cell per step (UpdatePos excludes a particle that moves
+// more than MovLimit < Scell; it goes to an out box), so the previous divide's order is
+// almost the new one.  The stable sort by box key is then a MERGE of two sequences that
+// are both already ordered by (new key, previous index): the STAYERS (key unchanged;
+// they keep their relative order) and the MOVERS (a few percent).  A mover is NEAR when
+// its key moved by one of the 27 (dx,dy,dz) cell offsets — its new box finds it by
+// scanning its 27 source boxes — else FAR (an exclusion to an out box; anything else),
+// kept in a short list that every box scans.  Three kernels replace presort + the two
+// radix passes + begincell:
+//   k_inc_classify  new key, near/far flags and their exclusive prefixes (one chained
+//                   scan with decoupled look-back), compacted mover lists;
+//   k_inc_boxes     per box: stayers + arrivals, chained scan over the boxes -> the new
+//                   begincell, positions of the arrivals in previous-index order, the
+//                   stayers' offset; np / npb / npbok / nout as k_begincell;
+//   k_inc_push      every particle pushed to its new position (gather_one: poscell,
+//                   press, VelMax) with its key for the next divide.
+// The result is the stable radix sort's, bit for bit (tests/test_divide_inc.py).
+constexpr int INC_BS = 256, INC_IPT = 4, INC_TILE = INC_BS * INC_IPT;
+constexpr int IB_BS = 256, IB_BPT = 2, IB_BOX = IB_BS * IB_BPT;  // boxes per k_inc_boxes block
+constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_PAY = (1ull << 60) - 1;
+constexpr unsigned INC_M = 0x7fffffffu;
+// Phase timestamps of the incremental-divide kernels (SPH_INC_DBG & 8: printed for every
+// 16th block of the 12th incremental divide; the 100 MHz device clock).
+#define TSDECL unsigned long long tsv[8]
+#define TSTAMP(k) \
+  do { \
+    if (s.dbg & 8) tsv[k] = wall_clock64(); \
+  } while (0)
+#define TSPRINT(name, nk) \
+  do { \
+    if ((s.dbg & 8) && threadIdx.x == 0 && s.gen == 12 && (blockIdx.x % 16 == 0 || blockIdx.x + 1 == gridDim.x)) { \
+      printf("TS %s %u %llu %llu %llu %llu %llu %llu\n", name, blockIdx.x, tsv[0], tsv[1], tsv[2], tsv[3], \
+             tsv[(nk) > 4 ? 4 : 3], tsv[(nk) > 5 ? 5 : 3]); \
+    } \
+  } while (0)
+
+__device__ __forceinline__ unsigned long long lb_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Decoupled look-back by one wave: the exclusive prefix (payload bits 0-59) of block b.
+// Status words: flag (62-63: aggregate / inclusive), generation (60-61: entries of the
+// previous divide read as not ready), payload.  The status words cross the XCDs (each
+// probe is a trip to the memory-side cache), so one probe reads 64 LBQ predecessors: lane l
+// holds blocks base - LBQ l - q, q < LBQ (slot LBQ l + q, nearest first).
+constexpr int LBQ = 4;  // look-back slots per lane (16: slower, more loads to the memory-side cache in flight)
+__device__ unsigned long long lookback(const unsigned long long* stat, unsigned b, unsigned gen) {
+  const unsigned lane = threadIdx.x & 63;
+  const unsigned long long vinc = LB_INC | (static_cast<unsigned long long>(gen & 3u) << 60);
+  unsigned long long excl = 0;
+  long base = long(b) - 1;
+  while (base >= 0) {
+    unsigned long long v[LBQ];
+    int qi = LBQ;           // this lane's first inclusive slot
+    bool allrdy = true;   // all LBQ slots ready
+    bool rdyupto = true;  // slots 0..qi ready
+#pragma unroll
+    for (int q = 0; q < LBQ; q++) {
+      const long j = base - LBQ * long(lane) - q;
+      v[q] = j >= 0 ? lb_load(stat + j) : vinc;
+    }
+#pragma unroll
+    for (int q = LBQ - 1; q >= 0; q--)
+      if ((v[q] >> 62) == 2 && unsigned((v[q] >> 60) & 3u) == (gen & 3u)) qi = q;
+#pragma unroll
+    for (int q = 0; q < LBQ; q++) {
+      const bool r = (v[q] >> 62) != 0 && unsigned((v[q] >> 60) & 3u) == (gen & 3u);
+      allrdy = allrdy && r;
+      if (q <= qi) rdyupto = rdyupto && r;
+    }
+    const unsigned long long hasinc = __ballot(qi < LBQ);
+    const unsigned L = hasinc ? unsigned(__ffsll(static_cast<long long>(hasinc))) - 1u : 64u;
+    const bool need = lane < L ? allrdy : (lane == L ? rdyupto : true);
+    if (__ballot(!need)) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    unsigned long long x = 0;
+#pragma unroll
+    for (int q = 0; q < LBQ; q++)
+      if (lane < L || (lane == L && q <= qi)) x += v[q] & LB_PAY;
+    unsigned lo = unsigned(x), hi = unsigned(x >> 32);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const unsigned l2 = __shfl_xor(lo, off, 64), h2 = __shfl_xor(hi, off, 64);
+      const unsigned sm = lo + l2;
+      hi = hi + h2 + (sm < lo ? 1u : 0u);
+      lo = sm;
+    }
+    excl += (static_cast<unsigned long long>(hi) << 32) | lo;
+    if (hasinc) break;
+    base -= 64 * LBQ;
+  }
+  return excl;
+}
+
+// The block's place in the scan order is its index: the dispatcher starts workgroups in
+// index order, so a block's predecessors are running or done and the look-back ends.
+// (A ticket from a device-scope atomic counter cost ~12 ns per block: all blocks
+// serialize on one address.)
+// A key change by one of the 27 cell offsets dx + dy ncx + dz nsheet (distinct offsets:
+// ncx >= 3 and ncy >= 3, or no y offsets when ncy = 1; checked on the host).
+__device__ __forceinline__ bool inc_near(int d, int ncx, int nsheet, bool usey, bool usez) {
+#pragma unroll
+  for (int dz = -1; dz <= 1; dz++) {
+#pragma unroll
+    for (int dy = -1; dy <= 1; dy++) {
+      if ((!usez && dz) || (!usey && dy)) continue;
+      const int r = d - dz * nsheet - dy * ncx;
+      if (r >= -1 && r <= 1) return true;
+    }
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict__ sc, const unsigned* __restrict__ dcell,
+                                                         const typecode* __restrict__ code, DivGrid g, unsigned dcc,
+                                                         IncDivScratch s, int usey, int usez) {
+  __shared__ unsigned s_cn[INC_IPT * 4], s_cf[INC_IPT * 4];
+  __shared__ unsigned long long s_excl;
+  const unsigned n = sc->np;
+  const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned b = blockIdx.x;
+  TSDECL;
+  TSTAMP(0);
+  if (b == 0 && threadIdx.x == 0) sc->ndiv = n;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  unsigned key[INC_IPT], rn[INC_IPT], rf[INC_IPT];
+  bool nr[INC_IPT], fr[INC_IPT];
+  // every load of the tile first (one memory latency), then the classification
+  unsigned dc[INC_IPT], old[INC_IPT];
+  typecode cd[INC_IPT];
+#pragma unroll
+  for (int k = 0; k < INC_IPT; k++) {
+    const unsigned i = b * INC_TILE + k * INC_BS + threadIdx.x;
+    const unsigned ii = i < n ? i : 0u;
+    dc[k] = dcell[ii];
+    cd[k] = code[ii];
+    old[k] = s.skeys[ii];
+  }
+#pragma unroll
+  for (int k = 0; k < INC_IPT; k++) {
+    const unsigned i = b * INC_TILE + k * INC_BS + threadIdx.x;
+    const bool valid = i < n;
+    key[k] = box_key(dc[k], cd[k], g, dcc);
+    const int d = int(key[k] - old[k]);
+    nr[k] = valid && d != 0 && inc_near(d, g.ncx, int(g.nsheet), usey != 0, usez != 0);
+    fr[k] = valid && d != 0 && !nr[k];
+    const unsigned long long bn = __ballot(nr[k]), bf = __ballot(fr[k]);
+    rn[k] = unsigned(__popcll(bn & lt));
+    rf[k] = unsigned(__popcll(bf & lt));
+    if (lane == 0) {
+      s_cn[k * 4 + w] = unsigned(__popcll(bn));
+      s_cf[k * 4 + w] = unsigned(__popcll(bf));
+    }
+  }
+  __syncthreads();
+  TSTAMP(1);
+  if (w == 0) {
+    unsigned an = 0, af = 0;
+#pragma unroll
+    for (int q = 0; q < INC_IPT * 4; q++) {
+      an += s_cn[q];
+      af += s_cf[q];
+    }
+    const unsigned long long pay = (static_cast<unsigned long long>(an) << 30) | af;
+    const unsigned long long gb = static_cast<unsigned long long>(s.gen & 3u) << 60;
+    unsigned long long excl = 0;
+    if (b == 0) {
+      if (lane == 0) lb_store(s.stat1, LB_INC | gb | pay);
+    } else {
+      if (lane == 0) lb_store(s.stat1 + b, LB_AGG | gb | pay);
+      if (!(s.dbg & 1)) excl = lookback(s.stat1, b, s.gen);
+      if (lane == 0) lb_store(s.stat1 + b, LB_INC | gb | (excl + pay));
+    }
+    if (lane == 0) {
+      s_excl = excl;
+      if (b == s.nb1 - 1) {  // all particles: the mover totals
+        s.ctr[2 * QSTRIDE] = unsigned(excl >> 30) + an;
+        s.ctr[2 * QSTRIDE + 1] = unsigned(excl & ((1ull << 30) - 1)) + af;
+      }
+    }
+  }
+  __syncthreads();
+  TSTAMP(2);
+  const unsigned en = unsigned(s_excl >> 30), ef = unsigned(s_excl & ((1ull << 30) - 1));
+#pragma unroll
+  for (int k = 0; k < INC_IPT; k++) {
+    const unsigned i = b * INC_TILE + k * INC_BS + threadIdx.x;
+    if (i >= n) continue;
+    unsigned pn = 0, pf = 0;
+    for (unsigned q = 0; q < unsigned(k * 4) + w; q++) {
+      pn += s_cn[q];
+      pf += s_cf[q];
+    }
+    const unsigned jn = en + pn + rn[k], jf = ef + pf + rf[k];
+    s.newkey[i] = key[k];
+    s.ln[i] = jn | (nr[k] ? 0x80000000u : 0u);
+    s.lf[i] = jf | (fr[k] ? 0x80000000u : 0u);
+    if (nr[k]) s.mkey[jn] = key[k];
+    if (fr[k]) s.mfar[jf] = make_uint2(i, key[k]);
+  }
+  TSTAMP(3);
+  TSPRINT("classify", 4);
+}
+
+// One block per IB_BOX consecutive boxes [c0, c0 + IB_BOX); no scan across blocks.
+// A near mover changes its key by at most omax = 1 + ncx + nsheet, so every near mover
+// with a previous key below c0 - omax lands below c0 and none from c0 + IB_BOX + omax or
+// above lands in the block: the block reads the near movers of that WINDOW of previous
+// keys (a contiguous range of the mover list, previous-index order) and
+//   begin[c] = #stayers below c       = S(obx(c))
+//            + #near movers below c   = Ln(obx(c0 - omax)) + #window keys < c0 + arrivals in [c0, c)
+//            + #far movers below c    = #far keys < c0 + far arrivals in [c0, c)
+// (S(x) = x - Ln(x) - Lf(x): stayers before index x).  Within a box the members are
+// ordered by previous index: near arrivals in list order (a stable rank per box, wave
+// match on the 9-bit box offset), the stayers after the near arrivals whose list index is
+// below Ln(obx(c)), far arrivals (a short list) by their previous index.  Two passes over
+// the window: counts, then (after the per-box scan) ranks -> positions.
+constexpr int IB_FCAP = 256;  // far arrivals of a block held in LDS (more: read from global memory)
+__global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc, DivGrid g,
+                                                     const unsigned* __restrict__ ob, unsigned* __restrict__ nbc,
+                                                     IncDivScratch s, unsigned omax) {
+  constexpr int NW = IB_BS / 64;
+  __shared__ unsigned s_obx[IB_BOX + 1], s_ln[IB_BOX + 1], s_lf[IB_BOX + 1];
+  __shared__ unsigned s_narr[IB_BOX], s_nbef[IB_BOX], s_farr[IB_BOX], s_fbef[IB_BOX], s_run[IB_BOX];
+  __shared__ unsigned s_begin[IB_BOX];
+  __shared__ unsigned s_wc[NW][IB_BOX];
+  __shared__ uint4 s_far[IB_FCAP];      // (f, previous index, key, Ln(previous index))
+  __shared__ unsigned s_fnb[IB_FCAP];   // near arrivals of its box before a far arrival
+  __shared__ unsigned s_wsum[IB_BPT][NW];
+  __shared__ unsigned s_jw[2], s_below, s_farbelow, s_nfar;
+  const unsigned b = blockIdx.x;
+  TSDECL;
+  TSTAMP(0);
+  const unsigned n = sc->ndiv;
+  const unsigned totn = s.ctr[2 * QSTRIDE], totf = s.ctr[2 * QSTRIDE + 1];
+  const long nctt = long(g.nctt);
+  const long c0 = long(b) * IB_BOX;
+  const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  auto obxg = [&](long x) -> unsigned { return x <= 0 ? 0u : (x >= nctt ? n : min(ob[x], n)); };
+  auto lnw = [&](unsigned x) -> unsigned { return x >= n ? totn : (s.ln[x] & INC_M); };
+  // ---- staging: obx and the mover prefixes at the block's box bounds and window ends
+  unsigned xo[IB_BPT + 1];
+#pragma unroll
+  for (int m = 0; m <= IB_BPT; m++) {
+    const int k = int(threadIdx.x) + m * IB_BS;
+    long c = c0 + k;
+    if (m == IB_BPT) c = threadIdx.x == 0 ? c0 + IB_BOX : (threadIdx.x == 1 ? c0 - long(omax) : c0 + IB_BOX + long(omax));
+    xo[m] = obxg(c);
+  }
+  unsigned pl[IB_BPT + 1], pf[IB_BPT + 1];
+#pragma unroll
+  for (int m = 0; m <= IB_BPT; m++) {
+    pl[m] = lnw(xo[m]);
+    pf[m] = xo[m] >= n ? totf : (s.lf[xo[m]] & INC_M);
+  }
+#pragma unroll
+  for (int m = 0; m <= IB_BPT; m++) {
+    const int k = int(threadIdx.x) + m * IB_BS;
+    if (m < IB_BPT || threadIdx.x == 0) {
+      const int kk = m < IB_BPT ? k : IB_BOX;
+      s_obx[kk] = xo[m];
+      s_ln[kk] = pl[m];
+      s_lf[kk] = pf[m];
+    } else if (threadIdx.x <= 2) {
+      s_jw[threadIdx.x - 1] = pl[m];
+    }
+  }
+  for (int k = int(threadIdx.x); k < IB_BOX; k += IB_BS) {
+    s_narr[k] = 0;
+    s_nbef[k] = 0;
+    s_farr[k] = 0;
+    s_fbef[k] = 0;
+    s_run[k] = 0;
+#pragma unroll
+    for (int q = 0; q < NW; q++) s_wc[q][k] = 0;
+  }
+  if (threadIdx.x == 0) {
+    s_below = 0;
+    s_farbelow = 0;
+    s_nfar = 0;
+  }
+  __syncthreads();
+  TSTAMP(1);
+  const unsigned jlo = s_jw[0], jhi = s_jw[1];
+  const unsigned cend = unsigned(min(c0 + IB_BOX, nctt));
+  // ---- far movers (a short list; usually empty): below the block, or arrivals
+  for (unsigned f = threadIdx.x; f < totf; f += IB_BS) {
+    const uint2 e = s.mfar[f];
+    if (e.y < unsigned(c0)) {
+      atomicAdd(&s_farbelow, 1u);
+    } else if (e.y < cend) {
+      const unsigned lc = e.y - unsigned(c0);
+      atomicAdd(&s_farr[lc], 1u);
+      if (e.x < s_obx[lc]) atomicAdd(&s_fbef[lc], 1u);
+      const unsigned k = atomicAdd(&s_nfar, 1u);
+      if (k < unsigned(IB_FCAP)) {
+        s_far[k] = make_uint4(f, e.x, e.y, lnw(e.x));
+        s_fnb[k] = 0;
+      }
+    }
+  }
+  __syncthreads();
+  const unsigned nfar = s_nfar;
+  const bool farlds = nfar <= unsigned(IB_FCAP);
+  // near arrivals of box c before a far arrival (rare): LDS counters, or counted from global
+  // memory below when the block has more far arrivals than IB_FCAP
+  auto far_near = [&](unsigned lc, unsigned j) {
+    if (!farlds) return;
+    for (unsigned k = 0; k < nfar; k++) {
+      const uint4 fe = s_far[k];
+      if (fe.z - unsigned(c0) == lc && j < fe.w) atomicAdd(&s_fnb[k], 1u);
+    }
+  };
+  // ---- pass 1: near arrivals per box, and the window's near movers below the block
+  {
+    unsigned below = 0;
+    for (unsigned base = jlo; base < jhi; base += IB_BS) {
+      const unsigned j = base + threadIdx.x;
+      const unsigned key = j < jhi ? s.mkey[j] : ~0u;
+      below += __popcll(__ballot(key < unsigned(c0)));
+      if (key >= unsigned(c0) && key < cend) {
+        const unsigned lc = key - unsigned(c0);
+        atomicAdd(&s_narr[lc], 1u);
+        if (j < s_ln[lc]) atomicAdd(&s_nbef[lc], 1u);
+        if (s_farr[lc]) far_near(lc, j);
+      }
+    }
+    if (lane == 0 && below) atomicAdd(&s_below, below);
+  }
+  __syncthreads();
+  TSTAMP(2);
+  // ---- per-box scan: begin, stayer offset, counts
+  const unsigned base0 = s_jw[0] + s_below + s_farbelow;
+  unsigned cnt[IB_BPT], xs[IB_BPT];
+#pragma unroll
+  for (int h = 0; h < IB_BPT; h++) {
+    const int k = h * IB_BS + int(threadIdx.x);
+    cnt[h] = s_narr[k] + s_farr[k];
+    unsigned x = cnt[h];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned y = __shfl_up(x, off, 64);
+      if (lane >= unsigned(off)) x += y;
+    }
+    xs[h] = x;
+    if (lane == 63) s_wsum[h][w] = x;
+  }
+  __syncthreads();
+  unsigned hpre = 0;
+#pragma unroll
+  for (int h = 0; h < IB_BPT; h++) {
+    unsigned wpre = 0, hsum = 0;
+#pragma unroll
+    for (int q = 0; q < NW; q++) {
+      wpre += unsigned(q) < w ? s_wsum[h][q] : 0u;
+      hsum += s_wsum[h][q];
+    }
+    const int k = h * IB_BS + int(threadIdx.x);
+    const unsigned S = s_obx[k] - s_ln[k] - s_lf[k];
+    const unsigned stay = (s_obx[k + 1] - s_obx[k]) - (s_ln[k + 1] - s_ln[k]) - (s_lf[k + 1] - s_lf[k]);
+    const unsigned begin = S + base0 + hpre + wpre + xs[h] - cnt[h];
+    hpre += hsum;
+    s_begin[k] = begin;
+    const long c = c0 + k;
+    if (c >= nctt) continue;
+    const unsigned cu = unsigned(c);
+    nbc[cu] = begin;
+    s.stayoff[cu] = begin + s_nbef[k] + s_fbef[k] - S;
+    const unsigned total = cnt[h] + stay;
+    // JCellDivCpuSingle::Divide counts + RunCellDivide, as k_begincell
+    if (cu == g.boxboundignore) sc->npbok = begin;
+    if (cu == g.boxfluid) sc->npb = begin;
+    if (cu == g.boxboundout) {
+      sc->np = begin;
+      if (total) {
+        sc->npbout = total;
+        sc->error_flags |= ERR_BOUNDOUT;
+      }
+    }
+    if (cu == g.boxfluidout) sc->nout += total;
+  }
+  __syncthreads();
+  TSTAMP(3);
+  // ---- pass 2: stable rank of every near arrival in its box -> its new position
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  for (unsigned base = jlo; base < jhi; base += IB_BS) {
+    const unsigned j = base + threadIdx.x;
+    const unsigned key = j < jhi ? s.mkey[j] : ~0u;
+    const bool valid = key >= unsigned(c0) && key < cend;
+    if (__syncthreads_or(valid) == 0) continue;  // block-uniform
+    const unsigned lc = valid ? key - unsigned(c0) : 0u;
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 9; bit++) {
+      const bool on = (lc >> bit) & 1u;
+      const unsigned long long bb = __ballot(on);
+      peers &= on ? bb : ~bb;
+    }
+    const unsigned rank = unsigned(__popcll(peers & lt)), pc = unsigned(__popcll(peers));
+    const bool leader = valid && (peers & lt) == 0ull;
+    if (leader) s_wc[w][lc] = pc;
+    __syncthreads();
+    if (valid) {
+      unsigned r = s_run[lc] + rank;
+      for (unsigned q = 0; q < w; q++) r += s_wc[q][lc];
+      // far arrivals of this box ahead of it (previous index below this mover's)
+      if (s_farr[lc]) {
+        if (farlds) {
+          for (unsigned k = 0; k < nfar; k++)
+            if (s_far[k].z == key && s_far[k].w <= j) r++;
+        } else {
+          for (unsigned f = 0; f < totf; f++) {
+            const uint2 e = s.mfar[f];
+            if (e.y == key && lnw(e.x) <= j) r++;
+          }
+        }
+      }
+      const unsigned stay = (s_obx[lc + 1] - s_obx[lc]) - (s_ln[lc + 1] - s_ln[lc]) - (s_lf[lc + 1] - s_lf[lc]);
+      s.mposnear[j] = s_begin[lc] + r + (j >= s_ln[lc] ? stay : 0u);
+    }
+    __syncthreads();
+    if (leader) {
+      atomicAdd(&s_run[lc], pc);
+      s_wc[w][lc] = 0;
+    }
+  }
+  // ---- far arrivals: near arrivals before them + far arrivals before them + stayers
+  for (unsigned k = threadIdx.x; k < nfar; k += IB_BS) {
+    uint4 fe;
+    unsigned nb = 0;
+    if (farlds) {
+      fe = s_far[k];
+      nb = s_fnb[k];
+    } else {  // the k-th far arrival of the block in list order, counted from global memory
+      unsigned seen = 0, f = 0;
+      for (; f < totf; f++) {
+        const uint2 e = s.mfar[f];
+        if (e.y >= unsigned(c0) && e.y < cend && seen++ == k) break;
+      }
+      const uint2 e = s.mfar[f];
+      fe = make_uint4(f, e.x, e.y, lnw(e.x));
+      for (unsigned j = jlo; j < fe.w; j++) nb += (s.mkey[j] == fe.z) ? 1u : 0u;
+    }
+    const unsigned lc = fe.z - unsigned(c0);
+    unsigned r = nb;
+    for (unsigned f = 0; f < totf; f++) {
+      const uint2 e = s.mfar[f];
+      if (e.y == fe.z && e.x < fe.y) r++;
+    }
+    const unsigned stay = (s_obx[lc + 1] - s_obx[lc]) - (s_ln[lc + 1] - s_ln[lc]) - (s_lf[lc + 1] - s_lf[lc]);
+    s.mposfar[fe.x] = s_begin[lc] + r + (fe.y >= s_obx[lc] ? stay : 0u);
+  }
+  TSTAMP(4);
+  TSTAMP(5);
+  TSPRINT("boxes", 6);
+}
+
+// Loads in three batches (one memory latency each): the particle states and the
+// classification words, the new positions, then the stores.
+template <bool WITHM1, bool WITHPRE>
+__global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, GatherArgs a, IncDivScratch s) {
+  const unsigned nd = sc->ndiv, n = sc->np, npb = sc->npb;
+  const unsigned i0 = blockIdx.x * (256 * GP) + threadIdx.x;
+  GatherRec<WITHM1, WITHPRE> q[GP];
+  unsigned key[GP], ln[GP], lf[GP], pos[GP];
+#pragma unroll
+  for (int k = 0; k < GP; k++) {
+    const unsigned i = i0 + 256 * k;
+    const unsigned ii = i < nd ? i : 0u;
+    key[k] = s.newkey[ii];
+    ln[k] = s.ln[ii];
+    lf[k] = s.lf[ii];
+    q[k].load(a.src, ii);
+  }
+#pragma unroll
+  for (int k = 0; k < GP; k++) {
+    const bool near = (ln[k] >> 31) != 0, far = (lf[k] >> 31) != 0;
+    const unsigned* tab = near ? s.mposnear : (far ? s.mposfar : s.stayoff);
+    const unsigned x = tab[near ? (ln[k] & INC_M) : (far ? (lf[k] & INC_M) : key[k])];
+    pos[k] = (near || far) ? x : x + (i0 + 256 * k) - ln[k] - lf[k];
+  }
+  float v2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < GP; k++) {
+    // particles of the out boxes leave the arrays, as in the pull gather
+    if (i0 + 256 * k < nd && pos[k] < n) {
+      gather_store<WITHM1, WITHPRE>(a, pos[k], q[k]);
+      s.skeys[pos[k]] = key[k];
+      if (pos[k] >= npb) v2 = fmaxf(v2, q[k].vr.x * q[k].vr.x + q[k].vr.y * q[k].vr.y + q[k].vr.z * q[k].vr.z);
+    }
+  }
+  wave_max_atomic(sc, RED_VELMAX2, v2);
+}
+
+void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& src, const PartArrays& dst,
+                       bool withm1, bool withpre, const KConst& K, const double dom_posmin[3], float4* poscell,
+                       float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
+                       IncDivScratch& s, const float4* phase_eos) {
+  s.gen++;
+  const int usey = g.ncy > 1, usez = g.ncz > 1;
+  const unsigned omax = 1u + (usey ? unsigned(g.ncx) : 0u) + (usez ? g.nsheet : 0u);
+  hipLaunchKernelGGL(k_inc_classify, dim3(s.nb1), dim3(INC_BS), 0, stm, sc, src.dcell, src.code, g, K.domcellcode, s,
+                     usey, usez);
+  hipLaunchKernelGGL(k_inc_boxes, dim3(s.nb2), dim3(IB_BS), 0, stm, sc, g, begincell_old, begincell_new, s, omax);
+  GatherArgs a;
+  a.phase_eos = phase_eos;
+  a.xoff = 0;
+  a.src = src;
+  a.dst = dst;
+  a.sortpart = nullptr;
+  a.poscell = poscell;
+  a.press = press;
+  a.posminx = dom_posmin[0];
+  a.posminy = dom_posmin[1];
+  a.posminz = dom_posmin[2];
+  a.scelld = K.scelld;
+  a.cteb = K.cteb;
+  a.ovrhopzero = K.ovrhopzero;
+  a.rhopzero = K.rhopzero;
+  a.gamma = K.gamma;
+  a.igamma = (K.gamma == float(int(K.gamma)) && K.gamma >= 1.f && K.gamma <= 16.f) ? int(K.gamma) : 0;
+  a.dcc = K.domcellcode;
+  a.withm1 = withm1;
+  a.withpre = withpre;
+  const unsigned nb = (cap + 256 * GP - 1) / (256 * GP);
+  if (withm1 && withpre) hipLaunchKernelGGL((k_inc_push<true, true>), dim3(nb), dim3(256), 0, stm, sc, a, s);
+  else if (withm1) hipLaunchKernelGGL((k_inc_push<true, false>), dim3(nb), dim3(256), 0, stm, sc, a, s);
+  else if (withpre) hipLaunchKernelGGL((k_inc_push<false, true>), dim3(nb), dim3(256), 0, stm, sc, a, s);
+  else hipLaunchKernelGGL((k_inc_push<false, false>), dim3(nb), dim3(256), 0, stm, sc, a, s);
+}
+
+unsigned inc_blocks_classify(unsigned cap) { return (cap + INC_TILE - 1) / INC_TILE; }
+unsigned inc_blocks_boxes(unsigned nctt) { return (nctt + IB_BOX - 1) / IB_BOX; }
 
 }  // namespace sphx

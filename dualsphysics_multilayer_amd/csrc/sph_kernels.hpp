@@ -109,6 +109,32 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
                    const PartArrays& dst, bool withm1, bool withpre, const KConst& K, const double dom_posmin[3],
                    float4* poscell, float* press, int xoff, const float4* phase_eos = nullptr);
 
+// Incremental divide (sph_divide.hip): the stable order of the previous divide merged with
+// the particles whose box changed; single domain, every divide after the first.
+struct IncDivScratch {
+  unsigned* skeys = nullptr;      // [cap] box key of the particle at each index (last divide)
+  unsigned* newkey = nullptr;     // [cap] box key of this divide
+  unsigned* ln = nullptr;         // [cap] near movers before i | bit 31: i is a near mover
+  unsigned* lf = nullptr;         // [cap] far movers before i | bit 31: i is a far mover
+  unsigned* mkey = nullptr;       // [cap] new keys of the near movers (previous-index order)
+  uint2* mfar = nullptr;          // [cap] (previous index, new key) of the far movers
+  unsigned* mposnear = nullptr;   // [cap] new positions of the movers
+  unsigned* mposfar = nullptr;    // [cap]
+  unsigned* stayoff = nullptr;    // [nctt] new index of a stayer = stayoff[key] + i - ln - lf
+  unsigned long long* stat1 = nullptr;  // look-back status per classify block [nb1]
+  unsigned long long* stat2 = nullptr;  // per box block [nb2]
+  unsigned* ctr = nullptr;        // tickets of the two scans (own 128-B lines) + mover totals
+  unsigned nb1 = 0, nb2 = 0, gen = 0;
+  int dbg = 0;  // SPH_INC_DBG ablations (timing only): 1 no classify look-back, 2 no box look-back, 4 no box count loops
+};
+unsigned inc_blocks_classify(unsigned cap);
+unsigned inc_blocks_boxes(unsigned nctt);
+// ctr: [0] / [QSTRIDE] tickets, [2 QSTRIDE] near total, [2 QSTRIDE + 1] far total
+void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& src, const PartArrays& dst,
+                       bool withm1, bool withpre, const KConst& K, const double dom_posmin[3], float4* poscell,
+                       float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
+                       IncDivScratch& s, const float4* phase_eos = nullptr);
+
 // ---- interaction (cusph::Interaction_Forces, JSphGpu_ker.cu:788-885) ----
 // With floating bodies (ftmassp != nullptr: particle mass per body, `code` of the
 // sorted particles) the kernel reads the p2 codes (JSphCpu.cpp:692-703).

@@ -354,6 +354,10 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   nctmax_ = slab() ? unsigned(C.dom_cells[0] + 2) * unsigned(G.ncy) * unsigned(G.ncz) : G.nct;
   if (const char* e = std::getenv("SPH_INTERACTION")) tiled_ = std::string(e) != "simple";
   if (const char* e = std::getenv("SPH_COMM_TIMEOUT_S")) comm_timeout_s_ = std::max(1.0, std::atof(e));
+  // incremental divide: distinct key offsets of the 27 neighbour cells (ncx >= 3; ncy >= 3
+  // or a single y row), 30-bit mover counts, single domain
+  inc_ok_ = !slab() && G.ncx >= 3 && (G.ncy >= 3 || G.ncy == 1) && n < (1u << 30);
+  if (const char* e = std::getenv("SPH_DIVIDE")) inc_ok_ = inc_ok_ && std::string(e) != "full";
   // The tiled kernel stages the 3x3 rows of 3 cells of CellMode=full, or the 5x5 rows of
   // 5 half-cells of CellMode=half (run_pass_half).
   nn_ = (C.rheology == SPH_RHEOLOGY_NN);
@@ -411,6 +415,16 @@ void SphGpuSingle::AllocFixed() {
   qctr_ = (unsigned*)dmalloc(QCTR_BYTES);
   check_hip(hipMemset(qctr_, 0, QCTR_BYTES), "zero work counters");
   sort_.digtot = (unsigned*)dmalloc(4 * (1u << RS_MAXBITS));
+  if (inc_ok_) {
+    begincell_alt_ = (unsigned*)dmalloc(4 * (2 * size_t(nctmax_) + 6));
+    inc_.stayoff = (unsigned*)dmalloc(4 * (2 * size_t(nctmax_) + 6));
+    inc_.nb2 = inc_blocks_boxes(G.nctt);
+    if (const char* e = std::getenv("SPH_INC_DBG")) inc_.dbg = std::atoi(e);
+    inc_.stat2 = (unsigned long long*)dmalloc(8 * size_t(inc_.nb2));
+    check_hip(hipMemset(inc_.stat2, 0, 8 * size_t(inc_.nb2)), "zero scan status");
+    inc_.ctr = (unsigned*)dmalloc(4 * 3 * QSTRIDE);
+    check_hip(hipMemset(inc_.ctr, 0, 4 * 3 * QSTRIDE), "zero scan tickets");
+  }
   sc_ = (DevScalars*)dmalloc(sizeof(DevScalars));
   dttrace_ = (double*)dmalloc(8 * size_t(tracecap_));
   pairs_ = (unsigned long long*)dmalloc(8 * 6);
@@ -476,6 +490,19 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
   for (int i = 0; i < 2; i++) {
     sort_.keys[i] = (unsigned*)dmalloc(4 * n);
     sort_.vals[i] = (unsigned*)dmalloc(4 * n);
+  }
+  if (inc_ok_) {
+    inc_.skeys = (unsigned*)dmalloc(4 * n);
+    inc_.newkey = (unsigned*)dmalloc(4 * n);
+    inc_.ln = (unsigned*)dmalloc(4 * n);
+    inc_.lf = (unsigned*)dmalloc(4 * n);
+    inc_.mkey = (unsigned*)dmalloc(4 * n);
+    inc_.mfar = (uint2*)dmalloc(8 * n);
+    inc_.mposnear = (unsigned*)dmalloc(4 * n);
+    inc_.mposfar = (unsigned*)dmalloc(4 * n);
+    inc_.nb1 = inc_blocks_classify(n);
+    inc_.stat1 = (unsigned long long*)dmalloc(8 * size_t(inc_.nb1));
+    check_hip(hipMemset(inc_.stat1, 0, 8 * size_t(inc_.nb1)), "zero scan status");
   }
   sort_.ntiles = unsigned((n + RS_TILE - 1) / RS_TILE);
   sort_.hist = (unsigned*)dmalloc(4 * size_t(sort_.ntiles) * (1u << RS_MAXBITS));
@@ -850,12 +877,23 @@ void SphGpuSingle::RunCellDivide() {
       !havepre_)
     Repartition();
   if (slab() && exchange_armed_) Exchange();
-  launch_presort(stream, cap_, sc_, cur_.dcell, cur_.code, G, C.dom_cellcode, sort_.keys[0], sort_.vals[0]);
-  const int res = launch_radix_sort(stream, cap_, sc_, sort_, keybits_);
-  launch_begincell(stream, cap_, sc_, sort_.keys[res], G, begincell_);
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET);
-  launch_gather(stream, cap_, sc_, sort_.vals[res], cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_,
-                G.xoff, nn_ ? phaseeos_ : nullptr);
+  if (inc_ok_ && inc_valid_) {
+    // the previous order merged with the particles whose box changed (sph_divide.hip)
+    launch_divide_inc(stream, cap_, sc_, cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_, G, begincell_,
+                      begincell_alt_, inc_, nn_ ? phaseeos_ : nullptr);
+    std::swap(begincell_, begincell_alt_);
+  } else {
+    launch_presort(stream, cap_, sc_, cur_.dcell, cur_.code, G, C.dom_cellcode, sort_.keys[0], sort_.vals[0]);
+    const int res = launch_radix_sort(stream, cap_, sc_, sort_, keybits_);
+    launch_begincell(stream, cap_, sc_, sort_.keys[res], G, begincell_);
+    launch_gather(stream, cap_, sc_, sort_.vals[res], cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_,
+                  G.xoff, nn_ ? phaseeos_ : nullptr);
+    if (inc_ok_)
+      check_hip(hipMemcpyAsync(inc_.skeys, sort_.keys[res], 4 * size_t(cap_), hipMemcpyDeviceToDevice, stream),
+                "keep sorted keys");
+  }
+  inc_valid_ = inc_ok_;
   std::swap(cur_, alt_);
   if (tiled_) {
     launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv);  // also zeroes the queues

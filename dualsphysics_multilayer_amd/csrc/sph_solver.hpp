@@ -146,6 +146,11 @@ class SphGpuSingle {
   bool qfresh_ = false;  // the tiled kernels' work queues were zeroed by the last item build
   bool tiled_ = true;             // SPH_INTERACTION=simple selects the one-lane-per-particle kernel
   SortScratch sort_;
+  // incremental divide (single domain, after the first divide; SPH_DIVIDE=full disables it)
+  IncDivScratch inc_;
+  unsigned* begincell_alt_ = nullptr;
+  bool inc_ok_ = false;     // usable for this grid/domain
+  bool inc_valid_ = false;  // inc_.skeys holds the keys of the current particle order
   DevScalars* sc_ = nullptr;
   DevScalars* sc_host_ = nullptr;  // pinned mirror for readback
   double* dttrace_ = nullptr;

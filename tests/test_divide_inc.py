@@ -1,0 +1,113 @@
+"""Incremental divide (sph_divide.hip, k_inc_classify / k_inc_boxes / k_inc_push).
+
+Every divide after the first merges the previous stable order with the particles whose
+box changed instead of re-sorting all keys.  The reference defines the order as the
+stable sort by box key (JCellDivCpuSingle.cpp:203-234, the CPU counting sort); the radix
+path (SPH_DIVIDE=full) is pinned to the oracle's order bit for bit
+(test_gpu_parity.py::test_initial_divide_order_is_the_oracles, and through every
+reference-PART test).  Here the incremental path must give the radix path's state BIT
+FOR BIT after every step — particle order, positions, velocities, densities, counts and
+the dt trace — on cases that move particles across cells in every direction, exclude
+particles (far movers to the out boxes), move bodies, and on 2-D (one y row), half
+cells and the NN solver.
+"""
+import copy
+
+import numpy as np
+import pytest
+
+from dualsphysics_multilayer_amd.case import DamBreak2DCase, DamBreakCase, WaveFlumeCase, WetDambreakNNCase
+
+pytestmark = pytest.mark.gpu
+
+
+def _solver(case, mode, monkeypatch):
+    from dualsphysics_multilayer_amd.core import SphGpuSingle
+
+    if mode == "full":
+        monkeypatch.setenv("SPH_DIVIDE", "full")
+    else:
+        monkeypatch.delenv("SPH_DIVIDE", raising=False)
+    s = SphGpuSingle(case, device=0)
+    monkeypatch.delenv("SPH_DIVIDE", raising=False)
+    return s
+
+
+def _same(case, nsteps, chunk, monkeypatch):
+    a = _solver(case, "inc", monkeypatch)
+    b = _solver(case, "full", monkeypatch)
+    done = 0
+    while done < nsteps:
+        a.run(chunk)
+        b.run(chunk)
+        done += chunk
+        sa, sb = a.stats(), b.stats()
+        for k in ("np", "npb", "npbok", "nout", "nstep", "error_flags"):
+            assert sa[k] == sb[k], (done, k, sa[k], sb[k])
+        pa, pb = a.particles(), b.particles()
+        for k in ("idp", "pos", "vel", "rhop"):  # device order: the divide's order itself
+            assert np.array_equal(pa[k], pb[k]), (done, k)
+    assert np.array_equal(a.dt_trace(), b.dt_trace())
+    return a.stats()
+
+
+def _stirred(case, frac, speed, seed=3):
+    """Fluid particles given random velocities so that many cross cell faces in every
+    direction (x, y, z and diagonals) within a few steps."""
+    c = copy.copy(case)
+    c.vel = case.vel.copy()
+    rng = np.random.default_rng(seed)
+    fl = np.arange(case.npb, case.np)
+    pick = rng.choice(fl, int(frac * len(fl)), replace=False)
+    c.vel[pick] = rng.uniform(-speed, speed, size=(len(pick), 3))
+    return c
+
+
+def test_inc_divide_verlet_stirred(monkeypatch):
+    case = _stirred(DamBreakCase(0.02, celldomfixed=True), 0.5, 3.0)
+    _same(case, 60, 5, monkeypatch)
+
+
+def test_inc_divide_symplectic_ddt1(monkeypatch):
+    case = _stirred(DamBreakCase(0.025, step_algorithm=2, tdensity=1, celldomfixed=True), 0.3, 2.0)
+    _same(case, 40, 4, monkeypatch)
+
+
+def test_inc_divide_exclusions(monkeypatch):
+    """Far movers: OUTMOVE / OUTPOS / OUTRHOP exclusions go to the out boxes (and leave np)."""
+    case = DamBreakCase(0.03, celldomfixed=True, rhopoutmax=1010.0)
+    rng = np.random.default_rng(7)
+    pick = rng.choice(np.arange(case.npb, case.np), 40, replace=False)
+    case.vel[pick[:10]] = [0, 0, 400.0]
+    case.vel[pick[10:20]] = [0, 0, -30.0]
+    case.vel[pick[20:30]] = [-120.0, 0, 0]
+    case.vel[pick[30:]] = [0, 25.0, 0]
+    st = _same(case, 30, 1, monkeypatch)
+    assert st["nout"] >= 10
+
+
+def test_inc_divide_half_cells(monkeypatch):
+    case = _stirred(DamBreakCase(0.025, cellmode=2, celldomfixed=True), 0.3, 2.0)
+    _same(case, 30, 5, monkeypatch)
+
+
+def test_inc_divide_2d(monkeypatch):
+    case = _stirred(DamBreak2DCase(0.01), 0.3, 2.0)
+    _same(case, 60, 10, monkeypatch)
+
+
+def test_inc_divide_bodies(monkeypatch):
+    """Piston, flap (moving boundaries) and a floating box (particles moved by the body)."""
+    _same(WaveFlumeCase(0.025), 40, 8, monkeypatch)
+
+
+def test_inc_divide_nn(monkeypatch):
+    _same(WetDambreakNNCase(0.025, width=0.2, scale=0.5), 20, 5, monkeypatch)
+
+
+def test_inc_divide_1m(monkeypatch):
+    """BASELINE cfg2 size: 1,025,964 particles, 20 steps (one Euler step at 40 is not
+    reached; the Verlet steps carry VelrhopM1 through the push)."""
+    case = DamBreakCase(0.0045)
+    assert case.np == 1025964
+    _same(case, 20, 10, monkeypatch)
