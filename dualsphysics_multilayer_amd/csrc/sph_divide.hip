@@ -478,22 +478,28 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
 // almost the new one.  The stable sort by box key is then a MERGE of two sequences that
 // are both already ordered by (new key, previous index): the STAYERS (key unchanged;
 // they keep their relative order) and the MOVERS (a few percent).  A mover is NEAR when
-// its key moved by one of the 27 (dx,dy,dz) cell offsets — its new box finds it by
-// scanning its 27 source boxes — else FAR (an exclusion to an out box; anything else),
-// kept in a short list that every box scans.  Three kernels replace presort + the two
-// radix passes + begincell:
-//   k_inc_classify  new key, near/far flags and their exclusive prefixes (one chained
-//                   scan with decoupled look-back), compacted mover lists;
-//   k_inc_boxes     per box: stayers + arrivals, chained scan over the boxes -> the new
-//                   begincell, positions of the arrivals in previous-index order, the
-//                   stayers' offset; np / npb / npbok / nout as k_begincell;
-//   k_inc_push      every particle pushed to its new position (gather_one: poscell,
+// its key moved by one of the 27 (dx,dy,dz) cell offsets, else FAR (an exclusion to an
+// out box; anything else), kept in a short list.  Three kernels replace presort + the two
+// radix passes + begincell, with no scan across blocks (a chained scan's look-back costs
+// ~2 us per probe here: the status words cross the XCDs):
+//   k_inc_classify  per tile of INC_TILE particles: new key, near/far flags and their
+//                   tile-local prefixes, the tile's counts (+ one atomic into its super
+//                   tile of 64), near movers' keys at tile-major slots, far movers
+//                   appended to a list;
+//   k_inc_boxes     per IB_BOX boxes: the mover prefixes of the tiles it reads (super +
+//                   tile counts), the new begincell and every arrival's position from the
+//                   window of previous keys that can reach its boxes, the stayers' offset;
+//                   np / npb / npbok / nout as k_begincell;
+//   k_inc_push      every particle pushed to its new position (gather_store: poscell,
 //                   press, VelMax) with its key for the next divide.
 // The result is the stable radix sort's, bit for bit (tests/test_divide_inc.py).
-constexpr int INC_BS = 256, INC_IPT = 4, INC_TILE = INC_BS * INC_IPT;
+constexpr int INC_BS = 256, INC_IPT = 4, INC_TILE = INC_BS * INC_IPT;  // = one k_inc_push block (GP = 4)
+static_assert(INC_IPT == GP, "k_inc_push covers one classify tile per block");
+static_assert(INC_TILE == int(INC_TILE_SIZE), "tile size of the host allocations");
+static_assert(INC_TILE <= 2048, "tile-local prefixes are 11 bits");
+constexpr int INC_SUP = 64;  // tiles per super tile
 constexpr int IB_BS = 256, IB_BPT = 2, IB_BOX = IB_BS * IB_BPT;  // boxes per k_inc_boxes block
-constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_PAY = (1ull << 60) - 1;
-constexpr unsigned INC_M = 0x7fffffffu;
+constexpr unsigned CW_NEAR = 0x80000000u, CW_FAR = 0x40000000u, CW_LOC = 0x7ffu;
 // Phase timestamps of the incremental-divide kernels (SPH_INC_DBG & 8: printed for every
 // 16th block of the 12th incremental divide; the 100 MHz device clock).
 #define TSDECL unsigned long long tsv[8]
@@ -509,73 +515,6 @@ constexpr unsigned INC_M = 0x7fffffffu;
     } \
   } while (0)
 
-__device__ __forceinline__ unsigned long long lb_load(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Decoupled look-back by one wave: the exclusive prefix (payload bits 0-59) of block b.
-// Status words: flag (62-63: aggregate / inclusive), generation (60-61: entries of the
-// previous divide read as not ready), payload.  The status words cross the XCDs (each
-// probe is a trip to the memory-side cache), so one probe reads 64 LBQ predecessors: lane l
-// holds blocks base - LBQ l - q, q < LBQ (slot LBQ l + q, nearest first).
-constexpr int LBQ = 4;  // look-back slots per lane (16: slower, more loads to the memory-side cache in flight)
-__device__ unsigned long long lookback(const unsigned long long* stat, unsigned b, unsigned gen) {
-  const unsigned lane = threadIdx.x & 63;
-  const unsigned long long vinc = LB_INC | (static_cast<unsigned long long>(gen & 3u) << 60);
-  unsigned long long excl = 0;
-  long base = long(b) - 1;
-  while (base >= 0) {
-    unsigned long long v[LBQ];
-    int qi = LBQ;           // this lane's first inclusive slot
-    bool allrdy = true;   // all LBQ slots ready
-    bool rdyupto = true;  // slots 0..qi ready
-#pragma unroll
-    for (int q = 0; q < LBQ; q++) {
-      const long j = base - LBQ * long(lane) - q;
-      v[q] = j >= 0 ? lb_load(stat + j) : vinc;
-    }
-#pragma unroll
-    for (int q = LBQ - 1; q >= 0; q--)
-      if ((v[q] >> 62) == 2 && unsigned((v[q] >> 60) & 3u) == (gen & 3u)) qi = q;
-#pragma unroll
-    for (int q = 0; q < LBQ; q++) {
-      const bool r = (v[q] >> 62) != 0 && unsigned((v[q] >> 60) & 3u) == (gen & 3u);
-      allrdy = allrdy && r;
-      if (q <= qi) rdyupto = rdyupto && r;
-    }
-    const unsigned long long hasinc = __ballot(qi < LBQ);
-    const unsigned L = hasinc ? unsigned(__ffsll(static_cast<long long>(hasinc))) - 1u : 64u;
-    const bool need = lane < L ? allrdy : (lane == L ? rdyupto : true);
-    if (__ballot(!need)) {
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    unsigned long long x = 0;
-#pragma unroll
-    for (int q = 0; q < LBQ; q++)
-      if (lane < L || (lane == L && q <= qi)) x += v[q] & LB_PAY;
-    unsigned lo = unsigned(x), hi = unsigned(x >> 32);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const unsigned l2 = __shfl_xor(lo, off, 64), h2 = __shfl_xor(hi, off, 64);
-      const unsigned sm = lo + l2;
-      hi = hi + h2 + (sm < lo ? 1u : 0u);
-      lo = sm;
-    }
-    excl += (static_cast<unsigned long long>(hi) << 32) | lo;
-    if (hasinc) break;
-    base -= 64 * LBQ;
-  }
-  return excl;
-}
-
-// The block's place in the scan order is its index: the dispatcher starts workgroups in
-// index order, so a block's predecessors are running or done and the look-back ends.
-// (A ticket from a device-scope atomic counter cost ~12 ns per block: all blocks
-// serialize on one address.)
 // A key change by one of the 27 cell offsets dx + dy ncx + dz nsheet (distinct offsets:
 // ncx >= 3 and ncy >= 3, or no y offsets when ncy = 1; checked on the host).
 __device__ __forceinline__ bool inc_near(int d, int ncx, int nsheet, bool usey, bool usez) {
@@ -595,15 +534,14 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
                                                          const typecode* __restrict__ code, DivGrid g, unsigned dcc,
                                                          IncDivScratch s, int usey, int usez) {
   __shared__ unsigned s_cn[INC_IPT * 4], s_cf[INC_IPT * 4];
-  __shared__ unsigned long long s_excl;
   const unsigned n = sc->np;
   const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const unsigned b = blockIdx.x;
+  const unsigned b = blockIdx.x;  // the tile
   TSDECL;
   TSTAMP(0);
   if (b == 0 && threadIdx.x == 0) sc->ndiv = n;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  unsigned key[INC_IPT], rn[INC_IPT], rf[INC_IPT];
+  unsigned key[INC_IPT], rn[INC_IPT], rf[INC_IPT], fpos[INC_IPT];
   bool nr[INC_IPT], fr[INC_IPT];
   // every load of the tile first (one memory latency), then the classification
   unsigned dc[INC_IPT], old[INC_IPT];
@@ -627,6 +565,13 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
     const unsigned long long bn = __ballot(nr[k]), bf = __ballot(fr[k]);
     rn[k] = unsigned(__popcll(bn & lt));
     rf[k] = unsigned(__popcll(bf & lt));
+    fpos[k] = 0;
+    if (bf) {  // far movers (rare): appended to the list, one atomic per wave
+      const unsigned lead = unsigned(__ffsll(static_cast<long long>(bf))) - 1u;
+      unsigned base = 0;
+      if (lane == lead) base = atomicAdd(&s.ctr[0], unsigned(__popcll(bf)));
+      fpos[k] = __shfl(base, int(lead), 64) + rf[k];
+    }
     if (lane == 0) {
       s_cn[k * 4 + w] = unsigned(__popcll(bn));
       s_cf[k * 4 + w] = unsigned(__popcll(bf));
@@ -634,34 +579,6 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
   }
   __syncthreads();
   TSTAMP(1);
-  if (w == 0) {
-    unsigned an = 0, af = 0;
-#pragma unroll
-    for (int q = 0; q < INC_IPT * 4; q++) {
-      an += s_cn[q];
-      af += s_cf[q];
-    }
-    const unsigned long long pay = (static_cast<unsigned long long>(an) << 30) | af;
-    const unsigned long long gb = static_cast<unsigned long long>(s.gen & 3u) << 60;
-    unsigned long long excl = 0;
-    if (b == 0) {
-      if (lane == 0) lb_store(s.stat1, LB_INC | gb | pay);
-    } else {
-      if (lane == 0) lb_store(s.stat1 + b, LB_AGG | gb | pay);
-      if (!(s.dbg & 1)) excl = lookback(s.stat1, b, s.gen);
-      if (lane == 0) lb_store(s.stat1 + b, LB_INC | gb | (excl + pay));
-    }
-    if (lane == 0) {
-      s_excl = excl;
-      if (b == s.nb1 - 1) {  // all particles: the mover totals
-        s.ctr[2 * QSTRIDE] = unsigned(excl >> 30) + an;
-        s.ctr[2 * QSTRIDE + 1] = unsigned(excl & ((1ull << 30) - 1)) + af;
-      }
-    }
-  }
-  __syncthreads();
-  TSTAMP(2);
-  const unsigned en = unsigned(s_excl >> 30), ef = unsigned(s_excl & ((1ull << 30) - 1));
 #pragma unroll
   for (int k = 0; k < INC_IPT; k++) {
     const unsigned i = b * INC_TILE + k * INC_BS + threadIdx.x;
@@ -671,31 +588,48 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
       pn += s_cn[q];
       pf += s_cf[q];
     }
-    const unsigned jn = en + pn + rn[k], jf = ef + pf + rf[k];
+    const unsigned ln = pn + rn[k], lf = pf + rf[k];  // tile-local exclusive prefixes
     s.newkey[i] = key[k];
-    s.ln[i] = jn | (nr[k] ? 0x80000000u : 0u);
-    s.lf[i] = jf | (fr[k] ? 0x80000000u : 0u);
-    if (nr[k]) s.mkey[jn] = key[k];
-    if (fr[k]) s.mfar[jf] = make_uint2(i, key[k]);
+    s.cw[i] = ln | (lf << 11) | (nr[k] ? CW_NEAR : 0u) | (fr[k] ? CW_FAR : 0u);
+    if (nr[k]) s.mkey[b * INC_TILE + ln] = key[k];
+    if (fr[k]) {
+      s.mfar[fpos[k]] = make_uint2(i, key[k]);
+      s.fidx[i] = fpos[k];
+    }
   }
+  if (threadIdx.x == 0) {
+    unsigned an = 0, af = 0;
+#pragma unroll
+    for (int q = 0; q < INC_IPT * 4; q++) {
+      an += s_cn[q];
+      af += s_cf[q];
+    }
+    s.tagg[b] = make_uint2(an, af);
+    if (an | af) atomicAdd(&s.tsup[b / INC_SUP], (static_cast<unsigned long long>(an) << 32) | af);
+  }
+  TSTAMP(2);
   TSTAMP(3);
   TSPRINT("classify", 4);
 }
 
-// One block per IB_BOX consecutive boxes [c0, c0 + IB_BOX); no scan across blocks.
+// One block per IB_BOX consecutive boxes [c0, c0 + IB_BOX).
+// Mover prefixes: Ln(x) / Lf(x) = near / far movers before index x = the tile prefix
+// (super-tile sums + the tile counts of the super tile) + the tile-local prefix of x.
 // A near mover changes its key by at most omax = 1 + ncx + nsheet, so every near mover
 // with a previous key below c0 - omax lands below c0 and none from c0 + IB_BOX + omax or
 // above lands in the block: the block reads the near movers of that WINDOW of previous
-// keys (a contiguous range of the mover list, previous-index order) and
+// keys (list indices [Ln(obx(c0 - omax)), Ln(obx(c0 + IB_BOX + omax))), previous-index
+// order) and
 //   begin[c] = #stayers below c       = S(obx(c))
 //            + #near movers below c   = Ln(obx(c0 - omax)) + #window keys < c0 + arrivals in [c0, c)
 //            + #far movers below c    = #far keys < c0 + far arrivals in [c0, c)
 // (S(x) = x - Ln(x) - Lf(x): stayers before index x).  Within a box the members are
 // ordered by previous index: near arrivals in list order (a stable rank per box, wave
 // match on the 9-bit box offset), the stayers after the near arrivals whose list index is
-// below Ln(obx(c)), far arrivals (a short list) by their previous index.  Two passes over
-// the window: counts, then (after the per-box scan) ranks -> positions.
+// at least Ln(obx(c)), far arrivals (a short list) by their previous index.  Two passes
+// over the window: counts, then (after the per-box scan) ranks -> positions.
 constexpr int IB_FCAP = 256;  // far arrivals of a block held in LDS (more: read from global memory)
+constexpr int IB_TPCAP = 1024;  // window tiles with LDS prefixes (more: computed from global memory)
 __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc, DivGrid g,
                                                      const unsigned* __restrict__ ob, unsigned* __restrict__ nbc,
                                                      IncDivScratch s, unsigned omax) {
@@ -704,47 +638,34 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   __shared__ unsigned s_narr[IB_BOX], s_nbef[IB_BOX], s_farr[IB_BOX], s_fbef[IB_BOX], s_run[IB_BOX];
   __shared__ unsigned s_begin[IB_BOX];
   __shared__ unsigned s_wc[NW][IB_BOX];
-  __shared__ uint4 s_far[IB_FCAP];      // (f, previous index, key, Ln(previous index))
+  __shared__ uint2 s_tp[IB_TPCAP];      // (near, far) movers before tile tA + k
+  __shared__ uint4 s_far[IB_FCAP];      // (f, previous index, key, Ln(previous index) clamped to the window)
   __shared__ unsigned s_fnb[IB_FCAP];   // near arrivals of its box before a far arrival
   __shared__ unsigned s_wsum[IB_BPT][NW];
-  __shared__ unsigned s_jw[2], s_below, s_farbelow, s_nfar;
+  __shared__ unsigned long long s_red[2][NW];
+  __shared__ unsigned s_xw[2], s_jw[2], s_below, s_farbelow, s_nfar;
   const unsigned b = blockIdx.x;
   TSDECL;
   TSTAMP(0);
   const unsigned n = sc->ndiv;
-  const unsigned totn = s.ctr[2 * QSTRIDE], totf = s.ctr[2 * QSTRIDE + 1];
+  const unsigned totf = s.ctr[0];
   const long nctt = long(g.nctt);
   const long c0 = long(b) * IB_BOX;
   const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned nsup = (s.nb1 + INC_SUP - 1) / INC_SUP;
   auto obxg = [&](long x) -> unsigned { return x <= 0 ? 0u : (x >= nctt ? n : min(ob[x], n)); };
-  auto lnw = [&](unsigned x) -> unsigned { return x >= n ? totn : (s.ln[x] & INC_M); };
-  // ---- staging: obx and the mover prefixes at the block's box bounds and window ends
+  // ---- 1. obx of the block's box bounds and of the window ends
   unsigned xo[IB_BPT + 1];
 #pragma unroll
   for (int m = 0; m <= IB_BPT; m++) {
-    const int k = int(threadIdx.x) + m * IB_BS;
-    long c = c0 + k;
+    long c = c0 + int(threadIdx.x) + m * IB_BS;
     if (m == IB_BPT) c = threadIdx.x == 0 ? c0 + IB_BOX : (threadIdx.x == 1 ? c0 - long(omax) : c0 + IB_BOX + long(omax));
     xo[m] = obxg(c);
   }
-  unsigned pl[IB_BPT + 1], pf[IB_BPT + 1];
 #pragma unroll
-  for (int m = 0; m <= IB_BPT; m++) {
-    pl[m] = lnw(xo[m]);
-    pf[m] = xo[m] >= n ? totf : (s.lf[xo[m]] & INC_M);
-  }
-#pragma unroll
-  for (int m = 0; m <= IB_BPT; m++) {
-    const int k = int(threadIdx.x) + m * IB_BS;
-    if (m < IB_BPT || threadIdx.x == 0) {
-      const int kk = m < IB_BPT ? k : IB_BOX;
-      s_obx[kk] = xo[m];
-      s_ln[kk] = pl[m];
-      s_lf[kk] = pf[m];
-    } else if (threadIdx.x <= 2) {
-      s_jw[threadIdx.x - 1] = pl[m];
-    }
-  }
+  for (int m = 0; m < IB_BPT; m++) s_obx[int(threadIdx.x) + m * IB_BS] = xo[m];
+  if (threadIdx.x == 0) s_obx[IB_BOX] = xo[IB_BPT];
+  if (threadIdx.x == 1 || threadIdx.x == 2) s_xw[threadIdx.x - 1] = xo[IB_BPT];
   for (int k = int(threadIdx.x); k < IB_BOX; k += IB_BS) {
     s_narr[k] = 0;
     s_nbef[k] = 0;
@@ -760,9 +681,138 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
     s_nfar = 0;
   }
   __syncthreads();
+  // ---- 2. the window's tiles [tA, tB]: their counts, the movers before tA, the totals;
+  // the tile-local prefixes of the block's box bounds (one batch of loads)
+  const unsigned xa = s_xw[0], xb = s_xw[1];
+  const unsigned tA = (xa < n ? xa : (n ? n - 1 : 0u)) / INC_TILE;
+  const unsigned tB = (xb < n ? xb : (n ? n - 1 : 0u)) / INC_TILE;
+  const unsigned ntp = tB - tA + 1;
+  const bool tplds = ntp <= unsigned(IB_TPCAP) && !(s.dbg & 16);
+  unsigned cwo[IB_BPT + 1];
+#pragma unroll
+  for (int m = 0; m <= IB_BPT; m++) cwo[m] = s.cw[xo[m] < n ? xo[m] : 0u];
+  uint2 ta[IB_TPCAP / IB_BS];
+#pragma unroll
+  for (int m = 0; m < IB_TPCAP / IB_BS; m++) {
+    const unsigned k = threadIdx.x + m * IB_BS;
+    ta[m] = (tplds && k < ntp) ? s.tagg[tA + k] : make_uint2(0u, 0u);
+  }
+  unsigned long long pre = 0, tot = 0;  // (near << 32 | far) before tA, and over all tiles
+  for (unsigned q = threadIdx.x; q < nsup; q += IB_BS) {
+    const unsigned long long v = s.tsup[q];
+    tot += v;
+    if (q < tA / INC_SUP) pre += v;
+  }
+  for (unsigned t = (tA / INC_SUP) * INC_SUP + threadIdx.x; t < tA; t += IB_BS) {
+    const uint2 v = s.tagg[t];
+    pre += (static_cast<unsigned long long>(v.x) << 32) | v.y;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    pre += __shfl_xor(pre, off, 64);
+    tot += __shfl_xor(tot, off, 64);
+  }
+  if (lane == 0) {
+    s_red[0][w] = pre;
+    s_red[1][w] = tot;
+  }
+  // tile counts -> LDS (exclusive scan below, by wave 0)
+#pragma unroll
+  for (int m = 0; m < IB_TPCAP / IB_BS; m++) s_tp[threadIdx.x + m * IB_BS] = ta[m];
+  __syncthreads();
+  pre = 0;
+  tot = 0;
+#pragma unroll
+  for (int q = 0; q < NW; q++) {
+    pre += s_red[0][q];
+    tot += s_red[1][q];
+  }
+  const unsigned totn = unsigned(tot >> 32);
+  if (w == 0 && tplds) {  // exclusive scan of the window's tile counts, 16 tiles per lane
+    constexpr int PL = IB_TPCAP / 64;
+    uint2 v[PL];
+    unsigned sn = 0, sf = 0;
+#pragma unroll
+    for (int q = 0; q < PL; q++) {
+      v[q] = s_tp[lane * PL + q];
+      sn += v[q].x;
+      sf += v[q].y;
+    }
+    unsigned xn = sn, xf = sf;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned yn = __shfl_up(xn, off, 64), yf = __shfl_up(xf, off, 64);
+      if (lane >= unsigned(off)) {
+        xn += yn;
+        xf += yf;
+      }
+    }
+    unsigned rn = unsigned(pre >> 32) + xn - sn, rf = unsigned(pre) + xf - sf;
+#pragma unroll
+    for (int q = 0; q < PL; q++) {
+      s_tp[lane * PL + q] = make_uint2(rn, rf);
+      rn += v[q].x;
+      rf += v[q].y;
+    }
+  }
+  __syncthreads();
+  // movers before tile t: LDS for the window's tiles, else from the super/tile counts
+  auto tp_of = [&](unsigned t) -> uint2 {
+    if (tplds && t >= tA && t - tA < ntp) return s_tp[t - tA];
+    unsigned long long p = 0;
+    for (unsigned q = 0; q < t / INC_SUP; q++) p += s.tsup[q];
+    for (unsigned u = (t / INC_SUP) * INC_SUP; u < t; u++) {
+      const uint2 v = s.tagg[u];
+      p += (static_cast<unsigned long long>(v.x) << 32) | v.y;
+    }
+    return make_uint2(unsigned(p >> 32), unsigned(p));
+  };
+  auto lnlf = [&](unsigned x, unsigned cw) -> uint2 {  // (Ln(x), Lf(x))
+    if (x >= n) return make_uint2(totn, totf);
+    const uint2 p = tp_of(x / INC_TILE);
+    return make_uint2(p.x + (cw & CW_LOC), p.y + ((cw >> 11) & CW_LOC));
+  };
+  // the tile holding near mover j of the window (largest t with Ln(t * INC_TILE) <= j)
+  auto slot_of = [&](unsigned j) -> unsigned {
+    unsigned lo = tA, hi = tB;
+    while (lo < hi) {
+      const unsigned mid = (lo + hi + 1) >> 1;
+      if (tp_of(mid).x <= j) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo * INC_TILE + (j - tp_of(lo).x);
+  };
+#pragma unroll
+  for (int m = 0; m < IB_BPT; m++) {
+    const uint2 l = lnlf(xo[m], cwo[m]);
+    s_ln[int(threadIdx.x) + m * IB_BS] = l.x;
+    s_lf[int(threadIdx.x) + m * IB_BS] = l.y;
+  }
+  {
+    const uint2 l = lnlf(xo[IB_BPT], cwo[IB_BPT]);
+    if (threadIdx.x == 0) {
+      s_ln[IB_BOX] = l.x;
+      s_lf[IB_BOX] = l.y;
+    }
+    if (threadIdx.x == 1 || threadIdx.x == 2) s_jw[threadIdx.x - 1] = l.x;
+  }
+  // movers before each tile that starts in this block's index range, for k_inc_push
+  for (unsigned t = tA + threadIdx.x; t <= tB; t += IB_BS) {
+    const unsigned x = t * INC_TILE;
+    if (x >= s_obx[0] && x < s_obx[IB_BOX] && x < n) {
+      const uint2 p = tp_of(t);
+      s.tpg[t] = p.x + p.y;
+    }
+  }
+  __syncthreads();
   TSTAMP(1);
   const unsigned jlo = s_jw[0], jhi = s_jw[1];
   const unsigned cend = unsigned(min(c0 + IB_BOX, nctt));
+  auto ln_clamped = [&](unsigned x) -> unsigned {  // Ln(x) of a far mover, clamped to the window
+    if (x < xa) return jlo;
+    if (x >= xb) return jhi;
+    return lnlf(x, s.cw[x]).x;
+  };
   // ---- far movers (a short list; usually empty): below the block, or arrivals
   for (unsigned f = threadIdx.x; f < totf; f += IB_BS) {
     const uint2 e = s.mfar[f];
@@ -774,35 +824,31 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
       if (e.x < s_obx[lc]) atomicAdd(&s_fbef[lc], 1u);
       const unsigned k = atomicAdd(&s_nfar, 1u);
       if (k < unsigned(IB_FCAP)) {
-        s_far[k] = make_uint4(f, e.x, e.y, lnw(e.x));
+        s_far[k] = make_uint4(f, e.x, e.y, ln_clamped(e.x));
         s_fnb[k] = 0;
       }
     }
   }
   __syncthreads();
   const unsigned nfar = s_nfar;
-  const bool farlds = nfar <= unsigned(IB_FCAP);
-  // near arrivals of box c before a far arrival (rare): LDS counters, or counted from global
-  // memory below when the block has more far arrivals than IB_FCAP
-  auto far_near = [&](unsigned lc, unsigned j) {
-    if (!farlds) return;
-    for (unsigned k = 0; k < nfar; k++) {
-      const uint4 fe = s_far[k];
-      if (fe.z - unsigned(c0) == lc && j < fe.w) atomicAdd(&s_fnb[k], 1u);
-    }
-  };
+  const bool farlds = nfar <= unsigned(IB_FCAP) && !(s.dbg & 32);
   // ---- pass 1: near arrivals per box, and the window's near movers below the block
   {
     unsigned below = 0;
     for (unsigned base = jlo; base < jhi; base += IB_BS) {
       const unsigned j = base + threadIdx.x;
-      const unsigned key = j < jhi ? s.mkey[j] : ~0u;
-      below += __popcll(__ballot(key < unsigned(c0)));
+      const unsigned key = j < jhi ? s.mkey[slot_of(j)] : ~0u;
+      below += unsigned(__popcll(__ballot(key < unsigned(c0))));
       if (key >= unsigned(c0) && key < cend) {
         const unsigned lc = key - unsigned(c0);
         atomicAdd(&s_narr[lc], 1u);
         if (j < s_ln[lc]) atomicAdd(&s_nbef[lc], 1u);
-        if (s_farr[lc]) far_near(lc, j);
+        if (s_farr[lc] && farlds) {  // near arrivals ahead of a far arrival of the same box
+          for (unsigned k = 0; k < nfar; k++) {
+            const uint4 fe = s_far[k];
+            if (fe.z == key && j < fe.w) atomicAdd(&s_fnb[k], 1u);
+          }
+        }
       }
     }
     if (lane == 0 && below) atomicAdd(&s_below, below);
@@ -810,7 +856,7 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   __syncthreads();
   TSTAMP(2);
   // ---- per-box scan: begin, stayer offset, counts
-  const unsigned base0 = s_jw[0] + s_below + s_farbelow;
+  const unsigned base0 = jlo + s_below + s_farbelow;
   unsigned cnt[IB_BPT], xs[IB_BPT];
 #pragma unroll
   for (int h = 0; h < IB_BPT; h++) {
@@ -865,7 +911,8 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   const unsigned long long lt = (1ull << lane) - 1ull;
   for (unsigned base = jlo; base < jhi; base += IB_BS) {
     const unsigned j = base + threadIdx.x;
-    const unsigned key = j < jhi ? s.mkey[j] : ~0u;
+    const unsigned sl = j < jhi ? slot_of(j) : 0u;
+    const unsigned key = j < jhi ? s.mkey[sl] : ~0u;
     const bool valid = key >= unsigned(c0) && key < cend;
     if (__syncthreads_or(valid) == 0) continue;  // block-uniform
     const unsigned lc = valid ? key - unsigned(c0) : 0u;
@@ -891,12 +938,12 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
         } else {
           for (unsigned f = 0; f < totf; f++) {
             const uint2 e = s.mfar[f];
-            if (e.y == key && lnw(e.x) <= j) r++;
+            if (e.y == key && ln_clamped(e.x) <= j) r++;
           }
         }
       }
       const unsigned stay = (s_obx[lc + 1] - s_obx[lc]) - (s_ln[lc + 1] - s_ln[lc]) - (s_lf[lc + 1] - s_lf[lc]);
-      s.mposnear[j] = s_begin[lc] + r + (j >= s_ln[lc] ? stay : 0u);
+      s.mposnear[sl] = s_begin[lc] + r + (j >= s_ln[lc] ? stay : 0u);
     }
     __syncthreads();
     if (leader) {
@@ -918,8 +965,8 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
         if (e.y >= unsigned(c0) && e.y < cend && seen++ == k) break;
       }
       const uint2 e = s.mfar[f];
-      fe = make_uint4(f, e.x, e.y, lnw(e.x));
-      for (unsigned j = jlo; j < fe.w; j++) nb += (s.mkey[j] == fe.z) ? 1u : 0u;
+      fe = make_uint4(f, e.x, e.y, ln_clamped(e.x));
+      for (unsigned j = jlo; j < fe.w; j++) nb += (s.mkey[slot_of(j)] == fe.z) ? 1u : 0u;
     }
     const unsigned lc = fe.z - unsigned(c0);
     unsigned r = nb;
@@ -935,29 +982,37 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   TSPRINT("boxes", 6);
 }
 
-// Loads in three batches (one memory latency each): the particle states and the
-// classification words, the new positions, then the stores.
+// One tile per block.  Loads in three batches (one memory latency each): the particle
+// states and the classification words, the new positions, then the stores.  Block 0
+// also clears the super-tile sums and the far count for the next divide.
 template <bool WITHM1, bool WITHPRE>
 __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, GatherArgs a, IncDivScratch s) {
   const unsigned nd = sc->ndiv, n = sc->np, npb = sc->npb;
-  const unsigned i0 = blockIdx.x * (256 * GP) + threadIdx.x;
+  const unsigned t = blockIdx.x;
+  const unsigned i0 = t * INC_TILE + threadIdx.x;
   GatherRec<WITHM1, WITHPRE> q[GP];
-  unsigned key[GP], ln[GP], lf[GP], pos[GP];
+  unsigned key[GP], cw[GP], fx[GP], pos[GP];
+  const unsigned tpg = i0 < nd ? s.tpg[t] : 0u;
 #pragma unroll
   for (int k = 0; k < GP; k++) {
     const unsigned i = i0 + 256 * k;
     const unsigned ii = i < nd ? i : 0u;
     key[k] = s.newkey[ii];
-    ln[k] = s.ln[ii];
-    lf[k] = s.lf[ii];
+    cw[k] = s.cw[ii];
     q[k].load(a.src, ii);
   }
 #pragma unroll
   for (int k = 0; k < GP; k++) {
-    const bool near = (ln[k] >> 31) != 0, far = (lf[k] >> 31) != 0;
+    const bool near = (cw[k] & CW_NEAR) != 0, far = (cw[k] & CW_FAR) != 0;
+    fx[k] = far ? s.fidx[i0 + 256 * k] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < GP; k++) {
+    const bool near = (cw[k] & CW_NEAR) != 0, far = (cw[k] & CW_FAR) != 0;
+    const unsigned ln = cw[k] & CW_LOC, lf = (cw[k] >> 11) & CW_LOC;
     const unsigned* tab = near ? s.mposnear : (far ? s.mposfar : s.stayoff);
-    const unsigned x = tab[near ? (ln[k] & INC_M) : (far ? (lf[k] & INC_M) : key[k])];
-    pos[k] = (near || far) ? x : x + (i0 + 256 * k) - ln[k] - lf[k];
+    const unsigned x = tab[near ? t * INC_TILE + ln : (far ? fx[k] : key[k])];
+    pos[k] = (near || far) ? x : x + (i0 + 256 * k) - tpg - ln - lf;
   }
   float v2 = 0.f;
 #pragma unroll
@@ -970,6 +1025,11 @@ __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, G
     }
   }
   wave_max_atomic(sc, RED_VELMAX2, v2);
+  if (t == 0) {
+    const unsigned nsup = (s.nb1 + INC_SUP - 1) / INC_SUP;
+    for (unsigned u = threadIdx.x; u < nsup; u += 256) s.tsup[u] = 0ull;
+    if (threadIdx.x == 0) s.ctr[0] = 0u;
+  }
 }
 
 void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& src, const PartArrays& dst,
@@ -1002,7 +1062,7 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
   a.dcc = K.domcellcode;
   a.withm1 = withm1;
   a.withpre = withpre;
-  const unsigned nb = (cap + 256 * GP - 1) / (256 * GP);
+  const unsigned nb = s.nb1;  // one tile per block
   if (withm1 && withpre) hipLaunchKernelGGL((k_inc_push<true, true>), dim3(nb), dim3(256), 0, stm, sc, a, s);
   else if (withm1) hipLaunchKernelGGL((k_inc_push<true, false>), dim3(nb), dim3(256), 0, stm, sc, a, s);
   else if (withpre) hipLaunchKernelGGL((k_inc_push<false, true>), dim3(nb), dim3(256), 0, stm, sc, a, s);

@@ -114,22 +114,25 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
 struct IncDivScratch {
   unsigned* skeys = nullptr;      // [cap] box key of the particle at each index (last divide)
   unsigned* newkey = nullptr;     // [cap] box key of this divide
-  unsigned* ln = nullptr;         // [cap] near movers before i | bit 31: i is a near mover
-  unsigned* lf = nullptr;         // [cap] far movers before i | bit 31: i is a far mover
-  unsigned* mkey = nullptr;       // [cap] new keys of the near movers (previous-index order)
-  uint2* mfar = nullptr;          // [cap] (previous index, new key) of the far movers
-  unsigned* mposnear = nullptr;   // [cap] new positions of the movers
-  unsigned* mposfar = nullptr;    // [cap]
-  unsigned* stayoff = nullptr;    // [nctt] new index of a stayer = stayoff[key] + i - ln - lf
-  unsigned long long* stat1 = nullptr;  // look-back status per classify block [nb1]
-  unsigned long long* stat2 = nullptr;  // per box block [nb2]
-  unsigned* ctr = nullptr;        // tickets of the two scans (own 128-B lines) + mover totals
+  unsigned* cw = nullptr;         // [cap] tile-local near / far prefixes (11 bits each) | near, far flags
+  unsigned* fidx = nullptr;       // [cap] far-list index of a far mover
+  uint2* tagg = nullptr;          // [tiles] (near, far) movers of each tile
+  unsigned long long* tsup = nullptr;  // [tiles / 64] (near << 32 | far) per super tile, cleared by k_inc_push
+  unsigned* tpg = nullptr;        // [tiles] movers before each tile (k_inc_boxes -> k_inc_push)
+  unsigned* mkey = nullptr;       // [cap] new keys of the near movers, at tile * INC_TILE + local rank
+  uint2* mfar = nullptr;          // [cap] (previous index, new key) of the far movers (appended)
+  unsigned* mposnear = nullptr;   // [cap] new positions of the near movers (same slots as mkey)
+  unsigned* mposfar = nullptr;    // [cap] new positions of the far movers
+  unsigned* stayoff = nullptr;    // [nctt] new index of a stayer = stayoff[key] + i - movers before i
+  unsigned* ctr = nullptr;        // [0]: far movers (cleared by k_inc_push)
   unsigned nb1 = 0, nb2 = 0, gen = 0;
-  int dbg = 0;  // SPH_INC_DBG ablations (timing only): 1 no classify look-back, 2 no box look-back, 4 no box count loops
+  // SPH_INC_DBG: 8 phase timestamps of the divide kernels (printf); 16 / 32 force the
+  // global-memory paths of the tile prefixes / far arrivals (tests)
+  int dbg = 0;
 };
+constexpr unsigned INC_TILE_SIZE = 1024;  // particles per classify tile (sph_divide.hip INC_TILE)
 unsigned inc_blocks_classify(unsigned cap);
 unsigned inc_blocks_boxes(unsigned nctt);
-// ctr: [0] / [QSTRIDE] tickets, [2 QSTRIDE] near total, [2 QSTRIDE + 1] far total
 void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& src, const PartArrays& dst,
                        bool withm1, bool withpre, const KConst& K, const double dom_posmin[3], float4* poscell,
                        float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,

@@ -420,10 +420,8 @@ void SphGpuSingle::AllocFixed() {
     inc_.stayoff = (unsigned*)dmalloc(4 * (2 * size_t(nctmax_) + 6));
     inc_.nb2 = inc_blocks_boxes(G.nctt);
     if (const char* e = std::getenv("SPH_INC_DBG")) inc_.dbg = std::atoi(e);
-    inc_.stat2 = (unsigned long long*)dmalloc(8 * size_t(inc_.nb2));
-    check_hip(hipMemset(inc_.stat2, 0, 8 * size_t(inc_.nb2)), "zero scan status");
-    inc_.ctr = (unsigned*)dmalloc(4 * 3 * QSTRIDE);
-    check_hip(hipMemset(inc_.ctr, 0, 4 * 3 * QSTRIDE), "zero scan tickets");
+    inc_.ctr = (unsigned*)dmalloc(4 * QSTRIDE);
+    check_hip(hipMemset(inc_.ctr, 0, 4 * QSTRIDE), "zero far count");
   }
   sc_ = (DevScalars*)dmalloc(sizeof(DevScalars));
   dttrace_ = (double*)dmalloc(8 * size_t(tracecap_));
@@ -492,17 +490,21 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
     sort_.vals[i] = (unsigned*)dmalloc(4 * n);
   }
   if (inc_ok_) {
+    inc_.nb1 = inc_blocks_classify(n);
+    const size_t ns = size_t(inc_.nb1) * INC_TILE_SIZE;  // tile-major mover slots
     inc_.skeys = (unsigned*)dmalloc(4 * n);
     inc_.newkey = (unsigned*)dmalloc(4 * n);
-    inc_.ln = (unsigned*)dmalloc(4 * n);
-    inc_.lf = (unsigned*)dmalloc(4 * n);
-    inc_.mkey = (unsigned*)dmalloc(4 * n);
+    inc_.cw = (unsigned*)dmalloc(4 * n);
+    inc_.fidx = (unsigned*)dmalloc(4 * n);
+    inc_.mkey = (unsigned*)dmalloc(4 * ns);
+    inc_.mposnear = (unsigned*)dmalloc(4 * ns);
     inc_.mfar = (uint2*)dmalloc(8 * n);
-    inc_.mposnear = (unsigned*)dmalloc(4 * n);
     inc_.mposfar = (unsigned*)dmalloc(4 * n);
-    inc_.nb1 = inc_blocks_classify(n);
-    inc_.stat1 = (unsigned long long*)dmalloc(8 * size_t(inc_.nb1));
-    check_hip(hipMemset(inc_.stat1, 0, 8 * size_t(inc_.nb1)), "zero scan status");
+    inc_.tagg = (uint2*)dmalloc(8 * size_t(inc_.nb1));
+    inc_.tpg = (unsigned*)dmalloc(4 * size_t(inc_.nb1));
+    const size_t nsup = (size_t(inc_.nb1) + 63) / 64;
+    inc_.tsup = (unsigned long long*)dmalloc(8 * nsup);
+    check_hip(hipMemset(inc_.tsup, 0, 8 * nsup), "zero super tiles");
   }
   sort_.ntiles = unsigned((n + RS_TILE - 1) / RS_TILE);
   sort_.hist = (unsigned*)dmalloc(4 * size_t(sort_.ntiles) * (1u << RS_MAXBITS));

@@ -21,20 +21,23 @@ from dualsphysics_multilayer_amd.case import DamBreak2DCase, DamBreakCase, WaveF
 pytestmark = pytest.mark.gpu
 
 
-def _solver(case, mode, monkeypatch):
+def _solver(case, mode, monkeypatch, dbg=0):
     from dualsphysics_multilayer_amd.core import SphGpuSingle
 
     if mode == "full":
         monkeypatch.setenv("SPH_DIVIDE", "full")
     else:
         monkeypatch.delenv("SPH_DIVIDE", raising=False)
+    if dbg:
+        monkeypatch.setenv("SPH_INC_DBG", str(dbg))
     s = SphGpuSingle(case, device=0)
     monkeypatch.delenv("SPH_DIVIDE", raising=False)
+    monkeypatch.delenv("SPH_INC_DBG", raising=False)
     return s
 
 
-def _same(case, nsteps, chunk, monkeypatch):
-    a = _solver(case, "inc", monkeypatch)
+def _same(case, nsteps, chunk, monkeypatch, dbg=0):
+    a = _solver(case, "inc", monkeypatch, dbg)
     b = _solver(case, "full", monkeypatch)
     done = 0
     while done < nsteps:
@@ -63,9 +66,10 @@ def _stirred(case, frac, speed, seed=3):
     return c
 
 
-def test_inc_divide_verlet_stirred(monkeypatch):
+@pytest.mark.parametrize("dbg", [0, 48])
+def test_inc_divide_verlet_stirred(monkeypatch, dbg):
     case = _stirred(DamBreakCase(0.02, celldomfixed=True), 0.5, 3.0)
-    _same(case, 60, 5, monkeypatch)
+    _same(case, 60, 5, monkeypatch, dbg)
 
 
 def test_inc_divide_symplectic_ddt1(monkeypatch):
@@ -73,17 +77,21 @@ def test_inc_divide_symplectic_ddt1(monkeypatch):
     _same(case, 40, 4, monkeypatch)
 
 
-def test_inc_divide_exclusions(monkeypatch):
-    """Far movers: OUTMOVE / OUTPOS / OUTRHOP exclusions go to the out boxes (and leave np)."""
+@pytest.mark.parametrize("nfast,dbg", [(40, 0), (40, 48), (900, 0)])
+def test_inc_divide_exclusions(monkeypatch, nfast, dbg):
+    """Far movers: OUTMOVE / OUTPOS / OUTRHOP exclusions go to the out boxes (and leave np).
+    900 at once exceed the far arrivals a block keeps in LDS (IB_FCAP); dbg 48 forces the
+    global-memory paths of the tile prefixes and far arrivals."""
     case = DamBreakCase(0.03, celldomfixed=True, rhopoutmax=1010.0)
     rng = np.random.default_rng(7)
-    pick = rng.choice(np.arange(case.npb, case.np), 40, replace=False)
-    case.vel[pick[:10]] = [0, 0, 400.0]
-    case.vel[pick[10:20]] = [0, 0, -30.0]
-    case.vel[pick[20:30]] = [-120.0, 0, 0]
-    case.vel[pick[30:]] = [0, 25.0, 0]
-    st = _same(case, 30, 1, monkeypatch)
-    assert st["nout"] >= 10
+    pick = rng.choice(np.arange(case.npb, case.np), nfast, replace=False)
+    q = nfast // 4
+    case.vel[pick[:q]] = [0, 0, 400.0]
+    case.vel[pick[q:2 * q]] = [0, 0, -30.0]
+    case.vel[pick[2 * q:3 * q]] = [-120.0, 0, 0]
+    case.vel[pick[3 * q:]] = [0, 25.0, 0]
+    st = _same(case, 30, 1, monkeypatch, dbg)
+    assert st["nout"] >= q
 
 
 def test_inc_divide_half_cells(monkeypatch):
