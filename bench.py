@@ -212,6 +212,9 @@ def main() -> None:
                          "(host-staged shared memory: ranks of one node without RCCL)")
     ap.add_argument("--ranks-per-gpu", type=int, default=1,
                     help="ranks sharing one GPU (device = LOCAL_RANK // this; needs --transport shm)")
+    ap.add_argument("--presteps", type=int, default=0,
+                    help="untimed steps before the warmup: time a developed flow (movers across cells, "
+                         "the incremental divide's real load) instead of the first steps from rest")
     ap.add_argument("--force-slab", action="store_true",
                     help="run the N>1 code path (gloo bootstrap + RCCL slab) even with one rank")
     args = ap.parse_args()
@@ -275,7 +278,7 @@ def main() -> None:
                            slot_bytes=256 << 20)
             if args.repartition and world > 1:
                 s.set_repartition(args.repartition, args.bound_weight, 0.05)
-            s.run(args.warmup)
+            s.run(args.presteps + args.warmup)
             s.sync()
             ok = torch.tensor([1], dtype=torch.int32)
         except Exception as e:  # noqa: BLE001
@@ -287,7 +290,7 @@ def main() -> None:
             raise SystemExit(3)
     else:
         s = SphGpuSingle(case, device=device)
-        s.run(args.warmup)
+        s.run(args.presteps + args.warmup)
         s.sync()
     wall["setup_and_warmup_s"] = time.perf_counter() - t_setup
     pairs0 = s.count_pairs()
@@ -379,6 +382,7 @@ def main() -> None:
                               "Laminar viscosity with the HBP effective viscosity, DDT Fourtakas full 0.1, shifting "
                               "Full (-10, TFS 2.75), CFL 0.1, RelaxationDt 0.2" % (case.np, dp, CFG5_WIDTH))),
                 "np": case.np,
+                "presteps": args.presteps,
                 "npb": case.npb,
                 "parallelism": (("slab-x%d (%s halo + migration, max-allreduce dt%s)"
                                  % (world, "RCCL" if args.transport == "rccl" else "shared-memory",

@@ -630,6 +630,8 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
 // over the window: counts, then (after the per-box scan) ranks -> positions.
 constexpr int IB_FCAP = 256;  // far arrivals of a block held in LDS (more: read from global memory)
 constexpr int IB_TPCAP = 1024;  // window tiles with LDS prefixes (more: computed from global memory)
+constexpr int IB_WCAP = 4096;   // window near movers staged in LDS (more: read from global memory)
+constexpr int IB_ACAP = 1024;   // near arrivals ranked through LDS buckets (more: chunked wave-match pass)
 __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc, DivGrid g,
                                                      const unsigned* __restrict__ ob, unsigned* __restrict__ nbc,
                                                      IncDivScratch s, unsigned omax) {
@@ -644,6 +646,12 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   __shared__ unsigned s_wsum[IB_BPT][NW];
   __shared__ unsigned long long s_red[2][NW];
   __shared__ unsigned s_xw[2], s_jw[2], s_below, s_farbelow, s_nfar;
+  __shared__ unsigned s_wkey[IB_WCAP];  // the window's near-mover keys (when they fit)
+  __shared__ uint2 s_arr[IB_ACAP];      // near arrivals (list index, box offset), unordered
+  __shared__ unsigned s_bkt[IB_ACAP];   // their list indices bucketed by box
+  __shared__ unsigned s_boff[IB_BOX];   // bucket offsets (exclusive scan of s_narr)
+  __shared__ unsigned s_nwsum[IB_BPT][IB_BS / 64];
+  __shared__ unsigned s_nar;
   const unsigned b = blockIdx.x;
   TSDECL;
   TSTAMP(0);
@@ -679,6 +687,7 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
     s_below = 0;
     s_farbelow = 0;
     s_nfar = 0;
+    s_nar = 0;
   }
   __syncthreads();
   // ---- 2. the window's tiles [tA, tB]: their counts, the movers before tA, the totals;
@@ -832,17 +841,39 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   __syncthreads();
   const unsigned nfar = s_nfar;
   const bool farlds = nfar <= unsigned(IB_FCAP) && !(s.dbg & 32);
+  // the window's keys into LDS: all loads of a round issued before the stores (one latency)
+  const bool wlds = jhi - jlo <= unsigned(IB_WCAP) && !(s.dbg & 16);
+  if (wlds) {
+    constexpr int WR = 8;
+    for (unsigned r0 = 0; r0 < jhi - jlo; r0 += WR * IB_BS) {
+      unsigned kk[WR];
+#pragma unroll
+      for (int m = 0; m < WR; m++) {
+        const unsigned e = r0 + threadIdx.x + m * IB_BS;
+        kk[m] = e < jhi - jlo ? s.mkey[slot_of(jlo + e)] : 0u;
+      }
+#pragma unroll
+      for (int m = 0; m < WR; m++) {
+        const unsigned e = r0 + threadIdx.x + m * IB_BS;
+        if (e < jhi - jlo) s_wkey[e] = kk[m];
+      }
+    }
+    __syncthreads();
+  }
+  auto wkey = [&](unsigned j) -> unsigned { return wlds ? s_wkey[j - jlo] : s.mkey[slot_of(j)]; };
   // ---- pass 1: near arrivals per box, and the window's near movers below the block
   {
     unsigned below = 0;
     for (unsigned base = jlo; base < jhi; base += IB_BS) {
       const unsigned j = base + threadIdx.x;
-      const unsigned key = j < jhi ? s.mkey[slot_of(j)] : ~0u;
+      const unsigned key = j < jhi ? wkey(j) : ~0u;
       below += unsigned(__popcll(__ballot(key < unsigned(c0))));
       if (key >= unsigned(c0) && key < cend) {
         const unsigned lc = key - unsigned(c0);
         atomicAdd(&s_narr[lc], 1u);
         if (j < s_ln[lc]) atomicAdd(&s_nbef[lc], 1u);
+        const unsigned a = atomicAdd(&s_nar, 1u);
+        if (a < unsigned(IB_ACAP)) s_arr[a] = make_uint2(j, lc);
         if (s_farr[lc] && farlds) {  // near arrivals ahead of a far arrival of the same box
           for (unsigned k = 0; k < nfar; k++) {
             const uint4 fe = s_far[k];
@@ -857,31 +888,43 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   TSTAMP(2);
   // ---- per-box scan: begin, stayer offset, counts
   const unsigned base0 = jlo + s_below + s_farbelow;
-  unsigned cnt[IB_BPT], xs[IB_BPT];
+  unsigned cnt[IB_BPT], xs[IB_BPT], xsn[IB_BPT];
 #pragma unroll
   for (int h = 0; h < IB_BPT; h++) {
     const int k = h * IB_BS + int(threadIdx.x);
     cnt[h] = s_narr[k] + s_farr[k];
-    unsigned x = cnt[h];
+    unsigned x = cnt[h], xn = s_narr[k];
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-      const unsigned y = __shfl_up(x, off, 64);
-      if (lane >= unsigned(off)) x += y;
+      const unsigned y = __shfl_up(x, off, 64), yn = __shfl_up(xn, off, 64);
+      if (lane >= unsigned(off)) {
+        x += y;
+        xn += yn;
+      }
     }
     xs[h] = x;
-    if (lane == 63) s_wsum[h][w] = x;
+    xsn[h] = xn;
+    if (lane == 63) {
+      s_wsum[h][w] = x;
+      s_nwsum[h][w] = xn;
+    }
   }
   __syncthreads();
-  unsigned hpre = 0;
+  unsigned hpre = 0, hpren = 0;
 #pragma unroll
   for (int h = 0; h < IB_BPT; h++) {
-    unsigned wpre = 0, hsum = 0;
+    unsigned wpre = 0, hsum = 0, wpren = 0, hsumn = 0;
 #pragma unroll
     for (int q = 0; q < NW; q++) {
       wpre += unsigned(q) < w ? s_wsum[h][q] : 0u;
       hsum += s_wsum[h][q];
+      wpren += unsigned(q) < w ? s_nwsum[h][q] : 0u;
+      hsumn += s_nwsum[h][q];
     }
     const int k = h * IB_BS + int(threadIdx.x);
+    s_boff[k] = hpren + wpren + xsn[h] - s_narr[k];
+    s_run[k] = 0;  // bucket fill counters
+    hpren += hsumn;
     const unsigned S = s_obx[k] - s_ln[k] - s_lf[k];
     const unsigned stay = (s_obx[k + 1] - s_obx[k]) - (s_ln[k + 1] - s_ln[k]) - (s_lf[k + 1] - s_lf[k]);
     const unsigned begin = S + base0 + hpre + wpre + xs[h] - cnt[h];
@@ -907,12 +950,45 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   }
   __syncthreads();
   TSTAMP(3);
-  // ---- pass 2: stable rank of every near arrival in its box -> its new position
+  // ---- pass 2: stable rank of every near arrival in its box -> its new position.
+  // Usually through LDS buckets (arrivals of one box, any order; rank = arrivals of the box
+  // with a smaller list index), else one wave-matched chunk of the window at a time.
+  const unsigned nar = s_nar;
+  const bool bucketed = nar <= unsigned(IB_ACAP) && !(s.dbg & 64);
+  auto near_pos = [&](unsigned j, unsigned lc, unsigned r) -> unsigned {
+    const unsigned key = unsigned(c0) + lc;
+    if (s_farr[lc]) {  // far arrivals of this box ahead of it (previous index below this mover's)
+      if (farlds) {
+        for (unsigned k = 0; k < nfar; k++)
+          if (s_far[k].z == key && s_far[k].w <= j) r++;
+      } else {
+        for (unsigned f = 0; f < totf; f++) {
+          const uint2 e = s.mfar[f];
+          if (e.y == key && ln_clamped(e.x) <= j) r++;
+        }
+      }
+    }
+    const unsigned stay = (s_obx[lc + 1] - s_obx[lc]) - (s_ln[lc + 1] - s_ln[lc]) - (s_lf[lc + 1] - s_lf[lc]);
+    return s_begin[lc] + r + (j >= s_ln[lc] ? stay : 0u);
+  };
+  if (bucketed) {
+    for (unsigned a = threadIdx.x; a < nar; a += IB_BS) {
+      const uint2 e = s_arr[a];
+      s_bkt[s_boff[e.y] + atomicAdd(&s_run[e.y], 1u)] = e.x;
+    }
+    __syncthreads();
+    for (unsigned a = threadIdx.x; a < nar; a += IB_BS) {
+      const uint2 e = s_arr[a];
+      const unsigned b0 = s_boff[e.y], b1 = b0 + s_narr[e.y];
+      unsigned r = 0;
+      for (unsigned q = b0; q < b1; q++) r += s_bkt[q] < e.x ? 1u : 0u;
+      s.mposnear[slot_of(e.x)] = near_pos(e.x, e.y, r);
+    }
+  }
   const unsigned long long lt = (1ull << lane) - 1ull;
-  for (unsigned base = jlo; base < jhi; base += IB_BS) {
+  for (unsigned base = jlo; base < (bucketed ? jlo : jhi); base += IB_BS) {
     const unsigned j = base + threadIdx.x;
-    const unsigned sl = j < jhi ? slot_of(j) : 0u;
-    const unsigned key = j < jhi ? s.mkey[sl] : ~0u;
+    const unsigned key = j < jhi ? wkey(j) : ~0u;
     const bool valid = key >= unsigned(c0) && key < cend;
     if (__syncthreads_or(valid) == 0) continue;  // block-uniform
     const unsigned lc = valid ? key - unsigned(c0) : 0u;
@@ -930,20 +1006,7 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
     if (valid) {
       unsigned r = s_run[lc] + rank;
       for (unsigned q = 0; q < w; q++) r += s_wc[q][lc];
-      // far arrivals of this box ahead of it (previous index below this mover's)
-      if (s_farr[lc]) {
-        if (farlds) {
-          for (unsigned k = 0; k < nfar; k++)
-            if (s_far[k].z == key && s_far[k].w <= j) r++;
-        } else {
-          for (unsigned f = 0; f < totf; f++) {
-            const uint2 e = s.mfar[f];
-            if (e.y == key && ln_clamped(e.x) <= j) r++;
-          }
-        }
-      }
-      const unsigned stay = (s_obx[lc + 1] - s_obx[lc]) - (s_ln[lc + 1] - s_ln[lc]) - (s_lf[lc + 1] - s_lf[lc]);
-      s.mposnear[sl] = s_begin[lc] + r + (j >= s_ln[lc] ? stay : 0u);
+      s.mposnear[slot_of(j)] = near_pos(j, lc, r);
     }
     __syncthreads();
     if (leader) {
@@ -966,7 +1029,7 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
       }
       const uint2 e = s.mfar[f];
       fe = make_uint4(f, e.x, e.y, ln_clamped(e.x));
-      for (unsigned j = jlo; j < fe.w; j++) nb += (s.mkey[slot_of(j)] == fe.z) ? 1u : 0u;
+      for (unsigned j = jlo; j < fe.w; j++) nb += (wkey(j) == fe.z) ? 1u : 0u;
     }
     const unsigned lc = fe.z - unsigned(c0);
     unsigned r = nb;

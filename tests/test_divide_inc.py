@@ -66,7 +66,7 @@ def _stirred(case, frac, speed, seed=3):
     return c
 
 
-@pytest.mark.parametrize("dbg", [0, 48])
+@pytest.mark.parametrize("dbg", [0, 48, 64, 112])
 def test_inc_divide_verlet_stirred(monkeypatch, dbg):
     case = _stirred(DamBreakCase(0.02, celldomfixed=True), 0.5, 3.0)
     _same(case, 60, 5, monkeypatch, dbg)
@@ -77,11 +77,11 @@ def test_inc_divide_symplectic_ddt1(monkeypatch):
     _same(case, 40, 4, monkeypatch)
 
 
-@pytest.mark.parametrize("nfast,dbg", [(40, 0), (40, 48), (900, 0)])
+@pytest.mark.parametrize("nfast,dbg", [(40, 0), (40, 48), (40, 64), (900, 0)])
 def test_inc_divide_exclusions(monkeypatch, nfast, dbg):
     """Far movers: OUTMOVE / OUTPOS / OUTRHOP exclusions go to the out boxes (and leave np).
     900 at once exceed the far arrivals a block keeps in LDS (IB_FCAP); dbg 48 forces the
-    global-memory paths of the tile prefixes and far arrivals."""
+    global-memory paths of the tile prefixes and far arrivals, 64 the chunked ranking pass."""
     case = DamBreakCase(0.03, celldomfixed=True, rhopoutmax=1010.0)
     rng = np.random.default_rng(7)
     pick = rng.choice(np.arange(case.npb, case.np), nfast, replace=False)
