@@ -23,6 +23,14 @@
 
 namespace sphx {
 
+// Staged records per row segment: 48 B each (position, velrhop, {press, tag, 1/rho}); the
+// NN drain stages one row (3 cells) at a time, so 412 records keep <= 20480 B of LDS per block
+// (8 blocks = 4 waves per SIMD) and a row rarely needs a second segment.
+#ifndef SPH_NN_TCAP
+#define SPH_NN_TCAP 412
+#endif
+constexpr int NN_TCAP = SPH_NN_TCAP;
+
 // Phase table in LDS: two float4 per phase.
 //   a = {mass, cs0, visco, tau_yield}, b = {m (HBP_m), n (HBP_n), tau_max, bi_multi}
 struct NNAcc {
@@ -35,6 +43,9 @@ struct NNP1 {
   float4 vr;       // velocity, rho
   float press;
   int ph;          // phase of p1
+  float inv_rho;   // 1/rho1
+  float mph;       // mass of p1's phase (the heavier-phase test of the shifting)
+  float taumax, bimulti;  // bi-viscosity constants of p1's phase
 };
 
 // GetEta_Effective (JSphCpu_Tensors.cpp:84-108): Herschel-Bulkley-Papanastasiou effective
@@ -43,7 +54,8 @@ __device__ __forceinline__ float nn_eta(float dmag, float tau_yield, float visco
                                         float bimulti1) {
   if (dmag <= ALMOSTZERO) dmag = ALMOSTZERO;
   float miou_yield = (taumax1 != 0.f ? taumax1 : tau_yield) * frcp(2.f * dmag);
-  const bool bi_region = taumax1 != 0.f && dmag <= taumax1 * frcp(2.f * bimulti1 * visco);
+  // dmag <= taumax1 / (2 bimulti1 visco), without a second reciprocal (all factors > 0)
+  const bool bi_region = taumax1 != 0.f && dmag * (2.f * bimulti1 * visco) <= taumax1;
   if (bi_region) miou_yield = bimulti1 * visco;
   const float miou_pap = miou_yield * (1.f - fexp2(-m * dmag * 1.4426950408889634f));  // exp(-m D)
   const bool cap = (miou_pap > m * tau_yield || dmag == ALMOSTZERO);
@@ -55,22 +67,27 @@ __device__ __forceinline__ float nn_eta(float dmag, float tau_yield, float visco
 
 // One pair of the fluid p1 (InteractionForcesFluid_NN_FDA_All, JSphCpu_NN_FDA.cpp:141-275).
 // BOUNDP2: p2 is a boundary particle (mass MassBound, phase = p1's phase).
+// `ok`: the reference's pair test (rr2 <= KernelSize2 and rr2 >= ALMOSTZERO).  A pair that
+// fails it comes in with dr = 0 and rr2 = 1e30: its kernel factor is 0, so every sum gets
+// +0, and the maxima, the DDT/shifting switches and the shifting reset are masked by ok —
+// branch-free, so two pairs can be interleaved.
 template <int TVISCO, int TDENSITY, bool SHIFT, bool BOUNDP2>
 __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restrict__ sph, const NNP1& p, float drx,
-                                        float dry, float drz, float rr2, const float4& B, const float2& C, NNAcc& a) {
-  // kernel (Wendland fac = bwen q (1-q/2)^3 / r = (bwen/h) (1-q/2)^3)
+                                        float dry, float drz, float rr2, bool ok, const float4& B, const float4& C,
+                                        NNAcc& a) {
+  // kernel (Wendland fac = bwen q (1-q/2)^3 / r = (bwen/h) (1-q/2)^3), 0 beyond 2h
   const float rad = fsqrt_(rr2);
-  const float wq = fmaf(K.mhalfovh, rad, 1.f);
+  const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
   const float fac = K.bwenovh * (wq * wq * wq);
   const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
   const int pp2 = BOUNDP2 ? p.ph : int(__float_as_uint(C.y));
   const float4 ph2 = sph[2 * pp2];
   const float massp2 = BOUNDP2 ? K.massbound : ph2.x;
   const float rho1 = p.vr.w, rho2 = B.w;
-  const float inv_rho2 = frcp(rho2);
+  const float inv_rho2 = C.z;  // staged 1/rho2
   // momentum (pressure)
   {
-    const float prs = (p.press + C.x) * frcp(rho1 * rho2);
+    const float prs = (p.press + C.x) * (p.inv_rho * inv_rho2);
     const float p_vpm = -prs * massp2;
     a.ax = fmaf(p_vpm, frx, a.ax);
     a.ay = fmaf(p_vpm, fry, a.ay);
@@ -87,20 +104,20 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   if (TDENSITY == 1 && a.delta != FLT_MAX) {
     const float visc_densi = K.ddtkh * cbar * (rhop1over2 - 1.f) * inv_re;
     const float delta = (p.ph == pp2 ? visc_densi * dot3 * massp2 : 0.f);
-    a.delta = (BOUNDP2 && !K.mdbc) ? FLT_MAX : a.delta + delta;
+    a.delta = (BOUNDP2 && !K.mdbc && ok) ? FLT_MAX : a.delta + delta;
   }
   if ((TDENSITY == 2 || (TDENSITY == 3 && !BOUNDP2)) && a.delta != FLT_MAX) {
     const float rh = 1.f + K.ddtgz * drz;
     const float drhop = K.rhopzero * fexp2(K.ovgamma * flog2(rh)) - K.rhopzero;
     const float visc_densi = K.ddtkh * cbar * ((rho2 - rho1) - drhop) * inv_re;
     const float delta = (p.ph == pp2 ? visc_densi * dot3 * massp2 * inv_rho2 : 0.f);
-    a.delta = BOUNDP2 ? FLT_MAX : a.delta - delta;
+    a.delta = (BOUNDP2 && ok) ? FLT_MAX : a.delta - delta;
   }
   // multiphase shifting (JSphCpu_NN_FDA.cpp:202-209): a heavier-phase neighbour resets x
   if (SHIFT && a.sx != FLT_MAX) {
-    const bool heavy = !BOUNDP2 && (sph[2 * p.ph].x > ph2.x) && p.ph != pp2;
+    const bool heavy = ok && !BOUNDP2 && (p.mph > ph2.x) && p.ph != pp2;
     const float massrhop = massp2 * inv_rho2;
-    const bool noshift = BOUNDP2 && (K.shiftmode == 1 || (K.shiftmode == 2 && C.y != 0.f));
+    const bool noshift = ok && BOUNDP2 && (K.shiftmode == 1 || (K.shiftmode == 2 && C.y != 0.f));
     a.sx = noshift ? FLT_MAX : (heavy ? 0.f : a.sx + massrhop * frx);
     a.sy += heavy ? 0.f : massrhop * fry;
     a.sz += heavy ? 0.f : massrhop * frz;
@@ -109,7 +126,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   // viscosity
   const float dot = drx * dvx + dry * dvy + drz * dvz;
   const float dot_rr2 = dot * inv_re;
-  a.visc = fmaxf(dot_rr2, a.visc);
+  a.visc = fmaxf(ok ? dot_rr2 : 0.f, a.visc);
   const float visco_nn = ph2.z;
   if (TVISCO == 1) {  // artificial
     if (dot < 0.f) {
@@ -139,11 +156,10 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     const float ii_d = ii1 - ii2;
     const float dmag = fabsf(ii_d);  // sqrt(II_D * II_D)
     const float4 ph2b = sph[2 * pp2 + 1];
-    const float4 ph1b = sph[2 * p.ph + 1];
-    const float eta = nn_eta(dmag, ph2.w, visco_nn, ph2b.x, ph2b.y, ph1b.z, ph1b.w);
-    a.visceta = fmaxf(eta, a.visceta);
+    const float eta = nn_eta(dmag, ph2.w, visco_nn, ph2b.x, ph2b.y, p.taumax, p.bimulti);
+    a.visceta = fmaxf(ok ? eta : 0.f, a.visceta);
     if (TVISCO == 2) {  // Morris operator
-      const float temp = 2.f * eta * frcp((rr2 + K.eta2) * rho2);
+      const float temp = 2.f * eta * (inv_re * inv_rho2);
       const float vtemp = massp2 * temp * dot3;
       a.ax = fmaf(vtemp, dvx, a.ax);
       a.ay = fmaf(vtemp, dvy, a.ay);
@@ -161,15 +177,15 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
 // Boundary p1 over fluid p2 (InteractionForcesBound_NN_FDA, JSphCpu_NN_FDA.cpp:48-113):
 // continuity with MassFluid and the visc-dt maximum.
 __device__ __forceinline__ void nn_bound_pair(const KConst& K, const NNP1& p, float drx, float dry, float drz,
-                                              float rr2, const float4& B, NNAcc& a) {
+                                              float rr2, bool ok, const float4& B, const float4& C, NNAcc& a) {
   const float rad = fsqrt_(rr2);
-  const float wq = fmaf(K.mhalfovh, rad, 1.f);
+  const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
   const float fac = K.bwenovh * (wq * wq * wq);
   const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
   const float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
-  a.ar = fmaf(K.massfluid * (dvx * frx + dvy * fry + dvz * frz), p.vr.w * frcp(B.w), a.ar);
+  a.ar = fmaf(K.massfluid * (dvx * frx + dvy * fry + dvz * frz), p.vr.w * C.z, a.ar);
   const float dot = drx * dvx + dry * dvy + drz * dvz;
-  a.visc = fmaxf(dot * frcp(rr2 + K.eta2), a.visc);
+  a.visc = fmaxf(ok ? dot * frcp(rr2 + K.eta2) : 0.f, a.visc);
 }
 
 // Staging of one row segment: positions relative to the item (sA + |A|^2), velrhop (sB),
@@ -178,7 +194,7 @@ __device__ __forceinline__ void nn_stage(const KConst& K, unsigned rs, unsigned 
                                          bool boundrow, const float4* __restrict__ poscell,
                                          const float4* __restrict__ velrhop, const float* __restrict__ press,
                                          const typecode* __restrict__ code, float4* __restrict__ sA,
-                                         float4* __restrict__ sB, float2* __restrict__ sC) {
+                                         float4* __restrict__ sB, float4* __restrict__ sC) {
   const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
   for (unsigned i = threadIdx.x; i < n; i += TB) {
     const float4 pc = poscell[rs + i];
@@ -186,10 +202,11 @@ __device__ __forceinline__ void nn_stage(const KConst& K, unsigned rs, unsigned 
     const float x2 = pc.x + float(cx2 - xo) * K.scell;
     const float y2 = pc.y + oy, z2 = pc.z + oz;
     sA[i] = make_float4(x2, y2, z2, x2 * x2 + y2 * y2 + z2 * z2);
-    sB[i] = velrhop[rs + i];
+    const float4 vr = velrhop[rs + i];
+    sB[i] = vr;
     const typecode c = code[rs + i];
     const unsigned tag = boundrow ? (CodeType(c) == 0 ? 1u : 0u) : unsigned(c & CODE_MASKVALUE);
-    sC[i] = make_float2(press[rs + i], boundrow ? float(tag) : __uint_as_float(tag));
+    sC[i] = make_float4(press[rs + i], boundrow ? float(tag) : __uint_as_float(tag), frcp(vr.w), 0.f);
   }
 }
 
@@ -200,7 +217,7 @@ __device__ __forceinline__ void nn_pass(const KConst& K, const DivGrid& g, const
                                         const unsigned* __restrict__ bc, const float4* __restrict__ poscell,
                                         const float4* __restrict__ velrhop, const float* __restrict__ press,
                                         const typecode* __restrict__ code, float4* __restrict__ sA,
-                                        float4* __restrict__ sB, float2* __restrict__ sC,
+                                        float4* __restrict__ sB, float4* __restrict__ sC,
                                         const float4* __restrict__ sph, NNAcc& a) {
   const unsigned cellinit = (KIND == 1 ? 0u : g.boxfluid);
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
@@ -211,8 +228,8 @@ __device__ __forceinline__ void nn_pass(const KConst& K, const DivGrid& g, const
       const unsigned rowbase = cellinit + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
       const unsigned rs = bc[rowbase + rc.xa], re = bc[rowbase + rc.xb + 1];
       const unsigned ls = bc[rowbase + rc.lxa], le = bc[rowbase + rc.lxb + 1];
-      for (unsigned seg = rs; seg < re; seg += TCAP) {
-        const unsigned segn = min(unsigned(TCAP), re - seg);
+      for (unsigned seg = rs; seg < re; seg += NN_TCAP) {
+        const unsigned segn = min(unsigned(NN_TCAP), re - seg);
         __syncthreads();
         nn_stage(K, seg, segn, rc.xo, dy, dz, KIND == 1, poscell, velrhop, press, code, sA, sB, sC);
         __syncthreads();
@@ -227,21 +244,46 @@ __device__ __forceinline__ void nn_pass(const KConst& K, const DivGrid& g, const
             c1 = 0ull;
             b0 += 64;
           }
-          while (c0) {  // ascending p2
-            const int j = b0 + int(__builtin_ctzll(c0));
+          // ascending p2, two per iteration (the first pair's sums are updated first)
+          auto pop = [&]() -> int {
+            const int j = b0 + int(__builtin_ctzll(c0 | (1ull << 63)));
             c0 &= c0 - 1ull;
-            if (!c0 && c1) {
-              c0 = c1;
-              c1 = 0ull;
-              b0 += 64;
+            const bool e = c0 == 0ull;
+            c0 = e ? c1 : c0;
+            b0 = e ? b0 + 64 : b0;
+            c1 = e ? 0ull : c1;
+            return j;
+          };
+          while (c0) {
+            const int j1 = pop();
+            const bool two = c0 != 0ull;
+            const int j2p = pop();
+            const int j2 = two ? j2p : j1;
+            const float4 A1 = sA[j1], A2 = sA[j2];
+            const float4 B1 = sB[j1], B2 = sB[j2];
+            float drx1 = p.x - A1.x, dry1 = p.y - A1.y, drz1 = p.z - A1.z;
+            float drx2 = p.x - A2.x, dry2 = p.y - A2.y, drz2 = p.z - A2.z;
+            float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
+            float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
+            const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
+            const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
+            // a pair outside the test: dr = 0 and rr2 = 1e30 (kernel factor 0, finite terms)
+            drx1 = ok1 ? drx1 : 0.f;
+            dry1 = ok1 ? dry1 : 0.f;
+            drz1 = ok1 ? drz1 : 0.f;
+            rr21 = ok1 ? rr21 : 1e30f;
+            drx2 = ok2 ? drx2 : 0.f;
+            dry2 = ok2 ? dry2 : 0.f;
+            drz2 = ok2 ? drz2 : 0.f;
+            rr22 = ok2 ? rr22 : 1e30f;
+            const float4 C1 = sC[j1], C2 = sC[j2];
+            if (KIND == 2) {
+              nn_bound_pair(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
+              nn_bound_pair(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
+            } else {
+              nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1>(K, sph, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
+              nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1>(K, sph, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
             }
-            const float4 A = sA[j];
-            const float drx = p.x - A.x, dry = p.y - A.y, drz = p.z - A.z;
-            const float rr2 = drx * drx + dry * dry + drz * drz;
-            if (!(rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO)) continue;
-            const float4 B = sB[j];
-            if (KIND == 2) nn_bound_pair(K, p, drx, dry, drz, rr2, B, a);
-            else nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1>(K, sph, p, drx, dry, drz, rr2, B, sC[j], a);
           }
         }
       }
@@ -256,9 +298,9 @@ __global__ __launch_bounds__(TB) void k_nn_tiled(DevScalars* __restrict__ sc, co
                                                  const typecode* __restrict__ code, const unsigned* __restrict__ bc,
                                                  DivGrid g, KConst K, const float4* __restrict__ phases,
                                                  float4* __restrict__ arace, float4* __restrict__ shiftpos) {
-  __shared__ float4 sA[TCAP + SPH_PAD];
-  __shared__ float4 sB[TCAP];
-  __shared__ float2 sC[TCAP];
+  __shared__ float4 sA[NN_TCAP + SPH_PAD];
+  __shared__ float4 sB[NN_TCAP];
+  __shared__ float4 sC[NN_TCAP];  // {press, tag, 1/rho, -}
   __shared__ float4 sph[2 * SPH_MAXPHASES];
   __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];
@@ -319,6 +361,10 @@ __global__ __launch_bounds__(TB) void k_nn_tiled(DevScalars* __restrict__ sc, co
         p.press = 0.f;
         p.ph = 0;
       }
+      p.inv_rho = frcp(p.vr.w);
+      p.mph = sph[2 * p.ph].x;
+      p.taumax = sph[2 * p.ph + 1].z;
+      p.bimulti = sph[2 * p.ph + 1].w;
       const int lxa = max(cx1 - 1, 0), lxb = min(cx1 + 1, g.ncx - 1);
       const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
       const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act};
