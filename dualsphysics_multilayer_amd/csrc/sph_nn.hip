@@ -11,23 +11,27 @@
 // Bulkley-Papanastasiou law evaluated from the pair's FDA velocity gradient
 // (Laminar: Morris operator; ConstEq: the stress tensor 2 eta D).
 //
-// Work decomposition: the items and LDS staging of sph_interaction_tiled.hip (sph_tiled.hpp),
-// with one difference that parity needs: the shifting x sum of the reference is RESET by
-// every pair with a heavier-phase neighbour (`heavyphase ? 0 : x + ...`,
-// JSphCpu_NN_FDA.cpp:206), so its value depends on the pair order.  The reference visits
-// the 3x3 rows z-major, y, then p2 ascending in the row — i.e. p2 in ascending cell-sorted
-// index.  Here every lane drains its candidates row by row in that same order (no mirrored
-// row pairs) and pops its candidate bits from low to high, one pair per iteration: every
-// p1 accumulates its pairs in exactly the reference's order.
+// Work decomposition: the items, LDS staging and mirrored drain units of
+// sph_interaction_tiled.hip (sph_tiled.hpp), with one order-dependent sum handled apart:
+// the shifting x sum of the reference is RESET by every pair with a heavier-phase
+// neighbour (`heavyphase ? 0 : x + ...`, JSphCpu_NN_FDA.cpp:206), so its value depends on
+// the pair order.  The reference visits the 3x3 rows z-major, y, then p2 ascending in the
+// row — i.e. p2 in ascending cell-sorted index.  The fluid pass drains point-mirrored row
+// pairs as one set (lanes with alike loop lengths; every other sum is order-free up to
+// rounding) and flags a heavier-phase neighbour; a block with a flagged lane then re-sweeps
+// its rows in the reference order for sx alone (nn_sx_sweep: phase interfaces only).  The
+// bound-p2 pass keeps the reference order throughout (its first no-shift pair freezes
+// every shifting sum).  cfg5: 1.85 -> 1.55 ms per interaction (SPH_NN_MIRROR=0: the
+// row-ordered drain of every pass).
 #include "sph_tiled.hpp"
 
 namespace sphx {
 
-// Staged records per row segment: 48 B each (position, velrhop, {press, tag, 1/rho}); the
-// NN drain stages one row (3 cells) at a time, so 412 records keep <= 20480 B of LDS per block
-// (8 blocks = 4 waves per SIMD) and a row rarely needs a second segment.
+// Staged records per row segment: 48 B each (position, velrhop, {press, tag, 1/rho}); 410
+// records + the 8-record pad + the phase table keep the block at 20472 B of LDS (8 blocks =
+// 4 waves per SIMD; 412 made it 20568 B, 7 blocks).
 #ifndef SPH_NN_TCAP
-#define SPH_NN_TCAP 412
+#define SPH_NN_TCAP 410
 #endif
 constexpr int NN_TCAP = SPH_NN_TCAP;
 
@@ -36,6 +40,7 @@ constexpr int NN_TCAP = SPH_NN_TCAP;
 struct NNAcc {
   float ax, ay, az, ar, delta, visc, visceta;
   float sx, sy, sz, sw;  // shifting sums (shiftposfsp1)
+  bool hv;               // mirrored drain: a heavier-phase neighbour was seen (sx needs the ordered sweep)
 };
 
 struct NNP1 {
@@ -71,7 +76,10 @@ __device__ __forceinline__ float nn_eta(float dmag, float tau_yield, float visco
 // fails it comes in with dr = 0 and rr2 = 1e30: its kernel factor is 0, so every sum gets
 // +0, and the maxima, the DDT/shifting switches and the shifting reset are masked by ok —
 // branch-free, so two pairs can be interleaved.
-template <int TVISCO, int TDENSITY, bool SHIFT, bool BOUNDP2>
+// ORDERED: pairs arrive in the reference's order (the shifting x sum is reset by a
+// heavier-phase p2); else in mirrored-unit order: sx skips the heavy pair and a.hv records
+// it, and the caller recomputes sx in the reference order (nn_sx_sweep) when any lane saw one.
+template <int TVISCO, int TDENSITY, bool SHIFT, bool BOUNDP2, bool ORDERED = true>
 __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restrict__ sph, const NNP1& p, float drx,
                                         float dry, float drz, float rr2, bool ok, const float4& B, const float4& C,
                                         NNAcc& a) {
@@ -118,7 +126,12 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     const bool heavy = ok && !BOUNDP2 && (p.mph > ph2.x) && p.ph != pp2;
     const float massrhop = massp2 * inv_rho2;
     const bool noshift = ok && BOUNDP2 && (K.shiftmode == 1 || (K.shiftmode == 2 && C.y != 0.f));
-    a.sx = noshift ? FLT_MAX : (heavy ? 0.f : a.sx + massrhop * frx);
+    if (ORDERED) {
+      a.sx = noshift ? FLT_MAX : (heavy ? 0.f : a.sx + massrhop * frx);
+    } else {  // fluid p2 only (noshift needs a bound p2)
+      a.sx += heavy ? 0.f : massrhop * frx;
+      a.hv |= heavy;
+    }
     a.sy += heavy ? 0.f : massrhop * fry;
     a.sz += heavy ? 0.f : massrhop * frz;
     a.sw -= heavy ? 0.f : massrhop * dot3;
@@ -194,8 +207,11 @@ __device__ __forceinline__ void nn_stage(const KConst& K, unsigned rs, unsigned 
                                          bool boundrow, const float4* __restrict__ poscell,
                                          const float4* __restrict__ velrhop, const float* __restrict__ press,
                                          const typecode* __restrict__ code, float4* __restrict__ sA,
-                                         float4* __restrict__ sB, float4* __restrict__ sC) {
+                                         float4* __restrict__ sB, float4* __restrict__ sC, unsigned dst = 0u) {
   const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
+  sA += dst;
+  sB += dst;
+  sC += dst;
   for (unsigned i = threadIdx.x; i < n; i += TB) {
     const float4 pc = poscell[rs + i];
     const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
@@ -291,8 +307,238 @@ __device__ __forceinline__ void nn_pass(const KConst& K, const DivGrid& g, const
   }
 }
 
+// Drain of one round of a mirrored unit's accepted candidates: four 64-bit words c0..c3 of
+// staged records from bases b0..b3, compacted into one chain and popped two pairs per
+// iteration with value selects only (the chain of drain_words, sph_interaction_tiled.hip).
+// KIND 0: fluid p1 / fluid p2 (sx in mirrored order, see nn_pair), 2: bound p1 / fluid p2.
+template <int TVISCO, int TDENSITY, bool SHIFT, int KIND>
+__device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restrict__ sph, const NNP1& p,
+                                          unsigned long long c0, unsigned long long c1, unsigned long long c2,
+                                          unsigned long long c3, int b0, int b1, int b2, int b3,
+                                          const float4* __restrict__ sA, const float4* __restrict__ sB,
+                                          const float4* __restrict__ sC, NNAcc& a) {
+#pragma unroll
+  for (int pass = 0; pass < 3; pass++) {  // drop empty words, keep the order
+    const bool e2 = c2 == 0ull;
+    c2 = e2 ? c3 : c2;
+    b2 = e2 ? b3 : b2;
+    c3 = e2 ? 0ull : c3;
+    const bool e1 = c1 == 0ull;
+    c1 = e1 ? c2 : c1;
+    b1 = e1 ? b2 : b1;
+    c2 = e1 ? c3 : c2;
+    b2 = e1 ? b3 : b2;
+    c3 = e1 ? 0ull : c3;
+    const bool e0 = c0 == 0ull;
+    c0 = e0 ? c1 : c0;
+    b0 = e0 ? b1 : b0;
+    c1 = e0 ? c2 : c1;
+    b1 = e0 ? b2 : b1;
+    c2 = e0 ? c3 : c2;
+    b2 = e0 ? b3 : b2;
+    c3 = e0 ? 0ull : c3;
+  }
+  auto pop = [&](void) -> int {
+    const int j = b0 + int(__builtin_ctzll(c0 | (1ull << 63)));
+    c0 &= c0 - 1ull;
+    const bool e = c0 == 0ull;
+    c0 = e ? c1 : c0;
+    b0 = e ? b1 : b0;
+    c1 = e ? c2 : c1;
+    b1 = e ? b2 : b1;
+    c2 = e ? c3 : c2;
+    b2 = e ? b3 : b2;
+    c3 = e ? 0ull : c3;
+    return j;
+  };
+  while (c0) {
+    const int j1 = pop();
+    const bool two = c0 != 0ull;
+    const int j2p = pop();
+    const int j2 = two ? j2p : j1;
+    const float4 A1 = sA[j1], A2 = sA[j2];
+    const float4 B1 = sB[j1], B2 = sB[j2];
+    float drx1 = p.x - A1.x, dry1 = p.y - A1.y, drz1 = p.z - A1.z;
+    float drx2 = p.x - A2.x, dry2 = p.y - A2.y, drz2 = p.z - A2.z;
+    float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
+    float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
+    const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
+    const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
+    drx1 = ok1 ? drx1 : 0.f;
+    dry1 = ok1 ? dry1 : 0.f;
+    drz1 = ok1 ? drz1 : 0.f;
+    rr21 = ok1 ? rr21 : 1e30f;
+    drx2 = ok2 ? drx2 : 0.f;
+    dry2 = ok2 ? dry2 : 0.f;
+    drz2 = ok2 ? drz2 : 0.f;
+    rr22 = ok2 ? rr22 : 1e30f;
+    const float4 C1 = sC[j1], C2 = sC[j2];
+    if (KIND == 2) {
+      nn_bound_pair(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
+      nn_bound_pair(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
+    } else {
+      nn_pair<TVISCO, TDENSITY, SHIFT, false, false>(K, sph, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
+      nn_pair<TVISCO, TDENSITY, SHIFT, false, false>(K, sph, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
+    }
+  }
+}
+
+// A pass over the 9 fluid rows (KIND 0: fluid p1, 2: bound p1) in drain units of two
+// point-mirrored rows ((dy,dz) with (-dy,-dz)) staged as one segment and drained as one
+// set, then the item's own row (run_pass of sph_interaction_tiled.hip): a particle's
+// candidate counts in mirrored rows complement each other, so the lanes' loop lengths are
+// alike.  Every sum but the shifting x sum is order-free (up to rounding); a heavier-phase
+// neighbour is flagged in a.hv and the caller redoes sx in the reference order.
+template <int TVISCO, int TDENSITY, bool SHIFT, int KIND>
+__device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid& g, const RowCtx& rc, const NNP1& p,
+                                                 float thr, const unsigned* __restrict__ bc,
+                                                 const float4* __restrict__ poscell,
+                                                 const float4* __restrict__ velrhop, const float* __restrict__ press,
+                                                 const typecode* __restrict__ code, float4* __restrict__ sA,
+                                                 float4* __restrict__ sB, float4* __restrict__ sC,
+                                                 const float4* __restrict__ sph, NNAcc& a) {
+  static_assert(KIND == 0 || KIND == 2, "fluid rows only (the bound pass keeps the reference order)");
+  const unsigned cellinit = g.boxfluid;
+  const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
+  for (int u = 0; u < 5; u++) {
+    const int dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
+    const int dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
+    const bool paired = u < 4;
+    unsigned rs[2] = {0, 0}, re[2] = {0, 0}, ls[2] = {0, 0}, le[2] = {0, 0};
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      if (k == 1 && !paired) break;
+      const int dz = k ? -dza : dza, dy = k ? -dya : dya;
+      const int z = rc.cz + dz, y = rc.cy + dy;
+      if (z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;
+      const unsigned rowbase = cellinit + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+      rs[k] = bc[rowbase + rc.xa];
+      re[k] = bc[rowbase + rc.xb + 1];
+      ls[k] = bc[rowbase + rc.lxa];
+      le[k] = bc[rowbase + rc.lxb + 1];
+    }
+    const unsigned n0 = re[0] - rs[0], n1 = re[1] - rs[1];
+    if (n0 + n1 == 0u) continue;  // block-uniform
+    if (n0 + n1 <= unsigned(NN_TCAP)) {
+      __syncthreads();
+      if (n0) nn_stage(K, rs[0], n0, rc.xo, dya, dza, false, poscell, velrhop, press, code, sA, sB, sC, 0u);
+      if (n1) nn_stage(K, rs[1], n1, rc.xo, -dya, -dza, false, poscell, velrhop, press, code, sA, sB, sC, n0);
+      __syncthreads();
+      const int wa0 = int(ls[0] - rs[0]), wa1 = rc.act && n0 ? int(le[0] - rs[0]) : wa0;
+      const int wb0 = int(n0 + ls[1] - rs[1]), wb1 = rc.act && n1 ? int(n0 + le[1] - rs[1]) : wb0;
+      for (int off = 0;; off += 128) {  // a second round only for windows of > 128 candidates
+        const int na = wa1 - wa0 - off, nb = wb1 - wb0 - off;
+        if (na <= 0 && nb <= 0) break;
+        unsigned long long c0, c1, c2, c3;
+        test128(sA, wa0 + off, min(na, 128), px2, py2, pz2, thr, c0, c1);
+        test128(sA, wb0 + off, min(nb, 128), px2, py2, pz2, thr, c2, c3);
+        nn_drain4<TVISCO, TDENSITY, SHIFT, KIND>(K, sph, p, c0, c1, c2, c3, wa0 + off, wa0 + off + 64, wb0 + off,
+                                                 wb0 + off + 64, sA, sB, sC, a);
+      }
+    } else {  // too long for one segment: each row on its own, in TCAP segments
+      for (int k = 0; k < 2; k++) {
+        const int dz = k ? -dza : dza, dy = k ? -dya : dya;
+        for (unsigned seg = rs[k]; seg < re[k]; seg += NN_TCAP) {
+          const unsigned segn = min(unsigned(NN_TCAP), re[k] - seg);
+          __syncthreads();
+          nn_stage(K, seg, segn, rc.xo, dy, dz, false, poscell, velrhop, press, code, sA, sB, sC, 0u);
+          __syncthreads();
+          const int w0 = int(max(ls[k], seg) - seg);
+          const int w1 = rc.act ? max(w0, int(min(le[k], seg + segn)) - int(seg)) : w0;
+          for (int off = w0; off < w1; off += 128) {
+            unsigned long long c0, c1;
+            test128(sA, off, min(w1 - off, 128), px2, py2, pz2, thr, c0, c1);
+            nn_drain4<TVISCO, TDENSITY, SHIFT, KIND>(K, sph, p, c0, c1, 0ull, 0ull, off, off + 64, 0, 0, sA, sB,
+                                                     sC, a);
+          }
+        }
+      }
+    }
+  }
+}
+
+// The shifting x sum of a fluid p1 over its fluid rows in the reference's pair order
+// (z-major rows, p2 ascending), reset by every heavier-phase neighbour
+// (JSphCpu_NN_FDA.cpp:202-209) — the same per-pair terms as nn_pair.  Run for a whole
+// block when any of its lanes met a heavier-phase neighbour in the mirrored pass
+// (phase interfaces only).
+__device__ __forceinline__ float nn_sx_sweep(const KConst& K, const DivGrid& g, const RowCtx& rc, const NNP1& p,
+                                             float thr, const unsigned* __restrict__ bc,
+                                             const float4* __restrict__ poscell,
+                                             const float4* __restrict__ velrhop, const float* __restrict__ press,
+                                             const typecode* __restrict__ code, float4* __restrict__ sA,
+                                             float4* __restrict__ sB, float4* __restrict__ sC,
+                                             const float4* __restrict__ sph) {
+  float sx = 0.f;
+  const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
+  for (int dz = -1; dz <= 1; dz++) {
+    for (int dy = -1; dy <= 1; dy++) {
+      const int z = rc.cz + dz, y = rc.cy + dy;
+      if (z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;  // block-uniform
+      const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+      const unsigned rs = bc[rowbase + rc.xa], re = bc[rowbase + rc.xb + 1];
+      const unsigned ls = bc[rowbase + rc.lxa], le = bc[rowbase + rc.lxb + 1];
+      for (unsigned seg = rs; seg < re; seg += NN_TCAP) {
+        const unsigned segn = min(unsigned(NN_TCAP), re - seg);
+        __syncthreads();
+        nn_stage(K, seg, segn, rc.xo, dy, dz, false, poscell, velrhop, press, code, sA, sB, sC, 0u);
+        __syncthreads();
+        const int w0 = int(max(ls, seg) - seg);
+        const int w1 = rc.act ? max(w0, int(min(le, seg + segn)) - int(seg)) : w0;
+        for (int off = w0; off < w1; off += 128) {
+          unsigned long long c0, c1;
+          test128(sA, off, min(w1 - off, 128), px2, py2, pz2, thr, c0, c1);
+          int b0 = off;
+          if (!c0) {
+            c0 = c1;
+            c1 = 0ull;
+            b0 += 64;
+          }
+          while (c0) {  // ascending p2
+            const int j = b0 + int(__builtin_ctzll(c0));
+            c0 &= c0 - 1ull;
+            const bool e = c0 == 0ull;
+            c0 = e ? c1 : c0;
+            b0 = e ? b0 + 64 : b0;
+            c1 = e ? 0ull : c1;
+            const float4 A = sA[j], C = sC[j];
+            float drx = p.x - A.x;
+            const float dry = p.y - A.y, drz = p.z - A.z;
+            float rr2 = drx * drx + dry * dry + drz * drz;
+            const bool ok = rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO;
+            drx = ok ? drx : 0.f;
+            rr2 = ok ? rr2 : 1e30f;
+            const float rad = fsqrt_(rr2);
+            const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
+            const float fac = K.bwenovh * (wq * wq * wq);
+            const float frx = fac * drx;
+            const int pp2 = int(__float_as_uint(C.y));
+            const float massp2 = sph[2 * pp2].x;
+            const bool heavy = ok && (p.mph > massp2) && p.ph != pp2;
+            const float massrhop = massp2 * C.z;
+            sx = heavy ? 0.f : sx + massrhop * frx;
+          }
+        }
+      }
+    }
+  }
+  return sx;
+}
+
+#ifndef SPH_NN_WAVES
+#define SPH_NN_WAVES 4  // register budget for 4 waves per SIMD (<= 128 VGPRs)
+#endif
+#if SPH_NN_WAVES
+#define SPH_NN_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SPH_NN_WAVES, SPH_NN_WAVES)))
+#else
+#define SPH_NN_WAVES_ATTR
+#endif
+#ifndef SPH_NN_MIRROR
+#define SPH_NN_MIRROR 1  // 0: every pass in the reference's row order (one row per drain unit)
+#endif
+
 template <int TVISCO, int TDENSITY, bool SHIFT>
-__global__ __launch_bounds__(TB) void k_nn_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
+__global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
                                                  unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
                                                  const float4* __restrict__ velrhop, const float* __restrict__ press,
                                                  const typecode* __restrict__ code, const unsigned* __restrict__ bc,
@@ -370,7 +616,12 @@ __global__ __launch_bounds__(TB) void k_nn_tiled(DevScalars* __restrict__ sc, co
       const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act};
       if (bitem) {
         NNAcc f = {};
+#if SPH_NN_MIRROR
+        nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 2>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
+                                                     sph, f);
+#else
         nn_pass<TVISCO, TDENSITY, SHIFT, 2>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f);
+#endif
         if (act) {
           arace[p1] = make_float4(0.f, 0.f, 0.f, (f.ar != 0.f || f.visc != 0.f) ? 0.f + f.ar : 0.f);
           viscmax = fmaxf(viscmax, f.visc);
@@ -380,7 +631,14 @@ __global__ __launch_bounds__(TB) void k_nn_tiled(DevScalars* __restrict__ sc, co
       // fluid p1: the fluid pass, then the bound pass; the shifting sums carry over
       // (shiftposfs[p1] is stored by the first pass and loaded by the second)
       NNAcc f = {}, b = {};
+#if SPH_NN_MIRROR
+      nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 0>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
+                                                   sph, f);
+      if (SHIFT && __syncthreads_or(int(f.hv)))
+        f.sx = nn_sx_sweep(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph);
+#else
       nn_pass<TVISCO, TDENSITY, SHIFT, 0>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f);
+#endif
       b.sx = f.sx;
       b.sy = f.sy;
       b.sz = f.sz;
