@@ -27,11 +27,12 @@
 
 namespace sphx {
 
-// Staged records per row segment: 48 B each (position, velrhop, {press, tag, 1/rho}); 410
+// Staged records per row segment: 41 B each (position, velrhop, {press, 1/rho}, tag); 480
 // records + the 8-record pad + the phase table keep the block at 20472 B of LDS (8 blocks =
-// 4 waves per SIMD; 412 made it 20568 B, 7 blocks).
+// 4 waves per SIMD), and a mirrored row pair mostly fits one segment (cfg5: 1.554 ms at
+// 410 records of 48 B, 1.515 ms at 480 of 41 B).
 #ifndef SPH_NN_TCAP
-#define SPH_NN_TCAP 410
+#define SPH_NN_TCAP 480
 #endif
 constexpr int NN_TCAP = SPH_NN_TCAP;
 
@@ -41,6 +42,19 @@ struct NNAcc {
   float ax, ay, az, ar, delta, visc, visceta;
   float sx, sy, sz, sw;  // shifting sums (shiftposfsp1)
   bool hv;               // mirrored drain: a heavier-phase neighbour was seen (sx needs the ordered sweep)
+};
+
+// Third part of a staged record: {press, 1/rho} (8 B) + the tag (1 B) — 41 B records in all.
+struct NNSC {
+  float2* c;
+  unsigned char* t;
+  // as the float4 {press, tag, 1/rho, 0} of the pair bodies: tag = phase index bits (fluid
+  // rows) or 1.0 for a fixed boundary particle (bound rows)
+  __device__ __forceinline__ float4 ld(int j, bool boundrow) const {
+    const float2 v = c[j];
+    const unsigned tg = t[j];
+    return make_float4(v.x, boundrow ? float(tg) : __uint_as_float(tg), v.y, 0.f);
+  }
 };
 
 struct NNP1 {
@@ -207,11 +221,12 @@ __device__ __forceinline__ void nn_stage(const KConst& K, unsigned rs, unsigned 
                                          bool boundrow, const float4* __restrict__ poscell,
                                          const float4* __restrict__ velrhop, const float* __restrict__ press,
                                          const typecode* __restrict__ code, float4* __restrict__ sA,
-                                         float4* __restrict__ sB, float4* __restrict__ sC, unsigned dst = 0u) {
+                                         float4* __restrict__ sB, NNSC sC, unsigned dst = 0u) {
   const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
   sA += dst;
   sB += dst;
-  sC += dst;
+  sC.c += dst;
+  sC.t += dst;
   for (unsigned i = threadIdx.x; i < n; i += TB) {
     const float4 pc = poscell[rs + i];
     const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
@@ -222,7 +237,8 @@ __device__ __forceinline__ void nn_stage(const KConst& K, unsigned rs, unsigned 
     sB[i] = vr;
     const typecode c = code[rs + i];
     const unsigned tag = boundrow ? (CodeType(c) == 0 ? 1u : 0u) : unsigned(c & CODE_MASKVALUE);
-    sC[i] = make_float4(press[rs + i], boundrow ? float(tag) : __uint_as_float(tag), frcp(vr.w), 0.f);
+    sC.c[i] = make_float2(press[rs + i], frcp(vr.w));
+    sC.t[i] = (unsigned char)tag;
   }
 }
 
@@ -233,7 +249,7 @@ __device__ __forceinline__ void nn_pass(const KConst& K, const DivGrid& g, const
                                         const unsigned* __restrict__ bc, const float4* __restrict__ poscell,
                                         const float4* __restrict__ velrhop, const float* __restrict__ press,
                                         const typecode* __restrict__ code, float4* __restrict__ sA,
-                                        float4* __restrict__ sB, float4* __restrict__ sC,
+                                        float4* __restrict__ sB, NNSC sC,
                                         const float4* __restrict__ sph, NNAcc& a) {
   const unsigned cellinit = (KIND == 1 ? 0u : g.boxfluid);
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
@@ -292,7 +308,7 @@ __device__ __forceinline__ void nn_pass(const KConst& K, const DivGrid& g, const
             dry2 = ok2 ? dry2 : 0.f;
             drz2 = ok2 ? drz2 : 0.f;
             rr22 = ok2 ? rr22 : 1e30f;
-            const float4 C1 = sC[j1], C2 = sC[j2];
+            const float4 C1 = sC.ld(j1, KIND == 1), C2 = sC.ld(j2, KIND == 1);
             if (KIND == 2) {
               nn_bound_pair(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
               nn_bound_pair(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
@@ -316,7 +332,7 @@ __device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restr
                                           unsigned long long c0, unsigned long long c1, unsigned long long c2,
                                           unsigned long long c3, int b0, int b1, int b2, int b3,
                                           const float4* __restrict__ sA, const float4* __restrict__ sB,
-                                          const float4* __restrict__ sC, NNAcc& a) {
+                                          const NNSC sC, NNAcc& a) {
 #pragma unroll
   for (int pass = 0; pass < 3; pass++) {  // drop empty words, keep the order
     const bool e2 = c2 == 0ull;
@@ -372,7 +388,7 @@ __device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restr
     dry2 = ok2 ? dry2 : 0.f;
     drz2 = ok2 ? drz2 : 0.f;
     rr22 = ok2 ? rr22 : 1e30f;
-    const float4 C1 = sC[j1], C2 = sC[j2];
+    const float4 C1 = sC.ld(j1, false), C2 = sC.ld(j2, false);
     if (KIND == 2) {
       nn_bound_pair(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
       nn_bound_pair(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
@@ -395,7 +411,7 @@ __device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid&
                                                  const float4* __restrict__ poscell,
                                                  const float4* __restrict__ velrhop, const float* __restrict__ press,
                                                  const typecode* __restrict__ code, float4* __restrict__ sA,
-                                                 float4* __restrict__ sB, float4* __restrict__ sC,
+                                                 float4* __restrict__ sB, NNSC sC,
                                                  const float4* __restrict__ sph, NNAcc& a) {
   static_assert(KIND == 0 || KIND == 2, "fluid rows only (the bound pass keeps the reference order)");
   const unsigned cellinit = g.boxfluid;
@@ -467,7 +483,7 @@ __device__ __forceinline__ float nn_sx_sweep(const KConst& K, const DivGrid& g, 
                                              const float4* __restrict__ poscell,
                                              const float4* __restrict__ velrhop, const float* __restrict__ press,
                                              const typecode* __restrict__ code, float4* __restrict__ sA,
-                                             float4* __restrict__ sB, float4* __restrict__ sC,
+                                             float4* __restrict__ sB, NNSC sC,
                                              const float4* __restrict__ sph) {
   float sx = 0.f;
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
@@ -501,7 +517,7 @@ __device__ __forceinline__ float nn_sx_sweep(const KConst& K, const DivGrid& g, 
             c0 = e ? c1 : c0;
             b0 = e ? b0 + 64 : b0;
             c1 = e ? 0ull : c1;
-            const float4 A = sA[j], C = sC[j];
+            const float4 A = sA[j], C = sC.ld(j, false);
             float drx = p.x - A.x;
             const float dry = p.y - A.y, drz = p.z - A.z;
             float rr2 = drx * drx + dry * dry + drz * drz;
@@ -546,7 +562,9 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
                                                  float4* __restrict__ arace, float4* __restrict__ shiftpos) {
   __shared__ float4 sA[NN_TCAP + SPH_PAD];
   __shared__ float4 sB[NN_TCAP];
-  __shared__ float4 sC[NN_TCAP];  // {press, tag, 1/rho, -}
+  __shared__ float2 sC2[NN_TCAP];  // {press, 1/rho}
+  __shared__ unsigned char sT[NN_TCAP];  // tag
+  const NNSC sC = {sC2, sT};
   __shared__ float4 sph[2 * SPH_MAXPHASES];
   __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];
