@@ -34,8 +34,8 @@ namespace sphx {
 // span more than TMAXCELLS x-cells; items may start and end inside a cell.  Full items
 // keep both waves of a block busy (cell-aligned items averaged 103 of 128 lanes at 1M)
 // and make the lanes' candidate counts more alike.
-// One launch: a block of IT_WAVES waves takes IT_WAVES consecutive rows (fluid rows, then
-// bound rows); each wave copies its row's cell begin
+// One launch: a block of IT_WAVES waves takes IT_WAVES consecutive rows of the order
+// (fluid y,z-row, bound y,z-row) interleaved; each wave copies its row's cell begin
 // offsets to LDS and lane 0 walks the row's items into LDS (a row of > IT_BUF items walks
 // again for the rest), the wave copies them to the block's slots: ONE atomic append per block into the counter of its XCD group (blocks
 // [g nb/8, (g+1) nb/8)), whose items live in region g of the list (ItemList, sph_tiled.hpp).
@@ -66,10 +66,10 @@ __global__ __launch_bounds__(64 * IT_WAVES) void k_items(const unsigned* __restr
   unsigned* pre = pre_all[w];
   unsigned short* nzfrom = nz_all[w];
   const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
-  const unsigned k = blockIdx.x * IT_WAVES + w;  // row: fluid rows, then bound rows
+  const unsigned k = blockIdx.x * IT_WAVES + w;  // row of the interleaved order
   const bool valid = k < 2u * nrows;
-  const bool bound = k >= nrows;
-  const unsigned rr = !valid ? 0u : bound ? k - nrows : k;
+  const bool bound = (k & 1u) != 0u;
+  const unsigned rr = valid ? k >> 1 : 0u;
   const unsigned y = rr % unsigned(g.ncy), z = rr / unsigned(g.ncy);
   const unsigned rowbase = (bound ? 0u : g.boxfluid) + z * g.nsheet + y * unsigned(g.ncx);
   const unsigned grp = (blockIdx.x * 8u) / gridDim.x;
@@ -711,11 +711,11 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
   __shared__ float4 sA[tcap + SPH_PAD];  // over-read pad of the 8-wide candidate test (<= 7 records)
   __shared__ float4 sB[tcap];
   __shared__ typename CRecT<FT>::type sC[tcap];  // press/rho, 1/rho (FT: mass-scaled + kind)
-  __shared__ unsigned s_item, s_slot;
-  __shared__ unsigned s_pre[9];  // item list region prefix (ItemList)
+  __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];  // lane -> p1 of the item (see lane_order)
   __shared__ unsigned s_nwave[4];
-  const unsigned nitems = item_list_init(qctr, g, s_pre);
+  const ItemList L = item_list(qctr, g);
+  const unsigned nitems = L.pre[8];
   const unsigned per = (nitems + 7) / 8;
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f;
@@ -728,19 +728,15 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
     for (;;) {
       // a group known to be exhausted (counters only grow; a stale read is smaller) costs
       // no atomic: probing all 8 queues was ~16k same-line atomics per launch
-      if (threadIdx.x == 0) {
-        const unsigned itc = (lo + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT) >= hi)
-                                 ? hi
-                                 : lo + atomicAdd(&qctr[xg * QSTRIDE], 1u);
-        s_item = itc;
-        s_slot = itc < hi ? item_slot(s_pre, g.itemcapg, itc) : 0u;  // one thread, prefix in LDS
-      }
+      if (threadIdx.x == 0)
+        s_item = (lo + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= hi)
+                     ? hi
+                     : lo + atomicAdd(&qctr[xg * QSTRIDE], 1u);
       __syncthreads();
-      const unsigned it = s_item, slot = s_slot;
+      const unsigned it = s_item;
       __syncthreads();
       if (it >= hi) break;
-      const uint4 item = items[slot];
+      const uint4 item = items[L.slot(it)];
       const bool bitem = (item.x & ITEM_BOUND) != 0u;
       const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
       const int a = int(item.y & 0xffffu), b = int(item.y >> 16);

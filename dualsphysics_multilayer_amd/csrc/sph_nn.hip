@@ -27,7 +27,7 @@
 
 namespace sphx {
 
-// Staged records per row segment: 41 B each (position, velrhop, {press, 1/rho}, tag); 478
+// Staged records per row segment: 41 B each (position, velrhop, {press, 1/rho}, tag); 480
 // records + the 8-record pad + the phase table keep the block at 20472 B of LDS (8 blocks =
 // 4 waves per SIMD), and a mirrored row pair mostly fits one segment (cfg5: 1.554 ms at
 // 410 records of 48 B, 1.515 ms at 480 of 41 B).
@@ -35,7 +35,7 @@ namespace sphx {
 #define SPH_NN_POWSKIP 0  // 1: skip D^(n-1) when every lane's p2 phase has n = 1 (more spills here)
 #endif
 #ifndef SPH_NN_TCAP
-#define SPH_NN_TCAP 478
+#define SPH_NN_TCAP 480
 #endif
 constexpr int NN_TCAP = SPH_NN_TCAP;
 
@@ -582,12 +582,12 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
   __shared__ unsigned char sT[NN_TCAP];  // tag
   const NNSC sC = {sC2, sT};
   __shared__ float4 sph[2 * SPH_MAXPHASES];
-  __shared__ unsigned s_item, s_slot;
-  __shared__ unsigned s_pre[9];  // item list region prefix (ItemList)
+  __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];
   __shared__ unsigned s_nwave[4];
   if (threadIdx.x < 2 * SPH_MAXPHASES) sph[threadIdx.x] = phases[threadIdx.x];
-  const unsigned nitems = item_list_init(qctr, g, s_pre);
+  const ItemList L = item_list(qctr, g);
+  const unsigned nitems = L.pre[8];
   const unsigned per = (nitems + 7) / 8;
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f, etamax = 0.f;
@@ -597,19 +597,15 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
     for (;;) {
       // a group known to be exhausted (counters only grow; a stale read is smaller) costs
       // no atomic: probing all 8 queues was ~16k same-line atomics per launch
-      if (threadIdx.x == 0) {
-        const unsigned itc = (lo + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT) >= hi)
-                                 ? hi
-                                 : lo + atomicAdd(&qctr[xg * QSTRIDE], 1u);
-        s_item = itc;
-        s_slot = itc < hi ? item_slot(s_pre, g.itemcapg, itc) : 0u;  // one thread, prefix in LDS
-      }
+      if (threadIdx.x == 0)
+        s_item = (lo + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= hi)
+                     ? hi
+                     : lo + atomicAdd(&qctr[xg * QSTRIDE], 1u);
       __syncthreads();
-      const unsigned it = s_item, slot = s_slot;
+      const unsigned it = s_item;
       __syncthreads();
       if (it >= hi) break;
-      const uint4 item = items[slot];
+      const uint4 item = items[L.slot(it)];
       const bool bitem = (item.x & ITEM_BOUND) != 0u;
       const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
       const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);
