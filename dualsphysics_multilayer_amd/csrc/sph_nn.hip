@@ -31,6 +31,9 @@ namespace sphx {
 // records + the 8-record pad + the phase table keep the block at 20472 B of LDS (8 blocks =
 // 4 waves per SIMD), and a mirrored row pair mostly fits one segment (cfg5: 1.554 ms at
 // 410 records of 48 B, 1.515 ms at 480 of 41 B).
+#ifndef SPH_NN_POWSKIP
+#define SPH_NN_POWSKIP 0  // 1: skip D^(n-1) when every lane's p2 phase has n = 1 (more spills here)
+#endif
 #ifndef SPH_NN_TCAP
 #define SPH_NN_TCAP 480
 #endif
@@ -79,7 +82,13 @@ __device__ __forceinline__ float nn_eta(float dmag, float tau_yield, float visco
   const float miou_pap = miou_yield * (1.f - fexp2(-m * dmag * 1.4426950408889634f));  // exp(-m D)
   const bool cap = (miou_pap > m * tau_yield || dmag == ALMOSTZERO);
   const float term1 = (taumax1 != 0.f ? miou_yield : (cap ? m * tau_yield : miou_pap));
-  const float miou_hb = visco * fexp2((n - 1.f) * flog2(dmag));  // visco * D^(n-1)
+  // visco * D^(n-1), exactly visco for n = 1 (skipped when no lane of the wave needs the power)
+  float miou_hb = visco;
+#if SPH_NN_POWSKIP
+  if (__ballot(n != 1.f)) miou_hb = (n != 1.f) ? visco * fexp2((n - 1.f) * flog2(dmag)) : visco;
+#else
+  miou_hb = visco * fexp2((n - 1.f) * flog2(dmag));
+#endif
   const float term2 = (bi_region ? visco : (cap ? visco : miou_hb));
   return term1 + term2;
 }
@@ -118,7 +127,8 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   // continuity
   const float rhop1over2 = rho1 * inv_rho2;
   float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
-  a.ar = fmaf(massp2 * (dvx * frx + dvy * fry + dvz * frz), rhop1over2, a.ar);
+  const float dot = drx * dvx + dry * dvy + drz * dvz;  // dv.fr = fac (dr.dv)
+  a.ar = fmaf(massp2 * (fac * dot), rhop1over2, a.ar);
   const float cbar = ph2.y;  // max(Cs0[pp2], Cs0[pp2])
   const float dot3 = fac * rr2;  // drx*frx+dry*fry+drz*frz
   const float inv_re = frcp(rr2 + K.eta2);
@@ -129,6 +139,10 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     a.delta = (BOUNDP2 && !K.mdbc && ok) ? FLT_MAX : a.delta + delta;
   }
   if ((TDENSITY == 2 || (TDENSITY == 3 && !BOUNDP2)) && a.delta != FLT_MAX) {
+    // rho0 (1 + ddtgz drz)^(1/gamma) - rho0 as the reference evaluates it in float: the
+    // three-term series of k_fluid_tiled (exact to 2e-6 of the term) removes the float
+    // cancellation of the reference, which the NN parity bar (10x the reference's own
+    // rounding floor) does not absorb: step-1 velocities moved 5.7e-7 against 2e-8
     const float rh = 1.f + K.ddtgz * drz;
     const float drhop = K.rhopzero * fexp2(K.ovgamma * flog2(rh)) - K.rhopzero;
     const float visc_densi = K.ddtkh * cbar * ((rho2 - rho1) - drhop) * inv_re;
@@ -151,7 +165,6 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     a.sw -= heavy ? 0.f : massrhop * dot3;
   }
   // viscosity
-  const float dot = drx * dvx + dry * dvy + drz * dvz;
   const float dot_rr2 = dot * inv_re;
   a.visc = fmaxf(ok ? dot_rr2 : 0.f, a.visc);
   const float visco_nn = ph2.z;
@@ -170,7 +183,10 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
       dvy = 2.f * p.vr.y;
       dvz = 2.f * p.vr.z;
     }
-    // GetVelocityGradients_FDA + GetStrainRateTensor (JSphCpu_Tensors.cpp:40-82)
+    // GetVelocityGradients_FDA + GetStrainRateTensor (JSphCpu_Tensors.cpp:40-82), in the
+    // reference's operation order: the effective viscosity divides by the invariant, whose
+    // explicit form cancels, so its rounding is part of the result (a closed form of the
+    // rank-one gradient's invariant moved step-1 velocities 30x past the noise floor)
     const float irr2 = frcp(rr2);
     const float a11 = dvx * drx * irr2, a12 = dvx * dry * irr2, a13 = dvx * drz * irr2;
     const float a21 = dvy * drx * irr2, a22 = dvy * dry * irr2, a23 = dvy * drz * irr2;
