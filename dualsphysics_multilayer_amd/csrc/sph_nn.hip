@@ -586,8 +586,7 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
   __shared__ unsigned char s_perm[TB];
   __shared__ unsigned s_nwave[4];
   if (threadIdx.x < 2 * SPH_MAXPHASES) sph[threadIdx.x] = phases[threadIdx.x];
-  const ItemList L = item_list(qctr, g);
-  const unsigned nitems = L.pre[8];
+  const unsigned nitems = sc->nitems;
   const unsigned per = (nitems + 7) / 8;
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f, etamax = 0.f;
@@ -605,7 +604,7 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
       const unsigned it = s_item;
       __syncthreads();
       if (it >= hi) break;
-      const uint4 item = items[L.slot(it)];
+      const uint4 item = items[it];
       const bool bitem = (item.x & ITEM_BOUND) != 0u;
       const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
       const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);

@@ -140,33 +140,6 @@ __device__ __forceinline__ unsigned lane_order(const float4* __restrict__ poscel
   return valid ? s_perm[me] : me;
 }
 
-// The item list of the last build (k_items): 8 regions of g.itemcapg slots, region r
-// holding cnt[r] items (the build's counter set g.itemset).  The interaction sees their
-// concatenation (region order = spatial order of the rows) as one list of n items, cut into
-// 8 equal XCD-group ranges as before; item_slot maps a list index to its slot.
-struct ItemList {
-  unsigned pre[9];  // exclusive prefix of the region counts; pre[8] = n
-  unsigned capg;
-  __device__ __forceinline__ unsigned slot(unsigned v) const {
-    unsigned r = 0;
-#pragma unroll
-    for (int k = 1; k < 8; k++) r += v >= pre[k] ? 1u : 0u;
-    return r * capg + (v - pre[r]);
-  }
-};
-__device__ __forceinline__ ItemList item_list(const unsigned* __restrict__ qctr, const DivGrid& g) {
-  ItemList L;
-  L.capg = g.itemcapg;
-  unsigned s = 0;
-#pragma unroll
-  for (int r = 0; r < 8; r++) {
-    L.pre[r] = s;
-    s += qctr[(QAPP + 8u * g.itemset + unsigned(r)) * QSTRIDE];
-  }
-  L.pre[8] = s;
-  return L;
-}
-
 // Item geometry shared by the passes of one p1.
 struct RowCtx {
   int cy, cz;     // the item's cell row
