@@ -158,6 +158,10 @@ __global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ coun
     run += v;
   }
   if (threadIdx.x == 1023) sc->nitems = part[1023];
+  __syncthreads();
+  // items of the bound rows (the list's tail): each XCD group takes its share of them
+  // after its fluid items (ItemGroups)
+  if (threadIdx.x == 0) sc->nitems_bound = part[1023] - counts[nrows2 / 2];
 }
 
 void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
@@ -692,8 +696,7 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
   __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];  // lane -> p1 of the item (see lane_order)
   __shared__ unsigned s_nwave[4];
-  const unsigned nitems = sc->nitems;
-  const unsigned per = (nitems + 7) / 8;
+  const ItemGroups IG(sc);
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f;
   const float cvisc_f = -K.visco * K.cs0f * K.kernelh * K.massfluid;
@@ -701,18 +704,19 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
 
   for (unsigned q = 0; q < 8; q++) {
     const unsigned xg = (grp + q) & 7;
-    const unsigned lo = xg * per, hi = min(nitems, lo + per);
+    const ItemGroup gr = IG.group(xg);
     for (;;) {
       // a group known to be exhausted (counters only grow; a stale read is smaller) costs
       // no atomic: probing all 8 queues was ~16k same-line atomics per launch
       if (threadIdx.x == 0)
-        s_item = (lo + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= hi)
-                     ? hi
-                     : lo + atomicAdd(&qctr[xg * QSTRIDE], 1u);
+        s_item = (__hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gr.n)
+                     ? gr.n
+                     : atomicAdd(&qctr[xg * QSTRIDE], 1u);
       __syncthreads();
-      const unsigned it = s_item;
+      const unsigned c = s_item;
       __syncthreads();
-      if (it >= hi) break;
+      if (c >= gr.n) break;
+      const unsigned it = gr.item(c);
       const uint4 item = items[it];
       const bool bitem = (item.x & ITEM_BOUND) != 0u;
       const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);

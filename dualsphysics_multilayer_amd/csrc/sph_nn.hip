@@ -586,24 +586,24 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
   __shared__ unsigned char s_perm[TB];
   __shared__ unsigned s_nwave[4];
   if (threadIdx.x < 2 * SPH_MAXPHASES) sph[threadIdx.x] = phases[threadIdx.x];
-  const unsigned nitems = sc->nitems;
-  const unsigned per = (nitems + 7) / 8;
+  const ItemGroups IG(sc);
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f, etamax = 0.f;
   for (unsigned q = 0; q < 8; q++) {
     const unsigned xg = (grp + q) & 7;
-    const unsigned lo = xg * per, hi = min(nitems, lo + per);
+    const ItemGroup gr = IG.group(xg);
     for (;;) {
       // a group known to be exhausted (counters only grow; a stale read is smaller) costs
       // no atomic: probing all 8 queues was ~16k same-line atomics per launch
       if (threadIdx.x == 0)
-        s_item = (lo + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= hi)
-                     ? hi
-                     : lo + atomicAdd(&qctr[xg * QSTRIDE], 1u);
+        s_item = (__hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gr.n)
+                     ? gr.n
+                     : atomicAdd(&qctr[xg * QSTRIDE], 1u);
       __syncthreads();
-      const unsigned it = s_item;
+      const unsigned c = s_item;
       __syncthreads();
-      if (it >= hi) break;
+      if (c >= gr.n) break;
+      const unsigned it = gr.item(c);
       const uint4 item = items[it];
       const bool bitem = (item.x & ITEM_BOUND) != 0u;
       const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);

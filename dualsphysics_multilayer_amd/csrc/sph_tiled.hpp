@@ -143,6 +143,40 @@ __device__ __forceinline__ unsigned lane_order(const float4* __restrict__ poscel
   return valid ? s_perm[me] : me;
 }
 
+// The per-XCD-group work of a tiled interaction: the item list is [fluid-row items | bound-row
+// items] in spatial order; group g takes the g-th eighth of the fluid items, then the g-th
+// eighth of the bound items (most of them cheap: no fluid in reach, or continuity only), so
+// every group ends on short items and the blocks' last items finish closer together
+// (SPH_ITEM_SPLIT 0: eighths of the whole list, the bound items all in the last groups).
+#ifndef SPH_ITEM_SPLIT
+#define SPH_ITEM_SPLIT 1
+#endif
+struct ItemGroup {
+  unsigned flo, nfg, blo, n;  // fluid range [flo, flo+nfg), then bound items from blo; n in all
+  __device__ __forceinline__ unsigned item(unsigned c) const { return c < nfg ? flo + c : blo + (c - nfg); }
+};
+struct ItemGroups {
+  unsigned nf, nb;
+  __device__ __forceinline__ explicit ItemGroups(const DevScalars* sc) {
+    const unsigned n = sc->nitems;
+#if SPH_ITEM_SPLIT
+    nb = min(sc->nitems_bound, n);
+#else
+    nb = 0u;
+#endif
+    nf = n - nb;
+  }
+  __device__ __forceinline__ ItemGroup group(unsigned g) const {
+    const unsigned pf = (nf + 7u) / 8u, pb = (nb + 7u) / 8u;
+    ItemGroup r;
+    r.flo = min(nf, g * pf);
+    r.nfg = min(nf, r.flo + pf) - r.flo;
+    r.blo = nf + min(nb, g * pb);
+    r.n = r.nfg + (nf + min(nb, (g + 1u) * pb) - r.blo);
+    return r;
+  }
+};
+
 // Item geometry shared by the passes of one p1.
 struct RowCtx {
   int cy, cz;     // the item's cell row
