@@ -54,20 +54,19 @@ def _stale(obj: str, src: str) -> bool:
     return os.path.getmtime(obj) < max(os.path.getmtime(d) for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, outdir: str | None = None, defines: list | None = None,
-          flags: list | None = None) -> str:
-    """Build libsphcore.so; `outdir`/`defines`/`flags` make diagnostic variants (e.g. ablations)."""
+def build(force: bool = False, verbose: bool = False, outdir: str | None = None, defines: list | None = None) -> str:
+    """Build libsphcore.so; `outdir`/`defines` make diagnostic variants (e.g. ablations)."""
     global OUTDIR
     saved = OUTDIR
     if outdir:
         OUTDIR = outdir
     try:
-        return _build(force, verbose, defines or [], flags or [])
+        return _build(force, verbose, defines or [])
     finally:
         OUTDIR = saved
 
 
-def _build(force: bool, verbose: bool, defines: list, flags: list) -> str:
+def _build(force: bool, verbose: bool, defines: list) -> str:
     os.makedirs(os.path.join(OUTDIR, "obj"), exist_ok=True)
     cc = hipcc()
     objs = []
@@ -76,10 +75,9 @@ def _build(force: bool, verbose: bool, defines: list, flags: list) -> str:
         src = os.path.join(CSRC, s)
         obj = os.path.join(OUTDIR, "obj", s + ".o")
         objs.append(obj)
-        if force or defines or flags or _stale(obj, src):
+        if force or defines or _stale(obj, src):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
-            extra = flags if s.endswith(".hip") else []
-            jobs.append([cc] + CXXFLAGS + extra + ["-D" + d for d in defines] + lang + ["-c", src, "-o", obj])
+            jobs.append([cc] + CXXFLAGS + ["-D" + d for d in defines] + lang + ["-c", src, "-o", obj])
     if jobs:
         with cf.ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
             for cmd, r in zip(jobs, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs)):

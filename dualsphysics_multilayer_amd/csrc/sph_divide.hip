@@ -1098,16 +1098,13 @@ __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, G
 void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& src, const PartArrays& dst,
                        bool withm1, bool withpre, const KConst& K, const double dom_posmin[3], float4* poscell,
                        float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
-                       IncDivScratch& s, const float4* phase_eos, hipEvent_t ev_boxes) {
+                       IncDivScratch& s, const float4* phase_eos) {
   s.gen++;
   const int usey = g.ncy > 1, usez = g.ncz > 1;
   const unsigned omax = 1u + (usey ? unsigned(g.ncx) : 0u) + (usez ? g.nsheet : 0u);
   hipLaunchKernelGGL(k_inc_classify, dim3(s.nb1), dim3(INC_BS), 0, stm, sc, src.dcell, src.code, g, K.domcellcode, s,
                      usey, usez);
   hipLaunchKernelGGL(k_inc_boxes, dim3(s.nb2), dim3(IB_BS), 0, stm, sc, g, begincell_old, begincell_new, s, omax);
-  // begincell and the counts are final here: work that needs only them (the interaction's
-  // item build) may start on another stream beside the push
-  if (ev_boxes) (void)hipEventRecord(ev_boxes, stm);
   GatherArgs a;
   a.phase_eos = phase_eos;
   a.xoff = 0;

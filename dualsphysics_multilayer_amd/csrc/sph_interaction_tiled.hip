@@ -472,9 +472,6 @@ __device__ __forceinline__ void stage_row(const KConst& K, unsigned rs, unsigned
   return;  // diagnostic: no staging loads
 #endif
   const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
-#if SPH_STAGE_PRIO
-  __builtin_amdgcn_s_setprio(SPH_STAGE_PRIO);  // staging waves issue their loads ahead of draining waves
-#endif
   for (unsigned i = threadIdx.x; i < re - rs; i += TB) {
     const float4 pc = poscell[rs + i];
     const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
@@ -486,9 +483,6 @@ __device__ __forceinline__ void stage_row(const KConst& K, unsigned rs, unsigned
     const float ir = frcp(vr.w);
     put_c(sC, dst + i, press[rs + i], ir, K, ft, rs + i);
   }
-#if SPH_STAGE_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
 }
 
 // Per-pass constants of the pair body for p2 of mass m2 (the Wendland bwen/h folded in).

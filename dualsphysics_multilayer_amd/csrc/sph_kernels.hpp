@@ -136,7 +136,7 @@ unsigned inc_blocks_boxes(unsigned nctt);
 void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& src, const PartArrays& dst,
                        bool withm1, bool withpre, const KConst& K, const double dom_posmin[3], float4* poscell,
                        float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
-                       IncDivScratch& s, const float4* phase_eos = nullptr, hipEvent_t ev_boxes = nullptr);
+                       IncDivScratch& s, const float4* phase_eos = nullptr);
 
 // ---- interaction (cusph::Interaction_Forces, JSphGpu_ker.cu:788-885) ----
 // With floating bodies (ftmassp != nullptr: particle mass per body, `code` of the

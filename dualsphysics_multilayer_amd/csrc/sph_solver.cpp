@@ -369,9 +369,6 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   }
   check_hip(hipSetDevice(device), "hipSetDevice");
   check_hip(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
-  check_hip(hipStreamCreateWithFlags(&istream_, hipStreamNonBlocking), "hipStreamCreate");
-  check_hip(hipEventCreateWithFlags(&iev_boxes_, hipEventDisableTiming), "hipEventCreate");
-  check_hip(hipEventCreateWithFlags(&iev_items_, hipEventDisableTiming), "hipEventCreate");
   try {
     AllocFixed();
     if (nn_) UploadPhases(cdef);
@@ -400,9 +397,6 @@ SphGpuSingle::~SphGpuSingle() {
   for (auto& e : pending_) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto e : evpool_) (void)hipEventDestroy(e);
   if (xev_) (void)hipEventDestroy(xev_);
-  if (iev_boxes_) (void)hipEventDestroy(iev_boxes_);
-  if (iev_items_) (void)hipEventDestroy(iev_items_);
-  if (istream_) (void)hipStreamDestroy(istream_);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -886,21 +880,11 @@ void SphGpuSingle::RunCellDivide() {
     Repartition();
   if (slab() && exchange_armed_) Exchange();
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET);
-  bool items_done = false;
   if (inc_ok_ && inc_valid_) {
-    // the previous order merged with the particles whose box changed (sph_divide.hip); the
-    // item build needs only the new begincell, so it runs on the side stream beside the push
+    // the previous order merged with the particles whose box changed (sph_divide.hip)
     launch_divide_inc(stream, cap_, sc_, cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_, G, begincell_,
-                      begincell_alt_, inc_, nn_ ? phaseeos_ : nullptr, tiled_ ? iev_boxes_ : nullptr);
+                      begincell_alt_, inc_, nn_ ? phaseeos_ : nullptr);
     std::swap(begincell_, begincell_alt_);
-    if (tiled_) {
-      check_hip(hipStreamWaitEvent(istream_, iev_boxes_, 0), "items: wait divide");
-      launch_items(istream_, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv);  // also zeroes the queues
-      check_hip(hipEventRecord(iev_items_, istream_), "items: record");
-      check_hip(hipStreamWaitEvent(stream, iev_items_, 0), "items: join");
-      qfresh_ = true;
-      items_done = true;
-    }
   } else {
     launch_presort(stream, cap_, sc_, cur_.dcell, cur_.code, G, C.dom_cellcode, sort_.keys[0], sort_.vals[0]);
     const int res = launch_radix_sort(stream, cap_, sc_, sort_, keybits_);
@@ -913,7 +897,7 @@ void SphGpuSingle::RunCellDivide() {
   }
   inc_valid_ = inc_ok_;
   std::swap(cur_, alt_);
-  if (tiled_ && !items_done) {
+  if (tiled_) {
     launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv);  // also zeroes the queues
     qfresh_ = true;
   }

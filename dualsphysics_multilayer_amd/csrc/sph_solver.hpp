@@ -200,9 +200,6 @@ class SphGpuSingle {
   std::vector<Ev> pending_;
   std::vector<hipEvent_t> evpool_;
   hipEvent_t xev_ = nullptr;  // exchange: counts arrived on the host (spin-waited)
-  // item build beside the incremental divide's push (RunCellDivide): side stream + events
-  hipStream_t istream_ = nullptr;
-  hipEvent_t iev_boxes_ = nullptr, iev_items_ = nullptr;
   double phase_ms_[4] = {0, 0, 0, 0};
   uint64_t phase_n_[4] = {0, 0, 0, 0};
   hipEvent_t cur_a_ = nullptr;

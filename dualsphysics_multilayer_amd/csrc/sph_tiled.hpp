@@ -17,9 +17,6 @@ constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
 #ifndef SPH_TCAP
 #define SPH_TCAP 504
 #endif
-#ifndef SPH_STAGE_PRIO
-#define SPH_STAGE_PRIO 0  // >0: wave priority while staging neighbour rows (s_setprio)
-#endif
 #ifndef SPH_PAD
 #define SPH_PAD 8
 #endif
