@@ -20,8 +20,8 @@
 // pairs as one set (lanes with alike loop lengths; every other sum is order-free up to
 // rounding) and flags a heavier-phase neighbour; a block with a flagged lane then re-sweeps
 // its rows in the reference order for sx alone (nn_sx_sweep: phase interfaces only).  The
-// bound-p2 pass keeps the reference order throughout (its first no-shift pair freezes
-// every shifting sum).  cfg5: 1.85 -> 1.55 ms per interaction (SPH_NN_MIRROR=0: the
+// bound-p2 pass keeps the reference order when its first no-shift pair can freeze every
+// shifting sum (ShiftMode NoBound/NoFixed), else it is drained in mirrored units too.  cfg5: 1.85 -> 1.55 ms per interaction (SPH_NN_MIRROR=0: the
 // row-ordered drain of every pass).
 #include "sph_tiled.hpp"
 
@@ -404,13 +404,13 @@ __device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restr
     dry2 = ok2 ? dry2 : 0.f;
     drz2 = ok2 ? drz2 : 0.f;
     rr22 = ok2 ? rr22 : 1e30f;
-    const float4 C1 = sC.ld(j1, false), C2 = sC.ld(j2, false);
+    const float4 C1 = sC.ld(j1, KIND == 1), C2 = sC.ld(j2, KIND == 1);
     if (KIND == 2) {
       nn_bound_pair(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
       nn_bound_pair(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
     } else {
-      nn_pair<TVISCO, TDENSITY, SHIFT, false, false>(K, sph, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
-      nn_pair<TVISCO, TDENSITY, SHIFT, false, false>(K, sph, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
+      nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1, false>(K, sph, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
+      nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1, false>(K, sph, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
     }
   }
 }
@@ -429,8 +429,9 @@ __device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid&
                                                  const typecode* __restrict__ code, float4* __restrict__ sA,
                                                  float4* __restrict__ sB, NNSC sC,
                                                  const float4* __restrict__ sph, NNAcc& a) {
-  static_assert(KIND == 0 || KIND == 2, "fluid rows only (the bound pass keeps the reference order)");
-  const unsigned cellinit = g.boxfluid;
+  // KIND 1 (bound p2) only where no pair can freeze the shifting sums (no shifting, or
+  // ShiftMode Full): the caller keeps the reference order otherwise
+  const unsigned cellinit = KIND == 1 ? 0u : g.boxfluid;
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
   for (int u = 0; u < 5; u++) {
     const int dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
@@ -453,8 +454,8 @@ __device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid&
     if (n0 + n1 == 0u) continue;  // block-uniform
     if (n0 + n1 <= unsigned(NN_TCAP)) {
       __syncthreads();
-      if (n0) nn_stage(K, rs[0], n0, rc.xo, dya, dza, false, poscell, velrhop, press, code, sA, sB, sC, 0u);
-      if (n1) nn_stage(K, rs[1], n1, rc.xo, -dya, -dza, false, poscell, velrhop, press, code, sA, sB, sC, n0);
+      if (n0) nn_stage(K, rs[0], n0, rc.xo, dya, dza, KIND == 1, poscell, velrhop, press, code, sA, sB, sC, 0u);
+      if (n1) nn_stage(K, rs[1], n1, rc.xo, -dya, -dza, KIND == 1, poscell, velrhop, press, code, sA, sB, sC, n0);
       __syncthreads();
       const int wa0 = int(ls[0] - rs[0]), wa1 = rc.act && n0 ? int(le[0] - rs[0]) : wa0;
       const int wb0 = int(n0 + ls[1] - rs[1]), wb1 = rc.act && n1 ? int(n0 + le[1] - rs[1]) : wb0;
@@ -473,7 +474,7 @@ __device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid&
         for (unsigned seg = rs[k]; seg < re[k]; seg += NN_TCAP) {
           const unsigned segn = min(unsigned(NN_TCAP), re[k] - seg);
           __syncthreads();
-          nn_stage(K, seg, segn, rc.xo, dy, dz, false, poscell, velrhop, press, code, sA, sB, sC, 0u);
+          nn_stage(K, seg, segn, rc.xo, dy, dz, KIND == 1, poscell, velrhop, press, code, sA, sB, sC, 0u);
           __syncthreads();
           const int w0 = int(max(ls[k], seg) - seg);
           const int w1 = rc.act ? max(w0, int(min(le[k], seg + segn)) - int(seg)) : w0;
@@ -677,7 +678,17 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
       b.sy = f.sy;
       b.sz = f.sz;
       b.sw = f.sw;
+#if SPH_NN_MIRROR
+      // the first no-shift bound pair (ShiftMode NoBound/NoFixed) freezes every shifting sum:
+      // only then is the bound pass order-dependent (uniform branch)
+      if (SHIFT && (K.shiftmode == 1 || K.shiftmode == 2))
+        nn_pass<TVISCO, TDENSITY, SHIFT, 1>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, b);
+      else
+        nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 1>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
+                                                     sph, b);
+#else
       nn_pass<TVISCO, TDENSITY, SHIFT, 1>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, b);
+#endif
       if (act) {
         // the two CPU passes' stores (JSphCpu_NN_FDA.cpp:278-296).  With shifting configured
         // the reference instantiates every interaction with shift=true (the predictor's too,
