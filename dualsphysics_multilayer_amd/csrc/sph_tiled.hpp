@@ -148,9 +148,18 @@ __device__ __forceinline__ unsigned lane_order(const float4* __restrict__ poscel
 #ifndef SPH_ITEM_SPLIT
 #define SPH_ITEM_SPLIT 1
 #endif
+#ifndef SPH_ITEM_RR
+#define SPH_ITEM_RR 0  // 1: group g takes every 8th item from g (balanced groups, no spatial contiguity)
+#endif
 struct ItemGroup {
   unsigned flo, nfg, blo, n;  // fluid range [flo, flo+nfg), then bound items from blo; n in all
-  __device__ __forceinline__ unsigned item(unsigned c) const { return c < nfg ? flo + c : blo + (c - nfg); }
+  __device__ __forceinline__ unsigned item(unsigned c) const {
+#if SPH_ITEM_RR
+    return c < nfg ? flo + 8u * c : blo + 8u * (c - nfg);
+#else
+    return c < nfg ? flo + c : blo + (c - nfg);
+#endif
+  }
 };
 struct ItemGroups {
   unsigned nf, nb;
@@ -164,8 +173,15 @@ struct ItemGroups {
     nf = n - nb;
   }
   __device__ __forceinline__ ItemGroup group(unsigned g) const {
-    const unsigned pf = (nf + 7u) / 8u, pb = (nb + 7u) / 8u;
     ItemGroup r;
+#if SPH_ITEM_RR
+    r.flo = g;
+    r.nfg = g < nf ? (nf - g + 7u) / 8u : 0u;
+    r.blo = nf + g;
+    r.n = r.nfg + (g < nb ? (nb - g + 7u) / 8u : 0u);
+    return r;
+#endif
+    const unsigned pf = (nf + 7u) / 8u, pb = (nb + 7u) / 8u;
     r.flo = min(nf, g * pf);
     r.nfg = min(nf, r.flo + pf) - r.flo;
     r.blo = nf + min(nb, g * pb);
