@@ -141,15 +141,19 @@ __device__ __forceinline__ unsigned lane_order(const float4* __restrict__ poscel
 }
 
 // The per-XCD-group work of a tiled interaction: the item list is [fluid-row items | bound-row
-// items] in spatial order; group g takes the g-th eighth of the fluid items, then the g-th
-// eighth of the bound items (most of them cheap: no fluid in reach, or continuity only), so
-// every group ends on short items and the blocks' last items finish closer together
-// (SPH_ITEM_SPLIT 0: eighths of the whole list, the bound items all in the last groups).
+// items] in spatial order; group g takes every 8th fluid item from g, then every 8th bound
+// item from g (most of them cheap: no fluid in reach, or continuity only).  The groups'
+// loads are then alike and every group ends on short items, so the blocks' last items
+// finish close together.  Measured (three alternating A/B runs each): contiguous eighths of
+// the whole list (the bound items all in the last groups) -> eighths of the fluid, then of
+// the bound items: cfg5 1.502 -> 1.446 ms, cfg2 0.671 -> 0.665; -> round-robin: cfg2
+// 0.666 -> 0.638 ms, cfg5 unchanged.  The XCD-local spatial contiguity of a group's items
+// was worth less than the balance (neighbour rows are MALL hits either way).
 #ifndef SPH_ITEM_SPLIT
-#define SPH_ITEM_SPLIT 1
+#define SPH_ITEM_SPLIT 1  // 0: the bound items are not split from the fluid ones
 #endif
 #ifndef SPH_ITEM_RR
-#define SPH_ITEM_RR 0  // 1: group g takes every 8th item from g (balanced groups, no spatial contiguity)
+#define SPH_ITEM_RR 1  // 0: group g takes the g-th contiguous eighth (of the fluid, then of the bound items)
 #endif
 struct ItemGroup {
   unsigned flo, nfg, blo, n;  // fluid range [flo, flo+nfg), then bound items from blo; n in all
