@@ -148,48 +148,47 @@ __device__ __forceinline__ unsigned lane_order(const float4* __restrict__ poscel
 // the whole list (the bound items all in the last groups) -> eighths of the fluid, then of
 // the bound items: cfg5 1.502 -> 1.446 ms, cfg2 0.671 -> 0.665; -> round-robin: cfg2
 // 0.666 -> 0.638 ms, cfg5 unchanged.  The XCD-local spatial contiguity of a group's items
-// was worth less than the balance (neighbour rows are MALL hits either way).
-#ifndef SPH_ITEM_SPLIT
-#define SPH_ITEM_SPLIT 1  // 0: the bound items are not split from the fluid ones
+// was worth less than the balance (neighbour rows are MALL hits either way).  Dealt in
+// chunks of 16 consecutive items (chunks of 1, 4, 16: same time) the L2-miss traffic of
+// the cfg2 interaction is 228 MB per launch instead of 397 MB.
+#ifndef SPH_ITEM_CHUNK
+#define SPH_ITEM_CHUNK 16  // round-robin granularity in items (a power of two)
 #endif
-#ifndef SPH_ITEM_RR
-#define SPH_ITEM_RR 1  // 0: group g takes the g-th contiguous eighth (of the fluid, then of the bound items)
-#endif
-struct ItemGroup {
-  unsigned flo, nfg, blo, n;  // fluid range [flo, flo+nfg), then bound items from blo; n in all
-  __device__ __forceinline__ unsigned item(unsigned c) const {
-#if SPH_ITEM_RR
-    return c < nfg ? flo + 8u * c : blo + 8u * (c - nfg);
-#else
-    return c < nfg ? flo + c : blo + (c - nfg);
-#endif
+// Items of one kind (fluid or bound) dealt to the 8 groups round-robin in chunks of CH.
+struct ItemDeal {
+  unsigned lo, n;  // the kind's list range [lo, lo + n)
+  __device__ __forceinline__ unsigned count(unsigned g) const {
+    constexpr unsigned CH = SPH_ITEM_CHUNK;
+    const unsigned nch = (n + CH - 1u) / CH;
+    if (g >= nch) return 0u;
+    unsigned c = ((nch - g + 7u) / 8u) * CH;
+    if ((nch - 1u) % 8u == g) c -= nch * CH - n;  // the kind's last chunk is short
+    return c;
   }
+  __device__ __forceinline__ unsigned item(unsigned g, unsigned c) const {
+    constexpr unsigned CH = SPH_ITEM_CHUNK;
+    return lo + (g + 8u * (c / CH)) * CH + (c % CH);
+  }
+};
+struct ItemGroup {
+  ItemDeal f, b;
+  unsigned g, nfg, n;
+  __device__ __forceinline__ unsigned item(unsigned c) const { return c < nfg ? f.item(g, c) : b.item(g, c - nfg); }
 };
 struct ItemGroups {
   unsigned nf, nb;
   __device__ __forceinline__ explicit ItemGroups(const DevScalars* sc) {
     const unsigned n = sc->nitems;
-#if SPH_ITEM_SPLIT
     nb = min(sc->nitems_bound, n);
-#else
-    nb = 0u;
-#endif
     nf = n - nb;
   }
   __device__ __forceinline__ ItemGroup group(unsigned g) const {
     ItemGroup r;
-#if SPH_ITEM_RR
-    r.flo = g;
-    r.nfg = g < nf ? (nf - g + 7u) / 8u : 0u;
-    r.blo = nf + g;
-    r.n = r.nfg + (g < nb ? (nb - g + 7u) / 8u : 0u);
-    return r;
-#endif
-    const unsigned pf = (nf + 7u) / 8u, pb = (nb + 7u) / 8u;
-    r.flo = min(nf, g * pf);
-    r.nfg = min(nf, r.flo + pf) - r.flo;
-    r.blo = nf + min(nb, g * pb);
-    r.n = r.nfg + (nf + min(nb, (g + 1u) * pb) - r.blo);
+    r.f = {0u, nf};
+    r.b = {nf, nb};
+    r.g = g;
+    r.nfg = r.f.count(g);
+    r.n = r.nfg + r.b.count(g);
     return r;
   }
 };
