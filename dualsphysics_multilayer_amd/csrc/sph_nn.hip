@@ -593,13 +593,20 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
   for (unsigned q = 0; q < 8; q++) {
     const unsigned xg = (grp + q) & 7;
     const ItemGroup gr = IG.group(xg);
+    // the group's first nst items go one to each of its own blocks without an atomic (all
+    // blocks claiming at once queued ~256 same-line atomics per counter); the counter deals
+    // the rest
+    const unsigned nst = (gridDim.x - xg + 7u) / 8u;
+    bool first = q == 0;
     for (;;) {
       // a group known to be exhausted (counters only grow; a stale read is smaller) costs
       // no atomic: probing all 8 queues was ~16k same-line atomics per launch
       if (threadIdx.x == 0)
-        s_item = (__hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gr.n)
+        s_item = first ? (blockIdx.x >> 3)
+                 : (nst + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gr.n)
                      ? gr.n
-                     : atomicAdd(&qctr[xg * QSTRIDE], 1u);
+                     : nst + atomicAdd(&qctr[xg * QSTRIDE], 1u);
+      first = false;
       __syncthreads();
       const unsigned c = s_item;
       __syncthreads();
