@@ -675,6 +675,9 @@ __device__ __forceinline__ TAcc pass_s(const KConst& K, const DivGrid& g, const 
                                              dstop0);
 }
 
+#if SPH_TAIL_DBG
+__device__ unsigned long long g_taildbg[3 * 4096];
+#endif
 template <int TDENSITY, bool FT = false, int S = 1>
 __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
                                                     unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
@@ -693,6 +696,10 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
   const ItemGroups IG(sc);
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f;
+#if SPH_TAIL_DBG
+  const unsigned long long tdbg0 = wall_clock64();
+  unsigned ndbg = 0;
+#endif
   const float cvisc_f = -K.visco * K.cs0f * K.kernelh * K.massfluid;
   const float cvisc_b = -K.viscobound * K.cs0f * K.kernelh * K.massbound;
 
@@ -719,6 +726,9 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
       if (c >= gr.n) break;
       const unsigned it = gr.item(c);
       const uint4 item = items[it];
+#if SPH_TAIL_DBG
+      ndbg++;
+#endif
       const bool bitem = (item.x & ITEM_BOUND) != 0u;
       const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
       const int a = int(item.y & 0xffffu), b = int(item.y >> 16);
@@ -811,6 +821,16 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
       }
     }
   }
+#if SPH_TAIL_DBG  // diagnostic: start/end of every block of one launch (100 MHz wall clock), printed next step
+  if (threadIdx.x == 0 && sc->nstep == 12 && blockIdx.x < 4096) {
+    g_taildbg[3 * blockIdx.x] = tdbg0;
+    g_taildbg[3 * blockIdx.x + 1] = wall_clock64();
+    g_taildbg[3 * blockIdx.x + 2] = ndbg;
+  }
+  if (threadIdx.x == 0 && blockIdx.x == 0 && sc->nstep == 13)
+    for (unsigned i = 0; i < min(gridDim.x, 4096u); i++)
+      printf("TAILDBG %u %llu %llu %llu\n", i, g_taildbg[3 * i], g_taildbg[3 * i + 1], g_taildbg[3 * i + 2]);
+#endif
   wave_max_atomic(sc, RED_VISCDT, viscmax);
   wave_max_atomic(sc, RED_ACEMAX2, ace2max);
   // (the queue counters are zeroed by k_items_scan, or by the solver before an interaction

@@ -17,6 +17,9 @@ constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
 #ifndef SPH_TCAP
 #define SPH_TCAP 504
 #endif
+#ifndef SPH_TAIL_DBG
+#define SPH_TAIL_DBG 0  // 1: print every block's start/end clock of one k_fluid_tiled launch
+#endif
 #ifndef SPH_PAD
 #define SPH_PAD 8
 #endif
