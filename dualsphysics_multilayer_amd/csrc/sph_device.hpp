@@ -96,8 +96,6 @@ struct DivGrid {
   unsigned nctt;        // size of begincell = 2*nct + 6
   unsigned boxdiscard;  // ghosts of the previous divide and particles handed to a neighbour
   int xoff, xown0, xown1;
-  unsigned itemcapg;    // item slots per region of the interaction's item list (k_items)
-  unsigned itemset;     // counter set of the last item build (alternates by build)
 };
 
 // dcell markers: excluded particle (JSphCpu::UpdatePos, JSphCpu.cpp:1262) and a
@@ -124,7 +122,7 @@ struct DevScalars {
 // RED_VISCETA: NN max effective viscosity (ViscEtaDtMax, JSphCpuSingle.cpp:633 in the v5.0 solver)
 constexpr int RED_VELMAX2 = 0, RED_ACEMAX2 = 1, RED_VISCDT = 2, RED_VISCETA = 3, RED_SLOTS = 64;
 
-constexpr unsigned ERR_DT_NAN = 1u, ERR_BOUNDOUT = 2u, ERR_HALO = 4u, ERR_ITEMS = 8u;
+constexpr unsigned ERR_DT_NAN = 1u, ERR_BOUNDOUT = 2u, ERR_HALO = 4u;
 
 // Wave-level max of a non-negative float, then one atomicMax per wave into a slot
 // chosen by the wave's global index (64 slots).

@@ -33,173 +33,144 @@ namespace sphx {
 // particles of one row (the row's last item shorter), cut earlier only where it would
 // span more than TMAXCELLS x-cells; items may start and end inside a cell.  Full items
 // keep both waves of a block busy (cell-aligned items averaged 103 of 128 lanes at 1M)
-// and make the lanes' candidate counts more alike.
-// One launch: a block of IT_WAVES waves takes IT_WAVES consecutive fluid rows (blocks
-// [0, nbk)) or bound rows (blocks [nbk, 2 nbk)); each wave copies its row's cell begin
-// offsets to LDS and lane 0 walks the row's items into LDS (a row of > IT_BUF items walks
-// again for the rest), the wave copies them to the block's slots: ONE atomic append per
-// block into the counter of its region (8 fluid regions of consecutive blocks, then 8
-// bound ones; ItemList in sph_tiled.hpp).  Device-scope atomics on one line serialize at
-// ~0.1 us each: one append per row cost 62 us at 1M, one per block 12.9 us, against 25 us
-// for the count + one-block scan + write kernels it replaces.  Within a region the blocks'
-// runs follow their completion order; no result depends on it (every p1 is summed by one
-// lane of the item that holds it, over its own candidates in a fixed order; the maxima are
-// order-free), and with the items dealt to the XCD groups round-robin the interaction does
-// not need spatial order either.  The counters alternate between two sets by build
-// (g.itemset): a build appends to its set and zeroes the other, which the previous build's
-// interactions (finished, stream order) read.
+// and make the lanes' candidate counts more alike.  One wave per row copies the row's
+// cell begin offsets to LDS, then lane 0 walks the items; the count and write passes
+// run the same walk, so the list is deterministic and in spatial (z, y, x) order, fluid
+// items first.
 constexpr int ROWCELLS_LDS = 1024;
-constexpr int IT_WAVES = 8;
-constexpr int IT_BUF = 64;  // items of a row kept in LDS by the counting walk (a longer row walks twice)
 
-__global__ __launch_bounds__(64 * IT_WAVES) void k_items(const unsigned* __restrict__ bc, DivGrid g, int tmaxc,
-                                                         DevScalars* __restrict__ sc, unsigned* __restrict__ qctr,
-                                                         uint4* __restrict__ items) {
-  __shared__ unsigned pre_all[IT_WAVES][ROWCELLS_LDS + 1];  // begin offset of every cell of the row, + row end
-  __shared__ unsigned short nz_all[IT_WAVES][ROWCELLS_LDS + 1];  // first non-empty owned cell >= x (xend if none)
-  __shared__ uint4 s_item[IT_WAVES][IT_BUF];
-  __shared__ unsigned s_n[IT_WAVES], s_off[IT_WAVES + 1];
-  const unsigned lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-  if (blockIdx.x == 0 && threadIdx.x < 8 + NREGIONS) {
-    // the interaction's item queues, and the other counter set, start over
-    if (threadIdx.x < 8) qctr[threadIdx.x * QSTRIDE] = 0u;
-    else qctr[(QAPP + NREGIONS * (g.itemset ^ 1u) + (threadIdx.x - 8u)) * QSTRIDE] = 0u;
-  }
-  unsigned* pre = pre_all[w];
-  unsigned short* nzfrom = nz_all[w];
+template <bool WRITE>
+__global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ bc, DivGrid g, int tmaxc,
+                                                   unsigned* __restrict__ counts, uint4* __restrict__ items) {
+  __shared__ unsigned pre[ROWCELLS_LDS + 1];            // begin offset of every cell of the row, + row end
+  __shared__ unsigned short nzfrom[ROWCELLS_LDS + 1];  // first non-empty owned cell >= x (xend if none)
   const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
-  // blocks [0, nbk) take the fluid rows, blocks [nbk, 2 nbk) the bound rows, IT_WAVES each
-  const unsigned nbk = (nrows + IT_WAVES - 1u) / IT_WAVES;
-  const bool bound = blockIdx.x >= nbk;
-  const unsigned bb = bound ? blockIdx.x - nbk : blockIdx.x;
-  const unsigned rr0 = bb * IT_WAVES + w;
-  const bool valid = rr0 < nrows;
-  const unsigned rr = valid ? rr0 : 0u;
+  const unsigned r = blockIdx.x;
+  const bool bound = r >= nrows;
+  const unsigned rr = bound ? r - nrows : r;
   const unsigned y = rr % unsigned(g.ncy), z = rr / unsigned(g.ncy);
   const unsigned rowbase = (bound ? 0u : g.boxfluid) + z * g.nsheet + y * unsigned(g.ncx);
-  const unsigned grp = (bound ? 8u : 0u) + (bb * 8u) / nbk;  // region: 8 fluid, then 8 bound
   const int ncx = g.ncx;
   // p1 only in the owned columns (slab ghosts are neighbours, never p1).
-  const int xbeg = g.xown0, xend = valid ? g.xown1 : g.xown0;  // an invalid wave walks an empty row
-  const bool lds = ncx <= ROWCELLS_LDS;  // very long rows: the same walk on global memory, cell by cell
-  if (lds) {
-    if (valid)
-      for (int x = int(lane); x <= ncx; x += 64) pre[x] = bc[rowbase + x];
-    __syncthreads();
-    // first non-empty owned cell at or after x: lane-local blocks, then a wave suffix-min
-    const int per = (ncx + 63) / 64, x0 = int(lane) * per, x1 = min(x0 + per, ncx);
-    int nz = xend;
-    if (valid)
-      for (int x = x1 - 1; x >= x0; x--) {
-        if (x >= xbeg && x < xend && pre[x + 1] > pre[x]) nz = x;
-        nzfrom[x] = (unsigned short)nz;
-      }
-    int suf = nz;
+  const int xbeg = g.xown0, xend = g.xown1;
+  uint4* out = WRITE ? items + counts[r] : nullptr;
+  unsigned nitems = 0;
+  auto emit = [&](int a, int e, unsigned p, unsigned q) {
+    if (WRITE)
+      out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(e) << 16), p, q);
+    nitems++;
+  };
+  if (ncx > ROWCELLS_LDS) {  // very long rows: the same walk on global memory, cell by cell
+    if (threadIdx.x != 0) return;
+    auto PRE = [&](int x) -> unsigned { return bc[rowbase + x]; };
+    unsigned p = PRE(xbeg);
+    const unsigned pend = PRE(xend);
+    int c = xbeg;
+    while (p < pend) {
+      while (PRE(c + 1) <= p) c++;
+      const unsigned q = min(min(p + unsigned(TB), pend), PRE(min(c + tmaxc, xend)));
+      int e = c;
+      while (PRE(e + 1) < q) e++;
+      emit(c, e, p, q);
+      p = q;
+      c = e;
+    }
+    if (!WRITE) counts[r] = nitems;
+    return;
+  }
+  for (int x = int(threadIdx.x); x <= ncx; x += 64) pre[x] = bc[rowbase + x];
+  __syncthreads();
+  // first non-empty owned cell at or after x: lane-local blocks, then a wave suffix-min
+  const int per = (ncx + 63) / 64, x0 = int(threadIdx.x) * per, x1 = min(x0 + per, ncx);
+  int nz = xend;
+  for (int x = x1 - 1; x >= x0; x--) {
+    if (x >= xbeg && x < xend && pre[x + 1] > pre[x]) nz = x;
+    nzfrom[x] = (unsigned short)nz;
+  }
+  int suf = nz;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int v = __shfl_down(suf, off, 64);
-      if (int(lane) + off < 64) suf = min(suf, v);
-    }
-    const int later = __shfl_down(suf, 1, 64);
-    const int carry = int(lane) < 63 ? later : xend;
-    if (valid) {
-      for (int x = x0; x < x1; x++)
-        if (int(nzfrom[x]) == xend) nzfrom[x] = (unsigned short)carry;
-      if (lane == 63) nzfrom[ncx] = (unsigned short)xend;
-    }
-    __syncthreads();
+  for (int off = 1; off < 64; off <<= 1) {
+    const int v = __shfl_down(suf, off, 64);
+    if (int(threadIdx.x) + off < 64) suf = min(suf, v);
   }
-  for (int pass = 0; pass < 2; pass++) {  // 0: count (items kept in LDS), 1: write at the block's slots
-    unsigned base = 0;
-    if (pass) {
-      __syncthreads();  // s_n, s_item complete
-      if (threadIdx.x == 0) {
-        unsigned tot = 0;
-        for (int i = 0; i < IT_WAVES; i++) {
-          s_off[i] = tot;
-          tot += s_n[i];
-        }
-        unsigned off = tot ? atomicAdd(&qctr[(QAPP + NREGIONS * g.itemset + grp) * QSTRIDE], tot) : 0u;
-        if (off + tot > g.itemcapg) {  // cannot happen with the host's bound; never write past it
-          atomicOr(&sc->error_flags, ERR_ITEMS);
-          off = ~0u;
-        }
-        s_off[IT_WAVES] = off;
-      }
-      __syncthreads();
-      if (s_off[IT_WAVES] == ~0u) return;
-      base = grp * g.itemcapg + s_off[IT_WAVES] + s_off[w];
-      const unsigned n = s_n[w];
-      for (unsigned i = lane; i < min(n, unsigned(IT_BUF)); i += 64) items[base + i] = s_item[w][i];
-      if (n <= unsigned(IT_BUF)) continue;  // wave-uniform: only a long row walks again
+  const int later = __shfl_down(suf, 1, 64);
+  const int carry = int(threadIdx.x) < 63 ? later : xend;
+  for (int x = x0; x < x1; x++)
+    if (int(nzfrom[x]) == xend) nzfrom[x] = (unsigned short)carry;
+  if (threadIdx.x == 63) nzfrom[ncx] = (unsigned short)xend;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  // Walk the items: the cell holding p is known (c), the cell holding q-1 is at most
+  // TMAXCELLS-1 cells further, an item ending at a cell end jumps to the next non-empty.
+  // The five offsets pre[c..c+4] of an item are independent LDS reads (one latency);
+  // the cell holding q-1 is c + #{k = 1..3 : pre[c+k] <= q-1}.
+  static_assert(TMAXCELLS == 4, "the walk reads pre[c..c+4]");
+  const unsigned pend = pre[xend];
+  int c = nzfrom[xbeg];
+  unsigned p = c < xend ? pre[c] : pend;
+  if (tmaxc != TMAXCELLS) {  // CellMode=half: longer items, the cell holding q-1 by a short scan
+    while (p < pend) {
+      const unsigned q = min(min(p + unsigned(TB), pend), pre[min(c + tmaxc, xend)]);
+      int e = c;
+      while (pre[e + 1] <= q - 1) e++;
+      emit(c, e, p, q);
+      p = q;
+      c = pre[e + 1] == q ? int(nzfrom[e + 1]) : e;
     }
-    if (lane != 0) continue;
-    unsigned nitems = 0;
-    auto emit = [&](int a, int e, unsigned p, unsigned q) {
-      const uint4 v = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(e) << 16), p, q);
-      if (!pass) {
-        if (nitems < unsigned(IT_BUF)) s_item[w][nitems] = v;
-      } else if (nitems >= unsigned(IT_BUF)) {
-        items[base + nitems] = v;
-      }
-      nitems++;
-    };
-    if (!valid) {
-    } else if (!lds) {
-      auto PRE = [&](int x) -> unsigned { return bc[rowbase + x]; };
-      unsigned p = PRE(xbeg);
-      const unsigned pend = PRE(xend);
-      int c = xbeg;
-      while (p < pend) {
-        while (PRE(c + 1) <= p) c++;
-        const unsigned q = min(min(p + unsigned(TB), pend), PRE(min(c + tmaxc, xend)));
-        int e = c;
-        while (PRE(e + 1) < q) e++;
-        emit(c, e, p, q);
-        p = q;
-        c = e;
-      }
-    } else {
-      // Walk the items: the cell holding p is known (c), the cell holding q-1 is at most
-      // TMAXCELLS-1 cells further, an item ending at a cell end jumps to the next non-empty.
-      // The five offsets pre[c..c+4] of an item are independent LDS reads (one latency);
-      // the cell holding q-1 is c + #{k = 1..3 : pre[c+k] <= q-1}.
-      static_assert(TMAXCELLS == 4, "the walk reads pre[c..c+4]");
-      const unsigned pend = pre[xend];
-      int c = nzfrom[xbeg];
-      unsigned p = c < xend ? pre[c] : pend;
-      if (tmaxc != TMAXCELLS) {  // CellMode=half: longer items, the cell holding q-1 by a short scan
-        while (p < pend) {
-          const unsigned q = min(min(p + unsigned(TB), pend), pre[min(c + tmaxc, xend)]);
-          int e = c;
-          while (pre[e + 1] <= q - 1) e++;
-          emit(c, e, p, q);
-          p = q;
-          c = pre[e + 1] == q ? int(nzfrom[e + 1]) : e;
-        }
-      } else {
-        while (p < pend) {
-          const unsigned p1 = pre[min(c + 1, xend)], p2 = pre[min(c + 2, xend)], p3 = pre[min(c + 3, xend)];
-          const unsigned p4 = pre[min(c + 4, xend)];
-          const unsigned q = min(min(p + unsigned(TB), pend), p4);
-          const int e = c + int(p1 <= q - 1) + int(p2 <= q - 1) + int(p3 <= q - 1);
-          emit(c, e, p, q);
-          p = q;
-          const unsigned pe1 = e + 1 - c == 1 ? p1 : e + 1 - c == 2 ? p2 : e + 1 - c == 3 ? p3 : p4;
-          c = pe1 == q ? int(nzfrom[e + 1]) : e;
-        }
-      }
-    }
-    if (!pass) s_n[w] = nitems;
+    if (!WRITE) counts[r] = nitems;
+    return;
   }
+  while (p < pend) {
+    const unsigned p1 = pre[min(c + 1, xend)], p2 = pre[min(c + 2, xend)], p3 = pre[min(c + 3, xend)];
+    const unsigned p4 = pre[min(c + 4, xend)];
+    const unsigned q = min(min(p + unsigned(TB), pend), p4);
+    const int e = c + int(p1 <= q - 1) + int(p2 <= q - 1) + int(p3 <= q - 1);
+    emit(c, e, p, q);
+    p = q;
+    const unsigned pe1 = e + 1 - c == 1 ? p1 : e + 1 - c == 2 ? p2 : e + 1 - c == 3 ? p3 : p4;
+    c = pe1 == q ? int(nzfrom[e + 1]) : e;
+  }
+  if (!WRITE) counts[r] = nitems;
 }
 
-void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, uint4* items, unsigned* qctr,
-                  int scelldiv) {
+// Exclusive scan of the per-row item counts (one block) -> item offsets, total; zeroes
+// the per-XCD work queues of the next interaction.
+__global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ counts, unsigned nrows2,
+                                                     DevScalars* __restrict__ sc, unsigned* __restrict__ qctr) {
+  __shared__ unsigned part[1024];
+  if (threadIdx.x < 8) qctr[threadIdx.x * QSTRIDE] = 0u;  // the interaction's item queues start over
+  const unsigned per = (nrows2 + 1023) / 1024;
+  const unsigned b0 = threadIdx.x * per, b1 = min(b0 + per, nrows2);
+  unsigned s = 0;
+  for (unsigned i = b0; i < b1; i++) s += counts[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const unsigned v = (threadIdx.x >= unsigned(off) ? part[threadIdx.x - off] : 0u);
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  unsigned run = (threadIdx.x ? part[threadIdx.x - 1] : 0u);
+  for (unsigned i = b0; i < b1; i++) {
+    const unsigned v = counts[i];
+    counts[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == 1023) sc->nitems = part[1023];
+  __syncthreads();
+  // items of the bound rows (the list's tail): each XCD group takes its share of them
+  // after its fluid items (ItemGroups)
+  if (threadIdx.x == 0) sc->nitems_bound = part[1023] - counts[nrows2 / 2];
+}
+
+void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
+                  uint4* items, unsigned* qctr, int scelldiv) {
   const int tmaxc = scelldiv == 1 ? TMAXCELLS : TMAXCELLS_HALF;
-  const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
-  const unsigned nb = 2u * ((nrows + IT_WAVES - 1) / IT_WAVES);
-  hipLaunchKernelGGL(k_items, dim3(nb), dim3(64 * IT_WAVES), 0, stm, begincell, g, tmaxc, sc, qctr, items);
+  const unsigned nrows2 = 2u * unsigned(g.ncy) * unsigned(g.ncz);
+  hipLaunchKernelGGL(k_items_rows<false>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, nullptr);
+  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, rowtmp, nrows2, sc, qctr);
+  hipLaunchKernelGGL(k_items_rows<true>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, items);
 }
 
 // ------------------------------------------------------------------------------------
@@ -719,12 +690,10 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
   __shared__ float4 sA[tcap + SPH_PAD];  // over-read pad of the 8-wide candidate test (<= 7 records)
   __shared__ float4 sB[tcap];
   __shared__ typename CRecT<FT>::type sC[tcap];  // press/rho, 1/rho (FT: mass-scaled + kind)
-  __shared__ unsigned s_item, s_slot;
-  __shared__ unsigned s_pre[NREGIONS + 1];  // item list region prefix (item_list_init)
+  __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];  // lane -> p1 of the item (see lane_order)
   __shared__ unsigned s_nwave[4];
-  item_list_init(qctr, g, s_pre);
-  const ItemGroups IG(s_pre[8], s_pre[NREGIONS] - s_pre[8]);
+  const ItemGroups IG(sc);
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f;
 #if SPH_TAIL_DBG
@@ -745,21 +714,18 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
     for (;;) {
       // a group known to be exhausted (counters only grow; a stale read is smaller) costs
       // no atomic: probing all 8 queues was ~16k same-line atomics per launch
-      if (threadIdx.x == 0) {
-        const unsigned cc = first ? (blockIdx.x >> 3)
-                            : (nst + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT) >= gr.n)
-                                ? gr.n
-                                : nst + atomicAdd(&qctr[xg * QSTRIDE], 1u);
-        s_item = cc;
-        s_slot = cc < gr.n ? item_slot(s_pre, g.itemcapg, gr.item(cc)) : 0u;  // one thread, prefix in LDS
-      }
+      if (threadIdx.x == 0)
+        s_item = first ? (blockIdx.x >> 3)
+                 : (nst + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gr.n)
+                     ? gr.n
+                     : nst + atomicAdd(&qctr[xg * QSTRIDE], 1u);
       first = false;
       __syncthreads();
-      const unsigned c = s_item, slot = s_slot;
+      const unsigned c = s_item;
       __syncthreads();
       if (c >= gr.n) break;
-      const uint4 item = items[slot];
+      const unsigned it = gr.item(c);
+      const uint4 item = items[it];
 #if SPH_TAIL_DBG
       ndbg++;
 #endif
@@ -867,7 +833,7 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
 #endif
   wave_max_atomic(sc, RED_VISCDT, viscmax);
   wave_max_atomic(sc, RED_ACEMAX2, ace2max);
-  // (the queue counters are zeroed by k_items, or by the solver before an interaction
+  // (the queue counters are zeroed by k_items_scan, or by the solver before an interaction
   // without a new item list)
 }
 

@@ -148,19 +148,14 @@ void launch_interaction(hipStream_t stm, unsigned cap, DevScalars* sc, const flo
 void launch_interaction_bound(hipStream_t stm, unsigned npbcap, DevScalars* sc, const float4* poscell,
                               const float4* velrhop, const unsigned* begincell, DivGrid g, const KConst& K,
                               float4* arace);
-// Work counters of the persistent tiled kernels (qctr), each on its own 128-B line
-// (device-scope atomics serialize per line): lines 0-7 the per-XCD-group item queues of the
-// interaction; lines QAPP + NREGIONS set + r the item build's append counter of region r,
-// in two sets alternating by build (k_items, DivGrid::itemset).
+// Work counters of the persistent tiled kernels (qctr): 8 per-XCD item queues + the
+// finished-block count, each on its own 128-B line (device-scope atomics serialize per line).
 constexpr int QSTRIDE = 32;
-constexpr int QAPP = 8;
-constexpr int NREGIONS = 16;  // item-list regions: 8 of fluid rows, then 8 of bound rows
-constexpr size_t QCTR_QUEUE_BYTES = 8 * QSTRIDE * sizeof(unsigned);
-constexpr size_t QCTR_BYTES = (QAPP + 2 * NREGIONS) * QSTRIDE * sizeof(unsigned);
+constexpr size_t QCTR_BYTES = 9 * QSTRIDE * sizeof(unsigned);
 // Tiled fluid interaction (sph_interaction_tiled.hip) and its per-divide item list.
 // scelldiv 1 (CellMode=full): items of <= 4 cells; 2 (half): <= TMAXCELLS_HALF half-cells.
-void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, uint4* items,
-                  unsigned* qctr, int scelldiv = 1);
+void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
+                  uint4* items, unsigned* qctr, int scelldiv = 1);
 // With floating bodies (ftmassp != nullptr) the staged p2 records carry their mass ratio
 // and kind (the FT instantiation; one more float2 of LDS per record).
 void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,

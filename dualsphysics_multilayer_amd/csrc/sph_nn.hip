@@ -35,7 +35,7 @@ namespace sphx {
 #define SPH_NN_POWSKIP 0  // 1: skip D^(n-1) when every lane's p2 phase has n = 1 (more spills here)
 #endif
 #ifndef SPH_NN_TCAP
-#define SPH_NN_TCAP 478
+#define SPH_NN_TCAP 480
 #endif
 constexpr int NN_TCAP = SPH_NN_TCAP;
 
@@ -583,13 +583,11 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
   __shared__ unsigned char sT[NN_TCAP];  // tag
   const NNSC sC = {sC2, sT};
   __shared__ float4 sph[2 * SPH_MAXPHASES];
-  __shared__ unsigned s_item, s_slot;
-  __shared__ unsigned s_pre[NREGIONS + 1];  // item list region prefix (item_list_init)
+  __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];
   __shared__ unsigned s_nwave[4];
   if (threadIdx.x < 2 * SPH_MAXPHASES) sph[threadIdx.x] = phases[threadIdx.x];
-  item_list_init(qctr, g, s_pre);
-  const ItemGroups IG(s_pre[8], s_pre[NREGIONS] - s_pre[8]);
+  const ItemGroups IG(sc);
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f, etamax = 0.f;
   for (unsigned q = 0; q < 8; q++) {
@@ -603,21 +601,18 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
     for (;;) {
       // a group known to be exhausted (counters only grow; a stale read is smaller) costs
       // no atomic: probing all 8 queues was ~16k same-line atomics per launch
-      if (threadIdx.x == 0) {
-        const unsigned cc = first ? (blockIdx.x >> 3)
-                            : (nst + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT) >= gr.n)
-                                ? gr.n
-                                : nst + atomicAdd(&qctr[xg * QSTRIDE], 1u);
-        s_item = cc;
-        s_slot = cc < gr.n ? item_slot(s_pre, g.itemcapg, gr.item(cc)) : 0u;  // one thread, prefix in LDS
-      }
+      if (threadIdx.x == 0)
+        s_item = first ? (blockIdx.x >> 3)
+                 : (nst + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gr.n)
+                     ? gr.n
+                     : nst + atomicAdd(&qctr[xg * QSTRIDE], 1u);
       first = false;
       __syncthreads();
-      const unsigned c = s_item, slot = s_slot;
+      const unsigned c = s_item;
       __syncthreads();
       if (c >= gr.n) break;
-      const uint4 item = items[slot];
+      const unsigned it = gr.item(c);
+      const uint4 item = items[it];
       const bool bitem = (item.x & ITEM_BOUND) != 0u;
       const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
       const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);

@@ -230,7 +230,7 @@ static KConst make_kconst(const SphConstants& c) {
 // A slab keeps the global y/z extent and the x-columns [c0-1, c1] (owned + one ghost
 // column per face).
 static DivGrid make_grid(const SphConstants& c, const SlabConfig* slab) {
-  DivGrid g{};
+  DivGrid g;
   g.ncx = int(c.dom_cells[0]);
   g.ncy = int(c.dom_cells[1]);
   g.ncz = int(c.dom_cells[2]);
@@ -411,6 +411,7 @@ void SphGpuSingle::AllocFixed() {
   if (slab()) {  // re-partition: column counts [2 ncx] + the ranks' bounds [nranks + 1]
     colcnt_ = (float*)dmalloc(4 * (2 * size_t(C.dom_cells[0]) + size_t(slabcfg_.nranks) + 1));
   }
+  rowtmp_ = (unsigned*)dmalloc(4 * 2 * size_t(G.ncy) * size_t(G.ncz));
   qctr_ = (unsigned*)dmalloc(QCTR_BYTES);
   check_hip(hipMemset(qctr_, 0, QCTR_BYTES), "zero work counters");
   sort_.digtot = (unsigned*)dmalloc(4 * (1u << RS_MAXBITS));
@@ -479,19 +480,9 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
   }
   poscell_ = (float4*)dmalloc(16 * n);
   press_ = (float*)dmalloc(4 * n);
-  // Interaction items (launch_items), in NREGIONS regions: an item holds TB particles
-  // unless it ends a row or reaches TMAXCELLS = 4 cells; a region holds the rows of 1/8 of
-  // the fluid (or bound) row blocks of k_items (<= 8 ceil(nrows / 64) + 8 rows) of <= the
-  // whole map's ncx + 2 cells (any slab after a re-partition), and any number of the n
-  // particles.
-  {
-    const size_t rpg = 8 * ((size_t(G.ncy) * size_t(G.ncz) + 63) / 64) + 8;
-    const size_t capg = n / 128 + rpg + rpg * (size_t(C.dom_cells[0]) + 2) / 2 + 2;
-    if (capg >= (1ull << 27)) throw SphError(SPH_ERR_ARG, "too many interaction items");
-    itemcapg_ = unsigned(capg);
-    G.itemcapg = itemcapg_;
-    items_ = (uint4*)dmalloc(16 * size_t(NREGIONS) * capg);
-  }
+  // Interaction items (launch_items): an item holds TB particles unless it ends a row
+  // (<= 2 per row: fluid and bound) or reaches TMAXCELLS = 4 cells (<= 1 per 4 cells).
+  items_ = (uint4*)dmalloc(16 * (n / 128 + 2 * size_t(G.ncy) * size_t(G.ncz) + size_t(nctmax_) / 2 + 2));
   arace_ = (float4*)dmalloc(16 * n);
   if (shift_) shiftpos_ = (float4*)dmalloc(16 * n);  // the interaction's shifting sums
   for (int i = 0; i < 2; i++) {
@@ -869,10 +860,7 @@ void SphGpuSingle::Repartition() {
   if (!changed) return;
   slabcfg_.c0 = nb[size_t(slabcfg_.rank)];
   slabcfg_.c1 = nb[size_t(slabcfg_.rank) + 1];
-  const unsigned itemset = G.itemset;
   G = make_grid(C, &slabcfg_);
-  G.itemcapg = itemcapg_;
-  G.itemset = itemset;
   keybits_ = bits_for(G.boxdiscard, 1);
   repart_count_++;
 }
@@ -910,8 +898,7 @@ void SphGpuSingle::RunCellDivide() {
   inc_valid_ = inc_ok_;
   std::swap(cur_, alt_);
   if (tiled_) {
-    G.itemset ^= 1u;  // this build's counter set (the interactions below read the same G)
-    launch_items(stream, sc_, begincell_, G, items_, qctr_, C.scelldiv);  // also zeroes the queues
+    launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv);  // also zeroes the queues
     qfresh_ = true;
   }
   if (nftp_) launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_, K, G);
@@ -937,7 +924,7 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
     TimedEnd(3);
   }
   if (tiled_ && !qfresh_)  // a second interaction on the same item list: queues start over
-    check_hip(hipMemsetAsync(qctr_, 0, QCTR_QUEUE_BYTES, stream), "zero work queues");
+    check_hip(hipMemsetAsync(qctr_, 0, QCTR_BYTES, stream), "zero work counters");
   qfresh_ = false;
   if (nn_) {
     // NN multiphase (sph_nn.hip); the shifting sums only where they are applied: the
@@ -1255,7 +1242,6 @@ void SphGpuSingle::CheckErrors() {
   if (s.error_flags & ERR_DT_NAN) throw SphError(SPH_ERR_DT, "The computed Dt is NaN or infinity");
   if (s.error_flags & ERR_HALO)
     throw SphError(SPH_ERR_UNSUPPORTED, "mDBC: a ghost node needs particles beyond the slab's ghost column");
-  if (s.error_flags & ERR_ITEMS) throw SphError(SPH_ERR_NOMEM, "interaction item list overflow");
 }
 
 unsigned SphGpuSingle::DtTrace(double* out, unsigned cap) {

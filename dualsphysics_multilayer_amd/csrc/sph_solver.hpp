@@ -140,8 +140,8 @@ class SphGpuSingle {
   float4* shiftpos_ = nullptr;  // shifting sums of the last interaction [cap]
   unsigned* begincell_ = nullptr;
   uint4* items_ = nullptr;        // tiled-interaction work items (per divide)
+  unsigned* rowtmp_ = nullptr;    // per-row item counts/offsets
   unsigned* qctr_ = nullptr;      // per-XCD-group work counters
-  unsigned itemcapg_ = 0;         // item slots per region of the item list
   unsigned nblocks_tiled_ = 2048;
   bool qfresh_ = false;  // the tiled kernels' work queues were zeroed by the last item build
   bool tiled_ = true;             // SPH_INTERACTION=simple selects the one-lane-per-particle kernel

@@ -15,7 +15,7 @@ namespace sphx {
 #endif
 constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
 #ifndef SPH_TCAP
-#define SPH_TCAP 503
+#define SPH_TCAP 504
 #endif
 #ifndef SPH_TAIL_DBG
 #define SPH_TAIL_DBG 0  // 1: print every block's start/end clock of one k_fluid_tiled launch
@@ -180,7 +180,11 @@ struct ItemGroup {
 };
 struct ItemGroups {
   unsigned nf, nb;
-  __device__ __forceinline__ ItemGroups(unsigned nfluid, unsigned nbound) : nf(nfluid), nb(nbound) {}
+  __device__ __forceinline__ explicit ItemGroups(const DevScalars* sc) {
+    const unsigned n = sc->nitems;
+    nb = min(sc->nitems_bound, n);
+    nf = n - nb;
+  }
   __device__ __forceinline__ ItemGroup group(unsigned g) const {
     ItemGroup r;
     r.f = {0u, nf};
@@ -191,29 +195,6 @@ struct ItemGroups {
     return r;
   }
 };
-
-// The item list of the last build (k_items): NREGIONS regions of g.itemcapg slots, region r
-// holding cnt[r] items (the build's counter set g.itemset); regions 0-7 hold the fluid
-// rows' items, 8-15 the bound rows'.  The interaction sees their concatenation as one list
-// of nf fluid then nb bound items (ItemGroups).  The region prefix stays in LDS and only the
-// thread that claims an item maps it to its slot (a prefix in registers of every thread
-// cost 14 SGPR spills to scratch).
-__device__ __forceinline__ void item_list_init(const unsigned* __restrict__ qctr, const DivGrid& g, unsigned* s_pre) {
-  if (threadIdx.x == 0) {
-    unsigned s = 0;
-    for (int r = 0; r < NREGIONS; r++) {
-      s_pre[r] = s;
-      s += qctr[(QAPP + NREGIONS * g.itemset + unsigned(r)) * QSTRIDE];
-    }
-    s_pre[NREGIONS] = s;
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ unsigned item_slot(const unsigned* s_pre, unsigned capg, unsigned v) {
-  unsigned r = 0;
-  for (int k = 1; k < NREGIONS; k++) r += v >= s_pre[k] ? 1u : 0u;
-  return r * capg + (v - s_pre[r]);
-}
 
 // Item geometry shared by the passes of one p1.
 struct RowCtx {
