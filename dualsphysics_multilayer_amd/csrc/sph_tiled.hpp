@@ -154,6 +154,9 @@ __device__ __forceinline__ unsigned lane_order(const float4* __restrict__ poscel
 // was worth less than the balance (neighbour rows are MALL hits either way).  Dealt in
 // chunks of 16 consecutive items (chunks of 1, 4, 16: same time) the L2-miss traffic of
 // the cfg2 interaction is 228 MB per launch instead of 397 MB.
+#ifndef SPH_ITEM_REV
+#define SPH_ITEM_REV 0
+#endif
 #ifndef SPH_ITEM_CHUNK
 #define SPH_ITEM_CHUNK 16  // round-robin granularity in items (a power of two)
 #endif
@@ -170,7 +173,11 @@ struct ItemDeal {
   }
   __device__ __forceinline__ unsigned item(unsigned g, unsigned c) const {
     constexpr unsigned CH = SPH_ITEM_CHUNK;
+#if SPH_ITEM_REV  // diagnostic: the kind's items in reverse order (top rows first)
+    return lo + (n - 1u - ((g + 8u * (c / CH)) * CH + (c % CH)));
+#else
     return lo + (g + 8u * (c / CH)) * CH + (c % CH);
+#endif
   }
 };
 struct ItemGroup {
