@@ -144,8 +144,9 @@ __device__ __forceinline__ unsigned lane_order(const float4* __restrict__ poscel
 }
 
 // The per-XCD-group work of a tiled interaction: the item list is [fluid-row items | bound-row
-// items] in spatial order; group g takes every 8th fluid item from g, then every 8th bound
-// item from g (most of them cheap: no fluid in reach, or continuity only).  The groups'
+// items] in spatial order; group g takes every 8th chunk of SPH_ITEM_CHUNK fluid items from
+// chunk g, then likewise of the bound items (most of them cheap: no fluid in reach, or
+// continuity only), its own first item statically (k_fluid_tiled / k_nn_tiled).  The groups'
 // loads are then alike and every group ends on short items, so the blocks' last items
 // finish close together.  Measured (three alternating A/B runs each): contiguous eighths of
 // the whole list (the bound items all in the last groups) -> eighths of the fluid, then of
@@ -155,7 +156,7 @@ __device__ __forceinline__ unsigned lane_order(const float4* __restrict__ poscel
 // chunks of 16 consecutive items (chunks of 1, 4, 16: same time) the L2-miss traffic of
 // the cfg2 interaction is 228 MB per launch instead of 397 MB.
 #ifndef SPH_ITEM_REV
-#define SPH_ITEM_REV 0
+#define SPH_ITEM_REV 0  // diagnostic: 1 deals each kind top rows first (+1.3 % at 1M)
 #endif
 #ifndef SPH_ITEM_CHUNK
 #define SPH_ITEM_CHUNK 16  // round-robin granularity in items (a power of two)
