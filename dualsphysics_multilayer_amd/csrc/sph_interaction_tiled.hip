@@ -53,26 +53,12 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
   const int ncx = g.ncx;
   // p1 only in the owned columns (slab ghosts are neighbours, never p1).
   const int xbeg = g.xown0, xend = g.xown1;
-  // counts/offsets: [fluid rows' full items | fluid rows' short items | bound rows' items]
-  // (short: < TB particles, a row's end or a sparse 4-cell run): the list puts the short
-  // fluid items after the full ones, so the XCD groups' last fluid items are the cheap ones
-  const unsigned cfull = bound ? 2u * nrows + rr : rr, cshort = bound ? cfull : nrows + rr;
-  uint4* outf = WRITE ? items + counts[cfull] : nullptr;
-  uint4* outs = WRITE ? items + counts[cshort] : nullptr;
-  unsigned nitems = 0, nfull = 0;
+  uint4* out = WRITE ? items + counts[r] : nullptr;
+  unsigned nitems = 0;
   auto emit = [&](int a, int e, unsigned p, unsigned q) {
-    const bool full = bound || q - p == unsigned(TB);
-    if (WRITE) {
-      const uint4 v = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(e) << 16), p, q);
-      if (full) outf[nfull] = v;
-      else outs[nitems - nfull] = v;
-    }
-    nfull += full ? 1u : 0u;
+    if (WRITE)
+      out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(e) << 16), p, q);
     nitems++;
-  };
-  auto put_counts = [&]() {
-    counts[cfull] = nfull;
-    if (!bound) counts[cshort] = nitems - nfull;
   };
   if (ncx > ROWCELLS_LDS) {  // very long rows: the same walk on global memory, cell by cell
     if (threadIdx.x != 0) return;
@@ -89,7 +75,7 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
       p = q;
       c = e;
     }
-    if (!WRITE) put_counts();
+    if (!WRITE) counts[r] = nitems;
     return;
   }
   for (int x = int(threadIdx.x); x <= ncx; x += 64) pre[x] = bc[rowbase + x];
@@ -131,7 +117,7 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
       p = q;
       c = pre[e + 1] == q ? int(nzfrom[e + 1]) : e;
     }
-    if (!WRITE) put_counts();
+    if (!WRITE) counts[r] = nitems;
     return;
   }
   while (p < pend) {
@@ -144,12 +130,11 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
     const unsigned pe1 = e + 1 - c == 1 ? p1 : e + 1 - c == 2 ? p2 : e + 1 - c == 3 ? p3 : p4;
     c = pe1 == q ? int(nzfrom[e + 1]) : e;
   }
-  if (!WRITE) put_counts();
+  if (!WRITE) counts[r] = nitems;
 }
 
-// Exclusive scan of the per-row item counts (one block; nrows2 = the 3 nrows counts of
-// k_items_rows) -> item offsets, total; zeroes the per-XCD work queues of the next
-// interaction.
+// Exclusive scan of the per-row item counts (one block) -> item offsets, total; zeroes
+// the per-XCD work queues of the next interaction.
 __global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ counts, unsigned nrows2,
                                                      DevScalars* __restrict__ sc, unsigned* __restrict__ qctr) {
   __shared__ unsigned part[1024];
@@ -175,8 +160,8 @@ __global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ coun
   if (threadIdx.x == 1023) sc->nitems = part[1023];
   __syncthreads();
   // items of the bound rows (the list's tail): each XCD group takes its share of them
-  // after its fluid items (ItemGroups); ncounts = 3 nrows (full, short, bound)
-  if (threadIdx.x == 0) sc->nitems_bound = part[1023] - counts[2u * (nrows2 / 3u)];
+  // after its fluid items (ItemGroups)
+  if (threadIdx.x == 0) sc->nitems_bound = part[1023] - counts[nrows2 / 2];
 }
 
 void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
@@ -184,7 +169,7 @@ void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, Di
   const int tmaxc = scelldiv == 1 ? TMAXCELLS : TMAXCELLS_HALF;
   const unsigned nrows2 = 2u * unsigned(g.ncy) * unsigned(g.ncz);
   hipLaunchKernelGGL(k_items_rows<false>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, nullptr);
-  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, rowtmp, 3u * (nrows2 / 2u), sc, qctr);
+  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, rowtmp, nrows2, sc, qctr);
   hipLaunchKernelGGL(k_items_rows<true>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, items);
 }
 

@@ -411,7 +411,7 @@ void SphGpuSingle::AllocFixed() {
   if (slab()) {  // re-partition: column counts [2 ncx] + the ranks' bounds [nranks + 1]
     colcnt_ = (float*)dmalloc(4 * (2 * size_t(C.dom_cells[0]) + size_t(slabcfg_.nranks) + 1));
   }
-  rowtmp_ = (unsigned*)dmalloc(4 * 3 * size_t(G.ncy) * size_t(G.ncz));  // full, short, bound item counts
+  rowtmp_ = (unsigned*)dmalloc(4 * 2 * size_t(G.ncy) * size_t(G.ncz));
   qctr_ = (unsigned*)dmalloc(QCTR_BYTES);
   check_hip(hipMemset(qctr_, 0, QCTR_BYTES), "zero work counters");
   sort_.digtot = (unsigned*)dmalloc(4 * (1u << RS_MAXBITS));
