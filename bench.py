@@ -78,27 +78,28 @@ def host_info(threads: int) -> dict:
         affinity = None
     return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": model,
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
-            "thread_rule": "threads = min(OMP_NUM_THREADS (else nproc), 64): the reference caps OpenMP at "
-                           "OMP_MAXTHREADS=64 (OmpDefs.h:39); on the GPU box OMP_NUM_THREADS is the box's CPU "
-                           "share of one GPU (16)", "threads": threads}
+            "thread_rule": "threads = min(nproc, 64) (BASELINE.md): the reference caps OpenMP at "
+                           "OMP_MAXTHREADS=64 (OmpDefs.h:39); `box_share` times OMP_NUM_THREADS threads, the "
+                           "GPU box's CPU share of one GPU (16)", "threads": threads}
 
 
-def _ref_run(exe: str, case: str, out: str, nsteps: int, threads: int) -> float:
+def _ref_run(exe: str, case: str, out: str, nsteps: int, threads: int, extra=()) -> float:
     """Simulation Runtime (step loop, s) of one reference run of `nsteps` steps."""
-    subprocess.run([exe, case, out, "-nsteps:%d" % nsteps, "-sv:none", "-svres:0", "-ompthreads:%d" % threads],
-                   capture_output=True, text=True, check=True, timeout=900)
+    subprocess.run([exe, case, out, "-nsteps:%d" % nsteps, "-sv:none", "-svres:0", "-ompthreads:%d" % threads]
+                   + list(extra), capture_output=True, text=True, check=True, timeout=900)
     log = open(os.path.join(out, "Run.out")).read()
     return float(re.search(r"Simulation Runtime\.*:\s*([0-9.eE+-]+)", log).group(1))
 
 
 def reference_cpu_baseline(dp: float, nsteps: int, threads: int, step: int = 1, ddt: int = 2,
-                           boundary: int = 1, flume: bool = False, first: int = 10, nn_width: float = 0.0
-                           ) -> dict | None:
+                           boundary: int = 1, flume: bool = False, first: int = 10, nn_width: float = 0.0,
+                           cellmode: str = "full") -> dict | None:
     """Times the REFERENCE CPU solver (oracle/_ref, built from the reference sources)
     on the same dam break (or wave flume, or -- nn_width > 0 -- the v5.0 NN solver on the
     NN wet dam break) over the step window [first, first+nsteps) (steps
     10-110): two runs of `first` and `first+nsteps` steps, the difference of their
-    'Simulation Runtime' (step loop only, no output) over nsteps."""
+    'Simulation Runtime' (step loop only, no output) over nsteps.  `cellmode` is passed
+    to the reference as -cellmode:<mode>, so both sides run the same cell division."""
     ref = os.path.join(ROOT, "oracle", "_ref")
     exe = os.path.join(ref, "DualSPHysics5.0NN_CPU_ref" if nn_width else "DualSPHysics5.2CPU_ref")
     gen = os.path.join(ref, "gennn_ref" if nn_width else "genflume_ref" if flume else "gencase_ref")
@@ -114,19 +115,20 @@ def reference_cpu_baseline(dp: float, nsteps: int, threads: int, step: int = 1, 
         out = subprocess.run(args, capture_output=True, text=True, check=True).stdout
         np_ = int(re.search(r"np=(\d+)", out).group(1))
         case = os.path.join(tmp, name)
-        t_a = _ref_run(exe, case, os.path.join(tmp, "a"), first, threads)
-        t_b = _ref_run(exe, case, os.path.join(tmp, "b"), first + nsteps, threads)
+        extra = () if nn_width else ("-cellmode:%s" % cellmode,)
+        t_a = _ref_run(exe, case, os.path.join(tmp, "a"), first, threads, extra)
+        t_b = _ref_run(exe, case, os.path.join(tmp, "b"), first + nsteps, threads, extra)
         sec = t_b - t_a
         return {"value": np_ * nsteps / sec, "unit": "particle-steps/s", "cores": threads, "kind": "reference",
                 "window_steps": [first, first + nsteps], "window_seconds": sec,
                 "sample": "reference %s CPU (built from /root/reference sources, -O3 -fopenmp "
-                          "-ffast-math), %d-particle %s (%s), %s, steps %d-%d (Simulation Runtime of a %d-step "
-                          "run minus that of a %d-step run), -ompthreads:%d"
+                          "-ffast-math), %d-particle %s (%s), %s, -cellmode:%s, steps %d-%d (Simulation Runtime "
+                          "of a %d-step run minus that of a %d-step run), -ompthreads:%d"
                           % ("DualSPHysics5.0 NNewtonian" if nn_width else "DualSPHysics5.2", np_,
                              "NN 3-phase wet dam break" if nn_width else "wave flume" if flume else "dam break",
                              "mDBC" if boundary == 2 else "DBC",
-                             "Verlet" if step == 1 else "Symplectic", first, first + nsteps, first + nsteps,
-                             first, threads)}
+                             "Verlet" if step == 1 else "Symplectic", cellmode, first, first + nsteps,
+                             first + nsteps, first, threads)}
     except Exception as e:  # noqa: BLE001
         sys.stderr.write("reference CPU baseline failed: %r\n" % (e,))
         return None
@@ -190,6 +192,90 @@ def weak_dp(target_np: int) -> float:
     return float("%.6g" % lo)
 
 
+def measure(case, args, rank: int, world: int, device: int, dist, use_slab: bool, steps: int, warmup: int,
+            presteps: int) -> dict:
+    """Build the solver (one domain, or this rank's x-slab), run presteps + warmup untimed
+    steps, then time exactly `steps` steps between barriers + device syncs; the elapsed
+    time is the max over ranks and the units (particles x steps) their sum."""
+    from dualsphysics_multilayer_amd.core import SphGpuSingle, SphGpuSlab, comm_unique_id, slab_partition
+
+    bounds = None
+    s = None
+    t_setup = time.perf_counter()
+    if use_slab:
+        import torch
+
+        # A failed slab setup on any rank ends every rank with a non-zero status: the run
+        # never degrades into per-GPU replicas.
+        err = None
+        try:
+            bounds = slab_partition(case, world, args.bound_weight)
+            if args.transport == "shm":
+                import uuid
+
+                ids = ["/sphbench_%s" % uuid.uuid4().hex[:12] if rank == 0 else None]
+            else:
+                ids = [comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(ids, src=0)
+            s = SphGpuSlab(case, rank, world, bounds, ids[0], device=device, transport=args.transport,
+                           slot_bytes=256 << 20)
+            if args.repartition and world > 1:
+                s.set_repartition(args.repartition, args.bound_weight, 0.05)
+            s.run(presteps + warmup)
+            s.sync()
+            ok = torch.tensor([1], dtype=torch.int32)
+        except Exception as e:  # noqa: BLE001
+            err = e
+            ok = torch.tensor([0], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            sys.stderr.write("rank %d: slab run failed: %r\n" % (rank, err if err else "failed on another rank"))
+            raise SystemExit(3)
+    else:
+        s = SphGpuSingle(case, device=device)
+        s.run(presteps + warmup)
+        s.sync()
+    setup_s = time.perf_counter() - t_setup
+    pairs0 = s.count_pairs()
+
+    def barrier():
+        if dist is not None:
+            import torch
+
+            dist.barrier()
+            torch.cuda.synchronize(device)
+
+    s.set_timing(True)
+    s.sync()
+    barrier()
+    t0 = time.perf_counter()
+    s.run(steps)
+    s.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    phase_ms, nlaunch = s.timing()
+    pairs1 = s.count_pairs()
+    st = s.stats()
+    units = float(st["np"]) * steps
+    per_rank_np = [int(st["np"])]
+    slab_info = None
+    if dist is not None:
+        import torch
+
+        tmax = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tot = torch.tensor([units], dtype=torch.float64)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        nps = [None] * world
+        dist.all_gather_object(nps, int(st["np"]))
+        infos = [None] * world
+        dist.all_gather_object(infos, s.slab_info() if bounds is not None else None)
+        elapsed, units, per_rank_np, slab_info = float(tmax.item()), float(tot.item()), nps, infos
+    s.close()
+    return dict(setup_s=setup_s, elapsed=elapsed, units=units, phase_ms=phase_ms, nlaunch=nlaunch, pairs0=pairs0,
+                pairs1=pairs1, st=st, bounds=bounds, per_rank_np=per_rank_np, slab_info=slab_info)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -215,6 +301,9 @@ def main() -> None:
     ap.add_argument("--presteps", type=int, default=0,
                     help="untimed steps before the warmup: time a developed flow (movers across cells, "
                          "the incremental divide's real load) instead of the first steps from rest")
+    ap.add_argument("--no-cfg3", action="store_true",
+                    help="cfg2: skip the extra cfg3 (10M, Symplectic) timing (keys cfg3_1gpu / strong_scaling_cfg3)")
+    ap.add_argument("--cfg3-steps", type=int, default=10, help="timed steps of the extra cfg3 measurement")
     ap.add_argument("--force-slab", action="store_true",
                     help="run the N>1 code path (gloo bootstrap + RCCL slab) even with one rank")
     args = ap.parse_args()
@@ -239,7 +328,6 @@ def main() -> None:
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from dualsphysics_multilayer_amd.case import DamBreakCase, WaveFlumeCase, WetDambreakNNCase
-    from dualsphysics_multilayer_amd.core import SphGpuSingle, SphGpuSlab, comm_unique_id, slab_partition
 
     cmode = 2 if args.cellmode == "half" else 1
     if cmode == 2 and args.workload not in ("cfg2", "cfg3"):
@@ -257,78 +345,32 @@ def main() -> None:
     else:
         dp = args.dp or CFG5_DP
         case = WetDambreakNNCase(dp, width=CFG5_WIDTH)
-    bounds = None
-    s = None
     wall = {}
     t_setup = time.perf_counter()
-    if use_slab:
-        # A failed slab setup on any rank ends every rank with a non-zero status: the run
-        # never degrades into per-GPU replicas.
-        err = None
-        try:
-            bounds = slab_partition(case, world, args.bound_weight)
-            if args.transport == "shm":
-                import uuid
-
-                ids = ["/sphbench_%s" % uuid.uuid4().hex[:12] if rank == 0 else None]
-            else:
-                ids = [comm_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(ids, src=0)
-            s = SphGpuSlab(case, rank, world, bounds, ids[0], device=device, transport=args.transport,
-                           slot_bytes=256 << 20)
-            if args.repartition and world > 1:
-                s.set_repartition(args.repartition, args.bound_weight, 0.05)
-            s.run(args.presteps + args.warmup)
-            s.sync()
-            ok = torch.tensor([1], dtype=torch.int32)
-        except Exception as e:  # noqa: BLE001
-            err = e
-            ok = torch.tensor([0], dtype=torch.int32)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 0:
-            sys.stderr.write("rank %d: slab run failed: %r\n" % (rank, err if err else "failed on another rank"))
-            raise SystemExit(3)
-    else:
-        s = SphGpuSingle(case, device=device)
-        s.run(args.presteps + args.warmup)
-        s.sync()
-    wall["setup_and_warmup_s"] = time.perf_counter() - t_setup
-    pairs0 = s.count_pairs()
-
-    def barrier():
-        if dist is not None:
-            import torch
-
-            dist.barrier()
-            torch.cuda.synchronize(device)
-
-    s.set_timing(True)
-    s.sync()
-    barrier()
-    t0 = time.perf_counter()
-    s.run(args.steps)
-    s.sync()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    phase_ms, nlaunch = s.timing()
-    pairs1 = s.count_pairs()
-    st = s.stats()
-
-    units = float(st["np"]) * args.steps
-    per_rank_np = [int(st["np"])]
-    slab_info = None
-    if dist is not None:
-        import torch
-
-        tmax = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tot = torch.tensor([units], dtype=torch.float64)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        nps = [None] * world
-        dist.all_gather_object(nps, int(st["np"]))
-        infos = [None] * world
-        dist.all_gather_object(infos, s.slab_info() if bounds is not None else None)
-        elapsed, units, per_rank_np, slab_info = float(tmax.item()), float(tot.item()), nps, infos
+    m = measure(case, args, rank, world, device, dist, use_slab, args.steps, args.warmup, args.presteps)
+    wall["setup_and_warmup_s"] = m["setup_s"]
+    elapsed, units, phase_ms, nlaunch = m["elapsed"], m["units"], m["phase_ms"], m["nlaunch"]
+    pairs0, pairs1, st, bounds, per_rank_np, slab_info = (m["pairs0"], m["pairs1"], m["st"], m["bounds"],
+                                                          m["per_rank_np"], m["slab_info"])
+    del t_setup
+    # North star's strong-scaling target is cfg3 (~10M, Symplectic + DDT) from 1 to 8 GPUs:
+    # time it beside the headline line -- on one GPU as `cfg3_1gpu`, on N ranks as
+    # `strong_scaling_cfg3` -- so one scaling run yields the 1 -> N strong-scaling ratio.
+    cfg3_extra = None
+    if args.workload == "cfg2" and not args.no_cfg3 and args.dp is None and args.cellmode == "full":
+        t3 = time.perf_counter()
+        c3 = DamBreakCase(CFG3_DP, step_algorithm=2, tdensity=1)
+        m3 = measure(c3, args, rank, world, device, dist, world > 1 or args.force_slab, args.cfg3_steps, 2, 0)
+        cfg3_extra = {"workload": "BASELINE cfg3: 3D dam break, %d particles (dp=%g), Symplectic, DDT (Molteni) "
+                                  "0.1, DBC, CellMode full" % (c3.np, CFG3_DP),
+                      "np": c3.np, "n_gpus": world, "steps": args.cfg3_steps, "warmup": 2,
+                      "ms_per_step": m3["elapsed"] / args.cfg3_steps * 1e3,
+                      "value": m3["units"] / m3["elapsed"], "unit": "particle-steps/s",
+                      "interaction_ms_per_call": float(m3["phase_ms"][0]),
+                      "divide_ms_per_call": float(m3["phase_ms"][2]),
+                      "parallelism": ("slab-x%d (RCCL)" % world) if m3["bounds"] is not None else "single",
+                      "owned_np_per_rank": m3["per_rank_np"],
+                      "wall_s": time.perf_counter() - t3}
 
     if rank == 0:
         pairs = (pairs0.astype("float64") + pairs1.astype("float64")) / 2.0
@@ -430,24 +472,36 @@ def main() -> None:
         }
         wall["timed_s"] = elapsed
         if not args.no_cpu_baseline and world == 1:
-            threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), 64)
+            # BASELINE.md's thread rule: min(nproc, 64) threads (the reference caps OpenMP at
+            # OMP_MAXTHREADS=64, OmpDefs.h:39) -> `value`; beside it the box's CPU share of one
+            # GPU (OMP_NUM_THREADS, 16 on the GPU box) on a shorter window.
+            threads = min(os.cpu_count() or 1, 64)
+            share = min(int(os.environ.get("OMP_NUM_THREADS", threads)), threads)
             t_cpu = time.perf_counter()
-            if nn:  # the v5.0 NN CPU solver runs ~3 s per step at 2M particles: a bounded sample
-                cb = reference_cpu_baseline(dp, min(args.cpu_steps, 6), threads, nn_width=CFG5_WIDTH, first=1)
-            else:
-                cb = reference_cpu_baseline(dp, args.cpu_steps, threads, case.step_algorithm, case.tdensity,
-                                            case.tboundary, flume=args.workload == "cfg4")
+
+            def ref_baseline(nthreads, nsteps):
+                if nn:  # the v5.0 NN CPU solver runs ~3 s per step at 2M particles: a bounded sample
+                    return reference_cpu_baseline(dp, min(nsteps, 6), nthreads, nn_width=CFG5_WIDTH, first=1)
+                return reference_cpu_baseline(dp, nsteps, nthreads, case.step_algorithm, case.tdensity,
+                                              case.tboundary, flume=args.workload == "cfg4", cellmode=args.cellmode)
+
+            cb = ref_baseline(threads, args.cpu_steps)
             if cb is None and not nn:  # the oracle restates the single-phase solver only
                 cb = port_cpu_baseline(case, min(args.cpu_steps, 10), threads)
             if cb is not None:
                 cb["gpu_over_cpu"] = value / cb["value"]
                 cb["host"] = host_info(threads)
+                if share != threads:
+                    cs = ref_baseline(share, max(args.cpu_steps // 3, 1))
+                    if cs is not None:
+                        cs["gpu_over_cpu"] = value / cs["value"]
+                        cb["box_share"] = cs
             res["cpu_baseline"] = cb
             wall["cpu_baseline_s"] = time.perf_counter() - t_cpu
         wall["process_s"] = time.perf_counter() - T_START
         res["wall_breakdown"] = wall
+        res["cfg3_1gpu" if world == 1 else "strong_scaling_cfg3"] = cfg3_extra
         print(json.dumps(res))
-    s.close()
     if dist is not None:
         dist.destroy_process_group()
 

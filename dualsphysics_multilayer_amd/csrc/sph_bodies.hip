@@ -263,6 +263,7 @@ __global__ void k_motion(const DevScalars* __restrict__ sc, MotionDev* __restric
   if (threadIdx.x != 0) return;
   const double timestep = (t0 >= 0 ? t0 : sc->tstep0), dt = (t0 >= 0 ? dt0 : sc->last_dt);
   for (int o = 0; o < md->nobj; o++) md->out[o].type = 0;  // PreMotion
+  if (t0 < 0 && halted(sc)) return;  // a fatal error stopped the run: nothing moves
   // JMotion::ProcesTime (JMotion.cpp:446-468): start the events that begin before t+dt
   bool looking = true;
   for (int c = md->eventnext; c >= 0 && looking; c--) {
@@ -516,7 +517,7 @@ __global__ void k_ft_forces(const DevScalars* __restrict__ sc, KConst K, FtBody*
                             const float* __restrict__ part, int predictor, const double4* __restrict__ tab,
                             const int2* __restrict__ desc) {
   const int cf = blockIdx.x * blockDim.x + threadIdx.x;
-  if (cf >= nbodies) return;
+  if (cf >= nbodies || halted(sc)) return;
   FtBody& b = bodies[cf];
   const double dt = (predictor ? sc->dt * .5 : sc->dt);
   if (!(sc->tstep0 >= double(b.ftpause))) {
@@ -602,7 +603,7 @@ __global__ __launch_bounds__(256) void k_ft_update(DevScalars* __restrict__ sc, 
                                                    PartArrays a, int predictor) {
   const unsigned fp = blockIdx.x * blockDim.x + threadIdx.x;
   const double dt = (predictor ? sc->dt * .5 : sc->dt);
-  if (fp < nftp) {
+  if (fp < nftp && !halted(sc)) {
     int cf = 0;
     while (cf + 1 < nbodies && fp >= bodies[cf + 1].begin) cf++;
     const FtBody& b = bodies[cf];
@@ -622,7 +623,7 @@ __global__ __launch_bounds__(256) void k_ft_update(DevScalars* __restrict__ sc, 
       a.velrhop[p] = v;
     }
   }
-  if (fp == 0 && !predictor) {
+  if (fp == 0 && !predictor && !halted(sc)) {
     const float fdt = float(dt);
     for (int cf = 0; cf < nbodies; cf++) {
       FtBody& b = bodies[cf];

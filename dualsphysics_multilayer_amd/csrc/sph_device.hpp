@@ -123,14 +123,26 @@ struct DevScalars {
 constexpr int RED_VELMAX2 = 0, RED_ACEMAX2 = 1, RED_VISCDT = 2, RED_VISCETA = 3, RED_SLOTS = 64;
 
 constexpr unsigned ERR_DT_NAN = 1u, ERR_BOUNDOUT = 2u, ERR_HALO = 4u;
+// Errors the reference throws on (DtVariable, JSphCpu.cpp:1622; AbortBoundOut in
+// RunCellDivide): once one is flagged, a batched run stops stepping ON THE DEVICE — k_dt
+// no longer advances time/nstep and the update, motion and floating kernels leave the
+// state as it was, so the run ends at the failing step and sph_solver_sync reports it.
+constexpr unsigned ERR_FATAL = ERR_DT_NAN | ERR_BOUNDOUT | ERR_HALO;
+__device__ __forceinline__ bool halted(const DevScalars* sc) { return (sc->error_flags & ERR_FATAL) != 0u; }
 
 // Wave-level max of a non-negative float, then one atomicMax per wave into a slot
 // chosen by the wave's global index (64 slots).
+// A NaN is carried as the canonical quiet NaN, whose bits exceed every finite value and
+// +inf: it wins the integer max and reaches k_dt, which then stops the run (ERR_DT_NAN).
 __device__ inline void wave_max_atomic(DevScalars* sc, int which, float v) {
+  unsigned b = (v != v) ? 0x7fc00000u : __float_as_uint(fmaxf(v, 0.f));
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  for (int off = 32; off > 0; off >>= 1) b = max(b, (unsigned)__shfl_xor((int)b, off, 64));
   const unsigned wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if ((threadIdx.x & 63) == 0 && v > 0.f) atomicMax(&sc->red[which][wave & (RED_SLOTS - 1)], __float_as_uint(v));
+  if ((threadIdx.x & 63) == 0 && b) atomicMax(&sc->red[which][wave & (RED_SLOTS - 1)], b);
 }
+// max that keeps a NaN (fmaxf drops it): per-thread VelMax accumulation, so that a NaN
+// velocity reaches the dt (the reference's DtVariable check, JSphCpu.cpp:1622)
+__device__ __forceinline__ float nanmax(float a, float x) { return (x != x || a != a) ? __builtin_nanf("") : fmaxf(a, x); }
 
 }  // namespace sphx

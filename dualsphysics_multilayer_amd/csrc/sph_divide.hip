@@ -434,7 +434,7 @@ __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, Gat
       float4 vr;
       bool fluid;
       gather_one<WITHM1, WITHPRE>(a, i, sp[k], vr, fluid, npb);
-      if (fluid) v2 = fmaxf(v2, vr.x * vr.x + vr.y * vr.y + vr.z * vr.z);  // CalcVelMaxOmp over fluid
+      if (fluid) v2 = nanmax(v2, vr.x * vr.x + vr.y * vr.y + vr.z * vr.z);  // CalcVelMaxOmp over fluid
     }
   }
   wave_max_atomic(sc, RED_VELMAX2, v2);
@@ -1061,7 +1061,9 @@ __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, G
     const unsigned i = i0 + 256 * k;
     const unsigned ii = i < nd ? i : 0u;
     key[k] = s.newkey[ii];
-    cw[k] = s.cw[ii];
+    // a tail lane (i >= nd) gets a zero classification word: it is neither a near nor a far
+    // mover, so it never indexes fidx / mposfar with particle 0's word
+    cw[k] = i < nd ? s.cw[ii] : 0u;
     q[k].load(a.src, ii);
   }
 #pragma unroll
@@ -1084,7 +1086,7 @@ __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, G
     if (i0 + 256 * k < nd && pos[k] < n) {
       gather_store<WITHM1, WITHPRE>(a, pos[k], q[k]);
       s.skeys[pos[k]] = key[k];
-      if (pos[k] >= npb) v2 = fmaxf(v2, q[k].vr.x * q[k].vr.x + q[k].vr.y * q[k].vr.y + q[k].vr.z * q[k].vr.z);
+      if (pos[k] >= npb) v2 = nanmax(v2, q[k].vr.x * q[k].vr.x + q[k].vr.y * q[k].vr.y + q[k].vr.z * q[k].vr.z);
     }
   }
   wave_max_atomic(sc, RED_VELMAX2, v2);

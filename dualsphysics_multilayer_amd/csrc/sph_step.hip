@@ -62,6 +62,7 @@ __global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double d
   sc->last_viscdt = viscdt;
   sc->last_visceta = visceta;
   if (mode == DT_PEEK) return;
+  if (halted(sc)) return;  // an earlier fatal error: the run no longer advances
   const double kh = double(K.kernelh);
   const double dt1 = (acemax ? sqrt(kh / acemax) : DBL_MAX);
   const double dt2 = kh / (fmax(cs0, velmax * 10.) + kh * double(viscdt));
@@ -69,9 +70,13 @@ __global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double d
   // solver forms them (JSphCpu.cpp:1687 of src_mphase/DSPH_v5.0_NNewtonian)
   const double dt3 = (K.nn ? double(K.kernelh * K.kernelh) / double(visceta * K.lamda) : DBL_MAX);
   double dt = cfl * fmin(dt3, fmin(dt1, dt2));
-  if (isnan(dt) || isinf(dt)) {
+  // a NaN maximum (a NaN velocity, acceleration or viscosity anywhere) also stops the run:
+  // fmin/fmax above would drop it, and the state it came from is already lost
+  if (isnan(dt) || isinf(dt) || isnan(velmax) || isnan(acemax) || isnan(viscdt) || isnan(visceta)) {
+    // the reference throws here (JSphCpu.cpp:1622): this step is not taken, and every
+    // later kernel of a batched run sees the flag (halted) and leaves the state alone
     sc->error_flags |= ERR_DT_NAN;
-    dt = dtmin;
+    return;
   }
   if (dt < dtmin) {
     dt = dtmin;
@@ -118,7 +123,12 @@ __global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ s
                                                 const float4* __restrict__ shiftpos) {
   const unsigned np = sc->np, npb = sc->npb;
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= np || slab_ghost(K, g, a.dcell, p)) return;
+  if (p >= np) return;
+  if (halted(sc)) {  // keep the state: the caller's velrhop/velrhopm1 swap then restores it
+    a.velrhopm1[p] = a.velrhop[p];
+    return;
+  }
+  if (slab_ghost(K, g, a.dcell, p)) return;
   const double dt = sc->dt;
   const double dt2 = (euler ? dt : dt + dt);
   const float4 ra = arace[p];
@@ -159,7 +169,14 @@ __global__ __launch_bounds__(256) void k_sym_pre(const DevScalars* __restrict__ 
                                                  const float4* __restrict__ arace, PartArrays a, DivGrid g) {
   const unsigned np = sc->np, npb = sc->npb;
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= np || slab_ghost(K, g, a.dcell, p)) return;
+  if (p >= np) return;
+  if (halted(sc)) {  // keep the state (the caller moved it into the pre arrays)
+    a.velrhop[p] = a.velrhoppre[p];
+    a.posxy[p] = a.posxypre[p];
+    a.posz[p] = a.poszpre[p];
+    return;
+  }
+  if (slab_ghost(K, g, a.dcell, p)) return;
   const double dt = sc->dt, dt05 = dt * .5;
   const float4 ra = arace[p];
   const float4 vp = a.velrhoppre[p];
@@ -207,7 +224,7 @@ __global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ 
                                                  const float4* __restrict__ shiftpos) {
   const unsigned np = sc->np, npb = sc->npb;
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= np || slab_ghost(K, g, a.dcell, p)) return;
+  if (p >= np || halted(sc) || slab_ghost(K, g, a.dcell, p)) return;
   const double dt = sc->dt, dt05 = dt * .5;
   const float4 ra = arace[p];
   const float4 vr = a.velrhop[p];

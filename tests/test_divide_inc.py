@@ -94,6 +94,25 @@ def test_inc_divide_exclusions(monkeypatch, nfast, dbg):
     assert st["nout"] >= q
 
 
+def test_inc_divide_first_particle_excluded(monkeypatch):
+    """No boundary particles (npb = 0) and np not a multiple of the 1024-particle tile: the
+    particle that sorts first is a far mover to the out boxes.  The push kernel's tail lanes
+    (index >= np) read particle 0's slot; they must not take its far-mover word."""
+    case = copy.copy(DamBreakCase(0.03, celldomfixed=True))
+    fl = slice(case.npb, case.np)
+    case.pos = case.pos[fl].copy()
+    case.vel = case.vel[fl].copy()
+    case.rhop = case.rhop[fl].copy()
+    case.np -= case.npb
+    case.npb = 0
+    case.idp = np.arange(case.np, dtype=np.uint32)
+    assert case.np % 1024 != 0
+    first = np.lexsort((case.pos[:, 0], case.pos[:, 1], case.pos[:, 2]))[0]
+    case.vel[first] = [0.0, 0.0, -400.0]
+    st = _same(case, 6, 1, monkeypatch)
+    assert st["nout"] >= 1 and st["npb"] == 0
+
+
 def test_inc_divide_half_cells(monkeypatch):
     case = _stirred(DamBreakCase(0.025, cellmode=2, celldomfixed=True), 0.3, 2.0)
     _same(case, 30, 5, monkeypatch)
