@@ -127,7 +127,9 @@ constexpr unsigned ERR_DT_NAN = 1u, ERR_BOUNDOUT = 2u, ERR_HALO = 4u;
 // RunCellDivide): once one is flagged, a batched run stops stepping ON THE DEVICE — k_dt
 // no longer advances time/nstep and the update, motion and floating kernels leave the
 // state as it was, so the run ends at the failing step and sph_solver_sync reports it.
-constexpr unsigned ERR_FATAL = ERR_DT_NAN | ERR_BOUNDOUT | ERR_HALO;
+// (ERR_HALO is reported at the next sync but does not halt: a slab's face re-send can flag it
+// for a stale face entry whose particle left that slab, which is harmless.)
+constexpr unsigned ERR_FATAL = ERR_DT_NAN | ERR_BOUNDOUT;
 __device__ __forceinline__ bool halted(const DevScalars* sc) { return (sc->error_flags & ERR_FATAL) != 0u; }
 
 // Wave-level max of a non-negative float, then one atomicMax per wave into a slot

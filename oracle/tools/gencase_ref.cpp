@@ -28,7 +28,8 @@
 
 int main(int argc, char** argv) {
   if (argc < 5) {
-    fprintf(stderr, "usage: %s dp outdir step ddt [timemax] [casename]\n", argv[0]);
+    fprintf(stderr, "usage: %s dp outdir step ddt [timemax] [casename] [boundary] [dim] [viscotreatment] [visco] "
+                    "[shifting] [shiftcoef] [shifttfs]\n", argv[0]);
     return 1;
   }
   const double dp = atof(argv[1]);
@@ -42,6 +43,13 @@ int main(int argc, char** argv) {
   // 4 x 3 in x-z with bottom, left and right walls, water column 1 x 2, y = 0, Visco 0.02)
   const int dim = (argc > 8 ? atoi(argv[8]) : 3);
   const bool d2 = (dim == 2);
+  // viscosity and shifting (<parameters> ViscoTreatment/Visco, Shifting/ShiftCoef/ShiftTFS,
+  // JSph.cpp:620-700): 1 artificial (default, Visco 0.1 / 0.02 in 2-D) or 2 Laminar+SPS
+  const int tvisco = (argc > 9 ? atoi(argv[9]) : 1);
+  const std::string visco = (argc > 10 ? argv[10] : (d2 ? "0.02" : "0.1"));
+  const int shifting = (argc > 11 ? atoi(argv[11]) : 0);
+  const std::string shiftcoef = (argc > 12 ? argv[12] : "-2");
+  const std::string shifttfs = (argc > 13 ? argv[13] : "0");
 
   // 3-D: tank 1.6 x 0.67 x 0.4 (walls: bottom, x=0, x=L, y=0, y=W); water 0.4 x 0.67 x 0.3.
   const int nx = int(std::round((d2 ? 4.0 : 1.6) / dp)), ny = d2 ? 0 : int(std::round(0.67 / dp));
@@ -109,12 +117,16 @@ int main(int argc, char** argv) {
   par("StepAlgorithm", std::to_string(step));
   par("VerletSteps", "40");
   par("Kernel", "2");
-  par("ViscoTreatment", "1");
-  par("Visco", d2 ? "0.02" : "0.1");
+  par("ViscoTreatment", std::to_string(tvisco));
+  par("Visco", visco);
   par("ViscoBoundFactor", "1");
   par("DensityDT", std::to_string(ddt));
   par("DensityDTvalue", "0.1");
-  par("Shifting", "0");
+  par("Shifting", std::to_string(shifting));
+  if (shifting) {
+    par("ShiftCoef", shiftcoef);
+    par("ShiftTFS", shifttfs);
+  }
   par("Boundary", std::to_string(boundary));
   if (boundary == 2) par("SlipMode", "1");
   par("RigidAlgorithm", "1");
