@@ -76,7 +76,13 @@ def host_info(threads: int) -> dict:
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         affinity = None
-    return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": model,
+    quota = None
+    try:  # cgroup v2 CPU quota ("max" or "<quota> <period>"): the CPUs this job may really use
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q[0] == "max" else float(q[0]) / float(q[1])
+    except (OSError, ValueError, IndexError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "cpu_model": model,
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
             "thread_rule": "threads = min(nproc, 64) (BASELINE.md): the reference caps OpenMP at "
                            "OMP_MAXTHREADS=64 (OmpDefs.h:39); `box_share` times OMP_NUM_THREADS threads, the "
