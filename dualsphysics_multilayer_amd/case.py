@@ -72,6 +72,12 @@ class DamBreakCase:
     tboundary: int = 1  # 1 DBC, 2 mDBC (<parameter Boundary>, JSph.cpp:626-640)
     slipmode: int = 1  # mDBC: only SLIP_Vel0 in this fork (JSph.cpp:788)
     mdbc_threshold: float = 0.0  # -mdbc_threshold (JSphCfgRun.cpp:124)
+    # ViscoTreatment 1 artificial / 2 Laminar+SPS (then `visco` is the kinematic viscosity,
+    # e.g. 1e-6), shifting mode 0-3 with ShiftCoef / ShiftTFS (JSph.cpp:620-700)
+    tvisco: int = 1
+    shift_mode: int = 0
+    shift_coef: float = -2.0
+    shift_tfs: float = 0.0
     # generated
     pos: np.ndarray = field(init=False, repr=False)
     vel: np.ndarray = field(init=False, repr=False)
@@ -232,8 +238,9 @@ class DamBreakCase:
             tboundary=self.tboundary,
             slipmode=self.slipmode,
             mdbc_threshold=self.mdbc_threshold,
-            rheology=1, velgrad=1, tvisco=1, nphases=0, phases=(), relaxation_dt=0.2,
-            shift_mode=0, shift_coef=-2.0, shift_tfs=0.0,
+            rheology=1, velgrad=1, tvisco=self.tvisco, nphases=0, phases=(), relaxation_dt=0.2,
+            shift_mode=self.shift_mode, shift_coef=float(np.float32(self.shift_coef)),
+            shift_tfs=float(np.float32(self.shift_tfs)),
             data2d=int(getattr(self, "data2d", False)),
             data2d_posy=0.0,
         )
@@ -328,6 +335,10 @@ class WaveFlumeCase:
     time0: float = 0.0
     symdtpre0: float = 0.0
     has_bodies: bool = True
+    tvisco: int = 1
+    shift_mode: int = 0
+    shift_coef: float = -2.0
+    shift_tfs: float = 0.0
 
     def __post_init__(self) -> None:
         dp = self.dp
@@ -493,6 +504,7 @@ class WetDambreakNNCase:
     scale: float = 1.0
     shift_tfs: float = 2.75
     tvisco: int = 2
+    velgrad: int = 1  # VelocityGradientType: 1 FDA, 2 SPH (JSph.cpp:617-622 of the v5.0 solver)
     tdensity: int = DDT_DDT2FULL
     shift_mode: int = 3
     step_algorithm: int = STEP_SYMPLECTIC
@@ -582,7 +594,7 @@ class WetDambreakNNCase:
         d = DamBreakCase.case_def(self)
         f32 = lambda v: float(np.float32(v))  # noqa: E731  (JXml ReadElementFloat / GetValueFloat)
         phases = tuple({k: (f32(v) if isinstance(v, float) else v) for k, v in ph.items()} for ph in self.phases)
-        d.update(rheology=2, velgrad=1, tvisco=self.tvisco, nphases=len(self.phases), phases=phases,
+        d.update(rheology=2, velgrad=self.velgrad, tvisco=self.tvisco, nphases=len(self.phases), phases=phases,
                  relaxation_dt=f32(self.relaxation_dt), shift_mode=self.shift_mode, shift_coef=f32(self.shift_coef),
                  shift_tfs=f32(self.shift_tfs))
         return d

@@ -190,7 +190,28 @@ void launch_mdbc_face_apply(hipStream_t stm, DevScalars* sc, const MdbcFaceRec* 
 void launch_nn_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
                      const float4* poscell, const float4* velrhop, const float* press, const typecode* code,
                      const unsigned* begincell, DivGrid g, const KConst& K, const float4* phases, float4* arace,
-                     float4* shiftpos, bool shift);
+                     float4* shiftpos, bool shift, float* viscoeta, float4* tau);
+// NN with SPH velocity gradients, second pass: the Morris / constitutive-equation /
+// artificial viscous force of every fluid p1 from the first pass's effective viscosities or
+// stress tensors (JSphCpu_NN_SPH.cpp:228-446), added onto arace; AceMax.
+void launch_nn_visc(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
+                    const float4* poscell, const float4* velrhop, const typecode* code, const float* viscoeta,
+                    const float4* tau, const unsigned* begincell, DivGrid g, const KConst& K, const float4* phases,
+                    float4* arace);
+// Slabs, SPH velocity gradients: the first pass's effective viscosity (Laminar) or stress
+// tensor (ConstEq) of the owned face-column fluid particles, for the neighbours' ghosts
+// (the second pass reads them for every p2).  Records {idp, v[7]}; count in slot 0 of
+// each buffer.  idxmap: idp -> local index of every held particle (apply side).
+struct NNFaceRec {
+  unsigned idp;
+  float v[7];
+};
+void launch_nn_face_pack(hipStream_t stm, unsigned cap, const DevScalars* sc, const PartArrays& a, const KConst& K,
+                         const DivGrid& g, const float* viscoeta, const float4* tau, NNFaceRec* sl, NNFaceRec* sr,
+                         unsigned capl, unsigned capr, unsigned* idxmap, unsigned nidx);
+void launch_nn_face_apply(hipStream_t stm, DevScalars* sc, const NNFaceRec* rl, const NNFaceRec* rr, unsigned capl,
+                          unsigned capr, const unsigned* idxmap, unsigned nidx, const unsigned* idp, float* viscoeta,
+                          float4* tau, bool withtau);
 // Pair counters (JDsPips).
 void launch_count_pairs(hipStream_t stm, unsigned cap, const DevScalars* sc, const float4* poscell,
                         const unsigned* begincell, DivGrid g, const KConst& K, unsigned long long* out6);

@@ -23,6 +23,8 @@
 // bound-p2 pass keeps the reference order when its first no-shift pair can freeze every
 // shifting sum (ShiftMode NoBound/NoFixed), else it is drained in mirrored units too.  cfg5: 1.85 -> 1.55 ms per interaction (SPH_NN_MIRROR=0: the
 // row-ordered drain of every pass).
+#include <algorithm>
+
 #include "sph_tiled.hpp"
 
 namespace sphx {
@@ -45,7 +47,22 @@ struct NNAcc {
   float ax, ay, az, ar, delta, visc, visceta;
   float sx, sy, sz, sw;  // shifting sums (shiftposfsp1)
   bool hv;               // mirrored drain: a heavier-phase neighbour was seen (sx needs the ordered sweep)
+  float gxx, gxy, gxz, gyy, gyz, gzz;  // SPH velocity gradients (TVISCO 4; gradvelp1, xy = du/dy + dv/dx)
 };
+
+// Interaction modes of k_nn_tiled (TVISCO template parameter):
+//   1, 2, 3  FDA velocity gradients (VelocityGradientType 1) with artificial, Laminar
+//            (Morris) or constitutive-equation viscosity, all in the pair loop
+//            (InteractionForcesFluid_NN_FDA_All, JSphCpu_NN_FDA.cpp:141-275);
+//   4        SPH velocity gradients (VelocityGradientType 2), Laminar or ConstEq: the pair
+//            loop of InteractionForcesFluid_NN_SPH_PressGrad (JSphCpu_NN_SPH.cpp:452-621)
+//            accumulates gradvel, and each p1 then gets its strain rate, effective viscosity
+//            and (ConstEq) stress tensor (_Visco_eta / _Visco_Stress_tensor, :128-222);
+//            the viscous force is the second pass k_nn_visc (Morris / ConsEq, :228-446);
+//   5        SPH gradients with artificial viscosity: PressGrad without a viscous term; the
+//            artificial term is k_nn_visc's (the Morris pass, whose bound-p2 velocity
+//            difference is 2 v1, JSphCpu_NN_SPH.cpp:403-405).
+constexpr int NN_SPH_GRAD = 4, NN_SPH_ART = 5;
 
 // Third part of a staged record: {press, 1/rho} (8 B) + the tag (1 B) — 41 B records in all.
 struct NNSC {
@@ -91,6 +108,25 @@ __device__ __forceinline__ float nn_eta(float dmag, float tau_yield, float visco
 #endif
   const float term2 = (bi_region ? visco : (cap ? visco : miou_hb));
   return term1 + term2;
+}
+
+// GetStrainRateTensor_tsym (JSphCpu_Tensors.cpp:185-208) of the SPH gradient (off-diagonal
+// entries hold du/dy + dv/dx): D = {xx, xy, xz, yy, yz, zz} and |D| = sqrt(II_D) with the
+// reference's expanded invariant.  II_D is a sum of squares up to rounding; where rounding
+// leaves it below 0 the reference takes the square root of a negative number (NaN viscosity,
+// with a printed warning) — here it is clamped to 0, i.e. |D| = 0.
+__device__ __forceinline__ float nn_strain_rate(float gxx, float gxy, float gxz, float gyy, float gyz, float gzz,
+                                                float d[6]) {
+  const float div_vel = (gxx + gyy + gzz) / 3.f;
+  d[0] = gxx - div_vel;
+  d[1] = 0.5f * gxy;
+  d[2] = 0.5f * gxz;
+  d[3] = gyy - div_vel;
+  d[4] = 0.5f * gyz;
+  d[5] = gzz - div_vel;
+  const float ii1 = d[0] * d[3] + d[3] * d[5] + d[0] * d[5];
+  const float ii2 = d[1] * d[1] + d[4] * d[4] + d[2] * d[2];
+  return sqrtf(fmaxf(-ii1 + ii2, 0.f));
 }
 
 // One pair of the fluid p1 (InteractionForcesFluid_NN_FDA_All, JSphCpu_NN_FDA.cpp:141-275).
@@ -177,7 +213,29 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
       a.ay = fmaf(-pi_visc, fry, a.ay);
       a.az = fmaf(-pi_visc, frz, a.az);
     }
-  } else {  // Laminar (2) or constitutive equation (3) with the FDA velocity gradient
+  } else if (TVISCO == NN_SPH_GRAD) {
+    // GetVelocityGradients_SPH_tsym (JSphCpu_Tensors.cpp:173-181), no slip on the tensor at a
+    // boundary p2 (u_g = 2 u_b - u_f, JSphCpu_NN_SPH.cpp:585-587); pairs outside the test
+    // have fr = 0
+    if (BOUNDP2) {
+      dvx = 2.f * p.vr.x;
+      dvy = 2.f * p.vr.y;
+      dvz = 2.f * p.vr.z;
+    }
+    const float volp2 = -massp2 * inv_rho2;
+    float dv = dvx * volp2;
+    a.gxx = fmaf(dv, frx, a.gxx);
+    a.gxy = fmaf(dv, fry, a.gxy);
+    a.gxz = fmaf(dv, frz, a.gxz);
+    dv = dvy * volp2;
+    a.gxy = fmaf(dv, frx, a.gxy);
+    a.gyy = fmaf(dv, fry, a.gyy);
+    a.gyz = fmaf(dv, frz, a.gyz);
+    dv = dvz * volp2;
+    a.gxz = fmaf(dv, frx, a.gxz);
+    a.gyz = fmaf(dv, fry, a.gyz);
+    a.gzz = fmaf(dv, frz, a.gzz);
+  } else if (TVISCO == 2 || TVISCO == 3) {  // Laminar (2) or constitutive equation (3) with the FDA velocity gradient
     if (BOUNDP2) {  // no slip on the tensor: u_g = 2 u_b - u_f with u_b = 0
       dvx = 2.f * p.vr.x;
       dvy = 2.f * p.vr.y;
@@ -201,7 +259,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     const float4 ph2b = sph[2 * pp2 + 1];
     const float eta = nn_eta(dmag, ph2.w, visco_nn, ph2b.x, ph2b.y, p.taumax, p.bimulti);
     a.visceta = fmaxf(ok ? eta : 0.f, a.visceta);
-    if (TVISCO == 2) {  // Morris operator
+    if constexpr (TVISCO == 2) {  // Morris operator
       const float temp = 2.f * eta * (inv_re * inv_rho2);
       const float vtemp = massp2 * temp * dot3;
       a.ax = fmaf(vtemp, dvx, a.ax);
@@ -576,7 +634,8 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
                                                  const float4* __restrict__ velrhop, const float* __restrict__ press,
                                                  const typecode* __restrict__ code, const unsigned* __restrict__ bc,
                                                  DivGrid g, KConst K, const float4* __restrict__ phases,
-                                                 float4* __restrict__ arace, float4* __restrict__ shiftpos) {
+                                                 float4* __restrict__ arace, float4* __restrict__ shiftpos,
+                                                 float* __restrict__ viscoeta, float4* __restrict__ tau) {
   __shared__ float4 sA[NN_TCAP + SPH_PAD];
   __shared__ float4 sB[NN_TCAP];
   __shared__ float2 sC2[NN_TCAP];  // {press, 1/rho}
@@ -722,7 +781,26 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
         if (SHIFT) shiftpos[p1] = make_float4(b.sx, b.sy, b.sz, b.sw);
         viscmax = fmaxf(viscmax, fmaxf(f.visc, b.visc));
         etamax = fmaxf(etamax, fmaxf(f.visceta, b.visceta));
-        ace2max = fmaxf(ace2max, ax * ax + ay * ay + az * az);
+        // SPH gradients: the viscous force and so AceMax come from the second pass (k_nn_visc)
+        if (TVISCO != NN_SPH_GRAD && TVISCO != NN_SPH_ART) ace2max = fmaxf(ace2max, ax * ax + ay * ay + az * az);
+        if constexpr (TVISCO == NN_SPH_GRAD) {
+          // gradvel[p1] += fluid sums, += bound sums (JSphCpu_NN_SPH.cpp:608-615), then
+          // _Visco_eta (strain rate tensor + effective viscosity of p1's phase, :171-222)
+          // and for ConstEq _Visco_Stress_tensor (tau = 2 eta D, :128-166)
+          const float gxx = f.gxx + b.gxx, gxy = f.gxy + b.gxy, gxz = f.gxz + b.gxz;
+          const float gyy = f.gyy + b.gyy, gyz = f.gyz + b.gyz, gzz = f.gzz + b.gzz;
+          float d[6];
+          const float dmag = nn_strain_rate(gxx, gxy, gxz, gyy, gyz, gzz, d);
+          const float4 pa = sph[2 * p.ph], pb = sph[2 * p.ph + 1];
+          const float eta = nn_eta(dmag, pa.w, pa.z, pb.x, pb.y, p.taumax, p.bimulti);
+          viscoeta[p1] = eta;
+          etamax = fmaxf(etamax, eta);
+          if (K.nntvisco == 3) {
+            const float e2 = 2.f * eta;
+            tau[2 * p1] = make_float4(e2 * d[0], e2 * d[1], e2 * d[2], e2 * d[3]);
+            tau[2 * p1 + 1] = make_float4(e2 * d[4], e2 * d[5], 0.f, 0.f);
+          }
+        }
       }
     }
   }
@@ -736,10 +814,10 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
 void launch_nn_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
                      const float4* poscell, const float4* velrhop, const float* press, const typecode* code,
                      const unsigned* begincell, DivGrid g, const KConst& K, const float4* phases, float4* arace,
-                     float4* shiftpos, bool shift) {
+                     float4* shiftpos, bool shift, float* viscoeta, float4* tau) {
 #define SPH_NN(TV, TD, SH)                                                                                       \
   hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, \
-                     press, code, begincell, g, K, phases, arace, shiftpos)
+                     press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau)
 #define SPH_NN_TD(TV, SH)          \
   switch (K.tdensity) {            \
     case 0: SPH_NN(TV, 0, SH); break; \
@@ -747,17 +825,462 @@ void launch_nn_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const ui
     case 2: SPH_NN(TV, 2, SH); break; \
     default: SPH_NN(TV, 3, SH); break; \
   }
+#define SPH_NN_TV(SH)                                                          \
+  if (K.nnvelgrad == 2) {                                                      \
+    if (K.nntvisco == 1) SPH_NN_TD(NN_SPH_ART, SH) else SPH_NN_TD(NN_SPH_GRAD, SH) \
+  } else if (K.nntvisco == 1) SPH_NN_TD(1, SH)                                 \
+  else if (K.nntvisco == 2) SPH_NN_TD(2, SH)                                   \
+  else SPH_NN_TD(3, SH)
   if (shift) {
-    if (K.nntvisco == 1) SPH_NN_TD(1, true)
-    else if (K.nntvisco == 2) SPH_NN_TD(2, true)
-    else SPH_NN_TD(3, true)
+    SPH_NN_TV(true)
   } else {
-    if (K.nntvisco == 1) SPH_NN_TD(1, false)
-    else if (K.nntvisco == 2) SPH_NN_TD(2, false)
-    else SPH_NN_TD(3, false)
+    SPH_NN_TV(false)
   }
+#undef SPH_NN_TV
 #undef SPH_NN_TD
 #undef SPH_NN
+}
+
+// ---------------------------------------------------------------------------------------
+// Second pass of the SPH velocity gradients: the viscous force of each fluid p1 over its
+// fluid rows, then its bound rows (InteractionForcesFluid_NN_SPH_Morris / _ConsEq,
+// JSphCpu_NN_SPH.cpp:228-446; GPU twins JSphGpu_NN_ker.cu:935-1120).  Every sum is
+// order-free, so all rows are drained in point-mirrored units.  Records of 48 B:
+//   sA {x, y, z, |A|^2} (item-relative position), and per mode
+//   VM_ART    sB {v, rho}     sC {m2, visco(pp2), cs0(pp2), 0}
+//   VM_MORRIS sB {v, rho}     sC {m2, eta2, 0, 0}
+//   VM_CONSEQ sB {txx, txy, txz, tyy} sC {tyz, tzz, rho2, m2}
+// A bound p2 takes p1's phase, MassBound, and p1's eta / stress tensor (:305, :426); its
+// velocity difference is 2 v1 (no slip, :403-405).
+constexpr int VM_ART = 1, VM_MORRIS = 2, VM_CONSEQ = 3;
+#ifndef SPH_NNV_TCAP
+#define SPH_NNV_TCAP 408  // 48-B records: 408 + pad + tables keep 8 blocks per CU (<= 20 KB)
+#endif
+constexpr int NNV_TCAP = SPH_NNV_TCAP;
+
+struct NNVP1 {
+  float x, y, z;
+  float4 vr;                // velocity, rho
+  float eta;                // Morris: visco_eta[p1]
+  float4 ta, tb;            // ConsEq: tau[p1] {xx, xy, xz, yy}, {yz, zz}
+  float visco, cs0;         // artificial: p1's phase (bound p2)
+};
+
+template <int VM>
+__device__ __forceinline__ void nnv_stage(const KConst& K, unsigned rs, unsigned n, unsigned dst, int xo, int dy,
+                                          int dz, bool boundrow, const float4* __restrict__ poscell,
+                                          const float4* __restrict__ velrhop, const typecode* __restrict__ code,
+                                          const float* __restrict__ viscoeta, const float4* __restrict__ tau,
+                                          const float4* __restrict__ sph, float4* __restrict__ sA,
+                                          float4* __restrict__ sB, float4* __restrict__ sC) {
+  const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
+  for (unsigned i = threadIdx.x; i < n; i += TB) {
+    const unsigned q = rs + i;
+    const float4 pc = poscell[q];
+    const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
+    const float x2 = pc.x + float(cx2 - xo) * K.scell;
+    const float y2 = pc.y + oy, z2 = pc.z + oz;
+    sA[dst + i] = make_float4(x2, y2, z2, x2 * x2 + y2 * y2 + z2 * z2);
+    const unsigned ph = boundrow ? 0u : unsigned(code[q] & CODE_MASKVALUE);
+    const float m2 = boundrow ? K.massbound : sph[2 * ph].x;
+    if constexpr (VM == VM_CONSEQ) {
+      const float rho2 = velrhop[q].w;
+      if (boundrow) {  // tau of p1 is used for a bound p2
+        sB[dst + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        sC[dst + i] = make_float4(0.f, 0.f, rho2, m2);
+      } else {
+        const float4 ta = tau[2 * q], tb = tau[2 * q + 1];
+        sB[dst + i] = ta;
+        sC[dst + i] = make_float4(tb.x, tb.y, rho2, m2);
+      }
+    } else {
+      sB[dst + i] = velrhop[q];
+      if constexpr (VM == VM_MORRIS)
+        sC[dst + i] = make_float4(m2, boundrow ? 0.f : viscoeta[q], 0.f, 0.f);
+      else
+        sC[dst + i] = make_float4(m2, sph[2 * ph].z, sph[2 * ph].y, 0.f);
+    }
+  }
+}
+
+// One pair (the reference's pair test rr2 <= KernelSize2 && rr2 >= ALMOSTZERO; a pair that
+// fails it comes in with dr = 0, rr2 = 1e30: fr = 0, and every term adds +0).
+template <int VM, bool BOUNDP2>
+__device__ __forceinline__ void nnv_pair(const KConst& K, const NNVP1& p, float drx, float dry, float drz, float rr2,
+                                         const float4& B, const float4& C, float3& acc) {
+  const float rad = fsqrt_(rr2);
+  const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
+  const float fac = K.bwenovh * (wq * wq * wq);
+  const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
+  if constexpr (VM == VM_CONSEQ) {
+    // tau_sum = tau1 + tau2 (tau2 = tau1 for a bound p2); (tau_sum . fr) / rho2 * m2
+    const float sxx = p.ta.x + (BOUNDP2 ? p.ta.x : B.x), sxy = p.ta.y + (BOUNDP2 ? p.ta.y : B.y);
+    const float sxz = p.ta.z + (BOUNDP2 ? p.ta.z : B.z), syy = p.ta.w + (BOUNDP2 ? p.ta.w : B.w);
+    const float syz = p.tb.x + (BOUNDP2 ? p.tb.x : C.x), szz = p.tb.y + (BOUNDP2 ? p.tb.y : C.y);
+    const float ir2 = frcp(C.z);
+    const float m2 = C.w;
+    acc.x = fmaf((sxx * frx + sxy * fry + sxz * frz) * ir2, m2, acc.x);
+    acc.y = fmaf((sxy * frx + syy * fry + syz * frz) * ir2, m2, acc.y);
+    acc.z = fmaf((sxz * frx + syz * fry + szz * frz) * ir2, m2, acc.z);
+  } else {
+    const float dvx = BOUNDP2 ? 2.f * p.vr.x : p.vr.x - B.x;
+    const float dvy = BOUNDP2 ? 2.f * p.vr.y : p.vr.y - B.y;
+    const float dvz = BOUNDP2 ? 2.f * p.vr.z : p.vr.z - B.z;
+    const float m2 = C.x;
+    const float rho2 = B.w;
+    if constexpr (VM == VM_MORRIS) {
+      // temp = (eta1 + eta2) / ((r2 + eta^2) rho2); vtemp = m2 temp (dr . fr)
+      const float eta2 = BOUNDP2 ? p.eta : C.y;
+      const float temp = (p.eta + eta2) * frcp((rr2 + K.eta2) * rho2);
+      const float vtemp = m2 * temp * (fac * rr2);
+      acc.x = fmaf(vtemp, dvx, acc.x);
+      acc.y = fmaf(vtemp, dvy, acc.y);
+      acc.z = fmaf(vtemp, dvz, acc.z);
+    } else {  // artificial, with the phase of p2 (p1's for a bound p2)
+      const float dot = drx * dvx + dry * dvy + drz * dvz;
+      if (dot < 0.f) {
+        const float visco = BOUNDP2 ? p.visco : C.y, cbar = BOUNDP2 ? p.cs0 : C.z;
+        const float dot_rr2 = dot * frcp(rr2 + K.eta2);
+        const float amubar = K.kernelh * dot_rr2;
+        const float robar = (p.vr.w + rho2) * 0.5f;
+        const float pi_visc = (-visco * cbar * amubar * frcp(robar)) * m2;
+        acc.x = fmaf(-pi_visc, frx, acc.x);
+        acc.y = fmaf(-pi_visc, fry, acc.y);
+        acc.z = fmaf(-pi_visc, frz, acc.z);
+      }
+    }
+  }
+}
+
+// The accepted candidates of one round (four 64-bit words), two pairs per iteration.
+template <int VM, bool BOUNDP2>
+__device__ __forceinline__ void nnv_drain4(const KConst& K, const NNVP1& p, unsigned long long c0,
+                                           unsigned long long c1, unsigned long long c2, unsigned long long c3, int b0,
+                                           int b1, int b2, int b3, const float4* __restrict__ sA,
+                                           const float4* __restrict__ sB, const float4* __restrict__ sC,
+                                           float3& acc) {
+#pragma unroll
+  for (int pass = 0; pass < 3; pass++) {  // drop empty words, keep the order
+    const bool e2 = c2 == 0ull;
+    c2 = e2 ? c3 : c2;
+    b2 = e2 ? b3 : b2;
+    c3 = e2 ? 0ull : c3;
+    const bool e1 = c1 == 0ull;
+    c1 = e1 ? c2 : c1;
+    b1 = e1 ? b2 : b1;
+    c2 = e1 ? c3 : c2;
+    b2 = e1 ? b3 : b2;
+    c3 = e1 ? 0ull : c3;
+    const bool e0 = c0 == 0ull;
+    c0 = e0 ? c1 : c0;
+    b0 = e0 ? b1 : b0;
+    c1 = e0 ? c2 : c1;
+    b1 = e0 ? b2 : b1;
+    c2 = e0 ? c3 : c2;
+    b2 = e0 ? b3 : b2;
+    c3 = e0 ? 0ull : c3;
+  }
+  auto pop = [&](void) -> int {
+    const int j = b0 + int(__builtin_ctzll(c0 | (1ull << 63)));
+    c0 &= c0 - 1ull;
+    const bool e = c0 == 0ull;
+    c0 = e ? c1 : c0;
+    b0 = e ? b1 : b0;
+    c1 = e ? c2 : c1;
+    b1 = e ? b2 : b1;
+    c2 = e ? c3 : c2;
+    b2 = e ? b3 : b2;
+    c3 = e ? 0ull : c3;
+    return j;
+  };
+  while (c0) {
+    const int j1 = pop();
+    const bool two = c0 != 0ull;
+    const int j2p = pop();
+    const int j2 = two ? j2p : j1;
+    const float4 A1 = sA[j1], A2 = sA[j2];
+    const float4 B1 = sB[j1], B2 = sB[j2];
+    const float4 C1 = sC[j1], C2 = sC[j2];
+    float drx1 = p.x - A1.x, dry1 = p.y - A1.y, drz1 = p.z - A1.z;
+    float drx2 = p.x - A2.x, dry2 = p.y - A2.y, drz2 = p.z - A2.z;
+    float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
+    float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
+    const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
+    const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
+    drx1 = ok1 ? drx1 : 0.f;
+    dry1 = ok1 ? dry1 : 0.f;
+    drz1 = ok1 ? drz1 : 0.f;
+    rr21 = ok1 ? rr21 : 1e30f;
+    drx2 = ok2 ? drx2 : 0.f;
+    dry2 = ok2 ? dry2 : 0.f;
+    drz2 = ok2 ? drz2 : 0.f;
+    rr22 = ok2 ? rr22 : 1e30f;
+    nnv_pair<VM, BOUNDP2>(K, p, drx1, dry1, drz1, rr21, B1, C1, acc);
+    nnv_pair<VM, BOUNDP2>(K, p, drx2, dry2, drz2, rr22, B2, C2, acc);
+  }
+}
+
+// A pass of the p1 over its 9 rows of one kind in point-mirrored drain units (the units of
+// nn_pass_mirrored), rows too long for one segment row by row in NNV_TCAP segments.
+template <int VM, bool BOUNDP2>
+__device__ __forceinline__ float3 nnv_pass(const KConst& K, const DivGrid& g, const RowCtx& rc, const NNVP1& p,
+                                           float thr, const unsigned* __restrict__ bc,
+                                           const float4* __restrict__ poscell, const float4* __restrict__ velrhop,
+                                           const typecode* __restrict__ code, const float* __restrict__ viscoeta,
+                                           const float4* __restrict__ tau, const float4* __restrict__ sph,
+                                           float4* __restrict__ sA, float4* __restrict__ sB,
+                                           float4* __restrict__ sC) {
+  float3 acc = make_float3(0.f, 0.f, 0.f);
+  const unsigned cellinit = BOUNDP2 ? 0u : g.boxfluid;
+  const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
+  for (int u = 0; u < 5; u++) {
+    const int dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
+    const int dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
+    const bool paired = u < 4;
+    unsigned rs[2] = {0, 0}, re[2] = {0, 0}, ls[2] = {0, 0}, le[2] = {0, 0};
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      if (k == 1 && !paired) break;
+      const int dz = k ? -dza : dza, dy = k ? -dya : dya;
+      const int z = rc.cz + dz, y = rc.cy + dy;
+      if (z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;
+      const unsigned rowbase = cellinit + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+      rs[k] = bc[rowbase + rc.xa];
+      re[k] = bc[rowbase + rc.xb + 1];
+      ls[k] = bc[rowbase + rc.lxa];
+      le[k] = bc[rowbase + rc.lxb + 1];
+    }
+    const unsigned n0 = re[0] - rs[0], n1 = re[1] - rs[1];
+    if (n0 + n1 == 0u) continue;  // block-uniform
+    if (n0 + n1 <= unsigned(NNV_TCAP)) {
+      __syncthreads();
+      if (n0)
+        nnv_stage<VM>(K, rs[0], n0, 0u, rc.xo, dya, dza, BOUNDP2, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
+                      sC);
+      if (n1)
+        nnv_stage<VM>(K, rs[1], n1, n0, rc.xo, -dya, -dza, BOUNDP2, poscell, velrhop, code, viscoeta, tau, sph, sA,
+                      sB, sC);
+      __syncthreads();
+      const int wa0 = int(ls[0] - rs[0]), wa1 = rc.act && n0 ? int(le[0] - rs[0]) : wa0;
+      const int wb0 = int(n0 + ls[1] - rs[1]), wb1 = rc.act && n1 ? int(n0 + le[1] - rs[1]) : wb0;
+      for (int off = 0;; off += 128) {
+        const int na = wa1 - wa0 - off, nb = wb1 - wb0 - off;
+        if (na <= 0 && nb <= 0) break;
+        unsigned long long c0, c1, c2, c3;
+        test128(sA, wa0 + off, min(na, 128), px2, py2, pz2, thr, c0, c1);
+        test128(sA, wb0 + off, min(nb, 128), px2, py2, pz2, thr, c2, c3);
+        nnv_drain4<VM, BOUNDP2>(K, p, c0, c1, c2, c3, wa0 + off, wa0 + off + 64, wb0 + off, wb0 + off + 64, sA, sB,
+                                sC, acc);
+      }
+    } else {
+      for (int k = 0; k < 2; k++) {
+        const int dz = k ? -dza : dza, dy = k ? -dya : dya;
+        for (unsigned seg = rs[k]; seg < re[k]; seg += NNV_TCAP) {
+          const unsigned segn = min(unsigned(NNV_TCAP), re[k] - seg);
+          __syncthreads();
+          nnv_stage<VM>(K, seg, segn, 0u, rc.xo, dy, dz, BOUNDP2, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
+                        sC);
+          __syncthreads();
+          const int w0 = int(max(ls[k], seg) - seg);
+          const int w1 = rc.act ? max(w0, int(min(le[k], seg + segn)) - int(seg)) : w0;
+          for (int off = w0; off < w1; off += 128) {
+            unsigned long long c0, c1;
+            test128(sA, off, min(w1 - off, 128), px2, py2, pz2, thr, c0, c1);
+            nnv_drain4<VM, BOUNDP2>(K, p, c0, c1, 0ull, 0ull, off, off + 64, 0, 0, sA, sB, sC, acc);
+          }
+        }
+      }
+    }
+  }
+  return acc;
+}
+
+template <int VM>
+__global__ __launch_bounds__(TB) void k_nn_visc(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
+                                                unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
+                                                const float4* __restrict__ velrhop, const typecode* __restrict__ code,
+                                                const float* __restrict__ viscoeta, const float4* __restrict__ tau,
+                                                const unsigned* __restrict__ bc, DivGrid g, KConst K,
+                                                const float4* __restrict__ phases, float4* __restrict__ arace) {
+  __shared__ float4 sA[NNV_TCAP + SPH_PAD];
+  __shared__ float4 sB[NNV_TCAP];
+  __shared__ float4 sC[NNV_TCAP];
+  __shared__ float4 sph[2 * SPH_MAXPHASES];
+  __shared__ unsigned s_item;
+  __shared__ unsigned char s_perm[TB];
+  __shared__ unsigned s_nwave[4];
+  if (threadIdx.x < 2 * SPH_MAXPHASES) sph[threadIdx.x] = phases[threadIdx.x];
+  const ItemGroups IG(sc);
+  const unsigned grp = blockIdx.x & 7;
+  float ace2max = 0.f;
+  for (unsigned q = 0; q < 8; q++) {
+    const unsigned xg = (grp + q) & 7;
+    const ItemGroup gr = IG.group(xg);
+    // fluid items only (a group's fluid items come first in its claim order)
+    const unsigned nst = (gridDim.x - xg + 7u) / 8u;
+    bool first = q == 0;
+    for (;;) {
+      if (threadIdx.x == 0)
+        s_item = first ? (blockIdx.x >> 3)
+                 : (nst + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gr.nfg)
+                     ? gr.nfg
+                     : nst + atomicAdd(&qctr[xg * QSTRIDE], 1u);
+      first = false;
+      __syncthreads();
+      const unsigned c = s_item;
+      __syncthreads();
+      if (c >= gr.nfg) break;
+      const uint4 item = items[gr.item(c)];
+      const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
+      const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);
+      const int xo = (ia + ib + 1) >> 1;
+      const int xa = max(ia - 1, 0), xb = min(ib + 1, g.ncx - 1);
+      const unsigned p1 = item.z + lane_order(poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
+      const bool act = threadIdx.x < item.w - item.z;
+      NNVP1 p;
+      int cx1 = ia;
+      p.eta = 0.f;
+      p.ta = p.tb = make_float4(0.f, 0.f, 0.f, 0.f);
+      p.visco = p.cs0 = 0.f;
+      if (act) {
+        const float4 pc1 = poscell[p1];
+        cx1 = int(DcelCellx(K.domcellcode, __float_as_uint(pc1.w)));
+        p.x = pc1.x + float(cx1 - xo) * K.scell;
+        p.y = pc1.y;
+        p.z = pc1.z;
+        p.vr = velrhop[p1];
+        const int ph = int(code[p1] & CODE_MASKVALUE);
+        if constexpr (VM == VM_MORRIS) p.eta = viscoeta[p1];
+        if constexpr (VM == VM_CONSEQ) {
+          p.ta = tau[2 * p1];
+          p.tb = tau[2 * p1 + 1];
+        }
+        if constexpr (VM == VM_ART) {
+          p.visco = sph[2 * ph].z;
+          p.cs0 = sph[2 * ph].y;
+        }
+      } else {
+        p.x = p.y = p.z = 1e30f;
+        p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
+      }
+      const int lxa = max(cx1 - 1, 0), lxb = min(cx1 + 1, g.ncx - 1);
+      const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
+      const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act};
+      const float3 f = nnv_pass<VM, false>(K, g, rc, p, thr, bc, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
+                                           sC);
+      const float3 b = nnv_pass<VM, true>(K, g, rc, p, thr, bc, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
+                                          sC);
+      if (act) {
+        // ace[p1] = ace[p1] + acep1 per pass when non-zero (JSphCpu_NN_SPH.cpp:442-444)
+        float4 r = arace[p1];
+        if (f.x != 0.f || f.y != 0.f || f.z != 0.f) {
+          r.x += f.x;
+          r.y += f.y;
+          r.z += f.z;
+        }
+        if (b.x != 0.f || b.y != 0.f || b.z != 0.f) {
+          r.x += b.x;
+          r.y += b.y;
+          r.z += b.z;
+        }
+        if (K.sim2d) r.y = 0.f;  // Simulate2D: Acec[].y = 0 after the whole interaction
+        arace[p1] = r;
+        ace2max = nanmax(ace2max, r.x * r.x + r.y * r.y + r.z * r.z);
+      }
+    }
+  }
+  wave_max_atomic(sc, RED_ACEMAX2, ace2max);
+}
+
+void launch_nn_visc(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
+                    const float4* poscell, const float4* velrhop, const typecode* code, const float* viscoeta,
+                    const float4* tau, const unsigned* begincell, DivGrid g, const KConst& K, const float4* phases,
+                    float4* arace) {
+#define SPH_NNV(VM)                                                                                             \
+  hipLaunchKernelGGL((k_nn_visc<VM>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, code, \
+                     viscoeta, tau, begincell, g, K, phases, arace)
+  if (K.nntvisco == 1) SPH_NNV(VM_ART);
+  else if (K.nntvisco == 2) SPH_NNV(VM_MORRIS);
+  else SPH_NNV(VM_CONSEQ);
+#undef SPH_NNV
+}
+
+// ---- slabs: the first pass's eta / tau of the face columns for the neighbours' ghosts ----
+__global__ __launch_bounds__(256) void k_nn_face_pack(const DevScalars* __restrict__ sc, PartArrays a, KConst K,
+                                                      DivGrid g, const float* __restrict__ viscoeta,
+                                                      const float4* __restrict__ tau, NNFaceRec* __restrict__ sl,
+                                                      NNFaceRec* __restrict__ sr, unsigned capl, unsigned capr,
+                                                      unsigned* __restrict__ idxmap, unsigned nidx) {
+  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= sc->np) return;
+  const unsigned id = a.idp[p];
+  if (id < nidx) idxmap[id] = p;
+  if (p < sc->npb) return;  // fluid only (bound p2 use p1's values)
+  const unsigned dc = a.dcell[p];
+  if (dc >= DCELL_DISCARD) return;
+  const int lcx = int(DcelCellx(K.domcellcode, dc)) - g.xoff;
+  for (int side = 0; side < 2; side++) {  // a slab of one owned column sends a particle both ways
+    NNFaceRec* dst = nullptr;
+    unsigned cap = 0;
+    if (side == 0 && lcx == g.xown0 && g.xown0 > 0) { dst = sl; cap = capl; }
+    if (side == 1 && lcx == g.xown1 - 1 && g.xown1 < g.ncx) { dst = sr; cap = capr; }
+    if (!dst) continue;
+    const unsigned k = atomicAdd(&dst[0].idp, 1u);
+    if (k + 1 >= cap) continue;  // cannot happen: the buffers hold every ghost sent at the divide
+    NNFaceRec r;
+    r.idp = id;
+    r.v[0] = viscoeta ? viscoeta[p] : 0.f;
+    const float4 ta = tau ? tau[2 * p] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 tb = tau ? tau[2 * p + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+    r.v[1] = ta.x;
+    r.v[2] = ta.y;
+    r.v[3] = ta.z;
+    r.v[4] = ta.w;
+    r.v[5] = tb.x;
+    r.v[6] = tb.y;
+    dst[k + 1] = r;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_nn_face_apply(DevScalars* __restrict__ sc, const NNFaceRec* __restrict__ rl,
+                                                       const NNFaceRec* __restrict__ rr, unsigned capl,
+                                                       unsigned capr, const unsigned* __restrict__ idxmap,
+                                                       unsigned nidx, const unsigned* __restrict__ idp,
+                                                       float* __restrict__ viscoeta, float4* __restrict__ tau,
+                                                       int withtau) {
+  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+  const NNFaceRec* r = (blockIdx.y == 0 ? rl : rr);
+  const unsigned cap = (blockIdx.y == 0 ? capl : capr);
+  if (!r || i + 1 >= cap || i >= r[0].idp) return;
+  const NNFaceRec q = r[i + 1];
+  const unsigned p = q.idp < nidx ? idxmap[q.idp] : 0xffffffffu;
+  if (p >= sc->np || idp[p] != q.idp) {  // every face particle arrived as a ghost at the divide
+    atomicOr(&sc->error_flags, ERR_HALO);
+    return;
+  }
+  viscoeta[p] = q.v[0];
+  if (withtau) {
+    tau[2 * p] = make_float4(q.v[1], q.v[2], q.v[3], q.v[4]);
+    tau[2 * p + 1] = make_float4(q.v[5], q.v[6], 0.f, 0.f);
+  }
+}
+
+void launch_nn_face_pack(hipStream_t stm, unsigned cap, const DevScalars* sc, const PartArrays& a, const KConst& K,
+                         const DivGrid& g, const float* viscoeta, const float4* tau, NNFaceRec* sl, NNFaceRec* sr,
+                         unsigned capl, unsigned capr, unsigned* idxmap, unsigned nidx) {
+  if (sl) hipMemsetAsync(sl, 0, sizeof(NNFaceRec), stm);
+  if (sr) hipMemsetAsync(sr, 0, sizeof(NNFaceRec), stm);
+  hipLaunchKernelGGL(k_nn_face_pack, dim3((cap + 255) / 256), dim3(256), 0, stm, sc, a, K, g, viscoeta, tau, sl, sr,
+                     capl, capr, idxmap, nidx);
+}
+
+void launch_nn_face_apply(hipStream_t stm, DevScalars* sc, const NNFaceRec* rl, const NNFaceRec* rr, unsigned capl,
+                          unsigned capr, const unsigned* idxmap, unsigned nidx, const unsigned* idp, float* viscoeta,
+                          float4* tau, bool withtau) {
+  const unsigned n = std::max(capl, capr);
+  if (!n) return;
+  hipLaunchKernelGGL(k_nn_face_apply, dim3((n + 255) / 256, 2), dim3(256), 0, stm, sc, rl, rr, capl, capr, idxmap,
+                     nidx, idp, viscoeta, tau, int(withtau));
 }
 
 }  // namespace sphx

@@ -128,8 +128,6 @@ void derive_constants(const SphCaseDef& c, SphConstants& k) {
   // NN multiphase: JSph::InitMultiPhase + ConfigConstantsMP (JSph.cpp:3137-3242, v5.0 solver)
   if (k.tboundary == SPH_BOUND_MDBC)
     throw SphError(SPH_ERR_ARG, "Multiphase formulations are not supported with BC_mDBC.");
-  if (k.velgrad != SPH_VELGRAD_FDA)
-    throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase: only the FDA velocity gradients are implemented");
   if (c.nphases < 1 || c.nphases > SPH_MAXPHASES) throw SphError(SPH_ERR_ARG, "The number of phases is invalid.");
   k.nphases = c.nphases;
   bool cs0_present = true;
@@ -200,6 +198,7 @@ static KConst make_kconst(const SphConstants& c) {
   K.scelldiv = c.scelldiv;
   K.nn = (c.rheology == SPH_RHEOLOGY_NN) ? 1 : 0;
   K.nntvisco = c.tvisco;
+  K.nnvelgrad = c.velgrad;
   K.shiftmode = c.shift_mode;
   K.sim2d = c.data2d;
   K.lamda = c.relaxation_dt;
@@ -361,7 +360,22 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   // The tiled kernel stages the 3x3 rows of 3 cells of CellMode=full, or the 5x5 rows of
   // 5 half-cells of CellMode=half (run_pass_half).
   nn_ = (C.rheology == SPH_RHEOLOGY_NN);
+  nnsph_ = nn_ && C.velgrad == SPH_VELGRAD_SPH;
+  casenp_ = cdef.np;
   shift_ = (C.shift_mode != SPH_SHIFT_NONE);
+  if (nnsph_ && slab()) {
+    // the first interaction's face records: the initial particles of the face and ghost
+    // columns (both sides of a face count the same particles); later from each exchange
+    const std::vector<unsigned> cx = initial_columns(C, init);
+    const bool hl = slabcfg_.rank > 0, hr = slabcfg_.rank + 1 < slabcfg_.nranks;
+    for (unsigned p : sel) {
+      const int c = int(cx[p]);
+      face_sl_ += (hl && c == slabcfg_.c0) ? 1u : 0u;
+      face_sr_ += (hr && c == slabcfg_.c1 - 1) ? 1u : 0u;
+      face_rl_ += (hl && c == slabcfg_.c0 - 1) ? 1u : 0u;
+      face_rr_ += (hr && c == slabcfg_.c1) ? 1u : 0u;
+    }
+  }
   if (nn_) {
     // the NN interaction is the tiled kernel of sph_nn.hip only
     if (C.scelldiv != 1) throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase: CellMode=half is not implemented");
@@ -423,6 +437,7 @@ void SphGpuSingle::AllocFixed() {
     inc_.ctr = (unsigned*)dmalloc(4 * QSTRIDE);
     check_hip(hipMemset(inc_.ctr, 0, 4 * QSTRIDE), "zero far count");
   }
+  if (nnsph_ && slab()) idxmap_ = (unsigned*)dmalloc(4 * size_t(std::max(casenp_, 1u)));
   sc_ = (DevScalars*)dmalloc(sizeof(DevScalars));
   dttrace_ = (double*)dmalloc(8 * size_t(tracecap_));
   pairs_ = (unsigned long long*)dmalloc(8 * 6);
@@ -485,6 +500,10 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
   items_ = (uint4*)dmalloc(16 * (n / 128 + 2 * size_t(G.ncy) * size_t(G.ncz) + size_t(nctmax_) / 2 + 2));
   arace_ = (float4*)dmalloc(16 * n);
   if (shift_) shiftpos_ = (float4*)dmalloc(16 * n);  // the interaction's shifting sums
+  if (nnsph_) {
+    viscoeta_ = (float*)dmalloc(4 * n);
+    if (C.tvisco == SPH_VISCO_CONSTEQ) tau_ = (float4*)dmalloc(32 * n);
+  }
   for (int i = 0; i < 2; i++) {
     sort_.keys[i] = (unsigned*)dmalloc(4 * n);
     sort_.vals[i] = (unsigned*)dmalloc(4 * n);
@@ -522,8 +541,9 @@ void SphGpuSingle::Free() {
   FreeParticles();
   for (void* p : allocs_) (void)hipFree(p);
   allocs_.clear();
-  for (void* p : {sendgbuf_, sendmbuf_, (void*)recvg_, (void*)recvm_})
+  for (void* p : {sendgbuf_, sendmbuf_, (void*)recvg_, (void*)recvm_, (void*)nnface_})
     if (p) (void)hipFree(p);
+  nnface_ = nullptr;
   sendgbuf_ = sendmbuf_ = nullptr;
   recvg_ = nullptr;
   recvm_ = nullptr;
@@ -732,6 +752,14 @@ void SphGpuSingle::Exchange() {
   check_hip(hipEventRecord(xev_, stream), "exchange: event");
   WaitEvent(xev_, "exchange: wait counts");
   const SlabCounts c = *slabcnt_host_;
+  if (nnsph_) {
+    // the neighbour's ghosts of this slab: the ghosts sent now + the migrants it sent here
+    // (it keeps them as ghosts); the neighbour derives the same sizes from its counts
+    face_sl_ = hl ? unsigned(c.sendl[0] + c.recvl[1]) : 0u;
+    face_sr_ = hr ? unsigned(c.sendr[0] + c.recvr[1]) : 0u;
+    face_rl_ = hl ? unsigned(c.recvl[0] + c.sendl[1]) : 0u;
+    face_rr_ = hr ? unsigned(c.recvr[0] + c.sendr[1]) : 0u;
+  }
   const unsigned long long gneed = std::max(c.sendl[0], c.sendr[0]), mneed = std::max(c.sendl[1], c.sendr[1]);
   if (gneed > send_.gcap || mneed > send_.mcap) {  // records past a capacity were not written: grow, pack again
     if (gneed > send_.gcap) {
@@ -932,7 +960,16 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
     // ComputeSymplecticPre) and Verlet
     TimedBegin(0);
     launch_nn_tiled(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, cur_.code, begincell_,
-                    G, K, phasek_, arace_, shiftpos_, shift_ && interstep != 2);
+                    G, K, phasek_, arace_, shiftpos_, shift_ && interstep != 2, viscoeta_, tau_);
+    if (nnsph_) {
+      // SPH velocity gradients: the viscous force is a second pass over the neighbours,
+      // reading their effective viscosities / stress tensors (JSphCpu_NN_SPH.cpp:671-696)
+      if (slab() && C.tvisco != SPH_VISCO_ARTIFICIAL && (transport_->has_left() || transport_->has_right()))
+        NNFaceExchange();
+      check_hip(hipMemsetAsync(qctr_, 0, QCTR_BYTES, stream), "zero work counters");
+      launch_nn_visc(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, cur_.code, viscoeta_, tau_,
+                     begincell_, G, K, phasek_, arace_);
+    }
   } else if (tiled_) {
     // The tiled kernel writes the arace of every owned particle (skipped boundary items
     // get ar = 0) and resets its own work counters at exit (zeroed once at allocation).
@@ -945,6 +982,29 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
                        ftmassp_);
   }
   TimedEnd(0);
+}
+
+// Slabs, SPH velocity gradients: the owned face-column fluid particles' eta (and tau) to the
+// neighbours, written into their ghost copies by idp before the second pass.  Fixed-size
+// records (count in slot 0) sized from the last exchange, so no host wait.
+void SphGpuSingle::NNFaceExchange() {
+  const bool hl = transport_->has_left(), hr = transport_->has_right();
+  const unsigned long long nsl = hl ? face_sl_ + 1ull : 0, nsr = hr ? face_sr_ + 1ull : 0;
+  const unsigned long long nrl = hl ? face_rl_ + 1ull : 0, nrr = hr ? face_rr_ + 1ull : 0;
+  const unsigned long long need = nsl + nsr + nrl + nrr;
+  if (need > nnfacecap_) {
+    check_hip(hipStreamSynchronize(stream), "nn faces: sync");
+    if (nnface_) check_hip(hipFree(nnface_), "hipFree");
+    nnfacecap_ = need + need / 2 + 1024;
+    check_hip(hipMalloc((void**)&nnface_, sizeof(NNFaceRec) * nnfacecap_), "hipMalloc NN face records");
+  }
+  NNFaceRec *sl = nnface_, *sr = sl + nsl, *rl = sr + nsr, *rr = rl + nrl;
+  launch_nn_face_pack(stream, cap_, sc_, cur_, K, G, viscoeta_, tau_, hl ? sl : nullptr, hr ? sr : nullptr,
+                      unsigned(nsl), unsigned(nsr), idxmap_, casenp_);
+  transport_->exchange(sl, sizeof(NNFaceRec) * nsl, sr, sizeof(NNFaceRec) * nsr, rl, sizeof(NNFaceRec) * nrl, rr,
+                       sizeof(NNFaceRec) * nrr, stream);
+  launch_nn_face_apply(stream, sc_, hl ? rl : nullptr, hr ? rr : nullptr, unsigned(nrl), unsigned(nrr), idxmap_,
+                       casenp_, cur_.idp, viscoeta_, tau_, C.tvisco == SPH_VISCO_CONSTEQ);
 }
 
 void SphGpuSingle::DtVariable(int mode) {

@@ -138,6 +138,19 @@ class SphGpuSingle {
   float4* phaseeos_ = nullptr;  // {rho0, cteb, gamma, integer gamma} per phase
   float phase_rho_[SPH_MAXPHASES] = {};
   float4* shiftpos_ = nullptr;  // shifting sums of the last interaction [cap]
+  // NN with SPH velocity gradients (VelocityGradientType 2): the first pass's effective
+  // viscosity [cap] and stress tensor (ConstEq) [2 cap], read by the second pass
+  bool nnsph_ = false;
+  float* viscoeta_ = nullptr;
+  float4* tau_ = nullptr;
+  // slabs: face records of eta / tau for the neighbours' ghosts; sizes (records) of the
+  // send-left, send-right, receive-left, receive-right regions, known to both sides of a face
+  NNFaceRec* nnface_ = nullptr;
+  unsigned long long nnfacecap_ = 0;
+  unsigned face_sl_ = 0, face_sr_ = 0, face_rl_ = 0, face_rr_ = 0;
+  unsigned* idxmap_ = nullptr;  // idp -> local index [CaseNp]
+  unsigned casenp_ = 0;
+  void NNFaceExchange();
   unsigned* begincell_ = nullptr;
   uint4* items_ = nullptr;        // tiled-interaction work items (per divide)
   unsigned* rowtmp_ = nullptr;    // per-row item counts/offsets

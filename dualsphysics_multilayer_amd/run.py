@@ -312,9 +312,12 @@ def parse_args(argv: list[str]) -> dict:
             v = _f32(full)
             if v > 10:
                 raise CaseError(f"invalid option {a}")
-            ov["visco"] = v
-        elif word == "VISCOLAMSPS":
-            raise CaseError("Laminar+SPS viscosity is not supported by this core.")
+            ov["visco"], ov["tvisco"] = v, 1
+        elif word == "VISCOLAMSPS":  # JSphCfgRun.cpp:329-333
+            v = _f32(full)
+            if v > 0.001:
+                raise CaseError(f"invalid option {a}")
+            ov["visco"], ov["tvisco"] = v, 2
         elif word == "VISCOBOUNDFACTOR":
             v = _f32(full)
             if v < 0:
@@ -330,9 +333,11 @@ def parse_args(argv: list[str]) -> dict:
             if not 0 <= v <= 1:
                 raise CaseError(f"invalid option {a}")
             ov["ddtvalue"] = v
-        elif word == "SHIFTING":
-            if full.upper() not in ("NONE", "0", ""):
-                raise CaseError("Shifting is not supported by this core.")
+        elif word == "SHIFTING":  # JSphCfgRun.cpp:355-362; JSph.cpp:825-835: ConfigBasic(mode) -> coef -2, TFS 0
+            modes = {"NONE": 0, "NOBOUND": 1, "NOFIXED": 2, "FULL": 3}
+            if full.upper() not in modes:
+                raise CaseError(f"invalid option {a}")
+            ov["shift_mode"], ov["shift_coef"], ov["shift_tfs"] = modes[full.upper()], -2.0, 0.0
         elif word == "SV":
             kinds = {s.strip().lower() for s in full.split(",") if s.strip()}
             bad = kinds - {"binx", "none", "info", "+binx", "-binx", "-csv", "-vtk", "-info", "+info"}

@@ -245,7 +245,8 @@ def _config_domain(p: _Params) -> _DomainCfg:
 # command-line overrides (JSphCfgRun -> JSph::LoadConfigCommands) this core takes
 OVERRIDES = ("step_algorithm", "verlet_steps", "tdensity", "ddtvalue", "visco", "viscoboundfactor", "cellmode",
              "celldomfixed", "cflnumber", "rhopoutmin", "rhopoutmax", "timemax", "timeout", "dtini", "dtmin",
-             "coefdtmin", "domain_fixed", "tboundary", "slipmode", "mdbc_threshold")
+             "coefdtmin", "domain_fixed", "tboundary", "slipmode", "mdbc_threshold", "tvisco", "shift_mode",
+             "shift_coef", "shift_tfs")
 
 
 class XmlCase:
@@ -433,8 +434,6 @@ class XmlCase:
             raise CaseError("Viscosity treatment is not valid.")
         if tv == 3 and self.rheology != 2:
             raise CaseError("ViscoTreatment 'Constitutive  eq.' not valid for Single-phase classic formulation.")
-        if tv != 1 and self.rheology != 2:
-            raise CaseError("Single-phase Laminar+SPS viscosity (ViscoTreatment=2) is not supported by this core.")
         self.tvisco = tv
         self.visco = p.num("Visco")
         self.viscoboundfactor = p.num("ViscoBoundFactor", True, 1.0)
@@ -469,8 +468,6 @@ class XmlCase:
                 raise CaseError("Shifting mode in <execution><parameters> is not valid.")
             coef = float(np.float32(p.num("ShiftCoef", True, -2)))
             if sm != 0 and coef != 0:
-                if self.rheology != 2:
-                    raise CaseError("Shifting is supported by this core in NN multiphase cases only.")
                 self.shift_mode, self.shift_coef = sm, coef
                 self.shift_tfs = float(np.float32(p.num("ShiftTFS", True, 0)))
         self.timemax = p.num("TimeMax")

@@ -10,7 +10,12 @@ Part_XXXX.bi4 is converted by partdump_ref and stored (sorted by idp) as
                               (keys s<step>_idp, s<step>_pos, ...)
                               plus dt trace ``dt`` (from the part times).
 
-Usage: python tests/golden/make_golden.py [--only NAME]
+Viscosity / shifting variants (EXT_CASES) also store ext = [ViscoTreatment, Visco,
+Shifting, ShiftCoef, ShiftTFS] and, with --noise, the reference's own rounding-noise floor
+noise_<step> = [dpos, dvel, drho]: the largest differences between the fast-math build and
+the same sources built without -ffast-math (``make -C oracle strict``).
+
+Usage: python tests/golden/make_golden.py [--only NAME] [--noise]
 """
 import argparse
 import os
@@ -39,6 +44,18 @@ CASES = {
     # 2-D (Simulate2D): the CaseDambreakVal2D geometry (gencase_ref dim 2); meta[6] = 2
     "verlet_ddt2_2d_dp0.02": (0.02, 1, 2, 100, (1, 10, 100), 1, (), 2),
     "symplectic_ddt1_2d_dp0.02": (0.02, 2, 1, 60, (1, 20, 60), 1, (), 2),
+}
+
+
+# Single-phase Laminar+SPS viscosity (ViscoTreatment 2; kinematic viscosity 1e-6 m2/s,
+# JSphCpu.cpp:765-809, ComputeSpsTau :929-954) and shifting (JSphShifting, modes 1-3).
+# name: (dp, step, ddt, nsteps, kept steps, (tvisco, visco, shifting, shiftcoef, shifttfs))
+EXT_CASES = {
+    "verlet_lamsps_ddt2_dp0.02": (0.02, 1, 2, 100, (1, 10, 100), (2, "1e-6", 0, "-2", "0")),
+    "symplectic_lamsps_ddt1_dp0.025": (0.025, 2, 1, 60, (1, 20, 60), (2, "1e-6", 0, "-2", "0")),
+    "verlet_shift_nobound_dp0.025": (0.025, 1, 2, 60, (1, 41, 60), (1, "0.1", 1, "-2", "0")),
+    "symplectic_shift_full_tfs_dp0.025": (0.025, 2, 2, 60, (1, 20, 60), (1, "0.1", 3, "-2", "2.75")),
+    "verlet_lamsps_shift_nofixed_dp0.03": (0.03, 1, 0, 45, (1, 41, 45), (2, "1e-6", 2, "-2", "1.5")),
 }
 
 
@@ -92,11 +109,64 @@ def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=(), dim=3):
         shutil.rmtree(tmp)
 
 
+def run_ext(exe, dp, step, ddt, nsteps, ext, tmp, tag):
+    tv, visco, sh, coef, tfs = ext
+    d = os.path.join(tmp, "case")
+    os.makedirs(d, exist_ok=True)
+    subprocess.check_call([os.path.join(REF, "gencase_ref"), repr(dp), d, str(step), str(ddt), "1.5", "CaseDambreak",
+                           "1", "3", str(tv), visco, str(sh), coef, tfs], stdout=subprocess.DEVNULL)
+    out = os.path.join(tmp, "out_" + tag)
+    subprocess.check_call([exe, os.path.join(d, "CaseDambreak"), out, "-nsteps:%d" % nsteps, "-svsteps:1",
+                           "-saveposdouble:1", "-sv:binx", "-svres:0"], stdout=subprocess.DEVNULL)
+    return out
+
+
+def make_ext(name, dp, step, ddt, nsteps, keep, ext, noise):
+    tmp = tempfile.mkdtemp(prefix="golden_")
+    try:
+        out = run_ext(os.path.join(REF, "DualSPHysics5.2CPU_ref"), dp, step, ddt, nsteps, ext, tmp, "fast")
+        outs = run_ext(os.path.join(REF, "DualSPHysics5.2CPU_strict"), dp, step, ddt, nsteps, ext, tmp,
+                       "strict") if noise else None
+        arrays, times = {}, []
+        fn = os.path.join(tmp, "p.bin")
+        for part in range(nsteps + 1):
+            subprocess.check_call([os.path.join(REF, "partdump_ref"), out, str(part), fn], stdout=subprocess.DEVNULL)
+            t, idp, pos, vel, rho = load_dump(fn)
+            o = np.argsort(idp, kind="stable")
+            idp, pos, vel, rho = idp[o], pos[o], vel[o], rho[o]
+            times.append(t)
+            if part in keep:
+                arrays.update({"s%d_idp" % part: idp, "s%d_pos" % part: pos, "s%d_vel" % part: vel,
+                               "s%d_rhop" % part: rho, "s%d_time" % part: np.float64(t)})
+                if outs:
+                    subprocess.check_call([os.path.join(REF, "partdump_ref"), outs, str(part), fn],
+                                          stdout=subprocess.DEVNULL)
+                    _, idps, poss, vels, rhos = load_dump(fn)
+                    o = np.argsort(idps, kind="stable")
+                    assert np.array_equal(idp, idps[o]), "strict build excluded other particles"
+                    arrays["noise_%d" % part] = np.array([np.abs(pos - poss[o]).max(), np.abs(vel - vels[o]).max(),
+                                                          np.abs(rho.astype(np.float64) - rhos[o]).max()])
+        arrays["times"] = np.array(times)
+        arrays["dt"] = np.diff(np.array(times))
+        arrays["meta"] = np.array([dp, step, ddt, nsteps], np.float64)
+        arrays["ext"] = np.array([float(v) for v in ext], np.float64)
+        np.savez_compressed(os.path.join(ROOT, "tests", "golden", name + ".npz"), **arrays)
+        print(name, "ok", os.path.getsize(os.path.join(ROOT, "tests", "golden", name + ".npz")),
+              {k: arrays[k] for k in arrays if k.startswith("noise")})
+    finally:
+        shutil.rmtree(tmp)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--only")
+    ap.add_argument("--noise", action="store_true")
     a = ap.parse_args()
     for name, spec in CASES.items():
         if a.only and a.only != name:
             continue
         make(name, *spec)
+    for name, spec in EXT_CASES.items():
+        if a.only and a.only != name:
+            continue
+        make_ext(name, *spec, a.noise)

@@ -40,6 +40,14 @@ CASES = {
     "sym_consteq_cs_dp0.025": (0.025, 0.2, 0.5, 2.75, 1, 3, 3, 3, 20.0, 2, 30, (1, 30)),
     # artificial viscosity with phase sound speeds, Molteni DDT, shifting NoBound, Verlet
     "ver_art_ddt1_cs_dp0.025": (0.025, 0.2, 0.5, 2.75, 1, 1, 1, 1, 20.0, 1, 45, (1, 41, 45)),
+    # SPH velocity gradients (VelocityGradientType 2): gradients by SPH summation, then the
+    # effective viscosity, then the Morris operator (Laminar) or the stress divergence (ConsEq)
+    "sph_sym_lam_dp0.02": (0.02, 0.2, 0.5, 2.75, 2, 2, 3, 3, 0.0, 2, 60, (1, 10, 60)),
+    "sph_sym_consteq_cs_dp0.025": (0.025, 0.2, 0.5, 2.75, 2, 3, 3, 3, 20.0, 2, 30, (1, 30)),
+    "sph_ver_lam_ddt1_nobound_dp0.025": (0.025, 0.2, 0.5, 2.75, 2, 2, 1, 1, 0.0, 1, 45, (1, 41, 45)),
+    # SPH gradients with artificial viscosity: the artificial term is the Morris pass's (bound p2
+    # with dv = 2 v1), phase sound speeds
+    "sph_ver_art_cs_dp0.025": (0.025, 0.2, 0.5, 2.75, 2, 1, 2, 0, 20.0, 1, 45, (1, 41, 45)),
 }
 
 

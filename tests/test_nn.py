@@ -20,6 +20,9 @@ from dualsphysics_multilayer_amd.case import WetDambreakNNCase
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REF = os.path.join(ROOT, "oracle", "_ref")
 NN_GOLDENS = ("sym_lam_dp0.02", "sym_consteq_cs_dp0.025", "ver_art_ddt1_cs_dp0.025")
+# VelocityGradientType 2 (SPH velocity gradients: k_nn_tiled<4|5> then k_nn_visc)
+NN_SPH_GOLDENS = ("sph_sym_lam_dp0.02", "sph_sym_consteq_cs_dp0.025", "sph_ver_lam_ddt1_nobound_dp0.025",
+                  "sph_ver_art_cs_dp0.025")
 # ulp-level floors (pos m, vel m/s, rho kg/m3): 10x noise of exactly 0 is no tolerance
 FLOOR = (2e-10, 2e-8, 2.5e-3)
 
@@ -32,7 +35,7 @@ def case_of(g):
     dp, width, scale, tfs, vg, tv, ddt, sh, cs, step, _ = g["meta"]
     return WetDambreakNNCase(float(dp), width=float(width), scale=float(scale), shift_tfs=float(tfs),
                              tvisco=int(tv), tdensity=int(ddt), shift_mode=int(sh), csound=float(cs),
-                             step_algorithm=int(step))
+                             step_algorithm=int(step), velgrad=int(vg))
 
 
 def nn_tol(g, k):
@@ -41,7 +44,7 @@ def nn_tol(g, k):
 
 
 # ---- CPU ----------------------------------------------------------------------------------
-@pytest.mark.parametrize("name", NN_GOLDENS)
+@pytest.mark.parametrize("name", NN_GOLDENS + NN_SPH_GOLDENS)
 def test_goldens_present_with_noise_floor(name):
     g = load_nn(name)
     ks = steps(g)
@@ -104,8 +107,8 @@ def test_invalid_nn_configurations_rejected():
     with pytest.raises(RuntimeError, match="phases"):
         case_derive(d)
     d = base.case_def()
-    d["velgrad"] = 2
-    with pytest.raises(RuntimeError, match="FDA"):
+    d["velgrad"] = 3
+    with pytest.raises(RuntimeError, match="gradient"):
         case_derive(d)
 
 
@@ -123,7 +126,7 @@ def check(got, ref, tol, k):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", NN_GOLDENS)
+@pytest.mark.parametrize("name", NN_GOLDENS + NN_SPH_GOLDENS)
 def test_gpu_nn_steps_match_reference_parts(name):
     g = load_nn(name)
     s = gpu(case_of(g))
@@ -149,11 +152,13 @@ def test_gpu_nn_dt_trace_matches_reference():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nslabs", [2])
-def test_gpu_nn_slabs_match_reference_parts(nslabs):
+@pytest.mark.parametrize("nslabs,name", [(2, "sym_lam_dp0.02"), (2, "sph_sym_lam_dp0.02"), (3, "sph_sym_consteq_cs_dp0.025")])
+def test_gpu_nn_slabs_match_reference_parts(nslabs, name):
+    """Slabs; with SPH gradients the first pass's eta / tau of the face columns go to the
+    neighbours' ghosts before the second pass (NNFaceExchange)."""
     from dualsphysics_multilayer_amd.core import SphSlabGroup, slab_partition
 
-    g = load_nn("sym_lam_dp0.02")
+    g = load_nn(name)
     case = case_of(g)
     grp = SphSlabGroup(case, slab_partition(case, nslabs))
     done = 0
@@ -176,7 +181,8 @@ def test_gpu_nn_deterministic():
         assert np.array_equal(pa[q], pb[q]), q
 
 
-def test_xml_loader_reads_the_nn_case(tmp_path):
+@pytest.mark.parametrize("velgrad", [1, 2])
+def test_xml_loader_reads_the_nn_case(tmp_path, velgrad):
     """xmlcase (the run driver's JSph::LoadCaseConfig) reads gennn_ref's case for the v5.0
     solver — RheologyTreatment, VelocityGradientType, ViscoTreatment, shifting, RelaxationDt
     and <special><nnphases> — into the same SphCaseDef and particle codes as the generator."""
@@ -185,10 +191,11 @@ def test_xml_loader_reads_the_nn_case(tmp_path):
         pytest.skip("oracle/_ref not built")
     from dualsphysics_multilayer_amd.xmlcase import XmlCase
 
-    subprocess.check_call([exe, "0.025", str(tmp_path), "0.2", "0.5", "5", "CaseNN", "2.75", "1", "3", "1", "1", "20"],
-                          stdout=subprocess.DEVNULL)
+    subprocess.check_call([exe, "0.025", str(tmp_path), "0.2", "0.5", "5", "CaseNN", "2.75", str(velgrad), "3", "1", "1",
+                           "20"], stdout=subprocess.DEVNULL)
     x = XmlCase(str(tmp_path / "CaseNN"))
-    c = WetDambreakNNCase(0.025, width=0.2, scale=0.5, csound=20.0, tvisco=3, tdensity=1, shift_mode=1)
+    c = WetDambreakNNCase(0.025, width=0.2, scale=0.5, csound=20.0, tvisco=3, tdensity=1, shift_mode=1,
+                          velgrad=velgrad)
     assert x.case_def() == c.case_def()
     assert np.array_equal(x.code, c.code) and np.array_equal(x.idp, c.idp)
     assert np.array_equal(x.pos, c.pos)

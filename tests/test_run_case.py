@@ -98,13 +98,11 @@ def test_simulationdomain_with_legacy_keys_is_refused(tmp_path):
 
 @pytest.mark.parametrize("edit,match", [
     (lambda x: x.replace('key="Kernel" value="2"', 'key="Kernel" value="1"'), "Wendland"),
-    (lambda x: x.replace('key="ViscoTreatment" value="1"', 'key="ViscoTreatment" value="2"'), "Laminar\\+SPS"),
     # mDBC without a <case>_Normals.nbi4 beside the case (JSph.cpp:1337)
     (lambda x: x.replace("<parameters>", '<parameters>\n<parameter key="Boundary" value="2"/>'), "normal vectors"),
     (lambda x: x.replace("<parameters>", '<parameters>\n<parameter key="Boundary" value="2"/>'
                          '<parameter key="SlipMode" value="2"/>'), "slip mode"),
     (lambda x: x.replace("<parameters>", '<parameters>\n<parameter key="XPeriodicIncY" value="0"/>'), "Periodic"),
-    (lambda x: x.replace('key="Shifting" value="0"', 'key="Shifting" value="3"'), "NN multiphase cases only"),
     (lambda x: x.replace('<data2d value="false"/>', '<data2d value="true"/>'), "dimension of the case"),
     (lambda x: x.replace("</parameters>", "</parameters>\n<special><wavepaddles/></special>"), "special"),
     (lambda x: x.replace('<fixed mkbound="0" mk="10"', '<moving mkbound="0" mk="10"').replace(
@@ -128,13 +126,22 @@ def test_case_particle_count_must_match(tmp_path):
 
 
 @pytest.mark.parametrize("argv,match", [
-    (["-cpu"], "GPU"), (["-mdbc_noslip"], "slip mode"), (["-initnorpla:mkbound=0"], "Normals"), (["-cubic"], "Wendland"), (["-viscolamsps:1e-6"], "Laminar"),
-    (["-shifting:full"], "Shifting"), (["-sv:vtk"], "not supported"), (["-cellmode:quarter"], "invalid"),
+    (["-cpu"], "GPU"), (["-mdbc_noslip"], "slip mode"), (["-initnorpla:mkbound=0"], "Normals"), (["-cubic"], "Wendland"), (["-viscolamsps:0.01"], "invalid"),
+    (["-shifting:sometimes"], "invalid"), (["-sv:vtk"], "not supported"), (["-cellmode:quarter"], "invalid"),
     (["-ddt:4"], "invalid"), (["-bogus"], "not supported"),
 ])
 def test_unsupported_options_raise(argv, match):
     with pytest.raises(CaseError, match=match):
         parse_args([CASE] + argv)
+
+
+def test_viscosity_and_shifting_options():
+    """-viscolamsps:<v> (v <= 0.001, JSphCfgRun.cpp:329-333) and -shifting:<mode>, which
+    configures ShiftCoef -2 and ShiftTFS 0 (JSphShifting::ConfigBasic defaults, JSph.cpp:825-835)."""
+    ov = parse_args([CASE, "-viscolamsps:1e-6", "-shifting:nobound"])["overrides"]
+    assert (ov["tvisco"], ov["visco"]) == (2, float(np.float32(1e-6)))
+    assert (ov["shift_mode"], ov["shift_coef"], ov["shift_tfs"]) == (1, -2.0, 0.0)
+    assert parse_args([CASE, "-viscoart:0.05"])["overrides"]["tvisco"] == 1
 
 
 def test_options_mirror_the_reference():
