@@ -5,7 +5,7 @@ import ctypes as C
 
 import numpy as np
 
-SPH_ABI_VERSION = 5
+SPH_ABI_VERSION = 6
 
 SPH_STATUS = {
     0: "SPH_OK",
@@ -176,6 +176,8 @@ class SphConstants(C.Structure):
         ("phase_cteb", C.c_float * SPH_MAXPHASES),
         ("data2d", C.c_int32),
         ("pad3", C.c_int32),
+        ("spssmag", C.c_float),
+        ("spsblin", C.c_float),
     ]
 
     def as_dict(self) -> dict:

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUTDIR = os.path.join(HERE, "lib")
 LIBNAME = "libsphcore.so"
-SOURCES = ["sph_divide.hip", "sph_interaction.hip", "sph_interaction_tiled.hip", "sph_nn.hip", "sph_step.hip", "sph_slab.hip", "sph_mdbc.hip", "sph_bodies.hip",
+SOURCES = ["sph_divide.hip", "sph_interaction.hip", "sph_interaction_tiled.hip", "sph_nn.hip", "sph_ext.hip", "sph_step.hip", "sph_slab.hip", "sph_mdbc.hip", "sph_bodies.hip",
            "sph_solver.cpp", "sph_comm.cpp", "sph_bi4.cpp", "sph_capi.cpp"]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 LDFLAGS = ["-L" + os.path.join(ROCM, "lib"), "-lrccl", "-Wl,-rpath," + os.path.join(ROCM, "lib"), "-pthread"]

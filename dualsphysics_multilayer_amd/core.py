@@ -453,6 +453,11 @@ class SphSlabGroup:
     def stats(self) -> list:
         return [m.stats() for m in self.members]
 
+    def set_time(self, time: float, symplectic_dtpre: float = 0.0) -> None:
+        """Restart time of every slab (JSph::InitRun with PartBegin)."""
+        for m in self.members:
+            m.set_time(time, symplectic_dtpre)
+
     def set_repartition(self, every: int, bound_weight: float = 0.3, tolerance: float = 0.05) -> None:
         """Re-balance the slabs' column bounds every `every` steps."""
         _check(load_library().sph_slab_group_set_repartition(self._h, every, bound_weight, tolerance))

@@ -69,6 +69,8 @@ struct KConst {
   int nn;          // RheologyTreatment == 2
   int nntvisco;    // TpVisco of the NN interaction: 1 artificial, 2 laminar, 3 constitutive eq.
   int nnvelgrad;   // VelocityGradientType: 1 FDA, 2 SPH (two passes: k_nn_tiled, then k_nn_visc)
+  int tvisco;      // single phase: 1 artificial, 2 Laminar+SPS (sph_ext.hip)
+  float spssmag, spsblin;  // Laminar+SPS constants SpsSmag, SpsBlin (JSph.cpp:1438-1443)
   int shiftmode;   // TpShifting: 0 none, 1 NoBound, 2 NoFixed, 3 Full
   int sim2d;       // Simulate2D: ace.y = 0 after the interaction
   float lamda;     // RelaxationDt of the viscous dt (JSphCpu.cpp:1687)

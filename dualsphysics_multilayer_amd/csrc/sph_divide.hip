@@ -321,11 +321,12 @@ struct GatherArgs {
 constexpr int GP = SPH_GP;
 
 // One particle's state, loaded from its source index (all loads issued before any store).
-template <bool WITHM1, bool WITHPRE> struct GatherRec {
+template <bool WITHM1, bool WITHPRE, bool WITHTAU = false> struct GatherRec {
   unsigned dc, idp;
   double2 pxy, pxypre;
   double pz, pzpre;
   float4 vr, m1, vpre;
+  float4 ta, tb;  // Laminar+SPS tau (src.tau set: JSphCpuSingle.cpp:463 sorts SpsTauc too)
   typecode code;
   __device__ __forceinline__ void load(const PartArrays& src, unsigned s) {
     dc = src.dcell[s];
@@ -340,12 +341,17 @@ template <bool WITHM1, bool WITHPRE> struct GatherRec {
       pzpre = src.poszpre[s];
       vpre = src.velrhoppre[s];
     }
+    if constexpr (WITHTAU) {
+      ta = src.tau[2 * s];
+      tb = src.tau[2 * s + 1];
+    }
   }
 };
 
 // Stores a loaded particle at its sorted index i with its poscell and press.
-template <bool WITHM1, bool WITHPRE>
-__device__ __forceinline__ void gather_store(const GatherArgs& a, unsigned i, const GatherRec<WITHM1, WITHPRE>& q) {
+template <bool WITHM1, bool WITHPRE, bool WITHTAU>
+__device__ __forceinline__ void gather_store(const GatherArgs& a, unsigned i,
+                                             const GatherRec<WITHM1, WITHPRE, WITHTAU>& q) {
   const unsigned dc = q.dc;
   const double2 pxy = q.pxy;
   const double pz = q.pz;
@@ -362,6 +368,10 @@ __device__ __forceinline__ void gather_store(const GatherArgs& a, unsigned i, co
     a.dst.posxypre[i] = q.pxypre;
     a.dst.poszpre[i] = q.pzpre;
     a.dst.velrhoppre[i] = q.vpre;
+  }
+  if constexpr (WITHTAU) {
+    a.dst.tau[2 * i] = q.ta;
+    a.dst.tau[2 * i + 1] = q.tb;
   }
   // PosCell (KerUpdatePosCell): position relative to the origin of its divide cell
   // (global cell -> the same floats on every slab); w = the local cell.
@@ -409,17 +419,17 @@ __device__ __forceinline__ void gather_store(const GatherArgs& a, unsigned i, co
 }
 
 
-template <bool WITHM1, bool WITHPRE>
+template <bool WITHM1, bool WITHPRE, bool WITHTAU>
 __device__ __forceinline__ void gather_one(const GatherArgs& a, unsigned i, unsigned s, float4& vr_out, bool& fluid,
                                            unsigned npb) {
-  GatherRec<WITHM1, WITHPRE> q;
+  GatherRec<WITHM1, WITHPRE, WITHTAU> q;
   q.load(a.src, s);
-  gather_store<WITHM1, WITHPRE>(a, i, q);
+  gather_store<WITHM1, WITHPRE, WITHTAU>(a, i, q);
   vr_out = q.vr;
   fluid = i >= npb;
 }
 
-template <bool WITHM1, bool WITHPRE>
+template <bool WITHM1, bool WITHPRE, bool WITHTAU>
 __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, GatherArgs a) {
   const unsigned n = sc->np, npb = sc->npb;
   const unsigned i0 = blockIdx.x * (256 * GP) + threadIdx.x;
@@ -433,7 +443,7 @@ __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, Gat
     if (i < n) {
       float4 vr;
       bool fluid;
-      gather_one<WITHM1, WITHPRE>(a, i, sp[k], vr, fluid, npb);
+      gather_one<WITHM1, WITHPRE, WITHTAU>(a, i, sp[k], vr, fluid, npb);
       if (fluid) v2 = nanmax(v2, vr.x * vr.x + vr.y * vr.y + vr.z * vr.z);  // CalcVelMaxOmp over fluid
     }
   }
@@ -464,10 +474,16 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
   a.withm1 = withm1;
   a.withpre = withpre;
   const unsigned nb = (cap + 256 * GP - 1) / (256 * GP);
-  if (withm1 && withpre) hipLaunchKernelGGL((k_gather<true, true>), dim3(nb), dim3(256), 0, stm, sc, a);
-  else if (withm1) hipLaunchKernelGGL((k_gather<true, false>), dim3(nb), dim3(256), 0, stm, sc, a);
-  else if (withpre) hipLaunchKernelGGL((k_gather<false, true>), dim3(nb), dim3(256), 0, stm, sc, a);
-  else hipLaunchKernelGGL((k_gather<false, false>), dim3(nb), dim3(256), 0, stm, sc, a);
+#define SPH_K_GATHER(M1, PRE, TAU) hipLaunchKernelGGL((k_gather<M1, PRE, TAU>), dim3(nb), dim3(256), 0, stm, sc, a)
+#define SPH_K_GATHER_T(M1, PRE) \
+  if (a.src.tau) SPH_K_GATHER(M1, PRE, true); \
+  else SPH_K_GATHER(M1, PRE, false)
+  if (withm1 && withpre) { SPH_K_GATHER_T(true, true); }
+  else if (withm1) { SPH_K_GATHER_T(true, false); }
+  else if (withpre) { SPH_K_GATHER_T(false, true); }
+  else { SPH_K_GATHER_T(false, false); }
+#undef SPH_K_GATHER_T
+#undef SPH_K_GATHER
 }
 
 // ---------------------------------------------------------------------------------
@@ -1048,12 +1064,12 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
 // One tile per block.  Loads in three batches (one memory latency each): the particle
 // states and the classification words, the new positions, then the stores.  Block 0
 // also clears the super-tile sums and the far count for the next divide.
-template <bool WITHM1, bool WITHPRE>
+template <bool WITHM1, bool WITHPRE, bool WITHTAU>
 __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, GatherArgs a, IncDivScratch s) {
   const unsigned nd = sc->ndiv, n = sc->np, npb = sc->npb;
   const unsigned t = blockIdx.x;
   const unsigned i0 = t * INC_TILE + threadIdx.x;
-  GatherRec<WITHM1, WITHPRE> q[GP];
+  GatherRec<WITHM1, WITHPRE, WITHTAU> q[GP];
   unsigned key[GP], cw[GP], fx[GP], pos[GP];
   const unsigned tpg = i0 < nd ? s.tpg[t] : 0u;
 #pragma unroll
@@ -1084,7 +1100,7 @@ __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, G
   for (int k = 0; k < GP; k++) {
     // particles of the out boxes leave the arrays, as in the pull gather
     if (i0 + 256 * k < nd && pos[k] < n) {
-      gather_store<WITHM1, WITHPRE>(a, pos[k], q[k]);
+      gather_store<WITHM1, WITHPRE, WITHTAU>(a, pos[k], q[k]);
       s.skeys[pos[k]] = key[k];
       if (pos[k] >= npb) v2 = nanmax(v2, q[k].vr.x * q[k].vr.x + q[k].vr.y * q[k].vr.y + q[k].vr.z * q[k].vr.z);
     }
@@ -1128,10 +1144,16 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
   a.withm1 = withm1;
   a.withpre = withpre;
   const unsigned nb = s.nb1;  // one tile per block
-  if (withm1 && withpre) hipLaunchKernelGGL((k_inc_push<true, true>), dim3(nb), dim3(256), 0, stm, sc, a, s);
-  else if (withm1) hipLaunchKernelGGL((k_inc_push<true, false>), dim3(nb), dim3(256), 0, stm, sc, a, s);
-  else if (withpre) hipLaunchKernelGGL((k_inc_push<false, true>), dim3(nb), dim3(256), 0, stm, sc, a, s);
-  else hipLaunchKernelGGL((k_inc_push<false, false>), dim3(nb), dim3(256), 0, stm, sc, a, s);
+#define SPH_K_INC_PUSH(M1, PRE, TAU) hipLaunchKernelGGL((k_inc_push<M1, PRE, TAU>), dim3(nb), dim3(256), 0, stm, sc, a, s)
+#define SPH_K_INC_PUSH_T(M1, PRE) \
+  if (a.src.tau) SPH_K_INC_PUSH(M1, PRE, true); \
+  else SPH_K_INC_PUSH(M1, PRE, false)
+  if (withm1 && withpre) { SPH_K_INC_PUSH_T(true, true); }
+  else if (withm1) { SPH_K_INC_PUSH_T(true, false); }
+  else if (withpre) { SPH_K_INC_PUSH_T(false, true); }
+  else { SPH_K_INC_PUSH_T(false, false); }
+#undef SPH_K_INC_PUSH_T
+#undef SPH_K_INC_PUSH
 }
 
 unsigned inc_blocks_classify(unsigned cap) { return (cap + INC_TILE - 1) / INC_TILE; }

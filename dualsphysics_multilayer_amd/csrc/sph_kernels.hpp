@@ -22,6 +22,7 @@ struct PartArrays {
   double2* posxypre = nullptr;   // Symplectic
   double* poszpre = nullptr;
   float4* velrhoppre = nullptr;
+  float4* tau = nullptr;         // Laminar+SPS: sub-particle stress tensor, [2i] {xx,xy,xz,yy}, [2i+1] {yz,zz}
 };
 
 // JSphCpu::UpdatePos (JSphCpu.cpp:1240-1293), single domain, no periodic/symmetry.
@@ -73,9 +74,16 @@ __device__ __forceinline__ void shift_displacement(const KConst& K, float4 rs, f
     else umagn *= (double(rs.w) - double(K.shifttfs)) / K.coeftfs;
   }
   const float sx = float(double(rs.x) * umagn), sy = float(double(rs.y) * umagn), sz = float(double(rs.z) * umagn);
-  dx += double(sx < K.shiftmaxdist ? sx : K.shiftmaxdist);
-  dy += double(sy < K.shiftmaxdist ? sy : K.shiftmaxdist);
-  dz += double(sz < K.shiftmaxdist ? sz : K.shiftmaxdist);
+  const float md = K.shiftmaxdist;
+  if (K.nn) {  // v5.0: clamped from above only (JSphShifting.cpp:412-414 of the NN solver)
+    dx += double(sx < md ? sx : md);
+    dy += double(sy < md ? sy : md);
+    dz += double(sz < md ? sz : md);
+  } else {  // v5.2: |shift| clamped to maxdist with its sign (JSphShifting.cpp:412-414)
+    dx += double(fabsf(sx) < md ? sx : (sx >= 0 ? md : -md));
+    dy += double(fabsf(sy) < md ? sy : (sy >= 0 ? md : -md));
+    dz += double(fabsf(sz) < md ? sz : (sz >= 0 ? md : -md));
+  }
 }
 
 // Scratch of the cell sort (DivideGpu).
@@ -191,6 +199,13 @@ void launch_nn_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const ui
                      const float4* poscell, const float4* velrhop, const float* press, const typecode* code,
                      const unsigned* begincell, DivGrid g, const KConst& K, const float4* phases, float4* arace,
                      float4* shiftpos, bool shift, float* viscoeta, float4* tau);
+// Single-phase interaction with Laminar+SPS viscosity and/or shifting (sph_ext.hip):
+// arace, shiftpos (when shiftstore), the new SPS tau into taunew (Laminar+SPS; `tau` holds
+// the previous interaction's), ViscDtMax / AceMax.
+void launch_fluid_ext(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
+                      const float4* poscell, const float4* velrhop, const float* press, const typecode* code,
+                      const float* ftmassp, const float4* tau, const unsigned* begincell, DivGrid g, const KConst& K,
+                      float4* arace, float4* shiftpos, float4* taunew, bool shiftstore);
 // NN with SPH velocity gradients, second pass: the Morris / constitutive-equation /
 // artificial viscous force of every fluid p1 from the first pass's effective viscosities or
 // stress tensors (JSphCpu_NN_SPH.cpp:228-446), added onto arace; AceMax.
@@ -313,6 +328,7 @@ struct SlabRec {
   unsigned short code, flags;
   unsigned pad;
   float4 normal;  // mDBC normal of a boundary particle (idp < nbound), else 0
+  float4 taua, taub;  // Laminar+SPS: the migrant's SPS stress tensor (PartArrays::tau)
 };
 // A GHOST copy for a neighbour: what a neighbour of the interaction needs, 40 B.  The
 // position travels as the float offset from its (global) cell origin, i.e. exactly the

@@ -1258,7 +1258,7 @@ __global__ __launch_bounds__(256) void k_nn_face_apply(DevScalars* __restrict__ 
     atomicOr(&sc->error_flags, ERR_HALO);
     return;
   }
-  viscoeta[p] = q.v[0];
+  if (viscoeta) viscoeta[p] = q.v[0];
   if (withtau) {
     tau[2 * p] = make_float4(q.v[1], q.v[2], q.v[3], q.v[4]);
     tau[2 * p + 1] = make_float4(q.v[5], q.v[6], 0.f, 0.f);

@@ -167,6 +167,8 @@ __device__ __forceinline__ void write_migrant(const PackArgs& q, unsigned p, Sla
   r.flags = 0;
   r.pad = 0;
   r.normal = (q.normal && r.idp < q.nbound) ? q.normal[r.idp] : make_float4(0.f, 0.f, 0.f, 0.f);
+  r.taua = q.a.tau ? q.a.tau[2 * p] : make_float4(0.f, 0.f, 0.f, 0.f);
+  r.taub = q.a.tau ? q.a.tau[2 * p + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
   *dst = r;
 }
 
@@ -273,6 +275,10 @@ __global__ __launch_bounds__(256) void k_unpack(UnpackArgs u) {
       a.poszpre[p] = r.poszpre;
     }
     if (u.normal && r.idp < u.nbound) u.normal[r.idp] = r.normal;  // the owner's turned normal
+    if (a.tau) {
+      a.tau[2 * p] = r.taua;
+      a.tau[2 * p + 1] = r.taub;
+    }
   } else {
     const SlabGhost r = u.gh[i - u.nm];
     const double ox = u.posminx + double(DcelCellx(u.dcc, r.dcell)) * u.scelld;

@@ -119,10 +119,11 @@ void derive_constants(const SphCaseDef& c, SphConstants& k) {
   if (k.rheology == SPH_RHEOLOGY_SINGLE) {
     if (k.tvisco == SPH_VISCO_CONSTEQ)
       throw SphError(SPH_ERR_ARG, "ViscoTreatment 'Constitutive  eq.' not valid for Single-phase classic formulation.");
-    if (k.tvisco != SPH_VISCO_ARTIFICIAL)
-      throw SphError(SPH_ERR_UNSUPPORTED, "single-phase Laminar+SPS viscosity is not implemented");
-    if (k.shift_mode != SPH_SHIFT_NONE)
-      throw SphError(SPH_ERR_UNSUPPORTED, "shifting is implemented for the NN multiphase formulation only");
+    if (k.tvisco == SPH_VISCO_LAMINARSPS) {  // JSph::ConfigConstants2 (JSph.cpp:1438-1443)
+      const double dp_sps = (k.data2d ? std::sqrt(c.dp * c.dp * 2.) / 2. : std::sqrt(c.dp * c.dp * 3.) / 3.);
+      k.spssmag = float(std::pow(0.12 * dp_sps, 2));
+      k.spsblin = float((2. / 3.) * 0.0066 * dp_sps * dp_sps);
+    }
     return;
   }
   // NN multiphase: JSph::InitMultiPhase + ConfigConstantsMP (JSph.cpp:3137-3242, v5.0 solver)
@@ -199,6 +200,9 @@ static KConst make_kconst(const SphConstants& c) {
   K.nn = (c.rheology == SPH_RHEOLOGY_NN) ? 1 : 0;
   K.nntvisco = c.tvisco;
   K.nnvelgrad = c.velgrad;
+  K.tvisco = c.tvisco;
+  K.spssmag = c.spssmag;
+  K.spsblin = c.spsblin;
   K.shiftmode = c.shift_mode;
   K.sim2d = c.data2d;
   K.lamda = c.relaxation_dt;
@@ -363,7 +367,13 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   nnsph_ = nn_ && C.velgrad == SPH_VELGRAD_SPH;
   casenp_ = cdef.np;
   shift_ = (C.shift_mode != SPH_SHIFT_NONE);
-  if (nnsph_ && slab()) {
+  sps_ = !nn_ && C.tvisco == SPH_VISCO_LAMINARSPS;
+  ext_ = !nn_ && (sps_ || shift_);
+  facex_ = slab() && (nnsph_ || sps_);
+  if (ext_ && C.scelldiv != 1)
+    throw SphError(SPH_ERR_UNSUPPORTED, "Laminar+SPS viscosity / shifting with CellMode=half is not implemented");
+  if (ext_) tiled_ = true;
+  if (facex_) {
     // the first interaction's face records: the initial particles of the face and ghost
     // columns (both sides of a face count the same particles); later from each exchange
     const std::vector<unsigned> cx = initial_columns(C, init);
@@ -437,7 +447,7 @@ void SphGpuSingle::AllocFixed() {
     inc_.ctr = (unsigned*)dmalloc(4 * QSTRIDE);
     check_hip(hipMemset(inc_.ctr, 0, 4 * QSTRIDE), "zero far count");
   }
-  if (nnsph_ && slab()) idxmap_ = (unsigned*)dmalloc(4 * size_t(std::max(casenp_, 1u)));
+  if (facex_) idxmap_ = (unsigned*)dmalloc(4 * size_t(std::max(casenp_, 1u)));
   sc_ = (DevScalars*)dmalloc(sizeof(DevScalars));
   dttrace_ = (double*)dmalloc(8 * size_t(tracecap_));
   pairs_ = (unsigned long long*)dmalloc(8 * 6);
@@ -485,6 +495,7 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
     a->posxy = (double2*)dmalloc(16 * n);
     a->posz = (double*)dmalloc(8 * n);
     a->velrhop = (float4*)dmalloc(16 * n);
+    if (sps_) a->tau = (float4*)dmalloc(32 * n);
     if (step_algorithm_ == SPH_STEP_VERLET) {
       a->velrhopm1 = (float4*)dmalloc(16 * n);
     } else {
@@ -500,6 +511,7 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
   items_ = (uint4*)dmalloc(16 * (n / 128 + 2 * size_t(G.ncy) * size_t(G.ncz) + size_t(nctmax_) / 2 + 2));
   arace_ = (float4*)dmalloc(16 * n);
   if (shift_) shiftpos_ = (float4*)dmalloc(16 * n);  // the interaction's shifting sums
+  if (sps_) taunew_ = (float4*)dmalloc(32 * n);
   if (nnsph_) {
     viscoeta_ = (float*)dmalloc(4 * n);
     if (C.tvisco == SPH_VISCO_CONSTEQ) tau_ = (float4*)dmalloc(32 * n);
@@ -575,6 +587,7 @@ void SphGpuSingle::Grow(unsigned np_live, unsigned newcap) {
   cp(cur_.posxypre, old.posxypre, 16 * n);
   cp(cur_.poszpre, old.poszpre, 8 * n);
   cp(cur_.velrhoppre, old.velrhoppre, 16 * n);
+  cp(cur_.tau, old.tau, 32 * n);
   check_hip(hipStreamSynchronize(stream), "grow: copy");
   for (void* p : oldallocs) (void)hipFree(p);
 }
@@ -626,6 +639,8 @@ void SphGpuSingle::Upload(const SphParticlesHost& h, const std::vector<unsigned>
   check_hip(hipMemcpy(cur_.posxy, pxy.data(), 16 * size_t(n), hipMemcpyHostToDevice), "upload posxy");
   check_hip(hipMemcpy(cur_.posz, pz.data(), 8 * size_t(n), hipMemcpyHostToDevice), "upload posz");
   check_hip(hipMemcpy(cur_.velrhop, vr.data(), 16 * size_t(n), hipMemcpyHostToDevice), "upload velrhop");
+  // InitRunCpu: SpsTauc = 0 (JSphCpu.cpp:423)
+  if (cur_.tau) check_hip(hipMemset(cur_.tau, 0, 32 * size_t(cap_)), "zero tau");
   DevScalars s;
   std::memset(&s, 0, sizeof(s));
   s.np = n;
@@ -752,7 +767,7 @@ void SphGpuSingle::Exchange() {
   check_hip(hipEventRecord(xev_, stream), "exchange: event");
   WaitEvent(xev_, "exchange: wait counts");
   const SlabCounts c = *slabcnt_host_;
-  if (nnsph_) {
+  if (facex_) {
     // the neighbour's ghosts of this slab: the ghosts sent now + the migrants it sent here
     // (it keeps them as ghosts); the neighbour derives the same sizes from its counts
     face_sl_ = hl ? unsigned(c.sendl[0] + c.recvl[1]) : 0u;
@@ -970,6 +985,14 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
       launch_nn_visc(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, cur_.code, viscoeta_, tau_,
                      begincell_, G, K, phasek_, arace_);
     }
+  } else if (ext_) {
+    // Laminar+SPS and/or shifting (sph_ext.hip).  Slabs with SPS: the ghosts' tau (the
+    // owners' from the last interaction) first
+    if (sps_ && slab() && (transport_->has_left() || transport_->has_right())) NNFaceExchange();
+    TimedBegin(0);
+    launch_fluid_ext(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, cur_.code, ftmassp_,
+                     cur_.tau, begincell_, G, K, arace_, shiftpos_, taunew_, interstep != 2);
+    if (sps_) std::swap(cur_.tau, taunew_);
   } else if (tiled_) {
     // The tiled kernel writes the arace of every owned particle (skipped boundary items
     // get ar = 0) and resets its own work counters at exit (zeroed once at allocation).
@@ -999,12 +1022,15 @@ void SphGpuSingle::NNFaceExchange() {
     check_hip(hipMalloc((void**)&nnface_, sizeof(NNFaceRec) * nnfacecap_), "hipMalloc NN face records");
   }
   NNFaceRec *sl = nnface_, *sr = sl + nsl, *rl = sr + nsr, *rr = rl + nrl;
-  launch_nn_face_pack(stream, cap_, sc_, cur_, K, G, viscoeta_, tau_, hl ? sl : nullptr, hr ? sr : nullptr,
-                      unsigned(nsl), unsigned(nsr), idxmap_, casenp_);
+  // NN: the first pass's eta (+ ConstEq tau); single phase Laminar+SPS: the particles' SPS tau
+  float* veta = sps_ ? nullptr : viscoeta_;
+  float4* tau = sps_ ? cur_.tau : tau_;
+  launch_nn_face_pack(stream, cap_, sc_, cur_, K, G, veta, tau, hl ? sl : nullptr, hr ? sr : nullptr, unsigned(nsl),
+                      unsigned(nsr), idxmap_, casenp_);
   transport_->exchange(sl, sizeof(NNFaceRec) * nsl, sr, sizeof(NNFaceRec) * nsr, rl, sizeof(NNFaceRec) * nrl, rr,
                        sizeof(NNFaceRec) * nrr, stream);
   launch_nn_face_apply(stream, sc_, hl ? rl : nullptr, hr ? rr : nullptr, unsigned(nrl), unsigned(nrr), idxmap_,
-                       casenp_, cur_.idp, viscoeta_, tau_, C.tvisco == SPH_VISCO_CONSTEQ);
+                       casenp_, cur_.idp, veta, tau, tau != nullptr);
 }
 
 void SphGpuSingle::DtVariable(int mode) {

@@ -141,6 +141,12 @@ class SphGpuSingle {
   // NN with SPH velocity gradients (VelocityGradientType 2): the first pass's effective
   // viscosity [cap] and stress tensor (ConstEq) [2 cap], read by the second pass
   bool nnsph_ = false;
+  // single phase with Laminar+SPS and/or shifting: k_fluid_ext (sph_ext.hip); sps_: the SPS
+  // stress tensor is particle state (PartArrays::tau, sorted by the divide), the interaction
+  // writes the new one to taunew_ (swapped after it)
+  bool ext_ = false, sps_ = false;
+  float4* taunew_ = nullptr;
+  bool facex_ = false;  // slab face exchange of per-particle values before the interaction
   float* viscoeta_ = nullptr;
   float4* tau_ = nullptr;
   // slabs: face records of eta / tau for the neighbours' ghosts; sizes (records) of the

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define SPH_ABI_VERSION 5
+#define SPH_ABI_VERSION 6
 
 typedef enum {
   SPH_OK = 0,
@@ -208,6 +208,7 @@ typedef struct SphConstants {
   float phase_mass[SPH_MAXPHASES];  /* StPhaseArray.mass = rho dp^3               */
   float phase_cteb[SPH_MAXPHASES];  /* StPhaseArray.CteB                          */
   int32_t data2d, pad3;
+  float spssmag, spsblin;           /* Laminar+SPS SpsSmag, SpsBlin (JSph.cpp:1438-1443) */
 } SphConstants;
 
 /* Step statistics kept on the device and read back on demand. */

@@ -57,6 +57,40 @@ EXT_CASES = {
     "symplectic_shift_full_tfs_dp0.025": (0.025, 2, 2, 60, (1, 20, 60), (1, "0.1", 3, "-2", "2.75")),
     "verlet_lamsps_shift_nofixed_dp0.03": (0.03, 1, 0, 45, (1, 41, 45), (2, "1e-6", 2, "-2", "1.5")),
 }
+# The same physics from a STIRRED state (restart fixtures): a dam break at rest has no
+# velocity gradient (no SPS stress) and no shifting displacement (|v| = 0) in its first
+# steps, so these start from the generated case with every fluid particle given the smooth
+# shear field of stir_velocity() plus a seeded random part, written as Part_0000 (the
+# core's PART writer, byte-identical to the reference's, tests/test_bi4.py) as the PART
+# of step 1 and run by the reference with -partbegin:1.  The npz adds s0_* (the stirred
+# start) and rst = [time, SymplecticDtPre, map_posmin xyz, map_posmax xyz].
+# (..., stir: "mild" or "shear" -- the strong short-wave shear under which the SPS eddy
+# viscosity (Smagorinsky, ~SpsSmag |S| ~ 1e-4 m2/s) is far above the parity tolerance)
+STIR_CASES = {
+    "stir_verlet_lamsps_ddt2_dp0.025": (0.025, 1, 2, 40, (1, 10, 40), (2, "1e-6", 0, "-2", "0"), "shear"),
+    "stir_symplectic_lamsps_ddt1_dp0.03": (0.03, 2, 1, 20, (1, 5, 20), (2, "1e-6", 0, "-2", "0"), "shear"),
+    "stir_verlet_shift_full_tfs_dp0.025": (0.025, 1, 2, 40, (1, 10, 40), (1, "0.1", 3, "-2", "2.75"), "mild"),
+    "stir_symplectic_lamsps_shift_nobound_dp0.03": (0.03, 2, 2, 20, (1, 5, 20), (2, "1e-6", 1, "-2", "0"), "shear"),
+}
+
+
+def stir_velocity(pos, idp, npb, kind="mild", seed=11):
+    """Fluid particles (idp >= npb) get a shear field plus seeded uniform noise:
+    mild:  u = 0.6 sin(2 pi z/0.3), v = 0.2 sin(2 pi y/0.67), w = 0.4 sin(2 pi x/0.4), +-0.15 m/s;
+    shear: u = 1.5 sin(2 pi z/0.1), v = 0.5 sin(2 pi y/0.15), w = 1.0 sin(2 pi x/0.1), +-0.05 m/s."""
+    rng = np.random.default_rng(seed)
+    v = np.zeros((len(idp), 3), np.float32)
+    fl = idp >= npb
+    x, y, z = pos[fl, 0], pos[fl, 1], pos[fl, 2]
+    if kind == "shear":
+        a, l, noise = (1.5, 0.5, 1.0), (0.1, 0.15, 0.1), 0.05
+    else:
+        a, l, noise = (0.6, 0.2, 0.4), (0.3, 0.67, 0.4), 0.15
+    v[fl, 0] = a[0] * np.sin(2 * np.pi * z / l[0])
+    v[fl, 1] = a[1] * np.sin(2 * np.pi * y / l[1])
+    v[fl, 2] = a[2] * np.sin(2 * np.pi * x / l[2])
+    v[fl] += rng.uniform(-noise, noise, size=(int(fl.sum()), 3)).astype(np.float32)
+    return v
 
 
 def load_dump(fn):
@@ -121,6 +155,78 @@ def run_ext(exe, dp, step, ddt, nsteps, ext, tmp, tag):
     return out
 
 
+def make_stir(name, dp, step, ddt, nsteps, keep, ext, stir, noise):
+    sys.path.insert(0, ROOT)
+    from dualsphysics_multilayer_amd.core import read_part, write_part
+
+    tmp = tempfile.mkdtemp(prefix="golden_")
+    try:
+        tv, visco, sh, coef, tfs = ext
+        d = os.path.join(tmp, "case")
+        os.makedirs(d)
+        subprocess.check_call([os.path.join(REF, "gencase_ref"), repr(dp), d, str(step), str(ddt), "1.5",
+                               "CaseDambreak", "1", "3", str(tv), visco, str(sh), coef, tfs], stdout=subprocess.DEVNULL)
+        # one step from rest: Part_0001 + Part_Head.ibi4 as the reference writes them; the
+        # stirred state is that Part_0001 with new fluid velocities (-partbegin:0 is no
+        # restart at all in JSph: PartBegin = 0 loads the case file)
+        first = os.path.join(tmp, "first")
+        subprocess.check_call([os.path.join(REF, "DualSPHysics5.2CPU_ref"), os.path.join(d, "CaseDambreak"), first,
+                               "-nsteps:1", "-svsteps:1", "-saveposdouble:1", "-sv:binx", "-svres:0"],
+                              stdout=subprocess.DEVNULL)
+        h, p = read_part(os.path.join(first, "Part_0001.bi4"))
+        npb = int(h["case_nfixed"])
+        p["vel"] = stir_velocity(p["pos"], p["idp"], npb, stir)
+        h.update(visco_type=int(tv), visco=float(visco), viscoboundfactor=1.0, gravity=[0.0, 0.0, -9.81], mkbound=10,
+                 mkfluid=0)
+        src = os.path.join(tmp, "src")
+        os.makedirs(src)
+        write_part(os.path.join(src, "Part_0001.bi4"), h, p)
+        shutil.copy(os.path.join(first, "Part_Head.ibi4"), os.path.join(src, "Part_Head.ibi4"))
+
+        def run(exe, tag):
+            out = os.path.join(tmp, "out_" + tag)
+            subprocess.check_call([exe, os.path.join(d, "CaseDambreak"), out, "-partbegin:1", src,
+                                   "-nsteps:%d" % nsteps, "-svsteps:1", "-saveposdouble:1", "-sv:binx", "-svres:0"],
+                                  stdout=subprocess.DEVNULL)
+            return out
+
+        out = run(os.path.join(REF, "DualSPHysics5.2CPU_ref"), "fast")
+        outs = run(os.path.join(REF, "DualSPHysics5.2CPU_strict"), "strict") if noise else None
+        o = np.argsort(p["idp"], kind="stable")
+        arrays = {"s0_idp": p["idp"][o], "s0_pos": p["pos"][o], "s0_vel": p["vel"][o], "s0_rhop": p["rhop"][o],
+                  "s0_time": np.float64(h["timestep"]),
+                  "rst": np.array([h["timestep"], h["symplectic_dtpre"]] + list(h["map_posmin"]) +
+                                  list(h["map_posmax"]), np.float64)}
+        times = [h["timestep"]]
+        fn = os.path.join(tmp, "p.bin")
+        for k in range(1, nsteps + 1):  # step k after the restart = output part 1 + k
+            subprocess.check_call([os.path.join(REF, "partdump_ref"), out, str(1 + k), fn], stdout=subprocess.DEVNULL)
+            t, idp, pos, vel, rho = load_dump(fn)
+            oo = np.argsort(idp, kind="stable")
+            idp, pos, vel, rho = idp[oo], pos[oo], vel[oo], rho[oo]
+            times.append(t)
+            if k in keep:
+                arrays.update({"s%d_idp" % k: idp, "s%d_pos" % k: pos, "s%d_vel" % k: vel,
+                               "s%d_rhop" % k: rho, "s%d_time" % k: np.float64(t)})
+                if outs:
+                    subprocess.check_call([os.path.join(REF, "partdump_ref"), outs, str(1 + k), fn],
+                                          stdout=subprocess.DEVNULL)
+                    _, idps, poss, vels, rhos = load_dump(fn)
+                    oo = np.argsort(idps, kind="stable")
+                    assert np.array_equal(idp, idps[oo]), "strict build excluded other particles"
+                    arrays["noise_%d" % k] = np.array([np.abs(pos - poss[oo]).max(), np.abs(vel - vels[oo]).max(),
+                                                       np.abs(rho.astype(np.float64) - rhos[oo]).max()])
+        arrays["times"] = np.array(times)
+        arrays["dt"] = np.diff(np.array(times))
+        arrays["meta"] = np.array([dp, step, ddt, nsteps], np.float64)
+        arrays["ext"] = np.array([float(v) for v in ext], np.float64)
+        np.savez_compressed(os.path.join(ROOT, "tests", "golden", name + ".npz"), **arrays)
+        print(name, "ok", os.path.getsize(os.path.join(ROOT, "tests", "golden", name + ".npz")),
+              {k: arrays[k] for k in arrays if k.startswith("noise")})
+    finally:
+        shutil.rmtree(tmp)
+
+
 def make_ext(name, dp, step, ddt, nsteps, keep, ext, noise):
     tmp = tempfile.mkdtemp(prefix="golden_")
     try:
@@ -170,3 +276,7 @@ if __name__ == "__main__":
         if a.only and a.only != name:
             continue
         make_ext(name, *spec, a.noise)
+    for name, spec in STIR_CASES.items():
+        if a.only and a.only != name:
+            continue
+        make_stir(name, *spec, a.noise)

@@ -1,0 +1,211 @@
+"""Single-phase Laminar+SPS viscosity and shifting (SURVEY.md §8(f) row 4, v5.2 solver).
+
+Pinned to the REFERENCE DualSPHysics v5.2 CPU solver built from its sources
+(oracle/_ref/DualSPHysics5.2CPU_ref): tests/golden/make_golden.py EXT_CASES runs it on
+gencase_ref's dam break with ViscoTreatment 2 (Laminar+SPS, Visco 1e-6) and/or
+Shifting 1-3, and stores its PARTs plus the reference's own rounding-noise floor (the same
+sources built without -ffast-math, noise_<step>).  The GPU core (k_fluid_ext through the
+C-ABI) is held to 10x that floor, with a few-ulp floor where the two builds agree.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from golden_io import by_idp, load, maxdiff, snapshot
+from golden_io import steps as _steps
+
+from dualsphysics_multilayer_amd.case import DamBreakCase
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.path.join(ROOT, "oracle", "_ref")
+EXT_GOLDENS = ("verlet_lamsps_ddt2_dp0.02", "symplectic_lamsps_ddt1_dp0.025", "verlet_shift_nobound_dp0.025",
+               "symplectic_shift_full_tfs_dp0.025", "verlet_lamsps_shift_nofixed_dp0.03")
+# the same physics from a stirred start (make_golden.py STIR_CASES: reference restarts from
+# a Part_0000 with a shear + random velocity field), where the SPS stress and the shifting
+# displacement act from the first step
+STIR_GOLDENS = ("stir_verlet_lamsps_ddt2_dp0.025", "stir_symplectic_lamsps_ddt1_dp0.03",
+                "stir_verlet_shift_full_tfs_dp0.025", "stir_symplectic_lamsps_shift_nobound_dp0.03")
+FLOOR = (2e-10, 2e-7, 2.5e-3)  # pos m, vel m/s, rho kg/m3: 10x a noise of exactly 0 is no tolerance
+
+
+def steps(g):
+    """Kept steps after the start (the stirred fixtures also hold their start as s0_*)."""
+    return [k for k in _steps(g) if k > 0]
+
+
+def case_of(g, **kw):
+    dp, step, ddt, _ = g["meta"][:4]
+    tv, visco, sh, coef, tfs = g["ext"]
+    a = dict(step_algorithm=int(step), tdensity=int(ddt), tvisco=int(tv), visco=float(visco), shift_mode=int(sh),
+             shift_coef=float(coef), shift_tfs=float(tfs))
+    a.update(kw)
+    return DamBreakCase(float(dp), **a)
+
+
+def stirred_case(g, **kw):
+    base = case_of(g, **kw)
+    rst = g["rst"]
+    hdr = dict(case_nfixed=base.npb, map_posmin=rst[2:5].tolist(), map_posmax=rst[5:8].tolist(), timestep=rst[0],
+               symplectic_dtpre=rst[1])
+    parts = {k: g["s0_" + k] for k in ("idp", "pos", "vel", "rhop")}
+    return base.restart_from(hdr, parts)
+
+
+def ext_tol(g, k):
+    n = g["noise_%d" % k]
+    return tuple(max(10.0 * float(n[i]), FLOOR[i]) for i in range(3))
+
+
+# ---- CPU ------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", EXT_GOLDENS + STIR_GOLDENS)
+def test_goldens_present_with_noise_floor(name):
+    g = load(name)
+    assert steps(g) and all(("noise_%d" % k) in g.files for k in steps(g))
+    assert len(g["ext"]) == 5
+
+
+def test_sps_constants_match_reference():
+    """SpsSmag = (0.12 dp_sps)^2, SpsBlin = (2/3) 0.0066 dp_sps^2, dp_sps = sqrt(3 dp^2)/3
+    (JSph::ConfigConstants2, JSph.cpp:1438-1443)."""
+    from dualsphysics_multilayer_amd.core import case_derive
+
+    k = case_derive(DamBreakCase(0.02, tvisco=2, visco=1e-6).case_def())
+    dps = np.sqrt(3 * 0.02 ** 2) / 3
+    assert k["spssmag"] == np.float32((0.12 * dps) ** 2)
+    assert k["spsblin"] == np.float32((2 / 3) * 0.0066 * dps * dps)
+    assert k["tvisco"] == 2
+
+
+@pytest.mark.parametrize("tv,sh", [(2, 0), (1, 3), (2, 2)])
+def test_xml_loader_reads_viscosity_and_shifting(tmp_path, tv, sh):
+    """xmlcase reads gencase_ref's ViscoTreatment / Visco / Shifting / ShiftCoef / ShiftTFS
+    into the same SphCaseDef as the product-side generator."""
+    exe = os.path.join(REF, "gencase_ref")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref not built")
+    from dualsphysics_multilayer_amd.xmlcase import XmlCase
+
+    visco = "1e-6" if tv == 2 else "0.1"
+    subprocess.check_call([exe, "0.05", str(tmp_path), "1", "2", "1.5", "CaseDambreak", "1", "3", str(tv), visco, str(sh),
+                           "-2", "2.75"], stdout=subprocess.DEVNULL)
+    x = XmlCase(str(tmp_path / "CaseDambreak"))
+    c = DamBreakCase(0.05, tvisco=tv, visco=float(visco), shift_mode=sh, shift_coef=-2.0,
+                     shift_tfs=2.75 if sh else 0.0)
+    assert x.case_def() == c.case_def()
+
+
+# ---- GPU ------------------------------------------------------------------------------------
+def gpu(case):
+    from dualsphysics_multilayer_amd.core import SphGpuSingle
+
+    return SphGpuSingle(case, device=0)
+
+
+def check(got, ref, tl, k):
+    assert np.array_equal(got["idp"], ref["idp"]), "excluded-particle set differs"
+    for q, t in zip(("pos", "vel", "rhop"), tl):
+        assert maxdiff(got, ref, q) <= t, (k, q, maxdiff(got, ref, q), t)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", EXT_GOLDENS)
+def test_gpu_ext_steps_match_reference_parts(name):
+    g = load(name)
+    s = gpu(case_of(g))
+    done = 0
+    for k in steps(g):
+        s.run(k - done)
+        done = k
+        ref = snapshot(g, k)
+        check(by_idp(s.particles()), ref, ext_tol(g, k), k)
+        assert abs(s.stats()["time"] - float(ref["time"])) <= 1e-9 * max(1.0, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", STIR_GOLDENS)
+def test_gpu_ext_stirred_match_reference_parts(name):
+    g = load(name)
+    case = stirred_case(g)
+    s = gpu(case)
+    s.set_time(case.time0, case.symdtpre0)
+    done = 0
+    for k in steps(g):
+        s.run(k - done)
+        done = k
+        ref = snapshot(g, k)
+        check(by_idp(s.particles()), ref, ext_tol(g, k), k)
+        assert abs(s.stats()["time"] - float(ref["time"])) <= 1e-9 * max(1.0, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,off,factor", [("stir_verlet_lamsps_ddt2_dp0.025", dict(tvisco=1, visco=0.0), 3.0),
+                                             ("stir_symplectic_lamsps_ddt1_dp0.03", dict(tvisco=1, visco=0.0), 3.0),
+                                             ("stir_verlet_shift_full_tfs_dp0.025", dict(shift_mode=0), 10.0)])
+def test_gpu_ext_stirred_terms_matter(name, off, factor):
+    """Sensitivity: the same stirred start without the SPS stress (inviscid: Laminar's 1e-6
+    is negligible) or without shifting departs from the reference PARTs by more than
+    `factor` x the parity tolerance at some kept step, so the matches above pin those terms."""
+    g = load(name)
+    case = stirred_case(g, **off)
+    s = gpu(case)
+    s.set_time(case.time0, case.symdtpre0)
+    done, worst = 0, 0.0
+    for k in steps(g):
+        s.run(k - done)
+        done = k
+        got, ref = by_idp(s.particles()), snapshot(g, k)
+        tp, tv, _ = ext_tol(g, k)
+        r = max(maxdiff(got, ref, "vel") / tv, maxdiff(got, ref, "pos") / tp)
+        print(name, "step", k, "without the term: dvel %.3g (tol %.3g), dpos %.3g (tol %.3g)"
+              % (maxdiff(got, ref, "vel"), tv, maxdiff(got, ref, "pos"), tp))
+        worst = max(worst, r)
+    assert worst > factor, worst
+
+
+@pytest.mark.gpu
+def test_gpu_ext_dt_trace_matches_reference():
+    g = load("verlet_lamsps_ddt2_dp0.02")
+    s = gpu(case_of(g))
+    n = len(g["dt"])
+    s.run(n)
+    dt = s.dt_trace()
+    assert len(dt) == n
+    assert np.abs(dt / g["dt"] - 1).max() < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nslabs,name", [(2, "verlet_lamsps_ddt2_dp0.02"), (3, "symplectic_lamsps_ddt1_dp0.025"),
+                                         (2, "verlet_shift_nobound_dp0.025"),
+                                         (3, "verlet_lamsps_shift_nofixed_dp0.03"),
+                                         (3, "stir_verlet_lamsps_ddt2_dp0.025"),
+                                         (2, "stir_symplectic_lamsps_shift_nobound_dp0.03")])
+def test_gpu_ext_slabs_match_reference_parts(nslabs, name):
+    """x-slabs: the SPS tau travels with the migrants and reaches the ghosts through the face
+    exchange before every interaction (the stirred starts move many particles across faces)."""
+    from dualsphysics_multilayer_amd.core import SphSlabGroup, slab_partition
+
+    g = load(name)
+    case = stirred_case(g) if name.startswith("stir_") else case_of(g)
+    grp = SphSlabGroup(case, slab_partition(case, nslabs))
+    if name.startswith("stir_"):
+        grp.set_time(case.time0, case.symdtpre0)
+    done = 0
+    for k in steps(g):
+        grp.run(k - done)
+        done = k
+        check(grp.particles(), snapshot(g, k), ext_tol(g, k), k)
+        times = [st["time"] for st in grp.stats()]
+        assert max(times) == min(times)
+
+
+@pytest.mark.gpu
+def test_gpu_ext_deterministic():
+    case = case_of(load("verlet_lamsps_shift_nofixed_dp0.03"))
+    a, b = gpu(case), gpu(case)
+    a.run(30)
+    b.run(30)
+    pa, pb = a.particles(), b.particles()
+    for q in ("idp", "pos", "vel", "rhop"):
+        assert np.array_equal(pa[q], pb[q]), q
