@@ -60,12 +60,12 @@ void launch_presort(hipStream_t stm, unsigned cap, const DevScalars* sc, const u
 // prologue; wave match via ballots + tagged LDS wave counts).
 __global__ __launch_bounds__(RS_BS) void k_rs_hist(const DevScalars* __restrict__ sc, const unsigned* __restrict__ keys,
                                                    unsigned shift, unsigned rbits, unsigned ntiles,
-                                                   unsigned* __restrict__ hist) {
+                                                   unsigned* __restrict__ hist, unsigned nfix) {
   __shared__ unsigned cnt[1 << RS_MAXBITS];
   const unsigned radix = 1u << rbits, mask = radix - 1;
   for (unsigned d = threadIdx.x; d < radix; d += RS_BS) cnt[d] = 0;
   __syncthreads();
-  const unsigned n = sc->ndiv;
+  const unsigned n = nfix != ~0u ? nfix : sc->ndiv;
   const unsigned base = blockIdx.x * RS_TILE;
 #pragma unroll 4
   for (int it = 0; it < RS_ITEMS; it++) {
@@ -128,13 +128,13 @@ __global__ __launch_bounds__(RS_BS) void k_rs_scatter(const DevScalars* __restri
                                                       unsigned* __restrict__ kout, unsigned* __restrict__ vout,
                                                       unsigned shift, unsigned rbits, unsigned ntiles,
                                                       const unsigned* __restrict__ hist,
-                                                      const unsigned* __restrict__ digtot) {
+                                                      const unsigned* __restrict__ digtot, unsigned nfix) {
   constexpr int NW = RS_BS / 64;
   __shared__ unsigned s_off[1 << RS_MAXBITS];
   __shared__ unsigned s_wc[NW][1 << RS_MAXBITS];
   __shared__ unsigned s_part[RS_BS];
   const unsigned radix = 1u << rbits, mask = radix - 1;
-  const unsigned n = sc->ndiv;
+  const unsigned n = nfix != ~0u ? nfix : sc->ndiv;
   const unsigned base = blockIdx.x * RS_TILE;
   if (base >= n) return;  // whole block uniform
   // exclusive scan of the digit totals (<= 2048, contiguous per thread) in LDS
@@ -209,18 +209,21 @@ __global__ __launch_bounds__(RS_BS) void k_rs_scatter(const DevScalars* __restri
   }
 }
 
-int launch_radix_sort(hipStream_t stm, unsigned cap, const DevScalars* sc, SortScratch& s, unsigned keybits) {
+int launch_radix_sort(hipStream_t stm, unsigned cap, const DevScalars* sc, SortScratch& s, unsigned keybits,
+                      unsigned nfix) {
   const unsigned passes = (keybits + RS_MAXBITS - 1) / RS_MAXBITS;
   const unsigned rbits = (keybits + passes - 1) / passes;
-  const unsigned ntiles = (cap + RS_TILE - 1) / RS_TILE;
+  const unsigned ntiles = ((nfix != ~0u && nfix < cap ? nfix : cap) + RS_TILE - 1) / RS_TILE;
+  if (ntiles == 0) return 0;
   int cur = 0;
   for (unsigned p = 0; p < passes; p++) {
     const unsigned shift = p * rbits;
     const unsigned radix = 1u << rbits;
-    hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(RS_BS), 0, stm, sc, s.keys[cur], shift, rbits, ntiles, s.hist);
+    hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(RS_BS), 0, stm, sc, s.keys[cur], shift, rbits, ntiles, s.hist,
+                       nfix);
     hipLaunchKernelGGL(k_rs_scan_tiles, dim3((radix + SCAN_D - 1) / SCAN_D), dim3(256), 0, stm, s.hist, ntiles, radix, s.digtot);
     hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(RS_BS), 0, stm, sc, s.keys[cur], s.vals[cur],
-                       s.keys[cur ^ 1], s.vals[cur ^ 1], shift, rbits, ntiles, s.hist, s.digtot);
+                       s.keys[cur ^ 1], s.vals[cur ^ 1], shift, rbits, ntiles, s.hist, s.digtot, nfix);
     cur ^= 1;
   }
   return cur;
@@ -516,6 +519,10 @@ static_assert(INC_TILE <= 2048, "tile-local prefixes are 11 bits");
 constexpr int INC_SUP = 64;  // tiles per super tile
 constexpr int IB_BS = 256, IB_BPT = 2, IB_BOX = IB_BS * IB_BPT;  // boxes per k_inc_boxes block
 constexpr unsigned CW_NEAR = 0x80000000u, CW_FAR = 0x40000000u, CW_LOC = 0x7ffu;
+// slab: DROP = an old particle whose key became the discard box (a stale ghost): counted
+// with the far movers in the prefixes (it is not a stayer) but kept out of the far list
+// and never pushed; APP = a particle the exchange appended (no previous key)
+constexpr unsigned CW_DROP = 0x20000000u, CW_APP = 0x10000000u;
 // Phase timestamps of the incremental-divide kernels (SPH_INC_DBG & 8: printed for every
 // 16th block of the 12th incremental divide; the 100 MHz device clock).
 #define TSDECL unsigned long long tsv[8]
@@ -551,6 +558,7 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
                                                          IncDivScratch s, int usey, int usez) {
   __shared__ unsigned s_cn[INC_IPT * 4], s_cf[INC_IPT * 4];
   const unsigned n = sc->np;
+  const unsigned nold = n - s.napp;  // the previous divide's particles; [nold, n) were appended
   const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const unsigned b = blockIdx.x;  // the tile
   TSDECL;
@@ -558,7 +566,7 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
   if (b == 0 && threadIdx.x == 0) sc->ndiv = n;
   const unsigned long long lt = (1ull << lane) - 1ull;
   unsigned key[INC_IPT], rn[INC_IPT], rf[INC_IPT], fpos[INC_IPT];
-  bool nr[INC_IPT], fr[INC_IPT];
+  bool nr[INC_IPT], fr[INC_IPT], dr[INC_IPT];
   // every load of the tile first (one memory latency), then the classification
   unsigned dc[INC_IPT], old[INC_IPT];
   typecode cd[INC_IPT];
@@ -573,24 +581,25 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
 #pragma unroll
   for (int k = 0; k < INC_IPT; k++) {
     const unsigned i = b * INC_TILE + k * INC_BS + threadIdx.x;
-    const bool valid = i < n;
+    const bool valid = i < nold;
     key[k] = box_key(dc[k], cd[k], g, dcc);
     const int d = int(key[k] - old[k]);
-    nr[k] = valid && d != 0 && inc_near(d, g.ncx, int(g.nsheet), usey != 0, usez != 0);
-    fr[k] = valid && d != 0 && !nr[k];
-    const unsigned long long bn = __ballot(nr[k]), bf = __ballot(fr[k]);
+    dr[k] = valid && d != 0 && key[k] == g.boxdiscard;
+    nr[k] = valid && d != 0 && !dr[k] && inc_near(d, g.ncx, int(g.nsheet), usey != 0, usez != 0);
+    fr[k] = valid && d != 0 && !nr[k] && !dr[k];
+    const unsigned long long bn = __ballot(nr[k]), bf = __ballot(fr[k]), bfd = __ballot(fr[k] || dr[k]);
     rn[k] = unsigned(__popcll(bn & lt));
-    rf[k] = unsigned(__popcll(bf & lt));
+    rf[k] = unsigned(__popcll(bfd & lt));
     fpos[k] = 0;
     if (bf) {  // far movers (rare): appended to the list, one atomic per wave
       const unsigned lead = unsigned(__ffsll(static_cast<long long>(bf))) - 1u;
       unsigned base = 0;
       if (lane == lead) base = atomicAdd(&s.ctr[0], unsigned(__popcll(bf)));
-      fpos[k] = __shfl(base, int(lead), 64) + rf[k];
+      fpos[k] = __shfl(base, int(lead), 64) + unsigned(__popcll(bf & lt));
     }
     if (lane == 0) {
       s_cn[k * 4 + w] = unsigned(__popcll(bn));
-      s_cf[k * 4 + w] = unsigned(__popcll(bf));
+      s_cf[k * 4 + w] = unsigned(__popcll(bfd));
     }
   }
   __syncthreads();
@@ -604,9 +613,15 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
       pn += s_cn[q];
       pf += s_cf[q];
     }
-    const unsigned ln = pn + rn[k], lf = pf + rf[k];  // tile-local exclusive prefixes
     s.newkey[i] = key[k];
-    s.cw[i] = ln | (lf << 11) | (nr[k] ? CW_NEAR : 0u) | (fr[k] ? CW_FAR : 0u);
+    if (i >= nold) {  // appended: the input of their own sort
+      s.cw[i] = CW_APP;
+      s.akin[i - nold] = key[k];
+      s.avin[i - nold] = i - nold;
+      continue;
+    }
+    const unsigned ln = pn + rn[k], lf = pf + rf[k];  // tile-local exclusive prefixes
+    s.cw[i] = ln | (lf << 11) | (nr[k] ? CW_NEAR : 0u) | (fr[k] ? CW_FAR : 0u) | (dr[k] ? CW_DROP : 0u);
     if (nr[k]) s.mkey[b * INC_TILE + ln] = key[k];
     if (fr[k]) {
       s.mfar[fpos[k]] = make_uint2(i, key[k]);
@@ -668,10 +683,11 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   __shared__ unsigned s_boff[IB_BOX];   // bucket offsets (exclusive scan of s_narr)
   __shared__ unsigned s_nwsum[IB_BPT][IB_BS / 64];
   __shared__ unsigned s_nar;
+  __shared__ unsigned s_ab[IB_BOX + 1];  // slab: appended particles with a key below each box
   const unsigned b = blockIdx.x;
   TSDECL;
   TSTAMP(0);
-  const unsigned n = sc->ndiv;
+  const unsigned n = sc->ndiv - s.napp;  // the previous divide's particles (all but the appended)
   const unsigned totf = s.ctr[0];
   const long nctt = long(g.nctt);
   const long c0 = long(b) * IB_BOX;
@@ -752,7 +768,7 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
     pre += s_red[0][q];
     tot += s_red[1][q];
   }
-  const unsigned totn = unsigned(tot >> 32);
+  const unsigned totn = unsigned(tot >> 32), totfc = unsigned(tot);  // far class: far list + drops
   if (w == 0 && tplds) {  // exclusive scan of the window's tile counts, 16 tiles per lane
     constexpr int PL = IB_TPCAP / 64;
     uint2 v[PL];
@@ -793,7 +809,7 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
     return make_uint2(unsigned(p >> 32), unsigned(p));
   };
   auto lnlf = [&](unsigned x, unsigned cw) -> uint2 {  // (Ln(x), Lf(x))
-    if (x >= n) return make_uint2(totn, totf);
+    if (x >= n) return make_uint2(totn, totfc);
     const uint2 p = tp_of(x / INC_TILE);
     return make_uint2(p.x + (cw & CW_LOC), p.y + ((cw >> 11) & CW_LOC));
   };
@@ -902,6 +918,14 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   }
   __syncthreads();
   TSTAMP(2);
+  // ---- slab: the appended particles (sorted by key) below each box of the block; they
+  // follow the old members of their box (larger previous index), in appended order
+  if (s.napp) {
+    for (int k = int(threadIdx.x); k <= IB_BOX; k += IB_BS)
+      s_ab[k] = lower_bound_u32(s.akeys, 0u, s.napp, unsigned(min(c0 + k, nctt)));
+    __syncthreads();
+  }
+  auto ab = [&](int k) -> unsigned { return s.napp ? s_ab[k] : 0u; };
   // ---- per-box scan: begin, stayer offset, counts
   const unsigned base0 = jlo + s_below + s_farbelow;
   unsigned cnt[IB_BPT], xs[IB_BPT], xsn[IB_BPT];
@@ -943,7 +967,7 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
     hpren += hsumn;
     const unsigned S = s_obx[k] - s_ln[k] - s_lf[k];
     const unsigned stay = (s_obx[k + 1] - s_obx[k]) - (s_ln[k + 1] - s_ln[k]) - (s_lf[k + 1] - s_lf[k]);
-    const unsigned begin = S + base0 + hpre + wpre + xs[h] - cnt[h];
+    const unsigned begin = S + base0 + hpre + wpre + xs[h] - cnt[h] + ab(k);
     hpre += hsum;
     s_begin[k] = begin;
     const long c = c0 + k;
@@ -951,7 +975,8 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
     const unsigned cu = unsigned(c);
     nbc[cu] = begin;
     s.stayoff[cu] = begin + s_nbef[k] + s_fbef[k] - S;
-    const unsigned total = cnt[h] + stay;
+    const unsigned total = cnt[h] + stay + (ab(k + 1) - ab(k));
+    for (unsigned e = ab(k); e < ab(k + 1); e++) s.apppos[s.avals[e]] = begin + cnt[h] + stay + (e - ab(k));
     // JCellDivCpuSingle::Divide counts + RunCellDivide, as k_begincell
     if (cu == g.boxboundignore) sc->npbok = begin;
     if (cu == g.boxfluid) sc->npb = begin;
@@ -1066,7 +1091,7 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
 // also clears the super-tile sums and the far count for the next divide.
 template <bool WITHM1, bool WITHPRE, bool WITHTAU>
 __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, GatherArgs a, IncDivScratch s) {
-  const unsigned nd = sc->ndiv, n = sc->np, npb = sc->npb;
+  const unsigned nd = sc->ndiv, n = sc->np, npb = sc->npb, nold = nd - s.napp;
   const unsigned t = blockIdx.x;
   const unsigned i0 = t * INC_TILE + threadIdx.x;
   GatherRec<WITHM1, WITHPRE, WITHTAU> q[GP];
@@ -1084,8 +1109,8 @@ __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, G
   }
 #pragma unroll
   for (int k = 0; k < GP; k++) {
-    const bool near = (cw[k] & CW_NEAR) != 0, far = (cw[k] & CW_FAR) != 0;
-    fx[k] = far ? s.fidx[i0 + 256 * k] : 0u;
+    const bool far = (cw[k] & CW_FAR) != 0, app = (cw[k] & CW_APP) != 0;
+    fx[k] = far ? s.fidx[i0 + 256 * k] : (app ? s.apppos[i0 + 256 * k - nold] : 0u);
   }
 #pragma unroll
   for (int k = 0; k < GP; k++) {
@@ -1094,6 +1119,8 @@ __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, G
     const unsigned* tab = near ? s.mposnear : (far ? s.mposfar : s.stayoff);
     const unsigned x = tab[near ? t * INC_TILE + ln : (far ? fx[k] : key[k])];
     pos[k] = (near || far) ? x : x + (i0 + 256 * k) - tpg - ln - lf;
+    if (cw[k] & CW_APP) pos[k] = fx[k];
+    if (cw[k] & CW_DROP) pos[k] = ~0u;
   }
   float v2 = 0.f;
 #pragma unroll
@@ -1116,16 +1143,23 @@ __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, G
 void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& src, const PartArrays& dst,
                        bool withm1, bool withpre, const KConst& K, const double dom_posmin[3], float4* poscell,
                        float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
-                       IncDivScratch& s, const float4* phase_eos) {
+                       IncDivScratch& s, SortScratch& srt, unsigned keybits, const float4* phase_eos) {
   s.gen++;
   const int usey = g.ncy > 1, usez = g.ncz > 1;
   const unsigned omax = 1u + (usey ? unsigned(g.ncx) : 0u) + (usez ? g.nsheet : 0u);
+  s.akin = srt.keys[0];
+  s.avin = srt.vals[0];
   hipLaunchKernelGGL(k_inc_classify, dim3(s.nb1), dim3(INC_BS), 0, stm, sc, src.dcell, src.code, g, K.domcellcode, s,
                      usey, usez);
+  if (s.napp) {  // slab: the appended particles, sorted by key apart (stable: appended order)
+    const int res = launch_radix_sort(stm, cap, sc, srt, keybits, s.napp);
+    s.akeys = srt.keys[res];
+    s.avals = srt.vals[res];
+  }
   hipLaunchKernelGGL(k_inc_boxes, dim3(s.nb2), dim3(IB_BS), 0, stm, sc, g, begincell_old, begincell_new, s, omax);
   GatherArgs a;
   a.phase_eos = phase_eos;
-  a.xoff = 0;
+  a.xoff = g.xoff;
   a.src = src;
   a.dst = dst;
   a.sortpart = nullptr;

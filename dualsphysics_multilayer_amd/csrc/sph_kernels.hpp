@@ -107,8 +107,10 @@ constexpr int RS_MAXBITS = 11;    // widest digit (2048 buckets)
 // PreSort: box key per particle (KerPreSortFull, JCellDivGpuSingle_ker.cu:41-102).
 void launch_presort(hipStream_t stm, unsigned cap, const DevScalars* sc, const unsigned* dcell, const typecode* code,
                     DivGrid g, unsigned domcellcode, unsigned* keys, unsigned* vals);
-// Stable LSD radix sort of (keys, vals) for the first sc->np entries; result in keys[res]/vals[res].
-int launch_radix_sort(hipStream_t stm, unsigned cap, const DevScalars* sc, SortScratch& s, unsigned keybits);
+// Stable LSD radix sort of (keys, vals) for the first sc->ndiv entries (or the first `nfix`
+// when given: a count the host knows); result in keys[res]/vals[res].
+int launch_radix_sort(hipStream_t stm, unsigned cap, const DevScalars* sc, SortScratch& s, unsigned keybits,
+                      unsigned nfix = ~0u);
 // begincell by lower-bound search + new counts (KerCalcBeginEndCell, JCellDivGpu_ker.cu:512-546).
 void launch_begincell(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned* skeys, DivGrid g, unsigned* begincell);
 // Gather + poscell + press + VelMax (KerSortDataParticles, JCellDivGpu_ker.cu:553-720; KerUpdatePosCell,
@@ -118,7 +120,9 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
                    float4* poscell, float* press, int xoff, const float4* phase_eos = nullptr);
 
 // Incremental divide (sph_divide.hip): the stable order of the previous divide merged with
-// the particles whose box changed; single domain, every divide after the first.
+// the particles whose box changed, every divide after the first.  On a slab the exchange
+// appended `napp` particles (migrants + ghosts) after the `nold` of the previous divide:
+// they are sorted apart (a small radix sort) and placed after the old members of their box.
 struct IncDivScratch {
   unsigned* skeys = nullptr;      // [cap] box key of the particle at each index (last divide)
   unsigned* newkey = nullptr;     // [cap] box key of this divide
@@ -133,6 +137,14 @@ struct IncDivScratch {
   unsigned* mposfar = nullptr;    // [cap] new positions of the far movers
   unsigned* stayoff = nullptr;    // [nctt] new index of a stayer = stayoff[key] + i - movers before i
   unsigned* ctr = nullptr;        // [0]: far movers (cleared by k_inc_push)
+  // slab: the appended particles [nold, nold + napp): keys / indices for their sort (written
+  // by k_inc_classify), the sorted result, and their new positions (k_inc_boxes)
+  unsigned* akin = nullptr;
+  unsigned* avin = nullptr;
+  const unsigned* akeys = nullptr;
+  const unsigned* avals = nullptr;
+  unsigned* apppos = nullptr;     // [cap]
+  unsigned nold = 0, napp = 0;
   unsigned nb1 = 0, nb2 = 0, gen = 0;
   // SPH_INC_DBG: 8 phase timestamps of the divide kernels (printf); 16 / 32 force the
   // global-memory paths of the tile prefixes / far arrivals (tests)
@@ -144,7 +156,7 @@ unsigned inc_blocks_boxes(unsigned nctt);
 void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& src, const PartArrays& dst,
                        bool withm1, bool withpre, const KConst& K, const double dom_posmin[3], float4* poscell,
                        float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
-                       IncDivScratch& s, const float4* phase_eos = nullptr);
+                       IncDivScratch& s, SortScratch& srt, unsigned keybits, const float4* phase_eos = nullptr);
 
 // ---- interaction (cusph::Interaction_Forces, JSphGpu_ker.cu:788-885) ----
 // With floating bodies (ftmassp != nullptr: particle mass per body, `code` of the

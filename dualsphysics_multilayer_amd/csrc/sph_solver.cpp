@@ -357,9 +357,9 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   nctmax_ = slab() ? unsigned(C.dom_cells[0] + 2) * unsigned(G.ncy) * unsigned(G.ncz) : G.nct;
   if (const char* e = std::getenv("SPH_INTERACTION")) tiled_ = std::string(e) != "simple";
   if (const char* e = std::getenv("SPH_COMM_TIMEOUT_S")) comm_timeout_s_ = std::max(1.0, std::atof(e));
-  // incremental divide: distinct key offsets of the 27 neighbour cells (ncx >= 3; ncy >= 3
-  // or a single y row), 30-bit mover counts, single domain
-  inc_ok_ = !slab() && G.ncx >= 3 && (G.ncy >= 3 || G.ncy == 1) && n < (1u << 30);
+  // incremental divide: distinct key offsets of the 27 neighbour cells (ncx >= 3, checked
+  // again per divide for a re-partitioned slab; ncy >= 3 or a single y row), 30-bit counts
+  inc_ok_ = G.ncx >= 3 && (G.ncy >= 3 || G.ncy == 1) && n < (1u << 29);
   if (const char* e = std::getenv("SPH_DIVIDE")) inc_ok_ = inc_ok_ && std::string(e) != "full";
   // The tiled kernel stages the 3x3 rows of 3 cells of CellMode=full, or the 5x5 rows of
   // 5 half-cells of CellMode=half (run_pass_half).
@@ -536,6 +536,8 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
     const size_t nsup = (size_t(inc_.nb1) + 63) / 64;
     inc_.tsup = (unsigned long long*)dmalloc(8 * nsup);
     check_hip(hipMemset(inc_.tsup, 0, 8 * nsup), "zero super tiles");
+    if (slab()) inc_.apppos = (unsigned*)dmalloc(4 * n);
+    inc_valid_ = false;  // new scratch: the next divide is a full one
   }
   sort_.ntiles = unsigned((n + RS_TILE - 1) / RS_TILE);
   sort_.hist = (unsigned*)dmalloc(4 * size_t(sort_.ntiles) * (1u << RS_MAXBITS));
@@ -824,6 +826,8 @@ void SphGpuSingle::Exchange() {
   transport_->group_end();
   launch_slab_unpack(stream, sc_, recvm_, unsigned(rml + rmr), recvg_, unsigned(rgl + rgr), c.np, cur_, K,
                      C.dom_posmin, withm1, withpre, slabcnt_, normal_, casenpb_);
+  inc_.nold = unsigned(c.np);  // the incremental divide places the appended [np, np + nin) apart
+  inc_.napp = unsigned(nin);
 }
 
 // The one host wait of a slab divide: spin on the event (a blocking synchronise wakes up
@@ -905,6 +909,7 @@ void SphGpuSingle::Repartition() {
   slabcfg_.c1 = nb[size_t(slabcfg_.rank) + 1];
   G = make_grid(C, &slabcfg_);
   keybits_ = bits_for(G.boxdiscard, 1);
+  inc_valid_ = false;  // the box keys changed: the next divide sorts from scratch
   repart_count_++;
 }
 
@@ -923,10 +928,12 @@ void SphGpuSingle::RunCellDivide() {
     Repartition();
   if (slab() && exchange_armed_) Exchange();
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET);
-  if (inc_ok_ && inc_valid_) {
-    // the previous order merged with the particles whose box changed (sph_divide.hip)
+  if (inc_ok_ && inc_valid_ && G.ncx >= 3) {
+    // the previous order merged with the particles whose box changed and, on a slab, the
+    // particles the exchange appended (sph_divide.hip)
+    inc_.nb2 = inc_blocks_boxes(G.nctt);
     launch_divide_inc(stream, cap_, sc_, cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_, G, begincell_,
-                      begincell_alt_, inc_, nn_ ? phaseeos_ : nullptr);
+                      begincell_alt_, inc_, sort_, keybits_, nn_ ? phaseeos_ : nullptr);
     std::swap(begincell_, begincell_alt_);
   } else {
     launch_presort(stream, cap_, sc_, cur_.dcell, cur_.code, G, C.dom_cellcode, sort_.keys[0], sort_.vals[0]);
@@ -939,6 +946,7 @@ void SphGpuSingle::RunCellDivide() {
                 "keep sorted keys");
   }
   inc_valid_ = inc_ok_;
+  inc_.napp = 0;
   std::swap(cur_, alt_);
   if (tiled_) {
     launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv);  // also zeroes the queues

@@ -138,3 +138,71 @@ def test_inc_divide_1m(monkeypatch):
     case = DamBreakCase(0.0045)
     assert case.np == 1025964
     _same(case, 20, 10, monkeypatch)
+
+
+# ---- slabs: the exchange appends migrants + ghosts after the previous order; stale ghosts
+# leave through the discard box (k_inc_classify DROP / APP classes) ------------------------
+def _group(case, nslabs, mode, monkeypatch, repart=0):
+    from dualsphysics_multilayer_amd.core import SphSlabGroup, case_derive, slab_partition
+
+    if mode == "full":
+        monkeypatch.setenv("SPH_DIVIDE", "full")
+    else:
+        monkeypatch.delenv("SPH_DIVIDE", raising=False)
+    if repart:  # an uneven start, so that the first re-partition moves the bounds
+        ncx = case_derive(case.case_def())["dom_cells"][0]
+        bounds = np.array([0] + [ncx - 2 * (nslabs - r) for r in range(1, nslabs)] + [ncx], np.int32)
+    else:
+        bounds = slab_partition(case, nslabs)
+    g = SphSlabGroup(case, bounds)
+    monkeypatch.delenv("SPH_DIVIDE", raising=False)
+    if repart:
+        g.set_repartition(repart, 0.3, 0.0)
+    return g
+
+
+def _same_slabs(case, nslabs, nsteps, chunk, monkeypatch, repart=0):
+    a = _group(case, nslabs, "inc", monkeypatch, repart)
+    b = _group(case, nslabs, "full", monkeypatch, repart)
+    done = 0
+    while done < nsteps:
+        a.run(chunk)
+        b.run(chunk)
+        done += chunk
+        for r, (ma, mb) in enumerate(zip(a.members, b.members)):
+            sa, sb = ma.stats(), mb.stats()
+            for k in ("np", "npb", "npbok", "nout", "nstep", "error_flags"):
+                assert sa[k] == sb[k], (done, r, k, sa[k], sb[k])
+            pa, pb = ma.particles(), mb.particles()
+            for k in ("idp", "pos", "vel", "rhop"):  # each slab's device order
+                assert np.array_equal(pa[k], pb[k]), (done, r, k)
+    if repart:
+        assert [m["repartitions"] for m in a.slab_info()] == [m["repartitions"] for m in b.slab_info()]
+    return a
+
+
+@pytest.mark.parametrize("nslabs", [2, 3])
+def test_inc_divide_slabs_verlet_stirred(monkeypatch, nslabs):
+    case = _stirred(DamBreakCase(0.025, celldomfixed=True), 0.5, 3.0)
+    _same_slabs(case, nslabs, 40, 5, monkeypatch)
+
+
+def test_inc_divide_slabs_symplectic_exclusions(monkeypatch):
+    case = _stirred(DamBreakCase(0.03, step_algorithm=2, tdensity=1, celldomfixed=True, rhopoutmax=1010.0), 0.3, 2.0)
+    rng = np.random.default_rng(5)
+    pick = rng.choice(np.arange(case.npb, case.np), 40, replace=False)
+    case.vel[pick[:20]] = [0, 0, 400.0]
+    case.vel[pick[20:]] = [-120.0, 0, 0]
+    _same_slabs(case, 3, 30, 3, monkeypatch)
+
+
+def test_inc_divide_slabs_bodies_and_nn(monkeypatch):
+    _same_slabs(WaveFlumeCase(0.025), 3, 24, 8, monkeypatch)
+    _same_slabs(WetDambreakNNCase(0.025, width=0.2, scale=0.5), 2, 12, 4, monkeypatch)
+
+
+def test_inc_divide_slabs_repartition(monkeypatch):
+    """A re-partition changes the slab grids: that divide sorts from scratch, later ones merge."""
+    case = _stirred(DamBreakCase(0.025, celldomfixed=True), 0.5, 3.0)
+    g = _same_slabs(case, 3, 30, 5, monkeypatch, repart=5)
+    assert max(m["repartitions"] for m in g.slab_info()) >= 1
