@@ -101,6 +101,16 @@ struct DivGrid {
   int xoff, xown0, xown1;
 };
 
+// Slab faces: a slab has xown0 (= ncx - xown1) ghost columns per face, the support radius
+// 2h in columns (1 with full cells, 2 with half cells).  The owned columns a neighbour
+// needs as its ghosts are the first / last xown0 owned ones.
+__host__ __device__ __forceinline__ bool in_left_face(const DivGrid& g, int lcx) {
+  return lcx >= g.xown0 && lcx < 2 * g.xown0;
+}
+__host__ __device__ __forceinline__ bool in_right_face(const DivGrid& g, int lcx) {
+  return lcx < g.xown1 && lcx >= g.xown1 - (g.ncx - g.xown1);
+}
+
 // dcell markers: excluded particle (JSphCpu::UpdatePos, JSphCpu.cpp:1262) and a
 // particle this rank drops at the next divide (slab ghosts).
 constexpr unsigned DCELL_OUT = 0xFFFFFFFFu, DCELL_DISCARD = 0xFFFFFFFEu;

@@ -441,8 +441,8 @@ __global__ __launch_bounds__(256) void k_mdbc_face_pack(const DevScalars* __rest
   // a slab of one owned column sends the same particle both ways
   for (int side = 0; side < 2; side++) {
     MdbcFaceRec* dst = nullptr;
-    if (side == 0 && lcx == g.xown0 && g.xown0 > 0) dst = sl;
-    if (side == 1 && lcx == g.xown1 - 1 && g.xown1 < g.ncx) dst = sr;
+    if (side == 0 && in_left_face(g, lcx) && g.xown0 > 0) dst = sl;
+    if (side == 1 && in_right_face(g, lcx) && g.xown1 < g.ncx) dst = sr;
     if (!dst) continue;
     const unsigned k = atomicAdd(&dst[0].idp, 1u);
     if (k + 1 < cap) dst[k + 1] = MdbcFaceRec{id, a.velrhop[p].w, press[p]};

@@ -1242,8 +1242,8 @@ __global__ __launch_bounds__(256) void k_nn_face_pack(const DevScalars* __restri
   for (int side = 0; side < 2; side++) {  // a slab of one owned column sends a particle both ways
     NNFaceRec* dst = nullptr;
     unsigned cap = 0;
-    if (side == 0 && lcx == g.xown0 && g.xown0 > 0) { dst = sl; cap = capl; }
-    if (side == 1 && lcx == g.xown1 - 1 && g.xown1 < g.ncx) { dst = sr; cap = capr; }
+    if (side == 0 && in_left_face(g, lcx) && g.xown0 > 0) { dst = sl; cap = capl; }
+    if (side == 1 && in_right_face(g, lcx) && g.xown1 < g.ncx) { dst = sr; cap = capr; }
     if (!dst) continue;
     const unsigned k = atomicAdd(&dst[0].idp, 1u);
     if (k + 1 >= cap) continue;  // cannot happen: the buffers hold every ghost sent at the divide

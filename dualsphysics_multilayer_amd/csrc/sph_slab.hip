@@ -44,8 +44,8 @@ __device__ __forceinline__ unsigned pack_class(const PackArgs& q, unsigned p) {
   if (lcx < q.g.xown0) return q.has_left ? 1u : 0u;
   if (lcx >= q.g.xown1) return q.has_right ? 2u : 0u;
   unsigned c = 4u;
-  if (lcx == q.g.xown0 && q.has_left) c |= 1u;
-  if (lcx == q.g.xown1 - 1 && q.has_right) c |= 2u;
+  if (in_left_face(q.g, lcx) && q.has_left) c |= 1u;
+  if (in_right_face(q.g, lcx) && q.has_right) c |= 2u;
   return c;
 }
 

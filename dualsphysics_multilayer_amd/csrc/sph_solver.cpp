@@ -230,8 +230,8 @@ static KConst make_kconst(const SphConstants& c) {
 }
 
 // Full-map cell grid (JCellDivCpuSingle::PrepareNct, JCellDivCpuSingle.cpp:105-121, with CellDomFixed).
-// A slab keeps the global y/z extent and the x-columns [c0-1, c1] (owned + one ghost
-// column per face).
+// A slab keeps the global y/z extent and the x-columns [c0-W, c1+W) (owned + W ghost
+// columns per face, W = scelldiv: the support radius 2h is one full cell or two half cells).
 static DivGrid make_grid(const SphConstants& c, const SlabConfig* slab) {
   DivGrid g;
   g.ncx = int(c.dom_cells[0]);
@@ -241,13 +241,14 @@ static DivGrid make_grid(const SphConstants& c, const SlabConfig* slab) {
   g.xown0 = 0;
   g.xown1 = g.ncx;
   if (slab) {
-    if (slab->nranks < 1 || slab->rank < 0 || slab->rank >= slab->nranks || slab->c0 < 0 || slab->c1 <= slab->c0 ||
+    const int W = int(c.scelldiv);
+    if (slab->nranks < 1 || slab->rank < 0 || slab->rank >= slab->nranks || slab->c0 < 0 || slab->c1 < slab->c0 + W ||
         slab->c1 > g.ncx)
-      throw SphError(SPH_ERR_ARG, "invalid slab columns");
-    g.xoff = slab->c0 - 1;
-    g.ncx = slab->c1 - slab->c0 + 2;
-    g.xown0 = 1;
-    g.xown1 = 1 + slab->c1 - slab->c0;
+      throw SphError(SPH_ERR_ARG, "invalid slab columns (a slab owns at least scelldiv columns)");
+    g.xoff = slab->c0 - W;
+    g.ncx = slab->c1 - slab->c0 + 2 * W;
+    g.xown0 = W;
+    g.xown1 = W + slab->c1 - slab->c0;
   }
   g.nsheet = unsigned(g.ncx) * unsigned(g.ncy);
   const unsigned long long nct = (unsigned long long)g.nsheet * unsigned(g.ncz);
@@ -275,8 +276,8 @@ static std::vector<unsigned> initial_columns(const SphConstants& C, const SphPar
 }
 
 // Column bounds b[0..nranks] at the quantiles of the weight prefix pre[0..ncx] (each slab
-// at least one column; a bound column goes to the side closer to its target).
-void partition_from_prefix(const std::vector<double>& pre, int nranks, int* b) {
+// at least minw columns; a bound column goes to the side closer to its target).
+void partition_from_prefix(const std::vector<double>& pre, int nranks, int* b, int minw) {
   const int ncx = int(pre.size()) - 1;
   b[0] = 0;
   b[nranks] = ncx;
@@ -286,8 +287,8 @@ void partition_from_prefix(const std::vector<double>& pre, int nranks, int* b) {
     while (c < ncx && pre[size_t(c)] < target) c++;
     int cut = c;
     if (cut > 0 && target - pre[size_t(cut) - 1] < pre[size_t(cut)] - target) cut--;
-    cut = std::max(cut, b[r - 1] + 1);
-    cut = std::min(cut, ncx - (nranks - r));
+    cut = std::max(cut, b[r - 1] + minw);
+    cut = std::min(cut, ncx - (nranks - r) * minw);
     b[r] = cut;
   }
 }
@@ -295,15 +296,15 @@ void partition_from_prefix(const std::vector<double>& pre, int nranks, int* b) {
 void slab_partition(const SphCaseDef& cdef, const SphParticlesHost& all, int nranks, double bound_weight, int* b) {
   SphConstants C;
   derive_constants(cdef, C);
-  const int ncx = int(C.dom_cells[0]);
-  if (nranks < 1 || nranks > ncx) throw SphError(SPH_ERR_ARG, "nranks must be in [1, x-cells]");
+  const int ncx = int(C.dom_cells[0]), W = int(C.scelldiv);
+  if (nranks < 1 || nranks * W > ncx) throw SphError(SPH_ERR_ARG, "nranks must be in [1, x-cells / scelldiv]");
   if (all.n != cdef.np) throw SphError(SPH_ERR_ARG, "particle count does not match the case");
   std::vector<double> w(size_t(ncx), 0.0);
   const std::vector<unsigned> cx = initial_columns(C, all);
   for (unsigned p = 0; p < all.n; p++) w[std::min<unsigned>(cx[p], unsigned(ncx - 1))] += (p < cdef.npb ? bound_weight : 1.0);
   std::vector<double> pre(size_t(ncx) + 1, 0.0);
   for (int c = 0; c < ncx; c++) pre[size_t(c) + 1] = pre[size_t(c)] + w[size_t(c)];
-  partition_from_prefix(pre, nranks, b);
+  partition_from_prefix(pre, nranks, b, W);
 }
 
 SphGpuSingle::SphGpuSingle(const SphCaseDef& cdef, const SphParticlesHost& init, int dev) : device(dev) {
@@ -316,8 +317,6 @@ SphGpuSingle::SphGpuSingle(const SphCaseDef& cdef, const SphParticlesHost& all, 
   if (!transport_) throw SphError(SPH_ERR_ARG, "slab without a transport");
   if (transport_->rank != slab.rank || transport_->nranks != slab.nranks)
     throw SphError(SPH_ERR_ARG, "slab rank does not match the transport");
-  if (cdef.cellmode == SPH_CELLMODE_HALF)
-    throw SphError(SPH_ERR_UNSUPPORTED, "CellMode=half is not implemented on the slab decomposition");
   Init(cdef, all);
 }
 
@@ -333,8 +332,9 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   unsigned nown = init.n;
   if (slab()) {
     const std::vector<unsigned> cx = initial_columns(C, init);
-    const int lo = slabcfg_.c0 - (slabcfg_.rank > 0 ? 1 : 0);
-    const int hi = slabcfg_.c1 + (slabcfg_.rank + 1 < slabcfg_.nranks ? 1 : 0);
+    const int W = int(C.scelldiv);
+    const int lo = slabcfg_.c0 - (slabcfg_.rank > 0 ? W : 0);
+    const int hi = slabcfg_.c1 + (slabcfg_.rank + 1 < slabcfg_.nranks ? W : 0);
     nown = 0;
     for (unsigned p = 0; p < init.n; p++) {
       const int c = int(cx[p]);
@@ -378,12 +378,13 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
     // columns (both sides of a face count the same particles); later from each exchange
     const std::vector<unsigned> cx = initial_columns(C, init);
     const bool hl = slabcfg_.rank > 0, hr = slabcfg_.rank + 1 < slabcfg_.nranks;
+    const int W = int(C.scelldiv), c0 = slabcfg_.c0, c1 = slabcfg_.c1;
     for (unsigned p : sel) {
       const int c = int(cx[p]);
-      face_sl_ += (hl && c == slabcfg_.c0) ? 1u : 0u;
-      face_sr_ += (hr && c == slabcfg_.c1 - 1) ? 1u : 0u;
-      face_rl_ += (hl && c == slabcfg_.c0 - 1) ? 1u : 0u;
-      face_rr_ += (hr && c == slabcfg_.c1) ? 1u : 0u;
+      face_sl_ += (hl && c >= c0 && c < c0 + W) ? 1u : 0u;
+      face_sr_ += (hr && c >= c1 - W && c < c1) ? 1u : 0u;
+      face_rl_ += (hl && c >= c0 - W && c < c0) ? 1u : 0u;
+      face_rr_ += (hr && c >= c1 && c < c1 + W) ? 1u : 0u;
     }
   }
   if (nn_) {
@@ -681,7 +682,7 @@ void SphGpuSingle::UploadNormals(const SphCaseDef& cdef, const SphParticlesHost&
       const unsigned cx = unsigned((h.pos[3 * p] - C.dom_posmin[0]) / double(C.scell));
       if (cx < cnt.size()) mx = std::max(mx, ++cnt[cx]);
     }
-    mdbcfacecap_ = 2 * mx + 64;
+    mdbcfacecap_ = 2 * mx * unsigned(C.scelldiv) + 64;  // W face columns
     check_hip(hipMalloc((void**)&mdbcface_, sizeof(MdbcFaceRec) * 4 * size_t(mdbcfacecap_)), "hipMalloc mDBC faces");
     allocs_.push_back(mdbcface_);
     check_hip(hipMalloc((void**)&bidx_, sizeof(unsigned) * std::max(cdef.npb, 1u)), "hipMalloc mDBC faces");
@@ -894,14 +895,15 @@ void SphGpuSingle::Repartition() {
   repart_last_imbalance_ = total > 0 ? maxload / (total / nr) : 1.0;
   if (!(repart_last_imbalance_ > 1.0 + repart_tol_)) return;
   std::vector<int> nb(old);
-  partition_from_prefix(pre, nr, nb.data());
+  const int W = int(C.scelldiv);  // every slab keeps at least its W face columns
+  partition_from_prefix(pre, nr, nb.data(), W);
   for (int r = 1; r < nr; r++) {  // inside the two slabs it separates, and increasing
-    nb[size_t(r)] = std::min(std::max(nb[size_t(r)], old[size_t(r) - 1] + 1), old[size_t(r) + 1] - 1);
-    nb[size_t(r)] = std::max(nb[size_t(r)], nb[size_t(r) - 1] + 1);
+    nb[size_t(r)] = std::min(std::max(nb[size_t(r)], old[size_t(r) - 1] + W), old[size_t(r) + 1] - W);
+    nb[size_t(r)] = std::max(nb[size_t(r)], nb[size_t(r) - 1] + W);
   }
   bool changed = false;
   for (int r = 1; r < nr; r++) {
-    if (nb[size_t(r)] >= nb[size_t(r) + 1]) return;  // the clamps left no valid split: keep the old one
+    if (nb[size_t(r)] + W > nb[size_t(r) + 1]) return;  // the clamps left no valid split: keep the old one
     changed |= nb[size_t(r)] != old[size_t(r)];
   }
   if (!changed) return;

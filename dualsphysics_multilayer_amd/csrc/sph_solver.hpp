@@ -30,7 +30,7 @@ void check_hip(hipError_t e, const char* what);
 void derive_constants(const SphCaseDef& c, SphConstants& k);
 // Column bounds of a particle-count-balanced x-slab split (sph_slab_partition).
 void slab_partition(const SphCaseDef& c, const SphParticlesHost& all, int nranks, double bound_weight, int* bounds);
-void partition_from_prefix(const std::vector<double>& prefix, int nranks, int* bounds);
+void partition_from_prefix(const std::vector<double>& prefix, int nranks, int* bounds, int minw = 1);
 // PART / case files (sph_bi4.cpp)
 void part_read(const std::string& path, SphPartHeader& h, SphParticlesHost* out);
 void part_write(const std::string& path, const SphPartHeader& h, const SphParticlesHost& p);

@@ -11,15 +11,13 @@ device-to-device copies as the transport — RCCL refuses two ranks on one devic
 import numpy as np
 import pytest
 
-from golden_io import tol, by_idp, load, maxdiff, meta, snapshot, steps
+from golden_io import cellmode, tol, by_idp, load, maxdiff, meta, snapshot, steps
 
 from dualsphysics_multilayer_amd.case import DamBreakCase
 
 pytestmark = pytest.mark.gpu
 
 oracle = pytest.importorskip("oracle.pyoracle")
-
-
 
 
 def group(case, nslabs, bounds=None):
@@ -226,3 +224,60 @@ def test_repartition_deterministic_and_matches_single():
         assert np.array_equal(pa[k], pb[k]), k
     check_close(pa, by_idp(one.particles()), 30)
     assert [i["cx_begin"] for i in a.slab_info()] == [i["cx_begin"] for i in b.slab_info()]
+
+
+# ---- CellMode=half: cells of h, two ghost columns per face (the support 2h) -----------------
+@pytest.mark.parametrize("nslabs", [2, 3])
+def test_half_cell_slabs_match_reference_parts(nslabs):
+    g_ = load("verlet_ddt2_half_dp0.025")
+    dp, step_alg, ddt, _ = meta(g_)
+    assert cellmode(g_) == 2
+    grp = group(DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt, cellmode=2), nslabs)
+    info = grp.slab_info()
+    assert min(i["cx_end"] - i["cx_begin"] for i in info) >= 2
+    done = 0
+    for k in steps(g_):
+        grp.run(k - done)
+        done = k
+        check_close(grp.particles(), snapshot(g_, k), k)
+        times = [s["time"] for s in grp.stats()]
+        assert max(times) == min(times)
+
+
+def test_half_cell_two_column_slabs_migration_and_repartition():
+    """Slabs of exactly two half-cell columns (each owned column is a face column of both
+    neighbours), fluid pushed along +x so particles migrate every few steps, then
+    re-balancing every 4 steps: against the single-domain oracle."""
+    from dualsphysics_multilayer_amd.core import case_derive
+
+    case = DamBreakCase(0.03, cellmode=2, celldomfixed=True)
+    case.vel[case.npb:, 0] = 2.0
+    ncx = case_derive(case.case_def())["dom_cells"][0]
+    grp = group(case, 4, np.array([0, 2, 4, 6, ncx], np.int32))
+    o = oracle.OracleSolver(case, nthreads=4)
+    done = 0
+    for k in (4, 12):
+        grp.run(k - done)
+        o.run(k - done)
+        done = k
+        check_close(grp.particles(), by_idp(o.particles()), k)
+    grp.set_repartition(4, 0.3, 0.0)
+    grp.run(12)
+    o.run(12)
+    check_close(grp.particles(), by_idp(o.particles()), 24)
+    info = grp.slab_info()
+    assert all(i["cx_end"] - i["cx_begin"] >= 2 for i in info)
+    assert max(i["repartitions"] for i in info) >= 1
+
+
+def test_half_cell_partition_keeps_two_columns():
+    """slab_partition with CellMode=half gives every slab at least the two face columns; a
+    slab narrower than that is refused."""
+    from dualsphysics_multilayer_amd.core import SphSlabGroup, case_derive, slab_partition
+
+    case = DamBreakCase(0.03, cellmode=2)
+    ncx = case_derive(case.case_def())["dom_cells"][0]
+    b = slab_partition(case, ncx // 2)
+    assert (np.diff(b) >= 2).all() and b[-1] == ncx
+    with pytest.raises(Exception):
+        SphSlabGroup(case, np.array([0, 1, ncx], np.int32))
