@@ -53,13 +53,28 @@ constexpr int TMAXCELLS = 4;   // max x-cells per item (CellMode=full: cells of 
 #define SPH_TMAXCELLS_HALF 32
 #endif
 constexpr int TMAXCELLS_HALF = SPH_TMAXCELLS_HALF;
+#ifndef SPH_TEST32
+#define SPH_TEST32 1  // candidate tests in groups of 32 through VCC + v_addc (test32); 0: 8-bit groups
+#endif
 
 // Candidate test of one window of n (<= 64) staged records -> one 64-bit mask (as
 // test128; used for the short 5-cell windows of CellMode=half).
+__device__ __forceinline__ unsigned test32(const float4* __restrict__ b, float px2, float py2, float pz2,
+                                           float thr);
 __device__ __forceinline__ unsigned long long test64(const float4* __restrict__ sA, int s0, int n, float px2,
                                                      float py2, float pz2, float thr) {
   unsigned long long m = 0ull;
   const float4* __restrict__ b = sA + s0;
+#if SPH_TEST32
+  unsigned w[2] = {0u, 0u};
+#pragma unroll
+  for (int g = 0; g < 2; g++) {
+    const int left = n - g * 32;
+    if (left <= 0) break;
+    w[g] = test32(b + g * 32, px2, py2, pz2, thr) & (left >= 32 ? ~0u : ((1u << left) - 1u));
+  }
+  return (static_cast<unsigned long long>(w[1]) << 32) | w[0];
+#endif
   for (int jo = 0; jo < 8; jo++) {
     const int left = n - jo * 8;
     if (left <= 0) break;
@@ -89,11 +104,41 @@ constexpr unsigned ITEM_BOUND = 0x80000000u;  // flag in item.x: p1 are boundary
 // relative); the body recomputes |p-A|^2 exactly and applies the reference's test, so no
 // pair is lost or added.  sA is padded past TCAP, so the 8-wide groups may over-read;
 // those bits are masked off.  n <= 0 gives empty masks.
+// 32 candidates b[0..31] -> bits (bit k = candidate k): the compare lands in VCC and
+// v_addc_co_u32 shifts it in (bits = 2 bits + vcc), two VALU per candidate besides the 3
+// FMAs instead of compare + select + or and the 8-bit group assembly.  Candidates in
+// descending order so candidate k ends at bit k.  (VCC only: no memory access.)
+__device__ __forceinline__ unsigned test32(const float4* __restrict__ b, float px2, float py2, float pz2,
+                                           float thr) {
+  unsigned bits = 0u;
+#pragma unroll 8
+  for (int ji = 31; ji >= 0; ji--) {
+    const float4 A = b[ji];
+    const float q = fmaf(px2, A.x, fmaf(py2, A.y, fmaf(pz2, A.z, A.w)));
+    asm("v_cmp_ge_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc" : "+v"(bits) : "v"(thr), "v"(q) : "vcc");
+  }
+  return bits;
+}
+
 __device__ __forceinline__ void test128(const float4* __restrict__ sA, int s0, int n, float px2, float py2,
                                         float pz2, float thr, unsigned long long& m0, unsigned long long& m1) {
   m0 = 0ull;
   m1 = 0ull;
   const float4* __restrict__ b = sA + s0;
+#if SPH_TEST32
+  // groups of 32 (a group past the window's end reads beyond the staged records: LDS of
+  // this block or out of range, read as 0; its bits are masked off)
+  unsigned w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int g = 0; g < 4; g++) {
+    const int left = n - g * 32;
+    if (left <= 0) break;
+    w[g] = test32(b + g * 32, px2, py2, pz2, thr) & (left >= 32 ? ~0u : ((1u << left) - 1u));
+  }
+  m0 = (static_cast<unsigned long long>(w[1]) << 32) | w[0];
+  m1 = (static_cast<unsigned long long>(w[3]) << 32) | w[2];
+  return;
+#endif
   for (int jo = 0; jo < 16; jo++) {
     const int left = n - jo * 8;
     if (left <= 0) break;
