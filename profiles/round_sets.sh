@@ -5,6 +5,11 @@ set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 T=${1:?round tag}
 shift || true
+# heartbeat: the reference CPU baseline of a 10M case runs minutes without output
+mkdir -p "$R/gpurun_out"
+( while sleep 50; do date >> "$R/gpurun_out/heartbeat.log"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 for c in ${*:-cfg2 cfg5 cfg3 cfg4}; do
   case $c in
     cfg2) bash "$R/profiles/collect.sh" "$T" --steps 20 --warmup 3 ;;
