@@ -78,6 +78,7 @@ struct KConst {
   float shiftmaxdist;   // float(Dp*0.1)
   float shiftcoef;      // ShiftCoef
   double coeftfs;       // (Simulate2D ? 2 : 3) - ShiftTFS
+  int nnbi;             // NN: some phase has a bi-viscosity region (tau_max != 0)
 };
 
 // NN phase constants on the device, two float4 per phase (sph_nn.hip loads them to LDS):

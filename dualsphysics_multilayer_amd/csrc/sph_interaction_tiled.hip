@@ -375,6 +375,15 @@ __device__ __forceinline__ void tile_unit4(const KConst& K, const P1& p, float t
 
 // Drain of one round of accepted candidates: four 64-bit words c0..c3 of staged records
 // from bases b0..b3 (see tile_unit).
+// Records addressed by byte offset j16 = 16 j of their index j.
+__device__ __forceinline__ const float4* at16(const float4* __restrict__ base, int j16) {
+  return reinterpret_cast<const float4*>(reinterpret_cast<const char*>(base) + j16);
+}
+__device__ __forceinline__ float2 at_rec(const float2* __restrict__ base, int j16) {
+  return *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(base) + (j16 >> 1));
+}
+__device__ __forceinline__ float4 at_rec(const float4* __restrict__ base, int j16) { return *at16(base, j16); }
+
 template <int TDENSITY, int MODE, bool FT>
 __device__ __forceinline__ void drain_words(const KConst& K, const P1& p, unsigned long long c0,
                                             unsigned long long c1, unsigned long long c2, unsigned long long c3,
@@ -405,8 +414,14 @@ __device__ __forceinline__ void drain_words(const KConst& K, const P1& p, unsign
       b2 = e0 ? b3 : b2;
       c3 = e0 ? 0ull : c3;
     }
+    // bases in bytes of a 16-B record (j16 = 16 j): one shift-add per pop gives the sA/sB
+    // address, a shift right the 8-B sC one
+    b0 <<= 4;
+    b1 <<= 4;
+    b2 <<= 4;
+    b3 <<= 4;
     auto pop = [&](void) -> int {
-      const int j = b0 + int(__builtin_ctzll(c0 | (1ull << 63)));
+      const int j = b0 + (int(__builtin_ctzll(c0 | (1ull << 63))) << 4);
       c0 &= c0 - 1ull;
       const bool e = c0 == 0ull;
       c0 = e ? c1 : c0;
@@ -423,9 +438,9 @@ __device__ __forceinline__ void drain_words(const KConst& K, const P1& p, unsign
       const bool two = c0 != 0ull;
       const int j2p = pop();
       const int j2 = two ? j2p : j1;
-      const float4 A1 = sA[j1], A2 = sA[j2];
-      const float4 B1 = sB[j1], B2 = sB[j2];
-      const typename CRecT<FT>::type C1 = sC[j1], C2 = sC[j2];
+      const float4 A1 = *at16(sA, j1), A2 = *at16(sA, j2);
+      const float4 B1 = *at16(sB, j1), B2 = *at16(sB, j2);
+      const typename CRecT<FT>::type C1 = at_rec(sC, j1), C2 = at_rec(sC, j2);
       const float drx1 = p.x - A1.x, dry1 = p.y - A1.y, drz1 = p.z - A1.z;
       const float drx2 = p.x - A2.x, dry2 = p.y - A2.y, drz2 = p.z - A2.z;
       const float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
@@ -435,6 +450,7 @@ __device__ __forceinline__ void drain_words(const KConst& K, const P1& p, unsign
       const bool ok1 = rr21 <= K.kernelsize2, ok2 = rr22m <= K.kernelsize2;
       pair_body<TDENSITY, MODE, FT>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, Q, a);
       pair_body<TDENSITY, MODE, FT>(K, p, drx2, dry2, drz2, rr22m, ok2, B2, C2, Q, a);
+      keep_w(A1, A2);  // 16-B reads (ds_read_b128) for the position records, see keep_w
     }
   }
 }

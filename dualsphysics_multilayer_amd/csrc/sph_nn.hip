@@ -39,6 +39,12 @@ namespace sphx {
 #ifndef SPH_NN_ONEPAIR
 #define SPH_NN_ONEPAIR 1  // one pair per drain iteration: no VGPR spill, 1.3% faster on cfg5 than two
 #endif
+#ifndef SPH_NN_GRAD12
+#define SPH_NN_GRAD12 0  // FDA velocity gradient as (dv_i / r^2) dr_j (12 products, not 18)
+#endif
+#ifndef SPH_NN_RSQ
+#define SPH_NN_RSQ 1  // FDA pairs: r and 1/r^2 from one v_rsq (0: v_sqrt + v_rcp)
+#endif
 #ifndef SPH_NN_TCAP
 #define SPH_NN_TCAP 480
 #endif
@@ -90,18 +96,14 @@ struct NNP1 {
   float taumax, bimulti;  // bi-viscosity constants of p1's phase
 };
 
-// GetEta_Effective (JSphCpu_Tensors.cpp:84-108): Herschel-Bulkley-Papanastasiou effective
-// viscosity with the optional bi-viscosity region of p1's phase (tau_max, Bi_multi).
-__device__ __forceinline__ float nn_eta(float dmag, float tau_yield, float visco, float m, float n, float taumax1,
-                                        float bimulti1) {
+// GetEta_Effective (JSphCpu_Tensors.cpp:116-142): Herschel-Bulkley-Papanastasiou effective
+// viscosity with the optional bi-viscosity region of p1's phase (tau_max, Bi_multi).  `bi`
+// (K.nnbi, uniform over the launch): some phase has tau_max != 0; without one the
+// bi-viscosity terms drop out (tau_max 0 selects tau_yield and no bi region), so that
+// branch computes the same values with fewer operations.
+__device__ __forceinline__ float nn_eta(bool bi, float dmag, float tau_yield, float visco, float m, float n,
+                                        float taumax1, float bimulti1) {
   if (dmag <= ALMOSTZERO) dmag = ALMOSTZERO;
-  float miou_yield = (taumax1 != 0.f ? taumax1 : tau_yield) * frcp(2.f * dmag);
-  // dmag <= taumax1 / (2 bimulti1 visco), without a second reciprocal (all factors > 0)
-  const bool bi_region = taumax1 != 0.f && dmag * (2.f * bimulti1 * visco) <= taumax1;
-  if (bi_region) miou_yield = bimulti1 * visco;
-  const float miou_pap = miou_yield * (1.f - fexp2(-m * dmag * 1.4426950408889634f));  // exp(-m D)
-  const bool cap = (miou_pap > m * tau_yield || dmag == ALMOSTZERO);
-  const float term1 = (taumax1 != 0.f ? miou_yield : (cap ? m * tau_yield : miou_pap));
   // visco * D^(n-1), exactly visco for n = 1 (skipped when no lane of the wave needs the power)
   float miou_hb = visco;
 #if SPH_NN_POWSKIP
@@ -109,6 +111,19 @@ __device__ __forceinline__ float nn_eta(float dmag, float tau_yield, float visco
 #else
   miou_hb = visco * fexp2((n - 1.f) * flog2(dmag));
 #endif
+  const float e = 1.f - fexp2(-m * dmag * 1.4426950408889634f);  // 1 - exp(-m D)
+  if (!bi) {
+    const float miou_pap = tau_yield * frcp(2.f * dmag) * e;
+    const bool cap = (miou_pap > m * tau_yield || dmag == ALMOSTZERO);
+    return (cap ? m * tau_yield : miou_pap) + (cap ? visco : miou_hb);
+  }
+  float miou_yield = (taumax1 != 0.f ? taumax1 : tau_yield) * frcp(2.f * dmag);
+  // dmag <= taumax1 / (2 bimulti1 visco), without a second reciprocal (all factors > 0)
+  const bool bi_region = taumax1 != 0.f && dmag * (2.f * bimulti1 * visco) <= taumax1;
+  if (bi_region) miou_yield = bimulti1 * visco;
+  const float miou_pap = miou_yield * e;
+  const bool cap = (miou_pap > m * tau_yield || dmag == ALMOSTZERO);
+  const float term1 = (taumax1 != 0.f ? miou_yield : (cap ? m * tau_yield : miou_pap));
   const float term2 = (bi_region ? visco : (cap ? visco : miou_hb));
   return term1 + term2;
 }
@@ -145,8 +160,12 @@ template <int TVISCO, int TDENSITY, bool SHIFT, bool BOUNDP2, bool ORDERED = tru
 __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restrict__ sph, const NNP1& p, float drx,
                                         float dry, float drz, float rr2, bool ok, const float4& B, const float4& C,
                                         NNAcc& a) {
-  // kernel (Wendland fac = bwen q (1-q/2)^3 / r = (bwen/h) (1-q/2)^3), 0 beyond 2h
-  const float rad = fsqrt_(rr2);
+  // kernel (Wendland fac = bwen q (1-q/2)^3 / r = (bwen/h) (1-q/2)^3), 0 beyond 2h.  With the
+  // FDA gradient (which needs 1/r^2 too) one v_rsq gives both: r = r^2 rsq, 1/r^2 = rsq^2
+  // (one transcendental instead of v_sqrt + v_rcp; ulp-level differences)
+  constexpr bool FDA = (TVISCO == 2 || TVISCO == 3) && SPH_NN_RSQ;
+  const float rsq = FDA ? __builtin_amdgcn_rsqf(rr2) : 0.f;
+  const float rad = FDA ? rr2 * rsq : fsqrt_(rr2);
   const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
   const float fac = K.bwenovh * (wq * wq * wq);
   const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
@@ -248,10 +267,17 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     // reference's operation order: the effective viscosity divides by the invariant, whose
     // explicit form cancels, so its rounding is part of the result (a closed form of the
     // rank-one gradient's invariant moved step-1 velocities 30x past the noise floor)
-    const float irr2 = frcp(rr2);
+    const float irr2 = FDA ? rsq * rsq : frcp(rr2);
+#if SPH_NN_GRAD12  // (dv_i / r^2) dr_j: 12 products instead of 18, rounding-level differences
+    const float tx = dvx * irr2, ty = dvy * irr2, tz = dvz * irr2;
+    const float a11 = tx * drx, a12 = tx * dry, a13 = tx * drz;
+    const float a21 = ty * drx, a22 = ty * dry, a23 = ty * drz;
+    const float a31 = tz * drx, a32 = tz * dry, a33 = tz * drz;
+#else
     const float a11 = dvx * drx * irr2, a12 = dvx * dry * irr2, a13 = dvx * drz * irr2;
     const float a21 = dvy * drx * irr2, a22 = dvy * dry * irr2, a23 = dvy * drz * irr2;
     const float a31 = dvz * drx * irr2, a32 = dvz * dry * irr2, a33 = dvz * drz * irr2;
+#endif
     const float div_vel = (a11 + a22 + a33) * (1.f / 3.f);
     const float d11 = a11 - div_vel, d22 = a22 - div_vel, d33 = a33 - div_vel;
     const float d12 = 0.5f * (a12 + a21), d13 = 0.5f * (a13 + a31), d23 = 0.5f * (a23 + a32);
@@ -260,7 +286,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     const float ii_d = ii1 - ii2;
     const float dmag = fabsf(ii_d);  // sqrt(II_D * II_D)
     const float4 ph2b = sph[2 * pp2 + 1];
-    const float eta = nn_eta(dmag, ph2.w, visco_nn, ph2b.x, ph2b.y, p.taumax, p.bimulti);
+    const float eta = nn_eta(K.nnbi != 0, dmag, ph2.w, visco_nn, ph2b.x, ph2b.y, p.taumax, p.bimulti);
     a.visceta = fmaxf(ok ? eta : 0.f, a.visceta);
     if constexpr (TVISCO == 2) {  // Morris operator
       const float temp = 2.f * eta * (inv_re * inv_rho2);
@@ -812,7 +838,7 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
           float d[6];
           const float dmag = nn_strain_rate(gxx, gxy, gxz, gyy, gyz, gzz, d);
           const float4 pa = sph[2 * p.ph], pb = sph[2 * p.ph + 1];
-          const float eta = nn_eta(dmag, pa.w, pa.z, pb.x, pb.y, p.taumax, p.bimulti);
+          const float eta = nn_eta(K.nnbi != 0, dmag, pa.w, pa.z, pb.x, pb.y, p.taumax, p.bimulti);
           viscoeta[p1] = eta;
           etamax = fmaxf(etamax, eta);
           if (K.nntvisco == 3) {

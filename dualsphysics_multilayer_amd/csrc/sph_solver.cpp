@@ -466,6 +466,7 @@ void SphGpuSingle::UploadPhases(const SphCaseDef& cdef) {
     const SphPhaseDef& ph = cdef.phases[p];
     tab[2 * p] = make_float4(C.phase_mass[p], float(ph.cs0), float(ph.visco), float(ph.tau_yield));
     tab[2 * p + 1] = make_float4(float(ph.hbp_m), float(ph.hbp_n), float(ph.tau_max), float(ph.bi_multi));
+    if (float(ph.tau_max) != 0.f) K.nnbi = 1;  // the pair bodies take the bi-viscosity branch
     const float gam = float(ph.gamma) ? float(ph.gamma) : C.gamma;
     const int ig = (gam == float(int(gam)) && gam >= 1.f && gam <= 16.f) ? int(gam) : 0;
     eos[p] = make_float4(float(ph.rho), C.phase_cteb[p], gam, float(ig));
