@@ -40,7 +40,7 @@ namespace sphx {
 #define SPH_NN_ONEPAIR 1  // one pair per drain iteration: no VGPR spill, 1.3% faster on cfg5 than two
 #endif
 #ifndef SPH_NN_GRAD12
-#define SPH_NN_GRAD12 0  // FDA velocity gradient as (dv_i / r^2) dr_j (12 products, not 18)
+#define SPH_NN_GRAD12 1  // FDA velocity gradient as (dv_i / r^2) dr_j (12 products, not 18; cfg5 -1.5 %)
 #endif
 #ifndef SPH_NN_RSQ
 #define SPH_NN_RSQ 1  // FDA pairs: r and 1/r^2 from one v_rsq (0: v_sqrt + v_rcp)
@@ -191,12 +191,15 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   const float dot3 = fac * rr2;  // drx*frx+dry*fry+drz*frz
   const float inv_re = frcp(rr2 + K.eta2);
   // density diffusion, only between particles of the same phase (JSphCpu_NN_FDA.cpp:181-199)
-  if (TDENSITY == 1 && a.delta != FLT_MAX) {
+  // (branch-free: once the sum is FLT_MAX it stays FLT_MAX, since FLT_MAX +- a finite
+  // pair term rounds back to FLT_MAX; a per-lane `if (a.delta != FLT_MAX)` costs exec-mask
+  // branches in every pair)
+  if (TDENSITY == 1) {
     const float visc_densi = K.ddtkh * cbar * (rhop1over2 - 1.f) * inv_re;
     const float delta = (p.ph == pp2 ? visc_densi * dot3 * massp2 : 0.f);
     a.delta = (BOUNDP2 && !K.mdbc && ok) ? FLT_MAX : a.delta + delta;
   }
-  if ((TDENSITY == 2 || (TDENSITY == 3 && !BOUNDP2)) && a.delta != FLT_MAX) {
+  if (TDENSITY == 2 || (TDENSITY == 3 && !BOUNDP2)) {
     // rho0 (1 + ddtgz drz)^(1/gamma) - rho0 as the reference evaluates it in float: the
     // three-term series of k_fluid_tiled (exact to 2e-6 of the term) removes the float
     // cancellation of the reference, which the NN parity bar (10x the reference's own
@@ -208,7 +211,8 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     a.delta = (BOUNDP2 && ok) ? FLT_MAX : a.delta - delta;
   }
   // multiphase shifting (JSphCpu_NN_FDA.cpp:202-209): a heavier-phase neighbour resets x
-  if (SHIFT && a.sx != FLT_MAX) {
+  // (ORDERED: a no-shift pair sets sx = FLT_MAX and every later pair leaves the sums alone)
+  if (SHIFT && (!ORDERED || a.sx != FLT_MAX)) {
     const bool heavy = ok && !BOUNDP2 && (p.mph > ph2.x) && p.ph != pp2;
     const float massrhop = massp2 * inv_rho2;
     const bool noshift = ok && BOUNDP2 && (K.shiftmode == 1 || (K.shiftmode == 2 && C.y != 0.f));
