@@ -147,6 +147,13 @@ __device__ __forceinline__ float nn_strain_rate(float gxx, float gxy, float gxz,
   return sqrtf(fmaxf(-ii1 + ii2, 0.f));
 }
 
+// Maximum of a running maximum m >= 0 and x, as one integer max of the bit patterns
+// (non-negative floats order like their bits; a negative x loses to m; a NaN x with the
+// sign clear sticks): fmaxf costs two v_max here, the first canonicalising its input.
+__device__ __forceinline__ float max_nonneg(float x, float m) {
+  return __int_as_float(max(__float_as_int(x), __float_as_int(m)));
+}
+
 // One pair of the fluid p1 (InteractionForcesFluid_NN_FDA_All, JSphCpu_NN_FDA.cpp:141-275).
 // BOUNDP2: p2 is a boundary particle (mass MassBound, phase = p1's phase).
 // `ok`: the reference's pair test (rr2 <= KernelSize2 and rr2 >= ALMOSTZERO).  A pair that
@@ -174,10 +181,12 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   const float massp2 = BOUNDP2 ? K.massbound : ph2.x;
   const float rho1 = p.vr.w, rho2 = B.w;
   const float inv_rho2 = C.z;  // staged 1/rho2
-  // momentum (pressure)
+  // m2/rho2: every per-pair use of 1/rho2 below comes with the mass of p2 (the reference's
+  // products re-associated, rounding-level differences)
+  const float massrhop = massp2 * inv_rho2;
+  // momentum (pressure): -(p1 + p2)/(rho1 rho2) m2
   {
-    const float prs = (p.press + C.x) * (p.inv_rho * inv_rho2);
-    const float p_vpm = -prs * massp2;
+    const float p_vpm = (p.press + C.x) * (p.inv_rho * -massrhop);
     a.ax = fmaf(p_vpm, frx, a.ax);
     a.ay = fmaf(p_vpm, fry, a.ay);
     a.az = fmaf(p_vpm, frz, a.az);
@@ -186,7 +195,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   const float rhop1over2 = rho1 * inv_rho2;
   float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
   const float dot = drx * dvx + dry * dvy + drz * dvz;  // dv.fr = fac (dr.dv)
-  a.ar = fmaf(massp2 * (fac * dot), rhop1over2, a.ar);
+  a.ar = fmaf(fac * dot, rho1 * massrhop, a.ar);  // m2 fac (dr.dv) rho1/rho2
   const float cbar = ph2.y;  // max(Cs0[pp2], Cs0[pp2])
   const float dot3 = fac * rr2;  // drx*frx+dry*fry+drz*frz
   const float inv_re = frcp(rr2 + K.eta2);
@@ -207,28 +216,28 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     const float rh = 1.f + K.ddtgz * drz;
     const float drhop = K.rhopzero * fexp2(K.ovgamma * flog2(rh)) - K.rhopzero;
     const float visc_densi = K.ddtkh * cbar * ((rho2 - rho1) - drhop) * inv_re;
-    const float delta = (p.ph == pp2 ? visc_densi * dot3 * massp2 * inv_rho2 : 0.f);
+    const float delta = (p.ph == pp2 ? visc_densi * dot3 * massrhop : 0.f);
     a.delta = (BOUNDP2 && ok) ? FLT_MAX : a.delta - delta;
   }
   // multiphase shifting (JSphCpu_NN_FDA.cpp:202-209): a heavier-phase neighbour resets x
   // (ORDERED: a no-shift pair sets sx = FLT_MAX and every later pair leaves the sums alone)
   if (SHIFT && (!ORDERED || a.sx != FLT_MAX)) {
     const bool heavy = ok && !BOUNDP2 && (p.mph > ph2.x) && p.ph != pp2;
-    const float massrhop = massp2 * inv_rho2;
     const bool noshift = ok && BOUNDP2 && (K.shiftmode == 1 || (K.shiftmode == 2 && C.y != 0.f));
+    const float mr = heavy ? 0.f : massrhop;  // a heavier-phase pair adds nothing (fma by 0)
     if (ORDERED) {
-      a.sx = noshift ? FLT_MAX : (heavy ? 0.f : a.sx + massrhop * frx);
+      a.sx = noshift ? FLT_MAX : (heavy ? 0.f : fmaf(massrhop, frx, a.sx));
     } else {  // fluid p2 only (noshift needs a bound p2)
-      a.sx += heavy ? 0.f : massrhop * frx;
-      a.hv |= heavy;
+      a.sx = fmaf(mr, frx, a.sx);
+      a.hv = heavy ? true : a.hv;
     }
-    a.sy += heavy ? 0.f : massrhop * fry;
-    a.sz += heavy ? 0.f : massrhop * frz;
-    a.sw -= heavy ? 0.f : massrhop * dot3;
+    a.sy = fmaf(mr, fry, a.sy);
+    a.sz = fmaf(mr, frz, a.sz);
+    a.sw = fmaf(-mr, dot3, a.sw);
   }
   // viscosity
   const float dot_rr2 = dot * inv_re;
-  a.visc = fmaxf(ok ? dot_rr2 : 0.f, a.visc);
+  a.visc = max_nonneg(ok ? dot_rr2 : 0.f, a.visc);
   const float visco_nn = ph2.z;
   if (TVISCO == 1) {  // artificial
     if (dot < 0.f) {
@@ -248,7 +257,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
       dvy = 2.f * p.vr.y;
       dvz = 2.f * p.vr.z;
     }
-    const float volp2 = -massp2 * inv_rho2;
+    const float volp2 = -massrhop;
     float dv = dvx * volp2;
     a.gxx = fmaf(dv, frx, a.gxx);
     a.gxy = fmaf(dv, fry, a.gxy);
@@ -291,19 +300,18 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     const float dmag = fabsf(ii_d);  // sqrt(II_D * II_D)
     const float4 ph2b = sph[2 * pp2 + 1];
     const float eta = nn_eta(K.nnbi != 0, dmag, ph2.w, visco_nn, ph2b.x, ph2b.y, p.taumax, p.bimulti);
-    a.visceta = fmaxf(ok ? eta : 0.f, a.visceta);
-    if constexpr (TVISCO == 2) {  // Morris operator
-      const float temp = 2.f * eta * (inv_re * inv_rho2);
-      const float vtemp = massp2 * temp * dot3;
+    a.visceta = max_nonneg(ok ? eta : 0.f, a.visceta);
+    if constexpr (TVISCO == 2) {  // Morris operator: m2 2 eta dot3 / ((r^2+eta^2) rho2)
+      const float vtemp = (2.f * eta) * (inv_re * massrhop) * dot3;
       a.ax = fmaf(vtemp, dvx, a.ax);
       a.ay = fmaf(vtemp, dvy, a.ay);
       a.az = fmaf(vtemp, dvz, a.az);
     } else {  // GetStressTensor: tau = 2 eta D
       const float e2 = 2.f * eta;
       const float t11 = e2 * d11, t12 = e2 * d12, t13 = e2 * d13, t22 = e2 * d22, t23 = e2 * d23, t33 = e2 * d33;
-      a.ax = fmaf((t11 * frx + t12 * fry + t13 * frz) * inv_rho2, massp2, a.ax);
-      a.ay = fmaf((t12 * frx + t22 * fry + t23 * frz) * inv_rho2, massp2, a.ay);
-      a.az = fmaf((t13 * frx + t23 * fry + t33 * frz) * inv_rho2, massp2, a.az);
+      a.ax = fmaf(t11 * frx + t12 * fry + t13 * frz, massrhop, a.ax);
+      a.ay = fmaf(t12 * frx + t22 * fry + t23 * frz, massrhop, a.ay);
+      a.az = fmaf(t13 * frx + t23 * fry + t33 * frz, massrhop, a.az);
     }
   }
 }
@@ -488,6 +496,7 @@ __device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restr
     const float4 C1 = sC.ld(j1, KIND == 1);
     if (KIND == 2) nn_bound_pair(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
     else nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1, false>(K, sph, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
+    keep_w(A1, B1);  // 16-B LDS reads (sph_tiled.hpp)
   }
 #else
   while (c0) {
