@@ -46,7 +46,7 @@ namespace sphx {
 #define SPH_NN_RSQ 1  // FDA pairs: r and 1/r^2 from one v_rsq (0: v_sqrt + v_rcp)
 #endif
 #ifndef SPH_NN_TCAP
-#define SPH_NN_TCAP 480
+#define SPH_NN_TCAP 476  // 476 x 41 B + pad + the 3-row phase table: 20436 B (8 blocks/CU)
 #endif
 constexpr int NN_TCAP = SPH_NN_TCAP;
 
@@ -101,29 +101,31 @@ struct NNP1 {
 // (K.nnbi, uniform over the launch): some phase has tau_max != 0; without one the
 // bi-viscosity terms drop out (tau_max 0 selects tau_yield and no bi region), so that
 // branch computes the same values with fewer operations.
-__device__ __forceinline__ float nn_eta(bool bi, float dmag, float tau_yield, float visco, float m, float n,
+__device__ __forceinline__ float nn_eta(bool bi, float dmag, float tau_yield, float visco, const float4& c,
                                         float taumax1, float bimulti1) {
+  // c: the phase's {m tau_yield, -m log2(e), n - 1, .} (the solver's third table row)
+  const float mtau = c.x;
   if (dmag <= ALMOSTZERO) dmag = ALMOSTZERO;
   // visco * D^(n-1), exactly visco for n = 1 (skipped when no lane of the wave needs the power)
   float miou_hb = visco;
 #if SPH_NN_POWSKIP
-  if (__ballot(n != 1.f)) miou_hb = (n != 1.f) ? visco * fexp2((n - 1.f) * flog2(dmag)) : visco;
+  if (__ballot(c.z != 0.f)) miou_hb = (c.z != 0.f) ? visco * fexp2(c.z * flog2(dmag)) : visco;
 #else
-  miou_hb = visco * fexp2((n - 1.f) * flog2(dmag));
+  miou_hb = visco * fexp2(c.z * flog2(dmag));
 #endif
-  const float e = 1.f - fexp2(-m * dmag * 1.4426950408889634f);  // 1 - exp(-m D)
+  const float e = 1.f - fexp2(c.y * dmag);  // 1 - exp(-m D)
   if (!bi) {
     const float miou_pap = tau_yield * frcp(2.f * dmag) * e;
-    const bool cap = (miou_pap > m * tau_yield || dmag == ALMOSTZERO);
-    return (cap ? m * tau_yield : miou_pap) + (cap ? visco : miou_hb);
+    const bool cap = (miou_pap > mtau || dmag == ALMOSTZERO);
+    return (cap ? mtau : miou_pap) + (cap ? visco : miou_hb);
   }
   float miou_yield = (taumax1 != 0.f ? taumax1 : tau_yield) * frcp(2.f * dmag);
   // dmag <= taumax1 / (2 bimulti1 visco), without a second reciprocal (all factors > 0)
   const bool bi_region = taumax1 != 0.f && dmag * (2.f * bimulti1 * visco) <= taumax1;
   if (bi_region) miou_yield = bimulti1 * visco;
   const float miou_pap = miou_yield * e;
-  const bool cap = (miou_pap > m * tau_yield || dmag == ALMOSTZERO);
-  const float term1 = (taumax1 != 0.f ? miou_yield : (cap ? m * tau_yield : miou_pap));
+  const bool cap = (miou_pap > mtau || dmag == ALMOSTZERO);
+  const float term1 = (taumax1 != 0.f ? miou_yield : (cap ? mtau : miou_pap));
   const float term2 = (bi_region ? visco : (cap ? visco : miou_hb));
   return term1 + term2;
 }
@@ -157,9 +159,10 @@ __device__ __forceinline__ float max_nonneg(float x, float m) {
 // One pair of the fluid p1 (InteractionForcesFluid_NN_FDA_All, JSphCpu_NN_FDA.cpp:141-275).
 // BOUNDP2: p2 is a boundary particle (mass MassBound, phase = p1's phase).
 // `ok`: the reference's pair test (rr2 <= KernelSize2 and rr2 >= ALMOSTZERO).  A pair that
-// fails it comes in with dr = 0 and rr2 = 1e30: its kernel factor is 0, so every sum gets
-// +0, and the maxima, the DDT/shifting switches and the shifting reset are masked by ok —
-// branch-free, so two pairs can be interleaved.
+// fails it comes in with rr2 = 1e30 (its dr unchanged): its kernel factor is 0, so fr and
+// dot3 = fac r^2 are 0 and every sum gets +0 (each term carries fr or dot3; the FDA terms are
+// finite with 1/r^2 = 1e-30), and the maxima, the DDT/shifting switches and the shifting
+// reset are masked by ok — branch-free, so two pairs can be interleaved.
 // ORDERED: pairs arrive in the reference's order (the shifting x sum is reset by a
 // heavier-phase p2); else in mirrored-unit order: sx skips the heavy pair and a.hv records
 // it, and the caller recomputes sx in the reference order (nn_sx_sweep) when any lane saw one.
@@ -178,6 +181,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
   const int pp2 = BOUNDP2 ? p.ph : int(__float_as_uint(C.y));
   const float4 ph2 = sph[2 * pp2];
+  const float4 ph2c = sph[2 * SPH_MAXPHASES + pp2];  // {m tau_yield, -m log2 e, n - 1, DDTkh cs0}
   const float massp2 = BOUNDP2 ? K.massbound : ph2.x;
   const float rho1 = p.vr.w, rho2 = B.w;
   const float inv_rho2 = C.z;  // staged 1/rho2
@@ -204,7 +208,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   // pair term rounds back to FLT_MAX; a per-lane `if (a.delta != FLT_MAX)` costs exec-mask
   // branches in every pair)
   if (TDENSITY == 1) {
-    const float visc_densi = K.ddtkh * cbar * (rhop1over2 - 1.f) * inv_re;
+    const float visc_densi = ph2c.w * (rhop1over2 - 1.f) * inv_re;  // DDTkh cbar (...) / (r^2+eta^2)
     const float delta = (p.ph == pp2 ? visc_densi * dot3 * massp2 : 0.f);
     a.delta = (BOUNDP2 && !K.mdbc && ok) ? FLT_MAX : a.delta + delta;
   }
@@ -215,14 +219,15 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     // rounding floor) does not absorb: step-1 velocities moved 5.7e-7 against 2e-8
     const float rh = 1.f + K.ddtgz * drz;
     const float drhop = K.rhopzero * fexp2(K.ovgamma * flog2(rh)) - K.rhopzero;
-    const float visc_densi = K.ddtkh * cbar * ((rho2 - rho1) - drhop) * inv_re;
+    const float visc_densi = ph2c.w * ((rho2 - rho1) - drhop) * inv_re;
     const float delta = (p.ph == pp2 ? visc_densi * dot3 * massrhop : 0.f);
     a.delta = (BOUNDP2 && ok) ? FLT_MAX : a.delta - delta;
   }
   // multiphase shifting (JSphCpu_NN_FDA.cpp:202-209): a heavier-phase neighbour resets x
   // (ORDERED: a no-shift pair sets sx = FLT_MAX and every later pair leaves the sums alone)
   if (SHIFT && (!ORDERED || a.sx != FLT_MAX)) {
-    const bool heavy = ok && !BOUNDP2 && (p.mph > ph2.x) && p.ph != pp2;
+    // (a heavier p1 phase differs from p2's: the phase test of the reference is implied)
+    const bool heavy = ok && !BOUNDP2 && (p.mph > ph2.x);
     const bool noshift = ok && BOUNDP2 && (K.shiftmode == 1 || (K.shiftmode == 2 && C.y != 0.f));
     const float mr = heavy ? 0.f : massrhop;  // a heavier-phase pair adds nothing (fma by 0)
     if (ORDERED) {
@@ -293,13 +298,13 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
 #endif
     const float div_vel = (a11 + a22 + a33) * (1.f / 3.f);
     const float d11 = a11 - div_vel, d22 = a22 - div_vel, d33 = a33 - div_vel;
-    const float d12 = 0.5f * (a12 + a21), d13 = 0.5f * (a13 + a31), d23 = 0.5f * (a23 + a32);
+    const float s12 = a12 + a21, s13 = a13 + a31, s23 = a23 + a32;  // 2 d12, 2 d13, 2 d23
     const float ii1 = d11 * d22 + d22 * d33 + d11 * d33;
-    const float ii2 = d12 * d12 + d23 * d23 + d13 * d13;
+    // d_ij^2 = s_ij^2 / 4 exactly (powers of two scale without rounding)
+    const float ii2 = 0.25f * (s12 * s12 + s23 * s23 + s13 * s13);
     const float ii_d = ii1 - ii2;
     const float dmag = fabsf(ii_d);  // sqrt(II_D * II_D)
-    const float4 ph2b = sph[2 * pp2 + 1];
-    const float eta = nn_eta(K.nnbi != 0, dmag, ph2.w, visco_nn, ph2b.x, ph2b.y, p.taumax, p.bimulti);
+    const float eta = nn_eta(K.nnbi != 0, dmag, ph2.w, visco_nn, ph2c, p.taumax, p.bimulti);
     a.visceta = max_nonneg(ok ? eta : 0.f, a.visceta);
     if constexpr (TVISCO == 2) {  // Morris operator: m2 2 eta dot3 / ((r^2+eta^2) rho2)
       const float vtemp = (2.f * eta) * (inv_re * massrhop) * dot3;
@@ -308,6 +313,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
       a.az = fmaf(vtemp, dvz, a.az);
     } else {  // GetStressTensor: tau = 2 eta D
       const float e2 = 2.f * eta;
+      const float d12 = 0.5f * s12, d13 = 0.5f * s13, d23 = 0.5f * s23;
       const float t11 = e2 * d11, t12 = e2 * d12, t13 = e2 * d13, t22 = e2 * d22, t23 = e2 * d23, t33 = e2 * d33;
       a.ax = fmaf(t11 * frx + t12 * fry + t13 * frz, massrhop, a.ax);
       a.ay = fmaf(t12 * frx + t22 * fry + t23 * frz, massrhop, a.ay);
@@ -414,14 +420,8 @@ __device__ __forceinline__ void nn_pass(const KConst& K, const DivGrid& g, const
             float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
             const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
             const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
-            // a pair outside the test: dr = 0 and rr2 = 1e30 (kernel factor 0, finite terms)
-            drx1 = ok1 ? drx1 : 0.f;
-            dry1 = ok1 ? dry1 : 0.f;
-            drz1 = ok1 ? drz1 : 0.f;
+            // a pair outside the test: rr2 = 1e30 (kernel factor 0, finite terms)
             rr21 = ok1 ? rr21 : 1e30f;
-            drx2 = ok2 ? drx2 : 0.f;
-            dry2 = ok2 ? dry2 : 0.f;
-            drz2 = ok2 ? drz2 : 0.f;
             rr22 = ok2 ? rr22 : 1e30f;
             const float4 C1 = sC.ld(j1, KIND == 1), C2 = sC.ld(j2, KIND == 1);
             if (KIND == 2) {
@@ -489,9 +489,6 @@ __device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restr
     float drx1 = p.x - A1.x, dry1 = p.y - A1.y, drz1 = p.z - A1.z;
     float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
     const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
-    drx1 = ok1 ? drx1 : 0.f;
-    dry1 = ok1 ? dry1 : 0.f;
-    drz1 = ok1 ? drz1 : 0.f;
     rr21 = ok1 ? rr21 : 1e30f;
     const float4 C1 = sC.ld(j1, KIND == 1);
     if (KIND == 2) nn_bound_pair(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
@@ -512,13 +509,7 @@ __device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restr
     float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
     const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
     const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
-    drx1 = ok1 ? drx1 : 0.f;
-    dry1 = ok1 ? dry1 : 0.f;
-    drz1 = ok1 ? drz1 : 0.f;
     rr21 = ok1 ? rr21 : 1e30f;
-    drx2 = ok2 ? drx2 : 0.f;
-    dry2 = ok2 ? dry2 : 0.f;
-    drz2 = ok2 ? drz2 : 0.f;
     rr22 = ok2 ? rr22 : 1e30f;
     const float4 C1 = sC.ld(j1, KIND == 1), C2 = sC.ld(j2, KIND == 1);
     if (KIND == 2) {
@@ -700,11 +691,11 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
   __shared__ float2 sC2[NN_TCAP];  // {press, 1/rho}
   __shared__ unsigned char sT[NN_TCAP];  // tag
   const NNSC sC = {sC2, sT};
-  __shared__ float4 sph[2 * SPH_MAXPHASES];
+  __shared__ float4 sph[3 * SPH_MAXPHASES];
   __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];
   __shared__ unsigned s_nwave[4];
-  if (threadIdx.x < 2 * SPH_MAXPHASES) sph[threadIdx.x] = phases[threadIdx.x];
+  if (threadIdx.x < 3 * SPH_MAXPHASES) sph[threadIdx.x] = phases[threadIdx.x];
   const ItemGroups IG(sc);
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f, etamax = 0.f;
@@ -850,8 +841,8 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
           const float gyy = f.gyy + b.gyy, gyz = f.gyz + b.gyz, gzz = f.gzz + b.gzz;
           float d[6];
           const float dmag = nn_strain_rate(gxx, gxy, gxz, gyy, gyz, gzz, d);
-          const float4 pa = sph[2 * p.ph], pb = sph[2 * p.ph + 1];
-          const float eta = nn_eta(K.nnbi != 0, dmag, pa.w, pa.z, pb.x, pb.y, p.taumax, p.bimulti);
+          const float4 pa = sph[2 * p.ph], pc = sph[2 * SPH_MAXPHASES + p.ph];
+          const float eta = nn_eta(K.nnbi != 0, dmag, pa.w, pa.z, pc, p.taumax, p.bimulti);
           viscoeta[p1] = eta;
           etamax = fmaxf(etamax, eta);
           if (K.nntvisco == 3) {

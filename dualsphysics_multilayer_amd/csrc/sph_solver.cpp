@@ -461,19 +461,25 @@ void SphGpuSingle::AllocFixed() {
 // NN phase tables (JSph::InitMultiPhase + ConfigConstantsMP): the interaction's constants
 // (sph_device.hpp layout) and the EOS of every phase for the divide's pressure.
 void SphGpuSingle::UploadPhases(const SphCaseDef& cdef) {
-  std::vector<float4> tab(2 * NN_MAXPH, make_float4(0.f, 0.f, 0.f, 0.f)), eos(NN_MAXPH, make_float4(1.f, 0.f, 1.f, 0.f));
+  // rows [0, 2 NN_MAXPH): {mass, cs0, visco, tau_yield}, {m, n, tau_max, bi_multi} per phase;
+  // rows [2 NN_MAXPH, 3 NN_MAXPH): per-phase products of the pair bodies, in float as the
+  // kernels formed them per pair: {m tau_yield, -m log2(e), n - 1, DDTkh cs0}
+  std::vector<float4> tab(3 * NN_MAXPH, make_float4(0.f, 0.f, 0.f, 0.f)), eos(NN_MAXPH, make_float4(1.f, 0.f, 1.f, 0.f));
   for (unsigned p = 0; p < C.nphases; p++) {
     const SphPhaseDef& ph = cdef.phases[p];
     tab[2 * p] = make_float4(C.phase_mass[p], float(ph.cs0), float(ph.visco), float(ph.tau_yield));
     tab[2 * p + 1] = make_float4(float(ph.hbp_m), float(ph.hbp_n), float(ph.tau_max), float(ph.bi_multi));
     if (float(ph.tau_max) != 0.f) K.nnbi = 1;  // the pair bodies take the bi-viscosity branch
+    const float m = float(ph.hbp_m);
+    tab[2 * NN_MAXPH + p] = make_float4(m * float(ph.tau_yield), -m * 1.4426950408889634f, float(ph.hbp_n) - 1.f,
+                                        K.ddtkh * float(ph.cs0));
     const float gam = float(ph.gamma) ? float(ph.gamma) : C.gamma;
     const int ig = (gam == float(int(gam)) && gam >= 1.f && gam <= 16.f) ? int(gam) : 0;
     eos[p] = make_float4(float(ph.rho), C.phase_cteb[p], gam, float(ig));
     phase_rho_[p] = float(ph.rho);
   }
   for (float4** dst : {&phasek_, &phaseeos_}) {
-    check_hip(hipMalloc((void**)dst, sizeof(float4) * 2 * NN_MAXPH), "hipMalloc phases");
+    check_hip(hipMalloc((void**)dst, sizeof(float4) * 3 * NN_MAXPH), "hipMalloc phases");
     allocs_.push_back(*dst);
   }
   check_hip(hipMemcpy(phasek_, tab.data(), sizeof(float4) * tab.size(), hipMemcpyHostToDevice), "upload phases");
