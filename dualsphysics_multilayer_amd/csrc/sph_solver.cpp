@@ -398,6 +398,7 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
     AllocFixed();
     if (nn_) UploadPhases(cdef);
     AllocParticles(cap_);
+    if (slab()) PresizeExchange(init);
     Upload(init, sel, nown);
     if (C.tboundary == SPH_BOUND_MDBC) UploadNormals(cdef, init);
     // ConfigDomain: RunCellDivide(true) (JSphCpuSingle.cpp:165-166), then InitRunGpu.
@@ -573,6 +574,35 @@ void SphGpuSingle::Free() {
   if (slabcnt_host_) (void)hipHostFree(slabcnt_host_);
   sc_host_ = nullptr;
   slabcnt_host_ = nullptr;
+}
+
+// Slab exchange buffers sized once from the case, from its densest x column: W face
+// columns of ghosts per face (+50 %), a quarter of that in migrants.  The face messages then
+// need no hipMalloc (and no stream synchronisation) mid-run; the grow paths of Exchange()
+// stay as the fallback for a flow that piles particles into a face column or a re-partition
+// that hands over many columns at once.
+void SphGpuSingle::PresizeExchange(const SphParticlesHost& h) {
+  std::vector<unsigned> cnt(size_t(C.dom_cells[0]) + 1, 0u);
+  unsigned mx = 0;
+  for (unsigned p = 0; p < h.n; p++) {
+    const double x = (h.pos[3 * p] - C.dom_posmin[0]) / double(C.scell);
+    if (!(x >= 0.0)) continue;
+    const size_t cx = size_t(x);
+    if (cx < cnt.size()) mx = std::max(mx, ++cnt[cx]);
+  }
+  const unsigned long long g = (unsigned long long)mx * C.scelldiv;
+  send_.gcap = g + g / 2 + 4096;
+  send_.mcap = g / 4 + 1024;
+  check_hip(hipMalloc(&sendgbuf_, 2 * sizeof(SlabGhost) * send_.gcap), "hipMalloc ghost send buffers");
+  send_.gl = (SlabGhost*)sendgbuf_;
+  send_.gr = send_.gl + send_.gcap;
+  check_hip(hipMalloc(&sendmbuf_, 2 * sizeof(SlabRec) * send_.mcap), "hipMalloc migrant send buffers");
+  send_.ml = (SlabRec*)sendmbuf_;
+  send_.mr = send_.ml + send_.mcap;
+  recvgcap_ = 2 * send_.gcap;
+  recvmcap_ = 2 * send_.mcap;
+  check_hip(hipMalloc((void**)&recvg_, sizeof(SlabGhost) * recvgcap_), "hipMalloc ghost receive buffer");
+  check_hip(hipMalloc((void**)&recvm_, sizeof(SlabRec) * recvmcap_), "hipMalloc migrant receive buffer");
 }
 
 // Slab capacity growth (a slab gains particles as the fluid moves across it): new

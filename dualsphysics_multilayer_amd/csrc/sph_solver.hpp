@@ -107,6 +107,7 @@ class SphGpuSingle {
   void FreeParticles();
   void Free();
   void Grow(unsigned np_live, unsigned newcap);
+  void PresizeExchange(const SphParticlesHost& h);
   void Upload(const SphParticlesHost& init, const std::vector<unsigned>& sel, unsigned nown);
   void UploadNormals(const SphCaseDef& cdef, const SphParticlesHost& init);
   void UploadPhases(const SphCaseDef& cdef);
