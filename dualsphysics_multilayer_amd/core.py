@@ -61,6 +61,7 @@ EXPORTED_SYMBOLS = (
     "sph_count_pairs",
     "sph_solver_set_time",
     "sph_solver_set_timing",
+    "sph_solver_set_timing_phases",
     "sph_solver_timing",
     "sph_slab_partition",
     "sph_comm_unique_id",
@@ -125,6 +126,7 @@ def load_library(path: str = LIB_PATH):
     L.sph_download_interaction.argtypes = [vp, C.POINTER(SphInterOut)]
     L.sph_count_pairs.argtypes = [vp, C.POINTER(C.c_uint64)]
     L.sph_solver_set_timing.argtypes = [vp, C.c_int]
+    L.sph_solver_set_timing_phases.argtypes = [vp, C.c_uint]
     L.sph_solver_set_time.argtypes = [vp, C.c_double, C.c_double]
     L.sph_solver_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
     L.sph_slab_partition.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.c_double, C.POINTER(C.c_int32)]
@@ -315,7 +317,9 @@ class SphGpuSingle:
         if head_path:
             write_part_head(head_path, hdr)
 
-    def set_timing(self, on: bool) -> None:
+    def set_timing(self, on: bool, phases: int = 0xF) -> None:
+        """Time the next steps' phases (bit i of `phases`: phase i of timing(); all by default)."""
+        _check(load_library().sph_solver_set_timing_phases(self._h, int(phases)))
         _check(load_library().sph_solver_set_timing(self._h, int(on)))
 
     def slab_info(self) -> dict:

@@ -181,6 +181,10 @@ int sph_solver_set_timing(SphSolver* s, int enabled) {
   NEED(s);
   return guard([&] { s->impl->SetTiming(enabled != 0); });
 }
+int sph_solver_set_timing_phases(SphSolver* s, unsigned mask) {
+  NEED(s);
+  return guard([&] { s->impl->SetTimingPhases(mask); });
+}
 int sph_solver_timing(SphSolver* s, double out_ms[4], uint64_t* launches) {
   NEED(s && out_ms);
   return guard([&] { s->impl->Timing(out_ms, launches); });

@@ -750,9 +750,14 @@ void SphGpuSingle::SetTiming(bool on) {
   timing_ = on;
   for (int i = 0; i < 4; i++) { phase_ms_[i] = 0; phase_n_[i] = 0; }
 }
+// Phases timed (bit i: phase i of phase_ms_; all by default).  Every event pair is a marker
+// in the stream, so a run timing only the interaction keeps the other launches back to back.
+void SphGpuSingle::SetTimingPhases(unsigned mask) {
+  Sync();
+  timing_mask_ = mask & 0xfu;
+}
 void SphGpuSingle::TimedBegin(int phase) {
-  (void)phase;
-  if (!timing_) return;
+  if (!timing_ || !((timing_mask_ >> phase) & 1u)) return;
   hipEvent_t a;
   if (!evpool_.empty()) { a = evpool_.back(); evpool_.pop_back(); }
   else check_hip(hipEventCreate(&a), "hipEventCreate");
@@ -760,7 +765,7 @@ void SphGpuSingle::TimedBegin(int phase) {
   cur_a_ = a;
 }
 void SphGpuSingle::TimedEnd(int phase) {
-  if (!timing_) return;
+  if (!timing_ || !((timing_mask_ >> phase) & 1u)) return;
   hipEvent_t b;
   if (!evpool_.empty()) { b = evpool_.back(); evpool_.pop_back(); }
   else check_hip(hipEventCreate(&b), "hipEventCreate");

@@ -78,6 +78,7 @@ class SphGpuSingle {
   void DownloadInteraction(SphInterOut& out);
   void CountPairs(uint64_t out[6]);
   void SetTiming(bool on);
+  void SetTimingPhases(unsigned mask);
   void SetTime(double time, double symdtpre);
   void Timing(double out_ms[4], uint64_t* launches);
   void CheckErrors();
@@ -216,6 +217,7 @@ class SphGpuSingle {
   void* sendmbuf_ = nullptr;
   // timing (hipEvents on the solver stream)
   bool timing_ = false;
+  unsigned timing_mask_ = 0xfu;  // phases timed (SetTiming, SPH_TIMING_PHASES)
   struct Ev { hipEvent_t a, b; int phase; };
   std::vector<Ev> pending_;
   std::vector<hipEvent_t> evpool_;

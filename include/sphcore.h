@@ -289,6 +289,12 @@ int sph_count_pairs(SphSolver* s, uint64_t out[6]);
  * VelrhopM1 = Velrhop and VerletStep = 0 hold from creation, as in the reference. */
 int sph_solver_set_time(SphSolver* s, double time, double symplectic_dtpre);
 int sph_solver_set_timing(SphSolver* s, int enabled);
+/* Which phases the timed region records (bit i = phase i of sph_solver_timing's out_ms;
+ * sph_solver_set_timing(s, 1) times all four).  Each timed phase puts two event markers
+ * in the solver stream; timing the interaction alone (mask 1) keeps the other launches
+ * back to back, ~18 us per Verlet step at 1M particles.  Replaces no reference call: the
+ * reference's JSphGpuSingle timers (TmgStart/TmgStop, JSphGpuSingle.cpp) sync per phase. */
+int sph_solver_set_timing_phases(SphSolver* s, unsigned mask);
 int sph_solver_timing(SphSolver* s, double out_ms[4], uint64_t* launches);
 
 /* ---- slab decomposition over x -------------------------------
