@@ -382,7 +382,8 @@ def main() -> None:
                       "value": m3["units"] / m3["elapsed"], "unit": "particle-steps/s",
                       "interaction_ms_per_call": float(m3["phase_ms"][0]),
                       "divide_ms_per_call": float(m3["phase_ms"][2]),
-                      "parallelism": ("slab-x%d (RCCL)" % world) if m3["bounds"] is not None else "single",
+                      "parallelism": ("slab-x%d (%s)" % (world, "RCCL" if args.transport == "rccl" else "shared-memory"))
+                                     if m3["bounds"] is not None else "single",
                       "owned_np_per_rank": m3["per_rank_np"],
                       "wall_s": time.perf_counter() - t3}
 

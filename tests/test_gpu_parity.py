@@ -126,6 +126,26 @@ def test_dt_trace_matches_reference_57k():
     assert len(dt) == nsteps
     assert np.abs(dt / g_["dt"] - 1).max() < 1e-5
 
+def test_timing_phases():
+    """The timed region records only the requested phases (sph_solver_set_timing_phases):
+    bench.py times the interaction alone inside its timed region, the breakdown after it;
+    timing does not change the results."""
+    case = DamBreakCase(0.025)
+    a, b = gpu(case), gpu(case)
+    a.set_timing(True, phases=1)
+    a.run(5)
+    ms, n = a.timing()
+    assert ms[0] > 0 and n == 5 and ms[1] == 0 and ms[2] == 0
+    a.set_timing(True)
+    a.run(5)
+    ms, n = a.timing()
+    assert ms[0] > 0 and ms[1] > 0 and ms[2] > 0 and n == 5
+    b.run(10)
+    pa, pb = a.particles(), b.particles()
+    for k in ("idp", "pos", "vel", "rhop"):
+        assert np.array_equal(pa[k], pb[k]), k
+
+
 def test_deterministic_bitwise():
     case = DamBreakCase(0.025)
     a, b = gpu(case), gpu(case)
