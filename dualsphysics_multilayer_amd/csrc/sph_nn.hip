@@ -199,10 +199,12 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   const float rhop1over2 = rho1 * inv_rho2;
   float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
   const float dot = drx * dvx + dry * dvy + drz * dvz;  // dv.fr = fac (dr.dv)
-  a.ar = fmaf(fac * dot, rho1 * massrhop, a.ar);  // m2 fac (dr.dv) rho1/rho2
+  a.ar = fmaf(fac * dot, massrhop, a.ar);  // m2 fac (dr.dv) / rho2; x rho1 after the pass
   const float cbar = ph2.y;  // max(Cs0[pp2], Cs0[pp2])
   const float dot3 = fac * rr2;  // drx*frx+dry*fry+drz*frz
   const float inv_re = frcp(rr2 + K.eta2);
+  // m2/rho2 dot3/(r^2+eta^2): the common factor of the DDT (Fourtakas) and Morris terms
+  const float xdm = inv_re * massrhop * dot3;
   // density diffusion, only between particles of the same phase (JSphCpu_NN_FDA.cpp:181-199)
   // (branch-free: once the sum is FLT_MAX it stays FLT_MAX, since FLT_MAX +- a finite
   // pair term rounds back to FLT_MAX; a per-lane `if (a.delta != FLT_MAX)` costs exec-mask
@@ -219,8 +221,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     // rounding floor) does not absorb: step-1 velocities moved 5.7e-7 against 2e-8
     const float rh = 1.f + K.ddtgz * drz;
     const float drhop = K.rhopzero * fexp2(K.ovgamma * flog2(rh)) - K.rhopzero;
-    const float visc_densi = ph2c.w * ((rho2 - rho1) - drhop) * inv_re;
-    const float delta = (p.ph == pp2 ? visc_densi * dot3 * massrhop : 0.f);
+    const float delta = (p.ph == pp2 ? ph2c.w * ((rho2 - rho1) - drhop) * xdm : 0.f);
     a.delta = (BOUNDP2 && ok) ? FLT_MAX : a.delta - delta;
   }
   // multiphase shifting (JSphCpu_NN_FDA.cpp:202-209): a heavier-phase neighbour resets x
@@ -307,7 +308,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     const float eta = nn_eta(K.nnbi != 0, dmag, ph2.w, visco_nn, ph2c, p.taumax, p.bimulti);
     a.visceta = max_nonneg(ok ? eta : 0.f, a.visceta);
     if constexpr (TVISCO == 2) {  // Morris operator: m2 2 eta dot3 / ((r^2+eta^2) rho2)
-      const float vtemp = (2.f * eta) * (inv_re * massrhop) * dot3;
+      const float vtemp = (2.f * eta) * xdm;
       a.ax = fmaf(vtemp, dvx, a.ax);
       a.ay = fmaf(vtemp, dvy, a.ay);
       a.az = fmaf(vtemp, dvz, a.az);
@@ -805,6 +806,8 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
 #else
       nn_pass<TVISCO, TDENSITY, SHIFT, 1>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, b);
 #endif
+      f.ar *= p.vr.w;  // the continuity sums' common rho1 (nn_pair)
+      b.ar *= p.vr.w;
       if (act) {
         // the two CPU passes' stores (JSphCpu_NN_FDA.cpp:278-296).  With shifting configured
         // the reference instantiates every interaction with shift=true (the predictor's too,
