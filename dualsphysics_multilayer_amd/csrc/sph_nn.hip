@@ -599,50 +599,61 @@ __device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid&
   }
 }
 
-// The shifting x sum of a fluid p1 over its fluid rows in the reference's pair order
-// (z-major rows, p2 ascending), reset by every heavier-phase neighbour
-// (JSphCpu_NN_FDA.cpp:202-209) — the same per-pair terms as nn_pair.  Run for a whole
-// block when any of its lanes met a heavier-phase neighbour in the mirrored pass
-// (phase interfaces only).
+// The shifting x sum of a fluid p1 over its fluid rows with the reference's reset: the
+// reference visits z-major rows, p2 ascending, and a heavier-phase neighbour sets the sum to
+// 0 (JSphCpu_NN_FDA.cpp:202-209), so the result is the sum of the terms AFTER the last
+// heavier-phase pair in that order.  This sweep walks the same pairs BACKWARDS (rows from
+// the last, p2 descending) and a lane stops at its first heavier-phase pair: the terms it
+// added are exactly the reference's, summed in the reverse order (rounding only), and rows
+// before that pair are never staged once every lane has stopped.  At a layer interface the
+// heavier p1 meets the lighter phase in the rows above it, the last ones of the order, so a
+// sweep typically stages 3 of the 9 rows.  Run for a block when any of its lanes met a
+// heavier-phase neighbour in the mirrored pass (phase interfaces only); `need`: this lane did
+// (the others keep their mirrored-order sum, which no reset touched).
 __device__ __forceinline__ float nn_sx_sweep(const KConst& K, const DivGrid& g, const RowCtx& rc, const NNP1& p,
                                              float thr, const unsigned* __restrict__ bc,
                                              const float4* __restrict__ poscell,
                                              const float4* __restrict__ velrhop, const float* __restrict__ press,
                                              const typecode* __restrict__ code, float4* __restrict__ sA,
                                              float4* __restrict__ sB, NNSC sC,
-                                             const float4* __restrict__ sph) {
+                                             const float4* __restrict__ sph, bool need, float sx_mirrored) {
   float sx = 0.f;
+  bool live = rc.act && need;  // still summing (no heavier-phase pair met yet, backwards)
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
-  for (int dz = -1; dz <= 1; dz++) {
-    for (int dy = -1; dy <= 1; dy++) {
+  for (int dz = 1; dz >= -1; dz--) {
+    for (int dy = 1; dy >= -1; dy--) {
+      if (!__syncthreads_or(int(live))) return need ? sx : sx_mirrored;  // block-uniform exit
       const int z = rc.cz + dz, y = rc.cy + dy;
       if (z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;  // block-uniform
       const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
       const unsigned rs = bc[rowbase + rc.xa], re = bc[rowbase + rc.xb + 1];
       const unsigned ls = bc[rowbase + rc.lxa], le = bc[rowbase + rc.lxb + 1];
-      for (unsigned seg = rs; seg < re; seg += NN_TCAP) {
-        const unsigned segn = min(unsigned(NN_TCAP), re - seg);
+      if (re == rs) continue;
+      // segments from the row's end
+      for (unsigned segn0 = (re - rs - 1u) % unsigned(NN_TCAP) + 1u, seg = re - segn0, segn = segn0;;) {
         __syncthreads();
         nn_stage(K, seg, segn, rc.xo, dy, dz, false, poscell, velrhop, press, code, sA, sB, sC, 0u);
         __syncthreads();
         const int w0 = int(max(ls, seg) - seg);
-        const int w1 = rc.act ? max(w0, int(min(le, seg + segn)) - int(seg)) : w0;
-        for (int off = w0; off < w1; off += 128) {
+        const int w1 = live ? max(w0, int(min(le, seg + segn)) - int(seg)) : w0;
+        // chunks of 128 from the window's end, each drained highest candidate first
+        for (int off = w0 + ((w1 - w0 - 1) / 128) * 128; live && off >= w0 && w1 > w0; off -= 128) {
           unsigned long long c0, c1;
           test128(sA, off, min(w1 - off, 128), px2, py2, pz2, thr, c0, c1);
-          int b0 = off;
-          if (!c0) {
-            c0 = c1;
-            c1 = 0ull;
-            b0 += 64;
+          int b1 = off + 64;
+          if (!c1) {
+            c1 = c0;
+            c0 = 0ull;
+            b1 = off;
           }
-          while (c0) {  // ascending p2
-            const int j = b0 + int(__builtin_ctzll(c0));
-            c0 &= c0 - 1ull;
-            const bool e = c0 == 0ull;
-            c0 = e ? c1 : c0;
-            b0 = e ? b0 + 64 : b0;
-            c1 = e ? 0ull : c1;
+          while (live && c1) {  // descending p2
+            const int k = 63 - int(__builtin_clzll(c1));
+            const int j = b1 + k;
+            c1 &= ~(1ull << k);
+            const bool e = c1 == 0ull;
+            c1 = e ? c0 : c1;
+            b1 = e ? off : b1;
+            c0 = e ? 0ull : c0;
             const float4 A = sA[j], C = sC.ld(j, false);
             float drx = p.x - A.x;
             const float dry = p.y - A.y, drz = p.z - A.z;
@@ -656,15 +667,18 @@ __device__ __forceinline__ float nn_sx_sweep(const KConst& K, const DivGrid& g, 
             const float frx = fac * drx;
             const int pp2 = int(__float_as_uint(C.y));
             const float massp2 = sph[2 * pp2].x;
-            const bool heavy = ok && (p.mph > massp2) && p.ph != pp2;
-            const float massrhop = massp2 * C.z;
-            sx = heavy ? 0.f : sx + massrhop * frx;
+            const bool heavy = ok && (p.mph > massp2);
+            if (heavy) live = false;  // the reference's reset: nothing before this pair counts
+            else sx += (massp2 * C.z) * frx;
           }
         }
+        if (seg == rs) break;
+        seg -= unsigned(NN_TCAP);
+        segn = unsigned(NN_TCAP);
       }
     }
   }
-  return sx;
+  return need ? sx : sx_mirrored;
 }
 
 #ifndef SPH_NN_WAVES
@@ -786,8 +800,11 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
 #if SPH_NN_MIRROR
       nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 0>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
                                                    sph, f);
-      if (SHIFT && __syncthreads_or(int(f.hv)))
-        f.sx = nn_sx_sweep(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph);
+#ifndef SPH_NN_NOSWEEP
+#define SPH_NN_NOSWEEP 0  // diagnostic only: 1 skips the ordered shifting-x re-sweep (wrong sx at interfaces)
+#endif
+      if (SHIFT && !SPH_NN_NOSWEEP && __syncthreads_or(int(f.hv)))
+        f.sx = nn_sx_sweep(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f.hv, f.sx);
 #else
       nn_pass<TVISCO, TDENSITY, SHIFT, 0>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f);
 #endif
