@@ -275,8 +275,6 @@ static std::vector<unsigned> initial_columns(const SphConstants& C, const SphPar
   return cx;
 }
 
-// Column bounds b[0..nranks] at the quantiles of the weight prefix pre[0..ncx] (each slab
-// at least minw columns; a bound column goes to the side closer to its target).
 // Contiguous split of the columns into nranks slabs of at least minw columns that
 // minimises the heaviest slab (the step time of the slowest rank): bisection on the load
 // bound L, each bound probed greedily (every slab takes columns while it stays <= L and
