@@ -217,7 +217,7 @@ class SphGpuSingle {
   void* sendmbuf_ = nullptr;
   // timing (hipEvents on the solver stream)
   bool timing_ = false;
-  unsigned timing_mask_ = 0xfu;  // phases timed (SetTiming, SPH_TIMING_PHASES)
+  unsigned timing_mask_ = 0xfu;  // phases timed (SetTimingPhases, sph_solver_set_timing_phases)
   struct Ev { hipEvent_t a, b; int phase; };
   std::vector<Ev> pending_;
   std::vector<hipEvent_t> evpool_;
