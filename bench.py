@@ -61,6 +61,22 @@ def dist_env():
     return rank, world, local
 
 
+def usable_cpus() -> int:
+    """CPUs this process may really use: the affinity mask, capped by the cgroup v2 CPU quota
+    (a 16-CPU cgroup on a 256-thread host must not run 64 OpenMP threads)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q[0] != "max":
+            n = min(n, max(1, int(float(q[0]) / float(q[1]))))
+    except (OSError, ValueError, IndexError):
+        pass
+    return max(1, n)
+
+
 def host_info(threads: int) -> dict:
     """What the CPU baseline ran on: logical CPUs of the machine, CPUs this process may use,
     the CPU model, and the thread rule (BASELINE.md asks for count and model)."""
@@ -84,9 +100,10 @@ def host_info(threads: int) -> dict:
         pass
     return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "cpu_model": model,
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
-            "thread_rule": "threads = min(nproc, 64) (BASELINE.md): the reference caps OpenMP at "
-                           "OMP_MAXTHREADS=64 (OmpDefs.h:39); `box_share` times OMP_NUM_THREADS threads, the "
-                           "GPU box's CPU share of one GPU (16)", "threads": threads}
+            "thread_rule": "threads = min(usable CPUs, 64), usable = min(sched_getaffinity, cgroup CPU quota): "
+                           "the reference at its best on the CPUs this job may use (it caps OpenMP at "
+                           "OMP_MAXTHREADS=64, OmpDefs.h:39); `oversubscribed` times min(nproc, 64) threads "
+                           "on the same CPUs, the literal BASELINE.md rule", "threads": threads}
 
 
 def _ref_run(exe: str, case: str, out: str, nsteps: int, threads: int, extra=()) -> float:
@@ -312,15 +329,20 @@ def main() -> None:
                          "(host-staged shared memory: ranks of one node without RCCL)")
     ap.add_argument("--ranks-per-gpu", type=int, default=1,
                     help="ranks sharing one GPU (device = LOCAL_RANK // this; needs --transport shm)")
-    ap.add_argument("--presteps", type=int, default=0,
-                    help="untimed steps before the warmup: time a developed flow (movers across cells, "
-                         "the incremental divide's real load) instead of the first steps from rest")
+    ap.add_argument("--presteps", type=int, default=None,
+                    help="untimed steps before the warmup (default: 10 - warmup, so the timed window starts "
+                         "at step 10 as BASELINE.md's 10-110); large values time a developed flow")
+    ap.add_argument("--developed-presteps", type=int, default=8000,
+                    help="cfg2 N=1: also time the same steps after this many steps (a developed flow, key "
+                         "`developed_flow`; 0: skip)")
     ap.add_argument("--no-cfg3", action="store_true",
                     help="cfg2: skip the extra cfg3 (10M, Symplectic) timing (keys cfg3_1gpu / strong_scaling_cfg3)")
     ap.add_argument("--cfg3-steps", type=int, default=10, help="timed steps of the extra cfg3 measurement")
     ap.add_argument("--force-slab", action="store_true",
                     help="run the N>1 code path (gloo bootstrap + RCCL slab) even with one rank")
     args = ap.parse_args()
+    if args.presteps is None:
+        args.presteps = max(0, 10 - args.warmup)
     if args.boundary is None:
         args.boundary = "mdbc" if args.workload == "cfg4" else "dbc"
 
@@ -387,6 +409,20 @@ def main() -> None:
                       "owned_np_per_rank": m3["per_rank_np"],
                       "wall_s": time.perf_counter() - t3}
 
+    # The flow after --developed-presteps steps (the surge under way: more particles change
+    # cells, so the incremental divide does more work than in the first steps from rest).
+    developed = None
+    if (args.workload == "cfg2" and world == 1 and not args.force_slab and args.developed_presteps > 0
+            and args.presteps < args.developed_presteps):
+        t4 = time.perf_counter()
+        m4 = measure(case, args, rank, world, device, dist, False, args.steps, args.warmup, args.developed_presteps)
+        developed = {"presteps": args.developed_presteps, "steps": args.steps,
+                     "timed_window": [args.developed_presteps + args.warmup,
+                                      args.developed_presteps + args.warmup + args.steps],
+                     "ms_per_step": m4["elapsed"] / args.steps * 1e3, "value": m4["units"] / m4["elapsed"],
+                     "unit": "particle-steps/s", "interaction_ms_per_call": float(m4["phase_ms"][0]),
+                     "divide_ms_per_call": float(m4["phase_ms"][2]), "wall_s": time.perf_counter() - t4}
+
     if rank == 0:
         pairs = (pairs0.astype("float64") + pairs1.astype("float64")) / 2.0
         ff_chk, ff_real, fb_chk, fb_real, bf_chk, bf_real = pairs
@@ -422,6 +458,7 @@ def main() -> None:
                      "synthetic: the NN wet dam break example extruded to 3D (case.py WetDambreakNNCase = "
                      "oracle/tools/gennn_ref)" if nn else
                      "synthetic: generated 3D dam-break lattice (SURVEY.md §8(c) recipe)"),
+            "timed_window": [args.presteps + args.warmup, args.presteps + args.warmup + args.steps],
             "config": {
                 "workload": (("BASELINE cfg2: 3D dam break, %d particles (dp=%g), Verlet, Wendland, artificial "
                               "viscosity 0.1, DDT2 0.1, %s, CFL 0.2, CellMode %s"
@@ -487,11 +524,12 @@ def main() -> None:
         }
         wall["timed_s"] = elapsed
         if not args.no_cpu_baseline and world == 1:
-            # BASELINE.md's thread rule: min(nproc, 64) threads (the reference caps OpenMP at
-            # OMP_MAXTHREADS=64, OmpDefs.h:39) -> `value`; beside it the box's CPU share of one
-            # GPU (OMP_NUM_THREADS, 16 on the GPU box) on a shorter window.
-            threads = min(os.cpu_count() or 1, 64)
-            share = min(int(os.environ.get("OMP_NUM_THREADS", threads)), threads)
+            # The reference at its best on the CPUs this job may use: min(usable CPUs, 64) threads
+            # (it caps OpenMP at OMP_MAXTHREADS=64, OmpDefs.h:39; usable = affinity capped by the
+            # cgroup quota, 16 on the GPU box) -> `value`; beside it, on a shorter window, the
+            # literal min(nproc, 64) of BASELINE.md, oversubscribed on a CPU-capped box.
+            threads = min(usable_cpus(), 64)
+            literal = min(os.cpu_count() or 1, 64)
             t_cpu = time.perf_counter()
 
             def ref_baseline(nthreads, nsteps):
@@ -506,16 +544,18 @@ def main() -> None:
             if cb is not None:
                 cb["gpu_over_cpu"] = value / cb["value"]
                 cb["host"] = host_info(threads)
-                if share != threads:
-                    cs = ref_baseline(share, max(args.cpu_steps // 3, 1))
+                if literal != threads:
+                    cs = ref_baseline(literal, max(args.cpu_steps // 3, 1))
                     if cs is not None:
                         cs["gpu_over_cpu"] = value / cs["value"]
-                        cb["box_share"] = cs
+                        cb["oversubscribed"] = cs
             res["cpu_baseline"] = cb
             wall["cpu_baseline_s"] = time.perf_counter() - t_cpu
         wall["process_s"] = time.perf_counter() - T_START
         res["wall_breakdown"] = wall
         res["cfg3_1gpu" if world == 1 else "strong_scaling_cfg3"] = cfg3_extra
+        if developed is not None:
+            res["developed_flow"] = developed
         print(json.dumps(res))
     if dist is not None:
         dist.destroy_process_group()

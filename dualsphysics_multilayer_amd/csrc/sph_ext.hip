@@ -365,9 +365,10 @@ __global__ __launch_bounds__(TB) void k_fluid_ext(DevScalars* __restrict__ sc, c
                                                   float4* __restrict__ arace, float4* __restrict__ shiftpos,
                                                   float4* __restrict__ taunew, int shiftstore) {
   constexpr int TCAPX = ExtCap<TVISCO>::v;
-  __shared__ float4 sA[TCAPX + SPH_PAD];
-  __shared__ float4 sB[TCAPX];
-  __shared__ float4 sC[TCAPX];
+  __shared__ float4 sABC[3 * TCAPX];  // sA, sB, sC: the candidate test's over-read stays inside
+  float4* const sA = sABC;
+  float4* const sB = sABC + TCAPX;
+  float4* const sC = sABC + 2 * TCAPX;
   __shared__ float4 sD[TVISCO == 2 ? TCAPX : 1];
   __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];

@@ -334,20 +334,12 @@ __device__ __forceinline__ void tile_unit(const KConst& K, const P1& p, float th
                                           const float4* __restrict__ sA, const float4* __restrict__ sB,
                                           const typename CRecT<FT>::type* __restrict__ sC, const PassK& Q, TAcc& a) {
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
-#if SPH_ABLATE == 2 || SPH_ABLATE == 3
-  a.visc += float(wa1 - wa0 + wb1 - wb0);
-  return;
-#endif
   for (int off = 0;; off += 128) {  // a second round only for windows of > 128 candidates
     const int na = wa1 - wa0 - off, nb = wb1 - wb0 - off;
     if (na <= 0 && nb <= 0) break;
     unsigned long long c0, c1, c2, c3;
     test128(sA, wa0 + off, min(na, 128), px2, py2, pz2, thr, c0, c1);
     test128(sA, wb0 + off, min(nb, 128), px2, py2, pz2, thr, c2, c3);
-#if SPH_ABLATE == 1
-    a.visc += float(__popcll(c0) + __popcll(c1) + __popcll(c2) + __popcll(c3));
-    continue;
-#endif
     drain_words<TDENSITY, MODE, FT>(K, p, c0, c1, c2, c3, wa0 + off, wa0 + off + 64, wb0 + off, wb0 + off + 64, sA,
                                     sB, sC, Q, a);
   }
@@ -484,9 +476,6 @@ __device__ __forceinline__ void stage_row(const KConst& K, unsigned rs, unsigned
                                           const float4* __restrict__ velrhop, const float* __restrict__ press,
                                           float4* __restrict__ sA, float4* __restrict__ sB, CR* __restrict__ sC,
                                           const FtRec& ft) {
-#if SPH_ABLATE == 3
-  return;  // diagnostic: no staging loads
-#endif
   const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
   for (unsigned i = threadIdx.x; i < re - rs; i += TB) {
     const float4 pc = poscell[rs + i];
@@ -525,9 +514,6 @@ __device__ __forceinline__ TAcc run_pass(const KConst& K, const DivGrid& g, cons
   TAcc acc = {};
   acc.dstop = dstop0;
   const unsigned cellinit = (MODE == 1 ? 0u : g.boxfluid);
-#if SPH_ABLATE == 4
-  return acc;  // diagnostic: items, lane order, p1 loads and stores only
-#endif
   for (int u = 0; u < 5; u++) {
     const int dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
     const int dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
@@ -691,11 +677,8 @@ __device__ __forceinline__ TAcc pass_s(const KConst& K, const DivGrid& g, const 
                                              dstop0);
 }
 
-#if SPH_TAIL_DBG
-__device__ unsigned long long g_taildbg[3 * 4096];
-#endif
 template <int TDENSITY, bool FT = false, int S = 1>
-__global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
+__global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
                                                     unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
                                                     const float4* __restrict__ velrhop,
                                                     const float* __restrict__ press,
@@ -703,8 +686,11 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
                                                     float4* __restrict__ arace, FtRec ft) {
   constexpr int tcap = TcapT<FT>::v;
   constexpr int TD = TDENSITY & 7;
-  __shared__ float4 sA[tcap + SPH_PAD];  // over-read pad of the 8-wide candidate test (<= 7 records)
-  __shared__ float4 sB[tcap];
+  // position records then velrhop records in ONE array: the candidate test's last group of
+  // 32 may read up to 31 records past a window that ends at tcap, which stays inside it
+  __shared__ float4 sAB[2 * tcap];
+  float4* const sA = sAB;
+  float4* const sB = sAB + tcap;
   __shared__ typename CRecT<FT>::type sC[tcap];  // press/rho, 1/rho (FT: mass-scaled + kind)
   __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];  // lane -> p1 of the item (see lane_order)
@@ -712,10 +698,6 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
   const ItemGroups IG(sc);
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f;
-#if SPH_TAIL_DBG
-  const unsigned long long tdbg0 = wall_clock64();
-  unsigned ndbg = 0;
-#endif
   const float cvisc_f = -K.visco * K.cs0f * K.kernelh * K.massfluid;
   const float cvisc_b = -K.viscobound * K.cs0f * K.kernelh * K.massbound;
 
@@ -742,9 +724,6 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
       if (c >= gr.n) break;
       const unsigned it = gr.item(c);
       const uint4 item = items[it];
-#if SPH_TAIL_DBG
-      ndbg++;
-#endif
       const bool bitem = (item.x & ITEM_BOUND) != 0u;
       const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
       const int a = int(item.y & 0xffffu), b = int(item.y >> 16);
@@ -765,14 +744,7 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
         }
       }
       {  // items hold <= TB particles: one p1 per lane
-#ifndef SPH_LANEORDER
-#define SPH_LANEORDER 1
-#endif
-#if SPH_LANEORDER
         const unsigned p1 = item.z + lane_order(poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
-#else
-        const unsigned p1 = item.z + threadIdx.x;
-#endif
         const bool act = threadIdx.x < item.w - item.z;
         P1 p;
         int cx1 = a;
@@ -837,16 +809,6 @@ __global__ __launch_bounds__(TB) SPH_WAVES_ATTR void k_fluid_tiled(DevScalars* _
       }
     }
   }
-#if SPH_TAIL_DBG  // diagnostic: start/end of every block of one launch (100 MHz wall clock), printed next step
-  if (threadIdx.x == 0 && sc->nstep == 12 && blockIdx.x < 4096) {
-    g_taildbg[3 * blockIdx.x] = tdbg0;
-    g_taildbg[3 * blockIdx.x + 1] = wall_clock64();
-    g_taildbg[3 * blockIdx.x + 2] = ndbg;
-  }
-  if (threadIdx.x == 0 && blockIdx.x == 0 && sc->nstep == 13)
-    for (unsigned i = 0; i < min(gridDim.x, 4096u); i++)
-      printf("TAILDBG %u %llu %llu %llu\n", i, g_taildbg[3 * i], g_taildbg[3 * i + 1], g_taildbg[3 * i + 2]);
-#endif
   wave_max_atomic(sc, RED_VISCDT, viscmax);
   wave_max_atomic(sc, RED_ACEMAX2, ace2max);
   // (the queue counters are zeroed by k_items_scan, or by the solver before an interaction

@@ -233,7 +233,7 @@ struct NNFaceRec {
   unsigned idp;
   float v[7];
 };
-void launch_nn_face_pack(hipStream_t stm, unsigned cap, const DevScalars* sc, const PartArrays& a, const KConst& K,
+void launch_nn_face_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, const KConst& K,
                          const DivGrid& g, const float* viscoeta, const float4* tau, NNFaceRec* sl, NNFaceRec* sr,
                          unsigned capl, unsigned capr, unsigned* idxmap, unsigned nidx);
 void launch_nn_face_apply(hipStream_t stm, DevScalars* sc, const NNFaceRec* rl, const NNFaceRec* rr, unsigned capl,
@@ -249,7 +249,7 @@ enum DtMode { DT_VERLET = 0, DT_SYM_PRE = 1, DT_SYM_COR = 2, DT_PEEK = 3 };
 // (launch_fold_maxima + SlabTransport::allreduce_max_u32); nullptr = fold the slots here.
 void launch_dt(hipStream_t stm, DevScalars* sc, const KConst& K, double cfl, double dtmin, double cs0, int mode,
                double* dttrace, unsigned tracecap, const unsigned* folded = nullptr);
-// folded[4]: VelMax^2, AceMax^2, ViscDtMax, ViscEtaDtMax
+// folded[5]: VelMax^2, AceMax^2, ViscDtMax, ViscEtaDtMax, this slab's fatal error flags
 void launch_fold_maxima(hipStream_t stm, DevScalars* sc, unsigned* folded, bool clear);
 // Update kernels skip slab ghosts (local column outside [g.xown0, g.xown1)) and mark
 // them DCELL_DISCARD for the next divide.

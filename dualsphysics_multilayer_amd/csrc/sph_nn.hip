@@ -33,18 +33,6 @@ namespace sphx {
 // records + the 8-record pad + the phase table keep the block at 20472 B of LDS (8 blocks =
 // 4 waves per SIMD), and a mirrored row pair mostly fits one segment (cfg5: 1.554 ms at
 // 410 records of 48 B, 1.515 ms at 480 of 41 B).
-#ifndef SPH_NN_POWSKIP
-#define SPH_NN_POWSKIP 0  // 1: skip D^(n-1) when every lane's p2 phase has n = 1 (more spills here)
-#endif
-#ifndef SPH_NN_ONEPAIR
-#define SPH_NN_ONEPAIR 1  // one pair per drain iteration: no VGPR spill, 1.3% faster on cfg5 than two
-#endif
-#ifndef SPH_NN_GRAD12
-#define SPH_NN_GRAD12 1  // FDA velocity gradient as (dv_i / r^2) dr_j (12 products, not 18; cfg5 -1.5 %)
-#endif
-#ifndef SPH_NN_RSQ
-#define SPH_NN_RSQ 1  // FDA pairs: r and 1/r^2 from one v_rsq (0: v_sqrt + v_rcp)
-#endif
 #ifndef SPH_NN_TCAP
 #define SPH_NN_TCAP 476  // 476 x 41 B + pad + the 3-row phase table: 20436 B (8 blocks/CU)
 #endif
@@ -108,11 +96,7 @@ __device__ __forceinline__ float nn_eta(bool bi, float dmag, float tau_yield, fl
   if (dmag <= ALMOSTZERO) dmag = ALMOSTZERO;
   // visco * D^(n-1), exactly visco for n = 1 (skipped when no lane of the wave needs the power)
   float miou_hb = visco;
-#if SPH_NN_POWSKIP
-  if (__ballot(c.z != 0.f)) miou_hb = (c.z != 0.f) ? visco * fexp2(c.z * flog2(dmag)) : visco;
-#else
   miou_hb = visco * fexp2(c.z * flog2(dmag));
-#endif
   const float e = 1.f - fexp2(c.y * dmag);  // 1 - exp(-m D)
   if (!bi) {
     const float miou_pap = tau_yield * frcp(2.f * dmag) * e;
@@ -173,7 +157,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   // kernel (Wendland fac = bwen q (1-q/2)^3 / r = (bwen/h) (1-q/2)^3), 0 beyond 2h.  With the
   // FDA gradient (which needs 1/r^2 too) one v_rsq gives both: r = r^2 rsq, 1/r^2 = rsq^2
   // (one transcendental instead of v_sqrt + v_rcp; ulp-level differences)
-  constexpr bool FDA = (TVISCO == 2 || TVISCO == 3) && SPH_NN_RSQ;
+  constexpr bool FDA = (TVISCO == 2 || TVISCO == 3);
   const float rsq = FDA ? __builtin_amdgcn_rsqf(rr2) : 0.f;
   const float rad = FDA ? rr2 * rsq : fsqrt_(rr2);
   const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
@@ -287,16 +271,10 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     // explicit form cancels, so its rounding is part of the result (a closed form of the
     // rank-one gradient's invariant moved step-1 velocities 30x past the noise floor)
     const float irr2 = FDA ? rsq * rsq : frcp(rr2);
-#if SPH_NN_GRAD12  // (dv_i / r^2) dr_j: 12 products instead of 18, rounding-level differences
     const float tx = dvx * irr2, ty = dvy * irr2, tz = dvz * irr2;
     const float a11 = tx * drx, a12 = tx * dry, a13 = tx * drz;
     const float a21 = ty * drx, a22 = ty * dry, a23 = ty * drz;
     const float a31 = tz * drx, a32 = tz * dry, a33 = tz * drz;
-#else
-    const float a11 = dvx * drx * irr2, a12 = dvx * dry * irr2, a13 = dvx * drz * irr2;
-    const float a21 = dvy * drx * irr2, a22 = dvy * dry * irr2, a23 = dvy * drz * irr2;
-    const float a31 = dvz * drx * irr2, a32 = dvz * dry * irr2, a33 = dvz * drz * irr2;
-#endif
     const float div_vel = (a11 + a22 + a33) * (1.f / 3.f);
     const float d11 = a11 - div_vel, d22 = a22 - div_vel, d33 = a33 - div_vel;
     const float s12 = a12 + a21, s13 = a13 + a31, s23 = a23 + a32;  // 2 d12, 2 d13, 2 d23
@@ -483,7 +461,6 @@ __device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restr
     c3 = e ? 0ull : c3;
     return j;
   };
-#if SPH_NN_ONEPAIR  // one pair per iteration (125 VGPRs, no scratch; the 2-pair interleave spills 48 B/lane)
   while (c0) {
     const int j1 = pop();
     const float4 A1 = sA[j1], B1 = sB[j1];
@@ -496,32 +473,6 @@ __device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restr
     else nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1, false>(K, sph, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
     keep_w(A1, B1);  // 16-B LDS reads (sph_tiled.hpp)
   }
-#else
-  while (c0) {
-    const int j1 = pop();
-    const bool two = c0 != 0ull;
-    const int j2p = pop();
-    const int j2 = two ? j2p : j1;
-    const float4 A1 = sA[j1], A2 = sA[j2];
-    const float4 B1 = sB[j1], B2 = sB[j2];
-    float drx1 = p.x - A1.x, dry1 = p.y - A1.y, drz1 = p.z - A1.z;
-    float drx2 = p.x - A2.x, dry2 = p.y - A2.y, drz2 = p.z - A2.z;
-    float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
-    float rr22 = drx2 * drx2 + dry2 * dry2 + drz2 * drz2;
-    const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
-    const bool ok2 = two && rr22 <= K.kernelsize2 && rr22 >= ALMOSTZERO;
-    rr21 = ok1 ? rr21 : 1e30f;
-    rr22 = ok2 ? rr22 : 1e30f;
-    const float4 C1 = sC.ld(j1, KIND == 1), C2 = sC.ld(j2, KIND == 1);
-    if (KIND == 2) {
-      nn_bound_pair(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
-      nn_bound_pair(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
-    } else {
-      nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1, false>(K, sph, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
-      nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1, false>(K, sph, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
-    }
-  }
-#endif
 }
 
 // A pass over the 9 fluid rows (KIND 0: fluid p1, 2: bound p1) in drain units of two
@@ -689,9 +640,6 @@ __device__ __forceinline__ float nn_sx_sweep(const KConst& K, const DivGrid& g, 
 #else
 #define SPH_NN_WAVES_ATTR
 #endif
-#ifndef SPH_NN_MIRROR
-#define SPH_NN_MIRROR 1  // 0: every pass in the reference's row order (one row per drain unit)
-#endif
 
 template <int TVISCO, int TDENSITY, bool SHIFT>
 __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
@@ -701,8 +649,9 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
                                                  DivGrid g, KConst K, const float4* __restrict__ phases,
                                                  float4* __restrict__ arace, float4* __restrict__ shiftpos,
                                                  float* __restrict__ viscoeta, float4* __restrict__ tau) {
-  __shared__ float4 sA[NN_TCAP + SPH_PAD];
-  __shared__ float4 sB[NN_TCAP];
+  __shared__ float4 sAB[2 * NN_TCAP];  // sA then sB: the candidate test's over-read stays inside
+  float4* const sA = sAB;
+  float4* const sB = sAB + NN_TCAP;
   __shared__ float2 sC2[NN_TCAP];  // {press, 1/rho}
   __shared__ unsigned char sT[NN_TCAP];  // tag
   const NNSC sC = {sC2, sT};
@@ -782,12 +731,8 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
       const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act};
       if (bitem) {
         NNAcc f = {};
-#if SPH_NN_MIRROR
         nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 2>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
                                                      sph, f);
-#else
-        nn_pass<TVISCO, TDENSITY, SHIFT, 2>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f);
-#endif
         if (act) {
           arace[p1] = make_float4(0.f, 0.f, 0.f, (f.ar != 0.f || f.visc != 0.f) ? 0.f + f.ar : 0.f);
           viscmax = fmaxf(viscmax, f.visc);
@@ -797,22 +742,14 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
       // fluid p1: the fluid pass, then the bound pass; the shifting sums carry over
       // (shiftposfs[p1] is stored by the first pass and loaded by the second)
       NNAcc f = {}, b = {};
-#if SPH_NN_MIRROR
       nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 0>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
                                                    sph, f);
-#ifndef SPH_NN_NOSWEEP
-#define SPH_NN_NOSWEEP 0  // diagnostic only: 1 skips the ordered shifting-x re-sweep (wrong sx at interfaces)
-#endif
-      if (SHIFT && !SPH_NN_NOSWEEP && __syncthreads_or(int(f.hv)))
+      if (SHIFT && __syncthreads_or(int(f.hv)))
         f.sx = nn_sx_sweep(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f.hv, f.sx);
-#else
-      nn_pass<TVISCO, TDENSITY, SHIFT, 0>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f);
-#endif
       b.sx = f.sx;
       b.sy = f.sy;
       b.sz = f.sz;
       b.sw = f.sw;
-#if SPH_NN_MIRROR
       // the first no-shift bound pair (ShiftMode NoBound/NoFixed) freezes every shifting sum:
       // only then is the bound pass order-dependent (uniform branch)
       if (SHIFT && (K.shiftmode == 1 || K.shiftmode == 2))
@@ -820,9 +757,6 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
       else
         nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 1>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
                                                      sph, b);
-#else
-      nn_pass<TVISCO, TDENSITY, SHIFT, 1>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, b);
-#endif
       f.ar *= p.vr.w;  // the continuity sums' common rho1 (nn_pair)
       b.ar *= p.vr.w;
       if (act) {
@@ -1172,9 +1106,10 @@ __global__ __launch_bounds__(TB) void k_nn_visc(DevScalars* __restrict__ sc, con
                                                 const float* __restrict__ viscoeta, const float4* __restrict__ tau,
                                                 const unsigned* __restrict__ bc, DivGrid g, KConst K,
                                                 const float4* __restrict__ phases, float4* __restrict__ arace) {
-  __shared__ float4 sA[NNV_TCAP + SPH_PAD];
-  __shared__ float4 sB[NNV_TCAP];
-  __shared__ float4 sC[NNV_TCAP];
+  __shared__ float4 sABC[3 * NNV_TCAP];  // sA, sB, sC: the candidate test's over-read stays inside
+  float4* const sA = sABC;
+  float4* const sB = sABC + NNV_TCAP;
+  float4* const sC = sABC + 2 * NNV_TCAP;
   __shared__ float4 sph[2 * SPH_MAXPHASES];
   __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];
@@ -1276,7 +1211,7 @@ void launch_nn_visc(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uin
 }
 
 // ---- slabs: the first pass's eta / tau of the face columns for the neighbours' ghosts ----
-__global__ __launch_bounds__(256) void k_nn_face_pack(const DevScalars* __restrict__ sc, PartArrays a, KConst K,
+__global__ __launch_bounds__(256) void k_nn_face_pack(DevScalars* __restrict__ sc, PartArrays a, KConst K,
                                                       DivGrid g, const float* __restrict__ viscoeta,
                                                       const float4* __restrict__ tau, NNFaceRec* __restrict__ sl,
                                                       NNFaceRec* __restrict__ sr, unsigned capl, unsigned capr,
@@ -1296,7 +1231,10 @@ __global__ __launch_bounds__(256) void k_nn_face_pack(const DevScalars* __restri
     if (side == 1 && in_right_face(g, lcx) && g.xown1 < g.ncx) { dst = sr; cap = capr; }
     if (!dst) continue;
     const unsigned k = atomicAdd(&dst[0].idp, 1u);
-    if (k + 1 >= cap) continue;  // cannot happen: the buffers hold every ghost sent at the divide
+    if (k + 1 >= cap) {  // the buffers hold every ghost sent at the divide; if not, say so
+      atomicOr(&sc->error_flags, ERR_HALO);
+      continue;
+    }
     NNFaceRec r;
     r.idp = id;
     r.v[0] = viscoeta ? viscoeta[p] : 0.f;
@@ -1335,7 +1273,7 @@ __global__ __launch_bounds__(256) void k_nn_face_apply(DevScalars* __restrict__ 
   }
 }
 
-void launch_nn_face_pack(hipStream_t stm, unsigned cap, const DevScalars* sc, const PartArrays& a, const KConst& K,
+void launch_nn_face_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, const KConst& K,
                          const DivGrid& g, const float* viscoeta, const float4* tau, NNFaceRec* sl, NNFaceRec* sr,
                          unsigned capl, unsigned capr, unsigned* idxmap, unsigned nidx) {
   if (sl) hipMemsetAsync(sl, 0, sizeof(NNFaceRec), stm);

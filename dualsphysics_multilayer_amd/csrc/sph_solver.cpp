@@ -390,8 +390,8 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   cap_ = slab() ? n + std::max(n / 2, 65536u) : n;
   keybits_ = bits_for(G.boxdiscard, 1);
   // grid-sized buffers hold the widest grid a slab can get from a re-partition (all
-  // columns + the two ghost columns), so they never move
-  nctmax_ = slab() ? unsigned(C.dom_cells[0] + 2) * unsigned(G.ncy) * unsigned(G.ncz) : G.nct;
+  // columns + W = scelldiv ghost columns per face), so they never move
+  nctmax_ = slab() ? unsigned(C.dom_cells[0] + 2 * C.scelldiv) * unsigned(G.ncy) * unsigned(G.ncz) : G.nct;
   if (const char* e = std::getenv("SPH_INTERACTION")) tiled_ = std::string(e) != "simple";
   if (const char* e = std::getenv("SPH_COMM_TIMEOUT_S")) comm_timeout_s_ = std::max(1.0, std::atof(e));
   // incremental divide: distinct key offsets of the 27 neighbour cells (ncx >= 3, checked
@@ -490,7 +490,7 @@ void SphGpuSingle::AllocFixed() {
   sc_ = (DevScalars*)dmalloc(sizeof(DevScalars));
   dttrace_ = (double*)dmalloc(8 * size_t(tracecap_));
   pairs_ = (unsigned long long*)dmalloc(8 * 6);
-  folded_ = (unsigned*)dmalloc(4 * 4);
+  folded_ = (unsigned*)dmalloc(4 * 8);
   slabcnt_ = (SlabCounts*)dmalloc(sizeof(SlabCounts));
   check_hip(hipHostMalloc((void**)&sc_host_, sizeof(DevScalars), hipHostMallocDefault), "hipHostMalloc");
   check_hip(hipHostMalloc((void**)&slabcnt_host_, sizeof(SlabCounts), hipHostMallocDefault), "hipHostMalloc");
@@ -1126,7 +1126,7 @@ void SphGpuSingle::DtVariable(int mode) {
   if (slab()) {
     // The three maxima span the whole domain: fold locally, max over all slabs.
     launch_fold_maxima(stream, sc_, folded_, mode != DT_PEEK);
-    transport_->allreduce_max_u32(folded_, 4, stream);
+    transport_->allreduce_max_u32(folded_, 5, stream);  // 4 maxima + the fatal error flags
     launch_dt(stream, sc_, K, C.cflnumber, C.dtmin, C.cs0, mode, dttrace_, tracecap_, folded_);
   } else {
     launch_dt(stream, sc_, K, C.cflnumber, C.dtmin, C.cs0, mode, dttrace_, tracecap_);
@@ -1416,7 +1416,9 @@ void SphGpuSingle::CheckErrors() {
   if (s.error_flags & ERR_BOUNDOUT) throw SphError(SPH_ERR_BOUNDOUT, "boundary particles were excluded (AbortBoundOut)");
   if (s.error_flags & ERR_DT_NAN) throw SphError(SPH_ERR_DT, "The computed Dt is NaN or infinity");
   if (s.error_flags & ERR_HALO)
-    throw SphError(SPH_ERR_UNSUPPORTED, "mDBC: a ghost node needs particles beyond the slab's ghost column");
+    throw SphError(SPH_ERR_UNSUPPORTED,
+                   "slab halo: an mDBC ghost node needs particles beyond the slab's ghost column, or a face "
+                   "record buffer overflowed");
 }
 
 unsigned SphGpuSingle::DtTrace(double* out, unsigned cap) {
@@ -1468,6 +1470,8 @@ void SphGpuSingle::DownloadInteraction(SphInterOut& out) {
   // Runs one interaction on the current state (like or_interaction) and reads ar/ace back.
   // Maxima accumulated so far (VelMax from the last divide) are kept for this call.
   Interaction_Forces(1);
+  // an inspection: the SPS stress tensor of the state stays the one the next step starts from
+  if (sps_) std::swap(cur_.tau, taunew_);
   DtVariable(DT_PEEK);
   const SphRunStats s = Stats();
   std::vector<float4> a(s.np);
@@ -1520,6 +1524,7 @@ void SphSlabGroup::Run(unsigned nsteps) {
       try {
         slabs[i]->Run(nsteps);
         slabs[i]->Sync();
+        slabs[i]->CheckErrors();  // a fatal error halts every slab at the same step (DtVariable)
       } catch (const SphError& e) {
         err[i] = std::current_exception();
         primary[i] = std::string(e.what()).find("aborted by another slab") == std::string::npos;

@@ -205,7 +205,7 @@ class SphGpuSingle {
   unsigned repart_every_ = 0, repart_count_ = 0;
   double repart_bw_ = 0.3, repart_tol_ = 0.05, repart_last_imbalance_ = 1.0;
   unsigned long long stepsdone_ = 0;
-  unsigned* folded_ = nullptr;   // 3 maxima for the allreduce
+  unsigned* folded_ = nullptr;   // 4 maxima + fatal error flags for the allreduce
   SlabCounts* slabcnt_ = nullptr;
   SlabCounts* slabcnt_host_ = nullptr;
   unsigned* packtiles_ = nullptr;

@@ -34,8 +34,12 @@ __device__ __forceinline__ void fold_slots(DevScalars* __restrict__ sc, bool cle
 __global__ void k_fold(DevScalars* __restrict__ sc, unsigned* __restrict__ folded, int clear) {
   unsigned m[4];
   fold_slots(sc, clear != 0, m);
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0) {
     for (int k = 0; k < 4; k++) folded[k] = m[k];
+    // a fatal error of this slab (e.g. ERR_BOUNDOUT from its divide) rides the same max
+    // all-reduce, so every slab halts at the same step, as the one reference domain does
+    folded[4] = sc->error_flags & ERR_FATAL;
+  }
 }
 
 void launch_fold_maxima(hipStream_t stm, DevScalars* sc, unsigned* folded, bool clear) {
@@ -48,6 +52,7 @@ __global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double d
   unsigned m[4];
   if (folded) {
     for (int k = 0; k < 4; k++) m[k] = folded[k];
+    if (l == 0) sc->error_flags |= folded[4];
   } else {
     fold_slots(sc, mode != DT_PEEK, m);
   }

@@ -9,32 +9,17 @@
 
 namespace sphx {
 
-#ifndef SPH_ABLATE
-#define SPH_ABLATE 0  // diagnostic builds: 1 = no pair body, 2 = no candidate test/body, 3 = 2 + no staging
-                     // loads, 4 = no neighbour rows at all (item overhead only)
-#endif
 constexpr int TB = 128;        // threads per block = max p1 per item (2 waves)
 #ifndef SPH_TCAP
 #define SPH_TCAP 504
 #endif
-#ifndef SPH_TAIL_DBG
-#define SPH_TAIL_DBG 0  // 1: print every block's start/end clock of one k_fluid_tiled launch
-#endif
-#ifndef SPH_PAD
-#define SPH_PAD 8
-#endif
-#ifndef SPH_WAVES
-#define SPH_WAVES 0  // >0: register budget of the fluid kernel for that many waves per SIMD (512/n VGPRs)
-#endif
-#if SPH_WAVES
-#define SPH_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(SPH_WAVES, SPH_WAVES)))
-#else
-#define SPH_WAVES_ATTR
-#endif
-// staged neighbour records per segment.  504 (+8 over-read pad) puts the block at
-// 20.3 KB of LDS, the most that keeps 8 blocks = 4 waves per SIMD.  Measured at 1M:
-// 0.806 ms vs 0.838 at 416 (a mirrored row pair fits one segment for 94% of the units
-// instead of 81%); 0.936 at 580 (7 blocks/CU), 1.02 at 672 (6 blocks/CU).
+// staged neighbour records per segment.  504 puts the block at 20.3 KB of LDS, the most
+// that keeps 8 blocks = 4 waves per SIMD.  Measured at 1M: 0.806 ms vs 0.838 at 416 (a
+// mirrored row pair fits one segment for 94% of the units instead of 81%); 0.936 at 580
+// (7 blocks/CU), 1.02 at 672 (6 blocks/CU).  The position records (sA) are followed by
+// the velrhop records (sB) in ONE LDS array in every tiled kernel, so the candidate
+// test's last group of 32 (up to 31 records past a window ending at the capacity) reads
+// inside that array; its bits are masked off.
 constexpr int TCAP = SPH_TCAP;
 // With floating bodies a record is 48 B (the third part a float4): 416 records keep the
 // block at <= 20 KB of LDS, i.e. the same 8 blocks (4 waves/SIMD) per CU.
@@ -53,59 +38,14 @@ constexpr int TMAXCELLS = 4;   // max x-cells per item (CellMode=full: cells of 
 #define SPH_TMAXCELLS_HALF 32
 #endif
 constexpr int TMAXCELLS_HALF = SPH_TMAXCELLS_HALF;
-#ifndef SPH_TEST32
-#define SPH_TEST32 1  // candidate tests in groups of 32 through VCC + v_addc (test32); 0: 8-bit groups
-#endif
-
-// Candidate test of one window of n (<= 64) staged records -> one 64-bit mask (as
-// test128; used for the short 5-cell windows of CellMode=half).
-__device__ __forceinline__ unsigned test32(const float4* __restrict__ b, float px2, float py2, float pz2,
-                                           float thr);
-__device__ __forceinline__ unsigned long long test64(const float4* __restrict__ sA, int s0, int n, float px2,
-                                                     float py2, float pz2, float thr) {
-  unsigned long long m = 0ull;
-  const float4* __restrict__ b = sA + s0;
-#if SPH_TEST32
-  unsigned w[2] = {0u, 0u};
-#pragma unroll
-  for (int g = 0; g < 2; g++) {
-    const int left = n - g * 32;
-    if (left <= 0) break;
-    w[g] = test32(b + g * 32, px2, py2, pz2, thr) & (left >= 32 ? ~0u : ((1u << left) - 1u));
-  }
-  return (static_cast<unsigned long long>(w[1]) << 32) | w[0];
-#endif
-  for (int jo = 0; jo < 8; jo++) {
-    const int left = n - jo * 8;
-    if (left <= 0) break;
-    unsigned bits = 0;
-#pragma unroll
-    for (int ji = 0; ji < 8; ji++) {
-      const float4 A = b[jo * 8 + ji];
-      const float q = fmaf(px2, A.x, fmaf(py2, A.y, fmaf(pz2, A.z, A.w)));
-      bits |= (q <= thr) ? (1u << ji) : 0u;
-    }
-    bits &= (left >= 8 ? 0xffu : ((1u << left) - 1u));
-    m |= (unsigned long long)bits << (jo * 8);
-  }
-  return m;
-}
 
 // Staged position records read whole: the drain uses x, y, z only, and a 12-B LDS read
 // (ds_read_b96) is serviced in 8 lane groups of 8 = 8 LDS cycles per wave-instruction,
 // against 4 for the 16-B ds_read_b128 (MI355X_MICROARCH.md §LDS).  An empty asm at the end
 // of the drain iteration takes the records' .w as operands, so the compiler keeps the full
 // 16-B loads without waiting for them earlier than their other uses.
-#ifndef SPH_LDS128
-#define SPH_LDS128 1
-#endif
 __device__ __forceinline__ void keep_w(const float4& a, const float4& b) {
-#if SPH_LDS128
   asm volatile("" ::"v"(a.w), "v"(b.w));
-#else
-  (void)a;
-  (void)b;
-#endif
 }
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
@@ -115,16 +55,14 @@ __device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x
 
 constexpr unsigned ITEM_BOUND = 0x80000000u;  // flag in item.x: p1 are boundary particles
 
-// Candidate test of one window: n (<= 128) staged records from sA+s0 with the expanded
-// form |p-A|^2 = |p|^2 + |A|^2 - 2 p.A (3 FMAs + 1 compare per candidate on one
-// ds_read_b128) against a threshold inflated by 1e-4 (the expanded form rounds to ~1e-6
-// relative); the body recomputes |p-A|^2 exactly and applies the reference's test, so no
-// pair is lost or added.  sA is padded past TCAP, so the 8-wide groups may over-read;
-// those bits are masked off.  n <= 0 gives empty masks.
+// Candidate test with the expanded form |p-A|^2 = |p|^2 + |A|^2 - 2 p.A (3 FMAs + 1
+// compare per candidate on one ds_read_b128) against a threshold inflated by 1e-4 (the
+// expanded form rounds to ~1e-6 relative); the body recomputes |p-A|^2 exactly and applies
+// the reference's test, so no pair is lost or added.
 // 32 candidates b[0..31] -> bits (bit k = candidate k): the compare lands in VCC and
 // v_addc_co_u32 shifts it in (bits = 2 bits + vcc), two VALU per candidate besides the 3
-// FMAs instead of compare + select + or and the 8-bit group assembly.  Candidates in
-// descending order so candidate k ends at bit k.  (VCC only: no memory access.)
+// FMAs instead of compare + select + or.  Candidates in descending order so candidate k
+// ends at bit k.  (VCC only: no memory access.)
 __device__ __forceinline__ unsigned test32(const float4* __restrict__ b, float px2, float py2, float pz2,
                                            float thr) {
   unsigned bits = 0u;
@@ -137,39 +75,38 @@ __device__ __forceinline__ unsigned test32(const float4* __restrict__ b, float p
   return bits;
 }
 
-__device__ __forceinline__ void test128(const float4* __restrict__ sA, int s0, int n, float px2, float py2,
-                                        float pz2, float thr, unsigned long long& m0, unsigned long long& m1) {
-  m0 = 0ull;
-  m1 = 0ull;
+// One window of n (<= 32 * NG) staged records from sA + s0 in groups of 32 -> words w[NG]
+// (a group past the window's end reads up to 31 records beyond it, inside the staging
+// array, and its bits are masked off).  n <= 0 gives empty words.
+template <int NG>
+__device__ __forceinline__ void test_groups(const float4* __restrict__ sA, int s0, int n, float px2, float py2,
+                                            float pz2, float thr, unsigned (&w)[NG]) {
   const float4* __restrict__ b = sA + s0;
-#if SPH_TEST32
-  // groups of 32 (a group past the window's end reads beyond the staged records: LDS of
-  // this block or out of range, read as 0; its bits are masked off)
-  unsigned w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-  for (int g = 0; g < 4; g++) {
+  for (int g = 0; g < NG; g++) w[g] = 0u;
+#pragma unroll
+  for (int g = 0; g < NG; g++) {
     const int left = n - g * 32;
     if (left <= 0) break;
     w[g] = test32(b + g * 32, px2, py2, pz2, thr) & (left >= 32 ? ~0u : ((1u << left) - 1u));
   }
+}
+
+// A window of <= 64 candidates -> one 64-bit mask (the short 5-cell windows of CellMode=half).
+__device__ __forceinline__ unsigned long long test64(const float4* __restrict__ sA, int s0, int n, float px2,
+                                                     float py2, float pz2, float thr) {
+  unsigned w[2];
+  test_groups<2>(sA, s0, n, px2, py2, pz2, thr, w);
+  return (static_cast<unsigned long long>(w[1]) << 32) | w[0];
+}
+
+// A window of <= 128 candidates -> two 64-bit masks.
+__device__ __forceinline__ void test128(const float4* __restrict__ sA, int s0, int n, float px2, float py2,
+                                        float pz2, float thr, unsigned long long& m0, unsigned long long& m1) {
+  unsigned w[4];
+  test_groups<4>(sA, s0, n, px2, py2, pz2, thr, w);
   m0 = (static_cast<unsigned long long>(w[1]) << 32) | w[0];
   m1 = (static_cast<unsigned long long>(w[3]) << 32) | w[2];
-  return;
-#endif
-  for (int jo = 0; jo < 16; jo++) {
-    const int left = n - jo * 8;
-    if (left <= 0) break;
-    unsigned bits = 0;
-#pragma unroll
-    for (int ji = 0; ji < 8; ji++) {
-      const float4 A = b[jo * 8 + ji];
-      const float q = fmaf(px2, A.x, fmaf(py2, A.y, fmaf(pz2, A.z, A.w)));
-      bits |= (q <= thr) ? (1u << ji) : 0u;
-    }
-    bits &= (left >= 8 ? 0xffu : ((1u << left) - 1u));
-    if (jo < 8) m0 |= (unsigned long long)bits << (jo * 8);
-    else m1 |= (unsigned long long)bits << ((jo - 8) * 8);
-  }
 }
 
 // Which p1 of the item each lane computes.  A lane's drain loops run as long as the
@@ -217,9 +154,6 @@ __device__ __forceinline__ unsigned lane_order(const float4* __restrict__ poscel
 // was worth less than the balance (neighbour rows are MALL hits either way).  Dealt in
 // chunks of 16 consecutive items (chunks of 1, 4, 16: same time) the L2-miss traffic of
 // the cfg2 interaction is 228 MB per launch instead of 397 MB.
-#ifndef SPH_ITEM_REV
-#define SPH_ITEM_REV 0  // diagnostic: 1 deals each kind top rows first (+1.3 % at 1M)
-#endif
 #ifndef SPH_ITEM_CHUNK
 #define SPH_ITEM_CHUNK 16  // round-robin granularity in items (a power of two)
 #endif
@@ -236,11 +170,7 @@ struct ItemDeal {
   }
   __device__ __forceinline__ unsigned item(unsigned g, unsigned c) const {
     constexpr unsigned CH = SPH_ITEM_CHUNK;
-#if SPH_ITEM_REV  // diagnostic: the kind's items in reverse order (top rows first)
-    return lo + (n - 1u - ((g + 8u * (c / CH)) * CH + (c % CH)));
-#else
     return lo + (g + 8u * (c / CH)) * CH + (c % CH);
-#endif
   }
 };
 struct ItemGroup {

@@ -3,10 +3,11 @@
 The small reference fixtures pin every formulation; these tests check the numbers the
 bench times, at full size:
 
-* cfg3, 3-D dam break of 9,969,118 particles, Symplectic + DDT (Molteni) 0.1: the GPU
-  after 1 and 2 steps against the oracle (the C++ restatement of JSphCpu pinned to the
-  reference's PARTs, tests/test_oracle_golden.py) at the step tolerances of
-  test_gpu_parity;
+* cfg2 (1,025,964 particles, Verlet + DDT2) and cfg3 (9,969,118 particles, Symplectic +
+  DDT (Molteni) 0.1): the GPU after 1 and 2 steps against the REFERENCE v5.2 solver run
+  here on the case gencase_ref writes, and cfg3 also against the oracle (the C++
+  restatement of JSphCpu pinned to the reference's PARTs, tests/test_oracle_golden.py),
+  at the step tolerances of test_gpu_parity;
 * cfg4, wave flume of 4,007,978 particles with a piston, a flap and a floating box, mDBC,
   Verlet + DDT2: the GPU after 1 and 2 steps against the REFERENCE v5.2 solver run here on
   the case genflume_ref writes (PARTs and the body state of PartFloat.fbi4), then 4 slabs
@@ -92,6 +93,45 @@ def test_cfg3_10m_matches_oracle():
         _check(by_idp(g.particles()), by_idp(o.particles()), tol(k), k)
         assert g.stats()["time"] == pytest.approx(o.stats()["time"], rel=1e-7)
     assert g.stats()["error_flags"] == 0
+
+
+def _dambreak_vs_reference(dp, step_algorithm, ddt, np_expected):
+    """The dam break of spacing dp as gencase_ref writes it for the reference, loaded by the
+    case-file reader; the GPU after 1 and 2 steps against the REFERENCE v5.2 CPU solver run
+    here on the same files (PARTs with double positions), at the step tolerances of
+    test_gpu_parity (10x the reference's fast-math noise floor)."""
+    _need("gencase_ref", "DualSPHysics5.2CPU_ref", "partdump_ref")
+    from dualsphysics_multilayer_amd.xmlcase import XmlCase
+
+    tmp = tempfile.mkdtemp(prefix="dambreak_")
+    try:
+        subprocess.check_call([os.path.join(REF, "gencase_ref"), repr(dp), tmp, str(step_algorithm), str(ddt), "1.5",
+                               "CaseDambreak", "1"], stdout=subprocess.DEVNULL)
+        case = XmlCase(os.path.join(tmp, "CaseDambreak"))
+        assert case.np == np_expected
+        ref, _ = _ref_parts("DualSPHysics5.2CPU_ref", os.path.join(tmp, "CaseDambreak"), 2, (1, 2), tmp, "ref")
+        g = _gpu(case)
+        done = 0
+        for k in (1, 2):
+            g.run(k - done)
+            done = k
+            _check(by_idp(g.particles()), ref[k], tol(k), k)
+            assert abs(g.stats()["time"] - ref[k]["time"]) <= 1e-9
+        assert g.stats()["error_flags"] == 0
+    finally:
+        shutil.rmtree(tmp)
+
+
+@pytest.mark.timeout(900)
+def test_cfg2_1m_matches_reference():
+    """BASELINE cfg2 (1,025,964 particles, Verlet, DDT2) against the reference binary."""
+    _dambreak_vs_reference(0.0045, 1, 2, 1025964)
+
+
+@pytest.mark.timeout(1500)
+def test_cfg3_10m_matches_reference():
+    """BASELINE cfg3 (9,969,118 particles, Symplectic, DDT Molteni) against the reference binary."""
+    _dambreak_vs_reference(CFG3_DP, 2, 1, 9969118)
 
 
 # ---- cfg4 -----------------------------------------------------------------------------------

@@ -88,6 +88,45 @@ def test_half_cells_match_oracle(ddt):
     assert np.abs(ig["ace"] - io["ace"]).max() <= 2e-4 * np.abs(io["ace"]).max()
     assert np.abs(ig["ar"] - io["ar"]).max() <= 2e-4 * np.abs(io["ar"]).max()
 
+def _restart_case(case, solver):
+    """The case with the solver's current state as its initial particles (idp order)."""
+    p = by_idp(solver.particles())
+    assert np.array_equal(p["idp"], np.arange(case.np)), "excluded particles"
+    case.pos[:] = p["pos"]
+    case.vel[:] = p["vel"]
+    case.rhop[:] = p["rhop"]
+    return case
+
+
+@pytest.mark.parametrize("size", ["57k", "1m"])
+@pytest.mark.parametrize("cellmode", [1, 2])
+@pytest.mark.parametrize("ddt", [0, 1, 2, 3])
+def test_interaction_identical_input(ddt, cellmode, size):
+    """SURVEY §7's minimum-slice bar: ONE Interaction_Forces (JSphCpu.cpp:548-822) on
+    IDENTICAL input -- the GPU state after k steps of a developing dam break, loaded into a
+    fresh GPU solver and into the oracle -- agrees per particle within 1e-5 of the array's
+    maximum for ar (continuity + the DDT term, as the reference adds Delta into Arc) and
+    ace, and within 1e-5 relative for the three maxima (VelMax, AceMax, ViscDtMax).  DDT
+    0-3, CellMode full and half, at the cfg1 (57k) and cfg2 (1M) sizes."""
+    dp, k = (0.0127, 40) if size == "57k" else (0.0045, 15)
+    case = DamBreakCase(dp, tdensity=ddt, cellmode=cellmode, celldomfixed=True)
+    src = gpu(case)
+    src.run(k)
+    case = _restart_case(case, src)
+    del src
+    g, o = gpu(case), oracle.OracleSolver(case, nthreads=16)
+    assert np.array_equal(g.particles()["idp"], o.particles()["idp"])
+    ig, io = g.interaction(), o.interaction()
+    ace_err = np.abs(ig["ace"] - io["ace"]).max() / np.abs(io["ace"]).max()
+    ar_err = np.abs(ig["ar"] - io["ar"]).max() / np.abs(io["ar"]).max()
+    print("ddt %d cellmode %d %s: ace %.2e ar %.2e of max" % (ddt, cellmode, size, ace_err, ar_err))
+    assert ace_err <= 1e-5, ace_err
+    assert ar_err <= 1e-5, ar_err
+    assert ig["velmax"] == pytest.approx(io["velmax"], rel=1e-5)
+    assert ig["acemax"] == pytest.approx(io["acemax"], rel=1e-5)
+    assert ig["viscdtmax"] == pytest.approx(io["viscdtmax"], rel=1e-5)
+
+
 def test_interaction_first_step_tight():
     """At t=0 (v=0) the interaction inputs are identical: ar/ace agree to float rounding."""
     case = DamBreakCase(0.02, tdensity=0, celldomfixed=True)

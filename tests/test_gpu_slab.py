@@ -281,3 +281,40 @@ def test_half_cell_partition_keeps_two_columns():
     assert (np.diff(b) >= 2).all() and b[-1] == ncx
     with pytest.raises(Exception):
         SphSlabGroup(case, np.array([0, 1, ncx], np.int32))
+
+
+def test_half_cell_one_slab_matches_single_domain():
+    """One slab holding every column with CellMode=half: its grid is the domain plus
+    W = 2 ghost columns per face, the widest a slab grid gets, so the grid-sized buffers
+    (begincell, items, the incremental divide's box table) must hold it; the run must
+    equal the single domain within the 20-step noise tolerance."""
+    case = DamBreakCase(0.025, cellmode=2)
+    from dualsphysics_multilayer_amd.core import case_derive
+
+    ncx = case_derive(case.case_def())["dom_cells"][0]
+    grp, one = group(case, 1, np.array([0, ncx], np.int32)), single(case)
+    grp.run(20)
+    one.run(20)
+    assert grp.stats()[0]["np"] == one.stats()["np"] == case.np
+    check_close(grp.particles(), by_idp(one.particles()), 20)
+
+
+def test_fatal_error_halts_every_slab_at_the_same_step():
+    """ERR_BOUNDOUT raised by ONE slab's divide (the piston of the wave flume driven out of
+    the map through x < MapRealPosMin: AbortBoundOut) travels with the dt maxima's
+    all-reduce, so every slab stops at the same step and the group run raises, as the one
+    reference domain stops the whole run."""
+    from dualsphysics_multilayer_amd.case import WaveFlumeCase
+    from dualsphysics_multilayer_amd.core import SphError
+
+    case = WaveFlumeCase(0.03)
+    pist = dict(case.motion["movs"][0])
+    pist["vec"], pist["vec2"] = (5.0, 0.0, 0.0), (-0.5, 0.0, 0.0)  # 5 Hz, 0.5 m towards -x
+    case.motion = dict(case.motion, movs=[pist] + list(case.motion["movs"][1:]))
+    grp = group(case, 3)
+    with pytest.raises(SphError, match="boundary particles were excluded"):
+        grp.run(80)
+    st = grp.stats()
+    assert len({s["nstep"] for s in st}) == 1 and 0 < st[0]["nstep"] < 80, [s["nstep"] for s in st]
+    assert len({s["time"] for s in st}) == 1
+    assert all(s["error_flags"] & 2 for s in st), [s["error_flags"] for s in st]
