@@ -5,7 +5,7 @@ import ctypes as C
 
 import numpy as np
 
-SPH_ABI_VERSION = 6
+SPH_ABI_VERSION = 7
 
 SPH_STATUS = {
     0: "SPH_OK",
@@ -178,6 +178,16 @@ class SphConstants(C.Structure):
         ("pad3", C.c_int32),
         ("spssmag", C.c_float),
         ("spsblin", C.c_float),
+        ("kernel", C.c_int32),
+        ("cub_a1", C.c_float),
+        ("cub_a2", C.c_float),
+        ("cub_aa", C.c_float),
+        ("cub_a24", C.c_float),
+        ("cub_c1", C.c_float),
+        ("cub_d1", C.c_float),
+        ("cub_c2", C.c_float),
+        ("cub_od_wdeltap", C.c_float),
+        ("pad4", C.c_int32),
     ]
 
     def as_dict(self) -> dict:

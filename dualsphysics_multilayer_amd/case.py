@@ -78,6 +78,7 @@ class DamBreakCase:
     shift_mode: int = 0
     shift_coef: float = -2.0
     shift_tfs: float = 0.0
+    kernel: int = 2  # <parameter Kernel>: 1 Cubic spline, 2 Wendland (JSph.cpp:554-559)
     # generated
     pos: np.ndarray = field(init=False, repr=False)
     vel: np.ndarray = field(init=False, repr=False)
@@ -127,7 +128,8 @@ class DamBreakCase:
         hd = self.dp * 0.5
         nor = np.zeros((bi.size, 3))
         nor[:, 0] = np.where(bi == 0, hd, np.where(bi == nx, -hd, 0.0))
-        nor[:, 1] = np.where(bj == 0, hd, np.where(bj == ny, -hd, 0.0))
+        if not getattr(self, "data2d", False):  # 2-D: no y walls, no y normal
+            nor[:, 1] = np.where(bj == 0, hd, np.where(bj == ny, -hd, 0.0))
         nor[:, 2] = np.where(bk == 0, hd, 0.0)
         return nor
 
@@ -219,7 +221,7 @@ class DamBreakCase:
             cflnumber=self.cflnumber,
             step_algorithm=self.step_algorithm,
             verlet_steps=self.verlet_steps,
-            kernel=2,
+            kernel=getattr(self, "kernel", 2),
             tdensity=self.tdensity,
             visco=self.visco,
             viscoboundfactor=self.viscoboundfactor,

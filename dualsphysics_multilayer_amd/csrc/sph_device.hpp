@@ -79,6 +79,10 @@ struct KConst {
   float shiftcoef;      // ShiftCoef
   double coeftfs;       // (Simulate2D ? 2 : 3) - ShiftTFS
   int nnbi;             // NN: some phase has a bi-viscosity region (tau_max != 0)
+  // kernel: 0 Wendland, 1 Cubic spline (StKCubicCte, FunSphKernel.h:51-84); kfold = the
+  // per-pass kernel factor folded out of the tiled sums (bwen/h, or 1 for the Cubic)
+  int cubic;
+  float kfold, cub_a2, cub_a24, cub_c1, cub_d1, cub_c2, cub_odw;
 };
 
 // NN phase constants on the device, two float4 per phase (sph_nn.hip loads them to LDS):

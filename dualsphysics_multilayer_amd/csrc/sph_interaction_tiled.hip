@@ -235,11 +235,24 @@ template <int TDENSITY, int MODE, bool FT = false, typename CR = float2>
 __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float drx, float dry, float drz, float rr2,
                                           bool ok, const float4& B, const CR& C, const PassK& Q, TAcc& a) {
   constexpr int TD = TDENSITY & 7;  // DDT mode; bit 3: the Fourtakas term as its series (K.ddtseries)
+  constexpr bool CUB = (TDENSITY & 16) != 0;  // bit 4: the Cubic spline kernel
   const float rad = fsqrt_(rr2);
-  // 1 - rad/2h clamped to [0, 1] (the fma's clamp modifier): 0 beyond the support radius,
-  // so the kernel factor needs no pair test
-  const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
-  const float w3 = wq * wq * wq;
+  float w3, wqc = 0.f, qc = 0.f;
+  if (CUB) {
+    // GetKernelCubic_Fac (FunSphKernel.h:105-117) with its constants not folded (PassK
+    // carries kfold = 1): c2 (2-q)^2 / r beyond h, (c1 q + d1 q^2) / r = (c1 + d1 q) / h
+    // within it (finite at r = 0); 2 - q clamped at 0, so nothing beyond the support
+    qc = rad * K.ovkernelh;
+    wqc = fmaxf(2.f - qc, 0.f);
+    const float ffar = K.cub_c2 * wqc * wqc * frcp(rad);
+    const float fnear = fmaf(K.cub_d1, qc, K.cub_c1) * K.ovkernelh;
+    w3 = rad > K.kernelh ? ffar : fnear;
+  } else {
+    // 1 - rad/2h clamped to [0, 1] (the fma's clamp modifier): 0 beyond the support radius,
+    // so the kernel factor needs no pair test
+    const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
+    w3 = wq * wq * wq;
+  }
   const float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
   const float dot = drx * dvx + dry * dvy + drz * dvz;
   const float re = rr2 + K.eta2;
@@ -256,7 +269,21 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
   const float wc = w3 * C.y;  // w3/rho2
   a.ar = fmaf(wc, dot, a.ar);
   if (MODE == 2) return;
-  const float S = fmaf(C.y, p.press, C.x);  // (p1+p2)/rho2
+  float S = fmaf(C.y, p.press, C.x);  // (p1+p2)/rho2
+  if (CUB) {
+    // tensile correction GetKernelCubic_Tensil (FunSphKernel.h:141-149) added to
+    // (p1+p2)/(rho1 rho2) (JSphCpu.cpp:713), here times rho1 (and the mass ratio r):
+    // fab (p1/rho1^2 k1 + p2/rho2^2 k2), fab = (Wab / Wab(dp))^4, k = 0.01 (p > 0) or -0.2
+    const float wab = rad > K.kernelh ? K.cub_a24 * (wqc * wqc * wqc)
+                                      : K.cub_a2 * fmaf(fmaf(0.75f, qc, -1.5f), qc * qc, 1.f);
+    float fab = wab * K.cub_odw;
+    fab *= fab;
+    fab *= fab;
+    const float r = crec_r(C);
+    const float t1 = p.press * p.inv_rho * p.inv_rho * (p.press > 0.f ? 0.01f : -0.2f);
+    const float t2 = C.x * C.y * (C.x > 0.f ? 0.01f : -0.2f) * frcp(r);  // r^2 p2/rho2^2 / r
+    S = fmaf(fab * p.vr.w, fmaf(r, t1, t2), S);
+  }
   float pv = Q.cvp * fminf(dot, 0.f) * rr;  // artificial viscosity only for approaching pairs
   if (FT) pv *= crec_r(C);  // viscosity with the p2 mass
   const float c = w3 * (S + pv);
@@ -493,7 +520,7 @@ __device__ __forceinline__ void stage_row(const KConst& K, unsigned rs, unsigned
 // Per-pass constants of the pair body for p2 of mass m2 (the Wendland bwen/h folded in).
 __device__ __forceinline__ PassK pass_k(const KConst& K, float cvisc, float m2, float rho1) {
   PassK q;
-  q.bm = K.bwenovh * m2;
+  q.bm = K.kfold * m2;
   q.ar1 = q.bm * rho1;
   q.cvp = 2.f * cvisc * rho1 / m2;
   q.kd = K.ddtkhcs * q.bm;
@@ -824,7 +851,8 @@ static void launch_fluid_tiled_s(hipStream_t stm, unsigned nblocks, DevScalars* 
   hipLaunchKernelGGL((k_fluid_tiled<TD, FTB, S>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell,   \
                      velrhop, press, begincell, g, K, arace, ft)
   // DDT 2/3 with the binomial series of the hydrostatic term (K.ddtseries) as TDENSITY | 8
-  const int td = (K.tdensity >= 2 && K.ddtseries) ? K.tdensity | 8 : K.tdensity;
+  // and the Cubic spline kernel as TDENSITY | 16
+  const int td = ((K.tdensity >= 2 && K.ddtseries) ? K.tdensity | 8 : K.tdensity) | (K.cubic ? 16 : 0);
   if (ft.massp) {
     switch (td) {
       case 0: SPH_TILED(0, true); break;
@@ -832,7 +860,13 @@ static void launch_fluid_tiled_s(hipStream_t stm, unsigned nblocks, DevScalars* 
       case 2: SPH_TILED(2, true); break;
       case 3: SPH_TILED(3, true); break;
       case 10: SPH_TILED(10, true); break;
-      default: SPH_TILED(11, true); break;
+      case 11: SPH_TILED(11, true); break;
+      case 16: SPH_TILED(16, true); break;
+      case 17: SPH_TILED(17, true); break;
+      case 18: SPH_TILED(18, true); break;
+      case 19: SPH_TILED(19, true); break;
+      case 26: SPH_TILED(26, true); break;
+      default: SPH_TILED(27, true); break;
     }
   } else {
     switch (td) {
@@ -841,7 +875,13 @@ static void launch_fluid_tiled_s(hipStream_t stm, unsigned nblocks, DevScalars* 
       case 2: SPH_TILED(2, false); break;
       case 3: SPH_TILED(3, false); break;
       case 10: SPH_TILED(10, false); break;
-      default: SPH_TILED(11, false); break;
+      case 11: SPH_TILED(11, false); break;
+      case 16: SPH_TILED(16, false); break;
+      case 17: SPH_TILED(17, false); break;
+      case 18: SPH_TILED(18, false); break;
+      case 19: SPH_TILED(19, false); break;
+      case 26: SPH_TILED(26, false); break;
+      default: SPH_TILED(27, false); break;
     }
   }
 #undef SPH_TILED

@@ -1,7 +1,7 @@
 // sph_mdbc.hip — modified Dynamic Boundary Conditions (mDBC) on gfx950, SURVEY.md §8(f) row 1.
 //
-// Reference: JSphCpu::InteractionMdbcCorrectionT2<tker,sim2d=false,SLIP_Vel0>
-// (JSphCpu.cpp:1020-1187), called once per interaction before PreInteraction_Forces
+// Reference: JSphCpu::InteractionMdbcCorrectionT2<tker,sim2d,SLIP_Vel0>
+// (JSphCpu.cpp:1020-1187; the sim2d branch with its 3x3 system in x, z: :1087-1110), called once per interaction before PreInteraction_Forces
 // except in the Symplectic corrector (JSphCpuSingle.cpp:525, MDBCCorrector=0); the GPU
 // twin is KerInteractionMdbcCorrection_Dbl (JSphGpu_ker.cu:1088-1250, the MDBCFastSingle=0
 // path: the 4x4 correction matrix accumulated and inverted in double, as the CPU does).
@@ -11,6 +11,8 @@
 // Over the fluid particles within the support of the ghost node:
 //   rho_g     = sum m W,   grad rho_g = sum m gradW
 //   A (4x4)   = sum V [W, dx W, dy W, dz W; gradW, dx gradW, ...]   (V = m / rho2)
+// (2-D: A is 3x3 over (1, x, z), JSphCpu.cpp:1087-1110, Determinant3x3 / InverseMatrix3x3
+// of FunctionsMath.h:91-93,157-172.)
 // If |det A| >= 1e-3: the first-order extrapolation (A^-1 [rho_g, grad rho_g]) mirrored
 // back to the particle; else if A11 > 0 the Shepard value rho_g / A11; with no fluid the
 // density is RhopZero.  Vel0 keeps the boundary velocity (zero for fixed walls).
@@ -48,6 +50,8 @@ struct MdbcArgs {
   float cteb, ovrhopzero, gamma;
   int igamma;
   int scelldiv;
+  int cubic;  // TKernel Cubic spline: GetKernelCubic_WabFac (FunSphKernel.h:122-136)
+  float kh, cub_a2, cub_a24, cub_c1, cub_d1, cub_c2;
 };
 
 // fmath::Determinant4x4 (FunctionsMath.h:186-199), double.
@@ -182,7 +186,7 @@ __global__ __launch_bounds__(256) void k_mdbc_list(const DevScalars* __restrict_
 // round with all loads issued before the arithmetic (the kernel is bound by the latency
 // of these L2 reads, not by its FP work).  The 5 float and 16 double partial sums are
 // reduced across the wave in a fixed butterfly order (deterministic) and lane 0 solves.
-template <int SD>
+template <int SD, bool D2>
 __global__ __launch_bounds__(256) void k_mdbc(
     const DevScalars* __restrict__ sc, MdbcArgs a, DivGrid g,
                                               const unsigned* __restrict__ list, const unsigned* __restrict__ nlist) {
@@ -279,11 +283,23 @@ __global__ __launch_bounds__(256) void k_mdbc(
           // form (bwen/h)(1-q/2)^3, finite when a fluid particle sits on the ghost node.
           const float rad = sqrtf(rr2);
           const float qq = rad * a.ovh;
-          const float wqq1 = 1.f - 0.5f * qq;
-          const float wqq2 = wqq1 * wqq1;
-          const float fac = a.bwenovh * wqq2 * wqq1;
-          const float wqq = qq + qq + 1.f;
-          const float wab = a.awen * wqq * wqq2 * wqq2;
+          float fac, wab;
+          if (a.cubic) {  // wave-uniform; fac within h as (c1 + d1 q) / h (finite at r = 0)
+            if (rad > a.kh) {
+              const float w1 = 2.f - qq, w2 = w1 * w1;
+              fac = a.cub_c2 * w2 / rad;
+              wab = a.cub_a24 * (w2 * w1);
+            } else {
+              fac = (a.cub_c1 + a.cub_d1 * qq) * a.ovh;
+              wab = a.cub_a2 * (1.f + (0.75f * qq - 1.5f) * (qq * qq));
+            }
+          } else {
+            const float wqq1 = 1.f - 0.5f * qq;
+            const float wqq2 = wqq1 * wqq1;
+            fac = a.bwenovh * wqq2 * wqq1;
+            const float wqq = qq + qq + 1.f;
+            wab = a.awen * wqq * wqq2 * wqq2;
+          }
           const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
           const float volp2 = a.massfluid / e.w;
           rhopp1 += a.massfluid * wab;
@@ -293,10 +309,16 @@ __global__ __launch_bounds__(256) void k_mdbc(
           const float vwab = wab * volp2;
           sumwab += vwab;
           const float vfrx = frx * volp2, vfry = fry * volp2, vfrz = frz * volp2;
-          m.a11 += vwab;  m.a12 += drx * vwab;  m.a13 += dry * vwab;  m.a14 += drz * vwab;
-          m.a21 += vfrx;  m.a22 += drx * vfrx;  m.a23 += dry * vfrx;  m.a24 += drz * vfrx;
-          m.a31 += vfry;  m.a32 += drx * vfry;  m.a33 += dry * vfry;  m.a34 += drz * vfry;
-          m.a41 += vfrz;  m.a42 += drx * vfrz;  m.a43 += dry * vfrz;  m.a44 += drz * vfrz;
+          if (D2) {  // a_corr2 (JSphCpu.cpp:1088-1091) in the a11..a33 slots
+            m.a11 += vwab;  m.a12 += drx * vwab;  m.a13 += drz * vwab;
+            m.a21 += vfrx;  m.a22 += drx * vfrx;  m.a23 += drz * vfrx;
+            m.a31 += vfrz;  m.a32 += drx * vfrz;  m.a33 += drz * vfrz;
+          } else {
+            m.a11 += vwab;  m.a12 += drx * vwab;  m.a13 += dry * vwab;  m.a14 += drz * vwab;
+            m.a21 += vfrx;  m.a22 += drx * vfrx;  m.a23 += dry * vfrx;  m.a24 += drz * vfrx;
+            m.a31 += vfry;  m.a32 += drx * vfry;  m.a33 += dry * vfry;  m.a34 += drz * vfry;
+            m.a41 += vfrz;  m.a42 += drx * vfrz;  m.a43 += dry * vfrz;  m.a44 += drz * vfrz;
+          }
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -322,6 +344,7 @@ __global__ __launch_bounds__(256) void k_mdbc(
 
 // Pass 3, one lane per listed particle: the reference's solve of the summed system
 // (kept out of pass 2, whose registers then hold only the accumulation).
+template <bool D2>
 __global__ __launch_bounds__(256) void k_mdbc_solve(MdbcArgs a, const unsigned* __restrict__ nlist) {
   const unsigned it = blockIdx.x * blockDim.x + threadIdx.x;
   if (it >= *nlist) return;
@@ -334,6 +357,33 @@ __global__ __launch_bounds__(256) void k_mdbc_solve(MdbcArgs a, const unsigned* 
     const float thr = a.threshold;
     if (!(sumwab >= thr || (thr >= 2.f && sumwab + 2.f >= thr))) return;
     float rhopfinal = FLT_MAX;
+    if (D2) {
+      // fmath::Determinant3x3 / InverseMatrix3x3 (FunctionsMath.h:91-93,157-172), double
+      const M4& d = m;
+      const double determ = d.a11 * d.a22 * d.a33 + d.a12 * d.a23 * d.a31 + d.a13 * d.a21 * d.a32 -
+                            d.a31 * d.a22 * d.a13 - d.a32 * d.a23 * d.a11 - d.a33 * d.a21 * d.a12;
+      if (fabs(determ) >= double(a.determlimit)) {
+        const double i11 = (d.a22 * d.a33 - d.a23 * d.a32) / determ;
+        const double i12 = -(d.a12 * d.a33 - d.a13 * d.a32) / determ;
+        const double i13 = (d.a12 * d.a23 - d.a13 * d.a22) / determ;
+        const double i21 = -(d.a21 * d.a33 - d.a23 * d.a31) / determ;
+        const double i22 = (d.a11 * d.a33 - d.a13 * d.a31) / determ;
+        const double i23 = -(d.a11 * d.a23 - d.a13 * d.a21) / determ;
+        const double i31 = (d.a21 * d.a32 - d.a22 * d.a31) / determ;
+        const double i32 = -(d.a11 * d.a32 - d.a12 * d.a31) / determ;
+        const double i33 = (d.a11 * d.a22 - d.a12 * d.a21) / determ;
+        const float rhoghost = float(i11 * rhopp1 + i12 * gx_ + i13 * gz_);
+        const float grx = -float(i21 * rhopp1 + i22 * gx_ + i23 * gz_);
+        const float grz = -float(i31 * rhopp1 + i32 * gx_ + i33 * gz_);
+        rhopfinal = (rhoghost + grx * (-bn.x) + grz * (-bn.z));  // JSphCpu.cpp:1099
+      } else if (m.a11 > 0) {
+        rhopfinal = float(rhopp1 / m.a11);
+      }
+      rhopfinal = (rhopfinal != FLT_MAX ? rhopfinal : a.rhopzero);
+      a.velrhop[p1].w = rhopfinal;
+      a.press[p1] = eos_press(a, rhopfinal);
+      return;
+    }
     const double determ = det4(m);
     if (fabs(determ) >= double(a.determlimit)) {
       // Rows of fmath::InverseMatrix4x4 (FunctionsMath.h:260-282) that the extrapolation reads.
@@ -402,20 +452,30 @@ void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const P
   a.gamma = K.gamma;
   a.igamma = (K.gamma == float(int(K.gamma)) && K.gamma >= 1.f && K.gamma <= 16.f) ? int(K.gamma) : 0;
   a.scelldiv = K.scelldiv;
+  a.cubic = K.cubic;
+  a.kh = K.kernelh;
+  a.cub_a2 = K.cub_a2;
+  a.cub_a24 = K.cub_a24;
+  a.cub_c1 = K.cub_c1;
+  a.cub_d1 = K.cub_d1;
+  a.cub_c2 = K.cub_c2;
   (void)hipMemsetAsync(nlist, 0, sizeof(unsigned), stm);
   const unsigned nb1 = (npbcap + 255u) / 256u;
   // 4 waves per block, one listed particle per wave at a time: enough blocks that the
   // latency-bound waves fill the CUs (2048 blocks left 2 waves per SIMD: 0.76 ms at 4M)
   const unsigned nb2 = std::min((npbcap + 3u) / 4u, 32768u);
+  const dim3 g3((npbcap + 255u) / 256u);
   if (K.scelldiv == 1) {
     hipLaunchKernelGGL(k_mdbc_list<1>, dim3(nb1), dim3(256), 0, stm, sc, a, g, list, nlist);
-    hipLaunchKernelGGL(k_mdbc<1>, dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
-    hipLaunchKernelGGL(k_mdbc_solve, dim3((npbcap + 255u) / 256u), dim3(256), 0, stm, a, nlist);
+    if (K.sim2d) hipLaunchKernelGGL((k_mdbc<1, true>), dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
+    else hipLaunchKernelGGL((k_mdbc<1, false>), dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
   } else {
     hipLaunchKernelGGL(k_mdbc_list<2>, dim3(nb1), dim3(256), 0, stm, sc, a, g, list, nlist);
-    hipLaunchKernelGGL(k_mdbc<2>, dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
-    hipLaunchKernelGGL(k_mdbc_solve, dim3((npbcap + 255u) / 256u), dim3(256), 0, stm, a, nlist);
+    if (K.sim2d) hipLaunchKernelGGL((k_mdbc<2, true>), dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
+    else hipLaunchKernelGGL((k_mdbc<2, false>), dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
   }
+  if (K.sim2d) hipLaunchKernelGGL(k_mdbc_solve<true>, g3, dim3(256), 0, stm, a, nlist);
+  else hipLaunchKernelGGL(k_mdbc_solve<false>, g3, dim3(256), 0, stm, a, nlist);
 }
 
 }  // namespace sphx

@@ -36,7 +36,8 @@ static unsigned cell_code(unsigned nx, unsigned ny, unsigned nz) {
 }
 
 void derive_constants(const SphCaseDef& c, SphConstants& k) {
-  if (c.kernel != SPH_KERNEL_WENDLAND) throw SphError(SPH_ERR_UNSUPPORTED, "only the Wendland kernel is implemented");
+  if (c.kernel != SPH_KERNEL_WENDLAND && c.kernel != SPH_KERNEL_CUBIC)
+    throw SphError(SPH_ERR_ARG, "Kernel choice is not valid.");
   if (c.cellmode != SPH_CELLMODE_FULL && c.cellmode != SPH_CELLMODE_HALF) throw SphError(SPH_ERR_ARG, "invalid cellmode");
   if (c.step_algorithm != SPH_STEP_VERLET && c.step_algorithm != SPH_STEP_SYMPLECTIC)
     throw SphError(SPH_ERR_ARG, "invalid step algorithm");
@@ -70,6 +71,23 @@ void derive_constants(const SphCaseDef& c, SphConstants& k) {
     k.awen = float(0.41778 / (h * h * h));
     k.bwen = float(-2.08891 / (h * h * h * h));
   }
+  k.kernel = c.kernel;
+  if (k.kernel == SPH_KERNEL_CUBIC) {  // GetKernelCubic_Ctes (FunSphKernel.h:51-84)
+    const double pi = 3.14159265358979323846;  // TypesDef.h:24
+    const double a1 = k.data2d ? 10. / (pi * 7.) : 1. / pi;
+    const double a2 = k.data2d ? a1 / (h * h) : a1 / (h * h * h);
+    const double aa = k.data2d ? a1 / (h * h * h) : a1 / (h * h * h * h);
+    const double deltap = 1. / 1.5;
+    const double wdeltap = a2 * (1. - 1.5 * deltap * deltap + 0.75 * deltap * deltap * deltap);
+    k.cub_od_wdeltap = float(1. / wdeltap);
+    k.cub_a1 = float(a1);
+    k.cub_a2 = float(a2);
+    k.cub_aa = float(aa);
+    k.cub_a24 = float(0.25 * a2);
+    k.cub_c1 = float(-3. * aa);
+    k.cub_d1 = float(9. * aa / 4.);
+    k.cub_c2 = float(-3. * aa / 4.);
+  }
   k.cs0 = std::sqrt(double(k.gamma) * double(k.cteb) / double(k.rhopzero));
   k.eta2 = float((h * 0.1) * (h * 0.1));
   k.ovrhopzero = 1.0f / k.rhopzero;
@@ -97,8 +115,6 @@ void derive_constants(const SphCaseDef& c, SphConstants& k) {
   if (k.slipmode != SPH_SLIP_VEL0)
     throw SphError(SPH_ERR_UNSUPPORTED, "Only the slip mode velocity=0 is allowed with mDBC conditions.");
   k.mdbc_threshold = (k.tboundary == SPH_BOUND_MDBC ? float(c.mdbc_threshold) : 0.f);
-  if (k.data2d && k.tboundary == SPH_BOUND_MDBC)
-    throw SphError(SPH_ERR_UNSUPPORTED, "mDBC in 2-D simulations is not implemented");
   // Rheology, viscosity and shifting options (JSph::LoadConfigParameters, JSph.cpp:608-700 of
   // the v5.0 solver; JSph.cpp:620-700 of v5.2).
   k.rheology = (c.rheology == 0 ? SPH_RHEOLOGY_SINGLE : c.rheology);
@@ -193,6 +209,16 @@ static KConst make_kconst(const SphConstants& c) {
   K.tdensity = c.tdensity;
   K.mhalfovh = -0.5f * K.ovkernelh;
   K.bwenovh = c.bwen * K.ovkernelh;
+  // Cubic spline (FunSphKernel.h:38-175): the tiled kernels evaluate its fac directly, so
+  // the per-pass factor the Wendland (bwen/h) takes is 1
+  K.cubic = (c.kernel == SPH_KERNEL_CUBIC) ? 1 : 0;
+  K.kfold = K.cubic ? 1.f : K.bwenovh;
+  K.cub_a2 = c.cub_a2;
+  K.cub_a24 = c.cub_a24;
+  K.cub_c1 = c.cub_c1;
+  K.cub_d1 = c.cub_d1;
+  K.cub_c2 = c.cub_c2;
+  K.cub_odw = c.cub_od_wdeltap;
   K.ddtkhcs = c.ddtkh * K.cs0f;
   K.awen = c.awen;
   K.mdbc = (c.tboundary == SPH_BOUND_MDBC) ? 1 : 0;
@@ -410,6 +436,10 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   if (ext_ && C.scelldiv != 1)
     throw SphError(SPH_ERR_UNSUPPORTED, "Laminar+SPS viscosity / shifting with CellMode=half is not implemented");
   if (ext_) tiled_ = true;
+  if (C.kernel == SPH_KERNEL_CUBIC && (nn_ || ext_))
+    throw SphError(SPH_ERR_UNSUPPORTED, "the Cubic spline kernel with NN multiphase / Laminar+SPS / shifting is not implemented");
+  if (C.kernel == SPH_KERNEL_CUBIC && !tiled_)
+    throw SphError(SPH_ERR_UNSUPPORTED, "the Cubic spline kernel runs on the tiled interaction only");
   if (facex_) {
     // the first interaction's face records: the initial particles of the face and ghost
     // columns (both sides of a face count the same particles); later from each exchange

@@ -406,11 +406,10 @@ class XmlCase:
 
     # -- JSph::LoadConfigParameters (the keys this core acts on; others refused) -----------
     def _load_parameters(self, p: _Params):
-        kern = p.int("Kernel", True, 2)
+        kern = p.int("Kernel", True, 2)  # JSph.cpp:554-559: 1 Cubic spline, 2 Wendland
         if kern not in (1, 2):
             raise CaseError("Kernel choice is not valid.")
-        if kern != 2:
-            raise CaseError("Only the Wendland kernel (Kernel=2) runs on the GPU path.")
+        self.kernel = kern
         rig = p.int("RigidAlgorithm", True, 1)
         if rig not in (0, 1, 2, 3):
             raise CaseError("Rigid algorithm is not valid.")
@@ -786,7 +785,7 @@ class XmlCase:
             dp=self.dp, h=self.h, cteb=self.cteb, rhop0=self.rhop0, gamma=self.gamma,
             massbound=self.massbound, massfluid=self.massfluid, gravity=tuple(self.gravity),
             cflnumber=self.cflnumber, step_algorithm=self.step_algorithm, verlet_steps=self.verlet_steps,
-            kernel=2, tdensity=self.tdensity, visco=self.visco, viscoboundfactor=self.viscoboundfactor,
+            kernel=self.kernel, tdensity=self.tdensity, visco=self.visco, viscoboundfactor=self.viscoboundfactor,
             ddtvalue=self.ddtvalue, coefdtmin=self.coefdtmin, dtini=self.dtini, dtmin=self.dtmin,
             rhopoutmin=self.rhopoutmin, rhopoutmax=self.rhopoutmax,
             map_realposmin=tuple(float(v) for v in pmin), map_realposmax=tuple(float(v) for v in pmax),

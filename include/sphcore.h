@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define SPH_ABI_VERSION 6
+#define SPH_ABI_VERSION 7
 
 typedef enum {
   SPH_OK = 0,
@@ -84,8 +84,9 @@ enum { SPH_CELLMODE_FULL = 1, SPH_CELLMODE_HALF = 2 };
  * allows only SLIP_Vel0 with mDBC (JSph.cpp:788). */
 enum { SPH_BOUND_DBC = 1, SPH_BOUND_MDBC = 2 };
 enum { SPH_SLIP_VEL0 = 1, SPH_SLIP_NOSLIP = 2, SPH_SLIP_FREESLIP = 3 };
-/* TpKernel (DualSphDef.h): only Wendland is on the hot path. */
-enum { SPH_KERNEL_WENDLAND = 2 };
+/* TpKernel (DualSphDef.h:355-359): Cubic spline (with its tensile correction) and
+ * quintic Wendland (the default). */
+enum { SPH_KERNEL_CUBIC = 1, SPH_KERNEL_WENDLAND = 2 };
 /* v5.0 NN multiphase solver (src_mphase/DSPH_v5.0_NNewtonian):
  * RheologyTreatment (JSph.cpp:608-614), VelocityGradientType (:616-621), TpVisco
  * (DualSphDef.h:374-378) and TpShifting (JSphShifting.h). */
@@ -141,7 +142,7 @@ typedef struct SphCaseDef {
   double cflnumber;
   int step_algorithm;       /* SPH_STEP_*                                  */
   int verlet_steps;         /* VerletSteps (40)                            */
-  int kernel;               /* SPH_KERNEL_WENDLAND                         */
+  int kernel;               /* SPH_KERNEL_CUBIC / SPH_KERNEL_WENDLAND      */
   int tdensity;             /* SPH_DDT_*                                   */
   double visco;             /* artificial viscosity alpha                  */
   double viscoboundfactor;
@@ -209,6 +210,10 @@ typedef struct SphConstants {
   float phase_cteb[SPH_MAXPHASES];  /* StPhaseArray.CteB                          */
   int32_t data2d, pad3;
   float spssmag, spsblin;           /* Laminar+SPS SpsSmag, SpsBlin (JSph.cpp:1438-1443) */
+  /* kernel (TKernel) and the Cubic spline constants StKCubicCte (FunSphKernel.h:51-84) */
+  int32_t kernel;
+  float cub_a1, cub_a2, cub_aa, cub_a24, cub_c1, cub_d1, cub_c2, cub_od_wdeltap;
+  int32_t pad4;
 } SphConstants;
 
 /* Step statistics kept on the device and read back on demand. */

@@ -83,7 +83,7 @@ unsigned CalcCellCode(u3 ncells) {
 // ---- JSph::ConfigConstants1/2 (JSph.cpp:1392-1457), ConfigCellDivision (:1772-1788),
 //      LoadCaseParticles map limits (:2056-2076), SelecDomain (:1794-1829) -------------
 void Derive(const SphCaseDef& c, SphConstants& k) {
-  if (c.kernel != SPH_KERNEL_WENDLAND) throw std::runtime_error("only the Wendland kernel is supported");
+  if (c.kernel != SPH_KERNEL_WENDLAND && c.kernel != SPH_KERNEL_CUBIC) throw std::runtime_error("Kernel choice is not valid.");
   if (c.cellmode != SPH_CELLMODE_FULL && c.cellmode != SPH_CELLMODE_HALF) throw std::runtime_error("invalid cellmode");
   memset(&k, 0, sizeof(k));
   // JSph::LoadConfigCtes (JSph.cpp:567-583): values narrowed to float.
@@ -115,6 +115,23 @@ void Derive(const SphCaseDef& c, SphConstants& k) {
   } else {
     k.awen = float(0.41778 / (h * h * h));  // FunSphKernel.h:198-199 (3D)
     k.bwen = float(-2.08891 / (h * h * h * h));
+  }
+  k.kernel = c.kernel;
+  if (k.kernel == SPH_KERNEL_CUBIC) {  // GetKernelCubic_Ctes (FunSphKernel.h:51-84)
+    const double pi = 3.14159265358979323846;  // TypesDef.h:24
+    const double a1 = k.data2d ? 10. / (pi * 7.) : 1. / pi;
+    const double a2 = k.data2d ? a1 / (h * h) : a1 / (h * h * h);
+    const double aa = k.data2d ? a1 / (h * h * h) : a1 / (h * h * h * h);
+    const double deltap = 1. / 1.5;
+    const double wdeltap = a2 * (1. - 1.5 * deltap * deltap + 0.75 * deltap * deltap * deltap);
+    k.cub_od_wdeltap = float(1. / wdeltap);
+    k.cub_a1 = float(a1);
+    k.cub_a2 = float(a2);
+    k.cub_aa = float(aa);
+    k.cub_a24 = float(0.25 * a2);
+    k.cub_c1 = float(-3. * aa);
+    k.cub_d1 = float(9. * aa / 4.);
+    k.cub_c2 = float(-3. * aa / 4.);
   }
   k.cs0 = std::sqrt(double(k.gamma) * double(k.cteb) / double(k.rhopzero));
   k.eta2 = float((h * 0.1) * (h * 0.1));
@@ -189,6 +206,49 @@ inline float WendlandWabFac(const SphConstants& k, float rr2, float& fac) {
   fac = k.bwen * qq * wqq2 * wqq1 / rad;
   const float wqq = qq + qq + 1.f;
   return k.awen * wqq * wqq2 * wqq2;
+}
+// Cubic spline (FunSphKernel.h:89-149): GetKernelCubic_Wab / _Fac / _WabFac / _Tensil.
+inline float CubicWab(const SphConstants& k, float rr2) {
+  const float rad = std::sqrt(rr2);
+  const float qq = rad / k.kernelh;
+  if (rad > k.kernelh) {
+    const float wqq1 = 2.0f - qq;
+    const float wqq2 = wqq1 * wqq1;
+    return k.cub_a24 * (wqq2 * wqq1);
+  }
+  const float wqq2 = qq * qq;
+  return k.cub_a2 * (1.0f + (0.75f * qq - 1.5f) * wqq2);
+}
+inline float CubicFac(const SphConstants& k, float rr2) {
+  const float rad = std::sqrt(rr2);
+  const float qq = rad / k.kernelh;
+  if (rad > k.kernelh) {
+    const float wqq1 = 2.0f - qq;
+    const float wqq2 = wqq1 * wqq1;
+    return k.cub_c2 * wqq2 / rad;
+  }
+  const float wqq2 = qq * qq;
+  return (k.cub_c1 * qq + k.cub_d1 * wqq2) / rad;
+}
+inline float CubicWabFac(const SphConstants& k, float rr2, float& fac) {
+  fac = CubicFac(k, rr2);
+  return CubicWab(k, rr2);
+}
+inline float CubicTensil(const SphConstants& k, float rr2, float rhopp1, float pressp1, float rhopp2, float pressp2) {
+  const float wab = CubicWab(k, rr2);
+  float fab = wab * k.cub_od_wdeltap;
+  fab *= fab;
+  fab *= fab;
+  const float tensilp1 = (pressp1 / (rhopp1 * rhopp1)) * (pressp1 > 0 ? 0.01f : -0.2f);
+  const float tensilp2 = (pressp2 / (rhopp2 * rhopp2)) * (pressp2 > 0 ? 0.01f : -0.2f);
+  return fab * (tensilp1 + tensilp2);
+}
+// GetKernel_Fac / GetKernel_WabFac<tker> (FunSphKernel.h:284-296), tker = TKernel.
+inline float KernelFac(const SphConstants& k, float rr2) {
+  return k.kernel == SPH_KERNEL_CUBIC ? CubicFac(k, rr2) : WendlandFac(k, rr2);
+}
+inline float KernelWabFac(const SphConstants& k, float rr2, float& fac) {
+  return k.kernel == SPH_KERNEL_CUBIC ? CubicWabFac(k, rr2, fac) : WendlandWabFac(k, rr2, fac);
 }
 inline float ComputePress(float rhop, const SphConstants& k) {
   return float(double(k.cteb) * (scalar_pow(double(rhop * k.ovrhopzero), double(k.gamma)) - 1.0f));
@@ -604,11 +664,14 @@ class Solver {
             const float drz = float(posp1.z - pos[p2].z);
             const float rr2 = drx * drx + dry * dry + drz * drz;
             if (rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO) {
-              const float fac = WendlandFac(K, rr2);
+              const float fac = KernelFac(K, rr2);
               const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
               const f4 velrhop2 = velrhop[p2];
               {  // Momentum (JSphCpu.cpp:712-716).
-                const float prs = (pressp1 + press[p2]) / (rhopp1 * velrhop2.w) + 0;
+                const float prs = (pressp1 + press[p2]) / (rhopp1 * velrhop2.w) +
+                                  (K.kernel == SPH_KERNEL_CUBIC
+                                       ? CubicTensil(K, rr2, rhopp1, pressp1, velrhop2.w, press[p2])
+                                       : 0);
                 const float p_vpm = -prs * massp2;
                 acep1.x += p_vpm * frx; acep1.y += p_vpm * fry; acep1.z += p_vpm * frz;
               }
@@ -682,7 +745,7 @@ class Solver {
             const float drz = float(posp1.z - pos[p2].z);
             const float rr2 = drx * drx + dry * dry + drz * drz;
             if (rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO) {
-              const float fac = WendlandFac(K, rr2);
+              const float fac = KernelFac(K, rr2);
               const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
               const f4 velrhop2 = velrhop[p2];
               const float dvx = velrhop1.x - velrhop2.x, dvy = velrhop1.y - velrhop2.y, dvz = velrhop1.z - velrhop2.z;
@@ -714,7 +777,7 @@ class Solver {
     if (K.data2d)
       for (unsigned p = npb; p < np; p++) ace[p].y = 0;
   }
-  // JSphCpu::InteractionMdbcCorrectionT2<Wendland,sim2d=false,SLIP_Vel0> (JSphCpu.cpp:1020-1187)
+  // JSphCpu::InteractionMdbcCorrectionT2<Wendland,sim2d,SLIP_Vel0> (JSphCpu.cpp:1020-1187)
   // over n = NpbOk boundary particles (UseNormalsFt=false; JSphCpu.cpp:1193-1210).
   void MdbcCorrection() {
     const DivData dv = GetDivData();
@@ -743,7 +806,7 @@ class Solver {
             const float rr2 = (drx * drx + dry * dry + drz * drz);
             if (rr2 <= K.kernelsize2 && CodeIsFluid(code[p2])) {
               float fac;
-              const float wab = WendlandWabFac(K, rr2, fac);
+              const float wab = KernelWabFac(K, rr2, fac);
               const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
               const f4 velrhopp2 = velrhop[p2];
               const float massp2 = K.massfluid;
@@ -755,15 +818,41 @@ class Solver {
               const float vwab = wab * volp2;
               sumwab += vwab;
               const float vfrx = frx * volp2, vfry = fry * volp2, vfrz = frz * volp2;
-              a.a11 += vwab;  a.a12 += drx * vwab;  a.a13 += dry * vwab;  a.a14 += drz * vwab;
-              a.a21 += vfrx;  a.a22 += drx * vfrx;  a.a23 += dry * vfrx;  a.a24 += drz * vfrx;
-              a.a31 += vfry;  a.a32 += drx * vfry;  a.a33 += dry * vfry;  a.a34 += drz * vfry;
-              a.a41 += vfrz;  a.a42 += drx * vfrz;  a.a43 += dry * vfrz;  a.a44 += drz * vfrz;
+              if (K.data2d) {  // a_corr2 (JSphCpu.cpp:1087-1091), kept in the a11..a33 slots
+                a.a11 += vwab;  a.a12 += drx * vwab;  a.a13 += drz * vwab;
+                a.a21 += vfrx;  a.a22 += drx * vfrx;  a.a23 += drz * vfrx;
+                a.a31 += vfrz;  a.a32 += drx * vfrz;  a.a33 += drz * vfrz;
+              } else {
+                a.a11 += vwab;  a.a12 += drx * vwab;  a.a13 += dry * vwab;  a.a14 += drz * vwab;
+                a.a21 += vfrx;  a.a22 += drx * vfrx;  a.a23 += dry * vfrx;  a.a24 += drz * vfrx;
+                a.a31 += vfry;  a.a32 += drx * vfry;  a.a33 += dry * vfry;  a.a34 += drz * vfry;
+                a.a41 += vfrz;  a.a42 += drx * vfrz;  a.a43 += dry * vfrz;  a.a44 += drz * vfrz;
+              }
             }
           }
         }
       if (sumwab >= mdbcthreshold || (mdbcthreshold >= 2 && sumwab + 2 >= mdbcthreshold)) {
         const f3 dpos{bn.x * (-1.f), bn.y * (-1.f), bn.z * (-1.f)};
+        if (K.data2d) {  // JSphCpu.cpp:1094-1110 (fmath::Determinant3x3 / InverseMatrix3x3)
+          const double d3 = a.a11 * a.a22 * a.a33 + a.a12 * a.a23 * a.a31 + a.a13 * a.a21 * a.a32 -
+                            a.a31 * a.a22 * a.a13 - a.a32 * a.a23 * a.a11 - a.a33 * a.a21 * a.a12;
+          if (std::fabs(d3) >= determlimit) {
+            const double i11 = (a.a22 * a.a33 - a.a23 * a.a32) / d3, i12 = -(a.a12 * a.a33 - a.a13 * a.a32) / d3;
+            const double i13 = (a.a12 * a.a23 - a.a13 * a.a22) / d3, i21 = -(a.a21 * a.a33 - a.a23 * a.a31) / d3;
+            const double i22 = (a.a11 * a.a33 - a.a13 * a.a31) / d3, i23 = -(a.a11 * a.a23 - a.a13 * a.a21) / d3;
+            const double i31 = (a.a21 * a.a32 - a.a22 * a.a31) / d3, i32 = -(a.a11 * a.a32 - a.a12 * a.a31) / d3;
+            const double i33 = (a.a11 * a.a22 - a.a12 * a.a21) / d3;
+            const float rhoghost = float(i11 * rhopp1 + i12 * gradrhopp1.x + i13 * gradrhopp1.z);
+            const float grx = -float(i21 * rhopp1 + i22 * gradrhopp1.x + i23 * gradrhopp1.z);
+            const float grz = -float(i31 * rhopp1 + i32 * gradrhopp1.x + i33 * gradrhopp1.z);
+            rhopfinal = (rhoghost + grx * dpos.x + grz * dpos.z);
+          } else if (a.a11 > 0) {
+            rhopfinal = float(rhopp1 / a.a11);
+          }
+          rhopfinal = (rhopfinal != FLT_MAX ? rhopfinal : K.rhopzero);
+          velrhop[p1].w = rhopfinal;
+          continue;
+        }
         const double determ = Determinant4x4(a);
         if (std::fabs(determ) >= determlimit) {
           const m4d inv = InverseMatrix4x4(a, determ);

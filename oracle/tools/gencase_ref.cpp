@@ -29,7 +29,7 @@
 int main(int argc, char** argv) {
   if (argc < 5) {
     fprintf(stderr, "usage: %s dp outdir step ddt [timemax] [casename] [boundary] [dim] [viscotreatment] [visco] "
-                    "[shifting] [shiftcoef] [shifttfs]\n", argv[0]);
+                    "[shifting] [shiftcoef] [shifttfs] [kernel]\n", argv[0]);
     return 1;
   }
   const double dp = atof(argv[1]);
@@ -50,6 +50,7 @@ int main(int argc, char** argv) {
   const int shifting = (argc > 11 ? atoi(argv[11]) : 0);
   const std::string shiftcoef = (argc > 12 ? argv[12] : "-2");
   const std::string shifttfs = (argc > 13 ? argv[13] : "0");
+  const int kernel = (argc > 14 ? atoi(argv[14]) : 2);  // 1 Cubic spline, 2 Wendland
 
   // 3-D: tank 1.6 x 0.67 x 0.4 (walls: bottom, x=0, x=L, y=0, y=W); water 0.4 x 0.67 x 0.3.
   const int nx = int(std::round((d2 ? 4.0 : 1.6) / dp)), ny = d2 ? 0 : int(std::round(0.67 / dp));
@@ -63,7 +64,9 @@ int main(int argc, char** argv) {
         if (k == 0 || i == 0 || i == nx || (!d2 && (j == 0 || j == ny))) {
           pos.push_back(TDouble3(i * dp, j * dp, k * dp));
           const double hd = dp * 0.5;
-          nor.push_back(TDouble3(i == 0 ? hd : (i == nx ? -hd : 0.), j == 0 ? hd : (j == ny ? -hd : 0.), k == 0 ? hd : 0.));
+          // 2-D: the particles sit at y = 0 and have no y walls (no y normal)
+          const double ny_ = d2 ? 0. : (j == 0 ? hd : (j == ny ? -hd : 0.));
+          nor.push_back(TDouble3(i == 0 ? hd : (i == nx ? -hd : 0.), ny_, k == 0 ? hd : 0.));
         }
   const unsigned nb = unsigned(pos.size());
   for (int k = 1; k <= mz; k++)
@@ -116,7 +119,7 @@ int main(int argc, char** argv) {
   auto par = [&](const char* k, const std::string& v) { fprintf(f, "<parameter key=\"%s\" value=\"%s\"/>\n", k, v.c_str()); };
   par("StepAlgorithm", std::to_string(step));
   par("VerletSteps", "40");
-  par("Kernel", "2");
+  par("Kernel", std::to_string(kernel));
   par("ViscoTreatment", std::to_string(tvisco));
   par("Visco", visco);
   par("ViscoBoundFactor", "1");

@@ -44,6 +44,15 @@ CASES = {
     # 2-D (Simulate2D): the CaseDambreakVal2D geometry (gencase_ref dim 2); meta[6] = 2
     "verlet_ddt2_2d_dp0.02": (0.02, 1, 2, 100, (1, 10, 100), 1, (), 2),
     "symplectic_ddt1_2d_dp0.02": (0.02, 2, 1, 60, (1, 20, 60), 1, (), 2),
+    # 2-D mDBC (the sim2d branch of InteractionMdbcCorrectionT2, JSphCpu.cpp:1087-1110)
+    "verlet_ddt2_mdbc_2d_dp0.02": (0.02, 1, 2, 100, (1, 10, 100), 2, (), 2),
+    "symplectic_ddt1_mdbc_2d_dp0.02": (0.02, 2, 1, 60, (1, 20, 60), 2, (), 2),
+    # Cubic spline kernel with its tensile correction (-cubic; FunSphKernel.h:38-175,
+    # JSphCpu.cpp:713): the kernel of examples/main/01_DamBreak/CaseDambreak_Def.xml:68; the
+    # npz carries kernel = 1
+    "verlet_ddt2_cubic_dp0.02": (0.02, 1, 2, 100, (1, 10, 100), 1, ("-cubic",)),
+    "symplectic_ddt1_cubic_mdbc_dp0.03": (0.03, 2, 1, 60, (1, 20, 60), 2, ("-cubic",)),
+    "verlet_ddt2_cubic_2d_dp0.02": (0.02, 1, 2, 100, (1, 10, 100), 1, ("-cubic",), 2),
 }
 
 
@@ -137,6 +146,8 @@ def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=(), dim=3):
         if dim != 3:
             m.append(dim)
         arrays["meta"] = np.array(m, np.float64)
+        if "-cubic" in extra:
+            arrays["kernel"] = np.int32(1)
         np.savez_compressed(os.path.join(ROOT, "tests", "golden", name + ".npz"), **arrays)
         print(name, "ok", os.path.getsize(os.path.join(ROOT, "tests", "golden", name + ".npz")))
     finally:

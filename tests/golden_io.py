@@ -38,6 +38,11 @@ def dim(g):
     return int(g["meta"][6]) if len(g["meta"]) > 6 else 3
 
 
+def kernel(g):
+    """1 Cubic spline, 2 Wendland (fixtures without the key)."""
+    return int(g["kernel"]) if "kernel" in g.files else 2
+
+
 def by_idp(p):
     o = np.argsort(p["idp"], kind="stable")
     return {k: (v[o] if isinstance(v, np.ndarray) and v.ndim >= 1 and len(v) == len(o) else v) for k, v in p.items()}

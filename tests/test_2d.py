@@ -158,3 +158,85 @@ def test_gpu_2d_slabs_match_reference():
         assert np.array_equal(got["idp"], ref["idp"])
         for q, t in zip(("pos", "vel", "rhop"), tol(k)):
             assert maxdiff(got, ref, q) <= t, (k, q, maxdiff(got, ref, q))
+
+
+# ---- 2-D mDBC: the sim2d branch of InteractionMdbcCorrectionT2 (JSphCpu.cpp:1087-1110) ----------
+MDBC_NAMES = ("verlet_ddt2_mdbc_2d_dp0.02", "symplectic_ddt1_mdbc_2d_dp0.02")
+
+
+def mdbc_case_of(g):
+    dp, step_alg, ddt, _ = meta(g)
+    return DamBreak2DCase(dp, step_algorithm=step_alg, tdensity=ddt, tboundary=2)
+
+
+def _mdbc_tol(step):
+    """10x the reference's noise floor with mDBC (tests/test_mdbc.py _tol)."""
+    if step <= 1:
+        return 1.4e-8, 2.2e-5, 1e-2
+    if step <= 20:
+        return 2e-7, 6e-5, 1e-2
+    return 2e-6, 2.1e-4, 2e-2
+
+
+def test_mdbc_2d_generator_matches_gencase_ref(tmp_path):
+    """The 2-D mDBC case (normals in x and z only) as gencase_ref writes it for the reference."""
+    exe = os.path.join(REF, "gencase_ref")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref not built")
+    from dualsphysics_multilayer_amd.xmlcase import XmlCase
+
+    subprocess.check_call([exe, "0.02", str(tmp_path), "1", "2", "1.5", "C2", "2", "2"], stdout=subprocess.DEVNULL)
+    c, x = DamBreak2DCase(0.02, tboundary=2), XmlCase(str(tmp_path / "C2"))
+    assert x.case_def() == c.case_def()
+    assert np.array_equal(x.boundnormal, c.boundnormal)
+    assert not c.boundnormal[:, 1].any()
+
+
+@pytest.mark.parametrize("name", MDBC_NAMES)
+def test_oracle_mdbc_2d_matches_reference(name):
+    oracle = pytest.importorskip("oracle.pyoracle")
+    g = load(name)
+    o = oracle.OracleSolver(mdbc_case_of(g), nthreads=4)
+    done = 0
+    for k in steps(g):
+        o.run(k - done)
+        done = k
+        got, ref = by_idp(o.particles()), snapshot(g, k)
+        assert np.array_equal(got["idp"], ref["idp"])
+        for q, t in zip(("pos", "vel", "rhop"), _mdbc_tol(k)):
+            assert maxdiff(got, ref, q) <= t, (k, q, maxdiff(got, ref, q))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", MDBC_NAMES)
+def test_gpu_mdbc_2d_matches_reference(name):
+    from dualsphysics_multilayer_amd.core import SphGpuSingle
+
+    g = load(name)
+    s = SphGpuSingle(mdbc_case_of(g), device=0)
+    done = 0
+    for k in steps(g):
+        s.run(k - done)
+        done = k
+        got, ref = by_idp(s.particles()), snapshot(g, k)
+        assert np.array_equal(got["idp"], ref["idp"])
+        for q, t in zip(("pos", "vel", "rhop"), _mdbc_tol(k)):
+            assert maxdiff(got, ref, q) <= t, (k, q, maxdiff(got, ref, q))
+        assert np.all(got["vel"][:, 1] == 0.0)
+
+
+@pytest.mark.gpu
+def test_gpu_mdbc_2d_slabs_match_reference():
+    from dualsphysics_multilayer_amd.core import SphSlabGroup, slab_partition
+
+    g = load(MDBC_NAMES[0])
+    case = mdbc_case_of(g)
+    grp = SphSlabGroup(case, slab_partition(case, 3))
+    done = 0
+    for k in steps(g):
+        grp.run(k - done)
+        done = k
+        got, ref = grp.particles(), snapshot(g, k)
+        assert np.array_equal(got["idp"], ref["idp"])
+        for q, t in zip(("pos", "vel", "rhop"), _mdbc_tol(k)):
+            assert maxdiff(got, ref, q) <= t, (k, q, maxdiff(got, ref, q))

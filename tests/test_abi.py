@@ -6,6 +6,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 from dualsphysics_multilayer_amd import _abi
@@ -92,6 +93,27 @@ def test_derived_constants_match_reference_log():
 
 def test_invalid_case_rejected():
     cdef = DamBreakCase(0.05).case_def()
-    cdef["kernel"] = 1
-    with pytest.raises(RuntimeError):
+    cdef["kernel"] = 3  # TpKernel: 1 Cubic, 2 Wendland (JSph.cpp:554-559)
+    with pytest.raises(RuntimeError, match="Kernel choice"):
         case_derive(cdef)
+
+
+def test_cubic_constants():
+    """GetKernelCubic_Ctes (FunSphKernel.h:51-84), 3-D and 2-D."""
+    import math
+
+    from dualsphysics_multilayer_amd.case import DamBreak2DCase
+
+    for c in (DamBreakCase(0.05, kernel=1), DamBreak2DCase(0.05, kernel=1)):
+        k = case_derive(c.case_def())
+        h = float(np.float32(c.h))
+        a1 = 10.0 / (math.pi * 7.0) if k["data2d"] else 1.0 / math.pi
+        a2 = a1 / h ** (2 if k["data2d"] else 3)
+        aa = a1 / h ** (3 if k["data2d"] else 4)
+        dlt = 1.0 / 1.5
+        wdp = a2 * (1.0 - 1.5 * dlt * dlt + 0.75 * dlt ** 3)
+        assert k["kernel"] == 1
+        for key, v in (("cub_a2", a2), ("cub_a24", 0.25 * a2), ("cub_c1", -3 * aa), ("cub_d1", 9 * aa / 4),
+                       ("cub_c2", -3 * aa / 4), ("cub_od_wdeltap", 1 / wdp)):
+            assert k[key] == pytest.approx(v, rel=1e-6), key
+        assert k["kernelsize"] == pytest.approx(2 * h, rel=1e-7)

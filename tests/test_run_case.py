@@ -97,7 +97,7 @@ def test_simulationdomain_with_legacy_keys_is_refused(tmp_path):
 
 
 @pytest.mark.parametrize("edit,match", [
-    (lambda x: x.replace('key="Kernel" value="2"', 'key="Kernel" value="1"'), "Wendland"),
+    (lambda x: x.replace('key="Kernel" value="2"', 'key="Kernel" value="3"'), "Kernel choice"),
     # mDBC without a <case>_Normals.nbi4 beside the case (JSph.cpp:1337)
     (lambda x: x.replace("<parameters>", '<parameters>\n<parameter key="Boundary" value="2"/>'), "normal vectors"),
     (lambda x: x.replace("<parameters>", '<parameters>\n<parameter key="Boundary" value="2"/>'
