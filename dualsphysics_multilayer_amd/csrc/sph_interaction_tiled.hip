@@ -210,6 +210,24 @@ struct PassK {
   float kd;   // ddtkh*cs0 * bwen/h * m2 (density diffusion)
 };
 
+// The Molteni DDT factor r (rho1/rho2 - 1) (JSphCpu.cpp:725-726) with the reference's
+// rounding: rho1/rho2 correctly rounded (the v_rcp estimate refined by one fma residual
+// step, exact for equal densities), then - 1 (exact: the quotient is within [0.5, 2]).
+// The float cancellation of that subtraction is part of the reference's result: the exact
+// (rho1 - rho2)/rho2 moved ar by 1.3e-5 of its maximum on the 1M state, 50x the
+// reference's own fast-math/strict floor there.  r = the p2 mass ratio (FT records).
+__device__ __forceinline__ float molteni(float rho1, float rho2, const float2& c) {
+  const float q0 = rho1 * c.y;  // c.y = 1/rho2 (v_rcp)
+  const float q = fmaf(fmaf(-rho2, q0, rho1), c.y, q0);
+  return q - 1.f;
+}
+__device__ __forceinline__ float molteni(float rho1, float rho2, const float4& c) {
+  const float ir = frcp(rho2);
+  const float q0 = rho1 * ir;
+  const float q = fmaf(fmaf(-rho2, q0, rho1), ir, q0);
+  return (q - 1.f) * c.z;  // c.z = r
+}
+
 // One pair body (JSphCpu.cpp:682-797 semantics, fast f32 intrinsics).
 // MODE 0: fluid p1 / fluid p2, 1: fluid p1 / bound p2, 2: bound p1 / fluid p2
 // (InteractionForcesBound, JSphCpu.cpp:577-612: continuity + visc-dt only).
@@ -293,18 +311,15 @@ __device__ __forceinline__ void pair_body(const KConst& K, const P1& p, float dr
   if (MODE == 1) {
     if (TD == 1 && K.mdbc) {  // mDBC: Molteni DDT over bound neighbours too (JSphCpu.cpp:730)
       const float t = w3 * rr2 * inv_re;
-      a.delta = fmaf(t, (p.vr.w - B.w) * C.y, a.delta);
+      a.delta = fmaf(t, molteni(p.vr.w, B.w, C), a.delta);
     } else if ((TD == 1 || TD == 2) && ok) {
       a.delta = FLT_MAX;  // DBC: no DDT next to the boundary
     }
     return;
   }
   if (TD == 1) {
-    // rho1/rho2 - 1 as (rho1 - rho2)*(1/rho2): exactly 0 for equal densities (rho1*rcp(rho2)
-    // - 1 with the approximate v_rcp leaves a +-1 ulp residue, which at t=0 is the whole
-    // Molteni sum); C.y = r/rho2 carries the p2 mass ratio r (1 without floating bodies)
     const float t = w3 * rr2 * inv_re;
-    a.delta = fmaf(t, (p.vr.w - B.w) * C.y, a.delta);
+    a.delta = fmaf(t, molteni(p.vr.w, B.w, C), a.delta);
     if (FT && ok && crec_kind(C) == 2.f) a.dstop = true;  // light floating p2
   } else if (TD == 2 || TD == 3) {
     float rho1h;  // rho1 + drhop

@@ -47,6 +47,7 @@ struct MdbcArgs {
   const unsigned* bc;
   double posminx, posminy, posminz, scelld;
   float kernelsize2, ovh, awen, bwenovh, massfluid, rhopzero, threshold, determlimit;
+  float kernelsize;
   float cteb, ovrhopzero, gamma;
   int igamma;
   int scelldiv;
@@ -151,11 +152,16 @@ __global__ __launch_bounds__(256) void k_mdbc_list(const DevScalars* __restrict_
     const float4 bn = a.normal[a.idp[p1]];
     if (bn.x != 0.f || bn.y != 0.f || bn.z != 0.f) {
       const GhostBox b = ghost_box<SD>(a, g, p1, bn);
-      // slab: the ghost node's cells must lie inside this slab's grid where a neighbour
-      // holds the rest of the domain (the grid edge of the whole map clamps, as the
-      // reference's search does)
-      if ((b.cxu - SD < 0 && g.xown0 > 0) || (b.cxu + SD >= g.ncx && g.xown1 < g.ncx))
-        atomicOr(&const_cast<DevScalars*>(sc)->error_flags, ERR_HALO);
+      // slab: every particle within the support of the ghost node must lie inside this
+      // slab's grid where a neighbour holds the rest of the domain (the grid edge of the
+      // whole map clamps, as the reference's search does); a ghost node in a ghost column
+      // is fine while its support stays off the grid edge
+      {
+        const double edge0 = a.posminx + double(g.xoff) * a.scelld, edge1 = edge0 + double(g.ncx) * a.scelld;
+        const double ks = double(a.kernelsize) * (1.0 + 1e-6);
+        if ((b.gx - ks < edge0 && g.xown0 > 0) || (b.gx + ks >= edge1 && g.xown1 < g.ncx))
+          atomicOr(&const_cast<DevScalars*>(sc)->error_flags, ERR_HALO);
+      }
       unsigned tot = 0;
       if (b.xini < b.xfin)
         for (int z = b.zini; z < b.zfin; z++)
@@ -440,6 +446,7 @@ void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const P
   a.posminz = dom_posmin[2];
   a.scelld = K.scelld;
   a.kernelsize2 = K.kernelsize2;
+  a.kernelsize = sqrtf(K.kernelsize2);
   a.ovh = K.ovkernelh;
   a.awen = K.awen;
   a.bwenovh = K.bwenovh;

@@ -114,16 +114,19 @@ def load_dump(fn):
     return t, idp.copy(), pos.copy(), vel.copy(), rho.copy()
 
 
-def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=(), dim=3):
+def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=(), dim=3, noise=False):
     tmp = tempfile.mkdtemp(prefix="golden_")
     try:
         subprocess.check_call([os.path.join(REF, "gencase_ref"), repr(dp), tmp, str(step), str(ddt), "1.5",
                                "CaseDambreak", str(boundary), str(dim)], stdout=subprocess.DEVNULL)
         out = os.path.join(tmp, "out")
-        subprocess.check_call(
-            [os.path.join(REF, "DualSPHysics5.2CPU_ref"), os.path.join(tmp, "CaseDambreak"), out,
-             "-nsteps:%d" % nsteps, "-svsteps:1", "-saveposdouble:1", "-sv:binx", "-svres:0"] + list(extra),
-            stdout=subprocess.DEVNULL)
+        for exe, o in (("DualSPHysics5.2CPU_ref", out), ("DualSPHysics5.2CPU_strict", out + "_strict")):
+            if o != out and not noise:
+                continue
+            subprocess.check_call(
+                [os.path.join(REF, exe), os.path.join(tmp, "CaseDambreak"), o,
+                 "-nsteps:%d" % nsteps, "-svsteps:1", "-saveposdouble:1", "-sv:binx", "-svres:0"] + list(extra),
+                stdout=subprocess.DEVNULL)
         arrays = {}
         times = []
         for part in range(nsteps + 1):
@@ -136,6 +139,14 @@ def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=(), dim=3):
             if part in keep:
                 arrays.update({"s%d_idp" % part: idp, "s%d_pos" % part: pos, "s%d_vel" % part: vel,
                                "s%d_rhop" % part: rho, "s%d_time" % part: np.float64(t)})
+                if noise:  # the strict build's PART of the same step: the reference's noise floor
+                    subprocess.check_call([os.path.join(REF, "partdump_ref"), out + "_strict", str(part), fn],
+                                          stdout=subprocess.DEVNULL)
+                    _, ids, poss, vels, rhos = load_dump(fn)
+                    o, os_ = np.argsort(idp, kind="stable"), np.argsort(ids, kind="stable")
+                    arrays["noise_%d" % part] = np.array([np.abs(pos[o] - poss[os_]).max(),
+                                                          np.abs(vel[o] - vels[os_]).max(),
+                                                          np.abs(rho[o] - rhos[os_]).max()])
         arrays["times"] = np.array(times)
         arrays["dt"] = np.diff(np.array(times))
         m = [dp, step, ddt, nsteps]
@@ -282,7 +293,7 @@ if __name__ == "__main__":
     for name, spec in CASES.items():
         if a.only and a.only != name:
             continue
-        make(name, *spec)
+        make(name, *spec, **({"noise": True} if a.noise else {}))
     for name, spec in EXT_CASES.items():
         if a.only and a.only != name:
             continue
