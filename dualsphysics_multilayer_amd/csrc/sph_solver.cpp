@@ -5,12 +5,28 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <chrono>
 #include <exception>
 #include <thread>
 
 namespace sphx {
+
+// SPH_TRACE_SLAB=1: one stderr line per slab phase (rank, step, phase) -- a diagnostic of the
+// slab protocol's host side (which rank waits where)
+static bool trace_slab() {
+  static const bool on = [] {
+    const char* e = std::getenv("SPH_TRACE_SLAB");
+    return e && *e == '1';
+  }();
+  return on;
+}
+#define SLAB_TRACE(what)                                                                                     \
+  do {                                                                                                      \
+    if (trace_slab() && slab())                                                                             \
+      std::fprintf(stderr, "slabtrace rank %d step %llu %s\n", slabcfg_.rank, stepsdone_, what);          \
+  } while (0)
 
 void check_hip(hipError_t e, const char* what) {
   if (e != hipSuccess) throw SphError(SPH_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -255,9 +271,16 @@ static KConst make_kconst(const SphConstants& c) {
   return K;
 }
 
+// Ghost columns per slab face: the support radius 2h is one full cell or two half cells
+// (scelldiv); with mDBC one column more, because a boundary particle's ghost node lies up
+// to |2 normal| (about dp, less than a cell) from it and its search reaches 2h around the
+// node (JSphCpu.cpp:1040-1047): a slab owning such a particle in its face column needs the
+// fluid one column beyond.
+int ghost_width(const SphConstants& c) { return int(c.scelldiv) + (c.tboundary == SPH_BOUND_MDBC ? 1 : 0); }
+
 // Full-map cell grid (JCellDivCpuSingle::PrepareNct, JCellDivCpuSingle.cpp:105-121, with CellDomFixed).
 // A slab keeps the global y/z extent and the x-columns [c0-W, c1+W) (owned + W ghost
-// columns per face, W = scelldiv: the support radius 2h is one full cell or two half cells).
+// columns per face, W = ghost_width).
 static DivGrid make_grid(const SphConstants& c, const SlabConfig* slab) {
   DivGrid g;
   g.ncx = int(c.dom_cells[0]);
@@ -267,10 +290,10 @@ static DivGrid make_grid(const SphConstants& c, const SlabConfig* slab) {
   g.xown0 = 0;
   g.xown1 = g.ncx;
   if (slab) {
-    const int W = int(c.scelldiv);
+    const int W = ghost_width(c);
     if (slab->nranks < 1 || slab->rank < 0 || slab->rank >= slab->nranks || slab->c0 < 0 || slab->c1 < slab->c0 + W ||
         slab->c1 > g.ncx)
-      throw SphError(SPH_ERR_ARG, "invalid slab columns (a slab owns at least scelldiv columns)");
+      throw SphError(SPH_ERR_ARG, "invalid slab columns (a slab owns at least its ghost width: scelldiv columns, +1 with mDBC)");
     g.xoff = slab->c0 - W;
     g.ncx = slab->c1 - slab->c0 + 2 * W;
     g.xown0 = W;
@@ -359,8 +382,8 @@ void partition_from_prefix(const std::vector<double>& pre, int nranks, int* b, i
 void slab_partition(const SphCaseDef& cdef, const SphParticlesHost& all, int nranks, double bound_weight, int* b) {
   SphConstants C;
   derive_constants(cdef, C);
-  const int ncx = int(C.dom_cells[0]), W = int(C.scelldiv);
-  if (nranks < 1 || nranks * W > ncx) throw SphError(SPH_ERR_ARG, "nranks must be in [1, x-cells / scelldiv]");
+  const int ncx = int(C.dom_cells[0]), W = ghost_width(C);
+  if (nranks < 1 || nranks * W > ncx) throw SphError(SPH_ERR_ARG, "nranks must be in [1, x-cells / ghost width]");
   if (all.n != cdef.np) throw SphError(SPH_ERR_ARG, "particle count does not match the case");
   std::vector<double> w(size_t(ncx), 0.0);
   const std::vector<unsigned> cx = initial_columns(C, all);
@@ -395,7 +418,7 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   unsigned nown = init.n;
   if (slab()) {
     const std::vector<unsigned> cx = initial_columns(C, init);
-    const int W = int(C.scelldiv);
+    const int W = ghost_width(C);
     const int lo = slabcfg_.c0 - (slabcfg_.rank > 0 ? W : 0);
     const int hi = slabcfg_.c1 + (slabcfg_.rank + 1 < slabcfg_.nranks ? W : 0);
     nown = 0;
@@ -416,8 +439,8 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   cap_ = slab() ? n + std::max(n / 2, 65536u) : n;
   keybits_ = bits_for(G.boxdiscard, 1);
   // grid-sized buffers hold the widest grid a slab can get from a re-partition (all
-  // columns + W = scelldiv ghost columns per face), so they never move
-  nctmax_ = slab() ? unsigned(C.dom_cells[0] + 2 * C.scelldiv) * unsigned(G.ncy) * unsigned(G.ncz) : G.nct;
+  // columns + W = ghost_width ghost columns per face), so they never move
+  nctmax_ = slab() ? unsigned(int(C.dom_cells[0]) + 2 * ghost_width(C)) * unsigned(G.ncy) * unsigned(G.ncz) : G.nct;
   if (const char* e = std::getenv("SPH_INTERACTION")) tiled_ = std::string(e) != "simple";
   if (const char* e = std::getenv("SPH_COMM_TIMEOUT_S")) comm_timeout_s_ = std::max(1.0, std::atof(e));
   // incremental divide: distinct key offsets of the 27 neighbour cells (ncx >= 3, checked
@@ -445,7 +468,7 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
     // columns (both sides of a face count the same particles); later from each exchange
     const std::vector<unsigned> cx = initial_columns(C, init);
     const bool hl = slabcfg_.rank > 0, hr = slabcfg_.rank + 1 < slabcfg_.nranks;
-    const int W = int(C.scelldiv), c0 = slabcfg_.c0, c1 = slabcfg_.c1;
+    const int W = ghost_width(C), c0 = slabcfg_.c0, c1 = slabcfg_.c1;
     for (unsigned p : sel) {
       const int c = int(cx[p]);
       face_sl_ += (hl && c >= c0 && c < c0 + W) ? 1u : 0u;
@@ -657,7 +680,7 @@ void SphGpuSingle::PresizeExchange(const SphParticlesHost& h) {
     const size_t cx = size_t(x);
     if (cx < cnt.size()) mx = std::max(mx, ++cnt[cx]);
   }
-  const unsigned long long g = (unsigned long long)mx * C.scelldiv;
+  const unsigned long long g = (unsigned long long)mx * unsigned(ghost_width(C));
   send_.gcap = g + g / 2 + 4096;
   send_.mcap = g / 4 + 1024;
   check_hip(hipMalloc(&sendgbuf_, 2 * sizeof(SlabGhost) * send_.gcap), "hipMalloc ghost send buffers");
@@ -786,7 +809,7 @@ void SphGpuSingle::UploadNormals(const SphCaseDef& cdef, const SphParticlesHost&
       const unsigned cx = unsigned((h.pos[3 * p] - C.dom_posmin[0]) / double(C.scell));
       if (cx < cnt.size()) mx = std::max(mx, ++cnt[cx]);
     }
-    mdbcfacecap_ = 2 * mx * unsigned(C.scelldiv) + 64;  // W face columns
+    mdbcfacecap_ = 2 * mx * unsigned(ghost_width(C)) + 64;  // W face columns
     check_hip(hipMalloc((void**)&mdbcface_, sizeof(MdbcFaceRec) * 4 * size_t(mdbcfacecap_)), "hipMalloc mDBC faces");
     allocs_.push_back(mdbcface_);
     check_hip(hipMalloc((void**)&bidx_, sizeof(unsigned) * std::max(cdef.npb, 1u)), "hipMalloc mDBC faces");
@@ -862,6 +885,7 @@ void SphGpuSingle::Exchange() {
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET), withpre = havepre_;
   const bool hl = transport_->has_left(), hr = transport_->has_right();
   if (!hl && !hr) return;  // a slab alone holds the whole domain: no ghosts, no migrants
+  SLAB_TRACE("exchange: pack");
   auto pack = [&] {
     launch_slab_pack(stream, cap_, sc_, cur_, G, K, C.dom_posmin, hl, hr, withm1, withpre, packtiles_, slabcnt_,
                      send_, normal_, casenpb_);
@@ -879,6 +903,7 @@ void SphGpuSingle::Exchange() {
   check_hip(hipEventRecord(xev_, stream), "exchange: event");
   WaitEvent(xev_, "exchange: wait counts");
   const SlabCounts c = *slabcnt_host_;
+  SLAB_TRACE("exchange: counts");
   if (facex_) {
     // the neighbour's ghosts of this slab: the ghosts sent now + the migrants it sent here
     // (it keeps them as ghosts); the neighbour derives the same sizes from its counts
@@ -936,6 +961,7 @@ void SphGpuSingle::Exchange() {
   transport_->group_end();
   launch_slab_unpack(stream, sc_, recvm_, unsigned(rml + rmr), recvg_, unsigned(rgl + rgr), c.np, cur_, K,
                      C.dom_posmin, withm1, withpre, slabcnt_, normal_, casenpb_);
+  SLAB_TRACE("exchange: done");
   inc_.nold = unsigned(c.np);  // the incremental divide places the appended [np, np + nin) apart
   inc_.napp = unsigned(nin);
 }
@@ -1004,7 +1030,7 @@ void SphGpuSingle::Repartition() {
   repart_last_imbalance_ = total > 0 ? maxload / (total / nr) : 1.0;
   if (!(repart_last_imbalance_ > 1.0 + repart_tol_)) return;
   std::vector<int> nb(old);
-  const int W = int(C.scelldiv);  // every slab keeps at least its W face columns
+  const int W = ghost_width(C);  // every slab keeps at least its W face columns
   partition_from_prefix(pre, nr, nb.data(), W);
   for (int r = 1; r < nr; r++) {  // inside the two slabs it separates, and increasing
     nb[size_t(r)] = std::min(std::max(nb[size_t(r)], old[size_t(r) - 1] + W), old[size_t(r) + 1] - W);
@@ -1154,6 +1180,7 @@ void SphGpuSingle::NNFaceExchange() {
 
 void SphGpuSingle::DtVariable(int mode) {
   if (slab()) {
+    SLAB_TRACE("dt allreduce");
     // The three maxima span the whole domain: fold locally, max over all slabs.
     launch_fold_maxima(stream, sc_, folded_, mode != DT_PEEK);
     transport_->allreduce_max_u32(folded_, 5, stream);  // 4 maxima + the fatal error flags
@@ -1222,6 +1249,7 @@ void SphGpuSingle::RunMotion() {
 
 void SphGpuSingle::RunFloating(bool predictor) {
   TimedBegin(1);
+  SLAB_TRACE("floating allreduce");
   // the body sums span the whole domain: each slab sums its owned particles, the
   // partial sums are added over the slabs, every slab integrates the same body
   launch_ft_partial(stream, sc_, ftbodies_, nftbodies_, ftridp_, arace_, cur_, ftpart_);

@@ -28,6 +28,8 @@ struct SphError : std::runtime_error {
 
 void check_hip(hipError_t e, const char* what);
 void derive_constants(const SphCaseDef& c, SphConstants& k);
+// Ghost columns per slab face (scelldiv, +1 with mDBC).
+int ghost_width(const SphConstants& c);
 // Column bounds of a particle-count-balanced x-slab split (sph_slab_partition).
 void slab_partition(const SphCaseDef& c, const SphParticlesHost& all, int nranks, double bound_weight, int* bounds);
 void partition_from_prefix(const std::vector<double>& prefix, int nranks, int* bounds, int minw = 1);

@@ -131,6 +131,9 @@ __global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ s
   if (p >= np) return;
   if (halted(sc)) {  // keep the state: the caller's velrhop/velrhopm1 swap then restores it
     a.velrhopm1[p] = a.velrhop[p];
+    // a slab still drops its ghosts: the next exchange sends fresh copies (without this the
+    // stale ones piled up, a duplicate set per halted step)
+    slab_ghost(K, g, a.dcell, p);
     return;
   }
   if (slab_ghost(K, g, a.dcell, p)) return;
@@ -179,6 +182,7 @@ __global__ __launch_bounds__(256) void k_sym_pre(const DevScalars* __restrict__ 
     a.velrhop[p] = a.velrhoppre[p];
     a.posxy[p] = a.posxypre[p];
     a.posz[p] = a.poszpre[p];
+    slab_ghost(K, g, a.dcell, p);  // ghosts are dropped all the same (k_verlet)
     return;
   }
   if (slab_ghost(K, g, a.dcell, p)) return;
@@ -229,7 +233,7 @@ __global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ 
                                                  const float4* __restrict__ shiftpos) {
   const unsigned np = sc->np, npb = sc->npb;
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= np || halted(sc) || slab_ghost(K, g, a.dcell, p)) return;
+  if (p >= np || slab_ghost(K, g, a.dcell, p) || halted(sc)) return;  // ghosts dropped even when halted
   const double dt = sc->dt, dt05 = dt * .5;
   const float4 ra = arace[p];
   const float4 vr = a.velrhop[p];

@@ -378,8 +378,10 @@ def test_gpu_bodies_on_slabs_with_repartition_match_reference(variant):
 @pytest.mark.gpu
 def test_gpu_mdbc_flap_normals_cross_slab_faces():
     """A fast, wide flap (no wait, 8 Hz, 12 degrees; mDBC, Symplectic): its particles cross
-    cell columns within the run.  On 3 slabs whose middle one is the flap's initial column
-    alone, every crossing flap particle migrates with its turned mDBC normal; the merged
+    cell columns within the run.  On 3 slabs whose middle one is the narrowest an mDBC slab
+    may be (its ghost width, 2 columns: the flap's initial column and the one before it),
+    every crossing flap particle migrates with its turned mDBC normal, and every ghost node's
+    support stays inside its slab's grid (no SPH_ERR_UNSUPPORTED halo error); the merged
     state holds the reference PARTs (single-domain tolerance) and the single-domain GPU run."""
     from dualsphysics_multilayer_amd.core import SphSlabGroup, case_derive
 
@@ -388,7 +390,8 @@ def test_gpu_mdbc_flap_normals_cross_slab_faces():
     flap = np.where((x.code & 0x1800) == 0x800)[0]
     flap = flap[x.pos[flap, 0] > x.pos[:, 0].mean()]  # the flap, not the piston
     cflap = int((x.pos[flap[0], 0] - k["map_realposmin"][0]) // np.float32(k["scell"]))
-    grp = SphSlabGroup(x, np.array([0, cflap, cflap + 1, k["dom_cells"][0]], np.int32))
+    b2 = min(cflap + 1, k["dom_cells"][0] - 2)
+    grp = SphSlabGroup(x, np.array([0, b2 - 2, b2, k["dom_cells"][0]], np.int32))
     one = _gpu(x)
     done = 0
     for kk in _kept(g):
@@ -406,6 +409,7 @@ def test_gpu_mdbc_flap_normals_cross_slab_faces():
     fin = grp.particles()["pos"][flap]
     cols = ((fin[:, 0] - k["map_realposmin"][0]) // np.float32(k["scell"])).astype(int)
     assert (cols != cflap).any()
+    assert all(st["error_flags"] == 0 for st in grp.stats())
 
 
 # ---- imposed floating velocities and external forces -----------------------------------------

@@ -228,8 +228,9 @@ def _bodies_worker(rank, world, port):
     WaveFlumeCase, the bench's cfg4 generator): (a) the body force/torque sums of
     k_ft_partial restated in numpy over each rank's OWNED floating particles, all-reduced
     (SUM) over gloo, equal the single-domain sums to float rounding; (b) the post-mDBC
-    face records: the owned boundary particles a rank sends from its first/last owned
-    column are exactly the boundary ghosts its neighbour holds in its ghost column."""
+    face records: the owned boundary particles a rank sends from its first/last W owned
+    columns are exactly the boundary ghosts its neighbour holds in its W ghost columns
+    (W = 2 with mDBC: a ghost node's search reaches one column past the face)."""
     _init(rank, world, port)
     from dualsphysics_multilayer_amd.case import WaveFlumeCase
     from dualsphysics_multilayer_amd.core import case_derive, slab_partition
@@ -266,15 +267,16 @@ def _bodies_worker(rank, world, port):
     isb = np.arange(case.np) < case.npb
     left = rank - 1 if rank > 0 else None
     right = rank + 1 if rank + 1 < world else None
-    send_l = case.idp[isb & owned & (col == c0)] if left is not None else np.zeros(0, np.uint32)
-    send_r = case.idp[isb & owned & (col == c1 - 1)] if right is not None else np.zeros(0, np.uint32)
+    W = int(k["scelldiv"]) + 1  # ghost columns per face with mDBC (sph_solver.cpp ghost_width)
+    send_l = case.idp[isb & owned & (col < c0 + W)] if left is not None else np.zeros(0, np.uint32)
+    send_r = case.idp[isb & owned & (col >= c1 - W)] if right is not None else np.zeros(0, np.uint32)
     got_from_left = _sendrecv_arrays([send_r], right, left, [np.uint32])
     got_from_right = _sendrecv_arrays([send_l], left, right, [np.uint32])
     if left is not None:
-        ghosts = case.idp[isb & (col == c0 - 1)]
+        ghosts = case.idp[isb & (col >= c0 - W) & (col < c0)]
         assert np.array_equal(np.sort(got_from_left[0]), np.sort(ghosts))
     if right is not None:
-        ghosts = case.idp[isb & (col == c1)]
+        ghosts = case.idp[isb & (col >= c1) & (col < c1 + W)]
         assert np.array_equal(np.sort(got_from_right[0]), np.sort(ghosts))
     dist.destroy_process_group()
 
