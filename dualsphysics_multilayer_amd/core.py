@@ -73,6 +73,8 @@ EXPORTED_SYMBOLS = (
     "sph_slab_group_member",
     "sph_slab_set_repartition",
     "sph_slab_group_set_repartition",
+    "sph_slab_set_overlap",
+    "sph_slab_group_set_overlap",
     "sph_slab_info",
     "sph_part_read",
     "sph_part_write",
@@ -141,6 +143,8 @@ def load_library(path: str = LIB_PATH):
     L.sph_slab_group_member.argtypes = [vp, C.c_int, C.POINTER(vp)]
     L.sph_slab_set_repartition.argtypes = [vp, C.c_uint32, C.c_double, C.c_double]
     L.sph_slab_group_set_repartition.argtypes = [vp, C.c_uint32, C.c_double, C.c_double]
+    L.sph_slab_set_overlap.argtypes = [vp, C.c_int]
+    L.sph_slab_group_set_overlap.argtypes = [vp, C.c_int]
     L.sph_slab_info.argtypes = [vp, C.POINTER(SphSlabInfo)]
     L.sph_part_read.argtypes = [C.c_char_p, C.POINTER(SphPartHeader), vp]
     L.sph_part_write.argtypes = [C.c_char_p, C.POINTER(SphPartHeader), vp]
@@ -332,6 +336,11 @@ class SphGpuSingle:
         """Slabs: re-balance the column bounds every `every` steps (collective)."""
         _check(load_library().sph_slab_set_repartition(self._h, every, bound_weight, tolerance))
 
+    def set_overlap(self, on: bool) -> None:
+        """Slabs: send a divide's ghost records beside the interaction of the items that
+        need none (default on; the results are bitwise the same either way)."""
+        _check(load_library().sph_slab_set_overlap(self._h, int(on)))
+
     def timing(self) -> tuple[np.ndarray, int]:
         ms = np.zeros(4, np.float64)
         n = C.c_uint64()
@@ -465,6 +474,10 @@ class SphSlabGroup:
     def set_repartition(self, every: int, bound_weight: float = 0.3, tolerance: float = 0.05) -> None:
         """Re-balance the slabs' column bounds every `every` steps."""
         _check(load_library().sph_slab_group_set_repartition(self._h, every, bound_weight, tolerance))
+
+    def set_overlap(self, on: bool) -> None:
+        """Ghost exchange beside the interior items' interaction (default on), every slab."""
+        _check(load_library().sph_slab_group_set_overlap(self._h, int(on)))
 
     def slab_info(self) -> list:
         return [m.slab_info() for m in self.members]

@@ -273,6 +273,19 @@ int sph_slab_group_set_repartition(SphSlabGroup* g, uint32_t every, double bound
   });
 }
 
+int sph_slab_set_overlap(SphSolver* s, int on) {
+  NEED(s);
+  NOT_MEMBER(s);
+  return guard([&] { s->impl->SetOverlap(on != 0); });
+}
+
+int sph_slab_group_set_overlap(SphSlabGroup* g, int on) {
+  NEED(g);
+  return guard([&] {
+    for (auto& m : g->impl->slabs) m->SetOverlap(on != 0);
+  });
+}
+
 int sph_slab_info(SphSolver* s, SphSlabInfo* out) {
   NEED(s && out);
   return guard([&] {

@@ -19,39 +19,23 @@
 
 namespace sphx {
 
-// ---------------------------------------------------------------------------------
-// Box key of one particle (KerPreSortFull, JCellDivGpuSingle_ker.cu:41-102).
-__device__ __forceinline__ unsigned box_key(unsigned rcell, typecode rcode, const DivGrid& g, unsigned dcc) {
-  if (rcell == DCELL_DISCARD) return g.boxdiscard;  // slab: stale ghost / particle handed to a neighbour
-  const unsigned cx = DcelCellx(dcc, rcell) - unsigned(g.xoff), cy = DcelCelly(dcc, rcell), cz = DcelCellz(dcc, rcell);
-  if (rcell != DCELL_OUT && (g.xown0 != 0 || g.xown1 != g.ncx) && cx >= unsigned(g.ncx))
-    return g.boxdiscard;  // slab: a migrant handed over beyond this slab's ghost columns (re-partition)
-  const unsigned cellsort = cx + cy * unsigned(g.ncx) + cz * g.nsheet;
-  const typecode codetype = CodeType(rcode), codeout = CodeSpecial(rcode);
-  if (codetype < CODE_TYPE_FLOATING)
-    return codeout < CODE_OUTIGNORE
-               ? ((cx < unsigned(g.ncx) && cy < unsigned(g.ncy) && cz < unsigned(g.ncz)) ? cellsort : g.boxboundignore)
-               : (codeout == CODE_OUTIGNORE ? g.boxboundoutignore : g.boxboundout);
-  return codeout <= CODE_OUTIGNORE ? (codeout < CODE_OUTIGNORE ? g.boxfluid + cellsort : g.boxfluidoutignore)
-                                   : (codetype == CODE_TYPE_FLOATING ? g.boxboundout : g.boxfluidout);
-}
-
 // PreSort — one thread per particle, bounded by the live count.
 __global__ __launch_bounds__(256) void k_presort(const DevScalars* __restrict__ sc, const unsigned* __restrict__ dcell,
                                                  const typecode* __restrict__ code, DivGrid g, unsigned dcc,
-                                                 unsigned* __restrict__ keys, unsigned* __restrict__ vals) {
+                                                 unsigned* __restrict__ keys, unsigned* __restrict__ vals,
+                                                 unsigned extra) {
   const unsigned n = sc->np;
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p == 0) const_cast<DevScalars*>(sc)->ndiv = n;
+  if (p == 0) const_cast<DevScalars*>(sc)->ndiv = n + extra;
   if (p >= n) return;
   vals[p] = p;
   keys[p] = box_key(dcell[p], code[p], g, dcc);
 }
 
 void launch_presort(hipStream_t stm, unsigned cap, const DevScalars* sc, const unsigned* dcell, const typecode* code,
-                    DivGrid g, unsigned domcellcode, unsigned* keys, unsigned* vals) {
+                    DivGrid g, unsigned domcellcode, unsigned* keys, unsigned* vals, unsigned extra) {
   const unsigned nb = (cap + 255) / 256;
-  hipLaunchKernelGGL(k_presort, dim3(nb), dim3(256), 0, stm, sc, dcell, code, g, domcellcode, keys, vals);
+  hipLaunchKernelGGL(k_presort, dim3(nb), dim3(256), 0, stm, sc, dcell, code, g, domcellcode, keys, vals, extra);
 }
 
 // ---------------------------------------------------------------------------------
@@ -311,6 +295,9 @@ struct GatherArgs {
   int xoff;
   // NN multiphase: per-phase EOS {rho0, cteb, gamma, integer gamma or 0} (nullptr: single phase)
   const float4* phase_eos;
+  // slab: sorted values >= vfirst are reserved ghost slots -> apppos[value - appbase]
+  unsigned vfirst, appbase;
+  unsigned* apppos;
 };
 
 // WITHM1 / WITHPRE are template parameters so every load of a particle is issued before
@@ -443,7 +430,9 @@ __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, Gat
 #pragma unroll
   for (int k = 0; k < GP; k++) {
     const unsigned i = i0 + 256 * k;
-    if (i < n) {
+    if (i < n && sp[k] >= a.vfirst) {  // a reserved ghost slot: filled by launch_ghost_scatter
+      a.apppos[sp[k] - a.appbase] = i;
+    } else if (i < n) {
       float4 vr;
       bool fluid;
       gather_one<WITHM1, WITHPRE, WITHTAU>(a, i, sp[k], vr, fluid, npb);
@@ -455,9 +444,13 @@ __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, Gat
 
 void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned* sortpart, const PartArrays& src,
                    const PartArrays& dst, bool withm1, bool withpre, const KConst& K, const double dom_posmin[3],
-                   float4* poscell, float* press, int xoff, const float4* phase_eos) {
+                   float4* poscell, float* press, int xoff, const float4* phase_eos, unsigned vfirst,
+                   unsigned appbase, unsigned* apppos) {
   GatherArgs a;
   a.phase_eos = phase_eos;
+  a.vfirst = vfirst;
+  a.appbase = appbase;
+  a.apppos = apppos;
   a.xoff = xoff;
   a.src = src;
   a.dst = dst;
@@ -920,12 +913,13 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   TSTAMP(2);
   // ---- slab: the appended particles (sorted by key) below each box of the block; they
   // follow the old members of their box (larger previous index), in appended order
-  if (s.napp) {
+  const unsigned napt = s.napp + s.nappv;  // appended particles + reserved ghost slots
+  if (napt) {
     for (int k = int(threadIdx.x); k <= IB_BOX; k += IB_BS)
-      s_ab[k] = lower_bound_u32(s.akeys, 0u, s.napp, unsigned(min(c0 + k, nctt)));
+      s_ab[k] = lower_bound_u32(s.akeys, 0u, napt, unsigned(min(c0 + k, nctt)));
     __syncthreads();
   }
-  auto ab = [&](int k) -> unsigned { return s.napp ? s_ab[k] : 0u; };
+  auto ab = [&](int k) -> unsigned { return napt ? s_ab[k] : 0u; };
   // ---- per-box scan: begin, stayer offset, counts
   const unsigned base0 = jlo + s_below + s_farbelow;
   unsigned cnt[IB_BPT], xs[IB_BPT], xsn[IB_BPT];
@@ -1143,22 +1137,29 @@ __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, G
 void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& src, const PartArrays& dst,
                        bool withm1, bool withpre, const KConst& K, const double dom_posmin[3], float4* poscell,
                        float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
-                       IncDivScratch& s, SortScratch& srt, unsigned keybits, const float4* phase_eos) {
+                       IncDivScratch& s, SortScratch& srt, unsigned keybits, const float4* phase_eos,
+                       const SlabFaces* faces, unsigned ngl, unsigned ngr) {
   s.gen++;
   const int usey = g.ncy > 1, usez = g.ncz > 1;
   const unsigned omax = 1u + (usey ? unsigned(g.ncx) : 0u) + (usez ? g.nsheet : 0u);
   s.akin = srt.keys[0];
   s.avin = srt.vals[0];
+  s.nappv = faces ? ngl + ngr : 0u;
   hipLaunchKernelGGL(k_inc_classify, dim3(s.nb1), dim3(INC_BS), 0, stm, sc, src.dcell, src.code, g, K.domcellcode, s,
                      usey, usez);
-  if (s.napp) {  // slab: the appended particles, sorted by key apart (stable: appended order)
-    const int res = launch_radix_sort(stm, cap, sc, srt, keybits, s.napp);
+  // slab: the reserved ghost slots after the appended particles
+  if (s.nappv) launch_ghost_keys(stm, *faces, g, ngl, ngr, s.akin + s.napp, s.avin + s.napp, s.napp);
+  if (s.napp + s.nappv) {  // slab: the appended particles, sorted by key apart (stable: appended order)
+    const int res = launch_radix_sort(stm, cap, sc, srt, keybits, s.napp + s.nappv);
     s.akeys = srt.keys[res];
     s.avals = srt.vals[res];
   }
   hipLaunchKernelGGL(k_inc_boxes, dim3(s.nb2), dim3(IB_BS), 0, stm, sc, g, begincell_old, begincell_new, s, omax);
   GatherArgs a;
   a.phase_eos = phase_eos;
+  a.vfirst = ~0u;
+  a.appbase = 0;
+  a.apppos = nullptr;
   a.xoff = g.xoff;
   a.src = src;
   a.dst = dst;
@@ -1188,6 +1189,63 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
   else { SPH_K_INC_PUSH_T(false, false); }
 #undef SPH_K_INC_PUSH_T
 #undef SPH_K_INC_PUSH
+}
+
+// ---------------------------------------------------------------------------------
+// Slab ghosts into their reserved slots (the exchange after the divide, sph_slab.hip): the
+// double position rebuilt as cell origin + offset and stored with its poscell and EOS
+// pressure exactly as the gather stores a particle (gather_store); the key for the next
+// divide (which drops the ghost: the update marks it DCELL_DISCARD).
+__global__ __launch_bounds__(256) void k_ghost_scatter(const SlabGhost* __restrict__ rec, unsigned ng,
+                                                       const unsigned* __restrict__ apppos, GatherArgs a, DivGrid g,
+                                                       unsigned* __restrict__ skeys) {
+  const unsigned e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ng) return;
+  const SlabGhost r = rec[e];
+  const unsigned slot = apppos[e];
+  GatherRec<false, false, false> q;
+  const double ox = a.posminx + double(DcelCellx(a.dcc, r.dcell)) * a.scelld;
+  const double oy = a.posminy + double(DcelCelly(a.dcc, r.dcell)) * a.scelld;
+  const double oz = a.posminz + double(DcelCellz(a.dcc, r.dcell)) * a.scelld;
+  q.dc = r.dcell;
+  q.idp = r.idp;
+  q.code = r.code;
+  q.pxy = make_double2(ox + double(r.rx), oy + double(r.ry));
+  q.pz = oz + double(r.rz);
+  q.vr = r.velrhop;
+  gather_store<false, false, false>(a, slot, q);
+  if (skeys) skeys[slot] = box_key(r.dcell, r.code, g, a.dcc);
+}
+
+void launch_ghost_scatter(hipStream_t stm, DevScalars* sc, const SlabGhost* rec, unsigned ng, const unsigned* apppos,
+                          const PartArrays& dst, const KConst& K, const double dom_posmin[3], float4* poscell,
+                          float* press, DivGrid g, unsigned* skeys, const float4* phase_eos) {
+  (void)sc;
+  if (!ng) return;
+  GatherArgs a;
+  a.phase_eos = phase_eos;
+  a.vfirst = ~0u;
+  a.appbase = 0;
+  a.apppos = nullptr;
+  a.xoff = g.xoff;
+  a.src = dst;
+  a.dst = dst;
+  a.sortpart = nullptr;
+  a.poscell = poscell;
+  a.press = press;
+  a.posminx = dom_posmin[0];
+  a.posminy = dom_posmin[1];
+  a.posminz = dom_posmin[2];
+  a.scelld = K.scelld;
+  a.cteb = K.cteb;
+  a.ovrhopzero = K.ovrhopzero;
+  a.rhopzero = K.rhopzero;
+  a.gamma = K.gamma;
+  a.igamma = (K.gamma == float(int(K.gamma)) && K.gamma >= 1.f && K.gamma <= 16.f) ? int(K.gamma) : 0;
+  a.dcc = K.domcellcode;
+  a.withm1 = 0;
+  a.withpre = 0;
+  hipLaunchKernelGGL(k_ghost_scatter, dim3((ng + 255) / 256), dim3(256), 0, stm, rec, ng, apppos, a, g, skeys);
 }
 
 unsigned inc_blocks_classify(unsigned cap) { return (cap + INC_TILE - 1) / INC_TILE; }

@@ -373,7 +373,7 @@ __global__ __launch_bounds__(TB) void k_fluid_ext(DevScalars* __restrict__ sc, c
   __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];
   __shared__ unsigned s_nwave[4];
-  const ItemGroups IG(sc);
+  const ItemGroups IG(qctr);
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f;
   // passes whose shifting cut-off depends on the pair order: the fluid rows with floating

@@ -39,11 +39,16 @@ namespace sphx {
 // items first.
 constexpr int ROWCELLS_LDS = 1024;
 
+struct ItemRanges {
+  int x[6];  // up to three local column ranges [x[2k], x[2k+1]) of p1 (empty when equal)
+};
+
 template <bool WRITE>
 __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ bc, DivGrid g, int tmaxc,
-                                                   unsigned* __restrict__ counts, uint4* __restrict__ items) {
+                                                   unsigned* __restrict__ counts, uint4* __restrict__ items,
+                                                   ItemRanges xr) {
   __shared__ unsigned pre[ROWCELLS_LDS + 1];            // begin offset of every cell of the row, + row end
-  __shared__ unsigned short nzfrom[ROWCELLS_LDS + 1];  // first non-empty owned cell >= x (xend if none)
+  __shared__ unsigned short nzfrom[ROWCELLS_LDS + 1];  // first non-empty cell >= x in the range (xend if none)
   const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
   const unsigned r = blockIdx.x;
   const bool bound = r >= nrows;
@@ -51,8 +56,6 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
   const unsigned y = rr % unsigned(g.ncy), z = rr / unsigned(g.ncy);
   const unsigned rowbase = (bound ? 0u : g.boxfluid) + z * g.nsheet + y * unsigned(g.ncx);
   const int ncx = g.ncx;
-  // p1 only in the owned columns (slab ghosts are neighbours, never p1).
-  const int xbeg = g.xown0, xend = g.xown1;
   uint4* out = WRITE ? items + counts[r] : nullptr;
   unsigned nitems = 0;
   auto emit = [&](int a, int e, unsigned p, unsigned q) {
@@ -60,87 +63,98 @@ __global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ 
       out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(e) << 16), p, q);
     nitems++;
   };
-  if (ncx > ROWCELLS_LDS) {  // very long rows: the same walk on global memory, cell by cell
-    if (threadIdx.x != 0) return;
-    auto PRE = [&](int x) -> unsigned { return bc[rowbase + x]; };
-    unsigned p = PRE(xbeg);
-    const unsigned pend = PRE(xend);
-    int c = xbeg;
-    while (p < pend) {
-      while (PRE(c + 1) <= p) c++;
-      const unsigned q = min(min(p + unsigned(TB), pend), PRE(min(c + tmaxc, xend)));
-      int e = c;
-      while (PRE(e + 1) < q) e++;
-      emit(c, e, p, q);
-      p = q;
-      c = e;
+  const bool lds = ncx <= ROWCELLS_LDS;
+  if (lds) {
+    for (int x = int(threadIdx.x); x <= ncx; x += 64) pre[x] = bc[rowbase + x];
+    __syncthreads();
+  }
+  // p1 only in the owned columns (slab ghosts are neighbours, never p1), in up to three column
+  // ranges (a slab's face columns and the columns between them), each walked on its own so
+  // no item crosses from one to the next
+  for (int rg = 0; rg < 3; rg++) {
+    const int xbeg = xr.x[2 * rg], xend = xr.x[2 * rg + 1];  // uniform over the block
+    if (xbeg >= xend) continue;
+    if (!lds) {  // very long rows: the same walk on global memory, cell by cell
+      if (threadIdx.x == 0) {
+        auto PRE = [&](int x) -> unsigned { return bc[rowbase + x]; };
+        unsigned p = PRE(xbeg);
+        const unsigned pend = PRE(xend);
+        int c = xbeg;
+        while (p < pend) {
+          while (PRE(c + 1) <= p) c++;
+          const unsigned q = min(min(p + unsigned(TB), pend), PRE(min(c + tmaxc, xend)));
+          int e = c;
+          while (PRE(e + 1) < q) e++;
+          emit(c, e, p, q);
+          p = q;
+          c = e;
+        }
+      }
+      continue;
     }
-    if (!WRITE) counts[r] = nitems;
-    return;
-  }
-  for (int x = int(threadIdx.x); x <= ncx; x += 64) pre[x] = bc[rowbase + x];
-  __syncthreads();
-  // first non-empty owned cell at or after x: lane-local blocks, then a wave suffix-min
-  const int per = (ncx + 63) / 64, x0 = int(threadIdx.x) * per, x1 = min(x0 + per, ncx);
-  int nz = xend;
-  for (int x = x1 - 1; x >= x0; x--) {
-    if (x >= xbeg && x < xend && pre[x + 1] > pre[x]) nz = x;
-    nzfrom[x] = (unsigned short)nz;
-  }
-  int suf = nz;
+    // first non-empty cell of the range at or after x: lane-local blocks, then a wave suffix-min
+    const int per = (ncx + 63) / 64, x0 = int(threadIdx.x) * per, x1 = min(x0 + per, ncx);
+    int nz = xend;
+    for (int x = x1 - 1; x >= x0; x--) {
+      if (x >= xbeg && x < xend && pre[x + 1] > pre[x]) nz = x;
+      nzfrom[x] = (unsigned short)nz;
+    }
+    int suf = nz;
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int v = __shfl_down(suf, off, 64);
-    if (int(threadIdx.x) + off < 64) suf = min(suf, v);
-  }
-  const int later = __shfl_down(suf, 1, 64);
-  const int carry = int(threadIdx.x) < 63 ? later : xend;
-  for (int x = x0; x < x1; x++)
-    if (int(nzfrom[x]) == xend) nzfrom[x] = (unsigned short)carry;
-  if (threadIdx.x == 63) nzfrom[ncx] = (unsigned short)xend;
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  // Walk the items: the cell holding p is known (c), the cell holding q-1 is at most
-  // TMAXCELLS-1 cells further, an item ending at a cell end jumps to the next non-empty.
-  // The five offsets pre[c..c+4] of an item are independent LDS reads (one latency);
-  // the cell holding q-1 is c + #{k = 1..3 : pre[c+k] <= q-1}.
-  static_assert(TMAXCELLS == 4, "the walk reads pre[c..c+4]");
-  const unsigned pend = pre[xend];
-  int c = nzfrom[xbeg];
-  unsigned p = c < xend ? pre[c] : pend;
-  if (tmaxc != TMAXCELLS) {  // CellMode=half: longer items, the cell holding q-1 by a short scan
-    while (p < pend) {
-      const unsigned q = min(min(p + unsigned(TB), pend), pre[min(c + tmaxc, xend)]);
-      int e = c;
-      while (pre[e + 1] <= q - 1) e++;
-      emit(c, e, p, q);
-      p = q;
-      c = pre[e + 1] == q ? int(nzfrom[e + 1]) : e;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int v = __shfl_down(suf, off, 64);
+      if (int(threadIdx.x) + off < 64) suf = min(suf, v);
     }
-    if (!WRITE) counts[r] = nitems;
-    return;
+    const int later = __shfl_down(suf, 1, 64);
+    const int carry = int(threadIdx.x) < 63 ? later : xend;
+    for (int x = x0; x < x1; x++)
+      if (int(nzfrom[x]) == xend) nzfrom[x] = (unsigned short)carry;
+    if (threadIdx.x == 63) nzfrom[ncx] = (unsigned short)xend;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      // Walk the items: the cell holding p is known (c), the cell holding q-1 is at most
+      // TMAXCELLS-1 cells further, an item ending at a cell end jumps to the next non-empty.
+      // The five offsets pre[c..c+4] of an item are independent LDS reads (one latency);
+      // the cell holding q-1 is c + #{k = 1..3 : pre[c+k] <= q-1}.
+      static_assert(TMAXCELLS == 4, "the walk reads pre[c..c+4]");
+      const unsigned pend = pre[xend];
+      int c = nzfrom[xbeg];
+      unsigned p = c < xend ? pre[c] : pend;
+      if (tmaxc != TMAXCELLS) {  // CellMode=half: longer items, the cell holding q-1 by a short scan
+        while (p < pend) {
+          const unsigned q = min(min(p + unsigned(TB), pend), pre[min(c + tmaxc, xend)]);
+          int e = c;
+          while (pre[e + 1] <= q - 1) e++;
+          emit(c, e, p, q);
+          p = q;
+          c = pre[e + 1] == q ? int(nzfrom[e + 1]) : e;
+        }
+      } else {
+        while (p < pend) {
+          const unsigned p1 = pre[min(c + 1, xend)], p2 = pre[min(c + 2, xend)], p3 = pre[min(c + 3, xend)];
+          const unsigned p4 = pre[min(c + 4, xend)];
+          const unsigned q = min(min(p + unsigned(TB), pend), p4);
+          const int e = c + int(p1 <= q - 1) + int(p2 <= q - 1) + int(p3 <= q - 1);
+          emit(c, e, p, q);
+          p = q;
+          const unsigned pe1 = e + 1 - c == 1 ? p1 : e + 1 - c == 2 ? p2 : e + 1 - c == 3 ? p3 : p4;
+          c = pe1 == q ? int(nzfrom[e + 1]) : e;
+        }
+      }
+    }
+    __syncthreads();  // nzfrom is rebuilt for the next range
   }
-  while (p < pend) {
-    const unsigned p1 = pre[min(c + 1, xend)], p2 = pre[min(c + 2, xend)], p3 = pre[min(c + 3, xend)];
-    const unsigned p4 = pre[min(c + 4, xend)];
-    const unsigned q = min(min(p + unsigned(TB), pend), p4);
-    const int e = c + int(p1 <= q - 1) + int(p2 <= q - 1) + int(p3 <= q - 1);
-    emit(c, e, p, q);
-    p = q;
-    const unsigned pe1 = e + 1 - c == 1 ? p1 : e + 1 - c == 2 ? p2 : e + 1 - c == 3 ? p3 : p4;
-    c = pe1 == q ? int(nzfrom[e + 1]) : e;
-  }
-  if (!WRITE) counts[r] = nitems;
+  if (!WRITE && threadIdx.x == 0) counts[r] = nitems;
 }
 
-// Exclusive scan of the per-row item counts (one block) -> item offsets, total; zeroes
-// the per-XCD work queues of the next interaction.
+// Exclusive scan of the per-row item counts (one block) -> item offsets, the list's counts
+// {all, bound} into qctr[QCTR_NITEMS]; zeroes the per-XCD work queues of the next interaction.
 __global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ counts, unsigned nrows2,
-                                                     DevScalars* __restrict__ sc, unsigned* __restrict__ qctr) {
+                                                     unsigned* __restrict__ qctr) {
   __shared__ unsigned part[1024];
   if (threadIdx.x < 8) qctr[threadIdx.x * QSTRIDE] = 0u;  // the interaction's item queues start over
   const unsigned per = (nrows2 + 1023) / 1024;
-  const unsigned b0 = threadIdx.x * per, b1 = min(b0 + per, nrows2);
+  const unsigned b0 = min(threadIdx.x * per, nrows2), b1 = min(b0 + per, nrows2);
   unsigned s = 0;
   for (unsigned i = b0; i < b1; i++) s += counts[i];
   part[threadIdx.x] = s;
@@ -157,20 +171,24 @@ __global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ coun
     counts[i] = run;
     run += v;
   }
-  if (threadIdx.x == 1023) sc->nitems = part[1023];
+  if (threadIdx.x == 1023) qctr[QCTR_NITEMS] = part[1023];
   __syncthreads();
   // items of the bound rows (the list's tail): each XCD group takes its share of them
   // after its fluid items (ItemGroups)
-  if (threadIdx.x == 0) sc->nitems_bound = part[1023] - counts[nrows2 / 2];
+  if (threadIdx.x == 0) qctr[QCTR_NITEMS + 1] = part[1023] - counts[nrows2 / 2];
 }
 
 void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
-                  uint4* items, unsigned* qctr, int scelldiv) {
+                  uint4* items, unsigned* qctr, int scelldiv, const int* xr) {
+  (void)sc;
   const int tmaxc = scelldiv == 1 ? TMAXCELLS : TMAXCELLS_HALF;
   const unsigned nrows2 = 2u * unsigned(g.ncy) * unsigned(g.ncz);
-  hipLaunchKernelGGL(k_items_rows<false>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, nullptr);
-  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, rowtmp, nrows2, sc, qctr);
-  hipLaunchKernelGGL(k_items_rows<true>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, items);
+  ItemRanges r = {{g.xown0, g.xown1, 0, 0, 0, 0}};
+  if (xr)
+    for (int k = 0; k < 6; k++) r.x[k] = xr[k];
+  hipLaunchKernelGGL(k_items_rows<false>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, nullptr, r);
+  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, rowtmp, nrows2, qctr);
+  hipLaunchKernelGGL(k_items_rows<true>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, items, r);
 }
 
 // ------------------------------------------------------------------------------------
@@ -737,7 +755,7 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
   __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];  // lane -> p1 of the item (see lane_order)
   __shared__ unsigned s_nwave[4];
-  const ItemGroups IG(sc);
+  const ItemGroups IG(qctr);
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f;
   const float cvisc_f = -K.visco * K.cs0f * K.kernelh * K.massfluid;

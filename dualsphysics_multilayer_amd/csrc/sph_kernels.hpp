@@ -86,6 +86,24 @@ __device__ __forceinline__ void shift_displacement(const KConst& K, float4 rs, f
   }
 }
 
+// Box key of one particle (KerPreSortFull, JCellDivGpuSingle_ker.cu:41-102).
+__device__ __forceinline__ unsigned box_key(unsigned rcell, typecode rcode, const DivGrid& g, unsigned dcc) {
+  if (rcell == DCELL_DISCARD) return g.boxdiscard;  // slab: stale ghost / particle handed to a neighbour
+  const unsigned cx = DcelCellx(dcc, rcell) - unsigned(g.xoff), cy = DcelCelly(dcc, rcell), cz = DcelCellz(dcc, rcell);
+  if (rcell != DCELL_OUT && (g.xown0 != 0 || g.xown1 != g.ncx) && cx >= unsigned(g.ncx))
+    return g.boxdiscard;  // slab: a migrant handed over beyond this slab's ghost columns (re-partition)
+  const unsigned cellsort = cx + cy * unsigned(g.ncx) + cz * g.nsheet;
+  const typecode codetype = CodeType(rcode), codeout = CodeSpecial(rcode);
+  if (codetype < CODE_TYPE_FLOATING)
+    return codeout < CODE_OUTIGNORE
+               ? ((cx < unsigned(g.ncx) && cy < unsigned(g.ncy) && cz < unsigned(g.ncz)) ? cellsort : g.boxboundignore)
+               : (codeout == CODE_OUTIGNORE ? g.boxboundoutignore : g.boxboundout);
+  return codeout <= CODE_OUTIGNORE ? (codeout < CODE_OUTIGNORE ? g.boxfluid + cellsort : g.boxfluidoutignore)
+                                   : (codetype == CODE_TYPE_FLOATING ? g.boxboundout : g.boxfluidout);
+}
+
+struct SlabFaces;  // the ghost exchange after the divide (below)
+
 // Scratch of the cell sort (DivideGpu).
 struct SortScratch {
   unsigned* keys[2] = {nullptr, nullptr};
@@ -105,8 +123,10 @@ constexpr int RS_MAXBITS = 11;    // widest digit (2048 buckets)
 
 // ---- divide (JCellDivGpuSingle::Divide + JSphGpuSingle::RunCellDivide) ----
 // PreSort: box key per particle (KerPreSortFull, JCellDivGpuSingle_ker.cu:41-102).
+// `extra` reserved entries follow the particles (slab ghost slots, launch_ghost_keys): the
+// sort covers np + extra keys.
 void launch_presort(hipStream_t stm, unsigned cap, const DevScalars* sc, const unsigned* dcell, const typecode* code,
-                    DivGrid g, unsigned domcellcode, unsigned* keys, unsigned* vals);
+                    DivGrid g, unsigned domcellcode, unsigned* keys, unsigned* vals, unsigned extra = 0);
 // Stable LSD radix sort of (keys, vals) for the first sc->ndiv entries (or the first `nfix`
 // when given: a count the host knows); result in keys[res]/vals[res].
 int launch_radix_sort(hipStream_t stm, unsigned cap, const DevScalars* sc, SortScratch& s, unsigned keybits,
@@ -115,9 +135,12 @@ int launch_radix_sort(hipStream_t stm, unsigned cap, const DevScalars* sc, SortS
 void launch_begincell(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned* skeys, DivGrid g, unsigned* begincell);
 // Gather + poscell + press + VelMax (KerSortDataParticles, JCellDivGpu_ker.cu:553-720; KerUpdatePosCell,
 // JSphGpuSimple_ker.cu:41-69; PreInteraction press/VelMax, JSphGpu.cpp:831-870).
+// Sorted entries with a value >= vfirst are reserved slots (no particle yet): their sorted
+// index goes to apppos[value - appbase] instead.
 void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned* sortpart, const PartArrays& src,
                    const PartArrays& dst, bool withm1, bool withpre, const KConst& K, const double dom_posmin[3],
-                   float4* poscell, float* press, int xoff, const float4* phase_eos = nullptr);
+                   float4* poscell, float* press, int xoff, const float4* phase_eos = nullptr, unsigned vfirst = ~0u,
+                   unsigned appbase = 0, unsigned* apppos = nullptr);
 
 // Incremental divide (sph_divide.hip): the stable order of the previous divide merged with
 // the particles whose box changed, every divide after the first.  On a slab the exchange
@@ -145,6 +168,10 @@ struct IncDivScratch {
   const unsigned* avals = nullptr;
   unsigned* apppos = nullptr;     // [cap]
   unsigned nold = 0, napp = 0;
+  // slab: reserved ghost slots after the appended particles (sorted with them: akin/avin
+  // [napp, napp + nappv), their positions apppos[napp + e]); no particle data until
+  // launch_ghost_scatter
+  unsigned nappv = 0;
   unsigned nb1 = 0, nb2 = 0, gen = 0;
   // SPH_INC_DBG: 8 phase timestamps of the divide kernels (printf); 16 / 32 force the
   // global-memory paths of the tile prefixes / far arrivals (tests)
@@ -156,7 +183,8 @@ unsigned inc_blocks_boxes(unsigned nctt);
 void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& src, const PartArrays& dst,
                        bool withm1, bool withpre, const KConst& K, const double dom_posmin[3], float4* poscell,
                        float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
-                       IncDivScratch& s, SortScratch& srt, unsigned keybits, const float4* phase_eos = nullptr);
+                       IncDivScratch& s, SortScratch& srt, unsigned keybits, const float4* phase_eos = nullptr,
+                       const SlabFaces* faces = nullptr, unsigned ngl = 0, unsigned ngr = 0);
 
 // ---- interaction (cusph::Interaction_Forces, JSphGpu_ker.cu:788-885) ----
 // With floating bodies (ftmassp != nullptr: particle mass per body, `code` of the
@@ -171,11 +199,17 @@ void launch_interaction_bound(hipStream_t stm, unsigned npbcap, DevScalars* sc, 
 // Work counters of the persistent tiled kernels (qctr): 8 per-XCD item queues + the
 // finished-block count, each on its own 128-B line (device-scope atomics serialize per line).
 constexpr int QSTRIDE = 32;
-constexpr size_t QCTR_BYTES = 9 * QSTRIDE * sizeof(unsigned);
+// Line 9 holds the list's item counts {all, bound} (k_items_scan; ItemGroups reads them), so
+// one counter block describes one item list.
+constexpr size_t QCTR_QUEUE_BYTES = 9 * QSTRIDE * sizeof(unsigned);  // what a re-run zeroes
+constexpr size_t QCTR_BYTES = 10 * QSTRIDE * sizeof(unsigned);
+constexpr int QCTR_NITEMS = 9 * QSTRIDE;
 // Tiled fluid interaction (sph_interaction_tiled.hip) and its per-divide item list.
 // scelldiv 1 (CellMode=full): items of <= 4 cells; 2 (half): <= TMAXCELLS_HALF half-cells.
+// p1 in the local columns [xr[0], xr[1]), [xr[2], xr[3]), [xr[4], xr[5]), each range's items
+// on their own (nullptr: the owned columns).
 void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
-                  uint4* items, unsigned* qctr, int scelldiv = 1);
+                  uint4* items, unsigned* qctr, int scelldiv = 1, const int* xr = nullptr);
 // With floating bodies (ftmassp != nullptr) the staged p2 records carry their mass ratio
 // and kind (the FT instantiation; one more float2 of LDS per record).
 void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
@@ -374,10 +408,47 @@ struct SlabSendBufs {
 // Classify every particle after an update (stable order) and write the records for
 // the two neighbours: tile counts -> scan -> scatter, four streams (ghost/migrant x
 // left/right).  has_left/has_right: the neighbour exists.
+// faces != nullptr (the ghost exchange after the divide): ghosts are counted per face box
+// into faces->msg[0/1] (zeroed here) instead of written as records.
 void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, DivGrid g, const KConst& K,
                       const double dom_posmin[3], bool has_left, bool has_right, bool withm1, bool withpre,
                       unsigned* tilecnt, SlabCounts* cnt, SlabSendBufs bufs, const float4* normal = nullptr,
-                      unsigned nbound = 0);
+                      unsigned nbound = 0, const SlabFaces* faces = nullptr);
+// ---- the ghost exchange after the divide (sph_slab.hip, sph_divide.hip) ----
+// Before the divide a slab sends each neighbour only the NUMBER of its ghosts per face box
+// (with the migrants); the receiver's divide reserves their slots (they follow the old
+// members of their box, as appended particles do) and the ghost records travel after the
+// divide, packed from the sender's sorted arrays in box order, while the interaction of
+// the items that reach no ghost column runs.  Face boxes: the boxes of the W face columns,
+// in key order — type (bound, fluid) major, then z, y, x: idx = ((type ncz + z) ncy + y) W
+// + xrel, nfb = 2 ncz ncy W (the sender's face columns and the receiver's ghost columns are
+// the same global columns).  A face message is {u64 ghosts, u64 migrants} + u32 count[nfb].
+constexpr unsigned FMSG_HDR = 4;  // u32 words of a face message's header
+struct SlabFaces {
+  unsigned* msg[4];  // send left, send right, receive left, receive right: [FMSG_HDR + nfb]
+  unsigned* pre[4];  // exclusive prefixes of their counts: [nfb + 1]
+  unsigned nfb = 0;
+  int W = 0;
+};
+// After the pack: prefixes of the send counts, the headers (ghost totals, the migrant
+// counts of `cnt`), cnt->sendl[0] / sendr[0] = the ghost totals.
+void launch_face_send_scan(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right);
+// After the message exchange: cnt->recvl / recvr from the received headers, prefixes of the
+// received counts.
+void launch_face_recv_scan(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right);
+// The divide's virtual keys of the ngl + ngr reserved ghost slots (left face first):
+// keys[e] = the receiver's box key, vals[e] = vbase + e.
+void launch_ghost_keys(hipStream_t stm, const SlabFaces& f, DivGrid g, unsigned ngl, unsigned ngr, unsigned* keys,
+                       unsigned* vals, unsigned vbase);
+// After the sender's divide: the ghost records of both faces from the sorted arrays, in face
+// box order (the old members of each box: its first count[idx] particles).
+void launch_ghost_pack(hipStream_t stm, DevScalars* sc, const SlabFaces& f, DivGrid g, const unsigned* begincell,
+                       const PartArrays& a, const float4* poscell, SlabSendBufs b, unsigned ngl, unsigned ngr);
+// The receiver: record e -> its reserved slot apppos[e] (position, poscell, EOS pressure as
+// the gather forms them; key for the next divide into skeys when given).
+void launch_ghost_scatter(hipStream_t stm, DevScalars* sc, const SlabGhost* rec, unsigned ng, const unsigned* apppos,
+                          const PartArrays& dst, const KConst& K, const double dom_posmin[3], float4* poscell,
+                          float* press, DivGrid g, unsigned* skeys, const float4* phase_eos = nullptr);
 // out[i] = (((0 + g[0][i]) + g[1][i]) + ...) over nranks rows of n floats (rank order).
 void launch_rank_ordered_sum(hipStream_t stm, const float* gathered, int n, int nranks, float* out);
 // Owned particles per GLOBAL x-column: counts[c] fluid (incl. floating), counts[ncxg + c]

@@ -660,7 +660,7 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
   __shared__ unsigned char s_perm[TB];
   __shared__ unsigned s_nwave[4];
   if (threadIdx.x < 3 * SPH_MAXPHASES) sph[threadIdx.x] = phases[threadIdx.x];
-  const ItemGroups IG(sc);
+  const ItemGroups IG(qctr);
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f, etamax = 0.f;
   for (unsigned q = 0; q < 8; q++) {
@@ -1115,7 +1115,7 @@ __global__ __launch_bounds__(TB) void k_nn_visc(DevScalars* __restrict__ sc, con
   __shared__ unsigned char s_perm[TB];
   __shared__ unsigned s_nwave[4];
   if (threadIdx.x < 2 * SPH_MAXPHASES) sph[threadIdx.x] = phases[threadIdx.x];
-  const ItemGroups IG(sc);
+  const ItemGroups IG(qctr);
   const unsigned grp = blockIdx.x & 7;
   float ace2max = 0.f;
   for (unsigned q = 0; q < 8; q++) {

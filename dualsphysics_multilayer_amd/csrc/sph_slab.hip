@@ -33,7 +33,48 @@ struct PackArgs {
   SlabSendBufs b;
   const float4* normal;  // mDBC normals by idp (nullptr without mDBC)
   unsigned nbound;
+  unsigned* fcnt[2];     // ghost counts per face box (the exchange after the divide), or nullptr
+  int W;
 };
+
+// ---- face boxes (sph_kernels.hpp SlabFaces) ----
+// Key of face box idx whose first column is the local column x0.
+__device__ __forceinline__ unsigned face_key(const DivGrid& g, int W, unsigned idx, int x0) {
+  const unsigned xrel = idx % unsigned(W);
+  unsigned t = idx / unsigned(W);
+  const unsigned y = t % unsigned(g.ncy);
+  t /= unsigned(g.ncy);
+  const unsigned z = t % unsigned(g.ncz), type = t / unsigned(g.ncz);
+  return (type ? g.boxfluid : 0u) + unsigned(x0) + xrel + y * unsigned(g.ncx) + z * g.nsheet;
+}
+// Face box of a box key (-1: not a cell box of the W columns from x0).
+__device__ __forceinline__ int face_idx(const DivGrid& g, int W, unsigned key, int x0) {
+  unsigned type, cs;
+  if (key < g.nct) {
+    type = 0u;
+    cs = key;
+  } else if (key >= g.boxfluid && key < g.boxfluid + g.nct) {
+    type = 1u;
+    cs = key - g.boxfluid;
+  } else {
+    return -1;
+  }
+  const int x = int(cs % unsigned(g.ncx)) - x0;
+  const unsigned r = cs / unsigned(g.ncx);
+  if (x < 0 || x >= W) return -1;
+  return int(((type * unsigned(g.ncz) + r / unsigned(g.ncy)) * unsigned(g.ncy) + r % unsigned(g.ncy)) * unsigned(W) +
+             unsigned(x));
+}
+// The face box holding entry j: the largest idx with pre[idx] <= j (pre[0] = 0 <= j < pre[nfb]).
+__device__ __forceinline__ unsigned face_of_entry(const unsigned* __restrict__ pre, unsigned nfb, unsigned j) {
+  unsigned lo = 0, hi = nfb - 1;
+  while (lo < hi) {
+    const unsigned mid = (lo + hi + 1) >> 1;
+    if (pre[mid] <= j) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
 
 // bit 0: record for the left neighbour, bit 1: record for the right, bit 2: stays owned
 // (so a record with bit 2 is a ghost copy, without it a migrant).
@@ -72,6 +113,17 @@ __global__ __launch_bounds__(PK_BS) void k_pack_count(const DevScalars* __restri
 #pragma unroll
       for (int k = 0; k < 4; k++) c4[k] += f[k] ? 1u : 0u;
       c4[4] += (c >> 2) & 1u;
+      if (q.fcnt[0] && (c & 4u) && (c & 3u)) {  // an owned face particle: count it per face box
+        const unsigned key = box_key(q.a.dcell[p], q.a.code[p], q.g, q.dcc);
+        if (c & 1u) {
+          const int fi = face_idx(q.g, q.W, key, q.g.xown0);
+          if (fi >= 0) atomicAdd(&q.fcnt[0][fi], 1u);
+        }
+        if (c & 2u) {
+          const int fi = face_idx(q.g, q.W, key, q.g.xown1 - q.W);
+          if (fi >= 0) atomicAdd(&q.fcnt[1][fi], 1u);
+        }
+      }
     }
   }
 #pragma unroll
@@ -200,7 +252,7 @@ __global__ __launch_bounds__(PK_BS) void k_pack_write(const DevScalars* __restri
         if (i < int(w)) pre += s_w[k][i];
         tot += s_w[k][i];
       }
-      if (f[k]) {
+      if (f[k] && !(k < 2 && q.fcnt[0])) {  // ghost records come after the divide (launch_ghost_pack)
         const unsigned long long slot = off[k] + pre + __popcll(bal[k] & lt);
         if (k < 2) {
           if (slot < q.b.gcap) write_ghost(q, p, (k == 0 ? q.b.gl : q.b.gr) + slot);
@@ -217,8 +269,16 @@ __global__ __launch_bounds__(PK_BS) void k_pack_write(const DevScalars* __restri
 void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, DivGrid g, const KConst& K,
                       const double dom_posmin[3], bool has_left, bool has_right, bool withm1, bool withpre,
                       unsigned* tilecnt, SlabCounts* cnt, SlabSendBufs bufs, const float4* normal,
-                      unsigned nbound) {
+                      unsigned nbound, const SlabFaces* faces) {
   PackArgs q;
+  q.fcnt[0] = q.fcnt[1] = nullptr;
+  q.W = g.xown0;
+  if (faces) {
+    q.fcnt[0] = faces->msg[0] + FMSG_HDR;
+    q.fcnt[1] = faces->msg[1] + FMSG_HDR;
+    (void)hipMemsetAsync(q.fcnt[0], 0, 4 * size_t(faces->nfb), stm);
+    (void)hipMemsetAsync(q.fcnt[1], 0, 4 * size_t(faces->nfb), stm);
+  }
   q.a = a;
   q.g = g;
   q.dcc = K.domcellcode;
@@ -239,6 +299,124 @@ void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartA
   hipLaunchKernelGGL(k_pack_count, dim3(q.ntiles), dim3(PK_BS), 0, stm, sc, q);
   hipLaunchKernelGGL(k_pack_scan, dim3(1), dim3(1024), 0, stm, sc, q);
   hipLaunchKernelGGL(k_pack_write, dim3(q.ntiles), dim3(PK_BS), 0, stm, sc, q);
+}
+
+// ---------------------------------------------------------------------------------
+// Face messages.  One block per face: exclusive scan of the nfb counts (a thread's chunk,
+// then a block scan of the chunk sums).
+__device__ void face_scan_block(const unsigned* __restrict__ cnt, unsigned* __restrict__ pre, unsigned n) {
+  __shared__ unsigned part[1024];
+  const unsigned per = (n + 1023) / 1024;
+  const unsigned b0 = min(threadIdx.x * per, n), b1 = min(b0 + per, n);
+  unsigned s = 0;
+  for (unsigned i = b0; i < b1; i++) s += cnt[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const unsigned v = threadIdx.x >= unsigned(off) ? part[threadIdx.x - off] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  unsigned run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
+  for (unsigned i = b0; i < b1; i++) {
+    pre[i] = run;
+    run += cnt[i];
+  }
+  if (threadIdx.x == 1023) pre[n] = part[1023];
+}
+
+__global__ __launch_bounds__(1024) void k_face_send_scan(SlabFaces f, SlabCounts* __restrict__ cnt, int hl, int hr) {
+  const int side = int(blockIdx.x);  // 0 left, 1 right
+  if (side == 0 ? !hl : !hr) return;
+  face_scan_block(f.msg[side] + FMSG_HDR, f.pre[side], f.nfb);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long ng = f.pre[side][f.nfb];
+    unsigned long long* h = reinterpret_cast<unsigned long long*>(f.msg[side]);
+    unsigned long long* sd = side == 0 ? cnt->sendl : cnt->sendr;
+    sd[0] = ng;
+    h[0] = ng;
+    h[1] = sd[1];
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_face_recv_scan(SlabFaces f, SlabCounts* __restrict__ cnt, int hl, int hr) {
+  const int side = int(blockIdx.x);
+  if (side == 0 ? !hl : !hr) return;
+  face_scan_block(f.msg[2 + side] + FMSG_HDR, f.pre[2 + side], f.nfb);
+  if (threadIdx.x == 0) {
+    const unsigned long long* h = reinterpret_cast<const unsigned long long*>(f.msg[2 + side]);
+    unsigned long long* rv = side == 0 ? cnt->recvl : cnt->recvr;
+    rv[0] = h[0];
+    rv[1] = h[1];
+  }
+}
+
+void launch_face_send_scan(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right) {
+  hipLaunchKernelGGL(k_face_send_scan, dim3(2), dim3(1024), 0, stm, f, cnt, int(has_left), int(has_right));
+}
+void launch_face_recv_scan(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right) {
+  hipLaunchKernelGGL(k_face_recv_scan, dim3(2), dim3(1024), 0, stm, f, cnt, int(has_left), int(has_right));
+}
+
+// Reserved ghost slots of the divide: entry e of the left face's ngl then the right face's ngr.
+__global__ __launch_bounds__(256) void k_ghost_keys(SlabFaces f, DivGrid g, unsigned ngl, unsigned ngr,
+                                                    unsigned* __restrict__ keys, unsigned* __restrict__ vals,
+                                                    unsigned vbase) {
+  const unsigned e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ngl + ngr) return;
+  const int side = e < ngl ? 0 : 1;
+  const unsigned j = side ? e - ngl : e;
+  const unsigned idx = face_of_entry(f.pre[2 + side], f.nfb, j);
+  // the left ghost columns are [0, W), the right ones [xown1, xown1 + W)
+  keys[e] = face_key(g, f.W, idx, side ? g.xown1 : 0);
+  vals[e] = vbase + e;
+}
+
+void launch_ghost_keys(hipStream_t stm, const SlabFaces& f, DivGrid g, unsigned ngl, unsigned ngr, unsigned* keys,
+                       unsigned* vals, unsigned vbase) {
+  if (ngl + ngr)
+    hipLaunchKernelGGL(k_ghost_keys, dim3((ngl + ngr + 255) / 256), dim3(256), 0, stm, f, g, ngl, ngr, keys, vals, vbase);
+}
+
+// Ghost records from the sorted arrays: record j of a face = particle begincell[key] + (j -
+// pre[idx]) of its face box (the box's old members come first, in previous-index order —
+// the order the pre-divide pack wrote them in).  Reads are contiguous per box.
+__global__ __launch_bounds__(256) void k_ghost_pack(DevScalars* __restrict__ sc, SlabFaces f, DivGrid g,
+                                                    const unsigned* __restrict__ bc, PartArrays a,
+                                                    const float4* __restrict__ poscell, SlabSendBufs b, unsigned ngl,
+                                                    unsigned ngr) {
+  const unsigned e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ngl + ngr) return;
+  const int side = e < ngl ? 0 : 1;
+  const unsigned j = side ? e - ngl : e;
+  const unsigned* pre = f.pre[side];
+  const unsigned idx = face_of_entry(pre, f.nfb, j);
+  const unsigned key = face_key(g, f.W, idx, side ? g.xown1 - f.W : g.xown0);
+  const unsigned i = bc[key] + (j - pre[idx]);
+  if (i >= bc[key + 1]) {  // the divide placed fewer particles in the box than were counted
+    atomicOr(&sc->error_flags, ERR_HALO);
+    return;
+  }
+  const float4 pc = poscell[i];
+  SlabGhost r;
+  r.rx = pc.x;
+  r.ry = pc.y;
+  r.rz = pc.z;
+  r.dcell = a.dcell[i];
+  r.velrhop = a.velrhop[i];
+  r.idp = a.idp[i];
+  r.code = a.code[i];
+  r.pad = 0;
+  (side ? b.gr : b.gl)[j] = r;
+}
+
+void launch_ghost_pack(hipStream_t stm, DevScalars* sc, const SlabFaces& f, DivGrid g, const unsigned* begincell,
+                       const PartArrays& a, const float4* poscell, SlabSendBufs b, unsigned ngl, unsigned ngr) {
+  if (ngl + ngr)
+    hipLaunchKernelGGL(k_ghost_pack, dim3((ngl + ngr + 255) / 256), dim3(256), 0, stm, sc, f, g, begincell, a, poscell,
+                       b, ngl, ngr);
 }
 
 // ---------------------------------------------------------------------------------

@@ -278,6 +278,13 @@ static KConst make_kconst(const SphConstants& c) {
 // fluid one column beyond.
 int ghost_width(const SphConstants& c) { return int(c.scelldiv) + (c.tboundary == SPH_BOUND_MDBC ? 1 : 0); }
 
+// Narrowest slab with neighbours on both sides: 2W columns, so that its two face column
+// sets are disjoint.  A particle arriving from a neighbour (< one cell of movement) then
+// lands in the face towards that neighbour, which keeps it as a ghost itself; in a narrower
+// slab it could land in the opposite face and be missing from the other neighbour's ghosts
+// until the next exchange.  A slab at the end of the map (one neighbour) needs W.
+int min_slab_width(const SphConstants& c) { return 2 * ghost_width(c); }
+
 // Full-map cell grid (JCellDivCpuSingle::PrepareNct, JCellDivCpuSingle.cpp:105-121, with CellDomFixed).
 // A slab keeps the global y/z extent and the x-columns [c0-W, c1+W) (owned + W ghost
 // columns per face, W = ghost_width).
@@ -291,9 +298,12 @@ static DivGrid make_grid(const SphConstants& c, const SlabConfig* slab) {
   g.xown1 = g.ncx;
   if (slab) {
     const int W = ghost_width(c);
-    if (slab->nranks < 1 || slab->rank < 0 || slab->rank >= slab->nranks || slab->c0 < 0 || slab->c1 < slab->c0 + W ||
-        slab->c1 > g.ncx)
-      throw SphError(SPH_ERR_ARG, "invalid slab columns (a slab owns at least its ghost width: scelldiv columns, +1 with mDBC)");
+    const bool both = slab->rank > 0 && slab->rank + 1 < slab->nranks;
+    if (slab->nranks < 1 || slab->rank < 0 || slab->rank >= slab->nranks || slab->c0 < 0 ||
+        slab->c1 < slab->c0 + (both ? min_slab_width(c) : W) || slab->c1 > g.ncx)
+      throw SphError(SPH_ERR_ARG,
+                     "invalid slab columns (a slab owns at least 2W columns, W at a map end; W = the ghost width: "
+                     "scelldiv columns, +1 with mDBC)");
     g.xoff = slab->c0 - W;
     g.ncx = slab->c1 - slab->c0 + 2 * W;
     g.xown0 = W;
@@ -382,8 +392,9 @@ void partition_from_prefix(const std::vector<double>& pre, int nranks, int* b, i
 void slab_partition(const SphCaseDef& cdef, const SphParticlesHost& all, int nranks, double bound_weight, int* b) {
   SphConstants C;
   derive_constants(cdef, C);
-  const int ncx = int(C.dom_cells[0]), W = ghost_width(C);
-  if (nranks < 1 || nranks * W > ncx) throw SphError(SPH_ERR_ARG, "nranks must be in [1, x-cells / ghost width]");
+  const int ncx = int(C.dom_cells[0]), W = min_slab_width(C);
+  if (nranks < 1 || (nranks > 1 && nranks * W > ncx))
+    throw SphError(SPH_ERR_ARG, "nranks must be in [1, x-cells / (2 x ghost width)]");
   if (all.n != cdef.np) throw SphError(SPH_ERR_ARG, "particle count does not match the case");
   std::vector<double> w(size_t(ncx), 0.0);
   const std::vector<unsigned> cx = initial_columns(C, all);
@@ -508,11 +519,18 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
 }
 
 SphGpuSingle::~SphGpuSingle() {
+  if (xstream_) (void)hipStreamSynchronize(xstream_);
   if (stream) (void)hipStreamSynchronize(stream);
   Free();
   for (auto& e : pending_) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
   for (auto e : evpool_) (void)hipEventDestroy(e);
   if (xev_) (void)hipEventDestroy(xev_);
+  if (ev_div_) (void)hipEventDestroy(ev_div_);
+  if (ev_ghost_) (void)hipEventDestroy(ev_ghost_);
+  if (xstream_) {
+    (void)hipStreamSynchronize(xstream_);
+    (void)hipStreamDestroy(xstream_);
+  }
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -545,6 +563,19 @@ void SphGpuSingle::AllocFixed() {
   pairs_ = (unsigned long long*)dmalloc(8 * 6);
   folded_ = (unsigned*)dmalloc(4 * 8);
   slabcnt_ = (SlabCounts*)dmalloc(sizeof(SlabCounts));
+  if (slab()) {
+    // face messages and their prefixes (the ghost exchange after the divide); the second
+    // item list and its counters
+    faces_.W = ghost_width(C);
+    faces_.nfb = 2u * unsigned(G.ncy) * unsigned(G.ncz) * unsigned(faces_.W);
+    for (int k = 0; k < 4; k++) {
+      faces_.msg[k] = (unsigned*)dmalloc(4 * (size_t(FMSG_HDR) + faces_.nfb));
+      faces_.pre[k] = (unsigned*)dmalloc(4 * (size_t(faces_.nfb) + 1));
+    }
+    rowtmpf_ = (unsigned*)dmalloc(4 * 2 * size_t(G.ncy) * size_t(G.ncz));
+    qctrf_ = (unsigned*)dmalloc(QCTR_BYTES);
+    check_hip(hipMemset(qctrf_, 0, QCTR_BYTES), "zero work counters");
+  }
   check_hip(hipHostMalloc((void**)&sc_host_, sizeof(DevScalars), hipHostMallocDefault), "hipHostMalloc");
   check_hip(hipHostMalloc((void**)&slabcnt_host_, sizeof(SlabCounts), hipHostMallocDefault), "hipHostMalloc");
 }
@@ -635,8 +666,12 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
     const size_t nsup = (size_t(inc_.nb1) + 63) / 64;
     inc_.tsup = (unsigned long long*)dmalloc(8 * nsup);
     check_hip(hipMemset(inc_.tsup, 0, 8 * nsup), "zero super tiles");
-    if (slab()) inc_.apppos = (unsigned*)dmalloc(4 * n);
     inc_valid_ = false;  // new scratch: the next divide is a full one
+  }
+  if (slab()) {
+    // new positions of the appended particles and reserved ghost slots (either divide)
+    inc_.apppos = (unsigned*)dmalloc(4 * n);
+    itemsf_ = (uint4*)dmalloc(16 * (n / 128 + 2 * size_t(G.ncy) * size_t(G.ncz) + size_t(nctmax_) / 2 + 2));
   }
   sort_.ntiles = unsigned((n + RS_TILE - 1) / RS_TILE);
   sort_.hist = (unsigned*)dmalloc(4 * size_t(sort_.ntiles) * (1u << RS_MAXBITS));
@@ -878,9 +913,12 @@ void SphGpuSingle::Timing(double out_ms[4], uint64_t* launches) {
 }
 
 // ---- phases ------------------------------------------------------------------------
-// Slab exchange before the divide's sort: pack ghosts and migrants (device), swap the
-// record counts with both neighbours device to device, then ONE host wait to size
-// the receives, move the records (ghosts 40 B, migrants 96 B), append what arrived.
+// Slab exchange before the divide: pack the migrants and count the ghosts per face box
+// (device), swap the face messages (migrant count, ghost count per face box) with both
+// neighbours device to device, then ONE host wait to size the transfers; move the migrants
+// (96-112 B records) and append them.  The divide reserves the ghosts' slots; their
+// records follow it (launch_ghost_pack -> GhostTransfer), beside the interaction of the
+// items that need no ghost when the step allows it (OverlapGhosts).
 void SphGpuSingle::Exchange() {
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET), withpre = havepre_;
   const bool hl = transport_->has_left(), hr = transport_->has_right();
@@ -888,17 +926,20 @@ void SphGpuSingle::Exchange() {
   SLAB_TRACE("exchange: pack");
   auto pack = [&] {
     launch_slab_pack(stream, cap_, sc_, cur_, G, K, C.dom_posmin, hl, hr, withm1, withpre, packtiles_, slabcnt_,
-                     send_, normal_, casenpb_);
+                     send_, normal_, casenpb_, &faces_);
+    launch_face_send_scan(stream, faces_, slabcnt_, hl, hr);
   };
   check_hip(hipMemsetAsync(slabcnt_, 0, sizeof(SlabCounts), stream), "exchange: reset counts");
   pack();
-  transport_->exchange(slabcnt_->sendl, 16, slabcnt_->sendr, 16, slabcnt_->recvl, hl ? 16 : 0, slabcnt_->recvr,
-                       hr ? 16 : 0, stream);
+  const size_t mb = 4 * (size_t(FMSG_HDR) + faces_.nfb);
+  transport_->exchange(faces_.msg[0], hl ? mb : 0, faces_.msg[1], hr ? mb : 0, faces_.msg[2], hl ? mb : 0,
+                       faces_.msg[3], hr ? mb : 0, stream);
+  launch_face_recv_scan(stream, faces_, slabcnt_, hl, hr);
   check_hip(hipMemcpyAsync(slabcnt_host_, slabcnt_, sizeof(SlabCounts), hipMemcpyDeviceToHost, stream),
             "exchange: read counts");
-  // The receive sizes must be on the host before the data transfers are posted: the one
-  // host wait of a step.  Spin on an event (a blocking synchronise wakes up tens of us
-  // later); the GPU idles from the counts copy until the next launches arrive.
+  // The transfer sizes must be on the host before the transfers are posted: the one host
+  // wait of a divide.  Spin on an event (a blocking synchronise wakes up tens of us later);
+  // the GPU idles from the counts copy until the next launches arrive.
   if (!xev_) check_hip(hipEventCreateWithFlags(&xev_, hipEventDisableTiming), "hipEventCreate");
   check_hip(hipEventRecord(xev_, stream), "exchange: event");
   WaitEvent(xev_, "exchange: wait counts");
@@ -913,23 +954,23 @@ void SphGpuSingle::Exchange() {
     face_rr_ = hr ? unsigned(c.recvr[0] + c.sendr[1]) : 0u;
   }
   const unsigned long long gneed = std::max(c.sendl[0], c.sendr[0]), mneed = std::max(c.sendl[1], c.sendr[1]);
-  if (gneed > send_.gcap || mneed > send_.mcap) {  // records past a capacity were not written: grow, pack again
-    if (gneed > send_.gcap) {
-      if (sendgbuf_) check_hip(hipFree(sendgbuf_), "hipFree");
-      send_.gcap = gneed + gneed / 2 + 4096;
-      check_hip(hipMalloc(&sendgbuf_, 2 * sizeof(SlabGhost) * send_.gcap), "hipMalloc ghost send buffers");
-      send_.gl = (SlabGhost*)sendgbuf_;
-      send_.gr = send_.gl + send_.gcap;
-    }
-    if (mneed > send_.mcap) {
-      if (sendmbuf_) check_hip(hipFree(sendmbuf_), "hipFree");
-      send_.mcap = mneed + mneed / 2 + 1024;
-      check_hip(hipMalloc(&sendmbuf_, 2 * sizeof(SlabRec) * send_.mcap), "hipMalloc migrant send buffers");
-      send_.ml = (SlabRec*)sendmbuf_;
-      send_.mr = send_.ml + send_.mcap;
-    }
+  if (gneed > send_.gcap) {  // the ghost records are packed after the divide: room for them
+    check_hip(hipStreamSynchronize(stream), "exchange: sync");
+    if (sendgbuf_) check_hip(hipFree(sendgbuf_), "hipFree");
+    send_.gcap = gneed + gneed / 2 + 4096;
+    check_hip(hipMalloc(&sendgbuf_, 2 * sizeof(SlabGhost) * send_.gcap), "hipMalloc ghost send buffers");
+    send_.gl = (SlabGhost*)sendgbuf_;
+    send_.gr = send_.gl + send_.gcap;
+  }
+  if (mneed > send_.mcap) {  // migrant records past the capacity were not written: grow, pack again
+    check_hip(hipStreamSynchronize(stream), "exchange: sync");
+    if (sendmbuf_) check_hip(hipFree(sendmbuf_), "hipFree");
+    send_.mcap = mneed + mneed / 2 + 1024;
+    check_hip(hipMalloc(&sendmbuf_, 2 * sizeof(SlabRec) * send_.mcap), "hipMalloc migrant send buffers");
+    send_.ml = (SlabRec*)sendmbuf_;
+    send_.mr = send_.ml + send_.mcap;
     check_hip(hipMemsetAsync(&slabcnt_->nkeep, 0, sizeof(unsigned), stream), "exchange: reset nkeep");
-    pack();
+    pack();  // the same counts (the face messages already sent are unchanged)
   }
   const unsigned long long rgl = hl ? c.recvl[0] : 0, rgr = hr ? c.recvr[0] : 0;
   const unsigned long long rml = hl ? c.recvl[1] : 0, rmr = hr ? c.recvr[1] : 0;
@@ -945,25 +986,53 @@ void SphGpuSingle::Exchange() {
     recvmcap_ = rml + rmr + (rml + rmr) / 2 + 1024;
     check_hip(hipMalloc((void**)&recvm_, sizeof(SlabRec) * recvmcap_), "hipMalloc migrant receive buffer");
   }
-  const unsigned long long nin = rgl + rgr + rml + rmr;
+  const unsigned long long nin = rgl + rgr + rml + rmr;  // the ghosts' slots are reserved by the divide
   if (c.np + nin > cap_) {
     const unsigned long long want = (c.np + nin) + (c.np + nin) / 2;
     if (want >= (1ull << 31)) throw SphError(SPH_ERR_NOMEM, "slab particle capacity overflow");
     Grow(c.np, unsigned(want));
   }
-  // ghosts and migrants of both faces in ONE transfer group (four concurrent streams over
-  // the two xGMI links)
-  transport_->group_begin();
-  transport_->exchange(send_.gl, sizeof(SlabGhost) * c.sendl[0], send_.gr, sizeof(SlabGhost) * c.sendr[0], recvg_,
-                       sizeof(SlabGhost) * rgl, recvg_ + rgl, sizeof(SlabGhost) * rgr, stream);
+  // the migrants of both faces (two concurrent streams over the two xGMI links)
   transport_->exchange(send_.ml, sizeof(SlabRec) * c.sendl[1], send_.mr, sizeof(SlabRec) * c.sendr[1], recvm_,
                        sizeof(SlabRec) * rml, recvm_ + rml, sizeof(SlabRec) * rmr, stream);
-  transport_->group_end();
-  launch_slab_unpack(stream, sc_, recvm_, unsigned(rml + rmr), recvg_, unsigned(rgl + rgr), c.np, cur_, K,
-                     C.dom_posmin, withm1, withpre, slabcnt_, normal_, casenpb_);
+  launch_slab_unpack(stream, sc_, recvm_, unsigned(rml + rmr), recvg_, 0u, c.np, cur_, K, C.dom_posmin, withm1,
+                     withpre, slabcnt_, normal_, casenpb_);
   SLAB_TRACE("exchange: done");
-  inc_.nold = unsigned(c.np);  // the incremental divide places the appended [np, np + nin) apart
-  inc_.napp = unsigned(nin);
+  xg_sl_ = hl ? c.sendl[0] : 0;
+  xg_sr_ = hr ? c.sendr[0] : 0;
+  xg_rl_ = rgl;
+  xg_rr_ = rgr;
+  xg_nm_ = unsigned(rml + rmr);
+  xg_np_ = unsigned(c.np + rml + rmr);
+  inc_.nold = unsigned(c.np);  // the incremental divide places the appended [np, np + nm) apart
+  inc_.napp = xg_nm_;
+}
+
+// The ghost records of the last divide: packed from the sorted face columns by the divide
+// (launch_ghost_pack), sent to / received from both neighbours on stream s, written into the
+// slots the divide reserved.
+void SphGpuSingle::GhostTransfer(hipStream_t s) {
+  SLAB_TRACE("ghosts: transfer");
+  transport_->exchange(send_.gl, sizeof(SlabGhost) * xg_sl_, send_.gr, sizeof(SlabGhost) * xg_sr_, recvg_,
+                       sizeof(SlabGhost) * xg_rl_, recvg_ + xg_rl_, sizeof(SlabGhost) * xg_rr_, s);
+  launch_ghost_scatter(s, sc_, recvg_, unsigned(xg_rl_ + xg_rr_), inc_.apppos + xg_nm_, cur_, K, C.dom_posmin,
+                       poscell_, press_, G, inc_ok_ ? inc_.skeys : nullptr, nn_ ? phaseeos_ : nullptr);
+}
+
+void SphGpuSingle::GhostFinish() {
+  if (!ghost_pending_) return;
+  GhostTransfer(stream);
+  ghost_pending_ = false;
+}
+
+// The interaction of the items that reach no ghost column can run while the ghosts are in
+// flight when nothing between the divide and it reads a ghost: the headline tiled kernel
+// inside Run(), without mDBC (its correction reads ghosts first), bodies (their particle map
+// is built after the divide) or the NN / Laminar+SPS / shifting kernels (face exchanges of
+// per-particle values first).
+bool SphGpuSingle::OverlapGhosts() const {
+  return slab() && overlap_ && in_run_ && tiled_ && !nn_ && !ext_ && !normal_ && !nftp_ && !nmotobj_ &&
+         (transport_->has_left() || transport_->has_right());
 }
 
 // The one host wait of a slab divide: spin on the event (a blocking synchronise wakes up
@@ -1030,7 +1099,7 @@ void SphGpuSingle::Repartition() {
   repart_last_imbalance_ = total > 0 ? maxload / (total / nr) : 1.0;
   if (!(repart_last_imbalance_ > 1.0 + repart_tol_)) return;
   std::vector<int> nb(old);
-  const int W = ghost_width(C);  // every slab keeps at least its W face columns
+  const int W = min_slab_width(C);  // every slab keeps its two disjoint face column sets
   partition_from_prefix(pre, nr, nb.data(), W);
   for (int r = 1; r < nr; r++) {  // inside the two slabs it separates, and increasing
     nb[size_t(r)] = std::min(std::max(nb[size_t(r)], old[size_t(r) - 1] + W), old[size_t(r) + 1] - W);
@@ -1063,31 +1132,67 @@ void SphGpuSingle::RunCellDivide() {
   if (slab() && exchange_armed_ && repart_every_ && (stepsdone_ % repart_every_) == 0 && transport_->nranks > 1 &&
       !havepre_)
     Repartition();
+  // the exchange of this divide: ghosts in reserved slots, their records after the sort
+  const bool ghosts = slab() && exchange_armed_ && (transport_->has_left() || transport_->has_right());
   if (slab() && exchange_armed_) Exchange();
+  const unsigned ngl = ghosts ? unsigned(xg_rl_) : 0u, ngr = ghosts ? unsigned(xg_rr_) : 0u;
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET);
   if (inc_ok_ && inc_valid_ && G.ncx >= 3) {
     // the previous order merged with the particles whose box changed and, on a slab, the
-    // particles the exchange appended (sph_divide.hip)
+    // particles the exchange appended and the ghosts' slots (sph_divide.hip)
     inc_.nb2 = inc_blocks_boxes(G.nctt);
     launch_divide_inc(stream, cap_, sc_, cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_, G, begincell_,
-                      begincell_alt_, inc_, sort_, keybits_, nn_ ? phaseeos_ : nullptr);
+                      begincell_alt_, inc_, sort_, keybits_, nn_ ? phaseeos_ : nullptr, ghosts ? &faces_ : nullptr, ngl,
+                      ngr);
     std::swap(begincell_, begincell_alt_);
   } else {
-    launch_presort(stream, cap_, sc_, cur_.dcell, cur_.code, G, C.dom_cellcode, sort_.keys[0], sort_.vals[0]);
+    // the ghosts' slots sort as entries [np, np + ngl + ngr) after the particles
+    launch_presort(stream, cap_, sc_, cur_.dcell, cur_.code, G, C.dom_cellcode, sort_.keys[0], sort_.vals[0], ngl + ngr);
+    if (ngl + ngr)
+      launch_ghost_keys(stream, faces_, G, ngl, ngr, sort_.keys[0] + xg_np_, sort_.vals[0] + xg_np_, xg_np_);
     const int res = launch_radix_sort(stream, cap_, sc_, sort_, keybits_);
     launch_begincell(stream, cap_, sc_, sort_.keys[res], G, begincell_);
     launch_gather(stream, cap_, sc_, sort_.vals[res], cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_,
-                  G.xoff, nn_ ? phaseeos_ : nullptr);
+                  G.xoff, nn_ ? phaseeos_ : nullptr, ghosts ? xg_np_ : ~0u, xg_np_ - xg_nm_, inc_.apppos);
     if (inc_ok_)
       check_hip(hipMemcpyAsync(inc_.skeys, sort_.keys[res], 4 * size_t(cap_), hipMemcpyDeviceToDevice, stream),
                 "keep sorted keys");
   }
   inc_valid_ = inc_ok_;
   inc_.napp = 0;
+  inc_.nappv = 0;
   std::swap(cur_, alt_);
+  // this slab's ghost records for the neighbours, from its sorted face columns
+  if (ghosts) launch_ghost_pack(stream, sc_, faces_, G, begincell_, cur_, poscell_, send_, unsigned(xg_sl_), unsigned(xg_sr_));
+  const bool overlap = ghosts && OverlapGhosts();
+  ghost_split_ = false;
   if (tiled_) {
-    launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv);  // also zeroes the queues
+    // Items (each build also zeroes its queues).  A slab with neighbours cuts its rows where
+    // the stencil (scelldiv columns) stops reaching a ghost column: the face items and the
+    // interior items never share an item, whether they run in one list or in two (with the
+    // ghost exchange beside the interior list) — the same items, so the same bits.
+    const int S = int(C.scelldiv), hl = slab() && transport_->has_left(), hr = slab() && transport_->has_right();
+    int ib = G.xown0 + (hl ? S : 0), ie = G.xown1 - (hr ? S : 0);
+    if (ib >= ie) ib = ie = G.xown0;  // a narrow slab: every item reaches a ghost column
+    if (overlap) {
+      const int xi[6] = {ib, ie, 0, 0, 0, 0}, xf[6] = {G.xown0, ib, ie, G.xown1, 0, 0};
+      launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv, xi);
+      launch_items(stream, sc_, begincell_, G, rowtmpf_, itemsf_, qctrf_, C.scelldiv, xf);
+      ghost_split_ = true;
+    } else {
+      const int xa[6] = {G.xown0, ib, ib, ie, ie, G.xown1};
+      launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv, xa);
+    }
     qfresh_ = true;
+  }
+  if (ghosts) {
+    if (overlap) {
+      if (!ev_div_) check_hip(hipEventCreateWithFlags(&ev_div_, hipEventDisableTiming), "hipEventCreate");
+      check_hip(hipEventRecord(ev_div_, stream), "divide: event");
+      ghost_pending_ = true;  // sent by the next interaction, beside its interior items
+    } else {
+      GhostTransfer(stream);
+    }
   }
   if (nftp_) launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_, K, G);
   TimedEnd(2);
@@ -1111,8 +1216,10 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
     }
     TimedEnd(3);
   }
-  if (tiled_ && !qfresh_)  // a second interaction on the same item list: queues start over
-    check_hip(hipMemsetAsync(qctr_, 0, QCTR_BYTES, stream), "zero work counters");
+  if (tiled_ && !qfresh_) {  // a second interaction on the same item list: queues start over
+    check_hip(hipMemsetAsync(qctr_, 0, QCTR_QUEUE_BYTES, stream), "zero work counters");
+    if (ghost_split_) check_hip(hipMemsetAsync(qctrf_, 0, QCTR_QUEUE_BYTES, stream), "zero work counters");
+  }
   qfresh_ = false;
   if (nn_) {
     // NN multiphase (sph_nn.hip); the shifting sums only where they are applied: the
@@ -1126,7 +1233,7 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
       // reading their effective viscosities / stress tensors (JSphCpu_NN_SPH.cpp:671-696)
       if (slab() && C.tvisco != SPH_VISCO_ARTIFICIAL && (transport_->has_left() || transport_->has_right()))
         NNFaceExchange();
-      check_hip(hipMemsetAsync(qctr_, 0, QCTR_BYTES, stream), "zero work counters");
+      check_hip(hipMemsetAsync(qctr_, 0, QCTR_QUEUE_BYTES, stream), "zero work counters");
       launch_nn_visc(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, cur_.code, viscoeta_, tau_,
                      begincell_, G, K, phasek_, arace_);
     }
@@ -1142,8 +1249,28 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
     // The tiled kernel writes the arace of every owned particle (skipped boundary items
     // get ar = 0) and resets its own work counters at exit (zeroed once at allocation).
     TimedBegin(0);  // the timed interval is the interaction kernel alone (rocprof's per-kernel average)
-    launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, begincell_, G, K,
-                       arace_, cur_.code, ftmassp_);
+    if (ghost_pending_) {
+      // Slab: the interior items now, the ghost records in flight on the exchange stream;
+      // there the face items follow their arrival.  The interior kernel leaves a few block
+      // slots free so that the transfer and scatter kernels start at once.
+      launch_fluid_tiled(stream, nblocks_tiled_ - 64, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, begincell_,
+                         G, K, arace_, cur_.code, ftmassp_);
+      if (!xstream_) check_hip(hipStreamCreateWithFlags(&xstream_, hipStreamNonBlocking), "hipStreamCreate");
+      if (!ev_ghost_) check_hip(hipEventCreateWithFlags(&ev_ghost_, hipEventDisableTiming), "hipEventCreate");
+      check_hip(hipStreamWaitEvent(xstream_, ev_div_, 0), "ghosts: wait divide");
+      GhostTransfer(xstream_);
+      launch_fluid_tiled(xstream_, nblocks_tiled_, sc_, itemsf_, qctrf_, poscell_, cur_.velrhop, press_, begincell_, G,
+                         K, arace_, cur_.code, ftmassp_);
+      check_hip(hipEventRecord(ev_ghost_, xstream_), "ghosts: event");
+      check_hip(hipStreamWaitEvent(stream, ev_ghost_, 0), "ghosts: join");
+      ghost_pending_ = false;
+    } else {
+      launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, begincell_, G, K,
+                         arace_, cur_.code, ftmassp_);
+      if (ghost_split_)  // the ghosts are in: the face items right after
+        launch_fluid_tiled(stream, nblocks_tiled_, sc_, itemsf_, qctrf_, poscell_, cur_.velrhop, press_, begincell_,
+                           G, K, arace_, cur_.code, ftmassp_);
+    }
   } else {
     TimedBegin(0);
     launch_interaction(stream, cap_, sc_, poscell_, cur_.velrhop, press_, begincell_, G, K, arace_, cur_.code,
@@ -1179,7 +1306,7 @@ void SphGpuSingle::NNFaceExchange() {
 }
 
 void SphGpuSingle::DtVariable(int mode) {
-  if (slab()) {
+  if (slab() && transport_->nranks > 1) {  // one rank: its own maxima are the domain's
     SLAB_TRACE("dt allreduce");
     // The three maxima span the whole domain: fold locally, max over all slabs.
     launch_fold_maxima(stream, sc_, folded_, mode != DT_PEEK);
@@ -1253,7 +1380,7 @@ void SphGpuSingle::RunFloating(bool predictor) {
   // the body sums span the whole domain: each slab sums its owned particles, the
   // partial sums are added over the slabs, every slab integrates the same body
   launch_ft_partial(stream, sc_, ftbodies_, nftbodies_, ftridp_, arace_, cur_, ftpart_);
-  if (slab()) transport_->allreduce_sum_f32(ftpart_, nftbodies_ * FT_NBLK * 6, stream);
+  if (slab() && transport_->nranks > 1) transport_->allreduce_sum_f32(ftpart_, nftbodies_ * FT_NBLK * 6, stream);
   launch_ft_body(stream, sc_, K, ftbodies_, nftbodies_, ftridp_, nftp_, cur_, predictor, ftpart_, fttab_,
                  fttabdesc_);
   TimedEnd(1);
@@ -1439,7 +1566,15 @@ unsigned SphGpuSingle::Floatings(SphFloatingState* out, unsigned cap) {
 
 void SphGpuSingle::Run(unsigned nsteps) {
   check_hip(hipSetDevice(device), "hipSetDevice");
-  for (unsigned s = 0; s < nsteps; s++) ComputeStep();
+  in_run_ = true;
+  try {
+    for (unsigned s = 0; s < nsteps; s++) ComputeStep();
+    GhostFinish();  // the state between runs is whole (ghosts in place)
+  } catch (...) {
+    in_run_ = false;
+    throw;
+  }
+  in_run_ = false;
   check_hip(hipGetLastError(), "kernel launch");
 }
 

@@ -30,6 +30,8 @@ void check_hip(hipError_t e, const char* what);
 void derive_constants(const SphCaseDef& c, SphConstants& k);
 // Ghost columns per slab face (scelldiv, +1 with mDBC).
 int ghost_width(const SphConstants& c);
+// Narrowest slab between two neighbours (2 x ghost width).
+int min_slab_width(const SphConstants& c);
 // Column bounds of a particle-count-balanced x-slab split (sph_slab_partition).
 void slab_partition(const SphCaseDef& c, const SphParticlesHost& all, int nranks, double bound_weight, int* bounds);
 void partition_from_prefix(const std::vector<double>& prefix, int nranks, int* bounds, int minw = 1);
@@ -92,6 +94,9 @@ class SphGpuSingle {
   // Slabs: re-balance the column bounds every `every` steps (0: never) when the most loaded
   // slab exceeds the mean by more than `tolerance`; collective (all ranks the same values).
   void SetRepartition(unsigned every, double bound_weight, double tolerance);
+  // Slabs: run the interaction of the items that reach no ghost column while the ghost
+  // records of the divide are in flight (default on; off = ghosts in place before it).
+  void SetOverlap(bool on) { overlap_ = on; }
   SlabConfig Slab() const { return slabcfg_; }
   unsigned RepartitionCount() const { return repart_count_; }
   double LastImbalance() const { return repart_last_imbalance_; }
@@ -115,6 +120,9 @@ class SphGpuSingle {
   void UploadNormals(const SphCaseDef& cdef, const SphParticlesHost& init);
   void UploadPhases(const SphCaseDef& cdef);
   void Exchange();
+  void GhostTransfer(hipStream_t s);  // the ghost records of the last divide into their slots
+  void GhostFinish();                 // ... on the solver stream, if still pending
+  bool OverlapGhosts() const;         // the interaction can start before the ghosts are in
   void WaitEvent(hipEvent_t ev, const char* what);
   void Repartition();
   void RunMotion();                 // JSphCpu::RunMotion after ComputeStep (JSphCpuSingle.cpp:1096)
@@ -164,7 +172,13 @@ class SphGpuSingle {
   unsigned* begincell_ = nullptr;
   uint4* items_ = nullptr;        // tiled-interaction work items (per divide)
   unsigned* rowtmp_ = nullptr;    // per-row item counts/offsets
-  unsigned* qctr_ = nullptr;      // per-XCD-group work counters
+  unsigned* qctr_ = nullptr;      // per-XCD-group work counters + the list's item counts
+  // slabs: the items of the p1 whose neighbour columns include a ghost column (the ghost
+  // exchange after the divide runs beside the interaction of the others)
+  uint4* itemsf_ = nullptr;
+  unsigned* rowtmpf_ = nullptr;
+  unsigned* qctrf_ = nullptr;
+  bool ghost_split_ = false;      // the last item build split the list (items_ | itemsf_)
   unsigned nblocks_tiled_ = 2048;
   bool qfresh_ = false;  // the tiled kernels' work queues were zeroed by the last item build
   bool tiled_ = true;             // SPH_INTERACTION=simple selects the one-lane-per-particle kernel
@@ -217,6 +231,16 @@ class SphGpuSingle {
   unsigned long long recvgcap_ = 0, recvmcap_ = 0;
   void* sendgbuf_ = nullptr;
   void* sendmbuf_ = nullptr;
+  // the ghost exchange after the divide (sph_kernels.hpp SlabFaces)
+  SlabFaces faces_{};
+  unsigned long long xg_sl_ = 0, xg_sr_ = 0, xg_rl_ = 0, xg_rr_ = 0;  // ghost records of this exchange
+  unsigned xg_nm_ = 0;            // migrants it appended (apppos[xg_nm_ + e] = slot of ghost e)
+  unsigned xg_np_ = 0;            // particles held after the migrants were appended
+  bool ghost_pending_ = false;    // the last divide's ghost records have not been sent yet
+  bool overlap_ = true;           // sph_slab_set_overlap
+  bool in_run_ = false;           // inside Run(): the next phase after a divide is the interaction
+  hipStream_t xstream_ = nullptr; // ghost transfer + scatter + face items beside the interior items
+  hipEvent_t ev_div_ = nullptr, ev_ghost_ = nullptr;
   // timing (hipEvents on the solver stream)
   bool timing_ = false;
   unsigned timing_mask_ = 0xfu;  // phases timed (SetTimingPhases, sph_solver_set_timing_phases)

@@ -180,9 +180,10 @@ struct ItemGroup {
 };
 struct ItemGroups {
   unsigned nf, nb;
-  __device__ __forceinline__ explicit ItemGroups(const DevScalars* sc) {
-    const unsigned n = sc->nitems;
-    nb = min(sc->nitems_bound, n);
+  // the list's counts {all, bound}, written by k_items_scan beside the work queues
+  __device__ __forceinline__ explicit ItemGroups(const unsigned* qctr) {
+    const unsigned n = qctr[QCTR_NITEMS];
+    nb = min(qctr[QCTR_NITEMS + 1], n);
     nf = n - nb;
   }
   __device__ __forceinline__ ItemGroup group(unsigned g) const {

@@ -318,7 +318,9 @@ typedef struct SphSlabDef {
 } SphSlabDef;
 
 /* Column bounds balancing sum(fluid) + bound_weight*sum(bound) particles per rank,
- * from the full initial particle set; cx_bounds[nranks+1] (first 0, last = cells). */
+ * from the full initial particle set; cx_bounds[nranks+1] (first 0, last = cells).
+ * Every slab gets at least 2W columns (W = ghost width: scelldiv, +1 with mDBC), the
+ * narrowest slab sph_slab_create accepts between two neighbours (W at a map end). */
 int sph_slab_partition(const SphCaseDef* cdef, const SphParticlesHost* all, int nranks, double bound_weight,
                        int32_t* cx_bounds);
 int sph_comm_unique_id(unsigned char id[128]);
@@ -351,6 +353,12 @@ int sph_slab_group_member(SphSlabGroup* g, int i, SphSolver** out);
  * the group) with the same values, before or between runs. */
 int sph_slab_set_repartition(SphSolver* s, uint32_t every, double bound_weight, double tolerance);
 int sph_slab_group_set_repartition(SphSlabGroup* g, uint32_t every, double bound_weight, double tolerance);
+/* Ghost exchange beside the interaction (default on): the ghost records of a divide travel
+ * while the items whose stencil reaches no ghost column interact; the face items follow.
+ * Off: the ghosts are in place before the interaction.  Results are bitwise the same.
+ * (No reference counterpart: the fork runs one domain per process, JSphGpuSingle.) */
+int sph_slab_set_overlap(SphSolver* s, int on);
+int sph_slab_group_set_overlap(SphSlabGroup* g, int on);
 typedef struct SphSlabInfo {
   int32_t rank, nranks, cx_begin, cx_end;  /* current owned columns [cx_begin, cx_end)        */
   uint32_t repartitions;                   /* bounds changes so far                          */

@@ -360,7 +360,8 @@ def test_gpu_bodies_on_slabs_with_repartition_match_reference(variant):
 
     x, g = _case(variant), _ref(variant)
     ncx = case_derive(x.case_def())["dom_cells"][0]
-    grp = SphSlabGroup(x, np.array([0, ncx // 5, ncx // 3, ncx], np.int32))
+    # uneven start; the middle slab 2W = 4 columns wide (the narrowest with mDBC)
+    grp = SphSlabGroup(x, np.array([0, ncx // 5, ncx // 5 + 4, ncx], np.int32))
     grp.set_repartition(4, 0.3, 0.0)
     done = 0
     for k in _kept(g):
@@ -379,7 +380,7 @@ def test_gpu_bodies_on_slabs_with_repartition_match_reference(variant):
 def test_gpu_mdbc_flap_normals_cross_slab_faces():
     """A fast, wide flap (no wait, 8 Hz, 12 degrees; mDBC, Symplectic): its particles cross
     cell columns within the run.  On 3 slabs whose middle one is the narrowest an mDBC slab
-    may be (its ghost width, 2 columns: the flap's initial column and the one before it),
+    may be (2W = 4 columns, the flap's initial column its last),
     every crossing flap particle migrates with its turned mDBC normal, and every ghost node's
     support stays inside its slab's grid (no SPH_ERR_UNSUPPORTED halo error); the merged
     state holds the reference PARTs (single-domain tolerance) and the single-domain GPU run."""
@@ -391,7 +392,7 @@ def test_gpu_mdbc_flap_normals_cross_slab_faces():
     flap = flap[x.pos[flap, 0] > x.pos[:, 0].mean()]  # the flap, not the piston
     cflap = int((x.pos[flap[0], 0] - k["map_realposmin"][0]) // np.float32(k["scell"]))
     b2 = min(cflap + 1, k["dom_cells"][0] - 2)
-    grp = SphSlabGroup(x, np.array([0, b2 - 2, b2, k["dom_cells"][0]], np.int32))
+    grp = SphSlabGroup(x, np.array([0, b2 - 4, b2, k["dom_cells"][0]], np.int32))
     one = _gpu(x)
     done = 0
     for kk in _kept(g):

@@ -80,7 +80,7 @@ def test_heavy_migration_matches_oracle():
     o = oracle.OracleSolver(case, nthreads=4)
     b0 = [s["np"] for s in grp.stats()]
     done = 0
-    for k in (5, 20):
+    for k in (10, 40):
         grp.run(k - done)
         o.run(k - done)
         done = k
@@ -89,9 +89,10 @@ def test_heavy_migration_matches_oracle():
     assert b0 != b1, "no particle changed slab"
 
 
-def test_single_column_slabs_and_exclusion():
-    """Slabs one column wide (ghost copies to both sides from the same column) and
-    excluded particles (OUTPOS through x < MapRealPosMin, OUTRHOP) in a slab run."""
+def test_narrowest_slabs_and_exclusion():
+    """The narrowest slabs (two columns between two neighbours: every owned column is a
+    face column) and excluded particles (OUTPOS through x < MapRealPosMin, OUTRHOP) in a
+    slab run."""
     case = DamBreakCase(0.03, celldomfixed=True, rhopoutmax=1010.0)
     rng = np.random.default_rng(7)
     pick = rng.choice(np.arange(case.npb, case.np), 12, replace=False)
@@ -101,7 +102,7 @@ def test_single_column_slabs_and_exclusion():
     from dualsphysics_multilayer_amd.core import case_derive
 
     ncx = case_derive(case.case_def())["dom_cells"][0]
-    bounds = np.array([0, 1, 2, 3, 4, ncx], np.int32)
+    bounds = np.array([0, 2, 4, 6, 8, ncx], np.int32)
     grp = group(case, 5, bounds)
     o = oracle.OracleSolver(case, nthreads=4)
     for k in range(1, 7):
@@ -141,9 +142,9 @@ def test_large_case_slabs_properties():
 
 
 def test_rccl_transport_single_rank():
-    """The RCCL transport end to end on one GPU: a 1-rank slab (ncclCommInitRank,
-    grouped send/recv with no neighbours, ncclAllReduce of the dt maxima) must step
-    like the single-domain solver."""
+    """The RCCL transport end to end on one GPU: a 1-rank slab (ncclCommInitRank; with no
+    neighbour it exchanges nothing and its own dt maxima are the domain's) must step like
+    the single-domain solver."""
     from dualsphysics_multilayer_amd.core import SphGpuSlab, case_derive, comm_unique_id
 
     case = DamBreakCase(0.025)
@@ -179,6 +180,68 @@ def test_cfg3_10m_slabs_match_single_domain():
     pg = grp.particles()
     assert np.array_equal(pg["idp"], p1["idp"])
     check_close(pg, p1, 5)
+
+
+def test_cfg3_10m_eight_slabs_with_repartition_match_single_domain():
+    """BASELINE cfg3's own split: the 10M case in 8 slabs (6 interior slabs with both faces,
+    the ghost exchange beside the interior items' interaction), re-partitioned every 2 steps
+    from step 4 on, against one domain after 8 steps: the same particles and simulated time,
+    fields within the 8-step noise tolerance."""
+    case = DamBreakCase(0.00205, step_algorithm=2, tdensity=1)
+    one = single(case)
+    one.run(8)
+    s1 = one.stats()
+    p1 = by_idp(one.particles())
+    one.close()
+    del one
+    grp = group(case, 8)
+    grp.run(4)
+    grp.set_repartition(2, 0.3, 0.0)
+    grp.run(4)
+    st = grp.stats()
+    assert sum(s["np"] for s in st) == s1["np"] == case.np
+    assert len({s["time"] for s in st}) == 1 and abs(st[0]["time"] - s1["time"]) <= 1e-9
+    assert all(s["error_flags"] == 0 for s in st)
+    assert max(i["repartitions"] for i in grp.slab_info()) >= 1
+    pg = grp.particles()
+    assert np.array_equal(pg["idp"], p1["idp"])
+    check_close(pg, p1, 8)
+
+
+@pytest.mark.parametrize("cfg", ["verlet_full", "symplectic_half", "verlet_repartition", "flume_bodies"])
+def test_ghost_overlap_is_bitwise_the_in_place_exchange(cfg):
+    """The ghost records of a divide sent beside the interaction of the items that reach no
+    ghost column (default) or put in place before the interaction: bitwise the same run."""
+    from dualsphysics_multilayer_amd.case import WaveFlumeCase
+    from dualsphysics_multilayer_amd.core import case_derive
+
+    rep = None
+    if cfg == "verlet_full":
+        case = DamBreakCase(0.025)
+        case.vel[case.npb:, 0] = 2.0
+        nslabs, bounds = 4, None
+    elif cfg == "symplectic_half":
+        case = DamBreakCase(0.03, step_algorithm=2, tdensity=1, cellmode=2, celldomfixed=True)
+        case.vel[case.npb:, 0] = -2.0
+        ncx = case_derive(case.case_def())["dom_cells"][0]
+        nslabs, bounds = 4, np.array([0, 4, 8, 12, ncx], np.int32)
+    elif cfg == "verlet_repartition":
+        case = DamBreakCase(0.025)
+        case.vel[case.npb:, 0] = 1.5
+        nslabs, bounds, rep = 3, None, (3, 0.3, 0.0)
+    else:  # moving boundaries + a floating body: ghosts in place before the interaction
+        case = WaveFlumeCase(0.03)
+        nslabs, bounds = 3, None
+    res = []
+    for ov in (True, False):
+        grp = group(case, nslabs, bounds)
+        grp.set_overlap(ov)
+        if rep:
+            grp.set_repartition(*rep)
+        grp.run(12)
+        res.append(grp.particles())
+    for k in ("idp", "pos", "vel", "rhop"):
+        assert np.array_equal(res[0][k], res[1][k]), k
 
 
 @pytest.mark.parametrize("name", ["verlet_ddt2_dp0.02", "symplectic_ddt1_dp0.025"])
@@ -244,16 +307,16 @@ def test_half_cell_slabs_match_reference_parts(nslabs):
         assert max(times) == min(times)
 
 
-def test_half_cell_two_column_slabs_migration_and_repartition():
-    """Slabs of exactly two half-cell columns (each owned column is a face column of both
-    neighbours), fluid pushed along +x so particles migrate every few steps, then
-    re-balancing every 4 steps: against the single-domain oracle."""
+def test_half_cell_narrowest_slabs_migration_and_repartition():
+    """Slabs of exactly four half-cell columns (two face columns towards each neighbour),
+    fluid pushed along +x so particles migrate every few steps, then re-balancing every 4
+    steps: against the single-domain oracle."""
     from dualsphysics_multilayer_amd.core import case_derive
 
     case = DamBreakCase(0.03, cellmode=2, celldomfixed=True)
     case.vel[case.npb:, 0] = 2.0
     ncx = case_derive(case.case_def())["dom_cells"][0]
-    grp = group(case, 4, np.array([0, 2, 4, 6, ncx], np.int32))
+    grp = group(case, 4, np.array([0, 4, 8, 12, ncx], np.int32))
     o = oracle.OracleSolver(case, nthreads=4)
     done = 0
     for k in (4, 12):
@@ -266,21 +329,24 @@ def test_half_cell_two_column_slabs_migration_and_repartition():
     o.run(12)
     check_close(grp.particles(), by_idp(o.particles()), 24)
     info = grp.slab_info()
-    assert all(i["cx_end"] - i["cx_begin"] >= 2 for i in info)
+    assert all(i["cx_end"] - i["cx_begin"] >= 4 for i in info)
     assert max(i["repartitions"] for i in info) >= 1
 
 
-def test_half_cell_partition_keeps_two_columns():
-    """slab_partition with CellMode=half gives every slab at least the two face columns; a
-    slab narrower than that is refused."""
+def test_half_cell_partition_keeps_disjoint_faces():
+    """slab_partition with CellMode=half gives every slab at least 2W = 4 columns (two
+    disjoint sets of two face columns); narrower slabs are refused: below W = 2 at a map
+    end, below 4 between two neighbours."""
     from dualsphysics_multilayer_amd.core import SphSlabGroup, case_derive, slab_partition
 
     case = DamBreakCase(0.03, cellmode=2)
     ncx = case_derive(case.case_def())["dom_cells"][0]
-    b = slab_partition(case, ncx // 2)
-    assert (np.diff(b) >= 2).all() and b[-1] == ncx
+    b = slab_partition(case, ncx // 4)
+    assert (np.diff(b) >= 4).all() and b[-1] == ncx
     with pytest.raises(Exception):
         SphSlabGroup(case, np.array([0, 1, ncx], np.int32))
+    with pytest.raises(Exception):
+        SphSlabGroup(case, np.array([0, 4, 7, ncx], np.int32))
 
 
 def test_half_cell_one_slab_matches_single_domain():

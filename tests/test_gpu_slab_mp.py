@@ -42,7 +42,8 @@ def merged(outs, k):
     return {q: v[o] for q, v in cat.items()}
 
 
-@pytest.mark.parametrize("golden,nranks", [("verlet_ddt2_dp0.02", 2), ("symplectic_ddt1_dp0.025", 3)])
+@pytest.mark.parametrize("golden,nranks", [("verlet_ddt2_dp0.02", 2), ("symplectic_ddt1_dp0.025", 3),
+                                           ("verlet_ddt2_dp0.02", 8)])
 def test_processes_match_reference_parts(tmp_path, golden, nranks):
     rc, outs, logs = run_ranks(tmp_path, nranks, golden)
     assert rc == [0] * nranks, logs

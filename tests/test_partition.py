@@ -1,7 +1,7 @@
 """Slab partition (sph_slab_partition, host C++ in the core library; no GPU needed).
 
-The x-columns are split into contiguous slabs of at least W columns (W = 1 full cells, 2
-half cells) minimising the heaviest slab's weight (fluid + bound_weight x bound particles
+The x-columns are split into contiguous slabs of at least 2W columns (W = the ghost width:
+1 with full cells, 2 with half cells; two disjoint face column sets per slab) minimising the heaviest slab's weight (fluid + bound_weight x bound particles
 per column): checked against an exhaustive dynamic programme on small dam breaks, and
 against the prefix-quantile split it replaced (never heavier).
 """
@@ -19,7 +19,7 @@ def column_weights(case, bw=0.3):
     cx = np.where(dx >= 0, (dx / scell).astype(np.int64), 0)
     cx = np.minimum(cx, ncx - 1)
     w = np.where(np.arange(case.np) < case.npb, bw, 1.0)
-    return np.bincount(cx, weights=w, minlength=ncx), int(k["scelldiv"])
+    return np.bincount(cx, weights=w, minlength=ncx), 2 * int(k["scelldiv"])
 
 
 def best_max_load(w, n, minw):
