@@ -245,6 +245,8 @@ class DamBreakCase:
             shift_tfs=float(np.float32(self.shift_tfs)),
             data2d=int(getattr(self, "data2d", False)),
             data2d_posy=0.0,
+            dtallparticles=int(getattr(self, "dtallparticles", 0)),
+            dtfixed=float(getattr(self, "dtfixed", 0.0)),
         )
 
 

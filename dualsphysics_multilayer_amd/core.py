@@ -18,6 +18,8 @@ import numpy as np
 
 from ._abi import (
     SPH_ABI_VERSION,
+    SPH_TTAB_DTFIXED,
+    SPH_TTAB_VISCO,
     SPH_STATUS,
     HostParticles,
     SphCaseDef,
@@ -85,6 +87,7 @@ EXPORTED_SYMBOLS = (
     "sph_solver_set_motion",
     "sph_solver_set_floatings",
     "sph_solver_set_floating_table",
+    "sph_solver_set_time_table",
     "sph_solver_floatings",
     "sph_partfloat_write",
 )
@@ -156,6 +159,7 @@ def load_library(path: str = LIB_PATH):
     L.sph_solver_set_motion.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(SphMotionMov), C.c_uint32,
                                         C.POINTER(SphMotionEvent)]
     L.sph_solver_set_floatings.argtypes = [vp, C.c_uint32, C.POINTER(SphFloatingDef), C.c_double]
+    L.sph_solver_set_time_table.argtypes = [vp, C.c_int32, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.sph_solver_set_floating_table.argtypes = [vp, C.c_uint32, C.c_int32, C.c_uint32, C.POINTER(C.c_double),
                                                 C.POINTER(C.c_double)]
     L.sph_solver_floatings.argtypes = [vp, C.c_uint32, C.POINTER(SphFloatingState), C.POINTER(C.c_uint32)]
@@ -203,9 +207,21 @@ class SphGpuSingle:
         self._time_set = None
         self._configure_bodies()
 
+    def set_time_table(self, kind: int, rows) -> None:
+        """DtFixedFile (kind SPH_TTAB_DTFIXED: rows (time s, dt ms)) or ViscoTime (SPH_TTAB_VISCO:
+        rows (time, Visco)) of the step; None / empty removes the table."""
+        rows = np.zeros((0, 2)) if rows is None else np.ascontiguousarray(rows, np.float64).reshape(-1, 2)
+        t, v = np.ascontiguousarray(rows[:, 0]), np.ascontiguousarray(rows[:, 1])
+        dp = C.POINTER(C.c_double)
+        _check(load_library().sph_solver_set_time_table(self._h, kind, len(rows), t.ctypes.data_as(dp),
+                                                         v.ctypes.data_as(dp)))
+
     def _configure_bodies(self) -> None:
-        """Motion program and floating bodies of the case (JSph::LoadCaseConfig)."""
+        """Time tables, motion program and floating bodies of the case (JSph::LoadCaseConfig)."""
         case, L = self.case, load_library()
+        for kind, key in ((SPH_TTAB_DTFIXED, "dtfixed_table"), (SPH_TTAB_VISCO, "visco_table")):
+            if getattr(case, key, None) is not None:
+                self.set_time_table(kind, getattr(case, key))
         if not getattr(case, "has_bodies", False):
             return
         # a restart sets the PART time first: the motion program is advanced to it

@@ -273,6 +273,11 @@ int sph_slab_group_set_repartition(SphSlabGroup* g, uint32_t every, double bound
   });
 }
 
+int sph_solver_set_time_table(SphSolver* s, int32_t kind, uint32_t n, const double* times, const double* values) {
+  NEED(s);
+  return guard([&] { s->impl->SetTimeTable(kind, n, times, values); });
+}
+
 int sph_slab_set_overlap(SphSolver* s, int on) {
   NEED(s);
   NOT_MEMBER(s);

@@ -126,6 +126,10 @@ void LocalHub::abort() {
 }
 
 class LocalTransport final : public SlabTransport {
+  // Copies on the DMA engines, not as blit kernels: like the xGMI transfers of the RCCL
+  // path they then run beside the interaction instead of queueing for its compute units.
+  static constexpr hipMemcpyKind kCopyKind = hipMemcpyDeviceToDeviceNoCU;
+
  public:
   LocalTransport(std::shared_ptr<LocalHub> hub, int r) : hub_(std::move(hub)) {
     rank = r;
@@ -143,12 +147,12 @@ class LocalTransport final : public SlabTransport {
     if (has_left() && nrl) {
       const LocalHub::Slot& L = hub_->slots[size_t(rank - 1)];
       if (L.nsr != nrl) throw SphError(SPH_ERR_COMM, "exchange: size mismatch with the left slab");
-      check_hip(hipMemcpyAsync(rl, L.sr, nrl, hipMemcpyDeviceToDevice, s), "exchange: copy from left");
+      check_hip(hipMemcpyAsync(rl, L.sr, nrl, kCopyKind, s), "exchange: copy from left");
     }
     if (has_right() && nrr) {
       const LocalHub::Slot& R = hub_->slots[size_t(rank + 1)];
       if (R.nsl != nrr) throw SphError(SPH_ERR_COMM, "exchange: size mismatch with the right slab");
-      check_hip(hipMemcpyAsync(rr, R.sl, nrr, hipMemcpyDeviceToDevice, s), "exchange: copy from right");
+      check_hip(hipMemcpyAsync(rr, R.sl, nrr, kCopyKind, s), "exchange: copy from right");
     }
     check_hip(hipStreamSynchronize(s), "exchange: copies");
     hub_->barrier();  // nobody reuses a send buffer before its copies are done

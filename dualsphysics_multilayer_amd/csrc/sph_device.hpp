@@ -83,7 +83,57 @@ struct KConst {
   // per-pass kernel factor folded out of the tiled sums (bwen/h, or 1 for the Cubic)
   int cubic;
   float kfold, cub_a2, cub_a24, cub_c1, cub_d1, cub_c2, cub_odw;
+  // time-dependent step options (JSph::LoadConfigParameters, JSph.cpp:619-622,697-707):
+  // DtAllParticles (VelMax over every particle, JSphCpu.cpp:475), DtFixed / DtFixedFile
+  // (JDsFixedDt: a constant dt, or dt(t) from rows of (time [s], dt [ms])) and ViscoTime
+  // (JDsViscoInput: Visco(t), evaluated at every step's TimeStep, JSphCpuSingle.cpp:1092)
+  int dtallp;
+  int dtfix_n;
+  double dtfix_val;
+  const double* dtfix_t;
+  const double* dtfix_v;
+  int visco_n;
+  float viscobf;  // ViscoBoundFactor: the boundary's visco from the current Visco
+  const float* visco_t;
+  const float* visco_v;
 };
+
+// JDsFixedDt::GetDt (JDsFixedDt.cpp) at TimeStep t: the constant, or the table's row interval
+// holding t (the reference's forward walk from the first row gives the same interval for
+// the non-decreasing times a run passes in), dt in ms -> s.
+__device__ __forceinline__ double fixed_dt(const KConst& K, double t) {
+  if (K.dtfix_val > 0) return K.dtfix_val;
+  const double* T = K.dtfix_t;
+  const double* V = K.dtfix_v;
+  const int n = K.dtfix_n;
+  int pos = 0;
+  double tini = T[0], tnext = (n > 1 ? T[1] : tini);
+  for (; tnext < t && pos + 2 < n; pos++) {
+    tini = tnext;
+    tnext = T[pos + 2];
+  }
+  if (t <= tini) return V[pos] / 1000;
+  if (t >= tnext) return V[pos + 1] / 1000;
+  const double f = (t - tini) / (tnext - tini);
+  return (f * (V[pos + 1] - V[pos]) + V[pos]) / 1000;
+}
+// JDsViscoInput::GetVisco (JDsViscoInput.cpp) at float(TimeStep), in its float/double mix.
+__device__ __forceinline__ float visco_at(const KConst& K, float t) {
+  const float* T = K.visco_t;
+  const float* V = K.visco_v;
+  const int n = K.visco_n;
+  int pos = 0;
+  float tini = T[0], tnext = (n > 1 ? T[1] : tini);
+  for (; tnext < t && pos + 2 < n; pos++) {
+    tini = tnext;
+    tnext = T[pos + 2];
+  }
+  if (t <= tini) return V[pos];
+  if (t >= tnext) return V[pos + 1];
+  const double f = double(t - tini) / double(tnext - tini);
+  const float vini = V[pos], vnext = V[pos + 1];
+  return float(f * (vnext - vini) + vini);
+}
 
 // NN phase constants on the device, two float4 per phase (sph_nn.hip loads them to LDS):
 //   [2k]   = {mass, cs0, visco, tau_yield}
@@ -123,7 +173,8 @@ constexpr unsigned DCELL_OUT = 0xFFFFFFFFu, DCELL_DISCARD = 0xFFFFFFFEu;
 // Device-resident step scalars.
 struct DevScalars {
   unsigned np, npb, npbok, nout;          // counts after the last divide
-  unsigned nitems, nitems_bound, nown, pad1; // tiled-interaction work items; owned particles (slab)
+  unsigned nitems, nitems_bound, nown;    // (unused); owned particles (slab)
+  float visco;                            // Visco of the step (ViscoTime; else K.visco)
   unsigned dtmodif, error_flags, npbout, ndiv;  // ndiv: particle count entering the divide
   unsigned long long nstep;
   double dt;        // dt of the step in flight

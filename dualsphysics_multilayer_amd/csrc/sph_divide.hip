@@ -298,6 +298,7 @@ struct GatherArgs {
   // slab: sorted values >= vfirst are reserved ghost slots -> apppos[value - appbase]
   unsigned vfirst, appbase;
   unsigned* apppos;
+  int allp;  // DtAllParticles: VelMax over every particle (JSphCpu.cpp:475), else fluid only
 };
 
 // WITHM1 / WITHPRE are template parameters so every load of a particle is issued before
@@ -436,7 +437,7 @@ __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, Gat
       float4 vr;
       bool fluid;
       gather_one<WITHM1, WITHPRE, WITHTAU>(a, i, sp[k], vr, fluid, npb);
-      if (fluid) v2 = nanmax(v2, vr.x * vr.x + vr.y * vr.y + vr.z * vr.z);  // CalcVelMaxOmp over fluid
+      if (fluid || a.allp) v2 = nanmax(v2, vr.x * vr.x + vr.y * vr.y + vr.z * vr.z);  // CalcVelMaxOmp
     }
   }
   wave_max_atomic(sc, RED_VELMAX2, v2);
@@ -451,6 +452,7 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
   a.vfirst = vfirst;
   a.appbase = appbase;
   a.apppos = apppos;
+  a.allp = K.dtallp;
   a.xoff = xoff;
   a.src = src;
   a.dst = dst;
@@ -652,6 +654,27 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
 // match on the 9-bit box offset), the stayers after the near arrivals whose list index is
 // at least Ln(obx(c)), far arrivals (a short list) by their previous index.  Two passes
 // over the window: counts, then (after the per-box scan) ranks -> positions.
+// Index of the first face box (SlabFaces order) whose key is >= key, for the face whose
+// first column is x0: the prefix of the face's counts there = its entries below key.
+__device__ __forceinline__ unsigned face_lower(const DivGrid& g, int W, unsigned key, int x0) {
+  const unsigned nfb1 = unsigned(g.ncz) * unsigned(g.ncy) * unsigned(W);  // face boxes of one type
+  unsigned type, cs;
+  if (key < g.nct) {
+    type = 0u;
+    cs = key;
+  } else if (key < g.boxfluid) {
+    return nfb1;  // BoundIgnore: after every bound face box
+  } else if (key < g.boxfluid + g.nct) {
+    type = 1u;
+    cs = key - g.boxfluid;
+  } else {
+    return 2u * nfb1;  // out and discard boxes: after every face box
+  }
+  const int x = int(cs % unsigned(g.ncx));
+  const unsigned r = cs / unsigned(g.ncx);  // z ncy + y
+  return type * nfb1 + r * unsigned(W) + unsigned(min(max(x - x0, 0), W));
+}
+
 constexpr int IB_FCAP = 256;  // far arrivals of a block held in LDS (more: read from global memory)
 constexpr int IB_TPCAP = 1024;  // window tiles with LDS prefixes (more: computed from global memory)
 constexpr int IB_WCAP = 4096;   // window near movers staged in LDS (more: read from global memory)
@@ -676,7 +699,9 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   __shared__ unsigned s_boff[IB_BOX];   // bucket offsets (exclusive scan of s_narr)
   __shared__ unsigned s_nwsum[IB_BPT][IB_BS / 64];
   __shared__ unsigned s_nar;
-  __shared__ unsigned s_ab[IB_BOX + 1];  // slab: appended particles with a key below each box
+  // slab: appended entries with a key below each box, per sorted list (migrants, left and
+  // right ghost slots)
+  __shared__ unsigned s_ab[3][IB_BOX + 1];
   const unsigned b = blockIdx.x;
   TSDECL;
   TSTAMP(0);
@@ -913,13 +938,28 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   TSTAMP(2);
   // ---- slab: the appended particles (sorted by key) below each box of the block; they
   // follow the old members of their box (larger previous index), in appended order
-  const unsigned napt = s.napp + s.nappv;  // appended particles + reserved ghost slots
+  // Appended entries, three lists sorted by key: the migrants (sorted apart), the left and
+  // the right face's reserved ghost slots (generated in key order).  A box holds entries of
+  // one list at most (migrants land in owned columns, ghosts in ghost columns).
+  const unsigned napt = s.napp + s.nvl + s.nvr;
   if (napt) {
-    for (int k = int(threadIdx.x); k <= IB_BOX; k += IB_BS)
-      s_ab[k] = lower_bound_u32(s.akeys, 0u, napt, unsigned(min(c0 + k, nctt)));
+    // migrants: the block's range of their sorted keys (two searches of a short list), then
+    // every box's bound inside it; ghost slots: the prefix of the face-box counts at the
+    // first face box at or after the box (O(1))
+    if (threadIdx.x < 2)
+      s_ab[0][threadIdx.x ? IB_BOX : 0] =
+          lower_bound_u32(s.akeys, 0u, s.napp, unsigned(min(c0 + (threadIdx.x ? IB_BOX : 0), nctt)));
+    __syncthreads();
+    const unsigned a0 = s_ab[0][0], a1 = s_ab[0][IB_BOX];
+    for (int k = int(threadIdx.x); k <= IB_BOX; k += IB_BS) {
+      const unsigned key = unsigned(min(c0 + k, nctt));
+      if (k > 0 && k < IB_BOX) s_ab[0][k] = a0 == a1 ? a0 : lower_bound_u32(s.akeys, a0, a1, key);
+      s_ab[1][k] = s.nvl ? s.vpre[0][face_lower(g, s.vW, key, 0)] : 0u;
+      s_ab[2][k] = s.nvr ? s.vpre[1][face_lower(g, s.vW, key, g.xown1)] : 0u;
+    }
     __syncthreads();
   }
-  auto ab = [&](int k) -> unsigned { return napt ? s_ab[k] : 0u; };
+  auto ab = [&](int k) -> unsigned { return napt ? s_ab[0][k] + s_ab[1][k] + s_ab[2][k] : 0u; };
   // ---- per-box scan: begin, stayer offset, counts
   const unsigned base0 = jlo + s_below + s_farbelow;
   unsigned cnt[IB_BPT], xs[IB_BPT], xsn[IB_BPT];
@@ -970,7 +1010,12 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
     nbc[cu] = begin;
     s.stayoff[cu] = begin + s_nbef[k] + s_fbef[k] - S;
     const unsigned total = cnt[h] + stay + (ab(k + 1) - ab(k));
-    for (unsigned e = ab(k); e < ab(k + 1); e++) s.apppos[s.avals[e]] = begin + cnt[h] + stay + (e - ab(k));
+    if (napt) {  // the box's appended entries after its old members
+      unsigned pos = begin + cnt[h] + stay;
+      for (unsigned e = s_ab[0][k]; e < s_ab[0][k + 1]; e++) s.apppos[s.avals[e]] = pos++;
+      for (unsigned j = s_ab[1][k]; j < s_ab[1][k + 1]; j++) s.apppos[s.napp + j] = pos++;
+      for (unsigned j = s_ab[2][k]; j < s_ab[2][k + 1]; j++) s.apppos[s.napp + s.nvl + j] = pos++;
+    }
     // JCellDivCpuSingle::Divide counts + RunCellDivide, as k_begincell
     if (cu == g.boxboundignore) sc->npbok = begin;
     if (cu == g.boxfluid) sc->npb = begin;
@@ -1123,7 +1168,8 @@ __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, G
     if (i0 + 256 * k < nd && pos[k] < n) {
       gather_store<WITHM1, WITHPRE, WITHTAU>(a, pos[k], q[k]);
       s.skeys[pos[k]] = key[k];
-      if (pos[k] >= npb) v2 = nanmax(v2, q[k].vr.x * q[k].vr.x + q[k].vr.y * q[k].vr.y + q[k].vr.z * q[k].vr.z);
+      if (pos[k] >= npb || a.allp)
+        v2 = nanmax(v2, q[k].vr.x * q[k].vr.x + q[k].vr.y * q[k].vr.y + q[k].vr.z * q[k].vr.z);
     }
   }
   wave_max_atomic(sc, RED_VELMAX2, v2);
@@ -1132,6 +1178,41 @@ __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, G
     for (unsigned u = threadIdx.x; u < nsup; u += 256) s.tsup[u] = 0ull;
     if (threadIdx.x == 0) s.ctr[0] = 0u;
   }
+}
+
+// A short list (the migrants of an exchange) sorted stably by key in one block: bitonic
+// sort of (key << 32 | index) in LDS (the indices are distinct, so the order is stable).
+__global__ __launch_bounds__(1024) void k_small_sort(const unsigned* __restrict__ kin, const unsigned* __restrict__ vin,
+                                                     unsigned n, unsigned* __restrict__ kout,
+                                                     unsigned* __restrict__ vout) {
+  __shared__ unsigned long long v[SMALLSORT_MAX];
+  for (unsigned i = threadIdx.x; i < SMALLSORT_MAX; i += 1024)
+    v[i] = i < n ? ((static_cast<unsigned long long>(kin[i]) << 32) | vin[i]) : ~0ull;
+  __syncthreads();
+  for (unsigned k = 2; k <= SMALLSORT_MAX; k <<= 1) {
+    for (unsigned j = k >> 1; j > 0; j >>= 1) {
+      for (unsigned i = threadIdx.x; i < SMALLSORT_MAX; i += 1024) {
+        const unsigned l = i ^ j;
+        if (l > i) {
+          const unsigned long long a = v[i], b = v[l];
+          if (((i & k) == 0) == (a > b)) {
+            v[i] = b;
+            v[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (unsigned i = threadIdx.x; i < n; i += 1024) {
+    kout[i] = unsigned(v[i] >> 32);
+    vout[i] = unsigned(v[i]);
+  }
+}
+
+void launch_small_sort(hipStream_t stm, const unsigned* kin, const unsigned* vin, unsigned n, unsigned* kout,
+                       unsigned* vout) {
+  if (n) hipLaunchKernelGGL(k_small_sort, dim3(1), dim3(1024), 0, stm, kin, vin, n, kout, vout);
 }
 
 void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& src, const PartArrays& dst,
@@ -1144,15 +1225,27 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
   const unsigned omax = 1u + (usey ? unsigned(g.ncx) : 0u) + (usez ? g.nsheet : 0u);
   s.akin = srt.keys[0];
   s.avin = srt.vals[0];
-  s.nappv = faces ? ngl + ngr : 0u;
+  s.nvl = faces ? ngl : 0u;
+  s.nvr = faces ? ngr : 0u;
   hipLaunchKernelGGL(k_inc_classify, dim3(s.nb1), dim3(INC_BS), 0, stm, sc, src.dcell, src.code, g, K.domcellcode, s,
                      usey, usez);
-  // slab: the reserved ghost slots after the appended particles
-  if (s.nappv) launch_ghost_keys(stm, *faces, g, ngl, ngr, s.akin + s.napp, s.avin + s.napp, s.napp);
-  if (s.napp + s.nappv) {  // slab: the appended particles, sorted by key apart (stable: appended order)
-    const int res = launch_radix_sort(stm, cap, sc, srt, keybits, s.napp + s.nappv);
-    s.akeys = srt.keys[res];
-    s.avals = srt.vals[res];
+  // slab: the reserved ghost slots are counted per face box (faces->pre: the received
+  // counts' prefixes); k_inc_boxes reads their bounds from the prefixes, no keys needed
+  if (faces) {
+    s.vpre[0] = faces->pre[2];
+    s.vpre[1] = faces->pre[3];
+    s.vW = faces->W;
+  }
+  if (s.napp) {  // slab: the appended migrants, sorted by key apart (stable: appended order)
+    if (s.napp <= SMALLSORT_MAX) {
+      launch_small_sort(stm, srt.keys[0], srt.vals[0], s.napp, srt.keys[1], srt.vals[1]);
+      s.akeys = srt.keys[1];
+      s.avals = srt.vals[1];
+    } else {
+      const int res = launch_radix_sort(stm, cap, sc, srt, keybits, s.napp);
+      s.akeys = srt.keys[res];
+      s.avals = srt.vals[res];
+    }
   }
   hipLaunchKernelGGL(k_inc_boxes, dim3(s.nb2), dim3(IB_BS), 0, stm, sc, g, begincell_old, begincell_new, s, omax);
   GatherArgs a;
@@ -1160,6 +1253,7 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
   a.vfirst = ~0u;
   a.appbase = 0;
   a.apppos = nullptr;
+  a.allp = K.dtallp;
   a.xoff = g.xoff;
   a.src = src;
   a.dst = dst;
@@ -1227,6 +1321,7 @@ void launch_ghost_scatter(hipStream_t stm, DevScalars* sc, const SlabGhost* rec,
   a.vfirst = ~0u;
   a.appbase = 0;
   a.apppos = nullptr;
+  a.allp = K.dtallp;
   a.xoff = g.xoff;
   a.src = dst;
   a.dst = dst;

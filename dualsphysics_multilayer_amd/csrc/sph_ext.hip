@@ -463,13 +463,15 @@ __global__ __launch_bounds__(TB) void k_fluid_ext(DevScalars* __restrict__ sc, c
         f.sx = FLT_MAX;
         if (TD) f.delta = FLT_MAX;
       }
-      ext_pass<TVISCO, TD, SHIFT, FT, 0>(K, E, g, rc, p, thr, bc, !ordf, K.visco, sA, sB, sC, sD, f);
+      const float visco = K.visco_n ? sc->visco : K.visco;  // ViscoTime (k_dt) or the case's
+      ext_pass<TVISCO, TD, SHIFT, FT, 0>(K, E, g, rc, p, thr, bc, !ordf, visco, sA, sB, sC, sD, f);
       b.sx = f.sx;
       b.sy = f.sy;
       b.sz = f.sz;
       b.sw = f.sw;
       if (p.ftp1 && TD) b.delta = FLT_MAX;
-      ext_pass<TVISCO, TD, SHIFT, FT, 1>(K, E, g, rc, p, thr, bc, !ordb, K.viscobound, sA, sB, sC, sD, b);
+      ext_pass<TVISCO, TD, SHIFT, FT, 1>(K, E, g, rc, p, thr, bc, !ordb, K.visco_n ? visco * K.viscobf : K.viscobound,
+                                         sA, sB, sC, sD, b);
       if (act) {
         // the two passes' stores (:800-818); with shifting both always store
         float ar = 0.f, ax = 0.f, ay = 0.f, az = 0.f, delta = 0.f;

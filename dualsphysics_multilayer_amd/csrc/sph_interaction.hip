@@ -166,6 +166,10 @@ __global__ __launch_bounds__(256) void k_interaction(DevScalars* __restrict__ sc
                                                      const float* __restrict__ press,
                                                      const unsigned* __restrict__ begincell, DivGrid g, KConst K,
                                                      float4* __restrict__ arace, FtView ft = {}) {
+  if (K.visco_n) {  // ViscoTime: the step's Visco (k_dt)
+    K.visco = sc->visco;
+    K.viscobound = K.visco * K.viscobf;
+  }
   const unsigned np = sc->np, npb = sc->npb, npbok = sc->npbok;
   const unsigned p1 = blockIdx.x * blockDim.x + threadIdx.x;
   float viscmax = 0.f, ace2 = 0.f;

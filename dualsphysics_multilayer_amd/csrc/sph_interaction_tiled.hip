@@ -40,155 +40,221 @@ namespace sphx {
 constexpr int ROWCELLS_LDS = 1024;
 
 struct ItemRanges {
-  int x[6];  // up to three local column ranges [x[2k], x[2k+1]) of p1 (empty when equal)
+  int x[6];  // column ranges [x[2k], x[2k+1]) of p1 (empty when equal): list A = range 0 (and
+             // 1, 2 with one list), list B = ranges 1, 2
+  int nl;    // lists: 1 or 2
 };
+constexpr int IR_WAVES = 4;  // rows per block: one wave each
 
+// One wave walks one (y,z) row of one kind (fluid or bound p1): its cell begin offsets to LDS,
+// then lane 0 emits the items of each column range of each list.  WRITE = false counts them
+// (counts[list][row]), true writes them at the scanned offsets.
 template <bool WRITE>
-__global__ __launch_bounds__(64) void k_items_rows(const unsigned* __restrict__ bc, DivGrid g, int tmaxc,
-                                                   unsigned* __restrict__ counts, uint4* __restrict__ items,
-                                                   ItemRanges xr) {
-  __shared__ unsigned pre[ROWCELLS_LDS + 1];            // begin offset of every cell of the row, + row end
-  __shared__ unsigned short nzfrom[ROWCELLS_LDS + 1];  // first non-empty cell >= x in the range (xend if none)
-  const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz);
-  const unsigned r = blockIdx.x;
+__global__ __launch_bounds__(64 * IR_WAVES) void k_items_rows(const unsigned* __restrict__ bc, DivGrid g, int tmaxc,
+                                                              unsigned* __restrict__ counts,
+                                                              uint4* __restrict__ items, ItemRanges xr) {
+  __shared__ unsigned s_pre[IR_WAVES][ROWCELLS_LDS + 1];  // begin offset of every cell of the row, + row end
+  __shared__ unsigned short s_nz[IR_WAVES][ROWCELLS_LDS + 1];  // first non-empty cell >= x in the range
+  const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz), nrows2 = 2u * nrows;
+  const unsigned w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const unsigned r = blockIdx.x * IR_WAVES + w;
+  if (r >= nrows2) return;  // whole waves (no block-wide barrier below)
+  unsigned* pre = s_pre[w];
+  unsigned short* nzfrom = s_nz[w];
   const bool bound = r >= nrows;
   const unsigned rr = bound ? r - nrows : r;
   const unsigned y = rr % unsigned(g.ncy), z = rr / unsigned(g.ncy);
   const unsigned rowbase = (bound ? 0u : g.boxfluid) + z * g.nsheet + y * unsigned(g.ncx);
   const int ncx = g.ncx;
-  uint4* out = WRITE ? items + counts[r] : nullptr;
-  unsigned nitems = 0;
-  auto emit = [&](int a, int e, unsigned p, unsigned q) {
-    if (WRITE)
-      out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(e) << 16), p, q);
-    nitems++;
-  };
+  {  // a row without particles in its ranges (most rows of the air above the water and of
+     // the boundary): no items, no staging
+    int xlo = ncx, xhi = 0;
+    for (int k = 0; k < 3; k++)
+      if (xr.x[2 * k] < xr.x[2 * k + 1]) {
+        xlo = min(xlo, xr.x[2 * k]);
+        xhi = max(xhi, xr.x[2 * k + 1]);
+      }
+    if (xlo >= xhi || bc[rowbase + xlo] == bc[rowbase + xhi]) {
+      if (!WRITE && lane == 0)
+        for (int list = 0; list < xr.nl; list++) counts[list * nrows2 + r] = 0u;
+      return;
+    }
+  }
   const bool lds = ncx <= ROWCELLS_LDS;
   if (lds) {
-    for (int x = int(threadIdx.x); x <= ncx; x += 64) pre[x] = bc[rowbase + x];
-    __syncthreads();
+    for (int x = int(lane); x <= ncx; x += 64) pre[x] = bc[rowbase + x];
+    __builtin_amdgcn_wave_barrier();
   }
-  // p1 only in the owned columns (slab ghosts are neighbours, never p1), in up to three column
-  // ranges (a slab's face columns and the columns between them), each walked on its own so
-  // no item crosses from one to the next
-  for (int rg = 0; rg < 3; rg++) {
-    const int xbeg = xr.x[2 * rg], xend = xr.x[2 * rg + 1];  // uniform over the block
-    if (xbeg >= xend) continue;
-    if (!lds) {  // very long rows: the same walk on global memory, cell by cell
-      if (threadIdx.x == 0) {
-        auto PRE = [&](int x) -> unsigned { return bc[rowbase + x]; };
-        unsigned p = PRE(xbeg);
-        const unsigned pend = PRE(xend);
-        int c = xbeg;
-        while (p < pend) {
-          while (PRE(c + 1) <= p) c++;
-          const unsigned q = min(min(p + unsigned(TB), pend), PRE(min(c + tmaxc, xend)));
-          int e = c;
-          while (PRE(e + 1) < q) e++;
-          emit(c, e, p, q);
-          p = q;
-          c = e;
+  for (int list = 0; list < xr.nl; list++) {
+    uint4* out = WRITE ? items + counts[list * nrows2 + r] : nullptr;
+    unsigned nitems = 0;
+    auto emit = [&](int a, int e, unsigned p, unsigned q) {
+      if (WRITE)
+        out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(e) << 16), p, q);
+      nitems++;
+    };
+    // p1 only in owned columns (slab ghosts are neighbours, never p1); each range walked on
+    // its own, so no item crosses from one to the next
+    for (int rg = (list ? 1 : 0); rg < (xr.nl == 2 && list == 0 ? 1 : 3); rg++) {
+      const int xbeg = xr.x[2 * rg], xend = xr.x[2 * rg + 1];  // uniform over the wave
+      if (xbeg >= xend) continue;
+      if (!lds) {  // very long rows: the same walk on global memory, cell by cell
+        if (lane == 0) {
+          auto PRE = [&](int x) -> unsigned { return bc[rowbase + x]; };
+          unsigned p = PRE(xbeg);
+          const unsigned pend = PRE(xend);
+          int c = xbeg;
+          while (p < pend) {
+            while (PRE(c + 1) <= p) c++;
+            const unsigned q = min(min(p + unsigned(TB), pend), PRE(min(c + tmaxc, xend)));
+            int e = c;
+            while (PRE(e + 1) < q) e++;
+            emit(c, e, p, q);
+            p = q;
+            c = e;
+          }
         }
+        continue;
       }
-      continue;
-    }
-    // first non-empty cell of the range at or after x: lane-local blocks, then a wave suffix-min
-    const int per = (ncx + 63) / 64, x0 = int(threadIdx.x) * per, x1 = min(x0 + per, ncx);
-    int nz = xend;
-    for (int x = x1 - 1; x >= x0; x--) {
-      if (x >= xbeg && x < xend && pre[x + 1] > pre[x]) nz = x;
-      nzfrom[x] = (unsigned short)nz;
-    }
-    int suf = nz;
+      // first non-empty cell of the range at or after x: lane-local blocks, then a wave suffix-min
+      const int per = (ncx + 63) / 64, x0 = int(lane) * per, x1 = min(x0 + per, ncx);
+      int nz = xend;
+      for (int x = x1 - 1; x >= x0; x--) {
+        if (x >= xbeg && x < xend && pre[x + 1] > pre[x]) nz = x;
+        nzfrom[x] = (unsigned short)nz;
+      }
+      int suf = nz;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int v = __shfl_down(suf, off, 64);
-      if (int(threadIdx.x) + off < 64) suf = min(suf, v);
-    }
-    const int later = __shfl_down(suf, 1, 64);
-    const int carry = int(threadIdx.x) < 63 ? later : xend;
-    for (int x = x0; x < x1; x++)
-      if (int(nzfrom[x]) == xend) nzfrom[x] = (unsigned short)carry;
-    if (threadIdx.x == 63) nzfrom[ncx] = (unsigned short)xend;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      // Walk the items: the cell holding p is known (c), the cell holding q-1 is at most
-      // TMAXCELLS-1 cells further, an item ending at a cell end jumps to the next non-empty.
-      // The five offsets pre[c..c+4] of an item are independent LDS reads (one latency);
-      // the cell holding q-1 is c + #{k = 1..3 : pre[c+k] <= q-1}.
-      static_assert(TMAXCELLS == 4, "the walk reads pre[c..c+4]");
-      const unsigned pend = pre[xend];
-      int c = nzfrom[xbeg];
-      unsigned p = c < xend ? pre[c] : pend;
-      if (tmaxc != TMAXCELLS) {  // CellMode=half: longer items, the cell holding q-1 by a short scan
-        while (p < pend) {
-          const unsigned q = min(min(p + unsigned(TB), pend), pre[min(c + tmaxc, xend)]);
-          int e = c;
-          while (pre[e + 1] <= q - 1) e++;
-          emit(c, e, p, q);
-          p = q;
-          c = pre[e + 1] == q ? int(nzfrom[e + 1]) : e;
-        }
-      } else {
-        while (p < pend) {
-          const unsigned p1 = pre[min(c + 1, xend)], p2 = pre[min(c + 2, xend)], p3 = pre[min(c + 3, xend)];
-          const unsigned p4 = pre[min(c + 4, xend)];
-          const unsigned q = min(min(p + unsigned(TB), pend), p4);
-          const int e = c + int(p1 <= q - 1) + int(p2 <= q - 1) + int(p3 <= q - 1);
-          emit(c, e, p, q);
-          p = q;
-          const unsigned pe1 = e + 1 - c == 1 ? p1 : e + 1 - c == 2 ? p2 : e + 1 - c == 3 ? p3 : p4;
-          c = pe1 == q ? int(nzfrom[e + 1]) : e;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_down(suf, off, 64);
+        if (int(lane) + off < 64) suf = min(suf, v);
+      }
+      const int later = __shfl_down(suf, 1, 64);
+      const int carry = int(lane) < 63 ? later : xend;
+      for (int x = x0; x < x1; x++)
+        if (int(nzfrom[x]) == xend) nzfrom[x] = (unsigned short)carry;
+      if (lane == 63) nzfrom[ncx] = (unsigned short)xend;
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) {
+        // Walk the items: the cell holding p is known (c), the cell holding q-1 is at most
+        // TMAXCELLS-1 cells further, an item ending at a cell end jumps to the next non-empty.
+        // The five offsets pre[c..c+4] of an item are independent LDS reads (one latency);
+        // the cell holding q-1 is c + #{k = 1..3 : pre[c+k] <= q-1}.
+        static_assert(TMAXCELLS == 4, "the walk reads pre[c..c+4]");
+        const unsigned pend = pre[xend];
+        int c = nzfrom[xbeg];
+        unsigned p = c < xend ? pre[c] : pend;
+        if (tmaxc != TMAXCELLS) {  // CellMode=half: longer items, the cell holding q-1 by a short scan
+          while (p < pend) {
+            const unsigned q = min(min(p + unsigned(TB), pend), pre[min(c + tmaxc, xend)]);
+            int e = c;
+            while (pre[e + 1] <= q - 1) e++;
+            emit(c, e, p, q);
+            p = q;
+            c = pre[e + 1] == q ? int(nzfrom[e + 1]) : e;
+          }
+        } else {
+          while (p < pend) {
+            const unsigned p1 = pre[min(c + 1, xend)], p2 = pre[min(c + 2, xend)], p3 = pre[min(c + 3, xend)];
+            const unsigned p4 = pre[min(c + 4, xend)];
+            const unsigned q = min(min(p + unsigned(TB), pend), p4);
+            const int e = c + int(p1 <= q - 1) + int(p2 <= q - 1) + int(p3 <= q - 1);
+            emit(c, e, p, q);
+            p = q;
+            const unsigned pe1 = e + 1 - c == 1 ? p1 : e + 1 - c == 2 ? p2 : e + 1 - c == 3 ? p3 : p4;
+            c = pe1 == q ? int(nzfrom[e + 1]) : e;
+          }
         }
       }
+      __builtin_amdgcn_wave_barrier();  // nzfrom is rebuilt for the next range
     }
-    __syncthreads();  // nzfrom is rebuilt for the next range
+    if (!WRITE && lane == 0) counts[list * nrows2 + r] = nitems;
   }
-  if (!WRITE && threadIdx.x == 0) counts[r] = nitems;
 }
 
-// Exclusive scan of the per-row item counts (one block) -> item offsets, the list's counts
-// {all, bound} into qctr[QCTR_NITEMS]; zeroes the per-XCD work queues of the next interaction.
-__global__ __launch_bounds__(1024) void k_items_scan(unsigned* __restrict__ counts, unsigned nrows2,
-                                                     unsigned* __restrict__ qctr) {
-  __shared__ unsigned part[1024];
-  if (threadIdx.x < 8) qctr[threadIdx.x * QSTRIDE] = 0u;  // the interaction's item queues start over
-  const unsigned per = (nrows2 + 1023) / 1024;
-  const unsigned b0 = min(threadIdx.x * per, nrows2), b1 = min(b0 + per, nrows2);
-  unsigned s = 0;
-  for (unsigned i = b0; i < b1; i++) s += counts[i];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const unsigned v = (threadIdx.x >= unsigned(off) ? part[threadIdx.x - off] : 0u);
+// Exclusive scan of the per-row item counts of the lists (one block, tiles of 8192 through
+// LDS) -> item offsets; each list's counts {all, bound, first item} into its counter block
+// (qctr[QCTR_NITEMS...]) and its per-XCD work queues zeroed for the next interaction.
+constexpr int IS_BS = 1024, IS_PT = 8, IS_TILE = IS_BS * IS_PT;
+__global__ __launch_bounds__(IS_BS) void k_items_scan(unsigned* __restrict__ counts, unsigned nrows2, int nl,
+                                                      unsigned* __restrict__ qa, unsigned* __restrict__ qb) {
+  __shared__ unsigned v[IS_TILE];
+  __shared__ unsigned wsum[IS_BS / 64];
+  __shared__ unsigned carry, mark[4];
+  if (threadIdx.x < 8) {  // the interaction's item queues start over
+    qa[threadIdx.x * QSTRIDE] = 0u;
+    if (nl == 2) qb[threadIdx.x * QSTRIDE] = 0u;
+  }
+  const unsigned n = unsigned(nl) * nrows2, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned nrows = nrows2 / 2;
+  if (threadIdx.x == 0) carry = 0;
+  for (unsigned t0 = 0; t0 < n; t0 += IS_TILE) {
+#pragma unroll
+    for (int k = 0; k < IS_PT; k++) {
+      const unsigned i = t0 + k * IS_BS + threadIdx.x;
+      v[k * IS_BS + threadIdx.x] = i < n ? counts[i] : 0u;
+    }
     __syncthreads();
-    part[threadIdx.x] += v;
+    unsigned x[IS_PT], sum = 0;
+#pragma unroll
+    for (int k = 0; k < IS_PT; k++) {
+      x[k] = sum;
+      sum += v[threadIdx.x * IS_PT + k];
+    }
+    unsigned inc = sum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned yv = __shfl_up(inc, off, 64);
+      if (lane >= unsigned(off)) inc += yv;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    unsigned before = carry;
+    for (unsigned q = 0; q < w; q++) before += wsum[q];
+    before += inc - sum;
+#pragma unroll
+    for (int k = 0; k < IS_PT; k++) {
+      const unsigned i = t0 + threadIdx.x * IS_PT + k;
+      // the offsets where each list's bound rows and the second list begin
+      if (i == nrows) mark[0] = before + x[k];
+      if (i == nrows2) mark[1] = before + x[k];
+      if (i == nrows2 + nrows) mark[2] = before + x[k];
+      v[threadIdx.x * IS_PT + k] = before + x[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < IS_PT; k++) {
+      const unsigned i = t0 + k * IS_BS + threadIdx.x;
+      if (i < n) counts[i] = v[k * IS_BS + threadIdx.x];
+    }
+    if (threadIdx.x == IS_BS - 1) carry = before + sum;
     __syncthreads();
   }
-  unsigned run = (threadIdx.x ? part[threadIdx.x - 1] : 0u);
-  for (unsigned i = b0; i < b1; i++) {
-    const unsigned v = counts[i];
-    counts[i] = run;
-    run += v;
+  if (threadIdx.x == 0) {
+    const unsigned tot = carry, na = nl == 2 ? mark[1] : tot;
+    qa[QCTR_NITEMS] = na;
+    qa[QCTR_NITEMS + 1] = na - mark[0];  // the bound rows' items: the list's tail (ItemGroups)
+    qa[QCTR_NITEMS + 2] = 0u;
+    if (nl == 2) {
+      qb[QCTR_NITEMS] = tot - na;
+      qb[QCTR_NITEMS + 1] = tot - mark[2];
+      qb[QCTR_NITEMS + 2] = na;  // the second list follows the first in the item array
+    }
   }
-  if (threadIdx.x == 1023) qctr[QCTR_NITEMS] = part[1023];
-  __syncthreads();
-  // items of the bound rows (the list's tail): each XCD group takes its share of them
-  // after its fluid items (ItemGroups)
-  if (threadIdx.x == 0) qctr[QCTR_NITEMS + 1] = part[1023] - counts[nrows2 / 2];
 }
 
 void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
-                  uint4* items, unsigned* qctr, int scelldiv, const int* xr) {
+                  uint4* items, unsigned* qctr, int scelldiv, const int* xr, unsigned* qctr2) {
   (void)sc;
   const int tmaxc = scelldiv == 1 ? TMAXCELLS : TMAXCELLS_HALF;
   const unsigned nrows2 = 2u * unsigned(g.ncy) * unsigned(g.ncz);
-  ItemRanges r = {{g.xown0, g.xown1, 0, 0, 0, 0}};
+  ItemRanges r = {{g.xown0, g.xown1, 0, 0, 0, 0}, qctr2 ? 2 : 1};
   if (xr)
     for (int k = 0; k < 6; k++) r.x[k] = xr[k];
-  hipLaunchKernelGGL(k_items_rows<false>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, nullptr, r);
-  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, rowtmp, nrows2, qctr);
-  hipLaunchKernelGGL(k_items_rows<true>, dim3(nrows2), dim3(64), 0, stm, begincell, g, tmaxc, rowtmp, items, r);
+  const unsigned nb = (nrows2 + IR_WAVES - 1) / IR_WAVES;
+  hipLaunchKernelGGL(k_items_rows<false>, dim3(nb), dim3(64 * IR_WAVES), 0, stm, begincell, g, tmaxc, rowtmp, nullptr, r);
+  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(IS_BS), 0, stm, rowtmp, nrows2, r.nl, qctr, qctr2);
+  hipLaunchKernelGGL(k_items_rows<true>, dim3(nb), dim3(64 * IR_WAVES), 0, stm, begincell, g, tmaxc, rowtmp, items, r);
 }
 
 // ------------------------------------------------------------------------------------
@@ -758,8 +824,10 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
   const ItemGroups IG(qctr);
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f;
-  const float cvisc_f = -K.visco * K.cs0f * K.kernelh * K.massfluid;
-  const float cvisc_b = -K.viscobound * K.cs0f * K.kernelh * K.massbound;
+  // Visco of the step: ViscoTime's value (device-resident, k_dt) or the case's
+  const float visco = K.visco_n ? sc->visco : K.visco, viscob = K.visco_n ? visco * K.viscobf : K.viscobound;
+  const float cvisc_f = -visco * K.cs0f * K.kernelh * K.massfluid;
+  const float cvisc_b = -viscob * K.cs0f * K.kernelh * K.massbound;
 
   for (unsigned q = 0; q < 8; q++) {
     const unsigned xg = (grp + q) & 7;

@@ -168,16 +168,23 @@ struct IncDivScratch {
   const unsigned* avals = nullptr;
   unsigned* apppos = nullptr;     // [cap]
   unsigned nold = 0, napp = 0;
-  // slab: reserved ghost slots after the appended particles (sorted with them: akin/avin
-  // [napp, napp + nappv), their positions apppos[napp + e]); no particle data until
-  // launch_ghost_scatter
-  unsigned nappv = 0;
+  // slab: reserved ghost slots after the old members of their boxes, like the appended
+  // particles: nvl of the left face, nvr of the right, counted per face box (vpre: the
+  // prefixes of the received counts, SlabFaces order, vW ghost columns), positions
+  // apppos[napp + e]; no particle data until launch_ghost_scatter
+  const unsigned* vpre[2] = {nullptr, nullptr};
+  int vW = 0;
+  unsigned nvl = 0, nvr = 0;
   unsigned nb1 = 0, nb2 = 0, gen = 0;
   // SPH_INC_DBG: 8 phase timestamps of the divide kernels (printf); 16 / 32 force the
   // global-memory paths of the tile prefixes / far arrivals (tests)
   int dbg = 0;
 };
 constexpr unsigned INC_TILE_SIZE = 1024;  // particles per classify tile (sph_divide.hip INC_TILE)
+// Stable sort of <= SMALLSORT_MAX (key, index) pairs in one block (the migrants of a divide).
+constexpr unsigned SMALLSORT_MAX = 4096;
+void launch_small_sort(hipStream_t stm, const unsigned* kin, const unsigned* vin, unsigned n, unsigned* kout,
+                       unsigned* vout);
 unsigned inc_blocks_classify(unsigned cap);
 unsigned inc_blocks_boxes(unsigned nctt);
 void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& src, const PartArrays& dst,
@@ -199,17 +206,19 @@ void launch_interaction_bound(hipStream_t stm, unsigned npbcap, DevScalars* sc, 
 // Work counters of the persistent tiled kernels (qctr): 8 per-XCD item queues + the
 // finished-block count, each on its own 128-B line (device-scope atomics serialize per line).
 constexpr int QSTRIDE = 32;
-// Line 9 holds the list's item counts {all, bound} (k_items_scan; ItemGroups reads them), so
-// one counter block describes one item list.
+// Line 9 holds the list's item counts {all, bound, first item} (k_items_scan; ItemGroups
+// reads them), so one counter block describes one item list.
 constexpr size_t QCTR_QUEUE_BYTES = 9 * QSTRIDE * sizeof(unsigned);  // what a re-run zeroes
 constexpr size_t QCTR_BYTES = 10 * QSTRIDE * sizeof(unsigned);
 constexpr int QCTR_NITEMS = 9 * QSTRIDE;
 // Tiled fluid interaction (sph_interaction_tiled.hip) and its per-divide item list.
 // scelldiv 1 (CellMode=full): items of <= 4 cells; 2 (half): <= TMAXCELLS_HALF half-cells.
 // p1 in the local columns [xr[0], xr[1]), [xr[2], xr[3]), [xr[4], xr[5]), each range's items
-// on their own (nullptr: the owned columns).
+// on their own (nullptr: the owned columns).  With qctr2: two lists in `items`, the first of
+// range 0 (counter block qctr), the second of ranges 1 and 2 after it (qctr2).  rowtmp holds
+// 2 x 2 ncy ncz counts.
 void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
-                  uint4* items, unsigned* qctr, int scelldiv = 1, const int* xr = nullptr);
+                  uint4* items, unsigned* qctr, int scelldiv = 1, const int* xr = nullptr, unsigned* qctr2 = nullptr);
 // With floating bodies (ftmassp != nullptr) the staged p2 records carry their mass ratio
 // and kind (the FT instantiation; one more float2 of LDS per record).
 void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
@@ -283,6 +292,8 @@ enum DtMode { DT_VERLET = 0, DT_SYM_PRE = 1, DT_SYM_COR = 2, DT_PEEK = 3 };
 // (launch_fold_maxima + SlabTransport::allreduce_max_u32); nullptr = fold the slots here.
 void launch_dt(hipStream_t stm, DevScalars* sc, const KConst& K, double cfl, double dtmin, double cs0, int mode,
                double* dttrace, unsigned tracecap, const unsigned* folded = nullptr);
+// sc->visco = Visco at the current TimeStep (ViscoTime table, else the case's).
+void launch_visco_init(hipStream_t stm, DevScalars* sc, const KConst& K);
 // folded[5]: VelMax^2, AceMax^2, ViscDtMax, ViscEtaDtMax, this slab's fatal error flags
 void launch_fold_maxima(hipStream_t stm, DevScalars* sc, unsigned* folded, bool clear);
 // Update kernels skip slab ghosts (local column outside [g.xown0, g.xown1)) and mark
@@ -396,7 +407,7 @@ struct SlabCounts {
   unsigned long long recvl[2], recvr[2];  // records from the left / right neighbour
   unsigned np;                            // particles before the exchange (sc->np)
   unsigned nkeep;                         // particles staying owned (not migrating, not dropped)
-  unsigned pad[2];
+  unsigned ghosts[2];                     // ghosts counted per face box for the left / right neighbour
 };
 struct SlabSendBufs {
   SlabGhost* gl;
@@ -430,12 +441,11 @@ struct SlabFaces {
   unsigned nfb = 0;
   int W = 0;
 };
-// After the pack: prefixes of the send counts, the headers (ghost totals, the migrant
-// counts of `cnt`), cnt->sendl[0] / sendr[0] = the ghost totals.
-void launch_face_send_scan(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right);
-// After the message exchange: cnt->recvl / recvr from the received headers, prefixes of the
-// received counts.
-void launch_face_recv_scan(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right);
+// (The pack writes the send messages' counts and headers.)  After the message exchange:
+// cnt->recvl / recvr from the received headers; then the prefixes of all four messages'
+// counts (off the host wait's path).
+void launch_face_hdr(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right);
+void launch_face_scan(hipStream_t stm, const SlabFaces& f, bool has_left, bool has_right);
 // The divide's virtual keys of the ngl + ngr reserved ghost slots (left face first):
 // keys[e] = the receiver's box key, vals[e] = vbase + e.
 void launch_ghost_keys(hipStream_t stm, const SlabFaces& f, DivGrid g, unsigned ngl, unsigned ngr, unsigned* keys,

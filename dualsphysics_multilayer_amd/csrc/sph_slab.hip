@@ -65,16 +65,6 @@ __device__ __forceinline__ int face_idx(const DivGrid& g, int W, unsigned key, i
   return int(((type * unsigned(g.ncz) + r / unsigned(g.ncy)) * unsigned(g.ncy) + r % unsigned(g.ncy)) * unsigned(W) +
              unsigned(x));
 }
-// The face box holding entry j: the largest idx with pre[idx] <= j (pre[0] = 0 <= j < pre[nfb]).
-__device__ __forceinline__ unsigned face_of_entry(const unsigned* __restrict__ pre, unsigned nfb, unsigned j) {
-  unsigned lo = 0, hi = nfb - 1;
-  while (lo < hi) {
-    const unsigned mid = (lo + hi + 1) >> 1;
-    if (pre[mid] <= j) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
 
 // bit 0: record for the left neighbour, bit 1: record for the right, bit 2: stays owned
 // (so a record with bit 2 is a ghost copy, without it a migrant).
@@ -100,12 +90,13 @@ __device__ __forceinline__ void streams(unsigned c, bool f[4]) {
 }
 
 __global__ __launch_bounds__(PK_BS) void k_pack_count(const DevScalars* __restrict__ sc, PackArgs q) {
-  __shared__ unsigned s[5][PK_BS / 64];
+  __shared__ unsigned s[7][PK_BS / 64];
   const unsigned n = sc->np;
   const unsigned base = blockIdx.x * PK_TILE;
-  unsigned c4[5] = {0, 0, 0, 0, 0};
+  unsigned c4[7] = {0, 0, 0, 0, 0, 0, 0};  // 4 streams, staying, ghosts per face (face boxes)
   for (int it = 0; it < PK_ITEMS; it++) {
     const unsigned p = base + it * PK_BS + threadIdx.x;
+    int fi[2] = {-1, -1};  // face box of an owned face particle, per face
     if (p < n) {
       const unsigned c = pack_class(q, p);
       bool f[4];
@@ -113,32 +104,43 @@ __global__ __launch_bounds__(PK_BS) void k_pack_count(const DevScalars* __restri
 #pragma unroll
       for (int k = 0; k < 4; k++) c4[k] += f[k] ? 1u : 0u;
       c4[4] += (c >> 2) & 1u;
-      if (q.fcnt[0] && (c & 4u) && (c & 3u)) {  // an owned face particle: count it per face box
+      if (q.fcnt[0] && (c & 4u) && (c & 3u)) {
         const unsigned key = box_key(q.a.dcell[p], q.a.code[p], q.g, q.dcc);
-        if (c & 1u) {
-          const int fi = face_idx(q.g, q.W, key, q.g.xown0);
-          if (fi >= 0) atomicAdd(&q.fcnt[0][fi], 1u);
-        }
-        if (c & 2u) {
-          const int fi = face_idx(q.g, q.W, key, q.g.xown1 - q.W);
-          if (fi >= 0) atomicAdd(&q.fcnt[1][fi], 1u);
+        if (c & 1u) fi[0] = face_idx(q.g, q.W, key, q.g.xown0);
+        if (c & 2u) fi[1] = face_idx(q.g, q.W, key, q.g.xown1 - q.W);
+      }
+    }
+    if (q.fcnt[0]) {
+      // count per face box with one atomic per distinct box of the wave (the particles are
+      // in the previous divide's cell order: a wave spans a few boxes)
+#pragma unroll
+      for (int side = 0; side < 2; side++) {
+        c4[5 + side] += fi[side] >= 0 ? 1u : 0u;
+        unsigned long long act = __ballot(fi[side] >= 0);
+        while (act) {
+          const int lead = __ffsll(static_cast<long long>(act)) - 1;
+          const int b = __shfl(fi[side], lead, 64);
+          const unsigned long long same = __ballot(fi[side] == b);
+          if (int(threadIdx.x & 63) == lead) atomicAdd(&q.fcnt[side][b], unsigned(__popcll(same)));
+          act &= ~same;
         }
       }
     }
   }
 #pragma unroll
-  for (int k = 0; k < 5; k++)
+  for (int k = 0; k < 7; k++)
     for (int off = 32; off > 0; off >>= 1) c4[k] += __shfl_xor(c4[k], off, 64);
   const unsigned w = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0)
-    for (int k = 0; k < 5; k++) s[k][w] = c4[k];
+    for (int k = 0; k < 7; k++) s[k][w] = c4[k];
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int k = 0; k < 5; k++) {
+    for (int k = 0; k < 7; k++) {
       unsigned t = 0;
       for (int i = 0; i < PK_BS / 64; i++) t += s[k][i];
       if (k < 4) q.tilecnt[k * q.ntiles + blockIdx.x] = t;
-      else if (t) atomicAdd(&q.cnt->nkeep, t);
+      else if (k == 4 && t) atomicAdd(&q.cnt->nkeep, t);
+      else if (k > 4 && t) atomicAdd(&q.cnt->ghosts[k - 5], t);  // the face messages' ghost totals
     }
   }
 }
@@ -171,11 +173,18 @@ __global__ __launch_bounds__(1024) void k_pack_scan(const DevScalars* __restrict
     }
   }
   if (threadIdx.x == 1023) {
-    q.cnt->sendl[0] = part[0][1023];
-    q.cnt->sendr[0] = part[1][1023];
+    // ghosts: the face-box totals of k_pack_count (exchange after the divide), else records
+    q.cnt->sendl[0] = q.fcnt[0] ? q.cnt->ghosts[0] : part[0][1023];
+    q.cnt->sendr[0] = q.fcnt[0] ? q.cnt->ghosts[1] : part[1][1023];
     q.cnt->sendl[1] = part[2][1023];
     q.cnt->sendr[1] = part[3][1023];
     q.cnt->np = sc->np;
+    if (q.fcnt[0])  // the face messages' headers {ghosts, migrants}
+      for (int side = 0; side < 2; side++) {
+        unsigned long long* h = reinterpret_cast<unsigned long long*>(q.fcnt[side] - FMSG_HDR);
+        h[0] = side ? q.cnt->sendr[0] : q.cnt->sendl[0];
+        h[1] = side ? q.cnt->sendr[1] : q.cnt->sendl[1];
+      }
   }
 }
 
@@ -278,6 +287,7 @@ void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartA
     q.fcnt[1] = faces->msg[1] + FMSG_HDR;
     (void)hipMemsetAsync(q.fcnt[0], 0, 4 * size_t(faces->nfb), stm);
     (void)hipMemsetAsync(q.fcnt[1], 0, 4 * size_t(faces->nfb), stm);
+    (void)hipMemsetAsync(cnt->ghosts, 0, sizeof(cnt->ghosts), stm);
   }
   q.a = a;
   q.g = g;
@@ -302,121 +312,141 @@ void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartA
 }
 
 // ---------------------------------------------------------------------------------
-// Face messages.  One block per face: exclusive scan of the nfb counts (a thread's chunk,
-// then a block scan of the chunk sums).
-__device__ void face_scan_block(const unsigned* __restrict__ cnt, unsigned* __restrict__ pre, unsigned n) {
-  __shared__ unsigned part[1024];
-  const unsigned per = (n + 1023) / 1024;
-  const unsigned b0 = min(threadIdx.x * per, n), b1 = min(b0 + per, n);
-  unsigned s = 0;
-  for (unsigned i = b0; i < b1; i++) s += cnt[i];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const unsigned v = threadIdx.x >= unsigned(off) ? part[threadIdx.x - off] : 0u;
+// Face messages.  After the exchange the received headers go to cnt->recvl / recvr (for the
+// host's one read of the counts); then one block per face message scans its nfb counts in
+// tiles of 8192 (coalesced loads into LDS, 8 consecutive per thread, wave + block scans).
+__global__ void k_face_hdr(SlabFaces f, SlabCounts* __restrict__ cnt, int hl, int hr) {
+  const int side = int(threadIdx.x);
+  if (side > 1 || (side == 0 ? !hl : !hr)) return;
+  const unsigned long long* h = reinterpret_cast<const unsigned long long*>(f.msg[2 + side]);
+  unsigned long long* rv = side == 0 ? cnt->recvl : cnt->recvr;
+  rv[0] = h[0];
+  rv[1] = h[1];
+}
+
+constexpr int FS_BS = 1024, FS_PT = 8, FS_TILE = FS_BS * FS_PT;
+__global__ __launch_bounds__(FS_BS) void k_face_scan(SlabFaces f, int hl, int hr) {
+  __shared__ unsigned v[FS_TILE];
+  __shared__ unsigned wsum[FS_BS / 64];
+  __shared__ unsigned carry;
+  const int m = int(blockIdx.x);  // send L, send R, receive L, receive R
+  if ((m & 1) ? !hr : !hl) return;
+  const unsigned* cnt = f.msg[m] + FMSG_HDR;
+  unsigned* pre = f.pre[m];
+  const unsigned n = f.nfb, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  for (unsigned t0 = 0; t0 < n; t0 += FS_TILE) {
+#pragma unroll
+    for (int k = 0; k < FS_PT; k++) {
+      const unsigned i = t0 + k * FS_BS + threadIdx.x;
+      v[k * FS_BS + threadIdx.x] = i < n ? cnt[i] : 0u;
+    }
     __syncthreads();
-    part[threadIdx.x] += v;
+    unsigned x[FS_PT], sum = 0;
+#pragma unroll
+    for (int k = 0; k < FS_PT; k++) {
+      x[k] = sum;
+      sum += v[threadIdx.x * FS_PT + k];
+    }
+    unsigned inc = sum;  // inclusive wave scan of the thread sums
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned y = __shfl_up(inc, off, 64);
+      if (lane >= unsigned(off)) inc += y;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    unsigned before = carry;
+    for (unsigned q = 0; q < w; q++) before += wsum[q];
+    before += inc - sum;
+#pragma unroll
+    for (int k = 0; k < FS_PT; k++) v[threadIdx.x * FS_PT + k] = before + x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FS_PT; k++) {
+      const unsigned i = t0 + k * FS_BS + threadIdx.x;
+      if (i < n) pre[i] = v[k * FS_BS + threadIdx.x];
+    }
+    if (threadIdx.x == FS_BS - 1) carry = before + sum;
     __syncthreads();
   }
-  unsigned run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
-  for (unsigned i = b0; i < b1; i++) {
-    pre[i] = run;
-    run += cnt[i];
-  }
-  if (threadIdx.x == 1023) pre[n] = part[1023];
+  if (threadIdx.x == 0) pre[n] = carry;
 }
 
-__global__ __launch_bounds__(1024) void k_face_send_scan(SlabFaces f, SlabCounts* __restrict__ cnt, int hl, int hr) {
-  const int side = int(blockIdx.x);  // 0 left, 1 right
-  if (side == 0 ? !hl : !hr) return;
-  face_scan_block(f.msg[side] + FMSG_HDR, f.pre[side], f.nfb);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned long long ng = f.pre[side][f.nfb];
-    unsigned long long* h = reinterpret_cast<unsigned long long*>(f.msg[side]);
-    unsigned long long* sd = side == 0 ? cnt->sendl : cnt->sendr;
-    sd[0] = ng;
-    h[0] = ng;
-    h[1] = sd[1];
-  }
+void launch_face_hdr(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right) {
+  hipLaunchKernelGGL(k_face_hdr, dim3(1), dim3(64), 0, stm, f, cnt, int(has_left), int(has_right));
+}
+void launch_face_scan(hipStream_t stm, const SlabFaces& f, bool has_left, bool has_right) {
+  hipLaunchKernelGGL(k_face_scan, dim3(4), dim3(FS_BS), 0, stm, f, int(has_left), int(has_right));
 }
 
-__global__ __launch_bounds__(1024) void k_face_recv_scan(SlabFaces f, SlabCounts* __restrict__ cnt, int hl, int hr) {
-  const int side = int(blockIdx.x);
-  if (side == 0 ? !hl : !hr) return;
-  face_scan_block(f.msg[2 + side] + FMSG_HDR, f.pre[2 + side], f.nfb);
-  if (threadIdx.x == 0) {
-    const unsigned long long* h = reinterpret_cast<const unsigned long long*>(f.msg[2 + side]);
-    unsigned long long* rv = side == 0 ? cnt->recvl : cnt->recvr;
-    rv[0] = h[0];
-    rv[1] = h[1];
-  }
-}
-
-void launch_face_send_scan(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right) {
-  hipLaunchKernelGGL(k_face_send_scan, dim3(2), dim3(1024), 0, stm, f, cnt, int(has_left), int(has_right));
-}
-void launch_face_recv_scan(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right) {
-  hipLaunchKernelGGL(k_face_recv_scan, dim3(2), dim3(1024), 0, stm, f, cnt, int(has_left), int(has_right));
-}
-
-// Reserved ghost slots of the divide: entry e of the left face's ngl then the right face's ngr.
-__global__ __launch_bounds__(256) void k_ghost_keys(SlabFaces f, DivGrid g, unsigned ngl, unsigned ngr,
-                                                    unsigned* __restrict__ keys, unsigned* __restrict__ vals,
-                                                    unsigned vbase) {
-  const unsigned e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= ngl + ngr) return;
-  const int side = e < ngl ? 0 : 1;
-  const unsigned j = side ? e - ngl : e;
-  const unsigned idx = face_of_entry(f.pre[2 + side], f.nfb, j);
+// Reserved ghost slots of the divide: one thread per face box (left face first) writes the
+// box key of its count[idx] entries at pre[idx] (left: entries [0, ngl), right: after them).
+__global__ __launch_bounds__(256) void k_ghost_keys(SlabFaces f, DivGrid g, unsigned ngl, unsigned* __restrict__ keys,
+                                                    unsigned* __restrict__ vals, unsigned vbase, int hl, int hr) {
+  const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int side = t < f.nfb ? 0 : 1;
+  const unsigned idx = side ? t - f.nfb : t;
+  if (idx >= f.nfb || (side ? !hr : !hl)) return;
+  const unsigned n = f.msg[2 + side][FMSG_HDR + idx];
+  if (!n) return;
+  const unsigned e0 = (side ? ngl : 0u) + f.pre[2 + side][idx];
   // the left ghost columns are [0, W), the right ones [xown1, xown1 + W)
-  keys[e] = face_key(g, f.W, idx, side ? g.xown1 : 0);
-  vals[e] = vbase + e;
+  const unsigned key = face_key(g, f.W, idx, side ? g.xown1 : 0);
+  for (unsigned j = 0; j < n; j++) {
+    keys[e0 + j] = key;
+    if (vals) vals[e0 + j] = vbase + e0 + j;
+  }
 }
 
 void launch_ghost_keys(hipStream_t stm, const SlabFaces& f, DivGrid g, unsigned ngl, unsigned ngr, unsigned* keys,
                        unsigned* vals, unsigned vbase) {
   if (ngl + ngr)
-    hipLaunchKernelGGL(k_ghost_keys, dim3((ngl + ngr + 255) / 256), dim3(256), 0, stm, f, g, ngl, ngr, keys, vals, vbase);
+    hipLaunchKernelGGL(k_ghost_keys, dim3((2 * f.nfb + 255) / 256), dim3(256), 0, stm, f, g, ngl, keys, vals, vbase,
+                       int(ngl > 0), int(ngr > 0));
 }
 
-// Ghost records from the sorted arrays: record j of a face = particle begincell[key] + (j -
-// pre[idx]) of its face box (the box's old members come first, in previous-index order —
-// the order the pre-divide pack wrote them in).  Reads are contiguous per box.
+// Ghost records from the sorted arrays, one thread per face box: its count[idx] first members
+// (the old members come first, in previous-index order — the order the pre-divide pack
+// counted them in) to records pre[idx].. of the face's message.  Reads are contiguous per box.
 __global__ __launch_bounds__(256) void k_ghost_pack(DevScalars* __restrict__ sc, SlabFaces f, DivGrid g,
                                                     const unsigned* __restrict__ bc, PartArrays a,
-                                                    const float4* __restrict__ poscell, SlabSendBufs b, unsigned ngl,
-                                                    unsigned ngr) {
-  const unsigned e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= ngl + ngr) return;
-  const int side = e < ngl ? 0 : 1;
-  const unsigned j = side ? e - ngl : e;
-  const unsigned* pre = f.pre[side];
-  const unsigned idx = face_of_entry(pre, f.nfb, j);
+                                                    const float4* __restrict__ poscell, SlabSendBufs b, int hl,
+                                                    int hr) {
+  const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int side = t < f.nfb ? 0 : 1;
+  const unsigned idx = side ? t - f.nfb : t;
+  if (idx >= f.nfb || (side ? !hr : !hl)) return;
+  const unsigned n = f.msg[side][FMSG_HDR + idx];
+  if (!n) return;
   const unsigned key = face_key(g, f.W, idx, side ? g.xown1 - f.W : g.xown0);
-  const unsigned i = bc[key] + (j - pre[idx]);
-  if (i >= bc[key + 1]) {  // the divide placed fewer particles in the box than were counted
+  const unsigned i0 = bc[key];
+  if (i0 + n > bc[key + 1]) {  // the divide placed fewer particles in the box than were counted
     atomicOr(&sc->error_flags, ERR_HALO);
     return;
   }
-  const float4 pc = poscell[i];
-  SlabGhost r;
-  r.rx = pc.x;
-  r.ry = pc.y;
-  r.rz = pc.z;
-  r.dcell = a.dcell[i];
-  r.velrhop = a.velrhop[i];
-  r.idp = a.idp[i];
-  r.code = a.code[i];
-  r.pad = 0;
-  (side ? b.gr : b.gl)[j] = r;
+  SlabGhost* out = (side ? b.gr : b.gl) + f.pre[side][idx];
+  for (unsigned j = 0; j < n; j++) {
+    const unsigned i = i0 + j;
+    const float4 pc = poscell[i];
+    SlabGhost r;
+    r.rx = pc.x;
+    r.ry = pc.y;
+    r.rz = pc.z;
+    r.dcell = a.dcell[i];
+    r.velrhop = a.velrhop[i];
+    r.idp = a.idp[i];
+    r.code = a.code[i];
+    r.pad = 0;
+    out[j] = r;
+  }
 }
 
 void launch_ghost_pack(hipStream_t stm, DevScalars* sc, const SlabFaces& f, DivGrid g, const unsigned* begincell,
                        const PartArrays& a, const float4* poscell, SlabSendBufs b, unsigned ngl, unsigned ngr) {
   if (ngl + ngr)
-    hipLaunchKernelGGL(k_ghost_pack, dim3((ngl + ngr + 255) / 256), dim3(256), 0, stm, sc, f, g, begincell, a, poscell,
-                       b, ngl, ngr);
+    hipLaunchKernelGGL(k_ghost_pack, dim3((2 * f.nfb + 255) / 256), dim3(256), 0, stm, sc, f, g, begincell, a,
+                       poscell, b, int(ngl > 0), int(ngr > 0));
 }
 
 // ---------------------------------------------------------------------------------

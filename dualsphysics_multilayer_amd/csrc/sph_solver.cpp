@@ -182,6 +182,9 @@ void derive_constants(const SphCaseDef& c, SphConstants& k) {
   // are read, and ConfigConstants2 keeps a non-zero DtMin)
   const float coefdtmin = float(c.coefdtmin) * 1.0e-5f;  // CoefDtMin*=1.0e-5f
   k.dtmin = (double(k.kernelh) / k.cs0) * double(coefdtmin);
+  k.dtallparticles = c.dtallparticles ? 1 : 0;  // JSph.cpp:697
+  if (!(c.dtfixed >= 0)) throw SphError(SPH_ERR_ARG, "DtFixed must not be negative");
+  k.dtfixed = c.dtfixed;  // max(0, DtFixed), JSph.cpp:699
 }
 
 static KConst make_kconst(const SphConstants& c) {
@@ -252,6 +255,9 @@ static KConst make_kconst(const SphConstants& c) {
   K.shiftcoef = c.shift_coef;
   K.shiftmaxdist = float(c.dp * 0.1);
   K.coeftfs = (c.data2d ? 2.0 : 3.0) - double(c.shift_tfs);
+  K.dtallp = c.dtallparticles;
+  K.dtfix_val = c.dtfixed;
+  K.viscobf = c.viscoboundfactor;
   {  // binomial coefficients of (1+x)^(1/gamma) - 1
     const double a = 1.0 / double(c.gamma);
     K.ddtc1 = float(a);
@@ -545,7 +551,7 @@ void SphGpuSingle::AllocFixed() {
   if (slab()) {  // re-partition: column counts [2 ncx] + the ranks' bounds [nranks + 1]
     colcnt_ = (float*)dmalloc(4 * (2 * size_t(C.dom_cells[0]) + size_t(slabcfg_.nranks) + 1));
   }
-  rowtmp_ = (unsigned*)dmalloc(4 * 2 * size_t(G.ncy) * size_t(G.ncz));
+  rowtmp_ = (unsigned*)dmalloc(4 * 4 * size_t(G.ncy) * size_t(G.ncz));  // two lists x (fluid, bound) rows
   qctr_ = (unsigned*)dmalloc(QCTR_BYTES);
   check_hip(hipMemset(qctr_, 0, QCTR_BYTES), "zero work counters");
   sort_.digtot = (unsigned*)dmalloc(4 * (1u << RS_MAXBITS));
@@ -572,7 +578,6 @@ void SphGpuSingle::AllocFixed() {
       faces_.msg[k] = (unsigned*)dmalloc(4 * (size_t(FMSG_HDR) + faces_.nfb));
       faces_.pre[k] = (unsigned*)dmalloc(4 * (size_t(faces_.nfb) + 1));
     }
-    rowtmpf_ = (unsigned*)dmalloc(4 * 2 * size_t(G.ncy) * size_t(G.ncz));
     qctrf_ = (unsigned*)dmalloc(QCTR_BYTES);
     check_hip(hipMemset(qctrf_, 0, QCTR_BYTES), "zero work counters");
   }
@@ -638,7 +643,8 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
   press_ = (float*)dmalloc(4 * n);
   // Interaction items (launch_items): an item holds TB particles unless it ends a row
   // (<= 2 per row: fluid and bound) or reaches TMAXCELLS = 4 cells (<= 1 per 4 cells).
-  items_ = (uint4*)dmalloc(16 * (n / 128 + 2 * size_t(G.ncy) * size_t(G.ncz) + size_t(nctmax_) / 2 + 2));
+  // (slabs: up to three column ranges per row)
+  items_ = (uint4*)dmalloc(16 * (n / 128 + 6 * size_t(G.ncy) * size_t(G.ncz) + size_t(nctmax_) / 2 + 2));
   arace_ = (float4*)dmalloc(16 * n);
   if (shift_) shiftpos_ = (float4*)dmalloc(16 * n);  // the interaction's shifting sums
   if (sps_) taunew_ = (float4*)dmalloc(32 * n);
@@ -671,7 +677,6 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
   if (slab()) {
     // new positions of the appended particles and reserved ghost slots (either divide)
     inc_.apppos = (unsigned*)dmalloc(4 * n);
-    itemsf_ = (uint4*)dmalloc(16 * (n / 128 + 2 * size_t(G.ncy) * size_t(G.ncz) + size_t(nctmax_) / 2 + 2));
   }
   sort_.ntiles = unsigned((n + RS_TILE - 1) / RS_TILE);
   sort_.hist = (unsigned*)dmalloc(4 * size_t(sort_.ntiles) * (1u << RS_MAXBITS));
@@ -867,6 +872,10 @@ void SphGpuSingle::SetTime(double time, double symdtpre) {
   check_hip(hipMemcpy(&sc_->time, &time, sizeof(double), hipMemcpyHostToDevice), "set time");
   if (symdtpre > 0)
     check_hip(hipMemcpy(&sc_->symdtpre, &symdtpre, sizeof(double), hipMemcpyHostToDevice), "set SymplecticDtPre");
+  if (K.visco_n) {  // ViscoTime at the restart time
+    launch_visco_init(stream, sc_, K);
+    Sync();
+  }
 }
 
 // ---- timing -----------------------------------------------------------------------
@@ -927,14 +936,13 @@ void SphGpuSingle::Exchange() {
   auto pack = [&] {
     launch_slab_pack(stream, cap_, sc_, cur_, G, K, C.dom_posmin, hl, hr, withm1, withpre, packtiles_, slabcnt_,
                      send_, normal_, casenpb_, &faces_);
-    launch_face_send_scan(stream, faces_, slabcnt_, hl, hr);
   };
   check_hip(hipMemsetAsync(slabcnt_, 0, sizeof(SlabCounts), stream), "exchange: reset counts");
   pack();
   const size_t mb = 4 * (size_t(FMSG_HDR) + faces_.nfb);
   transport_->exchange(faces_.msg[0], hl ? mb : 0, faces_.msg[1], hr ? mb : 0, faces_.msg[2], hl ? mb : 0,
                        faces_.msg[3], hr ? mb : 0, stream);
-  launch_face_recv_scan(stream, faces_, slabcnt_, hl, hr);
+  launch_face_hdr(stream, faces_, slabcnt_, hl, hr);
   check_hip(hipMemcpyAsync(slabcnt_host_, slabcnt_, sizeof(SlabCounts), hipMemcpyDeviceToHost, stream),
             "exchange: read counts");
   // The transfer sizes must be on the host before the transfers are posted: the one host
@@ -992,6 +1000,7 @@ void SphGpuSingle::Exchange() {
     if (want >= (1ull << 31)) throw SphError(SPH_ERR_NOMEM, "slab particle capacity overflow");
     Grow(c.np, unsigned(want));
   }
+  launch_face_scan(stream, faces_, hl, hr);  // slots of the received ghosts, records of the sent ones
   // the migrants of both faces (two concurrent streams over the two xGMI links)
   transport_->exchange(send_.ml, sizeof(SlabRec) * c.sendl[1], send_.mr, sizeof(SlabRec) * c.sendr[1], recvm_,
                        sizeof(SlabRec) * rml, recvm_ + rml, sizeof(SlabRec) * rmr, stream);
@@ -1160,7 +1169,7 @@ void SphGpuSingle::RunCellDivide() {
   }
   inc_valid_ = inc_ok_;
   inc_.napp = 0;
-  inc_.nappv = 0;
+  inc_.nvl = inc_.nvr = 0;
   std::swap(cur_, alt_);
   // this slab's ghost records for the neighbours, from its sorted face columns
   if (ghosts) launch_ghost_pack(stream, sc_, faces_, G, begincell_, cur_, poscell_, send_, unsigned(xg_sl_), unsigned(xg_sr_));
@@ -1174,10 +1183,9 @@ void SphGpuSingle::RunCellDivide() {
     const int S = int(C.scelldiv), hl = slab() && transport_->has_left(), hr = slab() && transport_->has_right();
     int ib = G.xown0 + (hl ? S : 0), ie = G.xown1 - (hr ? S : 0);
     if (ib >= ie) ib = ie = G.xown0;  // a narrow slab: every item reaches a ghost column
-    if (overlap) {
-      const int xi[6] = {ib, ie, 0, 0, 0, 0}, xf[6] = {G.xown0, ib, ie, G.xown1, 0, 0};
-      launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv, xi);
-      launch_items(stream, sc_, begincell_, G, rowtmpf_, itemsf_, qctrf_, C.scelldiv, xf);
+    if (overlap) {  // the interior list (qctr_), then the face list (qctrf_) after it
+      const int xr[6] = {ib, ie, G.xown0, ib, ie, G.xown1};
+      launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv, xr, qctrf_);
       ghost_split_ = true;
     } else {
       const int xa[6] = {G.xown0, ib, ib, ie, ie, G.xown1};
@@ -1259,7 +1267,7 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
       if (!ev_ghost_) check_hip(hipEventCreateWithFlags(&ev_ghost_, hipEventDisableTiming), "hipEventCreate");
       check_hip(hipStreamWaitEvent(xstream_, ev_div_, 0), "ghosts: wait divide");
       GhostTransfer(xstream_);
-      launch_fluid_tiled(xstream_, nblocks_tiled_, sc_, itemsf_, qctrf_, poscell_, cur_.velrhop, press_, begincell_, G,
+      launch_fluid_tiled(xstream_, nblocks_tiled_, sc_, items_, qctrf_, poscell_, cur_.velrhop, press_, begincell_, G,
                          K, arace_, cur_.code, ftmassp_);
       check_hip(hipEventRecord(ev_ghost_, xstream_), "ghosts: event");
       check_hip(hipStreamWaitEvent(stream, ev_ghost_, 0), "ghosts: join");
@@ -1268,7 +1276,7 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
       launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, begincell_, G, K,
                          arace_, cur_.code, ftmassp_);
       if (ghost_split_)  // the ghosts are in: the face items right after
-        launch_fluid_tiled(stream, nblocks_tiled_, sc_, itemsf_, qctrf_, poscell_, cur_.velrhop, press_, begincell_,
+        launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qctrf_, poscell_, cur_.velrhop, press_, begincell_,
                            G, K, arace_, cur_.code, ftmassp_);
     }
   } else {
@@ -1542,6 +1550,56 @@ void SphGpuSingle::SetFloatingTable(unsigned body, int kind, unsigned n, const d
   allocs_.push_back(fttabdesc_);
   check_hip(hipMemcpy(fttab_, all.data(), sizeof(double4) * all.size(), hipMemcpyHostToDevice), "upload tables");
   check_hip(hipMemcpy(fttabdesc_, desc.data(), sizeof(int2) * desc.size(), hipMemcpyHostToDevice), "upload tables");
+}
+
+// DtFixedFile (JDsFixedDt) and ViscoTime (JDsViscoInput) tables on the device; k_dt reads
+// them at every DtVariable (fixed dt) and at every step's end (the next step's Visco).
+void SphGpuSingle::SetTimeTable(int kind, unsigned n, const double* times, const double* values) {
+  if (kind != SPH_TTAB_DTFIXED && kind != SPH_TTAB_VISCO) throw SphError(SPH_ERR_ARG, "invalid time table kind");
+  if (n == 1 || (n && (!times || !values))) throw SphError(SPH_ERR_ARG, "Cannot be less than two values.");
+  for (unsigned i = 1; i < n; i++)
+    if (!(times[i] >= times[i - 1])) throw SphError(SPH_ERR_ARG, "time table times must be nondecreasing");
+  if (kind == SPH_TTAB_DTFIXED && n && C.dtfixed > 0)
+    throw SphError(SPH_ERR_ARG, "The parameters 'DtFixed' and 'DtFixedFile' cannot be used at the same time.");
+  if (kind == SPH_TTAB_VISCO && n && nn_)
+    throw SphError(SPH_ERR_UNSUPPORTED, "ViscoTime with NN multiphase (per-phase viscosities) is not implemented");
+  Sync();
+  void*& buf = (kind == SPH_TTAB_DTFIXED ? dttab_ : viscotab_);
+  if (buf) {
+    (void)hipFree(buf);
+    allocs_.erase(std::remove(allocs_.begin(), allocs_.end(), buf), allocs_.end());
+    buf = nullptr;
+  }
+  if (kind == SPH_TTAB_DTFIXED) {
+    K.dtfix_n = int(n);
+    K.dtfix_t = K.dtfix_v = nullptr;
+    if (n) {
+      std::vector<double> h(times, times + n);
+      h.insert(h.end(), values, values + n);
+      check_hip(hipMalloc(&buf, sizeof(double) * h.size()), "hipMalloc dt table");
+      allocs_.push_back(buf);
+      check_hip(hipMemcpy(buf, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice), "upload dt table");
+      K.dtfix_t = (const double*)buf;
+      K.dtfix_v = K.dtfix_t + n;
+    }
+  } else {
+    K.visco_n = int(n);
+    K.visco_t = K.visco_v = nullptr;
+    if (n) {  // JDsViscoInput reads float rows (ReadNextFloat)
+      std::vector<float> h(2 * size_t(n));
+      for (unsigned i = 0; i < n; i++) {
+        h[i] = float(times[i]);
+        h[n + i] = float(values[i]);
+      }
+      check_hip(hipMalloc(&buf, sizeof(float) * h.size()), "hipMalloc visco table");
+      allocs_.push_back(buf);
+      check_hip(hipMemcpy(buf, h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice), "upload visco table");
+      K.visco_t = (const float*)buf;
+      K.visco_v = K.visco_t + n;
+    }
+    launch_visco_init(stream, sc_, K);
+    Sync();
+  }
 }
 
 unsigned SphGpuSingle::Floatings(SphFloatingState* out, unsigned cap) {

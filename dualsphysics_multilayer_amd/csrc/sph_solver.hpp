@@ -91,6 +91,8 @@ class SphGpuSingle {
   void SetFloatings(unsigned nft, const SphFloatingDef* defs, double ftpause);
   // Imposed velocity / external force table of one body (SPH_FTTAB_*), before the first step.
   void SetFloatingTable(unsigned body, int kind, unsigned n, const double* times, const double* values);
+  // DtFixedFile / ViscoTime tables (SPH_TTAB_*); n = 0 removes one.
+  void SetTimeTable(int kind, unsigned n, const double* times, const double* values);
   // Slabs: re-balance the column bounds every `every` steps (0: never) when the most loaded
   // slab exceeds the mean by more than `tolerance`; collective (all ranks the same values).
   void SetRepartition(unsigned every, double bound_weight, double tolerance);
@@ -173,12 +175,10 @@ class SphGpuSingle {
   uint4* items_ = nullptr;        // tiled-interaction work items (per divide)
   unsigned* rowtmp_ = nullptr;    // per-row item counts/offsets
   unsigned* qctr_ = nullptr;      // per-XCD-group work counters + the list's item counts
-  // slabs: the items of the p1 whose neighbour columns include a ghost column (the ghost
-  // exchange after the divide runs beside the interaction of the others)
-  uint4* itemsf_ = nullptr;
-  unsigned* rowtmpf_ = nullptr;
+  // slabs: the list of the items whose p1 reach a ghost column (after the interior list in
+  // items_; the ghost exchange after the divide runs beside the interaction of the others)
   unsigned* qctrf_ = nullptr;
-  bool ghost_split_ = false;      // the last item build split the list (items_ | itemsf_)
+  bool ghost_split_ = false;      // the last item build made two lists
   unsigned nblocks_tiled_ = 2048;
   bool qfresh_ = false;  // the tiled kernels' work queues were zeroed by the last item build
   bool tiled_ = true;             // SPH_INTERACTION=simple selects the one-lane-per-particle kernel
@@ -206,6 +206,8 @@ class SphGpuSingle {
   int2* fttabdesc_ = nullptr;    // [body][SPH_FTTAB_*] = {first row, rows}
   std::vector<std::vector<double4>> fttabs_;  // host copy, [body * 4 + kind]
   int nftbodies_ = 0;
+  void* dttab_ = nullptr;        // DtFixedFile rows: times [n], dt in ms [n] (double)
+  void* viscotab_ = nullptr;     // ViscoTime rows: times [n], Visco [n] (float)
   unsigned nftp_ = 0;            // floating particles of the case (CaseNfloat)
   unsigned casenpb_ = 0;         // CaseNpb: first floating idp
   bool stepped_ = false;         // a step was issued (bodies are configured before it)

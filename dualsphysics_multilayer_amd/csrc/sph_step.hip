@@ -75,6 +75,9 @@ __global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double d
   // solver forms them (JSphCpu.cpp:1687 of src_mphase/DSPH_v5.0_NNewtonian)
   const double dt3 = (K.nn ? double(K.kernelh * K.kernelh) / double(visceta * K.lamda) : DBL_MAX);
   double dt = cfl * fmin(dt3, fmin(dt1, dt2));
+  // DtFixed / DtFixedFile at the step's TimeStep (the corrector's DtVariable sees the same
+  // TimeStep as the predictor's: the time advanced in between)
+  if (K.dtfix_n || K.dtfix_val > 0) dt = fixed_dt(K, mode == DT_SYM_COR ? sc->tstep0 : sc->time);
   // a NaN maximum (a NaN velocity, acceleration or viscosity anywhere) also stops the run:
   // fmin/fmax above would drop it, and the state it came from is already lost
   if (isnan(dt) || isinf(dt) || isnan(velmax) || isnan(acemax) || isnan(viscdt) || isnan(visceta)) {
@@ -104,6 +107,18 @@ __global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double d
     sc->last_dt = stepdt;
     sc->nstep++;
   }
+  // ViscoTime: Visco of the next step, at its TimeStep (JSphCpuSingle.cpp:1092), once the
+  // step in flight is done (the Symplectic corrector keeps the predictor's Visco)
+  if (K.visco_n && mode != DT_SYM_PRE) sc->visco = visco_at(K, float(sc->time));
+}
+
+// Visco at the current TimeStep (a new ViscoTime table, a restart time).
+__global__ void k_visco_init(DevScalars* __restrict__ sc, KConst K) {
+  if (threadIdx.x == 0) sc->visco = K.visco_n ? visco_at(K, float(sc->time)) : K.visco;
+}
+
+void launch_visco_init(hipStream_t stm, DevScalars* sc, const KConst& K) {
+  hipLaunchKernelGGL(k_visco_init, dim3(1), dim3(64), 0, stm, sc, K);
 }
 
 void launch_dt(hipStream_t stm, DevScalars* sc, const KConst& K, double cfl, double dtmin, double cs0, int mode,

@@ -179,17 +179,18 @@ struct ItemGroup {
   __device__ __forceinline__ unsigned item(unsigned c) const { return c < nfg ? f.item(g, c) : b.item(g, c - nfg); }
 };
 struct ItemGroups {
-  unsigned nf, nb;
-  // the list's counts {all, bound}, written by k_items_scan beside the work queues
+  unsigned nf, nb, lo;
+  // the list's counts {all, bound, first item}, written by k_items_scan beside the work queues
   __device__ __forceinline__ explicit ItemGroups(const unsigned* qctr) {
     const unsigned n = qctr[QCTR_NITEMS];
     nb = min(qctr[QCTR_NITEMS + 1], n);
     nf = n - nb;
+    lo = qctr[QCTR_NITEMS + 2];
   }
   __device__ __forceinline__ ItemGroup group(unsigned g) const {
     ItemGroup r;
-    r.f = {0u, nf};
-    r.b = {nf, nb};
+    r.f = {lo, nf};
+    r.b = {lo + nf, nb};
     r.g = g;
     r.nfg = r.f.count(g);
     r.n = r.nfg + r.b.count(g);

@@ -41,6 +41,35 @@ DBL_MAX = float(np.finfo(np.float64).max)
 CODE_TYPE_MOVING, CODE_TYPE_FLOATING = 0x800, 0x1000  # 16-bit typecode, DualSphDef.h:200-205
 
 
+def _read_datafile(path: str, what: str) -> np.ndarray:
+    """Rows of (time, value) of a JReadDatafile table (JDsFixedDt / JDsViscoInput::LoadFile):
+    '#' lines are remarks, the separator is the most frequent of tab/space, ';' and ',',
+    values are read as atof reads them; at least two rows."""
+    if not os.path.isfile(path):
+        raise CaseError(f"{what}: file not found {path}")
+    lines = [ln.strip() for ln in open(path).read().replace("\r", "").split("\n")]
+    lines = [ln for ln in lines if ln and not ln.startswith("#")]
+    head = "".join(lines[:20])
+    ws, sc, cm = head.count(" ") + head.count("\t"), head.count(";"), head.count(",")
+    sep = None if ws >= sc and ws >= cm else (";" if sc >= cm else ",")
+
+    def atof(v: str) -> float:
+        import re
+
+        m = re.match(r"\s*[-+]?(\d+\.?\d*|\.\d+)([eE][-+]?\d+)?", v)
+        return float(m.group(0)) if m else 0.0
+
+    rows = []
+    for ln in lines:
+        f = ln.split(sep) if sep else ln.split()
+        if len(f) < 2:
+            raise CaseError(f"{what}: value 2 does not exist in line '{ln}' of {path}")
+        rows.append((atof(f[0]), atof(f[1])))
+    if len(rows) < 2:
+        raise CaseError(f"{what}: Cannot be less than two values. ({path})")
+    return np.array(rows, np.float64)
+
+
 class CaseError(ValueError):
     """An invalid or unsupported case configuration (the reference's JException)."""
 
@@ -265,6 +294,7 @@ class XmlCase:
             casepath = casepath[:-4]
         self.casepath = casepath
         self.case_name = os.path.basename(casepath)
+        self._dircase = os.path.dirname(os.path.abspath(casepath))  # JSph::DirCase (data files)
         xmlfile = casepath + ".xml"
         if not os.path.exists(xmlfile):
             raise CaseError(f"Case configuration was not found: {xmlfile}")
@@ -436,8 +466,9 @@ class XmlCase:
         self.tvisco = tv
         self.visco = p.num("Visco")
         self.viscoboundfactor = p.num("ViscoBoundFactor", True, 1.0)
-        if p.values.get("ViscoTime"):
-            raise CaseError("ViscoTime is not supported by this core.")
+        # ViscoTime: Visco(t) from a data file next to the case (JDsViscoInput::LoadFile)
+        fv = p.values.get("ViscoTime", "")
+        self.visco_table = _read_datafile(os.path.join(self._dircase, fv), "ViscoTime") if fv else None
         bc = p.int("Boundary", True, 1)
         if bc not in (1, 2):
             raise CaseError("Boundary Condition method is not valid.")
@@ -474,10 +505,13 @@ class XmlCase:
         self.dtini = max(0.0, p.num("DtIni", True, 0.0))
         self.dtmin = max(0.0, p.num("DtMin", True, 0.0))
         self.coefdtmin = p.num("CoefDtMin", True, 0.05)
-        if p.int("DtAllParticles", True, 0) == 1:
-            raise CaseError("DtAllParticles is not supported by this core.")
-        if p.num("DtFixed", True, 0.0) > 0 or p.values.get("DtFixedFile", "none").lower() not in ("", "none"):
-            raise CaseError("DtFixed / DtFixedFile are not supported by this core.")
+        self.dtallparticles = 1 if p.int("DtAllParticles", True, 0) == 1 else 0  # JSph.cpp:697
+        self.dtfixed = max(0.0, p.num("DtFixed", True, 0.0))  # JSph.cpp:699-707
+        ff = p.values.get("DtFixedFile", "")
+        ff = "" if ff.upper() == "NONE" else ff
+        if self.dtfixed and ff:
+            raise CaseError("The parameters 'DtFixed' and 'DtFixedFile' cannot be used at the same time.")
+        self.dtfixed_table = _read_datafile(os.path.join(self._dircase, ff), "DtFixedFile") if ff else None
         self.rhopoutmin = p.num("RhopOutMin") if p.exists("RhopOutMin") else 700.0
         self.rhopoutmax = p.num("RhopOutMax") if p.exists("RhopOutMax") else 1300.0
         self.partsoutmax = p.num("PartsOutMax", True, 1.0)
@@ -769,7 +803,12 @@ class XmlCase:
         dt = CFL*min(sqrt(h/AceMax), h/(max(Cs0,10*VelMax) + h*ViscDtMax)) <= CFL*h/Cs0,
         floored at DtMin), used by the run driver to batch steps between outputs."""
         k = self._derived()
-        return max(k["cflnumber"] * k["kernelh"] / k["cs0"], k["dtmin"]) * (1 + 1e-9)
+        cap = k["cflnumber"] * k["kernelh"] / k["cs0"]
+        if self.dtfixed > 0:  # DtFixed / DtFixedFile replace the computed dt (JSphCpu.cpp:1621)
+            cap = self.dtfixed
+        elif self.dtfixed_table is not None:
+            cap = float(np.max(self.dtfixed_table[:, 1])) / 1000
+        return max(cap, k["dtmin"]) * (1 + 1e-9)
 
     def _derived(self) -> dict:
         from .core import case_derive
@@ -794,7 +833,7 @@ class XmlCase:
             rheology=self.rheology, velgrad=self.velgrad, tvisco=self.tvisco, nphases=len(self.phases),
             phases=self.phases, relaxation_dt=self.relaxation_dt, shift_mode=self.shift_mode,
             shift_coef=self.shift_coef, shift_tfs=self.shift_tfs, data2d=int(self.data2d),
-            data2d_posy=self.data2d_posy,
+            data2d_posy=self.data2d_posy, dtallparticles=self.dtallparticles, dtfixed=self.dtfixed,
         )
 
 

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define SPH_ABI_VERSION 7
+#define SPH_ABI_VERSION 8
 
 typedef enum {
   SPH_OK = 0,
@@ -176,6 +176,13 @@ typedef struct SphCaseDef {
   int32_t data2d;
   int32_t pad2d;
   double data2d_posy;
+  /* dt options (JSph::LoadConfigParameters, JSph.cpp:697-707): DtAllParticles = VelMax
+   * over every particle, not only the fluid (JSphCpu.cpp:475); dtfixed > 0 = <parameter
+   * DtFixed>, the dt of every step (JDsFixedDt; a DtFixedFile table goes through
+   * sph_solver_set_time_table) */
+  int32_t dtallparticles;
+  int32_t pad_dt;
+  double dtfixed;
 } SphCaseDef;
 
 /*
@@ -214,6 +221,8 @@ typedef struct SphConstants {
   int32_t kernel;
   float cub_a1, cub_a2, cub_aa, cub_a24, cub_c1, cub_d1, cub_c2, cub_od_wdeltap;
   int32_t pad4;
+  int32_t dtallparticles, pad5;     /* DtAllParticles                       */
+  double dtfixed;                   /* DtFixed (0: variable dt)             */
 } SphConstants;
 
 /* Step statistics kept on the device and read back on demand. */
@@ -484,6 +493,16 @@ enum { SPH_FTTAB_LINVEL = 0, SPH_FTTAB_ANGVEL = 1, SPH_FTTAB_LINFORCE = 2, SPH_F
 int sph_solver_set_floating_table(SphSolver* s, uint32_t body, int32_t kind, uint32_t n, const double* times,
                                   const double* values);
 int sph_solver_floatings(SphSolver* s, uint32_t cap, SphFloatingState* out, uint32_t* nft);
+/* Time tables of the step (call before the first step, or after sph_solver_set_time; on
+ * slabs on every rank; n >= 2 rows, times nondecreasing, n = 0 removes the table):
+ *   SPH_TTAB_DTFIXED  <parameter DtFixedFile>: dt(t) of every step, values in ms as in the
+ *                     file (JDsFixedDt::LoadFile/GetDt, JDsFixedDt.cpp; applied in DtVariable
+ *                     before the NaN check and the DtMin floor, JSphCpu.cpp:1621);
+ *   SPH_TTAB_VISCO    <parameter ViscoTime>: Visco(t) (JDsViscoInput, float rows), set at the
+ *                     start of every step from its TimeStep (JSphCpuSingle.cpp:1092); the
+ *                     boundary viscosity is Visco x ViscoBoundFactor. */
+enum { SPH_TTAB_DTFIXED = 0, SPH_TTAB_VISCO = 1 };
+int sph_solver_set_time_table(SphSolver* s, int32_t kind, uint32_t n, const double* times, const double* values);
 /* PartFloat.fbi4 (JPartFloatBi4Save::SaveInitial + AddPartFloat/SavePartFloat,
  * JPartFloatBi4.cpp:243-346): per-body head arrays [nft] and, per saved PART k, its
  * Cpart/Step/TimeStep and the body states center[k][nft][3], fvel, fomega, facelin,
