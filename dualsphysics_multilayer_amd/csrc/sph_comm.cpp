@@ -126,9 +126,10 @@ void LocalHub::abort() {
 }
 
 class LocalTransport final : public SlabTransport {
-  // Copies on the DMA engines, not as blit kernels: like the xGMI transfers of the RCCL
-  // path they then run beside the interaction instead of queueing for its compute units.
-  static constexpr hipMemcpyKind kCopyKind = hipMemcpyDeviceToDeviceNoCU;
+  // Blit-kernel copies: on one GPU they run in the block slots the interior interaction
+  // leaves free (sph_solver.cpp) at ~1 TB/s; the DMA engines (hipMemcpyDeviceToDeviceNoCU)
+  // move the ghost messages at ~50 GB/s, slower than the copy kernels even beside it.
+  static constexpr hipMemcpyKind kCopyKind = hipMemcpyDeviceToDevice;
 
  public:
   LocalTransport(std::shared_ptr<LocalHub> hub, int r) : hub_(std::move(hub)) {

@@ -148,6 +148,9 @@ void derive_constants(const SphCaseDef& c, SphConstants& k) {
     throw SphError(SPH_ERR_ARG, "Viscosity treatment is not valid.");
   if (k.shift_mode < SPH_SHIFT_NONE || k.shift_mode > SPH_SHIFT_FULL)
     throw SphError(SPH_ERR_ARG, "Shifting mode is not valid.");
+  k.dtallparticles = c.dtallparticles ? 1 : 0;  // JSph.cpp:697
+  if (!(c.dtfixed >= 0)) throw SphError(SPH_ERR_ARG, "DtFixed must not be negative");
+  k.dtfixed = c.dtfixed;  // max(0, DtFixed), JSph.cpp:699
   if (k.rheology == SPH_RHEOLOGY_SINGLE) {
     if (k.tvisco == SPH_VISCO_CONSTEQ)
       throw SphError(SPH_ERR_ARG, "ViscoTreatment 'Constitutive  eq.' not valid for Single-phase classic formulation.");
@@ -182,9 +185,6 @@ void derive_constants(const SphCaseDef& c, SphConstants& k) {
   // are read, and ConfigConstants2 keeps a non-zero DtMin)
   const float coefdtmin = float(c.coefdtmin) * 1.0e-5f;  // CoefDtMin*=1.0e-5f
   k.dtmin = (double(k.kernelh) / k.cs0) * double(coefdtmin);
-  k.dtallparticles = c.dtallparticles ? 1 : 0;  // JSph.cpp:697
-  if (!(c.dtfixed >= 0)) throw SphError(SPH_ERR_ARG, "DtFixed must not be negative");
-  k.dtfixed = c.dtfixed;  // max(0, DtFixed), JSph.cpp:699
 }
 
 static KConst make_kconst(const SphConstants& c) {

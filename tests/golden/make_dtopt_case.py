@@ -7,7 +7,7 @@ tests/golden/bi4/dtopt_<variant>/
                                     DtFixed (a constant dt), DtFixedFile (dt(t) in ms,
                                     JDsFixedDt), ViscoTime (Visco(t), JDsViscoInput),
                                     DtAllParticles (VelMax over every particle: the flume's
-                                    piston is faster than the still water)
+                                    fast flap, ~4 m/s at its tip, sets it)
   ref.npz                           the reference run (-nsteps:N -svsteps:1 -saveposdouble:1):
                                     PARTs at the kept steps (sorted by idp), every PART time,
                                     and noise_<k> = [dpos, dvel, drho] between the fast-math
@@ -35,6 +35,7 @@ VARIANTS = {
                                     {"dtfixed.csv": "# time(s);dt(ms)\n0;0.08\n0.006;0.22\n1;0.22\n"}),
     "verlet_ddt2_viscotime": ("dambreak", 0.03, 1, 2, 100, (1, 10, 100), {"ViscoTime": "visco.txt"},
                               {"visco.txt": "# time visco\n0 0.01\n0.004 0.6\n1 0.6\n"}),
+    # a fast wide flap (no wait, 8 Hz, 12 degrees): its tip, ~4 m/s, sets VelMax (10 VelMax > Cs0)
     "flume_verlet_ddt2_dtallparticles": ("flume", 0.03, 1, 2, 60, (1, 20, 60), {"DtAllParticles": "1"}, {}),
 }
 
@@ -48,7 +49,8 @@ def make(name, gen, dp, step, ddt, nsteps, keep, params, files):
         if gen == "dambreak":
             cmd = [os.path.join(REF, "gencase_ref"), repr(dp), tmp, str(step), str(ddt), "1.5", case, "1", "3"]
         else:
-            cmd = [os.path.join(REF, "genflume_ref"), repr(dp), tmp, str(step), str(ddt), "1.0", case, "1"]
+            cmd = [os.path.join(REF, "genflume_ref"), repr(dp), tmp, str(step), str(ddt), "1.0", case, "1", "1.2",
+                   "0.3", "0.4", "0.2", "0", "8", "12"]
         subprocess.check_call(cmd, stdout=subprocess.DEVNULL)
         fx = os.path.join(tmp, case + ".xml")
         txt = open(fx).read()
