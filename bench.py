@@ -265,7 +265,8 @@ def measure(case, args, rank: int, world: int, device: int, dist, use_slab: bool
         if dist is not None:
             import torch
 
-            dist.barrier()
+            if world > 1:  # a one-rank slab run (--force-slab) has no one to wait for
+                dist.barrier()
             torch.cuda.synchronize(device)
 
     # The timed region records HIP events around the interaction only (the roofline's launch

@@ -5,7 +5,7 @@ import ctypes as C
 
 import numpy as np
 
-SPH_ABI_VERSION = 8
+SPH_ABI_VERSION = 9
 
 SPH_STATUS = {
     0: "SPH_OK",
@@ -31,7 +31,7 @@ _CASEDEF_DEFAULTS = {"tboundary": SPH_BOUND_DBC, "slipmode": SPH_SLIP_VEL0, "mdb
                      "rheology": SPH_RHEOLOGY_SINGLE, "velgrad": SPH_VELGRAD_FDA, "tvisco": SPH_VISCO_ARTIFICIAL,
                      "nphases": 0, "relaxation_dt": 0.2, "shift_mode": SPH_SHIFT_NONE, "pad_shift": 0,
                      "shift_coef": -2.0, "shift_tfs": 0.0, "phases": (),
-                     "data2d": 0, "pad2d": 0, "data2d_posy": 0.0, "dtallparticles": 0, "pad_dt": 0,
+                     "data2d": 0, "pad2d": 0, "data2d_posy": 0.0, "dtallparticles": 0, "symmetry": 0,
                      "dtfixed": 0.0}
 SPH_TTAB_DTFIXED, SPH_TTAB_VISCO = 0, 1
 
@@ -99,7 +99,7 @@ class SphCaseDef(C.Structure):
         ("pad2d", C.c_int32),
         ("data2d_posy", C.c_double),
         ("dtallparticles", C.c_int32),
-        ("pad_dt", C.c_int32),
+        ("symmetry", C.c_int32),
         ("dtfixed", C.c_double),
     ]
 
@@ -194,7 +194,7 @@ class SphConstants(C.Structure):
         ("cub_od_wdeltap", C.c_float),
         ("pad4", C.c_int32),
         ("dtallparticles", C.c_int32),
-        ("pad5", C.c_int32),
+        ("symmetry", C.c_int32),
         ("dtfixed", C.c_double),
     ]
 

@@ -79,6 +79,9 @@ class DamBreakCase:
     shift_coef: float = -2.0
     shift_tfs: float = 0.0
     kernel: int = 2  # <parameter Kernel>: 1 Cubic spline, 2 Wendland (JSph.cpp:554-559)
+    # <parameter Symmetry> (JSph.cpp:714): the half tank y >= 0 with the plane y = 0 as a
+    # mirror — no y = 0 wall, the fluid from y = 0 (oracle/tools/gencase_ref sym 1)
+    symmetry: bool = False
     # generated
     pos: np.ndarray = field(init=False, repr=False)
     vel: np.ndarray = field(init=False, repr=False)
@@ -93,11 +96,12 @@ class DamBreakCase:
         mx, my, mz = _cround(0.4 / dp), _cround(0.67 / dp), _cround(0.3 / dp)
         # Boundary: loop order k, j, i over the full tank lattice, walls only.
         k, j, i = np.meshgrid(np.arange(nz + 1), np.arange(ny + 1), np.arange(nx + 1), indexing="ij")
-        wall = (k == 0) | (i == 0) | (i == nx) | (j == 0) | (j == ny)
+        wall = (k == 0) | (i == 0) | (i == nx) | ((j == 0) & (not self.symmetry)) | (j == ny)
         bi, bj, bk = i[wall], j[wall], k[wall]
         self._wall_ijk = (bi, bj, bk, nx, ny)
         # Fluid: i in [1,mx], j in [1,my-1], k in [1,mz], loop order k, j, i.
-        fk, fj, fi = np.meshgrid(np.arange(1, mz + 1), np.arange(1, my), np.arange(1, mx + 1), indexing="ij")
+        fk, fj, fi = np.meshgrid(np.arange(1, mz + 1), np.arange(0 if self.symmetry else 1, my),
+                                 np.arange(1, mx + 1), indexing="ij")
         ii = np.concatenate([bi, fi.ravel()]).astype(np.float64)
         jj = np.concatenate([bj, fj.ravel()]).astype(np.float64)
         kk = np.concatenate([bk, fk.ravel()]).astype(np.float64)
@@ -129,7 +133,8 @@ class DamBreakCase:
         nor = np.zeros((bi.size, 3))
         nor[:, 0] = np.where(bi == 0, hd, np.where(bi == nx, -hd, 0.0))
         if not getattr(self, "data2d", False):  # 2-D: no y walls, no y normal
-            nor[:, 1] = np.where(bj == 0, hd, np.where(bj == ny, -hd, 0.0))
+            y0 = 0.0 if getattr(self, "symmetry", False) else hd  # Symmetry: no y = 0 wall
+            nor[:, 1] = np.where(bj == 0, y0, np.where(bj == ny, -hd, 0.0))
         nor[:, 2] = np.where(bk == 0, hd, 0.0)
         return nor
 
@@ -203,6 +208,8 @@ class DamBreakCase:
         dif = dmax - dmin
         prcmax = np.array([0.0, 0.0, 0.5])  # posmax z="default + 50%"
         dmax = dmax + dif * prcmax
+        if getattr(self, "symmetry", False):
+            dmin[1] = 0.0  # JSph::ResizeMapLimits with Symmetry (JSph.cpp:1386)
         return dmin, dmax
 
     def case_def(self) -> dict:
@@ -247,6 +254,7 @@ class DamBreakCase:
             data2d_posy=0.0,
             dtallparticles=int(getattr(self, "dtallparticles", 0)),
             dtfixed=float(getattr(self, "dtfixed", 0.0)),
+            symmetry=int(bool(getattr(self, "symmetry", False))),
         )
 
 

@@ -574,7 +574,8 @@ def part_header(case, stats: dict | None = None, cpart: int = 0, app_name: str =
                 map_posmin=list(cd["map_realposmin"]), map_posmax=list(cd["map_realposmax"]),
                 case_posmin=pmin.tolist(), case_posmax=pmax.tolist(), pos_double=1,
                 visco_type=1, visco=case.visco, viscoboundfactor=case.viscoboundfactor,
-                gravity=list(case.gravity), mkbound=10, mkfluid=0)
+                gravity=list(case.gravity), mkbound=10, mkfluid=0,
+                symmetry=int(bool(cd.get("symmetry", 0))))
 
 
 def write_partfloat(path: str, floatings: list, parts: list, mkboundfirst: int = 10,

@@ -88,6 +88,7 @@ struct KConst {
   // (JDsFixedDt: a constant dt, or dt(t) from rows of (time [s], dt [ms])) and ViscoTime
   // (JDsViscoInput: Visco(t), evaluated at every step's TimeStep, JSphCpuSingle.cpp:1092)
   int dtallp;
+  int symmetry;  // Symmetry: images across y = 0 of the p2 near it (JSphCpu.cpp:566-613, 671-796)
   int dtfix_n;
   double dtfix_val;
   const double* dtfix_t;

@@ -1219,7 +1219,7 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
                        bool withm1, bool withpre, const KConst& K, const double dom_posmin[3], float4* poscell,
                        float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
                        IncDivScratch& s, SortScratch& srt, unsigned keybits, const float4* phase_eos,
-                       const SlabFaces* faces, unsigned ngl, unsigned ngr) {
+                       const SlabFaces* faces, unsigned ngl, unsigned ngr, hipEvent_t ev_boxes) {
   s.gen++;
   const int usey = g.ncy > 1, usez = g.ncz > 1;
   const unsigned omax = 1u + (usey ? unsigned(g.ncx) : 0u) + (usez ? g.nsheet : 0u);
@@ -1248,6 +1248,8 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
     }
   }
   hipLaunchKernelGGL(k_inc_boxes, dim3(s.nb2), dim3(IB_BS), 0, stm, sc, g, begincell_old, begincell_new, s, omax);
+  // the new begincell is final here: work that needs only it may start beside the push
+  if (ev_boxes) (void)hipEventRecord(ev_boxes, stm);
   GatherArgs a;
   a.phase_eos = phase_eos;
   a.vfirst = ~0u;

@@ -455,10 +455,14 @@ __device__ __forceinline__ void drain_words(const KConst& K, const P1& p, unsign
 // dry the next word shifts in.  Value selects only (a word picked by reference puts the
 // masks in scratch), no divergent branch in the loop (the second pop of an iteration is
 // unconditional; an empty pop's pair is masked off).
-template <int TDENSITY, int MODE, bool FT = false>
+// SELF (the Symmetry image of the own row): staged record `self` of window a is the lane's
+// own p1, whose image is no neighbour (the reference visits an image only after its
+// original passed the rr2 >= ALMOSTZERO test, JSphCpu.cpp:687,793-796).
+template <int TDENSITY, int MODE, bool FT = false, bool SELF = false>
 __device__ __forceinline__ void tile_unit(const KConst& K, const P1& p, float thr, int wa0, int wa1, int wb0, int wb1,
                                           const float4* __restrict__ sA, const float4* __restrict__ sB,
-                                          const typename CRecT<FT>::type* __restrict__ sC, const PassK& Q, TAcc& a) {
+                                          const typename CRecT<FT>::type* __restrict__ sC, const PassK& Q, TAcc& a,
+                                          int self = -1) {
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
   for (int off = 0;; off += 128) {  // a second round only for windows of > 128 candidates
     const int na = wa1 - wa0 - off, nb = wb1 - wb0 - off;
@@ -466,6 +470,11 @@ __device__ __forceinline__ void tile_unit(const KConst& K, const P1& p, float th
     unsigned long long c0, c1, c2, c3;
     test128(sA, wa0 + off, min(na, 128), px2, py2, pz2, thr, c0, c1);
     test128(sA, wb0 + off, min(nb, 128), px2, py2, pz2, thr, c2, c3);
+    if (SELF) {
+      const int k = self - (wa0 + off);
+      if (k >= 0 && k < 64) c0 &= ~(1ull << k);
+      else if (k >= 64 && k < 128) c1 &= ~(1ull << (k - 64));
+    }
     drain_words<TDENSITY, MODE, FT>(K, p, c0, c1, c2, c3, wa0 + off, wa0 + off + 64, wb0 + off, wb0 + off + 64, sA,
                                     sB, sC, Q, a);
   }
@@ -596,20 +605,23 @@ __device__ __forceinline__ void put_c(float4* sC, unsigned i, float pr, float ir
   const float rir = r * ir;
   sC[i] = make_float4(pr * rir, rir, r, kind);
 }
+// mir (Symmetry, rows of the first y row of a p1 in it): the records' images across y = 0,
+// position y and velocity y negated (JSphCpu.cpp:684,709).
 template <typename CR>
 __device__ __forceinline__ void stage_row(const KConst& K, unsigned rs, unsigned re, unsigned dst, int xo, int dy,
                                           int dz, const float4* __restrict__ poscell,
                                           const float4* __restrict__ velrhop, const float* __restrict__ press,
                                           float4* __restrict__ sA, float4* __restrict__ sB, CR* __restrict__ sC,
-                                          const FtRec& ft) {
+                                          const FtRec& ft, bool mir = false) {
   const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
   for (unsigned i = threadIdx.x; i < re - rs; i += TB) {
     const float4 pc = poscell[rs + i];
     const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
     const float x2 = pc.x + float(cx2 - xo) * K.scell;
-    const float y2 = pc.y + oy, z2 = pc.z + oz;
+    const float y2 = mir ? -(pc.y + oy) : pc.y + oy, z2 = pc.z + oz;
     sA[dst + i] = make_float4(x2, y2, z2, x2 * x2 + y2 * y2 + z2 * z2);
-    const float4 vr = velrhop[rs + i];
+    float4 vr = velrhop[rs + i];
+    if (mir) vr.y = -vr.y;
     sB[dst + i] = vr;
     const float ir = frcp(vr.w);
     put_c(sC, dst + i, press[rs + i], ir, K, ft, rs + i);
@@ -626,6 +638,11 @@ __device__ __forceinline__ PassK pass_k(const KConst& K, float cvisc, float m2, 
   return q;
 }
 
+// Staged index of the lane's own p1 in the records [rs, re) staged from 0, or -1.
+__device__ __forceinline__ int self_in(const RowCtx& rc, unsigned rs, unsigned re) {
+  return (rc.act && rc.p1 >= rs && rc.p1 < re) ? int(rc.p1 - rs) : -1;
+}
+
 // One interaction pass of the item's p1 over the 3x3 neighbour rows of one particle
 // kind: MODE 0/2 the fluid rows (fluid / bound p1), MODE 1 the bound rows (fluid p1).
 // Drain units: point-mirrored row pairs, then the item's own row; a pair of rows is
@@ -640,10 +657,18 @@ __device__ __forceinline__ TAcc run_pass(const KConst& K, const DivGrid& g, cons
   TAcc acc = {};
   acc.dstop = dstop0;
   const unsigned cellinit = (MODE == 1 ? 0u : g.boxfluid);
-  for (int u = 0; u < 5; u++) {
-    const int dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
+  // Symmetry: an item of the first y row (its p1 within 2h of y = 0; with cells of 2h that
+  // is every p1 of the row) also meets the images of that row's p2 (all within 2h of the
+  // plane): units 5 (rows dz = -1 / +1) and 6 (the own row, without the p1's own image).
+  // The reference visits an image right after its original when the original is within the
+  // support radius (JSphCpu.cpp:793-796); an image is never nearer than its original for
+  // y >= 0, so the images within the radius are exactly those.
+  const int nu = (K.symmetry && rc.cy == 0) ? 7 : 5;
+  for (int u = 0; u < nu; u++) {
+    const bool mir = u >= 5;
+    const int dza = (u == 0 || u == 1 || u == 2 || u == 5) ? -1 : 0;
     const int dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
-    const bool paired = u < 4;
+    const bool paired = u < 4 || u == 5;
     // rows (dya, dza) and (-dya, -dza); an out-of-grid row is empty
     unsigned rs[2] = {0, 0}, re[2] = {0, 0}, ls[2] = {0, 0}, le[2] = {0, 0};
 #pragma unroll
@@ -661,15 +686,21 @@ __device__ __forceinline__ TAcc run_pass(const KConst& K, const DivGrid& g, cons
     const unsigned n0 = re[0] - rs[0], n1 = re[1] - rs[1];
     if (n0 + n1 == 0u) continue;
     constexpr int tcap = TcapT<FT>::v;
+    // unit 6 (the own row's images): the lane's own record is skipped when it is in the
+    // staged rows (fluid p1, fluid rows)
     if (n0 + n1 <= unsigned(tcap)) {
       // both rows in one segment: [row a][row b]
       __syncthreads();
-      if (n0) stage_row(K, rs[0], re[0], 0u, rc.xo, dya, dza, poscell, velrhop, press, sA, sB, sC, ft);
-      if (n1) stage_row(K, rs[1], re[1], n0, rc.xo, -dya, -dza, poscell, velrhop, press, sA, sB, sC, ft);
+      if (n0) stage_row(K, rs[0], re[0], 0u, rc.xo, dya, dza, poscell, velrhop, press, sA, sB, sC, ft, mir);
+      if (n1) stage_row(K, rs[1], re[1], n0, rc.xo, -dya, -dza, poscell, velrhop, press, sA, sB, sC, ft, mir);
       __syncthreads();
       const int wa0 = int(ls[0] - rs[0]), wa1 = rc.act && n0 ? int(le[0] - rs[0]) : wa0;
       const int wb0 = int(n0 + ls[1] - rs[1]), wb1 = rc.act && n1 ? int(n0 + le[1] - rs[1]) : wb0;
-      tile_unit<TDENSITY, MODE, FT>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, Q, acc);
+      if (u == 6)
+        tile_unit<TDENSITY, MODE, FT, true>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, Q, acc,
+                                            self_in(rc, rs[0], re[0]));
+      else
+        tile_unit<TDENSITY, MODE, FT>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, Q, acc);
     } else {
       // too long for one segment: each row on its own, in TCAP segments
       for (int k = 0; k < 2; k++) {
@@ -677,11 +708,15 @@ __device__ __forceinline__ TAcc run_pass(const KConst& K, const DivGrid& g, cons
         for (unsigned seg = rs[k]; seg < re[k]; seg += tcap) {
           const unsigned segn = min(unsigned(tcap), re[k] - seg);
           __syncthreads();
-          stage_row(K, seg, seg + segn, 0u, rc.xo, dy, dz, poscell, velrhop, press, sA, sB, sC, ft);
+          stage_row(K, seg, seg + segn, 0u, rc.xo, dy, dz, poscell, velrhop, press, sA, sB, sC, ft, mir);
           __syncthreads();
           const int w0 = int(max(ls[k], seg) - seg);
           const int w1 = rc.act ? max(w0, int(min(le[k], seg + segn)) - int(seg)) : w0;
-          tile_unit<TDENSITY, MODE, FT>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, Q, acc);
+          if (u == 6)
+            tile_unit<TDENSITY, MODE, FT, true>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, Q, acc,
+                                                self_in(rc, seg, seg + segn));
+          else
+            tile_unit<TDENSITY, MODE, FT>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, Q, acc);
         }
       }
     }
@@ -892,7 +927,7 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
         p.inv_rho = frcp(p.vr.w);
         const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
         const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
-        const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act};
+        const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act, p1};
         // pass 0: fluid p2 (fluid p1: momentum/continuity/DDT; bound p1: continuity),
         // pass 1: bound p2 of fluid p1.  Each pass holds only its own accumulator.
         TAcc f, bnd = {0, 0, 0, 0, 0, 0, false};

@@ -25,7 +25,7 @@ struct PartArrays {
   float4* tau = nullptr;         // Laminar+SPS: sub-particle stress tensor, [2i] {xx,xy,xz,yy}, [2i+1] {yz,zz}
 };
 
-// JSphCpu::UpdatePos (JSphCpu.cpp:1240-1293), single domain, no periodic/symmetry.
+// JSphCpu::UpdatePos (JSphCpu.cpp:1240-1293), single domain, no periodic.
 __device__ __forceinline__ void update_pos(const KConst& K, double rx, double ry, double rz, double movx, double movy,
                                            double movz, bool outrhop, unsigned p, const PartArrays& a) {
   const bool outmove = (fabsf(float(movx)) > K.movlimit || fabsf(float(movy)) > K.movlimit ||
@@ -33,6 +33,7 @@ __device__ __forceinline__ void update_pos(const KConst& K, double rx, double ry
   rx += movx;
   ry += movy;
   rz += movz;
+  if (K.symmetry && ry < 0) ry = -ry;  // Symmetry: reflected across y = 0 (JSphCpu.cpp:1247)
   const double dx = rx - K.map_realposmin_x, dy = ry - K.map_realposmin_y, dz = rz - K.map_realposmin_z;
   const bool out = (dx != dx || dy != dy || dz != dz || dx < 0 || dy < 0 || dz < 0 || dx >= K.map_realsize_x ||
                     dy >= K.map_realsize_y || dz >= K.map_realsize_z);
@@ -191,7 +192,8 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
                        bool withm1, bool withpre, const KConst& K, const double dom_posmin[3], float4* poscell,
                        float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
                        IncDivScratch& s, SortScratch& srt, unsigned keybits, const float4* phase_eos = nullptr,
-                       const SlabFaces* faces = nullptr, unsigned ngl = 0, unsigned ngr = 0);
+                       const SlabFaces* faces = nullptr, unsigned ngl = 0, unsigned ngr = 0,
+                       hipEvent_t ev_boxes = nullptr);
 
 // ---- interaction (cusph::Interaction_Forces, JSphGpu_ker.cu:788-885) ----
 // With floating bodies (ftmassp != nullptr: particle mass per body, `code` of the

@@ -68,8 +68,7 @@ __device__ __forceinline__ int face_idx(const DivGrid& g, int W, unsigned key, i
 
 // bit 0: record for the left neighbour, bit 1: record for the right, bit 2: stays owned
 // (so a record with bit 2 is a ghost copy, without it a migrant).
-__device__ __forceinline__ unsigned pack_class(const PackArgs& q, unsigned p) {
-  const unsigned dc = q.a.dcell[p];
+__device__ __forceinline__ unsigned pack_class_dc(const PackArgs& q, unsigned dc) {
   if (dc == DCELL_DISCARD || dc == DCELL_OUT) return 0u;
   const int lcx = int(DcelCellx(q.dcc, dc)) - q.g.xoff;
   if (lcx < q.g.xown0) return q.has_left ? 1u : 0u;
@@ -78,6 +77,17 @@ __device__ __forceinline__ unsigned pack_class(const PackArgs& q, unsigned p) {
   if (in_left_face(q.g, lcx) && q.has_left) c |= 1u;
   if (in_right_face(q.g, lcx) && q.has_right) c |= 2u;
   return c;
+}
+
+// The dcell words of a thread's PK_ITEMS particles, loaded before any of them is classified:
+// the per-particle work (ballots, face atomics, LDS ranks) would otherwise serialise the
+// loads, one memory latency per item.
+__device__ __forceinline__ void load_dcells(const PackArgs& q, unsigned base, unsigned n, unsigned (&dcs)[PK_ITEMS]) {
+#pragma unroll
+  for (int it = 0; it < PK_ITEMS; it++) {
+    const unsigned p = base + it * PK_BS + threadIdx.x;
+    dcs[it] = p < n ? q.a.dcell[p] : DCELL_DISCARD;
+  }
 }
 
 // the four stream flags of a class
@@ -94,18 +104,21 @@ __global__ __launch_bounds__(PK_BS) void k_pack_count(const DevScalars* __restri
   const unsigned n = sc->np;
   const unsigned base = blockIdx.x * PK_TILE;
   unsigned c4[7] = {0, 0, 0, 0, 0, 0, 0};  // 4 streams, staying, ghosts per face (face boxes)
+  unsigned dcs[PK_ITEMS];
+  load_dcells(q, base, n, dcs);
+#pragma unroll
   for (int it = 0; it < PK_ITEMS; it++) {
     const unsigned p = base + it * PK_BS + threadIdx.x;
     int fi[2] = {-1, -1};  // face box of an owned face particle, per face
     if (p < n) {
-      const unsigned c = pack_class(q, p);
+      const unsigned c = pack_class_dc(q, dcs[it]);
       bool f[4];
       streams(c, f);
 #pragma unroll
       for (int k = 0; k < 4; k++) c4[k] += f[k] ? 1u : 0u;
       c4[4] += (c >> 2) & 1u;
       if (q.fcnt[0] && (c & 4u) && (c & 3u)) {
-        const unsigned key = box_key(q.a.dcell[p], q.a.code[p], q.g, q.dcc);
+        const unsigned key = box_key(dcs[it], q.a.code[p], q.g, q.dcc);
         if (c & 1u) fi[0] = face_idx(q.g, q.W, key, q.g.xown0);
         if (c & 2u) fi[1] = face_idx(q.g, q.W, key, q.g.xown1 - q.W);
       }
@@ -242,10 +255,13 @@ __global__ __launch_bounds__(PK_BS) void k_pack_write(const DevScalars* __restri
   for (int k = 0; k < 4; k++) off[k] = q.tilecnt[k * q.ntiles + blockIdx.x];
   const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const unsigned long long lt = (1ull << lane) - 1ull;
+  unsigned dcs[PK_ITEMS];
+  load_dcells(q, base, n, dcs);
+#pragma unroll
   for (int it = 0; it < PK_ITEMS; it++) {
     if (base + it * PK_BS >= n) break;  // uniform over the block
     const unsigned p = base + it * PK_BS + threadIdx.x;
-    const unsigned c = p < n ? pack_class(q, p) : 0u;
+    const unsigned c = p < n ? pack_class_dc(q, dcs[it]) : 0u;
     bool f[4];
     streams(c, f);
     unsigned long long bal[4];
@@ -406,47 +422,51 @@ void launch_ghost_keys(hipStream_t stm, const SlabFaces& f, DivGrid g, unsigned 
                        int(ngl > 0), int(ngr > 0));
 }
 
-// Ghost records from the sorted arrays, one thread per face box: its count[idx] first members
-// (the old members come first, in previous-index order — the order the pre-divide pack
-// counted them in) to records pre[idx].. of the face's message.  Reads are contiguous per box.
+// Ghost records from the sorted arrays, one thread per record (left face's records first):
+// record r of a face belongs to the face box idx with pre[idx] <= r < pre[idx + 1] (binary
+// search of the face's prefixes) and is that box's (r - pre[idx])-th member (the old members
+// come first, in previous-index order — the order the pre-divide pack counted them in).
+// Writes are contiguous per wave; a thread per box instead serialised the largest boxes
+// (135-200 us per cfg3 slab divide, against ~5 us for this form).
 __global__ __launch_bounds__(256) void k_ghost_pack(DevScalars* __restrict__ sc, SlabFaces f, DivGrid g,
                                                     const unsigned* __restrict__ bc, PartArrays a,
-                                                    const float4* __restrict__ poscell, SlabSendBufs b, int hl,
-                                                    int hr) {
+                                                    const float4* __restrict__ poscell, SlabSendBufs b, unsigned ngl,
+                                                    unsigned ngr) {
   const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int side = t < f.nfb ? 0 : 1;
-  const unsigned idx = side ? t - f.nfb : t;
-  if (idx >= f.nfb || (side ? !hr : !hl)) return;
-  const unsigned n = f.msg[side][FMSG_HDR + idx];
-  if (!n) return;
-  const unsigned key = face_key(g, f.W, idx, side ? g.xown1 - f.W : g.xown0);
-  const unsigned i0 = bc[key];
-  if (i0 + n > bc[key + 1]) {  // the divide placed fewer particles in the box than were counted
+  if (t >= ngl + ngr) return;
+  const int side = t < ngl ? 0 : 1;
+  const unsigned r = side ? t - ngl : t;
+  const unsigned* __restrict__ pre = f.pre[side];
+  unsigned lo = 0, hi = f.nfb;  // pre[lo] <= r < pre[hi]
+  while (hi - lo > 1u) {
+    const unsigned mid = (lo + hi) >> 1;
+    if (pre[mid] <= r) lo = mid;
+    else hi = mid;
+  }
+  const unsigned key = face_key(g, f.W, lo, side ? g.xown1 - f.W : g.xown0);
+  const unsigned i = bc[key] + (r - pre[lo]);
+  if (i >= bc[key + 1]) {  // the divide placed fewer particles in the box than were counted
     atomicOr(&sc->error_flags, ERR_HALO);
     return;
   }
-  SlabGhost* out = (side ? b.gr : b.gl) + f.pre[side][idx];
-  for (unsigned j = 0; j < n; j++) {
-    const unsigned i = i0 + j;
-    const float4 pc = poscell[i];
-    SlabGhost r;
-    r.rx = pc.x;
-    r.ry = pc.y;
-    r.rz = pc.z;
-    r.dcell = a.dcell[i];
-    r.velrhop = a.velrhop[i];
-    r.idp = a.idp[i];
-    r.code = a.code[i];
-    r.pad = 0;
-    out[j] = r;
-  }
+  const float4 pc = poscell[i];
+  SlabGhost rec;
+  rec.rx = pc.x;
+  rec.ry = pc.y;
+  rec.rz = pc.z;
+  rec.dcell = a.dcell[i];
+  rec.velrhop = a.velrhop[i];
+  rec.idp = a.idp[i];
+  rec.code = a.code[i];
+  rec.pad = 0;
+  (side ? b.gr : b.gl)[r] = rec;
 }
 
 void launch_ghost_pack(hipStream_t stm, DevScalars* sc, const SlabFaces& f, DivGrid g, const unsigned* begincell,
                        const PartArrays& a, const float4* poscell, SlabSendBufs b, unsigned ngl, unsigned ngr) {
   if (ngl + ngr)
-    hipLaunchKernelGGL(k_ghost_pack, dim3((2 * f.nfb + 255) / 256), dim3(256), 0, stm, sc, f, g, begincell, a,
-                       poscell, b, int(ngl > 0), int(ngr > 0));
+    hipLaunchKernelGGL(k_ghost_pack, dim3((ngl + ngr + 255) / 256), dim3(256), 0, stm, sc, f, g, begincell, a,
+                       poscell, b, ngl, ngr);
 }
 
 // ---------------------------------------------------------------------------------

@@ -149,6 +149,16 @@ void derive_constants(const SphCaseDef& c, SphConstants& k) {
   if (k.shift_mode < SPH_SHIFT_NONE || k.shift_mode > SPH_SHIFT_FULL)
     throw SphError(SPH_ERR_ARG, "Shifting mode is not valid.");
   k.dtallparticles = c.dtallparticles ? 1 : 0;  // JSph.cpp:697
+  // Symmetry (JSph.cpp:714; its checks :1174-1179, MapRealPosMin.y = 0 :1386)
+  k.symmetry = c.symmetry ? 1 : 0;
+  if (k.symmetry) {
+    if (k.data2d) throw SphError(SPH_ERR_ARG, "Symmetry is not allowed with 2-D simulations.");
+    if (k.tvisco != SPH_VISCO_ARTIFICIAL) throw SphError(SPH_ERR_ARG, "Symmetry is only allowed with Artificial viscosity.");
+    if (c.map_realposmin[1] != 0.0) throw SphError(SPH_ERR_ARG, "Symmetry needs MapRealPosMin.y = 0 (JSph.cpp:1386)");
+    if (k.rheology != SPH_RHEOLOGY_SINGLE || k.shift_mode != SPH_SHIFT_NONE || k.scelldiv != 1)
+      throw SphError(SPH_ERR_UNSUPPORTED, "Symmetry is implemented for the single-phase interaction without shifting, "
+                                          "CellMode=full");
+  }
   if (!(c.dtfixed >= 0)) throw SphError(SPH_ERR_ARG, "DtFixed must not be negative");
   k.dtfixed = c.dtfixed;  // max(0, DtFixed), JSph.cpp:699
   if (k.rheology == SPH_RHEOLOGY_SINGLE) {
@@ -256,6 +266,7 @@ static KConst make_kconst(const SphConstants& c) {
   K.shiftmaxdist = float(c.dp * 0.1);
   K.coeftfs = (c.data2d ? 2.0 : 3.0) - double(c.shift_tfs);
   K.dtallp = c.dtallparticles;
+  K.symmetry = c.symmetry;
   K.dtfix_val = c.dtfixed;
   K.viscobf = c.viscoboundfactor;
   {  // binomial coefficients of (1+x)^(1/gamma) - 1
@@ -480,6 +491,7 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
     throw SphError(SPH_ERR_UNSUPPORTED, "the Cubic spline kernel with NN multiphase / Laminar+SPS / shifting is not implemented");
   if (C.kernel == SPH_KERNEL_CUBIC && !tiled_)
     throw SphError(SPH_ERR_UNSUPPORTED, "the Cubic spline kernel runs on the tiled interaction only");
+  if (C.symmetry && !tiled_) throw SphError(SPH_ERR_UNSUPPORTED, "Symmetry runs on the tiled interaction only");
   if (facex_) {
     // the first interaction's face records: the initial particles of the face and ghost
     // columns (both sides of a face count the same particles); later from each exchange
@@ -526,6 +538,7 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
 
 SphGpuSingle::~SphGpuSingle() {
   if (xstream_) (void)hipStreamSynchronize(xstream_);
+  if (istream_) (void)hipStreamSynchronize(istream_);
   if (stream) (void)hipStreamSynchronize(stream);
   Free();
   for (auto& e : pending_) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
@@ -533,6 +546,9 @@ SphGpuSingle::~SphGpuSingle() {
   if (xev_) (void)hipEventDestroy(xev_);
   if (ev_div_) (void)hipEventDestroy(ev_div_);
   if (ev_ghost_) (void)hipEventDestroy(ev_ghost_);
+  if (ev_boxes_) (void)hipEventDestroy(ev_boxes_);
+  if (ev_items_) (void)hipEventDestroy(ev_items_);
+  if (istream_) (void)hipStreamDestroy(istream_);
   if (xstream_) {
     (void)hipStreamSynchronize(xstream_);
     (void)hipStreamDestroy(xstream_);
@@ -1146,13 +1162,20 @@ void SphGpuSingle::RunCellDivide() {
   if (slab() && exchange_armed_) Exchange();
   const unsigned ngl = ghosts ? unsigned(xg_rl_) : 0u, ngr = ghosts ? unsigned(xg_rr_) : 0u;
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET);
+  bool items_side = false;  // the item list built on istream_, beside the push
   if (inc_ok_ && inc_valid_ && G.ncx >= 3) {
     // the previous order merged with the particles whose box changed and, on a slab, the
     // particles the exchange appended and the ghosts' slots (sph_divide.hip)
     inc_.nb2 = inc_blocks_boxes(G.nctt);
+    items_side = tiled_;
+    if (items_side && !istream_) {
+      check_hip(hipStreamCreateWithFlags(&istream_, hipStreamNonBlocking), "hipStreamCreate");
+      check_hip(hipEventCreateWithFlags(&ev_boxes_, hipEventDisableTiming), "hipEventCreate");
+      check_hip(hipEventCreateWithFlags(&ev_items_, hipEventDisableTiming), "hipEventCreate");
+    }
     launch_divide_inc(stream, cap_, sc_, cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_, G, begincell_,
                       begincell_alt_, inc_, sort_, keybits_, nn_ ? phaseeos_ : nullptr, ghosts ? &faces_ : nullptr, ngl,
-                      ngr);
+                      ngr, items_side ? ev_boxes_ : nullptr);
     std::swap(begincell_, begincell_alt_);
   } else {
     // the ghosts' slots sort as entries [np, np + ngl + ngr) after the particles
@@ -1180,16 +1203,25 @@ void SphGpuSingle::RunCellDivide() {
     // the stencil (scelldiv columns) stops reaching a ghost column: the face items and the
     // interior items never share an item, whether they run in one list or in two (with the
     // ghost exchange beside the interior list) — the same items, so the same bits.
+    // After an incremental divide the build runs on istream_ from the moment the new
+    // begincell is final (k_inc_boxes), beside the push, and joins the solver stream here:
+    // cfg2 divide 0.0846 -> see DESIGN.md §4.
+    const hipStream_t is = items_side ? istream_ : stream;
+    if (items_side) check_hip(hipStreamWaitEvent(istream_, ev_boxes_, 0), "items: wait boxes");
     const int S = int(C.scelldiv), hl = slab() && transport_->has_left(), hr = slab() && transport_->has_right();
     int ib = G.xown0 + (hl ? S : 0), ie = G.xown1 - (hr ? S : 0);
     if (ib >= ie) ib = ie = G.xown0;  // a narrow slab: every item reaches a ghost column
     if (overlap) {  // the interior list (qctr_), then the face list (qctrf_) after it
       const int xr[6] = {ib, ie, G.xown0, ib, ie, G.xown1};
-      launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv, xr, qctrf_);
+      launch_items(is, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv, xr, qctrf_);
       ghost_split_ = true;
     } else {
       const int xa[6] = {G.xown0, ib, ib, ie, ie, G.xown1};
-      launch_items(stream, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv, xa);
+      launch_items(is, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv, xa);
+    }
+    if (items_side) {
+      check_hip(hipEventRecord(ev_items_, istream_), "items: event");
+      check_hip(hipStreamWaitEvent(stream, ev_items_, 0), "items: join");
     }
     qfresh_ = true;
   }
@@ -1470,6 +1502,7 @@ void SphGpuSingle::SetFloatings(unsigned nft, const SphFloatingDef* defs, double
   if (stepped_ || ftbodies_) throw SphError(SPH_ERR_STATE, "the floating bodies are configured once, before the first step");
   if (!nft || !defs) throw SphError(SPH_ERR_ARG, "no floating bodies");
   if (nn_) throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase with floating bodies is not implemented");
+  if (C.symmetry) throw SphError(SPH_ERR_ARG, "Symmetry is not allowed with floating bodies.");  // JSph.cpp:1177
   std::vector<FtBody> b(nft);
   std::vector<float> massp(nft);
   unsigned begin = casenpb_;

@@ -205,6 +205,7 @@ struct RowCtx {
   int lxa, lxb;   // this lane's own 3-cell x range
   int xo;         // x origin of item-relative positions
   bool act;       // lane holds a p1
+  unsigned p1;    // the lane's p1 (Symmetry: its own image is not a neighbour)
 };
 
 }  // namespace sphx

@@ -142,7 +142,8 @@ class CaseRun:
                     case_posmax=list(c.case_posmax), pos_double=int(self.sv_pos_double), peri_mode=0,
                     visco_type=1, visco=float(np.float32(c.visco)),
                     viscoboundfactor=float(np.float32(c.viscoboundfactor)),
-                    gravity=[float(np.float32(g)) for g in c.gravity], mkbound=fb[0]["mk"], mkfluid=fl[0]["mk"])
+                    gravity=[float(np.float32(g)) for g in c.gravity], mkbound=fb[0]["mk"], mkfluid=fl[0]["mk"],
+                    symmetry=int(cd.get("symmetry", 0)))  # JPartDataHead::ConfigSymmetry (JSph.cpp:2391)
 
     def _save(self, cpart: int, step: int) -> dict:
         st = self.solver.stats()

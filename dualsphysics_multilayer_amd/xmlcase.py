@@ -341,6 +341,13 @@ class XmlCase:
             raise CaseError("Cell mode is not valid.")
         if self.tboundary == 2 and self.slipmode != 1:  # JSph.cpp:788
             raise CaseError("Only the slip mode velocity=0 is allowed with mDBC conditions.")
+        if self.symmetry:  # JSph.cpp:1174-1179
+            if self.data2d:
+                raise CaseError("Symmetry is not allowed with 2-D simulations.")
+            if self.floatings:
+                raise CaseError("Symmetry is not allowed with floating bodies.")
+            if self.tvisco != 1:
+                raise CaseError("Symmetry is only allowed with Artificial viscosity.")
         # -- particles (JPartsLoad4::LoadParticles) ------------------------------------
         self.partbegin = int(partbegin)
         if self.partbegin:
@@ -384,6 +391,8 @@ class XmlCase:
             rmin = [c - border for c in cmin]
             rmax = [c + border for c in cmax]
             dmin, dmax = self._domain.resize(rmin, rmax, self.data2d)
+            if self.symmetry:
+                dmin[1] = 0.0  # JSph::ResizeMapLimits (JSph.cpp:1386)
             self._map = (np.array(dmin), np.array(dmax))
         # JSph::CheckRhopLimits (JSph.cpp:2021-2030) is done by the core at creation.
         self._boundnormal = None
@@ -515,8 +524,7 @@ class XmlCase:
         self.rhopoutmin = p.num("RhopOutMin") if p.exists("RhopOutMin") else 700.0
         self.rhopoutmax = p.num("RhopOutMax") if p.exists("RhopOutMax") else 1300.0
         self.partsoutmax = p.num("PartsOutMax", True, 1.0)
-        if p.int("Symmetry", True, 0):
-            raise CaseError("Symmetry is not supported by this core.")
+        self.symmetry = p.int("Symmetry", True, 0) != 0  # JSph.cpp:714 (checks: JSph::ConfigBoundary)
         for k in ("XPeriodicIncY", "XPeriodicIncZ", "YPeriodicIncX", "YPeriodicIncZ", "ZPeriodicIncX",
                   "ZPeriodicIncY", "XYPeriodic", "XZPeriodic", "YZPeriodic"):
             if p.exists(k):
@@ -834,6 +842,7 @@ class XmlCase:
             phases=self.phases, relaxation_dt=self.relaxation_dt, shift_mode=self.shift_mode,
             shift_coef=self.shift_coef, shift_tfs=self.shift_tfs, data2d=int(self.data2d),
             data2d_posy=self.data2d_posy, dtallparticles=self.dtallparticles, dtfixed=self.dtfixed,
+            symmetry=int(self.symmetry),
         )
 
 

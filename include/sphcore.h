@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define SPH_ABI_VERSION 8
+#define SPH_ABI_VERSION 9
 
 typedef enum {
   SPH_OK = 0,
@@ -181,7 +181,10 @@ typedef struct SphCaseDef {
    * DtFixed>, the dt of every step (JDsFixedDt; a DtFixedFile table goes through
    * sph_solver_set_time_table) */
   int32_t dtallparticles;
-  int32_t pad_dt;
+  /* <parameter Symmetry> (JSph.cpp:714): the plane y = 0 mirrors the particles; their
+   * images near it are neighbours (JSphCpu.cpp:566-613, 671-796), MapRealPosMin.y = 0
+   * (JSph.cpp:1386), a particle crossing y = 0 is reflected (JSphCpu.cpp:1247) */
+  int32_t symmetry;
   double dtfixed;
 } SphCaseDef;
 
@@ -221,7 +224,7 @@ typedef struct SphConstants {
   int32_t kernel;
   float cub_a1, cub_a2, cub_aa, cub_a24, cub_c1, cub_d1, cub_c2, cub_od_wdeltap;
   int32_t pad4;
-  int32_t dtallparticles, pad5;     /* DtAllParticles                       */
+  int32_t dtallparticles, symmetry; /* DtAllParticles, Symmetry            */
   double dtfixed;                   /* DtFixed (0: variable dt)             */
 } SphConstants;
 

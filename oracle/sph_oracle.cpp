@@ -179,6 +179,9 @@ void Derive(const SphCaseDef& c, SphConstants& k) {
   k.relaxation_dt = float(c.relaxation_dt);
   if (k.rheology != SPH_RHEOLOGY_SINGLE || k.tvisco != SPH_VISCO_ARTIFICIAL || k.shift_mode != SPH_SHIFT_NONE)
     throw std::runtime_error("the oracle restates the single-phase artificial-viscosity path only");
+  // Symmetry (JSph.cpp:714, checks :1174-1179; MapRealPosMin.y = 0, :1386, set by the case)
+  k.symmetry = c.symmetry ? 1 : 0;
+  if (k.symmetry && k.data2d) throw std::runtime_error("Symmetry is not allowed with 2-D simulations.");
 }
 
 // EOS as the reference binary evaluates it: FunSphEos.h:37-39 calls the unqualified
@@ -653,20 +656,26 @@ class Solver {
       const f3 velp1{velrhop[p1].x, velrhop[p1].y, velrhop[p1].z};
       const float rhopp1 = velrhop[p1].w;
       const float pressp1 = press[p1];
+      const bool rsymp1 = (K.symmetry && posp1.y <= K.kernelsize);  // JSphCpu.cpp:671
       const NgSearch g = NgInit(dcell[p1], boundp2, dv);
       for (int z = g.zini; z < g.zfin; z++)
         for (int y = g.yini; y < g.yfin; y++) {
           unsigned pif, pfi;
           NgRange(y, z, g, dv, pif, pfi);
+          // Symmetry (JSphCpu.cpp:680-684, 709, 793-796): a p2 within the support radius
+          // whose y is within it too is visited a second time as its image across y = 0
+          bool rsym = false;
           for (unsigned p2 = pif; p2 < pfi; p2++) {
             const float drx = float(posp1.x - pos[p2].x);
-            const float dry = float(posp1.y - pos[p2].y);
+            float dry = float(posp1.y - pos[p2].y);
+            if (rsym) dry = float(posp1.y + pos[p2].y);
             const float drz = float(posp1.z - pos[p2].z);
             const float rr2 = drx * drx + dry * dry + drz * drz;
             if (rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO) {
               const float fac = KernelFac(K, rr2);
               const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
-              const f4 velrhop2 = velrhop[p2];
+              f4 velrhop2 = velrhop[p2];
+              if (rsym) velrhop2.y = -velrhop2.y;
               {  // Momentum (JSphCpu.cpp:712-716).
                 const float prs = (pressp1 + press[p2]) / (rhopp1 * velrhop2.w) +
                                   (K.kernel == SPH_KERNEL_CUBIC
@@ -707,6 +716,10 @@ class Solver {
                   acep1.x -= pi_visc * frx; acep1.y -= pi_visc * fry; acep1.z -= pi_visc * frz;
                 }
               }
+              rsym = (rsymp1 && !rsym && float(posp1.y - dry) <= K.kernelsize);
+              if (rsym) p2--;
+            } else {
+              rsym = false;
             }
           }
         }
@@ -734,25 +747,33 @@ class Solver {
       float visc = 0, arp1 = 0;
       const d3 posp1 = pos[p1];
       const f4 velrhop1 = velrhop[p1];
+      const bool rsymp1 = (K.symmetry && posp1.y <= K.kernelsize);  // JSphCpu.cpp:566
       const NgSearch g = NgInit(dcell[p1], false, dv);
       for (int z = g.zini; z < g.zfin; z++)
         for (int y = g.yini; y < g.yfin; y++) {
           unsigned pif, pfi;
           NgRange(y, z, g, dv, pif, pfi);
+          bool rsym = false;  // Symmetry (JSphCpu.cpp:576-580, 600, 610-613)
           for (unsigned p2 = pif; p2 < pfi; p2++) {
             const float drx = float(posp1.x - pos[p2].x);
-            const float dry = float(posp1.y - pos[p2].y);
+            float dry = float(posp1.y - pos[p2].y);
+            if (rsym) dry = float(posp1.y + pos[p2].y);
             const float drz = float(posp1.z - pos[p2].z);
             const float rr2 = drx * drx + dry * dry + drz * drz;
             if (rr2 <= K.kernelsize2 && rr2 >= ALMOSTZERO) {
               const float fac = KernelFac(K, rr2);
               const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
-              const f4 velrhop2 = velrhop[p2];
+              f4 velrhop2 = velrhop[p2];
+              if (rsym) velrhop2.y = -velrhop2.y;
               const float dvx = velrhop1.x - velrhop2.x, dvy = velrhop1.y - velrhop2.y, dvz = velrhop1.z - velrhop2.z;
               arp1 += massp2 * (dvx * frx + dvy * fry + dvz * frz) * (velrhop1.w / velrhop2.w);
               const float dot = drx * dvx + dry * dvy + drz * dvz;
               const float dot_rr2 = dot / (rr2 + K.eta2);
               visc = std::max(dot_rr2, visc);
+              rsym = (rsymp1 && !rsym && float(posp1.y - dry) <= K.kernelsize);
+              if (rsym) p2--;
+            } else {
+              rsym = false;
             }
           }
         }
@@ -908,10 +929,11 @@ class Solver {
     return dt;
   }
 
-  // JSphCpu::UpdatePos (JSphCpu.cpp:1240-1293), no periodic / symmetry.
+  // JSphCpu::UpdatePos (JSphCpu.cpp:1240-1293), no periodic.
   void UpdatePos(d3 rpos, double movx, double movy, double movz, bool outrhop, unsigned p, std::vector<d3>& posv) {
     const bool outmove = (std::fabs(float(movx)) > K.movlimit || std::fabs(float(movy)) > K.movlimit || std::fabs(float(movz)) > K.movlimit);
     rpos.x += movx; rpos.y += movy; rpos.z += movz;
+    if (K.symmetry && rpos.y < 0) rpos.y = -rpos.y;  // JSphCpu.cpp:1247
     const double dx = rpos.x - K.map_realposmin[0], dy = rpos.y - K.map_realposmin[1], dz = rpos.z - K.map_realposmin[2];
     const bool out = (dx != dx || dy != dy || dz != dz || dx < 0 || dy < 0 || dz < 0 ||
                       dx >= K.map_realsize[0] || dy >= K.map_realsize[1] || dz >= K.map_realsize[2]);

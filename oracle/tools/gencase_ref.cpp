@@ -10,7 +10,8 @@
 // test checks that both produce the same particles bit for bit.
 //
 // usage: gencase_ref <dp> <outdir> <step:1=Verlet|2=Symplectic> <ddt:0..3> [timemax] [casename]
-//                    [boundary:1=DBC|2=mDBC] [dim:3|2]
+//                    [boundary:1=DBC|2=mDBC] [dim:3|2] [viscotreatment] [visco] [shifting] [shiftcoef]
+//                    [shifttfs] [kernel] [sym:0|1]
 //
 // With boundary=2 the case also gets <casename>_Normals.nbi4, written through the
 // reference's own JPartNormalData (JPartNormalData.cpp:178-207), as GenCase would: the
@@ -29,7 +30,7 @@
 int main(int argc, char** argv) {
   if (argc < 5) {
     fprintf(stderr, "usage: %s dp outdir step ddt [timemax] [casename] [boundary] [dim] [viscotreatment] [visco] "
-                    "[shifting] [shiftcoef] [shifttfs] [kernel]\n", argv[0]);
+                    "[shifting] [shiftcoef] [shifttfs] [kernel] [sym]\n", argv[0]);
     return 1;
   }
   const double dp = atof(argv[1]);
@@ -51,6 +52,9 @@ int main(int argc, char** argv) {
   const std::string shiftcoef = (argc > 12 ? argv[12] : "-2");
   const std::string shifttfs = (argc > 13 ? argv[13] : "0");
   const int kernel = (argc > 14 ? atoi(argv[14]) : 2);  // 1 Cubic spline, 2 Wendland
+  // sym 1: <parameter Symmetry> (JSph.cpp:714) on the half tank y >= 0: no y = 0 wall, the
+  // fluid from y = 0 (the plane y = 0 mirrors the particles)
+  const bool sym = (argc > 15 ? atoi(argv[15]) : 0) != 0;
 
   // 3-D: tank 1.6 x 0.67 x 0.4 (walls: bottom, x=0, x=L, y=0, y=W); water 0.4 x 0.67 x 0.3.
   const int nx = int(std::round((d2 ? 4.0 : 1.6) / dp)), ny = d2 ? 0 : int(std::round(0.67 / dp));
@@ -61,16 +65,16 @@ int main(int argc, char** argv) {
   for (int k = 0; k <= nz; k++)
     for (int j = 0; j <= ny; j++)
       for (int i = 0; i <= nx; i++)
-        if (k == 0 || i == 0 || i == nx || (!d2 && (j == 0 || j == ny))) {
+        if (k == 0 || i == 0 || i == nx || (!d2 && ((j == 0 && !sym) || j == ny))) {
           pos.push_back(TDouble3(i * dp, j * dp, k * dp));
           const double hd = dp * 0.5;
           // 2-D: the particles sit at y = 0 and have no y walls (no y normal)
-          const double ny_ = d2 ? 0. : (j == 0 ? hd : (j == ny ? -hd : 0.));
+          const double ny_ = d2 ? 0. : (j == 0 ? (sym ? 0. : hd) : (j == ny ? -hd : 0.));
           nor.push_back(TDouble3(i == 0 ? hd : (i == nx ? -hd : 0.), ny_, k == 0 ? hd : 0.));
         }
   const unsigned nb = unsigned(pos.size());
   for (int k = 1; k <= mz; k++)
-    for (int j = (d2 ? 0 : 1); j < (d2 ? 1 : my); j++)
+    for (int j = (d2 || sym ? 0 : 1); j < (d2 ? 1 : my); j++)
       for (int i = 1; i <= mx; i++) pos.push_back(TDouble3(i * dp, j * dp, k * dp));
   const unsigned np = unsigned(pos.size()), nf = np - nb;
 
@@ -132,6 +136,7 @@ int main(int argc, char** argv) {
   }
   par("Boundary", std::to_string(boundary));
   if (boundary == 2) par("SlipMode", "1");
+  if (sym) par("Symmetry", "1");
   par("RigidAlgorithm", "1");
   par("CoefDtMin", "0.05");
   par("DtIni", "0");

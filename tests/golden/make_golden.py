@@ -55,6 +55,14 @@ CASES = {
     "verlet_ddt2_cubic_2d_dp0.02": (0.02, 1, 2, 100, (1, 10, 100), 1, ("-cubic",), 2),
 }
 
+# Symmetry (<parameter Symmetry>, JSph.cpp:714): the half tank y >= 0 mirrored across y = 0
+# (gencase_ref sym 1: no y = 0 wall, fluid from y = 0); the npz carries symmetry = 1.
+# name: (dp, step, ddt, nsteps, kept steps, boundary)
+SYM_CASES = {
+    "verlet_ddt2_sym_dp0.02": (0.02, 1, 2, 100, (1, 10, 100), 1),
+    "symplectic_ddt1_sym_mdbc_dp0.025": (0.025, 2, 1, 60, (1, 20, 60), 2),
+}
+
 
 # Single-phase Laminar+SPS viscosity (ViscoTreatment 2; kinematic viscosity 1e-6 m2/s,
 # JSphCpu.cpp:765-809, ComputeSpsTau :929-954) and shifting (JSphShifting, modes 1-3).
@@ -114,11 +122,14 @@ def load_dump(fn):
     return t, idp.copy(), pos.copy(), vel.copy(), rho.copy()
 
 
-def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=(), dim=3, noise=False):
+def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=(), dim=3, noise=False, sym=False):
     tmp = tempfile.mkdtemp(prefix="golden_")
     try:
-        subprocess.check_call([os.path.join(REF, "gencase_ref"), repr(dp), tmp, str(step), str(ddt), "1.5",
-                               "CaseDambreak", str(boundary), str(dim)], stdout=subprocess.DEVNULL)
+        gen = [os.path.join(REF, "gencase_ref"), repr(dp), tmp, str(step), str(ddt), "1.5", "CaseDambreak",
+               str(boundary), str(dim)]
+        if sym:  # artificial viscosity 0.1, no shifting, Wendland, Symmetry
+            gen += ["1", "0.1", "0", "-2", "0", "2", "1"]
+        subprocess.check_call(gen, stdout=subprocess.DEVNULL)
         out = os.path.join(tmp, "out")
         for exe, o in (("DualSPHysics5.2CPU_ref", out), ("DualSPHysics5.2CPU_strict", out + "_strict")):
             if o != out and not noise:
@@ -159,6 +170,8 @@ def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=(), dim=3, noise=F
         arrays["meta"] = np.array(m, np.float64)
         if "-cubic" in extra:
             arrays["kernel"] = np.int32(1)
+        if sym:
+            arrays["symmetry"] = np.int32(1)
         np.savez_compressed(os.path.join(ROOT, "tests", "golden", name + ".npz"), **arrays)
         print(name, "ok", os.path.getsize(os.path.join(ROOT, "tests", "golden", name + ".npz")))
     finally:
@@ -294,6 +307,10 @@ if __name__ == "__main__":
         if a.only and a.only != name:
             continue
         make(name, *spec, **({"noise": True} if a.noise else {}))
+    for name, spec in SYM_CASES.items():
+        if a.only and a.only != name:
+            continue
+        make(name, *spec, noise=a.noise, sym=True)
     for name, spec in EXT_CASES.items():
         if a.only and a.only != name:
             continue
