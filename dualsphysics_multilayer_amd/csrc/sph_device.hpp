@@ -89,6 +89,7 @@ struct KConst {
   // (JDsViscoInput: Visco(t), evaluated at every step's TimeStep, JSphCpuSingle.cpp:1092)
   int dtallp;
   int symmetry;  // Symmetry: images across y = 0 of the p2 near it (JSphCpu.cpp:566-613, 671-796)
+  int nftbodies; // floating bodies (their particle masses: the NN kernel's fourth phase-table row)
   int dtfix_n;
   double dtfix_val;
   const double* dtfix_t;

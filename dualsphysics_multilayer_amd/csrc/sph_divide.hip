@@ -15,6 +15,9 @@
 //     domain are never neighbours of fluid, so the interaction order is unchanged
 //     (checked on the oracle: tests/test_oracle_celldomfixed.py).  This removes the
 //     per-step DtoH read of the cell limits (cudiv::LimitsCell, 2 syncs per divide).
+#include <cstring>
+
+#include "sph_items.hpp"
 #include "sph_kernels.hpp"
 
 namespace sphx {
@@ -1128,8 +1131,18 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
 // One tile per block.  Loads in three batches (one memory latency each): the particle
 // states and the classification words, the new positions, then the stores.  Block 0
 // also clears the super-tile sums and the far count for the next divide.
+// With an item build (ib.nblocks > 0) the launch has ib.nblocks more blocks after the tiles:
+// they run the item COUNT pass (sph_items.hpp) on the new begincell beside the push — the
+// push is HBM-bound, the row walks latency-bound — and the scan and write passes follow the
+// launch (launch_items_scan_write).  cfg2 1M divide phase: see DESIGN.md §4.
 template <bool WITHM1, bool WITHPRE, bool WITHTAU>
-__global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, GatherArgs a, IncDivScratch s) {
+__global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, GatherArgs a, IncDivScratch s,
+                                                  ItemBuild ib) {
+  if (blockIdx.x >= s.nb1) {
+    extern __shared__ unsigned char push_items_smem[];
+    items_pass_block<false>(ib, blockIdx.x - s.nb1, push_items_smem);
+    return;
+  }
   const unsigned nd = sc->ndiv, n = sc->np, npb = sc->npb, nold = nd - s.napp;
   const unsigned t = blockIdx.x;
   const unsigned i0 = t * INC_TILE + threadIdx.x;
@@ -1219,7 +1232,7 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
                        bool withm1, bool withpre, const KConst& K, const double dom_posmin[3], float4* poscell,
                        float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
                        IncDivScratch& s, SortScratch& srt, unsigned keybits, const float4* phase_eos,
-                       const SlabFaces* faces, unsigned ngl, unsigned ngr, hipEvent_t ev_boxes) {
+                       const SlabFaces* faces, unsigned ngl, unsigned ngr, const ItemBuild* items) {
   s.gen++;
   const int usey = g.ncy > 1, usez = g.ncz > 1;
   const unsigned omax = 1u + (usey ? unsigned(g.ncx) : 0u) + (usez ? g.nsheet : 0u);
@@ -1248,8 +1261,6 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
     }
   }
   hipLaunchKernelGGL(k_inc_boxes, dim3(s.nb2), dim3(IB_BS), 0, stm, sc, g, begincell_old, begincell_new, s, omax);
-  // the new begincell is final here: work that needs only it may start beside the push
-  if (ev_boxes) (void)hipEventRecord(ev_boxes, stm);
   GatherArgs a;
   a.phase_eos = phase_eos;
   a.vfirst = ~0u;
@@ -1274,8 +1285,14 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
   a.dcc = K.domcellcode;
   a.withm1 = withm1;
   a.withpre = withpre;
-  const unsigned nb = s.nb1;  // one tile per block
-#define SPH_K_INC_PUSH(M1, PRE, TAU) hipLaunchKernelGGL((k_inc_push<M1, PRE, TAU>), dim3(nb), dim3(256), 0, stm, sc, a, s)
+  // one tile per block, then the item count blocks (if any)
+  ItemBuild ib;
+  std::memset(&ib, 0, sizeof(ib));
+  if (items) ib = *items;
+  const unsigned nb = s.nb1 + (items ? ib.nblocks : 0u);
+  const unsigned lds = items ? ib.lds : 0u;
+#define SPH_K_INC_PUSH(M1, PRE, TAU) \
+  hipLaunchKernelGGL((k_inc_push<M1, PRE, TAU>), dim3(nb), dim3(256), lds, stm, sc, a, s, ib)
 #define SPH_K_INC_PUSH_T(M1, PRE) \
   if (a.src.tau) SPH_K_INC_PUSH(M1, PRE, true); \
   else SPH_K_INC_PUSH(M1, PRE, false)
@@ -1285,6 +1302,7 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
   else { SPH_K_INC_PUSH_T(false, false); }
 #undef SPH_K_INC_PUSH_T
 #undef SPH_K_INC_PUSH
+  if (items) launch_items_scan_write(stm, ib);
 }
 
 // ---------------------------------------------------------------------------------

@@ -280,30 +280,36 @@ __device__ __forceinline__ void ext_drain4(const KConst& K, const ExtP1& p, unsi
   }
 }
 
-// The 9 rows of one kind: MIRRORED drains point-mirrored row pairs as one set (order-free
-// sums), else rows in the reference's order (z-major, y, p2 ascending) for the passes
-// whose shifting cut-off makes the sums order-dependent.
-template <int TVISCO, int TD, bool SHIFT, bool FT, int KIND>
+// The (2S+1)^2 rows of one kind (S = scelldiv: 3x3 rows of cells of 2h, or 5x5 rows of
+// half-cells, JCellSearch_inline.h:38-44): MIRRORED drains point-mirrored row pairs as one
+// set (order-free sums), else rows in the reference's order (z-major, y, p2 ascending) for
+// the passes whose shifting cut-off makes the sums order-dependent.
+template <int TVISCO, int TD, bool SHIFT, bool FT, int KIND, int S>
 __device__ __forceinline__ void ext_pass(const KConst& K, const ExtArgs& E, const DivGrid& g, const RowCtx& rc,
                                          const ExtP1& p, float thr, const unsigned* __restrict__ bc, bool mirrored,
                                          float visco, float4* __restrict__ sA, float4* __restrict__ sB,
                                          float4* __restrict__ sC, float4* __restrict__ sD, ExtAcc& a) {
   constexpr int TCAPX = ExtCap<TVISCO>::v;
   constexpr bool WT = TVISCO == 2 && KIND != 2;
+  constexpr int NR = 2 * S + 1;           // rows per axis
+  constexpr int NPAIR = (NR * NR - 1) / 2;  // mirrored row pairs; the own row after them
   const unsigned cellinit = (KIND == 1 ? 0u : g.boxfluid);
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
-  const int nunits = mirrored ? 5 : 9;
+  const int nunits = mirrored ? NPAIR + 1 : NR * NR;
   for (int u = 0; u < nunits; u++) {
-    int dza, dya;
-    bool paired;
+    int dza = 0, dya = 0;
+    bool paired = false;
     if (mirrored) {
-      dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
-      dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
-      paired = u < 4;
+      paired = u < NPAIR;
+      if (S == 1) {
+        dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
+        dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
+      } else if (paired) {
+        half_row(u, dya, dza);
+      }
     } else {
-      dza = u / 3 - 1;
-      dya = u % 3 - 1;
-      paired = false;
+      dza = u / NR - S;
+      dya = u % NR - S;
     }
     unsigned rs[2] = {0, 0}, re[2] = {0, 0}, ls[2] = {0, 0}, le[2] = {0, 0};
 #pragma unroll
@@ -358,7 +364,7 @@ __device__ __forceinline__ void ext_pass(const KConst& K, const ExtArgs& E, cons
   }
 }
 
-template <int TVISCO, int TD, bool SHIFT, bool FT>
+template <int TVISCO, int TD, bool SHIFT, bool FT, int S>
 __global__ __launch_bounds__(TB) void k_fluid_ext(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
                                                   unsigned* __restrict__ qctr, ExtArgs E,
                                                   const unsigned* __restrict__ bc, DivGrid g, KConst K,
@@ -401,11 +407,11 @@ __global__ __launch_bounds__(TB) void k_fluid_ext(DevScalars* __restrict__ sc, c
       const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
       const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);
       const int xo = (ia + ib + 1) >> 1;
-      const int xa = max(ia - 1, 0), xb = min(ib + 1, g.ncx - 1);
+      const int xa = max(ia - S, 0), xb = min(ib + S, g.ncx - 1);
       if (bitem) {  // no fluid within reach: ar = 0 (PreInteraction reset), nothing else
         bool any = false;
-        for (int z = max(cz - 1, 0); z <= min(cz + 1, g.ncz - 1); z++)
-          for (int y = max(cy - 1, 0); y <= min(cy + 1, g.ncy - 1); y++) {
+        for (int z = max(cz - S, 0); z <= min(cz + S, g.ncz - 1); z++)
+          for (int y = max(cy - S, 0); y <= min(cy + S, g.ncy - 1); y++) {
             const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
             any |= bc[rowbase + xa] != bc[rowbase + xb + 1];
           }
@@ -443,12 +449,12 @@ __global__ __launch_bounds__(TB) void k_fluid_ext(DevScalars* __restrict__ sc, c
         p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
         p.press = 0.f;
       }
-      const int lxa = max(cx1 - 1, 0), lxb = min(cx1 + 1, g.ncx - 1);
+      const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
       const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
-      const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act};
+      const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act, p1};
       if (bitem) {
         ExtAcc f = {};
-        ext_pass<TVISCO, TD, SHIFT, FT, 2>(K, E, g, rc, p, thr, bc, true, 0.f, sA, sB, sC, sD, f);
+        ext_pass<TVISCO, TD, SHIFT, FT, 2, S>(K, E, g, rc, p, thr, bc, true, 0.f, sA, sB, sC, sD, f);
         if (act) {
           arace[p1] = make_float4(0.f, 0.f, 0.f, (f.ar != 0.f || f.visc != 0.f) ? 0.f + f.ar : 0.f);
           viscmax = fmaxf(viscmax, f.visc);
@@ -464,13 +470,13 @@ __global__ __launch_bounds__(TB) void k_fluid_ext(DevScalars* __restrict__ sc, c
         if (TD) f.delta = FLT_MAX;
       }
       const float visco = K.visco_n ? sc->visco : K.visco;  // ViscoTime (k_dt) or the case's
-      ext_pass<TVISCO, TD, SHIFT, FT, 0>(K, E, g, rc, p, thr, bc, !ordf, visco, sA, sB, sC, sD, f);
+      ext_pass<TVISCO, TD, SHIFT, FT, 0, S>(K, E, g, rc, p, thr, bc, !ordf, visco, sA, sB, sC, sD, f);
       b.sx = f.sx;
       b.sy = f.sy;
       b.sz = f.sz;
       b.sw = f.sw;
       if (p.ftp1 && TD) b.delta = FLT_MAX;
-      ext_pass<TVISCO, TD, SHIFT, FT, 1>(K, E, g, rc, p, thr, bc, !ordb, K.visco_n ? visco * K.viscobf : K.viscobound,
+      ext_pass<TVISCO, TD, SHIFT, FT, 1, S>(K, E, g, rc, p, thr, bc, !ordb, K.visco_n ? visco * K.viscobf : K.viscobound,
                                          sA, sB, sC, sD, b);
       if (act) {
         // the two passes' stores (:800-818); with shifting both always store
@@ -527,9 +533,14 @@ void launch_fluid_ext(hipStream_t stm, unsigned nblocks, DevScalars* sc, const u
                       float4* arace, float4* shiftpos, float4* taunew, bool shiftstore) {
   const ExtArgs E{poscell, velrhop, press, code, ftmassp, tau};
   const bool shift = K.shiftmode != 0, ft = ftmassp != nullptr;
+  // CellMode: cells of 2h (S = 1) or of h (S = 2)
 #define SPH_EXT(TV, TD, SH, FT)                                                                                  \
-  hipLaunchKernelGGL((k_fluid_ext<TV, TD, SH, FT>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, E, begincell, \
-                     g, K, arace, shiftpos, taunew, int(shiftstore))
+  if (K.scelldiv == 2)                                                                                           \
+    hipLaunchKernelGGL((k_fluid_ext<TV, TD, SH, FT, 2>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, E,     \
+                       begincell, g, K, arace, shiftpos, taunew, int(shiftstore));                               \
+  else                                                                                                           \
+    hipLaunchKernelGGL((k_fluid_ext<TV, TD, SH, FT, 1>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, E,     \
+                       begincell, g, K, arace, shiftpos, taunew, int(shiftstore))
 #define SPH_EXT_TD(TV, SH, FT)             \
   switch (K.tdensity) {                    \
     case 0: SPH_EXT(TV, 0, SH, FT); break; \

@@ -23,238 +23,52 @@
 //    only; parity tests hold it to the reference's noise floor.
 #include <cfloat>
 
+#include "sph_items.hpp"
 #include "sph_tiled.hpp"
 
 namespace sphx {
 
 // ------------------------------------------------------------------------------------
-// Item list (per divide).  Rows [0,nrows) are fluid rows (fluid p1), rows
-// [nrows,2*nrows) bound rows (bound p1, DBC).  An item is a run of TB consecutive
-// particles of one row (the row's last item shorter), cut earlier only where it would
-// span more than TMAXCELLS x-cells; items may start and end inside a cell.  Full items
-// keep both waves of a block busy (cell-aligned items averaged 103 of 128 lanes at 1M)
-// and make the lanes' candidate counts more alike.  One wave per row copies the row's
-// cell begin offsets to LDS, then lane 0 walks the items; the count and write passes
-// run the same walk, so the list is deterministic and in spatial (z, y, x) order, fluid
-// items first.
-constexpr int ROWCELLS_LDS = 1024;
-
-struct ItemRanges {
-  int x[6];  // column ranges [x[2k], x[2k+1]) of p1 (empty when equal): list A = range 0 (and
-             // 1, 2 with one list), list B = ranges 1, 2
-  int nl;    // lists: 1 or 2
-};
-constexpr int IR_WAVES = 4;  // rows per block: one wave each
-
-// One wave walks one (y,z) row of one kind (fluid or bound p1): its cell begin offsets to LDS,
-// then lane 0 emits the items of each column range of each list.  WRITE = false counts them
-// (counts[list][row]), true writes them at the scanned offsets.
+// Item list (per divide): the passes of sph_items.hpp as kernels.
 template <bool WRITE>
-__global__ __launch_bounds__(64 * IR_WAVES) void k_items_rows(const unsigned* __restrict__ bc, DivGrid g, int tmaxc,
-                                                              unsigned* __restrict__ counts,
-                                                              uint4* __restrict__ items, ItemRanges xr) {
-  __shared__ unsigned s_pre[IR_WAVES][ROWCELLS_LDS + 1];  // begin offset of every cell of the row, + row end
-  __shared__ unsigned short s_nz[IR_WAVES][ROWCELLS_LDS + 1];  // first non-empty cell >= x in the range
-  const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz), nrows2 = 2u * nrows;
-  const unsigned w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const unsigned r = blockIdx.x * IR_WAVES + w;
-  if (r >= nrows2) return;  // whole waves (no block-wide barrier below)
-  unsigned* pre = s_pre[w];
-  unsigned short* nzfrom = s_nz[w];
-  const bool bound = r >= nrows;
-  const unsigned rr = bound ? r - nrows : r;
-  const unsigned y = rr % unsigned(g.ncy), z = rr / unsigned(g.ncy);
-  const unsigned rowbase = (bound ? 0u : g.boxfluid) + z * g.nsheet + y * unsigned(g.ncx);
-  const int ncx = g.ncx;
-  {  // a row without particles in its ranges (most rows of the air above the water and of
-     // the boundary): no items, no staging
-    int xlo = ncx, xhi = 0;
-    for (int k = 0; k < 3; k++)
-      if (xr.x[2 * k] < xr.x[2 * k + 1]) {
-        xlo = min(xlo, xr.x[2 * k]);
-        xhi = max(xhi, xr.x[2 * k + 1]);
-      }
-    if (xlo >= xhi || bc[rowbase + xlo] == bc[rowbase + xhi]) {
-      if (!WRITE && lane == 0)
-        for (int list = 0; list < xr.nl; list++) counts[list * nrows2 + r] = 0u;
-      return;
-    }
-  }
-  const bool lds = ncx <= ROWCELLS_LDS;
-  if (lds) {
-    for (int x = int(lane); x <= ncx; x += 64) pre[x] = bc[rowbase + x];
-    __builtin_amdgcn_wave_barrier();
-  }
-  for (int list = 0; list < xr.nl; list++) {
-    uint4* out = WRITE ? items + counts[list * nrows2 + r] : nullptr;
-    unsigned nitems = 0;
-    auto emit = [&](int a, int e, unsigned p, unsigned q) {
-      if (WRITE)
-        out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(e) << 16), p, q);
-      nitems++;
-    };
-    // p1 only in owned columns (slab ghosts are neighbours, never p1); each range walked on
-    // its own, so no item crosses from one to the next
-    for (int rg = (list ? 1 : 0); rg < (xr.nl == 2 && list == 0 ? 1 : 3); rg++) {
-      const int xbeg = xr.x[2 * rg], xend = xr.x[2 * rg + 1];  // uniform over the wave
-      if (xbeg >= xend) continue;
-      if (!lds) {  // very long rows: the same walk on global memory, cell by cell
-        if (lane == 0) {
-          auto PRE = [&](int x) -> unsigned { return bc[rowbase + x]; };
-          unsigned p = PRE(xbeg);
-          const unsigned pend = PRE(xend);
-          int c = xbeg;
-          while (p < pend) {
-            while (PRE(c + 1) <= p) c++;
-            const unsigned q = min(min(p + unsigned(TB), pend), PRE(min(c + tmaxc, xend)));
-            int e = c;
-            while (PRE(e + 1) < q) e++;
-            emit(c, e, p, q);
-            p = q;
-            c = e;
-          }
-        }
-        continue;
-      }
-      // first non-empty cell of the range at or after x: lane-local blocks, then a wave suffix-min
-      const int per = (ncx + 63) / 64, x0 = int(lane) * per, x1 = min(x0 + per, ncx);
-      int nz = xend;
-      for (int x = x1 - 1; x >= x0; x--) {
-        if (x >= xbeg && x < xend && pre[x + 1] > pre[x]) nz = x;
-        nzfrom[x] = (unsigned short)nz;
-      }
-      int suf = nz;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int v = __shfl_down(suf, off, 64);
-        if (int(lane) + off < 64) suf = min(suf, v);
-      }
-      const int later = __shfl_down(suf, 1, 64);
-      const int carry = int(lane) < 63 ? later : xend;
-      for (int x = x0; x < x1; x++)
-        if (int(nzfrom[x]) == xend) nzfrom[x] = (unsigned short)carry;
-      if (lane == 63) nzfrom[ncx] = (unsigned short)xend;
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) {
-        // Walk the items: the cell holding p is known (c), the cell holding q-1 is at most
-        // TMAXCELLS-1 cells further, an item ending at a cell end jumps to the next non-empty.
-        // The five offsets pre[c..c+4] of an item are independent LDS reads (one latency);
-        // the cell holding q-1 is c + #{k = 1..3 : pre[c+k] <= q-1}.
-        static_assert(TMAXCELLS == 4, "the walk reads pre[c..c+4]");
-        const unsigned pend = pre[xend];
-        int c = nzfrom[xbeg];
-        unsigned p = c < xend ? pre[c] : pend;
-        if (tmaxc != TMAXCELLS) {  // CellMode=half: longer items, the cell holding q-1 by a short scan
-          while (p < pend) {
-            const unsigned q = min(min(p + unsigned(TB), pend), pre[min(c + tmaxc, xend)]);
-            int e = c;
-            while (pre[e + 1] <= q - 1) e++;
-            emit(c, e, p, q);
-            p = q;
-            c = pre[e + 1] == q ? int(nzfrom[e + 1]) : e;
-          }
-        } else {
-          while (p < pend) {
-            const unsigned p1 = pre[min(c + 1, xend)], p2 = pre[min(c + 2, xend)], p3 = pre[min(c + 3, xend)];
-            const unsigned p4 = pre[min(c + 4, xend)];
-            const unsigned q = min(min(p + unsigned(TB), pend), p4);
-            const int e = c + int(p1 <= q - 1) + int(p2 <= q - 1) + int(p3 <= q - 1);
-            emit(c, e, p, q);
-            p = q;
-            const unsigned pe1 = e + 1 - c == 1 ? p1 : e + 1 - c == 2 ? p2 : e + 1 - c == 3 ? p3 : p4;
-            c = pe1 == q ? int(nzfrom[e + 1]) : e;
-          }
-        }
-      }
-      __builtin_amdgcn_wave_barrier();  // nzfrom is rebuilt for the next range
-    }
-    if (!WRITE && lane == 0) counts[list * nrows2 + r] = nitems;
-  }
+__global__ __launch_bounds__(64 * IR_WAVES) void k_items_pass(ItemBuild b) {
+  extern __shared__ unsigned char items_smem[];
+  items_pass_block<WRITE>(b, blockIdx.x, items_smem);
 }
 
-// Exclusive scan of the per-row item counts of the lists (one block, tiles of 8192 through
-// LDS) -> item offsets; each list's counts {all, bound, first item} into its counter block
-// (qctr[QCTR_NITEMS...]) and its per-XCD work queues zeroed for the next interaction.
-constexpr int IS_BS = 1024, IS_PT = 8, IS_TILE = IS_BS * IS_PT;
-__global__ __launch_bounds__(IS_BS) void k_items_scan(unsigned* __restrict__ counts, unsigned nrows2, int nl,
-                                                      unsigned* __restrict__ qa, unsigned* __restrict__ qb) {
-  __shared__ unsigned v[IS_TILE];
-  __shared__ unsigned wsum[IS_BS / 64];
-  __shared__ unsigned carry, mark[4];
-  if (threadIdx.x < 8) {  // the interaction's item queues start over
-    qa[threadIdx.x * QSTRIDE] = 0u;
-    if (nl == 2) qb[threadIdx.x * QSTRIDE] = 0u;
-  }
-  const unsigned n = unsigned(nl) * nrows2, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const unsigned nrows = nrows2 / 2;
-  if (threadIdx.x == 0) carry = 0;
-  for (unsigned t0 = 0; t0 < n; t0 += IS_TILE) {
-#pragma unroll
-    for (int k = 0; k < IS_PT; k++) {
-      const unsigned i = t0 + k * IS_BS + threadIdx.x;
-      v[k * IS_BS + threadIdx.x] = i < n ? counts[i] : 0u;
-    }
-    __syncthreads();
-    unsigned x[IS_PT], sum = 0;
-#pragma unroll
-    for (int k = 0; k < IS_PT; k++) {
-      x[k] = sum;
-      sum += v[threadIdx.x * IS_PT + k];
-    }
-    unsigned inc = sum;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const unsigned yv = __shfl_up(inc, off, 64);
-      if (lane >= unsigned(off)) inc += yv;
-    }
-    if (lane == 63) wsum[w] = inc;
-    __syncthreads();
-    unsigned before = carry;
-    for (unsigned q = 0; q < w; q++) before += wsum[q];
-    before += inc - sum;
-#pragma unroll
-    for (int k = 0; k < IS_PT; k++) {
-      const unsigned i = t0 + threadIdx.x * IS_PT + k;
-      // the offsets where each list's bound rows and the second list begin
-      if (i == nrows) mark[0] = before + x[k];
-      if (i == nrows2) mark[1] = before + x[k];
-      if (i == nrows2 + nrows) mark[2] = before + x[k];
-      v[threadIdx.x * IS_PT + k] = before + x[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < IS_PT; k++) {
-      const unsigned i = t0 + k * IS_BS + threadIdx.x;
-      if (i < n) counts[i] = v[k * IS_BS + threadIdx.x];
-    }
-    if (threadIdx.x == IS_BS - 1) carry = before + sum;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const unsigned tot = carry, na = nl == 2 ? mark[1] : tot;
-    qa[QCTR_NITEMS] = na;
-    qa[QCTR_NITEMS + 1] = na - mark[0];  // the bound rows' items: the list's tail (ItemGroups)
-    qa[QCTR_NITEMS + 2] = 0u;
-    if (nl == 2) {
-      qb[QCTR_NITEMS] = tot - na;
-      qb[QCTR_NITEMS + 1] = tot - mark[2];
-      qb[QCTR_NITEMS + 2] = na;  // the second list follows the first in the item array
-    }
-  }
+__global__ __launch_bounds__(1024) void k_items_scan(ItemBuild b) {
+  __shared__ unsigned s[1024 / 64 + 4];
+  items_scan(b, s);
 }
 
-void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
-                  uint4* items, unsigned* qctr, int scelldiv, const int* xr, unsigned* qctr2) {
-  (void)sc;
-  const int tmaxc = scelldiv == 1 ? TMAXCELLS : TMAXCELLS_HALF;
-  const unsigned nrows2 = 2u * unsigned(g.ncy) * unsigned(g.ncz);
-  ItemRanges r = {{g.xown0, g.xown1, 0, 0, 0, 0}, qctr2 ? 2 : 1};
+ItemBuild make_item_build(const unsigned* begincell, DivGrid g, unsigned* rowtmp, uint4* items, unsigned* qctr,
+                          int scelldiv, const int* xr, unsigned* qctr2) {
+  ItemBuild b;
+  b.bc = begincell;
+  b.g = g;
+  b.tmaxc = scelldiv == 1 ? TMAXCELLS : TMAXCELLS_HALF;
+  b.xr = {{g.xown0, g.xown1, 0, 0, 0, 0}, qctr2 ? 2 : 1};
   if (xr)
-    for (int k = 0; k < 6; k++) r.x[k] = xr[k];
-  const unsigned nb = (nrows2 + IR_WAVES - 1) / IR_WAVES;
-  hipLaunchKernelGGL(k_items_rows<false>, dim3(nb), dim3(64 * IR_WAVES), 0, stm, begincell, g, tmaxc, rowtmp, nullptr, r);
-  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(IS_BS), 0, stm, rowtmp, nrows2, r.nl, qctr, qctr2);
-  hipLaunchKernelGGL(k_items_rows<true>, dim3(nb), dim3(64 * IR_WAVES), 0, stm, begincell, g, tmaxc, rowtmp, items, r);
+    for (int k = 0; k < 6; k++) b.xr.x[k] = xr[k];
+  b.nrows2 = 2u * unsigned(g.ncy) * unsigned(g.ncz);
+  b.counts = rowtmp;
+  b.items = items;
+  b.qa = qctr;
+  b.qb = qctr2;
+  b.nblocks = (b.nrows2 + IR_WAVES - 1) / IR_WAVES;
+  const unsigned L = b.rowlds();
+  b.lds = ((IR_WAVES * L * unsigned(sizeof(unsigned) + sizeof(unsigned short)) + 15u) / 16u) * 16u;
+  return b;
+}
+
+void launch_items_scan_write(hipStream_t stm, const ItemBuild& b) {
+  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, b);
+  hipLaunchKernelGGL(k_items_pass<true>, dim3(b.nblocks), dim3(64 * IR_WAVES), b.lds, stm, b);
+}
+
+void launch_items(hipStream_t stm, const ItemBuild& b) {
+  hipLaunchKernelGGL(k_items_pass<false>, dim3(b.nblocks), dim3(64 * IR_WAVES), b.lds, stm, b);
+  launch_items_scan_write(stm, b);
 }
 
 // ------------------------------------------------------------------------------------
@@ -722,18 +536,6 @@ __device__ __forceinline__ TAcc run_pass(const KConst& K, const DivGrid& g, cons
     }
   }
   return finish<TDENSITY, MODE, FT>(K, acc, p, Q);
-}
-
-// i-th of the 12 "lower" rows of the 5x5 CellMode=half stencil (dz < 0, or dz = 0 and
-// dy < 0); the other 12 are their point mirrors, the 25th the item's own row.
-__device__ __forceinline__ void half_row(int i, int& dy, int& dz) {
-  if (i < 10) {
-    dz = -2 + i / 5;
-    dy = -2 + i % 5;
-  } else {
-    dz = 0;
-    dy = i - 12;
-  }
 }
 
 // CellMode=half pass: units of HALF_LPU lower rows + their mirrors (2 or 4 rows staged as

@@ -104,6 +104,7 @@ __device__ __forceinline__ unsigned box_key(unsigned rcell, typecode rcode, cons
 }
 
 struct SlabFaces;  // the ghost exchange after the divide (below)
+struct ItemBuild;  // the per-divide item list of the tiled interactions (sph_items.hpp)
 
 // Scratch of the cell sort (DivideGpu).
 struct SortScratch {
@@ -193,7 +194,7 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
                        float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
                        IncDivScratch& s, SortScratch& srt, unsigned keybits, const float4* phase_eos = nullptr,
                        const SlabFaces* faces = nullptr, unsigned ngl = 0, unsigned ngr = 0,
-                       hipEvent_t ev_boxes = nullptr);
+                       const ItemBuild* items = nullptr);
 
 // ---- interaction (cusph::Interaction_Forces, JSphGpu_ker.cu:788-885) ----
 // With floating bodies (ftmassp != nullptr: particle mass per body, `code` of the
@@ -213,14 +214,8 @@ constexpr int QSTRIDE = 32;
 constexpr size_t QCTR_QUEUE_BYTES = 9 * QSTRIDE * sizeof(unsigned);  // what a re-run zeroes
 constexpr size_t QCTR_BYTES = 10 * QSTRIDE * sizeof(unsigned);
 constexpr int QCTR_NITEMS = 9 * QSTRIDE;
-// Tiled fluid interaction (sph_interaction_tiled.hip) and its per-divide item list.
-// scelldiv 1 (CellMode=full): items of <= 4 cells; 2 (half): <= TMAXCELLS_HALF half-cells.
-// p1 in the local columns [xr[0], xr[1]), [xr[2], xr[3]), [xr[4], xr[5]), each range's items
-// on their own (nullptr: the owned columns).  With qctr2: two lists in `items`, the first of
-// range 0 (counter block qctr), the second of ranges 1 and 2 after it (qctr2).  rowtmp holds
-// 2 x 2 ncy ncz counts.
-void launch_items(hipStream_t stm, DevScalars* sc, const unsigned* begincell, DivGrid g, unsigned* rowtmp,
-                  uint4* items, unsigned* qctr, int scelldiv = 1, const int* xr = nullptr, unsigned* qctr2 = nullptr);
+// Tiled fluid interaction (sph_interaction_tiled.hip); its per-divide item list is built
+// by sph_items.hpp (launch_items, or the incremental divide's push launch + launch_items_write).
 // With floating bodies (ftmassp != nullptr) the staged p2 records carry their mass ratio
 // and kind (the FT instantiation; one more float2 of LDS per record).
 void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
@@ -255,7 +250,7 @@ void launch_mdbc_face_apply(hipStream_t stm, DevScalars* sc, const MdbcFaceRec* 
 void launch_nn_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
                      const float4* poscell, const float4* velrhop, const float* press, const typecode* code,
                      const unsigned* begincell, DivGrid g, const KConst& K, const float4* phases, float4* arace,
-                     float4* shiftpos, bool shift, float* viscoeta, float4* tau);
+                     float4* shiftpos, bool shift, float* viscoeta, float4* tau, const float* ftmassp = nullptr);
 // Single-phase interaction with Laminar+SPS viscosity and/or shifting (sph_ext.hip):
 // arace, shiftpos (when shiftstore), the new SPS tau into taunew (Laminar+SPS; `tau` holds
 // the previous interaction's), ViscDtMax / AceMax.
@@ -269,7 +264,7 @@ void launch_fluid_ext(hipStream_t stm, unsigned nblocks, DevScalars* sc, const u
 void launch_nn_visc(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
                     const float4* poscell, const float4* velrhop, const typecode* code, const float* viscoeta,
                     const float4* tau, const unsigned* begincell, DivGrid g, const KConst& K, const float4* phases,
-                    float4* arace);
+                    float4* arace, const float* ftmassp = nullptr);
 // Slabs, SPH velocity gradients: the first pass's effective viscosity (Laminar) or stress
 // tensor (ConstEq) of the owned face-column fluid particles, for the neighbours' ghosts
 // (the second pass reads them for every p2).  Records {idp, v[7]}; count in slot 0 of

@@ -44,6 +44,7 @@ struct NNAcc {
   float ax, ay, az, ar, delta, visc, visceta;
   float sx, sy, sz, sw;  // shifting sums (shiftposfsp1)
   bool hv;               // mirrored drain: a heavier-phase neighbour was seen (sx needs the ordered sweep)
+  bool ftsx;             // a floating p2 under ShiftMode NoBound (or a floating p1): sx = FLT_MAX, final
   float gxx, gxy, gxz, gyy, gyz, gzz;  // SPH velocity gradients (TVISCO 4; gradvelp1, xy = du/dy + dv/dx)
 };
 
@@ -150,7 +151,12 @@ __device__ __forceinline__ float max_nonneg(float x, float m) {
 // ORDERED: pairs arrive in the reference's order (the shifting x sum is reset by a
 // heavier-phase p2); else in mirrored-unit order: sx skips the heavy pair and a.hv records
 // it, and the caller recomputes sx in the reference order (nn_sx_sweep) when any lane saw one.
-template <int TVISCO, int TDENSITY, bool SHIFT, bool BOUNDP2, bool ORDERED = true>
+// FT (floating bodies, JSphCpu_NN_FDA.cpp:203-215): a floating p2 (tag bit 7; the low bits
+// its body index, which the reference also uses as the phase index of its phase constants)
+// carries its body's particle mass (the fourth phase-table row), switches the Molteni DDT of
+// p1 off when it is not heavier than 1.2 MassFluid (DELTA_HEAVYFLOATING), takes no part in
+// the Fourtakas DDT, and under ShiftMode NoBound cancels p1's shifting.
+template <int TVISCO, int TDENSITY, bool SHIFT, bool BOUNDP2, bool ORDERED = true, bool FT = false>
 __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restrict__ sph, const NNP1& p, float drx,
                                         float dry, float drz, float rr2, bool ok, const float4& B, const float4& C,
                                         NNAcc& a) {
@@ -163,10 +169,12 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
   const float fac = K.bwenovh * (wq * wq * wq);
   const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
-  const int pp2 = BOUNDP2 ? p.ph : int(__float_as_uint(C.y));
+  const unsigned tg = BOUNDP2 ? 0u : __float_as_uint(C.y);
+  const bool ftp2 = FT && !BOUNDP2 && (tg & 0x80u) != 0u;
+  const int pp2 = BOUNDP2 ? p.ph : int(FT ? (tg & 0x7fu) : tg);
   const float4 ph2 = sph[2 * pp2];
   const float4 ph2c = sph[2 * SPH_MAXPHASES + pp2];  // {m tau_yield, -m log2 e, n - 1, DDTkh cs0}
-  const float massp2 = BOUNDP2 ? K.massbound : ph2.x;
+  const float massp2 = BOUNDP2 ? K.massbound : (ftp2 ? sph[3 * SPH_MAXPHASES + pp2].x : ph2.x);
   const float rho1 = p.vr.w, rho2 = B.w;
   const float inv_rho2 = C.z;  // staged 1/rho2
   // m2/rho2: every per-pair use of 1/rho2 below comes with the mass of p2 (the reference's
@@ -197,6 +205,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     const float visc_densi = ph2c.w * (rhop1over2 - 1.f) * inv_re;  // DDTkh cbar (...) / (r^2+eta^2)
     const float delta = (p.ph == pp2 ? visc_densi * dot3 * massp2 : 0.f);
     a.delta = (BOUNDP2 && !K.mdbc && ok) ? FLT_MAX : a.delta + delta;
+    if (FT && ftp2 && ok && massp2 <= K.massfluid * 1.2f) a.delta = FLT_MAX;
   }
   if (TDENSITY == 2 || (TDENSITY == 3 && !BOUNDP2)) {
     // rho0 (1 + ddtgz drz)^(1/gamma) - rho0 as the reference evaluates it in float: the
@@ -205,11 +214,15 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     // rounding floor) does not absorb: step-1 velocities moved 5.7e-7 against 2e-8
     const float rh = 1.f + K.ddtgz * drz;
     const float drhop = K.rhopzero * fexp2(K.ovgamma * flog2(rh)) - K.rhopzero;
-    const float delta = (p.ph == pp2 ? ph2c.w * ((rho2 - rho1) - drhop) * xdm : 0.f);
+    const float delta = (p.ph == pp2 && !ftp2 ? ph2c.w * ((rho2 - rho1) - drhop) * xdm : 0.f);
     a.delta = (BOUNDP2 && ok) ? FLT_MAX : a.delta - delta;
   }
   // multiphase shifting (JSphCpu_NN_FDA.cpp:202-209): a heavier-phase neighbour resets x
   // (ORDERED: a no-shift pair sets sx = FLT_MAX and every later pair leaves the sums alone)
+  if (FT && SHIFT && ftp2 && ok && K.shiftmode == 1) {
+    a.sx = FLT_MAX;  // every later pair leaves the sums alone (the reference's x != FLT_MAX test)
+    a.ftsx = true;
+  }
   if (SHIFT && (!ORDERED || a.sx != FLT_MAX)) {
     // (a heavier p1 phase differs from p2's: the phase test of the reference is implied)
     const bool heavy = ok && !BOUNDP2 && (p.mph > ph2.x);
@@ -303,14 +316,22 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
 
 // Boundary p1 over fluid p2 (InteractionForcesBound_NN_FDA, JSphCpu_NN_FDA.cpp:48-113):
 // continuity with MassFluid and the visc-dt maximum.
+// FT: a floating p2 with its body's particle mass (JSphCpu_NN_FDA.cpp:89-93).
+template <bool FT = false>
 __device__ __forceinline__ void nn_bound_pair(const KConst& K, const NNP1& p, float drx, float dry, float drz,
-                                              float rr2, bool ok, const float4& B, const float4& C, NNAcc& a) {
+                                              float rr2, bool ok, const float4& B, const float4& C, NNAcc& a,
+                                              const float4* __restrict__ sph) {
   const float rad = fsqrt_(rr2);
   const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
   const float fac = K.bwenovh * (wq * wq * wq);
   const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
   const float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
-  a.ar = fmaf(K.massfluid * (dvx * frx + dvy * fry + dvz * frz), p.vr.w * C.z, a.ar);
+  float m2 = K.massfluid;
+  if (FT) {
+    const unsigned tg = __float_as_uint(C.y);
+    if (tg & 0x80u) m2 = sph[3 * SPH_MAXPHASES + (tg & 0x7fu)].x;
+  }
+  a.ar = fmaf(m2 * (dvx * frx + dvy * fry + dvz * frz), p.vr.w * C.z, a.ar);
   const float dot = drx * dvx + dry * dvy + drz * dvz;
   a.visc = fmaxf(ok ? dot * frcp(rr2 + K.eta2) : 0.f, a.visc);
 }
@@ -336,15 +357,17 @@ __device__ __forceinline__ void nn_stage(const KConst& K, unsigned rs, unsigned 
     const float4 vr = velrhop[rs + i];
     sB[i] = vr;
     const typecode c = code[rs + i];
-    const unsigned tag = boundrow ? (CodeType(c) == 0 ? 1u : 0u) : unsigned(c & CODE_MASKVALUE);
+    // fluid rows: the phase (fluid) or, bit 7 set, the body index (floating)
+    const unsigned tag = boundrow ? (CodeType(c) == 0 ? 1u : 0u)
+                                  : (unsigned(c & CODE_MASKVALUE) | (CodeType(c) == CODE_TYPE_FLOATING ? 0x80u : 0u));
     sC.c[i] = make_float2(press[rs + i], frcp(vr.w));
     sC.t[i] = (unsigned char)tag;
   }
 }
 
-// One pass of a p1 over its 9 rows of one kind, z-major then y, p2 ascending.
-// KIND 0: fluid p1 / fluid p2, 1: fluid p1 / bound p2, 2: bound p1 / fluid p2.
-template <int TVISCO, int TDENSITY, bool SHIFT, int KIND>
+// One pass of a p1 over its (2S+1)^2 rows of one kind (S = scelldiv), z-major then y, p2
+// ascending.  KIND 0: fluid p1 / fluid p2, 1: fluid p1 / bound p2, 2: bound p1 / fluid p2.
+template <int TVISCO, int TDENSITY, bool SHIFT, int KIND, int S, bool FT>
 __device__ __forceinline__ void nn_pass(const KConst& K, const DivGrid& g, const RowCtx& rc, const NNP1& p, float thr,
                                         const unsigned* __restrict__ bc, const float4* __restrict__ poscell,
                                         const float4* __restrict__ velrhop, const float* __restrict__ press,
@@ -353,8 +376,8 @@ __device__ __forceinline__ void nn_pass(const KConst& K, const DivGrid& g, const
                                         const float4* __restrict__ sph, NNAcc& a) {
   const unsigned cellinit = (KIND == 1 ? 0u : g.boxfluid);
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
-  for (int dz = -1; dz <= 1; dz++) {
-    for (int dy = -1; dy <= 1; dy++) {
+  for (int dz = -S; dz <= S; dz++) {
+    for (int dy = -S; dy <= S; dy++) {
       const int z = rc.cz + dz, y = rc.cy + dy;
       if (z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;  // block-uniform
       const unsigned rowbase = cellinit + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
@@ -404,11 +427,11 @@ __device__ __forceinline__ void nn_pass(const KConst& K, const DivGrid& g, const
             rr22 = ok2 ? rr22 : 1e30f;
             const float4 C1 = sC.ld(j1, KIND == 1), C2 = sC.ld(j2, KIND == 1);
             if (KIND == 2) {
-              nn_bound_pair(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
-              nn_bound_pair(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
+              nn_bound_pair<FT>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a, sph);
+              nn_bound_pair<FT>(K, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a, sph);
             } else {
-              nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1>(K, sph, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
-              nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1>(K, sph, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
+              nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1, true, FT>(K, sph, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
+              nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1, true, FT>(K, sph, p, drx2, dry2, drz2, rr22, ok2, B2, C2, a);
             }
           }
         }
@@ -421,7 +444,7 @@ __device__ __forceinline__ void nn_pass(const KConst& K, const DivGrid& g, const
 // staged records from bases b0..b3, compacted into one chain and popped two pairs per
 // iteration with value selects only (the chain of drain_words, sph_interaction_tiled.hip).
 // KIND 0: fluid p1 / fluid p2 (sx in mirrored order, see nn_pair), 2: bound p1 / fluid p2.
-template <int TVISCO, int TDENSITY, bool SHIFT, int KIND>
+template <int TVISCO, int TDENSITY, bool SHIFT, int KIND, bool FT>
 __device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restrict__ sph, const NNP1& p,
                                           unsigned long long c0, unsigned long long c1, unsigned long long c2,
                                           unsigned long long c3, int b0, int b1, int b2, int b3,
@@ -469,8 +492,8 @@ __device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restr
     const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
     rr21 = ok1 ? rr21 : 1e30f;
     const float4 C1 = sC.ld(j1, KIND == 1);
-    if (KIND == 2) nn_bound_pair(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
-    else nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1, false>(K, sph, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
+    if (KIND == 2) nn_bound_pair<FT>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a, sph);
+    else nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1, false, FT>(K, sph, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
     keep_w(A1, B1);  // 16-B LDS reads (sph_tiled.hpp)
   }
 }
@@ -481,7 +504,7 @@ __device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restr
 // candidate counts in mirrored rows complement each other, so the lanes' loop lengths are
 // alike.  Every sum but the shifting x sum is order-free (up to rounding); a heavier-phase
 // neighbour is flagged in a.hv and the caller redoes sx in the reference order.
-template <int TVISCO, int TDENSITY, bool SHIFT, int KIND>
+template <int TVISCO, int TDENSITY, bool SHIFT, int KIND, int S, bool FT>
 __device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid& g, const RowCtx& rc, const NNP1& p,
                                                  float thr, const unsigned* __restrict__ bc,
                                                  const float4* __restrict__ poscell,
@@ -493,10 +516,16 @@ __device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid&
   // ShiftMode Full): the caller keeps the reference order otherwise
   const unsigned cellinit = KIND == 1 ? 0u : g.boxfluid;
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
-  for (int u = 0; u < 5; u++) {
-    const int dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
-    const int dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
-    const bool paired = u < 4;
+  constexpr int NPAIR = ((2 * S + 1) * (2 * S + 1) - 1) / 2;  // mirrored row pairs, then the own row
+  for (int u = 0; u <= NPAIR; u++) {
+    int dza = 0, dya = 0;
+    const bool paired = u < NPAIR;
+    if (S == 1) {
+      dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
+      dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
+    } else if (paired) {
+      half_row(u, dya, dza);  // the 12 lower rows of the 5x5 half-cell stencil (sph_tiled.hpp)
+    }
     unsigned rs[2] = {0, 0}, re[2] = {0, 0}, ls[2] = {0, 0}, le[2] = {0, 0};
 #pragma unroll
     for (int k = 0; k < 2; k++) {
@@ -525,7 +554,7 @@ __device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid&
         unsigned long long c0, c1, c2, c3;
         test128(sA, wa0 + off, min(na, 128), px2, py2, pz2, thr, c0, c1);
         test128(sA, wb0 + off, min(nb, 128), px2, py2, pz2, thr, c2, c3);
-        nn_drain4<TVISCO, TDENSITY, SHIFT, KIND>(K, sph, p, c0, c1, c2, c3, wa0 + off, wa0 + off + 64, wb0 + off,
+        nn_drain4<TVISCO, TDENSITY, SHIFT, KIND, FT>(K, sph, p, c0, c1, c2, c3, wa0 + off, wa0 + off + 64, wb0 + off,
                                                  wb0 + off + 64, sA, sB, sC, a);
       }
     } else {  // too long for one segment: each row on its own, in TCAP segments
@@ -541,7 +570,7 @@ __device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid&
           for (int off = w0; off < w1; off += 128) {
             unsigned long long c0, c1;
             test128(sA, off, min(w1 - off, 128), px2, py2, pz2, thr, c0, c1);
-            nn_drain4<TVISCO, TDENSITY, SHIFT, KIND>(K, sph, p, c0, c1, 0ull, 0ull, off, off + 64, 0, 0, sA, sB,
+            nn_drain4<TVISCO, TDENSITY, SHIFT, KIND, FT>(K, sph, p, c0, c1, 0ull, 0ull, off, off + 64, 0, 0, sA, sB,
                                                      sC, a);
           }
         }
@@ -561,6 +590,7 @@ __device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid&
 // sweep typically stages 3 of the 9 rows.  Run for a block when any of its lanes met a
 // heavier-phase neighbour in the mirrored pass (phase interfaces only); `need`: this lane did
 // (the others keep their mirrored-order sum, which no reset touched).
+template <int S, bool FT>
 __device__ __forceinline__ float nn_sx_sweep(const KConst& K, const DivGrid& g, const RowCtx& rc, const NNP1& p,
                                              float thr, const unsigned* __restrict__ bc,
                                              const float4* __restrict__ poscell,
@@ -571,8 +601,8 @@ __device__ __forceinline__ float nn_sx_sweep(const KConst& K, const DivGrid& g, 
   float sx = 0.f;
   bool live = rc.act && need;  // still summing (no heavier-phase pair met yet, backwards)
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
-  for (int dz = 1; dz >= -1; dz--) {
-    for (int dy = 1; dy >= -1; dy--) {
+  for (int dz = S; dz >= -S; dz--) {
+    for (int dy = S; dy >= -S; dy--) {
       if (!__syncthreads_or(int(live))) return need ? sx : sx_mirrored;  // block-uniform exit
       const int z = rc.cz + dz, y = rc.cy + dy;
       if (z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;  // block-uniform
@@ -616,9 +646,11 @@ __device__ __forceinline__ float nn_sx_sweep(const KConst& K, const DivGrid& g, 
             const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
             const float fac = K.bwenovh * (wq * wq * wq);
             const float frx = fac * drx;
-            const int pp2 = int(__float_as_uint(C.y));
-            const float massp2 = sph[2 * pp2].x;
-            const bool heavy = ok && (p.mph > massp2);
+            const unsigned tg = __float_as_uint(C.y);
+            const int pp2 = int(FT ? (tg & 0x7fu) : tg);
+            const float mph2 = sph[2 * pp2].x;  // the heavier-phase test: phase constants (a body's index too)
+            const float massp2 = (FT && (tg & 0x80u)) ? sph[3 * SPH_MAXPHASES + pp2].x : mph2;
+            const bool heavy = ok && (p.mph > mph2);
             if (heavy) live = false;  // the reference's reset: nothing before this pair counts
             else sx += (massp2 * C.z) * frx;
           }
@@ -641,25 +673,30 @@ __device__ __forceinline__ float nn_sx_sweep(const KConst& K, const DivGrid& g, 
 #define SPH_NN_WAVES_ATTR
 #endif
 
-template <int TVISCO, int TDENSITY, bool SHIFT>
+template <int TVISCO, int TDENSITY, bool SHIFT, int S, bool FT>
 __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
                                                  unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
                                                  const float4* __restrict__ velrhop, const float* __restrict__ press,
                                                  const typecode* __restrict__ code, const unsigned* __restrict__ bc,
                                                  DivGrid g, KConst K, const float4* __restrict__ phases,
                                                  float4* __restrict__ arace, float4* __restrict__ shiftpos,
-                                                 float* __restrict__ viscoeta, float4* __restrict__ tau) {
+                                                 float* __restrict__ viscoeta, float4* __restrict__ tau,
+                                                 const float* __restrict__ ftmassp) {
   __shared__ float4 sAB[2 * NN_TCAP];  // sA then sB: the candidate test's over-read stays inside
   float4* const sA = sAB;
   float4* const sB = sAB + NN_TCAP;
   __shared__ float2 sC2[NN_TCAP];  // {press, 1/rho}
   __shared__ unsigned char sT[NN_TCAP];  // tag
   const NNSC sC = {sC2, sT};
-  __shared__ float4 sph[3 * SPH_MAXPHASES];
+  // phase table (+ FT: a fourth row, the particle mass of every floating body)
+  __shared__ float4 sph[(FT ? 4 : 3) * SPH_MAXPHASES];
   __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];
   __shared__ unsigned s_nwave[4];
   if (threadIdx.x < 3 * SPH_MAXPHASES) sph[threadIdx.x] = phases[threadIdx.x];
+  if (FT && threadIdx.x < SPH_MAXPHASES)
+    sph[3 * SPH_MAXPHASES + threadIdx.x] =
+        make_float4(threadIdx.x < unsigned(K.nftbodies) ? ftmassp[threadIdx.x] : 0.f, 0.f, 0.f, 0.f);
   const ItemGroups IG(qctr);
   const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f, etamax = 0.f;
@@ -690,11 +727,11 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
       const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
       const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);
       const int xo = (ia + ib + 1) >> 1;
-      const int xa = max(ia - 1, 0), xb = min(ib + 1, g.ncx - 1);
+      const int xa = max(ia - S, 0), xb = min(ib + S, g.ncx - 1);
       if (bitem) {  // no fluid within reach: ar = 0 (PreInteraction reset), nothing else
         bool any = false;
-        for (int z = max(cz - 1, 0); z <= min(cz + 1, g.ncz - 1); z++)
-          for (int y = max(cy - 1, 0); y <= min(cy + 1, g.ncy - 1); y++) {
+        for (int z = max(cz - S, 0); z <= min(cz + S, g.ncz - 1); z++)
+          for (int y = max(cy - S, 0); y <= min(cy + S, g.ncy - 1); y++) {
             const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
             any |= bc[rowbase + xa] != bc[rowbase + xb + 1];
           }
@@ -715,6 +752,7 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
         p.z = pc1.z;
         p.vr = velrhop[p1];
         p.press = press[p1];
+        // a floating p1's code value is its body index, which the reference uses as its phase
         p.ph = bitem ? 0 : int(code[p1] & CODE_MASKVALUE);
       } else {
         p.x = p.y = p.z = 1e30f;
@@ -726,12 +764,12 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
       p.mph = sph[2 * p.ph].x;
       p.taumax = sph[2 * p.ph + 1].z;
       p.bimulti = sph[2 * p.ph + 1].w;
-      const int lxa = max(cx1 - 1, 0), lxb = min(cx1 + 1, g.ncx - 1);
+      const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
       const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
-      const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act};
+      const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act, p1};
       if (bitem) {
         NNAcc f = {};
-        nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 2>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
+        nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 2, S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
                                                      sph, f);
         if (act) {
           arace[p1] = make_float4(0.f, 0.f, 0.f, (f.ar != 0.f || f.visc != 0.f) ? 0.f + f.ar : 0.f);
@@ -742,21 +780,36 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
       // fluid p1: the fluid pass, then the bound pass; the shifting sums carry over
       // (shiftposfs[p1] is stored by the first pass and loaded by the second)
       NNAcc f = {}, b = {};
-      nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 0>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
-                                                   sph, f);
+      // a floating p1 gets no DDT and no shifting (JSphCpu_NN_FDA.cpp:159-164)
+      const bool ftp1 = FT && act && CodeType(code[p1]) == CODE_TYPE_FLOATING;
+      if (ftp1) {
+        if (TDENSITY) f.delta = FLT_MAX;
+        if (SHIFT) {
+          f.sx = FLT_MAX;
+          f.ftsx = true;
+        }
+      }
+      nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 0, S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB,
+                                                       sC, sph, f);
       if (SHIFT && __syncthreads_or(int(f.hv)))
-        f.sx = nn_sx_sweep(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f.hv, f.sx);
+        f.sx = nn_sx_sweep<S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f.hv, f.sx);
+      if (FT && f.ftsx) f.sx = FLT_MAX;  // x stays FLT_MAX once set (no reset after it)
       b.sx = f.sx;
       b.sy = f.sy;
       b.sz = f.sz;
       b.sw = f.sw;
+      if (FT) {  // the bound-row call starts over for a floating p1 too (deltap1, shiftposfsp1.x)
+        b.ftsx = f.ftsx;
+        if (ftp1 && TDENSITY) b.delta = FLT_MAX;
+      }
       // the first no-shift bound pair (ShiftMode NoBound/NoFixed) freezes every shifting sum:
       // only then is the bound pass order-dependent (uniform branch)
       if (SHIFT && (K.shiftmode == 1 || K.shiftmode == 2))
-        nn_pass<TVISCO, TDENSITY, SHIFT, 1>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, b);
+        nn_pass<TVISCO, TDENSITY, SHIFT, 1, S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, b);
       else
-        nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 1>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
+        nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 1, S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
                                                      sph, b);
+      if (FT && b.ftsx) b.sx = FLT_MAX;
       f.ar *= p.vr.w;  // the continuity sums' common rho1 (nn_pair)
       b.ar *= p.vr.w;
       if (act) {
@@ -818,10 +871,21 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
 void launch_nn_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
                      const float4* poscell, const float4* velrhop, const float* press, const typecode* code,
                      const unsigned* begincell, DivGrid g, const KConst& K, const float4* phases, float4* arace,
-                     float4* shiftpos, bool shift, float* viscoeta, float4* tau) {
-#define SPH_NN(TV, TD, SH)                                                                                       \
-  hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, \
-                     press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau)
+                     float4* shiftpos, bool shift, float* viscoeta, float4* tau, const float* ftmassp) {
+  // CellMode: cells of 2h (S = 1) or of h (S = 2); floating bodies (FT, cells of 2h only)
+#define SPH_NN(TV, TD, SH)                                                                                         \
+  if (ftmassp)                                                                                                     \
+    hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH, 1, true>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr,         \
+                       poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,    \
+                       ftmassp);                                                                                   \
+  else if (K.scelldiv == 2)                                                                                        \
+    hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH, 2, false>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr,        \
+                       poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,    \
+                       ftmassp);                                                                                   \
+  else                                                                                                             \
+    hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH, 1, false>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr,        \
+                       poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,    \
+                       ftmassp)
 #define SPH_NN_TD(TV, SH)          \
   switch (K.tdensity) {            \
     case 0: SPH_NN(TV, 0, SH); break; \
@@ -876,7 +940,8 @@ __device__ __forceinline__ void nnv_stage(const KConst& K, unsigned rs, unsigned
                                           const float4* __restrict__ velrhop, const typecode* __restrict__ code,
                                           const float* __restrict__ viscoeta, const float4* __restrict__ tau,
                                           const float4* __restrict__ sph, float4* __restrict__ sA,
-                                          float4* __restrict__ sB, float4* __restrict__ sC) {
+                                          float4* __restrict__ sB, float4* __restrict__ sC,
+                                          const float* __restrict__ ftmassp) {
   const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
   for (unsigned i = threadIdx.x; i < n; i += TB) {
     const unsigned q = rs + i;
@@ -885,8 +950,12 @@ __device__ __forceinline__ void nnv_stage(const KConst& K, unsigned rs, unsigned
     const float x2 = pc.x + float(cx2 - xo) * K.scell;
     const float y2 = pc.y + oy, z2 = pc.z + oz;
     sA[dst + i] = make_float4(x2, y2, z2, x2 * x2 + y2 * y2 + z2 * z2);
-    const unsigned ph = boundrow ? 0u : unsigned(code[q] & CODE_MASKVALUE);
-    const float m2 = boundrow ? K.massbound : sph[2 * ph].x;
+    const typecode cq = code[q];
+    const unsigned ph = boundrow ? 0u : unsigned(cq & CODE_MASKVALUE);
+    // a floating p2: its body's particle mass (JSphCpu_NN_SPH.cpp:283-288, 391-396); its
+    // body index doubles as the phase index of the phase constants, as in the reference
+    const float m2 = boundrow ? K.massbound
+                              : ((ftmassp && CodeType(cq) == CODE_TYPE_FLOATING) ? ftmassp[ph] : sph[2 * ph].x);
     if constexpr (VM == VM_CONSEQ) {
       const float rho2 = velrhop[q].w;
       if (boundrow) {  // tau of p1 is used for a bound p2
@@ -1024,23 +1093,29 @@ __device__ __forceinline__ void nnv_drain4(const KConst& K, const NNVP1& p, unsi
   }
 }
 
-// A pass of the p1 over its 9 rows of one kind in point-mirrored drain units (the units of
-// nn_pass_mirrored), rows too long for one segment row by row in NNV_TCAP segments.
-template <int VM, bool BOUNDP2>
+// A pass of the p1 over its (2S+1)^2 rows of one kind in point-mirrored drain units (the
+// units of nn_pass_mirrored), rows too long for one segment row by row in NNV_TCAP segments.
+template <int VM, bool BOUNDP2, int S>
 __device__ __forceinline__ float3 nnv_pass(const KConst& K, const DivGrid& g, const RowCtx& rc, const NNVP1& p,
                                            float thr, const unsigned* __restrict__ bc,
                                            const float4* __restrict__ poscell, const float4* __restrict__ velrhop,
                                            const typecode* __restrict__ code, const float* __restrict__ viscoeta,
                                            const float4* __restrict__ tau, const float4* __restrict__ sph,
                                            float4* __restrict__ sA, float4* __restrict__ sB,
-                                           float4* __restrict__ sC) {
+                                           float4* __restrict__ sC, const float* __restrict__ ftmassp) {
   float3 acc = make_float3(0.f, 0.f, 0.f);
   const unsigned cellinit = BOUNDP2 ? 0u : g.boxfluid;
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
-  for (int u = 0; u < 5; u++) {
-    const int dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
-    const int dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
-    const bool paired = u < 4;
+  constexpr int NPAIR = ((2 * S + 1) * (2 * S + 1) - 1) / 2;
+  for (int u = 0; u <= NPAIR; u++) {
+    int dza = 0, dya = 0;
+    const bool paired = u < NPAIR;
+    if (S == 1) {
+      dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
+      dya = (u == 0) ? -1 : (u == 1) ? 1 : (u == 2) ? 0 : (u == 3) ? -1 : 0;
+    } else if (paired) {
+      half_row(u, dya, dza);
+    }
     unsigned rs[2] = {0, 0}, re[2] = {0, 0}, ls[2] = {0, 0}, le[2] = {0, 0};
 #pragma unroll
     for (int k = 0; k < 2; k++) {
@@ -1060,10 +1135,10 @@ __device__ __forceinline__ float3 nnv_pass(const KConst& K, const DivGrid& g, co
       __syncthreads();
       if (n0)
         nnv_stage<VM>(K, rs[0], n0, 0u, rc.xo, dya, dza, BOUNDP2, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
-                      sC);
+                      sC, ftmassp);
       if (n1)
         nnv_stage<VM>(K, rs[1], n1, n0, rc.xo, -dya, -dza, BOUNDP2, poscell, velrhop, code, viscoeta, tau, sph, sA,
-                      sB, sC);
+                      sB, sC, ftmassp);
       __syncthreads();
       const int wa0 = int(ls[0] - rs[0]), wa1 = rc.act && n0 ? int(le[0] - rs[0]) : wa0;
       const int wb0 = int(n0 + ls[1] - rs[1]), wb1 = rc.act && n1 ? int(n0 + le[1] - rs[1]) : wb0;
@@ -1083,7 +1158,7 @@ __device__ __forceinline__ float3 nnv_pass(const KConst& K, const DivGrid& g, co
           const unsigned segn = min(unsigned(NNV_TCAP), re[k] - seg);
           __syncthreads();
           nnv_stage<VM>(K, seg, segn, 0u, rc.xo, dy, dz, BOUNDP2, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
-                        sC);
+                        sC, ftmassp);
           __syncthreads();
           const int w0 = int(max(ls[k], seg) - seg);
           const int w1 = rc.act ? max(w0, int(min(le[k], seg + segn)) - int(seg)) : w0;
@@ -1099,13 +1174,14 @@ __device__ __forceinline__ float3 nnv_pass(const KConst& K, const DivGrid& g, co
   return acc;
 }
 
-template <int VM>
+template <int VM, int S>
 __global__ __launch_bounds__(TB) void k_nn_visc(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
                                                 unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
                                                 const float4* __restrict__ velrhop, const typecode* __restrict__ code,
                                                 const float* __restrict__ viscoeta, const float4* __restrict__ tau,
                                                 const unsigned* __restrict__ bc, DivGrid g, KConst K,
-                                                const float4* __restrict__ phases, float4* __restrict__ arace) {
+                                                const float4* __restrict__ phases, float4* __restrict__ arace,
+                                                const float* __restrict__ ftmassp) {
   __shared__ float4 sABC[3 * NNV_TCAP];  // sA, sB, sC: the candidate test's over-read stays inside
   float4* const sA = sABC;
   float4* const sB = sABC + NNV_TCAP;
@@ -1139,7 +1215,7 @@ __global__ __launch_bounds__(TB) void k_nn_visc(DevScalars* __restrict__ sc, con
       const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
       const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);
       const int xo = (ia + ib + 1) >> 1;
-      const int xa = max(ia - 1, 0), xb = min(ib + 1, g.ncx - 1);
+      const int xa = max(ia - S, 0), xb = min(ib + S, g.ncx - 1);
       const unsigned p1 = item.z + lane_order(poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
       const bool act = threadIdx.x < item.w - item.z;
       NNVP1 p;
@@ -1168,13 +1244,13 @@ __global__ __launch_bounds__(TB) void k_nn_visc(DevScalars* __restrict__ sc, con
         p.x = p.y = p.z = 1e30f;
         p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
       }
-      const int lxa = max(cx1 - 1, 0), lxb = min(cx1 + 1, g.ncx - 1);
+      const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
       const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
-      const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act};
-      const float3 f = nnv_pass<VM, false>(K, g, rc, p, thr, bc, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
-                                           sC);
-      const float3 b = nnv_pass<VM, true>(K, g, rc, p, thr, bc, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
-                                          sC);
+      const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act, p1};
+      const float3 f = nnv_pass<VM, false, S>(K, g, rc, p, thr, bc, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
+                                              sC, ftmassp);
+      const float3 b = nnv_pass<VM, true, S>(K, g, rc, p, thr, bc, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
+                                             sC, ftmassp);
       if (act) {
         // ace[p1] = ace[p1] + acep1 per pass when non-zero (JSphCpu_NN_SPH.cpp:442-444)
         float4 r = arace[p1];
@@ -1200,10 +1276,14 @@ __global__ __launch_bounds__(TB) void k_nn_visc(DevScalars* __restrict__ sc, con
 void launch_nn_visc(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
                     const float4* poscell, const float4* velrhop, const typecode* code, const float* viscoeta,
                     const float4* tau, const unsigned* begincell, DivGrid g, const KConst& K, const float4* phases,
-                    float4* arace) {
+                    float4* arace, const float* ftmassp) {
 #define SPH_NNV(VM)                                                                                             \
-  hipLaunchKernelGGL((k_nn_visc<VM>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, code, \
-                     viscoeta, tau, begincell, g, K, phases, arace)
+  if (K.scelldiv == 2)                                                                                          \
+    hipLaunchKernelGGL((k_nn_visc<VM, 2>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop,   \
+                       code, viscoeta, tau, begincell, g, K, phases, arace, ftmassp);                                    \
+  else                                                                                                          \
+    hipLaunchKernelGGL((k_nn_visc<VM, 1>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop,   \
+                       code, viscoeta, tau, begincell, g, K, phases, arace, ftmassp)
   if (K.nntvisco == 1) SPH_NNV(VM_ART);
   else if (K.nntvisco == 2) SPH_NNV(VM_MORRIS);
   else SPH_NNV(VM_CONSEQ);

@@ -1,5 +1,6 @@
 // sph_solver.cpp — host orchestration (see sph_solver.hpp).
 #include "sph_solver.hpp"
+#include "sph_items.hpp"
 
 #include <algorithm>
 #include <cfloat>
@@ -484,8 +485,6 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   sps_ = !nn_ && C.tvisco == SPH_VISCO_LAMINARSPS;
   ext_ = !nn_ && (sps_ || shift_);
   facex_ = slab() && (nnsph_ || sps_);
-  if (ext_ && C.scelldiv != 1)
-    throw SphError(SPH_ERR_UNSUPPORTED, "Laminar+SPS viscosity / shifting with CellMode=half is not implemented");
   if (ext_) tiled_ = true;
   if (C.kernel == SPH_KERNEL_CUBIC && (nn_ || ext_))
     throw SphError(SPH_ERR_UNSUPPORTED, "the Cubic spline kernel with NN multiphase / Laminar+SPS / shifting is not implemented");
@@ -507,8 +506,7 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
     }
   }
   if (nn_) {
-    // the NN interaction is the tiled kernel of sph_nn.hip only
-    if (C.scelldiv != 1) throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase: CellMode=half is not implemented");
+    // the NN interaction is the tiled kernel of sph_nn.hip only (full or half cells)
     tiled_ = true;
   }
   check_hip(hipSetDevice(device), "hipSetDevice");
@@ -538,7 +536,6 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
 
 SphGpuSingle::~SphGpuSingle() {
   if (xstream_) (void)hipStreamSynchronize(xstream_);
-  if (istream_) (void)hipStreamSynchronize(istream_);
   if (stream) (void)hipStreamSynchronize(stream);
   Free();
   for (auto& e : pending_) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
@@ -546,9 +543,6 @@ SphGpuSingle::~SphGpuSingle() {
   if (xev_) (void)hipEventDestroy(xev_);
   if (ev_div_) (void)hipEventDestroy(ev_div_);
   if (ev_ghost_) (void)hipEventDestroy(ev_ghost_);
-  if (ev_boxes_) (void)hipEventDestroy(ev_boxes_);
-  if (ev_items_) (void)hipEventDestroy(ev_items_);
-  if (istream_) (void)hipStreamDestroy(istream_);
   if (xstream_) {
     (void)hipStreamSynchronize(xstream_);
     (void)hipStreamDestroy(xstream_);
@@ -567,7 +561,7 @@ void SphGpuSingle::AllocFixed() {
   if (slab()) {  // re-partition: column counts [2 ncx] + the ranks' bounds [nranks + 1]
     colcnt_ = (float*)dmalloc(4 * (2 * size_t(C.dom_cells[0]) + size_t(slabcfg_.nranks) + 1));
   }
-  rowtmp_ = (unsigned*)dmalloc(4 * 4 * size_t(G.ncy) * size_t(G.ncz));  // two lists x (fluid, bound) rows
+  rowtmp_ = (unsigned*)dmalloc(4 * ITEMS_ROWTMP(G.ncy, G.ncz));  // two lists x (fluid, bound) rows of item counts
   qctr_ = (unsigned*)dmalloc(QCTR_BYTES);
   check_hip(hipMemset(qctr_, 0, QCTR_BYTES), "zero work counters");
   sort_.digtot = (unsigned*)dmalloc(4 * (1u << RS_MAXBITS));
@@ -1162,20 +1156,36 @@ void SphGpuSingle::RunCellDivide() {
   if (slab() && exchange_armed_) Exchange();
   const unsigned ngl = ghosts ? unsigned(xg_rl_) : 0u, ngr = ghosts ? unsigned(xg_rr_) : 0u;
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET);
-  bool items_side = false;  // the item list built on istream_, beside the push
+  // Items (each build also zeroes its queues).  A slab with neighbours cuts its rows where
+  // the stencil (scelldiv columns) stops reaching a ghost column: the face items and the
+  // interior items never share an item, whether they run in one list or in two (with the
+  // ghost exchange beside the interior list) — the same items, so the same bits.
+  const bool overlap = ghosts && OverlapGhosts();
+  ghost_split_ = false;
+  ItemBuild ib;
+  if (tiled_) {
+    const int S = int(C.scelldiv), hl = slab() && transport_->has_left(), hr = slab() && transport_->has_right();
+    int ib0 = G.xown0 + (hl ? S : 0), ie0 = G.xown1 - (hr ? S : 0);
+    if (ib0 >= ie0) ib0 = ie0 = G.xown0;  // a narrow slab: every item reaches a ghost column
+    const bool inc = inc_ok_ && inc_valid_ && G.ncx >= 3;
+    const unsigned* bcnew = inc ? begincell_alt_ : begincell_;  // the begincell this divide writes
+    if (overlap) {  // the interior list (qctr_), then the face list (qctrf_) after it
+      const int xr[6] = {ib0, ie0, G.xown0, ib0, ie0, G.xown1};
+      ib = make_item_build(bcnew, G, rowtmp_, items_, qctr_, C.scelldiv, xr, qctrf_);
+      ghost_split_ = true;
+    } else {
+      const int xa[6] = {G.xown0, ib0, ib0, ie0, ie0, G.xown1};
+      ib = make_item_build(bcnew, G, rowtmp_, items_, qctr_, C.scelldiv, xa, nullptr);
+    }
+  }
   if (inc_ok_ && inc_valid_ && G.ncx >= 3) {
     // the previous order merged with the particles whose box changed and, on a slab, the
-    // particles the exchange appended and the ghosts' slots (sph_divide.hip)
+    // particles the exchange appended and the ghosts' slots (sph_divide.hip); the item
+    // count runs in the push launch, the item write right after it
     inc_.nb2 = inc_blocks_boxes(G.nctt);
-    items_side = tiled_;
-    if (items_side && !istream_) {
-      check_hip(hipStreamCreateWithFlags(&istream_, hipStreamNonBlocking), "hipStreamCreate");
-      check_hip(hipEventCreateWithFlags(&ev_boxes_, hipEventDisableTiming), "hipEventCreate");
-      check_hip(hipEventCreateWithFlags(&ev_items_, hipEventDisableTiming), "hipEventCreate");
-    }
     launch_divide_inc(stream, cap_, sc_, cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_, G, begincell_,
                       begincell_alt_, inc_, sort_, keybits_, nn_ ? phaseeos_ : nullptr, ghosts ? &faces_ : nullptr, ngl,
-                      ngr, items_side ? ev_boxes_ : nullptr);
+                      ngr, tiled_ ? &ib : nullptr);
     std::swap(begincell_, begincell_alt_);
   } else {
     // the ghosts' slots sort as entries [np, np + ngl + ngr) after the particles
@@ -1189,6 +1199,7 @@ void SphGpuSingle::RunCellDivide() {
     if (inc_ok_)
       check_hip(hipMemcpyAsync(inc_.skeys, sort_.keys[res], 4 * size_t(cap_), hipMemcpyDeviceToDevice, stream),
                 "keep sorted keys");
+    if (tiled_) launch_items(stream, ib);
   }
   inc_valid_ = inc_ok_;
   inc_.napp = 0;
@@ -1196,35 +1207,7 @@ void SphGpuSingle::RunCellDivide() {
   std::swap(cur_, alt_);
   // this slab's ghost records for the neighbours, from its sorted face columns
   if (ghosts) launch_ghost_pack(stream, sc_, faces_, G, begincell_, cur_, poscell_, send_, unsigned(xg_sl_), unsigned(xg_sr_));
-  const bool overlap = ghosts && OverlapGhosts();
-  ghost_split_ = false;
-  if (tiled_) {
-    // Items (each build also zeroes its queues).  A slab with neighbours cuts its rows where
-    // the stencil (scelldiv columns) stops reaching a ghost column: the face items and the
-    // interior items never share an item, whether they run in one list or in two (with the
-    // ghost exchange beside the interior list) — the same items, so the same bits.
-    // After an incremental divide the build runs on istream_ from the moment the new
-    // begincell is final (k_inc_boxes), beside the push, and joins the solver stream here:
-    // cfg2 divide 0.0846 -> see DESIGN.md §4.
-    const hipStream_t is = items_side ? istream_ : stream;
-    if (items_side) check_hip(hipStreamWaitEvent(istream_, ev_boxes_, 0), "items: wait boxes");
-    const int S = int(C.scelldiv), hl = slab() && transport_->has_left(), hr = slab() && transport_->has_right();
-    int ib = G.xown0 + (hl ? S : 0), ie = G.xown1 - (hr ? S : 0);
-    if (ib >= ie) ib = ie = G.xown0;  // a narrow slab: every item reaches a ghost column
-    if (overlap) {  // the interior list (qctr_), then the face list (qctrf_) after it
-      const int xr[6] = {ib, ie, G.xown0, ib, ie, G.xown1};
-      launch_items(is, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv, xr, qctrf_);
-      ghost_split_ = true;
-    } else {
-      const int xa[6] = {G.xown0, ib, ib, ie, ie, G.xown1};
-      launch_items(is, sc_, begincell_, G, rowtmp_, items_, qctr_, C.scelldiv, xa);
-    }
-    if (items_side) {
-      check_hip(hipEventRecord(ev_items_, istream_), "items: event");
-      check_hip(hipStreamWaitEvent(stream, ev_items_, 0), "items: join");
-    }
-    qfresh_ = true;
-  }
+  if (tiled_) qfresh_ = true;
   if (ghosts) {
     if (overlap) {
       if (!ev_div_) check_hip(hipEventCreateWithFlags(&ev_div_, hipEventDisableTiming), "hipEventCreate");
@@ -1267,7 +1250,7 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
     // ComputeSymplecticPre) and Verlet
     TimedBegin(0);
     launch_nn_tiled(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, cur_.code, begincell_,
-                    G, K, phasek_, arace_, shiftpos_, shift_ && interstep != 2, viscoeta_, tau_);
+                    G, K, phasek_, arace_, shiftpos_, shift_ && interstep != 2, viscoeta_, tau_, ftmassp_);
     if (nnsph_) {
       // SPH velocity gradients: the viscous force is a second pass over the neighbours,
       // reading their effective viscosities / stress tensors (JSphCpu_NN_SPH.cpp:671-696)
@@ -1275,7 +1258,7 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
         NNFaceExchange();
       check_hip(hipMemsetAsync(qctr_, 0, QCTR_QUEUE_BYTES, stream), "zero work counters");
       launch_nn_visc(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, cur_.code, viscoeta_, tau_,
-                     begincell_, G, K, phasek_, arace_);
+                     begincell_, G, K, phasek_, arace_, ftmassp_);
     }
   } else if (ext_) {
     // Laminar+SPS and/or shifting (sph_ext.hip).  Slabs with SPS: the ghosts' tau (the
@@ -1501,7 +1484,13 @@ void SphGpuSingle::SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* m
 void SphGpuSingle::SetFloatings(unsigned nft, const SphFloatingDef* defs, double ftpause) {
   if (stepped_ || ftbodies_) throw SphError(SPH_ERR_STATE, "the floating bodies are configured once, before the first step");
   if (!nft || !defs) throw SphError(SPH_ERR_ARG, "no floating bodies");
-  if (nn_) throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase with floating bodies is not implemented");
+  if (nn_) {
+    // the v5.0 NN solver indexes its phase constants with a floating particle's code value,
+    // its body index (JSphCpu_NN_FDA.cpp:199-200, 231, 267): bodies beyond the phases would
+    // read past the phase table there
+    if (nft > C.nphases) throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase: more floating bodies than phases");
+    if (C.scelldiv != 1) throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase with floating bodies: CellMode=full only");
+  }
   if (C.symmetry) throw SphError(SPH_ERR_ARG, "Symmetry is not allowed with floating bodies.");  // JSph.cpp:1177
   std::vector<FtBody> b(nft);
   std::vector<float> massp(nft);
@@ -1542,6 +1531,7 @@ void SphGpuSingle::SetFloatings(unsigned nft, const SphFloatingDef* defs, double
   check_hip(hipMemcpy(ftmassp_, massp.data(), sizeof(float) * nft, hipMemcpyHostToDevice), "upload floatings");
   nftbodies_ = int(nft);
   nftp_ = nftp;
+  K.nftbodies = int(nft);
   // floating p2 carry their own mass: the FT instantiation of the tiled kernel (or the
   // per-particle kernel under SPH_INTERACTION=simple / CellMode=half)
   launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_, K, G);
@@ -1554,6 +1544,10 @@ void SphGpuSingle::SetFloatingTable(unsigned body, int kind, unsigned n, const d
   if (stepped_) throw SphError(SPH_ERR_STATE, "floating tables are configured before the first step");
   if (!ftbodies_ || body >= unsigned(nftbodies_)) throw SphError(SPH_ERR_ARG, "floating table of an unknown body");
   if (kind < SPH_FTTAB_LINVEL || kind > SPH_FTTAB_ANGFORCE) throw SphError(SPH_ERR_ARG, "invalid floating table kind");
+  // v5.0 NN sums external forces inside FtCalcForces (JSphCpuSingle.cpp:847 of that solver),
+  // not beside the particle forces as v5.2 does
+  if (nn_ && kind >= SPH_FTTAB_LINFORCE)
+    throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase: external forces on floating bodies are not implemented");
   if (!n || !times || !values) throw SphError(SPH_ERR_ARG, "There are not times.");
   std::vector<double4> rows(n);
   for (unsigned i = 0; i < n; i++) {

@@ -243,9 +243,7 @@ class SphGpuSingle {
   bool in_run_ = false;           // inside Run(): the next phase after a divide is the interaction
   hipStream_t xstream_ = nullptr; // ghost transfer + scatter + face items beside the interior items
   hipEvent_t ev_div_ = nullptr, ev_ghost_ = nullptr;
-  // the item build beside the incremental divide's push (it needs only the new begincell)
-  hipStream_t istream_ = nullptr;
-  hipEvent_t ev_boxes_ = nullptr, ev_items_ = nullptr;
+
   // timing (hipEvents on the solver stream)
   bool timing_ = false;
   unsigned timing_mask_ = 0xfu;  // phases timed (SetTimingPhases, sph_solver_set_timing_phases)

@@ -198,6 +198,18 @@ struct ItemGroups {
   }
 };
 
+// i-th of the 12 "lower" rows of the 5x5 CellMode=half stencil (dz < 0, or dz = 0 and
+// dy < 0); the other 12 are their point mirrors, the 25th the item's own row.
+__device__ __forceinline__ void half_row(int i, int& dy, int& dz) {
+  if (i < 10) {
+    dz = -2 + i / 5;
+    dy = -2 + i % 5;
+  } else {
+    dz = 0;
+    dy = i - 12;
+  }
+}
+
 // Item geometry shared by the passes of one p1.
 struct RowCtx {
   int cy, cz;     // the item's cell row

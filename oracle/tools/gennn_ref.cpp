@@ -23,7 +23,10 @@
 // example's 3-D recommendation 2.75 unless given.
 //
 // usage: gennn_ref <dp> <outdir> [width=0.64] [scale=1] [timemax=5] [casename] [shifttfs=2.75]
-//                  [velgrad=1] [viscotreatment=2] [ddt=3] [shifting=3] [csound=0] [step=2]
+//                  [velgrad=1] [viscotreatment=2] [ddt=3] [shifting=3] [csound=0] [step=2] [float=0]
+// float 1: a floating box (mkbound 1, rhopbody 800, half-size 3 lattice spacings) centred at
+// x = 2.5 s, mid-width, one spacing below the top of the phase-0 layer (z = 0.5 s), replacing
+// the fluid lattice points it covers; its block follows the fixed one (JCaseParts order).
 // csound > 0 gives every phase <csound> (phase k: csound*(1 + 0.1 k)), the branch of
 // ConfigConstantsMP where each phase has its own sound speed and CteB (JSph.cpp:3222-3231).
 #include "JPartDataBi4.h"
@@ -54,6 +57,7 @@ int main(int argc, char** argv) {
   const int shifting = (argc > 11 ? atoi(argv[11]) : 3);
   const double csound = (argc > 12 ? atof(argv[12]) : 0.0);
   const int step = (argc > 13 ? atoi(argv[13]) : 2);
+  const bool withft = (argc > 14 ? atoi(argv[14]) : 0) != 0;
 
   const int nx = int(std::round(4.0 * s / dp)), nz = int(std::round(1.25 * s / dp)), ny = int(std::round(width / dp));
   const int nw = int(std::round(0.04 / dp));
@@ -67,18 +71,31 @@ int main(int argc, char** argv) {
     if (i <= x0 && k <= z0) return 0;
     return -1;
   };
+  const int nbh = 3, bic = int(std::round(2.5 * s / dp)), bjc = ny / 2, bkc = z0 - 1;
+  auto inbox = [&](int i, int j, int k) {
+    return withft && std::abs(i - bic) <= nbh && std::abs(j - bjc) <= nbh && std::abs(k - bkc) <= nbh;
+  };
   std::vector<tdouble3> pos;
   for (int k = 0; k <= nz; k++)
     for (int j = 0; j <= ny; j++)
       for (int i = 0; i <= nx; i++)
         if (wall(i, j, k)) pos.push_back(TDouble3(i * dp, j * dp, k * dp));
-  const unsigned nb = unsigned(pos.size());
+  const unsigned nfixed = unsigned(pos.size());
+  tdouble3 bcen = TDouble3(0);
+  for (int k = bkc - nbh; withft && k <= bkc + nbh; k++)
+    for (int j = bjc - nbh; j <= bjc + nbh; j++)
+      for (int i = bic - nbh; i <= bic + nbh; i++) {
+        pos.push_back(TDouble3(i * dp, j * dp, k * dp));
+        bcen = bcen + pos.back();
+      }
+  const unsigned nb = unsigned(pos.size()), nfloat = nb - nfixed;
+  if (nfloat) bcen = bcen / double(nfloat);
   unsigned nph[3] = {0, 0, 0};
   for (int ph = 0; ph < 3; ph++)
     for (int k = 0; k <= nz; k++)
       for (int j = 0; j <= ny; j++)
         for (int i = 0; i <= nx; i++)
-          if (!wall(i, j, k) && phase(i, k) == ph) {
+          if (!wall(i, j, k) && !inbox(i, j, k) && phase(i, k) == ph) {
             pos.push_back(TDouble3(i * dp, j * dp, k * dp));
             nph[ph]++;
           }
@@ -89,6 +106,14 @@ int main(int argc, char** argv) {
   const double h = coefh * std::sqrt(3. * dp * dp);
   const double mass = rho0 * dp * dp * dp;
   const double rhoph[3] = {2000., 1500., 1000.};
+  const double massp = 800. * dp * dp * dp, massbody = massp * nfloat;
+  double ixx = 0, iyy = 0, izz = 0;
+  for (unsigned q = nfixed; q < nb; q++) {
+    const tdouble3 r = pos[q] - bcen;
+    ixx += massp * (r.y * r.y + r.z * r.z);
+    iyy += massp * (r.x * r.x + r.z * r.z);
+    izz += massp * (r.x * r.x + r.y * r.y);
+  }
 
   std::vector<unsigned> idp(np);
   std::vector<tfloat3> vel(np, TFloat3(0));
@@ -106,7 +131,7 @@ int main(int argc, char** argv) {
 
   JPartDataBi4 pd;
   pd.ConfigBasic(0, 1, "gennn_ref", "gennn_ref", name, false, 0, dir);
-  pd.ConfigParticles(np, nb, 0, 0, nf, pmin, pmax, false, false);
+  pd.ConfigParticles(np, nfixed, 0, nfloat, nf, pmin, pmax, false, false);
   pd.ConfigCtes(dp, h, b, rho0, gamma, mass, mass);
   pd.AddPartInfo(0, 0, np, 0, 0, 0, pmin, pmax, 0, 0);
   pd.AddPartData(np, idp.data(), pos.data(), vel.data(), rhop.data());
@@ -119,8 +144,14 @@ int main(int argc, char** argv) {
   fprintf(f, "<gamma value=\"%g\"/>\n<rhop0 value=\"%g\"/>\n<dp value=\"%.10g\"/>\n", gamma, rho0, dp);
   fprintf(f, "<h value=\"%.10E\"/>\n<b value=\"%.10E\"/>\n<massbound value=\"%.10E\"/>\n<massfluid value=\"%.10E\"/>\n", h, b, mass, mass);
   fprintf(f, "</constants>\n");
-  fprintf(f, "<particles np=\"%u\" nb=\"%u\" nbf=\"%u\" mkboundfirst=\"11\" mkfluidfirst=\"1\">\n", np, nb, nb);
-  fprintf(f, "<fixed mkbound=\"0\" mk=\"11\" begin=\"0\" count=\"%u\"/>\n", nb);
+  fprintf(f, "<particles np=\"%u\" nb=\"%u\" nbf=\"%u\" mkboundfirst=\"11\" mkfluidfirst=\"1\">\n", np, nb, nfixed);
+  fprintf(f, "<fixed mkbound=\"0\" mk=\"11\" begin=\"0\" count=\"%u\"/>\n", nfixed);
+  if (nfloat) {
+    fprintf(f, "<floating mkbound=\"1\" mk=\"12\" begin=\"%u\" count=\"%u\">\n", nfixed, nfloat);
+    fprintf(f, "<massbody value=\"%.17g\"/>\n<masspart value=\"%.17g\"/>\n", massbody, massp);
+    fprintf(f, "<center x=\"%.17g\" y=\"%.17g\" z=\"%.17g\"/>\n", bcen.x, bcen.y, bcen.z);
+    fprintf(f, "<inertia x=\"%.17g\" y=\"%.17g\" z=\"%.17g\"/>\n</floating>\n", ixx, iyy, izz);
+  }
   unsigned begin = nb;
   for (int ph = 0; ph < 3; ph++) {
     fprintf(f, "<fluid mkfluid=\"%d\" mk=\"%d\" begin=\"%u\" count=\"%u\"/>\n", ph, ph + 1, begin, nph[ph]);

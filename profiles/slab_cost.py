@@ -56,8 +56,8 @@ def timed(obj, steps, warmup, timing_of=None):
         timing_of.set_timing(True)
         obj.run(steps)
         _sync(obj)
-        p, _ = timing_of.timing()
-        ph = [round(float(x) / steps, 4) for x in p]
+        p, _ = timing_of.timing()  # ms per call of each phase: interaction, update, divide, mdbc
+        ph = dict(zip(("interaction", "update", "divide", "mdbc"), (round(float(x), 4) for x in p)))
     return round(ms, 4), ph
 
 
@@ -67,6 +67,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--repeat", type=int, default=2, help="alternating repeats of the three runs")
+    ap.add_argument("--only", choices=("domain", "one_slab", "faces", "left"), default=None,
+                    help="one of the runs (e.g. under rocprofv3); left: [0, w) | [w, ncx), the big slab with one "
+                         "face in the water, whose face launch runs after the strip's (a trace isolates it)")
     a = ap.parse_args()
     case = DamBreakCase(**CFG[a.workload])
     ncx = int(slab_partition(case, 1)[-1])
@@ -75,25 +78,36 @@ def main():
     out = {"workload": a.workload, "np": int(case.np), "ncx": ncx, "steps": a.steps, "strip_columns": w,
            "domain_ms": [], "one_slab_ms": [], "faces_ms": [], "domain_phases_ms": None, "faces_mid_phases_ms": None}
     for _ in range(a.repeat):
-        s = SphGpuSingle(case)
-        ms, ph = timed(s, a.steps, a.warmup, s)
-        s.close()
-        out["domain_ms"].append(ms)
-        out["domain_phases_ms"] = ph
-        g = SphSlabGroup(case, np.array([0, ncx], np.int32))
-        ms, _ = timed(g, a.steps, a.warmup)
-        g.close()
-        out["one_slab_ms"].append(ms)
-        g = SphSlabGroup(case, np.array([0, w, ncx - w, ncx], np.int32))
-        ms, ph = timed(g, a.steps, a.warmup, g.members[1])
-        out["faces_np"] = [int(m.stats()["np"]) for m in g.members]
-        g.close()
-        out["faces_ms"].append(ms)
-        out["faces_mid_phases_ms"] = ph
+        if a.only in (None, "domain"):
+            s = SphGpuSingle(case)
+            ms, ph = timed(s, a.steps, a.warmup, s)
+            s.close()
+            out["domain_ms"].append(ms)
+            out["domain_phases_ms"] = ph
+        if a.only in (None, "one_slab"):
+            g = SphSlabGroup(case, np.array([0, ncx], np.int32))
+            ms, _ = timed(g, a.steps, a.warmup)
+            g.close()
+            out["one_slab_ms"].append(ms)
+        if a.only in (None, "faces"):
+            g = SphSlabGroup(case, np.array([0, w, ncx - w, ncx], np.int32))
+            ms, ph = timed(g, a.steps, a.warmup, g.members[1])
+            out["faces_np"] = [int(m.stats()["np"]) for m in g.members]
+            g.close()
+            out["faces_ms"].append(ms)
+            out["faces_mid_phases_ms"] = ph
+        if a.only == "left":
+            g = SphSlabGroup(case, np.array([0, w, ncx], np.int32))
+            ms, ph = timed(g, a.steps, a.warmup, g.members[1])
+            out["left_np"] = [int(m.stats()["np"]) for m in g.members]
+            g.close()
+            out.setdefault("left_ms", []).append(ms)
+            out["left_big_phases_ms"] = ph
         print("progress", json.dumps(out), flush=True)
-    d, o, f = min(out["domain_ms"]), min(out["one_slab_ms"]), min(out["faces_ms"])
-    out["one_slab_over_domain"] = round(o / d, 4)
-    out["faces_minus_domain_ms"] = round(f - d, 4)
+    if a.only is None:
+        d, o, f = min(out["domain_ms"]), min(out["one_slab_ms"]), min(out["faces_ms"])
+        out["one_slab_over_domain"] = round(o / d, 4)
+        out["faces_minus_domain_ms"] = round(f - d, 4)
     print(json.dumps(out), flush=True)
 
 

@@ -74,6 +74,13 @@ EXT_CASES = {
     "symplectic_shift_full_tfs_dp0.025": (0.025, 2, 2, 60, (1, 20, 60), (1, "0.1", 3, "-2", "2.75")),
     "verlet_lamsps_shift_nofixed_dp0.03": (0.03, 1, 0, 45, (1, 41, 45), (2, "1e-6", 2, "-2", "1.5")),
 }
+# the same options with CellMode=half (-cellmode:half: cells of h, 5x5 rows; the npz
+# carries cellmode = 2)
+EXT_HALF_CASES = {
+    "verlet_lamsps_ddt2_half_dp0.025": (0.025, 1, 2, 60, (1, 20, 60), (2, "1e-6", 0, "-2", "0")),
+    "symplectic_shift_full_tfs_half_dp0.025": (0.025, 2, 2, 60, (1, 20, 60), (1, "0.1", 3, "-2", "2.75")),
+    "verlet_lamsps_shift_nofixed_half_dp0.03": (0.03, 1, 0, 45, (1, 41, 45), (2, "1e-6", 2, "-2", "1.5")),
+}
 # The same physics from a STIRRED state (restart fixtures): a dam break at rest has no
 # velocity gradient (no SPS stress) and no shifting displacement (|v| = 0) in its first
 # steps, so these start from the generated case with every fluid particle given the smooth
@@ -178,7 +185,7 @@ def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=(), dim=3, noise=F
         shutil.rmtree(tmp)
 
 
-def run_ext(exe, dp, step, ddt, nsteps, ext, tmp, tag):
+def run_ext(exe, dp, step, ddt, nsteps, ext, tmp, tag, extra=()):
     tv, visco, sh, coef, tfs = ext
     d = os.path.join(tmp, "case")
     os.makedirs(d, exist_ok=True)
@@ -186,7 +193,7 @@ def run_ext(exe, dp, step, ddt, nsteps, ext, tmp, tag):
                            "1", "3", str(tv), visco, str(sh), coef, tfs], stdout=subprocess.DEVNULL)
     out = os.path.join(tmp, "out_" + tag)
     subprocess.check_call([exe, os.path.join(d, "CaseDambreak"), out, "-nsteps:%d" % nsteps, "-svsteps:1",
-                           "-saveposdouble:1", "-sv:binx", "-svres:0"], stdout=subprocess.DEVNULL)
+                           "-saveposdouble:1", "-sv:binx", "-svres:0"] + list(extra), stdout=subprocess.DEVNULL)
     return out
 
 
@@ -262,12 +269,12 @@ def make_stir(name, dp, step, ddt, nsteps, keep, ext, stir, noise):
         shutil.rmtree(tmp)
 
 
-def make_ext(name, dp, step, ddt, nsteps, keep, ext, noise):
+def make_ext(name, dp, step, ddt, nsteps, keep, ext, noise, extra=()):
     tmp = tempfile.mkdtemp(prefix="golden_")
     try:
-        out = run_ext(os.path.join(REF, "DualSPHysics5.2CPU_ref"), dp, step, ddt, nsteps, ext, tmp, "fast")
+        out = run_ext(os.path.join(REF, "DualSPHysics5.2CPU_ref"), dp, step, ddt, nsteps, ext, tmp, "fast", extra)
         outs = run_ext(os.path.join(REF, "DualSPHysics5.2CPU_strict"), dp, step, ddt, nsteps, ext, tmp,
-                       "strict") if noise else None
+                       "strict", extra) if noise else None
         arrays, times = {}, []
         fn = os.path.join(tmp, "p.bin")
         for part in range(nsteps + 1):
@@ -291,6 +298,8 @@ def make_ext(name, dp, step, ddt, nsteps, keep, ext, noise):
         arrays["dt"] = np.diff(np.array(times))
         arrays["meta"] = np.array([dp, step, ddt, nsteps], np.float64)
         arrays["ext"] = np.array([float(v) for v in ext], np.float64)
+        if "-cellmode:half" in extra:
+            arrays["cellmode"] = np.int32(2)
         np.savez_compressed(os.path.join(ROOT, "tests", "golden", name + ".npz"), **arrays)
         print(name, "ok", os.path.getsize(os.path.join(ROOT, "tests", "golden", name + ".npz")),
               {k: arrays[k] for k in arrays if k.startswith("noise")})
@@ -315,6 +324,10 @@ if __name__ == "__main__":
         if a.only and a.only != name:
             continue
         make_ext(name, *spec, a.noise)
+    for name, spec in EXT_HALF_CASES.items():
+        if a.only and a.only != name:
+            continue
+        make_ext(name, *spec, a.noise, extra=("-cellmode:half",))
     for name, spec in STIR_CASES.items():
         if a.only and a.only != name:
             continue

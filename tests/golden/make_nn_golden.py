@@ -48,17 +48,30 @@ CASES = {
     # SPH gradients with artificial viscosity: the artificial term is the Morris pass's (bound p2
     # with dv = 2 v1), phase sound speeds
     "sph_ver_art_cs_dp0.025": (0.025, 0.2, 0.5, 2.75, 2, 1, 2, 0, 20.0, 1, 45, (1, 41, 45)),
+    # CellMode=half (-cellmode:half: cells of h, 5x5 rows; the npz carries cellmode = 2)
+    "sym_lam_half_dp0.02": (0.02, 0.2, 0.5, 2.75, 1, 2, 3, 3, 0.0, 2, 60, (1, 10, 60), ("-cellmode:half",)),
+    "sph_sym_consteq_cs_half_dp0.025": (0.025, 0.2, 0.5, 2.75, 2, 3, 3, 3, 20.0, 2, 30, (1, 30),
+                                        ("-cellmode:half",)),
+    "ver_art_ddt1_cs_half_dp0.025": (0.025, 0.2, 0.5, 2.75, 1, 1, 1, 1, 20.0, 1, 45, (1, 41, 45),
+                                     ("-cellmode:half",)),
+    # a floating box (gennn_ref float 1: rhopbody 800 on the phase-0 layer; the npz carries
+    # floating = 1): floating mass, the DDT and shifting rules of floating p1 / p2
+    "ft_sym_lam_ddt3_dp0.025": (0.025, 0.4, 0.5, 2.75, 1, 2, 3, 3, 0.0, 2, 60, (1, 20, 60), (), 1),
+    "ft_ver_art_ddt1_nobound_cs_dp0.025": (0.025, 0.4, 0.5, 2.75, 1, 1, 1, 1, 20.0, 1, 45, (1, 41, 45), (), 1),
+    "ft_sph_sym_consteq_cs_dp0.025": (0.025, 0.4, 0.5, 2.75, 2, 3, 3, 3, 20.0, 2, 30, (1, 30), (), 1),
 }
 
 
 def run_case(exe, spec, tmp, nsteps):
     dp, width, scale, tfs, vg, tv, ddt, sh, cs, step = spec[:10]
+    ft = str(spec[13]) if len(spec) > 13 else "0"
     subprocess.check_call([os.path.join(REF, "gennn_ref"), repr(dp), tmp, repr(width), repr(scale), "5",
-                           "CaseNN", repr(tfs), str(vg), str(tv), str(ddt), str(sh), repr(cs), str(step)],
+                           "CaseNN", repr(tfs), str(vg), str(tv), str(ddt), str(sh), repr(cs), str(step), ft],
                           stdout=subprocess.DEVNULL)
     out = os.path.join(tmp, "out_" + os.path.basename(exe))
+    extra = list(spec[12]) if len(spec) > 12 else []
     subprocess.check_call([exe, os.path.join(tmp, "CaseNN"), out, "-nsteps:%d" % nsteps, "-svsteps:1",
-                           "-saveposdouble:1", "-sv:binx", "-svres:0"], stdout=subprocess.DEVNULL)
+                           "-saveposdouble:1", "-sv:binx", "-svres:0"] + extra, stdout=subprocess.DEVNULL)
     return out
 
 
@@ -91,6 +104,10 @@ def make(name, spec, noise):
         arrays["times"] = np.array(times)
         arrays["dt"] = np.diff(np.array(times))
         arrays["meta"] = np.array(list(spec[:11]), np.float64)
+        if len(spec) > 12 and "-cellmode:half" in spec[12]:
+            arrays["cellmode"] = np.int32(2)
+        if len(spec) > 13 and spec[13]:
+            arrays["floating"] = np.int32(1)
         fn = os.path.join(HERE, "nn_%s.npz" % name)
         np.savez_compressed(fn, **arrays)
         print(name, "ok", os.path.getsize(fn), {k: arrays[k] for k in arrays if k.startswith("noise")})

@@ -23,6 +23,8 @@ NN_GOLDENS = ("sym_lam_dp0.02", "sym_consteq_cs_dp0.025", "ver_art_ddt1_cs_dp0.0
 # VelocityGradientType 2 (SPH velocity gradients: k_nn_tiled<4|5> then k_nn_visc)
 NN_SPH_GOLDENS = ("sph_sym_lam_dp0.02", "sph_sym_consteq_cs_dp0.025", "sph_ver_lam_ddt1_nobound_dp0.025",
                   "sph_ver_art_cs_dp0.025")
+# CellMode=half (-cellmode:half, JCellSearch_inline.h:38-44: cells of h, 5x5 rows)
+NN_HALF_GOLDENS = ("sym_lam_half_dp0.02", "sph_sym_consteq_cs_half_dp0.025", "ver_art_ddt1_cs_half_dp0.025")
 # ulp-level floors (pos m, vel m/s, rho kg/m3): 10x noise of exactly 0 is no tolerance
 FLOOR = (2e-10, 2e-8, 2.5e-3)
 
@@ -35,16 +37,25 @@ def case_of(g):
     dp, width, scale, tfs, vg, tv, ddt, sh, cs, step, _ = g["meta"]
     return WetDambreakNNCase(float(dp), width=float(width), scale=float(scale), shift_tfs=float(tfs),
                              tvisco=int(tv), tdensity=int(ddt), shift_mode=int(sh), csound=float(cs),
-                             step_algorithm=int(step), velgrad=int(vg))
+                             step_algorithm=int(step), velgrad=int(vg),
+                             cellmode=int(g["cellmode"]) if "cellmode" in g.files else 1)
+
+
+# CellMode=half: 25 rows per pass drained in 12 mirrored pairs + the own row, against the
+# reference's z-major order of 25 rows, moves the step-1 positions by up to ~3e-10 m (the
+# sums' rounding; fast-math vs strict builds of the reference keep the order, so their noise
+# floor does not show this)
+FLOOR_HALF = (5e-10, 2e-8, 2.5e-3)
 
 
 def nn_tol(g, k):
     n = g["noise_%d" % k]
-    return tuple(max(10.0 * float(n[i]), FLOOR[i]) for i in range(3))
+    fl = FLOOR_HALF if "cellmode" in g.files and int(g["cellmode"]) == 2 else FLOOR
+    return tuple(max(10.0 * float(n[i]), fl[i]) for i in range(3))
 
 
 # ---- CPU ----------------------------------------------------------------------------------
-@pytest.mark.parametrize("name", NN_GOLDENS + NN_SPH_GOLDENS)
+@pytest.mark.parametrize("name", NN_GOLDENS + NN_SPH_GOLDENS + NN_HALF_GOLDENS)
 def test_goldens_present_with_noise_floor(name):
     g = load_nn(name)
     ks = steps(g)
@@ -126,7 +137,7 @@ def check(got, ref, tol, k):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", NN_GOLDENS + NN_SPH_GOLDENS)
+@pytest.mark.parametrize("name", NN_GOLDENS + NN_SPH_GOLDENS + NN_HALF_GOLDENS)
 def test_gpu_nn_steps_match_reference_parts(name):
     g = load_nn(name)
     s = gpu(case_of(g))
@@ -152,7 +163,8 @@ def test_gpu_nn_dt_trace_matches_reference():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nslabs,name", [(2, "sym_lam_dp0.02"), (2, "sph_sym_lam_dp0.02"), (3, "sph_sym_consteq_cs_dp0.025")])
+@pytest.mark.parametrize("nslabs,name", [(2, "sym_lam_dp0.02"), (2, "sph_sym_lam_dp0.02"), (3, "sph_sym_consteq_cs_dp0.025"),
+                                         (2, "sym_lam_half_dp0.02"), (3, "sph_sym_consteq_cs_half_dp0.025")])
 def test_gpu_nn_slabs_match_reference_parts(nslabs, name):
     """Slabs; with SPH gradients the first pass's eta / tau of the face columns go to the
     neighbours' ghosts before the second pass (NNFaceExchange)."""
@@ -199,3 +211,58 @@ def test_xml_loader_reads_the_nn_case(tmp_path, velgrad):
     assert x.case_def() == c.case_def()
     assert np.array_equal(x.code, c.code) and np.array_equal(x.idp, c.idp)
     assert np.array_equal(x.pos, c.pos)
+
+
+# ---- NN multiphase with a floating body (JSphCpu_NN_FDA.cpp:89-93, 159-164, 203-215) ------
+# gennn_ref float 1 (a box of rhopbody 800 on the phase-0 layer); make_nn_golden.py ft_* runs
+# the REFERENCE v5.0 NN solver on it.  The case comes back through the run driver's loader
+# (xmlcase), which configures the body as JSph::LoadCaseConfig does.
+NN_FT_GOLDENS = ("ft_sym_lam_ddt3_dp0.025", "ft_ver_art_ddt1_nobound_cs_dp0.025", "ft_sph_sym_consteq_cs_dp0.025")
+
+
+def ft_case(g, tmp_path):
+    from dualsphysics_multilayer_amd.xmlcase import XmlCase
+
+    exe = os.path.join(REF, "gennn_ref")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref not built")
+    dp, width, scale, tfs, vg, tv, ddt, sh, cs, step, _ = g["meta"]
+    subprocess.check_call([exe, repr(float(dp)), str(tmp_path), repr(float(width)), repr(float(scale)), "5", "CaseNN",
+                           repr(float(tfs)), str(int(vg)), str(int(tv)), str(int(ddt)), str(int(sh)), repr(float(cs)),
+                           str(int(step)), "1"], stdout=subprocess.DEVNULL)
+    return XmlCase(str(tmp_path / "CaseNN"))
+
+
+@pytest.mark.parametrize("name", NN_FT_GOLDENS)
+def test_ft_goldens_and_case(name, tmp_path):
+    g = load_nn(name)
+    assert int(g["floating"]) == 1 and all(("noise_%d" % k) in g.files for k in steps(g))
+    x = ft_case(g, tmp_path)
+    assert len(x.floatings) == 1 and x.rheology == 2
+    # the body sits in the phase-0 layer: its particles replace fluid lattice points
+    assert x.floatings[0]["count"] == 343
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NN_FT_GOLDENS)
+def test_gpu_nn_floating_match_reference_parts(name, tmp_path):
+    g = load_nn(name)
+    s = gpu(ft_case(g, tmp_path))
+    done = 0
+    for k in steps(g):
+        s.run(k - done)
+        done = k
+        ref = snapshot(g, k)
+        check(by_idp(s.particles()), ref, nn_tol(g, k), k)
+        assert abs(s.stats()["time"] - float(ref["time"])) <= 1e-9 * max(1.0, k)
+
+
+def test_nn_floating_body_moves_in_fixture(tmp_path):
+    """The reference integrates the body on the NN interaction's forces: it leaves its start
+    position within the fixture's steps (so the GPU test above sees the body dynamics)."""
+    g = load_nn(NN_FT_GOLDENS[0])
+    f = ft_case(g, tmp_path).floatings[0]
+    ref, start = snapshot(g, steps(g)[-1]), snapshot(g, steps(g)[0])
+    sel = (ref["idp"] >= f["idbegin"]) & (ref["idp"] < f["idbegin"] + f["count"])
+    assert sel.sum() == f["count"]
+    assert np.abs(ref["pos"][sel] - start["pos"][sel]).max() > 1e-6
