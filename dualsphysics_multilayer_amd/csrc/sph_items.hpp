@@ -178,9 +178,10 @@ __device__ __forceinline__ void items_scan(const ItemBuild& b, unsigned* s) {
   const unsigned nt = blockDim.x, nw = nt / 64, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   unsigned* wsum = s;
   unsigned* mark = s + nw;  // offsets where list A's bound rows, list B and its bound rows begin
-  if (threadIdx.x < 8) {    // the interaction's item queues start over
-    b.qa[threadIdx.x * QSTRIDE] = 0u;
-    if (nl == 2) b.qb[threadIdx.x * QSTRIDE] = 0u;
+  if (threadIdx.x < 8 * QCTR_COPIES) {  // the interactions' item queues (every copy) start over
+    const unsigned q = (threadIdx.x >> 3) * QCTR_WORDS + (threadIdx.x & 7) * QSTRIDE;
+    b.qa[q] = 0u;
+    if (nl == 2) b.qb[q] = 0u;
   }
   // thread t scans the contiguous chunk [t per, (t+1) per)
   const unsigned per = (n + nt - 1) / nt, i0 = threadIdx.x * per, i1 = min(i0 + per, n);
@@ -206,15 +207,15 @@ __device__ __forceinline__ void items_scan(const ItemBuild& b, unsigned* s) {
   }
   if (threadIdx.x == nt - 1) mark[3] = run;  // the total
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned tot = mark[3], na = nl == 2 ? mark[1] : tot;
-    b.qa[QCTR_NITEMS] = na;
-    b.qa[QCTR_NITEMS + 1] = na - mark[0];  // the bound rows' items: the list's tail (ItemGroups)
-    b.qa[QCTR_NITEMS + 2] = 0u;
+  if (threadIdx.x < QCTR_COPIES) {
+    const unsigned tot = mark[3], na = nl == 2 ? mark[1] : tot, c = threadIdx.x * QCTR_WORDS + QCTR_NITEMS;
+    b.qa[c] = na;
+    b.qa[c + 1] = na - mark[0];  // the bound rows' items: the list's tail (ItemGroups)
+    b.qa[c + 2] = 0u;
     if (nl == 2) {
-      b.qb[QCTR_NITEMS] = tot - na;
-      b.qb[QCTR_NITEMS + 1] = tot - mark[2];
-      b.qb[QCTR_NITEMS + 2] = na;  // the second list follows the first in the item array
+      b.qb[c] = tot - na;
+      b.qb[c + 1] = tot - mark[2];
+      b.qb[c + 2] = na;  // the second list follows the first in the item array
     }
   }
 }

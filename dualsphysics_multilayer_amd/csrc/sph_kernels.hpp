@@ -212,8 +212,13 @@ constexpr int QSTRIDE = 32;
 // Line 9 holds the list's item counts {all, bound, first item} (k_items_scan; ItemGroups
 // reads them), so one counter block describes one item list.
 constexpr size_t QCTR_QUEUE_BYTES = 9 * QSTRIDE * sizeof(unsigned);  // what a re-run zeroes
-constexpr size_t QCTR_BYTES = 10 * QSTRIDE * sizeof(unsigned);
+constexpr int QCTR_WORDS = 10 * QSTRIDE;
 constexpr int QCTR_NITEMS = 9 * QSTRIDE;
+// A list's counter blocks come in QCTR_COPIES copies (QCTR_WORDS apart), all set up by the
+// item build, so that the interactions on one item list (a Symplectic step's predictor and
+// corrector, NN's two passes) each start on fresh queues without a memset launch.
+constexpr int QCTR_COPIES = 2;
+constexpr size_t QCTR_BYTES = size_t(QCTR_COPIES) * QCTR_WORDS * sizeof(unsigned);
 // Tiled fluid interaction (sph_interaction_tiled.hip); its per-divide item list is built
 // by sph_items.hpp (launch_items, or the incremental divide's push launch + launch_items_write).
 // With floating bodies (ftmassp != nullptr) the staged p2 records carry their mass ratio

@@ -298,12 +298,9 @@ void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartA
   PackArgs q;
   q.fcnt[0] = q.fcnt[1] = nullptr;
   q.W = g.xown0;
-  if (faces) {
+  if (faces) {  // zero on entry: k_face_scan / k_unpack_finish of the last exchange reset them
     q.fcnt[0] = faces->msg[0] + FMSG_HDR;
     q.fcnt[1] = faces->msg[1] + FMSG_HDR;
-    (void)hipMemsetAsync(q.fcnt[0], 0, 4 * size_t(faces->nfb), stm);
-    (void)hipMemsetAsync(q.fcnt[1], 0, 4 * size_t(faces->nfb), stm);
-    (void)hipMemsetAsync(cnt->ghosts, 0, sizeof(cnt->ghosts), stm);
   }
   q.a = a;
   q.g = g;
@@ -347,8 +344,9 @@ __global__ __launch_bounds__(FS_BS) void k_face_scan(SlabFaces f, int hl, int hr
   __shared__ unsigned carry;
   const int m = int(blockIdx.x);  // send L, send R, receive L, receive R
   if ((m & 1) ? !hr : !hl) return;
-  const unsigned* cnt = f.msg[m] + FMSG_HDR;
+  unsigned* cnt = f.msg[m] + FMSG_HDR;
   unsigned* pre = f.pre[m];
+  const bool reset = m < 2;  // a send message's counts: zeroed for the next exchange once read
   const unsigned n = f.nfb, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (threadIdx.x == 0) carry = 0;
   for (unsigned t0 = 0; t0 < n; t0 += FS_TILE) {
@@ -356,6 +354,7 @@ __global__ __launch_bounds__(FS_BS) void k_face_scan(SlabFaces f, int hl, int hr
     for (int k = 0; k < FS_PT; k++) {
       const unsigned i = t0 + k * FS_BS + threadIdx.x;
       v[k * FS_BS + threadIdx.x] = i < n ? cnt[i] : 0u;
+      if (reset && i < n) cnt[i] = 0u;
     }
     __syncthreads();
     unsigned x[FS_PT], sum = 0;
@@ -521,10 +520,14 @@ __global__ __launch_bounds__(256) void k_unpack(UnpackArgs u) {
   }
 }
 
-__global__ void k_unpack_finish(DevScalars* __restrict__ sc, const SlabCounts* __restrict__ cnt, unsigned np,
+// The exchange's last kernel: the new counts, and the accumulated pack counts zeroed for the
+// next exchange (in place of memset launches).
+__global__ void k_unpack_finish(DevScalars* __restrict__ sc, SlabCounts* __restrict__ cnt, unsigned np,
                                 unsigned nm, unsigned ng) {
   sc->np = np + nm + ng;
   sc->nown = cnt->nkeep + nm;
+  cnt->nkeep = 0u;
+  cnt->ghosts[0] = cnt->ghosts[1] = 0u;
 }
 
 void launch_slab_unpack(hipStream_t stm, DevScalars* sc, const SlabRec* mig, unsigned nm, const SlabGhost* gh,

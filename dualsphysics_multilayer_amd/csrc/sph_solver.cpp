@@ -579,13 +579,19 @@ void SphGpuSingle::AllocFixed() {
   pairs_ = (unsigned long long*)dmalloc(8 * 6);
   folded_ = (unsigned*)dmalloc(4 * 8);
   slabcnt_ = (SlabCounts*)dmalloc(sizeof(SlabCounts));
+  // the accumulated counts (nkeep, ghosts) start at zero; k_unpack_finish zeroes them again
+  // at the end of every exchange
+  check_hip(hipMemset(slabcnt_, 0, sizeof(SlabCounts)), "zero slab counts");
   if (slab()) {
     // face messages and their prefixes (the ghost exchange after the divide); the second
     // item list and its counters
     faces_.W = ghost_width(C);
     faces_.nfb = 2u * unsigned(G.ncy) * unsigned(G.ncz) * unsigned(faces_.W);
     for (int k = 0; k < 4; k++) {
+      // the send messages' face-box counts accumulate in k_pack_count from zero; k_face_scan
+      // zeroes them again once it has their prefixes
       faces_.msg[k] = (unsigned*)dmalloc(4 * (size_t(FMSG_HDR) + faces_.nfb));
+      check_hip(hipMemset(faces_.msg[k], 0, 4 * (size_t(FMSG_HDR) + faces_.nfb)), "zero face messages");
       faces_.pre[k] = (unsigned*)dmalloc(4 * (size_t(faces_.nfb) + 1));
     }
     qctrf_ = (unsigned*)dmalloc(QCTR_BYTES);
@@ -947,8 +953,7 @@ void SphGpuSingle::Exchange() {
     launch_slab_pack(stream, cap_, sc_, cur_, G, K, C.dom_posmin, hl, hr, withm1, withpre, packtiles_, slabcnt_,
                      send_, normal_, casenpb_, &faces_);
   };
-  check_hip(hipMemsetAsync(slabcnt_, 0, sizeof(SlabCounts), stream), "exchange: reset counts");
-  pack();
+  pack();  // (its accumulated counts were zeroed by the last exchange's kernels: no memset launches)
   const size_t mb = 4 * (size_t(FMSG_HDR) + faces_.nfb);
   transport_->exchange(faces_.msg[0], hl ? mb : 0, faces_.msg[1], hr ? mb : 0, faces_.msg[2], hl ? mb : 0,
                        faces_.msg[3], hr ? mb : 0, stream);
@@ -987,8 +992,11 @@ void SphGpuSingle::Exchange() {
     check_hip(hipMalloc(&sendmbuf_, 2 * sizeof(SlabRec) * send_.mcap), "hipMalloc migrant send buffers");
     send_.ml = (SlabRec*)sendmbuf_;
     send_.mr = send_.ml + send_.mcap;
-    check_hip(hipMemsetAsync(&slabcnt_->nkeep, 0, sizeof(unsigned), stream), "exchange: reset nkeep");
-    pack();  // the same counts (the face messages already sent are unchanged)
+    // the counts accumulate again: start them over (the face messages already sent are unchanged)
+    check_hip(hipMemsetAsync(&slabcnt_->nkeep, 0, sizeof(unsigned) * 3, stream), "exchange: reset nkeep, ghosts");
+    for (int k = 0; k < 2; k++)
+      check_hip(hipMemsetAsync(faces_.msg[k] + FMSG_HDR, 0, 4 * size_t(faces_.nfb), stream), "exchange: reset faces");
+    pack();
   }
   const unsigned long long rgl = hl ? c.recvl[0] : 0, rgr = hr ? c.recvr[0] : 0;
   const unsigned long long rml = hl ? c.recvl[1] : 0, rmr = hr ? c.recvr[1] : 0;
@@ -1207,7 +1215,7 @@ void SphGpuSingle::RunCellDivide() {
   std::swap(cur_, alt_);
   // this slab's ghost records for the neighbours, from its sorted face columns
   if (ghosts) launch_ghost_pack(stream, sc_, faces_, G, begincell_, cur_, poscell_, send_, unsigned(xg_sl_), unsigned(xg_sr_));
-  if (tiled_) qfresh_ = true;
+  qpass_ = 0;
   if (ghosts) {
     if (overlap) {
       if (!ev_div_) check_hip(hipEventCreateWithFlags(&ev_div_, hipEventDisableTiming), "hipEventCreate");
@@ -1219,6 +1227,16 @@ void SphGpuSingle::RunCellDivide() {
   }
   if (nftp_) launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_, K, G);
   TimedEnd(2);
+}
+
+unsigned SphGpuSingle::NextQueueCopy() {
+  const unsigned c = qpass_ % QCTR_COPIES;
+  if (++qpass_ > unsigned(QCTR_COPIES)) {  // beyond the copies the item build zeroed
+    check_hip(hipMemsetAsync(qctr_ + c * QCTR_WORDS, 0, QCTR_QUEUE_BYTES, stream), "zero work counters");
+    if (ghost_split_)
+      check_hip(hipMemsetAsync(qctrf_ + c * QCTR_WORDS, 0, QCTR_QUEUE_BYTES, stream), "zero work counters");
+  }
+  return c * QCTR_WORDS;
 }
 
 void SphGpuSingle::Interaction_Forces(int interstep) {
@@ -1239,25 +1257,21 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
     }
     TimedEnd(3);
   }
-  if (tiled_ && !qfresh_) {  // a second interaction on the same item list: queues start over
-    check_hip(hipMemsetAsync(qctr_, 0, QCTR_QUEUE_BYTES, stream), "zero work counters");
-    if (ghost_split_) check_hip(hipMemsetAsync(qctrf_, 0, QCTR_QUEUE_BYTES, stream), "zero work counters");
-  }
-  qfresh_ = false;
+  const unsigned qc = tiled_ ? NextQueueCopy() : 0u;
+  unsigned *qa = qctr_ + qc, *qf = qctrf_ ? qctrf_ + qc : nullptr;
   if (nn_) {
     // NN multiphase (sph_nn.hip); the shifting sums only where they are applied: the
     // corrector (the predictor's RunShifting result is never used, shift=false in
     // ComputeSymplecticPre) and Verlet
     TimedBegin(0);
-    launch_nn_tiled(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, cur_.code, begincell_,
+    launch_nn_tiled(stream, nblocks_tiled_, sc_, items_, qa, poscell_, cur_.velrhop, press_, cur_.code, begincell_,
                     G, K, phasek_, arace_, shiftpos_, shift_ && interstep != 2, viscoeta_, tau_, ftmassp_);
     if (nnsph_) {
       // SPH velocity gradients: the viscous force is a second pass over the neighbours,
       // reading their effective viscosities / stress tensors (JSphCpu_NN_SPH.cpp:671-696)
       if (slab() && C.tvisco != SPH_VISCO_ARTIFICIAL && (transport_->has_left() || transport_->has_right()))
         NNFaceExchange();
-      check_hip(hipMemsetAsync(qctr_, 0, QCTR_QUEUE_BYTES, stream), "zero work counters");
-      launch_nn_visc(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, cur_.code, viscoeta_, tau_,
+      launch_nn_visc(stream, nblocks_tiled_, sc_, items_, qctr_ + NextQueueCopy(), poscell_, cur_.velrhop, cur_.code, viscoeta_, tau_,
                      begincell_, G, K, phasek_, arace_, ftmassp_);
     }
   } else if (ext_) {
@@ -1265,33 +1279,33 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
     // owners' from the last interaction) first
     if (sps_ && slab() && (transport_->has_left() || transport_->has_right())) NNFaceExchange();
     TimedBegin(0);
-    launch_fluid_ext(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, cur_.code, ftmassp_,
+    launch_fluid_ext(stream, nblocks_tiled_, sc_, items_, qa, poscell_, cur_.velrhop, press_, cur_.code, ftmassp_,
                      cur_.tau, begincell_, G, K, arace_, shiftpos_, taunew_, interstep != 2);
     if (sps_) std::swap(cur_.tau, taunew_);
   } else if (tiled_) {
     // The tiled kernel writes the arace of every owned particle (skipped boundary items
-    // get ar = 0) and resets its own work counters at exit (zeroed once at allocation).
+    // get ar = 0); its work queues are the copy NextQueueCopy picked.
     TimedBegin(0);  // the timed interval is the interaction kernel alone (rocprof's per-kernel average)
     if (ghost_pending_) {
       // Slab: the interior items now, the ghost records in flight on the exchange stream;
       // there the face items follow their arrival.  The interior kernel leaves a few block
       // slots free so that the transfer and scatter kernels start at once.
-      launch_fluid_tiled(stream, nblocks_tiled_ - 64, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, begincell_,
+      launch_fluid_tiled(stream, nblocks_tiled_ - 64, sc_, items_, qa, poscell_, cur_.velrhop, press_, begincell_,
                          G, K, arace_, cur_.code, ftmassp_);
       if (!xstream_) check_hip(hipStreamCreateWithFlags(&xstream_, hipStreamNonBlocking), "hipStreamCreate");
       if (!ev_ghost_) check_hip(hipEventCreateWithFlags(&ev_ghost_, hipEventDisableTiming), "hipEventCreate");
       check_hip(hipStreamWaitEvent(xstream_, ev_div_, 0), "ghosts: wait divide");
       GhostTransfer(xstream_);
-      launch_fluid_tiled(xstream_, nblocks_tiled_, sc_, items_, qctrf_, poscell_, cur_.velrhop, press_, begincell_, G,
+      launch_fluid_tiled(xstream_, nblocks_tiled_, sc_, items_, qf, poscell_, cur_.velrhop, press_, begincell_, G,
                          K, arace_, cur_.code, ftmassp_);
       check_hip(hipEventRecord(ev_ghost_, xstream_), "ghosts: event");
       check_hip(hipStreamWaitEvent(stream, ev_ghost_, 0), "ghosts: join");
       ghost_pending_ = false;
     } else {
-      launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qctr_, poscell_, cur_.velrhop, press_, begincell_, G, K,
+      launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qa, poscell_, cur_.velrhop, press_, begincell_, G, K,
                          arace_, cur_.code, ftmassp_);
       if (ghost_split_)  // the ghosts are in: the face items right after
-        launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qctrf_, poscell_, cur_.velrhop, press_, begincell_,
+        launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qf, poscell_, cur_.velrhop, press_, begincell_,
                            G, K, arace_, cur_.code, ftmassp_);
     }
   } else {

@@ -180,7 +180,9 @@ class SphGpuSingle {
   unsigned* qctrf_ = nullptr;
   bool ghost_split_ = false;      // the last item build made two lists
   unsigned nblocks_tiled_ = 2048;
-  bool qfresh_ = false;  // the tiled kernels' work queues were zeroed by the last item build
+  unsigned qpass_ = 0;  // interactions run on the current item list (the build zeroed QCTR_COPIES)
+  // The offset of the counter-block copy the next interaction on the item list runs on.
+  unsigned NextQueueCopy();
   bool tiled_ = true;             // SPH_INTERACTION=simple selects the one-lane-per-particle kernel
   SortScratch sort_;
   // incremental divide (single domain, after the first divide; SPH_DIVIDE=full disables it)

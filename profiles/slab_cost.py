@@ -67,6 +67,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--repeat", type=int, default=2, help="alternating repeats of the three runs")
+    ap.add_argument("--overlap", type=int, default=1, help="slab ghost overlap on (1) / off (0)")
     ap.add_argument("--only", choices=("domain", "one_slab", "faces", "left"), default=None,
                     help="one of the runs (e.g. under rocprofv3); left: [0, w) | [w, ncx), the big slab with one "
                          "face in the water, whose face launch runs after the strip's (a trace isolates it)")
@@ -76,6 +77,7 @@ def main():
     W = 1  # full cells, DBC: one ghost column per face
     w = 2 * W
     out = {"workload": a.workload, "np": int(case.np), "ncx": ncx, "steps": a.steps, "strip_columns": w,
+           "overlap": a.overlap,
            "domain_ms": [], "one_slab_ms": [], "faces_ms": [], "domain_phases_ms": None, "faces_mid_phases_ms": None}
     for _ in range(a.repeat):
         if a.only in (None, "domain"):
@@ -91,6 +93,7 @@ def main():
             out["one_slab_ms"].append(ms)
         if a.only in (None, "faces"):
             g = SphSlabGroup(case, np.array([0, w, ncx - w, ncx], np.int32))
+            g.set_overlap(bool(a.overlap))
             ms, ph = timed(g, a.steps, a.warmup, g.members[1])
             out["faces_np"] = [int(m.stats()["np"]) for m in g.members]
             g.close()
@@ -98,6 +101,7 @@ def main():
             out["faces_mid_phases_ms"] = ph
         if a.only == "left":
             g = SphSlabGroup(case, np.array([0, w, ncx], np.int32))
+            g.set_overlap(bool(a.overlap))
             ms, ph = timed(g, a.steps, a.warmup, g.members[1])
             out["left_np"] = [int(m.stats()["np"]) for m in g.members]
             g.close()
