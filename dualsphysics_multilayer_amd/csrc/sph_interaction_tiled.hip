@@ -42,7 +42,7 @@ __global__ __launch_bounds__(1024) void k_items_scan(ItemBuild b) {
 }
 
 ItemBuild make_item_build(const unsigned* begincell, DivGrid g, unsigned* rowtmp, uint4* items, unsigned* qctr,
-                          int scelldiv, const int* xr, unsigned* qctr2) {
+                          int scelldiv, const int* xr, unsigned* qctr2, uint4* rowitems, unsigned ricap) {
   ItemBuild b;
   b.bc = begincell;
   b.g = g;
@@ -53,6 +53,8 @@ ItemBuild make_item_build(const unsigned* begincell, DivGrid g, unsigned* rowtmp
   b.nrows2 = 2u * unsigned(g.ncy) * unsigned(g.ncz);
   b.counts = rowtmp;
   b.items = items;
+  b.rowitems = rowitems;
+  b.ricap = ricap;
   b.qa = qctr;
   b.qb = qctr2;
   b.nblocks = (b.nrows2 + IR_WAVES - 1) / IR_WAVES;

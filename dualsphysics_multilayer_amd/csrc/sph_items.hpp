@@ -8,6 +8,11 @@
 // launch cost more than the launch: one device-scope atomic per count block on one line,
 // ~4000 of them at 1M, serialise across the XCDs — the divide phase went 0.085 -> 0.105 ms.)
 //
+// The count pass also stages each row's items in a slot of `ricap` items per (list, row)
+// (rowitems); the write pass then copies the staged items to their offsets (one wave per
+// row, a coalesced copy) and walks again only a row whose items overflowed its slot.  cfg2
+// 1M: the write pass 14.4 -> see DESIGN.md §4.
+//
 // Rows [0,nrows) are fluid rows (fluid p1), rows [nrows,2*nrows) bound rows (bound p1,
 // DBC).  An item is a run of <= TB consecutive particles of one row, cut earlier only where
 // it would span more than tmaxc x-cells; items may start and end inside a cell.  One wave per
@@ -15,6 +20,8 @@
 // write passes run the same walk, so the list is deterministic and in spatial (z, y, x)
 // order, fluid items first.
 #pragma once
+#include <algorithm>
+
 #include "sph_kernels.hpp"
 #include "sph_tiled.hpp"
 
@@ -35,8 +42,10 @@ struct ItemBuild {
   DivGrid g;
   int tmaxc;            // max x-cells per item (TMAXCELLS / TMAXCELLS_HALF)
   ItemRanges xr;
-  unsigned* counts;     // [nl][nrows2] row counts, scanned in place into offsets
+  unsigned* counts;     // [nl][nrows2] row counts, scanned in place into offsets (+ the total)
   uint4* items;
+  uint4* rowitems;      // [nl][nrows2][ricap] the count pass's items of each row
+  unsigned ricap;       // staged items per (list, row)
   unsigned* qa;         // counter block of list A (its item counts + work queues)
   unsigned* qb;         // list B (nl == 2)
   unsigned nrows2;      // 2 ncy ncz
@@ -83,9 +92,13 @@ __device__ __forceinline__ void items_row(const ItemBuild& b, unsigned r, unsign
   for (int list = 0; list < xr.nl; list++) {
     uint4* out = WRITE ? b.items + b.counts[list * nrows2 + r] : nullptr;
     unsigned nitems = 0;
+    uint4* stage = WRITE ? nullptr : b.rowitems + size_t(list * nrows2 + r) * b.ricap;
     auto emit = [&](int a, int e, unsigned p, unsigned q) {
+      const uint4 it = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(e) << 16), p, q);
       if (WRITE)
-        out[nitems] = make_uint4((y | (z << 16)) | (bound ? ITEM_BOUND : 0u), unsigned(a) | (unsigned(e) << 16), p, q);
+        out[nitems] = it;
+      else if (nitems < b.ricap)
+        stage[nitems] = it;
       nitems++;
     };
     // p1 only in owned columns (slab ghosts are neighbours, never p1); each range walked on
@@ -205,7 +218,10 @@ __device__ __forceinline__ void items_scan(const ItemBuild& b, unsigned* s) {
     counts[i] = run;
     run += v;
   }
-  if (threadIdx.x == nt - 1) mark[3] = run;  // the total
+  if (threadIdx.x == nt - 1) {
+    mark[3] = run;  // the total
+    counts[n] = run;  // so that every row's count is the next offset minus its own
+  }
   __syncthreads();
   if (threadIdx.x < QCTR_COPIES) {
     const unsigned tot = mark[3], na = nl == 2 ? mark[1] : tot, c = threadIdx.x * QCTR_WORDS + QCTR_NITEMS;
@@ -220,6 +236,28 @@ __device__ __forceinline__ void items_scan(const ItemBuild& b, unsigned* s) {
   }
 }
 
+// The write pass of row r: its staged items copied to their offsets by the wave, or, when
+// a list's items overflowed the row's slot, the walk again.
+__device__ __forceinline__ void items_copy_row(const ItemBuild& b, unsigned r, unsigned* pre, unsigned short* nz) {
+  const unsigned lane = threadIdx.x & 63, nl = unsigned(b.xr.nl);
+  unsigned off[2], cnt[2];
+  bool fits = true;
+  for (unsigned list = 0; list < nl; list++) {
+    const unsigned i = list * b.nrows2 + r;
+    off[list] = b.counts[i];
+    cnt[list] = b.counts[i + 1] - off[list];
+    fits &= cnt[list] <= b.ricap;
+  }
+  if (!fits) {
+    items_row<true>(b, r, pre, nz);
+    return;
+  }
+  for (unsigned list = 0; list < nl; list++) {
+    const uint4* __restrict__ src = b.rowitems + size_t(list * b.nrows2 + r) * b.ricap;
+    for (unsigned k = lane; k < cnt[list]; k += 64) b.items[off[list] + k] = src[k];
+  }
+}
+
 // Block `blk` of a pass (IR_WAVES rows; dynamic LDS `smem` of b.lds bytes).
 template <bool WRITE>
 __device__ __forceinline__ void items_pass_block(const ItemBuild& b, unsigned blk, unsigned char* smem) {
@@ -227,17 +265,25 @@ __device__ __forceinline__ void items_pass_block(const ItemBuild& b, unsigned bl
   unsigned* pre = reinterpret_cast<unsigned*>(smem) + w * L;
   unsigned short* nz = reinterpret_cast<unsigned short*>(smem + IR_WAVES * L * sizeof(unsigned)) + w * L;
   const unsigned r = blk * IR_WAVES + w;
-  if (r < b.nrows2) items_row<WRITE>(b, r, pre, nz);
+  if (r >= b.nrows2) return;
+  if (WRITE)
+    items_copy_row(b, r, pre, nz);
+  else
+    items_row<false>(b, r, pre, nz);
 }
 
 // Host side (sph_interaction_tiled.hip).  scelldiv 1 (CellMode=full): items of <= 4 cells;
 // 2 (half): <= TMAXCELLS_HALF half-cells.  p1 in the local columns [xr[0], xr[1]),
 // [xr[2], xr[3]), [xr[4], xr[5]), each range's items on their own (nullptr: the owned
 // columns).  With qctr2: two lists in `items`, the first of range 0 (counter block qctr),
-// the second of ranges 1 and 2 after it (qctr2).  rowtmp holds 2 x 2 ncy ncz counts.
-inline size_t ITEMS_ROWTMP(int ncy, int ncz) { return 4 * size_t(ncy) * size_t(ncz); }
+// the second of ranges 1 and 2 after it (qctr2).  rowtmp holds 2 x 2 ncy ncz counts + 1;
+// rowitems 2 x 2 ncy ncz x ricap items.
+inline size_t ITEMS_ROWTMP(int ncy, int ncz) { return 4 * size_t(ncy) * size_t(ncz) + 1; }
+// Staged items per row: a row of ncx full cells holds ~ncx/4 items of 4 cells or, dense,
+// one item per 128 particles (~40 per cell of 2h) — ~ncx/3; longer rows walk again.
+inline unsigned ITEMS_RICAP(int ncx) { return unsigned(std::min(128, ncx / 2 + 8)); }
 ItemBuild make_item_build(const unsigned* begincell, DivGrid g, unsigned* rowtmp, uint4* items, unsigned* qctr,
-                          int scelldiv, const int* xr, unsigned* qctr2);
+                          int scelldiv, const int* xr, unsigned* qctr2, uint4* rowitems, unsigned ricap);
 void launch_items(hipStream_t stm, const ItemBuild& b);             // count, scan, write
 void launch_items_scan_write(hipStream_t stm, const ItemBuild& b);  // after a count done elsewhere
 

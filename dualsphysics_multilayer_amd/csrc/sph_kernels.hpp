@@ -215,8 +215,9 @@ constexpr size_t QCTR_QUEUE_BYTES = 9 * QSTRIDE * sizeof(unsigned);  // what a r
 constexpr int QCTR_WORDS = 10 * QSTRIDE;
 constexpr int QCTR_NITEMS = 9 * QSTRIDE;
 // A list's counter blocks come in QCTR_COPIES copies (QCTR_WORDS apart), all set up by the
-// item build, so that the interactions on one item list (a Symplectic step's predictor and
-// corrector, NN's two passes) each start on fresh queues without a memset launch.
+// item build, so that the interactions on one item list (NN's force and viscous passes; an
+// interaction without a divide before it, e.g. sph_download_interaction) each start on
+// fresh queues without a memset launch.
 constexpr int QCTR_COPIES = 2;
 constexpr size_t QCTR_BYTES = size_t(QCTR_COPIES) * QCTR_WORDS * sizeof(unsigned);
 // Tiled fluid interaction (sph_interaction_tiled.hip); its per-divide item list is built

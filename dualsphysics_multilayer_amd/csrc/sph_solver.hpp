@@ -174,6 +174,8 @@ class SphGpuSingle {
   unsigned* begincell_ = nullptr;
   uint4* items_ = nullptr;        // tiled-interaction work items (per divide)
   unsigned* rowtmp_ = nullptr;    // per-row item counts/offsets
+  uint4* rowitems_ = nullptr;     // per-row staged items of the count pass
+  unsigned ricap_ = 0;
   unsigned* qctr_ = nullptr;      // per-XCD-group work counters + the list's item counts
   // slabs: the list of the items whose p1 reach a ghost column (after the interior list in
   // items_; the ghost exchange after the divide runs beside the interaction of the others)
