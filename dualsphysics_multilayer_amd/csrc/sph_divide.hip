@@ -1133,14 +1133,14 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
 // also clears the super-tile sums and the far count for the next divide.
 // With an item build (ib.nblocks > 0) the launch has ib.nblocks more blocks after the tiles:
 // they run the item COUNT pass (sph_items.hpp) on the new begincell beside the push — the
-// push is HBM-bound, the row walks latency-bound — and the scan and write passes follow the
-// launch (launch_items_scan_write).  cfg2 1M divide phase: see DESIGN.md §4.
+// push is HBM-bound, the row walks latency-bound — and the place pass follows the launch
+// (launch_items_place).  cfg2 1M divide phase: see DESIGN.md §4.
 template <bool WITHM1, bool WITHPRE, bool WITHTAU>
 __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, GatherArgs a, IncDivScratch s,
                                                   ItemBuild ib) {
   if (blockIdx.x >= s.nb1) {
     extern __shared__ unsigned char push_items_smem[];
-    items_pass_block<false>(ib, blockIdx.x - s.nb1, push_items_smem);
+    items_count_block(ib, blockIdx.x - s.nb1, push_items_smem);
     return;
   }
   const unsigned nd = sc->ndiv, n = sc->np, npb = sc->npb, nold = nd - s.napp;
@@ -1302,7 +1302,7 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
   else { SPH_K_INC_PUSH_T(false, false); }
 #undef SPH_K_INC_PUSH_T
 #undef SPH_K_INC_PUSH
-  if (items) launch_items_scan_write(stm, ib);
+  if (items) launch_items_place(stm, ib);
 }
 
 // ---------------------------------------------------------------------------------

@@ -30,15 +30,14 @@ namespace sphx {
 
 // ------------------------------------------------------------------------------------
 // Item list (per divide): the passes of sph_items.hpp as kernels.
-template <bool WRITE>
-__global__ __launch_bounds__(64 * IR_WAVES) void k_items_pass(ItemBuild b) {
+__global__ __launch_bounds__(64 * IR_WAVES) void k_items_count(ItemBuild b) {
   extern __shared__ unsigned char items_smem[];
-  items_pass_block<WRITE>(b, blockIdx.x, items_smem);
+  items_count_block(b, blockIdx.x, items_smem);
 }
 
-__global__ __launch_bounds__(1024) void k_items_scan(ItemBuild b) {
-  __shared__ unsigned s[1024 / 64 + 4];
-  items_scan(b, s);
+__global__ __launch_bounds__(IP_BS) void k_items_place(ItemBuild b) {
+  extern __shared__ unsigned char items_smem[];
+  items_place_block(b, items_smem);
 }
 
 ItemBuild make_item_build(const unsigned* begincell, DivGrid g, unsigned* rowtmp, uint4* items, unsigned* qctr,
@@ -63,14 +62,15 @@ ItemBuild make_item_build(const unsigned* begincell, DivGrid g, unsigned* rowtmp
   return b;
 }
 
-void launch_items_scan_write(hipStream_t stm, const ItemBuild& b) {
-  hipLaunchKernelGGL(k_items_scan, dim3(1), dim3(1024), 0, stm, b);
-  hipLaunchKernelGGL(k_items_pass<true>, dim3(b.nblocks), dim3(64 * IR_WAVES), b.lds, stm, b);
+void launch_items_place(hipStream_t stm, const ItemBuild& b) {
+  const unsigned n = unsigned(b.xr.nl) * b.nrows2;
+  const unsigned lds = (((IP_BS / 64) * b.rowlds() * unsigned(sizeof(unsigned) + sizeof(unsigned short)) + 15u) / 16u) * 16u;
+  hipLaunchKernelGGL(k_items_place, dim3(items_place_blocks(n)), dim3(IP_BS), lds, stm, b);
 }
 
 void launch_items(hipStream_t stm, const ItemBuild& b) {
-  hipLaunchKernelGGL(k_items_pass<false>, dim3(b.nblocks), dim3(64 * IR_WAVES), b.lds, stm, b);
-  launch_items_scan_write(stm, b);
+  hipLaunchKernelGGL(k_items_count, dim3(b.nblocks), dim3(64 * IR_WAVES), b.lds, stm, b);
+  launch_items_place(stm, b);
 }
 
 // ------------------------------------------------------------------------------------
@@ -778,7 +778,7 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
   }
   wave_max_atomic(sc, RED_VISCDT, viscmax);
   wave_max_atomic(sc, RED_ACEMAX2, ace2max);
-  // (the queue counters are zeroed by k_items_scan, or by the solver before an interaction
+  // (the queue counters are zeroed by k_items_place, or by the solver before an interaction
   // without a new item list)
 }
 

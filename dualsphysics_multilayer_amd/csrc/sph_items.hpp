@@ -1,17 +1,15 @@
 // sph_items.hpp — the per-divide item list of the tiled interactions (k_fluid_tiled,
-// k_fluid_ext, k_nn_tiled), built from the new begincell in two passes over the (y,z)
-// rows: a COUNT pass (items per row and list), a one-block SCAN of the counts into item
-// offsets, then a WRITE pass (the same walk, writing the items at the offsets).  The count
-// pass is a device function so that it can run in the blocks the incremental divide's push
-// launch adds after its own (sph_divide.hip): the push is HBM-bound, the walk latency-bound,
-// and the two need only the new begincell.  (A last-block ticket in place of the scan
-// launch cost more than the launch: one device-scope atomic per count block on one line,
-// ~4000 of them at 1M, serialise across the XCDs — the divide phase went 0.085 -> 0.105 ms.)
-//
-// The count pass also stages each row's items in a slot of `ricap` items per (list, row)
-// (rowitems); the write pass then copies the staged items to their offsets (one wave per
-// row, a coalesced copy) and walks again only a row whose items overflowed its slot.  cfg2
-// 1M: the write pass 14.4 -> see DESIGN.md §4.
+// k_fluid_ext, k_nn_tiled), built from the new begincell in two launches over the (y,z)
+// rows: a COUNT pass (one wave per row walks its items, counts them per list and stages them
+// in the row's slot of `ricap` items, rowitems), then a PLACE pass (each block sums the counts
+// below its rows, scans its own, and copies the staged items to their offsets; a row whose
+// items overflowed its slot is walked again).  The count pass is a device function so that
+// it can run in the blocks the incremental divide's push launch adds after its own
+// (sph_divide.hip): the push is HBM-bound, the walk latency-bound, and the two need only the
+// new begincell.  cfg2 1M (rocprof): a one-block scan + a second walk took 4.8 + 14.4 us, the
+// place pass takes DESIGN.md §4's figure.  (A last-block ticket in place of a scan launch cost
+// more than the launch: one device-scope atomic per count block on one line, ~4000 of them at
+// 1M, serialise across the XCDs — the divide phase went 0.085 -> 0.105 ms.)
 //
 // Rows [0,nrows) are fluid rows (fluid p1), rows [nrows,2*nrows) bound rows (bound p1,
 // DBC).  An item is a run of <= TB consecutive particles of one row, cut earlier only where
@@ -56,10 +54,11 @@ struct ItemBuild {
 
 // One wave walks row r of one kind (fluid or bound p1): its cell begin offsets to LDS
 // (pre / nzfrom: this wave's rowlds() entries), then lane 0 emits the items of each column
-// range of each list.  WRITE = false counts them (counts[list][row]), true writes them at the
-// scanned offsets.
+// range of each list.  WRITE = false counts them (counts[list][row]) and stages them,
+// true writes the items of list `onelist` at item offset `outoff`.
 template <bool WRITE>
-__device__ __forceinline__ void items_row(const ItemBuild& b, unsigned r, unsigned* pre, unsigned short* nzfrom) {
+__device__ __forceinline__ void items_row(const ItemBuild& b, unsigned r, unsigned* pre, unsigned short* nzfrom,
+                                          int onelist = -1, unsigned outoff = 0) {
   const DivGrid& g = b.g;
   const ItemRanges& xr = b.xr;
   const unsigned nrows = unsigned(g.ncy) * unsigned(g.ncz), nrows2 = 2u * nrows;
@@ -89,8 +88,8 @@ __device__ __forceinline__ void items_row(const ItemBuild& b, unsigned r, unsign
     for (int x = int(lane); x <= ncx; x += 64) pre[x] = bc[rowbase + x];
     __builtin_amdgcn_wave_barrier();
   }
-  for (int list = 0; list < xr.nl; list++) {
-    uint4* out = WRITE ? b.items + b.counts[list * nrows2 + r] : nullptr;
+  for (int list = onelist < 0 ? 0 : onelist; list < (onelist < 0 ? xr.nl : onelist + 1); list++) {
+    uint4* out = WRITE ? b.items + outoff : nullptr;  // (WRITE: one list, at its offset)
     unsigned nitems = 0;
     uint4* stage = WRITE ? nullptr : b.rowitems + size_t(list * nrows2 + r) * b.ricap;
     auto emit = [&](int a, int e, unsigned p, unsigned q) {
@@ -180,96 +179,140 @@ __device__ __forceinline__ void items_row(const ItemBuild& b, unsigned r, unsign
   }
 }
 
-// Exclusive scan of the row counts of the lists by ONE block (blockDim a multiple of 64,
-// <= 1024), in place -> item offsets; each list's counts {all, bound, first item} into its
-// counter block (qctr[QCTR_NITEMS...]) and its per-XCD work queues zeroed for the next
-// interaction.  s: >= blockDim/64 + 4 words of LDS.  (Chunks of contiguous counts per
-// thread: a few thousand rows at 1M, ~16k at 10M.)
-__device__ __forceinline__ void items_scan(const ItemBuild& b, unsigned* s) {
-  unsigned* __restrict__ counts = b.counts;
-  const unsigned nrows2 = b.nrows2, nrows = nrows2 / 2, nl = unsigned(b.xr.nl), n = nl * nrows2;
-  const unsigned nt = blockDim.x, nw = nt / 64, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  unsigned* wsum = s;
-  unsigned* mark = s + nw;  // offsets where list A's bound rows, list B and its bound rows begin
-  if (threadIdx.x < 8 * QCTR_COPIES) {  // the interactions' item queues (every copy) start over
-    const unsigned q = (threadIdx.x >> 3) * QCTR_WORDS + (threadIdx.x & 7) * QSTRIDE;
-    b.qa[q] = 0u;
-    if (nl == 2) b.qb[q] = 0u;
-  }
-  // thread t scans the contiguous chunk [t per, (t+1) per)
-  const unsigned per = (n + nt - 1) / nt, i0 = threadIdx.x * per, i1 = min(i0 + per, n);
-  unsigned sum = 0;
-  for (unsigned i = i0; i < i1; i++) sum += counts[i];
-  unsigned inc = sum;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const unsigned v = __shfl_up(inc, off, 64);
-    if (lane >= unsigned(off)) inc += v;
-  }
-  if (lane == 63) wsum[w] = inc;
-  __syncthreads();
-  unsigned run = inc - sum;
-  for (unsigned q = 0; q < w; q++) run += wsum[q];
-  for (unsigned i = i0; i < i1; i++) {
-    if (i == nrows) mark[0] = run;
-    if (i == nrows2) mark[1] = run;
-    if (i == nrows2 + nrows) mark[2] = run;
-    const unsigned v = counts[i];
-    counts[i] = run;
-    run += v;
-  }
-  if (threadIdx.x == nt - 1) {
-    mark[3] = run;  // the total
-    counts[n] = run;  // so that every row's count is the next offset minus its own
-  }
-  __syncthreads();
-  if (threadIdx.x < QCTR_COPIES) {
-    const unsigned tot = mark[3], na = nl == 2 ? mark[1] : tot, c = threadIdx.x * QCTR_WORDS + QCTR_NITEMS;
-    b.qa[c] = na;
-    b.qa[c + 1] = na - mark[0];  // the bound rows' items: the list's tail (ItemGroups)
-    b.qa[c + 2] = 0u;
-    if (nl == 2) {
-      b.qb[c] = tot - na;
-      b.qb[c + 1] = tot - mark[2];
-      b.qb[c + 2] = na;  // the second list follows the first in the item array
-    }
-  }
+// The PLACE pass (k_items_place: scan + write in one launch).  Block k takes the (list, row)
+// entries [i0, i1) of the flattened counts: the items below i0 are one block reduction over
+// the counts before it (every block reads its own prefix of the raw counts: no scan kernel,
+// no cross-block ordering), its own entries an in-block exclusive scan, then its threads copy
+// the staged items to their offsets (a row whose items overflowed its slot is walked again).  One more block writes each list's counts {all, bound, first item} into its
+// counter blocks (QCTR_COPIES copies) and zeroes their work queues for the next interactions.
+constexpr int IP_BS = 512;        // threads of a place block (8 waves)
+constexpr int IP_MAXROWS = 1024;  // entries per place block (2 per thread)
+inline unsigned items_place_blocks(unsigned n) {
+  const unsigned want = std::min(128u, std::max(1u, n / 64u));
+  return std::max(want, (n + IP_MAXROWS - 1) / IP_MAXROWS) + 1u;  // + the counts block
 }
 
-// The write pass of row r: its staged items copied to their offsets by the wave, or, when
-// a list's items overflowed the row's slot, the walk again.
-__device__ __forceinline__ void items_copy_row(const ItemBuild& b, unsigned r, unsigned* pre, unsigned short* nz) {
-  const unsigned lane = threadIdx.x & 63, nl = unsigned(b.xr.nl);
-  unsigned off[2], cnt[2];
-  bool fits = true;
-  for (unsigned list = 0; list < nl; list++) {
-    const unsigned i = list * b.nrows2 + r;
-    off[list] = b.counts[i];
-    cnt[list] = b.counts[i + 1] - off[list];
-    fits &= cnt[list] <= b.ricap;
+__device__ __forceinline__ unsigned block_sum(unsigned v, unsigned* s_w) {
+  const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  __syncthreads();
+  if (lane == 0) s_w[w] = v;
+  __syncthreads();
+  unsigned t = 0;
+  for (unsigned q = 0; q < blockDim.x / 64; q++) t += s_w[q];
+  return t;
+}
+
+// This thread's part of the sum of counts[lo, hi): 16-B loads, several in flight (a strided
+// scalar loop waits one memory latency per element it reads).
+__device__ __forceinline__ unsigned partial_sum(const unsigned* __restrict__ counts, unsigned lo, unsigned hi) {
+  if (lo >= hi) return 0u;
+  unsigned s = 0;
+  const unsigned a = min((lo + 3u) & ~3u, hi), nv = (hi - a) / 4u, t = a + 4u * nv;
+  if (threadIdx.x < a - lo) s += counts[lo + threadIdx.x];
+  if (threadIdx.x < hi - t) s += counts[t + threadIdx.x];
+  const uint4* __restrict__ v = reinterpret_cast<const uint4*>(counts + a);
+#pragma unroll 4
+  for (unsigned k = threadIdx.x; k < nv; k += blockDim.x) {
+    const uint4 x = v[k];
+    s += (x.x + x.y) + (x.z + x.w);
   }
-  if (!fits) {
-    items_row<true>(b, r, pre, nz);
+  return s;
+}
+
+__device__ __forceinline__ void items_place_block(const ItemBuild& b, unsigned char* smem) {
+  __shared__ unsigned s_w[IP_BS / 64], s_off[IP_MAXROWS], s_cnt[IP_MAXROWS], s_tot;
+  const unsigned* __restrict__ counts = b.counts;
+  const unsigned nrows2 = b.nrows2, nrows = nrows2 / 2, nl = unsigned(b.xr.nl), n = nl * nrows2;
+  const unsigned nb = gridDim.x - 1;  // the last block: the lists' counts
+  const unsigned per = (n + nb - 1) / nb, i0 = blockIdx.x * per, i1 = min(i0 + per, n);
+  const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (blockIdx.x == nb) {  // the lists' counts and fresh work queues
+    // items below nrows, nrows2, nrows2 + nrows, n (the segments' sums, loads of all four
+    // issued before the first block reduction, then prefixes)
+    const unsigned p0 = partial_sum(counts, 0u, nrows), p1 = partial_sum(counts, nrows, nrows2);
+    const unsigned p2 = partial_sum(counts, nrows2, min(nrows2 + nrows, n));
+    const unsigned p3 = partial_sum(counts, min(nrows2 + nrows, n), n);
+    const unsigned m0 = block_sum(p0, s_w);
+    const unsigned m1 = m0 + block_sum(p1, s_w);
+    const unsigned m2 = m1 + block_sum(p2, s_w);
+    const unsigned m3 = m2 + block_sum(p3, s_w);
+    if (threadIdx.x < 8 * QCTR_COPIES) {
+      const unsigned q = (threadIdx.x >> 3) * QCTR_WORDS + (threadIdx.x & 7) * QSTRIDE;
+      b.qa[q] = 0u;
+      if (nl == 2) b.qb[q] = 0u;
+    }
+    if (threadIdx.x < QCTR_COPIES) {
+      const unsigned na = nl == 2 ? m1 : m3, c = threadIdx.x * QCTR_WORDS + QCTR_NITEMS;
+      b.qa[c] = na;
+      b.qa[c + 1] = na - m0;  // the bound rows' items: the list's tail (ItemGroups)
+      b.qa[c + 2] = 0u;
+      if (nl == 2) {
+        b.qb[c] = m3 - na;
+        b.qb[c + 1] = m3 - m2;
+        b.qb[c + 2] = na;  // the second list follows the first in the item array
+      }
+    }
     return;
   }
-  for (unsigned list = 0; list < nl; list++) {
-    const uint4* __restrict__ src = b.rowitems + size_t(list * b.nrows2 + r) * b.ricap;
-    for (unsigned k = lane; k < cnt[list]; k += 64) b.items[off[list] + k] = src[k];
+  if (i0 >= n) return;
+  const unsigned below = block_sum(partial_sum(counts, 0u, i0), s_w);
+  // own entries: two per thread, an exclusive scan
+  const unsigned e0 = i0 + 2 * threadIdx.x;
+  const unsigned v0 = e0 < i1 ? counts[e0] : 0u, v1 = e0 + 1 < i1 ? counts[e0 + 1] : 0u;
+  unsigned inc = v0 + v1;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned t = __shfl_up(inc, off, 64);
+    if (lane >= unsigned(off)) inc += t;
   }
+  __syncthreads();
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  unsigned run = below + inc - v0 - v1;
+  for (unsigned q = 0; q < w; q++) run += s_w[q];
+  if (e0 < i1) {
+    s_off[e0 - i0] = run;
+    s_cnt[e0 - i0] = v0;
+  }
+  if (e0 + 1 < i1) {
+    s_off[e0 + 1 - i0] = run + v0;
+    s_cnt[e0 + 1 - i0] = v1;
+  }
+  if (threadIdx.x == blockDim.x - 1) s_tot = run + v0 + v1 - below;  // the block's items
+  __syncthreads();
+  // The block's items are contiguous in the list: thread t copies items t, t + IP_BS, ... from
+  // their rows' slots (the row by a binary search of the offsets), all loads independent.
+  const unsigned nr = i1 - i0, tot = s_tot;
+  for (unsigned k = threadIdx.x; k < tot; k += blockDim.x) {
+    const unsigned o = below + k;
+    unsigned lo = 0, hi = nr - 1;  // the last row whose offset is <= o (empty rows before it share it)
+    while (lo < hi) {
+      const unsigned mid = (lo + hi + 1) >> 1;
+      if (s_off[mid] <= o) lo = mid;
+      else hi = mid - 1;
+    }
+    if (s_cnt[lo] <= b.ricap) b.items[o] = b.rowitems[size_t(i0 + lo) * b.ricap + (o - s_off[lo])];
+  }
+  // a row whose items overflowed its slot: walked again by one wave
+  const unsigned L = b.rowlds();
+  unsigned* pre = reinterpret_cast<unsigned*>(smem) + w * L;
+  unsigned short* nz = reinterpret_cast<unsigned short*>(smem + (IP_BS / 64) * L * sizeof(unsigned)) + w * L;
+  for (unsigned j = w; j < nr; j += IP_BS / 64)
+    if (s_cnt[j] > b.ricap) {
+      const unsigned i = i0 + j, list = i / nrows2;
+      items_row<true>(b, i - list * nrows2, pre, nz, int(list), s_off[j]);
+    }
 }
 
-// Block `blk` of a pass (IR_WAVES rows; dynamic LDS `smem` of b.lds bytes).
-template <bool WRITE>
-__device__ __forceinline__ void items_pass_block(const ItemBuild& b, unsigned blk, unsigned char* smem) {
+// Block `blk` of the count pass (IR_WAVES rows; dynamic LDS `smem` of b.lds bytes).
+__device__ __forceinline__ void items_count_block(const ItemBuild& b, unsigned blk, unsigned char* smem) {
   const unsigned L = b.rowlds(), w = threadIdx.x >> 6;
   unsigned* pre = reinterpret_cast<unsigned*>(smem) + w * L;
   unsigned short* nz = reinterpret_cast<unsigned short*>(smem + IR_WAVES * L * sizeof(unsigned)) + w * L;
   const unsigned r = blk * IR_WAVES + w;
-  if (r >= b.nrows2) return;
-  if (WRITE)
-    items_copy_row(b, r, pre, nz);
-  else
-    items_row<false>(b, r, pre, nz);
+  if (r < b.nrows2) items_row<false>(b, r, pre, nz);
 }
 
 // Host side (sph_interaction_tiled.hip).  scelldiv 1 (CellMode=full): items of <= 4 cells;
@@ -284,7 +327,7 @@ inline size_t ITEMS_ROWTMP(int ncy, int ncz) { return 4 * size_t(ncy) * size_t(n
 inline unsigned ITEMS_RICAP(int ncx) { return unsigned(std::min(128, ncx / 2 + 8)); }
 ItemBuild make_item_build(const unsigned* begincell, DivGrid g, unsigned* rowtmp, uint4* items, unsigned* qctr,
                           int scelldiv, const int* xr, unsigned* qctr2, uint4* rowitems, unsigned ricap);
-void launch_items(hipStream_t stm, const ItemBuild& b);             // count, scan, write
-void launch_items_scan_write(hipStream_t stm, const ItemBuild& b);  // after a count done elsewhere
+void launch_items(hipStream_t stm, const ItemBuild& b);        // count, place
+void launch_items_place(hipStream_t stm, const ItemBuild& b);  // after a count done elsewhere
 
 }  // namespace sphx

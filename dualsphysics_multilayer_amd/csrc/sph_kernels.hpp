@@ -209,7 +209,7 @@ void launch_interaction_bound(hipStream_t stm, unsigned npbcap, DevScalars* sc, 
 // Work counters of the persistent tiled kernels (qctr): 8 per-XCD item queues + the
 // finished-block count, each on its own 128-B line (device-scope atomics serialize per line).
 constexpr int QSTRIDE = 32;
-// Line 9 holds the list's item counts {all, bound, first item} (k_items_scan; ItemGroups
+// Line 9 holds the list's item counts {all, bound, first item} (k_items_place; ItemGroups
 // reads them), so one counter block describes one item list.
 constexpr size_t QCTR_QUEUE_BYTES = 9 * QSTRIDE * sizeof(unsigned);  // what a re-run zeroes
 constexpr int QCTR_WORDS = 10 * QSTRIDE;

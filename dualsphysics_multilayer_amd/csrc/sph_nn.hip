@@ -864,7 +864,7 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
   wave_max_atomic(sc, RED_VISCDT, viscmax);
   wave_max_atomic(sc, RED_ACEMAX2, ace2max);
   wave_max_atomic(sc, RED_VISCETA, etamax);
-  // (the queue counters are zeroed by k_items_scan, or by the solver before an interaction
+  // (the queue counters are zeroed by k_items_place, or by the solver before an interaction
   // without a new item list)
 }
 

@@ -180,7 +180,7 @@ struct ItemGroup {
 };
 struct ItemGroups {
   unsigned nf, nb, lo;
-  // the list's counts {all, bound, first item}, written by k_items_scan beside the work queues
+  // the list's counts {all, bound, first item}, written by k_items_place beside the work queues
   __device__ __forceinline__ explicit ItemGroups(const unsigned* qctr) {
     const unsigned n = qctr[QCTR_NITEMS];
     nb = min(qctr[QCTR_NITEMS + 1], n);
