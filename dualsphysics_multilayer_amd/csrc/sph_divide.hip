@@ -634,7 +634,7 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
       af += s_cf[q];
     }
     s.tagg[b] = make_uint2(an, af);
-    if (an | af) atomicAdd(&s.tsup[b / INC_SUP], (static_cast<unsigned long long>(an) << 32) | af);
+    if (an | af) atomicAdd(&s.tsup[(b / INC_SUP) * TSUP_STRIDE], (static_cast<unsigned long long>(an) << 32) | af);
   }
   TSTAMP(2);
   TSTAMP(3);
@@ -761,7 +761,7 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   }
   unsigned long long pre = 0, tot = 0;  // (near << 32 | far) before tA, and over all tiles
   for (unsigned q = threadIdx.x; q < nsup; q += IB_BS) {
-    const unsigned long long v = s.tsup[q];
+    const unsigned long long v = s.tsup[q * TSUP_STRIDE];
     tot += v;
     if (q < tA / INC_SUP) pre += v;
   }
@@ -822,7 +822,7 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   auto tp_of = [&](unsigned t) -> uint2 {
     if (tplds && t >= tA && t - tA < ntp) return s_tp[t - tA];
     unsigned long long p = 0;
-    for (unsigned q = 0; q < t / INC_SUP; q++) p += s.tsup[q];
+    for (unsigned q = 0; q < t / INC_SUP; q++) p += s.tsup[q * TSUP_STRIDE];
     for (unsigned u = (t / INC_SUP) * INC_SUP; u < t; u++) {
       const uint2 v = s.tagg[u];
       p += (static_cast<unsigned long long>(v.x) << 32) | v.y;
@@ -1188,7 +1188,7 @@ __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, G
   wave_max_atomic(sc, RED_VELMAX2, v2);
   if (t == 0) {
     const unsigned nsup = (s.nb1 + INC_SUP - 1) / INC_SUP;
-    for (unsigned u = threadIdx.x; u < nsup; u += 256) s.tsup[u] = 0ull;
+    for (unsigned u = threadIdx.x; u < nsup; u += 256) s.tsup[u * TSUP_STRIDE] = 0ull;
     if (threadIdx.x == 0) s.ctr[0] = 0u;
   }
 }

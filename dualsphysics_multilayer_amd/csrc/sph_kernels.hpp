@@ -144,6 +144,7 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
                    float4* poscell, float* press, int xoff, const float4* phase_eos = nullptr, unsigned vfirst = ~0u,
                    unsigned appbase = 0, unsigned* apppos = nullptr);
 
+constexpr unsigned TSUP_STRIDE = 16;  // u64 entries per super-tile line
 // Incremental divide (sph_divide.hip): the stable order of the previous divide merged with
 // the particles whose box changed, every divide after the first.  On a slab the exchange
 // appended `napp` particles (migrants + ghosts) after the `nold` of the previous divide:
@@ -154,7 +155,9 @@ struct IncDivScratch {
   unsigned* cw = nullptr;         // [cap] tile-local near / far prefixes (11 bits each) | near, far flags
   unsigned* fidx = nullptr;       // [cap] far-list index of a far mover
   uint2* tagg = nullptr;          // [tiles] (near, far) movers of each tile
-  unsigned long long* tsup = nullptr;  // [tiles / 64] (near << 32 | far) per super tile, cleared by k_inc_push
+  // [tiles / 64] (near << 32 | far) per super tile, each on its own 128-B line (TSUP_STRIDE:
+  // device-scope atomics serialise per line), cleared by k_inc_push
+  unsigned long long* tsup = nullptr;
   unsigned* tpg = nullptr;        // [tiles] movers before each tile (k_inc_boxes -> k_inc_push)
   unsigned* mkey = nullptr;       // [cap] new keys of the near movers, at tile * INC_TILE + local rank
   uint2* mfar = nullptr;          // [cap] (previous index, new key) of the far movers (appended)

@@ -689,8 +689,8 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
     inc_.tagg = (uint2*)dmalloc(8 * size_t(inc_.nb1));
     inc_.tpg = (unsigned*)dmalloc(4 * size_t(inc_.nb1));
     const size_t nsup = (size_t(inc_.nb1) + 63) / 64;
-    inc_.tsup = (unsigned long long*)dmalloc(8 * nsup);
-    check_hip(hipMemset(inc_.tsup, 0, 8 * nsup), "zero super tiles");
+    inc_.tsup = (unsigned long long*)dmalloc(8 * TSUP_STRIDE * nsup);
+    check_hip(hipMemset(inc_.tsup, 0, 8 * TSUP_STRIDE * nsup), "zero super tiles");
     inc_valid_ = false;  // new scratch: the next divide is a full one
   }
   if (slab()) {

@@ -6,7 +6,8 @@
 #      (separate passes: FETCH_SIZE and WRITE_SIZE do not fit one TCC pass,
 #       MI355X_MICROARCH.md §rocprofv3; never combined with sys/runtime traces)
 #   4. bench.py (default flags, incl. the CPU baseline)        -> <tag>/bench.json
-#   (the profiled passes 1-3 skip bench.py's extra cfg3 timing: --no-cfg3)
+#   (the profiled passes 1-3 skip bench.py's extra cfg3 timing and its developed-flow run:
+#    --no-cfg3 --developed-presteps 0; 8000 more steps under --pmc overran the tool's buffers)
 #      (reads the traffic of step 2-3 from profiles/<tag>/)
 # Results go to profiles/<tag>/ of the box copy and to gpurun_out/profiles/<tag>/.
 set -e
@@ -18,11 +19,11 @@ OUT=$R/gpurun_out/prof_$TAG
 DST=$R/profiles/$TAG
 export TMPDIR=/tmp
 mkdir -p "$OUT" "$DST"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 "$R/bench.py" $ARGS --no-cpu-baseline --no-cfg3 > "$OUT/kt.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- python3 "$R/bench.py" $ARGS --no-cpu-baseline --no-cfg3 --developed-presteps 0 > "$OUT/kt.log" 2>&1
 # provisional bench.json (workload, np) so step 4's bench finds this round's traffic
 grep '^{' "$OUT/kt.log" | tail -1 > "$DST/bench.json"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run -- python3 "$R/bench.py" $ARGS --no-cpu-baseline --no-cfg3 > "$OUT/fetch.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run -- python3 "$R/bench.py" $ARGS --no-cpu-baseline --no-cfg3 > "$OUT/write.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/fetch" -o run -- python3 "$R/bench.py" $ARGS --no-cpu-baseline --no-cfg3 --developed-presteps 0 > "$OUT/fetch.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o run -- python3 "$R/bench.py" $ARGS --no-cpu-baseline --no-cfg3 --developed-presteps 0 > "$OUT/write.log" 2>&1
 python3 "$R/profiles/summarize.py" "$OUT" "$DST"
 timeout -k 10 400 python3 "$R/bench.py" $ARGS > "$OUT/bench.log" 2>&1
 grep '^{' "$OUT/bench.log" | tail -1 > "$DST/bench.json"

@@ -3,7 +3,7 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=${1:-$R/gpurun_out/pmc}
-ARGS=${BENCH_ARGS:-"--steps 6 --warmup 2 --no-cpu-baseline"}
+ARGS=${BENCH_ARGS:-"--steps 6 --warmup 2 --no-cpu-baseline --developed-presteps 0"}
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 i=0
