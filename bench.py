@@ -438,7 +438,7 @@ def main() -> None:
         # the tiled kernel's instantiation: DDT mode (| 8: Fourtakas term as its series),
         # floating records, cell mode (sph_interaction_tiled.hip launch_fluid_tiled_s)
         ftb = "true" if getattr(case, "floatings", None) else "false"
-        kname = (["sphx::k_nn_tiled<%d, %d, true>" % (case.tvisco, case.tdensity)] if nn else
+        kname = (["sphx::k_nn_tiled<%d, %d, true," % (case.tvisco, case.tdensity)] if nn else
                  ["sphx::k_fluid_tiled<%d, %s, %d>" % (td, ftb, case.cellmode)
                   for td in ((case.tdensity | 8, case.tdensity) if case.tdensity >= 2 else (case.tdensity,))])
         traffic = profiled_traffic(kname, case.np, "BASELINE " + args.workload) if world == 1 else None

@@ -564,6 +564,9 @@ void SphGpuSingle::AllocFixed() {
   rowtmp_ = (unsigned*)dmalloc(4 * ITEMS_ROWTMP(G.ncy, G.ncz));  // two lists x (fluid, bound) rows of item counts
   // the count pass's staged items (sph_items.hpp), sized for the widest grid of the run
   ricap_ = ITEMS_RICAP(int(nctmax_ / (unsigned(G.ncy) * unsigned(G.ncz))));
+  // test hook: smaller slots send more rows down the place pass's second walk
+  // (tests/test_gpu_items.py checks the run is bitwise the same)
+  if (const char* e = std::getenv("SPH_ITEMS_RICAP")) ricap_ = std::max(1u, std::min(ricap_, unsigned(std::atoi(e))));
   rowitems_ = (uint4*)dmalloc(sizeof(uint4) * (ITEMS_ROWTMP(G.ncy, G.ncz) - 1) * ricap_);
   qctr_ = (unsigned*)dmalloc(QCTR_BYTES);
   check_hip(hipMemset(qctr_, 0, QCTR_BYTES), "zero work counters");
