@@ -1131,20 +1131,21 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
 // One tile per block.  Loads in three batches (one memory latency each): the particle
 // states and the classification words, the new positions, then the stores.  Block 0
 // also clears the super-tile sums and the far count for the next divide.
-// With an item build (ib.nblocks > 0) the launch has ib.nblocks more blocks after the tiles:
-// they run the item COUNT pass (sph_items.hpp) on the new begincell beside the push — the
-// push is HBM-bound, the row walks latency-bound — and the place pass follows the launch
-// (launch_items_place).  cfg2 1M divide phase: see DESIGN.md §4.
+// With an item build (ib.nblocks > 0) the launch has ib.nblocks more blocks BEFORE the tiles
+// (dispatched first, so their latency-bound row walks start with the push instead of
+// trailing it): they run the item COUNT pass (sph_items.hpp) on the new begincell beside
+// the HBM-bound push, and the place pass follows the launch (launch_items_place).  cfg2 1M
+// divide phase: see DESIGN.md §4.
 template <bool WITHM1, bool WITHPRE, bool WITHTAU>
 __global__ __launch_bounds__(256) void k_inc_push(DevScalars* __restrict__ sc, GatherArgs a, IncDivScratch s,
                                                   ItemBuild ib) {
-  if (blockIdx.x >= s.nb1) {
+  if (blockIdx.x < ib.nblocks) {
     extern __shared__ unsigned char push_items_smem[];
-    items_count_block(ib, blockIdx.x - s.nb1, push_items_smem);
+    items_count_block(ib, blockIdx.x, push_items_smem);
     return;
   }
   const unsigned nd = sc->ndiv, n = sc->np, npb = sc->npb, nold = nd - s.napp;
-  const unsigned t = blockIdx.x;
+  const unsigned t = blockIdx.x - ib.nblocks;
   const unsigned i0 = t * INC_TILE + threadIdx.x;
   GatherRec<WITHM1, WITHPRE, WITHTAU> q[GP];
   unsigned key[GP], cw[GP], fx[GP], pos[GP];
