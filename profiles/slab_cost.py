@@ -68,9 +68,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--repeat", type=int, default=2, help="alternating repeats of the three runs")
     ap.add_argument("--overlap", type=int, default=1, help="slab ghost overlap on (1) / off (0)")
-    ap.add_argument("--only", choices=("domain", "one_slab", "faces", "left"), default=None,
+    ap.add_argument("--only", choices=("domain", "one_slab", "faces", "left", "eight"), default=None,
                     help="one of the runs (e.g. under rocprofv3); left: [0, w) | [w, ncx), the big slab with one "
-                         "face in the water, whose face launch runs after the strip's (a trace isolates it)")
+                         "face in the water, whose face launch runs after the strip's (a trace isolates it); "
+                         "eight: BASELINE cfg3's 8-slab split in one process (its exchange kernels per divide "
+                         "at the 8-GPU slab size, from a rocprofv3 trace)")
     a = ap.parse_args()
     case = DamBreakCase(**CFG[a.workload])
     ncx = int(slab_partition(case, 1)[-1])
@@ -107,6 +109,14 @@ def main():
             g.close()
             out.setdefault("left_ms", []).append(ms)
             out["left_big_phases_ms"] = ph
+        if a.only == "eight":
+            g = SphSlabGroup(case, slab_partition(case, 8))
+            g.set_overlap(bool(a.overlap))
+            ms, ph = timed(g, a.steps, a.warmup, g.members[3])
+            out["eight_np"] = [int(m.stats()["np"]) for m in g.members]
+            g.close()
+            out.setdefault("eight_ms", []).append(ms)
+            out["eight_slab3_phases_ms"] = ph
         print("progress", json.dumps(out), flush=True)
     if a.only is None:
         d, o, f = min(out["domain_ms"]), min(out["one_slab_ms"]), min(out["faces_ms"])
