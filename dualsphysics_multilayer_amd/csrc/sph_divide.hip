@@ -515,7 +515,10 @@ static_assert(INC_IPT == GP, "k_inc_push covers one classify tile per block");
 static_assert(INC_TILE == int(INC_TILE_SIZE), "tile size of the host allocations");
 static_assert(INC_TILE <= 2048, "tile-local prefixes are 11 bits");
 constexpr int INC_SUP = 64;  // tiles per super tile
-constexpr int IB_BS = 256, IB_BPT = 2, IB_BOX = IB_BS * IB_BPT;  // boxes per k_inc_boxes block
+#ifndef SPH_IB_BPT
+#define SPH_IB_BPT 2
+#endif
+constexpr int IB_BS = 256, IB_BPT = SPH_IB_BPT, IB_BOX = IB_BS * IB_BPT;  // boxes per k_inc_boxes block
 constexpr unsigned CW_NEAR = 0x80000000u, CW_FAR = 0x40000000u, CW_LOC = 0x7ffu;
 // slab: DROP = an old particle whose key became the discard box (a stale ghost): counted
 // with the far movers in the prefixes (it is not a stayer) but kept out of the far list
