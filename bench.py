@@ -494,7 +494,7 @@ def main() -> None:
                            ("k_fluid_tiled<tdensity=%d, floating records> (Interaction_Forces)"
                             if getattr(case, "floatings", None) else "k_fluid_tiled<tdensity=%d> (Interaction_Forces)")
                            % case.tdensity),
-                "bound": "mfma",
+                "bound": "valu",
                 "bound_note": "FP32-VALU-bound pairwise kernel (no MFMA: irregular pairs); gfx950's FP32 vector "
                               "peak equals its FP32 MFMA peak, 157.3 TFLOP/s",
                 "achieved": achieved,

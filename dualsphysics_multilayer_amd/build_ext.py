@@ -46,12 +46,23 @@ def lib_path() -> str:
     return os.path.join(OUTDIR, LIBNAME)
 
 
+def _deps(obj: str, src: str) -> list:
+    """The headers a translation unit included (its -MMD file), or every header if unknown."""
+    dfile = obj + ".d"
+    if os.path.exists(dfile):
+        text = open(dfile).read().replace("\\\n", " ")
+        files = text.split(":", 1)[1].split() if ":" in text else []
+        if files and all(os.path.exists(f) for f in files):
+            return [src] + files
+    deps = [src] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith((".hpp", ".h"))]
+    deps.append(os.path.join(os.path.dirname(HERE), "include", "sphcore.h"))
+    return deps
+
+
 def _stale(obj: str, src: str) -> bool:
     if not os.path.exists(obj):
         return True
-    deps = [src] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith((".hpp", ".h"))]
-    deps.append(os.path.join(os.path.dirname(HERE), "include", "sphcore.h"))
-    return os.path.getmtime(obj) < max(os.path.getmtime(d) for d in deps)
+    return os.path.getmtime(obj) < max(os.path.getmtime(d) for d in _deps(obj, src))
 
 
 def build(force: bool = False, verbose: bool = False, outdir: str | None = None, defines: list | None = None) -> str:
@@ -77,7 +88,8 @@ def _build(force: bool, verbose: bool, defines: list) -> str:
         objs.append(obj)
         if force or defines or _stale(obj, src):
             lang = ["-x", "hip"] if s.endswith(".hip") else []
-            jobs.append([cc] + CXXFLAGS + ["-D" + d for d in defines] + lang + ["-c", src, "-o", obj])
+            jobs.append([cc] + CXXFLAGS + ["-D" + d for d in defines] + lang +
+                        ["-MMD", "-MF", obj + ".d", "-c", src, "-o", obj])
     if jobs:
         with cf.ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
             for cmd, r in zip(jobs, ex.map(lambda c: subprocess.run(c, capture_output=True, text=True), jobs)):

@@ -214,6 +214,12 @@ int sph_slab_create(const SphCaseDef* cdef, const SphParticlesHost* all, int dev
     sc.c1 = slab->cx_end;
     auto tr = sphx::make_rccl_transport(slab->comm_id, slab->rank, slab->nranks);
     auto* impl = new sphx::SphGpuSingle(*cdef, *all, device, sc, std::move(tr));
+    try {
+      impl->ShareDeviceCheck();  // overlap off for ranks that share a GPU (collective)
+    } catch (...) {
+      delete impl;
+      throw;
+    }
     *out = new SphSolver{impl, false};
   });
 }
@@ -231,6 +237,12 @@ int sph_slab_create_shm(const SphCaseDef* cdef, const SphParticlesHost* all, int
     sc.c1 = slab->cx_end;
     auto tr = sphx::make_shm_transport(shm_name, slab->rank, slab->nranks, slot_bytes);
     auto* impl = new sphx::SphGpuSingle(*cdef, *all, device, sc, std::move(tr));
+    try {
+      impl->ShareDeviceCheck();  // overlap off for ranks that share a GPU (collective)
+    } catch (...) {
+      delete impl;
+      throw;
+    }
     *out = new SphSolver{impl, false};
   });
 }

@@ -103,11 +103,21 @@ std::unique_ptr<SlabTransport> make_rccl_transport(const unsigned char id[128], 
 }
 
 // ---------------------------------------------------------------------------------
-LocalHub::LocalHub(int nslabs) : slots(size_t(nslabs)), n(nslabs) {}
+LocalHub::LocalHub(int nslabs) : slots(size_t(nslabs)), n(nslabs) {
+  if (const char* e = std::getenv("SPH_SLAB_TURNS")) turns = std::atoi(e) != 0;
+}
+
+LocalHub::~LocalHub() {
+  for (Slot& sl : slots)
+    for (hipEvent_t e : {sl.ready, sl.copied, sl.idone[0], sl.idone[1]})
+      if (e) (void)hipEventDestroy(e);
+}
+
+void LocalHub::throw_aborted() { throw SphError(SPH_ERR_COMM, "slab group aborted by another slab"); }
 
 void LocalHub::barrier() {
   std::unique_lock<std::mutex> lk(m_);
-  if (aborted_) throw SphError(SPH_ERR_COMM, "slab group aborted by another slab");
+  if (aborted_) throw_aborted();
   const unsigned long long g = gen_;
   if (++waiting_ == n) {
     waiting_ = 0;
@@ -116,7 +126,7 @@ void LocalHub::barrier() {
     return;
   }
   cv_.wait(lk, [&] { return gen_ != g || aborted_; });
-  if (gen_ == g) throw SphError(SPH_ERR_COMM, "slab group aborted by another slab");
+  if (gen_ == g) throw_aborted();
 }
 
 void LocalHub::abort() {
@@ -125,10 +135,15 @@ void LocalHub::abort() {
   cv_.notify_all();
 }
 
+// In-process slabs, point to point as RCCL's send/receive: post() records an event where the
+// send buffers are complete and publishes them; collect() makes the stream wait for the
+// neighbours' events and copies their buffers (blit kernels: on one GPU they run in the block
+// slots the interior interaction leaves free, sph_solver.cpp, at ~1 TB/s; the DMA engines,
+// hipMemcpyDeviceToDeviceNoCU, moved the ghost messages at ~50 GB/s).  No host thread waits
+// for the GPU: the host waits only for a neighbour's thread to have posted (or consumed), and
+// a rank's next post first makes its stream wait until the neighbours' copies of its
+// previous buffers are done.
 class LocalTransport final : public SlabTransport {
-  // Blit-kernel copies: on one GPU they run in the block slots the interior interaction
-  // leaves free (sph_solver.cpp) at ~1 TB/s; the DMA engines (hipMemcpyDeviceToDeviceNoCU)
-  // move the ghost messages at ~50 GB/s, slower than the copy kernels even beside it.
   static constexpr hipMemcpyKind kCopyKind = hipMemcpyDeviceToDevice;
 
  public:
@@ -138,25 +153,78 @@ class LocalTransport final : public SlabTransport {
   }
   void exchange(const void* sl, size_t nsl, const void* sr, size_t nsr, void* rl, size_t nrl, void* rr, size_t nrr,
                 hipStream_t s) override {
-    check_hip(hipStreamSynchronize(s), "exchange: send buffers");
+    post(sl, nsl, sr, nsr, s);
+    collect(rl, nrl, rr, nrr, s);
+  }
+  void post(const void* sl, size_t nsl, const void* sr, size_t nsr, hipStream_t s) override {
+    events(s);
     LocalHub::Slot& me = hub_->slots[size_t(rank)];
-    me.sl = sl;
-    me.nsl = nsl;
-    me.sr = sr;
-    me.nsr = nsr;
-    hub_->barrier();
-    if (has_left() && nrl) {
-      const LocalHub::Slot& L = hub_->slots[size_t(rank - 1)];
-      if (L.nsr != nrl) throw SphError(SPH_ERR_COMM, "exchange: size mismatch with the left slab");
-      check_hip(hipMemcpyAsync(rl, L.sr, nrl, kCopyKind, s), "exchange: copy from left");
+    const unsigned long long g = gen_ + 1;
+    // the neighbours have issued their copies of this rank's previous buffers: the stream
+    // waits for them before anything is written again (the caller writes the new buffers
+    // before posting them; drain_sends() covers buffers it frees or reallocates)
+    reuse_guard(s);
+    const hipError_t e = hipEventRecord(me.ready, s);
+    check_hip(e, "exchange: post");
+    hub_->publish([&] {
+      me.sl = sl;
+      me.nsl = has_left() ? nsl : 0;
+      me.sr = sr;
+      me.nsr = has_right() ? nsr : 0;
+      me.posted = g;
+    });
+    gen_ = g;
+  }
+  void collect(void* rl, size_t nrl, void* rr, size_t nrr, hipStream_t s) override {
+    LocalHub::Slot& me = hub_->slots[size_t(rank)];
+    const unsigned long long g = gen_;
+    const LocalHub::Slot* L = has_left() ? &hub_->slots[size_t(rank - 1)] : nullptr;
+    const LocalHub::Slot* R = has_right() ? &hub_->slots[size_t(rank + 1)] : nullptr;
+    hub_->wait_until([&] { return (!L || L->posted >= g) && (!R || R->posted >= g); });
+    if (L && nrl) {
+      if (L->nsr != nrl) throw SphError(SPH_ERR_COMM, "exchange: size mismatch with the left slab");
+      check_hip(hipStreamWaitEvent(s, L->ready, 0), "exchange: wait left");
+      check_hip(hipMemcpyAsync(rl, L->sr, nrl, kCopyKind, s), "exchange: copy from left");
     }
-    if (has_right() && nrr) {
+    if (R && nrr) {
+      if (R->nsl != nrr) throw SphError(SPH_ERR_COMM, "exchange: size mismatch with the right slab");
+      check_hip(hipStreamWaitEvent(s, R->ready, 0), "exchange: wait right");
+      check_hip(hipMemcpyAsync(rr, R->sl, nrr, kCopyKind, s), "exchange: copy from right");
+    }
+    check_hip(hipEventRecord(me.copied, s), "exchange: copies");
+    hub_->publish([&] { me.consumed = g; });
+  }
+  void drain_sends() override {
+    if (!gen_) return;
+    const unsigned long long g = gen_;
+    const LocalHub::Slot* L = has_left() ? &hub_->slots[size_t(rank - 1)] : nullptr;
+    const LocalHub::Slot* R = has_right() ? &hub_->slots[size_t(rank + 1)] : nullptr;
+    hub_->wait_until([&] { return (!L || L->consumed >= g) && (!R || R->consumed >= g); });
+    if (L) check_hip(hipEventSynchronize(L->copied), "exchange: drain left");
+    if (R) check_hip(hipEventSynchronize(R->copied), "exchange: drain right");
+  }
+  bool turns() const override { return hub_->turns; }
+  void turn_wait(int kind, hipStream_t a, hipStream_t b) override {
+    if (!hub_->turns || !has_left()) return;
+    const LocalHub::Slot& L = hub_->slots[size_t(rank - 1)];
+    const unsigned long long t = turn_[kind] + 1;
+    hub_->wait_until([&] { return L.turn[kind] >= t; });
+    if (a) check_hip(hipStreamWaitEvent(a, L.idone[kind], 0), "turn: wait");
+    if (b) check_hip(hipStreamWaitEvent(b, L.idone[kind], 0), "turn: wait");
+  }
+  void turn_done(int kind, hipStream_t s) override {
+    if (!hub_->turns) return;
+    events(s);
+    LocalHub::Slot& me = hub_->slots[size_t(rank)];
+    const unsigned long long t = turn_[kind] + 1;
+    // the right neighbour has issued its wait for this slab's previous turn
+    if (has_right()) {
       const LocalHub::Slot& R = hub_->slots[size_t(rank + 1)];
-      if (R.nsl != nrr) throw SphError(SPH_ERR_COMM, "exchange: size mismatch with the right slab");
-      check_hip(hipMemcpyAsync(rr, R.sl, nrr, kCopyKind, s), "exchange: copy from right");
+      hub_->wait_until([&] { return R.turn[kind] >= turn_[kind]; });
     }
-    check_hip(hipStreamSynchronize(s), "exchange: copies");
-    hub_->barrier();  // nobody reuses a send buffer before its copies are done
+    check_hip(hipEventRecord(me.idone[kind], s), "turn: record");
+    hub_->publish([&] { me.turn[kind] = t; });
+    turn_[kind] = t;
   }
   void allreduce_max_u32(unsigned* d, int n, hipStream_t s) override {
     if (n > 8) throw SphError(SPH_ERR_ARG, "allreduce: at most 8 values");
@@ -187,7 +255,31 @@ class LocalTransport final : public SlabTransport {
   }
 
  private:
+  // This slab's events, created on the device of its stream.
+  void events(hipStream_t s) {
+    LocalHub::Slot& me = hub_->slots[size_t(rank)];
+    if (me.ready) return;
+    int dev = 0, cur = 0;
+    check_hip(hipStreamGetDevice(s, &dev), "hipStreamGetDevice");
+    check_hip(hipGetDevice(&cur), "hipGetDevice");
+    check_hip(hipSetDevice(dev), "hipSetDevice");
+    for (hipEvent_t* e : {&me.ready, &me.copied, &me.idone[0], &me.idone[1]})
+      check_hip(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
+    check_hip(hipSetDevice(cur), "hipSetDevice");
+  }
+  // Before generation gen_ + 1 is posted: the neighbours consumed generation gen_ (their
+  // threads issued the copies) and the stream waits until those copies are done.
+  void reuse_guard(hipStream_t s) {
+    if (!gen_) return;
+    const unsigned long long g = gen_;
+    const LocalHub::Slot* L = has_left() ? &hub_->slots[size_t(rank - 1)] : nullptr;
+    const LocalHub::Slot* R = has_right() ? &hub_->slots[size_t(rank + 1)] : nullptr;
+    hub_->wait_until([&] { return (!L || L->consumed >= g) && (!R || R->consumed >= g); });
+    if (L) check_hip(hipStreamWaitEvent(s, L->copied, 0), "exchange: reuse left");
+    if (R) check_hip(hipStreamWaitEvent(s, R->copied, 0), "exchange: reuse right");
+  }
   std::shared_ptr<LocalHub> hub_;
+  unsigned long long gen_ = 0, turn_[2] = {0, 0};
 };
 
 std::unique_ptr<SlabTransport> make_local_transport(std::shared_ptr<LocalHub> hub, int rank) {

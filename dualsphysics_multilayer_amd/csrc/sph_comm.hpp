@@ -35,6 +35,31 @@ class SlabTransport {
   // column counts of the re-partition), added in rank order from 0.f so that both
   // transports give the same bits.
   virtual void allreduce_sum_f32(float* d, int n, hipStream_t s) = 0;
+  // The same exchange in two halves: post() when the send buffers are complete on stream s
+  // (nothing waits), collect() later on the same stream or one ordered after it.  RCCL and
+  // the shared-memory transport move the data in collect (one send/receive group); the
+  // in-process transport lets the neighbours copy from the posted buffers at once.  The
+  // send buffers stay untouched until the next post of the same transport.
+  virtual void post(const void* sl, size_t nsl, const void* sr, size_t nsr, hipStream_t s) {
+    (void)s;
+    posted_ = Posted{sl, nsl, sr, nsr};
+  }
+  virtual void collect(void* rl, size_t nrl, void* rr, size_t nrr, hipStream_t s) {
+    exchange(posted_.sl, posted_.nsl, posted_.sr, posted_.nsr, rl, nrl, rr, nrr, s);
+  }
+  // Before a send buffer is freed or reallocated: the neighbours' reads of every buffer this
+  // rank has sent are complete (RCCL / shm: the transfers are ordered on this rank's stream).
+  virtual void drain_sends() {}
+  // Measurement mode of the in-process transport (SPH_SLAB_TURNS=1, SphSlabGroup): slab r's
+  // interaction (kind TURN_INTERACTION) and the kernels of its divide after the exchange
+  // (TURN_DIVIDE) start on the GPU after slab r-1's of the same step have ended, so one GPU
+  // runs one slab's interaction (interior items + ghost transfer + face items) or divide at a
+  // time, as each rank does on its own GPU.  turn_wait() gates the streams a and b (either
+  // may be null), turn_done() ends the turn on stream s.  No-ops elsewhere.
+  enum { TURN_INTERACTION = 0, TURN_DIVIDE = 1 };
+  virtual bool turns() const { return false; }
+  virtual void turn_wait(int kind, hipStream_t a, hipStream_t b) { (void)kind; (void)a; (void)b; }
+  virtual void turn_done(int kind, hipStream_t s) { (void)kind; (void)s; }
   // Several exchanges fused into one transfer group (RCCL: ncclGroupStart/End).
   virtual void group_begin() {}
   virtual void group_end() {}
@@ -45,6 +70,14 @@ class SlabTransport {
   int rank = 0, nranks = 1;
   bool has_left() const { return rank > 0; }
   bool has_right() const { return rank + 1 < nranks; }
+
+ protected:
+  struct Posted {
+    const void* sl = nullptr;
+    size_t nsl = 0;
+    const void* sr = nullptr;
+    size_t nsr = 0;
+  } posted_;
 };
 
 // RCCL bootstrap: 128-byte ncclUniqueId created by rank 0 and broadcast by the host.
@@ -52,25 +85,53 @@ void rccl_unique_id(unsigned char id[128]);
 std::unique_ptr<SlabTransport> make_rccl_transport(const unsigned char id[128], int rank, int nranks);
 
 // Shared state of the in-process slabs: a generation barrier that can be aborted
-// (a failing slab wakes the others instead of leaving them blocked) and one mailbox
-// per slab.
+// (a failing slab wakes the others instead of leaving them blocked), one mailbox per
+// slab, and the point-to-point exchange state: the host threads only publish pointers,
+// events and generation counters (no host thread waits for the GPU), the copies wait for
+// the posting stream's event on the GPU.
 class LocalHub {
  public:
   explicit LocalHub(int n);
+  ~LocalHub();
   void barrier();  // throws if aborted
   void abort();
+  // Block until pred() holds (evaluated under the hub lock); throws if aborted.
+  template <class P>
+  void wait_until(P pred) {
+    std::unique_lock<std::mutex> lk(m_);
+    cv_.wait(lk, [&] { return aborted_ || pred(); });
+    if (aborted_) throw_aborted();
+  }
+  template <class F>
+  void publish(F f) {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      f();
+    }
+    cv_.notify_all();
+  }
   struct Slot {
+    // exchange generation g: the buffers posted (posted >= g), the neighbours' copies of
+    // them issued (consumed >= g: this slot's own copies of ITS neighbours' buffers)
     const void* sl = nullptr;
     size_t nsl = 0;
     const void* sr = nullptr;
     size_t nsr = 0;
+    unsigned long long posted = 0, consumed = 0;
+    hipEvent_t ready = nullptr;   // the posted buffers are complete
+    hipEvent_t copied = nullptr;  // this slot's copies of the neighbours' buffers are done
+    // turns (measurement mode), per kind: turns ended and the event of the last one
+    unsigned long long turn[2] = {0, 0};
+    hipEvent_t idone[2] = {nullptr, nullptr};
     unsigned vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     std::vector<float> fvals;
   };
   std::vector<Slot> slots;
   int n;
+  bool turns = false;  // SPH_SLAB_TURNS
 
  private:
+  [[noreturn]] static void throw_aborted();
   std::mutex m_;
   std::condition_variable cv_;
   int waiting_ = 0;

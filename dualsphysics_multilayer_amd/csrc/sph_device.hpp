@@ -198,9 +198,11 @@ constexpr unsigned ERR_DT_NAN = 1u, ERR_BOUNDOUT = 2u, ERR_HALO = 4u;
 // RunCellDivide): once one is flagged, a batched run stops stepping ON THE DEVICE — k_dt
 // no longer advances time/nstep and the update, motion and floating kernels leave the
 // state as it was, so the run ends at the failing step and sph_solver_sync reports it.
-// (ERR_HALO is reported at the next sync but does not halt: a slab's face re-send can flag it
-// for a stale face entry whose particle left that slab, which is harmless.)
-constexpr unsigned ERR_FATAL = ERR_DT_NAN | ERR_BOUNDOUT;
+// ERR_HALO (slabs: a ghost record the divide cannot fill, a face re-send record with no
+// ghost copy to land in, an mDBC ghost node reaching past the ghost columns) halts too: it
+// is folded into the dt all-reduce (folded[4]), so every slab stops at the same step rather
+// than stepping on with incomplete face data.
+constexpr unsigned ERR_FATAL = ERR_DT_NAN | ERR_BOUNDOUT | ERR_HALO;
 __device__ __forceinline__ bool halted(const DevScalars* sc) { return (sc->error_flags & ERR_FATAL) != 0u; }
 
 // Wave-level max of a non-negative float, then one atomicMax per wave into a slot

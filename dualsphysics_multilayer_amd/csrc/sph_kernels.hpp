@@ -240,18 +240,20 @@ void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const P
                  const double dom_posmin[3], float threshold, unsigned* list, unsigned* nlist, void* sums);
 constexpr size_t MDBC_SUM_BYTES = 152;  // sizeof(MdbcSum): 16 doubles + 5 floats + index
 // Slabs: (idp, rho, press) of the owned face-column boundary particles after mDBC, for
-// the neighbours' ghost copies (slot 0 holds the count; fixed capacity).
+// the neighbours' ghost copies (slot 0 holds the count).  Capacities capl / capr (records,
+// count slot included) are the exchange's face sizes + 1: both sides of a face derive the
+// same size, and it bounds the face's boundary particles, so no record is ever dropped.
 struct MdbcFaceRec {
   unsigned idp;
   float rho, press;
 };
 void launch_mdbc_face_pack(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& a,
                            const float* press, const KConst& K, const DivGrid& g, MdbcFaceRec* sl, MdbcFaceRec* sr,
-                           unsigned cap, unsigned* bidx, unsigned nbidx);
+                           unsigned capl, unsigned capr, unsigned* bidx, unsigned nbidx);
 // A record whose idp this slab does not hold as a boundary particle this step (bidx
-// stale or missing) raises ERR_HALO instead of writing.
+// stale or missing) raises ERR_HALO (fatal: every slab halts at this step) instead of writing.
 void launch_mdbc_face_apply(hipStream_t stm, DevScalars* sc, const MdbcFaceRec* rl, const MdbcFaceRec* rr,
-                            unsigned cap, const unsigned* bidx, unsigned nbidx, const unsigned* idp, float4* velrhop,
+                            unsigned capl, unsigned capr, const unsigned* bidx, unsigned nbidx, const unsigned* idp, float4* velrhop,
                             float* press);
 // NN multiphase interaction (sph_nn.hip; JSphCpu_NN_FDA.cpp of the v5.0 solver): all items
 // (fluid and bound p1) of the tiled item list; phases = the device phase table (2 float4

@@ -499,7 +499,7 @@ namespace sphx {
 __global__ __launch_bounds__(256) void k_mdbc_face_pack(const DevScalars* __restrict__ sc, PartArrays a,
                                                         const float* __restrict__ press, KConst K, DivGrid g,
                                                         MdbcFaceRec* __restrict__ sl, MdbcFaceRec* __restrict__ sr,
-                                                        unsigned cap, unsigned* __restrict__ bidx, unsigned nbidx) {
+                                                        unsigned capl, unsigned capr, unsigned* __restrict__ bidx, unsigned nbidx) {
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= sc->npb) return;
   const unsigned id = a.idp[p];
@@ -508,8 +508,9 @@ __global__ __launch_bounds__(256) void k_mdbc_face_pack(const DevScalars* __rest
   // a slab of one owned column sends the same particle both ways
   for (int side = 0; side < 2; side++) {
     MdbcFaceRec* dst = nullptr;
-    if (side == 0 && in_left_face(g, lcx) && g.xown0 > 0) dst = sl;
-    if (side == 1 && in_right_face(g, lcx) && g.xown1 < g.ncx) dst = sr;
+    unsigned cap = 0;
+    if (side == 0 && in_left_face(g, lcx) && g.xown0 > 0) { dst = sl; cap = capl; }
+    if (side == 1 && in_right_face(g, lcx) && g.xown1 < g.ncx) { dst = sr; cap = capr; }
     if (!dst) continue;
     const unsigned k = atomicAdd(&dst[0].idp, 1u);
     if (k + 1 < cap) dst[k + 1] = MdbcFaceRec{id, a.velrhop[p].w, press[p]};
@@ -519,12 +520,13 @@ __global__ __launch_bounds__(256) void k_mdbc_face_pack(const DevScalars* __rest
 
 __global__ __launch_bounds__(256) void k_mdbc_face_apply(DevScalars* __restrict__ sc,
                                                          const MdbcFaceRec* __restrict__ rl,
-                                                         const MdbcFaceRec* __restrict__ rr, unsigned cap,
-                                                         const unsigned* __restrict__ bidx, unsigned nbidx,
+                                                         const MdbcFaceRec* __restrict__ rr, unsigned capl,
+                                                         unsigned capr, const unsigned* __restrict__ bidx, unsigned nbidx,
                                                          const unsigned* __restrict__ idp,
                                                          float4* __restrict__ velrhop, float* __restrict__ press) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
   const MdbcFaceRec* r = (blockIdx.y == 0 ? rl : rr);
+  const unsigned cap = (blockIdx.y == 0 ? capl : capr);
   if (!r || i + 1 >= cap || i >= r[0].idp) return;
   const MdbcFaceRec q = r[i + 1];
   // bidx was rebuilt by this divide's face pack for the boundary particles held now; a
@@ -540,19 +542,21 @@ __global__ __launch_bounds__(256) void k_mdbc_face_apply(DevScalars* __restrict_
 
 void launch_mdbc_face_pack(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& a,
                            const float* press, const KConst& K, const DivGrid& g, MdbcFaceRec* sl, MdbcFaceRec* sr,
-                           unsigned cap, unsigned* bidx, unsigned nbidx) {
-  (void)hipMemsetAsync(sl, 0, sizeof(MdbcFaceRec), stm);
-  (void)hipMemsetAsync(sr, 0, sizeof(MdbcFaceRec), stm);
+                           unsigned capl, unsigned capr, unsigned* bidx, unsigned nbidx) {
+  if (capl) (void)hipMemsetAsync(sl, 0, sizeof(MdbcFaceRec), stm);
+  if (capr) (void)hipMemsetAsync(sr, 0, sizeof(MdbcFaceRec), stm);
   if (npbcap)
-    hipLaunchKernelGGL(k_mdbc_face_pack, dim3((npbcap + 255) / 256), dim3(256), 0, stm, sc, a, press, K, g, sl, sr, cap,
-                       bidx, nbidx);
+    hipLaunchKernelGGL(k_mdbc_face_pack, dim3((npbcap + 255) / 256), dim3(256), 0, stm, sc, a, press, K, g, sl, sr,
+                       capl, capr, bidx, nbidx);
 }
 
 void launch_mdbc_face_apply(hipStream_t stm, DevScalars* sc, const MdbcFaceRec* rl, const MdbcFaceRec* rr,
-                            unsigned cap, const unsigned* bidx, unsigned nbidx, const unsigned* idp, float4* velrhop,
-                            float* press) {
-  hipLaunchKernelGGL(k_mdbc_face_apply, dim3((cap + 255) / 256, 2), dim3(256), 0, stm, sc, rl, rr, cap, bidx, nbidx,
-                     idp, velrhop, press);
+                            unsigned capl, unsigned capr, const unsigned* bidx, unsigned nbidx, const unsigned* idp,
+                            float4* velrhop, float* press) {
+  const unsigned n = std::max(capl, capr);
+  if (!n) return;
+  hipLaunchKernelGGL(k_mdbc_face_apply, dim3((n + 255) / 256, 2), dim3(256), 0, stm, sc, rl, rr, capl, capr, bidx,
+                     nbidx, idp, velrhop, press);
 }
 
 }  // namespace sphx

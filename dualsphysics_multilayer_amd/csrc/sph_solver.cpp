@@ -465,7 +465,8 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   for (unsigned p : sel) npb0_ += (p < cdef.npb ? 1u : 0u);
   casenpb_ = cdef.npb;
   const unsigned n = unsigned(sel.size());
-  cap_ = slab() ? n + std::max(n / 2, 65536u) : n;
+  if (const char* e = std::getenv("SPH_SLAB_MINCAP")) slab_mincap_ = slab() && std::atoi(e) != 0;
+  cap_ = slab() ? n + (slab_mincap_ ? 16u : std::max(n / 2, 65536u)) : n;
   keybits_ = bits_for(G.boxdiscard, 1);
   // grid-sized buffers hold the widest grid a slab can get from a re-partition (all
   // columns + W = ghost_width ghost columns per face), so they never move
@@ -491,9 +492,10 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   if (C.kernel == SPH_KERNEL_CUBIC && !tiled_)
     throw SphError(SPH_ERR_UNSUPPORTED, "the Cubic spline kernel runs on the tiled interaction only");
   if (C.symmetry && !tiled_) throw SphError(SPH_ERR_UNSUPPORTED, "Symmetry runs on the tiled interaction only");
-  if (facex_) {
-    // the first interaction's face records: the initial particles of the face and ghost
-    // columns (both sides of a face count the same particles); later from each exchange
+  if (slab()) {
+    // the first interaction's face records (NN / SPS / mDBC face re-sends): the initial
+    // particles of the face and ghost columns (both sides of a face count the same
+    // particles); later from each exchange
     const std::vector<unsigned> cx = initial_columns(C, init);
     const bool hl = slabcfg_.rank > 0, hr = slabcfg_.rank + 1 < slabcfg_.nranks;
     const int W = ghost_width(C), c0 = slabcfg_.c0, c1 = slabcfg_.c1;
@@ -716,9 +718,10 @@ void SphGpuSingle::Free() {
   FreeParticles();
   for (void* p : allocs_) (void)hipFree(p);
   allocs_.clear();
-  for (void* p : {sendgbuf_, sendmbuf_, (void*)recvg_, (void*)recvm_, (void*)nnface_})
+  for (void* p : {sendgbuf_, sendmbuf_, (void*)recvg_, (void*)recvm_, (void*)nnface_, (void*)mdbcface_})
     if (p) (void)hipFree(p);
   nnface_ = nullptr;
+  mdbcface_ = nullptr;
   sendgbuf_ = sendmbuf_ = nullptr;
   recvg_ = nullptr;
   recvm_ = nullptr;
@@ -743,8 +746,8 @@ void SphGpuSingle::PresizeExchange(const SphParticlesHost& h) {
     if (cx < cnt.size()) mx = std::max(mx, ++cnt[cx]);
   }
   const unsigned long long g = (unsigned long long)mx * unsigned(ghost_width(C));
-  send_.gcap = g + g / 2 + 4096;
-  send_.mcap = g / 4 + 1024;
+  send_.gcap = slab_mincap_ ? 1 : g + g / 2 + 4096;
+  send_.mcap = slab_mincap_ ? 1 : g / 4 + 1024;
   check_hip(hipMalloc(&sendgbuf_, 2 * sizeof(SlabGhost) * send_.gcap), "hipMalloc ghost send buffers");
   send_.gl = (SlabGhost*)sendgbuf_;
   send_.gr = send_.gl + send_.gcap;
@@ -863,17 +866,8 @@ void SphGpuSingle::UploadNormals(const SphCaseDef& cdef, const SphParticlesHost&
   allocs_.push_back(normal_);
   check_hip(hipMemcpy(normal_, nor.data(), sizeof(float4) * nor.size(), hipMemcpyHostToDevice), "upload normals");
   if (slab()) {
-    // face-column boundary records: capacity from the densest x column of the case, x2
-    std::vector<unsigned> cnt(size_t(C.dom_cells[0]) + 1, 0u);
-    unsigned mx = 0;
-    for (unsigned p = 0; p < h.n; p++) {
-      if (h.idp[p] >= cdef.npb) continue;
-      const unsigned cx = unsigned((h.pos[3 * p] - C.dom_posmin[0]) / double(C.scell));
-      if (cx < cnt.size()) mx = std::max(mx, ++cnt[cx]);
-    }
-    mdbcfacecap_ = 2 * mx * unsigned(ghost_width(C)) + 64;  // W face columns
-    check_hip(hipMalloc((void**)&mdbcface_, sizeof(MdbcFaceRec) * 4 * size_t(mdbcfacecap_)), "hipMalloc mDBC faces");
-    allocs_.push_back(mdbcface_);
+    // face-column boundary records: sized per interaction from the exchange's face sizes
+    // (Interaction_Forces); the idp -> index map of the boundary particles
     check_hip(hipMalloc((void**)&bidx_, sizeof(unsigned) * std::max(cdef.npb, 1u)), "hipMalloc mDBC faces");
     allocs_.push_back(bidx_);
   }
@@ -948,7 +942,7 @@ void SphGpuSingle::Timing(double out_ms[4], uint64_t* launches) {
 // (device), swap the face messages (migrant count, ghost count per face box) with both
 // neighbours device to device, then ONE host wait to size the transfers; move the migrants
 // (96-112 B records) and append them.  The divide reserves the ghosts' slots; their
-// records follow it (launch_ghost_pack -> GhostTransfer), beside the interaction of the
+// records follow it (launch_ghost_pack -> post; GhostCollect), beside the interaction of the
 // items that need no ghost when the step allows it (OverlapGhosts).
 void SphGpuSingle::Exchange() {
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET), withpre = havepre_;
@@ -974,9 +968,10 @@ void SphGpuSingle::Exchange() {
   WaitEvent(xev_, "exchange: wait counts");
   const SlabCounts c = *slabcnt_host_;
   SLAB_TRACE("exchange: counts");
-  if (facex_) {
+  {
     // the neighbour's ghosts of this slab: the ghosts sent now + the migrants it sent here
-    // (it keeps them as ghosts); the neighbour derives the same sizes from its counts
+    // (it keeps them as ghosts); the neighbour derives the same sizes from its counts.  They
+    // size the face re-sends after the divide (NN eta / tau, SPS tau, mDBC densities) exactly
     face_sl_ = hl ? unsigned(c.sendl[0] + c.recvl[1]) : 0u;
     face_sr_ = hr ? unsigned(c.sendr[0] + c.recvr[1]) : 0u;
     face_rl_ = hl ? unsigned(c.recvl[0] + c.sendl[1]) : 0u;
@@ -984,17 +979,19 @@ void SphGpuSingle::Exchange() {
   }
   const unsigned long long gneed = std::max(c.sendl[0], c.sendr[0]), mneed = std::max(c.sendl[1], c.sendr[1]);
   if (gneed > send_.gcap) {  // the ghost records are packed after the divide: room for them
+    transport_->drain_sends();  // the neighbours' reads of the old buffer are done
     check_hip(hipStreamSynchronize(stream), "exchange: sync");
     if (sendgbuf_) check_hip(hipFree(sendgbuf_), "hipFree");
-    send_.gcap = gneed + gneed / 2 + 4096;
+    send_.gcap = slab_mincap_ ? gneed : gneed + gneed / 2 + 4096;
     check_hip(hipMalloc(&sendgbuf_, 2 * sizeof(SlabGhost) * send_.gcap), "hipMalloc ghost send buffers");
     send_.gl = (SlabGhost*)sendgbuf_;
     send_.gr = send_.gl + send_.gcap;
   }
   if (mneed > send_.mcap) {  // migrant records past the capacity were not written: grow, pack again
+    transport_->drain_sends();  // ... and the face messages are rewritten: their reads are done
     check_hip(hipStreamSynchronize(stream), "exchange: sync");
     if (sendmbuf_) check_hip(hipFree(sendmbuf_), "hipFree");
-    send_.mcap = mneed + mneed / 2 + 1024;
+    send_.mcap = slab_mincap_ ? mneed : mneed + mneed / 2 + 1024;
     check_hip(hipMalloc(&sendmbuf_, 2 * sizeof(SlabRec) * send_.mcap), "hipMalloc migrant send buffers");
     send_.ml = (SlabRec*)sendmbuf_;
     send_.mr = send_.ml + send_.mcap;
@@ -1009,18 +1006,18 @@ void SphGpuSingle::Exchange() {
   if (rgl + rgr > recvgcap_) {
     check_hip(hipStreamSynchronize(stream), "exchange: sync");
     if (recvg_) check_hip(hipFree(recvg_), "hipFree");
-    recvgcap_ = rgl + rgr + (rgl + rgr) / 2 + 4096;
+    recvgcap_ = slab_mincap_ ? rgl + rgr : rgl + rgr + (rgl + rgr) / 2 + 4096;
     check_hip(hipMalloc((void**)&recvg_, sizeof(SlabGhost) * recvgcap_), "hipMalloc ghost receive buffer");
   }
   if (rml + rmr > recvmcap_) {
     check_hip(hipStreamSynchronize(stream), "exchange: sync");
     if (recvm_) check_hip(hipFree(recvm_), "hipFree");
-    recvmcap_ = rml + rmr + (rml + rmr) / 2 + 1024;
+    recvmcap_ = slab_mincap_ ? rml + rmr : rml + rmr + (rml + rmr) / 2 + 1024;
     check_hip(hipMalloc((void**)&recvm_, sizeof(SlabRec) * recvmcap_), "hipMalloc migrant receive buffer");
   }
   const unsigned long long nin = rgl + rgr + rml + rmr;  // the ghosts' slots are reserved by the divide
   if (c.np + nin > cap_) {
-    const unsigned long long want = (c.np + nin) + (c.np + nin) / 2;
+    const unsigned long long want = (c.np + nin) + (slab_mincap_ ? 16 : (c.np + nin) / 2);
     if (want >= (1ull << 31)) throw SphError(SPH_ERR_NOMEM, "slab particle capacity overflow");
     Grow(c.np, unsigned(want));
   }
@@ -1041,20 +1038,26 @@ void SphGpuSingle::Exchange() {
   inc_.napp = xg_nm_;
 }
 
-// The ghost records of the last divide: packed from the sorted face columns by the divide
-// (launch_ghost_pack), sent to / received from both neighbours on stream s, written into the
-// slots the divide reserved.
-void SphGpuSingle::GhostTransfer(hipStream_t s) {
-  SLAB_TRACE("ghosts: transfer");
-  transport_->exchange(send_.gl, sizeof(SlabGhost) * xg_sl_, send_.gr, sizeof(SlabGhost) * xg_sr_, recvg_,
-                       sizeof(SlabGhost) * xg_rl_, recvg_ + xg_rl_, sizeof(SlabGhost) * xg_rr_, s);
+// The ghost records of the last divide: packed from the sorted face columns and posted by
+// the divide (launch_ghost_pack -> SlabTransport::post), received from both neighbours on
+// stream s, written into the slots the divide reserved.
+void SphGpuSingle::GhostCollect(hipStream_t s) {
+  SLAB_TRACE("ghosts: collect");
+  transport_->collect(recvg_, sizeof(SlabGhost) * xg_rl_, recvg_ + xg_rl_, sizeof(SlabGhost) * xg_rr_, s);
   launch_ghost_scatter(s, sc_, recvg_, unsigned(xg_rl_ + xg_rr_), inc_.apppos + xg_nm_, cur_, K, C.dom_posmin,
                        poscell_, press_, G, inc_ok_ ? inc_.skeys : nullptr, nn_ ? phaseeos_ : nullptr);
 }
 
+// The ghosts of the last divide still in flight (end of a run): in place on the solver stream.
 void SphGpuSingle::GhostFinish() {
   if (!ghost_pending_) return;
-  GhostTransfer(stream);
+  if (ghost_split_) {  // packed and posted on the exchange stream
+    GhostCollect(xstream_);
+    check_hip(hipEventRecord(ev_ghost_, xstream_), "ghosts: event");
+    check_hip(hipStreamWaitEvent(stream, ev_ghost_, 0), "ghosts: join");
+  } else {
+    GhostCollect(stream);
+  }
   ghost_pending_ = false;
 }
 
@@ -1063,10 +1066,11 @@ void SphGpuSingle::GhostFinish() {
 // inside Run(), without mDBC (its correction reads ghosts first), bodies (their particle map
 // is built after the divide) or the NN / Laminar+SPS / shifting kernels (face exchanges of
 // per-particle values first).
-bool SphGpuSingle::OverlapGhosts() const {
-  return slab() && overlap_ && in_run_ && tiled_ && !nn_ && !ext_ && !normal_ && !nftp_ && !nmotobj_ &&
+bool SphGpuSingle::OverlapEligible() const {
+  return slab() && in_run_ && tiled_ && !nn_ && !ext_ && !normal_ && !nftp_ && !nmotobj_ &&
          (transport_->has_left() || transport_->has_right());
 }
+bool SphGpuSingle::OverlapGhosts() const { return overlap_ && OverlapEligible(); }
 
 // The one host wait of a slab divide: spin on the event (a blocking synchronise wakes up
 // tens of us later) with a deadline, polling the transport's asynchronous error state.  A
@@ -1152,6 +1156,27 @@ void SphGpuSingle::Repartition() {
   repart_count_++;
 }
 
+void SphGpuSingle::ShareDeviceCheck() {
+  if (!slab() || transport_->nranks < 2) return;
+  char bus[64] = {0};
+  check_hip(hipDeviceGetPCIBusId(bus, int(sizeof(bus)) - 1, device), "hipDeviceGetPCIBusId");
+  unsigned h = 2166136261u;  // FNV-1a of the bus id, kept below 2^23: exact as a float sum term
+  for (const char* c = bus; *c; c++) h = (h ^ unsigned((unsigned char)*c)) * 16777619u;
+  const float mine = float((h & 0x7fffffu) + 1u);
+  const int nr = transport_->nranks;
+  std::vector<float> v(size_t(nr), 0.f);
+  v[size_t(slabcfg_.rank)] = mine;
+  float* d = nullptr;
+  check_hip(hipMalloc((void**)&d, sizeof(float) * size_t(nr)), "hipMalloc device check");
+  check_hip(hipMemcpy(d, v.data(), sizeof(float) * v.size(), hipMemcpyHostToDevice), "device check");
+  transport_->allreduce_sum_f32(d, nr, stream);
+  check_hip(hipMemcpyAsync(v.data(), d, sizeof(float) * v.size(), hipMemcpyDeviceToHost, stream), "device check");
+  check_hip(hipStreamSynchronize(stream), "device check");
+  (void)hipFree(d);
+  for (int r = 0; r < nr; r++)
+    if (r != slabcfg_.rank && v[size_t(r)] == mine) overlap_ = false;
+}
+
 void SphGpuSingle::SetRepartition(unsigned every, double bound_weight, double tolerance) {
   if (!slab()) throw SphError(SPH_ERR_STATE, "re-partitioning applies to slab solvers only");
   if (!(bound_weight >= 0) || !(tolerance >= 0)) throw SphError(SPH_ERR_ARG, "invalid re-partition weights");
@@ -1161,13 +1186,20 @@ void SphGpuSingle::SetRepartition(unsigned every, double bound_weight, double to
 }
 
 void SphGpuSingle::RunCellDivide() {
-  TimedBegin(2);
+  // turns measurement mode: the divide's kernels after the exchange are a turn of their own
+  // and the timed divide phase is those kernels alone (the exchange waits for neighbours)
+  const bool turn = slab() && exchange_armed_ && in_run_ && transport_->turns();
+  if (!turn) TimedBegin(2);
   if (slab() && exchange_armed_ && repart_every_ && (stepsdone_ % repart_every_) == 0 && transport_->nranks > 1 &&
       !havepre_)
     Repartition();
   // the exchange of this divide: ghosts in reserved slots, their records after the sort
   const bool ghosts = slab() && exchange_armed_ && (transport_->has_left() || transport_->has_right());
   if (slab() && exchange_armed_) Exchange();
+  if (turn) {
+    transport_->turn_wait(SlabTransport::TURN_DIVIDE, stream, nullptr);
+    TimedBegin(2);
+  }
   const unsigned ngl = ghosts ? unsigned(xg_rl_) : 0u, ngr = ghosts ? unsigned(xg_rr_) : 0u;
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET);
   // Items (each build also zeroes its queues).  A slab with neighbours cuts its rows where
@@ -1219,20 +1251,31 @@ void SphGpuSingle::RunCellDivide() {
   inc_.napp = 0;
   inc_.nvl = inc_.nvr = 0;
   std::swap(cur_, alt_);
-  // this slab's ghost records for the neighbours, from its sorted face columns
-  if (ghosts) launch_ghost_pack(stream, sc_, faces_, G, begincell_, cur_, poscell_, send_, unsigned(xg_sl_), unsigned(xg_sr_));
   qpass_ = 0;
   if (ghosts) {
+    // this slab's ghost records for the neighbours, from its sorted face columns, posted at
+    // once.  With the overlap they are packed on the exchange stream, so the interaction's
+    // interior items follow the divide directly on the solver stream; the transfer and the
+    // scatter follow in the interaction (also, in the turns measurement mode, the in-place
+    // transfer: it is then part of the slab's own interaction turn).
+    hipStream_t gs = stream;
     if (overlap) {
-      if (!ev_div_) check_hip(hipEventCreateWithFlags(&ev_div_, hipEventDisableTiming), "hipEventCreate");
+      ExchangeStream();
       check_hip(hipEventRecord(ev_div_, stream), "divide: event");
-      ghost_pending_ = true;  // sent by the next interaction, beside its interior items
+      check_hip(hipStreamWaitEvent(xstream_, ev_div_, 0), "ghosts: wait divide");
+      gs = xstream_;
+    }
+    launch_ghost_pack(gs, sc_, faces_, G, begincell_, cur_, poscell_, send_, unsigned(xg_sl_), unsigned(xg_sr_));
+    transport_->post(send_.gl, sizeof(SlabGhost) * xg_sl_, send_.gr, sizeof(SlabGhost) * xg_sr_, gs);
+    if (overlap || (transport_->turns() && OverlapEligible())) {
+      ghost_pending_ = true;
     } else {
-      GhostTransfer(stream);
+      GhostCollect(stream);
     }
   }
   if (nftp_) launch_ft_ridp(stream, cap_, sc_, cur_, casenpb_, nftp_, ftridp_, K, G);
   TimedEnd(2);
+  if (turn) transport_->turn_done(SlabTransport::TURN_DIVIDE, stream);
 }
 
 unsigned SphGpuSingle::NextQueueCopy() {
@@ -1246,19 +1289,49 @@ unsigned SphGpuSingle::NextQueueCopy() {
 }
 
 void SphGpuSingle::Interaction_Forces(int interstep) {
+  bool t0 = false;  // the interaction's timed interval has begun
+  auto begin0 = [&] {
+    if (!t0) TimedBegin(0);
+    t0 = true;
+  };
+  // turns measurement mode (SPH_SLAB_TURNS, in-process slabs): this slab's interaction starts
+  // on the GPU after the previous slab's has ended
+  const bool turn = slab() && transport_->turns();
+  if (turn) {
+    ExchangeStream();
+    transport_->turn_wait(SlabTransport::TURN_INTERACTION, stream, xstream_);
+  }
+  if (ghost_pending_ && !ghost_split_) {  // deferred in-place ghosts: the transfer is timed with it
+    begin0();
+    GhostCollect(stream);
+    ghost_pending_ = false;
+  }
   // mDBC boundary correction first, except in the Symplectic corrector (JSphCpuSingle.cpp:525).
   if (normal_ && interstep != 3) {
     TimedBegin(3);
     launch_mdbc(stream, slab() ? cap_ : npb0_, sc_, cur_, press_, normal_, begincell_, G, K, C.dom_posmin, C.mdbc_threshold,
                 mdbclist_ + 1, mdbclist_, mdbcsums_);
     if (slab() && (transport_->has_left() || transport_->has_right())) {
-      const size_t fb = sizeof(MdbcFaceRec) * mdbcfacecap_;
-      MdbcFaceRec *sl = mdbcface_, *sr = mdbcface_ + mdbcfacecap_, *rl = sr + mdbcfacecap_, *rr = rl + mdbcfacecap_;
-      launch_mdbc_face_pack(stream, cap_, sc_, cur_, press_, K, G, sl, sr, mdbcfacecap_, bidx_, casenpb_);
-      transport_->exchange(sl, transport_->has_left() ? fb : 0, sr, transport_->has_right() ? fb : 0, rl,
-                           transport_->has_left() ? fb : 0, rr, transport_->has_right() ? fb : 0, stream);
-      launch_mdbc_face_apply(stream, sc_, transport_->has_left() ? rl : nullptr,
-                             transport_->has_right() ? rr : nullptr, mdbcfacecap_, bidx_, casenpb_, cur_.idp,
+      // records per side = the face's particles at the last exchange + the count slot: both
+      // sides of a face derive the same size, and no face record can be dropped
+      const bool hl = transport_->has_left(), hr = transport_->has_right();
+      const unsigned nsl = hl ? face_sl_ + 1u : 0u, nsr = hr ? face_sr_ + 1u : 0u;
+      const unsigned nrl = hl ? face_rl_ + 1u : 0u, nrr = hr ? face_rr_ + 1u : 0u;
+      const unsigned long long need = 0ull + nsl + nsr + nrl + nrr;
+      if (need > mdbcfacecap_) {
+        transport_->drain_sends();
+        check_hip(hipStreamSynchronize(stream), "mDBC faces: sync");
+        if (mdbcface_) check_hip(hipFree(mdbcface_), "hipFree");
+        mdbcface_ = nullptr;
+        const unsigned long long want = slab_mincap_ ? need : need + need / 2 + 1024;
+        check_hip(hipMalloc((void**)&mdbcface_, sizeof(MdbcFaceRec) * want), "hipMalloc mDBC faces");
+        mdbcfacecap_ = want;
+      }
+      MdbcFaceRec *sl = mdbcface_, *sr = sl + nsl, *rl = sr + nsr, *rr = rl + nrl;
+      launch_mdbc_face_pack(stream, cap_, sc_, cur_, press_, K, G, sl, sr, nsl, nsr, bidx_, casenpb_);
+      transport_->exchange(sl, sizeof(MdbcFaceRec) * nsl, sr, sizeof(MdbcFaceRec) * nsr, rl, sizeof(MdbcFaceRec) * nrl,
+                           rr, sizeof(MdbcFaceRec) * nrr, stream);
+      launch_mdbc_face_apply(stream, sc_, hl ? rl : nullptr, hr ? rr : nullptr, nrl, nrr, bidx_, casenpb_, cur_.idp,
                              cur_.velrhop, press_);
     }
     TimedEnd(3);
@@ -1269,7 +1342,7 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
     // NN multiphase (sph_nn.hip); the shifting sums only where they are applied: the
     // corrector (the predictor's RunShifting result is never used, shift=false in
     // ComputeSymplecticPre) and Verlet
-    TimedBegin(0);
+    begin0();
     launch_nn_tiled(stream, nblocks_tiled_, sc_, items_, qa, poscell_, cur_.velrhop, press_, cur_.code, begincell_,
                     G, K, phasek_, arace_, shiftpos_, shift_ && interstep != 2, viscoeta_, tau_, ftmassp_);
     if (nnsph_) {
@@ -1284,24 +1357,22 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
     // Laminar+SPS and/or shifting (sph_ext.hip).  Slabs with SPS: the ghosts' tau (the
     // owners' from the last interaction) first
     if (sps_ && slab() && (transport_->has_left() || transport_->has_right())) NNFaceExchange();
-    TimedBegin(0);
+    begin0();
     launch_fluid_ext(stream, nblocks_tiled_, sc_, items_, qa, poscell_, cur_.velrhop, press_, cur_.code, ftmassp_,
                      cur_.tau, begincell_, G, K, arace_, shiftpos_, taunew_, interstep != 2);
     if (sps_) std::swap(cur_.tau, taunew_);
   } else if (tiled_) {
     // The tiled kernel writes the arace of every owned particle (skipped boundary items
     // get ar = 0); its work queues are the copy NextQueueCopy picked.
-    TimedBegin(0);  // the timed interval is the interaction kernel alone (rocprof's per-kernel average)
+    begin0();  // the timed interval is the interaction kernel alone (rocprof's per-kernel average)
     if (ghost_pending_) {
-      // Slab: the interior items now, the ghost records in flight on the exchange stream;
-      // there the face items follow their arrival.  The interior kernel leaves a few block
-      // slots free so that the transfer and scatter kernels start at once.
+      // Slab: the interior items now, the ghost records in flight on the exchange stream
+      // (packed and posted there after the divide); there the face items follow their
+      // arrival.  The interior kernel leaves a few block slots free so that the transfer and
+      // scatter kernels start at once.
       launch_fluid_tiled(stream, nblocks_tiled_ - 64, sc_, items_, qa, poscell_, cur_.velrhop, press_, begincell_,
                          G, K, arace_, cur_.code, ftmassp_);
-      if (!xstream_) check_hip(hipStreamCreateWithFlags(&xstream_, hipStreamNonBlocking), "hipStreamCreate");
-      if (!ev_ghost_) check_hip(hipEventCreateWithFlags(&ev_ghost_, hipEventDisableTiming), "hipEventCreate");
-      check_hip(hipStreamWaitEvent(xstream_, ev_div_, 0), "ghosts: wait divide");
-      GhostTransfer(xstream_);
+      GhostCollect(xstream_);
       launch_fluid_tiled(xstream_, nblocks_tiled_, sc_, items_, qf, poscell_, cur_.velrhop, press_, begincell_, G,
                          K, arace_, cur_.code, ftmassp_);
       check_hip(hipEventRecord(ev_ghost_, xstream_), "ghosts: event");
@@ -1315,11 +1386,19 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
                            G, K, arace_, cur_.code, ftmassp_);
     }
   } else {
-    TimedBegin(0);
+    begin0();
     launch_interaction(stream, cap_, sc_, poscell_, cur_.velrhop, press_, begincell_, G, K, arace_, cur_.code,
                        ftmassp_);
   }
   TimedEnd(0);
+  if (turn) transport_->turn_done(SlabTransport::TURN_INTERACTION, stream);
+}
+
+// The exchange stream and its events (created on first use).
+void SphGpuSingle::ExchangeStream() {
+  if (!xstream_) check_hip(hipStreamCreateWithFlags(&xstream_, hipStreamNonBlocking), "hipStreamCreate");
+  if (!ev_div_) check_hip(hipEventCreateWithFlags(&ev_div_, hipEventDisableTiming), "hipEventCreate");
+  if (!ev_ghost_) check_hip(hipEventCreateWithFlags(&ev_ghost_, hipEventDisableTiming), "hipEventCreate");
 }
 
 // Slabs, SPH velocity gradients: the owned face-column fluid particles' eta (and tau) to the
@@ -1331,9 +1410,10 @@ void SphGpuSingle::NNFaceExchange() {
   const unsigned long long nrl = hl ? face_rl_ + 1ull : 0, nrr = hr ? face_rr_ + 1ull : 0;
   const unsigned long long need = nsl + nsr + nrl + nrr;
   if (need > nnfacecap_) {
+    transport_->drain_sends();
     check_hip(hipStreamSynchronize(stream), "nn faces: sync");
     if (nnface_) check_hip(hipFree(nnface_), "hipFree");
-    nnfacecap_ = need + need / 2 + 1024;
+    nnfacecap_ = slab_mincap_ ? need : need + need / 2 + 1024;
     check_hip(hipMalloc((void**)&nnface_, sizeof(NNFaceRec) * nnfacecap_), "hipMalloc NN face records");
   }
   NNFaceRec *sl = nnface_, *sr = sl + nsl, *rl = sr + nsr, *rr = rl + nrl;

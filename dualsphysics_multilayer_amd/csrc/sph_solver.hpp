@@ -99,6 +99,9 @@ class SphGpuSingle {
   // Slabs: run the interaction of the items that reach no ghost column while the ghost
   // records of the divide are in flight (default on; off = ghosts in place before it).
   void SetOverlap(bool on) { overlap_ = on; }
+  // Collective over the slab's ranks (creation of separate-process ranks): the overlap off
+  // when another rank runs on this rank's GPU (the shared-device rule of SphSlabGroup).
+  void ShareDeviceCheck();
   SlabConfig Slab() const { return slabcfg_; }
   unsigned RepartitionCount() const { return repart_count_; }
   double LastImbalance() const { return repart_last_imbalance_; }
@@ -122,9 +125,11 @@ class SphGpuSingle {
   void UploadNormals(const SphCaseDef& cdef, const SphParticlesHost& init);
   void UploadPhases(const SphCaseDef& cdef);
   void Exchange();
-  void GhostTransfer(hipStream_t s);  // the ghost records of the last divide into their slots
-  void GhostFinish();                 // ... on the solver stream, if still pending
+  void GhostCollect(hipStream_t s);   // the posted ghost records of the last divide into their slots
+  void GhostFinish();                 // ... joined to the solver stream, if still pending
+  bool OverlapEligible() const;       // nothing between the divide and the interaction reads a ghost
   bool OverlapGhosts() const;         // the interaction can start before the ghosts are in
+  void ExchangeStream();              // xstream_ and its events
   void WaitEvent(hipEvent_t ev, const char* what);
   void Repartition();
   void RunMotion();                 // JSphCpu::RunMotion after ComputeStep (JSphCpuSingle.cpp:1096)
@@ -142,8 +147,11 @@ class SphGpuSingle {
   float4* normal_ = nullptr;      // mDBC: particle -> ghost node, by idp [CaseNbound]
   unsigned* mdbclist_ = nullptr;  // mDBC: wet boundary particles of this interaction [npb] + count
   void* mdbcsums_ = nullptr;      // mDBC: reduced sums per listed particle (pass 2 -> solve)
-  MdbcFaceRec* mdbcface_ = nullptr;  // slabs + mDBC: send left, send right, recv left, recv right [4][facecap]
-  unsigned mdbcfacecap_ = 0;
+  MdbcFaceRec* mdbcface_ = nullptr;  // slabs + mDBC: send left, send right, recv left, recv right (face sizes + 1)
+  unsigned long long mdbcfacecap_ = 0;
+  // SPH_SLAB_MINCAP test hook: every slab buffer starts at (or grows to) its minimum, so each
+  // grow-and-redo path runs (tests/test_gpu_slab.py checks the runs stay bitwise the same)
+  bool slab_mincap_ = false;
   unsigned* bidx_ = nullptr;         // slabs + mDBC: boundary idp -> index [CaseNpb]
   float4* arace_ = nullptr;
   // NN multiphase (v5.0 solver) and shifting

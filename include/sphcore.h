@@ -368,6 +368,8 @@ int sph_slab_group_set_repartition(SphSlabGroup* g, uint32_t every, double bound
 /* Ghost exchange beside the interaction (default on): the ghost records of a divide travel
  * while the items whose stencil reaches no ghost column interact; the face items follow.
  * Off: the ghosts are in place before the interaction.  Results are bitwise the same.
+ * Default off for slabs that share a GPU with another slab of the run (groups: same device
+ * id; sph_slab_create / _shm: same PCI bus id, checked collectively at creation).
  * (No reference counterpart: the fork runs one domain per process, JSphGpuSingle.) */
 int sph_slab_set_overlap(SphSolver* s, int on);
 int sph_slab_group_set_overlap(SphSlabGroup* g, int on);

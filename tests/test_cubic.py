@@ -115,7 +115,7 @@ def test_gpu_cubic_slabs_match_reference(name, nslabs):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cellmode", [1, 2])
-@pytest.mark.parametrize("ddt", [0, 2])
+@pytest.mark.parametrize("ddt", [0, 1, 2, 3])
 def test_gpu_cubic_interaction_identical_input(ddt, cellmode):
     """One Cubic interaction (tensile term included) on the same developing state, GPU vs
     oracle, per particle within 1e-5 of the array maximum (as test_gpu_parity)."""

@@ -4,14 +4,14 @@ The small reference fixtures pin every formulation; these tests check the number
 bench times, at full size:
 
 * cfg2 (1,025,964 particles, Verlet + DDT2) and cfg3 (9,969,118 particles, Symplectic +
-  DDT (Molteni) 0.1): the GPU after 1 and 2 steps against the REFERENCE v5.2 solver run
-  here on the case gencase_ref writes, and cfg3 also against the oracle (the C++
-  restatement of JSphCpu pinned to the reference's PARTs, tests/test_oracle_golden.py),
-  at the step tolerances of test_gpu_parity;
+  DDT (Molteni) 0.1): the GPU after steps 1, 2 and 10 (cfg2) / 1, 2 and 5 (cfg3) against
+  the REFERENCE v5.2 solver run here on the case gencase_ref writes, and cfg3 also against
+  the oracle (the C++ restatement of JSphCpu pinned to the reference's PARTs,
+  tests/test_oracle_golden.py), at the step tolerances of test_gpu_parity;
 * cfg4, wave flume of 4,007,978 particles with a piston, a flap and a floating box, mDBC,
-  Verlet + DDT2: the GPU after 1 and 2 steps against the REFERENCE v5.2 solver run here on
-  the case genflume_ref writes (PARTs and the body state of PartFloat.fbi4), then 4 slabs
-  against one domain over 10 steps;
+  Verlet + DDT2: the GPU after steps 1, 2 and 10 against the REFERENCE v5.2 solver run here
+  on the case genflume_ref writes (PARTs and the body state of PartFloat.fbi4), then 4
+  slabs against one domain over 10 steps;
 * cfg5, the 3-phase NN wet dam break of 2,015,071 particles: the GPU after 1 step against
   the REFERENCE v5.0 NN solver run here, at 10x the noise floor of its fast-math vs
   strict builds on the same case; per-phase density bounds, determinism and 2 slabs
@@ -95,9 +95,9 @@ def test_cfg3_10m_matches_oracle():
     assert g.stats()["error_flags"] == 0
 
 
-def _dambreak_vs_reference(dp, step_algorithm, ddt, np_expected):
+def _dambreak_vs_reference(dp, step_algorithm, ddt, np_expected, ks=(1, 2)):
     """The dam break of spacing dp as gencase_ref writes it for the reference, loaded by the
-    case-file reader; the GPU after 1 and 2 steps against the REFERENCE v5.2 CPU solver run
+    case-file reader; the GPU after the steps `ks` against the REFERENCE v5.2 CPU solver run
     here on the same files (PARTs with double positions), at the step tolerances of
     test_gpu_parity (10x the reference's fast-math noise floor)."""
     _need("gencase_ref", "DualSPHysics5.2CPU_ref", "partdump_ref")
@@ -109,10 +109,10 @@ def _dambreak_vs_reference(dp, step_algorithm, ddt, np_expected):
                                "CaseDambreak", "1"], stdout=subprocess.DEVNULL)
         case = XmlCase(os.path.join(tmp, "CaseDambreak"))
         assert case.np == np_expected
-        ref, _ = _ref_parts("DualSPHysics5.2CPU_ref", os.path.join(tmp, "CaseDambreak"), 2, (1, 2), tmp, "ref")
+        ref, _ = _ref_parts("DualSPHysics5.2CPU_ref", os.path.join(tmp, "CaseDambreak"), max(ks), ks, tmp, "ref")
         g = _gpu(case)
         done = 0
-        for k in (1, 2):
+        for k in ks:
             g.run(k - done)
             done = k
             _check(by_idp(g.particles()), ref[k], tol(k), k)
@@ -124,14 +124,16 @@ def _dambreak_vs_reference(dp, step_algorithm, ddt, np_expected):
 
 @pytest.mark.timeout(900)
 def test_cfg2_1m_matches_reference():
-    """BASELINE cfg2 (1,025,964 particles, Verlet, DDT2) against the reference binary."""
-    _dambreak_vs_reference(0.0045, 1, 2, 1025964)
+    """BASELINE cfg2 (1,025,964 particles, Verlet, DDT2) against the reference binary after
+    steps 1, 2 and 10."""
+    _dambreak_vs_reference(0.0045, 1, 2, 1025964, (1, 2, 10))
 
 
 @pytest.mark.timeout(1500)
 def test_cfg3_10m_matches_reference():
-    """BASELINE cfg3 (9,969,118 particles, Symplectic, DDT Molteni) against the reference binary."""
-    _dambreak_vs_reference(CFG3_DP, 2, 1, 9969118)
+    """BASELINE cfg3 (9,969,118 particles, Symplectic, DDT Molteni) against the reference binary
+    after steps 1, 2 and 5."""
+    _dambreak_vs_reference(CFG3_DP, 2, 1, 9969118, (1, 2, 5))
 
 
 # ---- cfg4 -----------------------------------------------------------------------------------
@@ -151,13 +153,14 @@ def test_cfg4_4m_flume_matches_reference():
                               stdout=subprocess.DEVNULL)
         case = XmlCase(os.path.join(tmp, "CaseFlume"))
         assert case.np == 4007978 and case.np == WaveFlumeCase(CFG4_DP, tboundary=2).np
-        ref, out = _ref_parts("DualSPHysics5.2CPU_ref", os.path.join(tmp, "CaseFlume"), 2, (1, 2), tmp, "ref")
+        ks = (1, 2, 10)
+        ref, out = _ref_parts("DualSPHysics5.2CPU_ref", os.path.join(tmp, "CaseFlume"), max(ks), ks, tmp, "ref")
         subprocess.check_call([os.path.join(REF, "ftdump_ref"), out, os.path.join(tmp, "ft.bin")],
                               stdout=subprocess.DEVNULL)
         _, fc, fv, fw = load_ft(os.path.join(tmp, "ft.bin"))
         g = _gpu(case)
         done = 0
-        for k in (1, 2):
+        for k in ks:
             g.run(k - done)
             done = k
             _check(by_idp(g.particles()), ref[k], _flume_tol(k), k)
