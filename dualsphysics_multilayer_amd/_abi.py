@@ -5,7 +5,7 @@ import ctypes as C
 
 import numpy as np
 
-SPH_ABI_VERSION = 9
+SPH_ABI_VERSION = 10
 
 SPH_STATUS = {
     0: "SPH_OK",
@@ -29,7 +29,7 @@ SPH_SHIFT_NONE, SPH_SHIFT_NOBOUND, SPH_SHIFT_NOFIXED, SPH_SHIFT_FULL = 0, 1, 2, 
 SPH_MAXPHASES = 8
 _CASEDEF_DEFAULTS = {"tboundary": SPH_BOUND_DBC, "slipmode": SPH_SLIP_VEL0, "mdbc_threshold": 0.0,
                      "rheology": SPH_RHEOLOGY_SINGLE, "velgrad": SPH_VELGRAD_FDA, "tvisco": SPH_VISCO_ARTIFICIAL,
-                     "nphases": 0, "relaxation_dt": 0.2, "shift_mode": SPH_SHIFT_NONE, "pad_shift": 0,
+                     "nphases": 0, "relaxation_dt": 0.2, "shift_mode": SPH_SHIFT_NONE, "mdbc_corrector": 0,
                      "shift_coef": -2.0, "shift_tfs": 0.0, "phases": (),
                      "data2d": 0, "pad2d": 0, "data2d_posy": 0.0, "dtallparticles": 0, "symmetry": 0,
                      "dtfixed": 0.0}
@@ -91,7 +91,7 @@ class SphCaseDef(C.Structure):
         ("nphases", C.c_uint32),
         ("relaxation_dt", C.c_double),
         ("shift_mode", C.c_int32),
-        ("pad_shift", C.c_int32),
+        ("mdbc_corrector", C.c_int32),
         ("shift_coef", C.c_double),
         ("shift_tfs", C.c_double),
         ("phases", SphPhaseDef * SPH_MAXPHASES),

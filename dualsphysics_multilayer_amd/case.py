@@ -72,6 +72,7 @@ class DamBreakCase:
     tboundary: int = 1  # 1 DBC, 2 mDBC (<parameter Boundary>, JSph.cpp:626-640)
     slipmode: int = 1  # mDBC: only SLIP_Vel0 in this fork (JSph.cpp:788)
     mdbc_threshold: float = 0.0  # -mdbc_threshold (JSphCfgRun.cpp:124)
+    mdbc_corrector: int = 0  # <parameter MDBCCorrector> (JSph.cpp:639)
     # ViscoTreatment 1 artificial / 2 Laminar+SPS (then `visco` is the kinematic viscosity,
     # e.g. 1e-6), shifting mode 0-3 with ShiftCoef / ShiftTFS (JSph.cpp:620-700)
     tvisco: int = 1
@@ -255,6 +256,7 @@ class DamBreakCase:
             dtallparticles=int(getattr(self, "dtallparticles", 0)),
             dtfixed=float(getattr(self, "dtfixed", 0.0)),
             symmetry=int(bool(getattr(self, "symmetry", False))),
+            mdbc_corrector=int(getattr(self, "mdbc_corrector", 0)) if self.tboundary == 2 else 0,
         )
 
 
@@ -351,6 +353,9 @@ class WaveFlumeCase:
     shift_mode: int = 0
     shift_coef: float = -2.0
     shift_tfs: float = 0.0
+    # mDBC on the floating box too (genflume_ref ftnormals=1): its outer layer gets normals
+    ftnormals: bool = False
+    mdbc_corrector: int = 0  # <parameter MDBCCorrector> (JSph.cpp:639)
 
     def __post_init__(self) -> None:
         dp = self.dp
@@ -377,7 +382,11 @@ class WaveFlumeCase:
         bk, bj, bi = np.meshgrid(np.arange(bkc - nbh, bkc + nbh + 1), np.arange(bjc - nbh, bjc + nbh + 1),
                                  np.arange(bic - nbh, bic + nbh + 1), indexing="ij")
         blocks.append((bi.ravel(), bj.ravel(), bk.ravel()))
-        nor.append(np.zeros((bi.size, 3)))
+        fnor = np.zeros((bi.size, 3))
+        if self.ftnormals and self.tboundary == 2:  # outer layer -> the nearest limit point
+            for ax, off in enumerate((bi.ravel() - bic, bj.ravel() - bjc, bk.ravel() - bkc)):
+                fnor[:, ax] = np.where(off == nbh, hd, np.where(off == -nbh, -hd, 0.0))
+        nor.append(fnor)
         # fluid minus the box
         wk, wj, wi = np.meshgrid(np.arange(1, kd + 1), np.arange(1, ny), np.arange(ip + 1, nx), indexing="ij")
         inbox = (np.abs(wi - bic) <= nbh) & (np.abs(wj - bjc) <= nbh) & (np.abs(wk - bkc) <= nbh)
@@ -459,7 +468,8 @@ class WaveFlumeCase:
         return _xml_e10(self._mass)
 
     def normals_double(self) -> np.ndarray:
-        """<case>_Normals.nbi4 contents (double3[CaseNbound]; zero for the floating box)."""
+        """<case>_Normals.nbi4 contents (double3[CaseNbound]; zero for the floating box unless
+        ftnormals)."""
         return self._normals[: self.case_nbound]
 
     @property

@@ -595,12 +595,40 @@ __global__ void k_ft_forces(const DevScalars* __restrict__ sc, KConst K, FtBody*
     b.fomegares[k] = fomega[k];
     b.fcenterres[k] = fcenter[k];
   }
+  if (!predictor) {
+    // mDBC on the body: its normals turn by the step's change of the (float) angles, in
+    // degrees (JSphCpuSingle.cpp:988-999: Move(center) Rotate(dang) Move(-center0), of
+    // which MulNormal uses the 3x3 part, JMatrix4::MatrixRot = RotZ RotX RotY of the
+    // nonzero angles, JMatrix4.h:270-324)
+    double dang[3];
+    for (int k = 0; k < 3; k++) {
+      const float na = float(double(b.angles[k]) + double(fomega[k]) * dt);  // as k_ft_update
+      dang[k] = double(na - b.angles[k]) * 57.29577951308232087684;
+    }
+    M4d r;
+    m4_identity(r);
+    const int ax[3] = {2, 0, 1};
+    for (int q = 0; q < 3; q++) {
+      const int k = ax[q];
+      if (!dang[k]) continue;
+      const double rad = dang[k] * 0.017453292519943295769;
+      const double cs = cos(rad), sn = sin(rad);
+      M4d m;
+      m4_identity(m);
+      if (k == 0) { m.a[5] = cs; m.a[6] = -sn; m.a[9] = sn; m.a[10] = cs; }        // MatrixRotX
+      else if (k == 1) { m.a[0] = cs; m.a[2] = sn; m.a[8] = -sn; m.a[10] = cs; }   // MatrixRotY
+      else { m.a[0] = cs; m.a[1] = -sn; m.a[4] = sn; m.a[5] = cs; }                // MatrixRotZ
+      m4_mul(r, m);
+    }
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) b.nrot[3 * i + j] = r.a[4 * i + j];
+  }
 }
 
 // Particle update + body state (RunFloating, JSphCpuSingle.cpp:950-1003).
 __global__ __launch_bounds__(256) void k_ft_update(DevScalars* __restrict__ sc, KConst K, FtBody* __restrict__ bodies,
                                                    int nbodies, const unsigned* __restrict__ ftridp, unsigned nftp,
-                                                   PartArrays a, int predictor) {
+                                                   PartArrays a, int predictor, float4* __restrict__ normal) {
   const unsigned fp = blockIdx.x * blockDim.x + threadIdx.x;
   const double dt = (predictor ? sc->dt * .5 : sc->dt);
   if (fp < nftp && !halted(sc)) {
@@ -621,6 +649,16 @@ __global__ __launch_bounds__(256) void k_ft_update(DevScalars* __restrict__ sc, 
       v.y = b.fvelres[1] + (w[2] * dx - w[0] * dz);
       v.z = b.fvelres[2] + (w[0] * dy - w[1] * dx);
       a.velrhop[p] = v;
+      if (normal && !predictor) {  // BoundNormalc[p] = float3(mat.MulNormal(double3(normal)))
+        const unsigned id = a.idp[p];
+        const float4 n = normal[id];
+        if (n.x != 0.f || n.y != 0.f || n.z != 0.f) {
+          const double nx = n.x, ny = n.y, nz = n.z;
+          const double* m = b.nrot;
+          normal[id] = make_float4(float(m[0] * nx + m[1] * ny + m[2] * nz), float(m[3] * nx + m[4] * ny + m[5] * nz),
+                                   float(m[6] * nx + m[7] * ny + m[8] * nz), 0.f);
+        }
+      }
     }
   }
   if (fp == 0 && !predictor && !halted(sc)) {
@@ -648,11 +686,11 @@ void launch_ft_partial(hipStream_t stm, DevScalars* sc, const FtBody* bodies, in
 
 void launch_ft_body(hipStream_t stm, DevScalars* sc, const KConst& K, FtBody* bodies, int nbodies,
                     const unsigned* ftridp, unsigned nftp, const PartArrays& a, bool predictor, const float* part,
-                    const double4* fttab, const int2* ftdesc) {
+                    const double4* fttab, const int2* ftdesc, float4* normal) {
   hipLaunchKernelGGL(k_ft_forces, dim3((nbodies + 63) / 64), dim3(64), 0, stm, sc, K, bodies, nbodies, part,
                      int(predictor), fttab, ftdesc);
   hipLaunchKernelGGL(k_ft_update, dim3((nftp + 255) / 256), dim3(256), 0, stm, sc, K, bodies, nbodies, ftridp, nftp,
-                     a, int(predictor));
+                     a, int(predictor), normal);
 }
 
 }  // namespace sphx

@@ -203,14 +203,31 @@ class LocalTransport final : public SlabTransport {
     if (L) check_hip(hipEventSynchronize(L->copied), "exchange: drain left");
     if (R) check_hip(hipEventSynchronize(R->copied), "exchange: drain right");
   }
+  void wait_sends(hipStream_t s) override {
+    if (!gen_) return;
+    reuse_guard(s);
+  }
   bool turns() const override { return hub_->turns; }
   void turn_wait(int kind, hipStream_t a, hipStream_t b) override {
-    if (!hub_->turns || !has_left()) return;
-    const LocalHub::Slot& L = hub_->slots[size_t(rank - 1)];
-    const unsigned long long t = turn_[kind] + 1;
-    hub_->wait_until([&] { return L.turn[kind] >= t; });
-    if (a) check_hip(hipStreamWaitEvent(a, L.idone[kind], 0), "turn: wait");
-    if (b) check_hip(hipStreamWaitEvent(b, L.idone[kind], 0), "turn: wait");
+    if (!hub_->turns) return;
+    if (has_left()) {
+      const LocalHub::Slot& L = hub_->slots[size_t(rank - 1)];
+      const unsigned long long t = turn_[kind] + 1;
+      hub_->wait_until([&] { return L.turn[kind] >= t; });
+      if (a) check_hip(hipStreamWaitEvent(a, L.idone[kind], 0), "turn: wait");
+      if (b) check_hip(hipStreamWaitEvent(b, L.idone[kind], 0), "turn: wait");
+    } else if (nranks > 1) {
+      // the chain of one kind starts after the last slab's turn of the other kind (the
+      // divides of a step all end before its first interaction, and the other way round)
+      const int other = 1 - kind;
+      const LocalHub::Slot& Z = hub_->slots[size_t(nranks - 1)];
+      const unsigned long long t = turn_[other];
+      if (t) {
+        hub_->wait_until([&] { return Z.turn[other] >= t; });
+        if (a) check_hip(hipStreamWaitEvent(a, Z.idone[other], 0), "turn: wait");
+        if (b) check_hip(hipStreamWaitEvent(b, Z.idone[other], 0), "turn: wait");
+      }
+    }
   }
   void turn_done(int kind, hipStream_t s) override {
     if (!hub_->turns) return;

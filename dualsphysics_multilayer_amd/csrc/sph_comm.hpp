@@ -50,6 +50,9 @@ class SlabTransport {
   // Before a send buffer is freed or reallocated: the neighbours' reads of every buffer this
   // rank has sent are complete (RCCL / shm: the transfers are ordered on this rank's stream).
   virtual void drain_sends() {}
+  // Stream s waits until the neighbours have read the buffers of the last post, before it
+  // writes them again (RCCL / shm: a send completes in this rank's stream order already).
+  virtual void wait_sends(hipStream_t s) { (void)s; }
   // Measurement mode of the in-process transport (SPH_SLAB_TURNS=1, SphSlabGroup): slab r's
   // interaction (kind TURN_INTERACTION) and the kernels of its divide after the exchange
   // (TURN_DIVIDE) start on the GPU after slab r-1's of the same step have ended, so one GPU

@@ -193,7 +193,12 @@ struct DevScalars {
 // RED_VISCETA: NN max effective viscosity (ViscEtaDtMax, JSphCpuSingle.cpp:633 in the v5.0 solver)
 constexpr int RED_VELMAX2 = 0, RED_ACEMAX2 = 1, RED_VISCDT = 2, RED_VISCETA = 3, RED_SLOTS = 64;
 
-constexpr unsigned ERR_DT_NAN = 1u, ERR_BOUNDOUT = 2u, ERR_HALO = 4u;
+constexpr unsigned ERR_DT_NAN = 1u, ERR_BOUNDOUT = 2u;
+// slab halo errors, by site: an mDBC ghost node whose support leaves the slab's grid, a face
+// record that does not fit its buffer, a face record with no ghost copy to land in, a ghost
+// record the divide cannot fill
+constexpr unsigned ERR_HALO_NODE = 4u, ERR_HALO_FACE = 8u, ERR_HALO_MISS = 16u, ERR_HALO_GHOST = 32u;
+constexpr unsigned ERR_HALO = ERR_HALO_NODE | ERR_HALO_FACE | ERR_HALO_MISS | ERR_HALO_GHOST;
 // Errors the reference throws on (DtVariable, JSphCpu.cpp:1622; AbortBoundOut in
 // RunCellDivide): once one is flagged, a batched run stops stepping ON THE DEVICE — k_dt
 // no longer advances time/nstep and the update, motion and floating kernels leave the

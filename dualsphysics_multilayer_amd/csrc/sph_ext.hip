@@ -56,19 +56,24 @@ struct ExtArgs {
   const float4* tau;     // Laminar+SPS: tau of the previous interaction [2 np]
 };
 
+// mir (Symmetry): the records' images across the plane y = 0 (JSphCpu.cpp:684,709): y and
+// the y velocity negated; the item's frame starts at y = cy scell, so the image of a record
+// at frame y is at -(y) - 2 cy scell (mirc = cy).
 __device__ __forceinline__ void ext_stage(const KConst& K, const ExtArgs& E, unsigned rs, unsigned n, unsigned dst,
                                           int xo, int dy, int dz, bool boundrow, bool withtau,
                                           float4* __restrict__ sA, float4* __restrict__ sB, float4* __restrict__ sC,
-                                          float4* __restrict__ sD) {
-  const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
+                                          float4* __restrict__ sD, bool mir = false, int mirc = 0) {
+  const float oy = float(dy) * K.scell, oz = float(dz) * K.scell, my = float(2 * mirc) * K.scell;
   for (unsigned i = threadIdx.x; i < n; i += TB) {
     const unsigned q = rs + i;
     const float4 pc = E.poscell[q];
     const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
     const float x2 = pc.x + float(cx2 - xo) * K.scell;
-    const float y2 = pc.y + oy, z2 = pc.z + oz;
+    const float y2 = mir ? -(pc.y + oy) - my : pc.y + oy, z2 = pc.z + oz;
     sA[dst + i] = make_float4(x2, y2, z2, x2 * x2 + y2 * y2 + z2 * z2);
-    sB[dst + i] = E.velrhop[q];
+    float4 vr = E.velrhop[q];
+    if (mir) vr.y = -vr.y;
+    sB[dst + i] = vr;
     const typecode c = E.code[q];
     float m2 = boundrow ? K.massbound : K.massfluid;
     bool flag = false, withtau2 = withtau && !boundrow;
@@ -89,6 +94,34 @@ __device__ __forceinline__ void ext_stage(const KConst& K, const ExtArgs& E, uns
   }
 }
 
+// Kernel factor fac (GetKernel_Fac<tker>, FunSphKernel.h:217-224 Wendland, :105-117 Cubic)
+// and, for the Cubic spline, its Wab (the tensile correction's, :122-136).  Beyond the support
+// (the masked pairs' rr2 = 1e30) both are 0.  The Cubic is a uniform runtime branch (K.cubic).
+__device__ __forceinline__ float ext_fac(const KConst& K, float rr2, float& wab) {
+  const float rad = fsqrt_(rr2);
+  if (K.cubic) {
+    const float qc = rad * K.ovkernelh;
+    const float wqc = fmaxf(2.f - qc, 0.f);
+    const bool far = rad > K.kernelh;
+    // beyond h: c2 (2-q)^2 / r; within it (c1 q + d1 q^2) / r = (c1 + d1 q) / h (finite at r = 0)
+    wab = far ? K.cub_a24 * (wqc * wqc * wqc) : K.cub_a2 * fmaf(fmaf(0.75f, qc, -1.5f), qc * qc, 1.f);
+    return far ? K.cub_c2 * wqc * wqc * frcp(rad) : fmaf(K.cub_d1, qc, K.cub_c1) * K.ovkernelh;
+  }
+  wab = 0.f;
+  const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
+  return K.bwenovh * (wq * wq * wq);
+}
+
+// GetKernelCubic_Tensil (FunSphKernel.h:141-149) from the pair's Wab.
+__device__ __forceinline__ float ext_tensil(const KConst& K, float wab, float rho1, float p1, float rho2, float p2) {
+  float fab = wab * K.cub_odw;
+  fab *= fab;
+  fab *= fab;
+  const float t1 = (p1 * frcp(rho1 * rho1)) * (p1 > 0.f ? 0.01f : -0.2f);
+  const float t2 = (p2 * frcp(rho2 * rho2)) * (p2 > 0.f ? 0.01f : -0.2f);
+  return fab * (t1 + t2);
+}
+
 // Fluid p1 pair (JSphCpu.cpp:682-797).  `ok` is the reference's pair test; a pair that fails
 // it arrives with dr = 0 and rr2 = 1e30 (kernel factor 0, every sum +0) and its switches
 // (DDT / shifting cut-offs, maxima) are masked.
@@ -96,9 +129,8 @@ template <int TVISCO, int TD, bool SHIFT, bool FT, bool BOUNDP2>
 __device__ __forceinline__ void ext_pair(const KConst& K, const ExtP1& p, float drx, float dry, float drz, float rr2,
                                          bool ok, const float4& B, const float4& C, const float4& D, float visco,
                                          ExtAcc& a) {
-  const float rad = fsqrt_(rr2);
-  const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
-  const float fac = K.bwenovh * (wq * wq * wq);
+  float wab;
+  const float fac = ext_fac(K, rr2, wab);
   const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
   const bool flag2 = C.y < 0.f;
   const bool ftp2 = FT && !BOUNDP2 && flag2;
@@ -109,8 +141,10 @@ __device__ __forceinline__ void ext_pair(const KConst& K, const ExtP1& p, float 
   }
   const float rho1 = p.vr.w, rho2 = B.w;
   const float inv_rho2 = frcp(rho2);
-  // momentum: -m2 (p1 + p2)/(rho1 rho2) fr
-  const float p_vpm = -((p.press + C.x) * frcp(rho1 * rho2)) * massp2;
+  // momentum: -m2 ((p1 + p2)/(rho1 rho2) + Cubic tensile correction) fr
+  float prs = (p.press + C.x) * frcp(rho1 * rho2);
+  if (K.cubic) prs += ext_tensil(K, wab, rho1, p.press, rho2, C.x);
+  const float p_vpm = -prs * massp2;
   a.ax = fmaf(p_vpm, frx, a.ax);
   a.ay = fmaf(p_vpm, fry, a.ay);
   a.az = fmaf(p_vpm, frz, a.az);
@@ -184,9 +218,8 @@ __device__ __forceinline__ void ext_pair(const KConst& K, const ExtP1& p, float 
 // Bound p1 over fluid p2 (InteractionForcesBound, :577-608): continuity and visc-dt.
 __device__ __forceinline__ void ext_bound_pair(const KConst& K, const ExtP1& p, float drx, float dry, float drz,
                                                float rr2, bool ok, const float4& B, const float4& C, ExtAcc& a) {
-  const float rad = fsqrt_(rr2);
-  const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
-  const float fac = K.bwenovh * (wq * wq * wq);
+  float wab;
+  const float fac = ext_fac(K, rr2, wab);
   const float dvx = p.vr.x - B.x, dvy = p.vr.y - B.y, dvz = p.vr.z - B.z;
   const float dot = drx * dvx + dry * dvy + drz * dvz;
   a.ar = fmaf(fabsf(C.y) * (fac * dot), p.vr.w * frcp(B.w), a.ar);
@@ -296,10 +329,29 @@ __device__ __forceinline__ void ext_pass(const KConst& K, const ExtArgs& E, cons
   const unsigned cellinit = (KIND == 1 ? 0u : g.boxfluid);
   const float px2 = -2.f * p.x, py2 = -2.f * p.y, pz2 = -2.f * p.z;
   const int nunits = mirrored ? NPAIR + 1 : NR * NR;
-  for (int u = 0; u < nunits; u++) {
+  // Symmetry: a p1 within 2h of y = 0 (the first S rows) also meets the images of the p2 of
+  // those rows (all within 2h of the plane), after its own rows: units of a mirrored z pair /
+  // the z = 0 row per image row (S == 1: the row itself; S == 2: rows 0 and 1), its own image
+  // skipped.  The reference visits an image right after its original when the original is
+  // within the support radius (JSphCpu.cpp:793-796); an image is never nearer than its
+  // original for y >= 0, so the images within the radius are exactly those.  Their order
+  // matters only for a shifting cut-off, which then has already frozen the sums (the passes
+  // drained in the reference's order are NoBound's / NoFixed's bound rows: the first bound
+  // pair in reach freezes them before its image; moving boundaries under NoFixed with
+  // Symmetry are refused).
+  const bool sym = K.symmetry && rc.cy < S;
+  const int nimg = sym ? S * (S + 1) : 0;  // image rows x (S mirrored z pairs + the z = 0 row)
+  for (int u = 0; u < nunits + nimg; u++) {
     int dza = 0, dya = 0;
-    bool paired = false;
-    if (mirrored) {
+    bool paired = false, mir = false, selfrow = false;
+    if (u >= nunits) {  // image unit: row ir of the first S rows, z unit iz
+      const int v = u - nunits, ir = v / (S + 1), iz = v % (S + 1);
+      mir = true;
+      dya = ir - rc.cy;
+      dza = iz < S ? -(iz + 1) : 0;
+      paired = iz < S;
+      selfrow = !paired && dya == 0;
+    } else if (mirrored) {
       paired = u < NPAIR;
       if (S == 1) {
         dza = (u == 0 || u == 1 || u == 2) ? -1 : 0;
@@ -315,7 +367,7 @@ __device__ __forceinline__ void ext_pass(const KConst& K, const ExtArgs& E, cons
 #pragma unroll
     for (int k = 0; k < 2; k++) {
       if (k == 1 && !paired) break;
-      const int dz = k ? -dza : dza, dy = k ? -dya : dya;
+      const int dz = k ? -dza : dza, dy = (k && !mir) ? -dya : dya;  // an image pair mirrors z only
       const int z = rc.cz + dz, y = rc.cy + dy;
       if (z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;
       const unsigned rowbase = cellinit + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
@@ -328,33 +380,46 @@ __device__ __forceinline__ void ext_pass(const KConst& K, const ExtArgs& E, cons
     if (n0 + n1 == 0u) continue;  // block-uniform
     if (n0 + n1 <= unsigned(TCAPX)) {
       __syncthreads();
-      if (n0) ext_stage(K, E, rs[0], n0, 0u, rc.xo, dya, dza, KIND == 1, WT, sA, sB, sC, sD);
-      if (n1) ext_stage(K, E, rs[1], n1, n0, rc.xo, -dya, -dza, KIND == 1, WT, sA, sB, sC, sD);
+      if (n0) ext_stage(K, E, rs[0], n0, 0u, rc.xo, dya, dza, KIND == 1, WT, sA, sB, sC, sD, mir, rc.cy);
+      if (n1) ext_stage(K, E, rs[1], n1, n0, rc.xo, mir ? dya : -dya, -dza, KIND == 1, WT, sA, sB, sC, sD, mir, rc.cy);
       __syncthreads();
       const int wa0 = int(ls[0] - rs[0]), wa1 = rc.act && n0 ? int(le[0] - rs[0]) : wa0;
       const int wb0 = int(n0 + ls[1] - rs[1]), wb1 = rc.act && n1 ? int(n0 + le[1] - rs[1]) : wb0;
+      // the own image (the lane's p1 in its own row's images) is no neighbour
+      const int self = (selfrow && rc.act && rc.p1 >= rs[0] && rc.p1 < re[0]) ? int(rc.p1 - rs[0]) : -1;
       for (int off = 0;; off += 128) {
         const int na = wa1 - wa0 - off, nb = wb1 - wb0 - off;
         if (na <= 0 && nb <= 0) break;
         unsigned long long c0, c1, c2, c3;
         test128(sA, wa0 + off, min(na, 128), px2, py2, pz2, thr, c0, c1);
         test128(sA, wb0 + off, min(nb, 128), px2, py2, pz2, thr, c2, c3);
+        if (self >= 0) {
+          const int ks = self - (wa0 + off);
+          if (ks >= 0 && ks < 64) c0 &= ~(1ull << ks);
+          else if (ks >= 64 && ks < 128) c1 &= ~(1ull << (ks - 64));
+        }
         ext_drain4<TVISCO, TD, SHIFT, FT, KIND>(K, p, c0, c1, c2, c3, wa0 + off, wa0 + off + 64, wb0 + off,
                                                 wb0 + off + 64, sA, sB, sC, sD, visco, a);
       }
     } else {
       for (int k = 0; k < (paired ? 2 : 1); k++) {
-        const int dz = k ? -dza : dza, dy = k ? -dya : dya;
+        const int dz = k ? -dza : dza, dy = (k && !mir) ? -dya : dya;
         for (unsigned seg = rs[k]; seg < re[k]; seg += TCAPX) {
           const unsigned segn = min(unsigned(TCAPX), re[k] - seg);
           __syncthreads();
-          ext_stage(K, E, seg, segn, 0u, rc.xo, dy, dz, KIND == 1, WT, sA, sB, sC, sD);
+          ext_stage(K, E, seg, segn, 0u, rc.xo, dy, dz, KIND == 1, WT, sA, sB, sC, sD, mir, rc.cy);
           __syncthreads();
           const int w0 = int(max(ls[k], seg) - seg);
           const int w1 = rc.act ? max(w0, int(min(le[k], seg + segn)) - int(seg)) : w0;
+          const int self = (selfrow && rc.act && rc.p1 >= seg && rc.p1 < seg + segn) ? int(rc.p1 - seg) : -1;
           for (int off = w0; off < w1; off += 128) {
             unsigned long long c0, c1;
             test128(sA, off, min(w1 - off, 128), px2, py2, pz2, thr, c0, c1);
+            if (self >= 0) {
+              const int ks = self - off;
+              if (ks >= 0 && ks < 64) c0 &= ~(1ull << ks);
+              else if (ks >= 64 && ks < 128) c1 &= ~(1ull << (ks - 64));
+            }
             ext_drain4<TVISCO, TD, SHIFT, FT, KIND>(K, p, c0, c1, 0ull, 0ull, off, off + 64, 0, 0, sA, sB, sC, sD,
                                                     visco, a);
           }

@@ -421,20 +421,21 @@ __device__ __forceinline__ void put_c(float4* sC, unsigned i, float pr, float ir
   const float rir = r * ir;
   sC[i] = make_float4(pr * rir, rir, r, kind);
 }
-// mir (Symmetry, rows of the first y row of a p1 in it): the records' images across y = 0,
-// position y and velocity y negated (JSphCpu.cpp:684,709).
+// mir (Symmetry, rows of the first y rows of a p1 in them): the records' images across y = 0,
+// position y and velocity y negated (JSphCpu.cpp:684,709); the item's frame starts at
+// y = mirc scell (its row), so the image of a record at frame y is at -y - 2 mirc scell.
 template <typename CR>
 __device__ __forceinline__ void stage_row(const KConst& K, unsigned rs, unsigned re, unsigned dst, int xo, int dy,
                                           int dz, const float4* __restrict__ poscell,
                                           const float4* __restrict__ velrhop, const float* __restrict__ press,
                                           float4* __restrict__ sA, float4* __restrict__ sB, CR* __restrict__ sC,
-                                          const FtRec& ft, bool mir = false) {
-  const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
+                                          const FtRec& ft, bool mir = false, int mirc = 0) {
+  const float oy = float(dy) * K.scell, oz = float(dz) * K.scell, my = float(2 * mirc) * K.scell;
   for (unsigned i = threadIdx.x; i < re - rs; i += TB) {
     const float4 pc = poscell[rs + i];
     const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
     const float x2 = pc.x + float(cx2 - xo) * K.scell;
-    const float y2 = mir ? -(pc.y + oy) : pc.y + oy, z2 = pc.z + oz;
+    const float y2 = mir ? -(pc.y + oy) - my : pc.y + oy, z2 = pc.z + oz;
     sA[dst + i] = make_float4(x2, y2, z2, x2 * x2 + y2 * y2 + z2 * z2);
     float4 vr = velrhop[rs + i];
     if (mir) vr.y = -vr.y;
@@ -620,6 +621,64 @@ __device__ __forceinline__ TAcc run_pass_half(const KConst& K, const DivGrid& g,
           const int w0 = int(max(lsk, seg) - seg);
           const int w1 = rc.act ? max(w0, int(min(lek, seg + segn)) - int(seg)) : w0;
           tile_unit<TDENSITY, MODE, FT>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, Q, acc);
+        }
+      }
+    }
+  }
+  // Symmetry with half cells: a p1 of the first two rows (within 2h of y = 0) also meets the
+  // images of the p2 of rows 0 and 1 (all within 2h of the plane), as in run_pass: per image
+  // row a unit of each mirrored z pair (dz = -+1, -+2) and the z = 0 row, its own image
+  // skipped (JSphCpu.cpp:671-796).
+  if (K.symmetry && rc.cy < 2) {
+    for (int v = 0; v < 6; v++) {
+      const int dya = v / 3 - rc.cy, iz = v % 3;
+      const int dza = iz < 2 ? -(iz + 1) : 0;
+      const bool paired = iz < 2, selfrow = !paired && dya == 0;
+      unsigned rs[2] = {0, 0}, re[2] = {0, 0}, ls[2] = {0, 0}, le[2] = {0, 0};
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        if (k == 1 && !paired) break;
+        const int dz = k ? -dza : dza;
+        const int z = rc.cz + dz, y = rc.cy + dya;
+        if (z < 0 || z >= g.ncz || y < 0 || y >= g.ncy) continue;
+        const unsigned rowbase = cellinit + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+        rs[k] = bc[rowbase + rc.xa];
+        re[k] = bc[rowbase + rc.xb + 1];
+        ls[k] = bc[rowbase + rc.lxa];
+        le[k] = bc[rowbase + rc.lxb + 1];
+      }
+      const unsigned n0 = re[0] - rs[0], n1 = re[1] - rs[1];
+      if (n0 + n1 == 0u) continue;
+      if (n0 + n1 <= unsigned(tcap)) {
+        __syncthreads();
+        if (n0) stage_row(K, rs[0], re[0], 0u, rc.xo, dya, dza, poscell, velrhop, press, sA, sB, sC, ft, true, rc.cy);
+        if (n1) stage_row(K, rs[1], re[1], n0, rc.xo, dya, -dza, poscell, velrhop, press, sA, sB, sC, ft, true, rc.cy);
+        __syncthreads();
+        const int wa0 = int(ls[0] - rs[0]), wa1 = rc.act && n0 ? int(le[0] - rs[0]) : wa0;
+        const int wb0 = int(n0 + ls[1] - rs[1]), wb1 = rc.act && n1 ? int(n0 + le[1] - rs[1]) : wb0;
+        if (selfrow)
+          tile_unit<TDENSITY, MODE, FT, true>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, Q, acc,
+                                              self_in(rc, rs[0], re[0]));
+        else
+          tile_unit<TDENSITY, MODE, FT>(K, p, thr, wa0, wa1, wb0, wb1, sA, sB, sC, Q, acc);
+      } else {
+        for (int k = 0; k < 2; k++) {
+          const int dz = k ? -dza : dza;
+          const unsigned rsk = k ? rs[1] : rs[0], rek = k ? re[1] : re[0], lsk = k ? ls[1] : ls[0],
+                         lek = k ? le[1] : le[0];
+          for (unsigned seg = rsk; seg < rek; seg += tcap) {
+            const unsigned segn = min(unsigned(tcap), rek - seg);
+            __syncthreads();
+            stage_row(K, seg, seg + segn, 0u, rc.xo, dya, dz, poscell, velrhop, press, sA, sB, sC, ft, true, rc.cy);
+            __syncthreads();
+            const int w0 = int(max(lsk, seg) - seg);
+            const int w1 = rc.act ? max(w0, int(min(lek, seg + segn)) - int(seg)) : w0;
+            if (selfrow)
+              tile_unit<TDENSITY, MODE, FT, true>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, Q, acc,
+                                                  self_in(rc, seg, seg + segn));
+            else
+              tile_unit<TDENSITY, MODE, FT>(K, p, thr, w0, w1, 0, 0, sA, sB, sC, Q, acc);
+          }
         }
       }
     }

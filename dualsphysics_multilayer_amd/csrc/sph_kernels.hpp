@@ -235,9 +235,12 @@ void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const
 // boundary particle p1 < npbok with a normal extrapolated from its ghost node; press
 // refreshed.  `normal` is indexed by idp; list[npbcap] + nlist: scratch of the
 // wet-particle list.
+// With floating normals (UseNormalsFt, JSphCpu.cpp:1199) the floating particles of ftridp[nft]
+// (owned, by idp - CaseNpb) are corrected too.
 void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& cur, float* press,
                  const float4* normal, const unsigned* begincell, DivGrid g, const KConst& K,
-                 const double dom_posmin[3], float threshold, unsigned* list, unsigned* nlist, void* sums);
+                 const double dom_posmin[3], float threshold, unsigned* list, unsigned* nlist, void* sums,
+                 const unsigned* ftridp = nullptr, unsigned nft = 0);
 constexpr size_t MDBC_SUM_BYTES = 152;  // sizeof(MdbcSum): 16 doubles + 5 floats + index
 // Slabs: (idp, rho, press) of the owned face-column boundary particles after mDBC, for
 // the neighbours' ghost copies (slot 0 holds the count).  Capacities capl / capr (records,
@@ -247,9 +250,11 @@ struct MdbcFaceRec {
   unsigned idp;
   float rho, press;
 };
-void launch_mdbc_face_pack(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& a,
+// floating: the floating particles (floating normals) are sent and mapped too (cap = the
+// particle capacity; else the boundary part only).
+void launch_mdbc_face_pack(hipStream_t stm, unsigned cap, const DevScalars* sc, const PartArrays& a,
                            const float* press, const KConst& K, const DivGrid& g, MdbcFaceRec* sl, MdbcFaceRec* sr,
-                           unsigned capl, unsigned capr, unsigned* bidx, unsigned nbidx);
+                           unsigned capl, unsigned capr, unsigned* bidx, unsigned nbidx, bool floating = false);
 // A record whose idp this slab does not hold as a boundary particle this step (bidx
 // stale or missing) raises ERR_HALO (fatal: every slab halts at this step) instead of writing.
 void launch_mdbc_face_apply(hipStream_t stm, DevScalars* sc, const MdbcFaceRec* rl, const MdbcFaceRec* rr,
@@ -358,6 +363,9 @@ struct FtBody {
   // per call
   float face[3], fomegaace[3], fvelres[3], fomegares[3];
   double fcenterres[3];
+  // mDBC on the body (floating normals): the rotation of its normals this step (the 3x3 part
+  // of Move(center) Rotate(dang) Move(-center0), JSphCpuSingle.cpp:988-999), row major
+  double nrot[9];
 };
 // k_motion over [sc->tstep0, +sc->last_dt) (or [t0, t0+dt) when t0 >= 0: restart
 // catch-up, no particle update), then the boundary particles.
@@ -374,9 +382,10 @@ constexpr int FT_NBLK = 32;  // partial-sum blocks per body; part = float[nbodie
 void launch_ft_partial(hipStream_t stm, DevScalars* sc, const FtBody* bodies, int nbodies, const unsigned* ftridp,
                        const float4* arace, const PartArrays& a, float* part);
 // fttab/ftdesc: the bodies' imposed-velocity / external-force tables (SPH_FTTAB_*), or nullptr.
+// normal (mDBC on floating bodies, by idp): turned with the body after a full step.
 void launch_ft_body(hipStream_t stm, DevScalars* sc, const KConst& K, FtBody* bodies, int nbodies,
                     const unsigned* ftridp, unsigned nftp, const PartArrays& a, bool predictor, const float* part,
-                    const double4* fttab = nullptr, const int2* ftdesc = nullptr);
+                    const double4* fttab = nullptr, const int2* ftdesc = nullptr, float4* normal = nullptr);
 
 // ---- slab decomposition (sph_slab.hip) ----
 // A particle MIGRATING to a neighbour: its full state, 112 B.  A boundary particle also

@@ -138,17 +138,28 @@ __device__ __forceinline__ GhostBox ghost_box(const MdbcArgs& a, const DivGrid& 
 // normal and fluid in the cells around their ghost node; a dry one gets what the
 // reference's correction gives it with empty sums (RhopZero when 0 >= threshold, else
 // unchanged).  Most of the tank's walls are dry, so pass 2 runs over a short list.
+// Threads [0, npbcap) take the boundary particles p1 < NpbOk, threads [npbcap, npbcap + nft)
+// the floating particles of ftridp (mDBC on floating bodies, JSphCpu.cpp:1199: n = Np).
 template <int SD>
 __global__ __launch_bounds__(256) void k_mdbc_list(const DevScalars* __restrict__ sc, MdbcArgs a, DivGrid g,
-                                                   unsigned* __restrict__ list, unsigned* __restrict__ nlist) {
-  const unsigned p1 = blockIdx.x * 256u + threadIdx.x;
+                                                   unsigned* __restrict__ list, unsigned* __restrict__ nlist,
+                                                   unsigned npbcap, const unsigned* __restrict__ ftridp,
+                                                   unsigned nft) {
+  const unsigned t = blockIdx.x * 256u + threadIdx.x;
+  unsigned p1 = 0xffffffffu;
+  if (t < npbcap) {
+    if (t < sc->npbok) p1 = t;
+  } else if (t - npbcap < nft) {
+    p1 = ftridp[t - npbcap];  // owned floating particle, or none
+  }
+  const bool valid = p1 != 0xffffffffu;
   bool keep = false;
   bool own = true;
-  if (p1 < sc->npbok && (g.xown0 > 0 || g.xown1 < g.ncx)) {  // slab: owned p1 only
+  if (valid && (g.xown0 > 0 || g.xown1 < g.ncx)) {  // slab: owned p1 only
     const int lcx = int(DcelCellx(a.domcellcode, a.dcell[p1])) - g.xoff;
     own = lcx >= g.xown0 && lcx < g.xown1;
   }
-  if (p1 < sc->npbok && own) {
+  if (valid && own) {
     const float4 bn = a.normal[a.idp[p1]];
     if (bn.x != 0.f || bn.y != 0.f || bn.z != 0.f) {
       const GhostBox b = ghost_box<SD>(a, g, p1, bn);
@@ -160,7 +171,7 @@ __global__ __launch_bounds__(256) void k_mdbc_list(const DevScalars* __restrict_
         const double edge0 = a.posminx + double(g.xoff) * a.scelld, edge1 = edge0 + double(g.ncx) * a.scelld;
         const double ks = double(a.kernelsize) * (1.0 + 1e-6);
         if ((b.gx - ks < edge0 && g.xown0 > 0) || (b.gx + ks >= edge1 && g.xown1 < g.ncx))
-          atomicOr(&const_cast<DevScalars*>(sc)->error_flags, ERR_HALO);
+          atomicOr(&const_cast<DevScalars*>(sc)->error_flags, ERR_HALO_NODE);
       }
       unsigned tot = 0;
       if (b.xini < b.xfin)
@@ -427,8 +438,10 @@ __global__ __launch_bounds__(256) void k_mdbc_solve(MdbcArgs a, const unsigned* 
 
 void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& cur, float* press,
                  const float4* normal, const unsigned* begincell, DivGrid g, const KConst& K,
-                 const double dom_posmin[3], float threshold, unsigned* list, unsigned* nlist, void* sums) {
-  if (!npbcap) return;
+                 const double dom_posmin[3], float threshold, unsigned* list, unsigned* nlist, void* sums,
+                 const unsigned* ftridp, unsigned nft) {
+  if (!npbcap && !nft) return;
+  if (!ftridp) nft = 0;
   MdbcArgs a;
   a.sums = static_cast<MdbcSum*>(sums);
   a.idp = cur.idp;
@@ -467,17 +480,18 @@ void launch_mdbc(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const P
   a.cub_d1 = K.cub_d1;
   a.cub_c2 = K.cub_c2;
   (void)hipMemsetAsync(nlist, 0, sizeof(unsigned), stm);
-  const unsigned nb1 = (npbcap + 255u) / 256u;
+  const unsigned nlistmax = npbcap + nft;
+  const unsigned nb1 = (nlistmax + 255u) / 256u;
   // 4 waves per block, one listed particle per wave at a time: enough blocks that the
   // latency-bound waves fill the CUs (2048 blocks left 2 waves per SIMD: 0.76 ms at 4M)
-  const unsigned nb2 = std::min((npbcap + 3u) / 4u, 32768u);
-  const dim3 g3((npbcap + 255u) / 256u);
+  const unsigned nb2 = std::min((nlistmax + 3u) / 4u, 32768u);
+  const dim3 g3((nlistmax + 255u) / 256u);
   if (K.scelldiv == 1) {
-    hipLaunchKernelGGL(k_mdbc_list<1>, dim3(nb1), dim3(256), 0, stm, sc, a, g, list, nlist);
+    hipLaunchKernelGGL(k_mdbc_list<1>, dim3(nb1), dim3(256), 0, stm, sc, a, g, list, nlist, npbcap, ftridp, nft);
     if (K.sim2d) hipLaunchKernelGGL((k_mdbc<1, true>), dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
     else hipLaunchKernelGGL((k_mdbc<1, false>), dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
   } else {
-    hipLaunchKernelGGL(k_mdbc_list<2>, dim3(nb1), dim3(256), 0, stm, sc, a, g, list, nlist);
+    hipLaunchKernelGGL(k_mdbc_list<2>, dim3(nb1), dim3(256), 0, stm, sc, a, g, list, nlist, npbcap, ftridp, nft);
     if (K.sim2d) hipLaunchKernelGGL((k_mdbc<2, true>), dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
     else hipLaunchKernelGGL((k_mdbc<2, false>), dim3(nb2), dim3(256), 0, stm, sc, a, g, list, nlist);
   }
@@ -499,9 +513,12 @@ namespace sphx {
 __global__ __launch_bounds__(256) void k_mdbc_face_pack(const DevScalars* __restrict__ sc, PartArrays a,
                                                         const float* __restrict__ press, KConst K, DivGrid g,
                                                         MdbcFaceRec* __restrict__ sl, MdbcFaceRec* __restrict__ sr,
-                                                        unsigned capl, unsigned capr, unsigned* __restrict__ bidx, unsigned nbidx) {
+                                                        unsigned capl, unsigned capr, unsigned* __restrict__ bidx, unsigned nbidx,
+                                                        int floating) {
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= sc->npb) return;
+  if (p >= (floating ? sc->np : sc->npb)) return;
+  // floating normals: the floating particles (held owned or as ghosts) are mapped and sent too
+  if (p >= sc->npb && CodeType(a.code[p]) != CODE_TYPE_FLOATING) return;
   const unsigned id = a.idp[p];
   if (id < nbidx) bidx[id] = p;
   const int lcx = int(DcelCellx(K.domcellcode, a.dcell[p])) - g.xoff;
@@ -514,7 +531,7 @@ __global__ __launch_bounds__(256) void k_mdbc_face_pack(const DevScalars* __rest
     if (!dst) continue;
     const unsigned k = atomicAdd(&dst[0].idp, 1u);
     if (k + 1 < cap) dst[k + 1] = MdbcFaceRec{id, a.velrhop[p].w, press[p]};
-    else atomicOr(&const_cast<DevScalars*>(sc)->error_flags, ERR_HALO);
+    else atomicOr(&const_cast<DevScalars*>(sc)->error_flags, ERR_HALO_FACE);
   }
 }
 
@@ -529,25 +546,25 @@ __global__ __launch_bounds__(256) void k_mdbc_face_apply(DevScalars* __restrict_
   const unsigned cap = (blockIdx.y == 0 ? capl : capr);
   if (!r || i + 1 >= cap || i >= r[0].idp) return;
   const MdbcFaceRec q = r[i + 1];
-  // bidx was rebuilt by this divide's face pack for the boundary particles held now; a
-  // stale entry (the particle left this slab) would point at another particle
+  // bidx was rebuilt by this divide's face pack for the boundary (and floating) particles
+  // held now; a stale entry (the particle left this slab) would point at another particle
   const unsigned p = (q.idp < nbidx ? bidx[q.idp] : 0xffffffffu);
-  if (p >= sc->npb || idp[p] != q.idp) {
-    atomicOr(&sc->error_flags, ERR_HALO);
+  if (p >= sc->np || idp[p] != q.idp) {
+    atomicOr(&sc->error_flags, ERR_HALO_MISS);
     return;
   }
   velrhop[p].w = q.rho;
   press[p] = q.press;
 }
 
-void launch_mdbc_face_pack(hipStream_t stm, unsigned npbcap, const DevScalars* sc, const PartArrays& a,
+void launch_mdbc_face_pack(hipStream_t stm, unsigned cap, const DevScalars* sc, const PartArrays& a,
                            const float* press, const KConst& K, const DivGrid& g, MdbcFaceRec* sl, MdbcFaceRec* sr,
-                           unsigned capl, unsigned capr, unsigned* bidx, unsigned nbidx) {
+                           unsigned capl, unsigned capr, unsigned* bidx, unsigned nbidx, bool floating) {
   if (capl) (void)hipMemsetAsync(sl, 0, sizeof(MdbcFaceRec), stm);
   if (capr) (void)hipMemsetAsync(sr, 0, sizeof(MdbcFaceRec), stm);
-  if (npbcap)
-    hipLaunchKernelGGL(k_mdbc_face_pack, dim3((npbcap + 255) / 256), dim3(256), 0, stm, sc, a, press, K, g, sl, sr,
-                       capl, capr, bidx, nbidx);
+  if (cap)
+    hipLaunchKernelGGL(k_mdbc_face_pack, dim3((cap + 255) / 256), dim3(256), 0, stm, sc, a, press, K, g, sl, sr,
+                       capl, capr, bidx, nbidx, int(floating));
 }
 
 void launch_mdbc_face_apply(hipStream_t stm, DevScalars* sc, const MdbcFaceRec* rl, const MdbcFaceRec* rr,

@@ -872,9 +872,13 @@ void launch_nn_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const ui
                      const float4* poscell, const float4* velrhop, const float* press, const typecode* code,
                      const unsigned* begincell, DivGrid g, const KConst& K, const float4* phases, float4* arace,
                      float4* shiftpos, bool shift, float* viscoeta, float4* tau, const float* ftmassp) {
-  // CellMode: cells of 2h (S = 1) or of h (S = 2); floating bodies (FT, cells of 2h only)
+  // CellMode: cells of 2h (S = 1) or of h (S = 2); floating bodies (FT)
 #define SPH_NN(TV, TD, SH)                                                                                         \
-  if (ftmassp)                                                                                                     \
+  if (ftmassp && K.scelldiv == 2)                                                                                  \
+    hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH, 2, true>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr,         \
+                       poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,    \
+                       ftmassp);                                                                                   \
+  else if (ftmassp)                                                                                                \
     hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH, 1, true>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr,         \
                        poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,    \
                        ftmassp);                                                                                   \
@@ -1312,7 +1316,7 @@ __global__ __launch_bounds__(256) void k_nn_face_pack(DevScalars* __restrict__ s
     if (!dst) continue;
     const unsigned k = atomicAdd(&dst[0].idp, 1u);
     if (k + 1 >= cap) {  // the buffers hold every ghost sent at the divide; if not, say so
-      atomicOr(&sc->error_flags, ERR_HALO);
+      atomicOr(&sc->error_flags, ERR_HALO_FACE);
       continue;
     }
     NNFaceRec r;
@@ -1343,7 +1347,7 @@ __global__ __launch_bounds__(256) void k_nn_face_apply(DevScalars* __restrict__ 
   const NNFaceRec q = r[i + 1];
   const unsigned p = q.idp < nidx ? idxmap[q.idp] : 0xffffffffu;
   if (p >= sc->np || idp[p] != q.idp) {  // every face particle arrived as a ghost at the divide
-    atomicOr(&sc->error_flags, ERR_HALO);
+    atomicOr(&sc->error_flags, ERR_HALO_MISS);
     return;
   }
   if (viscoeta) viscoeta[p] = q.v[0];

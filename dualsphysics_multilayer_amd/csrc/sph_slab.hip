@@ -445,7 +445,7 @@ __global__ __launch_bounds__(256) void k_ghost_pack(DevScalars* __restrict__ sc,
   const unsigned key = face_key(g, f.W, lo, side ? g.xown1 - f.W : g.xown0);
   const unsigned i = bc[key] + (r - pre[lo]);
   if (i >= bc[key + 1]) {  // the divide placed fewer particles in the box than were counted
-    atomicOr(&sc->error_flags, ERR_HALO);
+    atomicOr(&sc->error_flags, ERR_HALO_GHOST);
     return;
   }
   const float4 pc = poscell[i];

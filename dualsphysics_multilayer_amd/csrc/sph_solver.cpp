@@ -156,9 +156,8 @@ void derive_constants(const SphCaseDef& c, SphConstants& k) {
     if (k.data2d) throw SphError(SPH_ERR_ARG, "Symmetry is not allowed with 2-D simulations.");
     if (k.tvisco != SPH_VISCO_ARTIFICIAL) throw SphError(SPH_ERR_ARG, "Symmetry is only allowed with Artificial viscosity.");
     if (c.map_realposmin[1] != 0.0) throw SphError(SPH_ERR_ARG, "Symmetry needs MapRealPosMin.y = 0 (JSph.cpp:1386)");
-    if (k.rheology != SPH_RHEOLOGY_SINGLE || k.shift_mode != SPH_SHIFT_NONE || k.scelldiv != 1)
-      throw SphError(SPH_ERR_UNSUPPORTED, "Symmetry is implemented for the single-phase interaction without shifting, "
-                                          "CellMode=full");
+    if (k.rheology != SPH_RHEOLOGY_SINGLE)
+      throw SphError(SPH_ERR_UNSUPPORTED, "Symmetry is implemented for the single-phase interaction");
   }
   if (!(c.dtfixed >= 0)) throw SphError(SPH_ERR_ARG, "DtFixed must not be negative");
   k.dtfixed = c.dtfixed;  // max(0, DtFixed), JSph.cpp:699
@@ -466,6 +465,7 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   casenpb_ = cdef.npb;
   const unsigned n = unsigned(sel.size());
   if (const char* e = std::getenv("SPH_SLAB_MINCAP")) slab_mincap_ = slab() && std::atoi(e) != 0;
+  if (const char* e = std::getenv("SPH_SLAB_CUT")) cut_items_ = slab() && std::atoi(e) != 0;
   cap_ = slab() ? n + (slab_mincap_ ? 16u : std::max(n / 2, 65536u)) : n;
   keybits_ = bits_for(G.boxdiscard, 1);
   // grid-sized buffers hold the widest grid a slab can get from a re-partition (all
@@ -486,9 +486,10 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   sps_ = !nn_ && C.tvisco == SPH_VISCO_LAMINARSPS;
   ext_ = !nn_ && (sps_ || shift_);
   facex_ = slab() && (nnsph_ || sps_);
+  mdbc_corrector_ = cdef.tboundary == SPH_BOUND_MDBC && cdef.mdbc_corrector != 0;
   if (ext_) tiled_ = true;
-  if (C.kernel == SPH_KERNEL_CUBIC && (nn_ || ext_))
-    throw SphError(SPH_ERR_UNSUPPORTED, "the Cubic spline kernel with NN multiphase / Laminar+SPS / shifting is not implemented");
+  if (C.kernel == SPH_KERNEL_CUBIC && nn_)
+    throw SphError(SPH_ERR_UNSUPPORTED, "the Cubic spline kernel with NN multiphase is not implemented");
   if (C.kernel == SPH_KERNEL_CUBIC && !tiled_)
     throw SphError(SPH_ERR_UNSUPPORTED, "the Cubic spline kernel runs on the tiled interaction only");
   if (C.symmetry && !tiled_) throw SphError(SPH_ERR_UNSUPPORTED, "Symmetry runs on the tiled interaction only");
@@ -851,30 +852,44 @@ void SphGpuSingle::Upload(const SphParticlesHost& h, const std::vector<unsigned>
 // (particle -> boundary limit) as float, doubled (particle -> ghost node), kept by idp.
 void SphGpuSingle::UploadNormals(const SphCaseDef& cdef, const SphParticlesHost& h) {
   if (!h.boundnormal) throw SphError(SPH_ERR_ARG, "mDBC needs the boundary normals (<case>_Normals.nbi4)");
-  const unsigned nbound = cdef.npb;
-  std::vector<float4> nor(std::max(nbound, 1u), make_float4(0.f, 0.f, 0.f, 0.f));
+  // normals by idp: the boundary's [0, CaseNpb) and, when the floating bodies have normals
+  // (UseNormalsFt, JSph.cpp:1301-1306: mDBC on them too), theirs up to the last one given
+  unsigned nnor = cdef.npb, nftnor = 0;
+  for (unsigned p = 0; p < h.n; p++) {
+    const unsigned id = h.idp[p];
+    if (id < cdef.npb) continue;
+    const float x = h.boundnormal[3 * p], y = h.boundnormal[3 * p + 1], z = h.boundnormal[3 * p + 2];
+    if (x != 0.f || y != 0.f || z != 0.f) {
+      nnor = std::max(nnor, id + 1);
+      nftnor++;
+    }
+  }
+  ftnormals_ = nftnor > 0;
+  nnormal_ = nnor;
+  std::vector<float4> nor(std::max(nnor, 1u), make_float4(0.f, 0.f, 0.f, 0.f));
   unsigned nerr = 0;
   for (unsigned p = 0; p < h.n; p++) {
     const unsigned id = h.idp[p];
-    if (id >= nbound) continue;
+    if (id >= nnor) continue;
     const float x = h.boundnormal[3 * p], y = h.boundnormal[3 * p + 1], z = h.boundnormal[3 * p + 2];
-    if (x == 0.f && y == 0.f && z == 0.f) nerr++;
+    if (id < cdef.npb && x == 0.f && y == 0.f && z == 0.f) nerr++;
     nor[id] = make_float4(x * 2.f, y * 2.f, z * 2.f, 0.f);
   }
-  if (nerr == nbound) throw SphError(SPH_ERR_ARG, "No valid normal vectors for using mDBC.");
+  if (nerr == cdef.npb && !ftnormals_) throw SphError(SPH_ERR_ARG, "No valid normal vectors for using mDBC.");
   check_hip(hipMalloc((void**)&normal_, sizeof(float4) * nor.size()), "hipMalloc normals");
   allocs_.push_back(normal_);
   check_hip(hipMemcpy(normal_, nor.data(), sizeof(float4) * nor.size(), hipMemcpyHostToDevice), "upload normals");
   if (slab()) {
-    // face-column boundary records: sized per interaction from the exchange's face sizes
-    // (Interaction_Forces); the idp -> index map of the boundary particles
-    check_hip(hipMalloc((void**)&bidx_, sizeof(unsigned) * std::max(cdef.npb, 1u)), "hipMalloc mDBC faces");
+    // face-column boundary (and floating) records: sized per interaction from the exchange's
+    // face sizes (Interaction_Forces); the idp -> index map of those particles
+    check_hip(hipMalloc((void**)&bidx_, sizeof(unsigned) * std::max(nnor, 1u)), "hipMalloc mDBC faces");
     allocs_.push_back(bidx_);
   }
   // boundary particles migrate between slabs, but a slab never holds more boundary
   // particles (owned + ghost) than the case has: CaseNpb bounds every slab's npbok, so
-  // the list and sums keep their size when Grow() raises the particle capacity
-  const size_t nlist = size_t(slab() ? cdef.npb : npb0_) + 1;
+  // the list and sums keep their size when Grow() raises the particle capacity (and the
+  // floating particles with normals bound the floating part of the list)
+  const size_t nlist = size_t(slab() ? cdef.npb : npb0_) + nftnor + 1;
   check_hip(hipMalloc((void**)&mdbclist_, sizeof(unsigned) * nlist), "hipMalloc mDBC list");
   allocs_.push_back(mdbclist_);
   check_hip(hipMalloc(&mdbcsums_, MDBC_SUM_BYTES * nlist), "hipMalloc mDBC sums");
@@ -951,7 +966,7 @@ void SphGpuSingle::Exchange() {
   SLAB_TRACE("exchange: pack");
   auto pack = [&] {
     launch_slab_pack(stream, cap_, sc_, cur_, G, K, C.dom_posmin, hl, hr, withm1, withpre, packtiles_, slabcnt_,
-                     send_, normal_, casenpb_, &faces_);
+                     send_, normal_, nnormal_, &faces_);
   };
   pack();  // (its accumulated counts were zeroed by the last exchange's kernels: no memset launches)
   const size_t mb = 4 * (size_t(FMSG_HDR) + faces_.nfb);
@@ -1021,12 +1036,14 @@ void SphGpuSingle::Exchange() {
     if (want >= (1ull << 31)) throw SphError(SPH_ERR_NOMEM, "slab particle capacity overflow");
     Grow(c.np, unsigned(want));
   }
+  // k_face_scan zeroes the face counts of the messages just sent: the neighbours have read them
+  transport_->wait_sends(stream);
   launch_face_scan(stream, faces_, hl, hr);  // slots of the received ghosts, records of the sent ones
   // the migrants of both faces (two concurrent streams over the two xGMI links)
   transport_->exchange(send_.ml, sizeof(SlabRec) * c.sendl[1], send_.mr, sizeof(SlabRec) * c.sendr[1], recvm_,
                        sizeof(SlabRec) * rml, recvm_ + rml, sizeof(SlabRec) * rmr, stream);
   launch_slab_unpack(stream, sc_, recvm_, unsigned(rml + rmr), recvg_, 0u, c.np, cur_, K, C.dom_posmin, withm1,
-                     withpre, slabcnt_, normal_, casenpb_);
+                     withpre, slabcnt_, normal_, nnormal_);
   SLAB_TRACE("exchange: done");
   xg_sl_ = hl ? c.sendl[0] : 0;
   xg_sr_ = hr ? c.sendr[0] : 0;
@@ -1202,10 +1219,11 @@ void SphGpuSingle::RunCellDivide() {
   }
   const unsigned ngl = ghosts ? unsigned(xg_rl_) : 0u, ngr = ghosts ? unsigned(xg_rr_) : 0u;
   const bool withm1 = (step_algorithm_ == SPH_STEP_VERLET);
-  // Items (each build also zeroes its queues).  A slab with neighbours cuts its rows where
-  // the stencil (scelldiv columns) stops reaching a ghost column: the face items and the
-  // interior items never share an item, whether they run in one list or in two (with the
-  // ghost exchange beside the interior list) — the same items, so the same bits.
+  // Items (each build also zeroes its queues).  With the overlap a slab cuts its rows where
+  // the stencil (scelldiv columns) stops reaching a ghost column: the interior list runs
+  // while the ghost records are in flight, the face list (items of <= scelldiv columns) after
+  // them.  With the ghosts in place the rows are not cut (full items); SPH_SLAB_CUT=1 cuts
+  // them there too, which makes the two modes bitwise the same (a test hook).
   const bool overlap = ghosts && OverlapGhosts();
   ghost_split_ = false;
   ItemBuild ib;
@@ -1219,9 +1237,13 @@ void SphGpuSingle::RunCellDivide() {
       const int xr[6] = {ib0, ie0, G.xown0, ib0, ie0, G.xown1};
       ib = make_item_build(bcnew, G, rowtmp_, items_, qctr_, C.scelldiv, xr, qctrf_, rowitems_, ricap_);
       ghost_split_ = true;
-    } else {
+    } else if (cut_items_) {  // the overlap's items in one list (SPH_SLAB_CUT test hook)
       const int xa[6] = {G.xown0, ib0, ib0, ie0, ie0, G.xown1};
       ib = make_item_build(bcnew, G, rowtmp_, items_, qctr_, C.scelldiv, xa, nullptr, rowitems_, ricap_);
+    } else {
+      // ghosts in place: the rows' items over all owned columns, as in one domain (a row cut
+      // at the face columns leaves items of one cell there, ~1/3 of the block's lanes)
+      ib = make_item_build(bcnew, G, rowtmp_, items_, qctr_, C.scelldiv, nullptr, nullptr, rowitems_, ricap_);
     }
   }
   if (inc_ok_ && inc_valid_ && G.ncx >= 3) {
@@ -1306,11 +1328,12 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
     GhostCollect(stream);
     ghost_pending_ = false;
   }
-  // mDBC boundary correction first, except in the Symplectic corrector (JSphCpuSingle.cpp:525).
-  if (normal_ && interstep != 3) {
+  // mDBC boundary correction first, except in the Symplectic corrector unless MDBCCorrector
+  // (JSphCpuSingle.cpp:525); with floating normals the floating particles too (JSphCpu.cpp:1199).
+  if (normal_ && (mdbc_corrector_ || interstep != 3)) {
     TimedBegin(3);
     launch_mdbc(stream, slab() ? cap_ : npb0_, sc_, cur_, press_, normal_, begincell_, G, K, C.dom_posmin, C.mdbc_threshold,
-                mdbclist_ + 1, mdbclist_, mdbcsums_);
+                mdbclist_ + 1, mdbclist_, mdbcsums_, ftnormals_ ? ftridp_ : nullptr, ftnormals_ ? nftp_ : 0u);
     if (slab() && (transport_->has_left() || transport_->has_right())) {
       // records per side = the face's particles at the last exchange + the count slot: both
       // sides of a face derive the same size, and no face record can be dropped
@@ -1328,7 +1351,7 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
         mdbcfacecap_ = want;
       }
       MdbcFaceRec *sl = mdbcface_, *sr = sl + nsl, *rl = sr + nsr, *rr = rl + nrl;
-      launch_mdbc_face_pack(stream, cap_, sc_, cur_, press_, K, G, sl, sr, nsl, nsr, bidx_, casenpb_);
+      launch_mdbc_face_pack(stream, cap_, sc_, cur_, press_, K, G, sl, sr, nsl, nsr, bidx_, nnormal_, ftnormals_);
       transport_->exchange(sl, sizeof(MdbcFaceRec) * nsl, sr, sizeof(MdbcFaceRec) * nsr, rl, sizeof(MdbcFaceRec) * nrl,
                            rr, sizeof(MdbcFaceRec) * nrr, stream);
       launch_mdbc_face_apply(stream, sc_, hl ? rl : nullptr, hr ? rr : nullptr, nrl, nrr, bidx_, casenpb_, cur_.idp,
@@ -1505,13 +1528,18 @@ void SphGpuSingle::RunFloating(bool predictor) {
   launch_ft_partial(stream, sc_, ftbodies_, nftbodies_, ftridp_, arace_, cur_, ftpart_);
   if (slab() && transport_->nranks > 1) transport_->allreduce_sum_f32(ftpart_, nftbodies_ * FT_NBLK * 6, stream);
   launch_ft_body(stream, sc_, K, ftbodies_, nftbodies_, ftridp_, nftp_, cur_, predictor, ftpart_, fttab_,
-                 fttabdesc_);
+                 fttabdesc_, ftnormals_ ? normal_ : nullptr);
   TimedEnd(1);
 }
 
 // JDsMotion::Init (JDsMotion.cpp:94-106) + JMotion::Prepare (JMotion.cpp:303-317).
 void SphGpuSingle::SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* movs, unsigned nevt,
                              const SphMotionEvent* evts) {
+  // Symmetry + ShiftMode NoFixed: the images of a moving-boundary p2 would join the shifting
+  // sums before the first fixed p2 in the reference's order (JSphCpu.cpp:743-750, 793-796);
+  // this core visits the images after the rows (sph_ext.hip), exact only without them
+  if (C.symmetry && C.shift_mode == SPH_SHIFT_NOFIXED && nobj)
+    throw SphError(SPH_ERR_UNSUPPORTED, "Symmetry with ShiftMode NoFixed and moving boundaries is not implemented");
   if (stepped_ || motion_) throw SphError(SPH_ERR_STATE, "the motion is configured once, before the first step");
   if (!nobj || nobj > unsigned(MOT_MAXOBJ)) throw SphError(SPH_ERR_UNSUPPORTED, "number of moving objects out of range");
   if ((nmov && !movs) || (nevt && !evts)) throw SphError(SPH_ERR_ARG, "motion arrays missing");
@@ -1589,7 +1617,6 @@ void SphGpuSingle::SetFloatings(unsigned nft, const SphFloatingDef* defs, double
     // its body index (JSphCpu_NN_FDA.cpp:199-200, 231, 267): bodies beyond the phases would
     // read past the phase table there
     if (nft > C.nphases) throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase: more floating bodies than phases");
-    if (C.scelldiv != 1) throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase with floating bodies: CellMode=full only");
   }
   if (C.symmetry) throw SphError(SPH_ERR_ARG, "Symmetry is not allowed with floating bodies.");  // JSph.cpp:1177
   std::vector<FtBody> b(nft);
@@ -1793,10 +1820,13 @@ void SphGpuSingle::CheckErrors() {
   const SphRunStats s = Stats();
   if (s.error_flags & ERR_BOUNDOUT) throw SphError(SPH_ERR_BOUNDOUT, "boundary particles were excluded (AbortBoundOut)");
   if (s.error_flags & ERR_DT_NAN) throw SphError(SPH_ERR_DT, "The computed Dt is NaN or infinity");
-  if (s.error_flags & ERR_HALO)
-    throw SphError(SPH_ERR_UNSUPPORTED,
-                   "slab halo: an mDBC ghost node needs particles beyond the slab's ghost column, or a face "
-                   "record buffer overflowed");
+  if (s.error_flags & ERR_HALO_NODE)
+    throw SphError(SPH_ERR_UNSUPPORTED, "slab halo: an mDBC ghost node needs particles beyond the slab's ghost columns");
+  if (s.error_flags & ERR_HALO_FACE) throw SphError(SPH_ERR_STATE, "slab halo: a face record did not fit its buffer");
+  if (s.error_flags & ERR_HALO_MISS)
+    throw SphError(SPH_ERR_STATE, "slab halo: a face record found no ghost copy of its particle");
+  if (s.error_flags & ERR_HALO_GHOST)
+    throw SphError(SPH_ERR_STATE, "slab halo: a ghost record the divide did not place (face counts disagree)");
 }
 
 unsigned SphGpuSingle::DtTrace(double* out, unsigned cap) {

@@ -144,7 +144,10 @@ class SphGpuSingle {
   PartArrays cur_, alt_;
   float4* poscell_ = nullptr;
   float* press_ = nullptr;
-  float4* normal_ = nullptr;      // mDBC: particle -> ghost node, by idp [CaseNbound]
+  float4* normal_ = nullptr;      // mDBC: particle -> ghost node, by idp [nnormal_]
+  unsigned nnormal_ = 0;          // CaseNpb, or past the floating normals (mDBC on floating bodies)
+  bool ftnormals_ = false;        // UseNormalsFt: the floating bodies have normals (JSph.cpp:1301-1306)
+  bool mdbc_corrector_ = false;   // MDBCCorrector: mDBC before the Symplectic corrector too
   unsigned* mdbclist_ = nullptr;  // mDBC: wet boundary particles of this interaction [npb] + count
   void* mdbcsums_ = nullptr;      // mDBC: reduced sums per listed particle (pass 2 -> solve)
   MdbcFaceRec* mdbcface_ = nullptr;  // slabs + mDBC: send left, send right, recv left, recv right (face sizes + 1)
@@ -152,6 +155,7 @@ class SphGpuSingle {
   // SPH_SLAB_MINCAP test hook: every slab buffer starts at (or grows to) its minimum, so each
   // grow-and-redo path runs (tests/test_gpu_slab.py checks the runs stay bitwise the same)
   bool slab_mincap_ = false;
+  bool cut_items_ = false;  // SPH_SLAB_CUT test hook: in-place ghosts with the overlap's cut items
   unsigned* bidx_ = nullptr;         // slabs + mDBC: boundary idp -> index [CaseNpb]
   float4* arace_ = nullptr;
   // NN multiphase (v5.0 solver) and shifting

@@ -417,8 +417,7 @@ class XmlCase:
             raise CaseError("Old normal data file format (XXX_NormalData.nbi4) is invalid for current version.")
         if not out[: self.npb].any():
             raise CaseError("No valid normal vectors for using mDBC.")
-        if out[self.npb:].any():  # UseNormalsFt (JSph.cpp:1305): mDBC on floating bodies
-            raise CaseError("mDBC on floating bodies (floating normals) is not supported by this core.")
+        # floating normals (UseNormalsFt, JSph.cpp:1301-1306): mDBC on the floating bodies too
         return out
 
     @property
@@ -484,12 +483,12 @@ class XmlCase:
         self.tboundary = bc
         self.slipmode = 1
         self.mdbc_threshold = 0.0
+        self.mdbc_corrector = 0  # JSph.cpp:783: only with mDBC
         if bc == 2:  # JSph.cpp:631-641
             self.slipmode = p.int("SlipMode", True, 1)
             if self.slipmode not in (1, 2, 3):
                 raise CaseError("Slip mode is not valid.")
-            if p.int("MDBCCorrector", True, 0) != 0:
-                raise CaseError("MDBCCorrector=1 is not supported by this core.")
+            self.mdbc_corrector = int(p.int("MDBCCorrector", True, 0) != 0)
         if p.exists("DeltaSPH"):
             if p.exists("DensityDT"):
                 raise CaseError("The parameters 'DeltaSPH' and 'DensityDT' cannot be combined.")
@@ -842,7 +841,7 @@ class XmlCase:
             phases=self.phases, relaxation_dt=self.relaxation_dt, shift_mode=self.shift_mode,
             shift_coef=self.shift_coef, shift_tfs=self.shift_tfs, data2d=int(self.data2d),
             data2d_posy=self.data2d_posy, dtallparticles=self.dtallparticles, dtfixed=self.dtfixed,
-            symmetry=int(self.symmetry),
+            symmetry=int(self.symmetry), mdbc_corrector=int(self.mdbc_corrector),
         )
 
 

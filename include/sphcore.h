@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define SPH_ABI_VERSION 9
+#define SPH_ABI_VERSION 10
 
 typedef enum {
   SPH_OK = 0,
@@ -168,7 +168,8 @@ typedef struct SphCaseDef {
   double relaxation_dt;     /* RelaxationDt, lamda of the viscous dt       */
   /* shifting (JSphShifting::ConfigBasic; <parameter Shifting/ShiftCoef/ShiftTFS>) */
   int32_t shift_mode;       /* SPH_SHIFT_*                                 */
-  int32_t pad_shift;
+  int32_t mdbc_corrector;   /* <parameter MDBCCorrector>: mDBC also before the Symplectic
+                               corrector's interaction (JSph.cpp:639,783; JSphCpuSingle.cpp:525) */
   double shift_coef, shift_tfs;
   SphPhaseDef phases[SPH_MAXPHASES];
   /* 2-D simulation (<data2d>, JSph::LoadConfigCtes JSph.cpp:571-572): particles in the

@@ -15,10 +15,13 @@
 //                      JCaseParts.cpp:248-290: massbody, masspart, center, inertia)
 //   fluid   mkfluid 0  still water of depth d, minus the box
 // With boundary=2 (mDBC) the fixed/moving walls get normals (<case>_Normals.nbi4,
-// JPartNormalData.cpp:178-207) pointing to the boundary limit dp/2 towards the fluid.
+// JPartNormalData.cpp:178-207) pointing to the boundary limit dp/2 towards the fluid; with
+// ftnormals=1 the floating box's outer layer gets them too (from the particle to the nearest
+// point of the box's boundary limit, dp/2 outside it: a face, edge or corner point), which
+// makes the reference apply mDBC to the floating body (UseNormalsFt, JSph.cpp:1301-1306).
 //
 // usage: genflume_ref <dp> <outdir> <step:1|2> <ddt:0..3> [timemax] [casename] [boundary:1|2]
-//                     [L W H depth]
+//                     [L W H depth] [flapwait flapfreq flapampl] [ftnormals:0|1]
 #include "JPartDataBi4.h"
 #include "JPartNormalData.h"
 #include "Functions.h"
@@ -46,6 +49,7 @@ int main(int argc, char** argv) {
   // flap motion: wait, then mvrotsinu of this frequency (Hz) and amplitude (degrees)
   const std::string fwait = (argc > 12 ? argv[12] : "0.004"), ffreq = (argc > 13 ? argv[13] : "2"),
                     fampl = (argc > 14 ? argv[14] : "3");
+  const bool ftnormals = (argc > 15 ? atoi(argv[15]) != 0 : false);
 
   const int nx = int(std::round(L / dp)), ny = int(std::round(W / dp)), nz = int(std::round(H / dp));
   const int kd = int(std::round(D / dp));
@@ -89,7 +93,13 @@ int main(int argc, char** argv) {
     for (int j = bjc - nbh; j <= bjc + nbh; j++)
       for (int i = bic - nbh; i <= bic + nbh; i++) {
         pos.push_back(TDouble3(i * dp, j * dp, k * dp));
-        nor.push_back(TDouble3(0));
+        tdouble3 n = TDouble3(0);
+        if (ftnormals && boundary == 2) {  // outer layer: towards the nearest limit point
+          n.x = (i - bic == nbh ? hd : (bic - i == nbh ? -hd : 0.));
+          n.y = (j - bjc == nbh ? hd : (bjc - j == nbh ? -hd : 0.));
+          n.z = (k - bkc == nbh ? hd : (bkc - k == nbh ? -hd : 0.));
+        }
+        nor.push_back(n);
         bcen = bcen + pos.back();
       }
   const unsigned nfloat = unsigned(pos.size()) - npb;

@@ -16,9 +16,12 @@ send/receive over one xGMI link per face.
 
 Per slab and step, from its own streams' HIP events (sph_solver_timing): the interaction
 window per call (interior + ghost transfer + scatter + face items) and the divide kernels per
-call, with the ghost overlap on (the records in flight beside the interior items) and off (in
-place before the interaction, inside the timed turn); alternating repeats.  Prints one JSON
-line per repeat and a final summary.
+call, in three modes, alternating repeats:
+  overlap      the ghost records in flight beside the interior items (rows cut at the face
+               columns: an interior list, then a face list of one-column items);
+  inplace_cut  the ghosts in place before the interaction, the same cut items (SPH_SLAB_CUT=1);
+  inplace      the ghosts in place, rows not cut (full items: the default).
+Prints one JSON line per run and a final summary.
 """
 import argparse
 import json
@@ -35,8 +38,14 @@ from dualsphysics_multilayer_amd.case import DamBreakCase  # noqa: E402
 from dualsphysics_multilayer_amd.core import SphSlabGroup, slab_partition  # noqa: E402
 
 
-def run(case, bounds, overlap, steps, warmup):
+MODES = {"overlap": (1, 1), "inplace_cut": (0, 1), "inplace": (0, 0)}  # (overlap, cut)
+
+
+def run(case, bounds, mode, steps, warmup):
+    overlap, cut = MODES[mode]
+    os.environ["SPH_SLAB_CUT"] = str(cut)
     g = SphSlabGroup(case, np.asarray(bounds, np.int32))
+    os.environ.pop("SPH_SLAB_CUT")
     g.set_overlap(bool(overlap))
     g.run(warmup)  # a group run returns with every slab synchronised
     for m in g.members:
@@ -51,7 +60,7 @@ def run(case, bounds, overlap, steps, warmup):
                    "divide": round(float(p[2]), 4)})
     own = [int(m.stats()["np"]) for m in g.members]
     g.close()
-    return {"overlap": overlap, "wall_ms_per_step": round(wall, 3), "owned_np": own, "phases_ms_per_call": ph}
+    return {"mode": mode, "wall_ms_per_step": round(wall, 3), "owned_np": own, "phases_ms_per_call": ph}
 
 
 def main():
@@ -60,7 +69,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--repeat", type=int, default=2)
-    ap.add_argument("--only", type=int, default=None, help="overlap 1 or 0 only (one run, e.g. under rocprofv3)")
+    ap.add_argument("--only", choices=tuple(MODES), default=None, help="one mode only (e.g. under rocprofv3)")
     ap.add_argument("--dp", type=float, default=0.00205)
     a = ap.parse_args()
     if os.environ.get("SPH_SLAB_TURNS") != "1":
@@ -68,7 +77,7 @@ def main():
     case = DamBreakCase(a.dp, step_algorithm=2, tdensity=1)
     bounds = [int(x) for x in slab_partition(case, a.slabs)]
     res = {"workload": "cfg3", "np": int(case.np), "bounds": bounds, "steps": a.steps, "runs": []}
-    modes = [a.only] if a.only is not None else [1, 0]
+    modes = [a.only] if a.only is not None else list(MODES)
     for _ in range(a.repeat):
         for ov in modes:
             r = run(case, bounds, ov, a.steps, a.warmup)
@@ -76,13 +85,14 @@ def main():
             print("progress", json.dumps(r), flush=True)
     summ = {}
     for ov in modes:
-        rs = [r for r in res["runs"] if r["overlap"] == ov]
+        rs = [r for r in res["runs"] if r["mode"] == ov]
         n = len(rs[0]["phases_ms_per_call"])
         best = lambda k, i: min(r["phases_ms_per_call"][i][k] for r in rs)  # noqa: E731
-        summ["overlap%d" % ov] = {
+        summ[ov] = {
             "interaction_ms": [best("interaction", i) for i in range(n)],
             "divide_ms": [best("divide", i) for i in range(n)],
             "update_ms": [best("update", i) for i in range(n)],
+            "wall_ms_per_step": min(r["wall_ms_per_step"] for r in rs),
         }
     res["summary_min_over_repeats"] = summ
     print(json.dumps(res), flush=True)

@@ -36,6 +36,16 @@ VARIANTS = {
     # the floating box with imposed velocities ("none" components stay free) and external
     # forces (JLinearValue tables of <floating>, FtApplyImposedVel / GetFtExternalForce*)
     "verlet_ddt2_ftvel": (0.025, 1, 2, 1, 100, (1, 10, 50, 100), (), "ftvel"),
+    # mDBC on the floating box too (genflume_ref ftnormals=1: UseNormalsFt, the normals turned
+    # with the body, JSphCpuSingle.cpp:988-999), Verlet and Symplectic
+    "verlet_ddt2_mdbc_ftnor": (0.025, 1, 2, 2, 100, (1, 10, 50, 100),
+                               ("1.2", "0.3", "0.4", "0.2", "0.004", "2", "3", "1")),
+    "symplectic_ddt1_mdbc_ftnor": (0.025, 2, 1, 2, 60, (1, 10, 60),
+                                   ("1.2", "0.3", "0.4", "0.2", "0.004", "2", "3", "1")),
+    # MDBCCorrector=1: mDBC also before the Symplectic corrector's interaction (JSph.cpp:639,
+    # JSphCpuSingle.cpp:525), with the floating normals
+    "symplectic_ddt1_mdbc_corr": (0.025, 2, 1, 2, 60, (1, 10, 60),
+                                  ("1.2", "0.3", "0.4", "0.2", "0.004", "2", "3", "1"), "mdbccorr"),
 }
 
 # <floating> additions of the XML edits (JCasePartBlock_Floating::ReadXml, JCaseParts.cpp:270-285)
@@ -48,6 +58,8 @@ XML_EDITS = {
               '</linearforce>'
               '<angularforce><force time="0" x="0.002" y="0" z="-0.001"/><force time="0.015" x="0" y="0" z="0.003"/>'
               '</angularforce>'),
+    # (anchor, text): the text goes before the anchor
+    "mdbccorr": ("</parameters>", '<parameter key="MDBCCorrector" value="1"/>\n'),
 }
 
 
@@ -76,8 +88,10 @@ def make(name, dp, step, ddt, boundary, nsteps, keep, extra=(), xml_edit=None):
         if xml_edit:
             fx = os.path.join(tmp, "CaseFlume.xml")
             txt = open(fx).read()
-            assert txt.count("</floating>") == 1
-            open(fx, "w").write(txt.replace("</floating>", XML_EDITS[xml_edit] + "</floating>"))
+            edit = XML_EDITS[xml_edit]
+            anchor, text = edit if isinstance(edit, tuple) else ("</floating>", edit)
+            assert txt.count(anchor) == 1
+            open(fx, "w").write(txt.replace(anchor, text + anchor))
         files = ["CaseFlume.xml", "CaseFlume.bi4"] + (["CaseFlume_Normals.nbi4"] if boundary == 2 else [])
         for f in files:
             shutil.copy(os.path.join(tmp, f), os.path.join(out_dir, f))

@@ -62,6 +62,17 @@ SYM_CASES = {
     "verlet_ddt2_sym_dp0.02": (0.02, 1, 2, 100, (1, 10, 100), 1),
     "symplectic_ddt1_sym_mdbc_dp0.025": (0.025, 2, 1, 60, (1, 20, 60), 2),
 }
+# Symmetry with CellMode=half and with shifting (the reference refuses only 2-D, periodic y,
+# floating bodies, Chrono and a viscosity other than the artificial one, JSph.cpp:1174-1179).
+# name: (dp, step, ddt, nsteps, kept steps, boundary, extra args, (shifting, coef, tfs)); the
+# npz adds ext = [1, 0.1, shifting, coef, tfs] as make_ext's
+SYM_EXT_CASES = {
+    "verlet_ddt2_sym_half_dp0.02": (0.02, 1, 2, 100, (1, 10, 100), 1, ("-cellmode:half",), (0, "-2", "0")),
+    "symplectic_ddt2_sym_shift_full_tfs_dp0.025": (0.025, 2, 2, 60, (1, 20, 60), 1, (), (3, "-2", "2.75")),
+    "verlet_ddt2_sym_shift_nobound_dp0.025": (0.025, 1, 2, 60, (1, 41, 60), 1, (), (1, "-2", "0")),
+    "symplectic_ddt2_sym_shift_full_tfs_half_dp0.025": (0.025, 2, 2, 60, (1, 20, 60), 1, ("-cellmode:half",),
+                                                        (3, "-2", "2.75")),
+}
 
 
 # Single-phase Laminar+SPS viscosity (ViscoTreatment 2; kinematic viscosity 1e-6 m2/s,
@@ -90,6 +101,16 @@ EXT_HALF_CASES = {
 # start) and rst = [time, SymplecticDtPre, map_posmin xyz, map_posmax xyz].
 # (..., stir: "mild" or "shear" -- the strong short-wave shear under which the SPS eddy
 # viscosity (Smagorinsky, ~SpsSmag |S| ~ 1e-4 m2/s) is far above the parity tolerance)
+# Cubic spline kernel (-cubic, with its tensile correction) with Laminar+SPS and with
+# shifting (JSphCpu.cpp:631-822 templated on tker for every tvisco / shift); the npz carries
+# kernel = 1
+EXT_CUBIC_CASES = {
+    "verlet_lamsps_ddt2_cubic_dp0.02": (0.02, 1, 2, 100, (1, 10, 100), (2, "1e-6", 0, "-2", "0")),
+    "symplectic_shift_full_tfs_cubic_dp0.025": (0.025, 2, 2, 60, (1, 20, 60), (1, "0.1", 3, "-2", "2.75")),
+}
+STIR_CUBIC_CASES = {
+    "stir_verlet_lamsps_ddt2_cubic_dp0.025": (0.025, 1, 2, 40, (1, 10, 40), (2, "1e-6", 0, "-2", "0"), "shear"),
+}
 STIR_CASES = {
     "stir_verlet_lamsps_ddt2_dp0.025": (0.025, 1, 2, 40, (1, 10, 40), (2, "1e-6", 0, "-2", "0"), "shear"),
     "stir_symplectic_lamsps_ddt1_dp0.03": (0.03, 2, 1, 20, (1, 5, 20), (2, "1e-6", 0, "-2", "0"), "shear"),
@@ -134,8 +155,10 @@ def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=(), dim=3, noise=F
     try:
         gen = [os.path.join(REF, "gencase_ref"), repr(dp), tmp, str(step), str(ddt), "1.5", "CaseDambreak",
                str(boundary), str(dim)]
-        if sym:  # artificial viscosity 0.1, no shifting, Wendland, Symmetry
+        if sym is True:  # artificial viscosity 0.1, no shifting, Wendland, Symmetry
             gen += ["1", "0.1", "0", "-2", "0", "2", "1"]
+        elif sym:  # (shifting, coef, tfs): artificial viscosity 0.1, Wendland, Symmetry
+            gen += ["1", "0.1", str(sym[0]), sym[1], sym[2], "2", "1"]
         subprocess.check_call(gen, stdout=subprocess.DEVNULL)
         out = os.path.join(tmp, "out")
         for exe, o in (("DualSPHysics5.2CPU_ref", out), ("DualSPHysics5.2CPU_strict", out + "_strict")):
@@ -179,6 +202,8 @@ def make(name, dp, step, ddt, nsteps, keep, boundary=1, extra=(), dim=3, noise=F
             arrays["kernel"] = np.int32(1)
         if sym:
             arrays["symmetry"] = np.int32(1)
+        if sym and sym is not True:
+            arrays["ext"] = np.array([1.0, 0.1, float(sym[0]), float(sym[1]), float(sym[2])], np.float64)
         np.savez_compressed(os.path.join(ROOT, "tests", "golden", name + ".npz"), **arrays)
         print(name, "ok", os.path.getsize(os.path.join(ROOT, "tests", "golden", name + ".npz")))
     finally:
@@ -197,7 +222,7 @@ def run_ext(exe, dp, step, ddt, nsteps, ext, tmp, tag, extra=()):
     return out
 
 
-def make_stir(name, dp, step, ddt, nsteps, keep, ext, stir, noise):
+def make_stir(name, dp, step, ddt, nsteps, keep, ext, stir, noise, extra=()):
     sys.path.insert(0, ROOT)
     from dualsphysics_multilayer_amd.core import read_part, write_part
 
@@ -213,7 +238,7 @@ def make_stir(name, dp, step, ddt, nsteps, keep, ext, stir, noise):
         # restart at all in JSph: PartBegin = 0 loads the case file)
         first = os.path.join(tmp, "first")
         subprocess.check_call([os.path.join(REF, "DualSPHysics5.2CPU_ref"), os.path.join(d, "CaseDambreak"), first,
-                               "-nsteps:1", "-svsteps:1", "-saveposdouble:1", "-sv:binx", "-svres:0"],
+                               "-nsteps:1", "-svsteps:1", "-saveposdouble:1", "-sv:binx", "-svres:0"] + list(extra),
                               stdout=subprocess.DEVNULL)
         h, p = read_part(os.path.join(first, "Part_0001.bi4"))
         npb = int(h["case_nfixed"])
@@ -228,8 +253,8 @@ def make_stir(name, dp, step, ddt, nsteps, keep, ext, stir, noise):
         def run(exe, tag):
             out = os.path.join(tmp, "out_" + tag)
             subprocess.check_call([exe, os.path.join(d, "CaseDambreak"), out, "-partbegin:1", src,
-                                   "-nsteps:%d" % nsteps, "-svsteps:1", "-saveposdouble:1", "-sv:binx", "-svres:0"],
-                                  stdout=subprocess.DEVNULL)
+                                   "-nsteps:%d" % nsteps, "-svsteps:1", "-saveposdouble:1", "-sv:binx", "-svres:0"]
+                                  + list(extra), stdout=subprocess.DEVNULL)
             return out
 
         out = run(os.path.join(REF, "DualSPHysics5.2CPU_ref"), "fast")
@@ -262,6 +287,8 @@ def make_stir(name, dp, step, ddt, nsteps, keep, ext, stir, noise):
         arrays["dt"] = np.diff(np.array(times))
         arrays["meta"] = np.array([dp, step, ddt, nsteps], np.float64)
         arrays["ext"] = np.array([float(v) for v in ext], np.float64)
+        if "-cubic" in extra:
+            arrays["kernel"] = np.int32(1)
         np.savez_compressed(os.path.join(ROOT, "tests", "golden", name + ".npz"), **arrays)
         print(name, "ok", os.path.getsize(os.path.join(ROOT, "tests", "golden", name + ".npz")),
               {k: arrays[k] for k in arrays if k.startswith("noise")})
@@ -300,6 +327,8 @@ def make_ext(name, dp, step, ddt, nsteps, keep, ext, noise, extra=()):
         arrays["ext"] = np.array([float(v) for v in ext], np.float64)
         if "-cellmode:half" in extra:
             arrays["cellmode"] = np.int32(2)
+        if "-cubic" in extra:
+            arrays["kernel"] = np.int32(1)
         np.savez_compressed(os.path.join(ROOT, "tests", "golden", name + ".npz"), **arrays)
         print(name, "ok", os.path.getsize(os.path.join(ROOT, "tests", "golden", name + ".npz")),
               {k: arrays[k] for k in arrays if k.startswith("noise")})
@@ -320,6 +349,10 @@ if __name__ == "__main__":
         if a.only and a.only != name:
             continue
         make(name, *spec, noise=a.noise, sym=True)
+    for name, spec in SYM_EXT_CASES.items():
+        if a.only and a.only != name:
+            continue
+        make(name, *spec[:7], noise=a.noise, sym=spec[7])
     for name, spec in EXT_CASES.items():
         if a.only and a.only != name:
             continue
@@ -332,3 +365,11 @@ if __name__ == "__main__":
         if a.only and a.only != name:
             continue
         make_stir(name, *spec, a.noise)
+    for name, spec in EXT_CUBIC_CASES.items():
+        if a.only and a.only != name:
+            continue
+        make_ext(name, *spec, a.noise, extra=("-cubic",))
+    for name, spec in STIR_CUBIC_CASES.items():
+        if a.only and a.only != name:
+            continue
+        make_stir(name, *spec, a.noise, extra=("-cubic",))

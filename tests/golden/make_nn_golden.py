@@ -59,6 +59,10 @@ CASES = {
     "ft_sym_lam_ddt3_dp0.025": (0.025, 0.4, 0.5, 2.75, 1, 2, 3, 3, 0.0, 2, 60, (1, 20, 60), (), 1),
     "ft_ver_art_ddt1_nobound_cs_dp0.025": (0.025, 0.4, 0.5, 2.75, 1, 1, 1, 1, 20.0, 1, 45, (1, 41, 45), (), 1),
     "ft_sph_sym_consteq_cs_dp0.025": (0.025, 0.4, 0.5, 2.75, 2, 3, 3, 3, 20.0, 2, 30, (1, 30), (), 1),
+    # the floating body with CellMode=half (cells of h, 5x5 rows)
+    "ft_sym_lam_ddt3_half_dp0.025": (0.025, 0.4, 0.5, 2.75, 1, 2, 3, 3, 0.0, 2, 60, (1, 20, 60), ("-cellmode:half",), 1),
+    "ft_ver_art_ddt1_nobound_cs_half_dp0.025": (0.025, 0.4, 0.5, 2.75, 1, 1, 1, 1, 20.0, 1, 45, (1, 41, 45),
+                                                ("-cellmode:half",), 1),
 }
 
 

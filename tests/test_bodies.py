@@ -27,6 +27,10 @@ from dualsphysics_multilayer_amd.xmlcase import CaseError, XmlCase
 HERE = os.path.dirname(os.path.abspath(__file__))
 FIX = os.path.join(HERE, "golden", "bi4")
 VARIANTS = ["verlet_ddt2", "symplectic_ddt1_mdbc"]
+# mDBC on the floating box too (its outer layer has normals: UseNormalsFt, JSph.cpp:1301-1306;
+# the normals turned with the body, JSphCpuSingle.cpp:988-999), and MDBCCorrector=1 (mDBC also
+# before the Symplectic corrector, JSphCpuSingle.cpp:525)
+FT_VARIANTS = ["verlet_ddt2_mdbc_ftnor", "symplectic_ddt1_mdbc_ftnor", "symplectic_ddt1_mdbc_corr"]
 
 
 def _case(variant):
@@ -46,7 +50,7 @@ def _kept(g):
 
 
 # ---- case loader (CPU) ---------------------------------------------------------------------
-@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("variant", VARIANTS + FT_VARIANTS)
 def test_flume_case_blocks_and_codes(variant):
     x = _case(variant)
     assert x.has_bodies and x.case_nmoving == 2 * 16 * 11 and x.case_nfloat == 125
@@ -62,6 +66,18 @@ def test_flume_case_blocks_and_codes(variant):
     m = x.motion
     assert m["nobj"] == 2 and [v["type"] for v in m["movs"]] == [6, 1, 7]
     assert m["movs"][1]["duration"] == float(np.float32(0.004))  # GetAttributeFloat
+
+
+@pytest.mark.parametrize("variant", FT_VARIANTS)
+def test_floating_normals_and_corrector_loaded(variant):
+    """The loader takes the floating box's normals (its outer layer: 98 of 125 particles) and
+    MDBCCorrector (JSph.cpp:639,783) into the case definition."""
+    x = _case(variant)
+    nor = x.boundnormal
+    fl = (x.idp >= x.case_npb) & (x.idp < x.case_nbound)
+    assert (np.abs(nor[fl]).sum(axis=1) > 0).sum() == 125 - 27
+    assert not nor[x.idp >= x.case_nbound].any()
+    assert x.case_def()["mdbc_corrector"] == (1 if variant.endswith("_corr") else 0)
 
 
 def test_unsupported_body_features_refused(tmp_path):
@@ -147,7 +163,7 @@ def _tol(step):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("variant", VARIANTS + FT_VARIANTS)
 def test_gpu_flume_matches_reference_parts(variant):
     x, g = _case(variant), _ref(variant)
     s = _gpu(x)
@@ -170,7 +186,7 @@ def test_gpu_flume_matches_reference_parts(variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("variant", VARIANTS + FT_VARIANTS)
 def test_gpu_floating_body_matches_reference(variant):
     """Body state after every step vs PartFloat.fbi4 (center, fvel, fomega).  Measured on
     MI355X: center <= 2e-8 m, fvel <= 3.4e-6 m/s (|fvel| up to 0.12), fomega <= 3.9e-6
@@ -207,7 +223,8 @@ def test_gpu_bodies_deterministic():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant,nslabs", [("verlet_ddt2", 3), ("symplectic_ddt1_mdbc", 2)])
+@pytest.mark.parametrize("variant,nslabs", [("verlet_ddt2", 3), ("symplectic_ddt1_mdbc", 2),
+                                            ("verlet_ddt2_mdbc_ftnor", 3), ("symplectic_ddt1_mdbc_corr", 2)])
 def test_gpu_bodies_on_slabs_match_reference(variant, nslabs):
     """Moving boundaries, the floating body (force sums added over the slabs) and mDBC on
     the x-slab decomposition (in-process slabs on one GPU: the same pack / exchange /
@@ -230,7 +247,10 @@ def test_gpu_bodies_on_slabs_match_reference(variant, nslabs):
 
 
 @pytest.mark.parametrize("variant,kw", [("verlet_ddt2", dict()),
-                                        ("symplectic_ddt1_mdbc", dict(step_algorithm=2, tdensity=1, tboundary=2))])
+                                        ("symplectic_ddt1_mdbc", dict(step_algorithm=2, tdensity=1, tboundary=2)),
+                                        ("verlet_ddt2_mdbc_ftnor", dict(tboundary=2, ftnormals=True)),
+                                        ("symplectic_ddt1_mdbc_corr", dict(step_algorithm=2, tdensity=1, tboundary=2,
+                                                                           ftnormals=True, mdbc_corrector=1))])
 def test_product_flume_generator_is_the_reference_case(variant, kw):
     """case.py WaveFlumeCase (the bench's cfg4 generator) == the case genflume_ref wrote
     for the reference, bit for bit: particles, codes, normals, constants, motion program

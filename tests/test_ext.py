@@ -31,6 +31,10 @@ STIR_GOLDENS = ("stir_verlet_lamsps_ddt2_dp0.025", "stir_symplectic_lamsps_ddt1_
 # npz carries cellmode = 2)
 HALF_GOLDENS = ("verlet_lamsps_ddt2_half_dp0.025", "symplectic_shift_full_tfs_half_dp0.025",
                 "verlet_lamsps_shift_nofixed_half_dp0.03")
+# the Cubic spline kernel with Laminar+SPS / shifting (make_golden.py EXT_CUBIC_CASES,
+# STIR_CUBIC_CASES: -cubic, the npz carries kernel = 1)
+CUBIC_GOLDENS = ("verlet_lamsps_ddt2_cubic_dp0.02", "symplectic_shift_full_tfs_cubic_dp0.025")
+STIR_CUBIC_GOLDENS = ("stir_verlet_lamsps_ddt2_cubic_dp0.025",)
 FLOOR = (2e-10, 2e-7, 2.5e-3)  # pos m, vel m/s, rho kg/m3: 10x a noise of exactly 0 is no tolerance
 
 
@@ -44,7 +48,8 @@ def case_of(g, **kw):
     tv, visco, sh, coef, tfs = g["ext"]
     a = dict(step_algorithm=int(step), tdensity=int(ddt), tvisco=int(tv), visco=float(visco), shift_mode=int(sh),
              shift_coef=float(coef), shift_tfs=float(tfs),
-             cellmode=int(g["cellmode"]) if "cellmode" in g.files else 1)
+             cellmode=int(g["cellmode"]) if "cellmode" in g.files else 1,
+             kernel=int(g["kernel"]) if "kernel" in g.files else 2)
     a.update(kw)
     return DamBreakCase(float(dp), **a)
 
@@ -64,7 +69,7 @@ def ext_tol(g, k):
 
 
 # ---- CPU ------------------------------------------------------------------------------------
-@pytest.mark.parametrize("name", EXT_GOLDENS + STIR_GOLDENS + HALF_GOLDENS)
+@pytest.mark.parametrize("name", EXT_GOLDENS + STIR_GOLDENS + HALF_GOLDENS + CUBIC_GOLDENS + STIR_CUBIC_GOLDENS)
 def test_goldens_present_with_noise_floor(name):
     g = load(name)
     assert steps(g) and all(("noise_%d" % k) in g.files for k in steps(g))
@@ -115,7 +120,7 @@ def check(got, ref, tl, k):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", EXT_GOLDENS + HALF_GOLDENS)
+@pytest.mark.parametrize("name", EXT_GOLDENS + HALF_GOLDENS + CUBIC_GOLDENS)
 def test_gpu_ext_steps_match_reference_parts(name):
     g = load(name)
     s = gpu(case_of(g))
@@ -129,7 +134,7 @@ def test_gpu_ext_steps_match_reference_parts(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", STIR_GOLDENS)
+@pytest.mark.parametrize("name", STIR_GOLDENS + STIR_CUBIC_GOLDENS)
 def test_gpu_ext_stirred_match_reference_parts(name):
     g = load(name)
     case = stirred_case(g)
@@ -187,7 +192,8 @@ def test_gpu_ext_dt_trace_matches_reference():
                                          (3, "stir_verlet_lamsps_ddt2_dp0.025"),
                                          (2, "stir_symplectic_lamsps_shift_nobound_dp0.03"),
                                          (2, "verlet_lamsps_ddt2_half_dp0.025"),
-                                         (3, "verlet_lamsps_shift_nofixed_half_dp0.03")])
+                                         (3, "verlet_lamsps_shift_nofixed_half_dp0.03"),
+                                         (3, "symplectic_shift_full_tfs_cubic_dp0.025")])
 def test_gpu_ext_slabs_match_reference_parts(nslabs, name):
     """x-slabs: the SPS tau travels with the migrants and reaches the ghosts through the face
     exchange before every interaction (the stirred starts move many particles across faces)."""

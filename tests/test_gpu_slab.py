@@ -209,9 +209,10 @@ def test_cfg3_10m_eight_slabs_with_repartition_match_single_domain():
 
 
 @pytest.mark.parametrize("cfg", ["verlet_full", "symplectic_half", "verlet_repartition", "flume_bodies"])
-def test_ghost_overlap_is_bitwise_the_in_place_exchange(cfg):
+def test_ghost_overlap_is_bitwise_the_in_place_exchange(cfg, monkeypatch):
     """The ghost records of a divide sent beside the interaction of the items that reach no
-    ghost column (default) or put in place before the interaction: bitwise the same run."""
+    ghost column, or put in place before the interaction with the same (cut) items
+    (SPH_SLAB_CUT=1): bitwise the same run."""
     from dualsphysics_multilayer_amd.case import WaveFlumeCase
     from dualsphysics_multilayer_amd.core import case_derive
 
@@ -233,6 +234,7 @@ def test_ghost_overlap_is_bitwise_the_in_place_exchange(cfg):
         case = WaveFlumeCase(0.03)
         nslabs, bounds = 3, None
     res = []
+    monkeypatch.setenv("SPH_SLAB_CUT", "1")
     for ov in (True, False):
         grp = group(case, nslabs, bounds)
         grp.set_overlap(ov)

@@ -217,7 +217,9 @@ def test_xml_loader_reads_the_nn_case(tmp_path, velgrad):
 # gennn_ref float 1 (a box of rhopbody 800 on the phase-0 layer); make_nn_golden.py ft_* runs
 # the REFERENCE v5.0 NN solver on it.  The case comes back through the run driver's loader
 # (xmlcase), which configures the body as JSph::LoadCaseConfig does.
-NN_FT_GOLDENS = ("ft_sym_lam_ddt3_dp0.025", "ft_ver_art_ddt1_nobound_cs_dp0.025", "ft_sph_sym_consteq_cs_dp0.025")
+NN_FT_GOLDENS = ("ft_sym_lam_ddt3_dp0.025", "ft_ver_art_ddt1_nobound_cs_dp0.025", "ft_sph_sym_consteq_cs_dp0.025",
+                 # CellMode=half (the npz carries cellmode = 2)
+                 "ft_sym_lam_ddt3_half_dp0.025", "ft_ver_art_ddt1_nobound_cs_half_dp0.025")
 
 
 def ft_case(g, tmp_path):
@@ -230,6 +232,8 @@ def ft_case(g, tmp_path):
     subprocess.check_call([exe, repr(float(dp)), str(tmp_path), repr(float(width)), repr(float(scale)), "5", "CaseNN",
                            repr(float(tfs)), str(int(vg)), str(int(tv)), str(int(ddt)), str(int(sh)), repr(float(cs)),
                            str(int(step)), "1"], stdout=subprocess.DEVNULL)
+    if "cellmode" in g.files:  # -cellmode:half on the reference's command line
+        return XmlCase(str(tmp_path / "CaseNN"), cellmode=int(g["cellmode"]))
     return XmlCase(str(tmp_path / "CaseNN"))
 
 

@@ -14,16 +14,27 @@ on identical input against the oracle.
 import numpy as np
 import pytest
 
-from golden_io import boundary, by_idp, load, maxdiff, meta, snapshot, steps, tol
+from golden_io import boundary, by_idp, cellmode, load, maxdiff, meta, snapshot, steps, tol
 
 from dualsphysics_multilayer_amd.case import DamBreakCase
 
 NAMES = ("verlet_ddt2_sym_dp0.02", "symplectic_ddt1_sym_mdbc_dp0.025")
+# with CellMode=half (the images of rows 0 and 1 for a p1 of rows 0 and 1) and with shifting
+# (Full: every sum order-free; NoBound: the bound rows in the reference's order, the images
+# after them), tests/golden/make_golden.py SYM_EXT_CASES
+EXT_NAMES = ("verlet_ddt2_sym_half_dp0.02", "symplectic_ddt2_sym_shift_full_tfs_dp0.025",
+             "verlet_ddt2_sym_shift_nobound_dp0.025", "symplectic_ddt2_sym_shift_full_tfs_half_dp0.025")
 
 
 def case_of(g, **kw):
     dp, step_alg, ddt, _ = meta(g)
     kw.setdefault("symmetry", True)
+    kw.setdefault("cellmode", cellmode(g))
+    if "ext" in g.files:
+        _, _, sh, coef, tfs = g["ext"]
+        kw.setdefault("shift_mode", int(sh))
+        kw.setdefault("shift_coef", float(coef))
+        kw.setdefault("shift_tfs", float(tfs))
     return DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt, tboundary=boundary(g), **kw)
 
 
@@ -49,7 +60,7 @@ def test_case_matches_generator():
     """The half-tank lattice of case.py is gencase_ref's (its PART 0 position hash)."""
     import hashlib
 
-    for n in NAMES:
+    for n in NAMES + EXT_NAMES:
         g = load(n)
         c = case_of(g)
         assert int(g["symmetry"]) == 1
@@ -102,7 +113,7 @@ def test_symmetry_refusals():
 
 # ---- HIP path ------------------------------------------------------------------------------
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("name", NAMES + EXT_NAMES)
 def test_gpu_symmetry_matches_reference(name):
     from dualsphysics_multilayer_amd.core import SphGpuSingle
 
@@ -120,7 +131,7 @@ def test_gpu_symmetry_matches_reference(name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,nslabs", [(NAMES[0], 3), (NAMES[1], 2)])
+@pytest.mark.parametrize("name,nslabs", [(NAMES[0], 3), (NAMES[1], 2), (EXT_NAMES[0], 2), (EXT_NAMES[1], 3)])
 def test_gpu_symmetry_slabs_match_reference(name, nslabs):
     from dualsphysics_multilayer_amd.core import SphSlabGroup, slab_partition
 
