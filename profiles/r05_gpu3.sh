@@ -1,9 +1,7 @@
 #!/bin/bash
 # Round 5: slab / mDBC / body tests, then the three-mode turns measurement and a trace.
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests \
-
-  -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/gputest_r05d.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/gputest_r05d.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; grep -E "FAILED|passed|failed|^E  " gpurun_out/gputest_r05d.log | sort | uniq -c | sort -rn | head -30
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
