@@ -100,16 +100,16 @@ struct KConst {
   const float* visco_v;
 };
 
-// JDsFixedDt::GetDt (JDsFixedDt.cpp) at TimeStep t: the constant, or the table's row interval
-// holding t (the reference's forward walk from the first row gives the same interval for
-// the non-decreasing times a run passes in), dt in ms -> s.
-__device__ __forceinline__ double fixed_dt(const KConst& K, double t) {
+// JDsFixedDt::GetDt (JDsFixedDt.cpp:103-125) at TimeStep t: the constant, or the table's
+// row interval found by the reference's forward walk, which continues from the row the last
+// call stopped at (Position, kept in DevScalars::dtfix_pos; rows in any order, as the
+// reference's LoadFile accepts them), dt in ms -> s.
+__device__ __forceinline__ double fixed_dt(const KConst& K, double t, int& pos) {
   if (K.dtfix_val > 0) return K.dtfix_val;
   const double* T = K.dtfix_t;
   const double* V = K.dtfix_v;
   const int n = K.dtfix_n;
-  int pos = 0;
-  double tini = T[0], tnext = (n > 1 ? T[1] : tini);
+  double tini = T[pos], tnext = (pos + 1 < n ? T[pos + 1] : tini);
   for (; tnext < t && pos + 2 < n; pos++) {
     tini = tnext;
     tnext = T[pos + 2];
@@ -119,13 +119,13 @@ __device__ __forceinline__ double fixed_dt(const KConst& K, double t) {
   const double f = (t - tini) / (tnext - tini);
   return (f * (V[pos + 1] - V[pos]) + V[pos]) / 1000;
 }
-// JDsViscoInput::GetVisco (JDsViscoInput.cpp) at float(TimeStep), in its float/double mix.
-__device__ __forceinline__ float visco_at(const KConst& K, float t) {
+// JDsViscoInput::GetVisco (JDsViscoInput.cpp:103-127) at float(TimeStep), in its float/double
+// mix, walking on from the row of the last call (DevScalars::visco_pos).
+__device__ __forceinline__ float visco_at(const KConst& K, float t, int& pos) {
   const float* T = K.visco_t;
   const float* V = K.visco_v;
   const int n = K.visco_n;
-  int pos = 0;
-  float tini = T[0], tnext = (n > 1 ? T[1] : tini);
+  float tini = T[pos], tnext = (pos + 1 < n ? T[pos + 1] : tini);
   for (; tnext < t && pos + 2 < n; pos++) {
     tini = tnext;
     tnext = T[pos + 2];
@@ -186,6 +186,7 @@ struct DevScalars {
   double last_dt;
   double tstep0;    // TimeStep at the start of the step in flight (motion, FtPause)
   float last_velmax, last_acemax, last_viscdt, last_visceta;
+  int dtfix_pos, visco_pos;  // the DtFixedFile / ViscoTime tables' rows of the last lookup
   // Max-reductions (float bits of values >= 0) spread over RED_SLOTS slots so that
   // thousands of waves do not serialise on one address; k_dt folds and clears them.
   unsigned red[4][64];

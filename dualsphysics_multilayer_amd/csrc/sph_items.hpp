@@ -245,13 +245,17 @@ __device__ __forceinline__ void items_place_block(const ItemBuild& b, unsigned c
     }
     if (threadIdx.x < QCTR_COPIES) {
       const unsigned na = nl == 2 ? m1 : m3, c = threadIdx.x * QCTR_WORDS + QCTR_NITEMS;
+      // the deal's chunk (ItemDeal): 64 items for the lists of the large cases, else 16
+      const unsigned sh = m3 >= ITEM_CHUNK_BIG_N ? ITEM_CHUNK_BIG_LOG2 : ITEM_CHUNK_LOG2;
       b.qa[c] = na;
       b.qa[c + 1] = na - m0;  // the bound rows' items: the list's tail (ItemGroups)
       b.qa[c + 2] = 0u;
+      b.qa[c + 3] = sh;
       if (nl == 2) {
         b.qb[c] = m3 - na;
         b.qb[c + 1] = m3 - m2;
         b.qb[c + 2] = na;  // the second list follows the first in the item array
+        b.qb[c + 3] = sh;
       }
     }
     return;

@@ -526,9 +526,9 @@ __global__ __launch_bounds__(256) void k_mdbc_face_pack(const DevScalars* __rest
   for (int side = 0; side < 2; side++) {
     MdbcFaceRec* dst = nullptr;
     unsigned cap = 0;
-    if (side == 0 && in_left_face(g, lcx) && g.xown0 > 0) { dst = sl; cap = capl; }
-    if (side == 1 && in_right_face(g, lcx) && g.xown1 < g.ncx) { dst = sr; cap = capr; }
-    if (!dst) continue;
+    if (side == 0 && in_left_face(g, lcx)) { dst = sl; cap = capl; }
+    if (side == 1 && in_right_face(g, lcx)) { dst = sr; cap = capr; }
+    if (!dst) continue;  // no neighbour on that side
     const unsigned k = atomicAdd(&dst[0].idp, 1u);
     if (k + 1 < cap) dst[k + 1] = MdbcFaceRec{id, a.velrhop[p].w, press[p]};
     else atomicOr(&const_cast<DevScalars*>(sc)->error_flags, ERR_HALO_FACE);
@@ -560,8 +560,8 @@ __global__ __launch_bounds__(256) void k_mdbc_face_apply(DevScalars* __restrict_
 void launch_mdbc_face_pack(hipStream_t stm, unsigned cap, const DevScalars* sc, const PartArrays& a,
                            const float* press, const KConst& K, const DivGrid& g, MdbcFaceRec* sl, MdbcFaceRec* sr,
                            unsigned capl, unsigned capr, unsigned* bidx, unsigned nbidx, bool floating) {
-  if (capl) (void)hipMemsetAsync(sl, 0, sizeof(MdbcFaceRec), stm);
-  if (capr) (void)hipMemsetAsync(sr, 0, sizeof(MdbcFaceRec), stm);
+  if (sl) (void)hipMemsetAsync(sl, 0, sizeof(MdbcFaceRec), stm);
+  if (sr) (void)hipMemsetAsync(sr, 0, sizeof(MdbcFaceRec), stm);
   if (cap)
     hipLaunchKernelGGL(k_mdbc_face_pack, dim3((cap + 255) / 256), dim3(256), 0, stm, sc, a, press, K, g, sl, sr,
                        capl, capr, bidx, nbidx, int(floating));

@@ -901,6 +901,8 @@ void SphGpuSingle::SetTime(double time, double symdtpre) {
   if (motion_) throw SphError(SPH_ERR_STATE, "set the restart time before the motion (it is advanced to that time)");
   Sync();
   check_hip(hipMemcpy(&sc_->time, &time, sizeof(double), hipMemcpyHostToDevice), "set time");
+  // the tables' walks start again from their first rows (a restarted reference run loads them anew)
+  check_hip(hipMemset(&sc_->dtfix_pos, 0, 2 * sizeof(int)), "reset table rows");
   if (symdtpre > 0)
     check_hip(hipMemcpy(&sc_->symdtpre, &symdtpre, sizeof(double), hipMemcpyHostToDevice), "set SymplecticDtPre");
   if (K.visco_n) {  // ViscoTime at the restart time
@@ -968,6 +970,9 @@ void SphGpuSingle::Exchange() {
     launch_slab_pack(stream, cap_, sc_, cur_, G, K, C.dom_posmin, hl, hr, withm1, withpre, packtiles_, slabcnt_,
                      send_, normal_, nnormal_, &faces_);
   };
+  // the pack rewrites the migrant and face-message send buffers: the neighbours' copies of
+  // the last messages (in-process slabs copy asynchronously) are done first
+  transport_->wait_sends(stream);
   pack();  // (its accumulated counts were zeroed by the last exchange's kernels: no memset launches)
   const size_t mb = 4 * (size_t(FMSG_HDR) + faces_.nfb);
   transport_->exchange(faces_.msg[0], hl ? mb : 0, faces_.msg[1], hr ? mb : 0, faces_.msg[2], hl ? mb : 0,
@@ -1351,7 +1356,12 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
         mdbcfacecap_ = want;
       }
       MdbcFaceRec *sl = mdbcface_, *sr = sl + nsl, *rl = sr + nsr, *rr = rl + nrl;
-      launch_mdbc_face_pack(stream, cap_, sc_, cur_, press_, K, G, sl, sr, nsl, nsr, bidx_, nnormal_, ftnormals_);
+      // the neighbours' copies of the last message out of these buffers are done before the
+      // pack rewrites them (in-process slabs copy asynchronously); an end slab's grid keeps
+      // ghost columns on its outer side too: no records for that side
+      transport_->wait_sends(stream);
+      launch_mdbc_face_pack(stream, cap_, sc_, cur_, press_, K, G, hl ? sl : nullptr, hr ? sr : nullptr, nsl, nsr, bidx_,
+                            nnormal_, ftnormals_);
       transport_->exchange(sl, sizeof(MdbcFaceRec) * nsl, sr, sizeof(MdbcFaceRec) * nsr, rl, sizeof(MdbcFaceRec) * nrl,
                            rr, sizeof(MdbcFaceRec) * nrr, stream);
       launch_mdbc_face_apply(stream, sc_, hl ? rl : nullptr, hr ? rr : nullptr, nrl, nrr, bidx_, casenpb_, cur_.idp,
@@ -1443,6 +1453,7 @@ void SphGpuSingle::NNFaceExchange() {
   // NN: the first pass's eta (+ ConstEq tau); single phase Laminar+SPS: the particles' SPS tau
   float* veta = sps_ ? nullptr : viscoeta_;
   float4* tau = sps_ ? cur_.tau : tau_;
+  transport_->wait_sends(stream);  // the neighbours copied the last message out of these buffers
   launch_nn_face_pack(stream, cap_, sc_, cur_, K, G, veta, tau, hl ? sl : nullptr, hr ? sr : nullptr, unsigned(nsl),
                       unsigned(nsr), idxmap_, casenp_);
   transport_->exchange(sl, sizeof(NNFaceRec) * nsl, sr, sizeof(NNFaceRec) * nsr, rl, sizeof(NNFaceRec) * nrl, rr,
@@ -1711,14 +1722,13 @@ void SphGpuSingle::SetFloatingTable(unsigned body, int kind, unsigned n, const d
 void SphGpuSingle::SetTimeTable(int kind, unsigned n, const double* times, const double* values) {
   if (kind != SPH_TTAB_DTFIXED && kind != SPH_TTAB_VISCO) throw SphError(SPH_ERR_ARG, "invalid time table kind");
   if (n == 1 || (n && (!times || !values))) throw SphError(SPH_ERR_ARG, "Cannot be less than two values.");
-  for (unsigned i = 1; i < n; i++)
-    if (!(times[i] >= times[i - 1])) throw SphError(SPH_ERR_ARG, "time table times must be nondecreasing");
   if (kind == SPH_TTAB_DTFIXED && n && C.dtfixed > 0)
     throw SphError(SPH_ERR_ARG, "The parameters 'DtFixed' and 'DtFixedFile' cannot be used at the same time.");
   if (kind == SPH_TTAB_VISCO && n && nn_)
     throw SphError(SPH_ERR_UNSUPPORTED, "ViscoTime with NN multiphase (per-phase viscosities) is not implemented");
   Sync();
   void*& buf = (kind == SPH_TTAB_DTFIXED ? dttab_ : viscotab_);
+  check_hip(hipMemset(kind == SPH_TTAB_DTFIXED ? &sc_->dtfix_pos : &sc_->visco_pos, 0, sizeof(int)), "reset table row");
   if (buf) {
     (void)hipFree(buf);
     allocs_.erase(std::remove(allocs_.begin(), allocs_.end(), buf), allocs_.end());
@@ -1816,13 +1826,30 @@ SphRunStats SphGpuSingle::Stats() {
   return r;
 }
 
+// The face sizes of the last exchange and the records the last mDBC face pack counted.
+std::string SphGpuSingle::HaloDiag() {
+  unsigned cnt[2] = {0u, 0u};
+  if (mdbcface_ && slab()) {
+    const bool hl = transport_->has_left(), hr = transport_->has_right();
+    if (hl) check_hip(hipMemcpy(&cnt[0], &mdbcface_[0].idp, 4, hipMemcpyDeviceToHost), "read face count");
+    if (hr)
+      check_hip(hipMemcpy(&cnt[1], &mdbcface_[hl ? face_sl_ + 1u : 0u].idp, 4, hipMemcpyDeviceToHost),
+                "read face count");
+  }
+  return "slab " + std::to_string(slabcfg_.rank) + " face sizes sl " + std::to_string(face_sl_) + " sr " +
+         std::to_string(face_sr_) + " rl " + std::to_string(face_rl_) + " rr " + std::to_string(face_rr_) +
+         ", mDBC records counted " + std::to_string(cnt[0]) + " / " + std::to_string(cnt[1]);
+}
+
 void SphGpuSingle::CheckErrors() {
   const SphRunStats s = Stats();
   if (s.error_flags & ERR_BOUNDOUT) throw SphError(SPH_ERR_BOUNDOUT, "boundary particles were excluded (AbortBoundOut)");
   if (s.error_flags & ERR_DT_NAN) throw SphError(SPH_ERR_DT, "The computed Dt is NaN or infinity");
   if (s.error_flags & ERR_HALO_NODE)
     throw SphError(SPH_ERR_UNSUPPORTED, "slab halo: an mDBC ghost node needs particles beyond the slab's ghost columns");
-  if (s.error_flags & ERR_HALO_FACE) throw SphError(SPH_ERR_STATE, "slab halo: a face record did not fit its buffer");
+  if (s.error_flags & ERR_HALO_FACE)
+    throw SphError(SPH_ERR_STATE, "slab halo: a face record did not fit its buffer (step " + std::to_string(s.nstep) +
+                                      ", " + HaloDiag() + ")");
   if (s.error_flags & ERR_HALO_MISS)
     throw SphError(SPH_ERR_STATE, "slab halo: a face record found no ghost copy of its particle");
   if (s.error_flags & ERR_HALO_GHOST)
@@ -1953,7 +1980,22 @@ void SphSlabGroup::Run(unsigned nsteps) {
     });
   for (auto& t : th) t.join();
   for (size_t i = 0; i < n; i++)
-    if (err[i] && primary[i]) std::rethrow_exception(err[i]);
+    if (err[i] && primary[i]) {
+      try {
+        std::rethrow_exception(err[i]);
+      } catch (const SphError& e) {
+        // a face overflow is seen on every slab (folded): say where each slab stood
+        if (std::string(e.what()).find("did not fit") == std::string::npos) throw;
+        std::string m = e.what();
+        for (size_t j = 0; j < n; j++) {
+          try {
+            m += "; " + slabs[j]->HaloDiag();
+          } catch (...) {
+          }
+        }
+        throw SphError(e.status, m);
+      }
+    }
   for (size_t i = 0; i < n; i++)
     if (err[i]) std::rethrow_exception(err[i]);
 }

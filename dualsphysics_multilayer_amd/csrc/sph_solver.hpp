@@ -86,6 +86,7 @@ class SphGpuSingle {
   void SetTime(double time, double symdtpre);
   void Timing(double out_ms[4], uint64_t* launches);
   void CheckErrors();
+  std::string HaloDiag();
   // Moving boundaries / floating bodies (sph_bodies.hip), configured before the first step.
   void SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* movs, unsigned nevt, const SphMotionEvent* evts);
   void SetFloatings(unsigned nft, const SphFloatingDef* defs, double ftpause);

@@ -77,7 +77,7 @@ __global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double d
   double dt = cfl * fmin(dt3, fmin(dt1, dt2));
   // DtFixed / DtFixedFile at the step's TimeStep (the corrector's DtVariable sees the same
   // TimeStep as the predictor's: the time advanced in between)
-  if (K.dtfix_n || K.dtfix_val > 0) dt = fixed_dt(K, mode == DT_SYM_COR ? sc->tstep0 : sc->time);
+  if (K.dtfix_n || K.dtfix_val > 0) dt = fixed_dt(K, mode == DT_SYM_COR ? sc->tstep0 : sc->time, sc->dtfix_pos);
   // a NaN maximum (a NaN velocity, acceleration or viscosity anywhere) also stops the run:
   // fmin/fmax above would drop it, and the state it came from is already lost
   if (isnan(dt) || isinf(dt) || isnan(velmax) || isnan(acemax) || isnan(viscdt) || isnan(visceta)) {
@@ -109,12 +109,12 @@ __global__ void k_dt(DevScalars* __restrict__ sc, KConst K, double cfl, double d
   }
   // ViscoTime: Visco of the next step, at its TimeStep (JSphCpuSingle.cpp:1092), once the
   // step in flight is done (the Symplectic corrector keeps the predictor's Visco)
-  if (K.visco_n && mode != DT_SYM_PRE) sc->visco = visco_at(K, float(sc->time));
+  if (K.visco_n && mode != DT_SYM_PRE) sc->visco = visco_at(K, float(sc->time), sc->visco_pos);
 }
 
 // Visco at the current TimeStep (a new ViscoTime table, a restart time).
 __global__ void k_visco_init(DevScalars* __restrict__ sc, KConst K) {
-  if (threadIdx.x == 0) sc->visco = K.visco_n ? visco_at(K, float(sc->time)) : K.visco;
+  if (threadIdx.x == 0) sc->visco = K.visco_n ? visco_at(K, float(sc->time), sc->visco_pos) : K.visco;
 }
 
 void launch_visco_init(hipStream_t stm, DevScalars* sc, const KConst& K) {

@@ -153,24 +153,25 @@ __device__ __forceinline__ unsigned lane_order(const float4* __restrict__ poscel
 // 0.666 -> 0.638 ms, cfg5 unchanged.  The XCD-local spatial contiguity of a group's items
 // was worth less than the balance (neighbour rows are MALL hits either way).  Dealt in
 // chunks of 16 consecutive items (chunks of 1, 4, 16: same time) the L2-miss traffic of
-// the cfg2 interaction is 228 MB per launch instead of 397 MB.
-#ifndef SPH_ITEM_CHUNK
-#define SPH_ITEM_CHUNK 16  // round-robin granularity in items (a power of two)
-#endif
-// Items of one kind (fluid or bound) dealt to the 8 groups round-robin in chunks of CH.
+// the cfg2 interaction is 228 MB per launch instead of 397 MB.  Lists of >= ITEM_CHUNK_BIG_N
+// items (cfg3's 10M, cfg4's 4M) are dealt in chunks of 64: a group's neighbour rows stay in
+// its XCD's L2 longer (cfg3: 3.9 -> 2.2 GB of HBM traffic per launch at the same time,
+// DESIGN.md §9), while a list of a few thousand items keeps enough chunks per group.  The
+// item build writes the chunk's log2 beside the list's counts (QCTR_NITEMS + 3).
+constexpr unsigned ITEM_CHUNK_LOG2 = 4, ITEM_CHUNK_BIG_LOG2 = 6, ITEM_CHUNK_BIG_N = 32768;
+// Items of one kind (fluid or bound) dealt to the 8 groups round-robin in chunks of 2^sh.
 struct ItemDeal {
-  unsigned lo, n;  // the kind's list range [lo, lo + n)
+  unsigned lo, n, sh;  // the kind's list range [lo, lo + n), chunk log2
   __device__ __forceinline__ unsigned count(unsigned g) const {
-    constexpr unsigned CH = SPH_ITEM_CHUNK;
-    const unsigned nch = (n + CH - 1u) / CH;
+    const unsigned CH = 1u << sh;
+    const unsigned nch = (n + CH - 1u) >> sh;
     if (g >= nch) return 0u;
-    unsigned c = ((nch - g + 7u) / 8u) * CH;
-    if ((nch - 1u) % 8u == g) c -= nch * CH - n;  // the kind's last chunk is short
+    unsigned c = ((nch - g + 7u) / 8u) << sh;
+    if ((nch - 1u) % 8u == g) c -= (nch << sh) - n;  // the kind's last chunk is short
     return c;
   }
   __device__ __forceinline__ unsigned item(unsigned g, unsigned c) const {
-    constexpr unsigned CH = SPH_ITEM_CHUNK;
-    return lo + (g + 8u * (c / CH)) * CH + (c % CH);
+    return lo + ((g + 8u * (c >> sh)) << sh) + (c & ((1u << sh) - 1u));
   }
 };
 struct ItemGroup {
@@ -179,18 +180,20 @@ struct ItemGroup {
   __device__ __forceinline__ unsigned item(unsigned c) const { return c < nfg ? f.item(g, c) : b.item(g, c - nfg); }
 };
 struct ItemGroups {
-  unsigned nf, nb, lo;
-  // the list's counts {all, bound, first item}, written by k_items_place beside the work queues
+  unsigned nf, nb, lo, sh;
+  // the list's counts {all, bound, first item, chunk log2}, written by k_items_place beside
+  // the work queues
   __device__ __forceinline__ explicit ItemGroups(const unsigned* qctr) {
     const unsigned n = qctr[QCTR_NITEMS];
     nb = min(qctr[QCTR_NITEMS + 1], n);
     nf = n - nb;
     lo = qctr[QCTR_NITEMS + 2];
+    sh = min(qctr[QCTR_NITEMS + 3], 10u);
   }
   __device__ __forceinline__ ItemGroup group(unsigned g) const {
     ItemGroup r;
-    r.f = {lo, nf};
-    r.b = {lo + nf, nb};
+    r.f = {lo, nf, sh};
+    r.b = {lo + nf, nb, sh};
     r.g = g;
     r.nfg = r.f.count(g);
     r.n = r.nfg + r.b.count(g);

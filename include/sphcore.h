@@ -500,7 +500,8 @@ int sph_solver_set_floating_table(SphSolver* s, uint32_t body, int32_t kind, uin
                                   const double* values);
 int sph_solver_floatings(SphSolver* s, uint32_t cap, SphFloatingState* out, uint32_t* nft);
 /* Time tables of the step (call before the first step, or after sph_solver_set_time; on
- * slabs on every rank; n >= 2 rows, times nondecreasing, n = 0 removes the table):
+ * slabs on every rank; n >= 2 rows in any order, walked forward from the row of the last
+ * lookup as the reference walks them (Position), n = 0 removes the table):
  *   SPH_TTAB_DTFIXED  <parameter DtFixedFile>: dt(t) of every step, values in ms as in the
  *                     file (JDsFixedDt::LoadFile/GetDt, JDsFixedDt.cpp; applied in DtVariable
  *                     before the NaN check and the DtMin floor, JSphCpu.cpp:1621);

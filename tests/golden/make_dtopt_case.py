@@ -35,6 +35,14 @@ VARIANTS = {
                                     {"dtfixed.csv": "# time(s);dt(ms)\n0;0.08\n0.006;0.22\n1;0.22\n"}),
     "verlet_ddt2_viscotime": ("dambreak", 0.03, 1, 2, 100, (1, 10, 100), {"ViscoTime": "visco.txt"},
                               {"visco.txt": "# time visco\n0 0.01\n0.004 0.6\n1 0.6\n"}),
+    # rows out of time order: the reference walks them forward from the row of its last lookup
+    # (JDsFixedDt::GetDt / JDsViscoInput::GetVisco keep Position), so past 6 ms the dt comes
+    # from the (0.003 s, 1 s) interval, past 4 ms the Visco from the (0.002 s, 1 s) one
+    "verlet_ddt2_dtfixedfile_unordered": ("dambreak", 0.03, 1, 2, 100, (1, 40, 100), {"DtFixedFile": "dtfixed.csv"},
+                                          {"dtfixed.csv": "# time(s);dt(ms)\n0;0.08\n0.006;0.22\n0.003;0.15\n"
+                                                          "1;0.3\n"}),
+    "verlet_ddt2_viscotime_unordered": ("dambreak", 0.03, 1, 2, 100, (1, 50, 100), {"ViscoTime": "visco.txt"},
+                                        {"visco.txt": "# time visco\n0 0.01\n0.004 0.6\n0.002 0.3\n1 0.1\n"}),
     # a fast wide flap (no wait, 8 Hz, 12 degrees): its tip, ~4 m/s, sets VelMax (10 VelMax > Cs0)
     "flume_verlet_ddt2_dtallparticles": ("flume", 0.03, 1, 2, 60, (1, 20, 60), {"DtAllParticles": "1"}, {}),
 }

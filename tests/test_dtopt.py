@@ -21,7 +21,7 @@ from dualsphysics_multilayer_amd.xmlcase import XmlCase
 HERE = os.path.dirname(os.path.abspath(__file__))
 FIX = os.path.join(HERE, "golden", "bi4")
 VARIANTS = ("verlet_ddt2_dtfixed", "symplectic_ddt1_dtfixedfile", "verlet_ddt2_viscotime",
-            "flume_verlet_ddt2_dtallparticles")
+            "flume_verlet_ddt2_dtallparticles", "verlet_ddt2_dtfixedfile_unordered", "verlet_ddt2_viscotime_unordered")
 FLOOR = (2e-10, 2e-7, 2.5e-3)  # pos m, vel m/s, rho kg/m3 (as tests/test_ext.py)
 
 
@@ -93,6 +93,34 @@ def test_reference_used_the_fixed_dt():
     assert np.abs(dt[1:] - np.interp(t[:-2], [0, 0.006, 1], [0.08e-3, 0.22e-3, 0.22e-3])).max() < 1e-17
 
 
+def _walk(T, V, ts):
+    """JDsFixedDt::GetDt's walk (JDsFixedDt.cpp:111-124) with its persistent Position."""
+    pos, out = 0, []
+    for t in ts:
+        tini, tnext = T[pos], (T[pos + 1] if pos + 1 < len(T) else T[pos])
+        while tnext < t and pos + 2 < len(T):
+            tini, tnext = tnext, T[pos + 2]
+            pos += 1
+        out.append(V[pos] if t <= tini else V[pos + 1] if t >= tnext
+                   else (t - tini) / (tnext - tini) * (V[pos + 1] - V[pos]) + V[pos])
+    return np.array(out)
+
+
+def test_reference_walks_unordered_rows():
+    """A DtFixedFile with rows out of time order: the reference takes it, and past the
+    out-of-order row its dt follows the walk from the row of the last lookup (0.15 -> 0.3 ms
+    over [0.003 s, 1 s]), not the rows sorted by time; the loader keeps the file's order."""
+    x = _case("verlet_ddt2_dtfixedfile_unordered")
+    T, V = x.dtfixed_table[:, 0], x.dtfixed_table[:, 1] / 1000
+    assert list(T) == [0, 0.006, 0.003, 1]
+    t = _ref("verlet_ddt2_dtfixedfile_unordered")["times"]
+    dt = np.diff(t)
+    assert np.abs(dt - _walk(T, V, t[:-1])).max() < 1e-17
+    o = np.argsort(T, kind="stable")
+    assert np.abs(dt - np.interp(t[:-1], T[o], V[o])).max() > 1e-5
+    assert list(_case("verlet_ddt2_viscotime_unordered").visco_table[:, 0]) == [0, 0.004, 0.002, 1]
+
+
 # ---- GPU ----------------------------------------------------------------------------------------
 def _run_check(s, g, k0=0):
     done = k0
@@ -124,7 +152,8 @@ def test_gpu_matches_reference_parts(v):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("v", ["verlet_ddt2_viscotime", "symplectic_ddt1_dtfixedfile"])
+@pytest.mark.parametrize("v", ["verlet_ddt2_viscotime", "symplectic_ddt1_dtfixedfile",
+                               "verlet_ddt2_dtfixedfile_unordered"])
 def test_gpu_slabs_match_reference_parts(v):
     from dualsphysics_multilayer_amd.core import SphSlabGroup, slab_partition
 
