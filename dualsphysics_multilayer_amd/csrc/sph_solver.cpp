@@ -1364,7 +1364,7 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
                             nnormal_, ftnormals_);
       transport_->exchange(sl, sizeof(MdbcFaceRec) * nsl, sr, sizeof(MdbcFaceRec) * nsr, rl, sizeof(MdbcFaceRec) * nrl,
                            rr, sizeof(MdbcFaceRec) * nrr, stream);
-      launch_mdbc_face_apply(stream, sc_, hl ? rl : nullptr, hr ? rr : nullptr, nrl, nrr, bidx_, casenpb_, cur_.idp,
+      launch_mdbc_face_apply(stream, sc_, hl ? rl : nullptr, hr ? rr : nullptr, nrl, nrr, bidx_, nnormal_, cur_.idp,
                              cur_.velrhop, press_);
     }
     TimedEnd(3);
