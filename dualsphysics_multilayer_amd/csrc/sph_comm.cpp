@@ -104,12 +104,12 @@ std::unique_ptr<SlabTransport> make_rccl_transport(const unsigned char id[128], 
 
 // ---------------------------------------------------------------------------------
 LocalHub::LocalHub(int nslabs) : slots(size_t(nslabs)), n(nslabs) {
-  if (const char* e = std::getenv("SPH_SLAB_TURNS")) turns = std::atoi(e) != 0;
+  if (const char* e = std::getenv("SPH_SLAB_TURNS")) turns = std::max(0, std::min(2, std::atoi(e)));
 }
 
 LocalHub::~LocalHub() {
   for (Slot& sl : slots)
-    for (hipEvent_t e : {sl.ready, sl.copied, sl.idone[0], sl.idone[1]})
+    for (hipEvent_t e : {sl.ready, sl.copied, sl.idone[0], sl.idone[1], sl.idone[2], sl.idone[3]})
       if (e) (void)hipEventDestroy(e);
 }
 
@@ -207,9 +207,9 @@ class LocalTransport final : public SlabTransport {
     if (!gen_) return;
     reuse_guard(s);
   }
-  bool turns() const override { return hub_->turns; }
+  bool turns() const override { return hub_->turns != 0; }
   void turn_wait(int kind, hipStream_t a, hipStream_t b) override {
-    if (!hub_->turns) return;
+    if (!active(kind)) return;
     if (has_left()) {
       const LocalHub::Slot& L = hub_->slots[size_t(rank - 1)];
       const unsigned long long t = turn_[kind] + 1;
@@ -217,9 +217,9 @@ class LocalTransport final : public SlabTransport {
       if (a) check_hip(hipStreamWaitEvent(a, L.idone[kind], 0), "turn: wait");
       if (b) check_hip(hipStreamWaitEvent(b, L.idone[kind], 0), "turn: wait");
     } else if (nranks > 1) {
-      // the chain of one kind starts after the last slab's turn of the other kind (the
-      // divides of a step all end before its first interaction, and the other way round)
-      const int other = 1 - kind;
+      // the chain of one kind starts after the last slab's turn of the kind before it in the
+      // step's cycle (the divides of a step all end before its first interaction, ...)
+      const int other = hub_->turn_prev(kind);
       const LocalHub::Slot& Z = hub_->slots[size_t(nranks - 1)];
       const unsigned long long t = turn_[other];
       if (t) {
@@ -230,7 +230,7 @@ class LocalTransport final : public SlabTransport {
     }
   }
   void turn_done(int kind, hipStream_t s) override {
-    if (!hub_->turns) return;
+    if (!active(kind)) return;
     events(s);
     LocalHub::Slot& me = hub_->slots[size_t(rank)];
     const unsigned long long t = turn_[kind] + 1;
@@ -280,7 +280,7 @@ class LocalTransport final : public SlabTransport {
     check_hip(hipStreamGetDevice(s, &dev), "hipStreamGetDevice");
     check_hip(hipGetDevice(&cur), "hipGetDevice");
     check_hip(hipSetDevice(dev), "hipSetDevice");
-    for (hipEvent_t* e : {&me.ready, &me.copied, &me.idone[0], &me.idone[1]})
+    for (hipEvent_t* e : {&me.ready, &me.copied, &me.idone[0], &me.idone[1], &me.idone[2], &me.idone[3]})
       check_hip(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
     check_hip(hipSetDevice(cur), "hipSetDevice");
   }
@@ -295,8 +295,12 @@ class LocalTransport final : public SlabTransport {
     if (L) check_hip(hipStreamWaitEvent(s, L->copied, 0), "exchange: reuse left");
     if (R) check_hip(hipStreamWaitEvent(s, R->copied, 0), "exchange: reuse right");
   }
+  // the kinds of the chain: interactions and divides (SPH_SLAB_TURNS=1), or all four (2)
+  bool active(int kind) const {
+    return hub_->turns == 2 || (hub_->turns == 1 && (kind == TURN_INTERACTION || kind == TURN_DIVIDE));
+  }
   std::shared_ptr<LocalHub> hub_;
-  unsigned long long gen_ = 0, turn_[2] = {0, 0};
+  unsigned long long gen_ = 0, turn_[4] = {0, 0, 0, 0};
 };
 
 std::unique_ptr<SlabTransport> make_local_transport(std::shared_ptr<LocalHub> hub, int rank) {

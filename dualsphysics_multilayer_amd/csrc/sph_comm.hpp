@@ -53,13 +53,17 @@ class SlabTransport {
   // Stream s waits until the neighbours have read the buffers of the last post, before it
   // writes them again (RCCL / shm: a send completes in this rank's stream order already).
   virtual void wait_sends(hipStream_t s) { (void)s; }
-  // Measurement mode of the in-process transport (SPH_SLAB_TURNS=1, SphSlabGroup): slab r's
+  // Measurement mode of the in-process transport (SPH_SLAB_TURNS, SphSlabGroup): slab r's
   // interaction (kind TURN_INTERACTION) and the kernels of its divide after the exchange
   // (TURN_DIVIDE) start on the GPU after slab r-1's of the same step have ended, so one GPU
   // runs one slab's interaction (interior items + ghost transfer + face items) or divide at a
-  // time, as each rank does on its own GPU.  turn_wait() gates the streams a and b (either
-  // may be null), turn_done() ends the turn on stream s.  No-ops elsewhere.
-  enum { TURN_INTERACTION = 0, TURN_DIVIDE = 1 };
+  // time, as each rank does on its own GPU.  SPH_SLAB_TURNS=2 adds the update kernels
+  // (TURN_UPDATE) and the exchange's pack (TURN_PACK) to the chain (kinds in the step's cycle
+  // interaction -> update -> pack -> divide): every kernel of a slab's step then runs alone on
+  // the GPU but the few-us face-message / migrant copies and the unpack.  turn_wait() gates
+  // the streams a and b (either may be null), turn_done() ends the turn on stream s.  No-ops
+  // elsewhere.
+  enum { TURN_INTERACTION = 0, TURN_UPDATE = 1, TURN_PACK = 2, TURN_DIVIDE = 3, TURN_KINDS = 4 };
   virtual bool turns() const { return false; }
   virtual void turn_wait(int kind, hipStream_t a, hipStream_t b) { (void)kind; (void)a; (void)b; }
   virtual void turn_done(int kind, hipStream_t s) { (void)kind; (void)s; }
@@ -124,14 +128,20 @@ class LocalHub {
     hipEvent_t ready = nullptr;   // the posted buffers are complete
     hipEvent_t copied = nullptr;  // this slot's copies of the neighbours' buffers are done
     // turns (measurement mode), per kind: turns ended and the event of the last one
-    unsigned long long turn[2] = {0, 0};
-    hipEvent_t idone[2] = {nullptr, nullptr};
+    unsigned long long turn[4] = {0, 0, 0, 0};
+    hipEvent_t idone[4] = {nullptr, nullptr, nullptr, nullptr};
     unsigned vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     std::vector<float> fvals;
   };
   std::vector<Slot> slots;
   int n;
-  bool turns = false;  // SPH_SLAB_TURNS
+  int turns = 0;  // SPH_SLAB_TURNS: 1 interactions and divides, 2 every kernel of the step
+  // the kind whose chain ends before a chain of `kind` starts (the step's cycle of kinds)
+  int turn_prev(int kind) const {
+    if (turns == 1) return kind == TURN_KIND_I ? TURN_KIND_D : TURN_KIND_I;
+    return (kind + 3) % 4;
+  }
+  static constexpr int TURN_KIND_I = 0, TURN_KIND_D = 3;
 
  private:
   [[noreturn]] static void throw_aborted();

@@ -24,6 +24,7 @@
 // shifting sum (ShiftMode NoBound/NoFixed), else it is drained in mirrored units too.  cfg5: 1.85 -> 1.55 ms per interaction (SPH_NN_MIRROR=0: the
 // row-ordered drain of every pass).
 #include <algorithm>
+#include <stdexcept>
 
 #include "sph_tiled.hpp"
 
@@ -903,11 +904,23 @@ void launch_nn_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const ui
   } else if (K.nntvisco == 1) SPH_NN_TD(1, SH)                                 \
   else if (K.nntvisco == 2) SPH_NN_TD(2, SH)                                   \
   else SPH_NN_TD(3, SH)
+#ifdef SPH_NN_DIAG_CFG5
+  // diagnostic builds (kernel A/B at cfg5 only): the one instantiation pair of BASELINE cfg5
+  if (K.nnvelgrad == 2 || K.nntvisco != 2 || K.tdensity != 3 || ftmassp || K.scelldiv != 1)
+    throw std::runtime_error("SPH_NN_DIAG_CFG5 build: cfg5 only");
+  if (shift) hipLaunchKernelGGL((k_nn_tiled<2, 3, true, 1, false>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr,
+                                poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,
+                                ftmassp);
+  else hipLaunchKernelGGL((k_nn_tiled<2, 3, false, 1, false>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr,
+                          poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,
+                          ftmassp);
+#else
   if (shift) {
     SPH_NN_TV(true)
   } else {
     SPH_NN_TV(false)
   }
+#endif
 #undef SPH_NN_TV
 #undef SPH_NN_TD
 #undef SPH_NN

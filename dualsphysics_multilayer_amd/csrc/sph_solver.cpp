@@ -973,7 +973,11 @@ void SphGpuSingle::Exchange() {
   // the pack rewrites the migrant and face-message send buffers: the neighbours' copies of
   // the last messages (in-process slabs copy asynchronously) are done first
   transport_->wait_sends(stream);
+  // turns measurement mode 2: the pack kernels are a turn of their own
+  const bool pturn = in_run_ && transport_->turns();
+  if (pturn) transport_->turn_wait(SlabTransport::TURN_PACK, stream, nullptr);
   pack();  // (its accumulated counts were zeroed by the last exchange's kernels: no memset launches)
+  if (pturn) transport_->turn_done(SlabTransport::TURN_PACK, stream);
   const size_t mb = 4 * (size_t(FMSG_HDR) + faces_.nfb);
   transport_->exchange(faces_.msg[0], hl ? mb : 0, faces_.msg[1], hr ? mb : 0, faces_.msg[2], hl ? mb : 0,
                        faces_.msg[3], hr ? mb : 0, stream);
@@ -1474,7 +1478,16 @@ void SphGpuSingle::DtVariable(int mode) {
   }
 }
 
+// Turns measurement mode 2 (SPH_SLAB_TURNS=2, in-process slabs): the update kernels are a
+// turn of their own.
+void SphGpuSingle::UpdateTurn(bool begin) {
+  if (!(slab() && in_run_ && transport_->turns())) return;
+  if (begin) transport_->turn_wait(SlabTransport::TURN_UPDATE, stream, nullptr);
+  else transport_->turn_done(SlabTransport::TURN_UPDATE, stream);
+}
+
 void SphGpuSingle::ComputeVerlet() {
+  UpdateTurn(true);
   TimedBegin(1);
   verletstep_++;
   const bool euler = !(verletstep_ < C.verlet_steps);
@@ -1482,9 +1495,11 @@ void SphGpuSingle::ComputeVerlet() {
   if (euler) verletstep_ = 0;
   std::swap(cur_.velrhop, cur_.velrhopm1);
   TimedEnd(1);
+  UpdateTurn(false);
 }
 
 void SphGpuSingle::ComputeSymplecticPre() {
+  UpdateTurn(true);
   TimedBegin(1);
   std::swap(cur_.posxy, cur_.posxypre);
   std::swap(cur_.posz, cur_.poszpre);
@@ -1492,13 +1507,16 @@ void SphGpuSingle::ComputeSymplecticPre() {
   havepre_ = true;
   launch_sym_pre(stream, cap_, sc_, K, arace_, cur_, G);
   TimedEnd(1);
+  UpdateTurn(false);
 }
 
 void SphGpuSingle::ComputeSymplecticCorr() {
+  UpdateTurn(true);
   TimedBegin(1);
   launch_sym_cor(stream, cap_, sc_, K, arace_, cur_, G, shift_ ? shiftpos_ : nullptr);
   havepre_ = false;
   TimedEnd(1);
+  UpdateTurn(false);
 }
 
 void SphGpuSingle::ComputeStep() {

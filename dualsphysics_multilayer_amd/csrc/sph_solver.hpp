@@ -68,6 +68,7 @@ class SphGpuSingle {
   void RunCellDivide();
   void Interaction_Forces(int interstep);
   void DtVariable(int mode);
+  void UpdateTurn(bool begin);
   void ComputeVerlet();
   void ComputeSymplecticPre();
   void ComputeSymplecticCorr();

@@ -1,6 +1,6 @@
 """One slab's own step on one GPU, the other slabs kept out of its window.
 
-    SPH_SLAB_TURNS=1 python3 profiles/slab_turns.py [--slabs 8] [--steps 10] [--repeat 2]
+    SPH_SLAB_TURNS=1|2 python3 profiles/slab_turns.py [--slabs 8] [--steps 10] [--repeat 2]
     (under rocprofv3 --kernel-trace for the committed trace: --repeat 1 --only 1)
 
 BASELINE cfg3 (the 10M Symplectic + DDT1 dam break) in its 8-slab split, in-process on one
@@ -10,7 +10,10 @@ exchange stream, its face items — starts on the GPU only after slab r-1's inte
 the same step has ended, and likewise the kernels of its divide after the exchange.  So each
 slab's interaction and divide run with no other slab's interaction or divide beside them,
 as each rank's do on its own GPU; the slabs' exchanges (pack, face counts, migrants) and
-updates still run side by side.  The transfers are device-to-device copies (blit kernels in
+updates still run side by side.  SPH_SLAB_TURNS=2 chains the update kernels and the
+exchange's pack kernels too (every kernel of a slab's step alone on the GPU, except the
+few-us face-message and migrant copies and the unpack): the per-slab phase times are then
+uncontended by the other slabs.  The transfers are device-to-device copies (blit kernels in
 the block slots the interior launch leaves free); on the 8-GPU node they are RCCL
 send/receive over one xGMI link per face.
 
@@ -70,14 +73,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--only", choices=tuple(MODES), default=None, help="one mode only (e.g. under rocprofv3)")
+    ap.add_argument("--modes", default=None, help="comma-separated subset of the modes")
     ap.add_argument("--dp", type=float, default=0.00205)
     a = ap.parse_args()
-    if os.environ.get("SPH_SLAB_TURNS") != "1":
-        raise SystemExit("run with SPH_SLAB_TURNS=1 (the turns measurement mode)")
+    if os.environ.get("SPH_SLAB_TURNS") not in ("1", "2"):
+        raise SystemExit("run with SPH_SLAB_TURNS=1 or 2 (the turns measurement modes)")
     case = DamBreakCase(a.dp, step_algorithm=2, tdensity=1)
     bounds = [int(x) for x in slab_partition(case, a.slabs)]
-    res = {"workload": "cfg3", "np": int(case.np), "bounds": bounds, "steps": a.steps, "runs": []}
-    modes = [a.only] if a.only is not None else list(MODES)
+    res = {"workload": "cfg3", "np": int(case.np), "bounds": bounds, "steps": a.steps,
+           "turns_mode": int(os.environ["SPH_SLAB_TURNS"]), "runs": []}
+    modes = [a.only] if a.only is not None else (a.modes.split(",") if a.modes else list(MODES))
     for _ in range(a.repeat):
         for ov in modes:
             r = run(case, bounds, ov, a.steps, a.warmup)
@@ -94,6 +99,10 @@ def main():
             "update_ms": [best("update", i) for i in range(n)],
             "wall_ms_per_step": min(r["wall_ms_per_step"] for r in rs),
         }
+        # a slab's own step (Symplectic: two interactions, updates and divides per step)
+        summ[ov]["slab_kernels_ms_per_step"] = [
+            round(2 * (summ[ov]["interaction_ms"][i] + summ[ov]["update_ms"][i] + summ[ov]["divide_ms"][i]), 4)
+            for i in range(n)]
     res["summary_min_over_repeats"] = summ
     print(json.dumps(res), flush=True)
 
