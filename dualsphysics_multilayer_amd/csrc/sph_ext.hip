@@ -444,147 +444,132 @@ __global__ __launch_bounds__(TB) void k_fluid_ext(DevScalars* __restrict__ sc, c
   __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];
   __shared__ unsigned s_nwave[4];
-  const ItemGroups IG(qctr);
-  const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f;
   // passes whose shifting cut-off depends on the pair order: the fluid rows with floating
   // bodies under NoBound, the bound rows under NoBound / NoFixed
   const bool ordf = SHIFT && FT && K.shiftmode == 1;
   const bool ordb = SHIFT && (K.shiftmode == 1 || K.shiftmode == 2);
-  for (unsigned q = 0; q < 8; q++) {
-    const unsigned xg = (grp + q) & 7;
-    const ItemGroup gr = IG.group(xg);
-    const unsigned nst = (gridDim.x - xg + 7u) / 8u;
-    bool first = q == 0;
-    for (;;) {
-      if (threadIdx.x == 0)
-        s_item = first ? (blockIdx.x >> 3)
-                 : (nst + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gr.n)
-                     ? gr.n
-                     : nst + atomicAdd(&qctr[xg * QSTRIDE], 1u);
-      first = false;
-      __syncthreads();
-      const unsigned c = s_item;
-      __syncthreads();
-      if (c >= gr.n) break;
-      const uint4 item = items[gr.item(c)];
-      const bool bitem = (item.x & ITEM_BOUND) != 0u;
-      const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
-      const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);
-      const int xo = (ia + ib + 1) >> 1;
-      const int xa = max(ia - S, 0), xb = min(ib + S, g.ncx - 1);
-      if (bitem) {  // no fluid within reach: ar = 0 (PreInteraction reset), nothing else
-        bool any = false;
-        for (int z = max(cz - S, 0); z <= min(cz + S, g.ncz - 1); z++)
-          for (int y = max(cy - S, 0); y <= min(cy + S, g.ncy - 1); y++) {
-            const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
-            any |= bc[rowbase + xa] != bc[rowbase + xb + 1];
-          }
-        if (!any) {
-          for (unsigned p1 = item.z + threadIdx.x; p1 < item.w; p1 += TB) arace[p1] = make_float4(0.f, 0.f, 0.f, 0.f);
-          continue;
+  ItemCursor<false> cur(qctr);
+  for (;;) {
+    const unsigned it = cur.next(&s_item);
+    if (it == ITEM_NONE) break;
+    const uint4 item = items[it];
+    const bool bitem = (item.x & ITEM_BOUND) != 0u;
+    const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
+    const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);
+    const int xo = (ia + ib + 1) >> 1;
+    const int xa = max(ia - S, 0), xb = min(ib + S, g.ncx - 1);
+    if (bitem) {  // no fluid within reach: ar = 0 (PreInteraction reset), nothing else
+      bool any = false;
+      for (int z = max(cz - S, 0); z <= min(cz + S, g.ncz - 1); z++)
+        for (int y = max(cy - S, 0); y <= min(cy + S, g.ncy - 1); y++) {
+          const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+          any |= bc[rowbase + xa] != bc[rowbase + xb + 1];
         }
-      }
-      const unsigned p1 = item.z + lane_order(E.poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
-      const bool act = threadIdx.x < item.w - item.z;
-      ExtP1 p;
-      int cx1 = ia;
-      p.ftp1 = false;
-      for (int k = 0; k < 6; k++) p.t[k] = 0.f;
-      if (act) {
-        const float4 pc1 = E.poscell[p1];
-        cx1 = int(DcelCellx(K.domcellcode, __float_as_uint(pc1.w)));
-        p.x = pc1.x + float(cx1 - xo) * K.scell;
-        p.y = pc1.y;
-        p.z = pc1.z;
-        p.vr = E.velrhop[p1];
-        p.press = bitem ? 0.f : E.press[p1];
-        p.ftp1 = FT && !bitem && CodeType(E.code[p1]) == CODE_TYPE_FLOATING;
-        if (TVISCO == 2 && !bitem && !p.ftp1) {  // taup1: zero for a floating p1 (not fluid)
-          const float4 ta = E.tau[2 * p1], tb = E.tau[2 * p1 + 1];
-          p.t[0] = ta.x;
-          p.t[1] = ta.y;
-          p.t[2] = ta.z;
-          p.t[3] = ta.w;
-          p.t[4] = tb.x;
-          p.t[5] = tb.y;
-        }
-      } else {
-        p.x = p.y = p.z = 1e30f;
-        p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
-        p.press = 0.f;
-      }
-      const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
-      const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
-      const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act, p1};
-      if (bitem) {
-        ExtAcc f = {};
-        ext_pass<TVISCO, TD, SHIFT, FT, 2, S>(K, E, g, rc, p, thr, bc, true, 0.f, sA, sB, sC, sD, f);
-        if (act) {
-          arace[p1] = make_float4(0.f, 0.f, 0.f, (f.ar != 0.f || f.visc != 0.f) ? 0.f + f.ar : 0.f);
-          viscmax = fmaxf(viscmax, f.visc);
-        }
+      if (!any) {
+        for (unsigned p1 = item.z + threadIdx.x; p1 < item.w; p1 += TB) arace[p1] = make_float4(0.f, 0.f, 0.f, 0.f);
         continue;
       }
-      // fluid p1: the fluid pass, then the bound pass; the shifting sums carry over
-      // (shiftposfs[p1] is stored by the first pass and loaded by the second), a floating
-      // p1 starts with x = FLT_MAX (:662); DDT is off for a floating p1 (:661)
-      ExtAcc f = {}, b = {};
-      if (p.ftp1) {
-        f.sx = FLT_MAX;
-        if (TD) f.delta = FLT_MAX;
+    }
+    const unsigned p1 = item.z + lane_order(E.poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
+    const bool act = threadIdx.x < item.w - item.z;
+    ExtP1 p;
+    int cx1 = ia;
+    p.ftp1 = false;
+    for (int k = 0; k < 6; k++) p.t[k] = 0.f;
+    if (act) {
+      const float4 pc1 = E.poscell[p1];
+      cx1 = int(DcelCellx(K.domcellcode, __float_as_uint(pc1.w)));
+      p.x = pc1.x + float(cx1 - xo) * K.scell;
+      p.y = pc1.y;
+      p.z = pc1.z;
+      p.vr = E.velrhop[p1];
+      p.press = bitem ? 0.f : E.press[p1];
+      p.ftp1 = FT && !bitem && CodeType(E.code[p1]) == CODE_TYPE_FLOATING;
+      if (TVISCO == 2 && !bitem && !p.ftp1) {  // taup1: zero for a floating p1 (not fluid)
+        const float4 ta = E.tau[2 * p1], tb = E.tau[2 * p1 + 1];
+        p.t[0] = ta.x;
+        p.t[1] = ta.y;
+        p.t[2] = ta.z;
+        p.t[3] = ta.w;
+        p.t[4] = tb.x;
+        p.t[5] = tb.y;
       }
-      const float visco = K.visco_n ? sc->visco : K.visco;  // ViscoTime (k_dt) or the case's
-      ext_pass<TVISCO, TD, SHIFT, FT, 0, S>(K, E, g, rc, p, thr, bc, !ordf, visco, sA, sB, sC, sD, f);
-      b.sx = f.sx;
-      b.sy = f.sy;
-      b.sz = f.sz;
-      b.sw = f.sw;
-      if (p.ftp1 && TD) b.delta = FLT_MAX;
-      ext_pass<TVISCO, TD, SHIFT, FT, 1, S>(K, E, g, rc, p, thr, bc, !ordb, K.visco_n ? visco * K.viscobf : K.viscobound,
-                                         sA, sB, sC, sD, b);
+    } else {
+      p.x = p.y = p.z = 1e30f;
+      p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
+      p.press = 0.f;
+    }
+    const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
+    const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
+    const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act, p1};
+    if (bitem) {
+      ExtAcc f = {};
+      ext_pass<TVISCO, TD, SHIFT, FT, 2, S>(K, E, g, rc, p, thr, bc, true, 0.f, sA, sB, sC, sD, f);
       if (act) {
-        // the two passes' stores (:800-818); with shifting both always store
-        float ar = 0.f, ax = 0.f, ay = 0.f, az = 0.f, delta = 0.f;
-        float gxx = 0.f, gxy = 0.f, gxz = 0.f, gyy = 0.f, gyz = 0.f, gzz = 0.f;
-        if (SHIFT || f.ar != 0.f || f.ax != 0.f || f.ay != 0.f || f.az != 0.f || f.visc != 0.f) {
-          if (TD) delta = (f.delta == FLT_MAX ? FLT_MAX : 0.f + f.delta);
-          ar = f.ar;
-          ax = f.ax;
-          ay = f.ay;
-          az = f.az;
-          gxx = f.gxx, gxy = f.gxy, gxz = f.gxz, gyy = f.gyy, gyz = f.gyz, gzz = f.gzz;
-        }
-        if (SHIFT || b.ar != 0.f || b.ax != 0.f || b.ay != 0.f || b.az != 0.f || b.visc != 0.f) {
-          if (TD) delta = (delta == FLT_MAX || b.delta == FLT_MAX ? FLT_MAX : delta + b.delta);
-          ar += b.ar;
-          ax += b.ax;
-          ay += b.ay;
-          az += b.az;
-          gxx += b.gxx, gxy += b.gxy, gxz += b.gxz, gyy += b.gyy, gyz += b.gyz, gzz += b.gzz;
-        }
-        if (TD && delta != FLT_MAX) ar += delta;
-        if (K.sim2d) ay = 0.f;  // Simulate2D: Acec[].y = 0 (JSphCpuSingle.cpp:544-549)
-        arace[p1] = make_float4(ax, ay, az, ar);
-        if (SHIFT && shiftstore) shiftpos[p1] = make_float4(b.sx, b.sy, b.sz, b.sw);
-        viscmax = fmaxf(viscmax, fmaxf(f.visc, b.visc));
-        ace2max = nanmax(ace2max, ax * ax + ay * ay + az * az);
-        if constexpr (TVISCO == 2) {
-          // ComputeSpsTau (:929-954) of p1 from this interaction's gradients
-          const float pow1 = gxx * gxx + gyy * gyy + gzz * gzz;
-          const float prr = pow1 + pow1 + gxy * gxy + gxz * gxz + gyz * gyz;
-          const float visc_sps = K.spssmag * sqrtf(prr);
-          const float div_u = gxx + gyy + gzz;
-          const float sps_k = (2.0f / 3.0f) * visc_sps * div_u;
-          const float sps_blin = K.spsblin * prr;
-          const float sumsps = -(sps_k + sps_blin);
-          const float twovisc_sps = visc_sps + visc_sps;
-          const float one_rho2 = 1.0f / p.vr.w;
-          taunew[2 * p1] = make_float4(one_rho2 * (twovisc_sps * gxx + sumsps), one_rho2 * (visc_sps * gxy),
-                                       one_rho2 * (visc_sps * gxz), one_rho2 * (twovisc_sps * gyy + sumsps));
-          taunew[2 * p1 + 1] = make_float4(one_rho2 * (visc_sps * gyz), one_rho2 * (twovisc_sps * gzz + sumsps), 0.f,
-                                           0.f);
-        }
+        arace[p1] = make_float4(0.f, 0.f, 0.f, (f.ar != 0.f || f.visc != 0.f) ? 0.f + f.ar : 0.f);
+        viscmax = fmaxf(viscmax, f.visc);
+      }
+      continue;
+    }
+    // fluid p1: the fluid pass, then the bound pass; the shifting sums carry over
+    // (shiftposfs[p1] is stored by the first pass and loaded by the second), a floating
+    // p1 starts with x = FLT_MAX (:662); DDT is off for a floating p1 (:661)
+    ExtAcc f = {}, b = {};
+    if (p.ftp1) {
+      f.sx = FLT_MAX;
+      if (TD) f.delta = FLT_MAX;
+    }
+    const float visco = K.visco_n ? sc->visco : K.visco;  // ViscoTime (k_dt) or the case's
+    ext_pass<TVISCO, TD, SHIFT, FT, 0, S>(K, E, g, rc, p, thr, bc, !ordf, visco, sA, sB, sC, sD, f);
+    b.sx = f.sx;
+    b.sy = f.sy;
+    b.sz = f.sz;
+    b.sw = f.sw;
+    if (p.ftp1 && TD) b.delta = FLT_MAX;
+    ext_pass<TVISCO, TD, SHIFT, FT, 1, S>(K, E, g, rc, p, thr, bc, !ordb, K.visco_n ? visco * K.viscobf : K.viscobound,
+                                       sA, sB, sC, sD, b);
+    if (act) {
+      // the two passes' stores (:800-818); with shifting both always store
+      float ar = 0.f, ax = 0.f, ay = 0.f, az = 0.f, delta = 0.f;
+      float gxx = 0.f, gxy = 0.f, gxz = 0.f, gyy = 0.f, gyz = 0.f, gzz = 0.f;
+      if (SHIFT || f.ar != 0.f || f.ax != 0.f || f.ay != 0.f || f.az != 0.f || f.visc != 0.f) {
+        if (TD) delta = (f.delta == FLT_MAX ? FLT_MAX : 0.f + f.delta);
+        ar = f.ar;
+        ax = f.ax;
+        ay = f.ay;
+        az = f.az;
+        gxx = f.gxx, gxy = f.gxy, gxz = f.gxz, gyy = f.gyy, gyz = f.gyz, gzz = f.gzz;
+      }
+      if (SHIFT || b.ar != 0.f || b.ax != 0.f || b.ay != 0.f || b.az != 0.f || b.visc != 0.f) {
+        if (TD) delta = (delta == FLT_MAX || b.delta == FLT_MAX ? FLT_MAX : delta + b.delta);
+        ar += b.ar;
+        ax += b.ax;
+        ay += b.ay;
+        az += b.az;
+        gxx += b.gxx, gxy += b.gxy, gxz += b.gxz, gyy += b.gyy, gyz += b.gyz, gzz += b.gzz;
+      }
+      if (TD && delta != FLT_MAX) ar += delta;
+      if (K.sim2d) ay = 0.f;  // Simulate2D: Acec[].y = 0 (JSphCpuSingle.cpp:544-549)
+      arace[p1] = make_float4(ax, ay, az, ar);
+      if (SHIFT && shiftstore) shiftpos[p1] = make_float4(b.sx, b.sy, b.sz, b.sw);
+      viscmax = fmaxf(viscmax, fmaxf(f.visc, b.visc));
+      ace2max = nanmax(ace2max, ax * ax + ay * ay + az * az);
+      if constexpr (TVISCO == 2) {
+        // ComputeSpsTau (:929-954) of p1 from this interaction's gradients
+        const float pow1 = gxx * gxx + gyy * gyy + gzz * gzz;
+        const float prr = pow1 + pow1 + gxy * gxy + gxz * gxz + gyz * gyz;
+        const float visc_sps = K.spssmag * sqrtf(prr);
+        const float div_u = gxx + gyy + gzz;
+        const float sps_k = (2.0f / 3.0f) * visc_sps * div_u;
+        const float sps_blin = K.spsblin * prr;
+        const float sumsps = -(sps_k + sps_blin);
+        const float twovisc_sps = visc_sps + visc_sps;
+        const float one_rho2 = 1.0f / p.vr.w;
+        taunew[2 * p1] = make_float4(one_rho2 * (twovisc_sps * gxx + sumsps), one_rho2 * (visc_sps * gxy),
+                                     one_rho2 * (visc_sps * gxz), one_rho2 * (twovisc_sps * gyy + sumsps));
+        taunew[2 * p1 + 1] = make_float4(one_rho2 * (visc_sps * gyz), one_rho2 * (twovisc_sps * gzz + sumsps), 0.f,
+                                         0.f);
       }
     }
   }
@@ -601,10 +586,10 @@ void launch_fluid_ext(hipStream_t stm, unsigned nblocks, DevScalars* sc, const u
   // CellMode: cells of 2h (S = 1) or of h (S = 2)
 #define SPH_EXT(TV, TD, SH, FT)                                                                                  \
   if (K.scelldiv == 2)                                                                                           \
-    hipLaunchKernelGGL((k_fluid_ext<TV, TD, SH, FT, 2>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, E,     \
+    hipLaunchKernelGGL((k_fluid_ext<TV, TD, SH, FT, 2>), dim3(fit_grid((const void*)&k_fluid_ext<TV, TD, SH, FT, 2>, nblocks)), dim3(TB), 0, stm, sc, items, qctr, E,     \
                        begincell, g, K, arace, shiftpos, taunew, int(shiftstore));                               \
   else                                                                                                           \
-    hipLaunchKernelGGL((k_fluid_ext<TV, TD, SH, FT, 1>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, E,     \
+    hipLaunchKernelGGL((k_fluid_ext<TV, TD, SH, FT, 1>), dim3(fit_grid((const void*)&k_fluid_ext<TV, TD, SH, FT, 1>, nblocks)), dim3(TB), 0, stm, sc, items, qctr, E,     \
                        begincell, g, K, arace, shiftpos, taunew, int(shiftstore))
 #define SPH_EXT_TD(TV, SH, FT)             \
   switch (K.tdensity) {                    \

@@ -21,7 +21,10 @@
 //    IEEE division/sqrt/pow expansions; Wendland fac rewritten without the 1/rad
 //    (fac = bwen*q*(1-q/2)^3/rad = (bwen/h)*(1-q/2)^3).  Rounding-level differences
 //    only; parity tests hold it to the reference's noise floor.
+#include <algorithm>
 #include <cfloat>
+#include <cstdio>
+#include <vector>
 
 #include "sph_items.hpp"
 #include "sph_tiled.hpp"
@@ -701,8 +704,15 @@ __device__ __forceinline__ TAcc pass_s(const KConst& K, const DivGrid& g, const 
                                              dstop0);
 }
 
+#ifdef SPH_TAIL_DIAG
+// Diagnostic builds only: every block's start / end time (100 MHz clock) and item count of
+// the last launch, for the launch-tail analysis (tail_report).
+__device__ unsigned long long g_tail[2 * 8192];
+__device__ unsigned g_tail_items[8192];
+#endif
+
 template <int TDENSITY, bool FT = false, int S = 1>
-__global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_fluid_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
                                                     unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
                                                     const float4* __restrict__ velrhop,
                                                     const float* __restrict__ press,
@@ -719,119 +729,105 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
   __shared__ unsigned s_item;
   __shared__ unsigned char s_perm[TB];  // lane -> p1 of the item (see lane_order)
   __shared__ unsigned s_nwave[4];
-  const ItemGroups IG(qctr);
-  const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f;
+#ifdef SPH_TAIL_DIAG
+  const unsigned long long t_start = wall_clock64();
+  unsigned nit = 0;
+#endif
   // Visco of the step: ViscoTime's value (device-resident, k_dt) or the case's
   const float visco = K.visco_n ? sc->visco : K.visco, viscob = K.visco_n ? visco * K.viscobf : K.viscobound;
   const float cvisc_f = -visco * K.cs0f * K.kernelh * K.massfluid;
   const float cvisc_b = -viscob * K.cs0f * K.kernelh * K.massbound;
 
-  for (unsigned q = 0; q < 8; q++) {
-    const unsigned xg = (grp + q) & 7;
-    const ItemGroup gr = IG.group(xg);
-    // the group's first nst items go one to each of its own blocks without an atomic (all
-    // blocks claiming at once queued ~256 same-line atomics per counter); the counter deals
-    // the rest
-    const unsigned nst = (gridDim.x - xg + 7u) / 8u;
-    bool first = q == 0;
-    for (;;) {
-      // a group known to be exhausted (counters only grow; a stale read is smaller) costs
-      // no atomic: probing all 8 queues was ~16k same-line atomics per launch
-      if (threadIdx.x == 0)
-        s_item = first ? (blockIdx.x >> 3)
-                 : (nst + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gr.n)
-                     ? gr.n
-                     : nst + atomicAdd(&qctr[xg * QSTRIDE], 1u);
-      first = false;
-      __syncthreads();
-      const unsigned c = s_item;
-      __syncthreads();
-      if (c >= gr.n) break;
-      const unsigned it = gr.item(c);
-      const uint4 item = items[it];
-      const bool bitem = (item.x & ITEM_BOUND) != 0u;
-      const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
-      const int a = int(item.y & 0xffffu), b = int(item.y >> 16);
-      const int xo = (a + b + 1) >> 1;
-      const int xa = max(a - S, 0), xb = min(b + S, g.ncx - 1);
-      if (bitem) {
-        // Bound item: nothing to compute unless a fluid cell is in its neighbourhood;
-        // then its particles get ar = 0 (PreInteraction's reset).
-        bool any = false;
-        for (int z = max(cz - S, 0); z <= min(cz + S, g.ncz - 1); z++)
-          for (int y = max(cy - S, 0); y <= min(cy + S, g.ncy - 1); y++) {
-            const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
-            any |= bc[rowbase + xa] != bc[rowbase + xb + 1];
-          }
-        if (!any) {
-          for (unsigned p1 = item.z + threadIdx.x; p1 < item.w; p1 += TB) arace[p1] = make_float4(0.f, 0.f, 0.f, 0.f);
-          continue;
+  ItemCursor<false> cur(qctr);
+  for (;;) {
+    const unsigned it = cur.next(&s_item);
+    if (it == ITEM_NONE) break;
+#ifdef SPH_TAIL_DIAG
+    nit++;
+#endif
+    const uint4 item = items[it];
+    const bool bitem = (item.x & ITEM_BOUND) != 0u;
+    const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
+    const int a = int(item.y & 0xffffu), b = int(item.y >> 16);
+    const int xo = (a + b + 1) >> 1;
+    const int xa = max(a - S, 0), xb = min(b + S, g.ncx - 1);
+    if (bitem) {
+      // Bound item: nothing to compute unless a fluid cell is in its neighbourhood;
+      // then its particles get ar = 0 (PreInteraction's reset).
+      bool any = false;
+      for (int z = max(cz - S, 0); z <= min(cz + S, g.ncz - 1); z++)
+        for (int y = max(cy - S, 0); y <= min(cy + S, g.ncy - 1); y++) {
+          const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+          any |= bc[rowbase + xa] != bc[rowbase + xb + 1];
         }
+      if (!any) {
+        for (unsigned p1 = item.z + threadIdx.x; p1 < item.w; p1 += TB) arace[p1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        continue;
       }
-      {  // items hold <= TB particles: one p1 per lane
-        const unsigned p1 = item.z + lane_order(poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
-        const bool act = threadIdx.x < item.w - item.z;
-        P1 p;
-        int cx1 = a;
-        if (act) {
-          const float4 pc1 = poscell[p1];
-          cx1 = int(DcelCellx(K.domcellcode, __float_as_uint(pc1.w)));
-          p.x = pc1.x + float(cx1 - xo) * K.scell;
-          p.y = pc1.y;
-          p.z = pc1.z;
-          p.vr = velrhop[p1];
-          p.press = bitem ? 0.f : press[p1];
-        } else {
-          p.x = p.y = p.z = 1e30f;  // never within the support radius
-          p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
-          p.press = 0.f;
-        }
-        p.inv_rho = frcp(p.vr.w);
-        const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
-        const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
-        const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act, p1};
-        // pass 0: fluid p2 (fluid p1: momentum/continuity/DDT; bound p1: continuity),
-        // pass 1: bound p2 of fluid p1.  Each pass holds only its own accumulator.
-        TAcc f, bnd = {0, 0, 0, 0, 0, 0, false};
-        if (bitem) {
-          f = pass_s<TDENSITY, 2, FT, S>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell,
-                                         velrhop, press, sA, sB, sC, ft);
-        } else {
-          // a floating p1 gets no DDT (JSphCpu.cpp:659-662)
-          const bool ftp1 = FT && act && CodeType(ft.code[p1]) == CODE_TYPE_FLOATING;
-          f = pass_s<TDENSITY, 0, FT, S>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell,
+    }
+    {  // items hold <= TB particles: one p1 per lane
+      const unsigned p1 = item.z + lane_order(poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
+      const bool act = threadIdx.x < item.w - item.z;
+      P1 p;
+      int cx1 = a;
+      if (act) {
+        const float4 pc1 = poscell[p1];
+        cx1 = int(DcelCellx(K.domcellcode, __float_as_uint(pc1.w)));
+        p.x = pc1.x + float(cx1 - xo) * K.scell;
+        p.y = pc1.y;
+        p.z = pc1.z;
+        p.vr = velrhop[p1];
+        p.press = bitem ? 0.f : press[p1];
+      } else {
+        p.x = p.y = p.z = 1e30f;  // never within the support radius
+        p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
+        p.press = 0.f;
+      }
+      p.inv_rho = frcp(p.vr.w);
+      const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
+      const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
+      const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act, p1};
+      // pass 0: fluid p2 (fluid p1: momentum/continuity/DDT; bound p1: continuity),
+      // pass 1: bound p2 of fluid p1.  Each pass holds only its own accumulator.
+      TAcc f, bnd = {0, 0, 0, 0, 0, 0, false};
+      if (bitem) {
+        f = pass_s<TDENSITY, 2, FT, S>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell,
+                                       velrhop, press, sA, sB, sC, ft);
+      } else {
+        // a floating p1 gets no DDT (JSphCpu.cpp:659-662)
+        const bool ftp1 = FT && act && CodeType(ft.code[p1]) == CODE_TYPE_FLOATING;
+        f = pass_s<TDENSITY, 0, FT, S>(K, g, rc, p, thr, pass_k(K, cvisc_f, K.massfluid, p.vr.w), bc, poscell,
+                                       velrhop, press, sA, sB, sC, ft, ftp1);
+        bnd = pass_s<TDENSITY, 1, FT, S>(K, g, rc, p, thr, pass_k(K, cvisc_b, K.massbound, p.vr.w), bc, poscell,
                                          velrhop, press, sA, sB, sC, ft, ftp1);
-          bnd = pass_s<TDENSITY, 1, FT, S>(K, g, rc, p, thr, pass_k(K, cvisc_b, K.massbound, p.vr.w), bc, poscell,
-                                           velrhop, press, sA, sB, sC, ft, ftp1);
+      }
+      if (act && bitem) {
+        // InteractionForcesBound store (JSphCpu.cpp:617-621) onto the reset ar = 0.
+        arace[p1] = make_float4(0.f, 0.f, 0.f, (f.ar != 0.f || f.visc != 0.f) ? 0.f + f.ar : 0.f);
+        viscmax = fmaxf(viscmax, f.visc);
+      } else if (act) {
+        // Combine exactly as the two CPU passes store (JSphCpu.cpp:800-818).
+        float ar = 0.f, ax = 0.f, ay = 0.f, az = 0.f, delta = 0.f;
+        if (f.ar != 0.f || f.ax != 0.f || f.ay != 0.f || f.az != 0.f || f.visc != 0.f) {
+          if (TD) delta = (f.delta == FLT_MAX ? FLT_MAX : 0.f + f.delta);
+          ar = f.ar;
+          ax = f.ax;
+          ay = f.ay;
+          az = f.az;
         }
-        if (act && bitem) {
-          // InteractionForcesBound store (JSphCpu.cpp:617-621) onto the reset ar = 0.
-          arace[p1] = make_float4(0.f, 0.f, 0.f, (f.ar != 0.f || f.visc != 0.f) ? 0.f + f.ar : 0.f);
-          viscmax = fmaxf(viscmax, f.visc);
-        } else if (act) {
-          // Combine exactly as the two CPU passes store (JSphCpu.cpp:800-818).
-          float ar = 0.f, ax = 0.f, ay = 0.f, az = 0.f, delta = 0.f;
-          if (f.ar != 0.f || f.ax != 0.f || f.ay != 0.f || f.az != 0.f || f.visc != 0.f) {
-            if (TD) delta = (f.delta == FLT_MAX ? FLT_MAX : 0.f + f.delta);
-            ar = f.ar;
-            ax = f.ax;
-            ay = f.ay;
-            az = f.az;
-          }
-          if (bnd.ar != 0.f || bnd.ax != 0.f || bnd.ay != 0.f || bnd.az != 0.f || bnd.visc != 0.f) {
-            if (TD) delta = (delta == FLT_MAX || bnd.delta == FLT_MAX ? FLT_MAX : delta + bnd.delta);
-            ar += bnd.ar;
-            ax += bnd.ax;
-            ay += bnd.ay;
-            az += bnd.az;
-          }
-          if (TD && delta != FLT_MAX) ar += delta;
-          if (K.sim2d) ay = 0.f;  // Simulate2D: Acec[].y = 0 (JSphCpuSingle.cpp:544-549)
-          arace[p1] = make_float4(ax, ay, az, ar);
-          viscmax = fmaxf(viscmax, fmaxf(f.visc, bnd.visc));
-          ace2max = fmaxf(ace2max, ax * ax + ay * ay + az * az);
+        if (bnd.ar != 0.f || bnd.ax != 0.f || bnd.ay != 0.f || bnd.az != 0.f || bnd.visc != 0.f) {
+          if (TD) delta = (delta == FLT_MAX || bnd.delta == FLT_MAX ? FLT_MAX : delta + bnd.delta);
+          ar += bnd.ar;
+          ax += bnd.ax;
+          ay += bnd.ay;
+          az += bnd.az;
         }
+        if (TD && delta != FLT_MAX) ar += delta;
+        if (K.sim2d) ay = 0.f;  // Simulate2D: Acec[].y = 0 (JSphCpuSingle.cpp:544-549)
+        arace[p1] = make_float4(ax, ay, az, ar);
+        viscmax = fmaxf(viscmax, fmaxf(f.visc, bnd.visc));
+        ace2max = fmaxf(ace2max, ax * ax + ay * ay + az * az);
       }
     }
   }
@@ -839,7 +835,50 @@ __global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc,
   wave_max_atomic(sc, RED_ACEMAX2, ace2max);
   // (the queue counters are zeroed by k_items_place, or by the solver before an interaction
   // without a new item list)
+#ifdef SPH_TAIL_DIAG
+  if (threadIdx.x == 0 && blockIdx.x < 8192u) {
+    g_tail[2 * blockIdx.x] = t_start;
+    g_tail[2 * blockIdx.x + 1] = wall_clock64();
+    g_tail_items[blockIdx.x] = nit;
+  }
+#endif
 }
+
+#ifdef SPH_TAIL_DIAG
+// The last launch's block timeline: launch span, idle share of the block slots (start ramp +
+// tail), and the spread of the blocks' end times (stderr, one line per launch).
+static void tail_report(hipStream_t stm, unsigned nblocks) {
+  static int calls = 0;
+  if (++calls % 4 != 0) return;  // every 4th launch
+  const unsigned n = std::min(nblocks, 8192u);
+  std::vector<unsigned long long> t(2 * size_t(n));
+  std::vector<unsigned> it(n);
+  (void)hipStreamSynchronize(stm);
+  (void)hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_tail), sizeof(unsigned long long) * 2 * n);
+  (void)hipMemcpyFromSymbol(it.data(), HIP_SYMBOL(g_tail_items), sizeof(unsigned) * n);
+  unsigned long long s0 = ~0ull, e1 = 0, busy = 0;
+  std::vector<double> ends(n);
+  for (unsigned b = 0; b < n; b++) {
+    s0 = std::min(s0, t[2 * b]);
+    e1 = std::max(e1, t[2 * b + 1]);
+    busy += t[2 * b + 1] - t[2 * b];
+  }
+  std::vector<double> starts(n);
+  for (unsigned b = 0; b < n; b++) ends[b] = 0.01 * double(t[2 * b + 1] - s0);  // us
+  for (unsigned b = 0; b < n; b++) starts[b] = 0.01 * double(t[2 * b] - s0);
+  std::sort(ends.begin(), ends.end());
+  std::sort(starts.begin(), starts.end());
+  unsigned late = 0;  // blocks that started after the first block ended
+  for (unsigned b = 0; b < n; b++) late += starts[b] > ends[0];
+  fprintf(stderr, "TAILS start_p50 %.1f p75 %.1f p90 %.1f max %.1f late %u\n", starts[n / 2], starts[(3 * n) / 4],
+          starts[(9 * n) / 10], starts[n - 1], late);
+  const double span = 0.01 * double(e1 - s0);
+  const unsigned imin = *std::min_element(it.begin(), it.end()), imax = *std::max_element(it.begin(), it.end());
+  fprintf(stderr, "TAIL blocks %u span_us %.1f idle %.4f end_p10 %.1f p50 %.1f p90 %.1f first %.1f items %u-%u\n", n,
+          span, 1.0 - double(busy) * 0.01 / (double(n) * span), ends[n / 10], ends[n / 2], ends[(9 * n) / 10], ends[0],
+          imin, imax);
+}
+#endif
 
 template <int S>
 static void launch_fluid_tiled_s(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items,
@@ -847,7 +886,8 @@ static void launch_fluid_tiled_s(hipStream_t stm, unsigned nblocks, DevScalars* 
                                  const unsigned* begincell, DivGrid g, const KConst& K, float4* arace,
                                  const FtRec& ft) {
 #define SPH_TILED(TD, FTB)                                                                                    \
-  hipLaunchKernelGGL((k_fluid_tiled<TD, FTB, S>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell,   \
+  hipLaunchKernelGGL((k_fluid_tiled<TD, FTB, S>), dim3(fit_grid((const void*)&k_fluid_tiled<TD, FTB, S>, nblocks)), \
+                     dim3(TB), 0, stm, sc, items, qctr, poscell,                                                \
                      velrhop, press, begincell, g, K, arace, ft)
   // DDT 2/3 with the binomial series of the hydrostatic term (K.ddtseries) as TDENSITY | 8
   // and the Cubic spline kernel as TDENSITY | 16
@@ -894,6 +934,9 @@ void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const
     launch_fluid_tiled_s<2>(stm, nblocks, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft);
   else
     launch_fluid_tiled_s<1>(stm, nblocks, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft);
+#ifdef SPH_TAIL_DIAG
+  tail_report(stm, nblocks);
+#endif
 }
 
 }  // namespace sphx

@@ -238,8 +238,9 @@ __device__ __forceinline__ void items_place_block(const ItemBuild& b, unsigned c
     const unsigned m1 = m0 + block_sum(p1, s_w);
     const unsigned m2 = m1 + block_sum(p2, s_w);
     const unsigned m3 = m2 + block_sum(p3, s_w);
-    if (threadIdx.x < 8 * QCTR_COPIES) {
-      const unsigned q = (threadIdx.x >> 3) * QCTR_WORDS + (threadIdx.x & 7) * QSTRIDE;
+    if (threadIdx.x < 16 * QCTR_COPIES) {  // the fluid and bound queues of the 8 groups
+      const unsigned k = threadIdx.x & 15;
+      const unsigned q = (threadIdx.x >> 4) * QCTR_WORDS + (k < 8 ? k : QCTR_BQ + k - 8) * QSTRIDE;
       b.qa[q] = 0u;
       if (nl == 2) b.qb[q] = 0u;
     }

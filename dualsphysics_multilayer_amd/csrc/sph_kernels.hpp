@@ -209,14 +209,16 @@ void launch_interaction(hipStream_t stm, unsigned cap, DevScalars* sc, const flo
 void launch_interaction_bound(hipStream_t stm, unsigned npbcap, DevScalars* sc, const float4* poscell,
                               const float4* velrhop, const unsigned* begincell, DivGrid g, const KConst& K,
                               float4* arace);
-// Work counters of the persistent tiled kernels (qctr): 8 per-XCD item queues + the
-// finished-block count, each on its own 128-B line (device-scope atomics serialize per line).
+// Work counters of the persistent tiled kernels (qctr): per XCD group g an item queue of its
+// fluid-row items (line g) and one of its bound-row items (line QCTR_BQ + g), each on its own
+// 128-B line (device-scope atomics serialize per line; line 8 is unused).
 constexpr int QSTRIDE = 32;
-// Line 9 holds the list's item counts {all, bound, first item} (k_items_place; ItemGroups
-// reads them), so one counter block describes one item list.
-constexpr size_t QCTR_QUEUE_BYTES = 9 * QSTRIDE * sizeof(unsigned);  // what a re-run zeroes
-constexpr int QCTR_WORDS = 10 * QSTRIDE;
-constexpr int QCTR_NITEMS = 9 * QSTRIDE;
+constexpr int QCTR_BQ = 9;
+// Line 17 holds the list's item counts {all, bound, first item, chunk log2} (k_items_place;
+// ItemGroups reads them), so one counter block describes one item list.
+constexpr size_t QCTR_QUEUE_BYTES = 17 * QSTRIDE * sizeof(unsigned);  // what a re-run zeroes
+constexpr int QCTR_WORDS = 18 * QSTRIDE;
+constexpr int QCTR_NITEMS = 17 * QSTRIDE;
 // A list's counter blocks come in QCTR_COPIES copies (QCTR_WORDS apart), all set up by the
 // item build, so that the interactions on one item list (NN's force and viscous passes; an
 // interaction without a divide before it, e.g. sph_download_interaction) each start on

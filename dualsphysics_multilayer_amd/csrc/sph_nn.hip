@@ -698,166 +698,145 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
   if (FT && threadIdx.x < SPH_MAXPHASES)
     sph[3 * SPH_MAXPHASES + threadIdx.x] =
         make_float4(threadIdx.x < unsigned(K.nftbodies) ? ftmassp[threadIdx.x] : 0.f, 0.f, 0.f, 0.f);
-  const ItemGroups IG(qctr);
-  const unsigned grp = blockIdx.x & 7;
   float viscmax = 0.f, ace2max = 0.f, etamax = 0.f;
-  for (unsigned q = 0; q < 8; q++) {
-    const unsigned xg = (grp + q) & 7;
-    const ItemGroup gr = IG.group(xg);
-    // the group's first nst items go one to each of its own blocks without an atomic (all
-    // blocks claiming at once queued ~256 same-line atomics per counter); the counter deals
-    // the rest
-    const unsigned nst = (gridDim.x - xg + 7u) / 8u;
-    bool first = q == 0;
-    for (;;) {
-      // a group known to be exhausted (counters only grow; a stale read is smaller) costs
-      // no atomic: probing all 8 queues was ~16k same-line atomics per launch
-      if (threadIdx.x == 0)
-        s_item = first ? (blockIdx.x >> 3)
-                 : (nst + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gr.n)
-                     ? gr.n
-                     : nst + atomicAdd(&qctr[xg * QSTRIDE], 1u);
-      first = false;
-      __syncthreads();
-      const unsigned c = s_item;
-      __syncthreads();
-      if (c >= gr.n) break;
-      const unsigned it = gr.item(c);
-      const uint4 item = items[it];
-      const bool bitem = (item.x & ITEM_BOUND) != 0u;
-      const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
-      const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);
-      const int xo = (ia + ib + 1) >> 1;
-      const int xa = max(ia - S, 0), xb = min(ib + S, g.ncx - 1);
-      if (bitem) {  // no fluid within reach: ar = 0 (PreInteraction reset), nothing else
-        bool any = false;
-        for (int z = max(cz - S, 0); z <= min(cz + S, g.ncz - 1); z++)
-          for (int y = max(cy - S, 0); y <= min(cy + S, g.ncy - 1); y++) {
-            const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
-            any |= bc[rowbase + xa] != bc[rowbase + xb + 1];
-          }
-        if (!any) {
-          for (unsigned p1 = item.z + threadIdx.x; p1 < item.w; p1 += TB) arace[p1] = make_float4(0.f, 0.f, 0.f, 0.f);
-          continue;
+  ItemCursor<false> cur(qctr);
+  for (;;) {
+    const unsigned it = cur.next(&s_item);
+    if (it == ITEM_NONE) break;
+    const uint4 item = items[it];
+    const bool bitem = (item.x & ITEM_BOUND) != 0u;
+    const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
+    const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);
+    const int xo = (ia + ib + 1) >> 1;
+    const int xa = max(ia - S, 0), xb = min(ib + S, g.ncx - 1);
+    if (bitem) {  // no fluid within reach: ar = 0 (PreInteraction reset), nothing else
+      bool any = false;
+      for (int z = max(cz - S, 0); z <= min(cz + S, g.ncz - 1); z++)
+        for (int y = max(cy - S, 0); y <= min(cy + S, g.ncy - 1); y++) {
+          const unsigned rowbase = g.boxfluid + unsigned(z) * g.nsheet + unsigned(y) * unsigned(g.ncx);
+          any |= bc[rowbase + xa] != bc[rowbase + xb + 1];
         }
-      }
-      const unsigned p1 = item.z + lane_order(poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
-      const bool act = threadIdx.x < item.w - item.z;
-      NNP1 p;
-      int cx1 = ia;
-      if (act) {
-        const float4 pc1 = poscell[p1];
-        cx1 = int(DcelCellx(K.domcellcode, __float_as_uint(pc1.w)));
-        p.x = pc1.x + float(cx1 - xo) * K.scell;
-        p.y = pc1.y;
-        p.z = pc1.z;
-        p.vr = velrhop[p1];
-        p.press = press[p1];
-        // a floating p1's code value is its body index, which the reference uses as its phase
-        p.ph = bitem ? 0 : int(code[p1] & CODE_MASKVALUE);
-      } else {
-        p.x = p.y = p.z = 1e30f;
-        p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
-        p.press = 0.f;
-        p.ph = 0;
-      }
-      p.inv_rho = frcp(p.vr.w);
-      p.mph = sph[2 * p.ph].x;
-      p.taumax = sph[2 * p.ph + 1].z;
-      p.bimulti = sph[2 * p.ph + 1].w;
-      const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
-      const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
-      const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act, p1};
-      if (bitem) {
-        NNAcc f = {};
-        nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 2, S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
-                                                     sph, f);
-        if (act) {
-          arace[p1] = make_float4(0.f, 0.f, 0.f, (f.ar != 0.f || f.visc != 0.f) ? 0.f + f.ar : 0.f);
-          viscmax = fmaxf(viscmax, f.visc);
-        }
+      if (!any) {
+        for (unsigned p1 = item.z + threadIdx.x; p1 < item.w; p1 += TB) arace[p1] = make_float4(0.f, 0.f, 0.f, 0.f);
         continue;
       }
-      // fluid p1: the fluid pass, then the bound pass; the shifting sums carry over
-      // (shiftposfs[p1] is stored by the first pass and loaded by the second)
-      NNAcc f = {}, b = {};
-      // a floating p1 gets no DDT and no shifting (JSphCpu_NN_FDA.cpp:159-164)
-      const bool ftp1 = FT && act && CodeType(code[p1]) == CODE_TYPE_FLOATING;
-      if (ftp1) {
-        if (TDENSITY) f.delta = FLT_MAX;
-        if (SHIFT) {
-          f.sx = FLT_MAX;
-          f.ftsx = true;
-        }
-      }
-      nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 0, S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB,
-                                                       sC, sph, f);
-      if (SHIFT && __syncthreads_or(int(f.hv)))
-        f.sx = nn_sx_sweep<S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f.hv, f.sx);
-      if (FT && f.ftsx) f.sx = FLT_MAX;  // x stays FLT_MAX once set (no reset after it)
-      b.sx = f.sx;
-      b.sy = f.sy;
-      b.sz = f.sz;
-      b.sw = f.sw;
-      if (FT) {  // the bound-row call starts over for a floating p1 too (deltap1, shiftposfsp1.x)
-        b.ftsx = f.ftsx;
-        if (ftp1 && TDENSITY) b.delta = FLT_MAX;
-      }
-      // the first no-shift bound pair (ShiftMode NoBound/NoFixed) freezes every shifting sum:
-      // only then is the bound pass order-dependent (uniform branch)
-      if (SHIFT && (K.shiftmode == 1 || K.shiftmode == 2))
-        nn_pass<TVISCO, TDENSITY, SHIFT, 1, S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, b);
-      else
-        nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 1, S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
-                                                     sph, b);
-      if (FT && b.ftsx) b.sx = FLT_MAX;
-      f.ar *= p.vr.w;  // the continuity sums' common rho1 (nn_pair)
-      b.ar *= p.vr.w;
+    }
+    const unsigned p1 = item.z + lane_order(poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
+    const bool act = threadIdx.x < item.w - item.z;
+    NNP1 p;
+    int cx1 = ia;
+    if (act) {
+      const float4 pc1 = poscell[p1];
+      cx1 = int(DcelCellx(K.domcellcode, __float_as_uint(pc1.w)));
+      p.x = pc1.x + float(cx1 - xo) * K.scell;
+      p.y = pc1.y;
+      p.z = pc1.z;
+      p.vr = velrhop[p1];
+      p.press = press[p1];
+      // a floating p1's code value is its body index, which the reference uses as its phase
+      p.ph = bitem ? 0 : int(code[p1] & CODE_MASKVALUE);
+    } else {
+      p.x = p.y = p.z = 1e30f;
+      p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
+      p.press = 0.f;
+      p.ph = 0;
+    }
+    p.inv_rho = frcp(p.vr.w);
+    p.mph = sph[2 * p.ph].x;
+    p.taumax = sph[2 * p.ph + 1].z;
+    p.bimulti = sph[2 * p.ph + 1].w;
+    const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
+    const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
+    const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act, p1};
+    if (bitem) {
+      NNAcc f = {};
+      nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 2, S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
+                                                   sph, f);
       if (act) {
-        // the two CPU passes' stores (JSphCpu_NN_FDA.cpp:278-296).  With shifting configured
-        // the reference instantiates every interaction with shift=true (the predictor's too,
-        // whose sums ComputeSymplecticPre then ignores), so both passes always store.
-        const bool store = SHIFT || K.shiftmode != 0;
-        float ar = 0.f, ax = 0.f, ay = 0.f, az = 0.f, delta = 0.f;
-        if (store || f.ar != 0.f || f.ax != 0.f || f.ay != 0.f || f.az != 0.f || f.visc != 0.f) {
-          if (TDENSITY) delta = (f.delta == FLT_MAX ? FLT_MAX : 0.f + f.delta);
-          ar = f.ar;
-          ax = f.ax;
-          ay = f.ay;
-          az = f.az;
-        }
-        if (store || b.ar != 0.f || b.ax != 0.f || b.ay != 0.f || b.az != 0.f || b.visc != 0.f) {
-          if (TDENSITY) delta = (delta == FLT_MAX || b.delta == FLT_MAX ? FLT_MAX : delta + b.delta);
-          ar += b.ar;
-          ax += b.ax;
-          ay += b.ay;
-          az += b.az;
-        }
-        if (TDENSITY && delta != FLT_MAX) ar += delta;
-        if (K.sim2d) ay = 0.f;  // Simulate2D: Acec[].y = 0 (JSphCpuSingle.cpp:614-620)
-        arace[p1] = make_float4(ax, ay, az, ar);
-        if (SHIFT) shiftpos[p1] = make_float4(b.sx, b.sy, b.sz, b.sw);
-        viscmax = fmaxf(viscmax, fmaxf(f.visc, b.visc));
-        etamax = fmaxf(etamax, fmaxf(f.visceta, b.visceta));
-        // SPH gradients: the viscous force and so AceMax come from the second pass (k_nn_visc)
-        if (TVISCO != NN_SPH_GRAD && TVISCO != NN_SPH_ART) ace2max = fmaxf(ace2max, ax * ax + ay * ay + az * az);
-        if constexpr (TVISCO == NN_SPH_GRAD) {
-          // gradvel[p1] += fluid sums, += bound sums (JSphCpu_NN_SPH.cpp:608-615), then
-          // _Visco_eta (strain rate tensor + effective viscosity of p1's phase, :171-222)
-          // and for ConstEq _Visco_Stress_tensor (tau = 2 eta D, :128-166)
-          const float gxx = f.gxx + b.gxx, gxy = f.gxy + b.gxy, gxz = f.gxz + b.gxz;
-          const float gyy = f.gyy + b.gyy, gyz = f.gyz + b.gyz, gzz = f.gzz + b.gzz;
-          float d[6];
-          const float dmag = nn_strain_rate(gxx, gxy, gxz, gyy, gyz, gzz, d);
-          const float4 pa = sph[2 * p.ph], pc = sph[2 * SPH_MAXPHASES + p.ph];
-          const float eta = nn_eta(K.nnbi != 0, dmag, pa.w, pa.z, pc, p.taumax, p.bimulti);
-          viscoeta[p1] = eta;
-          etamax = fmaxf(etamax, eta);
-          if (K.nntvisco == 3) {
-            const float e2 = 2.f * eta;
-            tau[2 * p1] = make_float4(e2 * d[0], e2 * d[1], e2 * d[2], e2 * d[3]);
-            tau[2 * p1 + 1] = make_float4(e2 * d[4], e2 * d[5], 0.f, 0.f);
-          }
+        arace[p1] = make_float4(0.f, 0.f, 0.f, (f.ar != 0.f || f.visc != 0.f) ? 0.f + f.ar : 0.f);
+        viscmax = fmaxf(viscmax, f.visc);
+      }
+      continue;
+    }
+    // fluid p1: the fluid pass, then the bound pass; the shifting sums carry over
+    // (shiftposfs[p1] is stored by the first pass and loaded by the second)
+    NNAcc f = {}, b = {};
+    // a floating p1 gets no DDT and no shifting (JSphCpu_NN_FDA.cpp:159-164)
+    const bool ftp1 = FT && act && CodeType(code[p1]) == CODE_TYPE_FLOATING;
+    if (ftp1) {
+      if (TDENSITY) f.delta = FLT_MAX;
+      if (SHIFT) {
+        f.sx = FLT_MAX;
+        f.ftsx = true;
+      }
+    }
+    nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 0, S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB,
+                                                     sC, sph, f);
+    if (SHIFT && __syncthreads_or(int(f.hv)))
+      f.sx = nn_sx_sweep<S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f.hv, f.sx);
+    if (FT && f.ftsx) f.sx = FLT_MAX;  // x stays FLT_MAX once set (no reset after it)
+    b.sx = f.sx;
+    b.sy = f.sy;
+    b.sz = f.sz;
+    b.sw = f.sw;
+    if (FT) {  // the bound-row call starts over for a floating p1 too (deltap1, shiftposfsp1.x)
+      b.ftsx = f.ftsx;
+      if (ftp1 && TDENSITY) b.delta = FLT_MAX;
+    }
+    // the first no-shift bound pair (ShiftMode NoBound/NoFixed) freezes every shifting sum:
+    // only then is the bound pass order-dependent (uniform branch)
+    if (SHIFT && (K.shiftmode == 1 || K.shiftmode == 2))
+      nn_pass<TVISCO, TDENSITY, SHIFT, 1, S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, b);
+    else
+      nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 1, S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC,
+                                                   sph, b);
+    if (FT && b.ftsx) b.sx = FLT_MAX;
+    f.ar *= p.vr.w;  // the continuity sums' common rho1 (nn_pair)
+    b.ar *= p.vr.w;
+    if (act) {
+      // the two CPU passes' stores (JSphCpu_NN_FDA.cpp:278-296).  With shifting configured
+      // the reference instantiates every interaction with shift=true (the predictor's too,
+      // whose sums ComputeSymplecticPre then ignores), so both passes always store.
+      const bool store = SHIFT || K.shiftmode != 0;
+      float ar = 0.f, ax = 0.f, ay = 0.f, az = 0.f, delta = 0.f;
+      if (store || f.ar != 0.f || f.ax != 0.f || f.ay != 0.f || f.az != 0.f || f.visc != 0.f) {
+        if (TDENSITY) delta = (f.delta == FLT_MAX ? FLT_MAX : 0.f + f.delta);
+        ar = f.ar;
+        ax = f.ax;
+        ay = f.ay;
+        az = f.az;
+      }
+      if (store || b.ar != 0.f || b.ax != 0.f || b.ay != 0.f || b.az != 0.f || b.visc != 0.f) {
+        if (TDENSITY) delta = (delta == FLT_MAX || b.delta == FLT_MAX ? FLT_MAX : delta + b.delta);
+        ar += b.ar;
+        ax += b.ax;
+        ay += b.ay;
+        az += b.az;
+      }
+      if (TDENSITY && delta != FLT_MAX) ar += delta;
+      if (K.sim2d) ay = 0.f;  // Simulate2D: Acec[].y = 0 (JSphCpuSingle.cpp:614-620)
+      arace[p1] = make_float4(ax, ay, az, ar);
+      if (SHIFT) shiftpos[p1] = make_float4(b.sx, b.sy, b.sz, b.sw);
+      viscmax = fmaxf(viscmax, fmaxf(f.visc, b.visc));
+      etamax = fmaxf(etamax, fmaxf(f.visceta, b.visceta));
+      // SPH gradients: the viscous force and so AceMax come from the second pass (k_nn_visc)
+      if (TVISCO != NN_SPH_GRAD && TVISCO != NN_SPH_ART) ace2max = fmaxf(ace2max, ax * ax + ay * ay + az * az);
+      if constexpr (TVISCO == NN_SPH_GRAD) {
+        // gradvel[p1] += fluid sums, += bound sums (JSphCpu_NN_SPH.cpp:608-615), then
+        // _Visco_eta (strain rate tensor + effective viscosity of p1's phase, :171-222)
+        // and for ConstEq _Visco_Stress_tensor (tau = 2 eta D, :128-166)
+        const float gxx = f.gxx + b.gxx, gxy = f.gxy + b.gxy, gxz = f.gxz + b.gxz;
+        const float gyy = f.gyy + b.gyy, gyz = f.gyz + b.gyz, gzz = f.gzz + b.gzz;
+        float d[6];
+        const float dmag = nn_strain_rate(gxx, gxy, gxz, gyy, gyz, gzz, d);
+        const float4 pa = sph[2 * p.ph], pc = sph[2 * SPH_MAXPHASES + p.ph];
+        const float eta = nn_eta(K.nnbi != 0, dmag, pa.w, pa.z, pc, p.taumax, p.bimulti);
+        viscoeta[p1] = eta;
+        etamax = fmaxf(etamax, eta);
+        if (K.nntvisco == 3) {
+          const float e2 = 2.f * eta;
+          tau[2 * p1] = make_float4(e2 * d[0], e2 * d[1], e2 * d[2], e2 * d[3]);
+          tau[2 * p1 + 1] = make_float4(e2 * d[4], e2 * d[5], 0.f, 0.f);
         }
       }
     }
@@ -876,19 +855,19 @@ void launch_nn_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const ui
   // CellMode: cells of 2h (S = 1) or of h (S = 2); floating bodies (FT)
 #define SPH_NN(TV, TD, SH)                                                                                         \
   if (ftmassp && K.scelldiv == 2)                                                                                  \
-    hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH, 2, true>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr,         \
+    hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH, 2, true>), dim3(fit_grid((const void*)&k_nn_tiled<TV, TD, SH, 2, true>, nblocks)), dim3(TB), 0, stm, sc, items, qctr,         \
                        poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,    \
                        ftmassp);                                                                                   \
   else if (ftmassp)                                                                                                \
-    hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH, 1, true>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr,         \
+    hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH, 1, true>), dim3(fit_grid((const void*)&k_nn_tiled<TV, TD, SH, 1, true>, nblocks)), dim3(TB), 0, stm, sc, items, qctr,         \
                        poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,    \
                        ftmassp);                                                                                   \
   else if (K.scelldiv == 2)                                                                                        \
-    hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH, 2, false>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr,        \
+    hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH, 2, false>), dim3(fit_grid((const void*)&k_nn_tiled<TV, TD, SH, 2, false>, nblocks)), dim3(TB), 0, stm, sc, items, qctr,        \
                        poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,    \
                        ftmassp);                                                                                   \
   else                                                                                                             \
-    hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH, 1, false>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr,        \
+    hipLaunchKernelGGL((k_nn_tiled<TV, TD, SH, 1, false>), dim3(fit_grid((const void*)&k_nn_tiled<TV, TD, SH, 1, false>, nblocks)), dim3(TB), 0, stm, sc, items, qctr,        \
                        poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,    \
                        ftmassp)
 #define SPH_NN_TD(TV, SH)          \
@@ -908,10 +887,10 @@ void launch_nn_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const ui
   // diagnostic builds (kernel A/B at cfg5 only): the one instantiation pair of BASELINE cfg5
   if (K.nnvelgrad == 2 || K.nntvisco != 2 || K.tdensity != 3 || ftmassp || K.scelldiv != 1)
     throw std::runtime_error("SPH_NN_DIAG_CFG5 build: cfg5 only");
-  if (shift) hipLaunchKernelGGL((k_nn_tiled<2, 3, true, 1, false>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr,
+  if (shift) hipLaunchKernelGGL((k_nn_tiled<2, 3, true, 1, false>), dim3(fit_grid((const void*)&k_nn_tiled<2, 3, true, 1, false>, nblocks)), dim3(TB), 0, stm, sc, items, qctr,
                                 poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,
                                 ftmassp);
-  else hipLaunchKernelGGL((k_nn_tiled<2, 3, false, 1, false>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr,
+  else hipLaunchKernelGGL((k_nn_tiled<2, 3, false, 1, false>), dim3(fit_grid((const void*)&k_nn_tiled<2, 3, false, 1, false>, nblocks)), dim3(TB), 0, stm, sc, items, qctr,
                           poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,
                           ftmassp);
 #else
@@ -1208,83 +1187,67 @@ __global__ __launch_bounds__(TB) void k_nn_visc(DevScalars* __restrict__ sc, con
   __shared__ unsigned char s_perm[TB];
   __shared__ unsigned s_nwave[4];
   if (threadIdx.x < 2 * SPH_MAXPHASES) sph[threadIdx.x] = phases[threadIdx.x];
-  const ItemGroups IG(qctr);
-  const unsigned grp = blockIdx.x & 7;
   float ace2max = 0.f;
-  for (unsigned q = 0; q < 8; q++) {
-    const unsigned xg = (grp + q) & 7;
-    const ItemGroup gr = IG.group(xg);
-    // fluid items only (a group's fluid items come first in its claim order)
-    const unsigned nst = (gridDim.x - xg + 7u) / 8u;
-    bool first = q == 0;
-    for (;;) {
-      if (threadIdx.x == 0)
-        s_item = first ? (blockIdx.x >> 3)
-                 : (nst + __hip_atomic_load(&qctr[xg * QSTRIDE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gr.nfg)
-                     ? gr.nfg
-                     : nst + atomicAdd(&qctr[xg * QSTRIDE], 1u);
-      first = false;
-      __syncthreads();
-      const unsigned c = s_item;
-      __syncthreads();
-      if (c >= gr.nfg) break;
-      const uint4 item = items[gr.item(c)];
-      const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
-      const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);
-      const int xo = (ia + ib + 1) >> 1;
-      const int xa = max(ia - S, 0), xb = min(ib + S, g.ncx - 1);
-      const unsigned p1 = item.z + lane_order(poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
-      const bool act = threadIdx.x < item.w - item.z;
-      NNVP1 p;
-      int cx1 = ia;
-      p.eta = 0.f;
-      p.ta = p.tb = make_float4(0.f, 0.f, 0.f, 0.f);
-      p.visco = p.cs0 = 0.f;
-      if (act) {
-        const float4 pc1 = poscell[p1];
-        cx1 = int(DcelCellx(K.domcellcode, __float_as_uint(pc1.w)));
-        p.x = pc1.x + float(cx1 - xo) * K.scell;
-        p.y = pc1.y;
-        p.z = pc1.z;
-        p.vr = velrhop[p1];
-        const int ph = int(code[p1] & CODE_MASKVALUE);
-        if constexpr (VM == VM_MORRIS) p.eta = viscoeta[p1];
-        if constexpr (VM == VM_CONSEQ) {
-          p.ta = tau[2 * p1];
-          p.tb = tau[2 * p1 + 1];
-        }
-        if constexpr (VM == VM_ART) {
-          p.visco = sph[2 * ph].z;
-          p.cs0 = sph[2 * ph].y;
-        }
-      } else {
-        p.x = p.y = p.z = 1e30f;
-        p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
+  ItemCursor<true> cur(qctr);
+  for (;;) {
+    const unsigned it = cur.next(&s_item);
+    if (it == ITEM_NONE) break;
+    const uint4 item = items[it];
+    const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
+    const int ia = int(item.y & 0xffffu), ib = int(item.y >> 16);
+    const int xo = (ia + ib + 1) >> 1;
+    const int xa = max(ia - S, 0), xb = min(ib + S, g.ncx - 1);
+    const unsigned p1 = item.z + lane_order(poscell, item.z, item.w - item.z, 0.5f * K.scell, s_perm, s_nwave);
+    const bool act = threadIdx.x < item.w - item.z;
+    NNVP1 p;
+    int cx1 = ia;
+    p.eta = 0.f;
+    p.ta = p.tb = make_float4(0.f, 0.f, 0.f, 0.f);
+    p.visco = p.cs0 = 0.f;
+    if (act) {
+      const float4 pc1 = poscell[p1];
+      cx1 = int(DcelCellx(K.domcellcode, __float_as_uint(pc1.w)));
+      p.x = pc1.x + float(cx1 - xo) * K.scell;
+      p.y = pc1.y;
+      p.z = pc1.z;
+      p.vr = velrhop[p1];
+      const int ph = int(code[p1] & CODE_MASKVALUE);
+      if constexpr (VM == VM_MORRIS) p.eta = viscoeta[p1];
+      if constexpr (VM == VM_CONSEQ) {
+        p.ta = tau[2 * p1];
+        p.tb = tau[2 * p1 + 1];
       }
-      const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
-      const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
-      const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act, p1};
-      const float3 f = nnv_pass<VM, false, S>(K, g, rc, p, thr, bc, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
-                                              sC, ftmassp);
-      const float3 b = nnv_pass<VM, true, S>(K, g, rc, p, thr, bc, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
-                                             sC, ftmassp);
-      if (act) {
-        // ace[p1] = ace[p1] + acep1 per pass when non-zero (JSphCpu_NN_SPH.cpp:442-444)
-        float4 r = arace[p1];
-        if (f.x != 0.f || f.y != 0.f || f.z != 0.f) {
-          r.x += f.x;
-          r.y += f.y;
-          r.z += f.z;
-        }
-        if (b.x != 0.f || b.y != 0.f || b.z != 0.f) {
-          r.x += b.x;
-          r.y += b.y;
-          r.z += b.z;
-        }
-        if (K.sim2d) r.y = 0.f;  // Simulate2D: Acec[].y = 0 after the whole interaction
-        arace[p1] = r;
-        ace2max = nanmax(ace2max, r.x * r.x + r.y * r.y + r.z * r.z);
+      if constexpr (VM == VM_ART) {
+        p.visco = sph[2 * ph].z;
+        p.cs0 = sph[2 * ph].y;
       }
+    } else {
+      p.x = p.y = p.z = 1e30f;
+      p.vr = make_float4(0.f, 0.f, 0.f, 1.f);
+    }
+    const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
+    const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
+    const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act, p1};
+    const float3 f = nnv_pass<VM, false, S>(K, g, rc, p, thr, bc, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
+                                            sC, ftmassp);
+    const float3 b = nnv_pass<VM, true, S>(K, g, rc, p, thr, bc, poscell, velrhop, code, viscoeta, tau, sph, sA, sB,
+                                           sC, ftmassp);
+    if (act) {
+      // ace[p1] = ace[p1] + acep1 per pass when non-zero (JSphCpu_NN_SPH.cpp:442-444)
+      float4 r = arace[p1];
+      if (f.x != 0.f || f.y != 0.f || f.z != 0.f) {
+        r.x += f.x;
+        r.y += f.y;
+        r.z += f.z;
+      }
+      if (b.x != 0.f || b.y != 0.f || b.z != 0.f) {
+        r.x += b.x;
+        r.y += b.y;
+        r.z += b.z;
+      }
+      if (K.sim2d) r.y = 0.f;  // Simulate2D: Acec[].y = 0 after the whole interaction
+      arace[p1] = r;
+      ace2max = nanmax(ace2max, r.x * r.x + r.y * r.y + r.z * r.z);
     }
   }
   wave_max_atomic(sc, RED_ACEMAX2, ace2max);
@@ -1296,10 +1259,10 @@ void launch_nn_visc(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uin
                     float4* arace, const float* ftmassp) {
 #define SPH_NNV(VM)                                                                                             \
   if (K.scelldiv == 2)                                                                                          \
-    hipLaunchKernelGGL((k_nn_visc<VM, 2>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop,   \
+    hipLaunchKernelGGL((k_nn_visc<VM, 2>), dim3(fit_grid((const void*)&k_nn_visc<VM, 2>, nblocks)), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop,   \
                        code, viscoeta, tau, begincell, g, K, phases, arace, ftmassp);                                    \
   else                                                                                                          \
-    hipLaunchKernelGGL((k_nn_visc<VM, 1>), dim3(nblocks), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop,   \
+    hipLaunchKernelGGL((k_nn_visc<VM, 1>), dim3(fit_grid((const void*)&k_nn_visc<VM, 1>, nblocks)), dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop,   \
                        code, viscoeta, tau, begincell, g, K, phases, arace, ftmassp)
   if (K.nntvisco == 1) SPH_NNV(VM_ART);
   else if (K.nntvisco == 2) SPH_NNV(VM_MORRIS);

@@ -4,6 +4,8 @@
 // expanded-form candidate test and the lane order of an item's particles.
 #pragma once
 #include <cfloat>
+#include <mutex>
+#include <unordered_map>
 
 #include "sph_kernels.hpp"
 
@@ -174,32 +176,87 @@ struct ItemDeal {
     return lo + ((g + 8u * (c >> sh)) << sh) + (c & ((1u << sh) - 1u));
   }
 };
-struct ItemGroup {
-  ItemDeal f, b;
-  unsigned g, nfg, n;
-  __device__ __forceinline__ unsigned item(unsigned c) const { return c < nfg ? f.item(g, c) : b.item(g, c - nfg); }
-};
 struct ItemGroups {
-  unsigned nf, nb, lo, sh;
+  ItemDeal f, b;  // the fluid-row and bound-row items
   // the list's counts {all, bound, first item, chunk log2}, written by k_items_place beside
   // the work queues
   __device__ __forceinline__ explicit ItemGroups(const unsigned* qctr) {
     const unsigned n = qctr[QCTR_NITEMS];
-    nb = min(qctr[QCTR_NITEMS + 1], n);
-    nf = n - nb;
-    lo = qctr[QCTR_NITEMS + 2];
-    sh = min(qctr[QCTR_NITEMS + 3], 10u);
-  }
-  __device__ __forceinline__ ItemGroup group(unsigned g) const {
-    ItemGroup r;
-    r.f = {lo, nf, sh};
-    r.b = {lo + nf, nb, sh};
-    r.g = g;
-    r.nfg = r.f.count(g);
-    r.n = r.nfg + r.b.count(g);
-    return r;
+    const unsigned nb = min(qctr[QCTR_NITEMS + 1], n), nf = n - nb, lo = qctr[QCTR_NITEMS + 2];
+    const unsigned sh = min(qctr[QCTR_NITEMS + 3], 10u);
+    f = {lo, nf, sh};
+    b = {lo + nf, nb, sh};
   }
 };
+
+// The items of a block, claimed in two phases: the fluid-row items of its own group g, then
+// of the groups g+1, ..., g+7 (work stealing), and only then the bound-row items in the same
+// group order.  So the fluid work (~100 us per item at cfg2) of the whole launch is claimed
+// before any block takes a bound-row item (mostly cheap: no fluid in reach, or continuity
+// only), and the last items of the launch are bound-row ones wherever they can be.  (One
+// queue per group over [fluid | bound] let a block that had drained its group steal a heavy
+// fluid item late: cfg2 blocks ended over ~60 us, 9 % of the block slots idle.)  A block's
+// first fluid item of its own group is static (no start-up burst of ~256 same-line atomics
+// per counter); a group known to be exhausted costs no atomic (counters only grow).
+// FLUID_ONLY: the bound-row items are not claimed (NN's viscous pass).
+constexpr unsigned ITEM_NONE = 0xffffffffu;
+template <bool FLUID_ONLY = false>
+struct ItemCursor {
+  ItemGroups IG;
+  unsigned* qctr;
+  unsigned grp, ph = 0, q = 0;
+  bool first = true;
+  __device__ __forceinline__ explicit ItemCursor(unsigned* qc) : IG(qc), qctr(qc), grp(blockIdx.x & 7u) {}
+  // the next item of this block (block-uniform; ITEM_NONE at the end).  s_item: LDS word.
+  __device__ __forceinline__ unsigned next(unsigned* s_item) {
+    for (;;) {
+      if (q == 8u) {
+        if (FLUID_ONLY || ph) return ITEM_NONE;
+        ph = 1u;
+        q = 0u;
+      }
+      const unsigned xg = (grp + q) & 7u;
+      const ItemDeal& d = ph ? IG.b : IG.f;
+      const unsigned n = d.count(xg);
+      const unsigned nst = ph ? 0u : (gridDim.x - xg + 7u) / 8u;  // the group's static items
+      unsigned* ctr = &qctr[(ph ? QCTR_BQ + xg : xg) * QSTRIDE];
+      if (threadIdx.x == 0)
+        *s_item = first ? (blockIdx.x >> 3)
+                  : (nst + __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n)
+                      ? n
+                      : nst + atomicAdd(ctr, 1u);
+      first = false;
+      __syncthreads();
+      const unsigned c = *s_item;
+      __syncthreads();
+      if (c < n) return d.item(xg, c);
+      q++;
+    }
+  }
+};
+
+// Grid of a persistent tiled kernel: no more blocks than can be resident at once.  A block
+// that is not resident at the start begins only when a resident one exits — after the queues
+// ran dry — and then still runs its static first item (ItemGroups): at cfg3 (DDT1, 129 VGPRs,
+// 3 waves per SIMD = 6 blocks per CU) 512 of 2048 blocks started 5.7 ms into a 5.8 ms launch,
+// and 26 % of the launch's block slots idled.  The occupancy of each kernel on the current
+// device is looked up once.
+inline unsigned fit_grid(const void* kernel, unsigned want, int threads = TB) {
+  static std::mutex m;
+  static std::unordered_map<unsigned long long, unsigned> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const unsigned long long key = reinterpret_cast<unsigned long long>(kernel) ^ (unsigned long long)(dev) << 56;
+  std::lock_guard<std::mutex> lk(m);
+  auto it = cache.find(key);
+  if (it == cache.end()) {
+    int perc = 0, ncu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perc, kernel, threads, 0) != hipSuccess || perc <= 0) perc = 1;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 1;
+    it = cache.emplace(key, unsigned(perc) * unsigned(ncu)).first;
+  }
+  return want < it->second ? want : it->second;
+}
 
 // i-th of the 12 "lower" rows of the 5x5 CellMode=half stencil (dz < 0, or dz = 0 and
 // dy < 0); the other 12 are their point mirrors, the 25th the item's own row.
