@@ -439,8 +439,9 @@ def main() -> None:
         # floating records, cell mode (sph_interaction_tiled.hip launch_fluid_tiled_s)
         ftb = "true" if getattr(case, "floatings", None) else "false"
         kname = (["sphx::k_nn_tiled<%d, %d, true," % (case.tvisco, case.tdensity)] if nn else
-                 ["sphx::k_fluid_tiled<%d, %s, %d>" % (td, ftb, case.cellmode)
-                  for td in ((case.tdensity | 8, case.tdensity) if case.tdensity >= 2 else (case.tdensity,))])
+                 ["sphx::k_fluid_tiled%s<%d, %s, %d>" % (w4, td, ftb, case.cellmode)
+                  for td in ((case.tdensity | 8, case.tdensity) if case.tdensity >= 2 else (case.tdensity,))
+                  for w4 in ("", "_w4")])  # _w4: the 4-wave register budget (DDT1)
         traffic = profiled_traffic(kname, case.np, "BASELINE " + args.workload) if world == 1 else None
         res = {
             "metric": METRIC,

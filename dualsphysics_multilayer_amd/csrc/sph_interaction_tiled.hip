@@ -711,13 +711,13 @@ __device__ unsigned long long g_tail[2 * 8192];
 __device__ unsigned g_tail_items[8192];
 #endif
 
-template <int TDENSITY, bool FT = false, int S = 1>
-__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_fluid_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
-                                                    unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
-                                                    const float4* __restrict__ velrhop,
-                                                    const float* __restrict__ press,
-                                                    const unsigned* __restrict__ bc, DivGrid g, KConst K,
-                                                    float4* __restrict__ arace, FtRec ft) {
+// The kernel body (k_fluid_tiled / k_fluid_tiled_w4 below).
+template <int TDENSITY, bool FT, int S>
+__device__ __forceinline__ void fluid_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
+                                            unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
+                                            const float4* __restrict__ velrhop, const float* __restrict__ press,
+                                            const unsigned* __restrict__ bc, const DivGrid& g, const KConst& K,
+                                            float4* __restrict__ arace, const FtRec& ft) {
   constexpr int tcap = TcapT<FT>::v;
   constexpr int TD = TDENSITY & 7;
   // position records then velrhop records in ONE array: the candidate test's last group of
@@ -844,6 +844,32 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
 #endif
 }
 
+// The kernel.  A register budget of 4 waves per SIMD (<= 128 VGPRs; 8 blocks per CU) for the
+// instantiations whose natural allocation exceeds it (DDT1, the Cubic DDT 1/2 forms, with
+// floating bodies Cubic DDT2 series: 129-135 VGPRs, 3 waves per SIMD): cfg3 (DDT1) 5.84 ->
+// 5.49 ms per interaction; the others keep the compiler's allocation (cfg2's DDT2 series at
+// 113 VGPRs under the budget ran 0.609-0.618 ms against 0.585-0.593 at its own 125).
+template <int TD, bool FT>
+constexpr bool tiled_w4() {
+  return (TD & 7) == 1 || TD == 18 || TD == 26 || (FT && (TD == 19 || TD == 27));
+}
+template <int TDENSITY, bool FT = false, int S = 1>
+__global__ __launch_bounds__(TB) void k_fluid_tiled(DevScalars* __restrict__ sc, const uint4* __restrict__ items,
+                                                    unsigned* __restrict__ qctr, const float4* __restrict__ poscell,
+                                                    const float4* __restrict__ velrhop,
+                                                    const float* __restrict__ press,
+                                                    const unsigned* __restrict__ bc, DivGrid g, KConst K,
+                                                    float4* __restrict__ arace, FtRec ft) {
+  fluid_tiled<TDENSITY, FT, S>(sc, items, qctr, poscell, velrhop, press, bc, g, K, arace, ft);
+}
+template <int TDENSITY, bool FT = false, int S = 1>
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_fluid_tiled_w4(
+    DevScalars* __restrict__ sc, const uint4* __restrict__ items, unsigned* __restrict__ qctr,
+    const float4* __restrict__ poscell, const float4* __restrict__ velrhop, const float* __restrict__ press,
+    const unsigned* __restrict__ bc, DivGrid g, KConst K, float4* __restrict__ arace, FtRec ft) {
+  fluid_tiled<TDENSITY, FT, S>(sc, items, qctr, poscell, velrhop, press, bc, g, K, arace, ft);
+}
+
 #ifdef SPH_TAIL_DIAG
 // The last launch's block timeline: launch span, idle share of the block slots (start ramp +
 // tail), and the spread of the blocks' end times (stderr, one line per launch).
@@ -885,10 +911,16 @@ static void launch_fluid_tiled_s(hipStream_t stm, unsigned nblocks, DevScalars* 
                                  unsigned* qctr, const float4* poscell, const float4* velrhop, const float* press,
                                  const unsigned* begincell, DivGrid g, const KConst& K, float4* arace,
                                  const FtRec& ft) {
-#define SPH_TILED(TD, FTB)                                                                                    \
-  hipLaunchKernelGGL((k_fluid_tiled<TD, FTB, S>), dim3(fit_grid((const void*)&k_fluid_tiled<TD, FTB, S>, nblocks)), \
-                     dim3(TB), 0, stm, sc, items, qctr, poscell,                                                \
-                     velrhop, press, begincell, g, K, arace, ft)
+#define SPH_TILED(TD, FTB)                                                                                     \
+  do {                                                                                                         \
+    if constexpr (tiled_w4<TD, FTB>())                                                                          \
+      hipLaunchKernelGGL((k_fluid_tiled_w4<TD, FTB, S>),                                                       \
+                         dim3(fit_grid((const void*)&k_fluid_tiled_w4<TD, FTB, S>, nblocks)), dim3(TB), 0, stm, \
+                         sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft);                \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_fluid_tiled<TD, FTB, S>), dim3(fit_grid((const void*)&k_fluid_tiled<TD, FTB, S>, nblocks)), \
+                         dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft); \
+  } while (0)
   // DDT 2/3 with the binomial series of the hydrostatic term (K.ddtseries) as TDENSITY | 8
   // and the Cubic spline kernel as TDENSITY | 16
   const int td = ((K.tdensity >= 2 && K.ddtseries) ? K.tdensity | 8 : K.tdensity) | (K.cubic ? 16 : 0);

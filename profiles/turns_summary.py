@@ -47,19 +47,19 @@ def main(src, dst, timeline=None):
     interior_all = []  # (thread, t0, t1)
     for th, ev in by.items():
         for t0, t1, n, s, b in ev:
-            if n == "k_fluid_tiled" and b % 2048:
+            if n.startswith("k_fluid_tiled") and b % 2048:
                 interior_all.append((th, t0, t1))
     per = {}
     for th, ev in by.items():
         ev.sort()
-        inter = [(t0, t1, s) for t0, t1, n, s, b in ev if n == "k_fluid_tiled" and b % 2048]
+        inter = [(t0, t1, s) for t0, t1, n, s, b in ev if n.startswith("k_fluid_tiled") and b % 2048]
         if not inter:
             continue
         istreams = {s for _, _, s in inter}
         copies = [(t0, t1) for t0, t1, n, s, b in ev
                   if n in ("__amd_rocclr_copyBuffer", "dma_copy_d2d") and s not in istreams]
         scat = [(t0, t1) for t0, t1, n, s, b in ev if n == "k_ghost_scatter" and s not in istreams]
-        face = [(t0, t1) for t0, t1, n, s, b in ev if n == "k_fluid_tiled" and not b % 2048]
+        face = [(t0, t1) for t0, t1, n, s, b in ev if n.startswith("k_fluid_tiled") and not b % 2048]
 
         def inside(lst):
             return sum(1 for t0, _ in lst if any(a <= t0 < b for a, b, _ in inter))
@@ -92,7 +92,7 @@ def main(src, dst, timeline=None):
         # one interior launch of a slab with two faces (the busiest thread), +-0.5 ms around it
         th = max(per, key=lambda t: (per[t]["ghost_copies"] > 0, per[t]["interior_us_avg"]))
         ev = sorted(by[th])
-        inter = [(t0, t1) for t0, t1, n, s, b in ev if n == "k_fluid_tiled" and b % 2048]
+        inter = [(t0, t1) for t0, t1, n, s, b in ev if n.startswith("k_fluid_tiled") and b % 2048]
         a, b = inter[len(inter) // 2]
         t00 = a - 500_000
         with open(timeline, "w") as f:
