@@ -257,7 +257,7 @@ class SphGpuSingle {
   unsigned xg_nm_ = 0;            // migrants it appended (apppos[xg_nm_ + e] = slot of ghost e)
   unsigned xg_np_ = 0;            // particles held after the migrants were appended
   bool ghost_pending_ = false;    // the last divide's ghost records have not been sent yet
-  bool overlap_ = true;           // sph_slab_set_overlap
+  bool overlap_ = false;          // sph_slab_set_overlap (default off: DESIGN.md §6)
   bool in_run_ = false;           // inside Run(): the next phase after a divide is the interaction
   hipStream_t xstream_ = nullptr; // ghost transfer + scatter + face items beside the interior items
   hipEvent_t ev_div_ = nullptr, ev_ghost_ = nullptr;

@@ -366,11 +366,16 @@ int sph_slab_group_member(SphSlabGroup* g, int i, SphSolver** out);
  * the group) with the same values, before or between runs. */
 int sph_slab_set_repartition(SphSolver* s, uint32_t every, double bound_weight, double tolerance);
 int sph_slab_group_set_repartition(SphSlabGroup* g, uint32_t every, double bound_weight, double tolerance);
-/* Ghost exchange beside the interaction (default on): the ghost records of a divide travel
- * while the items whose stencil reaches no ghost column interact; the face items follow.
- * Off: the ghosts are in place before the interaction.  Results are bitwise the same.
- * Default off for slabs that share a GPU with another slab of the run (groups: same device
- * id; sph_slab_create / _shm: same PCI bus id, checked collectively at creation).
+/* Ghost exchange beside the interaction (default off): the ghost records of a divide travel
+ * while the items whose stencil reaches no ghost column interact; the face items follow (the
+ * rows are cut at the face columns for that).  Off: the ghosts are in place before the
+ * interaction, over uncut rows.  Results are bitwise the same.  Off by default since round 5:
+ * each slab's interaction measured alone on the GPU (the turns measurement mode of the
+ * in-process transport) took 1.03-1.13 ms with the overlap against 0.85-0.92 ms
+ * in place at the BASELINE cfg3 8-slab split — the cut rows' extra items cost more than the
+ * transfer the overlap hides.  Always off for slabs that share a GPU with another slab of the
+ * run (groups: same device id; sph_slab_create / _shm: same PCI bus id, checked collectively
+ * at creation).
  * (No reference counterpart: the fork runs one domain per process, JSphGpuSingle.) */
 int sph_slab_set_overlap(SphSolver* s, int on);
 int sph_slab_group_set_overlap(SphSlabGroup* g, int on);
