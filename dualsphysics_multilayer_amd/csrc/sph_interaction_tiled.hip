@@ -707,7 +707,7 @@ __device__ __forceinline__ TAcc pass_s(const KConst& K, const DivGrid& g, const 
 #ifdef SPH_TAIL_DIAG
 // Diagnostic builds only: every block's start / end time (100 MHz clock) and item count of
 // the last launch, for the launch-tail analysis (tail_report).
-__device__ unsigned long long g_tail[2 * 8192];
+__device__ unsigned long long g_tail[4 * 8192];  // start, end, last item's start, last item (index | bound << 31)
 __device__ unsigned g_tail_items[8192];
 #endif
 
@@ -732,7 +732,8 @@ __device__ __forceinline__ void fluid_tiled(DevScalars* __restrict__ sc, const u
   float viscmax = 0.f, ace2max = 0.f;
 #ifdef SPH_TAIL_DIAG
   const unsigned long long t_start = wall_clock64();
-  unsigned nit = 0;
+  unsigned long long t_last = t_start;
+  unsigned nit = 0, last_it = 0;
 #endif
   // Visco of the step: ViscoTime's value (device-resident, k_dt) or the case's
   const float visco = K.visco_n ? sc->visco : K.visco, viscob = K.visco_n ? visco * K.viscobf : K.viscobound;
@@ -743,10 +744,12 @@ __device__ __forceinline__ void fluid_tiled(DevScalars* __restrict__ sc, const u
   for (;;) {
     const unsigned it = cur.next(&s_item);
     if (it == ITEM_NONE) break;
+    const uint4 item = items[it];
 #ifdef SPH_TAIL_DIAG
     nit++;
+    t_last = wall_clock64();
+    last_it = it | (item.x & ITEM_BOUND);
 #endif
-    const uint4 item = items[it];
     const bool bitem = (item.x & ITEM_BOUND) != 0u;
     const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
     const int a = int(item.y & 0xffffu), b = int(item.y >> 16);
@@ -837,8 +840,10 @@ __device__ __forceinline__ void fluid_tiled(DevScalars* __restrict__ sc, const u
   // without a new item list)
 #ifdef SPH_TAIL_DIAG
   if (threadIdx.x == 0 && blockIdx.x < 8192u) {
-    g_tail[2 * blockIdx.x] = t_start;
-    g_tail[2 * blockIdx.x + 1] = wall_clock64();
+    g_tail[4 * blockIdx.x] = t_start;
+    g_tail[4 * blockIdx.x + 1] = wall_clock64();
+    g_tail[4 * blockIdx.x + 2] = t_last;
+    g_tail[4 * blockIdx.x + 3] = last_it;
     g_tail_items[blockIdx.x] = nit;
   }
 #endif
@@ -877,32 +882,48 @@ static void tail_report(hipStream_t stm, unsigned nblocks) {
   static int calls = 0;
   if (++calls % 4 != 0) return;  // every 4th launch
   const unsigned n = std::min(nblocks, 8192u);
-  std::vector<unsigned long long> t(2 * size_t(n));
+  std::vector<unsigned long long> t(4 * size_t(n));
   std::vector<unsigned> it(n);
   (void)hipStreamSynchronize(stm);
-  (void)hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_tail), sizeof(unsigned long long) * 2 * n);
+  (void)hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_tail), sizeof(unsigned long long) * 4 * n);
   (void)hipMemcpyFromSymbol(it.data(), HIP_SYMBOL(g_tail_items), sizeof(unsigned) * n);
   unsigned long long s0 = ~0ull, e1 = 0, busy = 0;
-  std::vector<double> ends(n);
   for (unsigned b = 0; b < n; b++) {
-    s0 = std::min(s0, t[2 * b]);
-    e1 = std::max(e1, t[2 * b + 1]);
-    busy += t[2 * b + 1] - t[2 * b];
+    s0 = std::min(s0, t[4 * b]);
+    e1 = std::max(e1, t[4 * b + 1]);
+    busy += t[4 * b + 1] - t[4 * b];
   }
-  std::vector<double> starts(n);
-  for (unsigned b = 0; b < n; b++) ends[b] = 0.01 * double(t[2 * b + 1] - s0);  // us
-  for (unsigned b = 0; b < n; b++) starts[b] = 0.01 * double(t[2 * b] - s0);
-  std::sort(ends.begin(), ends.end());
-  std::sort(starts.begin(), starts.end());
-  unsigned late = 0;  // blocks that started after the first block ended
-  for (unsigned b = 0; b < n; b++) late += starts[b] > ends[0];
-  fprintf(stderr, "TAILS start_p50 %.1f p75 %.1f p90 %.1f max %.1f late %u\n", starts[n / 2], starts[(3 * n) / 4],
-          starts[(9 * n) / 10], starts[n - 1], late);
+  std::vector<unsigned> ord(n);
+  for (unsigned b = 0; b < n; b++) ord[b] = b;
+  std::sort(ord.begin(), ord.end(), [&](unsigned x, unsigned y) { return t[4 * x + 1] < t[4 * y + 1]; });
+  auto us = [&](unsigned long long v) { return 0.01 * double(v - s0); };
   const double span = 0.01 * double(e1 - s0);
   const unsigned imin = *std::min_element(it.begin(), it.end()), imax = *std::max_element(it.begin(), it.end());
-  fprintf(stderr, "TAIL blocks %u span_us %.1f idle %.4f end_p10 %.1f p50 %.1f p90 %.1f first %.1f items %u-%u\n", n,
-          span, 1.0 - double(busy) * 0.01 / (double(n) * span), ends[n / 10], ends[n / 2], ends[(9 * n) / 10], ends[0],
-          imin, imax);
+  fprintf(stderr, "TAIL blocks %u span_us %.1f idle %.4f end_first %.1f p10 %.1f p50 %.1f p90 %.1f items %u-%u\n", n, span,
+          1.0 - double(busy) * 0.01 / (double(n) * span), us(t[4 * ord[0] + 1]), us(t[4 * ord[n / 10] + 1]),
+          us(t[4 * ord[n / 2] + 1]), us(t[4 * ord[(9 * n) / 10] + 1]), imin, imax);
+  // the last items: by end-time decile, the mean duration of the block's last item, its share of
+  // bound items and its mean list index; the latest claim
+  unsigned long long lastclaim = 0;
+  unsigned maxidx = 0;
+  for (unsigned b = 0; b < n; b++) {
+    lastclaim = std::max(lastclaim, t[4 * b + 2]);
+    maxidx = std::max(maxidx, unsigned(t[4 * b + 3] & 0x7fffffffu));
+  }
+  fprintf(stderr, "TAILL last_claim %.1f max_index %u |", us(lastclaim), maxidx);
+  for (int d = 0; d < 10; d++) {
+    double dur = 0, nb = 0, idx = 0;
+    const unsigned lo = d * n / 10, hi = (d + 1) * n / 10;
+    for (unsigned k = lo; k < hi; k++) {
+      const unsigned b = ord[k];
+      dur += 0.01 * double(t[4 * b + 1] - t[4 * b + 2]);
+      nb += (t[4 * b + 3] >> 31) & 1u;
+      idx += double(t[4 * b + 3] & 0x7fffffffu);
+    }
+    const double c = double(hi - lo);
+    fprintf(stderr, " d%d %.0fus b%.2f i%.0f", d, dur / c, nb / c, idx / c);
+  }
+  fprintf(stderr, "\n");
 }
 #endif
 
