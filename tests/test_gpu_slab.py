@@ -386,3 +386,30 @@ def test_fatal_error_halts_every_slab_at_the_same_step():
     assert len({s["nstep"] for s in st}) == 1 and 0 < st[0]["nstep"] < 80, [s["nstep"] for s in st]
     assert len({s["time"] for s in st}) == 1
     assert all(s["error_flags"] & 2 for s in st), [s["error_flags"] for s in st]
+
+
+@pytest.mark.parametrize("turns,overlap", [("1", True), ("2", False), ("2", True)])
+def test_turns_measurement_modes_are_bitwise_the_normal_run(turns, overlap, monkeypatch):
+    """The turns measurement modes (SPH_SLAB_TURNS=1: interactions and divides one slab at a
+    time; 2: updates and the exchange's pack too) only order the slabs' kernels on the GPU:
+    the run is bitwise the normal one, Verlet and Symplectic, ghosts in place or beside the
+    interaction."""
+    res = []
+    for step_alg, ddt, dp in ((1, 2, 0.025), (2, 1, 0.03)):
+        case = DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt)
+        case.vel[case.npb:, 0] = 1.5  # migration across the faces
+        out = []
+        for env in (None, turns):
+            if env is None:
+                monkeypatch.delenv("SPH_SLAB_TURNS", raising=False)
+            else:
+                monkeypatch.setenv("SPH_SLAB_TURNS", env)
+            grp = group(case, 3)
+            grp.set_overlap(overlap)
+            grp.run(10)
+            out.append(grp.particles())
+            grp.close()
+        res.append(out)
+    for a, b in res:
+        for k in ("idp", "pos", "vel", "rhop"):
+            assert np.array_equal(a[k], b[k]), k
