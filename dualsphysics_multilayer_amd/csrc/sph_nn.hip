@@ -96,13 +96,11 @@ __device__ __forceinline__ float nn_eta(bool bi, float dmag, float tau_yield, fl
   // c: the phase's {m tau_yield, -m log2(e), n - 1, .} (the solver's third table row)
   const float mtau = c.x;
   if (dmag <= ALMOSTZERO) dmag = ALMOSTZERO;
-  // visco * D^(n-1): exactly visco for n = 1 (c.z = 0: v_exp_f32(0) = 1), so the two
-  // transcendentals are skipped when no lane of the wave meets a phase with n != 1; likewise
-  // 1 - exp(-m D) is exactly 0 for m = 0 (bitwise the same values for finite D)
+  // visco * D^(n-1), exactly visco for n = 1 (a per-wave skip for n = 1 / m = 0 measured
+  // neutral-to-slower at cfg5)
   float miou_hb = visco;
-  if (__any(c.z != 0.f)) miou_hb = visco * fexp2(c.z * flog2(dmag));
-  float e = 0.f;  // 1 - exp(-m D)
-  if (__any(c.y != 0.f)) e = 1.f - fexp2(c.y * dmag);
+  miou_hb = visco * fexp2(c.z * flog2(dmag));
+  const float e = 1.f - fexp2(c.y * dmag);  // 1 - exp(-m D)
   if (!bi) {
     const float miou_pap = tau_yield * frcp(2.f * dmag) * e;
     const bool cap = (miou_pap > mtau || dmag == ALMOSTZERO);

@@ -75,13 +75,15 @@ def main():
     ap.add_argument("--only", choices=tuple(MODES), default=None, help="one mode only (e.g. under rocprofv3)")
     ap.add_argument("--modes", default=None, help="comma-separated subset of the modes")
     ap.add_argument("--dp", type=float, default=0.00205)
+    ap.add_argument("--bound-weight", type=float, default=None, help="slab_partition's bound weight (default 0.3)")
     a = ap.parse_args()
     if os.environ.get("SPH_SLAB_TURNS") not in ("1", "2"):
         raise SystemExit("run with SPH_SLAB_TURNS=1 or 2 (the turns measurement modes)")
     case = DamBreakCase(a.dp, step_algorithm=2, tdensity=1)
-    bounds = [int(x) for x in slab_partition(case, a.slabs)]
+    bounds = [int(x) for x in (slab_partition(case, a.slabs) if a.bound_weight is None
+                                else slab_partition(case, a.slabs, a.bound_weight))]
     res = {"workload": "cfg3", "np": int(case.np), "bounds": bounds, "steps": a.steps,
-           "turns_mode": int(os.environ["SPH_SLAB_TURNS"]), "runs": []}
+           "turns_mode": int(os.environ["SPH_SLAB_TURNS"]), "bound_weight": a.bound_weight, "runs": []}
     modes = [a.only] if a.only is not None else (a.modes.split(",") if a.modes else list(MODES))
     for _ in range(a.repeat):
         for ov in modes:
