@@ -417,9 +417,10 @@ struct SlabGhost {
   unsigned idp;
   unsigned short code, pad;
 };
-constexpr int PK_BS = 256, PK_ITEMS = 16, PK_TILE = PK_BS * PK_ITEMS;
+constexpr int PK_BS = 256, PK_ITEMS = 4, PK_TILE = PK_BS * PK_ITEMS;
 // Bytes of the pack kernels' tile counters for a capacity of n particles: [4][ntiles] u32.
-constexpr size_t PK_TILECNT_BYTES(size_t n) { return 4 * sizeof(unsigned) * ((n + PK_TILE - 1) / PK_TILE); }
+// per tile: the four record streams, the particles staying owned, the ghosts per face (k_pack_count)
+constexpr size_t PK_TILECNT_BYTES(size_t n) { return 7 * sizeof(unsigned) * ((n + PK_TILE - 1) / PK_TILE); }
 // Device counters of one exchange: [0] ghosts, [1] migrants, per neighbour.
 struct SlabCounts {
   unsigned long long sendl[2], sendr[2];  // records for the left / right neighbour

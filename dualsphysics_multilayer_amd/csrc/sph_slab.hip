@@ -147,20 +147,19 @@ __global__ __launch_bounds__(PK_BS) void k_pack_count(const DevScalars* __restri
   if ((threadIdx.x & 63) == 0)
     for (int k = 0; k < 7; k++) s[k][w] = c4[k];
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int k = 0; k < 7; k++) {
-      unsigned t = 0;
-      for (int i = 0; i < PK_BS / 64; i++) t += s[k][i];
-      if (k < 4) q.tilecnt[k * q.ntiles + blockIdx.x] = t;
-      else if (k == 4 && t) atomicAdd(&q.cnt->nkeep, t);
-      else if (k > 4 && t) atomicAdd(&q.cnt->ghosts[k - 5], t);  // the face messages' ghost totals
-    }
+  if (threadIdx.x < 7) {  // per tile; k_pack_scan sums them (no same-line atomics per block)
+    const unsigned k = threadIdx.x;
+    unsigned t = 0;
+    for (int i = 0; i < PK_BS / 64; i++) t += s[k][i];
+    q.tilecnt[k * q.ntiles + blockIdx.x] = t;
   }
 }
 
-// Exclusive scan of the tile counts (four streams), totals -> cnt.
+// Exclusive scan of the tile counts (four streams), totals -> cnt; the tiles' staying
+// particles and face ghosts summed (the face messages' ghost totals).
 __global__ __launch_bounds__(1024) void k_pack_scan(const DevScalars* __restrict__ sc, PackArgs q) {
   __shared__ unsigned part[4][1024];
+  __shared__ unsigned s_tot[3][16], s_fin[3];
   const unsigned nt = q.ntiles;
   const unsigned per = (nt + 1023) / 1024;
   const unsigned b0 = threadIdx.x * per, b1 = min(b0 + per, nt);
@@ -169,7 +168,25 @@ __global__ __launch_bounds__(1024) void k_pack_scan(const DevScalars* __restrict
     for (unsigned i = b0; i < b1; i++) s += q.tilecnt[d * nt + i];
     part[d][threadIdx.x] = s;
   }
+  {
+    unsigned t[3] = {0u, 0u, 0u};
+    for (unsigned i = b0; i < b1; i++)
+      for (int d = 0; d < 3; d++) t[d] += q.tilecnt[(4 + d) * nt + i];
+    for (int d = 0; d < 3; d++)
+      for (int off = 32; off > 0; off >>= 1) t[d] += __shfl_xor(t[d], off, 64);
+    if ((threadIdx.x & 63) == 0)
+      for (int d = 0; d < 3; d++) s_tot[d][threadIdx.x >> 6] = t[d];
+  }
   __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned t[3] = {0u, 0u, 0u};
+    for (int w = 0; w < 16; w++)
+      for (int d = 0; d < 3; d++) t[d] += s_tot[d][w];
+    q.cnt->nkeep = t[0];
+    q.cnt->ghosts[0] = t[1];
+    q.cnt->ghosts[1] = t[2];
+    for (int d = 0; d < 3; d++) s_fin[d] = t[d];
+  }
   for (int off = 1; off < 1024; off <<= 1) {
     unsigned v[4];
     for (int d = 0; d < 4; d++) v[d] = threadIdx.x >= unsigned(off) ? part[d][threadIdx.x - off] : 0u;
@@ -187,8 +204,8 @@ __global__ __launch_bounds__(1024) void k_pack_scan(const DevScalars* __restrict
   }
   if (threadIdx.x == 1023) {
     // ghosts: the face-box totals of k_pack_count (exchange after the divide), else records
-    q.cnt->sendl[0] = q.fcnt[0] ? q.cnt->ghosts[0] : part[0][1023];
-    q.cnt->sendr[0] = q.fcnt[0] ? q.cnt->ghosts[1] : part[1][1023];
+    q.cnt->sendl[0] = q.fcnt[0] ? s_fin[1] : part[0][1023];
+    q.cnt->sendr[0] = q.fcnt[0] ? s_fin[2] : part[1][1023];
     q.cnt->sendl[1] = part[2][1023];
     q.cnt->sendr[1] = part[3][1023];
     q.cnt->np = sc->np;

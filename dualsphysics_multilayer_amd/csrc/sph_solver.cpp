@@ -705,7 +705,7 @@ void SphGpuSingle::AllocParticles(unsigned cap) {
   }
   sort_.ntiles = unsigned((n + RS_TILE - 1) / RS_TILE);
   sort_.hist = (unsigned*)dmalloc(4 * size_t(sort_.ntiles) * (1u << RS_MAXBITS));
-  // slab pack tile counts: tilecnt[4][ntiles] (ghost L/R, migrant L/R; sph_slab.hip)
+  // slab pack tile counts: tilecnt[7][ntiles] (ghost L/R, migrant L/R, staying, face ghosts L/R; sph_slab.hip)
   packtiles_ = (unsigned*)dmalloc(PK_TILECNT_BYTES(n));
   cap_ = cap;
 }
