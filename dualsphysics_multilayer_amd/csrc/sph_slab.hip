@@ -163,29 +163,50 @@ __global__ __launch_bounds__(1024) void k_pack_scan(const DevScalars* __restrict
   const unsigned nt = q.ntiles;
   const unsigned per = (nt + 1023) / 1024;
   const unsigned b0 = threadIdx.x * per, b1 = min(b0 + per, nt);
-  for (int d = 0; d < 4; d++) {
-    unsigned s = 0;
-    for (unsigned i = b0; i < b1; i++) s += q.tilecnt[d * nt + i];
-    part[d][threadIdx.x] = s;
-  }
-  {
-    unsigned t[3] = {0u, 0u, 0u};
+  // a thread's tiles of all seven count arrays loaded at once (one memory latency) when they
+  // fit the registers (<= PS_MAX tiles per thread: capacities up to 4M particles), else in loops
+  constexpr unsigned PS_MAX = 4;
+  unsigned v[7][PS_MAX];
+  const bool inreg = per <= PS_MAX;
+  unsigned t[3] = {0u, 0u, 0u};
+  if (inreg) {
+#pragma unroll
+    for (int d = 0; d < 7; d++)
+#pragma unroll
+      for (unsigned k = 0; k < PS_MAX; k++) v[d][k] = b0 + k < b1 ? q.tilecnt[d * nt + b0 + k] : 0u;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      unsigned s = 0;
+#pragma unroll
+      for (unsigned k = 0; k < PS_MAX; k++) s += v[d][k];
+      part[d][threadIdx.x] = s;
+    }
+#pragma unroll
+    for (int d = 0; d < 3; d++)
+#pragma unroll
+      for (unsigned k = 0; k < PS_MAX; k++) t[d] += v[4 + d][k];
+  } else {
+    for (int d = 0; d < 4; d++) {
+      unsigned s = 0;
+      for (unsigned i = b0; i < b1; i++) s += q.tilecnt[d * nt + i];
+      part[d][threadIdx.x] = s;
+    }
     for (unsigned i = b0; i < b1; i++)
       for (int d = 0; d < 3; d++) t[d] += q.tilecnt[(4 + d) * nt + i];
-    for (int d = 0; d < 3; d++)
-      for (int off = 32; off > 0; off >>= 1) t[d] += __shfl_xor(t[d], off, 64);
-    if ((threadIdx.x & 63) == 0)
-      for (int d = 0; d < 3; d++) s_tot[d][threadIdx.x >> 6] = t[d];
   }
+  for (int d = 0; d < 3; d++)
+    for (int off = 32; off > 0; off >>= 1) t[d] += __shfl_xor(t[d], off, 64);
+  if ((threadIdx.x & 63) == 0)
+    for (int d = 0; d < 3; d++) s_tot[d][threadIdx.x >> 6] = t[d];
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned t[3] = {0u, 0u, 0u};
+    unsigned u[3] = {0u, 0u, 0u};
     for (int w = 0; w < 16; w++)
-      for (int d = 0; d < 3; d++) t[d] += s_tot[d][w];
-    q.cnt->nkeep = t[0];
-    q.cnt->ghosts[0] = t[1];
-    q.cnt->ghosts[1] = t[2];
-    for (int d = 0; d < 3; d++) s_fin[d] = t[d];
+      for (int d = 0; d < 3; d++) u[d] += s_tot[d][w];
+    q.cnt->nkeep = u[0];
+    q.cnt->ghosts[0] = u[1];
+    q.cnt->ghosts[1] = u[2];
+    for (int d = 0; d < 3; d++) s_fin[d] = u[d];
   }
   for (int off = 1; off < 1024; off <<= 1) {
     unsigned v[4];
@@ -196,10 +217,19 @@ __global__ __launch_bounds__(1024) void k_pack_scan(const DevScalars* __restrict
   }
   for (int d = 0; d < 4; d++) {
     unsigned run = threadIdx.x ? part[d][threadIdx.x - 1] : 0u;
-    for (unsigned i = b0; i < b1; i++) {
-      const unsigned v = q.tilecnt[d * nt + i];
-      q.tilecnt[d * nt + i] = run;
-      run += v;
+    if (inreg) {
+#pragma unroll
+      for (unsigned k = 0; k < PS_MAX; k++)
+        if (b0 + k < b1) {
+          q.tilecnt[d * nt + b0 + k] = run;
+          run += v[d][k];
+        }
+    } else {
+      for (unsigned i = b0; i < b1; i++) {
+        const unsigned x = q.tilecnt[d * nt + i];
+        q.tilecnt[d * nt + i] = run;
+        run += x;
+      }
     }
   }
   if (threadIdx.x == 1023) {
