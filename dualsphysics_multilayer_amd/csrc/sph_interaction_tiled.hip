@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstdio>
+#include <stdexcept>
 #include <vector>
 
 #include "sph_items.hpp"
@@ -983,10 +984,18 @@ void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const
                         const float4* poscell, const float4* velrhop, const float* press, const unsigned* begincell,
                         DivGrid g, const KConst& K, float4* arace, const typecode* code, const float* ftmassp) {
   const FtRec ft = {code, ftmassp};
+#ifdef SPH_TILED_DIAG_CFG2
+  // diagnostic builds (kernel A/B at cfg2 only): the one instantiation of BASELINE cfg2
+  if (K.scelldiv != 1 || ftmassp || !(K.tdensity == 2 && K.ddtseries) || K.cubic)
+    throw std::runtime_error("SPH_TILED_DIAG_CFG2 build: cfg2 only");
+  hipLaunchKernelGGL((k_fluid_tiled<10, false, 1>), dim3(fit_grid((const void*)&k_fluid_tiled<10, false, 1>, nblocks)),
+                     dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft);
+#else
   if (K.scelldiv == 2)
     launch_fluid_tiled_s<2>(stm, nblocks, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft);
   else
     launch_fluid_tiled_s<1>(stm, nblocks, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft);
+#endif
 #ifdef SPH_TAIL_DIAG
   tail_report(stm, nblocks);
 #endif
