@@ -14,9 +14,10 @@
 //    records the accepted ones as bits (two 64-bit masks, no LDS traffic), then walks
 //    the set bits.  The heavy body then runs only for real pairs (~16% of candidates)
 //    instead of for every candidate any lane of the wave accepted.
-//  * Persistent blocks with one atomic work counter per XCD group (blockIdx % 8),
-//    items of an XCD group are spatially contiguous -> neighbour rows stay in that
-//    XCD's L2.
+//  * Persistent blocks (as many as are co-resident, fit_grid) claiming items from work
+//    queues per XCD group (blockIdx % 8): chunks of consecutive items dealt round-robin to
+//    the groups, all groups' fluid-row items before any bound-row item (ItemCursor,
+//    sph_tiled.hpp).
 //  * Fast f32 transcendentals: v_rcp/v_sqrt/v_exp/v_log (<= 1 ulp) instead of the
 //    IEEE division/sqrt/pow expansions; Wendland fac rewritten without the 1/rad
 //    (fac = bwen*q*(1-q/2)^3/rad = (bwen/h)*(1-q/2)^3).  Rounding-level differences
