@@ -1,11 +1,11 @@
-"""ctypes mirror of the POD structs in include/sphcore.h (ABI version 5)."""
+"""ctypes mirror of the POD structs in include/sphcore.h (ABI version: SPH_ABI_VERSION below)."""
 from __future__ import annotations
 
 import ctypes as C
 
 import numpy as np
 
-SPH_ABI_VERSION = 10
+SPH_ABI_VERSION = 11
 
 SPH_STATUS = {
     0: "SPH_OK",
@@ -256,6 +256,8 @@ class SphSlabDef(C.Structure):
         ("nranks", C.c_int32),
         ("cx_begin", C.c_int32),
         ("cx_end", C.c_int32),
+        ("axis", C.c_int32),
+        ("pad", C.c_int32),
         ("comm_id", C.c_ubyte * 128),
     ]
 
@@ -267,7 +269,7 @@ class SphSlabInfo(C.Structure):
         ("cx_begin", C.c_int32),
         ("cx_end", C.c_int32),
         ("repartitions", C.c_uint32),
-        ("pad", C.c_uint32),
+        ("axis", C.c_int32),
         ("last_imbalance", C.c_double),
     ]
 

@@ -2,6 +2,11 @@
 
 Each translation unit is compiled separately (parallel) and linked with hipcc.
 The product library never links the oracle.
+
+One diagnostic define exists, for fast kernel A/B builds only (`build(outdir=..., defines=
+["SPH_DIAG_HEADLINE_ONLY"])`, profiles/ab.sh): it compiles just the interaction kernels of the
+BASELINE headline workloads (cfg2's k_fluid_tiled<10,false,1>, cfg5's k_nn_tiled<2,3,*>) and
+makes every other case throw.  The product build never sets it.
 """
 from __future__ import annotations
 

@@ -66,10 +66,12 @@ EXPORTED_SYMBOLS = (
     "sph_solver_set_timing_phases",
     "sph_solver_timing",
     "sph_slab_partition",
+    "sph_slab_partition_axis",
     "sph_comm_unique_id",
     "sph_slab_create",
     "sph_slab_create_shm",
     "sph_slab_group_create",
+    "sph_slab_group_create_axis",
     "sph_slab_group_destroy",
     "sph_slab_group_run",
     "sph_slab_group_member",
@@ -135,12 +137,16 @@ def load_library(path: str = LIB_PATH):
     L.sph_solver_set_time.argtypes = [vp, C.c_double, C.c_double]
     L.sph_solver_timing.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
     L.sph_slab_partition.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.c_double, C.POINTER(C.c_int32)]
+    L.sph_slab_partition_axis.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.c_double, C.c_int,
+                                          C.POINTER(C.c_int32)]
     L.sph_comm_unique_id.argtypes = [C.POINTER(C.c_ubyte)]
     L.sph_slab_create.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.POINTER(SphSlabDef), C.POINTER(vp)]
     L.sph_slab_create_shm.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int,
                                       C.POINTER(SphSlabDef), C.c_char_p, C.c_uint64, C.POINTER(vp)]
     L.sph_slab_group_create.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.POINTER(C.c_int32),
                                         C.POINTER(C.c_int32), C.POINTER(vp)]
+    L.sph_slab_group_create_axis.argtypes = [C.POINTER(SphCaseDef), vp, C.c_int, C.POINTER(C.c_int32), C.c_int,
+                                             C.POINTER(C.c_int32), C.POINTER(vp)]
     L.sph_slab_group_destroy.argtypes = [vp]
     L.sph_slab_group_run.argtypes = [vp, C.c_uint32]
     L.sph_slab_group_member.argtypes = [vp, C.c_int, C.POINTER(vp)]
@@ -343,7 +349,7 @@ class SphGpuSingle:
         _check(load_library().sph_solver_set_timing(self._h, int(on)))
 
     def slab_info(self) -> dict:
-        """Current owned columns of a slab, re-partitions so far, last measured imbalance."""
+        """Current owned cells of a slab (along its axis), re-partitions so far, last measured imbalance."""
         out = SphSlabInfo()
         _check(load_library().sph_slab_info(self._h, C.byref(out)))
         return {k: getattr(out, k) for k, _ in SphSlabInfo._fields_ if k != "pad"}
@@ -364,14 +370,15 @@ class SphGpuSingle:
         return ms, n.value
 
 
-# ---- slab decomposition over x -------------------------------------
-def slab_partition(case, nranks: int, bound_weight: float = 0.3) -> np.ndarray:
-    """x-cell column bounds [nranks+1] balancing fluid + bound_weight*bound particles."""
+# ---- slab decomposition over x or y --------------------------------
+def slab_partition(case, nranks: int, bound_weight: float = 0.3, axis: int = 0) -> np.ndarray:
+    """Cell bounds [nranks+1] along `axis` (0: x columns, 1: y rows) balancing
+    fluid + bound_weight*bound particles."""
     cdef = SphCaseDef.from_dict(case.case_def())
     init = case_particles(case)
     out = np.zeros(nranks + 1, np.int32)
-    _check(load_library().sph_slab_partition(C.byref(cdef), C.byref(init.view), nranks, bound_weight,
-                                             out.ctypes.data_as(C.POINTER(C.c_int32))))
+    _check(load_library().sph_slab_partition_axis(C.byref(cdef), C.byref(init.view), nranks, bound_weight, int(axis),
+                                                  out.ctypes.data_as(C.POINTER(C.c_int32))))
     return out
 
 
@@ -383,14 +390,15 @@ def comm_unique_id() -> bytes:
 
 
 class SphGpuSlab(SphGpuSingle):
-    """One slab of a domain decomposed over x, one process per GPU over RCCL.
+    """One slab of a domain decomposed over x (axis 0) or y (axis 1), one process per GPU
+    over RCCL.
 
-    Every rank passes the full case; `bounds` are the column bounds of all ranks
-    (slab_partition) and `comm_id` the id rank 0 created.  Run/phase calls are
+    Every rank passes the full case; `bounds` are the cell bounds of all ranks along the
+    axis (slab_partition) and `comm_id` the id rank 0 created.  Run/phase calls are
     collective.  stats()["np"] and particles() cover the owned particles only."""
 
     def __init__(self, case, rank: int, nranks: int, bounds, comm_id, device: int = 0, transport: str = "rccl",
-                 slot_bytes: int = 16 << 20):
+                 slot_bytes: int = 16 << 20, axis: int = 0):
         """transport "rccl": comm_id = comm_unique_id() of rank 0 (one process per GPU);
         "shm": comm_id = the shared-memory segment name ("/...", same on every rank; ranks of
         one node without RCCL, e.g. several on one GPU), slot_bytes per mailbox."""
@@ -398,7 +406,7 @@ class SphGpuSlab(SphGpuSingle):
         self.case = case
         self._cdef = SphCaseDef.from_dict(case.case_def())
         init = case_particles(case)
-        sd = SphSlabDef(rank, nranks, int(bounds[rank]), int(bounds[rank + 1]))
+        sd = SphSlabDef(rank, nranks, int(bounds[rank]), int(bounds[rank + 1]), int(axis))
         h = C.c_void_p()
         if transport == "shm":
             _check(L.sph_slab_create_shm(C.byref(self._cdef), C.byref(init.view), device, C.byref(sd),
@@ -435,7 +443,7 @@ class SphSlabGroup:
     Runs the same pack / exchange / reduce code as SphGpuSlab over device-to-device
     copies instead of RCCL — how the decomposition is tested on a one-GPU machine."""
 
-    def __init__(self, case, bounds, devices=None):
+    def __init__(self, case, bounds, devices=None, axis: int = 0):
         L = load_library()
         bounds = np.ascontiguousarray(bounds, np.int32)
         n = len(bounds) - 1
@@ -444,9 +452,10 @@ class SphSlabGroup:
         self._cdef = SphCaseDef.from_dict(case.case_def())
         init = case_particles(case)
         h = C.c_void_p()
-        _check(L.sph_slab_group_create(C.byref(self._cdef), C.byref(init.view), n,
-                                       devices.ctypes.data_as(C.POINTER(C.c_int32)),
-                                       bounds.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(h)))
+        _check(L.sph_slab_group_create_axis(C.byref(self._cdef), C.byref(init.view), n,
+                                            devices.ctypes.data_as(C.POINTER(C.c_int32)), int(axis),
+                                            bounds.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(h)))
+        self.axis = int(axis)
         self._h = h
         self.bounds = bounds
         self.members = []

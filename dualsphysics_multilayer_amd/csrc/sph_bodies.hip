@@ -392,8 +392,7 @@ __global__ __launch_bounds__(256) void k_ft_ridp(const DevScalars* __restrict__ 
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p < sc->npb || p >= sc->np) return;
   if (CodeType(code[p]) != CODE_TYPE_FLOATING) return;
-  const int lcx = int(DcelCellx(K.domcellcode, dcell[p])) - g.xoff;
-  if (lcx < g.xown0 || lcx >= g.xown1) return;  // slab ghost
+  if (!slab_owned(g, slab_local(g, K.domcellcode, dcell[p]))) return;  // slab ghost
   const unsigned k = idp[p] - casenpb;
   if (k < nftp) ftridp[k] = p;
 }

@@ -192,8 +192,12 @@ int sph_solver_timing(SphSolver* s, double out_ms[4], uint64_t* launches) {
 
 int sph_slab_partition(const SphCaseDef* cdef, const SphParticlesHost* all, int nranks, double bound_weight,
                        int32_t* cx_bounds) {
-  NEED(cdef && all && all->pos && cx_bounds && nranks >= 1);
-  return guard([&] { sphx::slab_partition(*cdef, *all, nranks, bound_weight, cx_bounds); });
+  return sph_slab_partition_axis(cdef, all, nranks, bound_weight, 0, cx_bounds);
+}
+int sph_slab_partition_axis(const SphCaseDef* cdef, const SphParticlesHost* all, int nranks, double bound_weight,
+                            int axis, int32_t* bounds) {
+  NEED(cdef && all && all->pos && bounds && nranks >= 1);
+  return guard([&] { sphx::slab_partition(*cdef, *all, nranks, bound_weight, bounds, axis); });
 }
 
 int sph_comm_unique_id(unsigned char id[128]) {
@@ -212,6 +216,7 @@ int sph_slab_create(const SphCaseDef* cdef, const SphParticlesHost* all, int dev
     sc.nranks = slab->nranks;
     sc.c0 = slab->cx_begin;
     sc.c1 = slab->cx_end;
+    sc.axis = slab->axis;
     auto tr = sphx::make_rccl_transport(slab->comm_id, slab->rank, slab->nranks);
     auto* impl = new sphx::SphGpuSingle(*cdef, *all, device, sc, std::move(tr));
     try {
@@ -235,6 +240,7 @@ int sph_slab_create_shm(const SphCaseDef* cdef, const SphParticlesHost* all, int
     sc.nranks = slab->nranks;
     sc.c0 = slab->cx_begin;
     sc.c1 = slab->cx_end;
+    sc.axis = slab->axis;
     auto tr = sphx::make_shm_transport(shm_name, slab->rank, slab->nranks, slot_bytes);
     auto* impl = new sphx::SphGpuSingle(*cdef, *all, device, sc, std::move(tr));
     try {
@@ -249,11 +255,15 @@ int sph_slab_create_shm(const SphCaseDef* cdef, const SphParticlesHost* all, int
 
 int sph_slab_group_create(const SphCaseDef* cdef, const SphParticlesHost* all, int nslabs, const int32_t* devices,
                           const int32_t* cx_bounds, SphSlabGroup** out) {
-  NEED(cdef && all && devices && cx_bounds && out && nslabs >= 1);
+  return sph_slab_group_create_axis(cdef, all, nslabs, devices, 0, cx_bounds, out);
+}
+int sph_slab_group_create_axis(const SphCaseDef* cdef, const SphParticlesHost* all, int nslabs,
+                               const int32_t* devices, int axis, const int32_t* bounds, SphSlabGroup** out) {
+  NEED(cdef && all && devices && bounds && out && nslabs >= 1);
   NEED(all->idp && all->pos && all->vel && all->rhop);
   return guard([&] {
-    std::vector<int> dev(devices, devices + nslabs), b(cx_bounds, cx_bounds + nslabs + 1);
-    auto* impl = new sphx::SphSlabGroup(*cdef, *all, nslabs, dev.data(), b.data());
+    std::vector<int> dev(devices, devices + nslabs), b(bounds, bounds + nslabs + 1);
+    auto* impl = new sphx::SphSlabGroup(*cdef, *all, nslabs, dev.data(), b.data(), axis);
     auto* g = new SphSlabGroup{impl, {}};
     for (auto& sl : impl->slabs) g->members.push_back(SphSolver{sl.get(), true});
     *out = g;
@@ -312,6 +322,7 @@ int sph_slab_info(SphSolver* s, SphSlabInfo* out) {
     out->nranks = c.nranks;
     out->cx_begin = c.c0;
     out->cx_end = c.c1;
+    out->axis = c.axis;
     out->repartitions = s->impl->RepartitionCount();
     out->last_imbalance = s->impl->LastImbalance();
   });

@@ -105,6 +105,7 @@ std::unique_ptr<SlabTransport> make_rccl_transport(const unsigned char id[128], 
 // ---------------------------------------------------------------------------------
 LocalHub::LocalHub(int nslabs) : slots(size_t(nslabs)), n(nslabs) {
   if (const char* e = std::getenv("SPH_SLAB_TURNS")) turns = std::max(0, std::min(2, std::atoi(e)));
+  if (turns) test_hook_notice("SPH_SLAB_TURNS");
 }
 
 LocalHub::~LocalHub() {
@@ -199,7 +200,16 @@ class LocalTransport final : public SlabTransport {
     const unsigned long long g = gen_;
     const LocalHub::Slot* L = has_left() ? &hub_->slots[size_t(rank - 1)] : nullptr;
     const LocalHub::Slot* R = has_right() ? &hub_->slots[size_t(rank + 1)] : nullptr;
-    hub_->wait_until([&] { return (!L || L->consumed >= g) && (!R || R->consumed >= g); });
+    // Each neighbour records one `copied` event per generation, so the wait below covers
+    // generation g only while neither has consumed g+1 (it cannot before this rank posts g+1);
+    // checked inside the hub lock, so that a change of the calling pattern fails loudly.
+    bool ahead = false;
+    hub_->wait_until([&] {
+      const bool done = (!L || L->consumed >= g) && (!R || R->consumed >= g);
+      if (done) ahead = (L && L->consumed != g) || (R && R->consumed != g);
+      return done;
+    });
+    if (ahead) throw SphError(SPH_ERR_COMM, "exchange: a neighbour consumed a later generation before this drain");
     if (L) check_hip(hipEventSynchronize(L->copied), "exchange: drain left");
     if (R) check_hip(hipEventSynchronize(R->copied), "exchange: drain right");
   }

@@ -144,28 +144,43 @@ __device__ __forceinline__ float visco_at(const KConst& K, float t, int& pos) {
 constexpr int NN_MAXPH = 8;
 
 // Cell grid of the (fixed) divide domain — StDivDataGpu (JCellDivDataGpu.h:26-79).
-// Slab decomposition (sph_slab.hip): a rank's grid covers the global x-columns
-// [xoff, xoff+ncx); the columns it owns are the local [xown0, xown1) and the
-// columns either side of them hold read-only ghost copies of the neighbours'
-// particles.  dcell stays GLOBAL (same cell code as a single domain); poscell.w
-// carries the LOCAL cell (global cx - xoff).  Single domain: xoff 0, own [0, ncx).
+// Slab decomposition (sph_slab.hip) along the SLAB AXIS (axis 0: x, axis 1: y): a rank's grid
+// covers the global cells [soff, soff + extent) of that axis (the full extent of the other
+// two); the ones it owns are the local [sown0, sown1) and the W cells either side of them
+// (the ghost rim, W = the ghost width) hold read-only ghost copies of the neighbours'
+// particles.  dcell stays GLOBAL (same cell code as a single domain); poscell.w carries the
+// LOCAL cell (the global one shifted by soff along the axis).  Single domain: axis 0, soff
+// 0, own [0, ncx).  x-slabs cut the cell rows at the faces; y-slabs keep every x row whole
+// (a row is all owned or all ghost), so their items and the ghost overlap's interior / face
+// lists are whole rows.
 struct DivGrid {
   int ncx, ncy, ncz;
   unsigned nsheet, nct;
   unsigned boxboundignore, boxfluid, boxboundout, boxfluidout, boxboundoutignore, boxfluidoutignore;
   unsigned nctt;        // size of begincell = 2*nct + 6
   unsigned boxdiscard;  // ghosts of the previous divide and particles handed to a neighbour
-  int xoff, xown0, xown1;
+  int axis;             // slab axis (0 x, 1 y)
+  int soff, sown0, sown1;
+  __host__ __device__ int extent() const { return axis ? ncy : ncx; }  // local cells along the axis
+  __host__ __device__ int offx() const { return axis ? 0 : soff; }
+  __host__ __device__ int offy() const { return axis ? soff : 0; }
+  __host__ __device__ bool split() const { return sown0 != 0 || sown1 != extent(); }  // a slab grid
 };
 
-// Slab faces: a slab has xown0 (= ncx - xown1) ghost columns per face, the support radius
-// 2h in columns (1 with full cells, 2 with half cells).  The owned columns a neighbour
-// needs as its ghosts are the first / last xown0 owned ones.
-__host__ __device__ __forceinline__ bool in_left_face(const DivGrid& g, int lcx) {
-  return lcx >= g.xown0 && lcx < 2 * g.xown0;
+// Local coordinate along the slab axis of a GLOBAL dcell.
+__host__ __device__ __forceinline__ int slab_local(const DivGrid& g, unsigned dcc, unsigned dc) {
+  return int(g.axis ? DcelCelly(dcc, dc) : DcelCellx(dcc, dc)) - g.soff;
 }
-__host__ __device__ __forceinline__ bool in_right_face(const DivGrid& g, int lcx) {
-  return lcx < g.xown1 && lcx >= g.xown1 - (g.ncx - g.xown1);
+__host__ __device__ __forceinline__ bool slab_owned(const DivGrid& g, int l) { return l >= g.sown0 && l < g.sown1; }
+
+// Slab faces: a slab has sown0 (= extent - sown1) ghost cells per face along the axis, the
+// support radius 2h in cells (1 with full cells, 2 with half cells; +1 with mDBC).  The owned
+// cells a neighbour needs as its ghosts are the first / last sown0 owned ones.
+__host__ __device__ __forceinline__ bool in_left_face(const DivGrid& g, int l) {
+  return l >= g.sown0 && l < 2 * g.sown0;
+}
+__host__ __device__ __forceinline__ bool in_right_face(const DivGrid& g, int l) {
+  return l < g.sown1 && l >= g.sown1 - (g.extent() - g.sown1);
 }
 
 // dcell markers: excluded particle (JSphCpu::UpdatePos, JSphCpu.cpp:1262) and a

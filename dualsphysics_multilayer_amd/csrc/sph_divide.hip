@@ -295,7 +295,7 @@ struct GatherArgs {
   int igamma;  // gamma as a small positive integer, else 0
   unsigned dcc;
   int withm1, withpre;
-  int xoff;
+  int xoff, yoff;  // slab: the local grid's offset (the slab axis only)
   // NN multiphase: per-phase EOS {rho0, cteb, gamma, integer gamma or 0} (nullptr: single phase)
   const float4* phase_eos;
   // slab: sorted values >= vfirst are reserved ghost slots -> apppos[value - appbase]
@@ -373,7 +373,7 @@ __device__ __forceinline__ void gather_store(const GatherArgs& a, unsigned i,
   const double ox = a.posminx + double(cx) * a.scelld;
   const double oy = a.posminy + double(cy) * a.scelld;
   const double oz = a.posminz + double(cz) * a.scelld;
-  const unsigned ldc = a.xoff ? DcelCell(a.dcc, cx - unsigned(a.xoff), cy, cz) : dc;
+  const unsigned ldc = (a.xoff | a.yoff) ? DcelCell(a.dcc, cx - unsigned(a.xoff), cy - unsigned(a.yoff), cz) : dc;
   a.poscell[i] = make_float4(float(pxy.x - ox), float(pxy.y - oy), float(pz - oz), __uint_as_float(ldc));
   // Press (PreInteractionVars_Forces, JSphCpu.cpp:451-453; FunSphEos.h:37-47) as the
   // reference binary evaluates it: the unqualified pow in namespace fsph is the C
@@ -448,7 +448,7 @@ __global__ __launch_bounds__(256) void k_gather(DevScalars* __restrict__ sc, Gat
 
 void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned* sortpart, const PartArrays& src,
                    const PartArrays& dst, bool withm1, bool withpre, const KConst& K, const double dom_posmin[3],
-                   float4* poscell, float* press, int xoff, const float4* phase_eos, unsigned vfirst,
+                   float4* poscell, float* press, int xoff, int yoff, const float4* phase_eos, unsigned vfirst,
                    unsigned appbase, unsigned* apppos) {
   GatherArgs a;
   a.phase_eos = phase_eos;
@@ -457,6 +457,7 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
   a.apppos = apppos;
   a.allp = K.dtallp;
   a.xoff = xoff;
+  a.yoff = yoff;
   a.src = src;
   a.dst = dst;
   a.sortpart = sortpart;
@@ -660,27 +661,6 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
 // match on the 9-bit box offset), the stayers after the near arrivals whose list index is
 // at least Ln(obx(c)), far arrivals (a short list) by their previous index.  Two passes
 // over the window: counts, then (after the per-box scan) ranks -> positions.
-// Index of the first face box (SlabFaces order) whose key is >= key, for the face whose
-// first column is x0: the prefix of the face's counts there = its entries below key.
-__device__ __forceinline__ unsigned face_lower(const DivGrid& g, int W, unsigned key, int x0) {
-  const unsigned nfb1 = unsigned(g.ncz) * unsigned(g.ncy) * unsigned(W);  // face boxes of one type
-  unsigned type, cs;
-  if (key < g.nct) {
-    type = 0u;
-    cs = key;
-  } else if (key < g.boxfluid) {
-    return nfb1;  // BoundIgnore: after every bound face box
-  } else if (key < g.boxfluid + g.nct) {
-    type = 1u;
-    cs = key - g.boxfluid;
-  } else {
-    return 2u * nfb1;  // out and discard boxes: after every face box
-  }
-  const int x = int(cs % unsigned(g.ncx));
-  const unsigned r = cs / unsigned(g.ncx);  // z ncy + y
-  return type * nfb1 + r * unsigned(W) + unsigned(min(max(x - x0, 0), W));
-}
-
 constexpr int IB_FCAP = 256;  // far arrivals of a block held in LDS (more: read from global memory)
 constexpr int IB_TPCAP = 1024;  // window tiles with LDS prefixes (more: computed from global memory)
 constexpr int IB_WCAP = 4096;   // window near movers staged in LDS (more: read from global memory)
@@ -961,7 +941,7 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
       const unsigned key = unsigned(min(c0 + k, nctt));
       if (k > 0 && k < IB_BOX) s_ab[0][k] = a0 == a1 ? a0 : lower_bound_u32(s.akeys, a0, a1, key);
       s_ab[1][k] = s.nvl ? s.vpre[0][face_lower(g, s.vW, key, 0)] : 0u;
-      s_ab[2][k] = s.nvr ? s.vpre[1][face_lower(g, s.vW, key, g.xown1)] : 0u;
+      s_ab[2][k] = s.nvr ? s.vpre[1][face_lower(g, s.vW, key, g.sown1)] : 0u;
     }
     __syncthreads();
   }
@@ -1271,7 +1251,8 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
   a.appbase = 0;
   a.apppos = nullptr;
   a.allp = K.dtallp;
-  a.xoff = g.xoff;
+  a.xoff = g.offx();
+  a.yoff = g.offy();
   a.src = src;
   a.dst = dst;
   a.sortpart = nullptr;
@@ -1346,7 +1327,8 @@ void launch_ghost_scatter(hipStream_t stm, DevScalars* sc, const SlabGhost* rec,
   a.appbase = 0;
   a.apppos = nullptr;
   a.allp = K.dtallp;
-  a.xoff = g.xoff;
+  a.xoff = g.offx();
+  a.yoff = g.offy();
   a.src = dst;
   a.dst = dst;
   a.sortpart = nullptr;

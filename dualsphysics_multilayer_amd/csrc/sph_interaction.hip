@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void k_interaction(DevScalars* __restrict__ sc
     const int cx = int(DcelCellx(K.domcellcode, dc)), cy = int(DcelCelly(K.domcellcode, dc)),
               cz = int(DcelCellz(K.domcellcode, dc));
     const Range3 rg = ngs_range(cx, cy, cz, g, K.scelldiv);
-    const bool own = cx >= g.xown0 && cx < g.xown1;  // slab ghosts are not p1
+    const bool own = slab_owned(g, g.axis ? cy : cx);  // slab ghosts are not p1
     if (!own) {
     } else if (!ONLYBOUND && p1 >= npb) {
       // ---- fluid p1 ----
@@ -300,9 +300,10 @@ __global__ __launch_bounds__(256) void k_count_pairs(const DevScalars* __restric
   unsigned long long c[6] = {0, 0, 0, 0, 0, 0};
   const float4 pc1 = p1 < np ? poscell[p1] : make_float4(0.f, 0.f, 0.f, 0.f);
   const int cx = int(DcelCellx(K.domcellcode, __float_as_uint(pc1.w)));
-  if (p1 < np && (p1 >= npb || p1 < npbok) && cx >= g.xown0 && cx < g.xown1) {
+  const int cy = int(DcelCelly(K.domcellcode, __float_as_uint(pc1.w)));
+  if (p1 < np && (p1 >= npb || p1 < npbok) && slab_owned(g, g.axis ? cy : cx)) {
     const unsigned dc = __float_as_uint(pc1.w);
-    const int cy = int(DcelCelly(K.domcellcode, dc)), cz = int(DcelCellz(K.domcellcode, dc));
+    const int cz = int(DcelCellz(K.domcellcode, dc));
     const Range3 rg = ngs_range(cx, cy, cz, g, K.scelldiv);
     const bool fluid = p1 >= npb;
     for (int pass = 0; pass < (fluid ? 2 : 1); pass++) {

@@ -51,7 +51,7 @@ ItemBuild make_item_build(const unsigned* begincell, DivGrid g, unsigned* rowtmp
   b.bc = begincell;
   b.g = g;
   b.tmaxc = scelldiv == 1 ? TMAXCELLS : TMAXCELLS_HALF;
-  b.xr = {{g.xown0, g.xown1, 0, 0, 0, 0}, qctr2 ? 2 : 1};
+  b.xr = {{g.sown0, g.sown1, 0, 0, 0, 0}, qctr2 ? 2 : 1};
   if (xr)
     for (int k = 0; k < 6; k++) b.xr.x[k] = xr[k];
   b.nrows2 = 2u * unsigned(g.ncy) * unsigned(g.ncz);
@@ -706,12 +706,6 @@ __device__ __forceinline__ TAcc pass_s(const KConst& K, const DivGrid& g, const 
                                              dstop0);
 }
 
-#ifdef SPH_TAIL_DIAG
-// Diagnostic builds only: every block's start / end time (100 MHz clock) and item count of
-// the last launch, for the launch-tail analysis (tail_report).
-__device__ unsigned long long g_tail[4 * 8192];  // start, end, last item's start, last item (index | bound << 31)
-__device__ unsigned g_tail_items[8192];
-#endif
 
 // The kernel body (k_fluid_tiled / k_fluid_tiled_w4 below).
 template <int TDENSITY, bool FT, int S>
@@ -732,11 +726,6 @@ __device__ __forceinline__ void fluid_tiled(DevScalars* __restrict__ sc, const u
   __shared__ unsigned char s_perm[TB];  // lane -> p1 of the item (see lane_order)
   __shared__ unsigned s_nwave[4];
   float viscmax = 0.f, ace2max = 0.f;
-#ifdef SPH_TAIL_DIAG
-  const unsigned long long t_start = wall_clock64();
-  unsigned long long t_last = t_start;
-  unsigned nit = 0, last_it = 0;
-#endif
   // Visco of the step: ViscoTime's value (device-resident, k_dt) or the case's
   const float visco = K.visco_n ? sc->visco : K.visco, viscob = K.visco_n ? visco * K.viscobf : K.viscobound;
   const float cvisc_f = -visco * K.cs0f * K.kernelh * K.massfluid;
@@ -747,11 +736,6 @@ __device__ __forceinline__ void fluid_tiled(DevScalars* __restrict__ sc, const u
     const unsigned it = cur.next(&s_item);
     if (it == ITEM_NONE) break;
     const uint4 item = items[it];
-#ifdef SPH_TAIL_DIAG
-    nit++;
-    t_last = wall_clock64();
-    last_it = it | (item.x & ITEM_BOUND);
-#endif
     const bool bitem = (item.x & ITEM_BOUND) != 0u;
     const int cy = int(item.x & 0xffffu), cz = int((item.x >> 16) & 0x7fffu);
     const int a = int(item.y & 0xffffu), b = int(item.y >> 16);
@@ -840,15 +824,6 @@ __device__ __forceinline__ void fluid_tiled(DevScalars* __restrict__ sc, const u
   wave_max_atomic(sc, RED_ACEMAX2, ace2max);
   // (the queue counters are zeroed by k_items_place, or by the solver before an interaction
   // without a new item list)
-#ifdef SPH_TAIL_DIAG
-  if (threadIdx.x == 0 && blockIdx.x < 8192u) {
-    g_tail[4 * blockIdx.x] = t_start;
-    g_tail[4 * blockIdx.x + 1] = wall_clock64();
-    g_tail[4 * blockIdx.x + 2] = t_last;
-    g_tail[4 * blockIdx.x + 3] = last_it;
-    g_tail_items[blockIdx.x] = nit;
-  }
-#endif
 }
 
 // The kernel.  A register budget of 4 waves per SIMD (<= 128 VGPRs; 8 blocks per CU) for the
@@ -877,71 +852,20 @@ __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   fluid_tiled<TDENSITY, FT, S>(sc, items, qctr, poscell, velrhop, press, bc, g, K, arace, ft);
 }
 
-#ifdef SPH_TAIL_DIAG
-// The last launch's block timeline: launch span, idle share of the block slots (start ramp +
-// tail), and the spread of the blocks' end times (stderr, one line per launch).
-static void tail_report(hipStream_t stm, unsigned nblocks) {
-  static int calls = 0;
-  if (++calls % 4 != 0) return;  // every 4th launch
-  const unsigned n = std::min(nblocks, 8192u);
-  std::vector<unsigned long long> t(4 * size_t(n));
-  std::vector<unsigned> it(n);
-  (void)hipStreamSynchronize(stm);
-  (void)hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_tail), sizeof(unsigned long long) * 4 * n);
-  (void)hipMemcpyFromSymbol(it.data(), HIP_SYMBOL(g_tail_items), sizeof(unsigned) * n);
-  unsigned long long s0 = ~0ull, e1 = 0, busy = 0;
-  for (unsigned b = 0; b < n; b++) {
-    s0 = std::min(s0, t[4 * b]);
-    e1 = std::max(e1, t[4 * b + 1]);
-    busy += t[4 * b + 1] - t[4 * b];
-  }
-  std::vector<unsigned> ord(n);
-  for (unsigned b = 0; b < n; b++) ord[b] = b;
-  std::sort(ord.begin(), ord.end(), [&](unsigned x, unsigned y) { return t[4 * x + 1] < t[4 * y + 1]; });
-  auto us = [&](unsigned long long v) { return 0.01 * double(v - s0); };
-  const double span = 0.01 * double(e1 - s0);
-  const unsigned imin = *std::min_element(it.begin(), it.end()), imax = *std::max_element(it.begin(), it.end());
-  fprintf(stderr, "TAIL blocks %u span_us %.1f idle %.4f end_first %.1f p10 %.1f p50 %.1f p90 %.1f items %u-%u\n", n, span,
-          1.0 - double(busy) * 0.01 / (double(n) * span), us(t[4 * ord[0] + 1]), us(t[4 * ord[n / 10] + 1]),
-          us(t[4 * ord[n / 2] + 1]), us(t[4 * ord[(9 * n) / 10] + 1]), imin, imax);
-  // the last items: by end-time decile, the mean duration of the block's last item, its share of
-  // bound items and its mean list index; the latest claim
-  unsigned long long lastclaim = 0;
-  unsigned maxidx = 0;
-  for (unsigned b = 0; b < n; b++) {
-    lastclaim = std::max(lastclaim, t[4 * b + 2]);
-    maxidx = std::max(maxidx, unsigned(t[4 * b + 3] & 0x7fffffffu));
-  }
-  fprintf(stderr, "TAILL last_claim %.1f max_index %u |", us(lastclaim), maxidx);
-  for (int d = 0; d < 10; d++) {
-    double dur = 0, nb = 0, idx = 0;
-    const unsigned lo = d * n / 10, hi = (d + 1) * n / 10;
-    for (unsigned k = lo; k < hi; k++) {
-      const unsigned b = ord[k];
-      dur += 0.01 * double(t[4 * b + 1] - t[4 * b + 2]);
-      nb += (t[4 * b + 3] >> 31) & 1u;
-      idx += double(t[4 * b + 3] & 0x7fffffffu);
-    }
-    const double c = double(hi - lo);
-    fprintf(stderr, " d%d %.0fus b%.2f i%.0f", d, dur / c, nb / c, idx / c);
-  }
-  fprintf(stderr, "\n");
-}
-#endif
 
 template <int S>
 static void launch_fluid_tiled_s(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items,
                                  unsigned* qctr, const float4* poscell, const float4* velrhop, const float* press,
                                  const unsigned* begincell, DivGrid g, const KConst& K, float4* arace,
-                                 const FtRec& ft) {
+                                 const FtRec& ft, unsigned reserve) {
 #define SPH_TILED(TD, FTB)                                                                                     \
   do {                                                                                                         \
     if constexpr (tiled_w4<TD, FTB>())                                                                          \
       hipLaunchKernelGGL((k_fluid_tiled_w4<TD, FTB, S>),                                                       \
-                         dim3(fit_grid((const void*)&k_fluid_tiled_w4<TD, FTB, S>, nblocks)), dim3(TB), 0, stm, \
+                         dim3(fit_grid((const void*)&k_fluid_tiled_w4<TD, FTB, S>, nblocks, TB, reserve)), dim3(TB), 0, stm, \
                          sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft);                \
     else                                                                                                       \
-      hipLaunchKernelGGL((k_fluid_tiled<TD, FTB, S>), dim3(fit_grid((const void*)&k_fluid_tiled<TD, FTB, S>, nblocks)), \
+      hipLaunchKernelGGL((k_fluid_tiled<TD, FTB, S>), dim3(fit_grid((const void*)&k_fluid_tiled<TD, FTB, S>, nblocks, TB, reserve)), \
                          dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft); \
   } while (0)
   // DDT 2/3 with the binomial series of the hydrostatic term (K.ddtseries) as TDENSITY | 8
@@ -983,22 +907,21 @@ static void launch_fluid_tiled_s(hipStream_t stm, unsigned nblocks, DevScalars* 
 
 void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
                         const float4* poscell, const float4* velrhop, const float* press, const unsigned* begincell,
-                        DivGrid g, const KConst& K, float4* arace, const typecode* code, const float* ftmassp) {
+                        DivGrid g, const KConst& K, float4* arace, const typecode* code, const float* ftmassp,
+                        unsigned reserve) {
   const FtRec ft = {code, ftmassp};
-#ifdef SPH_TILED_DIAG_CFG2
+#ifdef SPH_DIAG_HEADLINE_ONLY
   // diagnostic builds (kernel A/B at cfg2 only): the one instantiation of BASELINE cfg2
   if (K.scelldiv != 1 || ftmassp || !(K.tdensity == 2 && K.ddtseries) || K.cubic)
-    throw std::runtime_error("SPH_TILED_DIAG_CFG2 build: cfg2 only");
-  hipLaunchKernelGGL((k_fluid_tiled<10, false, 1>), dim3(fit_grid((const void*)&k_fluid_tiled<10, false, 1>, nblocks)),
+    throw std::runtime_error("SPH_DIAG_HEADLINE_ONLY build: cfg2 / cfg5 kernels only");
+  hipLaunchKernelGGL((k_fluid_tiled<10, false, 1>), dim3(fit_grid((const void*)&k_fluid_tiled<10, false, 1>, nblocks, TB, reserve)),
                      dim3(TB), 0, stm, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft);
 #else
   if (K.scelldiv == 2)
-    launch_fluid_tiled_s<2>(stm, nblocks, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft);
+    launch_fluid_tiled_s<2>(stm, nblocks, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft, reserve);
   else
-    launch_fluid_tiled_s<1>(stm, nblocks, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft);
-#endif
-#ifdef SPH_TAIL_DIAG
-  tail_report(stm, nblocks);
+    launch_fluid_tiled_s<1>(stm, nblocks, sc, items, qctr, poscell, velrhop, press, begincell, g, K, arace, ft,
+                            reserve);
 #endif
 }
 

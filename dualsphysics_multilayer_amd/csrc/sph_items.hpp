@@ -29,8 +29,9 @@ constexpr int IR_WAVES = 4;            // rows per block: one wave each (blocks 
 constexpr int ROWCELLS_LDS = 1024;     // longest row (cells) walked from LDS; longer: global memory
 
 struct ItemRanges {
-  int x[6];  // column ranges [x[2k], x[2k+1]) of p1 (empty when equal): list A = range 0 (and
-             // 1, 2 with one list), list B = ranges 1, 2
+  int x[6];  // ranges [x[2k], x[2k+1]) of p1 along the slab axis (empty when equal): list A =
+             // range 0 (and 1, 2 with one list), list B = ranges 1, 2.  x-slabs: column ranges
+             // of every row; y-slabs: the rows whose y is in a range, each over all its columns
   int nl;    // lists: 1 or 2
 };
 
@@ -69,14 +70,28 @@ __device__ __forceinline__ void items_row(const ItemBuild& b, unsigned r, unsign
   const unsigned rowbase = (bound ? 0u : g.boxfluid) + z * g.nsheet + y * unsigned(g.ncx);
   const int ncx = g.ncx;
   const unsigned* __restrict__ bc = b.bc;
+  // the column range [rx0, rx1) of range k in this row (y-slabs: the whole row or nothing)
+  auto range_x = [&](int k, int& rx0, int& rx1) {
+    if (g.axis == 0) {
+      rx0 = xr.x[2 * k];
+      rx1 = xr.x[2 * k + 1];
+    } else {
+      const bool in = int(y) >= xr.x[2 * k] && int(y) < xr.x[2 * k + 1];
+      rx0 = 0;
+      rx1 = in ? ncx : 0;
+    }
+  };
   {  // a row without particles in its ranges (most rows of the air above the water and of
      // the boundary): no items, no staging
     int xlo = ncx, xhi = 0;
-    for (int k = 0; k < 3; k++)
-      if (xr.x[2 * k] < xr.x[2 * k + 1]) {
-        xlo = min(xlo, xr.x[2 * k]);
-        xhi = max(xhi, xr.x[2 * k + 1]);
+    for (int k = 0; k < 3; k++) {
+      int rx0, rx1;
+      range_x(k, rx0, rx1);
+      if (rx0 < rx1) {
+        xlo = min(xlo, rx0);
+        xhi = max(xhi, rx1);
       }
+    }
     if (xlo >= xhi || bc[rowbase + xlo] == bc[rowbase + xhi]) {
       if (!WRITE && lane == 0)
         for (int list = 0; list < xr.nl; list++) b.counts[list * nrows2 + r] = 0u;
@@ -103,7 +118,8 @@ __device__ __forceinline__ void items_row(const ItemBuild& b, unsigned r, unsign
     // p1 only in owned columns (slab ghosts are neighbours, never p1); each range walked on
     // its own, so no item crosses from one to the next
     for (int rg = (list ? 1 : 0); rg < (xr.nl == 2 && list == 0 ? 1 : 3); rg++) {
-      const int xbeg = xr.x[2 * rg], xend = xr.x[2 * rg + 1];  // uniform over the wave
+      int xbeg, xend;  // uniform over the wave
+      range_x(rg, xbeg, xend);
       if (xbeg >= xend) continue;
       if (!lds) {  // very long rows: the same walk on global memory, cell by cell
         if (lane == 0) {

@@ -90,9 +90,10 @@ __device__ __forceinline__ void shift_displacement(const KConst& K, float4 rs, f
 // Box key of one particle (KerPreSortFull, JCellDivGpuSingle_ker.cu:41-102).
 __device__ __forceinline__ unsigned box_key(unsigned rcell, typecode rcode, const DivGrid& g, unsigned dcc) {
   if (rcell == DCELL_DISCARD) return g.boxdiscard;  // slab: stale ghost / particle handed to a neighbour
-  const unsigned cx = DcelCellx(dcc, rcell) - unsigned(g.xoff), cy = DcelCelly(dcc, rcell), cz = DcelCellz(dcc, rcell);
-  if (rcell != DCELL_OUT && (g.xown0 != 0 || g.xown1 != g.ncx) && cx >= unsigned(g.ncx))
-    return g.boxdiscard;  // slab: a migrant handed over beyond this slab's ghost columns (re-partition)
+  const unsigned cx = DcelCellx(dcc, rcell) - unsigned(g.offx()), cy = DcelCelly(dcc, rcell) - unsigned(g.offy()),
+                 cz = DcelCellz(dcc, rcell);
+  if (rcell != DCELL_OUT && g.split() && (g.axis ? cy >= unsigned(g.ncy) : cx >= unsigned(g.ncx)))
+    return g.boxdiscard;  // slab: a migrant handed over beyond this slab's ghost rim (re-partition)
   const unsigned cellsort = cx + cy * unsigned(g.ncx) + cz * g.nsheet;
   const typecode codetype = CodeType(rcode), codeout = CodeSpecial(rcode);
   if (codetype < CODE_TYPE_FLOATING)
@@ -101,6 +102,83 @@ __device__ __forceinline__ unsigned box_key(unsigned rcell, typecode rcode, cons
                : (codeout == CODE_OUTIGNORE ? g.boxboundoutignore : g.boxboundout);
   return codeout <= CODE_OUTIGNORE ? (codeout < CODE_OUTIGNORE ? g.boxfluid + cellsort : g.boxfluidoutignore)
                                    : (codetype == CODE_TYPE_FLOATING ? g.boxboundout : g.boxfluidout);
+}
+
+// ---- slab face boxes (the ghost exchange; sph_slab.hip, the incremental divide) ----
+// The W cells of a face along the slab axis, from the local axis cell s0, as (type, z, y, x)
+// boxes enumerated in box-key order: x-slabs ((type ncz + z) ncy + y) W + (x - s0), y-slabs
+// ((type ncz + z) W + (y - s0)) ncx + x.  The sender's face (its first / last owned cells)
+// and the receiver's ghost rim number the same global boxes alike.
+__host__ __device__ __forceinline__ unsigned face_boxes_per_type(const DivGrid& g, int W) {
+  return unsigned(g.ncz) * unsigned(W) * unsigned(g.axis ? g.ncx : g.ncy);
+}
+// Box key of face box idx.
+__device__ __forceinline__ unsigned face_key(const DivGrid& g, int W, unsigned idx, int s0) {
+  if (g.axis == 0) {
+    const unsigned xrel = idx % unsigned(W);
+    unsigned t = idx / unsigned(W);
+    const unsigned y = t % unsigned(g.ncy);
+    t /= unsigned(g.ncy);
+    const unsigned z = t % unsigned(g.ncz), type = t / unsigned(g.ncz);
+    return (type ? g.boxfluid : 0u) + unsigned(s0) + xrel + y * unsigned(g.ncx) + z * g.nsheet;
+  }
+  const unsigned x = idx % unsigned(g.ncx);
+  unsigned t = idx / unsigned(g.ncx);
+  const unsigned yrel = t % unsigned(W);
+  t /= unsigned(W);
+  const unsigned z = t % unsigned(g.ncz), type = t / unsigned(g.ncz);
+  return (type ? g.boxfluid : 0u) + x + (unsigned(s0) + yrel) * unsigned(g.ncx) + z * g.nsheet;
+}
+// Face box of a box key (-1: not a cell box of the face's W cells from s0).
+__device__ __forceinline__ int face_idx(const DivGrid& g, int W, unsigned key, int s0) {
+  unsigned type, cs;
+  if (key < g.nct) {
+    type = 0u;
+    cs = key;
+  } else if (key >= g.boxfluid && key < g.boxfluid + g.nct) {
+    type = 1u;
+    cs = key - g.boxfluid;
+  } else {
+    return -1;
+  }
+  const int x = int(cs % unsigned(g.ncx));
+  const unsigned r = cs / unsigned(g.ncx);  // z ncy + y
+  const int y = int(r % unsigned(g.ncy));
+  const unsigned tz = type * unsigned(g.ncz) + r / unsigned(g.ncy);
+  if (g.axis == 0) {
+    const int xr = x - s0;
+    if (xr < 0 || xr >= W) return -1;
+    return int((tz * unsigned(g.ncy) + unsigned(y)) * unsigned(W) + unsigned(xr));
+  }
+  const int yr = y - s0;
+  if (yr < 0 || yr >= W) return -1;
+  return int((tz * unsigned(W) + unsigned(yr)) * unsigned(g.ncx) + unsigned(x));
+}
+// Index of the first face box whose key is >= key (the prefix of the face's counts there =
+// its entries below key).
+__device__ __forceinline__ unsigned face_lower(const DivGrid& g, int W, unsigned key, int s0) {
+  const unsigned nfb1 = face_boxes_per_type(g, W);  // face boxes of one type
+  unsigned type, cs;
+  if (key < g.nct) {
+    type = 0u;
+    cs = key;
+  } else if (key < g.boxfluid) {
+    return nfb1;  // BoundIgnore: after every bound face box
+  } else if (key < g.boxfluid + g.nct) {
+    type = 1u;
+    cs = key - g.boxfluid;
+  } else {
+    return 2u * nfb1;  // out and discard boxes: after every face box
+  }
+  const int x = int(cs % unsigned(g.ncx));
+  const unsigned r = cs / unsigned(g.ncx);  // z ncy + y
+  if (g.axis == 0) return type * nfb1 + r * unsigned(W) + unsigned(min(max(x - s0, 0), W));
+  const int y = int(r % unsigned(g.ncy)), z = int(r / unsigned(g.ncy));
+  const unsigned zb = type * nfb1 + unsigned(z) * unsigned(W) * unsigned(g.ncx);  // the first box of this z
+  const int yr = y - s0;
+  if (yr < 0) return zb;
+  if (yr >= W) return zb + unsigned(W) * unsigned(g.ncx);
+  return zb + unsigned(yr) * unsigned(g.ncx) + unsigned(x);
 }
 
 struct SlabFaces;  // the ghost exchange after the divide (below)
@@ -141,7 +219,7 @@ void launch_begincell(hipStream_t stm, unsigned cap, DevScalars* sc, const unsig
 // index goes to apppos[value - appbase] instead.
 void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned* sortpart, const PartArrays& src,
                    const PartArrays& dst, bool withm1, bool withpre, const KConst& K, const double dom_posmin[3],
-                   float4* poscell, float* press, int xoff, const float4* phase_eos = nullptr, unsigned vfirst = ~0u,
+                   float4* poscell, float* press, int xoff, int yoff, const float4* phase_eos = nullptr, unsigned vfirst = ~0u,
                    unsigned appbase = 0, unsigned* apppos = nullptr);
 
 constexpr unsigned TSUP_STRIDE = 16;  // u64 entries per super-tile line
@@ -232,7 +310,7 @@ constexpr size_t QCTR_BYTES = size_t(QCTR_COPIES) * QCTR_WORDS * sizeof(unsigned
 void launch_fluid_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const uint4* items, unsigned* qctr,
                         const float4* poscell, const float4* velrhop, const float* press, const unsigned* begincell,
                         DivGrid g, const KConst& K, float4* arace, const typecode* code = nullptr,
-                        const float* ftmassp = nullptr);
+                        const float* ftmassp = nullptr, unsigned reserve = 0);
 // mDBC boundary correction (sph_mdbc.hip; JSphCpu.cpp:1020-1187): density of every
 // boundary particle p1 < npbok with a normal extrapolated from its ghost node; press
 // refreshed.  `normal` is indexed by idp; list[npbcap] + nlist: scratch of the
@@ -311,7 +389,7 @@ void launch_dt(hipStream_t stm, DevScalars* sc, const KConst& K, double cfl, dou
 void launch_visco_init(hipStream_t stm, DevScalars* sc, const KConst& K);
 // folded[5]: VelMax^2, AceMax^2, ViscDtMax, ViscEtaDtMax, this slab's fatal error flags
 void launch_fold_maxima(hipStream_t stm, DevScalars* sc, unsigned* folded, bool clear);
-// Update kernels skip slab ghosts (local column outside [g.xown0, g.xown1)) and mark
+// Update kernels skip slab ghosts (local cell along the slab axis outside [g.sown0, g.sown1)) and mark
 // them DCELL_DISCARD for the next divide.
 // shiftpos (nullptr: no shifting): the interaction's shifting sums, turned into the
 // displacement of JSphShifting::RunCpu inside the update.

@@ -121,9 +121,9 @@ __device__ __forceinline__ GhostBox ghost_box(const MdbcArgs& a, const DivGrid& 
   b.gx = pxy.x + double(bn.x);
   b.gy = pxy.y + double(bn.y);
   b.gz = a.posz[p1] + double(bn.z);
-  const int cx = int((b.gx - a.posminx) / a.scelld) - g.xoff;
+  const int cx = int((b.gx - a.posminx) / a.scelld) - g.offx();
   b.cxu = cx;
-  const int cy = int((b.gy - a.posminy) / a.scelld);
+  const int cy = int((b.gy - a.posminy) / a.scelld) - g.offy();
   const int cz = int((b.gz - a.posminz) / a.scelld);
   b.xini = max(cx - SD, 0);
   b.xfin = min(cx + SD + 1, g.ncx);
@@ -155,10 +155,7 @@ __global__ __launch_bounds__(256) void k_mdbc_list(const DevScalars* __restrict_
   const bool valid = p1 != 0xffffffffu;
   bool keep = false;
   bool own = true;
-  if (valid && (g.xown0 > 0 || g.xown1 < g.ncx)) {  // slab: owned p1 only
-    const int lcx = int(DcelCellx(a.domcellcode, a.dcell[p1])) - g.xoff;
-    own = lcx >= g.xown0 && lcx < g.xown1;
-  }
+  if (valid && g.split()) own = slab_owned(g, slab_local(g, a.domcellcode, a.dcell[p1]));  // slab: owned p1 only
   if (valid && own) {
     const float4 bn = a.normal[a.idp[p1]];
     if (bn.x != 0.f || bn.y != 0.f || bn.z != 0.f) {
@@ -168,9 +165,10 @@ __global__ __launch_bounds__(256) void k_mdbc_list(const DevScalars* __restrict_
       // whole map clamps, as the reference's search does); a ghost node in a ghost column
       // is fine while its support stays off the grid edge
       {
-        const double edge0 = a.posminx + double(g.xoff) * a.scelld, edge1 = edge0 + double(g.ncx) * a.scelld;
+        const double pmin = g.axis ? a.posminy : a.posminx, gs = g.axis ? b.gy : b.gx;
+        const double edge0 = pmin + double(g.soff) * a.scelld, edge1 = edge0 + double(g.extent()) * a.scelld;
         const double ks = double(a.kernelsize) * (1.0 + 1e-6);
-        if ((b.gx - ks < edge0 && g.xown0 > 0) || (b.gx + ks >= edge1 && g.xown1 < g.ncx))
+        if ((gs - ks < edge0 && g.sown0 > 0) || (gs + ks >= edge1 && g.sown1 < g.extent()))
           atomicOr(&const_cast<DevScalars*>(sc)->error_flags, ERR_HALO_NODE);
       }
       unsigned tot = 0;
@@ -521,7 +519,7 @@ __global__ __launch_bounds__(256) void k_mdbc_face_pack(const DevScalars* __rest
   if (p >= sc->npb && CodeType(a.code[p]) != CODE_TYPE_FLOATING) return;
   const unsigned id = a.idp[p];
   if (id < nbidx) bidx[id] = p;
-  const int lcx = int(DcelCellx(K.domcellcode, a.dcell[p])) - g.xoff;
+  const int lcx = slab_local(g, K.domcellcode, a.dcell[p]);
   // a slab of one owned column sends the same particle both ways
   for (int side = 0; side < 2; side++) {
     MdbcFaceRec* dst = nullptr;

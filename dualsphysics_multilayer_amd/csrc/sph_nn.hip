@@ -98,8 +98,7 @@ __device__ __forceinline__ float nn_eta(bool bi, float dmag, float tau_yield, fl
   if (dmag <= ALMOSTZERO) dmag = ALMOSTZERO;
   // visco * D^(n-1), exactly visco for n = 1 (a per-wave skip for n = 1 / m = 0 measured
   // neutral-to-slower at cfg5)
-  float miou_hb = visco;
-  miou_hb = visco * fexp2(c.z * flog2(dmag));
+  const float miou_hb = visco * fexp2(c.z * flog2(dmag));
   const float e = 1.f - fexp2(c.y * dmag);  // 1 - exp(-m D)
   if (!bi) {
     const float miou_pap = tau_yield * frcp(2.f * dmag) * e;
@@ -884,10 +883,10 @@ void launch_nn_tiled(hipStream_t stm, unsigned nblocks, DevScalars* sc, const ui
   } else if (K.nntvisco == 1) SPH_NN_TD(1, SH)                                 \
   else if (K.nntvisco == 2) SPH_NN_TD(2, SH)                                   \
   else SPH_NN_TD(3, SH)
-#ifdef SPH_NN_DIAG_CFG5
+#ifdef SPH_DIAG_HEADLINE_ONLY
   // diagnostic builds (kernel A/B at cfg5 only): the one instantiation pair of BASELINE cfg5
   if (K.nnvelgrad == 2 || K.nntvisco != 2 || K.tdensity != 3 || ftmassp || K.scelldiv != 1)
-    throw std::runtime_error("SPH_NN_DIAG_CFG5 build: cfg5 only");
+    throw std::runtime_error("SPH_DIAG_HEADLINE_ONLY build: cfg2 / cfg5 kernels only");
   if (shift) hipLaunchKernelGGL((k_nn_tiled<2, 3, true, 1, false>), dim3(fit_grid((const void*)&k_nn_tiled<2, 3, true, 1, false>, nblocks)), dim3(TB), 0, stm, sc, items, qctr,
                                 poscell, velrhop, press, code, begincell, g, K, phases, arace, shiftpos, viscoeta, tau,
                                 ftmassp);
@@ -1284,12 +1283,12 @@ __global__ __launch_bounds__(256) void k_nn_face_pack(DevScalars* __restrict__ s
   if (p < sc->npb) return;  // fluid only (bound p2 use p1's values)
   const unsigned dc = a.dcell[p];
   if (dc >= DCELL_DISCARD) return;
-  const int lcx = int(DcelCellx(K.domcellcode, dc)) - g.xoff;
+  const int lcx = slab_local(g, K.domcellcode, dc);
   for (int side = 0; side < 2; side++) {  // a slab of one owned column sends a particle both ways
     NNFaceRec* dst = nullptr;
     unsigned cap = 0;
-    if (side == 0 && in_left_face(g, lcx) && g.xown0 > 0) { dst = sl; cap = capl; }
-    if (side == 1 && in_right_face(g, lcx) && g.xown1 < g.ncx) { dst = sr; cap = capr; }
+    if (side == 0 && in_left_face(g, lcx) && g.sown0 > 0) { dst = sl; cap = capl; }
+    if (side == 1 && in_right_face(g, lcx) && g.sown1 < g.extent()) { dst = sr; cap = capr; }
     if (!dst) continue;
     const unsigned k = atomicAdd(&dst[0].idp, 1u);
     if (k + 1 >= cap) {  // the buffers hold every ghost sent at the divide; if not, say so

@@ -37,42 +37,13 @@ struct PackArgs {
   int W;
 };
 
-// ---- face boxes (sph_kernels.hpp SlabFaces) ----
-// Key of face box idx whose first column is the local column x0.
-__device__ __forceinline__ unsigned face_key(const DivGrid& g, int W, unsigned idx, int x0) {
-  const unsigned xrel = idx % unsigned(W);
-  unsigned t = idx / unsigned(W);
-  const unsigned y = t % unsigned(g.ncy);
-  t /= unsigned(g.ncy);
-  const unsigned z = t % unsigned(g.ncz), type = t / unsigned(g.ncz);
-  return (type ? g.boxfluid : 0u) + unsigned(x0) + xrel + y * unsigned(g.ncx) + z * g.nsheet;
-}
-// Face box of a box key (-1: not a cell box of the W columns from x0).
-__device__ __forceinline__ int face_idx(const DivGrid& g, int W, unsigned key, int x0) {
-  unsigned type, cs;
-  if (key < g.nct) {
-    type = 0u;
-    cs = key;
-  } else if (key >= g.boxfluid && key < g.boxfluid + g.nct) {
-    type = 1u;
-    cs = key - g.boxfluid;
-  } else {
-    return -1;
-  }
-  const int x = int(cs % unsigned(g.ncx)) - x0;
-  const unsigned r = cs / unsigned(g.ncx);
-  if (x < 0 || x >= W) return -1;
-  return int(((type * unsigned(g.ncz) + r / unsigned(g.ncy)) * unsigned(g.ncy) + r % unsigned(g.ncy)) * unsigned(W) +
-             unsigned(x));
-}
-
 // bit 0: record for the left neighbour, bit 1: record for the right, bit 2: stays owned
 // (so a record with bit 2 is a ghost copy, without it a migrant).
 __device__ __forceinline__ unsigned pack_class_dc(const PackArgs& q, unsigned dc) {
   if (dc == DCELL_DISCARD || dc == DCELL_OUT) return 0u;
-  const int lcx = int(DcelCellx(q.dcc, dc)) - q.g.xoff;
-  if (lcx < q.g.xown0) return q.has_left ? 1u : 0u;
-  if (lcx >= q.g.xown1) return q.has_right ? 2u : 0u;
+  const int lcx = slab_local(q.g, q.dcc, dc);
+  if (lcx < q.g.sown0) return q.has_left ? 1u : 0u;
+  if (lcx >= q.g.sown1) return q.has_right ? 2u : 0u;
   unsigned c = 4u;
   if (in_left_face(q.g, lcx) && q.has_left) c |= 1u;
   if (in_right_face(q.g, lcx) && q.has_right) c |= 2u;
@@ -119,8 +90,8 @@ __global__ __launch_bounds__(PK_BS) void k_pack_count(const DevScalars* __restri
       c4[4] += (c >> 2) & 1u;
       if (q.fcnt[0] && (c & 4u) && (c & 3u)) {
         const unsigned key = box_key(dcs[it], q.a.code[p], q.g, q.dcc);
-        if (c & 1u) fi[0] = face_idx(q.g, q.W, key, q.g.xown0);
-        if (c & 2u) fi[1] = face_idx(q.g, q.W, key, q.g.xown1 - q.W);
+        if (c & 1u) fi[0] = face_idx(q.g, q.W, key, q.g.sown0);
+        if (c & 2u) fi[1] = face_idx(q.g, q.W, key, q.g.sown1 - q.W);
       }
     }
     if (q.fcnt[0]) {
@@ -344,7 +315,7 @@ void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartA
                       unsigned nbound, const SlabFaces* faces) {
   PackArgs q;
   q.fcnt[0] = q.fcnt[1] = nullptr;
-  q.W = g.xown0;
+  q.W = g.sown0;
   if (faces) {  // zero on entry: k_face_scan / k_unpack_finish of the last exchange reset them
     q.fcnt[0] = faces->msg[0] + FMSG_HDR;
     q.fcnt[1] = faces->msg[1] + FMSG_HDR;
@@ -453,8 +424,8 @@ __global__ __launch_bounds__(256) void k_ghost_keys(SlabFaces f, DivGrid g, unsi
   const unsigned n = f.msg[2 + side][FMSG_HDR + idx];
   if (!n) return;
   const unsigned e0 = (side ? ngl : 0u) + f.pre[2 + side][idx];
-  // the left ghost columns are [0, W), the right ones [xown1, xown1 + W)
-  const unsigned key = face_key(g, f.W, idx, side ? g.xown1 : 0);
+  // the left ghost rim is [0, W), the right one [sown1, sown1 + W)
+  const unsigned key = face_key(g, f.W, idx, side ? g.sown1 : 0);
   for (unsigned j = 0; j < n; j++) {
     keys[e0 + j] = key;
     if (vals) vals[e0 + j] = vbase + e0 + j;
@@ -489,7 +460,7 @@ __global__ __launch_bounds__(256) void k_ghost_pack(DevScalars* __restrict__ sc,
     if (pre[mid] <= r) lo = mid;
     else hi = mid;
   }
-  const unsigned key = face_key(g, f.W, lo, side ? g.xown1 - f.W : g.xown0);
+  const unsigned key = face_key(g, f.W, lo, side ? g.sown1 - f.W : g.sown0);
   const unsigned i = bc[key] + (r - pre[lo]);
   if (i >= bc[key + 1]) {  // the divide placed fewer particles in the box than were counted
     atomicOr(&sc->error_flags, ERR_HALO_GHOST);
@@ -622,9 +593,8 @@ __global__ __launch_bounds__(256) void k_column_counts(const DevScalars* __restr
   if (p >= sc->np) return;
   const unsigned dc = a.dcell[p];
   if (dc == DCELL_DISCARD || dc == DCELL_OUT) return;
-  const int gcx = int(DcelCellx(dcc, dc));
-  const int lcx = gcx - g.xoff;
-  if (lcx < g.xown0 || lcx >= g.xown1 || gcx >= ncxg) return;  // ghosts are counted by their owner
+  const int lcx = slab_local(g, dcc, dc), gcx = lcx + g.soff;
+  if (!slab_owned(g, lcx) || gcx >= ncxg) return;  // ghosts are counted by their owner
   const bool fluid = CodeType(a.code[p]) >= CODE_TYPE_FLOATING;
   atomicAdd(&cnt[(fluid ? 0 : ncxg) + gcx], 1u);
 }

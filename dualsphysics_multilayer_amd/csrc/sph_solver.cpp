@@ -29,6 +29,16 @@ static bool trace_slab() {
       std::fprintf(stderr, "slabtrace rank %d step %llu %s\n", slabcfg_.rank, stepsdone_, what);          \
   } while (0)
 
+// Test hooks read from the environment (buffer sizing, item cutting, slab turns) change how a
+// run is executed, never its results; a production run must not pick one up silently, so the
+// first one met is reported once on stderr.
+void test_hook_notice(const char* name) {
+  static bool said = false;
+  if (said) return;
+  said = true;
+  std::fprintf(stderr, "libsphcore: test hook %s is set in the environment (measurement / test mode)\n", name);
+}
+
 void check_hip(hipError_t e, const char* what) {
   if (e != hipSuccess) throw SphError(SPH_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -303,28 +313,32 @@ int ghost_width(const SphConstants& c) { return int(c.scelldiv) + (c.tboundary =
 int min_slab_width(const SphConstants& c) { return 2 * ghost_width(c); }
 
 // Full-map cell grid (JCellDivCpuSingle::PrepareNct, JCellDivCpuSingle.cpp:105-121, with CellDomFixed).
-// A slab keeps the global y/z extent and the x-columns [c0-W, c1+W) (owned + W ghost
-// columns per face, W = ghost_width).
+// A slab keeps the global extent of the other two axes and the cells [c0-W, c1+W) of its
+// slab axis (owned + W ghost cells per face, W = ghost_width).
 static DivGrid make_grid(const SphConstants& c, const SlabConfig* slab) {
   DivGrid g;
   g.ncx = int(c.dom_cells[0]);
   g.ncy = int(c.dom_cells[1]);
   g.ncz = int(c.dom_cells[2]);
-  g.xoff = 0;
-  g.xown0 = 0;
-  g.xown1 = g.ncx;
+  g.axis = 0;
+  g.soff = 0;
+  g.sown0 = 0;
+  g.sown1 = g.ncx;
   if (slab) {
     const int W = ghost_width(c);
     const bool both = slab->rank > 0 && slab->rank + 1 < slab->nranks;
+    if (slab->axis != 0 && slab->axis != 1) throw SphError(SPH_ERR_ARG, "slab axis must be 0 (x) or 1 (y)");
+    const int ext = slab->axis ? g.ncy : g.ncx;
     if (slab->nranks < 1 || slab->rank < 0 || slab->rank >= slab->nranks || slab->c0 < 0 ||
-        slab->c1 < slab->c0 + (both ? min_slab_width(c) : W) || slab->c1 > g.ncx)
+        slab->c1 < slab->c0 + (both ? min_slab_width(c) : W) || slab->c1 > ext)
       throw SphError(SPH_ERR_ARG,
-                     "invalid slab columns (a slab owns at least 2W columns, W at a map end; W = the ghost width: "
-                     "scelldiv columns, +1 with mDBC)");
-    g.xoff = slab->c0 - W;
-    g.ncx = slab->c1 - slab->c0 + 2 * W;
-    g.xown0 = W;
-    g.xown1 = W + slab->c1 - slab->c0;
+                     "invalid slab cells (a slab owns at least 2W cells of its axis, W at a map end; W = the ghost "
+                     "width: scelldiv cells, +1 with mDBC)");
+    g.axis = slab->axis;
+    g.soff = slab->c0 - W;
+    (slab->axis ? g.ncy : g.ncx) = slab->c1 - slab->c0 + 2 * W;
+    g.sown0 = W;
+    g.sown1 = W + slab->c1 - slab->c0;
   }
   g.nsheet = unsigned(g.ncx) * unsigned(g.ncy);
   const unsigned long long nct = (unsigned long long)g.nsheet * unsigned(g.ncz);
@@ -341,11 +355,11 @@ static DivGrid make_grid(const SphConstants& c, const SlabConfig* slab) {
   return g;
 }
 
-// Global x-cell column of every initial particle (JSph::LoadDcellParticles, JSph.cpp:1690-1711).
-static std::vector<unsigned> initial_columns(const SphConstants& C, const SphParticlesHost& h) {
+// Global cell of every initial particle along `axis` (JSph::LoadDcellParticles, JSph.cpp:1690-1711).
+static std::vector<unsigned> initial_columns(const SphConstants& C, const SphParticlesHost& h, int axis) {
   std::vector<unsigned> cx(h.n);
   for (unsigned p = 0; p < h.n; p++) {
-    const double dx = h.pos[3 * p] - C.dom_posmin[0];
+    const double dx = h.pos[3 * p + axis] - C.dom_posmin[axis];
     cx[p] = dx >= 0 ? unsigned(dx / double(C.scell)) : 0u;
   }
   return cx;
@@ -406,15 +420,17 @@ void partition_from_prefix(const std::vector<double>& pre, int nranks, int* b, i
   }
 }
 
-void slab_partition(const SphCaseDef& cdef, const SphParticlesHost& all, int nranks, double bound_weight, int* b) {
+void slab_partition(const SphCaseDef& cdef, const SphParticlesHost& all, int nranks, double bound_weight, int* b,
+                    int axis) {
   SphConstants C;
   derive_constants(cdef, C);
-  const int ncx = int(C.dom_cells[0]), W = min_slab_width(C);
+  if (axis != 0 && axis != 1) throw SphError(SPH_ERR_ARG, "slab axis must be 0 (x) or 1 (y)");
+  const int ncx = int(C.dom_cells[axis]), W = min_slab_width(C);
   if (nranks < 1 || (nranks > 1 && nranks * W > ncx))
-    throw SphError(SPH_ERR_ARG, "nranks must be in [1, x-cells / (2 x ghost width)]");
+    throw SphError(SPH_ERR_ARG, "nranks must be in [1, cells of the slab axis / (2 x ghost width)]");
   if (all.n != cdef.np) throw SphError(SPH_ERR_ARG, "particle count does not match the case");
   std::vector<double> w(size_t(ncx), 0.0);
-  const std::vector<unsigned> cx = initial_columns(C, all);
+  const std::vector<unsigned> cx = initial_columns(C, all, axis);
   for (unsigned p = 0; p < all.n; p++) w[std::min<unsigned>(cx[p], unsigned(ncx - 1))] += (p < cdef.npb ? bound_weight : 1.0);
   std::vector<double> pre(size_t(ncx) + 1, 0.0);
   for (int c = 0; c < ncx; c++) pre[size_t(c) + 1] = pre[size_t(c)] + w[size_t(c)];
@@ -445,7 +461,7 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   std::vector<unsigned> sel;
   unsigned nown = init.n;
   if (slab()) {
-    const std::vector<unsigned> cx = initial_columns(C, init);
+    const std::vector<unsigned> cx = initial_columns(C, init, slabcfg_.axis);
     const int W = ghost_width(C);
     const int lo = slabcfg_.c0 - (slabcfg_.rank > 0 ? W : 0);
     const int hi = slabcfg_.c1 + (slabcfg_.rank + 1 < slabcfg_.nranks ? W : 0);
@@ -466,11 +482,18 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
   const unsigned n = unsigned(sel.size());
   if (const char* e = std::getenv("SPH_SLAB_MINCAP")) slab_mincap_ = slab() && std::atoi(e) != 0;
   if (const char* e = std::getenv("SPH_SLAB_CUT")) cut_items_ = slab() && std::atoi(e) != 0;
+  if (slab_mincap_ || cut_items_) test_hook_notice(slab_mincap_ ? "SPH_SLAB_MINCAP" : "SPH_SLAB_CUT");
   cap_ = slab() ? n + (slab_mincap_ ? 16u : std::max(n / 2, 65536u)) : n;
   keybits_ = bits_for(G.boxdiscard, 1);
-  // grid-sized buffers hold the widest grid a slab can get from a re-partition (all
-  // columns + W = ghost_width ghost columns per face), so they never move
-  nctmax_ = slab() ? unsigned(int(C.dom_cells[0]) + 2 * ghost_width(C)) * unsigned(G.ncy) * unsigned(G.ncz) : G.nct;
+  // grid-sized buffers hold the widest grid a slab can get from a re-partition (all cells
+  // of the slab axis + W = ghost_width ghost cells per face), so they never move
+  gmax_ncx_ = int(C.dom_cells[0]) + (slab() && slabcfg_.axis == 0 ? 2 * ghost_width(C) : 0);
+  gmax_ncy_ = int(C.dom_cells[1]) + (slab() && slabcfg_.axis == 1 ? 2 * ghost_width(C) : 0);
+  nctmax_ = slab() ? unsigned(gmax_ncx_) * unsigned(gmax_ncy_) * unsigned(G.ncz) : G.nct;
+  if (slab() && slabcfg_.axis == 1) {
+    if (C.dom_cells[1] < 2u) throw SphError(SPH_ERR_UNSUPPORTED, "y-slabs of a 2-D case (one y row)");
+    if (C.symmetry) throw SphError(SPH_ERR_UNSUPPORTED, "Symmetry (the y = 0 mirror) on y-slabs");
+  }
   if (const char* e = std::getenv("SPH_INTERACTION")) tiled_ = std::string(e) != "simple";
   if (const char* e = std::getenv("SPH_COMM_TIMEOUT_S")) comm_timeout_s_ = std::max(1.0, std::atof(e));
   // incremental divide: distinct key offsets of the 27 neighbour cells (ncx >= 3, checked
@@ -497,7 +520,7 @@ void SphGpuSingle::Init(const SphCaseDef& cdef, const SphParticlesHost& init) {
     // the first interaction's face records (NN / SPS / mDBC face re-sends): the initial
     // particles of the face and ghost columns (both sides of a face count the same
     // particles); later from each exchange
-    const std::vector<unsigned> cx = initial_columns(C, init);
+    const std::vector<unsigned> cx = initial_columns(C, init, slabcfg_.axis);
     const bool hl = slabcfg_.rank > 0, hr = slabcfg_.rank + 1 < slabcfg_.nranks;
     const int W = ghost_width(C), c0 = slabcfg_.c0, c1 = slabcfg_.c1;
     for (unsigned p : sel) {
@@ -562,15 +585,16 @@ void SphGpuSingle::AllocFixed() {
   };
   begincell_ = (unsigned*)dmalloc(4 * (2 * size_t(nctmax_) + 6));
   if (slab()) {  // re-partition: column counts [2 ncx] + the ranks' bounds [nranks + 1]
-    colcnt_ = (float*)dmalloc(4 * (2 * size_t(C.dom_cells[0]) + size_t(slabcfg_.nranks) + 1));
+    colcnt_ = (float*)dmalloc(4 * (2 * size_t(C.dom_cells[slabcfg_.axis]) + size_t(slabcfg_.nranks) + 1));
   }
-  rowtmp_ = (unsigned*)dmalloc(4 * ITEMS_ROWTMP(G.ncy, G.ncz));  // two lists x (fluid, bound) rows of item counts
+  // two lists x (fluid, bound) rows of item counts, for the widest grid of the run
+  rowtmp_ = (unsigned*)dmalloc(4 * ITEMS_ROWTMP(std::max(G.ncy, gmax_ncy_), G.ncz));
   // the count pass's staged items (sph_items.hpp), sized for the widest grid of the run
-  ricap_ = ITEMS_RICAP(int(nctmax_ / (unsigned(G.ncy) * unsigned(G.ncz))));
+  ricap_ = ITEMS_RICAP(std::max(G.ncx, gmax_ncx_));
   // test hook: smaller slots send more rows down the place pass's second walk
   // (tests/test_gpu_items.py checks the run is bitwise the same)
   if (const char* e = std::getenv("SPH_ITEMS_RICAP")) ricap_ = std::max(1u, std::min(ricap_, unsigned(std::atoi(e))));
-  rowitems_ = (uint4*)dmalloc(sizeof(uint4) * (ITEMS_ROWTMP(G.ncy, G.ncz) - 1) * ricap_);
+  rowitems_ = (uint4*)dmalloc(sizeof(uint4) * (ITEMS_ROWTMP(std::max(G.ncy, gmax_ncy_), G.ncz) - 1) * ricap_);
   qctr_ = (unsigned*)dmalloc(QCTR_BYTES);
   check_hip(hipMemset(qctr_, 0, QCTR_BYTES), "zero work counters");
   sort_.digtot = (unsigned*)dmalloc(4 * (1u << RS_MAXBITS));
@@ -595,7 +619,7 @@ void SphGpuSingle::AllocFixed() {
     // face messages and their prefixes (the ghost exchange after the divide); the second
     // item list and its counters
     faces_.W = ghost_width(C);
-    faces_.nfb = 2u * unsigned(G.ncy) * unsigned(G.ncz) * unsigned(faces_.W);
+    faces_.nfb = 2u * face_boxes_per_type(G, faces_.W);  // the full extent of the other axes: fixed
     for (int k = 0; k < 4; k++) {
       // the send messages' face-box counts accumulate in k_pack_count from zero; k_face_scan
       // zeroes them again once it has their prefixes
@@ -732,16 +756,17 @@ void SphGpuSingle::Free() {
   slabcnt_host_ = nullptr;
 }
 
-// Slab exchange buffers sized once from the case, from its densest x column: W face
-// columns of ghosts per face (+50 %), a quarter of that in migrants.  The face messages then
+// Slab exchange buffers sized once from the case, from its densest cell slice along the
+// slab axis: W face slices of ghosts per face (+50 %), a quarter of that in migrants.  The face messages then
 // need no hipMalloc (and no stream synchronisation) mid-run; the grow paths of Exchange()
 // stay as the fallback for a flow that piles particles into a face column or a re-partition
 // that hands over many columns at once.
 void SphGpuSingle::PresizeExchange(const SphParticlesHost& h) {
-  std::vector<unsigned> cnt(size_t(C.dom_cells[0]) + 1, 0u);
+  const int ax = slabcfg_.axis;
+  std::vector<unsigned> cnt(size_t(C.dom_cells[ax]) + 1, 0u);
   unsigned mx = 0;
   for (unsigned p = 0; p < h.n; p++) {
-    const double x = (h.pos[3 * p] - C.dom_posmin[0]) / double(C.scell);
+    const double x = (h.pos[3 * p + ax] - C.dom_posmin[ax]) / double(C.scell);
     if (!(x >= 0.0)) continue;
     const size_t cx = size_t(x);
     if (cx < cnt.size()) mx = std::max(mx, ++cnt[cx]);
@@ -1134,7 +1159,7 @@ void SphGpuSingle::WaitEvent(hipEvent_t ev, const char* what) {
 // (the usual pack rule) give the neighbours their ghost columns during the hand-over.
 // Called between an update and the divide (all ranks, same step).
 void SphGpuSingle::Repartition() {
-  const int ncxg = int(C.dom_cells[0]), nr = slabcfg_.nranks;
+  const int ncxg = int(C.dom_cells[slabcfg_.axis]), nr = slabcfg_.nranks;
   launch_column_counts(stream, cap_, sc_, cur_, G, K, ncxg, colcnt_);
   std::vector<float> bnd(size_t(nr) + 1, 0.f);
   bnd[size_t(slabcfg_.rank)] = float(slabcfg_.c0);  // each rank contributes its own bound
@@ -1200,7 +1225,7 @@ void SphGpuSingle::ShareDeviceCheck() {
   check_hip(hipStreamSynchronize(stream), "device check");
   (void)hipFree(d);
   for (int r = 0; r < nr; r++)
-    if (r != slabcfg_.rank && v[size_t(r)] == mine) overlap_ = false;
+    if (r != slabcfg_.rank && v[size_t(r)] == mine) MarkSharedDevice();
 }
 
 void SphGpuSingle::SetRepartition(unsigned every, double bound_weight, double tolerance) {
@@ -1238,16 +1263,17 @@ void SphGpuSingle::RunCellDivide() {
   ItemBuild ib;
   if (tiled_) {
     const int S = int(C.scelldiv), hl = slab() && transport_->has_left(), hr = slab() && transport_->has_right();
-    int ib0 = G.xown0 + (hl ? S : 0), ie0 = G.xown1 - (hr ? S : 0);
-    if (ib0 >= ie0) ib0 = ie0 = G.xown0;  // a narrow slab: every item reaches a ghost column
-    const bool inc = inc_ok_ && inc_valid_ && G.ncx >= 3;
+    // the owned cells along the slab axis whose stencil (scelldiv cells) reaches no ghost
+    int ib0 = G.sown0 + (hl ? S : 0), ie0 = G.sown1 - (hr ? S : 0);
+    if (ib0 >= ie0) ib0 = ie0 = G.sown0;  // a narrow slab: every item reaches a ghost cell
+    const bool inc = inc_ok_ && inc_valid_ && G.ncx >= 3 && (G.ncy >= 3 || G.ncy == 1);
     const unsigned* bcnew = inc ? begincell_alt_ : begincell_;  // the begincell this divide writes
     if (overlap) {  // the interior list (qctr_), then the face list (qctrf_) after it
-      const int xr[6] = {ib0, ie0, G.xown0, ib0, ie0, G.xown1};
+      const int xr[6] = {ib0, ie0, G.sown0, ib0, ie0, G.sown1};
       ib = make_item_build(bcnew, G, rowtmp_, items_, qctr_, C.scelldiv, xr, qctrf_, rowitems_, ricap_);
       ghost_split_ = true;
     } else if (cut_items_) {  // the overlap's items in one list (SPH_SLAB_CUT test hook)
-      const int xa[6] = {G.xown0, ib0, ib0, ie0, ie0, G.xown1};
+      const int xa[6] = {G.sown0, ib0, ib0, ie0, ie0, G.sown1};
       ib = make_item_build(bcnew, G, rowtmp_, items_, qctr_, C.scelldiv, xa, nullptr, rowitems_, ricap_);
     } else {
       // ghosts in place: the rows' items over all owned columns, as in one domain (a row cut
@@ -1255,7 +1281,7 @@ void SphGpuSingle::RunCellDivide() {
       ib = make_item_build(bcnew, G, rowtmp_, items_, qctr_, C.scelldiv, nullptr, nullptr, rowitems_, ricap_);
     }
   }
-  if (inc_ok_ && inc_valid_ && G.ncx >= 3) {
+  if (inc_ok_ && inc_valid_ && G.ncx >= 3 && (G.ncy >= 3 || G.ncy == 1)) {
     // the previous order merged with the particles whose box changed and, on a slab, the
     // particles the exchange appended and the ghosts' slots (sph_divide.hip); the item
     // count runs in the push launch, the item write right after it
@@ -1272,7 +1298,7 @@ void SphGpuSingle::RunCellDivide() {
     const int res = launch_radix_sort(stream, cap_, sc_, sort_, keybits_);
     launch_begincell(stream, cap_, sc_, sort_.keys[res], G, begincell_);
     launch_gather(stream, cap_, sc_, sort_.vals[res], cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_,
-                  G.xoff, nn_ ? phaseeos_ : nullptr, ghosts ? xg_np_ : ~0u, xg_np_ - xg_nm_, inc_.apppos);
+                  G.offx(), G.offy(), nn_ ? phaseeos_ : nullptr, ghosts ? xg_np_ : ~0u, xg_np_ - xg_nm_, inc_.apppos);
     if (inc_ok_)
       check_hip(hipMemcpyAsync(inc_.skeys, sort_.keys[res], 4 * size_t(cap_), hipMemcpyDeviceToDevice, stream),
                 "keep sorted keys");
@@ -1407,8 +1433,8 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
       // (packed and posted there after the divide); there the face items follow their
       // arrival.  The interior kernel leaves a few block slots free so that the transfer and
       // scatter kernels start at once.
-      launch_fluid_tiled(stream, nblocks_tiled_ - 64, sc_, items_, qa, poscell_, cur_.velrhop, press_, begincell_,
-                         G, K, arace_, cur_.code, ftmassp_);
+      launch_fluid_tiled(stream, nblocks_tiled_, sc_, items_, qa, poscell_, cur_.velrhop, press_, begincell_, G, K,
+                         arace_, cur_.code, ftmassp_, 64);
       GhostCollect(xstream_);
       launch_fluid_tiled(xstream_, nblocks_tiled_, sc_, items_, qf, poscell_, cur_.velrhop, press_, begincell_, G,
                          K, arace_, cur_.code, ftmassp_);
@@ -1904,8 +1930,7 @@ void SphGpuSingle::Download(SphParticlesHost& out) {
   unsigned k = 0;
   for (unsigned p = 0; p < n; p++) {
     if (slab()) {  // owned particles only
-      const int lcx = int(DcelCellx(C.dom_cellcode, dcell[p])) - G.xoff;
-      if (lcx < G.xown0 || lcx >= G.xown1) continue;
+      if (!slab_owned(G, slab_local(G, C.dom_cellcode, dcell[p]))) continue;
     }
     if (out.idp) out.idp[k] = idp[p];
     if (out.code) out.code[k] = code[p];
@@ -1954,7 +1979,7 @@ void SphGpuSingle::CountPairs(uint64_t out[6]) {
 
 // ---- in-process slab group -----------------------------------------------------------
 SphSlabGroup::SphSlabGroup(const SphCaseDef& cdef, const SphParticlesHost& all, int nslabs, const int* devices,
-                           const int* bounds)
+                           const int* bounds, int axis)
     : hub_(std::make_shared<LocalHub>(nslabs)) {
   if (nslabs < 1) throw SphError(SPH_ERR_ARG, "nslabs < 1");
   for (int i = 0; i < nslabs; i++) {
@@ -1963,6 +1988,7 @@ SphSlabGroup::SphSlabGroup(const SphCaseDef& cdef, const SphParticlesHost& all, 
     sc.nranks = nslabs;
     sc.c0 = bounds[i];
     sc.c1 = bounds[i + 1];
+    sc.axis = axis;
     slabs.emplace_back(new SphGpuSingle(cdef, all, devices[i], sc, make_local_transport(hub_, i)));
   }
   // Slabs sharing a GPU: the ghosts go before the interaction (one item list).  There the
@@ -1972,7 +1998,7 @@ SphSlabGroup::SphSlabGroup(const SphCaseDef& cdef, const SphParticlesHost& all, 
   // Slabs on their own GPUs keep the overlap (sph_slab_group_set_overlap changes either).
   for (int i = 0; i < nslabs; i++)
     for (int j = 0; j < nslabs; j++)
-      if (i != j && devices[i] == devices[j]) slabs[i]->SetOverlap(false);
+      if (i != j && devices[i] == devices[j]) slabs[i]->MarkSharedDevice();
 }
 
 void SphSlabGroup::Run(unsigned nsteps) {

@@ -27,13 +27,15 @@ struct SphError : std::runtime_error {
 };
 
 void check_hip(hipError_t e, const char* what);
+void test_hook_notice(const char* name);
 void derive_constants(const SphCaseDef& c, SphConstants& k);
 // Ghost columns per slab face (scelldiv, +1 with mDBC).
 int ghost_width(const SphConstants& c);
 // Narrowest slab between two neighbours (2 x ghost width).
 int min_slab_width(const SphConstants& c);
-// Column bounds of a particle-count-balanced x-slab split (sph_slab_partition).
-void slab_partition(const SphCaseDef& c, const SphParticlesHost& all, int nranks, double bound_weight, int* bounds);
+// Cell bounds along `axis` (0 x, 1 y) of a particle-count-balanced slab split (sph_slab_partition).
+void slab_partition(const SphCaseDef& c, const SphParticlesHost& all, int nranks, double bound_weight, int* bounds,
+                    int axis = 0);
 void partition_from_prefix(const std::vector<double>& prefix, int nranks, int* bounds, int minw = 1);
 // PART / case files (sph_bi4.cpp)
 void part_read(const std::string& path, SphPartHeader& h, SphParticlesHost* out);
@@ -51,7 +53,8 @@ void normals_write(const std::string& path, const char* case_name, double dp, do
 
 // This rank's slab: owned global x-cell columns [c0, c1) of nranks.
 struct SlabConfig {
-  int rank = 0, nranks = 1, c0 = 0, c1 = 0;
+  int rank = 0, nranks = 1, c0 = 0, c1 = 0;  // owned global cells [c0, c1) along the slab axis
+  int axis = 0;                              // 0: x-slabs, 1: y-slabs
 };
 
 class SphGpuSingle {
@@ -100,7 +103,13 @@ class SphGpuSingle {
   void SetRepartition(unsigned every, double bound_weight, double tolerance);
   // Slabs: run the interaction of the items that reach no ghost column while the ghost
   // records of the divide are in flight (default on; off = ghosts in place before it).
-  void SetOverlap(bool on) { overlap_ = on; }
+  // never on for a slab that shares its GPU with another slab of the run (ShareDeviceCheck,
+  // the in-process group constructor): the ghost overlap only pays with a GPU of its own
+  void SetOverlap(bool on) { overlap_ = on && !shared_device_; }
+  void MarkSharedDevice() {
+    shared_device_ = true;
+    overlap_ = false;
+  }
   // Collective over the slab's ranks (creation of separate-process ranks): the overlap off
   // when another rank runs on this rank's GPU (the shared-device rule of SphSlabGroup).
   void ShareDeviceCheck();
@@ -237,6 +246,7 @@ class SphGpuSingle {
   bool exchange_armed_ = false;  // the initial divide has no exchange (ghosts come with the case)
   double comm_timeout_s_ = 120.0;  // SPH_COMM_TIMEOUT_S: deadline of a slab host wait
   unsigned nctmax_ = 0;            // cells of the widest grid (grid-sized buffers)
+  int gmax_ncx_ = 0, gmax_ncy_ = 0;  // its x / y extents
   float* colcnt_ = nullptr;        // re-partition: column counts + bounds (device)
   unsigned repart_every_ = 0, repart_count_ = 0;
   double repart_bw_ = 0.3, repart_tol_ = 0.05, repart_last_imbalance_ = 1.0;
@@ -258,6 +268,7 @@ class SphGpuSingle {
   unsigned xg_np_ = 0;            // particles held after the migrants were appended
   bool ghost_pending_ = false;    // the last divide's ghost records have not been sent yet
   bool overlap_ = false;          // sph_slab_set_overlap (default off: DESIGN.md §6)
+  bool shared_device_ = false;    // another slab of the run uses the same GPU
   bool in_run_ = false;           // inside Run(): the next phase after a divide is the interaction
   hipStream_t xstream_ = nullptr; // ghost transfer + scatter + face items beside the interior items
   hipEvent_t ev_div_ = nullptr, ev_ghost_ = nullptr;
@@ -278,7 +289,7 @@ class SphGpuSingle {
 class SphSlabGroup {
  public:
   SphSlabGroup(const SphCaseDef& cdef, const SphParticlesHost& all, int nslabs, const int* devices,
-               const int* bounds);
+               const int* bounds, int axis = 0);
   void Run(unsigned nsteps);
   std::vector<std::unique_ptr<SphGpuSingle>> slabs;
 

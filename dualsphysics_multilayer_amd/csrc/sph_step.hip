@@ -129,9 +129,8 @@ void launch_dt(hipStream_t stm, DevScalars* sc, const KConst& K, double cfl, dou
 // Slab ghost: its local column is outside the owned range.  The owner updates it; here
 // it is only dropped at the next divide (fresh copies arrive with the exchange).
 __device__ __forceinline__ bool slab_ghost(const KConst& K, const DivGrid& g, unsigned* dcell, unsigned p) {
-  if (g.xown0 == 0 && g.xown1 == g.ncx) return false;  // single domain
-  const int lcx = int(DcelCellx(K.domcellcode, dcell[p])) - g.xoff;
-  if (lcx >= g.xown0 && lcx < g.xown1) return false;
+  if (!g.split()) return false;  // single domain
+  if (slab_owned(g, slab_local(g, K.domcellcode, dcell[p]))) return false;
   dcell[p] = DCELL_DISCARD;
   return true;
 }

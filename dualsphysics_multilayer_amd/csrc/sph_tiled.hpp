@@ -240,8 +240,10 @@ struct ItemCursor {
 // ran dry — and then still runs its static first item (ItemGroups): at cfg3 (DDT1, 129 VGPRs,
 // 3 waves per SIMD = 6 blocks per CU) 512 of 2048 blocks started 5.7 ms into a 5.8 ms launch,
 // and 26 % of the launch's block slots idled.  The occupancy of each kernel on the current
-// device is looked up once.
-inline unsigned fit_grid(const void* kernel, unsigned want, int threads = TB) {
+// device is looked up once.  `reserve` block slots are left free (the ghost overlap's
+// interior launch, so that the transfer and scatter kernels start at once): the cap by
+// residency comes first, then the reserve is taken off it (at least one block stays).
+inline unsigned fit_grid(const void* kernel, unsigned want, int threads = TB, unsigned reserve = 0) {
   static std::mutex m;
   static std::unordered_map<unsigned long long, unsigned> cache;
   int dev = 0;
@@ -255,7 +257,8 @@ inline unsigned fit_grid(const void* kernel, unsigned want, int threads = TB) {
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 1;
     it = cache.emplace(key, unsigned(perc) * unsigned(ncu)).first;
   }
-  return want < it->second ? want : it->second;
+  const unsigned cap = it->second > reserve ? it->second - reserve : 1u;
+  return want < cap ? want : cap;
 }
 
 // i-th of the 12 "lower" rows of the 5x5 CellMode=half stencil (dz < 0, or dz = 0 and

@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define SPH_ABI_VERSION 10
+#define SPH_ABI_VERSION 11
 
 typedef enum {
   SPH_OK = 0,
@@ -315,10 +315,12 @@ int sph_solver_set_timing(SphSolver* s, int enabled);
 int sph_solver_set_timing_phases(SphSolver* s, unsigned mask);
 int sph_solver_timing(SphSolver* s, double out_ms[4], uint64_t* launches);
 
-/* ---- slab decomposition over x -------------------------------
- * Rank r owns the global x-cell columns [cx_begin, cx_end) and holds ghost copies of
- * the neighbours' particles in the column either side (one column = 2h, the support
- * radius).  Every divide exchanges migrants and ghosts with rank-1 / rank+1, every
+/* ---- slab decomposition over x or y --------------------------
+ * Rank r owns the global cells [cx_begin, cx_end) of the slab axis (axis 0: x-cell
+ * columns, axis 1: y-cell rows; the full extent of the other axes) and holds ghost copies
+ * of the neighbours' particles in the W cells either side (one cell = 2h, the support
+ * radius).  y-slabs keep every x row of cells whole on one rank (no rows cut at the faces,
+ * whole-row items), for a domain whose load is spread along y (the dam breaks).  Every divide exchanges migrants and ghosts with rank-1 / rank+1, every
  * dt max-reduces VelMax/AceMax/ViscDtMax over all ranks, so every rank steps with the
  * single-domain dt and each particle sees its single-domain neighbour set.
  * On a slab solver: sph_solver_run and the phase calls are COLLECTIVE (all ranks
@@ -326,7 +328,9 @@ int sph_solver_timing(SphSolver* s, double out_ms[4], uint64_t* launches);
  * sph_download_particles returns the owned particles only. */
 typedef struct SphSlabDef {
   int32_t rank, nranks;
-  int32_t cx_begin, cx_end;       /* owned global x-cell columns [begin, end)        */
+  int32_t cx_begin, cx_end;       /* owned global cells [begin, end) of the slab axis  */
+  int32_t axis;                   /* 0: x-slabs (default), 1: y-slabs (3-D cases)       */
+  int32_t pad;
   unsigned char comm_id[128];     /* sph_comm_unique_id() of rank 0, same on all ranks */
 } SphSlabDef;
 
@@ -336,6 +340,9 @@ typedef struct SphSlabDef {
  * narrowest slab sph_slab_create accepts between two neighbours (W at a map end). */
 int sph_slab_partition(const SphCaseDef* cdef, const SphParticlesHost* all, int nranks, double bound_weight,
                        int32_t* cx_bounds);
+/* The same along `axis` (0 x, 1 y): bounds[nranks+1] in cells of that axis. */
+int sph_slab_partition_axis(const SphCaseDef* cdef, const SphParticlesHost* all, int nranks, double bound_weight,
+                            int axis, int32_t* bounds);
 int sph_comm_unique_id(unsigned char id[128]);
 /* One process per GPU over RCCL: every rank passes the FULL initial particle set
  * and keeps its owned + ghost columns. */
@@ -355,6 +362,8 @@ int sph_slab_create_shm(const SphCaseDef* cdef, const SphParticlesHost* all, int
 typedef struct SphSlabGroup SphSlabGroup;
 int sph_slab_group_create(const SphCaseDef* cdef, const SphParticlesHost* all, int nslabs, const int32_t* devices,
                           const int32_t* cx_bounds, SphSlabGroup** out);
+int sph_slab_group_create_axis(const SphCaseDef* cdef, const SphParticlesHost* all, int nslabs,
+                               const int32_t* devices, int axis, const int32_t* bounds, SphSlabGroup** out);
 int sph_slab_group_destroy(SphSlabGroup* g);
 int sph_slab_group_run(SphSlabGroup* g, uint32_t nsteps);
 int sph_slab_group_member(SphSlabGroup* g, int i, SphSolver** out);
@@ -380,9 +389,9 @@ int sph_slab_group_set_repartition(SphSlabGroup* g, uint32_t every, double bound
 int sph_slab_set_overlap(SphSolver* s, int on);
 int sph_slab_group_set_overlap(SphSlabGroup* g, int on);
 typedef struct SphSlabInfo {
-  int32_t rank, nranks, cx_begin, cx_end;  /* current owned columns [cx_begin, cx_end)        */
+  int32_t rank, nranks, cx_begin, cx_end;  /* current owned cells of the slab axis           */
   uint32_t repartitions;                   /* bounds changes so far                          */
-  uint32_t pad;
+  int32_t axis;                            /* the slab axis (0 x, 1 y)                       */
   double last_imbalance;                   /* max slab load / mean at the last check (1 = even) */
 } SphSlabInfo;
 int sph_slab_info(SphSolver* s, SphSlabInfo* out);

@@ -44,10 +44,10 @@ from dualsphysics_multilayer_amd.core import SphSlabGroup, slab_partition  # noq
 MODES = {"overlap": (1, 1), "inplace_cut": (0, 1), "inplace": (0, 0)}  # (overlap, cut)
 
 
-def run(case, bounds, mode, steps, warmup):
+def run(case, bounds, mode, steps, warmup, axis=0):
     overlap, cut = MODES[mode]
     os.environ["SPH_SLAB_CUT"] = str(cut)
-    g = SphSlabGroup(case, np.asarray(bounds, np.int32))
+    g = SphSlabGroup(case, np.asarray(bounds, np.int32), axis=axis)
     os.environ.pop("SPH_SLAB_CUT")
     g.set_overlap(bool(overlap))
     g.run(warmup)  # a group run returns with every slab synchronised
@@ -76,18 +76,19 @@ def main():
     ap.add_argument("--modes", default=None, help="comma-separated subset of the modes")
     ap.add_argument("--dp", type=float, default=0.00205)
     ap.add_argument("--bound-weight", type=float, default=None, help="slab_partition's bound weight (default 0.3)")
+    ap.add_argument("--axis", type=int, default=0, choices=(0, 1), help="slab axis: 0 x-slabs, 1 y-slabs")
     a = ap.parse_args()
     if os.environ.get("SPH_SLAB_TURNS") not in ("1", "2"):
         raise SystemExit("run with SPH_SLAB_TURNS=1 or 2 (the turns measurement modes)")
     case = DamBreakCase(a.dp, step_algorithm=2, tdensity=1)
-    bounds = [int(x) for x in (slab_partition(case, a.slabs) if a.bound_weight is None
-                                else slab_partition(case, a.slabs, a.bound_weight))]
-    res = {"workload": "cfg3", "np": int(case.np), "bounds": bounds, "steps": a.steps,
+    bw = 0.3 if a.bound_weight is None else a.bound_weight
+    bounds = [int(x) for x in slab_partition(case, a.slabs, bw, a.axis)]
+    res = {"workload": "cfg3", "np": int(case.np), "axis": a.axis, "bounds": bounds, "steps": a.steps,
            "turns_mode": int(os.environ["SPH_SLAB_TURNS"]), "bound_weight": a.bound_weight, "runs": []}
     modes = [a.only] if a.only is not None else (a.modes.split(",") if a.modes else list(MODES))
     for _ in range(a.repeat):
         for ov in modes:
-            r = run(case, bounds, ov, a.steps, a.warmup)
+            r = run(case, bounds, ov, a.steps, a.warmup, a.axis)
             res["runs"].append(r)
             print("progress", json.dumps(r), flush=True)
     summ = {}

@@ -81,25 +81,25 @@ class _SubCase:
         return self._cdef
 
 
-def _columns(case, k):
+def _columns(case, k, axis=0):
     # JSph::LoadDcellParticles: unsigned(dx / double(float scell)) with the map minimum
-    dx = case.pos[:, 0] - k["dom_posmin"][0]
+    dx = case.pos[:, axis] - k["dom_posmin"][axis]
     return np.floor(dx / np.float64(np.float32(k["scell"]))).astype(np.int64)
 
 
-def _halo_worker(rank, world, port):
+def _halo_worker(rank, world, port, axis=0):
     _init(rank, world, port)
     from dualsphysics_multilayer_amd.case import DamBreakCase
     from dualsphysics_multilayer_amd.core import case_derive, slab_partition
     from oracle.pyoracle import OracleSolver
 
     case = DamBreakCase(0.03, celldomfixed=True)
-    bounds = slab_partition(case, world, 0.3)
+    bounds = slab_partition(case, world, 0.3, axis)
     allb = [None] * world
     dist.all_gather_object(allb, bounds.tolist())
     assert all(b == allb[0] for b in allb), "ranks disagree on the partition"
     k = case_derive(case.case_def())
-    cx = _columns(case, k)
+    cx = _columns(case, k, axis)  # cells along the slab axis (x columns or y rows)
     c0, c1 = int(bounds[rank]), int(bounds[rank + 1])
     own = np.nonzero((cx >= c0) & (cx < c1))[0]
     # ghost exchange: my first column to the left, my last column to the right
@@ -210,13 +210,14 @@ def _protocol_worker(rank, world, port):
     dist.destroy_process_group()
 
 
-def _spawn(fn):
-    mp.spawn(fn, args=(WORLD, _free_port()), nprocs=WORLD, join=True)
+def _spawn(fn, *extra):
+    mp.spawn(fn, args=(WORLD, _free_port()) + extra, nprocs=WORLD, join=True)
 
 
-def test_halo_gives_single_domain_interaction():
+@pytest.mark.parametrize("axis", [0, 1], ids=["x_slabs", "y_slabs"])
+def test_halo_gives_single_domain_interaction(axis):
     pytest.importorskip("oracle.pyoracle")
-    _spawn(_halo_worker)
+    _spawn(_halo_worker, axis)
 
 
 def test_exchange_protocol_invariants():
