@@ -10,9 +10,10 @@ timed region starts.
 Workloads:
   cfg2 (default): 3D dam break, WCSPH + artificial viscosity + DDT2, Verlet.  N=1: the
         BASELINE cfg2 case (1,025,964 particles).  N>1 (torchrun, one process per GPU):
-        weak scaling — a dam break of ~N x 1,025,964 particles slab-decomposed over x
-        across the N ranks (RCCL halo/migration exchange + max-allreduce of the dt
-        maxima inside libsphcore); value = all particles x steps / max rank time.
+        weak scaling — a dam break of ~N x 1,025,964 particles slab-decomposed across the
+        N ranks (y-slabs by default for the dam breaks, --slab-axis; RCCL halo/migration
+        exchange + max-allreduce of the dt maxima inside libsphcore); value = all
+        particles x steps / max rank time.
   cfg3: BASELINE cfg3, 3D dam break of ~10M particles (dp 0.00205), Symplectic + DDT
         (Molteni, delta-SPH) 0.1, slab-split over N ranks (strong scaling).
   cfg4: BASELINE cfg4, wave flume of ~4.0M particles (dp 0.00265): piston (mvrectsinu) +
@@ -232,7 +233,7 @@ def measure(case, args, rank: int, world: int, device: int, dist, use_slab: bool
         # never degrades into per-GPU replicas.
         err = None
         try:
-            bounds = slab_partition(case, world, args.bound_weight)
+            bounds = slab_partition(case, world, args.bound_weight, args.axis)
             if args.transport == "shm":
                 import uuid
 
@@ -241,7 +242,7 @@ def measure(case, args, rank: int, world: int, device: int, dist, use_slab: bool
                 ids = [comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(ids, src=0)
             s = SphGpuSlab(case, rank, world, bounds, ids[0], device=device, transport=args.transport,
-                           slot_bytes=256 << 20)
+                           slot_bytes=256 << 20, axis=args.axis)
             if args.repartition and world > 1:
                 s.set_repartition(args.repartition, args.bound_weight, 0.05)
             s.run(presteps + warmup)
@@ -339,6 +340,9 @@ def main() -> None:
     ap.add_argument("--no-cfg3", action="store_true",
                     help="cfg2: skip the extra cfg3 (10M, Symplectic) timing (keys cfg3_1gpu / strong_scaling_cfg3)")
     ap.add_argument("--cfg3-steps", type=int, default=10, help="timed steps of the extra cfg3 measurement")
+    ap.add_argument("--slab-axis", choices=("auto", "x", "y"), default="auto",
+                    help="N>1 slab axis: y keeps every x row of cells whole on one rank (the dam breaks: "
+                         "their load is spread evenly along y; DESIGN.md §6); auto = y for cfg2/cfg3, x otherwise")
     ap.add_argument("--force-slab", action="store_true",
                     help="run the N>1 code path (gloo bootstrap + RCCL slab) even with one rank")
     args = ap.parse_args()
@@ -346,6 +350,7 @@ def main() -> None:
         args.presteps = max(0, 10 - args.warmup)
     if args.boundary is None:
         args.boundary = "mdbc" if args.workload == "cfg4" else "dbc"
+    args.axis = {"x": 0, "y": 1}.get(args.slab_axis, 1 if args.workload in ("cfg2", "cfg3") else 0)
 
     rank, world, local = dist_env()
     if args.gpus != world and world > 1:
@@ -397,7 +402,9 @@ def main() -> None:
     if args.workload == "cfg2" and not args.no_cfg3 and args.dp is None and args.cellmode == "full":
         t3 = time.perf_counter()
         c3 = DamBreakCase(CFG3_DP, step_algorithm=2, tdensity=1)
-        m3 = measure(c3, args, rank, world, device, dist, world > 1 or args.force_slab, args.cfg3_steps, 2, 0)
+        a3 = argparse.Namespace(**vars(args))
+        a3.axis = {"x": 0, "y": 1}.get(args.slab_axis, 1)  # the cfg3 dam break: y-slabs unless told otherwise
+        m3 = measure(c3, a3, rank, world, device, dist, world > 1 or args.force_slab, args.cfg3_steps, 2, 0)
         cfg3_extra = {"workload": "BASELINE cfg3: 3D dam break, %d particles (dp=%g), Symplectic, DDT (Molteni) "
                                   "0.1, DBC, CellMode full" % (c3.np, CFG3_DP),
                       "np": c3.np, "n_gpus": world, "steps": args.cfg3_steps, "warmup": 2,
@@ -405,8 +412,10 @@ def main() -> None:
                       "value": m3["units"] / m3["elapsed"], "unit": "particle-steps/s",
                       "interaction_ms_per_call": float(m3["phase_ms"][0]),
                       "divide_ms_per_call": float(m3["phase_ms"][2]),
-                      "parallelism": ("slab-x%d (%s)" % (world, "RCCL" if args.transport == "rccl" else "shared-memory"))
+                      "parallelism": ("slab-%s%d (%s)" % ("xy"[a3.axis], world,
+                                                           "RCCL" if args.transport == "rccl" else "shared-memory"))
                                      if m3["bounds"] is not None else "single",
+                      "slab_bounds_cells": None if m3["bounds"] is None else [int(b) for b in m3["bounds"]],
                       "owned_np_per_rank": m3["per_rank_np"],
                       "wall_s": time.perf_counter() - t3}
 
@@ -480,8 +489,8 @@ def main() -> None:
                 "np": case.np,
                 "presteps": args.presteps,
                 "npb": case.npb,
-                "parallelism": (("slab-x%d (%s halo + migration, max-allreduce dt%s)"
-                                 % (world, "RCCL" if args.transport == "rccl" else "shared-memory",
+                "parallelism": (("slab-%s%d (%s halo + migration, max-allreduce dt%s)"
+                                 % ("xy"[args.axis], world, "RCCL" if args.transport == "rccl" else "shared-memory",
                                     "" if args.ranks_per_gpu == 1 else ", %d ranks per GPU" % args.ranks_per_gpu))
                                 if bounds is not None else "single"),
                 "slab_bounds_cells": None if bounds is None else [int(b) for b in bounds],

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -326,6 +327,15 @@ std::unique_ptr<SlabTransport> make_local_transport(std::shared_ptr<LocalHub> hu
 // neighbours' mailboxes -> device, barrier (nobody refills a mailbox before it was read).
 // A barrier that waits past the deadline or sees the abort flag raises SPH_ERR_COMM
 // after setting the flag, so every rank ends instead of hanging.
+//
+// Conformance (the precondition of the RCCL transport, whose ncclSend / ncclRecv pairs hang
+// rather than fail when their sizes or order differ): every call publishes its kind, element
+// count and sequence number, and after the first barrier each rank checks that its
+// neighbours (an exchange) or all ranks (a reduction) are in the same call, and that every
+// message a neighbour sends it has exactly the size it receives — zero-size sides included,
+// which this transport could otherwise pass over silently.  SPH_COMM_LOG=<dir> (a test hook)
+// also appends every call of rank r to <dir>/rank<r>.log ("seq kind nsl nsr nrl nrr" or
+// "seq kind n") for an offline check of the same pairing (tests/test_gpu_slab_mp.py).
 namespace {
 constexpr int SHM_MAXRANKS = 64;
 constexpr uint64_t SHM_MAGIC = 0x53504853484d3031ull;  // "SPHSHM01"
@@ -336,6 +346,8 @@ struct ShmHead {
   std::atomic<uint64_t> abort;
   std::atomic<uint64_t> arrive[SHM_MAXRANKS];
   uint64_t nsl[SHM_MAXRANKS], nsr[SHM_MAXRANKS];
+  // conformance: every rank's current collective (kind, element count) and its sequence number
+  uint64_t opkind[SHM_MAXRANKS], opseq[SHM_MAXRANKS];
 };
 static_assert(sizeof(ShmHead) <= 4096, "shm head");
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "lock-free atomics in shared memory");
@@ -385,8 +397,15 @@ class ShmTransport final : public SlabTransport {
       if (head_->nranks != n || head_->slot != slot) throw SphError(SPH_ERR_ARG, "shm transport: layout mismatch");
     }
     slot_ = slot;
+    if (const char* e = std::getenv("SPH_COMM_LOG")) {
+      test_hook_notice("SPH_COMM_LOG");
+      const std::string path = std::string(e) + "/rank" + std::to_string(r) + ".log";
+      log_ = std::fopen(path.c_str(), "w");
+      if (!log_) throw SphError(SPH_ERR_ARG, "SPH_COMM_LOG: cannot write " + path);
+    }
   }
   ~ShmTransport() override {
+    if (log_) std::fclose(log_);
     unmap();
     if (rank == 0) (void)shm_unlink(name_.c_str());
   }
@@ -403,20 +422,20 @@ class ShmTransport final : public SlabTransport {
     if (has_right() && nsr) check_hip(hipMemcpy(box(rank, 1), sr, nsr, hipMemcpyDeviceToHost), "exchange: to mailbox");
     head_->nsl[rank] = has_left() ? nsl : 0;
     head_->nsr[rank] = has_right() ? nsr : 0;
+    announce(OP_EXCHANGE, 0);
+    if (log_)
+      std::fprintf(log_, "%llu X %zu %zu %zu %zu\n", (unsigned long long)seq_, has_left() ? nsl : 0,
+                   has_right() ? nsr : 0, has_left() ? nrl : 0, has_right() ? nrr : 0);
     barrier();
-    if (has_left() && nrl) {
-      if (head_->nsr[rank - 1] != nrl) throw SphError(SPH_ERR_COMM, "exchange: size mismatch with the left rank");
-      check_hip(hipMemcpy(rl, box(rank - 1, 1), nrl, hipMemcpyHostToDevice), "exchange: from left");
-    }
-    if (has_right() && nrr) {
-      if (head_->nsl[rank + 1] != nrr) throw SphError(SPH_ERR_COMM, "exchange: size mismatch with the right rank");
-      check_hip(hipMemcpy(rr, box(rank + 1, 0), nrr, hipMemcpyHostToDevice), "exchange: from right");
-    }
+    if (has_left()) conform(rank - 1, OP_EXCHANGE, 0, head_->nsr[rank - 1], nrl, "left");
+    if (has_right()) conform(rank + 1, OP_EXCHANGE, 0, head_->nsl[rank + 1], nrr, "right");
+    if (has_left() && nrl) check_hip(hipMemcpy(rl, box(rank - 1, 1), nrl, hipMemcpyHostToDevice), "exchange: from left");
+    if (has_right() && nrr) check_hip(hipMemcpy(rr, box(rank + 1, 0), nrr, hipMemcpyHostToDevice), "exchange: from right");
     barrier();
   }
   void allreduce_max_u32(unsigned* d, int n, hipStream_t s) override {
     std::vector<unsigned> v(size_t(n), 0u);
-    reduce_in(d, 4 * size_t(n), s);
+    reduce_in(d, 4 * size_t(n), s, OP_MAX_U32, n);
     for (int r = 0; r < nranks; r++) {
       const unsigned* x = (const unsigned*)box(r, 0);
       for (int i = 0; i < n; i++) v[size_t(i)] = std::max(v[size_t(i)], x[i]);
@@ -426,7 +445,7 @@ class ShmTransport final : public SlabTransport {
   // Summed in rank order from 0.f, as LocalTransport and launch_rank_ordered_sum do.
   void allreduce_sum_f32(float* d, int n, hipStream_t s) override {
     std::vector<float> v(size_t(n), 0.f);
-    reduce_in(d, 4 * size_t(n), s);
+    reduce_in(d, 4 * size_t(n), s, OP_SUM_F32, n);
     for (int r = 0; r < nranks; r++) {
       const float* x = (const float*)box(r, 0);
       for (int i = 0; i < n; i++) v[size_t(i)] += x[i];
@@ -467,11 +486,39 @@ class ShmTransport final : public SlabTransport {
       }
     }
   }
-  void reduce_in(const void* d, size_t bytes, hipStream_t s) {
+  void reduce_in(const void* d, size_t bytes, hipStream_t s, unsigned kind, int n) {
     if (bytes > slot_) throw SphError(SPH_ERR_NOMEM, "shm transport: reduction larger than the mailbox");
     check_hip(hipStreamSynchronize(s), "allreduce: values");
     check_hip(hipMemcpy(box(rank, 0), d, bytes, hipMemcpyDeviceToHost), "allreduce: read");
+    announce(kind, unsigned(n));
+    if (log_) std::fprintf(log_, "%llu %c %d\n", (unsigned long long)seq_, kind == OP_MAX_U32 ? 'M' : 'S', n);
     barrier();
+    for (int r = 0; r < nranks; r++)
+      if (r != rank) conform(r, kind, unsigned(n), 0, 0, "reduction");
+  }
+  // conformance (above): this rank's call, then the check of a peer's after the barrier
+  enum : unsigned { OP_EXCHANGE = 1, OP_MAX_U32 = 2, OP_SUM_F32 = 3 };
+  void announce(unsigned kind, unsigned n) {
+    seq_++;
+    head_->opkind[rank] = (uint64_t(kind) << 32) | n;
+    head_->opseq[rank] = seq_;
+  }
+  void conform(int peer, unsigned kind, unsigned n, uint64_t peer_sends, uint64_t i_receive, const char* side) {
+    const uint64_t k = head_->opkind[peer], q = head_->opseq[peer];
+    if (q != seq_ || k != ((uint64_t(kind) << 32) | n)) {
+      abort();
+      throw SphError(SPH_ERR_COMM, std::string("slab transport conformance: rank ") + std::to_string(peer) +
+                                       " is in another collective (call " + std::to_string(q) + " kind " +
+                                       std::to_string(k >> 32) + ") than rank " + std::to_string(rank) +
+                                       " (call " + std::to_string(seq_) + " kind " + std::to_string(kind) + ")");
+    }
+    if (kind == OP_EXCHANGE && peer_sends != i_receive) {
+      abort();
+      throw SphError(SPH_ERR_COMM, std::string("slab transport conformance: the ") + side + " rank sends " +
+                                       std::to_string(peer_sends) + " bytes where rank " + std::to_string(rank) +
+                                       " receives " + std::to_string(i_receive) + " (call " + std::to_string(seq_) +
+                                       ")");
+    }
   }
   void reduce_out(void* d, const void* v, size_t bytes, hipStream_t s) {
     barrier();  // every rank has read every mailbox
@@ -481,8 +528,9 @@ class ShmTransport final : public SlabTransport {
   std::string name_;
   char* base_ = nullptr;
   ShmHead* head_ = nullptr;
-  uint64_t bytes_ = 0, slot_ = 0, gen_ = 0;
+  uint64_t bytes_ = 0, slot_ = 0, gen_ = 0, seq_ = 0;
   double timeout_s_ = 120.0;
+  std::FILE* log_ = nullptr;
 };
 
 std::unique_ptr<SlabTransport> make_shm_transport(const char* name, int rank, int nranks, uint64_t slot_bytes) {

@@ -542,8 +542,7 @@ struct SlabFaces {
 // (The pack writes the send messages' counts and headers.)  After the message exchange:
 // cnt->recvl / recvr from the received headers; then the prefixes of all four messages'
 // counts (off the host wait's path).
-void launch_face_hdr(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right);
-void launch_face_scan(hipStream_t stm, const SlabFaces& f, bool has_left, bool has_right);
+void launch_face_scan(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right);
 // The divide's virtual keys of the ngl + ngr reserved ghost slots (left face first):
 // keys[e] = the receiver's box key, vals[e] = vbase + e.
 void launch_ghost_keys(hipStream_t stm, const SlabFaces& f, DivGrid g, unsigned ngl, unsigned ngr, unsigned* keys,
@@ -566,6 +565,7 @@ void launch_column_counts(hipStream_t stm, unsigned cap, const DevScalars* sc, c
 // Append nm received migrants at [np, np+nm) and ng ghosts after them; set sc->np, sc->nown.
 void launch_slab_unpack(hipStream_t stm, DevScalars* sc, const SlabRec* mig, unsigned nm, const SlabGhost* gh,
                         unsigned ng, unsigned np, const PartArrays& a, const KConst& K, const double dom_posmin[3],
-                        bool withm1, bool withpre, SlabCounts* cnt, float4* normal = nullptr, unsigned nbound = 0);
+                        bool withm1, bool withpre, SlabCounts* cnt, float4* normal = nullptr, unsigned nbound = 0,
+                        const SlabFaces* faces = nullptr, bool has_left = false, bool has_right = false);
 
 }  // namespace sphx

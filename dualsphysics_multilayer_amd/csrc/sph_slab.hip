@@ -316,7 +316,7 @@ void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartA
   PackArgs q;
   q.fcnt[0] = q.fcnt[1] = nullptr;
   q.W = g.sown0;
-  if (faces) {  // zero on entry: k_face_scan / k_unpack_finish of the last exchange reset them
+  if (faces) {  // zero on entry: k_unpack of the last exchange reset them
     q.fcnt[0] = faces->msg[0] + FMSG_HDR;
     q.fcnt[1] = faces->msg[1] + FMSG_HDR;
   }
@@ -343,74 +343,77 @@ void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartA
 }
 
 // ---------------------------------------------------------------------------------
-// Face messages.  After the exchange the received headers go to cnt->recvl / recvr (for the
-// host's one read of the counts); then one block per face message scans its nfb counts in
-// tiles of 8192 (coalesced loads into LDS, 8 consecutive per thread, wave + block scans).
-__global__ void k_face_hdr(SlabFaces f, SlabCounts* __restrict__ cnt, int hl, int hr) {
-  const int side = int(threadIdx.x);
-  if (side > 1 || (side == 0 ? !hl : !hr)) return;
-  const unsigned long long* h = reinterpret_cast<const unsigned long long*>(f.msg[2 + side]);
-  unsigned long long* rv = side == 0 ? cnt->recvl : cnt->recvr;
-  rv[0] = h[0];
-  rv[1] = h[1];
-}
-
+// Face messages.  After their exchange one launch (before the host reads the counts): the
+// received headers go to cnt->recvl / recvr (for the host's one read of the counts), and the
+// exclusive prefixes of all four messages' nfb counts, one block per (message, tile of 8192):
+// a block adds the counts of its message's earlier tiles (a block reduction; no inter-block
+// ordering) to the scan of its own tile (coalesced loads into LDS, 8 consecutive per thread,
+// wave + block scans).  The send messages' counts are zeroed for the next exchange by the
+// exchange's unpack (k_unpack), once the neighbours have copied them.  (One block per message
+// walking its tiles in turn took 16-38 us per exchange at the cfg3 y-slab face size, 25k
+// boxes per message; one launch for the header and another for the scan, 6 + that.)
 constexpr int FS_BS = 1024, FS_PT = 8, FS_TILE = FS_BS * FS_PT;
-__global__ __launch_bounds__(FS_BS) void k_face_scan(SlabFaces f, int hl, int hr) {
+__global__ __launch_bounds__(FS_BS) void k_face_scan(SlabFaces f, SlabCounts* __restrict__ cnt, int hl, int hr) {
   __shared__ unsigned v[FS_TILE];
   __shared__ unsigned wsum[FS_BS / 64];
-  __shared__ unsigned carry;
-  const int m = int(blockIdx.x);  // send L, send R, receive L, receive R
+  const int m = int(blockIdx.y);  // send L, send R, receive L, receive R
   if ((m & 1) ? !hr : !hl) return;
-  unsigned* cnt = f.msg[m] + FMSG_HDR;
-  unsigned* pre = f.pre[m];
-  const bool reset = m < 2;  // a send message's counts: zeroed for the next exchange once read
+  const unsigned t0 = blockIdx.x * unsigned(FS_TILE);
+  const unsigned* __restrict__ c = f.msg[m] + FMSG_HDR;
+  unsigned* __restrict__ pre = f.pre[m];
   const unsigned n = f.nfb, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (threadIdx.x == 0) carry = 0;
-  for (unsigned t0 = 0; t0 < n; t0 += FS_TILE) {
-#pragma unroll
-    for (int k = 0; k < FS_PT; k++) {
-      const unsigned i = t0 + k * FS_BS + threadIdx.x;
-      v[k * FS_BS + threadIdx.x] = i < n ? cnt[i] : 0u;
-      if (reset && i < n) cnt[i] = 0u;
-    }
-    __syncthreads();
-    unsigned x[FS_PT], sum = 0;
-#pragma unroll
-    for (int k = 0; k < FS_PT; k++) {
-      x[k] = sum;
-      sum += v[threadIdx.x * FS_PT + k];
-    }
-    unsigned inc = sum;  // inclusive wave scan of the thread sums
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const unsigned y = __shfl_up(inc, off, 64);
-      if (lane >= unsigned(off)) inc += y;
-    }
-    if (lane == 63) wsum[w] = inc;
-    __syncthreads();
-    unsigned before = carry;
-    for (unsigned q = 0; q < w; q++) before += wsum[q];
-    before += inc - sum;
-#pragma unroll
-    for (int k = 0; k < FS_PT; k++) v[threadIdx.x * FS_PT + k] = before + x[k];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < FS_PT; k++) {
-      const unsigned i = t0 + k * FS_BS + threadIdx.x;
-      if (i < n) pre[i] = v[k * FS_BS + threadIdx.x];
-    }
-    if (threadIdx.x == FS_BS - 1) carry = before + sum;
-    __syncthreads();
+  if (m >= 2 && blockIdx.x == 0 && threadIdx.x == 0) {  // the received header {ghosts, migrants}
+    const unsigned long long* h = reinterpret_cast<const unsigned long long*>(f.msg[m]);
+    unsigned long long* rv = m == 2 ? cnt->recvl : cnt->recvr;
+    rv[0] = h[0];
+    rv[1] = h[1];
   }
-  if (threadIdx.x == 0) pre[n] = carry;
+  // this tile's counts (loads in flight) and the sum of the earlier tiles' counts
+#pragma unroll
+  for (int k = 0; k < FS_PT; k++) {
+    const unsigned i = t0 + k * FS_BS + threadIdx.x;
+    v[k * FS_BS + threadIdx.x] = i < n ? c[i] : 0u;
+  }
+  unsigned below = 0;
+  for (unsigned i = threadIdx.x; i < t0; i += FS_BS) below += c[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) below += __shfl_xor(below, off, 64);
+  if (lane == 0) wsum[w] = below;
+  __syncthreads();
+  unsigned base = 0;
+  for (unsigned q = 0; q < FS_BS / 64; q++) base += wsum[q];
+  __syncthreads();  // wsum is reused below
+  unsigned x[FS_PT], sum = 0;
+#pragma unroll
+  for (int k = 0; k < FS_PT; k++) {
+    x[k] = sum;
+    sum += v[threadIdx.x * FS_PT + k];
+  }
+  unsigned inc = sum;  // inclusive wave scan of the thread sums
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned y = __shfl_up(inc, off, 64);
+    if (lane >= unsigned(off)) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  unsigned before = base;
+  for (unsigned q = 0; q < w; q++) before += wsum[q];
+  before += inc - sum;
+#pragma unroll
+  for (int k = 0; k < FS_PT; k++) v[threadIdx.x * FS_PT + k] = before + x[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < FS_PT; k++) {
+    const unsigned i = t0 + k * FS_BS + threadIdx.x;
+    if (i < n) pre[i] = v[k * FS_BS + threadIdx.x];
+  }
+  if (threadIdx.x == FS_BS - 1 && t0 + FS_TILE >= n) pre[n] = before + sum;
 }
 
-void launch_face_hdr(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right) {
-  hipLaunchKernelGGL(k_face_hdr, dim3(1), dim3(64), 0, stm, f, cnt, int(has_left), int(has_right));
-}
-void launch_face_scan(hipStream_t stm, const SlabFaces& f, bool has_left, bool has_right) {
-  hipLaunchKernelGGL(k_face_scan, dim3(4), dim3(FS_BS), 0, stm, f, int(has_left), int(has_right));
+void launch_face_scan(hipStream_t stm, const SlabFaces& f, SlabCounts* cnt, bool has_left, bool has_right) {
+  const unsigned nt = (f.nfb + FS_TILE - 1) / FS_TILE;
+  hipLaunchKernelGGL(k_face_scan, dim3(nt ? nt : 1u, 4), dim3(FS_BS), 0, stm, f, cnt, int(has_left), int(has_right));
 }
 
 // Reserved ghost slots of the divide: one thread per face box (left face first) writes the
@@ -496,13 +499,32 @@ struct UnpackArgs {
   double posminx, posminy, posminz, scelld;
   int withm1, withpre;
   SlabCounts* cnt;
+  DevScalars* sc;
   float4* normal;
   unsigned nbound;
+  unsigned nfb;
+  unsigned* fmsg[2];  // the send face messages' counts (zeroed here), or nullptr
 };
 
+// The exchange's last kernel: the migrants appended after the np particles; thread 0 sets the
+// new counts and zeroes the accumulated pack counts, the threads from nm + ng on zero the send
+// face messages' counts (k_pack_count accumulates them from zero), in place of memset launches.
 __global__ __launch_bounds__(256) void k_unpack(UnpackArgs u) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= u.nm + u.ng) return;
+  if (i == 0) {
+    u.sc->np = u.np + u.nm + u.ng;
+    u.sc->nown = u.cnt->nkeep + u.nm;
+    u.cnt->nkeep = 0u;
+    u.cnt->ghosts[0] = u.cnt->ghosts[1] = 0u;
+  }
+  if (i >= u.nm + u.ng) {
+    const unsigned z = i - (u.nm + u.ng);
+    if (z < 2u * u.nfb) {
+      unsigned* c = u.fmsg[z < u.nfb ? 0 : 1];
+      if (c) c[z < u.nfb ? z : z - u.nfb] = 0u;
+    }
+    return;
+  }
   const unsigned p = u.np + i;
   PartArrays& a = u.a;
   if (i < u.nm) {
@@ -538,19 +560,10 @@ __global__ __launch_bounds__(256) void k_unpack(UnpackArgs u) {
   }
 }
 
-// The exchange's last kernel: the new counts, and the accumulated pack counts zeroed for the
-// next exchange (in place of memset launches).
-__global__ void k_unpack_finish(DevScalars* __restrict__ sc, SlabCounts* __restrict__ cnt, unsigned np,
-                                unsigned nm, unsigned ng) {
-  sc->np = np + nm + ng;
-  sc->nown = cnt->nkeep + nm;
-  cnt->nkeep = 0u;
-  cnt->ghosts[0] = cnt->ghosts[1] = 0u;
-}
-
 void launch_slab_unpack(hipStream_t stm, DevScalars* sc, const SlabRec* mig, unsigned nm, const SlabGhost* gh,
                         unsigned ng, unsigned np, const PartArrays& a, const KConst& K, const double dom_posmin[3],
-                        bool withm1, bool withpre, SlabCounts* cnt, float4* normal, unsigned nbound) {
+                        bool withm1, bool withpre, SlabCounts* cnt, float4* normal, unsigned nbound,
+                        const SlabFaces* faces, bool has_left, bool has_right) {
   UnpackArgs u;
   u.normal = normal;
   u.nbound = nbound;
@@ -568,8 +581,12 @@ void launch_slab_unpack(hipStream_t stm, DevScalars* sc, const SlabRec* mig, uns
   u.withm1 = withm1;
   u.withpre = withpre;
   u.cnt = cnt;
-  if (nm + ng) hipLaunchKernelGGL(k_unpack, dim3((nm + ng + 255) / 256), dim3(256), 0, stm, u);
-  hipLaunchKernelGGL(k_unpack_finish, dim3(1), dim3(1), 0, stm, sc, cnt, np, nm, ng);
+  u.sc = sc;
+  u.nfb = faces ? faces->nfb : 0u;
+  u.fmsg[0] = faces && has_left ? faces->msg[0] + FMSG_HDR : nullptr;
+  u.fmsg[1] = faces && has_right ? faces->msg[1] + FMSG_HDR : nullptr;
+  const unsigned nthr = nm + ng + 2u * u.nfb;
+  hipLaunchKernelGGL(k_unpack, dim3(nthr ? (nthr + 255) / 256 : 1u), dim3(256), 0, stm, u);
 }
 
 // ---------------------------------------------------------------------------------

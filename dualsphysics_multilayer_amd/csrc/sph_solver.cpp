@@ -1006,7 +1006,9 @@ void SphGpuSingle::Exchange() {
   const size_t mb = 4 * (size_t(FMSG_HDR) + faces_.nfb);
   transport_->exchange(faces_.msg[0], hl ? mb : 0, faces_.msg[1], hr ? mb : 0, faces_.msg[2], hl ? mb : 0,
                        faces_.msg[3], hr ? mb : 0, stream);
-  launch_face_hdr(stream, faces_, slabcnt_, hl, hr);
+  // received headers -> the counts the host reads; the prefixes of all four messages' counts
+  // (slots of the received ghosts, records of the sent ones) in the same launch
+  launch_face_scan(stream, faces_, slabcnt_, hl, hr);
   check_hip(hipMemcpyAsync(slabcnt_host_, slabcnt_, sizeof(SlabCounts), hipMemcpyDeviceToHost, stream),
             "exchange: read counts");
   // The transfer sizes must be on the host before the transfers are posted: the one host
@@ -1070,14 +1072,13 @@ void SphGpuSingle::Exchange() {
     if (want >= (1ull << 31)) throw SphError(SPH_ERR_NOMEM, "slab particle capacity overflow");
     Grow(c.np, unsigned(want));
   }
-  // k_face_scan zeroes the face counts of the messages just sent: the neighbours have read them
+  // k_unpack zeroes the face counts of the messages just sent: the neighbours have read them
   transport_->wait_sends(stream);
-  launch_face_scan(stream, faces_, hl, hr);  // slots of the received ghosts, records of the sent ones
   // the migrants of both faces (two concurrent streams over the two xGMI links)
   transport_->exchange(send_.ml, sizeof(SlabRec) * c.sendl[1], send_.mr, sizeof(SlabRec) * c.sendr[1], recvm_,
                        sizeof(SlabRec) * rml, recvm_ + rml, sizeof(SlabRec) * rmr, stream);
   launch_slab_unpack(stream, sc_, recvm_, unsigned(rml + rmr), recvg_, 0u, c.np, cur_, K, C.dom_posmin, withm1,
-                     withpre, slabcnt_, normal_, nnormal_);
+                     withpre, slabcnt_, normal_, nnormal_, &faces_, hl, hr);
   SLAB_TRACE("exchange: done");
   xg_sl_ = hl ? c.sendl[0] : 0;
   xg_sr_ = hr ? c.sendr[0] : 0;

@@ -2,7 +2,7 @@
 tests/test_gpu_slab_mp.py; every rank a separate process, all on cuda:0).
 
     python tests/slab_rank.py <rank> <nranks> <shm name> <golden> <out.npz> [skew|balanced]
-                              [repartition K] [die-after-create]
+                              [repartition K] [die-after-create] [axis=0|1]
 
 Runs the golden's dam break to each of its kept steps (SphGpuSlab, collective calls in
 the same order on every rank) and saves this rank's OWNED particles at every kept step."""
@@ -25,16 +25,17 @@ def main(argv):
     rank, nranks, name, golden, out = int(argv[0]), int(argv[1]), argv[2], argv[3], argv[4]
     layout = argv[5] if len(argv) > 5 else "balanced"
     every = int(argv[6]) if len(argv) > 6 else 0
-    die = len(argv) > 7 and argv[7] == "die-after-create"
+    die = "die-after-create" in argv[7:]
+    axis = next((int(a.split("=")[1]) for a in argv[7:] if a.startswith("axis=")), 0)
     g = load(golden)
     dp, step_alg, ddt, _ = meta(g)
     case = DamBreakCase(dp, step_algorithm=step_alg, tdensity=ddt)
-    if layout == "skew":  # rank 0 holds all but the last 2 columns per other rank
-        ncx = case_derive(case.case_def())["dom_cells"][0]
+    if layout == "skew":  # rank 0 holds all but the last 2 cells (of the slab axis) per other rank
+        ncx = case_derive(case.case_def())["dom_cells"][axis]
         bounds = [0] + [ncx - 2 * (nranks - r) for r in range(1, nranks)] + [ncx]
     else:
-        bounds = list(slab_partition(case, nranks))
-    s = SphGpuSlab(case, rank, nranks, bounds, name, device=0, transport="shm", slot_bytes=8 << 20)
+        bounds = list(slab_partition(case, nranks, 0.3, axis))
+    s = SphGpuSlab(case, rank, nranks, bounds, name, device=0, transport="shm", slot_bytes=8 << 20, axis=axis)
     if every:
         s.set_repartition(every, 0.3, 0.0)
     if die:
