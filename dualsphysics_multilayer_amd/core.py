@@ -92,6 +92,10 @@ EXPORTED_SYMBOLS = (
     "sph_solver_set_time_table",
     "sph_solver_floatings",
     "sph_partfloat_write",
+    "sph_partfloat_read",
+    "sph_extra_normals_read",
+    "sph_extra_normals_write",
+    "sph_download_normals",
 )
 
 
@@ -170,6 +174,12 @@ def load_library(path: str = LIB_PATH):
                                                 C.POINTER(C.c_double)]
     L.sph_solver_floatings.argtypes = [vp, C.c_uint32, C.POINTER(SphFloatingState), C.POINTER(C.c_uint32)]
     L.sph_partfloat_write.argtypes = [C.c_char_p, C.c_char_p, C.c_uint32, C.c_uint32] + [vp] * 6 + [C.c_uint32] + [vp] * 8
+    L.sph_partfloat_read.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32, vp, vp, vp, vp]
+    L.sph_extra_normals_read.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.POINTER(C.c_uint32),
+                                         C.POINTER(C.c_int32)]
+    L.sph_extra_normals_write.argtypes = [C.c_char_p, C.c_char_p, C.c_uint32, C.c_uint32, C.c_double, C.c_uint32,
+                                          C.c_uint32, C.c_int32, C.c_uint32, vp]
+    L.sph_download_normals.argtypes = [vp, C.c_uint32, vp, C.POINTER(C.c_uint32), C.POINTER(C.c_int32)]
     if L.sph_abi_version() != SPH_ABI_VERSION:
         raise SphError(3, "ABI version mismatch")
     _lib = L
@@ -326,6 +336,15 @@ class SphGpuSingle:
             return  # already applied at creation (cases with moving/floating bodies)
         _check(load_library().sph_solver_set_time(self._h, time, symplectic_dtpre))
         self._time_set = (time, symplectic_dtpre)
+
+    def normals(self) -> tuple[np.ndarray, bool]:
+        """mDBC: the current vectors particle -> ghost node by idp, and UseNormalsFt."""
+        L = load_library()
+        n, ft = C.c_uint32(), C.c_int32()
+        _check(L.sph_download_normals(self._h, 0, None, C.byref(n), C.byref(ft)))
+        out = np.zeros((n.value, 3), np.float32)
+        _check(L.sph_download_normals(self._h, n.value, out.ctypes.data, C.byref(n), C.byref(ft)))
+        return out, bool(ft.value)
 
     def floatings(self) -> list:
         """State of the floating bodies (FtObjs: center, fvel, fomega, angles, facelin, faceang)."""
@@ -609,3 +628,34 @@ def write_partfloat(path: str, floatings: list, parts: list, mkboundfirst: int =
                                               *[ptr(a) for a in head], len(parts), ptr(cp), ptr(st), ptr(ts),
                                               ptr(cen), *[ptr(arr[k]) for k in ("fvel", "fomega", "facelin",
                                                                                 "faceang")]))
+
+
+# ---- restart of floating bodies and mDBC (JSphCpu::InitFloating, JDsExtraData) -----------
+def read_partfloat(path: str, cpart: int, nft: int) -> dict:
+    """Body state of PART `cpart` in PartFloat.fbi4: center (nft, 3) f64, fvel / fomega f32, time."""
+    center = np.zeros((nft, 3), np.float64)
+    fvel = np.zeros((nft, 3), np.float32)
+    fomega = np.zeros((nft, 3), np.float32)
+    t = C.c_double()
+    _check(load_library().sph_partfloat_read(path.encode(), int(cpart), int(nft), center.ctypes.data,
+                                             fvel.ctypes.data, fomega.ctypes.data, C.byref(t)))
+    return dict(center=center, fvel=fvel, fomega=fomega, time=t.value)
+
+
+def read_extra_normals(path: str, casenbound: int, casenfloat: int) -> tuple[np.ndarray, bool]:
+    """PartExtra_%04u.bi4: the normals by idp (vectors to the ghost node) and UseNormalsFt."""
+    L = load_library()
+    n, ft = C.c_uint32(), C.c_int32()
+    _check(L.sph_extra_normals_read(path.encode(), casenbound, casenfloat, 0, None, C.byref(n), C.byref(ft)))
+    out = np.zeros((n.value, 3), np.float32)
+    _check(L.sph_extra_normals_read(path.encode(), casenbound, casenfloat, n.value, out.ctypes.data, C.byref(n),
+                                    C.byref(ft)))
+    return out, bool(ft.value)
+
+
+def write_extra_normals(path: str, app: str, cpart: int, step: int, time: float, casenbound: int, casenfloat: int,
+                        normals: np.ndarray, usenormalsft: bool) -> None:
+    nor = np.ascontiguousarray(normals, np.float32).reshape(-1, 3)
+    _check(load_library().sph_extra_normals_write(path.encode(), app.encode(), int(cpart), int(step), float(time),
+                                                  int(casenbound), int(casenfloat), int(usenormalsft), len(nor),
+                                                  nor.ctypes.data))

@@ -268,6 +268,23 @@ Item read_file(const std::string& path, const std::string& filecode) {
   return root;
 }
 
+std::vector<Item> read_list_file(const std::string& path, const std::string& filecode) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw SphError(SPH_ERR_ARG, "bi4: cannot open " + path);
+  std::vector<uint8_t> d((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  if (d.size() < 64) throw SphError(SPH_ERR_ARG, "bi4: no header in " + path);
+  const std::vector<uint8_t> h = head(filecode);
+  if (std::memcmp(d.data(), h.data(), 59) != 0) throw SphError(SPH_ERR_ARG, "bi4: file code is not " + filecode);
+  if (d[60] != 0) throw SphError(SPH_ERR_UNSUPPORTED, "bi4: big-endian files are not supported");
+  Reader r(d.data() + 64, d.size() - 64);
+  std::vector<Item> items;
+  while (r.i < d.size() - 64) {
+    items.emplace_back();
+    parse_item(r, items.back());
+  }
+  return items;
+}
+
 void write_list_file(const std::string& path, const std::string& filecode, const Item& head,
                      const std::vector<Item>& items) {
   Writer w;
@@ -585,6 +602,81 @@ void partfloat_write(const std::string& path, const char* app, uint32_t mkboundf
     it.add_array("faceang", bi4::Float3, nft, faceang + size_t(3) * nft * k);
   }
   bi4::write_list_file(path, "JPartFloatBi4", head, parts);
+}
+
+// The body state of PART cpart (JPartFloatBi4Load::LoadFile + LoadPart/LoadPartItem,
+// JPartFloatBi4.cpp:525-660): the item whose name ends in PART_%04u, its center / fvel /
+// fomega arrays of FtCount bodies — what JSphCpu::InitFloating restores at a restart
+// (JSphCpu.cpp:1885-1905: center, fvel, fomega; the angles start again from 0).
+void partfloat_read(const std::string& path, uint32_t cpart, uint32_t nft, double* center, float* fvel,
+                    float* fomega, double* timestep) {
+  const std::vector<bi4::Item> items = bi4::read_list_file(path, "JPartFloatBi4");
+  if (items.empty()) throw SphError(SPH_ERR_ARG, "PartFloat: no head item in " + path);
+  if (items[0].get_uint("FtCount", 0) != nft)
+    throw SphError(SPH_ERR_ARG, "PartFloat: the number of floating bodies does not match the case (" + path + ")");
+  char nm[32];
+  std::snprintf(nm, sizeof(nm), "PART_%04u", cpart);
+  const std::string want(nm);
+  for (size_t k = 1; k < items.size(); k++) {
+    const std::string& n = items[k].name;
+    if (n.size() < want.size() || n.compare(n.size() - want.size(), want.size(), want) != 0) continue;
+    const bi4::Item& it = items[k];
+    auto arr = [&](const char* a, int32_t type) -> const bi4::Array& {
+      const bi4::Array* x = it.array(a);
+      if (!x || x->type != type || x->count != nft)
+        throw SphError(SPH_ERR_ARG, std::string("PartFloat: array ") + a + " is missing or invalid in " + path);
+      return *x;
+    };
+    if (center) std::memcpy(center, arr("center", bi4::Double3).bytes.data(), size_t(nft) * 24);
+    if (fvel) std::memcpy(fvel, arr("fvel", bi4::Float3).bytes.data(), size_t(nft) * 12);
+    if (fomega) std::memcpy(fomega, arr("fomega", bi4::Float3).bytes.data(), size_t(nft) * 12);
+    if (timestep) *timestep = it.get_double("TimeStep", 0.0);
+    return;
+  }
+  throw SphError(SPH_ERR_ARG, "PartFloat: " + want + " not found in " + path);
+}
+
+// mDBC normals of a PART (PartExtra_%04u.bi4, JDsExtraDataSave / JDsExtraDataLoad,
+// JDsExtraData.cpp:80-225): root values AppName, FormatVer, CaseNbound, CaseNfloat, Cpart,
+// Step, TimeStep, UseNormalsFt and the array Normals (float3[nsize], nsize = CaseNbound, or
+// CaseNbound - CaseNfloat without floating normals) by idp: each boundary particle's vector
+// to its ghost node (the full distance: twice the case's normal) at that PART.  What a
+// restart with mDBC reloads (JSph::ConfigBoundNormals, JSph.cpp:1308-1316).
+static const char* kExtraCode = "JPartExtraBi4";
+
+uint32_t extra_normals_read(const std::string& path, uint32_t casenbound, uint32_t casenfloat, uint32_t cap,
+                            float* normals, int32_t* usenormalsft) {
+  const bi4::Item root = bi4::read_file(path, kExtraCode);
+  if (root.get_uint("CaseNbound", ~0ull) != casenbound)
+    throw SphError(SPH_ERR_ARG, "PartExtra: CaseNbound value does not match (" + path + ")");
+  if (root.get_uint("CaseNfloat", ~0ull) != casenfloat)
+    throw SphError(SPH_ERR_ARG, "PartExtra: CaseNfloat value does not match (" + path + ")");
+  const bi4::Array* a = root.array("Normals");
+  if (!a || a->type != bi4::Float3)
+    throw SphError(SPH_ERR_ARG, "PartExtra: the array 'Normals' is missing or type invalid (" + path + ")");
+  if (usenormalsft) *usenormalsft = root.get_bool("UseNormalsFt", false) ? 1 : 0;
+  if (normals) {
+    if (cap < a->count) throw SphError(SPH_ERR_ARG, "PartExtra: normals buffer too small");
+    std::memcpy(normals, a->bytes.data(), size_t(a->count) * 12);
+  }
+  return a->count;
+}
+
+void extra_normals_write(const std::string& path, const char* app, uint32_t cpart, uint32_t step, double timestep,
+                         uint32_t casenbound, uint32_t casenfloat, int32_t usenormalsft, uint32_t nsize,
+                         const float* normals) {
+  bi4::Item root;
+  root.name = kExtraCode;
+  root.set_text("AppName", app ? app : "");
+  root.set_pod("FormatVer", bi4::Uint, uint32_t(211030));
+  root.set_pod("CaseNbound", bi4::Uint, casenbound);
+  root.set_pod("CaseNfloat", bi4::Uint, casenfloat);
+  root.set_pod("Cpart", bi4::Int, int32_t(cpart));
+  root.set_pod("Step", bi4::Uint, step);
+  root.set_pod("TimeStep", bi4::Double, timestep);
+  root.set_pod("UseNormalsFt", bi4::Bool, int32_t(usenormalsft ? 1 : 0));
+  root.add_array("Normals", bi4::Float3, nsize, normals);
+  bi4::write_file(path, kExtraCode, root);
 }
 
 void bi4_rewrite(const std::string& src, const std::string& dst) {

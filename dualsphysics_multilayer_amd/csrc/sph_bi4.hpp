@@ -73,7 +73,9 @@ struct Item {
 // Read / write a whole container file; `filecode` is checked against the header title.
 Item read_file(const std::string& path, const std::string& filecode);
 void write_file(const std::string& path, const std::string& filecode, const Item& root);
-// A list file (JBinaryData::SaveFileListApp): head item then items appended after it.
+// A list file (JBinaryData::SaveFileListApp / LoadFileListApp): head item then items appended
+// after it; read back as [head, item 1, ...].
+std::vector<Item> read_list_file(const std::string& path, const std::string& filecode);
 void write_list_file(const std::string& path, const std::string& filecode, const Item& head,
                      const std::vector<Item>& items);
 

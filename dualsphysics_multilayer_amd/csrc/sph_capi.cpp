@@ -177,6 +177,32 @@ int sph_partfloat_write(const char* path, const char* app, uint32_t mkboundfirst
                           step, timestep, center, fvel, fomega, facelin, faceang);
   });
 }
+int sph_partfloat_read(const char* path, uint32_t cpart, uint32_t nft, double* center, float* fvel, float* fomega,
+                       double* timestep) {
+  NEED(path && nft);
+  return guard([&] { sphx::partfloat_read(path, cpart, nft, center, fvel, fomega, timestep); });
+}
+int sph_extra_normals_read(const char* path, uint32_t casenbound, uint32_t casenfloat, uint32_t cap, float* normals,
+                           uint32_t* nsize, int32_t* usenormalsft) {
+  NEED(path && nsize);
+  return guard([&] { *nsize = sphx::extra_normals_read(path, casenbound, casenfloat, cap, normals, usenormalsft); });
+}
+int sph_extra_normals_write(const char* path, const char* app, uint32_t cpart, uint32_t step, double timestep,
+                            uint32_t casenbound, uint32_t casenfloat, int32_t usenormalsft, uint32_t nsize,
+                            const float* normals) {
+  NEED(path && (normals || !nsize));
+  return guard([&] {
+    sphx::extra_normals_write(path, app, cpart, step, timestep, casenbound, casenfloat, usenormalsft, nsize, normals);
+  });
+}
+int sph_download_normals(SphSolver* s, uint32_t cap, float* normals, uint32_t* n, int32_t* usenormalsft) {
+  NEED(s && n);
+  return guard([&] {
+    int ft = 0;
+    *n = s->impl->DownloadNormals(normals, cap, &ft);
+    if (usenormalsft) *usenormalsft = ft;
+  });
+}
 int sph_solver_set_timing(SphSolver* s, int enabled) {
   NEED(s);
   return guard([&] { s->impl->SetTiming(enabled != 0); });

@@ -84,6 +84,19 @@ struct NNP1 {
   float inv_rho;   // 1/rho1
   float mph;       // mass of p1's phase (the heavier-phase test of the shifting)
   float taumax, bimulti;  // bi-viscosity constants of p1's phase
+  int uph;         // the item's phase (that of its first particle; -1: none): see NNUni
+  bool p1uni;      // this lane's p1 is a fluid particle of phase uph (or the lane is idle)
+};
+
+// A single-phase drain unit (the bulk of every phase): every staged record of the unit and
+// every p1 of the block are fluid particles of one phase k (a block vote after the staging).
+// Its pairs then take that phase's constants from SGPRs, read once per item, instead of the
+// dependent LDS chain record -> phase tag -> the phase table's two rows of every pair, and
+// the same-phase / heavier-phase tests of the pair body are known (DDT on, no shifting reset).
+// The values are those the table gives, so the result is bitwise the general path's.
+struct NNUni {
+  float4 a, c;  // sph[2 k] = {mass, cs0, visco, tau_yield}, sph[2 SPH_MAXPHASES + k]
+  int k;
 };
 
 // GetEta_Effective (JSphCpu_Tensors.cpp:116-142): Herschel-Bulkley-Papanastasiou effective
@@ -157,10 +170,11 @@ __device__ __forceinline__ float max_nonneg(float x, float m) {
 // carries its body's particle mass (the fourth phase-table row), switches the Molteni DDT of
 // p1 off when it is not heavier than 1.2 MassFluid (DELTA_HEAVYFLOATING), takes no part in
 // the Fourtakas DDT, and under ShiftMode NoBound cancels p1's shifting.
-template <int TVISCO, int TDENSITY, bool SHIFT, bool BOUNDP2, bool ORDERED = true, bool FT = false>
+template <int TVISCO, int TDENSITY, bool SHIFT, bool BOUNDP2, bool ORDERED = true, bool FT = false, bool UNI = false>
 __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restrict__ sph, const NNP1& p, float drx,
                                         float dry, float drz, float rr2, bool ok, const float4& B, const float4& C,
-                                        NNAcc& a) {
+                                        NNAcc& a, const NNUni& u = NNUni{}) {
+  static_assert(!UNI || (!BOUNDP2 && !ORDERED), "single-phase units: fluid p2 in mirrored order only");
   // kernel (Wendland fac = bwen q (1-q/2)^3 / r = (bwen/h) (1-q/2)^3), 0 beyond 2h.  With the
   // FDA gradient (which needs 1/r^2 too) one v_rsq gives both: r = r^2 rsq, 1/r^2 = rsq^2
   // (one transcendental instead of v_sqrt + v_rcp; ulp-level differences)
@@ -170,11 +184,12 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   const float wq = __builtin_amdgcn_fmed3f(fmaf(K.mhalfovh, rad, 1.f), 0.f, 1.f);
   const float fac = K.bwenovh * (wq * wq * wq);
   const float frx = fac * drx, fry = fac * dry, frz = fac * drz;
-  const unsigned tg = BOUNDP2 ? 0u : __float_as_uint(C.y);
-  const bool ftp2 = FT && !BOUNDP2 && (tg & 0x80u) != 0u;
-  const int pp2 = BOUNDP2 ? p.ph : int(FT ? (tg & 0x7fu) : tg);
-  const float4 ph2 = sph[2 * pp2];
-  const float4 ph2c = sph[2 * SPH_MAXPHASES + pp2];  // {m tau_yield, -m log2 e, n - 1, DDTkh cs0}
+  const unsigned tg = (BOUNDP2 || UNI) ? 0u : __float_as_uint(C.y);
+  const bool ftp2 = FT && !BOUNDP2 && !UNI && (tg & 0x80u) != 0u;
+  const int pp2 = UNI ? u.k : BOUNDP2 ? p.ph : int(FT ? (tg & 0x7fu) : tg);
+  const bool samephase = UNI || p.ph == pp2;
+  const float4 ph2 = UNI ? u.a : sph[2 * pp2];
+  const float4 ph2c = UNI ? u.c : sph[2 * SPH_MAXPHASES + pp2];  // {m tau_yield, -m log2 e, n - 1, DDTkh cs0}
   const float massp2 = BOUNDP2 ? K.massbound : (ftp2 ? sph[3 * SPH_MAXPHASES + pp2].x : ph2.x);
   const float rho1 = p.vr.w, rho2 = B.w;
   const float inv_rho2 = C.z;  // staged 1/rho2
@@ -204,7 +219,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   // branches in every pair)
   if (TDENSITY == 1) {
     const float visc_densi = ph2c.w * (rhop1over2 - 1.f) * inv_re;  // DDTkh cbar (...) / (r^2+eta^2)
-    const float delta = (p.ph == pp2 ? visc_densi * dot3 * massp2 : 0.f);
+    const float delta = (samephase ? visc_densi * dot3 * massp2 : 0.f);
     a.delta = (BOUNDP2 && !K.mdbc && ok) ? FLT_MAX : a.delta + delta;
     if (FT && ftp2 && ok && massp2 <= K.massfluid * 1.2f) a.delta = FLT_MAX;
   }
@@ -215,7 +230,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
     // rounding floor) does not absorb: step-1 velocities moved 5.7e-7 against 2e-8
     const float rh = 1.f + K.ddtgz * drz;
     const float drhop = K.rhopzero * fexp2(K.ovgamma * flog2(rh)) - K.rhopzero;
-    const float delta = (p.ph == pp2 && !ftp2 ? ph2c.w * ((rho2 - rho1) - drhop) * xdm : 0.f);
+    const float delta = (samephase && !ftp2 ? ph2c.w * ((rho2 - rho1) - drhop) * xdm : 0.f);
     a.delta = (BOUNDP2 && ok) ? FLT_MAX : a.delta - delta;
   }
   // multiphase shifting (JSphCpu_NN_FDA.cpp:202-209): a heavier-phase neighbour resets x
@@ -226,7 +241,7 @@ __device__ __forceinline__ void nn_pair(const KConst& K, const float4* __restric
   }
   if (SHIFT && (!ORDERED || a.sx != FLT_MAX)) {
     // (a heavier p1 phase differs from p2's: the phase test of the reference is implied)
-    const bool heavy = ok && !BOUNDP2 && (p.mph > ph2.x);
+    const bool heavy = !UNI && ok && !BOUNDP2 && (p.mph > ph2.x);
     const bool noshift = ok && BOUNDP2 && (K.shiftmode == 1 || (K.shiftmode == 2 && C.y != 0.f));
     const float mr = heavy ? 0.f : massrhop;  // a heavier-phase pair adds nothing (fma by 0)
     if (ORDERED) {
@@ -339,11 +354,13 @@ __device__ __forceinline__ void nn_bound_pair(const KConst& K, const NNP1& p, fl
 
 // Staging of one row segment: positions relative to the item (sA + |A|^2), velrhop (sB),
 // {press, tag} (sC): tag = phase index (fluid rows) or 1 for a fixed boundary particle.
+// `same`: cleared when a record this thread stages is not a fluid particle of phase `uph`.
 __device__ __forceinline__ void nn_stage(const KConst& K, unsigned rs, unsigned n, int xo, int dy, int dz,
                                          bool boundrow, const float4* __restrict__ poscell,
                                          const float4* __restrict__ velrhop, const float* __restrict__ press,
                                          const typecode* __restrict__ code, float4* __restrict__ sA,
-                                         float4* __restrict__ sB, NNSC sC, unsigned dst = 0u) {
+                                         float4* __restrict__ sB, NNSC sC, unsigned dst = 0u, bool* same = nullptr,
+                                         int uph = -1) {
   const float oy = float(dy) * K.scell, oz = float(dz) * K.scell;
   sA += dst;
   sB += dst;
@@ -363,6 +380,7 @@ __device__ __forceinline__ void nn_stage(const KConst& K, unsigned rs, unsigned 
                                   : (unsigned(c & CODE_MASKVALUE) | (CodeType(c) == CODE_TYPE_FLOATING ? 0x80u : 0u));
     sC.c[i] = make_float2(press[rs + i], frcp(vr.w));
     sC.t[i] = (unsigned char)tag;
+    if (same) *same = *same && int(tag) == uph;
   }
 }
 
@@ -445,12 +463,12 @@ __device__ __forceinline__ void nn_pass(const KConst& K, const DivGrid& g, const
 // staged records from bases b0..b3, compacted into one chain and popped two pairs per
 // iteration with value selects only (the chain of drain_words, sph_interaction_tiled.hip).
 // KIND 0: fluid p1 / fluid p2 (sx in mirrored order, see nn_pair), 2: bound p1 / fluid p2.
-template <int TVISCO, int TDENSITY, bool SHIFT, int KIND, bool FT>
+template <int TVISCO, int TDENSITY, bool SHIFT, int KIND, bool FT, bool UNI = false>
 __device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restrict__ sph, const NNP1& p,
                                           unsigned long long c0, unsigned long long c1, unsigned long long c2,
                                           unsigned long long c3, int b0, int b1, int b2, int b3,
                                           const float4* __restrict__ sA, const float4* __restrict__ sB,
-                                          const NNSC sC, NNAcc& a) {
+                                          const NNSC sC, NNAcc& a, const NNUni& u = NNUni{}) {
 #pragma unroll
   for (int pass = 0; pass < 3; pass++) {  // drop empty words, keep the order
     const bool e2 = c2 == 0ull;
@@ -492,9 +510,16 @@ __device__ __forceinline__ void nn_drain4(const KConst& K, const float4* __restr
     float rr21 = drx1 * drx1 + dry1 * dry1 + drz1 * drz1;
     const bool ok1 = rr21 <= K.kernelsize2 && rr21 >= ALMOSTZERO;
     rr21 = ok1 ? rr21 : 1e30f;
-    const float4 C1 = sC.ld(j1, KIND == 1);
+    float4 C1;
+    if (UNI) {  // no phase tag: the unit's phase is known
+      const float2 v = sC.c[j1];
+      C1 = make_float4(v.x, 0.f, v.y, 0.f);
+    } else {
+      C1 = sC.ld(j1, KIND == 1);
+    }
     if (KIND == 2) nn_bound_pair<FT>(K, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a, sph);
-    else nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1, false, FT>(K, sph, p, drx1, dry1, drz1, rr21, ok1, B1, C1, a);
+    else nn_pair<TVISCO, TDENSITY, SHIFT, KIND == 1, false, FT, UNI>(K, sph, p, drx1, dry1, drz1, rr21, ok1, B1, C1,
+                                                                    a, u);
     keep_w(A1, B1);  // 16-B LDS reads (sph_tiled.hpp)
   }
 }
@@ -512,7 +537,8 @@ __device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid&
                                                  const float4* __restrict__ velrhop, const float* __restrict__ press,
                                                  const typecode* __restrict__ code, float4* __restrict__ sA,
                                                  float4* __restrict__ sB, NNSC sC,
-                                                 const float4* __restrict__ sph, NNAcc& a) {
+                                                 const float4* __restrict__ sph, NNAcc& a,
+                                                 const NNUni& unph = NNUni{}) {
   // KIND 1 (bound p2) only where no pair can freeze the shifting sums (no shifting, or
   // ShiftMode Full): the caller keeps the reference order otherwise
   const unsigned cellinit = KIND == 1 ? 0u : g.boxfluid;
@@ -544,9 +570,12 @@ __device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid&
     if (n0 + n1 == 0u) continue;  // block-uniform
     if (n0 + n1 <= unsigned(NN_TCAP)) {
       __syncthreads();
-      if (n0) nn_stage(K, rs[0], n0, rc.xo, dya, dza, KIND == 1, poscell, velrhop, press, code, sA, sB, sC, 0u);
-      if (n1) nn_stage(K, rs[1], n1, rc.xo, -dya, -dza, KIND == 1, poscell, velrhop, press, code, sA, sB, sC, n0);
-      __syncthreads();
+      bool same = KIND == 0 && unph.k >= 0 && p.p1uni;
+      if (n0) nn_stage(K, rs[0], n0, rc.xo, dya, dza, KIND == 1, poscell, velrhop, press, code, sA, sB, sC, 0u, &same, unph.k);
+      if (n1)
+        nn_stage(K, rs[1], n1, rc.xo, -dya, -dza, KIND == 1, poscell, velrhop, press, code, sA, sB, sC, n0, &same, unph.k);
+      // the block's vote (and the barrier after the staging): a single-phase unit (NNUni)
+      const bool uni = KIND == 0 ? __syncthreads_and(int(same)) != 0 : (__syncthreads(), false);
       const int wa0 = int(ls[0] - rs[0]), wa1 = rc.act && n0 ? int(le[0] - rs[0]) : wa0;
       const int wb0 = int(n0 + ls[1] - rs[1]), wb1 = rc.act && n1 ? int(n0 + le[1] - rs[1]) : wb0;
       for (int off = 0;; off += 128) {  // a second round only for windows of > 128 candidates
@@ -555,8 +584,12 @@ __device__ __forceinline__ void nn_pass_mirrored(const KConst& K, const DivGrid&
         unsigned long long c0, c1, c2, c3;
         test128(sA, wa0 + off, min(na, 128), px2, py2, pz2, thr, c0, c1);
         test128(sA, wb0 + off, min(nb, 128), px2, py2, pz2, thr, c2, c3);
-        nn_drain4<TVISCO, TDENSITY, SHIFT, KIND, FT>(K, sph, p, c0, c1, c2, c3, wa0 + off, wa0 + off + 64, wb0 + off,
-                                                 wb0 + off + 64, sA, sB, sC, a);
+        if (KIND == 0 && uni)
+          nn_drain4<TVISCO, TDENSITY, SHIFT, KIND, FT, KIND == 0>(K, sph, p, c0, c1, c2, c3, wa0 + off, wa0 + off + 64,
+                                                                  wb0 + off, wb0 + off + 64, sA, sB, sC, a, unph);
+        else
+          nn_drain4<TVISCO, TDENSITY, SHIFT, KIND, FT>(K, sph, p, c0, c1, c2, c3, wa0 + off, wa0 + off + 64, wb0 + off,
+                                                   wb0 + off + 64, sA, sB, sC, a);
       }
     } else {  // too long for one segment: each row on its own, in TCAP segments
       for (int k = 0; k < 2; k++) {
@@ -745,6 +778,25 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
     p.mph = sph[2 * p.ph].x;
     p.taumax = sph[2 * p.ph + 1].z;
     p.bimulti = sph[2 * p.ph + 1].w;
+    // the item's phase: that of its first particle when it is a fluid particle (NNUni)
+    NNUni u;
+    {
+      const typecode c0 = code[item.z];
+      u.k = (bitem || CodeType(c0) != CODE_TYPE_FLUID) ? -1 : int(c0 & CODE_MASKVALUE);
+      u.k = __builtin_amdgcn_readfirstlane(u.k);
+      const int kk = u.k < 0 ? 0 : u.k;
+      const float4 ta = sph[2 * kk], tc = sph[2 * SPH_MAXPHASES + kk];
+      u.a = make_float4(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ta.x))),
+                        __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ta.y))),
+                        __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ta.z))),
+                        __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(ta.w))));
+      u.c = make_float4(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(tc.x))),
+                        __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(tc.y))),
+                        __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(tc.z))),
+                        __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(tc.w))));
+    }
+    p.uph = u.k;
+    p.p1uni = !act || (int(code[p1] & CODE_MASKVALUE) == u.k && CodeType(code[p1]) == CODE_TYPE_FLUID);
     const int lxa = max(cx1 - S, 0), lxb = min(cx1 + S, g.ncx - 1);
     const float thr = K.kernelsize2 * 1.0001f - (p.x * p.x + p.y * p.y + p.z * p.z);
     const RowCtx rc{cy, cz, xa, xb, lxa, lxb, xo, act, p1};
@@ -771,7 +823,7 @@ __global__ __launch_bounds__(TB) SPH_NN_WAVES_ATTR void k_nn_tiled(DevScalars* _
       }
     }
     nn_pass_mirrored<TVISCO, TDENSITY, SHIFT, 0, S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB,
-                                                     sC, sph, f);
+                                                     sC, sph, f, u);
     if (SHIFT && __syncthreads_or(int(f.hv)))
       f.sx = nn_sx_sweep<S, FT>(K, g, rc, p, thr, bc, poscell, velrhop, press, code, sA, sB, sC, sph, f.hv, f.sx);
     if (FT && f.ftsx) f.sx = FLT_MAX;  // x stays FLT_MAX once set (no reset after it)

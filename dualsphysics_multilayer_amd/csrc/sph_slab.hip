@@ -374,8 +374,14 @@ __global__ __launch_bounds__(FS_BS) void k_face_scan(SlabFaces f, SlabCounts* __
     const unsigned i = t0 + k * FS_BS + threadIdx.x;
     v[k * FS_BS + threadIdx.x] = i < n ? c[i] : 0u;
   }
-  unsigned below = 0;
-  for (unsigned i = threadIdx.x; i < t0; i += FS_BS) below += c[i];
+  unsigned below = 0;  // the earlier tiles: FS_PT loads per thread in flight at once
+  for (unsigned i0 = 0; i0 < t0; i0 += FS_TILE) {
+    unsigned e[FS_PT];
+#pragma unroll
+    for (int k = 0; k < FS_PT; k++) e[k] = c[i0 + k * FS_BS + threadIdx.x];  // whole tiles: in range
+#pragma unroll
+    for (int k = 0; k < FS_PT; k++) below += e[k];
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) below += __shfl_xor(below, off, 64);
   if (lane == 0) wsum[w] = below;

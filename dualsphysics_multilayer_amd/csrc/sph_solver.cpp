@@ -1969,6 +1969,22 @@ void SphGpuSingle::DownloadInteraction(SphInterOut& out) {
   Sync();
 }
 
+unsigned SphGpuSingle::DownloadNormals(float* out, unsigned cap, int* usenormalsft) {
+  if (!normal_) throw SphError(SPH_ERR_STATE, "the case has no mDBC normals");
+  if (usenormalsft) *usenormalsft = ftnormals_ ? 1 : 0;
+  if (!out) return nnormal_;
+  if (cap < nnormal_) throw SphError(SPH_ERR_ARG, "normals buffer too small");
+  Sync();
+  std::vector<float4> v(nnormal_);
+  check_hip(hipMemcpy(v.data(), normal_, sizeof(float4) * nnormal_, hipMemcpyDeviceToHost), "download normals");
+  for (unsigned i = 0; i < nnormal_; i++) {
+    out[3 * i] = v[i].x;
+    out[3 * i + 1] = v[i].y;
+    out[3 * i + 2] = v[i].z;
+  }
+  return nnormal_;
+}
+
 void SphGpuSingle::CountPairs(uint64_t out[6]) {
   check_hip(hipMemsetAsync(pairs_, 0, 8 * 6, stream), "memset pairs");
   launch_count_pairs(stream, cap_, sc_, poscell_, begincell_, G, K, pairs_);

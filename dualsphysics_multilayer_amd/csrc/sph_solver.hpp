@@ -48,6 +48,13 @@ void partfloat_write(const std::string& path, const char* app, uint32_t mkboundf
                      const uint32_t* step, const double* timestep, const double* center, const float* fvel,
                      const float* fomega, const float* facelin, const float* faceang);
 uint32_t normals_read(const std::string& path, uint32_t cap, double* out);
+void partfloat_read(const std::string& path, uint32_t cpart, uint32_t nft, double* center, float* fvel,
+                    float* fomega, double* timestep);
+uint32_t extra_normals_read(const std::string& path, uint32_t casenbound, uint32_t casenfloat, uint32_t cap,
+                            float* normals, int32_t* usenormalsft);
+void extra_normals_write(const std::string& path, const char* app, uint32_t cpart, uint32_t step, double timestep,
+                         uint32_t casenbound, uint32_t casenfloat, int32_t usenormalsft, uint32_t nsize,
+                         const float* normals);
 void normals_write(const std::string& path, const char* case_name, double dp, double h, double dist, uint32_t nbound,
                    const double* nor);
 
@@ -83,6 +90,8 @@ class SphGpuSingle {
   SphRunStats Stats();
   unsigned DtTrace(double* out, unsigned cap);
   void Download(SphParticlesHost& out);
+  // mDBC: the current vectors particle -> ghost node by idp (the extra data of a PART)
+  unsigned DownloadNormals(float* out, unsigned cap, int* usenormalsft);
   void DownloadInteraction(SphInterOut& out);
   void CountPairs(uint64_t out[6]);
   void SetTiming(bool on);

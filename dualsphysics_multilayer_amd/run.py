@@ -97,12 +97,35 @@ def cell_domain_limits(k: dict, pos: np.ndarray, npb: int) -> tuple[list, list]:
     return (dpm + scell * lo).tolist(), (dpm + scell * hi).tolist()
 
 
+class _ExtraParts:
+    """JDsExtraDataSave::Config + CheckSave (JDsExtraData.cpp:63-80): an interval n (every PART
+    cpart > 0 with cpart % n == 0) or a JRangeFilter list such as "2,5-7"."""
+
+    def __init__(self, spec: str):
+        spec = str(spec).strip()
+        self.every, self.allowed = 0, None
+        if spec.isdigit():
+            self.every = int(spec)
+            return
+        self.every, self.allowed = 1, set()
+        for tok in spec.split(","):
+            tok = tok.strip()
+            a, _, b = tok.partition("-")
+            if not a.isdigit() or (b and not b.isdigit()):
+                raise CaseError(f"invalid SaveExtraParts value {spec!r}")
+            self.allowed.update(range(int(a), int(b or a) + 1))
+
+    def check(self, cpart: int) -> bool:
+        return (cpart > 0 and self.every > 0 and cpart % self.every == 0
+                and (self.allowed is None or cpart in self.allowed))
+
+
 class CaseRun:
     """One case on one GPU from its initial (or restart) state to TimeMax."""
 
     def __init__(self, case: XmlCase, dirout: str, *, device: int = 0, nsteps_break: int = 0,
                  sv_all_steps: bool = False, sv_pos_double: bool = False, save: bool = True,
-                 app_name: str = "dualsphysics_multilayer_amd", log=None):
+                 app_name: str = "dualsphysics_multilayer_amd", log=None, sv_extra_parts: str | None = None):
         self.case = case
         self.dirout = dirout
         self.nsteps_break = int(nsteps_break)
@@ -121,6 +144,10 @@ class CaseRun:
         self.parts: list[dict] = []
         self._nout_prev = 0
         self._ftparts: list[dict] = []
+        # SaveExtraParts / -svextraparts (JSph.cpp:598,765; JDsExtraDataSave::Config): the mDBC
+        # normals of every n-th PART (or of the listed PARTs), for a restart with mDBC
+        sv = getattr(case, "sv_extra_parts", "") if sv_extra_parts is None else sv_extra_parts
+        self._extra = _ExtraParts(sv) if (sv and case.tboundary == 2) else None
         if save:
             os.makedirs(dirout, exist_ok=True)
 
@@ -162,6 +189,19 @@ class CaseRun:
                     [b for b in self.case.blocks if b["type"] == "fixed"]) == 1 and len(
                     [b for b in self.case.blocks if b["type"] == "fluid"]) == 1:
                 write_part_head(os.path.join(self.dirout, "Part_Head.ibi4"), hdr)
+            if self._extra is not None and self._extra.check(cpart):
+                # PartExtra_%04u.bi4 (JSphGpuSingle::SaveExtraData, JSphGpuSingle.cpp:946-968)
+                from .core import write_extra_normals
+
+                nor, useft = self.solver.normals()
+                nfl = int(getattr(self.case, "case_nfloat", 0))
+                useft = useft and nfl > 0
+                nsize = self.case.case_nbound if useft else self.case.case_nbound - nfl
+                vnor = np.zeros((nsize, 3), np.float32)
+                m = min(nsize, len(nor))
+                vnor[:m] = nor[:m]
+                write_extra_normals(os.path.join(self.dirout, "PartExtra_%04u.bi4" % cpart), self.app_name, cpart,
+                                    step, float(st["time"]), self.case.case_nbound, nfl, vnor, useft)
             if getattr(self.case, "floatings", None):
                 # PartFloat.fbi4: the body states of every saved PART (JSphCpuSingle SaveData ->
                 # JPartFloatBi4Save::AddPartFloat/SavePartFloat)
@@ -234,7 +274,7 @@ USAGE = """usage: python -m dualsphysics_multilayer_amd <case> [<dirout>] [optio
   <case>        case path without extension (<case>.xml + <case>.bi4)
   options (as DualSPHysics): -gpu[:id] -symplectic -verlet[:steps] -wendland -viscoart:v
   -viscoboundfactor:v -ddt:0..3 -ddtvalue:v -dbc -mdbc -mdbc_threshold:v -cellmode:full|half -cellfixed[:0|1]
-  -saveposdouble[:0|1] -sv:binx|none -partbegin:n <dir> -rhopout:min:max -cfl:v -tmax:t
+  -saveposdouble[:0|1] -svextraparts:<n|list> -sv:binx|none -partbegin:n <dir> -rhopout:min:max -cfl:v -tmax:t
   -tout:t -domain_fixed:xmin:ymin:zmin:xmax:ymax:zmax -nsteps:n -svsteps[:0|1] -nortimes[:0|1]
   -dirout <dir> -name <case> -stable -svres -svtimers -ompthreads:n (accepted, no effect)"""
 
@@ -246,7 +286,7 @@ def _f32(s: str) -> float:
 def parse_args(argv: list[str]) -> dict:
     """JSphCfgRun::LoadArgv for the options this core runs; the rest raise CaseError."""
     o = dict(case=None, dirout=None, device=0, overrides={}, partbegin=0, partbegin_dir=None, nsteps=0,
-             svsteps=False, nortimes=False, saveposdouble=False, save=True, domain_fixed=None)
+             svsteps=False, nortimes=False, saveposdouble=False, save=True, domain_fixed=None, svextraparts=None)
     ov = o["overrides"]
     pos = []
     i = 0
@@ -278,6 +318,8 @@ def parse_args(argv: list[str]) -> dict:
             pass  # the sort is always stable; logs / threads / defaults have no effect here
         elif word == "SAVEPOSDOUBLE":
             o["saveposdouble"] = (int(full) if full else 1) != 0
+        elif word == "SVEXTRAPARTS":  # JSphCfgRun.cpp:287: PART interval or list of the extra data
+            o["svextraparts"] = full
         elif word == "CELLMODE":
             v = full.upper()  # JSphCfgRun.cpp:295-299
             if v in ("HALF", "H"):
@@ -417,7 +459,7 @@ def main(argv: list[str] | None = None) -> int:
         case = load_from_args(o)
         dirout = o["dirout"] or os.path.join(os.path.dirname(o["case"]) or ".", case.case_name + "_out")
         r = CaseRun(case, dirout, device=o["device"], nsteps_break=o["nsteps"], sv_all_steps=o["svsteps"],
-                    sv_pos_double=o["saveposdouble"], save=o["save"])
+                    sv_pos_double=o["saveposdouble"], save=o["save"], sv_extra_parts=o["svextraparts"])
         try:
             r.run()
         finally:

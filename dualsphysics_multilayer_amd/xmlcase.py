@@ -350,8 +350,10 @@ class XmlCase:
                 raise CaseError("Symmetry is only allowed with Artificial viscosity.")
         # -- particles (JPartsLoad4::LoadParticles) ------------------------------------
         self.partbegin = int(partbegin)
+        self.partbegin_dir = None
         if self.partbegin:
             d = partbegin_dir if partbegin_dir is not None else os.path.dirname(casepath)
+            self.partbegin_dir = d
             fn = os.path.join(d, "Part_%04u.bi4" % self.partbegin)
         else:
             fn = casepath + ".bi4"
@@ -375,8 +377,7 @@ class XmlCase:
         if self.npb != self.case_npb:
             raise CaseError(f"{fn}: {self.npb} boundary particles loaded, the case has {self.case_npb}.")
         if self.floatings and self.partbegin:
-            raise CaseError("Restart of a case with floating bodies (PartFloat.fbi4 state) is not supported by "
-                            "this core.")
+            self._restart_floatings()
         if self.floatings and self.rigidalgorithm != 1:
             raise CaseError("Only RigidAlgorithm=1 (SPH) floating bodies are supported by this core.")
         # case limits (JPartsLoad4 CasePosMin/Max; computed when the file has none)
@@ -399,13 +400,40 @@ class XmlCase:
         if self.tboundary == 2:
             self._boundnormal = self._load_normals()
 
+    # -- JSphCpu::InitFloating (JSphCpu.cpp:1885-1905) ---------------------------------------
+    def _restart_floatings(self) -> None:
+        """Restart: every body continues from its state at the PART in PartFloat.fbi4 (center,
+        fvel, fomega; the reference starts its angles again from 0)."""
+        from .core import read_partfloat
+
+        fn = os.path.join(self.partbegin_dir, "PartFloat.fbi4")
+        if not os.path.exists(fn):
+            raise CaseError(f"File of floating data was not found: {fn}")
+        st = read_partfloat(fn, self.partbegin, len(self.floatings))
+        for k, f in enumerate(self.floatings):
+            f["center"] = tuple(float(x) for x in st["center"][k])
+            f["linvelini"] = tuple(float(x) for x in st["fvel"][k])
+            f["angvelini"] = tuple(float(x) for x in st["fomega"][k])
+
     # -- JSph::LoadBoundNormals (JSph.cpp:1265-1295) ------------------------------------------
     def _load_normals(self) -> np.ndarray:
-        from .core import read_normals
+        from .core import read_extra_normals, read_normals
 
-        if self.partbegin:  # JSph::ConfigBoundNormals needs the run's extra data (JSph.cpp:1308-1315)
-            raise CaseError("No extra data available to restart at PART_%04d with mDBC." % self.partbegin)
         out = np.zeros((self.np, 3), np.float32)
+        if self.partbegin:
+            # JSph::ConfigBoundNormals (JSph.cpp:1308-1316): the normals of the PART from the
+            # run's extra data; they are the vectors to the ghost node already, so they are
+            # halved here (exact) for the core, which doubles the case file's normals
+            fn = os.path.join(self.partbegin_dir, "PartExtra_%04u.bi4" % self.partbegin)
+            if not os.path.exists(fn):
+                raise CaseError("No extra data available to restart at PART_%04d with mDBC." % self.partbegin)
+            nor, useft = read_extra_normals(fn, self.case_nbound, getattr(self, "case_nfloat", 0))
+            sel = self.idp < np.uint32(len(nor))
+            sel[self.npb:] &= useft  # floating particles only with UseNormalsFt
+            out[sel] = nor[self.idp[sel]] * np.float32(0.5)
+            if not out[: self.npb].any():
+                raise CaseError("No valid normal vectors for using mDBC.")
+            return out
         fn = self.casepath + "_Normals.nbi4"
         if os.path.exists(fn):
             nor = read_normals(fn)
@@ -448,6 +476,8 @@ class XmlCase:
         if kern not in (1, 2):
             raise CaseError("Kernel choice is not valid.")
         self.kernel = kern
+        # SaveExtraParts (JSph.cpp:598): PART interval (or list) of the mDBC extra data files
+        self.sv_extra_parts = p.values.get("SaveExtraParts", "")
         rig = p.int("RigidAlgorithm", True, 1)
         if rig not in (0, 1, 2, 3):
             raise CaseError("Rigid algorithm is not valid.")

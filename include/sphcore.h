@@ -32,6 +32,8 @@
  *   sph_solver_run ............. JSphGpuSingle::Run main loop (JSphGpuSingle.cpp:853-880):
  *                                ComputeStep_Ver/_Sym + RunCellDivide, device-resident dt
  *   sph_download_particles ..... JSphGpuSingle::ParticlesDataDown (feeds SaveData)
+ *   sph_partfloat_read, sph_extra_normals_read/write, sph_download_normals: restart of floating
+ *     bodies and mDBC (JSphCpu::InitFloating, JSph::ConfigBoundNormals, JDsExtraData)
  *   sph_normals_read/write ..... JSph::LoadBoundNormals (JSph.cpp:1265-1295) over
  *                                JPartNormalData::LoadFile/SaveFile (JPartNormalData.cpp:178-257)
  *   sph_count_pairs ............ JDsPips::ComputeGpu (JDsPips.cpp:187-262) — work counter
@@ -533,6 +535,27 @@ int sph_partfloat_write(const char* path, const char* app, uint32_t mkboundfirst
                         const float* massp, const float* radius, uint32_t nparts, const uint32_t* cpart,
                         const uint32_t* step, const double* timestep, const double* center, const float* fvel,
                         const float* fomega, const float* facelin, const float* faceang);
+/* Restart of floating bodies (JSphCpu::InitFloating, JSphCpu.cpp:1885-1905): the state of
+ * PART cpart in PartFloat.fbi4 (JPartFloatBi4Load::LoadPart) — center[nft][3], fvel, fomega
+ * (any pointer may be NULL) and its TimeStep.  The reference restarts a body with these and
+ * its angles at 0; a run driver passes them as the body's center / initial velocities. */
+int sph_partfloat_read(const char* path, uint32_t cpart, uint32_t nft, double* center, float* fvel, float* fomega,
+                       double* timestep);
+/* mDBC extra data of a PART, PartExtra_%04u.bi4 (JDsExtraDataSave / JDsExtraDataLoad,
+ * JDsExtraData.cpp; written every SaveExtraParts-th PART, -svextraparts): the Normals
+ * float3[nsize] by idp, each the boundary particle's vector to its ghost node (twice the case
+ * file's normal; turned with moving and floating bodies) and UseNormalsFt.  A restart with mDBC
+ * reloads them (JSph::ConfigBoundNormals, JSph.cpp:1308-1316).  read: normals may be NULL
+ * (nsize only); the case's CaseNbound / CaseNfloat must match the file's. */
+int sph_extra_normals_read(const char* path, uint32_t casenbound, uint32_t casenfloat, uint32_t cap, float* normals,
+                           uint32_t* nsize, int32_t* usenormalsft);
+int sph_extra_normals_write(const char* path, const char* app, uint32_t cpart, uint32_t step, double timestep,
+                            uint32_t casenbound, uint32_t casenfloat, int32_t usenormalsft, uint32_t nsize,
+                            const float* normals);
+/* The solver's current mDBC vectors particle -> ghost node by idp ([n][3]; normals NULL: n
+ * only) and whether the floating bodies have them (UseNormalsFt) — JSphGpuSingle::SaveExtraData
+ * (JSphGpuSingle.cpp:946-968). */
+int sph_download_normals(SphSolver* s, uint32_t cap, float* normals, uint32_t* n, int32_t* usenormalsft);
 
 #ifdef __cplusplus
 }
