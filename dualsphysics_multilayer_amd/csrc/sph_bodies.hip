@@ -476,21 +476,32 @@ __global__ __launch_bounds__(FT_BS) void k_ft_partial(const DevScalars* __restri
 }
 
 // JLinearValue::GetValue3f at time t (JLinearValue.cpp:209-247 FindTime, :301-329
-// GetValue3d, :387-390) of one table of n (time, x, y, z) rows with nondecreasing times:
-// the bracketing rows are the first row >= 1 whose time is >= t (else the last) and the
-// row before it (what FindTime's cached search settles on for sorted times), the factor
+// GetValue3d, :387-390) of one table of n (time, x, y, z) rows, in any row order as the
+// reference reads them (<vel> elements or a file): FindTime walks from the row of its last
+// call (back while the row's time is >= t, then forward to the first later row whose time is
+// >= t, the row before it as the lower one), and a call at the TimeStep of the last one keeps
+// that interval (the Symplectic predictor and corrector of one step); the factor
 // (t - tpre)/(tnext - tpre) clamped to [0,1] (0 for equal times), linear interpolation in
-// double without contraction; DBL_MAX ("none") propagates from the earlier row, an
-// interval ending in "none" keeps the earlier value; DBL_MAX -> FLT_MAX.
-__device__ void ft_table_eval(const double4* __restrict__ tab, int2 d, double t, float out[3]) {
-  const double4* T = tab + d.x;
-  const int n = d.y;
-  int pos = 0, posnext = 0;
-  if (n > 1) {
-    posnext = 1;
-    while (posnext + 1 < n && T[posnext].x < t) posnext++;
-    pos = posnext - 1;
+// double without contraction; DBL_MAX ("none") propagates from the earlier row, an interval
+// ending in "none" keeps the earlier value; DBL_MAX -> FLT_MAX.
+__device__ void ft_table_eval(const double4* __restrict__ tab, FtTabDesc& d, double t, float out[3]) {
+  const double4* T = tab + d.first;
+  const int n = d.n;
+  if (d.pos < 0 || t != d.t) {
+    int pos = d.pos < 0 ? 0 : d.pos, posnext = pos;
+    double tpre = T[pos].x, tnext = tpre;
+    if (n > 1) {
+      while (tpre >= t && pos > 0) tpre = T[--pos].x;  // back
+      posnext = pos + 1 < n ? pos + 1 : pos;
+      tnext = T[posnext].x;
+      while (tnext < t && posnext + 1 < n) tnext = T[++posnext].x;  // forward
+      if (posnext - pos > 1) pos = posnext - 1;
+    }
+    d.pos = pos;
+    d.posnext = posnext;
+    d.t = t;
   }
+  const int pos = d.pos, posnext = d.posnext;
   const double tpre = T[pos].x, tnext = T[posnext].x, tdif = tnext - tpre;
   double f = tdif != 0.0 ? (t - tpre) / tdif : 0.0;
   if (f < 0.) f = 0.;
@@ -514,7 +525,7 @@ __device__ void ft_table_eval(const double4* __restrict__ tab, int2 d, double t,
 // tables (desc[body*4 + kind] = {first row, rows}, kinds SPH_FTTAB_*; nullptr: none).
 __global__ void k_ft_forces(const DevScalars* __restrict__ sc, KConst K, FtBody* __restrict__ bodies, int nbodies,
                             const float* __restrict__ part, int predictor, const double4* __restrict__ tab,
-                            const int2* __restrict__ desc) {
+                            FtTabDesc* __restrict__ desc) {
   const int cf = blockIdx.x * blockDim.x + threadIdx.x;
   if (cf >= nbodies || halted(sc)) return;
   FtBody& b = bodies[cf];
@@ -537,12 +548,12 @@ __global__ void k_ft_forces(const DevScalars* __restrict__ sc, KConst K, FtBody*
   float fo[3] = {red[3], red[4], red[5]};
   // external forces (RunFloating, JSphCpuSingle.cpp:904-914; added in FtCalcForces :797-798)
   const double tstep = sc->tstep0;
-  if (desc && desc[cf * 4 + 2].y) {
+  if (desc && desc[cf * 4 + 2].n) {
     float e[3];
     ft_table_eval(tab, desc[cf * 4 + 2], tstep, e);
     for (int k = 0; k < 3; k++) face[k] = face[k] + e[k];
   }
-  if (desc && desc[cf * 4 + 3].y) {
+  if (desc && desc[cf * 4 + 3].n) {
     float e[3];
     ft_table_eval(tab, desc[cf * 4 + 3], tstep, e);
     for (int k = 0; k < 3; k++) fo[k] = fo[k] + e[k];
@@ -567,13 +578,13 @@ __global__ void k_ft_forces(const DevScalars* __restrict__ sc, KConst K, FtBody*
   for (int k = 0; k < 3; k++) fcenter[k] = b.center[k] + dt * fvel0[k];
   for (int k = 0; k < 3; k++) fvel[k] = float(dt * face[k] + fvel0[k]);
   // FtApplyImposedVel (JSphCpuSingle.cpp:874-891): components given by the tables
-  if (desc && desc[cf * 4 + 0].y) {
+  if (desc && desc[cf * 4 + 0].n) {
     float v[3];
     ft_table_eval(tab, desc[cf * 4 + 0], tstep, v);
     for (int k = 0; k < 3; k++)
       if (v[k] != FLT_MAX) fvel[k] = v[k];
   }
-  if (desc && desc[cf * 4 + 1].y) {
+  if (desc && desc[cf * 4 + 1].n) {
     float v[3];
     ft_table_eval(tab, desc[cf * 4 + 1], tstep, v);
     for (int k = 0; k < 3; k++)
@@ -685,7 +696,7 @@ void launch_ft_partial(hipStream_t stm, DevScalars* sc, const FtBody* bodies, in
 
 void launch_ft_body(hipStream_t stm, DevScalars* sc, const KConst& K, FtBody* bodies, int nbodies,
                     const unsigned* ftridp, unsigned nftp, const PartArrays& a, bool predictor, const float* part,
-                    const double4* fttab, const int2* ftdesc, float4* normal) {
+                    const double4* fttab, FtTabDesc* ftdesc, float4* normal) {
   hipLaunchKernelGGL(k_ft_forces, dim3((nbodies + 63) / 64), dim3(64), 0, stm, sc, K, bodies, nbodies, part,
                      int(predictor), fttab, ftdesc);
   hipLaunchKernelGGL(k_ft_update, dim3((nftp + 255) / 256), dim3(256), 0, stm, sc, K, bodies, nbodies, ftridp, nftp,

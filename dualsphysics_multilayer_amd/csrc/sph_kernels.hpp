@@ -432,6 +432,15 @@ struct MotionDev {
   MotOut out[MOT_MAXOBJ];
 };
 // Floating body (StFloatingData + StFtoForces/StFtoForcesRes), device resident.
+// One JLinearValue table of a floating body on the device: its rows [first, first + n) of
+// the table buffer and the lookup state the reference keeps between calls (FindTime's
+// Position / PositionNext for the TimeStep of the last call; pos < 0: none yet).
+struct FtTabDesc {
+  int first, n;
+  int pos, posnext;
+  double t;
+};
+
 struct FtBody {
   unsigned begin, count;   // floating-particle index range (idp - CaseNpb)
   unsigned constraints;    // FTCON_* bits (DualSphDef.h:445-453)
@@ -465,7 +474,7 @@ void launch_ft_partial(hipStream_t stm, DevScalars* sc, const FtBody* bodies, in
 // normal (mDBC on floating bodies, by idp): turned with the body after a full step.
 void launch_ft_body(hipStream_t stm, DevScalars* sc, const KConst& K, FtBody* bodies, int nbodies,
                     const unsigned* ftridp, unsigned nftp, const PartArrays& a, bool predictor, const float* part,
-                    const double4* fttab = nullptr, const int2* ftdesc = nullptr, float4* normal = nullptr);
+                    const double4* fttab = nullptr, FtTabDesc* ftdesc = nullptr, float4* normal = nullptr);
 
 // ---- slab decomposition (sph_slab.hip) ----
 // A particle MIGRATING to a neighbour: its full state, 112 B.  A boundary particle also

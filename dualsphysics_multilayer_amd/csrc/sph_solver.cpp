@@ -924,6 +924,7 @@ void SphGpuSingle::UploadNormals(const SphCaseDef& cdef, const SphParticlesHost&
 // Restart: TimeStep and SymplecticDtPre of the loaded PART (JSph::InitRun, JSph.cpp:2094-2106).
 void SphGpuSingle::SetTime(double time, double symdtpre) {
   if (motion_) throw SphError(SPH_ERR_STATE, "set the restart time before the motion (it is advanced to that time)");
+  UploadFloatingTables();  // the floating tables' lookups start over (a restart's new JLinearValues)
   Sync();
   check_hip(hipMemcpy(&sc_->time, &time, sizeof(double), hipMemcpyHostToDevice), "set time");
   // the tables' walks start again from their first rows (a restarted reference run loads them anew)
@@ -1733,8 +1734,7 @@ void SphGpuSingle::SetFloatingTable(unsigned body, int kind, unsigned n, const d
     throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase: external forces on floating bodies are not implemented");
   if (!n || !times || !values) throw SphError(SPH_ERR_ARG, "There are not times.");
   std::vector<double4> rows(n);
-  for (unsigned i = 0; i < n; i++) {
-    if (i && !(times[i] >= times[i - 1])) throw SphError(SPH_ERR_ARG, "floating table times must be nondecreasing");
+  for (unsigned i = 0; i < n; i++) {  // rows in the order given (any time order, as the reference)
     const double* v = values + 3 * size_t(i);
     if (kind >= SPH_FTTAB_LINFORCE && (v[0] == DBL_MAX || v[1] == DBL_MAX || v[2] == DBL_MAX))
       throw SphError(SPH_ERR_ARG, "external forces have no 'none' components");
@@ -1742,10 +1742,15 @@ void SphGpuSingle::SetFloatingTable(unsigned body, int kind, unsigned n, const d
   }
   fttabs_.resize(size_t(nftbodies_) * 4);
   fttabs_[size_t(body) * 4 + size_t(kind)] = rows;
+  UploadFloatingTables();
+}
+
+void SphGpuSingle::UploadFloatingTables() {
+  if (fttabs_.empty()) return;
   std::vector<double4> all;
-  std::vector<int2> desc(fttabs_.size(), make_int2(0, 0));
+  std::vector<FtTabDesc> desc(fttabs_.size());
   for (size_t t = 0; t < fttabs_.size(); t++) {
-    desc[t] = make_int2(int(all.size()), int(fttabs_[t].size()));
+    desc[t] = FtTabDesc{int(all.size()), int(fttabs_[t].size()), -1, -1, 0.0};
     all.insert(all.end(), fttabs_[t].begin(), fttabs_[t].end());
   }
   Sync();
@@ -1754,12 +1759,14 @@ void SphGpuSingle::SetFloatingTable(unsigned body, int kind, unsigned n, const d
     (void)hipFree(p);
     allocs_.erase(std::remove(allocs_.begin(), allocs_.end(), p), allocs_.end());
   }
-  check_hip(hipMalloc((void**)&fttab_, sizeof(double4) * all.size()), "hipMalloc floating tables");
+  check_hip(hipMalloc((void**)&fttab_, sizeof(double4) * std::max<size_t>(all.size(), 1)), "hipMalloc floating tables");
   allocs_.push_back(fttab_);
-  check_hip(hipMalloc((void**)&fttabdesc_, sizeof(int2) * desc.size()), "hipMalloc floating tables");
+  check_hip(hipMalloc((void**)&fttabdesc_, sizeof(FtTabDesc) * desc.size()), "hipMalloc floating tables");
   allocs_.push_back(fttabdesc_);
-  check_hip(hipMemcpy(fttab_, all.data(), sizeof(double4) * all.size(), hipMemcpyHostToDevice), "upload tables");
-  check_hip(hipMemcpy(fttabdesc_, desc.data(), sizeof(int2) * desc.size(), hipMemcpyHostToDevice), "upload tables");
+  if (!all.empty())
+    check_hip(hipMemcpy(fttab_, all.data(), sizeof(double4) * all.size(), hipMemcpyHostToDevice), "upload tables");
+  check_hip(hipMemcpy(fttabdesc_, desc.data(), sizeof(FtTabDesc) * desc.size(), hipMemcpyHostToDevice),
+            "upload tables");
 }
 
 // DtFixedFile (JDsFixedDt) and ViscoTime (JDsViscoInput) tables on the device; k_dt reads

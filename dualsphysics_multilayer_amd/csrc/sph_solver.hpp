@@ -239,7 +239,8 @@ class SphGpuSingle {
   float* ftmassp_ = nullptr;     // particle mass per body (interaction)
   float* ftpart_ = nullptr;      // partial force sums [body][FT_NBLK][6]
   double4* fttab_ = nullptr;     // JLinearValue rows (time, x, y, z) of every body's tables
-  int2* fttabdesc_ = nullptr;    // [body][SPH_FTTAB_*] = {first row, rows}
+  FtTabDesc* fttabdesc_ = nullptr;  // [body][SPH_FTTAB_*] = {first row, rows, lookup state}
+  void UploadFloatingTables();    // (again at a restart: the lookups start over, as new JLinearValues)
   std::vector<std::vector<double4>> fttabs_;  // host copy, [body * 4 + kind]
   int nftbodies_ = 0;
   void* dttab_ = nullptr;        // DtFixedFile rows: times [n], dt in ms [n] (double)

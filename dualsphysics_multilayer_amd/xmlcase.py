@@ -41,10 +41,11 @@ DBL_MAX = float(np.finfo(np.float64).max)
 CODE_TYPE_MOVING, CODE_TYPE_FLOATING = 0x800, 0x1000  # 16-bit typecode, DualSphDef.h:200-205
 
 
-def _read_datafile(path: str, what: str) -> np.ndarray:
-    """Rows of (time, value) of a JReadDatafile table (JDsFixedDt / JDsViscoInput::LoadFile):
-    '#' lines are remarks, the separator is the most frequent of tab/space, ';' and ',',
-    values are read as atof reads them; at least two rows."""
+def _read_datafile(path: str, what: str, nvalues: int = 1, special: bool = False) -> np.ndarray:
+    """Rows of (time, value...) of a JReadDatafile table (JDsFixedDt / JDsViscoInput /
+    JLinearValue::LoadFile, JLinearValue.cpp:427-452): '#' lines are remarks, the separator is
+    the most frequent of tab/space, ';' and ',', values are read as atof reads them ("none" is
+    DBL_MAX where the table allows special values); at least two rows."""
     if not os.path.isfile(path):
         raise CaseError(f"{what}: file not found {path}")
     lines = [ln.strip() for ln in open(path).read().replace("\r", "").split("\n")]
@@ -62,9 +63,10 @@ def _read_datafile(path: str, what: str) -> np.ndarray:
     rows = []
     for ln in lines:
         f = ln.split(sep) if sep else ln.split()
-        if len(f) < 2:
-            raise CaseError(f"{what}: value 2 does not exist in line '{ln}' of {path}")
-        rows.append((atof(f[0]), atof(f[1])))
+        if len(f) < 1 + nvalues:
+            raise CaseError(f"{what}: value {len(f) + 1} does not exist in line '{ln}' of {path}")
+        rows.append((atof(f[0]),) + tuple(DBL_MAX if special and v.strip().lower() == "none" else atof(v)
+                                         for v in f[1:1 + nvalues]))
     if len(rows) < 2:
         raise CaseError(f"{what}: Cannot be less than two values. ({path})")
     return np.array(rows, np.float64)
@@ -574,7 +576,7 @@ class XmlCase:
             b = dict(type=e.tag, mk=int(e.get("mk")), begin=int(e.get("begin")), count=int(e.get("count")),
                      mktype=int(e.get("mkfluid") if e.tag == "fluid" else e.get("mkbound")))
             if e.tag == "floating":
-                b["floating"] = self._load_floating(e)
+                b["floating"] = self._load_floating(e, self._dircase)
             blocks.append(b)
         kinds = ("fixed", "moving", "floating", "fluid")
         bytype = {k: [b for b in blocks if b["type"] == k] for k in kinds}
@@ -649,7 +651,7 @@ class XmlCase:
 
     # -- JCasePartBlock_Floating::ReadXml (JCaseParts.cpp:248-290) ------------------------------
     @staticmethod
-    def _load_floating(e) -> dict:
+    def _load_floating(e, casedir: str = ".") -> dict:
         def d3(name, optional=False, default=(0.0, 0.0, 0.0)):
             x = e.find(name)
             if x is None:
@@ -685,19 +687,19 @@ class XmlCase:
         # imposed velocities ("none" components free) and external forces (JCaseParts.cpp:272-285)
         for name, sub, special in (("linearvel", "vel", True), ("angularvel", "vel", True),
                                    ("linearforce", "force", False), ("angularforce", "force", False)):
-            tab = XmlCase._load_linear_values(e, name, sub, special)
+            tab = XmlCase._load_linear_values(e, name, sub, special, casedir)
             if tab is not None:
                 f[name] = tab
         return f
 
     # -- JLinearValue::ReadXmlValues (JLinearValue.cpp:493-527), attributes time:x:y:z ---------------
     @staticmethod
-    def _load_linear_values(e, name, sub, special):
+    def _load_linear_values(e, name, sub, special, casedir):
         x = e.find(name)
         if x is None:
             return None
-        if x.get("file"):
-            raise CaseError(f"<{name} file=...>: tables from files are not supported by this core.")
+        if x.get("file"):  # JSph.cpp:1064-1080: LoadFile(DirCase + file), rows in file order
+            return _read_datafile(os.path.join(casedir, x.get("file")), f"<{name}>", 3, special)
         rows = []
         for r in x.findall(sub):
             t = _attr_double(r, "time", sub)
@@ -714,9 +716,7 @@ class XmlCase:
             rows.append((t,) + tuple(vals))
         if not rows:
             raise CaseError("There are not times.")
-        if any(rows[i][0] < rows[i - 1][0] for i in range(1, len(rows))):
-            raise CaseError(f"<{name}>: times must be nondecreasing.")
-        return np.array(rows, np.float64)
+        return np.array(rows, np.float64)  # in the XML's order (JLinearValue walks them as they come)
 
     # -- JMotion::ReadXml (JMotion.cpp:556-700) + JDsMotion::ConfigObjects (JDsMotion.cpp:67-89) --
     def _load_motion(self, node):

@@ -36,6 +36,10 @@ VARIANTS = {
     # the floating box with imposed velocities ("none" components stay free) and external
     # forces (JLinearValue tables of <floating>, FtApplyImposedVel / GetFtExternalForce*)
     "verlet_ddt2_ftvel": (0.025, 1, 2, 1, 100, (1, 10, 50, 100), (), "ftvel"),
+    # the same tables in the reference's other forms: <linearvel> from a data file
+    # (JLinearValue::LoadFile) and <angularvel> rows out of time order, which JLinearValue walks
+    # as they come (FindTime's persistent Position)
+    "verlet_ddt2_ftvel_file_unordered": (0.025, 1, 2, 1, 100, (1, 10, 50, 100), (), "ftvelfile"),
     # mDBC on the floating box too (genflume_ref ftnormals=1: UseNormalsFt, the normals turned
     # with the body, JSphCpuSingle.cpp:988-999), Verlet and Symplectic
     "verlet_ddt2_mdbc_ftnor": (0.025, 1, 2, 2, 100, (1, 10, 50, 100),
@@ -58,8 +62,19 @@ XML_EDITS = {
               '</linearforce>'
               '<angularforce><force time="0" x="0.002" y="0" z="-0.001"/><force time="0.015" x="0" y="0" z="0.003"/>'
               '</angularforce>'),
+    "ftvelfile": ('<linearvel file="FtLinVel.csv"/>'
+                  '<angularvel><vel time="0" x="none" y="0.4" z="none"/><vel time="0.02" x="none" y="-0.2" z="none"/>'
+                  '<vel time="0.008" x="none" y="-0.6" z="none"/><vel time="0.03" x="none" y="0.1" z="none"/>'
+                  '</angularvel>'
+                  '<linearforce><force time="0.03" x="0.5" y="0.2" z="1"/><force time="0" x="0" y="0.2" z="3"/>'
+                  '</linearforce>'),
     # (anchor, text): the text goes before the anchor
     "mdbccorr": ("</parameters>", '<parameter key="MDBCCorrector" value="1"/>\n'),
+}
+# data files of the XML edits (written beside the case)
+DATA_FILES = {
+    "ftvelfile": {"FtLinVel.csv": "# time;vx;vy;vz (m/s)\n0;0.05;none;none\n0.02;-0.1;none;0.05\n"
+                                  "0.006;0.2;none;none\n0.025;0;none;none\n"},
 }
 
 
@@ -92,7 +107,11 @@ def make(name, dp, step, ddt, boundary, nsteps, keep, extra=(), xml_edit=None):
             anchor, text = edit if isinstance(edit, tuple) else ("</floating>", edit)
             assert txt.count(anchor) == 1
             open(fx, "w").write(txt.replace(anchor, text + anchor))
-        files = ["CaseFlume.xml", "CaseFlume.bi4"] + (["CaseFlume_Normals.nbi4"] if boundary == 2 else [])
+        datafiles = DATA_FILES.get(xml_edit, {}) if xml_edit else {}
+        for fn, text in datafiles.items():
+            open(os.path.join(tmp, fn), "w").write(text)
+        files = (["CaseFlume.xml", "CaseFlume.bi4"] + (["CaseFlume_Normals.nbi4"] if boundary == 2 else [])
+                 + sorted(datafiles))
         for f in files:
             shutil.copy(os.path.join(tmp, f), os.path.join(out_dir, f))
         out = os.path.join(tmp, "out")

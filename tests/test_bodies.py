@@ -94,11 +94,8 @@ def test_unsupported_body_features_refused(tmp_path):
 
     with pytest.raises(CaseError, match="RigidAlgorithm"):
         XmlCase(variant(lambda s: s.replace('key="RigidAlgorithm" value="1"', 'key="RigidAlgorithm" value="2"')))
-    with pytest.raises(CaseError, match="from files"):
+    with pytest.raises(CaseError, match="file not found"):  # a table file the case does not have
         XmlCase(variant(lambda s: s.replace("</floating>", '<linearvel file="vel.csv"/></floating>')))
-    with pytest.raises(CaseError, match="nondecreasing"):
-        XmlCase(variant(lambda s: s.replace("</floating>", '<linearforce><force time="1" x="0" y="0" z="0"/>'
-                                                          '<force time="0" x="0" y="0" z="0"/></linearforce></floating>')))
     with pytest.raises(CaseError, match="mvcir"):
         XmlCase(variant(lambda s: s.replace("<wait ", "<mvcir ")))
     with pytest.raises(CaseError, match="mobile objects"):
@@ -435,6 +432,19 @@ def test_gpu_mdbc_flap_normals_cross_slab_faces():
 
 # ---- imposed floating velocities and external forces -----------------------------------------
 FTVEL = "verlet_ddt2_ftvel"
+# the same kind of tables as a data file (<linearvel file=...>, JLinearValue::LoadFile) and
+# with rows out of time order (<angularvel>, <linearforce>), walked as the reference walks them
+FTVEL_FILE = "verlet_ddt2_ftvel_file_unordered"
+
+
+def test_floating_tables_from_file_and_unordered_loaded():
+    f = _case(FTVEL_FILE).floatings[0]
+    big = np.finfo(np.float64).max
+    lv = f["linearvel"]  # the data file, in its row order, "none" -> DBL_MAX
+    assert lv.shape == (4, 4) and list(lv[:, 0]) == [0.0, 0.02, 0.006, 0.025]
+    assert lv[0, 1] == 0.05 and lv[0, 2] == big and lv[1, 3] == 0.05 and lv[2, 1] == 0.2
+    assert list(f["angularvel"][:, 0]) == [0.0, 0.02, 0.008, 0.03]  # XML order kept
+    assert list(f["linearforce"][:, 0]) == [0.03, 0.0]
 
 
 def test_floating_tables_loaded():
@@ -452,12 +462,13 @@ def test_floating_tables_loaded():
 
 
 @pytest.mark.gpu
-def test_gpu_floating_imposed_velocity_matches_reference():
+@pytest.mark.parametrize("variant", [FTVEL, FTVEL_FILE])
+def test_gpu_floating_imposed_velocity_matches_reference(variant):
     """The floating box with imposed x/z velocities and y rotation rate over time (free
     components integrated) and external forces/torques (JSphCpuSingle.cpp:874-924): body
     state after every step vs the reference's PartFloat.fbi4 -- imposed components equal the
     reference's to float rounding of the table time --, particles vs the reference PARTs."""
-    x, g = _case(FTVEL), _ref(FTVEL)
+    x, g = _case(variant), _ref(variant)
     s = _gpu(x)
     n = int(g["meta"][3])
     kept = set(_kept(g))
@@ -479,6 +490,9 @@ def test_gpu_floating_imposed_velocity_matches_reference():
     # the imposed components are the table's values (step 1: TimeStep 0)
     b1 = g["ft_fvel"][1, 0]
     assert b1[0] == np.float32(0.05) and g["ft_fomega"][1, 0][1] == np.float32(0.4)
+    if variant == FTVEL_FILE:  # the unordered rows matter: the reference's walk is not a sorted lookup
+        srt = _ref(FTVEL)
+        assert np.abs(g["ft_fomega"][:, 0, 1] - srt["ft_fomega"][:, 0, 1]).max() > 0
 
 
 @pytest.mark.gpu

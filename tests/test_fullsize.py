@@ -198,8 +198,9 @@ NN_FLOOR = (2e-10, 2e-8, 2.5e-3)
 
 
 def test_cfg5_2m_nn_matches_reference():
-    """1 step of the 2M NN case against the reference v5.0 NN solver, at 10x the fast-math vs
-    strict difference of the reference itself on this case (with few-ulp floors)."""
+    """Steps 1 and 3 of the 2M NN case against the reference v5.0 NN solver, at 10x the
+    fast-math vs strict difference of the reference itself on this case at the same step
+    (with few-ulp floors)."""
     _need("gennn_ref", "DualSPHysics5.0NN_CPU_ref", "partdump_ref")
     strict = os.path.exists(os.path.join(REF, "DualSPHysics5.0NN_CPU_strict"))
     from dualsphysics_multilayer_amd.xmlcase import XmlCase
@@ -210,17 +211,24 @@ def test_cfg5_2m_nn_matches_reference():
                               stdout=subprocess.DEVNULL)
         case = XmlCase(os.path.join(tmp, "CaseNN"))
         assert case.np == WetDambreakNNCase(CFG5_DP, width=CFG5_WIDTH).np == 2015071
-        ref, _ = _ref_parts("DualSPHysics5.0NN_CPU_ref", os.path.join(tmp, "CaseNN"), 1, (1,), tmp, "ref")
-        if strict:
-            refs, _ = _ref_parts("DualSPHysics5.0NN_CPU_strict", os.path.join(tmp, "CaseNN"), 1, (1,), tmp, "strict")
-            noise = [maxdiff(ref[1], refs[1], q) for q in ("pos", "vel", "rhop")]
-        else:  # the noise floor of the 20k-particle fixture at step 1 (tests/golden/nn_sym_lam_dp0.02.npz)
-            noise = list(np.load(os.path.join(HERE, "golden", "nn_sym_lam_dp0.02.npz"))["noise_1"])
-        tl = tuple(max(10.0 * float(noise[i]), NN_FLOOR[i]) for i in range(3))
+        ref, _ = _ref_parts("DualSPHysics5.0NN_CPU_ref", os.path.join(tmp, "CaseNN"), 3, (1, 3), tmp, "ref")
         g = _gpu(case)
-        g.run(1)
-        _check(by_idp(g.particles()), ref[1], tl, 1)
-        assert abs(g.stats()["time"] - ref[1]["time"]) <= 1e-9
+        done = 0
+        for k in (1, 3):
+            if strict:
+                if k == 1:
+                    refs, _ = _ref_parts("DualSPHysics5.0NN_CPU_strict", os.path.join(tmp, "CaseNN"), 3, (1, 3), tmp,
+                                         "strict")
+                noise = [maxdiff(ref[k], refs[k], q) for q in ("pos", "vel", "rhop")]
+            else:  # the noise floor of the 20k-particle fixture (tests/golden/nn_sym_lam_dp0.02.npz):
+                # step 1, or step 10 for step 3
+                noise = list(np.load(os.path.join(HERE, "golden", "nn_sym_lam_dp0.02.npz"))["noise_%d" % (1 if k == 1
+                                                                                                          else 10)])
+            tl = tuple(max(10.0 * float(noise[i]), NN_FLOOR[i]) for i in range(3))
+            g.run(k - done)
+            done = k
+            _check(by_idp(g.particles()), ref[k], tl, k)
+            assert abs(g.stats()["time"] - ref[k]["time"]) <= 1e-9 * k
     finally:
         shutil.rmtree(tmp)
 
