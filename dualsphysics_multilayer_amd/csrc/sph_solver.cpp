@@ -1728,10 +1728,10 @@ void SphGpuSingle::SetFloatingTable(unsigned body, int kind, unsigned n, const d
   if (stepped_) throw SphError(SPH_ERR_STATE, "floating tables are configured before the first step");
   if (!ftbodies_ || body >= unsigned(nftbodies_)) throw SphError(SPH_ERR_ARG, "floating table of an unknown body");
   if (kind < SPH_FTTAB_LINVEL || kind > SPH_FTTAB_ANGFORCE) throw SphError(SPH_ERR_ARG, "invalid floating table kind");
-  // v5.0 NN sums external forces inside FtCalcForces (JSphCpuSingle.cpp:847 of that solver),
-  // not beside the particle forces as v5.2 does
-  if (nn_ && kind >= SPH_FTTAB_LINFORCE)
-    throw SphError(SPH_ERR_UNSUPPORTED, "NN multiphase: external forces on floating bodies are not implemented");
+  // External forces: v5.2 adds them to FtoForces before FtCalcForces adds the particle sums
+  // (sum + (0 + ext)); the v5.0 NN solver adds them inside FtCalcForces after the sums
+  // (FtSumExternalForces, JSphCpuSingle.cpp:849 of that solver): the same float additions, so
+  // both run k_ft_forces's (sph_bodies.hip).
   if (!n || !times || !values) throw SphError(SPH_ERR_ARG, "There are not times.");
   std::vector<double4> rows(n);
   for (unsigned i = 0; i < n; i++) {  // rows in the order given (any time order, as the reference)
@@ -1776,8 +1776,9 @@ void SphGpuSingle::SetTimeTable(int kind, unsigned n, const double* times, const
   if (n == 1 || (n && (!times || !values))) throw SphError(SPH_ERR_ARG, "Cannot be less than two values.");
   if (kind == SPH_TTAB_DTFIXED && n && C.dtfixed > 0)
     throw SphError(SPH_ERR_ARG, "The parameters 'DtFixed' and 'DtFixedFile' cannot be used at the same time.");
-  if (kind == SPH_TTAB_VISCO && n && nn_)
-    throw SphError(SPH_ERR_UNSUPPORTED, "ViscoTime with NN multiphase (per-phase viscosities) is not implemented");
+  // NN multiphase: ViscoTime sets Visco every step (JSphCpuSingle.cpp:1128 of the v5.0 solver),
+  // which no NN interaction reads (they take the phases' viscosities, JSphCpu_NN_FDA.cpp:267,
+  // JSphCpu_NN_SPH.cpp:202,413): the table is kept and, as there, changes nothing.
   Sync();
   void*& buf = (kind == SPH_TTAB_DTFIXED ? dttab_ : viscotab_);
   check_hip(hipMemset(kind == SPH_TTAB_DTFIXED ? &sc_->dtfix_pos : &sc_->visco_pos, 0, sizeof(int)), "reset table row");

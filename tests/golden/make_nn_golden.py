@@ -63,7 +63,35 @@ CASES = {
     "ft_sym_lam_ddt3_half_dp0.025": (0.025, 0.4, 0.5, 2.75, 1, 2, 3, 3, 0.0, 2, 60, (1, 20, 60), ("-cellmode:half",), 1),
     "ft_ver_art_ddt1_nobound_cs_half_dp0.025": (0.025, 0.4, 0.5, 2.75, 1, 1, 1, 1, 20.0, 1, 45, (1, 41, 45),
                                                 ("-cellmode:half",), 1),
+    # external forces on the floating body (FtSumExternalForces inside FtCalcForces of the v5.0
+    # solver) and a ViscoTime table (Visco changes every step; the NN interactions take the
+    # phases' viscosities, so it leaves the result unchanged): the npz carries xmledit
+    "ft_sym_lam_ddt3_extforce_viscotime_dp0.025": (0.025, 0.4, 0.5, 2.75, 1, 2, 3, 3, 0.0, 2, 60, (1, 20, 60), (), 1,
+                                                   "extforce_viscotime"),
 }
+
+# XML edits (anchor, text inserted before it) and data files written beside the case
+XML_EDITS = {
+    "extforce_viscotime": [
+        ("</floating>", '<linearforce><force time="0" x="0.4" y="0" z="2"/><force time="0.02" x="-0.3" y="0.1" z="0.5"/>'
+                        '</linearforce><angularforce><force time="0" x="0" y="0.002" z="0"/>'
+                        '<force time="0.03" x="0.001" y="-0.002" z="0"/></angularforce>'),
+        ("</parameters>", '<parameter key="ViscoTime" value="ViscoT.csv"/>\n'),
+    ],
+}
+DATA_FILES = {"extforce_viscotime": {"ViscoT.csv": "# time;visco\n0;0.05\n0.01;0.2\n0.05;0.01\n"}}
+
+
+def apply_edit(casedir, key):
+    """The XML edit and data files of `key` on the case gennn_ref wrote into casedir."""
+    fx = os.path.join(casedir, "CaseNN.xml")
+    txt = open(fx).read()
+    for anchor, text in XML_EDITS[key]:
+        assert txt.count(anchor) == 1, anchor
+        txt = txt.replace(anchor, text + anchor)
+    open(fx, "w").write(txt)
+    for fn, body in DATA_FILES.get(key, {}).items():
+        open(os.path.join(casedir, fn), "w").write(body)
 
 
 def run_case(exe, spec, tmp, nsteps):
@@ -72,6 +100,8 @@ def run_case(exe, spec, tmp, nsteps):
     subprocess.check_call([os.path.join(REF, "gennn_ref"), repr(dp), tmp, repr(width), repr(scale), "5",
                            "CaseNN", repr(tfs), str(vg), str(tv), str(ddt), str(sh), repr(cs), str(step), ft],
                           stdout=subprocess.DEVNULL)
+    if len(spec) > 14 and spec[14]:
+        apply_edit(tmp, spec[14])
     out = os.path.join(tmp, "out_" + os.path.basename(exe))
     extra = list(spec[12]) if len(spec) > 12 else []
     subprocess.check_call([exe, os.path.join(tmp, "CaseNN"), out, "-nsteps:%d" % nsteps, "-svsteps:1",
@@ -112,6 +142,8 @@ def make(name, spec, noise):
             arrays["cellmode"] = np.int32(2)
         if len(spec) > 13 and spec[13]:
             arrays["floating"] = np.int32(1)
+        if len(spec) > 14 and spec[14]:
+            arrays["xmledit"] = np.array(spec[14])
         fn = os.path.join(HERE, "nn_%s.npz" % name)
         np.savez_compressed(fn, **arrays)
         print(name, "ok", os.path.getsize(fn), {k: arrays[k] for k in arrays if k.startswith("noise")})

@@ -9,6 +9,7 @@ with a floor of a few float ulps where the two reference builds agree bit for bi
 """
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -219,7 +220,9 @@ def test_xml_loader_reads_the_nn_case(tmp_path, velgrad):
 # (xmlcase), which configures the body as JSph::LoadCaseConfig does.
 NN_FT_GOLDENS = ("ft_sym_lam_ddt3_dp0.025", "ft_ver_art_ddt1_nobound_cs_dp0.025", "ft_sph_sym_consteq_cs_dp0.025",
                  # CellMode=half (the npz carries cellmode = 2)
-                 "ft_sym_lam_ddt3_half_dp0.025", "ft_ver_art_ddt1_nobound_cs_half_dp0.025")
+                 "ft_sym_lam_ddt3_half_dp0.025", "ft_ver_art_ddt1_nobound_cs_half_dp0.025",
+                 # external forces on the body and a ViscoTime table (the npz carries xmledit)
+                 "ft_sym_lam_ddt3_extforce_viscotime_dp0.025")
 
 
 def ft_case(g, tmp_path):
@@ -232,6 +235,11 @@ def ft_case(g, tmp_path):
     subprocess.check_call([exe, repr(float(dp)), str(tmp_path), repr(float(width)), repr(float(scale)), "5", "CaseNN",
                            repr(float(tfs)), str(int(vg)), str(int(tv)), str(int(ddt)), str(int(sh)), repr(float(cs)),
                            str(int(step)), "1"], stdout=subprocess.DEVNULL)
+    if "xmledit" in g.files:  # the generator's XML edit and data files (make_nn_golden.py)
+        sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+        from make_nn_golden import apply_edit
+
+        apply_edit(str(tmp_path), str(g["xmledit"]))
     if "cellmode" in g.files:  # -cellmode:half on the reference's command line
         return XmlCase(str(tmp_path / "CaseNN"), cellmode=int(g["cellmode"]))
     return XmlCase(str(tmp_path / "CaseNN"))
