@@ -661,33 +661,49 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
 // match on the 9-bit box offset), the stayers after the near arrivals whose list index is
 // at least Ln(obx(c)), far arrivals (a short list) by their previous index.  Two passes
 // over the window: counts, then (after the per-box scan) ranks -> positions.
-constexpr int IB_FCAP = 256;  // far arrivals of a block held in LDS (more: read from global memory)
+// LDS: 52 KB per block, so 3 blocks (12 waves) share a CU: the kernel is a chain of dependent
+// global-memory latencies per block, and a 1M (cfg2) divide has ~700 blocks, a 1.25M y-slab
+// of cfg3 ~1050.  (At 77 KB, 2 blocks per CU: the launch ran in 1.4-2 rounds of blocks.)  The
+// window's near-mover keys are held as 16-bit codes relative to the block (below / box / above),
+// the arrivals as packed words, and arrays whose lifetimes do not overlap share their storage.
+constexpr int IB_FCAP = 128;  // far arrivals of a block held in LDS (more: read from global memory)
 constexpr int IB_TPCAP = 1024;  // window tiles with LDS prefixes (more: computed from global memory)
 constexpr int IB_WCAP = 4096;   // window near movers staged in LDS (more: read from global memory)
 constexpr int IB_ACAP = 1024;   // near arrivals ranked through LDS buckets (more: chunked wave-match pass)
+static_assert(IB_BOX <= 512 && IB_ACAP <= 2 * IB_BOX, "packed arrivals (9-bit box offset); buckets in s_nfbef");
+// window code of a previous-key window entry: 0 below the block's boxes, 1 + the box offset
+// inside them, WC_ABOVE above
+constexpr unsigned WC_ABOVE = 0xffffu;
 __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc, DivGrid g,
                                                      const unsigned* __restrict__ ob, unsigned* __restrict__ nbc,
                                                      IncDivScratch s, unsigned omax) {
   constexpr int NW = IB_BS / 64;
   __shared__ unsigned s_obx[IB_BOX + 1], s_ln[IB_BOX + 1], s_lf[IB_BOX + 1];
-  __shared__ unsigned s_narr[IB_BOX], s_nbef[IB_BOX], s_farr[IB_BOX], s_fbef[IB_BOX], s_run[IB_BOX];
+  __shared__ unsigned s_narr[IB_BOX], s_farr[IB_BOX], s_run[IB_BOX];
+  // near / far arrivals of each box ahead of its stayers (up to the per-box scan), then the
+  // buckets of pass 2
+  __shared__ unsigned s_nfbef[2][IB_BOX];
+  unsigned* const s_nbef = s_nfbef[0];
+  unsigned* const s_fbef = s_nfbef[1];
+  unsigned* const s_bkt = &s_nfbef[0][0];  // near arrivals' window indices bucketed by box
+  // slab: the appended entries below each box (s_ab, up to the per-box scan); then the wave
+  // counts of the unbucketed pass 2 (s_wc)
+  constexpr int ABWC = NW * IB_BOX > 3 * (IB_BOX + 1) ? NW * IB_BOX : 3 * (IB_BOX + 1);
+  __shared__ unsigned s_abwc[ABWC];
+  unsigned(*const s_ab)[IB_BOX + 1] = reinterpret_cast<unsigned(*)[IB_BOX + 1]>(s_abwc);
+  unsigned(*const s_wc)[IB_BOX] = reinterpret_cast<unsigned(*)[IB_BOX]>(s_abwc);
   __shared__ unsigned s_begin[IB_BOX];
-  __shared__ unsigned s_wc[NW][IB_BOX];
   __shared__ uint2 s_tp[IB_TPCAP];      // (near, far) movers before tile tA + k
   __shared__ uint4 s_far[IB_FCAP];      // (f, previous index, key, Ln(previous index) clamped to the window)
   __shared__ unsigned s_fnb[IB_FCAP];   // near arrivals of its box before a far arrival
   __shared__ unsigned s_wsum[IB_BPT][NW];
   __shared__ unsigned long long s_red[2][NW];
   __shared__ unsigned s_xw[2], s_jw[2], s_below, s_farbelow, s_nfar;
-  __shared__ unsigned s_wkey[IB_WCAP];  // the window's near-mover keys (when they fit)
-  __shared__ uint2 s_arr[IB_ACAP];      // near arrivals (list index, box offset), unordered
-  __shared__ unsigned s_bkt[IB_ACAP];   // their list indices bucketed by box
+  __shared__ unsigned short s_wcode[IB_WCAP];  // the window's near-mover key codes (when they fit)
+  __shared__ unsigned s_arr[IB_ACAP];  // near arrivals (window index << 9 | box offset), unordered
   __shared__ unsigned s_boff[IB_BOX];   // bucket offsets (exclusive scan of s_narr)
   __shared__ unsigned s_nwsum[IB_BPT][IB_BS / 64];
   __shared__ unsigned s_nar;
-  // slab: appended entries with a key below each box, per sorted list (migrants, left and
-  // right ghost slots)
-  __shared__ unsigned s_ab[3][IB_BOX + 1];
   const unsigned b = blockIdx.x;
   TSDECL;
   TSTAMP(0);
@@ -716,8 +732,6 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
     s_farr[k] = 0;
     s_fbef[k] = 0;
     s_run[k] = 0;
-#pragma unroll
-    for (int q = 0; q < NW; q++) s_wc[q][k] = 0;
   }
   if (threadIdx.x == 0) {
     s_below = 0;
@@ -853,6 +867,9 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   TSTAMP(1);
   const unsigned jlo = s_jw[0], jhi = s_jw[1];
   const unsigned cend = unsigned(min(c0 + IB_BOX, nctt));
+  auto wcode_of = [&](unsigned key) -> unsigned {
+    return key < unsigned(c0) ? 0u : (key < cend ? key - unsigned(c0) + 1u : WC_ABOVE);
+  };
   auto ln_clamped = [&](unsigned x) -> unsigned {  // Ln(x) of a far mover, clamped to the window
     if (x < xa) return jlo;
     if (x >= xb) return jhi;
@@ -891,25 +908,25 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
 #pragma unroll
       for (int m = 0; m < WR; m++) {
         const unsigned e = r0 + threadIdx.x + m * IB_BS;
-        if (e < jhi - jlo) s_wkey[e] = kk[m];
+        if (e < jhi - jlo) s_wcode[e] = (unsigned short)wcode_of(kk[m]);
       }
     }
     __syncthreads();
   }
-  auto wkey = [&](unsigned j) -> unsigned { return wlds ? s_wkey[j - jlo] : s.mkey[slot_of(j)]; };
+  auto wcode = [&](unsigned j) -> unsigned { return wlds ? s_wcode[j - jlo] : wcode_of(s.mkey[slot_of(j)]); };
   // ---- pass 1: near arrivals per box, and the window's near movers below the block
   {
     unsigned below = 0;
     for (unsigned base = jlo; base < jhi; base += IB_BS) {
       const unsigned j = base + threadIdx.x;
-      const unsigned key = j < jhi ? wkey(j) : ~0u;
-      below += unsigned(__popcll(__ballot(key < unsigned(c0))));
-      if (key >= unsigned(c0) && key < cend) {
-        const unsigned lc = key - unsigned(c0);
+      const unsigned wc = j < jhi ? wcode(j) : WC_ABOVE;
+      below += unsigned(__popcll(__ballot(wc == 0u)));
+      if (wc != 0u && wc != WC_ABOVE) {
+        const unsigned lc = wc - 1u, key = unsigned(c0) + lc;
         atomicAdd(&s_narr[lc], 1u);
         if (j < s_ln[lc]) atomicAdd(&s_nbef[lc], 1u);
         const unsigned a = atomicAdd(&s_nar, 1u);
-        if (a < unsigned(IB_ACAP)) s_arr[a] = make_uint2(j, lc);
+        if (a < unsigned(IB_ACAP)) s_arr[a] = ((j - jlo) << 9) | lc;
         if (s_farr[lc] && farlds) {  // near arrivals ahead of a far arrival of the same box
           for (unsigned k = 0; k < nfar; k++) {
             const uint4 fe = s_far[k];
@@ -1020,7 +1037,7 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   // Usually through LDS buckets (arrivals of one box, any order; rank = arrivals of the box
   // with a smaller list index), else one wave-matched chunk of the window at a time.
   const unsigned nar = s_nar;
-  const bool bucketed = nar <= unsigned(IB_ACAP) && !(s.dbg & 64);
+  const bool bucketed = nar <= unsigned(IB_ACAP) && jhi - jlo < (1u << 23) && !(s.dbg & 64);
   auto near_pos = [&](unsigned j, unsigned lc, unsigned r) -> unsigned {
     const unsigned key = unsigned(c0) + lc;
     if (s_farr[lc]) {  // far arrivals of this box ahead of it (previous index below this mover's)
@@ -1039,25 +1056,28 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
   };
   if (bucketed) {
     for (unsigned a = threadIdx.x; a < nar; a += IB_BS) {
-      const uint2 e = s_arr[a];
-      s_bkt[s_boff[e.y] + atomicAdd(&s_run[e.y], 1u)] = e.x;
+      const unsigned e = s_arr[a], lc = e & 511u;
+      s_bkt[s_boff[lc] + atomicAdd(&s_run[lc], 1u)] = e >> 9;
     }
     __syncthreads();
     for (unsigned a = threadIdx.x; a < nar; a += IB_BS) {
-      const uint2 e = s_arr[a];
-      const unsigned b0 = s_boff[e.y], b1 = b0 + s_narr[e.y];
+      const unsigned e = s_arr[a], lc = e & 511u, jr = e >> 9;
+      const unsigned b0 = s_boff[lc], b1 = b0 + s_narr[lc];
       unsigned r = 0;
-      for (unsigned q = b0; q < b1; q++) r += s_bkt[q] < e.x ? 1u : 0u;
-      s.mposnear[slot_of(e.x)] = near_pos(e.x, e.y, r);
+      for (unsigned q = b0; q < b1; q++) r += s_bkt[q] < jr ? 1u : 0u;
+      s.mposnear[slot_of(jlo + jr)] = near_pos(jlo + jr, lc, r);
     }
+  } else {  // the wave counts (storage of the slab's s_ab, dead since the per-box scan)
+    for (int k = int(threadIdx.x); k < NW * IB_BOX; k += IB_BS) s_abwc[k] = 0u;
+    __syncthreads();
   }
   const unsigned long long lt = (1ull << lane) - 1ull;
   for (unsigned base = jlo; base < (bucketed ? jlo : jhi); base += IB_BS) {
     const unsigned j = base + threadIdx.x;
-    const unsigned key = j < jhi ? wkey(j) : ~0u;
-    const bool valid = key >= unsigned(c0) && key < cend;
+    const unsigned wc = j < jhi ? wcode(j) : WC_ABOVE;
+    const bool valid = wc != 0u && wc != WC_ABOVE;
     if (__syncthreads_or(valid) == 0) continue;  // block-uniform
-    const unsigned lc = valid ? key - unsigned(c0) : 0u;
+    const unsigned lc = valid ? wc - 1u : 0u;
     unsigned long long peers = __ballot(valid);
 #pragma unroll
     for (int bit = 0; bit < 9; bit++) {
@@ -1095,7 +1115,7 @@ __global__ __launch_bounds__(IB_BS) void k_inc_boxes(DevScalars* __restrict__ sc
       }
       const uint2 e = s.mfar[f];
       fe = make_uint4(f, e.x, e.y, ln_clamped(e.x));
-      for (unsigned j = jlo; j < fe.w; j++) nb += (wkey(j) == fe.z) ? 1u : 0u;
+      for (unsigned j = jlo; j < fe.w; j++) nb += (wcode(j) == fe.z - unsigned(c0) + 1u) ? 1u : 0u;
     }
     const unsigned lc = fe.z - unsigned(c0);
     unsigned r = nb;
