@@ -5,7 +5,7 @@ import ctypes as C
 
 import numpy as np
 
-SPH_ABI_VERSION = 11
+SPH_ABI_VERSION = 12
 
 SPH_STATUS = {
     0: "SPH_OK",
@@ -363,10 +363,15 @@ def _ptr(arr: np.ndarray | None, ctype):
 class SphMotionMov(C.Structure):
     _fields_ = [
         ("obj", C.c_int32), ("id", C.c_int32), ("next", C.c_int32), ("type", C.c_int32), ("prev", C.c_int32),
-        ("pad", C.c_int32), ("duration", C.c_double), ("vec", C.c_double * 3), ("vec2", C.c_double * 3),
-        ("phase", C.c_double * 3), ("axisp1", C.c_double * 3), ("axisp2", C.c_double * 3),
-        ("ang", C.c_double), ("ang2", C.c_double), ("ang3", C.c_double),
+        ("fields", C.c_int32), ("data_first", C.c_uint32), ("data_n", C.c_uint32), ("duration", C.c_double),
+        ("vec", C.c_double * 3), ("vec2", C.c_double * 3), ("phase", C.c_double * 3), ("axisp1", C.c_double * 3),
+        ("axisp2", C.c_double * 3), ("ref", C.c_double * 3), ("ang", C.c_double), ("ang2", C.c_double),
+        ("ang3", C.c_double),
     ]
+
+
+class SphMotionObj(C.Structure):
+    _fields_ = [("parent", C.c_int32), ("ref", C.c_int32)]
 
 
 class SphMotionEvent(C.Structure):
@@ -413,6 +418,18 @@ def motion_arrays(motion: dict):
     for i, e in enumerate(motion["evts"]):
         _fill(evts[i], e)
     return movs, evts
+
+
+def motion_tree_arrays(motion: dict):
+    """The tree form (motion["objs"]: nodes depth first with parent / ref; movement and event
+    `obj` are node indices; motion["rows"]: the file movements' table rows, 4 doubles each):
+    SphMotionObj[], SphMotionMov[], SphMotionEvent[], the rows (float64, C order)."""
+    nodes = (SphMotionObj * len(motion["objs"]))()
+    for i, o in enumerate(motion["objs"]):
+        nodes[i].parent, nodes[i].ref = int(o["parent"]), int(o["ref"])
+    movs, evts = motion_arrays(motion)
+    rows = np.ascontiguousarray(np.asarray(motion.get("rows", np.zeros((0, 4))), np.float64).reshape(-1, 4))
+    return nodes, movs, evts, rows
 
 
 def floating_array(floatings: list):

@@ -438,10 +438,11 @@ class WaveFlumeCase:
         f32 = lambda v: float(np.float32(v))  # noqa: E731  (JXml::GetAttributeFloat)
         hinge = float("%.10g" % (nx * dp))
         zero3 = (0.0, 0.0, 0.0)
-        mov = lambda **kw: dict(dict(obj=0, id=1, next=0, type=1, prev=0, duration=f32(100), vec=zero3,  # noqa: E731
-                                     vec2=zero3, phase=zero3, axisp1=zero3, axisp2=zero3, ang=0.0, ang2=0.0,
-                                     ang3=0.0), **kw)
-        self.motion = dict(nobj=2, movs=[
+        mov = lambda **kw: dict(dict(obj=0, id=1, next=0, type=1, prev=0, fields=0, data_first=0,  # noqa: E731
+                                     data_n=0, duration=f32(100), vec=zero3, vec2=zero3, phase=zero3, axisp1=zero3,
+                                     axisp2=zero3, ref=zero3, ang=0.0, ang2=0.0, ang3=0.0), **kw)
+        # the tree form of XmlCase.motion: two top-level objreal nodes (refs 0, 1), no tables
+        self.motion = dict(nobj=2, objs=[dict(parent=-1, ref=0), dict(parent=-1, ref=1)], rows=[], movs=[
             mov(obj=0, type=6, vec=(1.5, 0.0, 0.0), vec2=(0.02, 0.0, 0.0)),
             mov(obj=1, id=1, next=2, type=1, duration=f32(0.004)),
             mov(obj=1, id=2, type=7, axisp1=(hinge, 0.0, 0.0), axisp2=(hinge, 1.0, 0.0), ang=2.0, ang2=3.0),

@@ -33,8 +33,10 @@ from ._abi import (
     SphFloatingState,
     SphMotionEvent,
     SphMotionMov,
+    SphMotionObj,
     floating_array,
     motion_arrays,
+    motion_tree_arrays,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -87,6 +89,7 @@ EXPORTED_SYMBOLS = (
     "sph_normals_write",
     "sph_bi4_rewrite",
     "sph_solver_set_motion",
+    "sph_solver_set_motion_tree",
     "sph_solver_set_floatings",
     "sph_solver_set_floating_table",
     "sph_solver_set_time_table",
@@ -168,6 +171,9 @@ def load_library(path: str = LIB_PATH):
                                     C.POINTER(C.c_double)]
     L.sph_solver_set_motion.argtypes = [vp, C.c_uint32, C.c_uint32, C.POINTER(SphMotionMov), C.c_uint32,
                                         C.POINTER(SphMotionEvent)]
+    L.sph_solver_set_motion_tree.argtypes = [vp, C.c_uint32, C.POINTER(SphMotionObj), C.c_uint32,
+                                             C.POINTER(SphMotionMov), C.c_uint32, C.POINTER(SphMotionEvent),
+                                             C.c_uint32, C.POINTER(C.c_double)]
     L.sph_solver_set_floatings.argtypes = [vp, C.c_uint32, C.POINTER(SphFloatingDef), C.c_double]
     L.sph_solver_set_time_table.argtypes = [vp, C.c_int32, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_double)]
     L.sph_solver_set_floating_table.argtypes = [vp, C.c_uint32, C.c_int32, C.c_uint32, C.POINTER(C.c_double),
@@ -243,7 +249,12 @@ class SphGpuSingle:
         # a restart sets the PART time first: the motion program is advanced to it
         if getattr(case, "time0", 0.0) or getattr(case, "symdtpre0", 0.0):
             self.set_time(case.time0, case.symdtpre0)
-        if getattr(case, "motion", None):
+        if getattr(case, "motion", None) and "objs" in case.motion:  # nested objects / file tables
+            nodes, movs, evts, rows = motion_tree_arrays(case.motion)
+            _check(L.sph_solver_set_motion_tree(self._h, len(case.motion["objs"]), nodes, len(case.motion["movs"]),
+                                                movs, len(case.motion["evts"]), evts, len(rows),
+                                                rows.ctypes.data_as(C.POINTER(C.c_double))))
+        elif getattr(case, "motion", None):
             movs, evts = motion_arrays(case.motion)
             _check(L.sph_solver_set_motion(self._h, case.motion["nobj"], len(case.motion["movs"]), movs,
                                            len(case.motion["evts"]), evts))

@@ -10,10 +10,11 @@
 //   (JSphCpu.cpp:1692-1790; GPU cusph::MoveLinBound/MoveMatBound, JSphGpu_ker.cu:2032+).
 //   Here one wave restates the event/active-movement machinery (k_motion) over a
 //   program uploaded once, then a grid over the boundary particles applies the
-//   per-object displacement (k_move_bound).  Supported movements: wait, mvrect,
-//   mvrectace, mvrot, mvrotace, mvrectsinu, mvrotsinu, chained by `next`, started by
-//   <begin> events (finish optional); nested objects and file-driven movements are
-//   refused by the loader.
+//   per-object displacement (k_move_bound).  Every movement of JMotion::ReadXml: wait,
+//   mvrect, mvrectace, mvrot, mvrotace, mvcir, mvcirace, mvrectsinu, mvrotsinu, mvcirsinu,
+//   mvrectfile (mvfile, mvpredef), mvrotfile, mvnull, flash movements (negative duration),
+//   chained by `next`, started by <begin> events (finish optional), in a tree of nested
+//   <obj> / <objreal> objects (a parent's motion moves its children and their axes).
 // * Floating bodies (RigidAlgorithm=1, SPH).  JSphCpuSingle::RunFloating
 //   (JSphCpuSingle.cpp:897-1010): FtCalcForcesSum (:748-768), FtCalcForces (:775-815),
 //   FtCalcForcesRes (:822-858), constraints (:863-873), then the particle update and the
@@ -35,9 +36,6 @@
 namespace sphx {
 
 // ---- 4x4 double matrices (JMatrix4d) --------------------------------------------------
-struct M4d {
-  double a[16];  // row major, a[4*r+c]
-};
 __device__ inline void m4_identity(M4d& m) {
   for (int i = 0; i < 16; i++) m.a[i] = (i % 5 == 0 ? 1.0 : 0.0);
 }
@@ -55,6 +53,15 @@ __device__ inline void m4_mov(M4d& m, double x, double y, double z) {  // Matrix
   m.a[3] = x;
   m.a[7] = y;
   m.a[11] = z;
+}
+// JMatrix4::MulPoint
+__device__ inline void m4_point(const M4d& m, const double* p, double* q) {
+  const double x = m.a[0] * p[0] + m.a[1] * p[1] + m.a[2] * p[2] + m.a[3];
+  const double y = m.a[4] * p[0] + m.a[5] * p[1] + m.a[6] * p[2] + m.a[7];
+  const double z = m.a[8] * p[0] + m.a[9] * p[1] + m.a[10] * p[2] + m.a[11];
+  q[0] = x;
+  q[1] = y;
+  q[2] = z;
 }
 // JMatrix4::MatrixRot(ang [degrees], axisp1, axisp2) (JMatrix4.h:332-366)
 __device__ inline M4d m4_rot(double ang, const double* p1, const double* p2) {
@@ -90,14 +97,9 @@ __device__ inline M4d m4_rot(double ang, const double* p1, const double* p2) {
   return t;
 }
 
-// JMotionPos (JMotionPos.cpp:29-107): accumulated motion of one object in one step.
-struct MPos {
-  bool simple;
-  double s[3];
-  M4d m;
-};
+// JMotionPos (JMotionPos.cpp:29-107, JMotionPos.h:52).
 __device__ inline void mpos_reset(MPos& p) {
-  p.simple = true;
+  p.simple = 1;
   p.s[0] = p.s[1] = p.s[2] = 0;
   m4_identity(p.m);
 }
@@ -112,44 +114,125 @@ __device__ inline void mpos_move(MPos& p, double x, double y, double z) {
     m4_mul(p.m, mv);
   }
 }
-__device__ inline void mpos_rotate(MPos& p, double ang, const double* p1, const double* p2) {
+__device__ inline void mpos_tomatrix(MPos& p) {
   if (p.simple) {
     m4_mov(p.m, p.s[0], p.s[1], p.s[2]);
-    p.simple = false;
+    p.simple = 0;
   }
+}
+__device__ inline void mpos_rotate(MPos& p, double ang, const double* p1, const double* p2) {
+  mpos_tomatrix(p);
   const M4d r = m4_rot(ang, p1, p2);
   m4_mul(p.m, r);
+}
+__device__ inline void mpos_movemix(MPos& p, const MPos& q) {
+  if (p.simple && !q.simple) mpos_tomatrix(p);
+  if (q.simple) mpos_move(p, q.s[0], q.s[1], q.s[2]);
+  else m4_mul(p.m, q.m);
+}
+__device__ inline void mpos_point(const MPos& p, double* x) {  // PointMove, in place
+  if (p.simple) {
+    x[0] = x[0] + p.s[0];
+    x[1] = x[1] + p.s[1];
+    x[2] = x[2] + p.s[2];
+  } else {
+    m4_point(p.m, x, x);
+  }
 }
 
 // ---- motion program ----------------------------------------------------------------------
 // JMotionMovActive (JMotionObj.cpp:40-208): ConfigData of a (next) movement.
-__device__ inline void act_config(MotAct& a, const MotMov& mv) {
+__device__ inline void act_config(MotAct& a, const MotMov& mv, const double* __restrict__ data) {
   a.vel[0] = a.vel[1] = a.vel[2] = 0;
   a.velang = 0;
   a.phase[0] = a.phase[1] = a.phase[2] = 0;
   a.phaseuni = 0;
+  a.dfindex = 0;
+  a.dflast[0] = a.dflast[1] = a.dflast[2] = 0;
+  a.dflastang = 0;
   switch (mv.type) {
     case SPH_MOV_RECT: a.vel[0] = mv.v[0]; a.vel[1] = mv.v[1]; a.vel[2] = mv.v[2]; break;
     case SPH_MOV_RECTACE: a.vel[0] = mv.v2[0]; a.vel[1] = mv.v2[1]; a.vel[2] = mv.v2[2]; break;
-    case SPH_MOV_ROT: a.velang = mv.ang; break;
-    case SPH_MOV_ROTACE: a.velang = mv.ang2; break;
+    case SPH_MOV_ROT: case SPH_MOV_CIR: a.velang = mv.ang; break;
+    case SPH_MOV_ROTACE: case SPH_MOV_CIRACE: a.velang = mv.ang2; break;
     case SPH_MOV_RECTSINU:
       a.phase[0] = mv.phase[0]; a.phase[1] = mv.phase[1]; a.phase[2] = mv.phase[2];
       break;
-    case SPH_MOV_ROTSINU: a.phaseuni = mv.ang3; break;
+    case SPH_MOV_ROTSINU: case SPH_MOV_CIRSINU: a.phaseuni = mv.ang3; break;
+    case SPH_MOV_RECTFILE: {  // DfConfig(true): the table's first position
+      const double* r = data + 4 * mv.dfirst;
+      a.dflast[0] = r[1]; a.dflast[1] = r[2]; a.dflast[2] = r[3];
+    } break;
+    case SPH_MOV_ROTFILE: a.dflastang = data[4 * mv.dfirst + 1]; break;
     default: break;
   }
 }
+// JMotionMovActive constructor / NextMov: the flash flag and the finish of a movement that
+// starts at a.start.
+__device__ inline void act_span(MotAct& a, const MotMov& mv) {
+  a.flash = mv.time < 0;
+  a.finish = a.flash ? a.start : a.start + mv.time;
+  if (a.eventfinish >= 0 && a.eventfinish < a.finish) a.finish = a.eventfinish;
+}
 
-// One object: JMotionObj::ProcesTime (JMotionObj.cpp:368-580) without parents/children.
-// Returns true when the object moved (modif) in [timestep, timestep+dt).
-__device__ bool obj_proces_time(MotionDev& md, MotObj& o, const MotMov* movs, double timestep, double dt,
-                                MPos& modpos) {
+// JMotionMovActive::BinarySearch (JMotionObj.cpp:112-139) over the times of a table.
+__device__ unsigned df_search(unsigned size, const double* __restrict__ d, double t) {
+  unsigned ret = 0;
+  if (size > 1) {
+    int ccen = 0, cmin = 0, cmax = int(size) - 1;
+    while (cmin <= cmax) {
+      ccen = ((cmax - cmin) / 2) + cmin;
+      const double tc = d[4 * ccen];
+      if (tc == t) cmin = cmax + 1;
+      else if (t < tc) cmax = ccen - 1;
+      else cmin = ccen + 1;
+    }
+    if (ccen && ccen < int(size) && t < d[4 * ccen]) ccen--;
+    ret = unsigned(ccen);
+    while (ret && t == d[4 * (ret - 1)]) ret--;
+  }
+  return ret;
+}
+// DfGetNewPos / DfGetNewAng (JMotionObj.cpp:144-178): the table interpolated at t, from the
+// persistent index; k = 1 (x, y, z) or the angle column.
+__device__ void df_value(MotAct& a, const MotMov& mv, const double* __restrict__ data, double t, double* out, int nk) {
+  const double* d = data + 4 * mv.dfirst;
+  const unsigned n = unsigned(mv.dn);
+  unsigned idx = unsigned(a.dfindex);
+  if (idx == 0) idx = df_search(n, d, t);
+  while (idx < n && t > d[4 * idx]) idx++;
+  a.dfindex = int(idx);
+  if (idx >= n) {  // beyond the last instant: the last value
+    for (int k = 0; k < nk; k++) out[k] = d[4 * (n - 1) + 1 + k];
+  } else {
+    const unsigned i0 = idx ? idx - 1 : 0;  // (the reference reads row -1 at t <= the first time)
+    const double tfactor = (t - d[4 * i0]) / (d[4 * idx] - d[4 * i0]);
+    for (int k = 0; k < nk; k++) {
+      const double v0 = d[4 * i0 + 1 + k], v1 = d[4 * idx + 1 + k];
+      out[k] = (nk == 1 || ((mv.fields >> k) & 1)) ? v0 + tfactor * (v1 - v0) : 0.0;
+    }
+  }
+}
+
+// One node: JMotionObj::ProcesTime (JMotionObj.cpp:368-580) for this object; its children
+// follow it in the node order.  Returns modif (the object moved in [timestep, +dt)).
+__device__ bool obj_proces_time(MotionDev& md, int oi, const MotMov* movs, const double* __restrict__ data,
+                                double timestep, double dt) {
+  MotObj& o = md.obj[oi];
+  o.active = 1;
+  const MotObj* par = o.parent >= 0 ? &md.obj[o.parent] : nullptr;
+  if (par && par->moving)  // the parent's motion of this step moves every axis of the object
+    for (int k = 0; k < md.naxis; k++)
+      if (md.axis[k].obj == oi) {
+        mpos_point(par->modpos, md.axis[k].p1);
+        mpos_point(par->modpos, md.axis[k].p2);
+      }
   bool modif = false;
   int na = o.na;
   if (na) {
     const double tstepfin = timestep + dt;
-    mpos_reset(modpos);
+    mpos_reset(o.modpos);
+    MPos& modpos = o.modpos;
     for (int ca = 0; ca < na; ca++) {
       MotAct& amov = o.act[ca];
       if (amov.del) {  // erase the active movement marked in the previous step
@@ -166,8 +249,8 @@ __device__ bool obj_proces_time(MotionDev& md, MotObj& o, const MotMov* movs, do
         double dtmov = (tstepfin > amov.finish ? amov.finish - timestep2 : dt2);
         const double dtover = dt2 - dtmov;
         if (timestep2 < amov.start) dtmov -= (amov.start - timestep2);
-        if (dtmov > 0) {
-          const double t = dtmov;
+        if (dtmov > 0 || amov.flash) {
+          const double t = amov.flash ? -mv.time : dtmov;
           switch (mv.type) {
             case SPH_MOV_RECT:
               mpos_move(modpos, mv.v[0] * t, mv.v[1] * t, mv.v[2] * t);
@@ -184,13 +267,39 @@ __device__ bool obj_proces_time(MotionDev& md, MotObj& o, const MotMov* movs, do
               modif = true;
             } break;
             case SPH_MOV_ROT:
-              mpos_rotate(modpos, mv.ang * t, mv.p1, mv.p2);
+              mpos_rotate(modpos, mv.ang * t, md.axis[mv.ax].p1, md.axis[mv.ax].p2);
               modif = true;
               break;
             case SPH_MOV_ROTACE: {
               const double at = mv.ang * t;
-              mpos_rotate(modpos, amov.velang * t + 0.5 * at * t, mv.p1, mv.p2);
+              mpos_rotate(modpos, amov.velang * t + 0.5 * at * t, md.axis[mv.ax].p1, md.axis[mv.ax].p2);
               amov.velang += at;
+              modif = true;
+            } break;
+            case SPH_MOV_CIR:
+            case SPH_MOV_CIRACE:
+            case SPH_MOV_CIRSINU: {  // the reference point turns about the axis; the object follows it
+              double ang;
+              if (mv.type == SPH_MOV_CIR) {
+                ang = mv.ang * t;
+              } else if (mv.type == SPH_MOV_CIRACE) {
+                const double at = mv.ang * t;
+                ang = amov.velang * t + 0.5 * at * t;
+                amov.velang += at;
+              } else {
+                double ph = amov.phaseuni;
+                ang = mv.ang2 * sin(ph);
+                ph += double(mv.ang * (3.14159265358979323846 + 3.14159265358979323846) * t);
+                ang = mv.ang2 * sin(ph) - ang;
+                amov.phaseuni = ph;
+              }
+              const M4d m = m4_rot(ang, md.axis[mv.ax].p1, md.axis[mv.ax].p2);
+              MotAxis& r = md.axis[mv.rax];
+              m4_point(m, r.p1, r.p2);
+              mpos_move(modpos, r.p2[0] - r.p1[0], r.p2[1] - r.p1[1], r.p2[2] - r.p1[2]);
+              r.p1[0] = r.p2[0];
+              r.p1[1] = r.p2[1];
+              r.p1[2] = r.p2[2];
               modif = true;
             } break;
             case SPH_MOV_RECTSINU: {
@@ -213,38 +322,63 @@ __device__ bool obj_proces_time(MotionDev& md, MotObj& o, const MotMov* movs, do
               double ang = mv.ang2 * sin(ph);
               ph += double(mv.ang * (3.14159265358979323846 + 3.14159265358979323846) * t);
               ang = mv.ang2 * sin(ph) - ang;
-              mpos_rotate(modpos, ang, mv.p1, mv.p2);
+              mpos_rotate(modpos, ang, md.axis[mv.ax].p1, md.axis[mv.ax].p2);
               amov.phaseuni = ph;
               modif = true;
             } break;
-            default: break;  // wait
+            case SPH_MOV_RECTFILE:
+            case SPH_MOV_ROTFILE: {  // the table at the time since the movement began
+              double tt = timestep - amov.start;
+              if (tt < 0) tt = 0;
+              tt += data[4 * mv.dfirst];
+              tt += t;
+              if (mv.type == SPH_MOV_RECTFILE) {
+                double np[3];
+                df_value(amov, mv, data, tt, np, 3);
+                mpos_move(modpos, np[0] - amov.dflast[0], np[1] - amov.dflast[1], np[2] - amov.dflast[2]);
+                amov.dflast[0] = np[0];
+                amov.dflast[1] = np[1];
+                amov.dflast[2] = np[2];
+              } else {
+                double na1;
+                df_value(amov, mv, data, tt, &na1, 1);
+                mpos_rotate(modpos, na1 - amov.dflastang, md.axis[mv.ax].p1, md.axis[mv.ax].p2);
+                amov.dflastang = na1;
+              }
+              modif = true;
+            } break;
+            default: break;  // wait, null
           }
         }
-        // chain to the next movement to consume the rest of dt
+        // chain to the next movement to consume the rest of dt (JMotionMovActive::NextMov)
         if ((dtover > 0 || dtmov == 0) && mv.nextidx >= 0) {
           const MotMov& nm = movs[mv.nextidx];
-          amov.start += mv.time;
+          if (!amov.flash) amov.start += mv.time;
           const double velp[3] = {amov.vel[0], amov.vel[1], amov.vel[2]};
           const double php[3] = {amov.phase[0], amov.phase[1], amov.phase[2]};
           const double velangp = amov.velang, phaseunip = amov.phaseuni;
           amov.mov = mv.nextidx;
-          amov.finish = amov.start + nm.time;
-          if (amov.eventfinish >= 0 && amov.eventfinish < amov.finish) amov.finish = amov.eventfinish;
-          act_config(amov, nm);
+          act_span(amov, nm);
+          act_config(amov, nm, data);
           if (nm.prev) {
             if (nm.type == SPH_MOV_RECTACE) { amov.vel[0] = velp[0]; amov.vel[1] = velp[1]; amov.vel[2] = velp[2]; }
-            if (nm.type == SPH_MOV_ROTACE) amov.velang = velangp;
+            if (nm.type == SPH_MOV_ROTACE || nm.type == SPH_MOV_CIRACE) amov.velang = velangp;
             if (nm.type == SPH_MOV_RECTSINU) { amov.phase[0] = php[0]; amov.phase[1] = php[1]; amov.phase[2] = php[2]; }
-            if (nm.type == SPH_MOV_ROTSINU) amov.phaseuni = phaseunip;
+            if (nm.type == SPH_MOV_ROTSINU || nm.type == SPH_MOV_CIRSINU) amov.phaseuni = phaseunip;
           }
           dt2 = dtover;
           timestep2 = amov.start;
-          if (timestep2 <= amov.finish) rep = true;
+          if (timestep2 <= amov.finish || amov.flash) rep = true;
         }
       } while (rep);
       if (tstepfin > amov.finish) amov.del = 1;
     }
     o.na = na;
+  }
+  if (par && par->moving) {  // the parent's motion on top of the object's own
+    if (modif) mpos_movemix(o.modpos, par->modpos);
+    else o.modpos = par->modpos;
+    modif = true;
   }
   if (modif) {
     o.moving = 1;
@@ -257,12 +391,13 @@ __device__ bool obj_proces_time(MotionDev& md, MotObj& o, const MotMov* movs, do
 }
 
 // JSph::CalcMotion + JMotion::ProcesTimeSimple for [sc->tstep0, sc->tstep0 + stepdt),
-// results in md->out[obj] (JMotionListData::Sp_Movedt, JMotionList.cpp:43-61).
+// results in md->out[ref] (JMotionListData::Sp_Movedt, JMotionList.cpp:43-61).
 __global__ void k_motion(const DevScalars* __restrict__ sc, MotionDev* __restrict__ md,
-                         const MotMov* __restrict__ movs, const MotEvt* __restrict__ evts, double t0, double dt0) {
+                         const MotMov* __restrict__ movs, const MotEvt* __restrict__ evts,
+                         const double* __restrict__ data, double t0, double dt0) {
   if (threadIdx.x != 0) return;
   const double timestep = (t0 >= 0 ? t0 : sc->tstep0), dt = (t0 >= 0 ? dt0 : sc->last_dt);
-  for (int o = 0; o < md->nobj; o++) md->out[o].type = 0;  // PreMotion
+  for (int r = 0; r < md->nref; r++) md->out[r].type = 0;  // PreMotion
   if (t0 < 0 && halted(sc)) return;  // a fatal error stopped the run: nothing moves
   // JMotion::ProcesTime (JMotion.cpp:446-468): start the events that begin before t+dt
   bool looking = true;
@@ -270,20 +405,19 @@ __global__ void k_motion(const DevScalars* __restrict__ sc, MotionDev* __restric
     const MotEvt& e = evts[c];
     if (e.start < timestep + dt) {
       MotObj& o = md->obj[e.obj];
-      if (o.na < MOT_MAXACT) {
+      if (o.na < MOT_MAXACT) {  // JMotionObj::BeginEvent
         MotAct& a = o.act[o.na++];
         const MotMov& mv = movs[e.mov];
         a.mov = e.mov;
         a.start = e.start;
         a.eventfinish = e.finish;
-        a.finish = a.start + mv.time;
-        if (e.finish >= 0 && e.finish < a.finish) a.finish = e.finish;
+        act_span(a, mv);
         a.del = 0;
-        act_config(a, mv);
+        act_config(a, mv, data);
       } else {
         md->overflow = 1;
       }
-      o.active = 1;
+      for (int q = e.obj; q >= 0 && !md->obj[q].active; q = md->obj[q].parent) md->obj[q].active = 1;
       md->eventnext--;
       md->objsactive = 1;
     } else {
@@ -292,30 +426,38 @@ __global__ void k_motion(const DevScalars* __restrict__ sc, MotionDev* __restric
   }
   if (md->objsactive) {
     md->objsactive = 0;
-    for (int oi = 0; oi < md->nobj; oi++) {
-      MotObj& o = md->obj[oi];
-      if (!o.active) continue;
-      MPos mp;
-      mpos_reset(mp);
-      const bool modif = obj_proces_time(*md, o, movs, timestep, dt, mp);
-      md->objsactive |= o.active;
-      if (modif) {
-        MotOut& r = md->out[oi];
-        if (mp.simple) {
-          r.type = 1;
-          for (int k = 0; k < 3; k++) {
-            r.mov[k] = mp.s[k];
-            r.vel[k] = mp.s[k] / dt;
-          }
-        } else {
-          r.type = 2;
-          for (int k = 0; k < 12; k++) r.m[k] = mp.m.a[k];
+    // the top-level objects that are active, each followed by its whole subtree
+    bool proc[MOT_MAXOBJ], modif[MOT_MAXOBJ];
+    for (int i = 0; i < md->nobj; i++) {
+      const int p = md->obj[i].parent;
+      proc[i] = p < 0 ? md->obj[i].active != 0 : proc[p];
+      modif[i] = proc[i] && obj_proces_time(*md, i, movs, data, timestep, dt);
+    }
+    // Active |= the children's (after each child's own subtree)
+    for (int i = md->nobj - 1; i >= 0; i--) {
+      const int p = md->obj[i].parent;
+      if (proc[i] && p >= 0) md->obj[p].active |= md->obj[i].active;
+    }
+    for (int i = 0; i < md->nobj; i++)
+      if (proc[i] && md->obj[i].parent < 0) md->objsactive |= md->obj[i].active;
+    for (int i = 0; i < md->nobj; i++) {
+      const MotObj& o = md->obj[i];
+      if (!modif[i] || o.ref < 0) continue;
+      MotOut& r = md->out[o.ref];
+      if (o.modpos.simple) {
+        r.type = 1;
+        for (int k = 0; k < 3; k++) {
+          r.mov[k] = o.modpos.s[k];
+          r.vel[k] = o.modpos.s[k] / dt;
         }
+      } else {
+        r.type = 2;
+        for (int k = 0; k < 12; k++) r.m[k] = o.modpos.m.a[k];
       }
     }
     // ProcesTimeSimple records the movements only when ProcesTime reports active objects
     if (!md->objsactive)
-      for (int o = 0; o < md->nobj; o++) md->out[o].type = 0;
+      for (int r = 0; r < md->nref; r++) md->out[r].type = 0;
   }
 }
 
@@ -330,7 +472,7 @@ __global__ __launch_bounds__(256) void k_move_bound(const DevScalars* __restrict
   const typecode c = a.code[p];
   if (CodeType(c) != CODE_TYPE_MOVING || !CodeIsNormal(c)) return;
   const unsigned obj = c & CODE_MASKVALUE;
-  if (obj >= unsigned(md->nobj)) return;
+  if (obj >= unsigned(md->nref)) return;
   const MotOut& r = md->out[obj];
   if (r.type == 0) return;
   const double2 pxy = a.posxy[p];
@@ -371,15 +513,16 @@ __global__ __launch_bounds__(256) void k_move_bound(const DevScalars* __restrict
 }
 
 void launch_motion(hipStream_t stm, unsigned npbcap, DevScalars* sc, const KConst& K, MotionDev* md,
-                   const MotMov* movs, const MotEvt* evts, const PartArrays& a, float4* normal, const DivGrid&) {
-  hipLaunchKernelGGL(k_motion, dim3(1), dim3(64), 0, stm, sc, md, movs, evts, -1.0, 0.0);
+                   const MotMov* movs, const MotEvt* evts, const double* data, const PartArrays& a, float4* normal,
+                   const DivGrid&) {
+  hipLaunchKernelGGL(k_motion, dim3(1), dim3(64), 0, stm, sc, md, movs, evts, data, -1.0, 0.0);
   const unsigned nb = (npbcap + 255) / 256;
   if (nb) hipLaunchKernelGGL(k_move_bound, dim3(nb), dim3(256), 0, stm, sc, K, md, a, normal);
 }
 
 void launch_motion_advance(hipStream_t stm, DevScalars* sc, MotionDev* md, const MotMov* movs, const MotEvt* evts,
-                           double t0, double dt) {
-  hipLaunchKernelGGL(k_motion, dim3(1), dim3(64), 0, stm, sc, md, movs, evts, t0, dt);
+                           const double* data, double t0, double dt) {
+  hipLaunchKernelGGL(k_motion, dim3(1), dim3(64), 0, stm, sc, md, movs, evts, data, t0, dt);
 }
 
 // ---- floating bodies ------------------------------------------------------------------------

@@ -149,6 +149,12 @@ int sph_solver_set_motion(SphSolver* s, uint32_t nobj, uint32_t nmov, const SphM
   NEED(s);
   return guard([&] { s->impl->SetMotion(nobj, nmov, movs, nevt, evts); });
 }
+int sph_solver_set_motion_tree(SphSolver* s, uint32_t nnode, const SphMotionObj* nodes, uint32_t nmov,
+                               const SphMotionMov* movs, uint32_t nevt, const SphMotionEvent* evts, uint32_t nrows,
+                               const double* rows) {
+  NEED(s && nodes && (rows || !nrows));
+  return guard([&] { s->impl->SetMotionTree(nnode, nodes, nmov, movs, nevt, evts, nrows, rows); });
+}
 int sph_solver_set_floatings(SphSolver* s, uint32_t nft, const SphFloatingDef* defs, double ftpause) {
   NEED(s && defs);
   return guard([&] { s->impl->SetFloatings(nft, defs, ftpause); });

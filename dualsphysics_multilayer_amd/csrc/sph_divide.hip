@@ -19,6 +19,7 @@
 
 #include "sph_items.hpp"
 #include "sph_kernels.hpp"
+#include "sph_incdiv.hpp"
 
 namespace sphx {
 
@@ -511,20 +512,11 @@ void launch_gather(hipStream_t stm, unsigned cap, DevScalars* sc, const unsigned
 //   k_inc_push      every particle pushed to its new position (gather_store: poscell,
 //                   press, VelMax) with its key for the next divide.
 // The result is the stable radix sort's, bit for bit (tests/test_divide_inc.py).
-constexpr int INC_BS = 256, INC_IPT = 4, INC_TILE = INC_BS * INC_IPT;  // = one k_inc_push block (GP = 4)
 static_assert(INC_IPT == GP, "k_inc_push covers one classify tile per block");
-static_assert(INC_TILE == int(INC_TILE_SIZE), "tile size of the host allocations");
-static_assert(INC_TILE <= 2048, "tile-local prefixes are 11 bits");
-constexpr int INC_SUP = 64;  // tiles per super tile
 #ifndef SPH_IB_BPT
 #define SPH_IB_BPT 2
 #endif
 constexpr int IB_BS = 256, IB_BPT = SPH_IB_BPT, IB_BOX = IB_BS * IB_BPT;  // boxes per k_inc_boxes block
-constexpr unsigned CW_NEAR = 0x80000000u, CW_FAR = 0x40000000u, CW_LOC = 0x7ffu;
-// slab: DROP = an old particle whose key became the discard box (a stale ghost): counted
-// with the far movers in the prefixes (it is not a stayer) but kept out of the far list
-// and never pushed; APP = a particle the exchange appended (no previous key)
-constexpr unsigned CW_DROP = 0x20000000u, CW_APP = 0x10000000u;
 // Phase timestamps of the incremental-divide kernels (SPH_INC_DBG & 8: printed for every
 // 16th block of the 12th incremental divide; the 100 MHz device clock).
 #define TSDECL unsigned long long tsv[8]
@@ -540,109 +532,10 @@ constexpr unsigned CW_DROP = 0x20000000u, CW_APP = 0x10000000u;
     } \
   } while (0)
 
-// A key change by one of the 27 cell offsets dx + dy ncx + dz nsheet (distinct offsets:
-// ncx >= 3 and ncy >= 3, or no y offsets when ncy = 1; checked on the host).
-__device__ __forceinline__ bool inc_near(int d, int ncx, int nsheet, bool usey, bool usez) {
-#pragma unroll
-  for (int dz = -1; dz <= 1; dz++) {
-#pragma unroll
-    for (int dy = -1; dy <= 1; dy++) {
-      if ((!usez && dz) || (!usey && dy)) continue;
-      const int r = d - dz * nsheet - dy * ncx;
-      if (r >= -1 && r <= 1) return true;
-    }
-  }
-  return false;
-}
-
 __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict__ sc, const unsigned* __restrict__ dcell,
                                                          const typecode* __restrict__ code, DivGrid g, unsigned dcc,
                                                          IncDivScratch s, int usey, int usez) {
-  __shared__ unsigned s_cn[INC_IPT * 4], s_cf[INC_IPT * 4];
-  const unsigned n = sc->np;
-  const unsigned nold = n - s.napp;  // the previous divide's particles; [nold, n) were appended
-  const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const unsigned b = blockIdx.x;  // the tile
-  TSDECL;
-  TSTAMP(0);
-  if (b == 0 && threadIdx.x == 0) sc->ndiv = n;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  unsigned key[INC_IPT], rn[INC_IPT], rf[INC_IPT], fpos[INC_IPT];
-  bool nr[INC_IPT], fr[INC_IPT], dr[INC_IPT];
-  // every load of the tile first (one memory latency), then the classification
-  unsigned dc[INC_IPT], old[INC_IPT];
-  typecode cd[INC_IPT];
-#pragma unroll
-  for (int k = 0; k < INC_IPT; k++) {
-    const unsigned i = b * INC_TILE + k * INC_BS + threadIdx.x;
-    const unsigned ii = i < n ? i : 0u;
-    dc[k] = dcell[ii];
-    cd[k] = code[ii];
-    old[k] = s.skeys[ii];
-  }
-#pragma unroll
-  for (int k = 0; k < INC_IPT; k++) {
-    const unsigned i = b * INC_TILE + k * INC_BS + threadIdx.x;
-    const bool valid = i < nold;
-    key[k] = box_key(dc[k], cd[k], g, dcc);
-    const int d = int(key[k] - old[k]);
-    dr[k] = valid && d != 0 && key[k] == g.boxdiscard;
-    nr[k] = valid && d != 0 && !dr[k] && inc_near(d, g.ncx, int(g.nsheet), usey != 0, usez != 0);
-    fr[k] = valid && d != 0 && !nr[k] && !dr[k];
-    const unsigned long long bn = __ballot(nr[k]), bf = __ballot(fr[k]), bfd = __ballot(fr[k] || dr[k]);
-    rn[k] = unsigned(__popcll(bn & lt));
-    rf[k] = unsigned(__popcll(bfd & lt));
-    fpos[k] = 0;
-    if (bf) {  // far movers (rare): appended to the list, one atomic per wave
-      const unsigned lead = unsigned(__ffsll(static_cast<long long>(bf))) - 1u;
-      unsigned base = 0;
-      if (lane == lead) base = atomicAdd(&s.ctr[0], unsigned(__popcll(bf)));
-      fpos[k] = __shfl(base, int(lead), 64) + unsigned(__popcll(bf & lt));
-    }
-    if (lane == 0) {
-      s_cn[k * 4 + w] = unsigned(__popcll(bn));
-      s_cf[k * 4 + w] = unsigned(__popcll(bfd));
-    }
-  }
-  __syncthreads();
-  TSTAMP(1);
-#pragma unroll
-  for (int k = 0; k < INC_IPT; k++) {
-    const unsigned i = b * INC_TILE + k * INC_BS + threadIdx.x;
-    if (i >= n) continue;
-    unsigned pn = 0, pf = 0;
-    for (unsigned q = 0; q < unsigned(k * 4) + w; q++) {
-      pn += s_cn[q];
-      pf += s_cf[q];
-    }
-    s.newkey[i] = key[k];
-    if (i >= nold) {  // appended: the input of their own sort
-      s.cw[i] = CW_APP;
-      s.akin[i - nold] = key[k];
-      s.avin[i - nold] = i - nold;
-      continue;
-    }
-    const unsigned ln = pn + rn[k], lf = pf + rf[k];  // tile-local exclusive prefixes
-    s.cw[i] = ln | (lf << 11) | (nr[k] ? CW_NEAR : 0u) | (fr[k] ? CW_FAR : 0u) | (dr[k] ? CW_DROP : 0u);
-    if (nr[k]) s.mkey[b * INC_TILE + ln] = key[k];
-    if (fr[k]) {
-      s.mfar[fpos[k]] = make_uint2(i, key[k]);
-      s.fidx[i] = fpos[k];
-    }
-  }
-  if (threadIdx.x == 0) {
-    unsigned an = 0, af = 0;
-#pragma unroll
-    for (int q = 0; q < INC_IPT * 4; q++) {
-      an += s_cn[q];
-      af += s_cf[q];
-    }
-    s.tagg[b] = make_uint2(an, af);
-    if (an | af) atomicAdd(&s.tsup[(b / INC_SUP) * TSUP_STRIDE], (static_cast<unsigned long long>(an) << 32) | af);
-  }
-  TSTAMP(2);
-  TSTAMP(3);
-  TSPRINT("classify", 4);
+  inc_classify_tile(sc, dcell, code, g, dcc, s, usey, usez, blockIdx.x);
 }
 
 // One block per IB_BOX consecutive boxes [c0, c0 + IB_BOX).
@@ -1236,7 +1129,7 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
                        bool withm1, bool withpre, const KConst& K, const double dom_posmin[3], float4* poscell,
                        float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
                        IncDivScratch& s, SortScratch& srt, unsigned keybits, const float4* phase_eos,
-                       const SlabFaces* faces, unsigned ngl, unsigned ngr, const ItemBuild* items) {
+                       const SlabFaces* faces, unsigned ngl, unsigned ngr, const ItemBuild* items, bool classified) {
   s.gen++;
   const int usey = g.ncy > 1, usez = g.ncz > 1;
   const unsigned omax = 1u + (usey ? unsigned(g.ncx) : 0u) + (usez ? g.nsheet : 0u);
@@ -1244,8 +1137,10 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
   s.avin = srt.vals[0];
   s.nvl = faces ? ngl : 0u;
   s.nvr = faces ? ngr : 0u;
-  hipLaunchKernelGGL(k_inc_classify, dim3(s.nb1), dim3(INC_BS), 0, stm, sc, src.dcell, src.code, g, K.domcellcode, s,
-                     usey, usez);
+  // (classified: the update kernel classified its own tiles, sph_incdiv.hpp)
+  if (!classified)
+    hipLaunchKernelGGL(k_inc_classify, dim3(s.nb1), dim3(INC_BS), 0, stm, sc, src.dcell, src.code, g, K.domcellcode,
+                       s, usey, usez);
   // slab: the reserved ghost slots are counted per face box (faces->pre: the received
   // counts' prefixes); k_inc_boxes reads their bounds from the prefixes, no keys needed
   if (faces) {

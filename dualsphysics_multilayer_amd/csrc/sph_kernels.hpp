@@ -275,7 +275,7 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
                        float* press, DivGrid g, const unsigned* begincell_old, unsigned* begincell_new,
                        IncDivScratch& s, SortScratch& srt, unsigned keybits, const float4* phase_eos = nullptr,
                        const SlabFaces* faces = nullptr, unsigned ngl = 0, unsigned ngr = 0,
-                       const ItemBuild* items = nullptr);
+                       const ItemBuild* items = nullptr, bool classified = false);
 
 // ---- interaction (cusph::Interaction_Forces, JSphGpu_ker.cu:788-885) ----
 // With floating bodies (ftmassp != nullptr: particle mass per body, `code` of the
@@ -393,19 +393,22 @@ void launch_fold_maxima(hipStream_t stm, DevScalars* sc, unsigned* folded, bool 
 // them DCELL_DISCARD for the next divide.
 // shiftpos (nullptr: no shifting): the interaction's shifting sums, turned into the
 // displacement of JSphShifting::RunCpu inside the update.
+// cls (not null): the incremental divide's classification rides on the update (sph_incdiv.hpp)
 void launch_verlet(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, bool euler, const float4* arace,
-                   PartArrays a, DivGrid g, const float4* shiftpos = nullptr);
+                   PartArrays a, DivGrid g, const float4* shiftpos = nullptr, const IncDivScratch* cls = nullptr);
 void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
-                    DivGrid g);
+                    DivGrid g, const IncDivScratch* cls = nullptr);
 void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
-                    DivGrid g, const float4* shiftpos = nullptr);
+                    DivGrid g, const float4* shiftpos = nullptr, const IncDivScratch* cls = nullptr);
 
 // ---- moving boundaries and floating bodies (sph_bodies.hip) ----
-constexpr int MOT_MAXOBJ = 32, MOT_MAXACT = 4;
+constexpr int MOT_MAXOBJ = 32, MOT_MAXACT = 4, MOT_MAXAXIS = 64;
 struct MotMov {     // one movement of the program (JMotionMov*), units as SphMotionMov
-  int type, nextidx, prev, pad;
-  double time;      // duration
-  double v[3], v2[3], phase[3], p1[3], p2[3];
+  int type, nextidx, prev, fields;
+  int ax, rax;      // its axis and (circular) reference point in MotionDev::axis, or -1
+  int dfirst, dn;   // file movements: rows [dfirst, dfirst + dn) of the table rows
+  double time;      // duration (< 0: flash)
+  double v[3], v2[3], phase[3];
   double ang, ang2, ang3;
 };
 struct MotEvt {     // JMotionEvent
@@ -413,13 +416,27 @@ struct MotEvt {     // JMotionEvent
   double start, finish;
 };
 struct MotAct {     // JMotionMovActive
-  int mov, del;
+  int mov, del, flash, dfindex;
   double start, finish, eventfinish;
   double vel[3], velang, phase[3], phaseuni;
+  double dflast[3], dflastang;  // the file movements' last position / angle
 };
-struct MotObj {     // JMotionObj run state
-  int active, moving, na, pad;
+struct M4d {        // JMatrix4d, row major a[4*r+c]
+  double a[16];
+};
+struct MPos {       // JMotionPos: accumulated motion of one object in one step
+  int simple, pad;
+  double s[3];
+  M4d m;
+};
+struct MotObj {     // JMotionObj run state; nodes depth first (a parent before its children)
+  int active, moving, na, parent, ref, pad;
   MotAct act[MOT_MAXACT];
+  MPos modpos;      // its motion of the current step (read by its children)
+};
+struct MotAxis {    // JMotionAxis: moved with the parent object; a circular reference point is
+  double p1[3], p2[3];  // moved by its movement
+  int obj, pad;
 };
 struct MotOut {     // JMotionListData of one object for the step: 0 none, 1 linear, 2 matrix
   int type, pad;
@@ -427,9 +444,10 @@ struct MotOut {     // JMotionListData of one object for the step: 0 none, 1 lin
   double m[12];
 };
 struct MotionDev {
-  int nobj, eventnext, objsactive, overflow;
+  int nobj, nref, eventnext, objsactive, overflow, naxis;
   MotObj obj[MOT_MAXOBJ];
-  MotOut out[MOT_MAXOBJ];
+  MotOut out[MOT_MAXOBJ];  // by ref
+  MotAxis axis[MOT_MAXAXIS];
 };
 // Floating body (StFloatingData + StFtoForces/StFtoForcesRes), device resident.
 // One JLinearValue table of a floating body on the device: its rows [first, first + n) of
@@ -459,9 +477,10 @@ struct FtBody {
 // k_motion over [sc->tstep0, +sc->last_dt) (or [t0, t0+dt) when t0 >= 0: restart
 // catch-up, no particle update), then the boundary particles.
 void launch_motion(hipStream_t stm, unsigned npbcap, DevScalars* sc, const KConst& K, MotionDev* md,
-                   const MotMov* movs, const MotEvt* evts, const PartArrays& a, float4* normal, const DivGrid& g);
+                   const MotMov* movs, const MotEvt* evts, const double* data, const PartArrays& a, float4* normal,
+                   const DivGrid& g);
 void launch_motion_advance(hipStream_t stm, DevScalars* sc, MotionDev* md, const MotMov* movs, const MotEvt* evts,
-                           double t0, double dt);
+                           const double* data, double t0, double dt);
 // Owned floating particles only (slab ghosts are summed by their owner).
 void launch_ft_ridp(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, unsigned casenpb,
                     unsigned nftp, unsigned* ftridp, const KConst& K, const DivGrid& g);

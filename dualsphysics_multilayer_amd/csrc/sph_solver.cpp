@@ -1290,7 +1290,7 @@ void SphGpuSingle::RunCellDivide() {
     inc_.nb2 = inc_blocks_boxes(G.nctt);
     launch_divide_inc(stream, cap_, sc_, cur_, alt_, withm1, havepre_, K, C.dom_posmin, poscell_, press_, G, begincell_,
                       begincell_alt_, inc_, sort_, keybits_, nn_ ? phaseeos_ : nullptr, ghosts ? &faces_ : nullptr, ngl,
-                      ngr, tiled_ ? &ib : nullptr);
+                      ngr, tiled_ ? &ib : nullptr, classified_);
     std::swap(begincell_, begincell_alt_);
   } else {
     // the ghosts' slots sort as entries [np, np + ngl + ngr) after the particles
@@ -1307,6 +1307,7 @@ void SphGpuSingle::RunCellDivide() {
     if (tiled_) launch_items(stream, ib);
   }
   inc_valid_ = inc_ok_;
+  classified_ = false;
   inc_.napp = 0;
   inc_.nvl = inc_.nvr = 0;
   std::swap(cur_, alt_);
@@ -1514,12 +1515,24 @@ void SphGpuSingle::UpdateTurn(bool begin) {
   else transport_->turn_done(SlabTransport::TURN_UPDATE, stream);
 }
 
+// The divide's classification in the update kernel (sph_incdiv.hpp): the next divide is
+// incremental and nothing moves a particle between the update and the divide (one domain:
+// no exchange, no re-partition; no floating bodies, no moving boundaries).  SPH_CLS_SPLIT=1
+// (test hook) keeps the separate k_inc_classify launch.
+const IncDivScratch* SphGpuSingle::ClassifyInUpdate() {
+  static const bool split = std::getenv("SPH_CLS_SPLIT") && std::atoi(std::getenv("SPH_CLS_SPLIT"));
+  const bool ok = !split && !slab() && inc_ok_ && inc_valid_ && G.ncx >= 3 && (G.ncy >= 3 || G.ncy == 1) &&
+                  !nftbodies_ && !nmotobj_ && inc_.napp == 0;
+  classified_ = ok;
+  return ok ? &inc_ : nullptr;
+}
+
 void SphGpuSingle::ComputeVerlet() {
   UpdateTurn(true);
   TimedBegin(1);
   verletstep_++;
   const bool euler = !(verletstep_ < C.verlet_steps);
-  launch_verlet(stream, cap_, sc_, K, euler, arace_, cur_, G, shift_ ? shiftpos_ : nullptr);
+  launch_verlet(stream, cap_, sc_, K, euler, arace_, cur_, G, shift_ ? shiftpos_ : nullptr, ClassifyInUpdate());
   if (euler) verletstep_ = 0;
   std::swap(cur_.velrhop, cur_.velrhopm1);
   TimedEnd(1);
@@ -1533,7 +1546,7 @@ void SphGpuSingle::ComputeSymplecticPre() {
   std::swap(cur_.posz, cur_.poszpre);
   std::swap(cur_.velrhop, cur_.velrhoppre);
   havepre_ = true;
-  launch_sym_pre(stream, cap_, sc_, K, arace_, cur_, G);
+  launch_sym_pre(stream, cap_, sc_, K, arace_, cur_, G, ClassifyInUpdate());
   TimedEnd(1);
   UpdateTurn(false);
 }
@@ -1541,7 +1554,7 @@ void SphGpuSingle::ComputeSymplecticPre() {
 void SphGpuSingle::ComputeSymplecticCorr() {
   UpdateTurn(true);
   TimedBegin(1);
-  launch_sym_cor(stream, cap_, sc_, K, arace_, cur_, G, shift_ ? shiftpos_ : nullptr);
+  launch_sym_cor(stream, cap_, sc_, K, arace_, cur_, G, shift_ ? shiftpos_ : nullptr, ClassifyInUpdate());
   havepre_ = false;
   TimedEnd(1);
   UpdateTurn(false);
@@ -1573,7 +1586,7 @@ void SphGpuSingle::ComputeStep() {
 // ---- moving boundaries and floating bodies ------------------------------------------------
 void SphGpuSingle::RunMotion() {
   TimedBegin(1);
-  launch_motion(stream, slab() ? cap_ : npb0_, sc_, K, motion_, motmovs_, motevts_, cur_, normal_, G);
+  launch_motion(stream, slab() ? cap_ : npb0_, sc_, K, motion_, motmovs_, motevts_, motdata_, cur_, normal_, G);
   TimedEnd(1);
 }
 
@@ -1589,34 +1602,96 @@ void SphGpuSingle::RunFloating(bool predictor) {
   TimedEnd(1);
 }
 
-// JDsMotion::Init (JDsMotion.cpp:94-106) + JMotion::Prepare (JMotion.cpp:303-317).
+// The flat program: one top-level object per ref (sph_solver_set_motion).
 void SphGpuSingle::SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* movs, unsigned nevt,
                              const SphMotionEvent* evts) {
+  if (!nobj || nobj > unsigned(MOT_MAXOBJ)) throw SphError(SPH_ERR_UNSUPPORTED, "number of moving objects out of range");
+  std::vector<SphMotionObj> nodes(nobj);
+  for (unsigned k = 0; k < nobj; k++) nodes[k] = SphMotionObj{-1, int32_t(k)};
+  SetMotionTree(nobj, nodes.data(), nmov, movs, nevt, evts, 0, nullptr);
+}
+
+// JDsMotion::Init (JDsMotion.cpp:94-106) + JMotion::ReadXml / ObjAdd / AxisAdd / MovAdd* /
+// EventAdd / Prepare (JMotion.cpp:96-317,556-700): the program uploaded once; k_motion runs
+// it every step.
+void SphGpuSingle::SetMotionTree(unsigned nnode, const SphMotionObj* nodes, unsigned nmov, const SphMotionMov* movs,
+                                 unsigned nevt, const SphMotionEvent* evts, unsigned nrows, const double* rows) {
   // Symmetry + ShiftMode NoFixed: the images of a moving-boundary p2 would join the shifting
   // sums before the first fixed p2 in the reference's order (JSphCpu.cpp:743-750, 793-796);
   // this core visits the images after the rows (sph_ext.hip), exact only without them
-  if (C.symmetry && C.shift_mode == SPH_SHIFT_NOFIXED && nobj)
+  if (C.symmetry && C.shift_mode == SPH_SHIFT_NOFIXED && nnode)
     throw SphError(SPH_ERR_UNSUPPORTED, "Symmetry with ShiftMode NoFixed and moving boundaries is not implemented");
   if (stepped_ || motion_) throw SphError(SPH_ERR_STATE, "the motion is configured once, before the first step");
-  if (!nobj || nobj > unsigned(MOT_MAXOBJ)) throw SphError(SPH_ERR_UNSUPPORTED, "number of moving objects out of range");
-  if ((nmov && !movs) || (nevt && !evts)) throw SphError(SPH_ERR_ARG, "motion arrays missing");
+  if (!nnode || nnode > unsigned(MOT_MAXOBJ)) throw SphError(SPH_ERR_UNSUPPORTED, "number of motion objects out of range");
+  if ((nmov && !movs) || (nevt && !evts) || (nrows && !rows)) throw SphError(SPH_ERR_ARG, "motion arrays missing");
+  MotionDev md;
+  std::memset(&md, 0, sizeof(md));
+  md.nobj = int(nnode);
+  // the tree: depth first, a parent before its children, every subtree contiguous (the
+  // parent of a node is the previous node or one of its ancestors)
+  std::vector<int> seen(MOT_MAXOBJ, 0);
+  int nref = 0;
+  for (unsigned i = 0; i < nnode; i++) {
+    const int p = nodes[i].parent;
+    bool ok = p < 0 || (p < int(i) && p >= 0);
+    if (ok && p >= 0) {
+      ok = false;
+      for (int q = int(i) - 1; q >= 0 && !ok; q = md.obj[q].parent) ok = (q == p);
+    }
+    if (!ok) throw SphError(SPH_ERR_ARG, "motion objects: not in depth-first order");
+    const int r = nodes[i].ref;
+    if (r >= MOT_MAXOBJ || r < -1) throw SphError(SPH_ERR_ARG, "motion objects: ref out of range");
+    if (r >= 0) {
+      if (seen[r]++) throw SphError(SPH_ERR_ARG, "motion objects: a ref is used twice");
+      nref = std::max(nref, r + 1);
+    }
+    md.obj[i].parent = p;
+    md.obj[i].ref = r;
+  }
+  for (int r = 0; r < nref; r++)  // JMotion::CreateMotList
+    if (!seen[r]) throw SphError(SPH_ERR_ARG, "Motion references are no consecutives.");
+  md.nref = nref;
   std::vector<MotMov> mv(std::max(nmov, 1u));
   auto find = [&](int obj, int id) -> int {
     for (unsigned k = 0; k < nmov; k++)
       if (movs[k].obj == obj && movs[k].id == id) return int(k);
     return -1;
   };
+  // JMotion::AxisAdd: an axis of two distinct points is shared by the object's movements that
+  // name the same points; a circular movement's reference point (p1 == p2) is its own
+  auto axis_add = [&](int obj, const double* p1, const double* p2) -> int {
+    const bool same = p1[0] == p2[0] && p1[1] == p2[1] && p1[2] == p2[2];
+    if (!same)
+      for (int k = 0; k < md.naxis; k++) {
+        const MotAxis& a = md.axis[k];
+        if (a.obj == obj && a.p1[0] == p1[0] && a.p1[1] == p1[1] && a.p1[2] == p1[2] && a.p2[0] == p2[0] &&
+            a.p2[1] == p2[1] && a.p2[2] == p2[2])
+          return k;
+      }
+    if (md.naxis >= MOT_MAXAXIS) throw SphError(SPH_ERR_UNSUPPORTED, "too many motion axes");
+    MotAxis& a = md.axis[md.naxis];
+    for (int c = 0; c < 3; c++) {
+      a.p1[c] = p1[c];
+      a.p2[c] = p2[c];
+    }
+    a.obj = obj;
+    return md.naxis++;
+  };
   for (unsigned k = 0; k < nmov; k++) {
     const SphMotionMov& m = movs[k];
-    if (m.obj < 0 || unsigned(m.obj) >= nobj) throw SphError(SPH_ERR_ARG, "movement of an unknown object");
-    if (m.type < SPH_MOV_WAIT || m.type > SPH_MOV_ROTSINU) throw SphError(SPH_ERR_UNSUPPORTED, "movement type");
-    if (!(m.duration >= 0)) throw SphError(SPH_ERR_UNSUPPORTED, "movements with a negative duration (flash)");
+    if (m.obj < 0 || unsigned(m.obj) >= nnode) throw SphError(SPH_ERR_ARG, "movement of an unknown object");
+    if (m.type < SPH_MOV_WAIT || m.type > SPH_MOV_NULL) throw SphError(SPH_ERR_UNSUPPORTED, "movement type");
+    if (m.type == SPH_MOV_WAIT && m.duration < 0)
+      throw SphError(SPH_ERR_ARG, "Wating times lenght lower than zero are not allowed.");
+    if (find(m.obj, m.id) != int(k)) throw SphError(SPH_ERR_ARG, "Cannot add a movement with a existing id inside the object.");
     MotMov& d = mv[k];
     std::memset(&d, 0, sizeof(d));
     d.type = m.type;
     d.prev = m.prev;
+    d.fields = m.fields;
     d.time = m.duration;
     d.nextidx = -1;
+    d.ax = d.rax = -1;
     if (m.next) {
       d.nextidx = find(m.obj, m.next);
       if (d.nextidx < 0) throw SphError(SPH_ERR_ARG, "movement `next` is not defined in its object");
@@ -1625,16 +1700,27 @@ void SphGpuSingle::SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* m
       d.v[c] = m.vec[c];
       d.v2[c] = m.vec2[c];
       d.phase[c] = m.phase[c];
-      d.p1[c] = m.axisp1[c];
-      d.p2[c] = m.axisp2[c];
     }
     d.ang = m.ang;
     d.ang2 = m.ang2;
     d.ang3 = m.ang3;
+    const bool rot = m.type == SPH_MOV_ROT || m.type == SPH_MOV_ROTACE || m.type == SPH_MOV_ROTSINU ||
+                     m.type == SPH_MOV_ROTFILE;
+    const bool cir = m.type == SPH_MOV_CIR || m.type == SPH_MOV_CIRACE || m.type == SPH_MOV_CIRSINU;
+    if (rot || cir) d.ax = axis_add(m.obj, m.axisp1, m.axisp2);
+    if (cir) d.rax = axis_add(m.obj, m.ref, m.ref);
+    if (m.type == SPH_MOV_RECTFILE || m.type == SPH_MOV_ROTFILE) {
+      if (m.data_n < 2 || size_t(m.data_first) + m.data_n > nrows)
+        throw SphError(SPH_ERR_ARG, "file movement: its table rows are out of range (at least two)");
+      if (m.type == SPH_MOV_RECTFILE && !(m.fields & 7)) throw SphError(SPH_ERR_ARG, "You need at least one position field.");
+      d.dfirst = int(m.data_first);
+      d.dn = int(m.data_n);
+    }
   }
   // events ordered from last to first start, with the reference's exchange sort
   std::vector<MotEvt> ev(nevt);
   for (unsigned k = 0; k < nevt; k++) {
+    if (evts[k].obj < 0 || unsigned(evts[k].obj) >= nnode) throw SphError(SPH_ERR_ARG, "event of an unknown object");
     ev[k].obj = evts[k].obj;
     ev[k].mov = find(evts[k].obj, evts[k].mov);
     if (ev[k].mov < 0) throw SphError(SPH_ERR_ARG, "event of an undefined movement");
@@ -1644,9 +1730,6 @@ void SphGpuSingle::SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* m
   for (unsigned c = 0; c + 1 < nevt; c++)
     for (unsigned c2 = c + 1; c2 < nevt; c2++)
       if (ev[c].start < ev[c2].start) std::swap(ev[c], ev[c2]);
-  MotionDev md;
-  std::memset(&md, 0, sizeof(md));
-  md.nobj = int(nobj);
   md.eventnext = int(nevt) - 1;
   check_hip(hipMalloc((void**)&motion_, sizeof(MotionDev)), "hipMalloc motion");
   allocs_.push_back(motion_);
@@ -1654,14 +1737,18 @@ void SphGpuSingle::SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* m
   allocs_.push_back(motmovs_);
   check_hip(hipMalloc((void**)&motevts_, sizeof(MotEvt) * std::max(nevt, 1u)), "hipMalloc motion");
   allocs_.push_back(motevts_);
+  check_hip(hipMalloc((void**)&motdata_, sizeof(double) * 4 * std::max(nrows, 1u)), "hipMalloc motion");
+  allocs_.push_back(motdata_);
   check_hip(hipMemcpy(motion_, &md, sizeof(md), hipMemcpyHostToDevice), "upload motion");
   check_hip(hipMemcpy(motmovs_, mv.data(), sizeof(MotMov) * mv.size(), hipMemcpyHostToDevice), "upload motion");
   if (nevt) check_hip(hipMemcpy(motevts_, ev.data(), sizeof(MotEvt) * nevt, hipMemcpyHostToDevice), "upload motion");
-  nmotobj_ = nobj;
+  if (nrows)
+    check_hip(hipMemcpy(motdata_, rows, sizeof(double) * 4 * nrows, hipMemcpyHostToDevice), "upload motion tables");
+  nmotobj_ = unsigned(nref);
   // restart: JDsMotion::SetTimeMod/ResetTime run the program from 0 to the PART time
   double t0 = 0;
   check_hip(hipMemcpy(&t0, &sc_->time, sizeof(double), hipMemcpyDeviceToHost), "read time");
-  if (t0 > 0) launch_motion_advance(stream, sc_, motion_, motmovs_, motevts_, 0.0, t0);
+  if (t0 > 0) launch_motion_advance(stream, sc_, motion_, motmovs_, motevts_, motdata_, 0.0, t0);
   Sync();
 }
 

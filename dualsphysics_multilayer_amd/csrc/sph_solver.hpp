@@ -102,6 +102,8 @@ class SphGpuSingle {
   std::string HaloDiag();
   // Moving boundaries / floating bodies (sph_bodies.hip), configured before the first step.
   void SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* movs, unsigned nevt, const SphMotionEvent* evts);
+  void SetMotionTree(unsigned nnode, const SphMotionObj* nodes, unsigned nmov, const SphMotionMov* movs, unsigned nevt,
+                     const SphMotionEvent* evts, unsigned nrows, const double* rows);
   void SetFloatings(unsigned nft, const SphFloatingDef* defs, double ftpause);
   // Imposed velocity / external force table of one body (SPH_FTTAB_*), before the first step.
   void SetFloatingTable(unsigned body, int kind, unsigned n, const double* times, const double* values);
@@ -233,6 +235,9 @@ class SphGpuSingle {
   MotionDev* motion_ = nullptr;
   MotMov* motmovs_ = nullptr;
   MotEvt* motevts_ = nullptr;
+  double* motdata_ = nullptr;  // rows of the file movements' tables (4 doubles each)
+  bool classified_ = false;     // the last update classified the particles for the divide
+  const IncDivScratch* ClassifyInUpdate();
   unsigned nmotobj_ = 0;
   FtBody* ftbodies_ = nullptr;
   unsigned* ftridp_ = nullptr;   // floating particle (idp - CaseNpb) -> position, per divide

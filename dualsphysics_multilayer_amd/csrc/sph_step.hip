@@ -10,6 +10,7 @@
 #include <cfloat>
 
 #include "sph_kernels.hpp"
+#include "sph_incdiv.hpp"
 
 namespace sphx {
 
@@ -137,12 +138,10 @@ __device__ __forceinline__ bool slab_ghost(const KConst& K, const DivGrid& g, un
 
 // ComputeVerlet (JSphCpu.cpp:1381-1399): bound -> ComputeVelrhopBound, fluid -> ComputeVerletVarsFluid.
 // New values are written in velrhopm1 (the caller swaps velrhop/velrhopm1 afterwards).
-__global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ sc, KConst K, int euler,
-                                                const float4* __restrict__ arace, PartArrays a, DivGrid g,
-                                                const float4* __restrict__ shiftpos) {
-  const unsigned np = sc->np, npb = sc->npb;
-  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= np) return;
+__device__ __forceinline__ void verlet_part(const DevScalars* __restrict__ sc, const KConst& K, int euler,
+                                            const float4* __restrict__ arace, const PartArrays& a, const DivGrid& g,
+                                            const float4* __restrict__ shiftpos, unsigned p) {
+  const unsigned npb = sc->npb;
   if (halted(sc)) {  // keep the state: the caller's velrhop/velrhopm1 swap then restores it
     a.velrhopm1[p] = a.velrhop[p];
     // a slab still drops its ghosts: the next exchange sends fresh copies (without this the
@@ -178,20 +177,19 @@ __global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ s
   update_pos(K, pxy.x, pxy.y, a.posz[p], dx, dy, dz, outrhop, p, a);
   a.velrhopm1[p] = nv;
 }
-
-void launch_verlet(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, bool euler, const float4* arace,
-                   PartArrays a, DivGrid g, const float4* shiftpos) {
-  const unsigned nb = (cap + 255) / 256;
-  hipLaunchKernelGGL(k_verlet, dim3(nb), dim3(256), 0, stm, sc, K, int(euler), arace, a, g, shiftpos);
+__global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ sc, KConst K, int euler,
+                                                const float4* __restrict__ arace, PartArrays a, DivGrid g,
+                                                const float4* __restrict__ shiftpos) {
+  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < sc->np) verlet_part(sc, K, euler, arace, a, g, shiftpos, p);
 }
 
 // ComputeSymplecticPre (JSphCpu.cpp:1406-1504).  The caller has already moved the
 // current pos/velrhop into the *pre arrays (pointer swap); new values go to pos/velrhop.
-__global__ __launch_bounds__(256) void k_sym_pre(const DevScalars* __restrict__ sc, KConst K,
-                                                 const float4* __restrict__ arace, PartArrays a, DivGrid g) {
-  const unsigned np = sc->np, npb = sc->npb;
-  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= np) return;
+__device__ __forceinline__ void sym_pre_part(const DevScalars* __restrict__ sc, const KConst& K,
+                                             const float4* __restrict__ arace, const PartArrays& a, const DivGrid& g,
+                                             unsigned p) {
+  const unsigned npb = sc->npb;
   if (halted(sc)) {  // keep the state (the caller moved it into the pre arrays)
     a.velrhop[p] = a.velrhoppre[p];
     a.posxy[p] = a.posxypre[p];
@@ -234,20 +232,18 @@ __global__ __launch_bounds__(256) void k_sym_pre(const DevScalars* __restrict__ 
     a.posz[p] = pz;
   }
 }
-
-void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
-                    DivGrid g) {
-  const unsigned nb = (cap + 255) / 256;
-  hipLaunchKernelGGL(k_sym_pre, dim3(nb), dim3(256), 0, stm, sc, K, arace, a, g);
+__global__ __launch_bounds__(256) void k_sym_pre(const DevScalars* __restrict__ sc, KConst K,
+                                                 const float4* __restrict__ arace, PartArrays a, DivGrid g) {
+  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < sc->np) sym_pre_part(sc, K, arace, a, g, p);
 }
 
 // ComputeSymplecticCorr (JSphCpu.cpp:1510-1606).
-__global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ sc, KConst K,
-                                                 const float4* __restrict__ arace, PartArrays a, DivGrid g,
-                                                 const float4* __restrict__ shiftpos) {
-  const unsigned np = sc->np, npb = sc->npb;
-  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= np || slab_ghost(K, g, a.dcell, p) || halted(sc)) return;  // ghosts dropped even when halted
+__device__ __forceinline__ void sym_cor_part(const DevScalars* __restrict__ sc, const KConst& K,
+                                             const float4* __restrict__ arace, const PartArrays& a, const DivGrid& g,
+                                             const float4* __restrict__ shiftpos, unsigned p) {
+  const unsigned npb = sc->npb;
+  if (slab_ghost(K, g, a.dcell, p) || halted(sc)) return;  // ghosts dropped even when halted
   const double dt = sc->dt, dt05 = dt * .5;
   const float4 ra = arace[p];
   const float4 vr = a.velrhop[p];
@@ -288,9 +284,65 @@ __global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ 
     a.posz[p] = pz;
   }
 }
+__global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ sc, KConst K,
+                                                 const float4* __restrict__ arace, PartArrays a, DivGrid g,
+                                                 const float4* __restrict__ shiftpos) {
+  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < sc->np) sym_cor_part(sc, K, arace, a, g, shiftpos, p);
+}
 
+// The update with the incremental divide's classification of the same particles (sph_incdiv.hpp):
+// one block per classify tile updates its INC_TILE particles (INC_IPT per thread at stride
+// INC_BS, the classify mapping) and then classifies them from the dcell / code it has just
+// written (each thread reads back its own stores).  The single-domain step without bodies:
+// nothing moves a particle between the update and the divide.
+enum { UPD_VERLET = 0, UPD_SYM_PRE = 1, UPD_SYM_COR = 2 };
+template <int KIND>
+__global__ __launch_bounds__(INC_BS) void k_update_cls(DevScalars* __restrict__ sc, KConst K, int euler,
+                                                       const float4* __restrict__ arace, PartArrays a, DivGrid g,
+                                                       const float4* __restrict__ shiftpos, IncDivScratch s, int usey,
+                                                       int usez) {
+  const unsigned np = sc->np;
+#pragma unroll
+  for (int k = 0; k < INC_IPT; k++) {
+    const unsigned p = blockIdx.x * INC_TILE + k * INC_BS + threadIdx.x;
+    if (p >= np) continue;
+    if (KIND == UPD_VERLET) verlet_part(sc, K, euler, arace, a, g, shiftpos, p);
+    else if (KIND == UPD_SYM_PRE) sym_pre_part(sc, K, arace, a, g, p);
+    else sym_cor_part(sc, K, arace, a, g, shiftpos, p);
+  }
+  inc_classify_tile(sc, a.dcell, a.code, g, K.domcellcode, s, usey, usez, blockIdx.x);
+}
+
+// cls: the divide's scratch when the classification rides on the update (nullptr: the
+// per-particle kernel, the divide classifies).
+void launch_verlet(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, bool euler, const float4* arace,
+                   PartArrays a, DivGrid g, const float4* shiftpos, const IncDivScratch* cls) {
+  if (cls) {
+    hipLaunchKernelGGL(k_update_cls<UPD_VERLET>, dim3(cls->nb1), dim3(INC_BS), 0, stm, sc, K, int(euler), arace, a,
+                       g, shiftpos, *cls, int(g.ncy > 1), int(g.ncz > 1));
+    return;
+  }
+  const unsigned nb = (cap + 255) / 256;
+  hipLaunchKernelGGL(k_verlet, dim3(nb), dim3(256), 0, stm, sc, K, int(euler), arace, a, g, shiftpos);
+}
+void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
+                    DivGrid g, const IncDivScratch* cls) {
+  if (cls) {
+    hipLaunchKernelGGL(k_update_cls<UPD_SYM_PRE>, dim3(cls->nb1), dim3(INC_BS), 0, stm, sc, K, 0, arace, a, g,
+                       static_cast<const float4*>(nullptr), *cls, int(g.ncy > 1), int(g.ncz > 1));
+    return;
+  }
+  const unsigned nb = (cap + 255) / 256;
+  hipLaunchKernelGGL(k_sym_pre, dim3(nb), dim3(256), 0, stm, sc, K, arace, a, g);
+}
 void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
-                    DivGrid g, const float4* shiftpos) {
+                    DivGrid g, const float4* shiftpos, const IncDivScratch* cls) {
+  if (cls) {
+    hipLaunchKernelGGL(k_update_cls<UPD_SYM_COR>, dim3(cls->nb1), dim3(INC_BS), 0, stm, sc, K, 0, arace, a, g,
+                       shiftpos, *cls, int(g.ncy > 1), int(g.ncz > 1));
+    return;
+  }
   const unsigned nb = (cap + 255) / 256;
   hipLaunchKernelGGL(k_sym_cor, dim3(nb), dim3(256), 0, stm, sc, K, arace, a, g, shiftpos);
 }

@@ -72,6 +72,31 @@ def _read_datafile(path: str, what: str, nvalues: int = 1, special: bool = False
     return np.array(rows, np.float64)
 
 
+def _read_datafile_cols(path: str, what: str, ncols: int) -> np.ndarray:
+    """Every row's first ncols values of a JReadDatafile table (separators and remarks as
+    _read_datafile; JMotionDataFile::LoadFilePos / LoadFileAng, JMotionMov.cpp:252-300)."""
+    if not os.path.isfile(path):
+        raise CaseError(f"{what}: file not found {path}")
+    lines = [ln.strip() for ln in open(path).read().replace("\r", "").split("\n")]
+    lines = [ln for ln in lines if ln and not ln.startswith("#")]
+    head = "".join(lines[:20])
+    ws, sc, cm = head.count(" ") + head.count("\t"), head.count(";"), head.count(",")
+    sep = None if ws >= sc and ws >= cm else (";" if sc >= cm else ",")
+    import re
+
+    def atof(v: str) -> float:
+        m = re.match(r"\s*[-+]?(\d+\.?\d*|\.\d+)([eE][-+]?\d+)?", v)
+        return float(m.group(0)) if m else 0.0
+
+    rows = []
+    for ln in lines:
+        f = ln.split(sep) if sep else ln.split()
+        if len(f) < ncols:
+            raise CaseError(f"{what}: value {len(f) + 1} does not exist in line '{ln}' of {path}")
+        rows.append(tuple(atof(v) for v in f[:ncols]))
+    return np.array(rows, np.float64).reshape(-1, ncols)
+
+
 class CaseError(ValueError):
     """An invalid or unsupported case configuration (the reference's JException)."""
 
@@ -719,86 +744,158 @@ class XmlCase:
         return np.array(rows, np.float64)  # in the XML's order (JLinearValue walks them as they come)
 
     # -- JMotion::ReadXml (JMotion.cpp:556-700) + JDsMotion::ConfigObjects (JDsMotion.cpp:67-89) --
+    MOV_TYPES = {"wait": 1, "mvrect": 2, "mvrectace": 3, "mvrot": 4, "mvrotace": 5, "mvrectsinu": 6, "mvrotsinu": 7,
+                 "mvcir": 8, "mvcirace": 9, "mvcirsinu": 10, "mvrectfile": 11, "mvfile": 11, "mvpredef": 11,
+                 "mvrotfile": 12, "mvnull": 13}
+
     def _load_motion(self, node):
+        """The motion program as a tree of objects (<obj> virtual, <objreal ref>), depth first:
+        motion = {nobj: the moving blocks, objs: [{parent, ref}], movs / evts with `obj` = the
+        node index, rows: the file movements' tables, (t, x, y, z) / (t, degrees, 0, 0)}."""
         self.motion = None
         nobj = len(self.moving_blocks)
         if node is None or not len(list(node)):
             if nobj:
                 raise CaseError("The number of mobile objects do not match the predefined motions in XML file.")
             return
-        movs, evts, refs = [], [], []
+        objs, movs, evts, rows = [], [], [], []
         deg2rad, rad2deg = 0.017453292519943295769, 57.29577951308232087684
         f32 = lambda v: float(np.float32(v))  # JXml::GetAttributeFloat
-        for obj in node:
-            if obj.tag.startswith("_"):
-                continue
-            if obj.tag not in ("objreal", "obj"):
-                raise CaseError(f"<motion>: unknown element <{obj.tag}>.")
-            if obj.tag == "obj" or obj.find("objreal") is not None or obj.find("obj") is not None:
-                raise CaseError("<motion>: nested or virtual motion objects are not supported by this core.")
-            ref = int(obj.get("ref"))
-            refs.append(ref)
-            for m in obj:
+        casedir = self._dircase
+
+        def read(ele, parent):
+            for m in ele:
                 t = m.tag
-                if t.startswith("_") or t == "begin":
+                if t.startswith("_"):
                     continue
-                types = {"wait": 1, "mvrect": 2, "mvrectace": 3, "mvrot": 4, "mvrotace": 5, "mvrectsinu": 6,
-                         "mvrotsinu": 7}
-                if t not in types:
-                    raise CaseError(f"<motion>: movement <{t}> is not supported by this core.")
-                units = m.get("anglesunits", "degrees")
-                if units not in ("degrees", "radians"):
-                    raise CaseError("<motion>: invalid anglesunits.")
-                deg = units == "degrees"
-                mv = dict(obj=ref, id=int(m.get("id")), next=int(m.get("next", 0)), type=types[t], prev=0,
-                          duration=f32(m.get("duration")), vec=(0.0,) * 3, vec2=(0.0,) * 3, phase=(0.0,) * 3,
-                          axisp1=(0.0,) * 3, axisp2=(0.0,) * 3, ang=0.0, ang2=0.0, ang3=0.0)
-                if mv["duration"] < 0:
-                    raise CaseError("<motion>: flash movements (negative duration) are not supported by this core.")
+                if t in ("obj", "objreal"):
+                    ref = -1
+                    if t == "objreal":
+                        if m.get("ref") is None:
+                            raise CaseError("<motion><objreal>: the attribute 'ref' is not found.")
+                        ref = int(m.get("ref"))
+                        if any(o["ref"] == ref for o in objs):
+                            raise CaseError(f"Cannot add a new object with an existing real reference (ref={ref}).")
+                    objs.append(dict(parent=parent, ref=ref))
+                    read(m, len(objs) - 1)
+                elif t in XmlCase.MOV_TYPES:
+                    if parent < 0:
+                        raise CaseError("Missing object.")
+                    movs.append(self._motion_mov(m, t, parent, rows, casedir, f32, deg2rad, rad2deg))
+                elif parent < 0 or t != "begin":
+                    raise CaseError(f"<motion>: unknown element <{t}>.")
+            if parent >= 0:  # the object's events, after its elements (JMotion.cpp:688-700)
+                for b in ele.findall("begin"):
+                    evts.append(dict(obj=parent, mov=int(b.get("mov")), start=f32(b.get("start")),
+                                     finish=f32(b.get("finish")) if b.get("finish") is not None else -1.0))
 
-                def v3(name):
-                    x = m.find(name)
-                    if x is None:
-                        raise CaseError(f"<motion><{t}>: the item is not found '{name}'.")
-                    return tuple(_attr_double(x, a, name) for a in "xyz")
-
-                def v1(name, attr):
-                    x = m.find(name)
-                    if x is None:
-                        raise CaseError(f"<motion><{t}>: the item is not found '{name}'.")
-                    return _attr_double(x, attr, name)
-
-                if t == "mvrect":
-                    mv["vec"] = v3("vel")
-                elif t == "mvrectace":
-                    mv["vec"] = v3("ace")
-                    mv["prev"] = int(m.find("velini") is None)
-                    mv["vec2"] = v3("velini") if not mv["prev"] else (0.0,) * 3
-                elif t in ("mvrot", "mvrotace", "mvrotsinu"):
-                    mv["axisp1"], mv["axisp2"] = v3("axisp1"), v3("axisp2")
-                    if t == "mvrot":  # MovAddRotation: kept in degrees
-                        mv["ang"] = v1("vel", "ang") * (1.0 if deg else rad2deg)
-                    elif t == "mvrotace":
-                        mv["ang"] = v1("ace", "ang") * (1.0 if deg else rad2deg)
-                        mv["prev"] = int(m.find("velini") is None)
-                        mv["ang2"] = (v1("velini", "ang") * (1.0 if deg else rad2deg)) if not mv["prev"] else 0.0
-                    else:  # MovAddRotSinu: ampl in degrees, phase in radians
-                        mv["ang"] = v1("freq", "v")
-                        mv["ang2"] = v1("ampl", "v") * (1.0 if deg else rad2deg)
-                        mv["prev"] = int(m.find("phase") is None)
-                        mv["ang3"] = (v1("phase", "v") * (deg2rad if deg else 1.0)) if not mv["prev"] else 0.0
-                elif t == "mvrectsinu":  # MovAddRecSinu: phase in radians
-                    mv["vec"], mv["vec2"] = v3("freq"), v3("ampl")
-                    mv["prev"] = int(m.find("phase") is None)
-                    mv["phase"] = (tuple(x * deg2rad for x in v3("phase")) if deg else v3("phase")) \
-                        if not mv["prev"] else (0.0,) * 3
-                movs.append(mv)
-            for b in obj.findall("begin"):
-                evts.append(dict(obj=ref, mov=int(b.get("mov")), start=f32(b.get("start")),
-                                 finish=f32(b.get("finish")) if b.get("finish") is not None else -1.0))
+        read(node, -1)
+        refs = [o["ref"] for o in objs if o["ref"] >= 0]
         if nobj != max(refs, default=-1) + 1:
             raise CaseError("The number of mobile objects do not match the predefined motions in XML file.")
-        self.motion = dict(nobj=nobj, movs=movs, evts=evts)
+        if sorted(refs) != list(range(len(refs))):
+            raise CaseError("Motion references are no consecutives.")
+        self.motion = dict(nobj=nobj, objs=objs, movs=movs, evts=evts, rows=rows)
+
+    @staticmethod
+    def _motion_mov(m, t, obj, rows, casedir, f32, deg2rad, rad2deg):
+        """One movement as JMotion::ReadXml + MovAdd* hold it (JMotion.cpp:198-300,568-680):
+        rotation speeds, accelerations and amplitudes in degrees, phases in radians."""
+        typ = XmlCase.MOV_TYPES[t]
+        mv = dict(obj=obj, id=int(m.get("id")), next=0, type=typ, prev=0, fields=0, data_first=0, data_n=0,
+                  duration=0.0, vec=(0.0,) * 3, vec2=(0.0,) * 3, phase=(0.0,) * 3, axisp1=(0.0,) * 3,
+                  axisp2=(0.0,) * 3, ref=(0.0,) * 3, ang=0.0, ang2=0.0, ang3=0.0)
+        deg = True
+        if t != "mvnull":
+            mv["duration"] = f32(m.get("duration"))
+            mv["next"] = int(m.get("next", 0))
+            units = m.get("anglesunits", "degrees")
+            if units not in ("degrees", "radians"):
+                raise CaseError("<motion>: invalid anglesunits.")
+            deg = units == "degrees"
+        if t == "wait" and mv["duration"] < 0:
+            raise CaseError("Wating times lenght lower than zero are not allowed.")
+
+        def v3(name):
+            x = m.find(name)
+            if x is None:
+                raise CaseError(f"<motion><{t}>: the item is not found '{name}'.")
+            return tuple(_attr_double(x, a, name) for a in "xyz")
+
+        def v1(name, attr):
+            x = m.find(name)
+            if x is None:
+                raise CaseError(f"<motion><{t}>: the item is not found '{name}'.")
+            return _attr_double(x, attr, name)
+
+        toang = 1.0 if deg else rad2deg  # speeds / accelerations / amplitudes kept in degrees
+        if t in ("mvrot", "mvrotace", "mvrotsinu", "mvcir", "mvcirace", "mvcirsinu", "mvrotfile"):
+            mv["axisp1"], mv["axisp2"] = v3("axisp1"), v3("axisp2")
+        if t in ("mvcir", "mvcirace", "mvcirsinu"):
+            mv["ref"] = v3("ref")
+        if t == "mvrect":
+            mv["vec"] = v3("vel")
+        elif t == "mvrectace":
+            mv["vec"] = v3("ace")
+            mv["prev"] = int(m.find("velini") is None)
+            mv["vec2"] = v3("velini") if not mv["prev"] else (0.0,) * 3
+        elif t in ("mvrot", "mvcir"):
+            mv["ang"] = v1("vel", "ang") * toang
+        elif t in ("mvrotace", "mvcirace"):
+            mv["ang"] = v1("ace", "ang") * toang
+            mv["prev"] = int(m.find("velini") is None)
+            mv["ang2"] = (v1("velini", "ang") * toang) if not mv["prev"] else 0.0
+        elif t in ("mvrotsinu", "mvcirsinu"):  # ampl in degrees, phase in radians
+            mv["ang"] = v1("freq", "v")
+            mv["ang2"] = v1("ampl", "v") * toang
+            mv["prev"] = int(m.find("phase") is None)
+            mv["ang3"] = (v1("phase", "v") * (deg2rad if deg else 1.0)) if not mv["prev"] else 0.0
+        elif t == "mvrectsinu":  # MovAddRecSinu: phase in radians
+            mv["vec"], mv["vec2"] = v3("freq"), v3("ampl")
+            mv["prev"] = int(m.find("phase") is None)
+            mv["phase"] = (tuple(x * deg2rad for x in v3("phase")) if deg else v3("phase")) \
+                if not mv["prev"] else (0.0,) * 3
+        elif t in ("mvrectfile", "mvfile", "mvpredef", "mvrotfile"):
+            ef = m.find("file")
+            if ef is None or ef.get("name") is None:
+                raise CaseError(f"<motion><{t}>: the item is not found 'file'.")
+            fn = ef.get("name")
+            path = fn if ("/" in fn or "\\" in fn) else os.path.join(casedir, fn)
+            if t == "mvrotfile":  # JMotionDataFile::LoadFileAng: time, angle (radians -> degrees)
+                tab = _read_datafile_cols(path, f"<motion><{t}>", 2)
+                ang = tab[:, 1] if deg else tab[:, 1] * rad2deg
+                new = [(float(a), float(b), 0.0, 0.0) for a, b in zip(tab[:, 0], ang)]
+                if len(new) < 2:
+                    raise CaseError(f"Cannot be less than two angles. ({path})")
+            else:  # LoadFilePos: `fields` values per row; x / y / z where given, else 0
+                def iattr(name, default=None):
+                    v = ef.get(name)
+                    if v is None:
+                        if default is None:
+                            raise CaseError(f"<motion><{t}><file>: the attribute '{name}' is not found.")
+                        return default
+                    return int(v)
+
+                fields, ft = iattr("fields"), iattr("fieldtime")
+                fx, fy, fz = iattr("fieldx", -1), iattr("fieldy", -1), iattr("fieldz", -1)
+                if ft < 0:
+                    raise CaseError("The 'time' is not defined.")
+                if ft >= fields:
+                    raise CaseError("the position of field 'time' is invalid.")
+                if fx < 0 and fy < 0 and fz < 0:
+                    raise CaseError("You need at least one position field.")
+                for nm, f in (("x", fx), ("y", fy), ("z", fz)):
+                    if f >= fields:
+                        raise CaseError(f"the position of field '{nm}' is invalid.")
+                tab = _read_datafile_cols(path, f"<motion><{t}>", fields)
+                new = [(float(r[ft]), float(r[fx]) if fx >= 0 else 0.0, float(r[fy]) if fy >= 0 else 0.0,
+                        float(r[fz]) if fz >= 0 else 0.0) for r in tab]
+                if len(new) < 2:
+                    raise CaseError(f"Cannot be less than two positions. ({path})")
+                mv["fields"] = (fx >= 0) | ((fy >= 0) << 1) | ((fz >= 0) << 2)
+            mv["data_first"], mv["data_n"] = len(rows), len(new)
+            rows.extend(new)
+        return mv
 
     def _check_loaded(self, h, prt):
         """JPartsLoad4::CheckConfig (JPartsLoad4.cpp:264-300)."""

@@ -45,7 +45,9 @@
  *                                492-516) over the .bi4 container of JBinaryData
  *                                (JBinaryData.cpp:700-1160,1467-1545): PART and case files
  *   sph_solver_set_motion ...... JDsMotion::Init + JSph::CalcMotion/JSphCpu::RunMotion
- *                                (JDsMotion.cpp:94-137, JSph.cpp:2308, JSphCpu.cpp:1692-1789)
+ *     (+ _tree)                  (JDsMotion.cpp:94-137, JSph.cpp:2308, JSphCpu.cpp:1692-1789;
+ *                                nested objects, circular / file / flash movements:
+ *                                JMotion.cpp:96-317,556-700, JMotionObj.cpp:40-580)
  *   sph_solver_set_floatings ... JSph::LoadCaseConfig floating objects (JSph.cpp:1046-1100) +
  *                                JSphCpuSingle::RunFloating (JSphCpuSingle.cpp:897-1010)
  *   sph_solver_set_floating_table  FtLinearVel/FtAngularVel/FtLinearForce/FtAngularForce
@@ -62,7 +64,7 @@
 extern "C" {
 #endif
 
-#define SPH_ABI_VERSION 11
+#define SPH_ABI_VERSION 12
 
 typedef enum {
   SPH_OK = 0,
@@ -456,18 +458,27 @@ enum {
   SPH_MOV_ROT = 4,       /* <mvrot>       ang = vel, axis                            */
   SPH_MOV_ROTACE = 5,    /* <mvrotace>    ang = ace, ang2 = velini (prev)            */
   SPH_MOV_RECTSINU = 6,  /* <mvrectsinu>  vec = freq, vec2 = ampl, phase (prev)      */
-  SPH_MOV_ROTSINU = 7    /* <mvrotsinu>   ang = freq, ang2 = ampl, ang3 = phase (prev), axis */
+  SPH_MOV_ROTSINU = 7,   /* <mvrotsinu>   ang = freq, ang2 = ampl, ang3 = phase (prev), axis */
+  SPH_MOV_CIR = 8,       /* <mvcir>       ang = vel, axis, ref                       */
+  SPH_MOV_CIRACE = 9,    /* <mvcirace>    ang = ace, ang2 = velini (prev), axis, ref */
+  SPH_MOV_CIRSINU = 10,  /* <mvcirsinu>   ang = freq, ang2 = ampl, ang3 = phase (prev), axis, ref */
+  SPH_MOV_RECTFILE = 11, /* <mvrectfile> (<mvfile>, <mvpredef>): positions of a table  */
+  SPH_MOV_ROTFILE = 12,  /* <mvrotfile>   angles (degrees) of a table, axis          */
+  SPH_MOV_NULL = 13      /* <mvnull>                                                 */
 };
 typedef struct SphMotionMov {
-  int32_t obj;       /* moving object = objreal ref = moving-block index             */
-  int32_t id;        /* movement id inside the object                               */
-  int32_t next;      /* id of the next movement of the object (0: none)             */
-  int32_t type;      /* SPH_MOV_*                                                   */
-  int32_t prev;      /* velprev / phaseprev: take the value of the previous movement */
-  int32_t pad;
-  double duration;   /* >= 0 (flash movements are not supported)                    */
+  int32_t obj;         /* motion object: its index in the nodes of sph_solver_set_motion_tree
+                          (sph_solver_set_motion: the objreal ref = moving-block index)    */
+  int32_t id;          /* movement id inside the object                                 */
+  int32_t next;        /* id of the next movement of the object (0: none)               */
+  int32_t type;        /* SPH_MOV_*                                                     */
+  int32_t prev;        /* velprev / phaseprev: take the value of the previous movement   */
+  int32_t fields;      /* RECTFILE: bit k set when coordinate k is in the file (fieldx/y/z >= 0) */
+  uint32_t data_first; /* RECTFILE / ROTFILE: its first row of the tree call's table rows */
+  uint32_t data_n;     /* ... and its rows (>= 2)                                        */
+  double duration;     /* < 0: a flash movement (applied whole at its start)            */
   double vec[3], vec2[3], phase[3];
-  double axisp1[3], axisp2[3];
+  double axisp1[3], axisp2[3], ref[3];
   double ang, ang2, ang3;
 } SphMotionMov;
 /* <begin mov start finish>: movement `mov` (id) of object `obj` starts at `start`
@@ -482,6 +493,21 @@ typedef struct SphMotionEvent {
  * every step (no host round trip), applied as JSphCpu::RunMotion (JSphCpu.cpp:1758-1789). */
 int sph_solver_set_motion(SphSolver* s, uint32_t nobj, uint32_t nmov, const SphMotionMov* movs, uint32_t nevt,
                           const SphMotionEvent* evts);
+/* A motion object of the program's tree (<obj> / <objreal> nested in each other,
+ * JMotion::ReadXml + ObjAdd, JMotion.cpp:96-114,556-565): listed depth first, a parent
+ * before its children and every subtree contiguous.  ref = the objreal ref (moving-block
+ * index; the refs are 0..n-1), -1 for a virtual <obj> (its motion moves its children). */
+typedef struct SphMotionObj {
+  int32_t parent;  /* index of the parent node, -1 at the top level */
+  int32_t ref;
+} SphMotionObj;
+/* The motion program as a tree of objects, with the tables of its file movements: rows of
+ * four doubles {time, x, y, z} (RECTFILE) or {time, angle in degrees, 0, 0} (ROTFILE), as
+ * JMotionDataFile loads them (JMotionMov.cpp:252-300).  sph_solver_set_motion is this call
+ * with one top-level node per ref and no tables. */
+int sph_solver_set_motion_tree(SphSolver* s, uint32_t nnode, const SphMotionObj* nodes, uint32_t nmov,
+                               const SphMotionMov* movs, uint32_t nevt, const SphMotionEvent* evts, uint32_t nrows,
+                               const double* rows);
 
 /* Floating body (JCasePartBlock_Floating, JCaseParts.cpp:248-290 -> StFloatingData,
  * JSph.cpp:1046-1100), RigidAlgorithm=1 (SPH forces). */

@@ -10,8 +10,10 @@ while [ $# -gt 0 ] && [ "$1" != "--" ]; do V+=("$1"); shift; done
 ARGS=${*:-"--steps 40 --warmup 5"}
 for i in $(seq 1 $N); do
   for v in "${V[@]}"; do
-    if [ "$v" = main ]; then lib=$R/dualsphysics_multilayer_amd/lib/libsphcore.so; else lib=$R/$v/libsphcore.so; fi
-    SPH_LIB=$lib timeout -k 10 200 python3 "$R/bench.py" $ARGS --no-cpu-baseline --no-cfg3 > /tmp/ab.json 2>/tmp/ab.err || { cat /tmp/ab.err; exit 1; }
+    # "main:VAR=value" = the in-tree library with a test-hook environment variable
+    envs=""; name=${v%%:*}; [ "$name" != "$v" ] && envs=${v#*:}
+    if [ "$name" = main ]; then lib=$R/dualsphysics_multilayer_amd/lib/libsphcore.so; else lib=$R/$name/libsphcore.so; fi
+    env $envs SPH_LIB=$lib timeout -k 10 200 python3 "$R/bench.py" $ARGS --no-cpu-baseline --no-cfg3 > /tmp/ab.json 2>/tmp/ab.err || { cat /tmp/ab.err; exit 1; }
     python3 -c "
 import json,sys
 d=json.loads([l for l in open('/tmp/ab.json') if l.startswith('{')][-1])

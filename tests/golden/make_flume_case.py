@@ -50,6 +50,13 @@ VARIANTS = {
     # JSphCpuSingle.cpp:525), with the floating normals
     "symplectic_ddt1_mdbc_corr": (0.025, 2, 1, 2, 60, (1, 10, 60),
                                   ("1.2", "0.3", "0.4", "0.2", "0.004", "2", "3", "1"), "mdbccorr"),
+    # other motion programs (JMotion.cpp:556-700, JMotionObj.cpp:368-580): the piston as the
+    # child of a virtual object (its own circular movements on top of its parent's sinusoid,
+    # its axes moved by the parent), the flap turning at constant speed then accelerating
+    "verlet_ddt2_motion_nested_cir": (0.025, 1, 2, 1, 60, (1, 10, 30, 60), (), "motion_nested_cir"),
+    "symplectic_ddt1_motion_nested_cir": (0.025, 2, 1, 1, 40, (1, 10, 40), (), "motion_nested_cir"),
+    # positions / angles from data files, a flash movement, mvnull, an event with a finish
+    "verlet_ddt2_motion_files_flash": (0.025, 1, 2, 1, 60, (1, 10, 30, 60), (), "motion_files_flash"),
 }
 
 # <floating> additions of the XML edits (JCasePartBlock_Floating::ReadXml, JCaseParts.cpp:270-285)
@@ -70,11 +77,42 @@ XML_EDITS = {
                   '</linearforce>'),
     # (anchor, text): the text goes before the anchor
     "mdbccorr": ("</parameters>", '<parameter key="MDBCCorrector" value="1"/>\n'),
+    # {"motion": text}: the case's whole <motion> program replaced
+    "motion_nested_cir": {"motion": """<motion>
+<obj><begin mov="1" start="0"/>
+<mvrectsinu id="1" duration="100"><freq x="2" y="0" z="0"/><ampl x="0.01" y="0" z="0"/><phase x="0" y="0" z="0"/></mvrectsinu>
+<objreal ref="0"><begin mov="1" start="0.002"/>
+<mvcir id="1" duration="0.004" next="2"><axisp1 x="0.05" y="0" z="0.2"/><axisp2 x="0.05" y="1" z="0.2"/><ref x="0.07" y="0" z="0.2"/><vel ang="1500"/></mvcir>
+<mvcirace id="2" duration="0.004" next="3"><axisp1 x="0.05" y="0" z="0.2"/><axisp2 x="0.05" y="1" z="0.2"/><ref x="0.07" y="0" z="0.2"/><ace ang="-20000"/></mvcirace>
+<mvcirsinu id="3" duration="100"><axisp1 x="0.05" y="0" z="0.2"/><axisp2 x="0.05" y="1" z="0.2"/><ref x="0.07" y="0" z="0.2"/><freq v="5"/><ampl v="8"/></mvcirsinu>
+</objreal>
+</obj>
+<objreal ref="1"><begin mov="1" start="0"/>
+<wait id="1" duration="0.003" next="2"/>
+<mvrot id="2" duration="0.005" next="3" anglesunits="radians"><axisp1 x="1.2" y="0" z="0"/><axisp2 x="1.2" y="1" z="0"/><vel ang="-0.8"/></mvrot>
+<mvrotace id="3" duration="100"><axisp1 x="1.2" y="0" z="0"/><axisp2 x="1.2" y="1" z="0"/><ace ang="500"/></mvrotace>
+</objreal>
+</motion>"""},
+    "motion_files_flash": {"motion": """<motion>
+<objreal ref="0"><begin mov="1" start="0"/>
+<mvrectfile id="1" duration="0.006" next="2"><file name="PistonPos.csv" fields="4" fieldtime="0" fieldx="1" fieldz="3"/></mvrectfile>
+<mvrect id="2" duration="-0.01" next="3"><vel x="0.2" y="0" z="0"/></mvrect>
+<mvrotfile id="3" duration="100" anglesunits="radians"><axisp1 x="0.05" y="0" z="0"/><axisp2 x="0.05" y="1" z="0"/><file name="PistonAng.csv"/></mvrotfile>
+</objreal>
+<objreal ref="1"><begin mov="1" start="0"/><begin mov="2" start="0.004" finish="0.012"/>
+<mvnull id="1"/>
+<mvfile id="2" duration="100"><file name="FlapPos.csv" fields="3" fieldtime="0" fieldx="1"/></mvfile>
+</objreal>
+</motion>"""},
 }
 # data files of the XML edits (written beside the case)
 DATA_FILES = {
     "ftvelfile": {"FtLinVel.csv": "# time;vx;vy;vz (m/s)\n0;0.05;none;none\n0.02;-0.1;none;0.05\n"
                                   "0.006;0.2;none;none\n0.025;0;none;none\n"},
+    "motion_files_flash": {
+        "PistonPos.csv": "# time;x;unused;z\n0;0;9;0\n0.002;0.001;9;0.0005\n0.004;0.0035;9;0.001\n0.01;0.004;9;0\n",
+        "PistonAng.csv": "# time ang(rad)\n0 0\n0.004 0.02\n0.02 -0.01\n",
+        "FlapPos.csv": "0,0,5\n0.003,-0.002,5\n0.006,-0.001,5\n0.01,-0.003,5\n"},
 }
 
 
@@ -104,9 +142,13 @@ def make(name, dp, step, ddt, boundary, nsteps, keep, extra=(), xml_edit=None):
             fx = os.path.join(tmp, "CaseFlume.xml")
             txt = open(fx).read()
             edit = XML_EDITS[xml_edit]
-            anchor, text = edit if isinstance(edit, tuple) else ("</floating>", edit)
-            assert txt.count(anchor) == 1
-            open(fx, "w").write(txt.replace(anchor, text + anchor))
+            if isinstance(edit, dict):  # the <motion> program replaced
+                i, j = txt.index("<motion>"), txt.index("</motion>") + len("</motion>")
+                open(fx, "w").write(txt[:i] + edit["motion"] + txt[j:])
+            else:
+                anchor, text = edit if isinstance(edit, tuple) else ("</floating>", edit)
+                assert txt.count(anchor) == 1
+                open(fx, "w").write(txt.replace(anchor, text + anchor))
         datafiles = DATA_FILES.get(xml_edit, {}) if xml_edit else {}
         for fn, text in datafiles.items():
             open(os.path.join(tmp, fn), "w").write(text)

@@ -96,7 +96,7 @@ def test_unsupported_body_features_refused(tmp_path):
         XmlCase(variant(lambda s: s.replace('key="RigidAlgorithm" value="1"', 'key="RigidAlgorithm" value="2"')))
     with pytest.raises(CaseError, match="file not found"):  # a table file the case does not have
         XmlCase(variant(lambda s: s.replace("</floating>", '<linearvel file="vel.csv"/></floating>')))
-    with pytest.raises(CaseError, match="mvcir"):
+    with pytest.raises(CaseError, match="not found 'axisp1'"):  # an mvcir needs its axis (tests/test_motion.py)
         XmlCase(variant(lambda s: s.replace("<wait ", "<mvcir ")))
     with pytest.raises(CaseError, match="mobile objects"):
         XmlCase(variant(lambda s: s.replace('<objreal ref="1">', '<objreal ref="3">')))
