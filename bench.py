@@ -196,6 +196,33 @@ def profiled_traffic(kernel_prefix, np_: int, workload: str):
     return found
 
 
+def profiled_valu_flop(kernel_prefix, np_: int, workload: str):
+    """EXECUTED FP32 flop per launch of the dominant kernel from the latest committed PMC
+    passes of the same workload (profiles/<round>/pmc/counters.json, per-dispatch averages):
+    64 lanes x (ADD + MUL + TRANS + 2 FMA) F32 wave-instructions, the
+    counter-based counterpart of the algorithmic flop model; None if there is none."""
+    import glob
+
+    found = None
+    for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*"))):
+        cj, bj = os.path.join(d, "pmc", "counters.json"), os.path.join(d, "bench.json")
+        if not (os.path.exists(cj) and os.path.exists(bj)):
+            continue
+        try:
+            b = json.load(open(bj))
+            if b["config"]["np"] != np_ or b["n_gpus"] != 1 or not b["config"]["workload"].startswith(workload):
+                continue
+            prefixes = (kernel_prefix,) if isinstance(kernel_prefix, str) else tuple(kernel_prefix)
+            for k, v in json.load(open(cj)).items():
+                if (k[5:] if k.startswith("void ") else k).startswith(prefixes):
+                    fl = 64.0 * (v["SQ_INSTS_VALU_ADD_F32"] + v["SQ_INSTS_VALU_MUL_F32"] + v["SQ_INSTS_VALU_TRANS_F32"]
+                                 + 2.0 * v["SQ_INSTS_VALU_FMA_F32"])
+                    found = {"flop": fl, "source": os.path.relpath(cj, ROOT) + " (%s)" % k}
+        except (KeyError, ValueError):
+            continue
+    return found
+
+
 CFG2_DP, CFG2_NP = 0.0045, 1025964
 CFG3_DP = 0.00205  # 9,969,118 particles (BASELINE cfg3: ~10M)
 CFG4_DP = 0.00265  # 4,007,978 particles (BASELINE cfg4: wave flume ~4M)
@@ -452,6 +479,7 @@ def main() -> None:
                   for td in ((case.tdensity | 8, case.tdensity) if case.tdensity >= 2 else (case.tdensity,))
                   for w4 in ("", "_w4")])  # _w4: the 4-wave register budget (DDT1)
         traffic = profiled_traffic(kname, case.np, "BASELINE " + args.workload) if world == 1 else None
+        vflop = profiled_valu_flop(kname, case.np, "BASELINE " + args.workload) if world == 1 else None
         res = {
             "metric": METRIC,
             "value": value,
@@ -515,6 +543,10 @@ def main() -> None:
                 "traffic_unit": "bytes per launch (HBM, PMC)",
                 "traffic_source": traffic["source"] if traffic else None,
                 "traffic_profiled_avg_ms": (traffic["avg_ns"] / 1e6) if traffic and traffic["avg_ns"] else None,
+                "frac_counters": (vflop["flop"] / (inter_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS)
+                                 if vflop and inter_ms > 0 else None,
+                "executed_flop_per_launch_pmc": vflop["flop"] if vflop else None,
+                "executed_flop_source": vflop["source"] if vflop else None,
                 "avg_launch_ms": inter_ms,
                 "launches": int(nlaunch),
                 "algorithmic_flop_per_launch": flops,

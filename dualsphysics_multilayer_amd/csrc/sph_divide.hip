@@ -538,6 +538,25 @@ __global__ __launch_bounds__(INC_BS) void k_inc_classify(DevScalars* __restrict_
   inc_classify_tile(sc, dcell, code, g, dcc, s, usey, usez, blockIdx.x);
 }
 
+// After an update that classified its particles (sph_incdiv.hpp), a slab's exchange appended
+// s.napp migrants at [nold, np): their keys (the input of their own sort) and class, and the
+// divide's particle count — the part of inc_classify_tile that concerns them.
+__global__ __launch_bounds__(256) void k_inc_classify_app(DevScalars* __restrict__ sc,
+                                                          const unsigned* __restrict__ dcell,
+                                                          const typecode* __restrict__ code, DivGrid g, unsigned dcc,
+                                                          IncDivScratch s) {
+  const unsigned n = sc->np, nold = n - s.napp;
+  if (blockIdx.x == 0 && threadIdx.x == 0) sc->ndiv = n;
+  const unsigned e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= s.napp) return;
+  const unsigned i = nold + e;
+  const unsigned key = box_key(dcell[i], code[i], g, dcc);
+  s.newkey[i] = key;
+  s.cw[i] = CW_APP;
+  s.akin[e] = key;
+  s.avin[e] = e;
+}
+
 // One block per IB_BOX consecutive boxes [c0, c0 + IB_BOX).
 // Mover prefixes: Ln(x) / Lf(x) = near / far movers before index x = the tile prefix
 // (super-tile sums + the tile counts of the super tile) + the tile-local prefix of x.
@@ -1137,10 +1156,14 @@ void launch_divide_inc(hipStream_t stm, unsigned cap, DevScalars* sc, const Part
   s.avin = srt.vals[0];
   s.nvl = faces ? ngl : 0u;
   s.nvr = faces ? ngr : 0u;
-  // (classified: the update kernel classified its own tiles, sph_incdiv.hpp)
+  // (classified: the update kernel classified its own tiles, sph_incdiv.hpp; the particles a
+  // slab's exchange appended since are classified here)
   if (!classified)
     hipLaunchKernelGGL(k_inc_classify, dim3(s.nb1), dim3(INC_BS), 0, stm, sc, src.dcell, src.code, g, K.domcellcode,
                        s, usey, usez);
+  else if (s.napp)
+    hipLaunchKernelGGL(k_inc_classify_app, dim3((s.napp + 255) / 256), dim3(256), 0, stm, sc, src.dcell, src.code, g,
+                       K.domcellcode, s);
   // slab: the reserved ghost slots are counted per face box (faces->pre: the received
   // counts' prefixes); k_inc_boxes reads their bounds from the prefixes, no keys needed
   if (faces) {

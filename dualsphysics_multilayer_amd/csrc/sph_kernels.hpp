@@ -393,13 +393,17 @@ void launch_fold_maxima(hipStream_t stm, DevScalars* sc, unsigned* folded, bool 
 // them DCELL_DISCARD for the next divide.
 // shiftpos (nullptr: no shifting): the interaction's shifting sums, turned into the
 // displacement of JSphShifting::RunCpu inside the update.
-// cls (not null): the incremental divide's classification rides on the update (sph_incdiv.hpp)
+// cls (not null): the incremental divide's classification rides on the update (sph_incdiv.hpp);
+// pk (not null, with cls): the slab exchange's count pass too (sph_slabpack.hpp)
+struct PackArgs;
 void launch_verlet(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, bool euler, const float4* arace,
-                   PartArrays a, DivGrid g, const float4* shiftpos = nullptr, const IncDivScratch* cls = nullptr);
+                   PartArrays a, DivGrid g, const float4* shiftpos = nullptr, const IncDivScratch* cls = nullptr,
+                   const PackArgs* pk = nullptr);
 void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
-                    DivGrid g, const IncDivScratch* cls = nullptr);
+                    DivGrid g, const IncDivScratch* cls = nullptr, const PackArgs* pk = nullptr);
 void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
-                    DivGrid g, const float4* shiftpos = nullptr, const IncDivScratch* cls = nullptr);
+                    DivGrid g, const float4* shiftpos = nullptr, const IncDivScratch* cls = nullptr,
+                    const PackArgs* pk = nullptr);
 
 // ---- moving boundaries and floating bodies (sph_bodies.hip) ----
 constexpr int MOT_MAXOBJ = 32, MOT_MAXACT = 4, MOT_MAXAXIS = 64;
@@ -542,6 +546,25 @@ struct SlabSendBufs {
   SlabRec* mr;
   unsigned long long gcap, mcap;  // records beyond the capacity are counted, not written
 };
+// The pack's arguments (sph_slab.hip; the count pass also in the slab update, sph_slabpack.hpp).
+struct PackArgs {
+  PartArrays a;
+  DivGrid g;
+  unsigned dcc;
+  double posminx, posminy, posminz, scelld;
+  int has_left, has_right, withm1, withpre;
+  unsigned* tilecnt;  // [4][ntiles]: ghost L, ghost R, migrant L, migrant R
+  unsigned ntiles;
+  SlabCounts* cnt;
+  SlabSendBufs b;
+  const float4* normal;  // mDBC normals by idp (nullptr without mDBC)
+  unsigned nbound;
+  unsigned* fcnt[2];     // ghost counts per face box (the exchange after the divide), or nullptr
+  int W;
+};
+PackArgs make_pack_args(unsigned cap, const PartArrays& a, DivGrid g, const KConst& K, const double dom_posmin[3],
+                        bool has_left, bool has_right, bool withm1, bool withpre, unsigned* tilecnt, SlabCounts* cnt,
+                        SlabSendBufs bufs, const float4* normal, unsigned nbound, const SlabFaces* faces);
 // Classify every particle after an update (stable order) and write the records for
 // the two neighbours: tile counts -> scan -> scatter, four streams (ghost/migrant x
 // left/right).  has_left/has_right: the neighbour exists.
@@ -550,7 +573,7 @@ struct SlabSendBufs {
 void launch_slab_pack(hipStream_t stm, unsigned cap, DevScalars* sc, const PartArrays& a, DivGrid g, const KConst& K,
                       const double dom_posmin[3], bool has_left, bool has_right, bool withm1, bool withpre,
                       unsigned* tilecnt, SlabCounts* cnt, SlabSendBufs bufs, const float4* normal = nullptr,
-                      unsigned nbound = 0, const SlabFaces* faces = nullptr);
+                      unsigned nbound = 0, const SlabFaces* faces = nullptr, bool counted = false);
 // ---- the ghost exchange after the divide (sph_slab.hip, sph_divide.hip) ----
 // Before the divide a slab sends each neighbour only the NUMBER of its ghosts per face box
 // (with the migrants); the receiver's divide reserves their slots (they follow the old

@@ -992,9 +992,11 @@ void SphGpuSingle::Exchange() {
   const bool hl = transport_->has_left(), hr = transport_->has_right();
   if (!hl && !hr) return;  // a slab alone holds the whole domain: no ghosts, no migrants
   SLAB_TRACE("exchange: pack");
+  // (the first pack's count pass may have run in the update kernel, FuseUpdate)
   auto pack = [&] {
     launch_slab_pack(stream, cap_, sc_, cur_, G, K, C.dom_posmin, hl, hr, withm1, withpre, packtiles_, slabcnt_,
-                     send_, normal_, nnormal_, &faces_);
+                     send_, normal_, nnormal_, &faces_, packcounted_);
+    packcounted_ = false;
   };
   // the pack rewrites the migrant and face-message send buffers: the neighbours' copies of
   // the last messages (in-process slabs copy asynchronously) are done first
@@ -1161,6 +1163,8 @@ void SphGpuSingle::WaitEvent(hipEvent_t ev, const char* what) {
 // (the usual pack rule) give the neighbours their ghost columns during the hand-over.
 // Called between an update and the divide (all ranks, same step).
 void SphGpuSingle::Repartition() {
+  // (FuseUpdate leaves the count pass to the exchange at a re-partitioning divide)
+  if (packcounted_) throw SphError(SPH_ERR_STATE, "internal: the update counted the pack of a re-partitioning divide");
   const int ncxg = int(C.dom_cells[slabcfg_.axis]), nr = slabcfg_.nranks;
   launch_column_counts(stream, cap_, sc_, cur_, G, K, ncxg, colcnt_);
   std::vector<float> bnd(size_t(nr) + 1, 0.f);
@@ -1515,16 +1519,32 @@ void SphGpuSingle::UpdateTurn(bool begin) {
   else transport_->turn_done(SlabTransport::TURN_UPDATE, stream);
 }
 
-// The divide's classification in the update kernel (sph_incdiv.hpp): the next divide is
-// incremental and nothing moves a particle between the update and the divide (one domain:
-// no exchange, no re-partition; no floating bodies, no moving boundaries).  SPH_CLS_SPLIT=1
-// (test hook) keeps the separate k_inc_classify launch.
-const IncDivScratch* SphGpuSingle::ClassifyInUpdate() {
+// The next divide's classification (sph_incdiv.hpp) and, on a slab with neighbours, its
+// exchange's count pass (sph_slabpack.hpp) in the update kernel: the next divide is
+// incremental and nothing moves a particle between the update and the divide (no floating
+// bodies, no moving boundaries; no re-partition at that divide, which changes the slab's
+// columns and hence every key).  pre_at_divide: whether the Symplectic pre-state is held at
+// the divide (the re-partition's condition).  SPH_CLS_SPLIT=1 (test hook) keeps the separate
+// k_inc_classify and k_pack_count launches.
+SphGpuSingle::UpdateFuse SphGpuSingle::FuseUpdate(bool pre_at_divide) {
   static const bool split = std::getenv("SPH_CLS_SPLIT") && std::atoi(std::getenv("SPH_CLS_SPLIT"));
-  const bool ok = !split && !slab() && inc_ok_ && inc_valid_ && G.ncx >= 3 && (G.ncy >= 3 || G.ncy == 1) &&
-                  !nftbodies_ && !nmotobj_ && inc_.napp == 0;
-  classified_ = ok;
-  return ok ? &inc_ : nullptr;
+  classified_ = packcounted_ = false;
+  UpdateFuse f;
+  const bool repart = slab() && exchange_armed_ && repart_every_ && (stepsdone_ % repart_every_) == 0 &&
+                      transport_->nranks > 1 && !pre_at_divide;
+  if (split || repart || !inc_ok_ || !inc_valid_ || !(G.ncx >= 3 && (G.ncy >= 3 || G.ncy == 1)) || nftbodies_ ||
+      nmotobj_ || inc_.napp != 0)
+    return f;
+  classified_ = true;
+  f.cls = &inc_;
+  const bool hl = slab() && transport_->has_left(), hr = slab() && transport_->has_right();
+  if (slab() && exchange_armed_ && (hl || hr)) {
+    pack_args_ = make_pack_args(cap_, cur_, G, K, C.dom_posmin, hl, hr, step_algorithm_ == SPH_STEP_VERLET,
+                                pre_at_divide, packtiles_, slabcnt_, send_, normal_, nnormal_, &faces_);
+    packcounted_ = true;
+    f.pk = &pack_args_;
+  }
+  return f;
 }
 
 void SphGpuSingle::ComputeVerlet() {
@@ -1532,7 +1552,8 @@ void SphGpuSingle::ComputeVerlet() {
   TimedBegin(1);
   verletstep_++;
   const bool euler = !(verletstep_ < C.verlet_steps);
-  launch_verlet(stream, cap_, sc_, K, euler, arace_, cur_, G, shift_ ? shiftpos_ : nullptr, ClassifyInUpdate());
+  const UpdateFuse fu = FuseUpdate(false);
+  launch_verlet(stream, cap_, sc_, K, euler, arace_, cur_, G, shift_ ? shiftpos_ : nullptr, fu.cls, fu.pk);
   if (euler) verletstep_ = 0;
   std::swap(cur_.velrhop, cur_.velrhopm1);
   TimedEnd(1);
@@ -1546,7 +1567,8 @@ void SphGpuSingle::ComputeSymplecticPre() {
   std::swap(cur_.posz, cur_.poszpre);
   std::swap(cur_.velrhop, cur_.velrhoppre);
   havepre_ = true;
-  launch_sym_pre(stream, cap_, sc_, K, arace_, cur_, G, ClassifyInUpdate());
+  const UpdateFuse fu = FuseUpdate(true);
+  launch_sym_pre(stream, cap_, sc_, K, arace_, cur_, G, fu.cls, fu.pk);
   TimedEnd(1);
   UpdateTurn(false);
 }
@@ -1554,7 +1576,8 @@ void SphGpuSingle::ComputeSymplecticPre() {
 void SphGpuSingle::ComputeSymplecticCorr() {
   UpdateTurn(true);
   TimedBegin(1);
-  launch_sym_cor(stream, cap_, sc_, K, arace_, cur_, G, shift_ ? shiftpos_ : nullptr, ClassifyInUpdate());
+  const UpdateFuse fu = FuseUpdate(false);
+  launch_sym_cor(stream, cap_, sc_, K, arace_, cur_, G, shift_ ? shiftpos_ : nullptr, fu.cls, fu.pk);
   havepre_ = false;
   TimedEnd(1);
   UpdateTurn(false);

@@ -237,7 +237,13 @@ class SphGpuSingle {
   MotEvt* motevts_ = nullptr;
   double* motdata_ = nullptr;  // rows of the file movements' tables (4 doubles each)
   bool classified_ = false;     // the last update classified the particles for the divide
-  const IncDivScratch* ClassifyInUpdate();
+  bool packcounted_ = false;    // ... and ran the slab exchange's count pass
+  PackArgs pack_args_;
+  struct UpdateFuse {
+    const IncDivScratch* cls = nullptr;
+    const PackArgs* pk = nullptr;
+  };
+  UpdateFuse FuseUpdate(bool pre_at_divide);
   unsigned nmotobj_ = 0;
   FtBody* ftbodies_ = nullptr;
   unsigned* ftridp_ = nullptr;   // floating particle (idp - CaseNpb) -> position, per divide

@@ -11,6 +11,7 @@
 
 #include "sph_kernels.hpp"
 #include "sph_incdiv.hpp"
+#include "sph_slabpack.hpp"
 
 namespace sphx {
 
@@ -294,14 +295,16 @@ __global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ 
 // The update with the incremental divide's classification of the same particles (sph_incdiv.hpp):
 // one block per classify tile updates its INC_TILE particles (INC_IPT per thread at stride
 // INC_BS, the classify mapping) and then classifies them from the dcell / code it has just
-// written (each thread reads back its own stores).  The single-domain step without bodies:
-// nothing moves a particle between the update and the divide.
+// written (each thread reads back its own stores).  A step without bodies: nothing moves a
+// particle between the update and the divide.  PACK (a slab with neighbours): also the
+// exchange's count pass over the same tile (sph_slabpack.hpp, PK_TILE = INC_TILE).
 enum { UPD_VERLET = 0, UPD_SYM_PRE = 1, UPD_SYM_COR = 2 };
-template <int KIND>
+static_assert(PK_TILE == INC_TILE && PK_BS == INC_BS, "the pack's tiles are the classify tiles");
+template <int KIND, bool PACK>
 __global__ __launch_bounds__(INC_BS) void k_update_cls(DevScalars* __restrict__ sc, KConst K, int euler,
                                                        const float4* __restrict__ arace, PartArrays a, DivGrid g,
                                                        const float4* __restrict__ shiftpos, IncDivScratch s, int usey,
-                                                       int usez) {
+                                                       int usez, PackArgs q) {
   const unsigned np = sc->np;
 #pragma unroll
   for (int k = 0; k < INC_IPT; k++) {
@@ -312,35 +315,45 @@ __global__ __launch_bounds__(INC_BS) void k_update_cls(DevScalars* __restrict__ 
     else sym_cor_part(sc, K, arace, a, g, shiftpos, p);
   }
   inc_classify_tile(sc, a.dcell, a.code, g, K.domcellcode, s, usey, usez, blockIdx.x);
+  if (PACK) pack_count_tile(sc, q, blockIdx.x);
+}
+template <int KIND>
+static void launch_update_cls(hipStream_t stm, DevScalars* sc, const KConst& K, int euler, const float4* arace,
+                              const PartArrays& a, const DivGrid& g, const float4* shiftpos, const IncDivScratch& s,
+                              const PackArgs* pk) {
+  const int usey = g.ncy > 1, usez = g.ncz > 1;
+  if (pk)
+    hipLaunchKernelGGL((k_update_cls<KIND, true>), dim3(s.nb1), dim3(INC_BS), 0, stm, sc, K, euler, arace, a, g,
+                       shiftpos, s, usey, usez, *pk);
+  else
+    hipLaunchKernelGGL((k_update_cls<KIND, false>), dim3(s.nb1), dim3(INC_BS), 0, stm, sc, K, euler, arace, a, g,
+                       shiftpos, s, usey, usez, PackArgs{});
 }
 
 // cls: the divide's scratch when the classification rides on the update (nullptr: the
 // per-particle kernel, the divide classifies).
 void launch_verlet(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, bool euler, const float4* arace,
-                   PartArrays a, DivGrid g, const float4* shiftpos, const IncDivScratch* cls) {
+                   PartArrays a, DivGrid g, const float4* shiftpos, const IncDivScratch* cls, const PackArgs* pk) {
   if (cls) {
-    hipLaunchKernelGGL(k_update_cls<UPD_VERLET>, dim3(cls->nb1), dim3(INC_BS), 0, stm, sc, K, int(euler), arace, a,
-                       g, shiftpos, *cls, int(g.ncy > 1), int(g.ncz > 1));
+    launch_update_cls<UPD_VERLET>(stm, sc, K, int(euler), arace, a, g, shiftpos, *cls, pk);
     return;
   }
   const unsigned nb = (cap + 255) / 256;
   hipLaunchKernelGGL(k_verlet, dim3(nb), dim3(256), 0, stm, sc, K, int(euler), arace, a, g, shiftpos);
 }
 void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
-                    DivGrid g, const IncDivScratch* cls) {
+                    DivGrid g, const IncDivScratch* cls, const PackArgs* pk) {
   if (cls) {
-    hipLaunchKernelGGL(k_update_cls<UPD_SYM_PRE>, dim3(cls->nb1), dim3(INC_BS), 0, stm, sc, K, 0, arace, a, g,
-                       static_cast<const float4*>(nullptr), *cls, int(g.ncy > 1), int(g.ncz > 1));
+    launch_update_cls<UPD_SYM_PRE>(stm, sc, K, 0, arace, a, g, nullptr, *cls, pk);
     return;
   }
   const unsigned nb = (cap + 255) / 256;
   hipLaunchKernelGGL(k_sym_pre, dim3(nb), dim3(256), 0, stm, sc, K, arace, a, g);
 }
 void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
-                    DivGrid g, const float4* shiftpos, const IncDivScratch* cls) {
+                    DivGrid g, const float4* shiftpos, const IncDivScratch* cls, const PackArgs* pk) {
   if (cls) {
-    hipLaunchKernelGGL(k_update_cls<UPD_SYM_COR>, dim3(cls->nb1), dim3(INC_BS), 0, stm, sc, K, 0, arace, a, g,
-                       shiftpos, *cls, int(g.ncy > 1), int(g.ncz > 1));
+    launch_update_cls<UPD_SYM_COR>(stm, sc, K, 0, arace, a, g, shiftpos, *cls, pk);
     return;
   }
   const unsigned nb = (cap + 255) / 256;
