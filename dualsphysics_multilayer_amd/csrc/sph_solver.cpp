@@ -1527,7 +1527,11 @@ void SphGpuSingle::UpdateTurn(bool begin) {
 // the divide (the re-partition's condition).  SPH_CLS_SPLIT=1 (test hook) keeps the separate
 // k_inc_classify and k_pack_count launches.
 SphGpuSingle::UpdateFuse SphGpuSingle::FuseUpdate(bool pre_at_divide) {
-  static const bool split = std::getenv("SPH_CLS_SPLIT") && std::atoi(std::getenv("SPH_CLS_SPLIT"));
+  static const bool split = [] {
+    const bool on = std::getenv("SPH_CLS_SPLIT") && std::atoi(std::getenv("SPH_CLS_SPLIT"));
+    if (on) test_hook_notice("SPH_CLS_SPLIT");
+    return on;
+  }();
   classified_ = packcounted_ = false;
   UpdateFuse f;
   const bool repart = slab() && exchange_armed_ && repart_every_ && (stepsdone_ % repart_every_) == 0 &&
