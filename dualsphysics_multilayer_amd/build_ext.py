@@ -104,10 +104,14 @@ def _build(force: bool, verbose: bool, defines: list) -> str:
                     raise RuntimeError("HIP compile failed: %s" % cmd[-3])
     out = lib_path()
     if jobs or not os.path.exists(out):
-        cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out] + objs + LDFLAGS
+        # linked beside and renamed into place: a reader (a running test, a copy of the tree)
+        # sees the old library or the new one, never a half-written file
+        tmp = out + ".tmp%d" % os.getpid()
+        cmd = [cc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs + LDFLAGS
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode:
             raise RuntimeError("link failed:\n" + r.stdout + r.stderr)
+        os.replace(tmp, out)
     return out
 
 

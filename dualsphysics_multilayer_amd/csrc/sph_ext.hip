@@ -58,11 +58,13 @@ struct ExtArgs {
 
 // mir (Symmetry): the records' images across the plane y = 0 (JSphCpu.cpp:684,709): y and
 // the y velocity negated; the item's frame starts at y = cy scell, so the image of a record
-// at frame y is at -(y) - 2 cy scell (mirc = cy).
+// at frame y is at -(y) - 2 cy scell (mirc = cy).  inl (Symmetry in a pass drained in the
+// reference's order): each record followed by its image, at dst + 2 i and dst + 2 i + 1 —
+// the reference visits an image right after its original (JSphCpu.cpp:793-796).
 __device__ __forceinline__ void ext_stage(const KConst& K, const ExtArgs& E, unsigned rs, unsigned n, unsigned dst,
                                           int xo, int dy, int dz, bool boundrow, bool withtau,
                                           float4* __restrict__ sA, float4* __restrict__ sB, float4* __restrict__ sC,
-                                          float4* __restrict__ sD, bool mir = false, int mirc = 0) {
+                                          float4* __restrict__ sD, bool mir = false, int mirc = 0, bool inl = false) {
   const float oy = float(dy) * K.scell, oz = float(dz) * K.scell, my = float(2 * mirc) * K.scell;
   for (unsigned i = threadIdx.x; i < n; i += TB) {
     const unsigned q = rs + i;
@@ -70,10 +72,11 @@ __device__ __forceinline__ void ext_stage(const KConst& K, const ExtArgs& E, uns
     const int cx2 = int(DcelCellx(K.domcellcode, __float_as_uint(pc.w)));
     const float x2 = pc.x + float(cx2 - xo) * K.scell;
     const float y2 = mir ? -(pc.y + oy) - my : pc.y + oy, z2 = pc.z + oz;
-    sA[dst + i] = make_float4(x2, y2, z2, x2 * x2 + y2 * y2 + z2 * z2);
+    const unsigned d = inl ? dst + 2 * i : dst + i;
+    sA[d] = make_float4(x2, y2, z2, x2 * x2 + y2 * y2 + z2 * z2);
     float4 vr = E.velrhop[q];
     if (mir) vr.y = -vr.y;
-    sB[dst + i] = vr;
+    sB[d] = vr;
     const typecode c = E.code[q];
     float m2 = boundrow ? K.massbound : K.massfluid;
     bool flag = false, withtau2 = withtau && !boundrow;
@@ -89,8 +92,15 @@ __device__ __forceinline__ void ext_stage(const KConst& K, const ExtArgs& E, uns
       ta = E.tau[2 * q];
       tb = E.tau[2 * q + 1];
     }
-    sC[dst + i] = make_float4(E.press[q], flag ? -m2 : m2, tb.x, tb.y);
-    if (withtau) sD[dst + i] = ta;
+    sC[d] = make_float4(E.press[q], flag ? -m2 : m2, tb.x, tb.y);
+    if (withtau) sD[d] = ta;
+    if (inl) {  // the image right after it
+      const float yi = -(pc.y + oy) - my;
+      sA[d + 1] = make_float4(x2, yi, z2, x2 * x2 + yi * yi + z2 * z2);
+      sB[d + 1] = make_float4(vr.x, -vr.y, vr.z, vr.w);
+      sC[d + 1] = sC[d];
+      if (withtau) sD[d + 1] = ta;
+    }
   }
 }
 
@@ -335,12 +345,14 @@ __device__ __forceinline__ void ext_pass(const KConst& K, const ExtArgs& E, cons
   // skipped.  The reference visits an image right after its original when the original is
   // within the support radius (JSphCpu.cpp:793-796); an image is never nearer than its
   // original for y >= 0, so the images within the radius are exactly those.  Their order
-  // matters only for a shifting cut-off, which then has already frozen the sums (the passes
-  // drained in the reference's order are NoBound's / NoFixed's bound rows: the first bound
-  // pair in reach freezes them before its image; moving boundaries under NoFixed with
-  // Symmetry are refused).
+  // matters only for a shifting cut-off: the passes drained in the reference's order
+  // (NoBound's / NoFixed's bound rows — under NoFixed a moving boundary's image counts until
+  // the first fixed pair) take each image right after its original (inline, its records
+  // staged as [record, image] pairs); the order-free passes take the images after the rows,
+  // in units of their own.
   const bool sym = K.symmetry && rc.cy < S;
-  const int nimg = sym ? S * (S + 1) : 0;  // image rows x (S mirrored z pairs + the z = 0 row)
+  const bool inl = sym && !mirrored;
+  const int nimg = (sym && !inl) ? S * (S + 1) : 0;  // image rows x (S mirrored z pairs + the z = 0 row)
   for (int u = 0; u < nunits + nimg; u++) {
     int dza = 0, dya = 0;
     bool paired = false, mir = false, selfrow = false;
@@ -378,15 +390,20 @@ __device__ __forceinline__ void ext_pass(const KConst& K, const ExtArgs& E, cons
     }
     const unsigned n0 = re[0] - rs[0], n1 = re[1] - rs[1];
     if (n0 + n1 == 0u) continue;  // block-uniform
-    if (n0 + n1 <= unsigned(TCAPX)) {
+    // inline images (an ordered pass's row of the first S y rows: one row, not paired): the
+    // row staged as [record, image] pairs, m = 2 staged records per particle
+    const bool rowinl = inl && rc.cy + dya < S;
+    const unsigned m = rowinl ? 2u : 1u;
+    if (m * n0 + n1 <= unsigned(TCAPX)) {
       __syncthreads();
-      if (n0) ext_stage(K, E, rs[0], n0, 0u, rc.xo, dya, dza, KIND == 1, WT, sA, sB, sC, sD, mir, rc.cy);
+      if (n0) ext_stage(K, E, rs[0], n0, 0u, rc.xo, dya, dza, KIND == 1, WT, sA, sB, sC, sD, mir, rc.cy, rowinl);
       if (n1) ext_stage(K, E, rs[1], n1, n0, rc.xo, mir ? dya : -dya, -dza, KIND == 1, WT, sA, sB, sC, sD, mir, rc.cy);
       __syncthreads();
-      const int wa0 = int(ls[0] - rs[0]), wa1 = rc.act && n0 ? int(le[0] - rs[0]) : wa0;
+      const int wa0 = int(m * (ls[0] - rs[0])), wa1 = rc.act && n0 ? int(m * (le[0] - rs[0])) : wa0;
       const int wb0 = int(n0 + ls[1] - rs[1]), wb1 = rc.act && n1 ? int(n0 + le[1] - rs[1]) : wb0;
       // the own image (the lane's p1 in its own row's images) is no neighbour
-      const int self = (selfrow && rc.act && rc.p1 >= rs[0] && rc.p1 < re[0]) ? int(rc.p1 - rs[0]) : -1;
+      const bool own = rc.act && rc.p1 >= rs[0] && rc.p1 < re[0];
+      const int self = (selfrow && own) ? int(rc.p1 - rs[0]) : ((rowinl && own) ? int(2 * (rc.p1 - rs[0]) + 1) : -1);
       for (int off = 0;; off += 128) {
         const int na = wa1 - wa0 - off, nb = wb1 - wb0 - off;
         if (na <= 0 && nb <= 0) break;
@@ -404,14 +421,15 @@ __device__ __forceinline__ void ext_pass(const KConst& K, const ExtArgs& E, cons
     } else {
       for (int k = 0; k < (paired ? 2 : 1); k++) {
         const int dz = k ? -dza : dza, dy = (k && !mir) ? -dya : dya;
-        for (unsigned seg = rs[k]; seg < re[k]; seg += TCAPX) {
-          const unsigned segn = min(unsigned(TCAPX), re[k] - seg);
+        for (unsigned seg = rs[k]; seg < re[k]; seg += unsigned(TCAPX) / m) {
+          const unsigned segn = min(unsigned(TCAPX) / m, re[k] - seg);
           __syncthreads();
-          ext_stage(K, E, seg, segn, 0u, rc.xo, dy, dz, KIND == 1, WT, sA, sB, sC, sD, mir, rc.cy);
+          ext_stage(K, E, seg, segn, 0u, rc.xo, dy, dz, KIND == 1, WT, sA, sB, sC, sD, mir, rc.cy, rowinl);
           __syncthreads();
-          const int w0 = int(max(ls[k], seg) - seg);
-          const int w1 = rc.act ? max(w0, int(min(le[k], seg + segn)) - int(seg)) : w0;
-          const int self = (selfrow && rc.act && rc.p1 >= seg && rc.p1 < seg + segn) ? int(rc.p1 - seg) : -1;
+          const int w0 = int(m * (max(ls[k], seg) - seg));
+          const int w1 = rc.act ? max(w0, int(m) * (int(min(le[k], seg + segn)) - int(seg))) : w0;
+          const bool own = rc.act && rc.p1 >= seg && rc.p1 < seg + segn;
+          const int self = (selfrow && own) ? int(rc.p1 - seg) : ((rowinl && own) ? int(2 * (rc.p1 - seg) + 1) : -1);
           for (int off = w0; off < w1; off += 128) {
             unsigned long long c0, c1;
             test128(sA, off, min(w1 - off, 128), px2, py2, pz2, thr, c0, c1);

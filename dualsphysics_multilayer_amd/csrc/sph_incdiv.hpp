@@ -34,50 +34,64 @@ __device__ __forceinline__ bool inc_near(int d, int ncx, int nsheet, bool usey, 
   return false;
 }
 
-// Tile b (INC_TILE particles, INC_IPT per thread at stride INC_BS; blocks of INC_BS threads,
-// every thread of the block calls it): new key, near/far flags and their tile-local prefixes,
-// the tile's counts (+ one atomic into its super tile of 64), near movers' keys at
-// tile-major slots, far movers appended to a list.
+// The tile's particle i = b INC_TILE + k INC_BS + t of a block of BS threads: BS = INC_BS
+// (k = 0..3 per thread, t = the thread) or BS = INC_TILE (one particle per thread: k and t
+// from the thread index) — the same order of waves (k, t / 64) either way.
+template <int BS>
+struct TileMap {
+  static_assert(BS == INC_BS || BS == INC_TILE, "tiles of 4 particles per thread or of one");
+  static constexpr int IPT = INC_TILE / BS;
+  __device__ __forceinline__ static int k(int e) { return BS == INC_BS ? e : int(threadIdx.x) / INC_BS; }
+  __device__ __forceinline__ static unsigned t() { return threadIdx.x % unsigned(INC_BS); }
+};
+
+// Tile b (INC_TILE particles; every thread of the block calls it): new key, near/far flags and
+// their tile-local prefixes, the tile's counts (+ one atomic into its super tile of 64), near
+// movers' keys at tile-major slots, far movers appended to a list.
+template <int BS = INC_BS>
 __device__ __forceinline__ void inc_classify_tile(DevScalars* __restrict__ sc, const unsigned* __restrict__ dcell,
                                                   const typecode* __restrict__ code, const DivGrid& g, unsigned dcc,
                                                   const IncDivScratch& s, int usey, int usez, unsigned b) {
+  using M = TileMap<BS>;
+  constexpr int IPT = M::IPT;
   __shared__ unsigned s_cn[INC_IPT * 4], s_cf[INC_IPT * 4];
   const unsigned n = sc->np;
   const unsigned nold = n - s.napp;  // the previous divide's particles; [nold, n) were appended
-  const unsigned lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned lane = threadIdx.x & 63, w = M::t() >> 6;
   if (b == 0 && threadIdx.x == 0) sc->ndiv = n;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  unsigned key[INC_IPT], rn[INC_IPT], rf[INC_IPT], fpos[INC_IPT];
-  bool nr[INC_IPT], fr[INC_IPT], dr[INC_IPT];
+  unsigned key[IPT], rn[IPT], rf[IPT], fpos[IPT];
+  bool nr[IPT], fr[IPT], dr[IPT];
   // every load of the tile first (one memory latency), then the classification
-  unsigned dc[INC_IPT], old[INC_IPT];
-  typecode cd[INC_IPT];
+  unsigned dc[IPT], old[IPT];
+  typecode cd[IPT];
 #pragma unroll
-  for (int k = 0; k < INC_IPT; k++) {
-    const unsigned i = b * INC_TILE + k * INC_BS + threadIdx.x;
+  for (int e = 0; e < IPT; e++) {
+    const unsigned i = b * INC_TILE + M::k(e) * INC_BS + M::t();
     const unsigned ii = i < n ? i : 0u;
-    dc[k] = dcell[ii];
-    cd[k] = code[ii];
-    old[k] = s.skeys[ii];
+    dc[e] = dcell[ii];
+    cd[e] = code[ii];
+    old[e] = s.skeys[ii];
   }
 #pragma unroll
-  for (int k = 0; k < INC_IPT; k++) {
-    const unsigned i = b * INC_TILE + k * INC_BS + threadIdx.x;
+  for (int e = 0; e < IPT; e++) {
+    const int k = M::k(e);
+    const unsigned i = b * INC_TILE + k * INC_BS + M::t();
     const bool valid = i < nold;
-    key[k] = box_key(dc[k], cd[k], g, dcc);
-    const int d = int(key[k] - old[k]);
-    dr[k] = valid && d != 0 && key[k] == g.boxdiscard;
-    nr[k] = valid && d != 0 && !dr[k] && inc_near(d, g.ncx, int(g.nsheet), usey != 0, usez != 0);
-    fr[k] = valid && d != 0 && !nr[k] && !dr[k];
-    const unsigned long long bn = __ballot(nr[k]), bf = __ballot(fr[k]), bfd = __ballot(fr[k] || dr[k]);
-    rn[k] = unsigned(__popcll(bn & lt));
-    rf[k] = unsigned(__popcll(bfd & lt));
-    fpos[k] = 0;
+    key[e] = box_key(dc[e], cd[e], g, dcc);
+    const int d = int(key[e] - old[e]);
+    dr[e] = valid && d != 0 && key[e] == g.boxdiscard;
+    nr[e] = valid && d != 0 && !dr[e] && inc_near(d, g.ncx, int(g.nsheet), usey != 0, usez != 0);
+    fr[e] = valid && d != 0 && !nr[e] && !dr[e];
+    const unsigned long long bn = __ballot(nr[e]), bf = __ballot(fr[e]), bfd = __ballot(fr[e] || dr[e]);
+    rn[e] = unsigned(__popcll(bn & lt));
+    rf[e] = unsigned(__popcll(bfd & lt));
+    fpos[e] = 0;
     if (bf) {  // far movers (rare): appended to the list, one atomic per wave
       const unsigned lead = unsigned(__ffsll(static_cast<long long>(bf))) - 1u;
       unsigned base = 0;
       if (lane == lead) base = atomicAdd(&s.ctr[0], unsigned(__popcll(bf)));
-      fpos[k] = __shfl(base, int(lead), 64) + unsigned(__popcll(bf & lt));
+      fpos[e] = __shfl(base, int(lead), 64) + unsigned(__popcll(bf & lt));
     }
     if (lane == 0) {
       s_cn[k * 4 + w] = unsigned(__popcll(bn));
@@ -86,27 +100,28 @@ __device__ __forceinline__ void inc_classify_tile(DevScalars* __restrict__ sc, c
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < INC_IPT; k++) {
-    const unsigned i = b * INC_TILE + k * INC_BS + threadIdx.x;
+  for (int e = 0; e < IPT; e++) {
+    const int k = M::k(e);
+    const unsigned i = b * INC_TILE + k * INC_BS + M::t();
     if (i >= n) continue;
     unsigned pn = 0, pf = 0;
     for (unsigned q = 0; q < unsigned(k * 4) + w; q++) {
       pn += s_cn[q];
       pf += s_cf[q];
     }
-    s.newkey[i] = key[k];
+    s.newkey[i] = key[e];
     if (i >= nold) {  // appended: the input of their own sort
       s.cw[i] = CW_APP;
-      s.akin[i - nold] = key[k];
+      s.akin[i - nold] = key[e];
       s.avin[i - nold] = i - nold;
       continue;
     }
-    const unsigned ln = pn + rn[k], lf = pf + rf[k];  // tile-local exclusive prefixes
-    s.cw[i] = ln | (lf << 11) | (nr[k] ? CW_NEAR : 0u) | (fr[k] ? CW_FAR : 0u) | (dr[k] ? CW_DROP : 0u);
-    if (nr[k]) s.mkey[b * INC_TILE + ln] = key[k];
-    if (fr[k]) {
-      s.mfar[fpos[k]] = make_uint2(i, key[k]);
-      s.fidx[i] = fpos[k];
+    const unsigned ln = pn + rn[e], lf = pf + rf[e];  // tile-local exclusive prefixes
+    s.cw[i] = ln | (lf << 11) | (nr[e] ? CW_NEAR : 0u) | (fr[e] ? CW_FAR : 0u) | (dr[e] ? CW_DROP : 0u);
+    if (nr[e]) s.mkey[b * INC_TILE + ln] = key[e];
+    if (fr[e]) {
+      s.mfar[fpos[e]] = make_uint2(i, key[e]);
+      s.fidx[i] = fpos[e];
     }
   }
   if (threadIdx.x == 0) {

@@ -41,16 +41,25 @@ __device__ __forceinline__ void streams(unsigned c, bool f[4]) {
   f[3] = (c & 2u) && !stay;  // migrant -> right
 }
 
+// The count pass of one tile (PK_TILE particles; BS = PK_BS threads with PK_ITEMS particles each
+// at stride PK_BS, or BS = PK_TILE threads with one particle each: the same particle order).
+template <int BS = PK_BS>
 __device__ __forceinline__ void pack_count_tile(const DevScalars* __restrict__ sc, const PackArgs& q, unsigned tile) {
-  __shared__ unsigned s[7][PK_BS / 64];
+  static_assert(BS == PK_BS || BS == PK_TILE, "tiles of PK_ITEMS particles per thread or of one");
+  constexpr int IPT = PK_TILE / BS;
+  __shared__ unsigned s[7][BS / 64];
   const unsigned n = sc->np;
   const unsigned base = tile * PK_TILE;
   unsigned c4[7] = {0, 0, 0, 0, 0, 0, 0};  // 4 streams, staying, ghosts per face (face boxes)
-  unsigned dcs[PK_ITEMS];
-  load_dcells(q, base, n, dcs);
+  unsigned dcs[IPT];
 #pragma unroll
-  for (int it = 0; it < PK_ITEMS; it++) {
-    const unsigned p = base + it * PK_BS + threadIdx.x;
+  for (int it = 0; it < IPT; it++) {
+    const unsigned p = base + it * BS + threadIdx.x;
+    dcs[it] = p < n ? q.a.dcell[p] : DCELL_DISCARD;
+  }
+#pragma unroll
+  for (int it = 0; it < IPT; it++) {
+    const unsigned p = base + it * BS + threadIdx.x;
     int fi[2] = {-1, -1};  // face box of an owned face particle, per face
     if (p < n) {
       const unsigned c = pack_class_dc(q, dcs[it]);
@@ -92,7 +101,7 @@ __device__ __forceinline__ void pack_count_tile(const DevScalars* __restrict__ s
   if (threadIdx.x < 7) {  // per tile; k_pack_scan sums them (no same-line atomics per block)
     const unsigned k = threadIdx.x;
     unsigned t = 0;
-    for (int i = 0; i < PK_BS / 64; i++) t += s[k][i];
+    for (int i = 0; i < BS / 64; i++) t += s[k][i];
     q.tilecnt[k * q.ntiles + tile] = t;
   }
 }

@@ -1643,11 +1643,6 @@ void SphGpuSingle::SetMotion(unsigned nobj, unsigned nmov, const SphMotionMov* m
 // it every step.
 void SphGpuSingle::SetMotionTree(unsigned nnode, const SphMotionObj* nodes, unsigned nmov, const SphMotionMov* movs,
                                  unsigned nevt, const SphMotionEvent* evts, unsigned nrows, const double* rows) {
-  // Symmetry + ShiftMode NoFixed: the images of a moving-boundary p2 would join the shifting
-  // sums before the first fixed p2 in the reference's order (JSphCpu.cpp:743-750, 793-796);
-  // this core visits the images after the rows (sph_ext.hip), exact only without them
-  if (C.symmetry && C.shift_mode == SPH_SHIFT_NOFIXED && nnode)
-    throw SphError(SPH_ERR_UNSUPPORTED, "Symmetry with ShiftMode NoFixed and moving boundaries is not implemented");
   if (stepped_ || motion_) throw SphError(SPH_ERR_STATE, "the motion is configured once, before the first step");
   if (!nnode || nnode > unsigned(MOT_MAXOBJ)) throw SphError(SPH_ERR_UNSUPPORTED, "number of motion objects out of range");
   if ((nmov && !movs) || (nevt && !evts) || (nrows && !rows)) throw SphError(SPH_ERR_ARG, "motion arrays missing");

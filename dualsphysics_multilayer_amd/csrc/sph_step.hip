@@ -293,29 +293,27 @@ __global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ 
 }
 
 // The update with the incremental divide's classification of the same particles (sph_incdiv.hpp):
-// one block per classify tile updates its INC_TILE particles (INC_IPT per thread at stride
-// INC_BS, the classify mapping) and then classifies them from the dcell / code it has just
-// written (each thread reads back its own stores).  A step without bodies: nothing moves a
+// one block of INC_TILE threads per classify tile updates its particles (one per thread, as
+// the per-particle kernels: 4 per thread left the dependent loads of each particle
+// unoverlapped, 45 vs 31 us at a 1.25M slab) and then classifies them from the dcell / code it
+// has just written (each thread reads back its own stores).  A step without bodies: nothing moves a
 // particle between the update and the divide.  PACK (a slab with neighbours): also the
 // exchange's count pass over the same tile (sph_slabpack.hpp, PK_TILE = INC_TILE).
 enum { UPD_VERLET = 0, UPD_SYM_PRE = 1, UPD_SYM_COR = 2 };
-static_assert(PK_TILE == INC_TILE && PK_BS == INC_BS, "the pack's tiles are the classify tiles");
+static_assert(PK_TILE == INC_TILE, "the pack's tiles are the classify tiles");
 template <int KIND, bool PACK>
-__global__ __launch_bounds__(INC_BS) void k_update_cls(DevScalars* __restrict__ sc, KConst K, int euler,
-                                                       const float4* __restrict__ arace, PartArrays a, DivGrid g,
-                                                       const float4* __restrict__ shiftpos, IncDivScratch s, int usey,
-                                                       int usez, PackArgs q) {
-  const unsigned np = sc->np;
-#pragma unroll
-  for (int k = 0; k < INC_IPT; k++) {
-    const unsigned p = blockIdx.x * INC_TILE + k * INC_BS + threadIdx.x;
-    if (p >= np) continue;
+__global__ __launch_bounds__(INC_TILE) void k_update_cls(DevScalars* __restrict__ sc, KConst K, int euler,
+                                                         const float4* __restrict__ arace, PartArrays a, DivGrid g,
+                                                         const float4* __restrict__ shiftpos, IncDivScratch s,
+                                                         int usey, int usez, PackArgs q) {
+  const unsigned p = blockIdx.x * INC_TILE + threadIdx.x;
+  if (p < sc->np) {
     if (KIND == UPD_VERLET) verlet_part(sc, K, euler, arace, a, g, shiftpos, p);
     else if (KIND == UPD_SYM_PRE) sym_pre_part(sc, K, arace, a, g, p);
     else sym_cor_part(sc, K, arace, a, g, shiftpos, p);
   }
-  inc_classify_tile(sc, a.dcell, a.code, g, K.domcellcode, s, usey, usez, blockIdx.x);
-  if (PACK) pack_count_tile(sc, q, blockIdx.x);
+  inc_classify_tile<INC_TILE>(sc, a.dcell, a.code, g, K.domcellcode, s, usey, usez, blockIdx.x);
+  if (PACK) pack_count_tile<PK_TILE>(sc, q, blockIdx.x);
 }
 template <int KIND>
 static void launch_update_cls(hipStream_t stm, DevScalars* sc, const KConst& K, int euler, const float4* arace,
@@ -323,10 +321,10 @@ static void launch_update_cls(hipStream_t stm, DevScalars* sc, const KConst& K, 
                               const PackArgs* pk) {
   const int usey = g.ncy > 1, usez = g.ncz > 1;
   if (pk)
-    hipLaunchKernelGGL((k_update_cls<KIND, true>), dim3(s.nb1), dim3(INC_BS), 0, stm, sc, K, euler, arace, a, g,
+    hipLaunchKernelGGL((k_update_cls<KIND, true>), dim3(s.nb1), dim3(INC_TILE), 0, stm, sc, K, euler, arace, a, g,
                        shiftpos, s, usey, usez, *pk);
   else
-    hipLaunchKernelGGL((k_update_cls<KIND, false>), dim3(s.nb1), dim3(INC_BS), 0, stm, sc, K, euler, arace, a, g,
+    hipLaunchKernelGGL((k_update_cls<KIND, false>), dim3(s.nb1), dim3(INC_TILE), 0, stm, sc, K, euler, arace, a, g,
                        shiftpos, s, usey, usez, PackArgs{});
 }
 

@@ -21,7 +21,9 @@
 // makes the reference apply mDBC to the floating body (UseNormalsFt, JSph.cpp:1301-1306).
 //
 // usage: genflume_ref <dp> <outdir> <step:1|2> <ddt:0..3> [timemax] [casename] [boundary:1|2]
-//                     [L W H depth] [flapwait flapfreq flapampl] [ftnormals:0|1]
+//                     [L W H depth] [flapwait flapfreq flapampl] [ftnormals:0|1] [nofloat:0|1]
+// nofloat=1: no floating box (the water fills its place), e.g. for Symmetry, which the
+// reference refuses with floating bodies.
 #include "JPartDataBi4.h"
 #include "JPartNormalData.h"
 #include "Functions.h"
@@ -50,6 +52,7 @@ int main(int argc, char** argv) {
   const std::string fwait = (argc > 12 ? argv[12] : "0.004"), ffreq = (argc > 13 ? argv[13] : "2"),
                     fampl = (argc > 14 ? argv[14] : "3");
   const bool ftnormals = (argc > 15 ? atoi(argv[15]) != 0 : false);
+  const bool nofloat = (argc > 16 ? atoi(argv[16]) != 0 : false);
 
   const int nx = int(std::round(L / dp)), ny = int(std::round(W / dp)), nz = int(std::round(H / dp));
   const int kd = int(std::round(D / dp));
@@ -59,7 +62,7 @@ int main(int argc, char** argv) {
   const int nbh = std::max(2, int(std::round(0.03 / dp)));
   const int bic = int(std::round(0.55 * L / dp)), bjc = ny / 2, bkc = kd - 1;
   auto inbox = [&](int i, int j, int k) {
-    return std::abs(i - bic) <= nbh && std::abs(j - bjc) <= nbh && std::abs(k - bkc) <= nbh;
+    return !nofloat && std::abs(i - bic) <= nbh && std::abs(j - bjc) <= nbh && std::abs(k - bkc) <= nbh;
   };
   const double hd = dp * 0.5;
   std::vector<tdouble3> pos, nor;
@@ -89,7 +92,7 @@ int main(int argc, char** argv) {
   const unsigned npb = unsigned(pos.size());
   // floating box
   tdouble3 bcen = TDouble3(0);
-  for (int k = bkc - nbh; k <= bkc + nbh; k++)
+  for (int k = bkc - nbh; k <= bkc + nbh && !nofloat; k++)
     for (int j = bjc - nbh; j <= bjc + nbh; j++)
       for (int i = bic - nbh; i <= bic + nbh; i++) {
         pos.push_back(TDouble3(i * dp, j * dp, k * dp));
@@ -103,7 +106,7 @@ int main(int argc, char** argv) {
         bcen = bcen + pos.back();
       }
   const unsigned nfloat = unsigned(pos.size()) - npb;
-  bcen = bcen / double(nfloat);
+  if (nfloat) bcen = bcen / double(nfloat);
   const unsigned nbound = unsigned(pos.size());
   // fluid
   for (int k = 1; k <= kd; k++)
@@ -174,10 +177,12 @@ int main(int argc, char** argv) {
   fprintf(f, "<fixed mkbound=\"0\" mk=\"10\" begin=\"0\" count=\"%u\"/>\n", nfixed);
   fprintf(f, "<moving mkbound=\"1\" mk=\"11\" begin=\"%u\" count=\"%u\" refmotion=\"0\"/>\n", nfixed, npiston);
   fprintf(f, "<moving mkbound=\"2\" mk=\"12\" begin=\"%u\" count=\"%u\" refmotion=\"1\"/>\n", nfixed + npiston, nflap);
-  fprintf(f, "<floating mkbound=\"3\" mk=\"13\" begin=\"%u\" count=\"%u\">\n", npb, nfloat);
-  fprintf(f, "<massbody value=\"%.17g\"/>\n<masspart value=\"%.17g\"/>\n", massbody, massp);
-  fprintf(f, "<center x=\"%.17g\" y=\"%.17g\" z=\"%.17g\"/>\n", bcen.x, bcen.y, bcen.z);
-  fprintf(f, "<inertia x=\"%.17g\" y=\"%.17g\" z=\"%.17g\"/>\n</floating>\n", ixx, iyy, izz);
+  if (nfloat) {
+    fprintf(f, "<floating mkbound=\"3\" mk=\"13\" begin=\"%u\" count=\"%u\">\n", npb, nfloat);
+    fprintf(f, "<massbody value=\"%.17g\"/>\n<masspart value=\"%.17g\"/>\n", massbody, massp);
+    fprintf(f, "<center x=\"%.17g\" y=\"%.17g\" z=\"%.17g\"/>\n", bcen.x, bcen.y, bcen.z);
+    fprintf(f, "<inertia x=\"%.17g\" y=\"%.17g\" z=\"%.17g\"/>\n</floating>\n", ixx, iyy, izz);
+  }
   fprintf(f, "<fluid mkfluid=\"0\" mk=\"0\" begin=\"%u\" count=\"%u\"/>\n</particles>\n", nbound, nf);
   fprintf(f, "<parameters>\n");
   auto par = [&](const char* k, const std::string& v) { fprintf(f, "<parameter key=\"%s\" value=\"%s\"/>\n", k, v.c_str()); };

@@ -37,4 +37,5 @@ timeout -k 10 400 python3 "$R/bench.py" $ARGS > "$OUT/bench.log" 2>&1
 grep '^{' "$OUT/bench.log" | tail -1 > "$DST/bench.json"
 mkdir -p "$R/gpurun_out/profiles/$TAG"
 cp -r "$DST"/* "$R/gpurun_out/profiles/$TAG/"
+rm -rf "$OUT/kt" "$OUT/fetch" "$OUT/write" "$OUT/pmc"  # the raw traces (summarised above) stay on the box
 echo collect-done

@@ -57,6 +57,14 @@ VARIANTS = {
     "symplectic_ddt1_motion_nested_cir": (0.025, 2, 1, 1, 40, (1, 10, 40), (), "motion_nested_cir"),
     # positions / angles from data files, a flash movement, mvnull, an event with a finish
     "verlet_ddt2_motion_files_flash": (0.025, 1, 2, 1, 60, (1, 10, 30, 60), (), "motion_files_flash"),
+    # Symmetry (y = 0 mirror) with ShiftMode NoFixed and moving boundaries (the piston and the
+    # flap; no floating box: genflume_ref nofloat=1, the reference refuses Symmetry with
+    # floating bodies): the images of a moving p2 join the shifting sums before the first
+    # fixed p2 in the reference's order (JSphCpu.cpp:743-750,793-796)
+    "verlet_ddt2_sym_nofixed": (0.025, 1, 2, 1, 60, (1, 10, 30, 60),
+                                ("1.2", "0.3", "0.4", "0.2", "0.004", "2", "3", "0", "1"), "sym_nofixed"),
+    "symplectic_ddt1_sym_nofixed": (0.025, 2, 1, 1, 40, (1, 10, 40),
+                                    ("1.2", "0.3", "0.4", "0.2", "0.004", "2", "3", "0", "1"), "sym_nofixed"),
 }
 
 # <floating> additions of the XML edits (JCasePartBlock_Floating::ReadXml, JCaseParts.cpp:270-285)
@@ -77,6 +85,10 @@ XML_EDITS = {
                   '</linearforce>'),
     # (anchor, text): the text goes before the anchor
     "mdbccorr": ("</parameters>", '<parameter key="MDBCCorrector" value="1"/>\n'),
+    # {"replace": [(old, new)]}: text replaced
+    "sym_nofixed": {"replace": [('<parameter key="Shifting" value="0"/>',
+                                 '<parameter key="Symmetry" value="1"/>\n<parameter key="Shifting" value="2"/>\n'
+                                 '<parameter key="ShiftCoef" value="-2"/>\n<parameter key="ShiftTFS" value="0"/>')]},
     # {"motion": text}: the case's whole <motion> program replaced
     "motion_nested_cir": {"motion": """<motion>
 <obj><begin mov="1" start="0"/>
@@ -142,7 +154,12 @@ def make(name, dp, step, ddt, boundary, nsteps, keep, extra=(), xml_edit=None):
             fx = os.path.join(tmp, "CaseFlume.xml")
             txt = open(fx).read()
             edit = XML_EDITS[xml_edit]
-            if isinstance(edit, dict):  # the <motion> program replaced
+            if isinstance(edit, dict) and "replace" in edit:
+                for old, new in edit["replace"]:
+                    assert txt.count(old) == 1
+                    txt = txt.replace(old, new)
+                open(fx, "w").write(txt)
+            elif isinstance(edit, dict):  # the <motion> program replaced
                 i, j = txt.index("<motion>"), txt.index("</motion>") + len("</motion>")
                 open(fx, "w").write(txt[:i] + edit["motion"] + txt[j:])
             else:
@@ -169,11 +186,12 @@ def make(name, dp, step, ddt, boundary, nsteps, keep, extra=(), xml_edit=None):
             if part in keep:
                 arrays.update({"s%d_idp" % part: idp, "s%d_pos" % part: pos, "s%d_vel" % part: vel,
                                "s%d_rhop" % part: rho, "s%d_time" % part: np.float64(t)})
-        subprocess.check_call([os.path.join(REF, "ftdump_ref"), out, os.path.join(tmp, "ft.bin")],
-                              stdout=subprocess.DEVNULL)
-        ft, fc, fv, fw = load_ft(os.path.join(tmp, "ft.bin"))
-        arrays.update(times=np.array(times), ft_time=ft, ft_center=fc, ft_fvel=fv, ft_fomega=fw,
-                      meta=np.array([dp, step, ddt, nsteps, boundary], np.float64))
+        if os.path.exists(os.path.join(out, "PartFloat.fbi4")):  # (no floating box: nofloat=1)
+            subprocess.check_call([os.path.join(REF, "ftdump_ref"), out, os.path.join(tmp, "ft.bin")],
+                                  stdout=subprocess.DEVNULL)
+            ft, fc, fv, fw = load_ft(os.path.join(tmp, "ft.bin"))
+            arrays.update(ft_time=ft, ft_center=fc, ft_fvel=fv, ft_fomega=fw)
+        arrays.update(times=np.array(times), meta=np.array([dp, step, ddt, nsteps, boundary], np.float64))
         np.savez_compressed(os.path.join(out_dir, "ref.npz"), **arrays)
         print(name, "ok", sorted(os.listdir(out_dir)))
     finally:

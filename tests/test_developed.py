@@ -1,0 +1,67 @@
+"""The developed flow (VERDICT r5 "shallow full-size pins"): the
+3-D dam break of the headline (cfg2 geometry and physics: Verlet, DDT2 0.1, artificial
+viscosity 0.1) run for 1.0 s — the surge crosses the tank, hits the far wall at ~0.45 s,
+runs up and rolls back, the regime the bench's `--developed-presteps` times — against the
+REFERENCE CPU solver's PARTs every 0.01 s (tests/golden/make_3d_developed.py, dp 0.015,
+36,936 particles, ~2,400 steps).  Two SPH runs drift apart particle by particle (float
+noise grows through the chaotic surge), so the pin is on bulk quantities of the fluid:
+the surge front, the centre of mass and the kinetic energy per unit mass at every output.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from golden.make_3d_developed import NAME, stats  # noqa: E402
+
+FIX = os.path.join(HERE, "golden", NAME + ".npz")
+
+
+def load():
+    g = np.load(FIX)
+    return g["times"], g["stats"], g["meta"]
+
+
+def test_reference_trace_is_the_developed_surge():
+    """The fixture holds what the test relies on: the front reaches the far wall (x = 1.6 m)
+    and the kinetic energy peaks and falls back as the surge runs up and rolls back."""
+    t, st, meta = load()
+    assert meta[3] == 1.0 and len(t) == 101 and abs(t[-1] - 1.0) < 0.011
+    front, ke = st[:, 0], st[:, 3]
+    assert front[0] < 0.41 and front.max() > 1.55
+    k = int(np.argmax(ke))
+    assert 0.4 < t[k] < 0.8 and ke[-1] < 0.6 * ke[k]
+    assert np.all(st[:, 4] == st[0, 4])  # no fluid particle leaves the domain
+
+
+@pytest.mark.gpu
+def test_gpu_developed_flow_matches_reference_bulk():
+    """Measured on MI355X (the tolerances are ~3x that): front <=, centre of
+    mass and kinetic energy likewise at every 0.01-s output over 1.0 s."""
+    from golden_io import by_idp
+
+    from dualsphysics_multilayer_amd.case import DamBreakCase
+    from dualsphysics_multilayer_amd.core import SphGpuSingle
+
+    t, st, meta = load()
+    dp = float(meta[0])
+    case = DamBreakCase(dp)
+    s = SphGpuSingle(case, device=0)
+    dev = []
+    for tk, ref in zip(t[1:], st[1:]):
+        while s.stats()["time"] < tk - 1e-12:
+            s.run(1)
+        p = by_idp(s.particles())
+        got = stats(p["idp"], p["pos"], p["vel"], case.npb)
+        dev.append(np.abs(got - ref) / np.array([1.0, 1.0, 1.0, max(ref[3], 1e-3), 1.0]))
+    s.close()
+    dev = np.array(dev)
+    worst = dev.max(axis=0)
+    print("worst front %.4f m, com x %.4f m, com z %.4f m, ke rel %.4f, count %d" % tuple(worst))
+    assert worst[4] == 0
+    assert worst[0] <= dp, worst
+    assert worst[1] <= 0.25 * dp and worst[2] <= 0.25 * dp, worst
+    assert worst[3] <= 0.05, worst

@@ -190,3 +190,57 @@ def test_case_xml_symmetry(tmp_path):
     ref = DamBreakCase(0.04, symmetry=True)
     assert np.array_equal(np.sort(x.pos, axis=0), np.sort(ref.pos, axis=0))
     assert cd["map_realposmin"] == ref.case_def()["map_realposmin"]
+
+
+# Symmetry with ShiftMode NoFixed and moving boundaries (the flume's piston and flap, no
+# floating box: tests/golden/make_flume_case.py *_sym_nofixed): under NoFixed only a FIXED
+# boundary pair freezes the shifting sums, so a moving boundary's image — visited right after
+# its original (JSphCpu.cpp:743-750, 793-796) — counts if it comes before the first fixed
+# pair: the ordered bound pass stages each row of the first S y rows as [record, image] pairs
+# (sph_ext.hip).  Tolerances: the flume's (tests/test_bodies.py).
+FLUME_SYM = ("verlet_ddt2_sym_nofixed", "symplectic_ddt1_sym_nofixed")
+
+
+def _flume_tol(step):
+    if step <= 1:
+        return 1.4e-8, 2.2e-5, 1e-2
+    if step <= 20:
+        return 2e-7, 6e-5, 1e-2
+    return 2e-6, 2.1e-4, 2e-2
+
+
+@pytest.mark.parametrize("name", FLUME_SYM)
+def test_flume_symmetry_nofixed_case_loaded(name):
+    import os
+
+    from dualsphysics_multilayer_amd.xmlcase import XmlCase
+
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "bi4", "flume_" + name)
+    x = XmlCase(os.path.join(d, "CaseFlume"))
+    assert x.symmetry and x.shift_mode == 2 and x.case_nmoving == 2 * 176 and x.case_nfloat == 0
+    assert x.motion["nobj"] == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", FLUME_SYM)
+def test_gpu_symmetry_nofixed_moving_boundaries_match_reference(name):
+    import os
+
+    from dualsphysics_multilayer_amd.core import SphGpuSingle
+    from dualsphysics_multilayer_amd.xmlcase import XmlCase
+
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "bi4", "flume_" + name)
+    x = XmlCase(os.path.join(d, "CaseFlume"))
+    g = np.load(os.path.join(d, "ref.npz"))
+    kept = sorted(int(k[1:].split("_")[0]) for k in g.files if k.startswith("s") and k.endswith("_idp"))
+    s = SphGpuSingle(x, device=0)
+    done = 0
+    for k in kept:
+        s.run(k - done)
+        done = k
+        ref = {q: g["s%d_%s" % (k, q)] for q in ("idp", "pos", "vel", "rhop")}
+        got = by_idp(s.particles())
+        assert np.array_equal(got["idp"], ref["idp"])
+        for q, t in zip(("pos", "vel", "rhop"), _flume_tol(k)):
+            assert maxdiff(got, ref, q) <= t, (k, q, maxdiff(got, ref, q))
+    s.close()
