@@ -110,9 +110,12 @@ LocalHub::LocalHub(int nslabs) : slots(size_t(nslabs)), n(nslabs) {
 }
 
 LocalHub::~LocalHub() {
-  for (Slot& sl : slots)
-    for (hipEvent_t e : {sl.ready, sl.copied, sl.idone[0], sl.idone[1], sl.idone[2], sl.idone[3]})
+  for (Slot& sl : slots) {
+    for (hipEvent_t e : {sl.ready, sl.copied, sl.idone[0], sl.idone[1], sl.idone[2], sl.idone[3], sl.arev[0], sl.arev[1]})
       if (e) (void)hipEventDestroy(e);
+    for (void* b : sl.arbuf)
+      if (b) (void)hipFree(b);
+  }
 }
 
 void LocalHub::throw_aborted() { throw SphError(SPH_ERR_COMM, "slab group aborted by another slab"); }
@@ -256,6 +259,11 @@ class LocalTransport final : public SlabTransport {
   }
   void allreduce_max_u32(unsigned* d, int n, hipStream_t s) override {
     if (n > 8) throw SphError(SPH_ERR_ARG, "allreduce: at most 8 values");
+    if (device_reduce()) {
+      const RankPtrs p = gather_device(d, 4 * size_t(n), s);
+      launch_rank_max_u32(s, p, n, nranks, d);
+      return;
+    }
     unsigned v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     check_hip(hipMemcpyAsync(v, d, 4 * size_t(n), hipMemcpyDeviceToHost, s), "allreduce: read");
     check_hip(hipStreamSynchronize(s), "allreduce: read");
@@ -269,6 +277,11 @@ class LocalTransport final : public SlabTransport {
   }
   // Summed in rank order (deterministic).
   void allreduce_sum_f32(float* d, int n, hipStream_t s) override {
+    if (device_reduce()) {
+      const RankPtrs p = gather_device(d, 4 * size_t(n), s);
+      launch_rank_ordered_sum(s, p, n, nranks, d);
+      return;
+    }
     std::vector<float>& mine = hub_->slots[size_t(rank)].fvals;
     mine.resize(size_t(n));
     check_hip(hipMemcpyAsync(mine.data(), d, 4 * size_t(n), hipMemcpyDeviceToHost, s), "allreduce: read");
@@ -291,7 +304,8 @@ class LocalTransport final : public SlabTransport {
     check_hip(hipStreamGetDevice(s, &dev), "hipStreamGetDevice");
     check_hip(hipGetDevice(&cur), "hipGetDevice");
     check_hip(hipSetDevice(dev), "hipSetDevice");
-    for (hipEvent_t* e : {&me.ready, &me.copied, &me.idone[0], &me.idone[1], &me.idone[2], &me.idone[3]})
+    for (hipEvent_t* e : {&me.ready, &me.copied, &me.idone[0], &me.idone[1], &me.idone[2], &me.idone[3], &me.arev[0],
+                          &me.arev[1]})
       check_hip(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
     check_hip(hipSetDevice(cur), "hipSetDevice");
   }
@@ -310,8 +324,45 @@ class LocalTransport final : public SlabTransport {
   bool active(int kind) const {
     return hub_->turns == 2 || (hub_->turns == 1 && (kind == TURN_INTERACTION || kind == TURN_DIVIDE));
   }
+  bool device_reduce() const { return hub_->onedev && nranks <= RankPtrs::MAXR; }
+  // A reduction's inputs on the device, as RCCL's all-reduce keeps them: this slab's `bytes`
+  // of d are copied into its buffer of the generation's parity and the event recorded; after
+  // the host barrier (every slab's buffer and event of the generation published) stream s
+  // waits for the other slabs' events and gets their buffers to fold.  Two parities: a slab
+  // writes parity k again (generation g + 2) only after its stream has waited for every
+  // slab's copy of generation g + 1, which each slab's stream issued after its fold of g; and
+  // it records arev[k] again only after the barrier of g + 1, which every slab reaches after
+  // issuing its waits on arev[k] of g.  A larger reduction (the same sizes on every slab, as
+  // the calls are collective) first drains every slab's stream, then reallocates.
+  RankPtrs gather_device(const void* d, size_t bytes, hipStream_t s) {
+    events(s);
+    LocalHub::Slot& me = hub_->slots[size_t(rank)];
+    const int par = int(argen_ & 1ull);
+    argen_++;
+    if (bytes > me.arcap) {
+      check_hip(hipStreamSynchronize(s), "allreduce: grow");
+      hub_->barrier();  // no slab reads the old buffers any more
+      for (void*& b : me.arbuf) {
+        if (b) check_hip(hipFree(b), "hipFree");
+        b = nullptr;
+      }
+      const size_t cap = std::max<size_t>(256, bytes + bytes / 2);
+      for (void*& b : me.arbuf) check_hip(hipMalloc(&b, cap), "hipMalloc allreduce buffer");
+      me.arcap = cap;
+    }
+    check_hip(hipMemcpyAsync(me.arbuf[par], d, bytes, hipMemcpyDeviceToDevice, s), "allreduce: stage");
+    check_hip(hipEventRecord(me.arev[par], s), "allreduce: event");
+    hub_->barrier();
+    RankPtrs p{};
+    for (int q = 0; q < nranks; q++) {
+      const LocalHub::Slot& o = hub_->slots[size_t(q)];
+      p.p[q] = o.arbuf[par];
+      if (q != rank) check_hip(hipStreamWaitEvent(s, o.arev[par], 0), "allreduce: wait");
+    }
+    return p;
+  }
   std::shared_ptr<LocalHub> hub_;
-  unsigned long long gen_ = 0, turn_[4] = {0, 0, 0, 0};
+  unsigned long long gen_ = 0, turn_[4] = {0, 0, 0, 0}, argen_ = 0;
 };
 
 std::unique_ptr<SlabTransport> make_local_transport(std::shared_ptr<LocalHub> hub, int rank) {

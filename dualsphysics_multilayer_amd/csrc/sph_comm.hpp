@@ -132,10 +132,18 @@ class LocalHub {
     hipEvent_t idone[4] = {nullptr, nullptr, nullptr, nullptr};
     unsigned vals[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     std::vector<float> fvals;
+    // device reductions (slabs of one GPU): this slab's values of generation parity k in
+    // arbuf[k] (arcap bytes each), complete at arev[k]
+    void* arbuf[2] = {nullptr, nullptr};
+    size_t arcap = 0;
+    hipEvent_t arev[2] = {nullptr, nullptr};
   };
   std::vector<Slot> slots;
   int n;
   int turns = 0;  // SPH_SLAB_TURNS: 1 interactions and divides, 2 every kernel of the step
+  // every slab on one GPU (SphSlabGroup): the reductions stay on the device (each stream waits
+  // for the other slabs' values and folds them), as RCCL's all-reduce does; else host-staged
+  bool onedev = false;
   // the kind whose chain ends before a chain of `kind` starts (the step's cycle of kinds)
   int turn_prev(int kind) const {
     if (turns == 1) return kind == TURN_KIND_I ? TURN_KIND_D : TURN_KIND_I;

@@ -45,13 +45,23 @@ struct TileMap {
   __device__ __forceinline__ static unsigned t() { return threadIdx.x % unsigned(INC_BS); }
 };
 
+// A particle's classification inputs held in registers by the update kernel that has just
+// written them (one particle per thread): its new dcell and code, its previous divide's key.
+struct ClsVals {
+  unsigned dc;
+  typecode cd;
+  unsigned old;
+};
+
 // Tile b (INC_TILE particles; every thread of the block calls it): new key, near/far flags and
 // their tile-local prefixes, the tile's counts (+ one atomic into its super tile of 64), near
-// movers' keys at tile-major slots, far movers appended to a list.
+// movers' keys at tile-major slots, far movers appended to a list.  vals (BS = INC_TILE only):
+// the thread's particle's inputs, instead of loads of dcell / code / skeys.
 template <int BS = INC_BS>
 __device__ __forceinline__ void inc_classify_tile(DevScalars* __restrict__ sc, const unsigned* __restrict__ dcell,
                                                   const typecode* __restrict__ code, const DivGrid& g, unsigned dcc,
-                                                  const IncDivScratch& s, int usey, int usez, unsigned b) {
+                                                  const IncDivScratch& s, int usey, int usez, unsigned b,
+                                                  const ClsVals* vals = nullptr) {
   using M = TileMap<BS>;
   constexpr int IPT = M::IPT;
   __shared__ unsigned s_cn[INC_IPT * 4], s_cf[INC_IPT * 4];
@@ -67,6 +77,12 @@ __device__ __forceinline__ void inc_classify_tile(DevScalars* __restrict__ sc, c
   typecode cd[IPT];
 #pragma unroll
   for (int e = 0; e < IPT; e++) {
+    if (vals) {
+      dc[e] = vals->dc;
+      cd[e] = vals->cd;
+      old[e] = vals->old;
+      continue;
+    }
     const unsigned i = b * INC_TILE + M::k(e) * INC_BS + M::t();
     const unsigned ii = i < n ? i : 0u;
     dc[e] = dcell[ii];

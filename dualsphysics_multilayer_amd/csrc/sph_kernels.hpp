@@ -26,8 +26,11 @@ struct PartArrays {
 };
 
 // JSphCpu::UpdatePos (JSphCpu.cpp:1240-1293), single domain, no periodic.
-__device__ __forceinline__ void update_pos(const KConst& K, double rx, double ry, double rz, double movx, double movy,
-                                           double movz, bool outrhop, unsigned p, const PartArrays& a) {
+// Returns the new dcell; rcode (optional): the particle's code held in registers, updated in
+// place (else read from a.code when the particle leaves).
+__device__ __forceinline__ unsigned update_pos(const KConst& K, double rx, double ry, double rz, double movx,
+                                               double movy, double movz, bool outrhop, unsigned p, const PartArrays& a,
+                                               typecode* rcode_in = nullptr) {
   const bool outmove = (fabsf(float(movx)) > K.movlimit || fabsf(float(movy)) > K.movlimit ||
                         fabsf(float(movz)) > K.movlimit);
   rx += movx;
@@ -40,16 +43,19 @@ __device__ __forceinline__ void update_pos(const KConst& K, double rx, double ry
   a.posxy[p] = make_double2(rx, ry);
   a.posz[p] = rz;
   if (outrhop || outmove || out) {
-    typecode rcode = a.code[p];
+    typecode rcode = rcode_in ? *rcode_in : a.code[p];
     if (out) rcode = CodeSetNormal(rcode) | CODE_OUTPOS;
     else if (outrhop) rcode = CodeSetNormal(rcode) | CODE_OUTRHOP;
     else rcode = CodeSetNormal(rcode) | CODE_OUTMOVE;
     a.code[p] = rcode;
+    if (rcode_in) *rcode_in = rcode;
     a.dcell[p] = DCELL_OUT;
-  } else {
-    const unsigned cx = unsigned(dx / K.scelld), cy = unsigned(dy / K.scelld), cz = unsigned(dz / K.scelld);
-    a.dcell[p] = DcelCell(K.domcellcode, cx, cy, cz);
+    return DCELL_OUT;
   }
+  const unsigned cx = unsigned(dx / K.scelld), cy = unsigned(dy / K.scelld), cz = unsigned(dz / K.scelld);
+  const unsigned dc = DcelCell(K.domcellcode, cx, cy, cz);
+  a.dcell[p] = dc;
+  return dc;
 }
 // Boundary and floating particles: UpdatePos with outrhop=false (MoveLinBound/MoveMatBound,
 // JSphCpu.cpp:1699,1721; RunFloating, JSphCpuSingle.cpp:969).
@@ -609,6 +615,14 @@ void launch_ghost_scatter(hipStream_t stm, DevScalars* sc, const SlabGhost* rec,
                           float* press, DivGrid g, unsigned* skeys, const float4* phase_eos = nullptr);
 // out[i] = (((0 + g[0][i]) + g[1][i]) + ...) over nranks rows of n floats (rank order).
 void launch_rank_ordered_sum(hipStream_t stm, const float* gathered, int n, int nranks, float* out);
+// The same over the ranks' own buffers (in-process slabs of one GPU, LocalTransport), and the
+// max of n uint32 values over them.
+struct RankPtrs {
+  static constexpr int MAXR = 16;
+  const void* p[MAXR];
+};
+void launch_rank_ordered_sum(hipStream_t stm, const RankPtrs& rp, int n, int nranks, float* out);
+void launch_rank_max_u32(hipStream_t stm, const RankPtrs& rp, int n, int nranks, unsigned* out);
 // Owned particles per GLOBAL x-column: counts[c] fluid (incl. floating), counts[ncxg + c]
 // boundary (the re-partition's weights), as floats (exact integers).
 void launch_column_counts(hipStream_t stm, unsigned cap, const DevScalars* sc, const PartArrays& a, DivGrid g,

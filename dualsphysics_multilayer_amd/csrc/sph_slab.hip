@@ -517,6 +517,31 @@ void launch_rank_ordered_sum(hipStream_t stm, const float* gathered, int n, int 
   if (n > 0) hipLaunchKernelGGL(k_rank_ordered_sum, dim3((n + 255) / 256), dim3(256), 0, stm, gathered, n, nranks, out);
 }
 
+__global__ void k_rank_ordered_sum_p(RankPtrs rp, int n, int nranks, float* __restrict__ out) {
+  const int i = int(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= n) return;
+  float v = 0.f;
+  for (int r = 0; r < nranks; r++) v = __fadd_rn(v, static_cast<const float*>(rp.p[r])[i]);
+  out[i] = v;
+}
+
+void launch_rank_ordered_sum(hipStream_t stm, const RankPtrs& rp, int n, int nranks, float* out) {
+  if (n > 0) hipLaunchKernelGGL(k_rank_ordered_sum_p, dim3((n + 255) / 256), dim3(256), 0, stm, rp, n, nranks, out);
+}
+
+__global__ void k_rank_max_u32(RankPtrs rp, int n, int nranks, unsigned* __restrict__ out) {
+  const int i = int(threadIdx.x);
+  if (i >= n) return;
+  unsigned v = 0u;
+  for (int r = 0; r < nranks; r++) v = max(v, static_cast<const unsigned*>(rp.p[r])[i]);
+  out[i] = v;
+}
+
+// (nranks <= RankPtrs::MAXR and n <= 64: LocalTransport's device_reduce and its 8-value limit)
+void launch_rank_max_u32(hipStream_t stm, const RankPtrs& rp, int n, int nranks, unsigned* out) {
+  if (n > 0) hipLaunchKernelGGL(k_rank_max_u32, dim3(1), dim3(64), 0, stm, rp, n, nranks, out);
+}
+
 // Owned particles per global column (u32 atomics in LDS-free global memory: integer counts
 // are order independent, so every run and every rank sees the same numbers).
 __global__ __launch_bounds__(256) void k_column_counts(const DevScalars* __restrict__ sc, PartArrays a, DivGrid g,

@@ -2133,6 +2133,8 @@ SphSlabGroup::SphSlabGroup(const SphCaseDef& cdef, const SphParticlesHost& all, 
   for (int i = 0; i < nslabs; i++)
     for (int j = 0; j < nslabs; j++)
       if (i != j && devices[i] == devices[j]) slabs[i]->MarkSharedDevice();
+  // one GPU: the dt maxima and the floating / re-partition sums reduce on the device
+  hub_->onedev = std::all_of(devices, devices + nslabs, [&](int d) { return d == devices[0]; });
 }
 
 void SphSlabGroup::Run(unsigned nsteps) {

@@ -130,93 +130,146 @@ void launch_dt(hipStream_t stm, DevScalars* sc, const KConst& K, double cfl, dou
 
 // Slab ghost: its local column is outside the owned range.  The owner updates it; here
 // it is only dropped at the next divide (fresh copies arrive with the exchange).
-__device__ __forceinline__ bool slab_ghost(const KConst& K, const DivGrid& g, unsigned* dcell, unsigned p) {
-  if (!g.split()) return false;  // single domain
-  if (slab_owned(g, slab_local(g, K.domcellcode, dcell[p]))) return false;
-  dcell[p] = DCELL_DISCARD;
-  return true;
+__device__ __forceinline__ bool slab_ghost(const KConst& K, const DivGrid& g, unsigned dc) {
+  return g.split() && !slab_owned(g, slab_local(g, K.domcellcode, dc));
+}
+
+enum { UPD_VERLET = 0, UPD_SYM_PRE = 1, UPD_SYM_COR = 2 };
+
+// One particle's update inputs, all loaded before any of its stores: one memory latency per
+// particle instead of a chain of them (the stores to the particle arrays would otherwise keep
+// each later load behind the branch that needs it).  Per kind:
+//   Verlet: v1 = velrhop, v2 = velrhop (Euler) or velrhopm1, pos = posxy / posz (fluid)
+//   SymPre: v1 = velrhoppre, pos = posxypre / poszpre (every particle: copied when halted)
+//   SymCor: v1 = velrhop, v2 = velrhoppre, pos = posxypre / poszpre (fluid, floating)
+struct UpdIn {
+  float4 ra, v1, v2, sh;
+  double2 pxy;
+  double pz;
+  unsigned dcell;
+  typecode code;
+};
+// The particle's dcell and code after its update: the next divide's classification inputs.
+struct UpdOut {
+  unsigned dcell;
+  typecode code;
+};
+
+template <int KIND>
+__device__ __forceinline__ UpdIn upd_load(int euler, const float4* __restrict__ arace, const PartArrays& a,
+                                          const float4* __restrict__ shiftpos, unsigned p, unsigned npb) {
+  UpdIn in;
+  in.dcell = a.dcell[p];
+  in.code = a.code[p];
+  in.ra = arace[p];
+  if (KIND == UPD_SYM_PRE) {
+    in.v1 = a.velrhoppre[p];
+    in.v2 = in.v1;
+  } else {
+    in.v1 = a.velrhop[p];
+    // (velrhopm1 read on Euler steps too: a select between it and v1 as pointers put `in` in
+    // scratch memory)
+    in.v2 = (KIND == UPD_SYM_COR ? a.velrhoppre[p] : a.velrhopm1[p]);
+    if (KIND == UPD_VERLET && euler) in.v2 = in.v1;
+  }
+  in.pxy = make_double2(0., 0.);
+  in.pz = 0.;
+  in.sh = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (KIND == UPD_SYM_PRE || p >= npb) {
+    in.pxy = (KIND == UPD_VERLET ? a.posxy : a.posxypre)[p];
+    in.pz = (KIND == UPD_VERLET ? a.posz : a.poszpre)[p];
+  }
+  if (KIND != UPD_SYM_PRE && shiftpos && p >= npb) in.sh = shiftpos[p];
+  // every load issued here, before the first store: without this use the compiler sinks the
+  // loads only one branch needs (code, position, shifting) into it, behind the stores before it
+  asm volatile("" ::"v"(unsigned(in.code)), "v"(in.pxy.x), "v"(in.pxy.y), "v"(in.pz), "v"(in.sh.x));
+  return in;
 }
 
 // ComputeVerlet (JSphCpu.cpp:1381-1399): bound -> ComputeVelrhopBound, fluid -> ComputeVerletVarsFluid.
 // New values are written in velrhopm1 (the caller swaps velrhop/velrhopm1 afterwards).
-__device__ __forceinline__ void verlet_part(const DevScalars* __restrict__ sc, const KConst& K, int euler,
-                                            const float4* __restrict__ arace, const PartArrays& a, const DivGrid& g,
-                                            const float4* __restrict__ shiftpos, unsigned p) {
-  const unsigned npb = sc->npb;
-  if (halted(sc)) {  // keep the state: the caller's velrhop/velrhopm1 swap then restores it
-    a.velrhopm1[p] = a.velrhop[p];
-    // a slab still drops its ghosts: the next exchange sends fresh copies (without this the
-    // stale ones piled up, a duplicate set per halted step)
-    slab_ghost(K, g, a.dcell, p);
-    return;
+__device__ __forceinline__ UpdOut verlet_part(const DevScalars* __restrict__ sc, const KConst& K, int euler,
+                                              const PartArrays& a, const DivGrid& g, bool shift, unsigned p,
+                                              unsigned npb, const UpdIn& in) {
+  UpdOut o{in.dcell, in.code};
+  const bool ghost = slab_ghost(K, g, in.dcell);
+  if (ghost) {
+    a.dcell[p] = DCELL_DISCARD;
+    o.dcell = DCELL_DISCARD;
   }
-  if (slab_ghost(K, g, a.dcell, p)) return;
+  if (halted(sc)) {  // keep the state: the caller's velrhop/velrhopm1 swap then restores it
+    a.velrhopm1[p] = in.v1;
+    // a slab still drops its ghosts (above): the next exchange sends fresh copies (without
+    // this the stale ones piled up, a duplicate set per halted step)
+    return o;
+  }
+  if (ghost) return o;
   const double dt = sc->dt;
   const double dt2 = (euler ? dt : dt + dt);
-  const float4 ra = arace[p];
-  const float4 vr2 = (euler ? a.velrhop[p] : a.velrhopm1[p]);
+  const float4 ra = in.ra;
+  const float4 vr2 = in.v2;
   const float rhopnew = float(double(vr2.w) + dt2 * double(ra.w));
   if (p < npb) {
     a.velrhopm1[p] = make_float4(0.f, 0.f, 0.f, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
-    return;
+    return o;
   }
-  const float4 vr1 = a.velrhop[p];
-  if (CodeType(a.code[p]) == CODE_TYPE_FLOATING) {  // JSphCpu.cpp:1352-1355: RunFloating moves it
+  const float4 vr1 = in.v1;
+  if (CodeType(in.code) == CODE_TYPE_FLOATING) {  // JSphCpu.cpp:1352-1355: RunFloating moves it
     a.velrhopm1[p] = make_float4(vr1.x, vr1.y, vr1.z, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
-    return;
+    return o;
   }
   const double dt205 = 0.5 * dt * dt;
   const double agx = double(ra.x) + K.gravxd, agy = double(ra.y) + K.gravyd, agz = double(ra.z) + K.gravzd;
   double dx = double(vr1.x) * dt + agx * dt205;
   double dy = double(vr1.y) * dt + agy * dt205;
   double dz = double(vr1.z) * dt + agz * dt205;
-  if (shiftpos) shift_displacement(K, shiftpos[p], vr1, dt, dx, dy, dz);  // RunShifting(dt) before ComputeVerlet
+  if (shift) shift_displacement(K, in.sh, vr1, dt, dx, dy, dz);  // RunShifting(dt) before ComputeVerlet
   const bool outrhop = (rhopnew < K.rhopoutmin || rhopnew > K.rhopoutmax);
   const float4 nv = make_float4(float(double(vr2.x) + agx * dt2), float(double(vr2.y) + agy * dt2),
                                 float(double(vr2.z) + agz * dt2), rhopnew);
-  const double2 pxy = a.posxy[p];
-  update_pos(K, pxy.x, pxy.y, a.posz[p], dx, dy, dz, outrhop, p, a);
+  typecode rcode = in.code;
+  o.dcell = update_pos(K, in.pxy.x, in.pxy.y, in.pz, dx, dy, dz, outrhop, p, a, &rcode);
+  o.code = rcode;
   a.velrhopm1[p] = nv;
-}
-__global__ __launch_bounds__(256) void k_verlet(const DevScalars* __restrict__ sc, KConst K, int euler,
-                                                const float4* __restrict__ arace, PartArrays a, DivGrid g,
-                                                const float4* __restrict__ shiftpos) {
-  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < sc->np) verlet_part(sc, K, euler, arace, a, g, shiftpos, p);
+  return o;
 }
 
 // ComputeSymplecticPre (JSphCpu.cpp:1406-1504).  The caller has already moved the
 // current pos/velrhop into the *pre arrays (pointer swap); new values go to pos/velrhop.
-__device__ __forceinline__ void sym_pre_part(const DevScalars* __restrict__ sc, const KConst& K,
-                                             const float4* __restrict__ arace, const PartArrays& a, const DivGrid& g,
-                                             unsigned p) {
-  const unsigned npb = sc->npb;
-  if (halted(sc)) {  // keep the state (the caller moved it into the pre arrays)
-    a.velrhop[p] = a.velrhoppre[p];
-    a.posxy[p] = a.posxypre[p];
-    a.posz[p] = a.poszpre[p];
-    slab_ghost(K, g, a.dcell, p);  // ghosts are dropped all the same (k_verlet)
-    return;
+__device__ __forceinline__ UpdOut sym_pre_part(const DevScalars* __restrict__ sc, const KConst& K,
+                                               const PartArrays& a, const DivGrid& g, unsigned p, unsigned npb,
+                                               const UpdIn& in) {
+  UpdOut o{in.dcell, in.code};
+  const bool ghost = slab_ghost(K, g, in.dcell);
+  if (ghost) {  // ghosts are dropped all the same, halted or not (verlet_part)
+    a.dcell[p] = DCELL_DISCARD;
+    o.dcell = DCELL_DISCARD;
   }
-  if (slab_ghost(K, g, a.dcell, p)) return;
+  const double2 pxy = in.pxy;
+  const double pz = in.pz;
+  if (halted(sc)) {  // keep the state (the caller moved it into the pre arrays)
+    a.velrhop[p] = in.v1;
+    a.posxy[p] = pxy;
+    a.posz[p] = pz;
+    return o;
+  }
+  if (ghost) return o;
   const double dt = sc->dt, dt05 = dt * .5;
-  const float4 ra = arace[p];
-  const float4 vp = a.velrhoppre[p];
+  const float4 ra = in.ra;
+  const float4 vp = in.v1;
   const float rhopnew = float(double(vp.w) + dt05 * double(ra.w));
-  const double2 pxy = a.posxypre[p];
-  const double pz = a.poszpre[p];
   if (p < npb) {
     a.velrhop[p] = make_float4(vp.x, vp.y, vp.z, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
     a.posxy[p] = pxy;
     a.posz[p] = pz;
-    return;
+    return o;
   }
-  typecode rcode = a.code[p];
+  typecode rcode = in.code;
   if (CodeType(rcode) == CODE_TYPE_FLOATING) {  // JSphCpu.cpp:1475-1478 (+ position copied, :1498)
     a.velrhop[p] = make_float4(vp.x, vp.y, vp.z, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
     a.posxy[p] = pxy;
     a.posz[p] = pz;
-    return;
+    return o;
   }
   const double dx = double(vp.x) * dt05, dy = double(vp.y) * dt05, dz = double(vp.z) * dt05;
   const bool outrhop = (rhopnew < K.rhopoutmin || rhopnew > K.rhopoutmax);
@@ -227,40 +280,43 @@ __device__ __forceinline__ void sym_pre_part(const DevScalars* __restrict__ sc, 
     rcode = CodeSetNormal(rcode) | CODE_OUTRHOP;
     a.code[p] = rcode;
   }
-  if (CodeIsFluid(rcode)) update_pos(K, pxy.x, pxy.y, pz, dx, dy, dz, CodeIsOutRhop(rcode), p, a);
-  else {
+  if (CodeIsFluid(rcode)) {
+    o.dcell = update_pos(K, pxy.x, pxy.y, pz, dx, dy, dz, CodeIsOutRhop(rcode), p, a, &rcode);
+  } else {
     a.posxy[p] = pxy;
     a.posz[p] = pz;
   }
-}
-__global__ __launch_bounds__(256) void k_sym_pre(const DevScalars* __restrict__ sc, KConst K,
-                                                 const float4* __restrict__ arace, PartArrays a, DivGrid g) {
-  const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < sc->np) sym_pre_part(sc, K, arace, a, g, p);
+  o.code = rcode;
+  return o;
 }
 
 // ComputeSymplecticCorr (JSphCpu.cpp:1510-1606).
-__device__ __forceinline__ void sym_cor_part(const DevScalars* __restrict__ sc, const KConst& K,
-                                             const float4* __restrict__ arace, const PartArrays& a, const DivGrid& g,
-                                             const float4* __restrict__ shiftpos, unsigned p) {
-  const unsigned npb = sc->npb;
-  if (slab_ghost(K, g, a.dcell, p) || halted(sc)) return;  // ghosts dropped even when halted
+__device__ __forceinline__ UpdOut sym_cor_part(const DevScalars* __restrict__ sc, const KConst& K,
+                                               const PartArrays& a, const DivGrid& g, bool shift, unsigned p,
+                                               unsigned npb, const UpdIn& in) {
+  UpdOut o{in.dcell, in.code};
+  if (slab_ghost(K, g, in.dcell)) {  // ghosts dropped even when halted
+    a.dcell[p] = DCELL_DISCARD;
+    o.dcell = DCELL_DISCARD;
+    return o;
+  }
+  if (halted(sc)) return o;
   const double dt = sc->dt, dt05 = dt * .5;
-  const float4 ra = arace[p];
-  const float4 vr = a.velrhop[p];
-  const float4 vp = a.velrhoppre[p];
+  const float4 ra = in.ra;
+  const float4 vr = in.v1;
+  const float4 vp = in.v2;
   const double epsilon_rdot = (-double(ra.w) / double(vr.w)) * dt;
   const float rhopnew = float(double(vp.w) * (2. - epsilon_rdot) / (2. + epsilon_rdot));
   if (p < npb) {
     a.velrhop[p] = make_float4(0.f, 0.f, 0.f, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
-    return;  // boundary keeps its position (already restored by the predictor)
+    return o;  // boundary keeps its position (already restored by the predictor)
   }
-  typecode rcode = a.code[p];
+  typecode rcode = in.code;
   if (CodeType(rcode) == CODE_TYPE_FLOATING) {  // JSphCpu.cpp:1577-1580, 1595
     a.velrhop[p] = make_float4(vp.x, vp.y, vp.z, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
-    a.posxy[p] = a.posxypre[p];
-    a.posz[p] = a.poszpre[p];
-    return;
+    a.posxy[p] = in.pxy;
+    a.posz[p] = in.pz;
+    return o;
   }
   const float4 nv = make_float4(float(double(vp.x) + (double(ra.x) + K.gravxd) * dt),
                                 float(double(vp.y) + (double(ra.y) + K.gravyd) * dt),
@@ -270,36 +326,49 @@ __device__ __forceinline__ void sym_cor_part(const DevScalars* __restrict__ sc, 
   double dz = (double(vp.z) + double(nv.z)) * dt05;
   // RunShifting(dt) after the corrector's interaction, with the predicted velocity
   // (JSphCpuSingle.cpp:764 of the v5.0 solver, JSphShifting.cpp:388-418)
-  if (shiftpos) shift_displacement(K, shiftpos[p], vr, dt, dx, dy, dz);
+  if (shift) shift_displacement(K, in.sh, vr, dt, dx, dy, dz);
   const bool outrhop = (rhopnew < K.rhopoutmin || rhopnew > K.rhopoutmax);
   if (outrhop && CodeIsNormal(rcode)) {
     rcode = CodeSetNormal(rcode) | CODE_OUTRHOP;
     a.code[p] = rcode;
   }
   a.velrhop[p] = nv;
-  const double2 pxy = a.posxypre[p];
-  const double pz = a.poszpre[p];
-  if (CodeIsFluid(rcode)) update_pos(K, pxy.x, pxy.y, pz, dx, dy, dz, CodeIsOutRhop(rcode), p, a);
-  else {
-    a.posxy[p] = pxy;
-    a.posz[p] = pz;
+  if (CodeIsFluid(rcode)) {
+    o.dcell = update_pos(K, in.pxy.x, in.pxy.y, in.pz, dx, dy, dz, CodeIsOutRhop(rcode), p, a, &rcode);
+  } else {
+    a.posxy[p] = in.pxy;
+    a.posz[p] = in.pz;
   }
+  o.code = rcode;
+  return o;
 }
-__global__ __launch_bounds__(256) void k_sym_cor(const DevScalars* __restrict__ sc, KConst K,
-                                                 const float4* __restrict__ arace, PartArrays a, DivGrid g,
-                                                 const float4* __restrict__ shiftpos) {
+
+// One particle's update of kind KIND (loads first, then the kind's arithmetic and stores).
+template <int KIND>
+__device__ __forceinline__ UpdOut upd_part(const DevScalars* __restrict__ sc, const KConst& K, int euler,
+                                           const float4* __restrict__ arace, const PartArrays& a, const DivGrid& g,
+                                           const float4* __restrict__ shiftpos, unsigned p, unsigned npb) {
+  const UpdIn in = upd_load<KIND>(euler, arace, a, shiftpos, p, npb);
+  if (KIND == UPD_VERLET) return verlet_part(sc, K, euler, a, g, shiftpos != nullptr, p, npb, in);
+  if (KIND == UPD_SYM_PRE) return sym_pre_part(sc, K, a, g, p, npb, in);
+  return sym_cor_part(sc, K, a, g, shiftpos != nullptr, p, npb, in);
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void k_update(const DevScalars* __restrict__ sc, KConst K, int euler,
+                                                const float4* __restrict__ arace, PartArrays a, DivGrid g,
+                                                const float4* __restrict__ shiftpos) {
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < sc->np) sym_cor_part(sc, K, arace, a, g, shiftpos, p);
+  if (p < sc->np) upd_part<KIND>(sc, K, euler, arace, a, g, shiftpos, p, sc->npb);
 }
 
 // The update with the incremental divide's classification of the same particles (sph_incdiv.hpp):
-// one block of INC_TILE threads per classify tile updates its particles (one per thread, as
-// the per-particle kernels: 4 per thread left the dependent loads of each particle
-// unoverlapped, 45 vs 31 us at a 1.25M slab) and then classifies them from the dcell / code it
-// has just written (each thread reads back its own stores).  A step without bodies: nothing moves a
-// particle between the update and the divide.  PACK (a slab with neighbours): also the
+// one block of INC_TILE threads per classify tile updates its particles (one per thread, the
+// per-particle kernels' mapping) and classifies them from the dcell and code it has just
+// computed, in registers (with the previous key, loaded with the update's inputs): the block
+// waits for one memory latency, not for a chain of reloads.  A step without bodies: nothing
+// moves a particle between the update and the divide.  PACK (a slab with neighbours): also the
 // exchange's count pass over the same tile (sph_slabpack.hpp, PK_TILE = INC_TILE).
-enum { UPD_VERLET = 0, UPD_SYM_PRE = 1, UPD_SYM_COR = 2 };
 static_assert(PK_TILE == INC_TILE, "the pack's tiles are the classify tiles");
 template <int KIND, bool PACK>
 __global__ __launch_bounds__(INC_TILE) void k_update_cls(DevScalars* __restrict__ sc, KConst K, int euler,
@@ -307,13 +376,15 @@ __global__ __launch_bounds__(INC_TILE) void k_update_cls(DevScalars* __restrict_
                                                          const float4* __restrict__ shiftpos, IncDivScratch s,
                                                          int usey, int usez, PackArgs q) {
   const unsigned p = blockIdx.x * INC_TILE + threadIdx.x;
+  ClsVals v{DCELL_DISCARD, 0, 0u};
   if (p < sc->np) {
-    if (KIND == UPD_VERLET) verlet_part(sc, K, euler, arace, a, g, shiftpos, p);
-    else if (KIND == UPD_SYM_PRE) sym_pre_part(sc, K, arace, a, g, p);
-    else sym_cor_part(sc, K, arace, a, g, shiftpos, p);
+    v.old = s.skeys[p];
+    const UpdOut o = upd_part<KIND>(sc, K, euler, arace, a, g, shiftpos, p, sc->npb);
+    v.dc = o.dcell;
+    v.cd = o.code;
   }
-  inc_classify_tile<INC_TILE>(sc, a.dcell, a.code, g, K.domcellcode, s, usey, usez, blockIdx.x);
-  if (PACK) pack_count_tile<PK_TILE>(sc, q, blockIdx.x);
+  inc_classify_tile<INC_TILE>(sc, a.dcell, a.code, g, K.domcellcode, s, usey, usez, blockIdx.x, &v);
+  if (PACK) pack_count_tile<PK_TILE>(sc, q, blockIdx.x, true, v.dc, v.cd);
 }
 template <int KIND>
 static void launch_update_cls(hipStream_t stm, DevScalars* sc, const KConst& K, int euler, const float4* arace,
@@ -337,7 +408,7 @@ void launch_verlet(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& 
     return;
   }
   const unsigned nb = (cap + 255) / 256;
-  hipLaunchKernelGGL(k_verlet, dim3(nb), dim3(256), 0, stm, sc, K, int(euler), arace, a, g, shiftpos);
+  hipLaunchKernelGGL(k_update<UPD_VERLET>, dim3(nb), dim3(256), 0, stm, sc, K, int(euler), arace, a, g, shiftpos);
 }
 void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
                     DivGrid g, const IncDivScratch* cls, const PackArgs* pk) {
@@ -346,7 +417,7 @@ void launch_sym_pre(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst&
     return;
   }
   const unsigned nb = (cap + 255) / 256;
-  hipLaunchKernelGGL(k_sym_pre, dim3(nb), dim3(256), 0, stm, sc, K, arace, a, g);
+  hipLaunchKernelGGL(k_update<UPD_SYM_PRE>, dim3(nb), dim3(256), 0, stm, sc, K, 0, arace, a, g, nullptr);
 }
 void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst& K, const float4* arace, PartArrays a,
                     DivGrid g, const float4* shiftpos, const IncDivScratch* cls, const PackArgs* pk) {
@@ -355,7 +426,7 @@ void launch_sym_cor(hipStream_t stm, unsigned cap, DevScalars* sc, const KConst&
     return;
   }
   const unsigned nb = (cap + 255) / 256;
-  hipLaunchKernelGGL(k_sym_cor, dim3(nb), dim3(256), 0, stm, sc, K, arace, a, g, shiftpos);
+  hipLaunchKernelGGL(k_update<UPD_SYM_COR>, dim3(nb), dim3(256), 0, stm, sc, K, 0, arace, a, g, shiftpos);
 }
 
 }  // namespace sphx

@@ -1,12 +1,25 @@
 #!/bin/bash
-# Round 6 profile sets (2): cfg3 and cfg4 — kernel stats, traffic, bench line with CPU baseline.
+# Round 6: where the fused update's time goes — kernel stats of cfg2 with the fused update and
+# with the separate launches (SPH_CLS_SPLIT=1), and the cfg3 8 y-slab turns trace with the
+# separate launches.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p "$R/gpurun_out/r06"
 cd "$R"
-mkdir -p gpurun_out
-( while sleep 50; do date >> "$R/gpurun_out/heartbeat.log"; done ) &
-HB=$!
-trap 'kill $HB 2>/dev/null' EXIT
-timeout -k 10 1000 bash profiles/collect.sh r06_a_cfg3 --workload cfg3 --steps 6 --warmup 2 --cpu-steps 3 || exit $?
-timeout -k 10 700 bash profiles/collect.sh r06_a_cfg4 --workload cfg4 --steps 10 --warmup 2 --cpu-steps 6 || exit $?
-cat profiles/r06_a_cfg3/bench.json | head -c 400; echo
-cat profiles/r06_a_cfg4/bench.json | head -c 400; echo
+export TMPDIR=/tmp
+for v in fused split; do
+  e=""; [ $v = split ] && e="SPH_CLS_SPLIT=1"
+  env $e timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/r06/ks14_$v" -o run -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-cfg3 --developed-presteps 0 > "$R/gpurun_out/r06/ks14_$v.log" 2>&1 || exit $?
+  f=$(find gpurun_out/r06/ks14_$v -name "*kernel_stats.csv" | head -1)
+  cp "$f" gpurun_out/r06/ks14_${v}_stats.csv
+  python3 -c "
+import csv
+for r in csv.DictReader(open('$f')):
+    n=r['Name']
+    if any(k in n for k in ('k_update','k_inc_classify','k_inc_push','k_inc_boxes','k_items_place','k_dt','k_pack')):
+        print('$v', n.split('(')[0][:60], r['Calls'], round(float(r['AverageNs'])/1e3,2))"
+  rm -rf gpurun_out/r06/ks14_$v
+done
+SPH_CLS_SPLIT=1 SPH_SLAB_TURNS=2 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/r06/trace_y14" -o run -- python3 "$R/profiles/slab_turns.py" --axis 1 --modes inplace --repeat 1 --steps 6 > "$R/gpurun_out/r06/trace_y14.log" 2>&1 || exit $?
+f=$(find gpurun_out/r06/trace_y14 -name "*kernel_trace.csv" | head -1)
+python3 profiles/turns2_breakdown.py "$f" gpurun_out/r06/trace_y14_breakdown.json | tail -8
+rm -rf gpurun_out/r06/trace_y14
