@@ -34,14 +34,14 @@ __device__ __forceinline__ bool inc_near(int d, int ncx, int nsheet, bool usey, 
   return false;
 }
 
-// The tile's particle i = b INC_TILE + k INC_BS + t of a block of BS threads: BS = INC_BS
-// (k = 0..3 per thread, t = the thread) or BS = INC_TILE (one particle per thread: k and t
-// from the thread index) — the same order of waves (k, t / 64) either way.
+// The tile's particle i = b INC_TILE + k INC_BS + t of a block of BS threads (BS a multiple of
+// INC_BS dividing INC_TILE): a thread's e-th particle is e BS + its index, so k = e BS / INC_BS
+// + index / INC_BS and t = index % INC_BS — the same order of waves (k, t / 64) for every BS.
 template <int BS>
 struct TileMap {
-  static_assert(BS == INC_BS || BS == INC_TILE, "tiles of 4 particles per thread or of one");
+  static_assert(BS % INC_BS == 0 && INC_TILE % BS == 0, "blocks of INC_BS .. INC_TILE threads");
   static constexpr int IPT = INC_TILE / BS;
-  __device__ __forceinline__ static int k(int e) { return BS == INC_BS ? e : int(threadIdx.x) / INC_BS; }
+  __device__ __forceinline__ static int k(int e) { return e * (BS / INC_BS) + int(threadIdx.x) / INC_BS; }
   __device__ __forceinline__ static unsigned t() { return threadIdx.x % unsigned(INC_BS); }
 };
 
@@ -55,8 +55,8 @@ struct ClsVals {
 
 // Tile b (INC_TILE particles; every thread of the block calls it): new key, near/far flags and
 // their tile-local prefixes, the tile's counts (+ one atomic into its super tile of 64), near
-// movers' keys at tile-major slots, far movers appended to a list.  vals (BS = INC_TILE only):
-// the thread's particle's inputs, instead of loads of dcell / code / skeys.
+// movers' keys at tile-major slots, far movers appended to a list.  vals: the inputs of the
+// thread's IPT particles in registers, instead of loads of dcell / code / skeys.
 template <int BS = INC_BS>
 __device__ __forceinline__ void inc_classify_tile(DevScalars* __restrict__ sc, const unsigned* __restrict__ dcell,
                                                   const typecode* __restrict__ code, const DivGrid& g, unsigned dcc,
@@ -78,9 +78,9 @@ __device__ __forceinline__ void inc_classify_tile(DevScalars* __restrict__ sc, c
 #pragma unroll
   for (int e = 0; e < IPT; e++) {
     if (vals) {
-      dc[e] = vals->dc;
-      cd[e] = vals->cd;
-      old[e] = vals->old;
+      dc[e] = vals[e].dc;
+      cd[e] = vals[e].cd;
+      old[e] = vals[e].old;
       continue;
     }
     const unsigned i = b * INC_TILE + M::k(e) * INC_BS + M::t();

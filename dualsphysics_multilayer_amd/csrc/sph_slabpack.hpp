@@ -3,6 +3,7 @@
 // (sph_step.hip) run it on the tile they have just updated, so the exchange after an update
 // starts with its scan (one pass over the particles' dcell / code less per divide).
 #pragma once
+#include "sph_incdiv.hpp"
 #include "sph_kernels.hpp"
 
 namespace sphx {
@@ -41,13 +42,12 @@ __device__ __forceinline__ void streams(unsigned c, bool f[4]) {
   f[3] = (c & 2u) && !stay;  // migrant -> right
 }
 
-// The count pass of one tile (PK_TILE particles; BS = PK_BS threads with PK_ITEMS particles each
-// at stride PK_BS, or BS = PK_TILE threads with one particle each: the same particle order).
-// vdc / vcd (BS = PK_TILE only, with vals): the thread's particle's dcell and code in registers.
+// The count pass of one tile (PK_TILE particles; BS threads with PK_TILE / BS particles each at
+// stride BS).  vals: the dcell and code of the thread's particles in registers.
 template <int BS = PK_BS>
 __device__ __forceinline__ void pack_count_tile(const DevScalars* __restrict__ sc, const PackArgs& q, unsigned tile,
-                                                bool vals = false, unsigned vdc = 0u, typecode vcd = 0) {
-  static_assert(BS == PK_BS || BS == PK_TILE, "tiles of PK_ITEMS particles per thread or of one");
+                                                const ClsVals* vals = nullptr) {
+  static_assert(BS % 64 == 0 && PK_TILE % BS == 0, "whole waves, whole tiles");
   constexpr int IPT = PK_TILE / BS;
   __shared__ unsigned s[7][BS / 64];
   const unsigned n = sc->np;
@@ -57,7 +57,7 @@ __device__ __forceinline__ void pack_count_tile(const DevScalars* __restrict__ s
 #pragma unroll
   for (int it = 0; it < IPT; it++) {
     const unsigned p = base + it * BS + threadIdx.x;
-    dcs[it] = p < n ? (vals ? vdc : q.a.dcell[p]) : DCELL_DISCARD;
+    dcs[it] = p < n ? (vals ? vals[it].dc : q.a.dcell[p]) : DCELL_DISCARD;
   }
 #pragma unroll
   for (int it = 0; it < IPT; it++) {
@@ -71,7 +71,7 @@ __device__ __forceinline__ void pack_count_tile(const DevScalars* __restrict__ s
       for (int k = 0; k < 4; k++) c4[k] += f[k] ? 1u : 0u;
       c4[4] += (c >> 2) & 1u;
       if (q.fcnt[0] && (c & 4u) && (c & 3u)) {
-        const unsigned key = box_key(dcs[it], vals ? vcd : q.a.code[p], q.g, q.dcc);
+        const unsigned key = box_key(dcs[it], vals ? vals[it].cd : q.a.code[p], q.g, q.dcc);
         if (c & 1u) fi[0] = face_idx(q.g, q.W, key, q.g.sown0);
         if (c & 2u) fi[1] = face_idx(q.g, q.W, key, q.g.sown1 - q.W);
       }

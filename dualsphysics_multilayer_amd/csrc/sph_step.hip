@@ -180,10 +180,13 @@ __device__ __forceinline__ UpdIn upd_load(int euler, const float4* __restrict__ 
     in.pz = (KIND == UPD_VERLET ? a.posz : a.poszpre)[p];
   }
   if (KIND != UPD_SYM_PRE && shiftpos && p >= npb) in.sh = shiftpos[p];
-  // every load issued here, before the first store: without this use the compiler sinks the
-  // loads only one branch needs (code, position, shifting) into it, behind the stores before it
-  asm volatile("" ::"v"(unsigned(in.code)), "v"(in.pxy.x), "v"(in.pxy.y), "v"(in.pz), "v"(in.sh.x));
   return in;
+}
+// After the loads of a thread's particles, before the first store: every load issued (without
+// this use the compiler sinks the loads only one branch needs — code, position, shifting —
+// into it, behind the stores before it).
+__device__ __forceinline__ void upd_keep(const UpdIn& in) {
+  asm volatile("" ::"v"(unsigned(in.code)), "v"(in.pxy.x), "v"(in.pxy.y), "v"(in.pz), "v"(in.sh.x));
 }
 
 // ComputeVerlet (JSphCpu.cpp:1381-1399): bound -> ComputeVelrhopBound, fluid -> ComputeVerletVarsFluid.
@@ -343,15 +346,14 @@ __device__ __forceinline__ UpdOut sym_cor_part(const DevScalars* __restrict__ sc
   return o;
 }
 
-// One particle's update of kind KIND (loads first, then the kind's arithmetic and stores).
+// One particle's update of kind KIND from its loaded inputs (the kind's arithmetic and stores).
 template <int KIND>
-__device__ __forceinline__ UpdOut upd_part(const DevScalars* __restrict__ sc, const KConst& K, int euler,
-                                           const float4* __restrict__ arace, const PartArrays& a, const DivGrid& g,
-                                           const float4* __restrict__ shiftpos, unsigned p, unsigned npb) {
-  const UpdIn in = upd_load<KIND>(euler, arace, a, shiftpos, p, npb);
-  if (KIND == UPD_VERLET) return verlet_part(sc, K, euler, a, g, shiftpos != nullptr, p, npb, in);
+__device__ __forceinline__ UpdOut upd_compute(const DevScalars* __restrict__ sc, const KConst& K, int euler,
+                                              const PartArrays& a, const DivGrid& g, bool shift, unsigned p,
+                                              unsigned npb, const UpdIn& in) {
+  if (KIND == UPD_VERLET) return verlet_part(sc, K, euler, a, g, shift, p, npb, in);
   if (KIND == UPD_SYM_PRE) return sym_pre_part(sc, K, a, g, p, npb, in);
-  return sym_cor_part(sc, K, a, g, shiftpos != nullptr, p, npb, in);
+  return sym_cor_part(sc, K, a, g, shift, p, npb, in);
 }
 
 template <int KIND>
@@ -359,32 +361,59 @@ __global__ __launch_bounds__(256) void k_update(const DevScalars* __restrict__ s
                                                 const float4* __restrict__ arace, PartArrays a, DivGrid g,
                                                 const float4* __restrict__ shiftpos) {
   const unsigned p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < sc->np) upd_part<KIND>(sc, K, euler, arace, a, g, shiftpos, p, sc->npb);
+  if (p >= sc->np) return;
+  const unsigned npb = sc->npb;
+  const UpdIn in = upd_load<KIND>(euler, arace, a, shiftpos, p, npb);
+  upd_keep(in);
+  upd_compute<KIND>(sc, K, euler, a, g, shiftpos != nullptr, p, npb, in);
 }
 
 // The update with the incremental divide's classification of the same particles (sph_incdiv.hpp):
-// one block of INC_TILE threads per classify tile updates its particles (one per thread, the
-// per-particle kernels' mapping) and classifies them from the dcell and code it has just
-// computed, in registers (with the previous key, loaded with the update's inputs): the block
-// waits for one memory latency, not for a chain of reloads.  A step without bodies: nothing
+// one block of UPD_BS threads per classify tile updates its INC_TILE particles (INC_TILE /
+// UPD_BS per thread at stride UPD_BS: every input of all of them loaded first, one memory
+// latency) and classifies them from the dcell and code it has just computed, in registers
+// (with the previous keys, loaded with the update's inputs).  A step without bodies: nothing
 // moves a particle between the update and the divide.  PACK (a slab with neighbours): also the
 // exchange's count pass over the same tile (sph_slabpack.hpp, PK_TILE = INC_TILE).
+// 512 threads x 2 particles (98 VGPRs, 5 waves/SIMD): at a cfg3 y-slab 47 vs 60 us per call
+// for 1024 x 1 (profiles/r06_turns8/turns14_*.log), cfg2 alike (profiles/r06_ab/ab14*.log).
+#ifndef SPH_UPD_BS
+#define SPH_UPD_BS 512
+#endif
+constexpr int UPD_BS = SPH_UPD_BS, UPD_IPT = INC_TILE / UPD_BS;
 static_assert(PK_TILE == INC_TILE, "the pack's tiles are the classify tiles");
 template <int KIND, bool PACK>
-__global__ __launch_bounds__(INC_TILE) void k_update_cls(DevScalars* __restrict__ sc, KConst K, int euler,
-                                                         const float4* __restrict__ arace, PartArrays a, DivGrid g,
-                                                         const float4* __restrict__ shiftpos, IncDivScratch s,
-                                                         int usey, int usez, PackArgs q) {
-  const unsigned p = blockIdx.x * INC_TILE + threadIdx.x;
-  ClsVals v{DCELL_DISCARD, 0, 0u};
-  if (p < sc->np) {
-    v.old = s.skeys[p];
-    const UpdOut o = upd_part<KIND>(sc, K, euler, arace, a, g, shiftpos, p, sc->npb);
-    v.dc = o.dcell;
-    v.cd = o.code;
+__global__ __launch_bounds__(UPD_BS) void k_update_cls(DevScalars* __restrict__ sc, KConst K, int euler,
+                                                       const float4* __restrict__ arace, PartArrays a, DivGrid g,
+                                                       const float4* __restrict__ shiftpos, IncDivScratch s,
+                                                       int usey, int usez, PackArgs q) {
+  const unsigned np = sc->np, npb = sc->npb;
+  const unsigned base = blockIdx.x * INC_TILE + threadIdx.x;
+  ClsVals v[UPD_IPT];
+  UpdIn in[UPD_IPT];
+#pragma unroll
+  for (int e = 0; e < UPD_IPT; e++) {
+    const unsigned p = base + e * UPD_BS;
+    v[e] = ClsVals{DCELL_DISCARD, 0, 0u};
+    if (p < np) {
+      v[e].old = s.skeys[p];
+      in[e] = upd_load<KIND>(euler, arace, a, shiftpos, p, npb);
+    }
   }
-  inc_classify_tile<INC_TILE>(sc, a.dcell, a.code, g, K.domcellcode, s, usey, usez, blockIdx.x, &v);
-  if (PACK) pack_count_tile<PK_TILE>(sc, q, blockIdx.x, true, v.dc, v.cd);
+#pragma unroll
+  for (int e = 0; e < UPD_IPT; e++)
+    if (base + e * UPD_BS < np) upd_keep(in[e]);
+#pragma unroll
+  for (int e = 0; e < UPD_IPT; e++) {
+    const unsigned p = base + e * UPD_BS;
+    if (p < np) {
+      const UpdOut o = upd_compute<KIND>(sc, K, euler, a, g, shiftpos != nullptr, p, npb, in[e]);
+      v[e].dc = o.dcell;
+      v[e].cd = o.code;
+    }
+  }
+  inc_classify_tile<UPD_BS>(sc, a.dcell, a.code, g, K.domcellcode, s, usey, usez, blockIdx.x, v);
+  if (PACK) pack_count_tile<UPD_BS>(sc, q, blockIdx.x, v);
 }
 template <int KIND>
 static void launch_update_cls(hipStream_t stm, DevScalars* sc, const KConst& K, int euler, const float4* arace,
@@ -392,10 +421,10 @@ static void launch_update_cls(hipStream_t stm, DevScalars* sc, const KConst& K, 
                               const PackArgs* pk) {
   const int usey = g.ncy > 1, usez = g.ncz > 1;
   if (pk)
-    hipLaunchKernelGGL((k_update_cls<KIND, true>), dim3(s.nb1), dim3(INC_TILE), 0, stm, sc, K, euler, arace, a, g,
+    hipLaunchKernelGGL((k_update_cls<KIND, true>), dim3(s.nb1), dim3(UPD_BS), 0, stm, sc, K, euler, arace, a, g,
                        shiftpos, s, usey, usez, *pk);
   else
-    hipLaunchKernelGGL((k_update_cls<KIND, false>), dim3(s.nb1), dim3(INC_TILE), 0, stm, sc, K, euler, arace, a, g,
+    hipLaunchKernelGGL((k_update_cls<KIND, false>), dim3(s.nb1), dim3(UPD_BS), 0, stm, sc, K, euler, arace, a, g,
                        shiftpos, s, usey, usez, PackArgs{});
 }
 

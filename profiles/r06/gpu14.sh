@@ -23,3 +23,14 @@ SPH_CLS_SPLIT=1 SPH_SLAB_TURNS=2 timeout -k 10 400 rocprofv3 --kernel-trace --ou
 f=$(find gpurun_out/r06/trace_y14 -name "*kernel_trace.csv" | head -1)
 python3 profiles/turns2_breakdown.py "$f" gpurun_out/r06/trace_y14_breakdown.json | tail -8
 rm -rf gpurun_out/r06/trace_y14
+# the fused update's block shape: the previous commit's library (base: 1024 threads, dcell /
+# code reloaded), this one (1024 threads, one load phase, registers), 512 threads x 2 particles
+for v in gpurun_var/base main gpurun_var/u512; do
+  lib=$R/$v/libsphcore.so; [ $v = main ] && lib=$R/dualsphysics_multilayer_amd/lib/libsphcore.so
+  SPH_LIB=$lib SPH_SLAB_TURNS=2 timeout -k 10 300 python -u profiles/slab_turns.py --axis 1 --slabs 8 --steps 8 --repeat 1 --modes inplace > gpurun_out/r06/turns14_$(basename $v).log 2>&1 || exit $?
+  python3 -c "
+import json; d=json.loads(open('gpurun_out/r06/turns14_$(basename $v).log').read().strip().splitlines()[-1])['summary_min_over_repeats']['inplace']
+print('$v', 'wall', d['wall_ms_per_step'], 'update', d['update_ms'], 'divide', d['divide_ms'], 'kern', d['slab_kernels_ms_per_step'])"
+done
+timeout -k 10 500 bash profiles/ab.sh 2 gpurun_var/base main gpurun_var/u512 -- --steps 40 --warmup 5 > gpurun_out/r06/ab14.log 2>&1 || exit $?
+cat gpurun_out/r06/ab14.log
