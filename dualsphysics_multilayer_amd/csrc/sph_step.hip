@@ -375,12 +375,13 @@ __global__ __launch_bounds__(256) void k_update(const DevScalars* __restrict__ s
 // (with the previous keys, loaded with the update's inputs).  A step without bodies: nothing
 // moves a particle between the update and the divide.  PACK (a slab with neighbours): also the
 // exchange's count pass over the same tile (sph_slabpack.hpp, PK_TILE = INC_TILE).
-// 512 threads x 2 particles (98 VGPRs, 5 waves/SIMD): at a cfg3 y-slab 47 vs 60 us per call
-// for 1024 x 1 (profiles/r06_turns8/turns14_*.log), cfg2 alike (profiles/r06_ab/ab14*.log).
-#ifndef SPH_UPD_BS
-#define SPH_UPD_BS 512
-#endif
-constexpr int UPD_BS = SPH_UPD_BS, UPD_IPT = INC_TILE / UPD_BS;
+// One particle per thread: the per-particle kernels' code shape, and bitwise their results
+// (the incremental divide's tests compare it with the radix path, which runs k_update).  512
+// threads x 2 particles ran 47 vs 60 us per call at a cfg3 y-slab, but its positions differed
+// from k_update's (14 of 20 tests/test_divide_inc.py red, the order equal;
+// profiles/r06_ab/test16_*.log) — most likely the unrolled pair's multiply-adds contracted
+// otherwise under -ffp-contract=fast; not pursued.
+constexpr int UPD_BS = INC_TILE, UPD_IPT = INC_TILE / UPD_BS;
 static_assert(PK_TILE == INC_TILE, "the pack's tiles are the classify tiles");
 template <int KIND, bool PACK>
 __global__ __launch_bounds__(UPD_BS) void k_update_cls(DevScalars* __restrict__ sc, KConst K, int euler,

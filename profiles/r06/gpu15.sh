@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6: the fused update at 512 threads x 2 particles — full GPU suite, the cfg3 8 y-slab
+# Round 6: the fused update (1024 x 1, every load first, registers) — full GPU suite, the cfg3 8 y-slab
 # turns run, its kernel trace, the cfg3 single domain on the same box, the T8 summary.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p "$R/gpurun_out/r06"
