@@ -379,9 +379,9 @@ __global__ __launch_bounds__(256) void k_update(const DevScalars* __restrict__ s
 // (the incremental divide's tests compare it with the radix path, which runs k_update).  512
 // threads x 2 particles ran 47 vs 60 us per call at a cfg3 y-slab, but its positions differed
 // from k_update's (14 of 20 tests/test_divide_inc.py red, the order equal;
-// profiles/r06_ab/test16_*.log).  Not contraction (the update's f64 FMAs are its division and
-// square-root expansions, the same count per particle in both shapes); cause not found, the
-// shape not used.
+// profiles/r06_ab/test16_*.log): one-ulp position differences in ~0.2 % of the particles of a
+// stirred case, velocities and densities bitwise (profiles/r06_ab/dbg18_upd512_stirred.log).
+// The f64 FMA count per particle is the same in both shapes; cause not found, shape not used.
 constexpr int UPD_BS = INC_TILE, UPD_IPT = INC_TILE / UPD_BS;
 static_assert(PK_TILE == INC_TILE, "the pack's tiles are the classify tiles");
 template <int KIND, bool PACK>
