@@ -25,6 +25,14 @@ struct PartArrays {
   float4* tau = nullptr;         // Laminar+SPS: sub-particle stress tensor, [2i] {xx,xy,xz,yy}, [2i+1] {yz,zz}
 };
 
+// A double product that is not fused into a following add (an opaque use of the rounded
+// product): the update's arithmetic as the reference's plain multiplies and adds, whatever the
+// surrounding code shape (sph_step.hip).
+__device__ __forceinline__ double nc(double x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 // JSphCpu::UpdatePos (JSphCpu.cpp:1240-1293), single domain, no periodic.
 // Returns the new dcell; rcode (optional): the particle's code held in registers, updated in
 // place (else read from a.code when the particle leaves).
@@ -75,7 +83,7 @@ __device__ __forceinline__ void shift_displacement(const KConst& K, float4 rs, f
   if (rs.x == 3.402823466e+38f) return;
   const double coefumagn = dt * double(K.shiftcoef) * double(K.kernelh);
   const double vx = double(v.x), vy = double(v.y), vz = double(v.z);
-  double umagn = coefumagn * sqrt(vx * vx + vy * vy + vz * vz);
+  double umagn = coefumagn * sqrt(nc(vx * vx) + nc(vy * vy) + nc(vz * vz));
   if (K.shifttfs != 0.f) {
     if (rs.w < K.shifttfs) umagn = 0;
     else umagn *= (double(rs.w) - double(K.shifttfs)) / K.coeftfs;

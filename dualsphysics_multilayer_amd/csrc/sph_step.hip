@@ -136,6 +136,12 @@ __device__ __forceinline__ bool slab_ghost(const KConst& K, const DivGrid& g, un
 
 enum { UPD_VERLET = 0, UPD_SYM_PRE = 1, UPD_SYM_COR = 2 };
 
+// The update's products are kept out of multiply-add fusion (nc, sph_kernels.hpp): the
+// reference's doubles are plain multiplies and adds, and without it -ffp-contract=fast (which
+// fuses across statements and ignores `#pragma clang fp contract`) chose per code shape which
+// product to fuse — one-ulp position differences between the fused update at 512 x 2 and the
+// per-particle kernel (profiles/r06_ab/dbg18_upd512_stirred.log).
+
 // One particle's update inputs, all loaded before any of its stores: one memory latency per
 // particle instead of a chain of them (the stores to the particle arrays would otherwise keep
 // each later load behind the branch that needs it).  Per kind:
@@ -211,7 +217,7 @@ __device__ __forceinline__ UpdOut verlet_part(const DevScalars* __restrict__ sc,
   const double dt2 = (euler ? dt : dt + dt);
   const float4 ra = in.ra;
   const float4 vr2 = in.v2;
-  const float rhopnew = float(double(vr2.w) + dt2 * double(ra.w));
+  const float rhopnew = float(double(vr2.w) + nc(dt2 * double(ra.w)));
   if (p < npb) {
     a.velrhopm1[p] = make_float4(0.f, 0.f, 0.f, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
     return o;
@@ -223,13 +229,13 @@ __device__ __forceinline__ UpdOut verlet_part(const DevScalars* __restrict__ sc,
   }
   const double dt205 = 0.5 * dt * dt;
   const double agx = double(ra.x) + K.gravxd, agy = double(ra.y) + K.gravyd, agz = double(ra.z) + K.gravzd;
-  double dx = double(vr1.x) * dt + agx * dt205;
-  double dy = double(vr1.y) * dt + agy * dt205;
-  double dz = double(vr1.z) * dt + agz * dt205;
+  double dx = nc(double(vr1.x) * dt) + nc(agx * dt205);
+  double dy = nc(double(vr1.y) * dt) + nc(agy * dt205);
+  double dz = nc(double(vr1.z) * dt) + nc(agz * dt205);
   if (shift) shift_displacement(K, in.sh, vr1, dt, dx, dy, dz);  // RunShifting(dt) before ComputeVerlet
   const bool outrhop = (rhopnew < K.rhopoutmin || rhopnew > K.rhopoutmax);
-  const float4 nv = make_float4(float(double(vr2.x) + agx * dt2), float(double(vr2.y) + agy * dt2),
-                                float(double(vr2.z) + agz * dt2), rhopnew);
+  const float4 nv = make_float4(float(double(vr2.x) + nc(agx * dt2)), float(double(vr2.y) + nc(agy * dt2)),
+                                float(double(vr2.z) + nc(agz * dt2)), rhopnew);
   typecode rcode = in.code;
   o.dcell = update_pos(K, in.pxy.x, in.pxy.y, in.pz, dx, dy, dz, outrhop, p, a, &rcode);
   o.code = rcode;
@@ -260,7 +266,7 @@ __device__ __forceinline__ UpdOut sym_pre_part(const DevScalars* __restrict__ sc
   const double dt = sc->dt, dt05 = dt * .5;
   const float4 ra = in.ra;
   const float4 vp = in.v1;
-  const float rhopnew = float(double(vp.w) + dt05 * double(ra.w));
+  const float rhopnew = float(double(vp.w) + nc(dt05 * double(ra.w)));
   if (p < npb) {
     a.velrhop[p] = make_float4(vp.x, vp.y, vp.z, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
     a.posxy[p] = pxy;
@@ -274,11 +280,11 @@ __device__ __forceinline__ UpdOut sym_pre_part(const DevScalars* __restrict__ sc
     a.posz[p] = pz;
     return o;
   }
-  const double dx = double(vp.x) * dt05, dy = double(vp.y) * dt05, dz = double(vp.z) * dt05;
+  const double dx = nc(double(vp.x) * dt05), dy = nc(double(vp.y) * dt05), dz = nc(double(vp.z) * dt05);
   const bool outrhop = (rhopnew < K.rhopoutmin || rhopnew > K.rhopoutmax);
-  a.velrhop[p] = make_float4(float(double(vp.x) + (double(ra.x) + K.gravxd) * dt05),
-                             float(double(vp.y) + (double(ra.y) + K.gravyd) * dt05),
-                             float(double(vp.z) + (double(ra.z) + K.gravzd) * dt05), rhopnew);
+  a.velrhop[p] = make_float4(float(double(vp.x) + nc((double(ra.x) + K.gravxd) * dt05)),
+                             float(double(vp.y) + nc((double(ra.y) + K.gravyd) * dt05)),
+                             float(double(vp.z) + nc((double(ra.z) + K.gravzd) * dt05)), rhopnew);
   if (outrhop && CodeIsNormal(rcode)) {
     rcode = CodeSetNormal(rcode) | CODE_OUTRHOP;
     a.code[p] = rcode;
@@ -308,8 +314,8 @@ __device__ __forceinline__ UpdOut sym_cor_part(const DevScalars* __restrict__ sc
   const float4 ra = in.ra;
   const float4 vr = in.v1;
   const float4 vp = in.v2;
-  const double epsilon_rdot = (-double(ra.w) / double(vr.w)) * dt;
-  const float rhopnew = float(double(vp.w) * (2. - epsilon_rdot) / (2. + epsilon_rdot));
+  const double epsilon_rdot = nc((-double(ra.w) / double(vr.w)) * dt);
+  const float rhopnew = float(nc(double(vp.w) * (2. - epsilon_rdot)) / (2. + epsilon_rdot));
   if (p < npb) {
     a.velrhop[p] = make_float4(0.f, 0.f, 0.f, (rhopnew < K.rhopzero ? K.rhopzero : rhopnew));
     return o;  // boundary keeps its position (already restored by the predictor)
@@ -321,12 +327,12 @@ __device__ __forceinline__ UpdOut sym_cor_part(const DevScalars* __restrict__ sc
     a.posz[p] = in.pz;
     return o;
   }
-  const float4 nv = make_float4(float(double(vp.x) + (double(ra.x) + K.gravxd) * dt),
-                                float(double(vp.y) + (double(ra.y) + K.gravyd) * dt),
-                                float(double(vp.z) + (double(ra.z) + K.gravzd) * dt), rhopnew);
-  double dx = (double(vp.x) + double(nv.x)) * dt05;
-  double dy = (double(vp.y) + double(nv.y)) * dt05;
-  double dz = (double(vp.z) + double(nv.z)) * dt05;
+  const float4 nv = make_float4(float(double(vp.x) + nc((double(ra.x) + K.gravxd) * dt)),
+                                float(double(vp.y) + nc((double(ra.y) + K.gravyd) * dt)),
+                                float(double(vp.z) + nc((double(ra.z) + K.gravzd) * dt)), rhopnew);
+  double dx = nc((double(vp.x) + double(nv.x)) * dt05);
+  double dy = nc((double(vp.y) + double(nv.y)) * dt05);
+  double dz = nc((double(vp.z) + double(nv.z)) * dt05);
   // RunShifting(dt) after the corrector's interaction, with the predicted velocity
   // (JSphCpuSingle.cpp:764 of the v5.0 solver, JSphShifting.cpp:388-418)
   if (shift) shift_displacement(K, in.sh, vr, dt, dx, dy, dz);
@@ -375,14 +381,11 @@ __global__ __launch_bounds__(256) void k_update(const DevScalars* __restrict__ s
 // (with the previous keys, loaded with the update's inputs).  A step without bodies: nothing
 // moves a particle between the update and the divide.  PACK (a slab with neighbours): also the
 // exchange's count pass over the same tile (sph_slabpack.hpp, PK_TILE = INC_TILE).
-// One particle per thread: the per-particle kernels' code shape, and bitwise their results
-// (the incremental divide's tests compare it with the radix path, which runs k_update).  512
-// threads x 2 particles ran 47 vs 60 us per call at a cfg3 y-slab, but its positions differed
-// from k_update's (14 of 20 tests/test_divide_inc.py red, the order equal;
-// profiles/r06_ab/test16_*.log): one-ulp position differences in ~0.2 % of the particles of a
-// stirred case, velocities and densities bitwise (profiles/r06_ab/dbg18_upd512_stirred.log).
-// The f64 FMA count per particle is the same in both shapes; cause not found, shape not used.
-constexpr int UPD_BS = INC_TILE, UPD_IPT = INC_TILE / UPD_BS;
+// 512 threads x 2 particles (98 VGPRs, 5 waves/SIMD): at a cfg3 y-slab 47 vs 60 us per call
+// for 1024 x 1 (profiles/r06_turns8/turns14_*.log).  Bitwise the per-particle kernels since
+// the update's products are kept out of multiply-add fusion (nc, above; before that the
+// unrolled pair fused other products: profiles/r06_ab/test16_*.log, dbg18_upd512_stirred.log).
+constexpr int UPD_BS = 512, UPD_IPT = INC_TILE / UPD_BS;
 static_assert(PK_TILE == INC_TILE, "the pack's tiles are the classify tiles");
 template <int KIND, bool PACK>
 __global__ __launch_bounds__(UPD_BS) void k_update_cls(DevScalars* __restrict__ sc, KConst K, int euler,
