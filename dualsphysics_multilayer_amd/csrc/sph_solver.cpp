@@ -1461,6 +1461,11 @@ void SphGpuSingle::Interaction_Forces(int interstep) {
                        ftmassp_);
   }
   TimedEnd(0);
+  if (turn && fold_turn_ >= 0) {  // the next DtVariable's fold, inside this slab's turn
+    launch_fold_maxima(stream, sc_, folded_, fold_turn_ != 0);
+    folded_ready_ = true;
+  }
+  fold_turn_ = -1;
   if (turn) transport_->turn_done(SlabTransport::TURN_INTERACTION, stream);
 }
 
@@ -1503,7 +1508,8 @@ void SphGpuSingle::DtVariable(int mode) {
   if (slab() && transport_->nranks > 1) {  // one rank: its own maxima are the domain's
     SLAB_TRACE("dt allreduce");
     // The three maxima span the whole domain: fold locally, max over all slabs.
-    launch_fold_maxima(stream, sc_, folded_, mode != DT_PEEK);
+    if (!folded_ready_) launch_fold_maxima(stream, sc_, folded_, mode != DT_PEEK);
+    folded_ready_ = false;
     transport_->allreduce_max_u32(folded_, 5, stream);  // 4 maxima + the fatal error flags
     launch_dt(stream, sc_, K, C.cflnumber, C.dtmin, C.cs0, mode, dttrace_, tracecap_, folded_);
   } else {
@@ -1590,17 +1596,22 @@ void SphGpuSingle::ComputeSymplecticCorr() {
 void SphGpuSingle::ComputeStep() {
   stepped_ = true;
   stepsdone_++;
+  // (turns mode: each interaction's turn ends with the fold of the DtVariable after it)
+  const bool foldturn = slab() && transport_->nranks > 1 && transport_->turns();
   if (step_algorithm_ == SPH_STEP_VERLET) {
+    if (foldturn) fold_turn_ = 1;
     Interaction_Forces(1);
     DtVariable(DT_VERLET);
     ComputeVerlet();
     if (nftbodies_) RunFloating(false);
   } else {
+    if (foldturn) fold_turn_ = 1;
     Interaction_Forces(2);
     DtVariable(DT_SYM_PRE);
     ComputeSymplecticPre();
     if (nftbodies_) RunFloating(true);
     RunCellDivide();
+    if (foldturn) fold_turn_ = 1;
     Interaction_Forces(3);
     DtVariable(DT_SYM_COR);
     ComputeSymplecticCorr();

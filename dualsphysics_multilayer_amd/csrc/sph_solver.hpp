@@ -259,6 +259,11 @@ class SphGpuSingle {
   unsigned nftp_ = 0;            // floating particles of the case (CaseNfloat)
   unsigned casenpb_ = 0;         // CaseNpb: first floating idp
   bool stepped_ = false;         // a step was issued (bodies are configured before it)
+  // turns measurement mode: the dt maxima of the next DtVariable are folded at the end of the
+  // interaction's turn (fold_turn_: its clear flag, -1 none), so that k_fold runs alone on the
+  // GPU as on a rank's own; folded_ready_: DtVariable finds them folded
+  int fold_turn_ = -1;
+  bool folded_ready_ = false;
   std::vector<void*> allocs_;   // fixed-size allocations
   std::vector<void*> pallocs_;  // capacity-sized (per-particle) allocations
   // slab decomposition
