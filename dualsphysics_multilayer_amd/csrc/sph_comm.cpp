@@ -186,15 +186,21 @@ class LocalTransport final : public SlabTransport {
     const LocalHub::Slot* L = has_left() ? &hub_->slots[size_t(rank - 1)] : nullptr;
     const LocalHub::Slot* R = has_right() ? &hub_->slots[size_t(rank + 1)] : nullptr;
     hub_->wait_until([&] { return (!L || L->posted >= g) && (!R || R->posted >= g); });
-    if (L && nrl) {
+    const bool cl = L && nrl, cr = R && nrr;
+    if (cl) {
       if (L->nsr != nrl) throw SphError(SPH_ERR_COMM, "exchange: size mismatch with the left slab");
       check_hip(hipStreamWaitEvent(s, L->ready, 0), "exchange: wait left");
-      check_hip(hipMemcpyAsync(rl, L->sr, nrl, kCopyKind, s), "exchange: copy from left");
     }
-    if (R && nrr) {
+    if (cr) {
       if (R->nsl != nrr) throw SphError(SPH_ERR_COMM, "exchange: size mismatch with the right slab");
       check_hip(hipStreamWaitEvent(s, R->ready, 0), "exchange: wait right");
-      check_hip(hipMemcpyAsync(rr, R->sl, nrr, kCopyKind, s), "exchange: copy from right");
+    }
+    if (hub_->onedev && cl && cr) {
+      // both faces in one kernel, as RCCL moves a send/receive group (slabs of one GPU)
+      launch_copy_pair(s, rl, L->sr, nrl, rr, R->sl, nrr);
+    } else {
+      if (cl) check_hip(hipMemcpyAsync(rl, L->sr, nrl, kCopyKind, s), "exchange: copy from left");
+      if (cr) check_hip(hipMemcpyAsync(rr, R->sl, nrr, kCopyKind, s), "exchange: copy from right");
     }
     check_hip(hipEventRecord(me.copied, s), "exchange: copies");
     hub_->publish([&] { me.consumed = g; });

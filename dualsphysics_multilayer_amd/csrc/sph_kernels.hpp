@@ -631,6 +631,8 @@ struct RankPtrs {
 };
 void launch_rank_ordered_sum(hipStream_t stm, const RankPtrs& rp, int n, int nranks, float* out);
 void launch_rank_max_u32(hipStream_t stm, const RankPtrs& rp, int n, int nranks, unsigned* out);
+// Two device-to-device copies in one launch (the in-process transport's two faces, on one GPU).
+void launch_copy_pair(hipStream_t stm, void* d0, const void* s0, size_t n0, void* d1, const void* s1, size_t n1);
 // Owned particles per GLOBAL x-column: counts[c] fluid (incl. floating), counts[ncxg + c]
 // boundary (the re-partition's weights), as floats (exact integers).
 void launch_column_counts(hipStream_t stm, unsigned cap, const DevScalars* sc, const PartArrays& a, DivGrid g,

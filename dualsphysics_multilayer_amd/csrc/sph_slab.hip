@@ -17,6 +17,8 @@
 // multi-GPU path in this fork (JSphGpuSingle only); this follows the single-domain
 // semantics exactly: the owner of a particle computes it with the same neighbour set
 // it would have in one domain.
+#include <algorithm>
+
 #include "sph_kernels.hpp"
 #include "sph_slabpack.hpp"
 
@@ -535,6 +537,34 @@ __global__ void k_rank_max_u32(RankPtrs rp, int n, int nranks, unsigned* __restr
   unsigned v = 0u;
   for (int r = 0; r < nranks; r++) v = max(v, static_cast<const unsigned*>(rp.p[r])[i]);
   out[i] = v;
+}
+
+// blockIdx.y: which copy; 16-B words when both pointers and the size allow, else 4-B, else bytes.
+__global__ __launch_bounds__(256) void k_copy_pair(unsigned char* __restrict__ d0, const unsigned char* __restrict__ s0,
+                                                   size_t n0, unsigned char* __restrict__ d1,
+                                                   const unsigned char* __restrict__ s1, size_t n1) {
+  unsigned char* d = blockIdx.y ? d1 : d0;
+  const unsigned char* src = blockIdx.y ? s1 : s0;
+  const size_t n = blockIdx.y ? n1 : n0;
+  const size_t stride = size_t(gridDim.x) * blockDim.x, t0 = size_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const size_t al = (reinterpret_cast<size_t>(d) | reinterpret_cast<size_t>(src) | n);
+  if ((al & 15u) == 0) {
+    for (size_t i = t0; i < n / 16; i += stride)
+      reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(src)[i];
+  } else if ((al & 3u) == 0) {
+    for (size_t i = t0; i < n / 4; i += stride)
+      reinterpret_cast<unsigned*>(d)[i] = reinterpret_cast<const unsigned*>(src)[i];
+  } else {
+    for (size_t i = t0; i < n; i += stride) d[i] = src[i];
+  }
+}
+
+void launch_copy_pair(hipStream_t stm, void* d0, const void* s0, size_t n0, void* d1, const void* s1, size_t n1) {
+  const size_t words = (std::max(n0, n1) + 15) / 16;
+  const unsigned nb = unsigned(std::min<size_t>(std::max<size_t>((words + 255) / 256, 1), 1024));
+  hipLaunchKernelGGL(k_copy_pair, dim3(nb, 2), dim3(256), 0, stm, static_cast<unsigned char*>(d0),
+                     static_cast<const unsigned char*>(s0), n0, static_cast<unsigned char*>(d1),
+                     static_cast<const unsigned char*>(s1), n1);
 }
 
 // (nranks <= RankPtrs::MAXR and n <= 64: LocalTransport's device_reduce and its 8-value limit)
